@@ -1,0 +1,190 @@
+"""ORACLE (test infrastructure only) — StructureFind numeric cores restated in
+vectorised NumPy: compartment (distance decay, O/E, Pearson correlation,
+top-3 PCA, PC selection) and the directionality-index TAD scan.
+
+Pinned against golden vectors produced by the reference's own methods
+(tests/golden/make_golden.py → tests/golden/compartment_*.npz, di_*.npz).
+
+Deviation recorded in SURVEY.md §0.5 / §8(c): the reference's
+``PCA(n_components=3)`` (StructureFind.py:338) uses randomized SVD for inputs
+larger than 500×500; the oracle uses the exact SVD (``svd_solver='full'``).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+# ---------------------------------------------------------------- compartment
+def distance_decay(M, gap_ratio=0.05):
+    """Distance_Decay (StructureFind.py:201-271) with ``G_array=None``.
+
+    Gap columns: nonzero fraction <= 0.05.  decline[d] = sum of nonzero
+    entries at |i-j| = d whose COLUMN is not a gap, divided by the number of
+    valid pairs (2(size-d) - gaps, or size - |G| for d = 0) when positive.
+    Returns (decline, G, NG)."""
+    M = np.asarray(M, dtype=np.float64)
+    size = M.shape[0]
+    frac = (M != 0).sum(axis=0) / float(size)
+    gmask = frac <= gap_ratio
+    G = np.nonzero(gmask)[0]
+    NG = np.nonzero(~gmask)[0]
+    i, j = np.nonzero(M)
+    keep = ~gmask[j]
+    i, j = i[keep], j[keep]
+    d = np.abs(j - i)
+    decline = np.bincount(d, weights=M[i, j], minlength=size + 1).astype(np.float64)[:size + 1]
+    dd = np.arange(size)
+    n_lo = np.searchsorted(G, size - 1 - dd, side="right")     # #{g <= size-1-d}
+    n_hi = G.size - np.searchsorted(G, dd, side="left")        # #{g >= d}
+    bin_num = 2.0 * (size - dd) - (n_lo + n_hi)
+    bin_num[0] = float(size) - G.size
+    ok = bin_num > 0
+    out = decline[:size].copy()
+    out[ok] = out[ok] / bin_num[ok]
+    return out, G, NG
+
+
+def oe_matrix(M, decline):
+    """O/E with the zero-decline fix (Get_PCA :323-329). Returns full N×N O/E."""
+    M = np.asarray(M, dtype=np.float64)
+    dec = np.array(decline, dtype=np.float64)
+    dec[dec == 0] = dec[np.nonzero(dec)].min()
+    N = M.shape[0]
+    idx = np.arange(N)
+    D = dec[np.abs(idx[:, None] - idx[None, :])]
+    OE = np.zeros_like(M)
+    nz = M != 0
+    OE[nz] = M[nz] / D[nz]
+    return OE
+
+
+def pearson_columns(X):
+    """np.corrcoef(X, rowvar=False) with NaN→0, inf→1 (Get_PCA :335-337)."""
+    with np.errstate(invalid="ignore", divide="ignore"):
+        C = np.corrcoef(X, rowvar=False)
+    C = np.atleast_2d(C)
+    C[np.isnan(C)] = 0
+    C[np.isinf(C)] = 1
+    return C
+
+
+def top_components(C, k=3):
+    """Top-k right singular vectors of the column-centred matrix — what
+    ``PCA(n_components=k).fit(C).components_`` returns, exact SVD
+    (Get_PCA :338-340).  Signs follow sklearn>=1.5 (max-|.| entry positive)."""
+    X = C - C.mean(axis=0)
+    _, _, Vt = np.linalg.svd(X, full_matrices=False)
+    V = Vt[:k].copy()
+    for r in range(V.shape[0]):
+        if V[r, np.argmax(np.abs(V[r]))] < 0:
+            V[r] = -V[r]
+    return V
+
+
+def get_pca(decline, M, NG):
+    """Get_PCA (StructureFind.py:302-342), SA=False. Returns (pcs, Cor, OE[:, NG])."""
+    OE = oe_matrix(M, decline)[:, NG]
+    C = pearson_columns(OE)
+    return top_components(C, 3), C, OE
+
+
+def means_minus(C, pc, eps=1e-5):
+    """Select_PC_new.means_minus (StructureFind.py:375-402)."""
+    loc = np.arange(len(pc))
+    a, b = pc > 0, pc < 0
+    if not a.any() or not b.any():
+        return 0
+    la, lb = loc[a], loc[b]
+    size_a = la.max() - la.min()
+    size_b = lb.max() - lb.min()
+    lens = max(la.max(), lb.max()) - min(la.min(), lb.min())
+    Ca, Cb, Cab = C[a][:, a], C[b][:, b], C[a][:, b]
+    va = Ca[(Ca > -1) & (Ca < 1 - eps)]
+    vb = Cb[(Cb > -1) & (Cb < 1 - eps)]
+    vab = Cab[(Cab > -1) & (Cab < 1)]
+    same = np.concatenate([va, vb])
+    if vab.size == 0 or vab.mean() == 0 or vab.mean() == -1 or size_a <= lens / 2 or size_b <= lens / 2:
+        return 0
+    return same.mean() - vab.mean()
+
+
+def select_ab(OE, pc):
+    """Select_PC_new.select_ab (:403-413): flip so that the A compartment has
+    the larger mean nonzero O/E."""
+    a, b = pc > 0, pc < 0
+    A, B = OE[a][:, a], OE[b][:, b]
+    va = A[A != 0].mean()
+    vb = B[B != 0].mean()
+    return pc.copy() * -1 if vb > va else pc
+
+
+def select_pc(C, OE_ng, pcs):
+    """Select_PC_new (:374-423). ``OE_ng`` = OE rows and columns at NG."""
+    nums, values = 0, 0
+    for i in range(len(pcs)):
+        m = means_minus(C, pcs[i])
+        if m > values:
+            values, nums = m, i
+    return select_ab(OE_ng, pcs[nums]), nums
+
+
+def select_allelic_pc(pcs_full, trad_pc):
+    """Select_Allelic_PC (:446-460): max |Pearson| with the traditional PC."""
+    pcc = [abs(np.corrcoef(pc, trad_pc)[0][1]) for pc in pcs_full]
+    return pcs_full[int(np.argmax(pcc))], int(np.argmax(pcc))
+
+
+def compartment(M):
+    """Traditional compartment call for one chromosome (Compartment :509-527).
+    Returns (pc_full[N], selected_index, pcs, Cor)."""
+    dec, G, NG = distance_decay(M)
+    pcs, C, OE = get_pca(dec, M, NG)
+    pc, k = select_pc(C, OE[NG], pcs)
+    out = np.zeros(M.shape[0])
+    out[NG] = pc
+    return out, k, pcs, C
+
+
+# ------------------------------------------------------------------- TAD / DI
+def get_gap(M, min_tad, res):
+    """Get_Gap (StructureFind.py:721-751) plus the first/last-bin rule of
+    Data_preprocess (:875-883). Returns sorted int64 gap indices."""
+    M = np.asarray(M)
+    N = M.shape[0]
+    lb = int(min_tad / res)
+    t = 2 * lb * 0.8
+    gap = np.ones(N, dtype=bool)
+    for i in range(lb, N - lb):
+        gap[i] = np.count_nonzero(M[i - lb:i + lb, i]) < t
+    gap[0] = True
+    gap[N - 1] = True
+    return np.nonzero(gap)[0].astype(np.int64)
+
+
+def get_di(M, gap, w, test_type="ttest"):
+    """Get_DI (StructureFind.py:804-839) with a constant window ``w`` bins."""
+    M = np.asarray(M, dtype=np.float64)
+    N = M.shape[0]
+    g = np.zeros(N, dtype=bool)
+    g[np.asarray(gap, dtype=np.int64)] = True
+    DI = np.zeros(N)
+    for j in range(N):
+        if g[j] or j < w or j > N - w - 1:
+            continue
+        up = M[j - w:j, j][::-1]
+        down = M[j + 1:j + w + 1, j]
+        val = 0.0
+        if test_type == "ttest":
+            um, dm = up.mean(), down.mean()
+            ud = np.sum((up - um) ** 2 / (up.size * (up.size - 1)))
+            dd = np.sum((down - dm) ** 2 / (down.size * (down.size - 1)))
+            den = np.sqrt(ud + dd)
+            if den != 0:
+                val = (dm - um) / den
+        else:
+            us, ds = up.sum(), down.sum()
+            e = float(us + ds) / 2.0
+            if us != ds and e != 0:
+                val = float(ds - us) / abs(ds - us) * ((us - e) ** 2 / e + (ds - e) ** 2 / e)
+        DI[j] = val
+    return DI

@@ -1,0 +1,77 @@
+"""Known-answer tests that pin the ICE oracle (cooler restatement).
+
+cooler itself is absent: parity for ICE is unpinned by the
+reference; these analytic properties pin the restatement instead."""
+import numpy as np
+import pytest
+
+from hichap_master_amd import synth
+from oracle import ice_ref
+
+
+def _circulant_dkd(n, rng, width=6):
+    """M = D K D with K a circulant band (constant marginals off the diagonal)."""
+    d = np.exp(rng.normal(0, 0.4, size=n))
+    b1, b2, c = [], [], []
+    for i in range(n):
+        for k in range(1, width + 1):
+            j = (i + k) % n
+            a, b = min(i, j), max(i, j)
+            b1.append(a); b2.append(b); c.append(d[a] * d[b] * (1.0 / k))
+    b1, b2, c = np.array(b1), np.array(b2), np.array(c)
+    o = np.lexsort((b2, b1))
+    return b1[o], b2[o], c[o], d
+
+
+def test_dkd_recovery():
+    rng = np.random.default_rng(1)
+    n = 200
+    b1, b2, c, d = _circulant_dkd(n, rng)
+    w, st = ice_ref.balance(b1, b2, c, n, [0, n], min_nnz=0, mad_max=0, tol=1e-12, max_iters=5000)
+    assert st["converged"]
+    r = w * d
+    np.testing.assert_allclose(r / r.mean(), 1.0, rtol=1e-6)
+
+
+def test_balanced_marginals_are_one():
+    rng = np.random.default_rng(2)
+    b1, b2, c, off = synth.coo_genome([300, 200], rng, A=20.0, trans_density=0.01)
+    n = int(off[-1])
+    w, st = ice_ref.balance(b1, b2, c, n, off, max_iters=1000)
+    assert st["converged"]
+    keep = (b2 - b1) >= 1
+    bal = c[keep] * w[b1[keep]] * w[b2[keep]]
+    marg = ice_ref.marginalize(b1[keep], b2[keep], np.nan_to_num(bal), n)
+    good = np.isfinite(w)
+    np.testing.assert_allclose(marg[good], 1.0, rtol=1e-2)
+
+
+def test_uniform_matrix_constant_weights():
+    n = 50
+    i, j = np.triu_indices(n, 1)
+    w, st = ice_ref.balance(i, j, np.full(i.size, 3.0), n, [0, n], mad_max=0, min_nnz=0)
+    np.testing.assert_allclose(w, w[0], rtol=1e-12)
+    assert st["iters"] == 1
+
+
+def test_low_nnz_bin_is_masked():
+    rng = np.random.default_rng(3)
+    b1, b2, c, off = synth.coo_genome([200], rng, A=20.0, gap_frac=0.0)
+    n = int(off[-1])
+    sel = (b1 != 17) & (b2 != 17) | ((b1 == 17) & (b2 - b1 <= 3) & (b2 - b1 >= 1))
+    w, _ = ice_ref.balance(b1[sel], b2[sel], c[sel], n, off)
+    assert np.isnan(w[17])
+    assert np.isfinite(w[16])
+
+
+def test_cis_only_ignores_trans():
+    rng = np.random.default_rng(4)
+    b1, b2, c, off = synth.coo_genome([150, 120], rng, A=20.0, trans_density=0.02)
+    n = int(off[-1])
+    w, st = ice_ref.balance(b1, b2, c, n, off, cis_only=True, max_iters=1000)
+    chrom = np.repeat([0, 1], [150, 120])
+    cis = chrom[b1] == chrom[b2]
+    assert (~cis).sum() > 0
+    w2, st2 = ice_ref.balance(b1[cis], b2[cis], c[cis], n, off, cis_only=True, max_iters=1000)
+    np.testing.assert_allclose(w, w2, rtol=1e-12, equal_nan=True)
+    assert len(st["scale"]) == 2 and st["chrom_converged"].all()
