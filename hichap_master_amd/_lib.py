@@ -1,0 +1,141 @@
+"""ctypes binding of libhichap_hip.so (the C-ABI declared in
+include/hichap_hip.h).
+
+The shared library is built in-tree by ``__graft_entry__.build()`` (or
+``make -C hichap_master_amd/csrc``).  There is no CPU fallback: if the library
+is missing or no GPU is visible, every compute entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libhichap_hip.so")
+
+HH_OK = 0
+
+
+class HipLibraryError(RuntimeError):
+    """Raised when the HIP library is missing or a C-ABI call fails."""
+
+    def __init__(self, code, msg):
+        super().__init__(f"[hh rc={code}] {msg}")
+        self.code = code
+
+
+class MatrixInfo(C.Structure):
+    _fields_ = [(n, C.c_int64) for n in (
+        "n_bins", "row_lo", "row_hi", "nnz_upper", "n_entries", "n_slots", "n_chunks",
+        "n_segments", "n_ovf_chunks", "device_bytes")] + [
+        (n, C.c_int32) for n in ("n_chroms", "ignore_diags", "cis_only", "device")]
+
+
+class SynthParams(C.Structure):
+    _fields_ = [
+        ("n_chroms", C.c_int32), ("chrom_nbins", C.POINTER(C.c_int32)),
+        ("A", C.c_double), ("decay", C.c_double), ("comp_strength", C.c_double),
+        ("vis_sigma", C.c_double), ("gap_frac", C.c_double), ("trans_density", C.c_double),
+        ("comp_block", C.c_int32), ("ignore_diags", C.c_int32), ("cis_only", C.c_int32),
+        ("pad_", C.c_int32), ("seed", C.c_uint64)]
+
+
+class IceOpts(C.Structure):
+    _fields_ = [
+        ("mad_max", C.c_int32), ("min_nnz", C.c_int32), ("min_count", C.c_double),
+        ("tol", C.c_double), ("max_iters", C.c_int32), ("rescale_marginals", C.c_int32),
+        ("check_every", C.c_int32), ("pad_", C.c_int32)]
+
+
+P = C.c_void_p
+I32, I64, F64 = C.c_int32, C.c_int64, C.c_double
+PI32, PI64, PF64 = C.POINTER(C.c_int32), C.POINTER(C.c_int64), C.POINTER(C.c_double)
+
+# name -> (restype, argtypes); every function returns int status unless noted
+SIGNATURES = {
+    "hh_last_error": (C.c_char_p, []),
+    "hh_version": (C.c_int, []),
+    "hh_device_count": (C.c_int, [PI32]),
+    "hh_set_device": (C.c_int, [I32]),
+    "hh_synchronize": (C.c_int, [P]),
+    "hh_tune": (C.c_int, [C.c_char_p, I64]),
+    "hh_matrix_from_pixels": (C.c_int, [P, P, P, I64, I64, P, I32, I32, I32, I64, I64, P, C.POINTER(P)]),
+    "hh_matrix_free": (C.c_int, [P]),
+    "hh_matrix_get_info": (C.c_int, [P, C.POINTER(MatrixInfo)]),
+    "hh_matrix_export_upper": (C.c_int, [P, P, P, P, PI64]),
+    "hh_synth_count": (C.c_int, [C.POINTER(SynthParams), P, P, P]),
+    "hh_synth_build": (C.c_int, [C.POINTER(SynthParams), P, I64, I64, P, C.POINTER(P)]),
+    "hh_ice_balance": (C.c_int, [P, C.POINTER(IceOpts), P, P, P, P, P, PF64, P]),
+    "hh_ice_create": (C.c_int, [P, C.POINTER(IceOpts), C.POINTER(P)]),
+    "hh_ice_free": (C.c_int, [P]),
+    "hh_ice_n_groups": (C.c_int, [P, PI32]),
+    "hh_ice_marg_local": (C.c_int, [P, I32, P, P]),
+    "hh_ice_set_marg": (C.c_int, [P, P, I32, I64, P, P]),
+    "hh_ice_filter_nnz": (C.c_int, [P, P]),
+    "hh_ice_filter_count_mad": (C.c_int, [P, P]),
+    "hh_ice_update": (C.c_int, [P, P]),
+    "hh_ice_active_groups": (C.c_int, [P, PI32, P]),
+    "hh_ice_iterations_done": (C.c_int, [P, PI32]),
+    "hh_ice_run": (C.c_int, [P, I32, P]),
+    "hh_ice_finalize": (C.c_int, [P, P, P, P, P, P, P]),
+    "hh_ice_last_sweep_timing": (C.c_int, [P, PF64, PI32, PF64]),
+}
+
+_lib = None
+
+
+def load(path: str = LIB_PATH):
+    """Load the shared library and declare every signature (fails loudly)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise HipLibraryError(-100, f"{path} not built; run __graft_entry__.build() "
+                                    f"or `make -C hichap_master_amd/csrc`")
+    # torch-ROCm ships its own HIP runtime with the same SONAME as /opt/rocm's
+    # (libamdhip64.so.7).  Importing torch first makes that runtime the
+    # process's only one, so torch streams/allocations and this library agree.
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
+    lib = C.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def call(name, *args):
+    """Call a status-returning entry point; raise on failure."""
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if rc != HH_OK:
+        msg = lib.hh_last_error().decode(errors="replace")
+        raise HipLibraryError(rc, f"{name}: {msg}")
+    return rc
+
+
+def ptr(a):
+    """Raw pointer of a NumPy array or torch tensor (None -> NULL)."""
+    if a is None:
+        return None
+    if hasattr(a, "data_ptr"):
+        return C.c_void_p(a.data_ptr())
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def device_count() -> int:
+    n = C.c_int32(0)
+    try:
+        call("hh_device_count", C.byref(n))
+    except HipLibraryError:
+        return 0
+    return int(n.value)
+
+
+def require_gpu():
+    if device_count() < 1:
+        raise HipLibraryError(-101, "no HIP device visible: the HIP path has no CPU fallback")

@@ -1,0 +1,693 @@
+// ICE balancing on the pixel-chunk layout (cooler balance_cooler semantics,
+// oracle/ice_ref.py; HiCHap call sites matrixBuilding.py:708/713/1537/1542/
+// 1761/1766).
+//
+// One iteration:
+//   K1 k_sweep   one wave per segment (<= 8 chunks of one row): streams the
+//                packed (count, col) entries, gathers b[col], accumulates
+//                sum(count * b[col]) in fp64 -> part[seg]          [HBM bound]
+//   K2 k_marg    per local row: marg = b_r * (sum_seg part + 2 * diag * b_r)
+//                (cooler's bincount(bin1) + bincount(bin2))
+//   K3 k_stats1  per tile of 1024 bins: nonzero count and sum
+//      k_stats2  per tile: sum of squared deviations from the group mean
+//      k_update  per tile: b /= marg/mean (marg==0 -> 1); first tile of the
+//                group records var/mean/iters and the next active flag.
+// All reductions use fixed trees -> bitwise deterministic, and independent of
+// how rows are sharded across GPUs.
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <limits>
+
+#include "ice_internal.hpp"
+
+namespace hh {
+constexpr int kTile = 1024;
+constexpr int kThreads = 256;
+
+// One packed entry: count = e >> k, column = base + (e & mask).  `bb` is
+// b + base, so the gather index is a 32-bit unsigned offset.
+// ABL (timing ablations only, results wrong): 1 = no gather, 2 = gather b[base].
+template <int ABL>
+__device__ __forceinline__ double entry_dot(uint32_t e, const double* __restrict__ bb, uint32_t mask,
+                                            int k, double acc) {
+    if (ABL == 1) return acc + (double)(e >> k);
+    if (ABL == 2) return fma((double)(e >> k), bb[0], acc);
+    return fma((double)(e >> k), bb[e & mask], acc);
+}
+
+template <int U, int ABL>
+__device__ __forceinline__ double sweep_segment(const uint4* __restrict__ pay, const uint32_t* __restrict__ hdr,
+                                                int c, int c1, int lane, const double* __restrict__ b) {
+    double acc0 = 0.0, acc1 = 0.0;
+    for (; c + U <= c1; c += U) {
+        uint4 v[U];
+        uint32_t h[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            v[u] = pay[(size_t)(c + u) * 64 + lane];
+            h[u] = hdr[c + u];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int kb = (int)(h[u] >> kHdrShift);
+            const uint32_t mk = (1u << kb) - 1u;
+            const double* bb = b + (h[u] & kHdrBaseMask);
+            acc0 = entry_dot<ABL>(v[u].x, bb, mk, kb, acc0);
+            acc1 = entry_dot<ABL>(v[u].y, bb, mk, kb, acc1);
+            acc0 = entry_dot<ABL>(v[u].z, bb, mk, kb, acc0);
+            acc1 = entry_dot<ABL>(v[u].w, bb, mk, kb, acc1);
+        }
+    }
+    for (; c < c1; ++c) {
+        const uint4 v = pay[(size_t)c * 64 + lane];
+        const uint32_t h = hdr[c];
+        const int kb = (int)(h >> kHdrShift);
+        const uint32_t mk = (1u << kb) - 1u;
+        const double* bb = b + (h & kHdrBaseMask);
+        acc0 = entry_dot<ABL>(v.x, bb, mk, kb, acc0);
+        acc1 = entry_dot<ABL>(v.y, bb, mk, kb, acc1);
+        acc0 = entry_dot<ABL>(v.z, bb, mk, kb, acc0);
+        acc1 = entry_dot<ABL>(v.w, bb, mk, kb, acc1);
+    }
+    return wave_sum(acc0 + acc1);
+}
+
+// One wave per segment.
+template <int U, int ABL>
+__global__ __launch_bounds__(kThreads) void k_sweep(const uint4* __restrict__ pay,
+                                                    const uint32_t* __restrict__ hdr,
+                                                    const int32_t* __restrict__ seg_begin,
+                                                    const uint16_t* __restrict__ seg_group,
+                                                    const uint8_t* __restrict__ act, int nseg,
+                                                    const double* __restrict__ b,
+                                                    double* __restrict__ part) {
+    const int lb = (int)xcd_remap(blockIdx.x, gridDim.x);
+    const int s = __builtin_amdgcn_readfirstlane(lb * 4 + (int)(threadIdx.x >> 6));
+    if (s >= nseg) return;
+    if (act[seg_group[s]] == 0) return;
+    const int lane = threadIdx.x & 63;
+    const double acc = sweep_segment<U, ABL>(pay, hdr, seg_begin[s], seg_begin[s + 1], lane, b);
+    if (lane == 0) part[s] = acc;
+}
+
+// Persistent variant: a fixed grid; wave w of XCD-contiguous block range
+// takes segments w, w + W, ... (W = total waves).
+template <int U, int ABL>
+__global__ __launch_bounds__(kThreads) void k_sweep_persist(const uint4* __restrict__ pay,
+                                                            const uint32_t* __restrict__ hdr,
+                                                            const int32_t* __restrict__ seg_begin,
+                                                            const uint16_t* __restrict__ seg_group,
+                                                            const uint8_t* __restrict__ act, int nseg,
+                                                            const double* __restrict__ b,
+                                                            double* __restrict__ part) {
+    const int lb = (int)xcd_remap(blockIdx.x, gridDim.x);
+    const int W = (int)gridDim.x * 4;
+    const int lane = threadIdx.x & 63;
+    // contiguous ranges of segments per wave keep each XCD on nearby rows
+    const int w = __builtin_amdgcn_readfirstlane(lb * 4 + (int)(threadIdx.x >> 6));
+    const int per = (nseg + W - 1) / W;
+    const int s0 = w * per, s1 = min(nseg, s0 + per);
+    for (int s = s0; s < s1; ++s) {
+        if (act[seg_group[s]] == 0) continue;
+        const double acc = sweep_segment<U, ABL>(pay, hdr, seg_begin[s], seg_begin[s + 1], lane, b);
+        if (lane == 0) part[s] = acc;
+    }
+}
+
+__global__ void k_marg(const int32_t* __restrict__ row_seg, const double* __restrict__ part,
+                       const double* __restrict__ diag, const uint16_t* __restrict__ row_group,
+                       const uint8_t* __restrict__ act, const double* __restrict__ b, long long row_lo,
+                       int nloc, double* __restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nloc) return;
+    if (act[row_group[i]] == 0) return;
+    double s = 0.0;
+    for (int k = row_seg[i]; k < row_seg[i + 1]; ++k) s += part[k];
+    const double br = b[row_lo + i];
+    out[i] = br * fma(2.0 * diag[i], br, s);
+}
+
+__global__ void k_scatter(const double* __restrict__ g, int world, long long maxlen,
+                          const long long* __restrict__ rank_rows, double* __restrict__ marg) {
+    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (long long)world * maxlen) return;
+    const int k = (int)(t / maxlen);
+    const long long off = t - (long long)k * maxlen;
+    const long long lo = rank_rows[k], hi = rank_rows[k + 1];
+    if (lo + off < hi) marg[lo + off] = g[t];
+}
+
+__global__ void k_filter_lt(const double* __restrict__ marg, long long n, double thr,
+                            double* __restrict__ bias) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n && marg[i] < thr) bias[i] = 0.0;
+}
+
+struct TileArgs {
+    const int32_t* tile_lo;
+    const int32_t* tile_hi;
+    const int32_t* tile_group;
+    const int32_t* group_tile_ptr;
+    double* tile_cnt;
+    double* tile_sum;
+    double* tile_sq;
+};
+
+__global__ __launch_bounds__(kThreads) void k_stats1(TileArgs ta, const uint8_t* __restrict__ act,
+                                                     const double* __restrict__ marg) {
+    __shared__ double sh[16];
+    const int t = blockIdx.x;
+    if (act[ta.tile_group[t]] == 0) return;
+    double c = 0.0, s = 0.0;
+    for (int i = ta.tile_lo[t] + threadIdx.x; i < ta.tile_hi[t]; i += kThreads) {
+        const double x = marg[i];
+        if (x != 0.0) { c += 1.0; s += x; }
+    }
+    c = block_sum(c, sh);
+    s = block_sum(s, sh);
+    if (threadIdx.x == 0) { ta.tile_cnt[t] = c; ta.tile_sum[t] = s; }
+}
+
+// Group totals over the group's tiles in a fixed order (every block of the
+// group computes the identical value).
+__device__ __forceinline__ void group_totals(const TileArgs& ta, int g, double* sh, double& cnt,
+                                             double& sum, double* sq) {
+    const int t0 = ta.group_tile_ptr[g], t1 = ta.group_tile_ptr[g + 1];
+    double c = 0.0, s = 0.0, q = 0.0;
+    for (int t = t0 + threadIdx.x; t < t1; t += kThreads) {
+        c += ta.tile_cnt[t];
+        s += ta.tile_sum[t];
+        if (sq) q += ta.tile_sq[t];
+    }
+    cnt = block_sum(c, sh);
+    sum = block_sum(s, sh);
+    if (sq) *sq = block_sum(q, sh);
+}
+
+__global__ __launch_bounds__(kThreads) void k_stats2(TileArgs ta, const uint8_t* __restrict__ act,
+                                                     const double* __restrict__ marg) {
+    __shared__ double sh[16];
+    const int t = blockIdx.x;
+    const int g = ta.tile_group[t];
+    if (act[g] == 0) return;
+    double cnt, sum;
+    group_totals(ta, g, sh, cnt, sum, nullptr);
+    const double mean = sum / cnt;
+    double q = 0.0;
+    for (int i = ta.tile_lo[t] + threadIdx.x; i < ta.tile_hi[t]; i += kThreads) {
+        const double x = marg[i];
+        if (x != 0.0) { const double d = x - mean; q = fma(d, d, q); }
+    }
+    q = block_sum(q, sh);
+    if (threadIdx.x == 0) ta.tile_sq[t] = q;
+}
+
+struct GroupState {
+    double* var;
+    double* mean;
+    int32_t* iters;
+    uint8_t* empty;
+};
+
+__global__ __launch_bounds__(kThreads) void k_update(TileArgs ta, const uint8_t* __restrict__ act,
+                                                     uint8_t* __restrict__ nxt,
+                                                     const double* __restrict__ marg,
+                                                     double* __restrict__ bias, GroupState gs,
+                                                     double tol, int max_iters) {
+    __shared__ double sh[16];
+    const int t = blockIdx.x;
+    const int g = ta.tile_group[t];
+    const bool first = t == ta.group_tile_ptr[g];
+    if (act[g] == 0) {
+        if (first && threadIdx.x == 0) nxt[g] = 0;
+        return;
+    }
+    double cnt, sum, sq;
+    group_totals(ta, g, sh, cnt, sum, &sq);
+    const int lo = ta.tile_lo[t], hi = ta.tile_hi[t];
+    if (cnt == 0.0) {  // no nonzero marginal: cooler sets the group's bias to NaN
+        for (int i = lo + threadIdx.x; i < hi; i += kThreads) bias[i] = __builtin_nan("");
+        if (first && threadIdx.x == 0) {
+            gs.empty[g] = 1;
+            gs.var[g] = 0.0;
+            gs.mean[g] = __builtin_nan("");
+            gs.iters[g] += 1;
+            nxt[g] = 0;
+        }
+        return;
+    }
+    const double mean = sum / cnt;
+    const double var = sq / cnt;
+    for (int i = lo + threadIdx.x; i < hi; i += kThreads) {
+        double m = marg[i] / mean;
+        if (m == 0.0) m = 1.0;
+        bias[i] /= m;
+    }
+    if (first && threadIdx.x == 0) {
+        gs.var[g] = var;
+        gs.mean[g] = mean;
+        const int it = gs.iters[g] + 1;
+        gs.iters[g] = it;
+        nxt[g] = (var < tol || it >= max_iters) ? 0 : 1;
+    }
+}
+
+static double np_median(std::vector<double> v) {
+    if (v.empty()) return std::numeric_limits<double>::quiet_NaN();
+    const size_t k = v.size() / 2;
+    std::nth_element(v.begin(), v.begin() + k, v.end());
+    const double hi = v[k];
+    if (v.size() & 1) return hi;
+    const double lo = *std::max_element(v.begin(), v.begin() + k);
+    return (lo + hi) / 2.0;
+}
+
+static inline unsigned nblocks(long long n, int t) { return (unsigned)((n + t - 1) / t); }
+
+}  // namespace hh
+
+using namespace hh;
+
+struct hh_ice {
+    hh_matrix* m = nullptr;
+    hh_ice_opts o{};
+    int64_t n = 0, nloc = 0;
+    int32_t G = 1;
+    std::vector<int64_t> glo, ghi;
+    int32_t n_tiles = 0;
+    DBuf<int32_t> tile_lo, tile_hi, tile_group, group_tile_ptr;
+    DBuf<double> bias, marg, part, tile_cnt, tile_sum, tile_sq;
+    DBuf<uint8_t> active;  // 2 x G (parity double buffer)
+    DBuf<double> g_var, g_mean;
+    DBuf<int32_t> g_iters;
+    DBuf<uint8_t> g_empty;
+    DBuf<long long> rank_rows;
+    std::vector<int64_t> h_rank_rows;
+    int32_t iters_done = 0;
+    PinnedBuf<uint8_t> h_active;
+    // timing of the last hh_ice_run
+    std::vector<hipEvent_t> ev;
+    double sweep_ms = 0.0, iter_ms = 0.0;
+    int32_t sweep_launches = 0;
+    ~hh_ice() {
+        for (auto e : ev) (void)hipEventDestroy(e);
+    }
+    bool full() const { return m->row_lo == 0 && m->row_hi == m->n_bins; }
+    TileArgs ta() {
+        return TileArgs{tile_lo.p, tile_hi.p, tile_group.p, group_tile_ptr.p, tile_cnt.p, tile_sum.p, tile_sq.p};
+    }
+    uint8_t* act() { return active.p + (iters_done & 1) * G; }
+    uint8_t* nxt() { return active.p + (1 - (iters_done & 1)) * G; }
+};
+
+namespace hh {
+
+// Tuning knobs (hh_tune): chunks loaded per wave before their gathers,
+// persistent grid (blocks per CU, 0 = one wave per segment), ablation.
+static int g_sweep_unroll = 4;
+static int g_sweep_persist = 0;
+static int g_sweep_ablate = 0;
+
+template <int U, int ABL>
+static void launch_sweep(const ChunkLayer& L, const uint8_t* act, const double* b, double* part, hipStream_t s) {
+    const uint4* pay = reinterpret_cast<const uint4*>(L.pay.p);
+    if (g_sweep_persist > 0) {
+        const long long nb = std::min<long long>(256LL * g_sweep_persist, (L.n_segs + 3) / 4);
+        hipLaunchKernelGGL((k_sweep_persist<U, ABL>), dim3((unsigned)nb), dim3(kThreads), 0, s, pay, L.hdr.p,
+                           L.seg_begin.p, L.seg_group.p, act, (int)L.n_segs, b, part);
+    } else {
+        const long long nb = (L.n_segs + 3) / 4;
+        hipLaunchKernelGGL((k_sweep<U, ABL>), dim3((unsigned)nb), dim3(kThreads), 0, s, pay, L.hdr.p,
+                           L.seg_begin.p, L.seg_group.p, act, (int)L.n_segs, b, part);
+    }
+}
+
+template <int ABL>
+static void launch_sweep_u(const ChunkLayer& L, const uint8_t* act, const double* b, double* part, hipStream_t s) {
+    switch (g_sweep_unroll) {
+        case 1: launch_sweep<1, ABL>(L, act, b, part, s); break;
+        case 2: launch_sweep<2, ABL>(L, act, b, part, s); break;
+        case 8: launch_sweep<8, ABL>(L, act, b, part, s); break;
+        default: launch_sweep<4, ABL>(L, act, b, part, s); break;
+    }
+}
+
+static void sweep_layer(const ChunkLayer& L, const uint8_t* act, const double* b, double* part,
+                        hipStream_t s) {
+    if (L.n_segs == 0) return;
+    switch (g_sweep_ablate) {
+        case 1: launch_sweep_u<1>(L, act, b, part, s); break;
+        case 2: launch_sweep_u<2>(L, act, b, part, s); break;
+        default: launch_sweep_u<0>(L, act, b, part, s); break;
+    }
+    HIP_CHECK(hipGetLastError());
+}
+
+static void marg_weighted(hh_ice* S, double* out, hipStream_t s, bool timed, int slot) {
+    hh_matrix* m = S->m;
+    if (timed) HIP_CHECK(hipEventRecord(S->ev[2 * slot], s));
+    sweep_layer(m->main, S->act(), S->bias.p, S->part.p, s);
+    if (timed) HIP_CHECK(hipEventRecord(S->ev[2 * slot + 1], s));
+    if (S->nloc == 0) return;
+    hipLaunchKernelGGL(k_marg, dim3(nblocks(S->nloc, kThreads)), dim3(kThreads), 0, s, m->main.row_seg.p,
+                       S->part.p, m->diag.p,
+                       m->row_group.p, S->act(), S->bias.p, (long long)m->row_lo, (int)S->nloc, out);
+    HIP_CHECK(hipGetLastError());
+}
+
+static void update(hh_ice* S, hipStream_t s) {
+    TileArgs ta = S->ta();
+    if (S->n_tiles) {
+        hipLaunchKernelGGL(k_stats1, dim3(S->n_tiles), dim3(kThreads), 0, s, ta, S->act(), S->marg.p);
+        hipLaunchKernelGGL(k_stats2, dim3(S->n_tiles), dim3(kThreads), 0, s, ta, S->act(), S->marg.p);
+        GroupState gs{S->g_var.p, S->g_mean.p, S->g_iters.p, S->g_empty.p};
+        hipLaunchKernelGGL(k_update, dim3(S->n_tiles), dim3(kThreads), 0, s, ta, S->act(), S->nxt(),
+                           S->marg.p, S->bias.p, gs, S->o.tol, S->o.max_iters);
+        HIP_CHECK(hipGetLastError());
+    }
+    // groups without tiles never run; keep their flag cleared in the next buffer
+    S->iters_done += 1;
+}
+
+static void check_opts(const hh_ice_opts* o) {
+    HH_REQUIRE(o, "null options");
+    HH_REQUIRE(o->max_iters >= 1, "max_iters must be >= 1");
+    HH_REQUIRE(o->min_nnz >= 0 && o->mad_max >= 0, "negative filter threshold");
+}
+
+}  // namespace hh
+
+extern "C" {
+
+int hh_tune(const char* key, int64_t value) {
+    return guard([&] {
+        HH_REQUIRE(key, "null key");
+        const std::string k(key);
+        if (k == "sweep_unroll") {
+            HH_REQUIRE(value == 1 || value == 2 || value == 4 || value == 8, "sweep_unroll must be 1, 2, 4 or 8");
+            g_sweep_unroll = (int)value;
+        } else if (k == "sweep_persist") {
+            HH_REQUIRE(value >= 0 && value <= 64, "sweep_persist must be in [0, 64]");
+            g_sweep_persist = (int)value;
+        } else if (k == "sweep_ablate") {
+            HH_REQUIRE(value >= 0 && value <= 2, "sweep_ablate must be 0, 1 or 2");
+            g_sweep_ablate = (int)value;
+        } else {
+            HH_THROW(HH_ERR_ARG, "unknown tuning key " + k);
+        }
+    });
+}
+
+int hh_ice_create(hh_matrix* m, const hh_ice_opts* o, hh_ice** out) {
+    return guard([&] {
+        HH_REQUIRE(m && out, "null");
+        check_opts(o);
+        HIP_CHECK(hipSetDevice(m->device));
+        auto S = std::make_unique<hh_ice>();
+        S->m = m;
+        S->o = *o;
+        if (S->o.check_every <= 0) S->o.check_every = 8;
+        S->n = m->n_bins;
+        S->nloc = m->nloc();
+        if (m->cis_only) {
+            S->G = m->n_chroms;
+            for (int c = 0; c < m->n_chroms; ++c) {
+                S->glo.push_back(m->chrom_offsets[c]);
+                S->ghi.push_back(m->chrom_offsets[c + 1]);
+            }
+        } else {
+            S->G = 1;
+            S->glo = {0};
+            S->ghi = {m->n_bins};
+        }
+        std::vector<int32_t> tlo, thi, tg, gtp(S->G + 1, 0);
+        for (int g = 0; g < S->G; ++g) {
+            gtp[g] = (int32_t)tlo.size();
+            for (int64_t b = S->glo[g]; b < S->ghi[g]; b += kTile) {
+                tlo.push_back((int32_t)b);
+                thi.push_back((int32_t)std::min<int64_t>(b + kTile, S->ghi[g]));
+                tg.push_back(g);
+            }
+        }
+        gtp[S->G] = (int32_t)tlo.size();
+        S->n_tiles = (int32_t)tlo.size();
+        hipStream_t s = 0;
+        S->tile_lo = to_device(tlo, s);
+        S->tile_hi = to_device(thi, s);
+        S->tile_group = to_device(tg, s);
+        S->group_tile_ptr = to_device(gtp, s);
+        S->bias.alloc(S->n);
+        std::vector<double> ones(S->n, 1.0);
+        S->bias.upload(ones.data(), S->n, s);
+        S->marg.alloc(S->n);
+        S->marg.zero(s);
+        S->part.alloc(std::max<int64_t>(m->main.n_segs, 1));
+        S->tile_cnt.alloc(std::max(S->n_tiles, 1));
+        S->tile_sum.alloc(std::max(S->n_tiles, 1));
+        S->tile_sq.alloc(std::max(S->n_tiles, 1));
+        std::vector<uint8_t> act(2 * S->G, 0);
+        std::vector<uint8_t> emp(S->G, 0);
+        for (int g = 0; g < S->G; ++g) {
+            act[g] = gtp[g + 1] > gtp[g] ? 1 : 0;
+            emp[g] = act[g] ? 0 : 1;
+        }
+        S->active = to_device(act, s);
+        S->g_empty = to_device(emp, s);
+        S->g_var.alloc(S->G);
+        S->g_var.zero(s);
+        std::vector<double> nan(S->G, std::numeric_limits<double>::quiet_NaN());
+        S->g_mean = to_device(nan, s);
+        S->g_iters.alloc(S->G);
+        S->g_iters.zero(s);
+        S->h_active.alloc(2 * S->G);
+        HIP_CHECK(hipStreamSynchronize(s));
+        *out = S.release();
+    });
+}
+
+int hh_ice_free(hh_ice* s) {
+    return guard([&] { delete s; });
+}
+
+int hh_ice_n_groups(const hh_ice* s, int32_t* n) {
+    return guard([&] { HH_REQUIRE(s && n, "null"); *n = s->G; });
+}
+
+int hh_ice_marg_local(hh_ice* S, int32_t mode, double* marg_local, void* stream) {
+    return guard([&] {
+        HH_REQUIRE(S, "null");
+        HH_REQUIRE(mode >= 0 && mode <= 2, "mode must be 0, 1 or 2");
+        HH_REQUIRE(marg_local || S->full(), "marg_local required for a sharded matrix");
+        hipStream_t s = as_stream(stream);
+        double* out = marg_local ? marg_local : S->marg.p + S->m->row_lo;
+        if (mode == 2) {
+            marg_weighted(S, out, s, false, 0);
+        } else {
+            const DBuf<double>& src = mode == 0 ? S->m->row_nnz2 : S->m->row_sum2;
+            if (S->nloc)
+                HIP_CHECK(hipMemcpyAsync(out, src.p, S->nloc * sizeof(double), hipMemcpyDeviceToDevice, s));
+        }
+    });
+}
+
+int hh_ice_set_marg(hh_ice* S, const double* gathered, int32_t world, int64_t maxlen,
+                    const int64_t* rank_rows, void* stream) {
+    return guard([&] {
+        HH_REQUIRE(S && gathered && rank_rows && world >= 1 && maxlen >= 0, "bad arguments");
+        hipStream_t s = as_stream(stream);
+        std::vector<int64_t> rr(rank_rows, rank_rows + world + 1);
+        HH_REQUIRE(rr[0] == 0 && rr[world] == S->n, "rank_rows must span [0, n_bins]");
+        for (int k = 0; k < world; ++k) HH_REQUIRE(rr[k + 1] - rr[k] <= maxlen && rr[k] <= rr[k + 1], "bad rank_rows");
+        if (rr != S->h_rank_rows) {
+            HIP_CHECK(hipStreamSynchronize(s));
+            S->h_rank_rows = rr;
+            std::vector<long long> ll(rr.begin(), rr.end());
+            S->rank_rows = to_device(ll, s);
+        }
+        const long long tot = (long long)world * maxlen;
+        if (tot)
+            hipLaunchKernelGGL(k_scatter, dim3(nblocks(tot, kThreads)), dim3(kThreads), 0, s, gathered, world,
+                               (long long)maxlen, S->rank_rows.p, S->marg.p);
+        HIP_CHECK(hipGetLastError());
+    });
+}
+
+int hh_ice_filter_nnz(hh_ice* S, void* stream) {
+    return guard([&] {
+        HH_REQUIRE(S, "null");
+        if (S->o.min_nnz > 0)
+            hipLaunchKernelGGL(k_filter_lt, dim3(nblocks(S->n, kThreads)), dim3(kThreads), 0, as_stream(stream),
+                               S->marg.p, (long long)S->n, (double)S->o.min_nnz, S->bias.p);
+        HIP_CHECK(hipGetLastError());
+    });
+}
+
+int hh_ice_filter_count_mad(hh_ice* S, void* stream) {
+    return guard([&] {
+        HH_REQUIRE(S, "null");
+        hipStream_t s = as_stream(stream);
+        if (S->o.min_count != 0.0)
+            hipLaunchKernelGGL(k_filter_lt, dim3(nblocks(S->n, kThreads)), dim3(kThreads), 0, s, S->marg.p,
+                               (long long)S->n, S->o.min_count, S->bias.p);
+        HIP_CHECK(hipGetLastError());
+        if (S->o.mad_max <= 0) return;
+        // MAD-max filter (cooler balance_cooler): per-chromosome median
+        // normalisation of the raw marginal, then a log-MAD cutoff.  O(n) host
+        // work with numpy's median semantics; run once per balance.
+        std::vector<double> marg(S->n), bias(S->n);
+        S->marg.download(marg.data(), S->n, s);
+        S->bias.download(bias.data(), S->n, s);
+        HIP_CHECK(hipStreamSynchronize(s));
+        const auto& off = S->m->chrom_offsets;
+        std::vector<double> pos;
+        for (int c = 0; c < S->m->n_chroms; ++c) {
+            pos.clear();
+            for (int64_t i = off[c]; i < off[c + 1]; ++i)
+                if (marg[i] > 0) pos.push_back(marg[i]);
+            const double med = np_median(pos);
+            for (int64_t i = off[c]; i < off[c + 1]; ++i) marg[i] = marg[i] / med;
+        }
+        std::vector<double> logm;
+        for (double x : marg)
+            if (x > 0) logm.push_back(std::log(x));
+        const double med = np_median(logm);
+        std::vector<double> dev(logm.size());
+        for (size_t k = 0; k < logm.size(); ++k) dev[k] = std::fabs(logm[k] - med);
+        const double cutoff = std::exp(med - S->o.mad_max * np_median(dev));
+        for (int64_t i = 0; i < S->n; ++i)
+            if (marg[i] < cutoff) bias[i] = 0.0;
+        S->bias.upload(bias.data(), S->n, s);
+        HIP_CHECK(hipStreamSynchronize(s));
+    });
+}
+
+int hh_ice_update(hh_ice* S, void* stream) {
+    return guard([&] {
+        HH_REQUIRE(S, "null");
+        update(S, as_stream(stream));
+    });
+}
+
+int hh_ice_active_groups(hh_ice* S, int32_t* n_active, void* stream) {
+    return guard([&] {
+        HH_REQUIRE(S && n_active, "null");
+        hipStream_t s = as_stream(stream);
+        HIP_CHECK(hipMemcpyAsync(S->h_active.p, S->act(), S->G, hipMemcpyDeviceToHost, s));
+        HIP_CHECK(hipStreamSynchronize(s));
+        int a = 0;
+        for (int g = 0; g < S->G; ++g) a += S->h_active.p[g] ? 1 : 0;
+        *n_active = a;
+    });
+}
+
+int hh_ice_iterations_done(const hh_ice* S, int32_t* iters) {
+    return guard([&] { HH_REQUIRE(S && iters, "null"); *iters = S->iters_done; });
+}
+
+int hh_ice_run(hh_ice* S, int32_t n, void* stream) {
+    return guard([&] {
+        HH_REQUIRE(S && n >= 0, "bad arguments");
+        HH_REQUIRE(S->full(), "hh_ice_run needs a matrix holding every row (use the sharded API)");
+        hipStream_t s = as_stream(stream);
+        const size_t need = 2 * (size_t)n + 2;
+        while (S->ev.size() < need) {
+            hipEvent_t e;
+            HIP_CHECK(hipEventCreate(&e));
+            S->ev.push_back(e);
+        }
+        HIP_CHECK(hipEventRecord(S->ev[2 * n], s));
+        for (int k = 0; k < n; ++k) {
+            marg_weighted(S, S->marg.p, s, true, k);
+            update(S, s);
+        }
+        HIP_CHECK(hipEventRecord(S->ev[2 * n + 1], s));
+        HIP_CHECK(hipStreamSynchronize(s));
+        double tot = 0.0;
+        for (int k = 0; k < n; ++k) {
+            float ms = 0.f;
+            HIP_CHECK(hipEventElapsedTime(&ms, S->ev[2 * k], S->ev[2 * k + 1]));
+            tot += ms;
+        }
+        float all = 0.f;
+        HIP_CHECK(hipEventElapsedTime(&all, S->ev[2 * n], S->ev[2 * n + 1]));
+        S->sweep_ms = tot;
+        S->iter_ms = all;
+        S->sweep_launches = n;
+    });
+}
+
+int hh_ice_last_sweep_timing(const hh_ice* S, double* sweep_ms_total, int32_t* sweep_launches,
+                             double* iter_ms_total) {
+    return guard([&] {
+        HH_REQUIRE(S, "null");
+        if (sweep_ms_total) *sweep_ms_total = S->sweep_ms;
+        if (sweep_launches) *sweep_launches = S->sweep_launches;
+        if (iter_ms_total) *iter_ms_total = S->iter_ms;
+    });
+}
+
+int hh_ice_finalize(hh_ice* S, double* weights, double* scale, double* var, int32_t* iters,
+                    int32_t* converged, void* stream) {
+    return guard([&] {
+        HH_REQUIRE(S && weights, "null");
+        hipStream_t s = as_stream(stream);
+        const int G = S->G;
+        std::vector<double> b(S->n), gm(G), gv(G);
+        std::vector<int32_t> gi(G);
+        std::vector<uint8_t> ge(G);
+        S->bias.download(b.data(), S->n, s);
+        S->g_mean.download(gm.data(), G, s);
+        S->g_var.download(gv.data(), G, s);
+        S->g_iters.download(gi.data(), G, s);
+        S->g_empty.download(ge.data(), G, s);
+        HIP_CHECK(hipStreamSynchronize(s));
+        for (int g = 0; g < G; ++g) {
+            const double sc = gm[g];
+            for (int64_t i = S->glo[g]; i < S->ghi[g]; ++i) {
+                if (b[i] == 0.0) b[i] = std::numeric_limits<double>::quiet_NaN();
+                if (S->o.rescale_marginals) b[i] /= std::sqrt(sc);
+            }
+            if (scale) scale[g] = sc;
+            if (var) var[g] = gv[g];
+            if (iters) iters[g] = gi[g];
+            if (converged) converged[g] = gv[g] < S->o.tol ? 1 : 0;
+        }
+        std::copy(b.begin(), b.end(), weights);
+    });
+}
+
+int hh_ice_balance(hh_matrix* m, const hh_ice_opts* o, double* weights, double* scale, double* var,
+                   int32_t* iters, int32_t* converged, double* sweep_seconds, void* stream) {
+    hh_ice* S = nullptr;
+    int rc = hh_ice_create(m, o, &S);
+    if (rc) return rc;
+    rc = guard([&] {
+        HH_REQUIRE(S->full(), "hh_ice_balance needs a matrix holding every row");
+        auto ok = [](int r) { if (r) throw Error(r, hh_last_error()); };
+        ok(hh_ice_marg_local(S, 0, nullptr, stream));
+        ok(hh_ice_filter_nnz(S, stream));
+        ok(hh_ice_marg_local(S, 1, nullptr, stream));
+        ok(hh_ice_filter_count_mad(S, stream));
+        HIP_CHECK(hipStreamSynchronize(as_stream(stream)));
+        const auto t0 = std::chrono::steady_clock::now();
+        while (S->iters_done < S->o.max_iters) {
+            const int k = std::min(S->o.check_every, S->o.max_iters - S->iters_done);
+            hipStream_t s = as_stream(stream);
+            for (int j = 0; j < k; ++j) {
+                marg_weighted(S, S->marg.p, s, false, 0);
+                update(S, s);
+            }
+            int32_t na = 0;
+            ok(hh_ice_active_groups(S, &na, stream));
+            if (na == 0) break;
+        }
+        const auto t1 = std::chrono::steady_clock::now();
+        if (sweep_seconds) *sweep_seconds = std::chrono::duration<double>(t1 - t0).count();
+        ok(hh_ice_finalize(S, weights, scale, var, iters, converged, stream));
+    });
+    hh_ice_free(S);
+    return rc;
+}
+
+}  // extern "C"

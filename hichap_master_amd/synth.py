@@ -144,3 +144,65 @@ def coo_to_dense(bin1, bin2, count, n):
     M[bin1, bin2] = count
     M[bin2, bin1] = count
     return M
+
+
+# ----------------------------------------------------- device-generator model
+HG19_ORDER = [str(i) for i in range(1, 23)] + ["X"]
+
+
+def genome_bins(res, diploid=False, chroms=None):
+    """Per-chromosome bin counts (HiCHap's ``l // res + 1``) for hg19 chr1-22,X;
+    diploid = maternal copies then paternal copies (matrixBuilding.py:429-454)."""
+    chroms = chroms or HG19_ORDER
+    nb = chrom_bins([HG19[c] for c in chroms], res)
+    return nb + nb if diploid else nb
+
+
+def _modulation_samples(k=4096, vis_sigma=0.3, comp=0.3, seed=0):
+    rng = np.random.default_rng(seed)
+    v = np.exp(vis_sigma * rng.normal(size=(2, k)))
+    s = np.where(rng.random(k) < 0.5, 1.0 + comp, 1.0 - comp)
+    return v[0] * v[1] * s, float(np.mean(v[0] * v[1]))
+
+
+def expected_nnz(chrom_nbins, A, trans_density=0.0, decay=1.08, vis_sigma=0.3, comp=0.3,
+                 gap_frac=0.02, ignore_diags=1):
+    """Expected upper-triangle pixel count of the device generator's model
+    (hh_synth_*): sum over cis distances of P(Poisson(lambda) > 0), plus the
+    uniform trans density.  Used to pick ``A`` for a target nnz."""
+    nb = np.asarray(chrom_nbins, dtype=np.int64)
+    m, ev = _modulation_samples(vis_sigma=vis_sigma, comp=comp)
+    L = int(nb.max())
+    d = np.arange(max(ignore_diags, 1), L)
+    # pairs at distance d summed over chromosomes
+    pairs = np.zeros(d.size)
+    for Lc in nb:
+        pairs[: max(Lc - d[0], 0)] += Lc - d[: max(Lc - d[0], 0)]
+    # P(count > 0) is smooth in d: evaluate on a log grid and interpolate
+    grid = np.unique(np.round(np.geomspace(d[0], d[-1] if d.size else 1, 256)).astype(np.int64))
+    lam = A * (grid[:, None] + 1.0) ** -decay * m[None, :]
+    pg = np.mean(-np.expm1(-lam), axis=1)
+    p = np.interp(d, grid, pg)
+    keep = (1 - gap_frac) ** 2
+    cis = float(np.sum(pairs * p)) * keep
+    tot = float(nb.sum())
+    trans_pairs = (tot * tot - float(np.sum(nb.astype(np.float64) ** 2))) / 2.0
+    trans = trans_density * ev * keep * trans_pairs
+    return cis, trans
+
+
+def calibrate(chrom_nbins, target_nnz, trans_frac=0.0, **kw):
+    """(A, trans_density) whose expected nnz is ``target_nnz`` with the given
+    trans fraction."""
+    nb = np.asarray(chrom_nbins, dtype=np.float64)
+    _, ev = _modulation_samples()
+    keep = (1 - kw.get("gap_frac", 0.02)) ** 2
+    trans_pairs = (nb.sum() ** 2 - np.sum(nb ** 2)) / 2.0
+    tdens = trans_frac * target_nnz / (ev * keep * trans_pairs) if trans_frac > 0 else 0.0
+    want = target_nnz * (1.0 - trans_frac)
+    lo, hi = 1e-2, 1e6
+    for _ in range(48):
+        mid = np.sqrt(lo * hi)
+        c, _ = expected_nnz(chrom_nbins, mid, 0.0, **kw)
+        lo, hi = (mid, hi) if c < want else (lo, mid)
+    return float(np.sqrt(lo * hi)), float(tdens)

@@ -1,0 +1,178 @@
+/*
+ * hichap_hip.h — C-ABI of libhichap_hip.so, the MI355X (gfx950) hot path of
+ * HiCHap's bias correction and structure analysis.
+ *
+ * Plain C types only (no torch / HIP types in signatures: streams are passed
+ * as `void*` = hipStream_t, device buffers as plain pointers).  Every entry
+ * point returns HH_OK (0) or a negative HH_ERR_* code; on error the message is
+ * available from hh_last_error() (thread-local) and output buffers are left
+ * untouched.  No C++ exception crosses this boundary.
+ *
+ * What each entry point replaces in the reference (/root/reference):
+ *   ICE                 `cooler balance --ignore-diags 1 [--cis-only] --force`
+ *                       subprocess strings, HiCHap/matrixBuilding.py:708, :713,
+ *                       :1537, :1542, :1761, :1766 (algorithm: cooler.balance,
+ *                       third-party, see oracle/ice_ref.py)
+ *   hh_twostep          TwoStepCorrection, matrixBuilding.py:984-1023
+ *   hh_genomewide_*     GenomeWideMatrixCorrection, matrixBuilding.py:857-901
+ *   hh_compartment_*    StructureFind.Distance_Decay / Get_PCA / Select_PC_new,
+ *                       StructureFind.py:201-423
+ *   hh_di_scan          StructureFind.Get_Gap / Get_DI, StructureFind.py:721-839
+ */
+#ifndef HICHAP_HIP_H
+#define HICHAP_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HH_OK 0
+#define HH_ERR_ARG -1   /* invalid argument / unsupported input            */
+#define HH_ERR_HIP -2   /* HIP runtime error                               */
+#define HH_ERR_OOM -3   /* device or host allocation failed                */
+#define HH_ERR_STATE -4 /* call not valid in the object's current state    */
+
+/* ------------------------------------------------------------ runtime */
+const char* hh_last_error(void);
+int hh_version(void);                 /* (major<<16)|(minor<<8)|patch */
+int hh_device_count(int32_t* n);
+int hh_set_device(int32_t device);
+int hh_synchronize(void* stream);
+/* Performance knobs (no effect on results): "sweep_unroll" in {1,2,4,8}. */
+int hh_tune(const char* key, int64_t value);
+
+/* ---------------------------------------------------- contact matrix
+ * A contact matrix resident in HBM in the "pixel-chunk" layout:
+ * the symmetric matrix (both triangles of cooler's upper-triangle pixel table)
+ * stored row by row for the rows [row_lo, row_hi) a rank owns, each row cut
+ * into chunks of 256 entries packed as uint32 (count:16 | col - base:16) with
+ * one int32 base column per chunk, plus an overflow layer for counts >= 2^16
+ * and a per-row diagonal.  Static filters (ignore_diags, cis_only zero_trans,
+ * zero counts) are applied at build time.
+ */
+typedef struct hh_matrix hh_matrix;
+
+typedef struct {
+    int64_t n_bins;        /* bins of the whole matrix                       */
+    int64_t row_lo, row_hi;/* rows held by this object                      */
+    int64_t nnz_upper;     /* kept pixels with bin2 - bin1 >= ignore_diags   */
+    int64_t n_entries;     /* symmetric off-diagonal entries stored          */
+    int64_t n_slots;       /* chunk slots (entries + padding)                */
+    int64_t n_chunks;
+    int64_t n_segments;
+    int64_t n_ovf_chunks;  /* chunks of the >= 2^16 overflow layer          */
+    int64_t device_bytes;  /* HBM held by the matrix                         */
+    int32_t n_chroms;
+    int32_t ignore_diags;
+    int32_t cis_only;
+    int32_t device;
+} hh_matrix_info;
+
+/* Build from cooler's pixel table (upper triangle bin1 <= bin2; any order,
+ * sorted input is fastest).  Counts must be non-negative integers < 2^32
+ * (cooler `count`, int32 in HiCHap's traditional coolers, matrixBuilding.py:196).
+ * chrom_offsets[n_chroms+1] = cooler `indexes/chrom_offset`. Rows outside
+ * [row_lo, row_hi) are not stored (a shard for multi-GPU genome-wide ICE). */
+int hh_matrix_from_pixels(const int64_t* bin1, const int64_t* bin2, const double* count,
+                          int64_t nnz, int64_t n_bins, const int64_t* chrom_offsets,
+                          int32_t n_chroms, int32_t ignore_diags, int32_t cis_only,
+                          int64_t row_lo, int64_t row_hi, void* stream, hh_matrix** out);
+int hh_matrix_free(hh_matrix* m);
+int hh_matrix_get_info(const hh_matrix* m, hh_matrix_info* info);
+/* Copy the stored upper-triangle pixels (bin1 <= bin2, bin1 in the local rows
+ * for which bin1 is the row) back to the host; *nnz_inout = capacity on entry,
+ * count on exit.  For checking only. */
+int hh_matrix_export_upper(const hh_matrix* m, int64_t* bin1, int64_t* bin2, double* count,
+                           int64_t* nnz_inout);
+
+/* Synthetic whole-genome contact matrices generated directly in HBM
+ * (SURVEY.md §8(d) model; counter-based hashing keyed on the unordered bin
+ * pair, so every shard of every rank sees the same matrix). */
+typedef struct {
+    int32_t n_chroms;
+    const int32_t* chrom_nbins; /* host array [n_chroms]                     */
+    double A;                   /* cis amplitude                              */
+    double decay;               /* power-law exponent (1.08)                  */
+    double comp_strength;       /* 0.3                                        */
+    double vis_sigma;           /* log-normal visibility sigma (0.3)          */
+    double gap_frac;            /* fraction of empty bins (0.02)              */
+    double trans_density;       /* uniform trans pixel density                */
+    int32_t comp_block;         /* compartment block length in bins           */
+    int32_t ignore_diags;
+    int32_t cis_only;
+    int32_t pad_;
+    uint64_t seed;
+} hh_synth_params;
+
+/* Pass 1 over ALL rows: per-row chunk counts and upper-triangle pixel counts
+ * (host arrays of n_bins). Used to partition rows across ranks. */
+int hh_synth_count(const hh_synth_params* p, int32_t* row_chunks, int64_t* row_nnz_upper,
+                   void* stream);
+/* Pass 2: build rows [row_lo, row_hi) using the pass-1 chunk counts. */
+int hh_synth_build(const hh_synth_params* p, const int32_t* row_chunks, int64_t row_lo,
+                   int64_t row_hi, void* stream, hh_matrix** out);
+
+/* ---------------------------------------------------------------- ICE
+ * cooler's balance_cooler semantics (oracle/ice_ref.py). */
+typedef struct {
+    int32_t mad_max;           /* 5                                         */
+    int32_t min_nnz;           /* 10                                        */
+    double min_count;          /* 0                                         */
+    double tol;                /* 1e-5                                      */
+    int32_t max_iters;         /* 200                                       */
+    int32_t rescale_marginals; /* 1                                         */
+    int32_t check_every;       /* host polls convergence every k sweeps (0=8)*/
+    int32_t pad_;
+} hh_ice_opts;
+
+/* One-call balance on one GPU (the matrix must hold every row).
+ * weights[n_bins] (host) receive cooler's bins/weight (NaN = masked).
+ * Per group (1 group genome-wide, n_chroms groups when cis_only):
+ * scale[], var[], iters[], converged[] (host arrays).
+ * sweep_seconds (may be NULL) = wall time of the iteration loop only. */
+int hh_ice_balance(hh_matrix* m, const hh_ice_opts* o, double* weights, double* scale,
+                   double* var, int32_t* iters, int32_t* converged, double* sweep_seconds,
+                   void* stream);
+
+/* Fine-grained device API used by the multi-GPU driver (one process per GPU;
+ * the marginal vector is exchanged with an all-gather over RCCL by the
+ * caller).  All calls are asynchronous on `stream` unless noted. */
+typedef struct hh_ice hh_ice;
+int hh_ice_create(hh_matrix* m, const hh_ice_opts* o, hh_ice** out);
+int hh_ice_free(hh_ice* s);
+int hh_ice_n_groups(const hh_ice* s, int32_t* n);
+/* mode: 0 = binarized (nnz), 1 = raw counts, 2 = count*b_i*b_j.
+ * Writes the marginal of the local rows to marg_local[row_hi - row_lo]
+ * (device).  When the matrix holds every row, marg_local may be NULL and the
+ * result lands in the internal full marginal directly. */
+int hh_ice_marg_local(hh_ice* s, int32_t mode, double* marg_local, void* stream);
+/* Scatter an all-gathered, per-rank padded marginal (world x maxlen, device)
+ * into the internal full marginal; rank_rows[world+1] host row offsets. */
+int hh_ice_set_marg(hh_ice* s, const double* gathered, int32_t world, int64_t maxlen,
+                    const int64_t* rank_rows, void* stream);
+/* Filters (after set_marg of the matching mode).  mad uses host medians:
+ * synchronous. */
+int hh_ice_filter_nnz(hh_ice* s, void* stream);
+int hh_ice_filter_count_mad(hh_ice* s, void* stream);
+/* One ICE update after set_marg(mode 2): variance, bias update, convergence. */
+int hh_ice_update(hh_ice* s, void* stream);
+/* Number of still-active groups (synchronous). */
+int hh_ice_active_groups(hh_ice* s, int32_t* n_active, void* stream);
+int hh_ice_iterations_done(const hh_ice* s, int32_t* iters);
+/* Full sweeps on one GPU without host polling (bench / single-GPU): runs
+ * `n` iterations of marg(mode 2) + update back to back. */
+int hh_ice_run(hh_ice* s, int32_t n, void* stream);
+/* Final weights + stats (synchronous), as hh_ice_balance. */
+int hh_ice_finalize(hh_ice* s, double* weights, double* scale, double* var, int32_t* iters,
+                    int32_t* converged, void* stream);
+/* Kernel timing of the last hh_ice_run (HIP events on the run's stream):
+ * total ms of the sweep kernel, launches. */
+int hh_ice_last_sweep_timing(const hh_ice* s, double* sweep_ms_total, int32_t* sweep_launches,
+                             double* iter_ms_total);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HICHAP_HIP_H */

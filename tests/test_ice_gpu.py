@@ -1,0 +1,179 @@
+"""ICE on the GPU (through the C-ABI) against the CPU oracle."""
+import numpy as np
+import pytest
+
+from hichap_master_amd import synth
+from oracle import ice_ref
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ice():
+    from hichap_master_amd import _lib, ice as ice_mod
+    _lib.require_gpu()
+    return ice_mod
+
+
+def _case(seed, sizes=(400, 300), A=25.0, trans=0.01, **kw):
+    rng = np.random.default_rng(seed)
+    return synth.coo_genome(list(sizes), rng, A=A, trans_density=trans, **kw)
+
+
+def _filtered_upper(b1, b2, c, off, ignore_diags, cis_only):
+    chrom = np.repeat(np.arange(len(off) - 1), np.diff(off))
+    keep = (c != 0) & (b2 - b1 >= ignore_diags)
+    if cis_only:
+        keep &= chrom[b1] == chrom[b2]
+    o = np.lexsort((b2[keep], b1[keep]))
+    return b1[keep][o], b2[keep][o], c[keep][o].astype(np.float64)
+
+
+@pytest.mark.parametrize("ignore_diags,cis_only", [(1, False), (0, False), (2, True)])
+def test_export_roundtrip(ice, ignore_diags, cis_only):
+    b1, b2, c, off = _case(1)
+    n = int(off[-1])
+    m = ice.ContactMatrix.from_pixels(b1, b2, c, n, off, ignore_diags, cis_only)
+    e1, e2, ec = m.export_upper()
+    f1, f2, fc = _filtered_upper(b1, b2, c, off, ignore_diags, cis_only)
+    np.testing.assert_array_equal(e1, f1)
+    np.testing.assert_array_equal(e2, f2)
+    np.testing.assert_array_equal(ec, fc)
+    assert m.info()["nnz_upper"] == f1.size
+
+
+@pytest.mark.parametrize("seed", [2, 3])
+@pytest.mark.parametrize("cis_only", [False, True])
+def test_balance_matches_oracle(ice, seed, cis_only):
+    b1, b2, c, off = _case(seed, sizes=(500, 350, 200))
+    n = int(off[-1])
+    w, st = ice.balance(b1, b2, c, n, off, cis_only=cis_only, max_iters=500)
+    wr, sr = ice_ref.balance(b1, b2, c, n, off, cis_only=cis_only, max_iters=500)
+    np.testing.assert_array_equal(np.isnan(w), np.isnan(wr))
+    np.testing.assert_allclose(w, wr, rtol=1e-9, equal_nan=True)
+    np.testing.assert_allclose(st["scale"], sr["scale"], rtol=1e-9)
+    np.testing.assert_array_equal(st["iters"], sr["iters"])
+    assert st["converged"] == sr["converged"]
+
+
+def test_balance_unconverged_cap(ice):
+    b1, b2, c, off = _case(4)
+    n = int(off[-1])
+    w, st = ice.balance(b1, b2, c, n, off, max_iters=7)
+    wr, sr = ice_ref.balance(b1, b2, c, n, off, max_iters=7)
+    assert st["iters"] == 7 and not st["converged"]
+    np.testing.assert_allclose(st["var"], sr["var"], rtol=1e-9)
+    np.testing.assert_allclose(w, wr, rtol=1e-10, equal_nan=True)
+
+
+def test_large_counts(ice):
+    """Counts up to 2^32-1 fit: a chunk's (count, column-offset) bit split adapts."""
+    b1, b2, c, off = _case(5, sizes=(300,), A=40.0, trans=0.0)
+    c = c.astype(np.int64)
+    rng = np.random.default_rng(0)
+    big = rng.random(c.size) < 0.05
+    c[big] = c[big] * 40000 + rng.integers(0, 70000, size=big.sum())
+    c[np.argmax(c)] = 2**32 - 1
+    n = int(off[-1])
+    m = ice.ContactMatrix.from_pixels(b1, b2, c, n, off)
+    _, _, ec = m.export_upper()
+    f1, f2, fc = _filtered_upper(b1, b2, c, off, 1, False)
+    np.testing.assert_array_equal(ec, fc)
+    w, st = ice.balance_matrix(m, ice.IceOptions(max_iters=300))
+    wr, sr = ice_ref.balance(b1, b2, c, n, off, max_iters=300)
+    np.testing.assert_allclose(w, wr, rtol=1e-9, equal_nan=True)
+
+
+def test_diag_kept_and_unsorted_input(ice):
+    b1, b2, c, off = _case(6, sizes=(250,), trans=0.0)
+    perm = np.random.default_rng(1).permutation(b1.size)
+    n = int(off[-1])
+    w, st = ice.balance(b1[perm], b2[perm], c[perm], n, off, ignore_diags=0, max_iters=400)
+    wr, sr = ice_ref.balance(b1, b2, c, n, off, ignore_diags=0, max_iters=400)
+    np.testing.assert_allclose(w, wr, rtol=1e-9, equal_nan=True)
+
+
+def test_empty_chromosome_cis_only(ice):
+    b1, b2, c, off = _case(7, sizes=(200, 60, 150), trans=0.0)
+    chrom = np.repeat(np.arange(3), np.diff(off))
+    keep = chrom[b1] != 1
+    n = int(off[-1])
+    w, st = ice.balance(b1[keep], b2[keep], c[keep], n, off, cis_only=True, max_iters=400)
+    wr, sr = ice_ref.balance(b1[keep], b2[keep], c[keep], n, off, cis_only=True, max_iters=400)
+    assert np.isnan(w[200:260]).all()
+    np.testing.assert_allclose(w, wr, rtol=1e-9, equal_nan=True)
+    assert np.isnan(st["scale"][1]) and np.isnan(sr["scale"][1])
+
+
+def test_invalid_counts_rejected(ice):
+    from hichap_master_amd._lib import HipLibraryError
+    with pytest.raises(HipLibraryError):
+        ice.ContactMatrix.from_pixels([0, 1], [5, 6], [1.5, 2.0], 10, [0, 10])
+    with pytest.raises(HipLibraryError):
+        ice.ContactMatrix.from_pixels([0, 1], [5, 60], [1, 2], 10, [0, 10])
+
+
+def test_sharded_equals_full_bitwise(ice):
+    """Two row shards on one GPU with a manual gather == the one-shard run."""
+    import torch
+    from hichap_master_amd import dist
+    b1, b2, c, off = _case(8, sizes=(500, 400))
+    n = int(off[-1])
+    opts = ice.IceOptions(max_iters=300)
+    w_full, st_full = ice.balance(b1, b2, c, n, off, max_iters=300)
+    rr = dist.partition_rows(np.bincount(b1, minlength=n) + np.bincount(b2, minlength=n), 2)
+    shards = [ice.ContactMatrix.from_pixels(b1, b2, c, n, off, row_range=(rr[k], rr[k + 1])) for k in range(2)]
+    states = [ice.IceState(m, opts) for m in shards]
+    maxlen = int(np.max(np.diff(rr)))
+    loc = [torch.zeros(maxlen, dtype=torch.float64, device="cuda") for _ in range(2)]
+    gat = torch.zeros(2 * maxlen, dtype=torch.float64, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+
+    def exchange(mode):
+        for k in range(2):
+            states[k].marg_local(mode, loc[k], s)
+        for k in range(2):
+            gat[k * maxlen:(k + 1) * maxlen].copy_(loc[k])
+        for k in range(2):
+            states[k].set_marg(gat, 2, maxlen, rr, s)
+    exchange(0)
+    for st_ in states:
+        st_.filter_nnz(s)
+    exchange(1)
+    for st_ in states:
+        st_.filter_count_mad(s)
+    for it in range(300):
+        exchange(2)
+        for st_ in states:
+            st_.update(s)
+        if it % 8 == 7 and states[0].active_groups(s) == 0:
+            break
+    w0, s0 = states[0].finalize(s)
+    w1, s1 = states[1].finalize(s)
+    np.testing.assert_array_equal(w0, w1)
+    np.testing.assert_array_equal(w0, w_full)
+    assert s0["iters"] == st_full["iters"]
+
+
+def test_synthetic_generator_matches_oracle(ice):
+    sizes = [700, 500, 300]
+    kw = dict(A=40.0, trans_density=0.002, comp_block=50, seed=11)
+    m = ice.ContactMatrix.synthetic(sizes, **kw)
+    inf = m.info()
+    b1, b2, c = m.export_upper()
+    assert inf["nnz_upper"] == b1.size
+    assert (b2 - b1 >= 1).all()
+    # symmetric storage: every pixel appears in both rows -> entries = 2 * pixels
+    assert inf["n_entries"] == 2 * b1.size
+    # shards see the same matrix
+    rc, ru = ice.synth_row_counts(sizes, **kw)
+    half = ice.ContactMatrix.synthetic(sizes, row_range=(0, 800), row_chunks=rc, **kw)
+    h1, h2, hc = half.export_upper()
+    sel = b1 < 800
+    np.testing.assert_array_equal(h1, b1[sel]); np.testing.assert_array_equal(h2, b2[sel])
+    np.testing.assert_array_equal(hc, c[sel])
+    off = m.chrom_offsets
+    w, st = ice.balance_matrix(m, ice.IceOptions(max_iters=400))
+    wr, sr = ice_ref.balance(b1, b2, c, int(off[-1]), off, max_iters=400)
+    np.testing.assert_allclose(w, wr, rtol=1e-9, equal_nan=True)
+    assert st["iters"] == sr["iters"]
