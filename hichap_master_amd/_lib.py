@@ -26,8 +26,8 @@ class HipLibraryError(RuntimeError):
 
 class MatrixInfo(C.Structure):
     _fields_ = [(n, C.c_int64) for n in (
-        "n_bins", "row_lo", "row_hi", "nnz_upper", "n_entries", "n_slots", "n_chunks",
-        "n_segments", "n_ovf_chunks", "device_bytes")] + [
+        "n_bins", "row_lo", "row_hi", "nnz_upper", "n_entries", "n_slots", "n_tiles",
+        "n_units", "n_wide", "device_bytes")] + [
         (n, C.c_int32) for n in ("n_chroms", "ignore_diags", "cis_only", "device")]
 
 
@@ -64,7 +64,7 @@ SIGNATURES = {
     "hh_matrix_get_info": (C.c_int, [P, C.POINTER(MatrixInfo)]),
     "hh_matrix_export_upper": (C.c_int, [P, P, P, P, PI64]),
     "hh_synth_count": (C.c_int, [C.POINTER(SynthParams), P, P, P]),
-    "hh_synth_build": (C.c_int, [C.POINTER(SynthParams), P, I64, I64, P, C.POINTER(P)]),
+    "hh_synth_build": (C.c_int, [C.POINTER(SynthParams), I64, I64, P, C.POINTER(P)]),
     "hh_ice_balance": (C.c_int, [P, C.POINTER(IceOpts), P, P, P, P, P, PF64, P]),
     "hh_ice_create": (C.c_int, [P, C.POINTER(IceOpts), C.POINTER(P)]),
     "hh_ice_free": (C.c_int, [P]),

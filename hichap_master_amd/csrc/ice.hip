@@ -25,105 +25,145 @@ namespace hh {
 constexpr int kTile = 1024;
 constexpr int kThreads = 256;
 
-// One packed entry: count = e >> k, column = base + (e & mask).  `bb` is
-// b + base, so the gather index is a 32-bit unsigned offset.
-// ABL (timing ablations only, results wrong): 1 = no gather, 2 = gather b[base].
-template <int ABL>
-__device__ __forceinline__ double entry_dot(uint32_t e, const double* __restrict__ bb, uint32_t mask,
-                                            int k, double acc) {
-    if (ABL == 1) return acc + (double)(e >> k);
-    if (ABL == 2) return fma((double)(e >> k), bb[0], acc);
-    return fma((double)(e >> k), bb[e & mask], acc);
+// ---------------------------------------------------------------- K1
+// One workgroup per unit (a run of tiles of one row-block, or a row range of
+// one large tile).  Per tile: the 8192 bias values of the tile's columns are
+// staged in LDS (coalesced 16-B loads, L2/MALL resident), then every entry
+// gathers its b from LDS.  Rows are interleaved over the 8 waves; a row's
+// entries in the tile are read as uint4 (4 entries per lane) by a lane group
+// of G = 4..64 lanes (G from the tile's mean row length), reduced with
+// xor-shuffles inside the group and added to the row's LDS accumulator,
+// which only that wave touches -> fixed summation order (deterministic).
+constexpr int kSweepThreads = 512;
+constexpr int kSweepWaves = kSweepThreads / 64;
+
+// LDS image of the tile's bias values, XOR-rotated so that a wave reading
+// columns c, c+4, c+8, ... (one uint4 of 4 consecutive entries per lane on a
+// dense row) hits 32 distinct 8-byte bank slots: element e = 32h + l is kept
+// at 32h + ((l + h) mod 32).
+__device__ __forceinline__ uint32_t swz(uint32_t e) { return (e & ~31u) | ((e + (e >> 5)) & 31u); }
+
+__device__ __forceinline__ double tile_dot(const uint4 v, const double* __restrict__ bl, double a) {
+    a = fma((double)(v.x >> kWBits), bl[swz(v.x & kColMask)], a);
+    a = fma((double)(v.y >> kWBits), bl[swz(v.y & kColMask)], a);
+    a = fma((double)(v.z >> kWBits), bl[swz(v.z & kColMask)], a);
+    a = fma((double)(v.w >> kWBits), bl[swz(v.w & kColMask)], a);
+    return a;
 }
 
-template <int U, int ABL>
-__device__ __forceinline__ double sweep_segment(const uint4* __restrict__ pay, const uint32_t* __restrict__ hdr,
-                                                int c, int c1, int lane, const double* __restrict__ b) {
-    double acc0 = 0.0, acc1 = 0.0;
-    for (; c + U <= c1; c += U) {
-        uint4 v[U];
-        uint32_t h[U];
+// NB row batches of a wave in flight together (loads of all of them issued
+// before any is consumed) so short rows still keep ~NB KiB per wave in flight.
+template <int G, int NB>
+__device__ __forceinline__ void tile_rows(const uint4* __restrict__ pay4, const uint32_t* __restrict__ rp,
+                                          const double* __restrict__ bl, double* __restrict__ acc, int ra,
+                                          int rb, int wave, int lane) {
+    constexpr int RP = 64 / G;              // rows per wave step
+    constexpr int S = kSweepWaves * RP;     // row distance between a wave's batches
+    const int gi = lane / G, li = lane % G;
+    for (int r0 = ra + wave * RP; r0 < rb; r0 += NB * S) {
+        uint32_t q[NB], qe[NB];
+        double a[NB];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            v[u] = pay[(size_t)(c + u) * 64 + lane];
-            h[u] = hdr[c + u];
+        for (int k = 0; k < NB; ++k) {
+            const int r = r0 + k * S + gi;
+            q[k] = qe[k] = 0;
+            if (r < rb) {
+                q[k] = (rp[r] >> 2) + li;
+                qe[k] = rp[r + 1] >> 2;
+            }
+            a[k] = 0.0;
+        }
+        bool more = false;
+#pragma unroll
+        for (int k = 0; k < NB; ++k) more |= q[k] < qe[k];
+        while (more) {
+            uint4 v[NB];
+#pragma unroll
+            for (int k = 0; k < NB; ++k) v[k] = q[k] < qe[k] ? pay4[q[k]] : make_uint4(0u, 0u, 0u, 0u);
+            more = false;
+#pragma unroll
+            for (int k = 0; k < NB; ++k) {
+                a[k] = tile_dot(v[k], bl, a[k]);
+                q[k] += G;
+                more |= q[k] < qe[k];
+            }
         }
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int kb = (int)(h[u] >> kHdrShift);
-            const uint32_t mk = (1u << kb) - 1u;
-            const double* bb = b + (h[u] & kHdrBaseMask);
-            acc0 = entry_dot<ABL>(v[u].x, bb, mk, kb, acc0);
-            acc1 = entry_dot<ABL>(v[u].y, bb, mk, kb, acc1);
-            acc0 = entry_dot<ABL>(v[u].z, bb, mk, kb, acc0);
-            acc1 = entry_dot<ABL>(v[u].w, bb, mk, kb, acc1);
+        for (int k = 0; k < NB; ++k) {
+            double x = a[k];
+#pragma unroll
+            for (int o = G >> 1; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+            const int r = r0 + k * S + gi;
+            if (li == 0 && r < rb) acc[r - ra] += x;
         }
     }
-    for (; c < c1; ++c) {
-        const uint4 v = pay[(size_t)c * 64 + lane];
-        const uint32_t h = hdr[c];
-        const int kb = (int)(h >> kHdrShift);
-        const uint32_t mk = (1u << kb) - 1u;
-        const double* bb = b + (h & kHdrBaseMask);
-        acc0 = entry_dot<ABL>(v.x, bb, mk, kb, acc0);
-        acc1 = entry_dot<ABL>(v.y, bb, mk, kb, acc1);
-        acc0 = entry_dot<ABL>(v.z, bb, mk, kb, acc0);
-        acc1 = entry_dot<ABL>(v.w, bb, mk, kb, acc1);
+}
+
+__global__ __launch_bounds__(kSweepThreads) void k_sweep_tiled(TileDev T, const uint8_t* __restrict__ act,
+                                                                int n_units, const double* __restrict__ b,
+                                                                long long n_bins, double* __restrict__ part) {
+    __shared__ __attribute__((aligned(16))) double bl[kW];
+    __shared__ double acc[kR];
+    const int u = blockIdx.x;
+    if (u >= n_units) return;
+    {
+        bool on = false;
+        for (int g = T.u_glo[u]; g <= T.u_ghi[u]; ++g) on |= act[g] != 0;
+        if (!on) return;
     }
-    return wave_sum(acc0 + acc1);
-}
-
-// One wave per segment.
-template <int U, int ABL>
-__global__ __launch_bounds__(kThreads) void k_sweep(const uint4* __restrict__ pay,
-                                                    const uint32_t* __restrict__ hdr,
-                                                    const int32_t* __restrict__ seg_begin,
-                                                    const uint16_t* __restrict__ seg_group,
-                                                    const uint8_t* __restrict__ act, int nseg,
-                                                    const double* __restrict__ b,
-                                                    double* __restrict__ part) {
-    const int lb = (int)xcd_remap(blockIdx.x, gridDim.x);
-    const int s = __builtin_amdgcn_readfirstlane(lb * 4 + (int)(threadIdx.x >> 6));
-    if (s >= nseg) return;
-    if (act[seg_group[s]] == 0) return;
-    const int lane = threadIdx.x & 63;
-    const double acc = sweep_segment<U, ABL>(pay, hdr, seg_begin[s], seg_begin[s + 1], lane, b);
-    if (lane == 0) part[s] = acc;
-}
-
-// Persistent variant: a fixed grid; wave w of XCD-contiguous block range
-// takes segments w, w + W, ... (W = total waves).
-template <int U, int ABL>
-__global__ __launch_bounds__(kThreads) void k_sweep_persist(const uint4* __restrict__ pay,
-                                                            const uint32_t* __restrict__ hdr,
-                                                            const int32_t* __restrict__ seg_begin,
-                                                            const uint16_t* __restrict__ seg_group,
-                                                            const uint8_t* __restrict__ act, int nseg,
-                                                            const double* __restrict__ b,
-                                                            double* __restrict__ part) {
-    const int lb = (int)xcd_remap(blockIdx.x, gridDim.x);
-    const int W = (int)gridDim.x * 4;
-    const int lane = threadIdx.x & 63;
-    // contiguous ranges of segments per wave keep each XCD on nearby rows
-    const int w = __builtin_amdgcn_readfirstlane(lb * 4 + (int)(threadIdx.x >> 6));
-    const int per = (nseg + W - 1) / W;
-    const int s0 = w * per, s1 = min(nseg, s0 + per);
-    for (int s = s0; s < s1; ++s) {
-        if (act[seg_group[s]] == 0) continue;
-        const double acc = sweep_segment<U, ABL>(pay, hdr, seg_begin[s], seg_begin[s + 1], lane, b);
-        if (lane == 0) part[s] = acc;
+    const int ra = T.u_rlo[u], rb = T.u_rhi[u];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int k = threadIdx.x; k < rb - ra; k += kSweepThreads) acc[k] = 0.0;
+    for (int t = T.u_tlo[u]; t < T.u_thi[u]; ++t) {
+        const long long c0 = (long long)T.tile_J[t] * kW;
+        __syncthreads();  // previous tile's LDS reads are done
+        if (c0 + kW <= n_bins) {
+            const double2* src = reinterpret_cast<const double2*>(b + c0);
+            double2 v[kW / 2 / kSweepThreads];
+#pragma unroll
+            for (int k = 0; k < kW / 2 / kSweepThreads; ++k) v[k] = src[threadIdx.x + k * kSweepThreads];
+#pragma unroll
+            for (int k = 0; k < kW / 2 / kSweepThreads; ++k) {
+                const uint32_t e = 2u * (threadIdx.x + k * kSweepThreads);
+                bl[swz(e)] = v[k].x;
+                bl[swz(e + 1)] = v[k].y;
+            }
+        } else {
+            for (int k = threadIdx.x; k < kW; k += kSweepThreads) bl[swz(k)] = c0 + k < n_bins ? b[c0 + k] : 0.0;
+        }
+        __syncthreads();
+        const uint32_t* rp = T.tile_rp + (size_t)t * (kR + 1);
+        const uint4* pay4 = reinterpret_cast<const uint4*>(T.pay + T.tile_ent[t]);
+        // lane-group width from the mean row length of the unit's rows in this tile
+        const uint32_t tot = rp[rb] - rp[ra];
+        const uint32_t mean4 = tot / (uint32_t)(4 * (rb - ra));  // uint4 per row
+        if (mean4 >= 48) tile_rows<64, 4>(pay4, rp, bl, acc, ra, rb, wave, lane);
+        else if (mean4 >= 24) tile_rows<32, 4>(pay4, rp, bl, acc, ra, rb, wave, lane);
+        else if (mean4 >= 12) tile_rows<16, 4>(pay4, rp, bl, acc, ra, rb, wave, lane);
+        else if (mean4 >= 6) tile_rows<8, 4>(pay4, rp, bl, acc, ra, rb, wave, lane);
+        else tile_rows<4, 4>(pay4, rp, bl, acc, ra, rb, wave, lane);
     }
+    __syncthreads();
+    for (int k = threadIdx.x; k < rb - ra; k += kSweepThreads) part[T.u_slot[u] + k] = acc[k];
 }
 
-__global__ void k_marg(const int32_t* __restrict__ row_seg, const double* __restrict__ part,
+// ---------------------------------------------------------------- K2
+// marg_r = b_r * (sum of the row's unit partials + wide entries + 2 diag b_r)
+__global__ void k_marg(TileDev T, const double* __restrict__ part, const long long* __restrict__ wide_ptr,
+                       const int32_t* __restrict__ wide_col, const double* __restrict__ wide_cnt,
                        const double* __restrict__ diag, const uint16_t* __restrict__ row_group,
                        const uint8_t* __restrict__ act, const double* __restrict__ b, long long row_lo,
                        int nloc, double* __restrict__ out) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nloc) return;
     if (act[row_group[i]] == 0) return;
+    const int rbk = i / kR, rl = i % kR;
     double s = 0.0;
-    for (int k = row_seg[i]; k < row_seg[i + 1]; ++k) s += part[k];
+    for (int u = T.blk_unit_ptr[rbk]; u < T.blk_unit_ptr[rbk + 1]; ++u) {
+        const int lo = T.u_rlo[u], hi = T.u_rhi[u];
+        if (rl >= lo && rl < hi) s += part[T.u_slot[u] + rl - lo];
+    }
+    for (long long q = wide_ptr[i]; q < wide_ptr[i + 1]; ++q) s = fma(wide_cnt[q], b[wide_col[q]], s);
     const double br = b[row_lo + i];
     out[i] = br * fma(2.0 * diag[i], br, s);
 }
@@ -303,56 +343,22 @@ struct hh_ice {
 
 namespace hh {
 
-// Tuning knobs (hh_tune): chunks loaded per wave before their gathers,
-// persistent grid (blocks per CU, 0 = one wave per segment), ablation.
-static int g_sweep_unroll = 4;
-static int g_sweep_persist = 0;
-static int g_sweep_ablate = 0;
-
-template <int U, int ABL>
-static void launch_sweep(const ChunkLayer& L, const uint8_t* act, const double* b, double* part, hipStream_t s) {
-    const uint4* pay = reinterpret_cast<const uint4*>(L.pay.p);
-    if (g_sweep_persist > 0) {
-        const long long nb = std::min<long long>(256LL * g_sweep_persist, (L.n_segs + 3) / 4);
-        hipLaunchKernelGGL((k_sweep_persist<U, ABL>), dim3((unsigned)nb), dim3(kThreads), 0, s, pay, L.hdr.p,
-                           L.seg_begin.p, L.seg_group.p, act, (int)L.n_segs, b, part);
-    } else {
-        const long long nb = (L.n_segs + 3) / 4;
-        hipLaunchKernelGGL((k_sweep<U, ABL>), dim3((unsigned)nb), dim3(kThreads), 0, s, pay, L.hdr.p,
-                           L.seg_begin.p, L.seg_group.p, act, (int)L.n_segs, b, part);
-    }
-}
-
-template <int ABL>
-static void launch_sweep_u(const ChunkLayer& L, const uint8_t* act, const double* b, double* part, hipStream_t s) {
-    switch (g_sweep_unroll) {
-        case 1: launch_sweep<1, ABL>(L, act, b, part, s); break;
-        case 2: launch_sweep<2, ABL>(L, act, b, part, s); break;
-        case 8: launch_sweep<8, ABL>(L, act, b, part, s); break;
-        default: launch_sweep<4, ABL>(L, act, b, part, s); break;
-    }
-}
-
-static void sweep_layer(const ChunkLayer& L, const uint8_t* act, const double* b, double* part,
-                        hipStream_t s) {
-    if (L.n_segs == 0) return;
-    switch (g_sweep_ablate) {
-        case 1: launch_sweep_u<1>(L, act, b, part, s); break;
-        case 2: launch_sweep_u<2>(L, act, b, part, s); break;
-        default: launch_sweep_u<0>(L, act, b, part, s); break;
-    }
+static void sweep(const hh_matrix* m, const uint8_t* act, const double* b, double* part, hipStream_t s) {
+    if (m->n_units == 0) return;
+    hipLaunchKernelGGL(k_sweep_tiled, dim3((unsigned)m->n_units), dim3(kSweepThreads), 0, s, m->dev(), act,
+                       (int)m->n_units, b, (long long)m->n_bins, part);
     HIP_CHECK(hipGetLastError());
 }
 
 static void marg_weighted(hh_ice* S, double* out, hipStream_t s, bool timed, int slot) {
     hh_matrix* m = S->m;
     if (timed) HIP_CHECK(hipEventRecord(S->ev[2 * slot], s));
-    sweep_layer(m->main, S->act(), S->bias.p, S->part.p, s);
+    sweep(m, S->act(), S->bias.p, S->part.p, s);
     if (timed) HIP_CHECK(hipEventRecord(S->ev[2 * slot + 1], s));
     if (S->nloc == 0) return;
-    hipLaunchKernelGGL(k_marg, dim3(nblocks(S->nloc, kThreads)), dim3(kThreads), 0, s, m->main.row_seg.p,
-                       S->part.p, m->diag.p,
-                       m->row_group.p, S->act(), S->bias.p, (long long)m->row_lo, (int)S->nloc, out);
+    hipLaunchKernelGGL(k_marg, dim3(nblocks(S->nloc, kThreads)), dim3(kThreads), 0, s, m->dev(), S->part.p,
+                       m->wide_ptr.p, m->wide_col.p, m->wide_cnt.p, m->diag.p, m->row_group.p, S->act(),
+                       S->bias.p, (long long)m->row_lo, (int)S->nloc, out);
     HIP_CHECK(hipGetLastError());
 }
 
@@ -384,16 +390,8 @@ int hh_tune(const char* key, int64_t value) {
     return guard([&] {
         HH_REQUIRE(key, "null key");
         const std::string k(key);
-        if (k == "sweep_unroll") {
-            HH_REQUIRE(value == 1 || value == 2 || value == 4 || value == 8, "sweep_unroll must be 1, 2, 4 or 8");
-            g_sweep_unroll = (int)value;
-        } else if (k == "sweep_persist") {
-            HH_REQUIRE(value >= 0 && value <= 64, "sweep_persist must be in [0, 64]");
-            g_sweep_persist = (int)value;
-        } else if (k == "sweep_ablate") {
-            HH_REQUIRE(value >= 0 && value <= 2, "sweep_ablate must be 0, 1 or 2");
-            g_sweep_ablate = (int)value;
-        } else {
+        if (k == "none") {
+            (void)value;        } else {
             HH_THROW(HH_ERR_ARG, "unknown tuning key " + k);
         }
     });
@@ -442,7 +440,7 @@ int hh_ice_create(hh_matrix* m, const hh_ice_opts* o, hh_ice** out) {
         S->bias.upload(ones.data(), S->n, s);
         S->marg.alloc(S->n);
         S->marg.zero(s);
-        S->part.alloc(std::max<int64_t>(m->main.n_segs, 1));
+        S->part.alloc(std::max<int64_t>(m->n_part, 1));
         S->tile_cnt.alloc(std::max(S->n_tiles, 1));
         S->tile_sum.alloc(std::max(S->n_tiles, 1));
         S->tile_sq.alloc(std::max(S->n_tiles, 1));

@@ -1,11 +1,6 @@
-// Contact-matrix construction in HBM: cooler pixel table -> pixel-chunk
-// layout (host build + upload), and the on-device synthetic genome generator.
-//
-// Layout: the symmetric matrix stored row by row; each row's
-// off-diagonal entries, sorted by column, are cut into chunks of 256 packed
-// uint32 entries (count << k | col - base) with an int32 base column and a
-// column-offset width k per chunk (ice_internal.hpp).  Chunks of a row are
-// grouped into segments of <= 8 chunks (one wave of the sweep kernel each).
+// Contact-matrix construction in HBM: cooler pixel table -> tiled pixel
+// layout (ice_internal.hpp): tile/unit planning shared with the
+// on-device generator (synth.hip), host fill + upload, and export for checks.
 #include <algorithm>
 #include <cmath>
 #include <numeric>
@@ -17,61 +12,114 @@ namespace hh {
 static thread_local std::string g_last_error;
 void set_error(const std::string& msg) { g_last_error = msg; }
 
-void make_segments(const std::vector<int64_t>& row_chunks, const std::vector<uint16_t>& row_group,
-                   HostLayer& h) {
-    const size_t nloc = row_chunks.size();
-    h.row_seg.assign(nloc + 1, 0);
-    h.seg_begin.clear();
-    h.seg_group.clear();
-    int64_t chunk = 0;
-    for (size_t r = 0; r < nloc; ++r) {
-        h.row_seg[r] = (int32_t)h.seg_begin.size();
-        for (int64_t k = 0; k < row_chunks[r]; k += kSegChunks) {
-            h.seg_begin.push_back((int32_t)(chunk + k));
-            h.seg_group.push_back(row_group[r]);
+TilePlan plan_tiles(const uint16_t* cnt, int64_t nloc, int32_t nJ, const std::vector<uint16_t>& row_group) {
+    TilePlan P;
+    P.nloc = nloc;
+    P.nJ = nJ;
+    P.nrb = (nloc + kR - 1) / kR;
+    P.tile_of.assign((size_t)P.nrb * nJ, -1);
+    P.blk_tile_ptr.assign(P.nrb + 1, 0);
+    P.blk_unit_ptr.assign(P.nrb + 1, 0);
+    int64_t ent = 0;
+    std::vector<uint32_t> rp(kR + 1);
+    for (int64_t rb = 0; rb < P.nrb; ++rb) {
+        P.blk_tile_ptr[rb] = (int32_t)P.tile_J.size();
+        const int64_t r0 = rb * kR, r1 = std::min<int64_t>(nloc, r0 + kR);
+        for (int32_t J = 0; J < nJ; ++J) {
+            rp[0] = 0;
+            for (int k = 0; k < kR; ++k) {
+                const int64_t r = r0 + k;
+                const uint32_t c = r < r1 ? (uint32_t)pad4(cnt[r * nJ + J]) : 0u;
+                rp[k + 1] = rp[k] + c;
+            }
+            if (rp[kR] == 0) continue;
+            P.tile_of[rb * nJ + J] = (int32_t)P.tile_J.size();
+            P.tile_J.push_back(J);
+            P.tile_ent.push_back(ent);
+            P.tile_rb.push_back((int32_t)rb);
+            P.tile_rp.insert(P.tile_rp.end(), rp.begin(), rp.end());
+            ent += rp[kR];
         }
-        chunk += row_chunks[r];
     }
-    h.row_seg[nloc] = (int32_t)h.seg_begin.size();
-    h.seg_begin.push_back((int32_t)chunk);
-    if (chunk > INT32_MAX - 1) HH_THROW(HH_ERR_ARG, "too many chunks for one shard (> 2^31); use more ranks");
+    P.blk_tile_ptr[P.nrb] = (int32_t)P.tile_J.size();
+    P.n_entries_padded = ent;
+    // units
+    auto emit = [&](int64_t rb, int32_t ta, int32_t tb, int32_t rlo, int32_t rhi) {
+        const int64_t g0 = rb * kR + rlo, g1 = rb * kR + rhi - 1;
+        P.u_tlo.push_back(ta);
+        P.u_thi.push_back(tb);
+        P.u_rb.push_back((int32_t)rb);
+        P.u_rlo.push_back(rlo);
+        P.u_rhi.push_back(rhi);
+        P.u_slot.push_back((int32_t)P.n_part);
+        P.u_glo.push_back(row_group[g0]);
+        P.u_ghi.push_back(row_group[g1]);
+        P.n_part += rhi - rlo;
+    };
+    for (int64_t rb = 0; rb < P.nrb; ++rb) {
+        P.blk_unit_ptr[rb] = (int32_t)P.u_tlo.size();
+        const int32_t nr = (int32_t)(std::min<int64_t>(nloc, rb * kR + kR) - rb * kR);
+        const int32_t ta = P.blk_tile_ptr[rb], tb = P.blk_tile_ptr[rb + 1];
+        int32_t cur = ta;
+        int64_t cur_sz = 0;
+        for (int32_t t = ta; t < tb; ++t) {
+            const uint32_t* trp = &P.tile_rp[(size_t)t * (kR + 1)];
+            const int64_t sz = trp[kR];
+            if (sz > kUnitEntries) {
+                if (cur < t) emit(rb, cur, t, 0, nr);
+                int32_t rlo = 0;
+                int64_t acc = 0;
+                for (int32_t k = 0; k < nr; ++k) {
+                    const int64_t len = trp[k + 1] - trp[k];
+                    if (acc > 0 && acc + len > kUnitEntries) {
+                        emit(rb, t, t + 1, rlo, k);
+                        rlo = k;
+                        acc = 0;
+                    }
+                    acc += len;
+                }
+                emit(rb, t, t + 1, rlo, nr);
+                cur = t + 1;
+                cur_sz = 0;
+            } else {
+                if (cur < t && cur_sz + sz > kUnitEntries) {
+                    emit(rb, cur, t, 0, nr);
+                    cur = t;
+                    cur_sz = 0;
+                }
+                cur_sz += sz;
+            }
+        }
+        if (cur < tb) emit(rb, cur, tb, 0, nr);
+    }
+    P.blk_unit_ptr[P.nrb] = (int32_t)P.u_tlo.size();
+    if (P.n_part > INT32_MAX || P.tile_J.size() > (size_t)INT32_MAX) HH_THROW(HH_ERR_ARG, "plan too large");
+    return P;
 }
 
-void upload_layer(const HostLayer& h, ChunkLayer& d, hipStream_t s) {
-    d.n_chunks = (int64_t)h.hdr.size();
-    d.n_segs = (int64_t)h.seg_group.size();
-    d.n_entries = h.n_entries;
-    d.pay = to_device(h.pay, s);
-    d.hdr = to_device(h.hdr, s);
-    d.seg_begin = to_device(h.seg_begin, s);
-    d.row_seg = to_device(h.row_seg, s);
-    d.seg_group = to_device(h.seg_group, s);
-}
-
-// Append one row (sorted columns) to a host layer; returns the chunks added.
-static int64_t chunk_row(const int32_t* cols, const uint32_t* vals, int64_t n, HostLayer& h) {
-    int64_t added = 0;
-    int64_t k = 0;
-    while (k < n) {
-        const int32_t b = cols[k];
-        const int64_t start = k;
-        uint32_t maxc = 0;
-        while (k < n && k - start < kChunk) {
-            const uint32_t mc = std::max(maxc, vals[k]);
-            if (nbits((uint32_t)(cols[k] - b)) + nbits(mc) > 32) break;
-            maxc = mc;
-            ++k;
-        }
-        const int kb = nbits((uint32_t)(cols[k - 1] - b));
-        const size_t off = h.pay.size();
-        h.pay.resize(off + kChunk, 0u);
-        for (int64_t q = start; q < k; ++q)
-            h.pay[off + slot_of((int)(q - start))] = (uint32_t)((uint64_t)vals[q] << kb) | (uint32_t)(cols[q] - b);
-        h.hdr.push_back(make_hdr(b, kb));
-        h.n_entries += k - start;
-        ++added;
-    }
-    return added;
+void upload_plan(const TilePlan& P, hh_matrix& m, hipStream_t s) {
+    m.nJ = P.nJ;
+    m.nrb = P.nrb;
+    m.n_tiles = (int64_t)P.tile_J.size();
+    m.n_units = (int64_t)P.u_tlo.size();
+    m.n_part = P.n_part;
+    m.n_slots = P.n_entries_padded;
+    m.tile_J = to_device(P.tile_J, s);
+    m.tile_rb = to_device(P.tile_rb, s);
+    std::vector<long long> te(P.tile_ent.begin(), P.tile_ent.end());
+    m.tile_ent = to_device(te, s);
+    m.tile_rp = to_device(P.tile_rp, s);
+    m.blk_tile_ptr = to_device(P.blk_tile_ptr, s);
+    m.u_tlo = to_device(P.u_tlo, s);
+    m.u_thi = to_device(P.u_thi, s);
+    m.u_rb = to_device(P.u_rb, s);
+    m.u_rlo = to_device(P.u_rlo, s);
+    m.u_rhi = to_device(P.u_rhi, s);
+    m.u_slot = to_device(P.u_slot, s);
+    m.u_glo = to_device(P.u_glo, s);
+    m.u_ghi = to_device(P.u_ghi, s);
+    m.blk_unit_ptr = to_device(P.blk_unit_ptr, s);
+    HIP_CHECK(hipStreamSynchronize(s));  // the plan's host vectors may die after return
 }
 
 }  // namespace hh
@@ -81,7 +129,7 @@ using namespace hh;
 extern "C" {
 
 const char* hh_last_error(void) { return g_last_error.c_str(); }
-int hh_version(void) { return (0 << 16) | (1 << 8) | 0; }
+int hh_version(void) { return (0 << 16) | (2 << 8) | 0; }
 
 int hh_device_count(int32_t* n) {
     return guard([&] {
@@ -106,8 +154,10 @@ int hh_matrix_from_pixels(const int64_t* bin1, const int64_t* bin2, const double
     return guard([&] {
         HH_REQUIRE(out && n_bins > 0 && nnz >= 0 && n_chroms > 0 && chrom_offsets, "bad arguments");
         HH_REQUIRE(nnz == 0 || (bin1 && bin2 && count), "null pixel arrays");
-        HH_REQUIRE(n_bins < kMaxBins, "n_bins must be < 2^27");
+        HH_REQUIRE(n_bins < kMaxBins, "n_bins must be < 2^30");
         HH_REQUIRE(0 <= row_lo && row_lo <= row_hi && row_hi <= n_bins, "bad row range");
+        HH_REQUIRE(row_lo % kR == 0 && (row_hi % kR == 0 || row_hi == n_bins),
+                   "shard rows must be aligned to 256-row blocks");
         HH_REQUIRE(chrom_offsets[0] == 0 && chrom_offsets[n_chroms] == n_bins, "chrom_offsets must span [0, n_bins]");
         HH_REQUIRE(n_chroms < 65535, "too many chromosomes");
         HH_REQUIRE(ignore_diags >= 0, "ignore_diags must be >= 0");
@@ -129,7 +179,6 @@ int hh_matrix_from_pixels(const int64_t* bin1, const int64_t* bin2, const double
         const int64_t nloc = row_hi - row_lo;
         std::vector<double> diag(nloc, 0.0), rnnz(nloc, 0.0), rsum(nloc, 0.0);
         std::vector<int64_t> deg(nloc + 1, 0);
-        // pass 1: validate, filter, count row degrees
         auto keep = [&](int64_t i, int64_t& a, int64_t& b, uint32_t& c) -> bool {
             a = bin1[i];
             b = bin2[i];
@@ -144,6 +193,7 @@ int hh_matrix_from_pixels(const int64_t* bin1, const int64_t* bin2, const double
             c = (uint32_t)v;
             return true;
         };
+        // pass 1: validate, filter, count row degrees, marginals
         int64_t nnz_upper = 0;
         for (int64_t i = 0; i < nnz; ++i) {
             int64_t a, b;
@@ -163,17 +213,19 @@ int hh_matrix_from_pixels(const int64_t* bin1, const int64_t* bin2, const double
             if (inb) { ++deg[b - row_lo + 1]; rnnz[b - row_lo] += 1.0; rsum[b - row_lo] += c; }
         }
         for (int64_t r = 0; r < nloc; ++r) deg[r + 1] += deg[r];
+        // pass 2: symmetric CSR rows
         std::vector<int32_t> cols(deg[nloc]);
         std::vector<uint32_t> vals(deg[nloc]);
-        std::vector<int64_t> pos(deg.begin(), deg.end() - 1);
-        for (int64_t i = 0; i < nnz; ++i) {
-            int64_t a, b;
-            uint32_t c;
-            if (!keep(i, a, b, c) || a == b) continue;
-            if (a >= row_lo && a < row_hi) { cols[pos[a - row_lo]] = (int32_t)b; vals[pos[a - row_lo]++] = c; }
-            if (b >= row_lo && b < row_hi) { cols[pos[b - row_lo]] = (int32_t)a; vals[pos[b - row_lo]++] = c; }
+        {
+            std::vector<int64_t> pos(deg.begin(), deg.end() - 1);
+            for (int64_t i = 0; i < nnz; ++i) {
+                int64_t a, b;
+                uint32_t c;
+                if (!keep(i, a, b, c) || a == b) continue;
+                if (a >= row_lo && a < row_hi) { cols[pos[a - row_lo]] = (int32_t)b; vals[pos[a - row_lo]++] = c; }
+                if (b >= row_lo && b < row_hi) { cols[pos[b - row_lo]] = (int32_t)a; vals[pos[b - row_lo]++] = c; }
+            }
         }
-        // rows must be column-sorted for chunking; sort rows that are not
         std::vector<std::pair<int32_t, uint32_t>> tmp;
         for (int64_t r = 0; r < nloc; ++r) {
             const int64_t lo = deg[r], hi = deg[r + 1];
@@ -183,21 +235,52 @@ int hh_matrix_from_pixels(const int64_t* bin1, const int64_t* bin2, const double
             std::stable_sort(tmp.begin(), tmp.end(), [](auto& x, auto& y) { return x.first < y.first; });
             for (int64_t k = lo; k < hi; ++k) { cols[k] = tmp[k - lo].first; vals[k] = tmp[k - lo].second; }
         }
-        // chunk layer
+        // tile counts (entries with count > kCntMax go to the wide list)
+        const int32_t nJ = (int32_t)((n_bins + kW - 1) / kW);
+        std::vector<uint16_t> cnt((size_t)nloc * nJ, 0);
+        std::vector<long long> wptr(nloc + 1, 0);
+        for (int64_t r = 0; r < nloc; ++r) {
+            for (int64_t k = deg[r]; k < deg[r + 1]; ++k) {
+                if (vals[k] > kCntMax) ++wptr[r + 1];
+                else ++cnt[(size_t)r * nJ + (cols[k] >> kWBits)];
+            }
+        }
+        for (int64_t r = 0; r < nloc; ++r) wptr[r + 1] += wptr[r];
         std::vector<uint16_t> bg = bin_groups(*m);
         std::vector<uint16_t> rgroup(bg.begin() + row_lo, bg.begin() + row_hi);
-        HostLayer hm;
-        std::vector<int64_t> rc(nloc, 0);
-        hm.pay.reserve((size_t)(deg[nloc] + nloc * 64));
-        for (int64_t r = 0; r < nloc; ++r)
-            rc[r] = chunk_row(cols.data() + deg[r], vals.data() + deg[r], deg[r + 1] - deg[r], hm);
-        make_segments(rc, rgroup, hm);
-        upload_layer(hm, m->main, s);
+        TilePlan P = plan_tiles(cnt.data(), nloc, nJ, rgroup);
+        // fill payload + wide list
+        std::vector<uint32_t> pay(P.n_entries_padded, 0u);
+        std::vector<int32_t> wcol(wptr[nloc]);
+        std::vector<double> wcnt(wptr[nloc]);
+        for (int64_t r = 0; r < nloc; ++r) {
+            const int64_t rb = r / kR, k = r % kR;
+            int32_t curJ = -1;
+            int64_t pos = 0;
+            int64_t wp = wptr[r];
+            for (int64_t q = deg[r]; q < deg[r + 1]; ++q) {
+                if (vals[q] > kCntMax) { wcol[wp] = cols[q]; wcnt[wp++] = vals[q]; continue; }
+                const int32_t J = cols[q] >> kWBits;
+                if (J != curJ) {
+                    const int32_t t = P.tile_of[rb * nJ + J];
+                    pos = P.tile_ent[t] + P.tile_rp[(size_t)t * (kR + 1) + k];
+                    curJ = J;
+                }
+                pay[pos++] = (vals[q] << kWBits) | ((uint32_t)cols[q] & kColMask);
+            }
+        }
+        upload_plan(P, *m, s);
+        m->pay = to_device(pay, s);
+        m->wide_ptr = to_device(wptr, s);
+        m->wide_col = to_device(wcol, s);
+        m->wide_cnt = to_device(wcnt, s);
+        m->n_wide = wptr[nloc];
         m->diag = to_device(diag, s);
         m->row_nnz2 = to_device(rnnz, s);
         m->row_sum2 = to_device(rsum, s);
         m->row_group = to_device(rgroup, s);
         m->nnz_upper = nnz_upper;
+        m->n_entries = deg[nloc];
         HIP_CHECK(hipStreamSynchronize(s));  // host vectors die here
         *out = m.release();
     });
@@ -214,11 +297,11 @@ int hh_matrix_get_info(const hh_matrix* m, hh_matrix_info* info) {
         info->row_lo = m->row_lo;
         info->row_hi = m->row_hi;
         info->nnz_upper = m->nnz_upper;
-        info->n_entries = m->main.n_entries;
-        info->n_slots = m->main.n_chunks * kChunk;
-        info->n_chunks = m->main.n_chunks;
-        info->n_segments = m->main.n_segs;
-        info->n_ovf_chunks = 0;
+        info->n_entries = m->n_entries;
+        info->n_slots = m->n_slots;
+        info->n_tiles = m->n_tiles;
+        info->n_units = m->n_units;
+        info->n_wide = m->n_wide;
         info->device_bytes = (int64_t)m->device_bytes();
         info->n_chroms = m->n_chroms;
         info->ignore_diags = m->ignore_diags;
@@ -233,18 +316,36 @@ int hh_matrix_export_upper(const hh_matrix* m, int64_t* bin1, int64_t* bin2, dou
         HH_REQUIRE(m && nnz_inout, "null");
         HIP_CHECK(hipSetDevice(m->device));
         const int64_t nloc = m->nloc();
-        const ChunkLayer& L = m->main;
-        std::vector<uint32_t> pay(L.pay.n);
-        std::vector<uint32_t> hdr(L.hdr.n);
-        std::vector<int32_t> row_seg(L.row_seg.n), seg_begin(L.seg_begin.n);
-        std::vector<double> diag(nloc);
         HIP_CHECK(hipDeviceSynchronize());
-        L.pay.download(pay.data(), pay.size(), 0);
-        L.hdr.download(hdr.data(), hdr.size(), 0);
-        L.row_seg.download(row_seg.data(), row_seg.size(), 0);
-        L.seg_begin.download(seg_begin.data(), seg_begin.size(), 0);
+        std::vector<uint32_t> pay(m->pay.n), rp(m->tile_rp.n);
+        std::vector<int32_t> tJ(m->tile_J.n), trb(m->tile_rb.n), wcol(m->wide_col.n);
+        std::vector<long long> tent(m->tile_ent.n), wptr(m->wide_ptr.n);
+        std::vector<double> wcnt(m->wide_cnt.n), diag(nloc);
+        m->pay.download(pay.data(), pay.size(), 0);
+        m->tile_rp.download(rp.data(), rp.size(), 0);
+        m->tile_J.download(tJ.data(), tJ.size(), 0);
+        m->tile_rb.download(trb.data(), trb.size(), 0);
+        m->tile_ent.download(tent.data(), tent.size(), 0);
+        m->wide_ptr.download(wptr.data(), wptr.size(), 0);
+        m->wide_col.download(wcol.data(), wcol.size(), 0);
+        m->wide_cnt.download(wcnt.data(), wcnt.size(), 0);
         m->diag.download(diag.data(), nloc, 0);
         HIP_CHECK(hipDeviceSynchronize());
+        std::vector<std::vector<std::pair<int64_t, double>>> rows(nloc);
+        for (size_t t = 0; t < tJ.size(); ++t) {
+            const uint32_t* trp = &rp[t * (kR + 1)];
+            for (int k = 0; k < kR; ++k) {
+                const int64_t r = (int64_t)trb[t] * kR + k;
+                for (uint32_t q = trp[k]; q < trp[k + 1]; ++q) {
+                    const uint32_t e = pay[tent[t] + q];
+                    const uint32_t c = e >> kWBits;
+                    if (!c) continue;
+                    rows[r].emplace_back((int64_t)tJ[t] * kW + (e & kColMask), (double)c);
+                }
+            }
+        }
+        for (int64_t r = 0; r < nloc; ++r)
+            for (long long q = wptr[r]; q < wptr[r + 1]; ++q) rows[r].emplace_back(wcol[q], wcnt[q]);
         int64_t cnt = 0;
         const int64_t cap = *nnz_inout;
         auto emit = [&](int64_t i, int64_t j, double v) {
@@ -255,18 +356,9 @@ int hh_matrix_export_upper(const hh_matrix* m, int64_t* bin1, int64_t* bin2, dou
         for (int64_t r = 0; r < nloc; ++r) {
             const int64_t gr = m->row_lo + r;
             emit(gr, gr, diag[r]);
-            const int64_t c0 = seg_begin[row_seg[r]], c1 = seg_begin[row_seg[r + 1]];
-            for (int64_t c = c0; c < c1; ++c) {
-                const int kb = (int)(hdr[c] >> kHdrShift);
-                const int64_t base = hdr[c] & kHdrBaseMask;
-                const uint32_t mask = kb ? (0xFFFFFFFFu >> (32 - kb)) : 0u;
-                for (int k = 0; k < kChunk; ++k) {
-                    const uint32_t e = pay[(size_t)c * kChunk + slot_of(k)];
-                    const int64_t col = base + (int64_t)(e & mask);
-                    const double v = kb == 32 ? 0.0 : (double)(e >> kb);
-                    if (col > gr) emit(gr, col, v);
-                }
-            }
+            std::sort(rows[r].begin(), rows[r].end());
+            for (auto& e : rows[r])
+                if (e.first > gr) emit(gr, e.first, e.second);
         }
         *nnz_inout = cnt;
     });

@@ -4,16 +4,17 @@
 //
 // Model: cis lambda(i,j) = A (|i-j|+1)^-decay
 // (1 + c s_i s_j) v_i v_j, counts ~ Poisson(lambda) (inversion below 16,
-// normal approximation above; clamped to 2^20); trans pixels uniform with
-// density p * v_i v_j, count 1 or 2.  Every draw is a pure function of
-// (seed, min(i,j), max(i,j)), so row i's lower half equals column i's upper
-// half and every shard of every rank sees the same matrix.
+// normal approximation above; clamped to 2^19 - 1 so every entry fits a
+// tile slot); trans pixels uniform with density p * v_i v_j, count 1 or 2.
+// Every draw is a pure function of (seed, min(i,j), max(i,j)), so row i's
+// lower half equals column i's upper half and every shard of every rank sees
+// the same matrix.
 //
-// One wave per row scans its candidate columns 64 at a time and compacts the
-// nonzeros into 256-entry chunks with ballots (the same greedy chunking rule
-// as the host builder in matrix.hip).  Pass 0 counts chunks per row, pass 1
-// records each chunk's base column and column-offset width k, pass 2 writes
-// the packed entries.
+// One wave per row scans its candidate columns 64 at a time (column tiles are
+// 8192 = 128 x 64 wide, so a 64-column group never straddles a tile).
+// Pass 0 counts entries per (row, tile) and the row marginals; the host plans
+// tiles/units (plan_tiles, shared with the pixel-table builder); pass 1
+// compacts each row's nonzeros into its tile slots with ballots.
 #include <cmath>
 #include <numeric>
 
@@ -21,11 +22,10 @@
 
 namespace hh {
 
-constexpr uint32_t kSynthCountMax = 1u << 20;
-
 struct SynthDev {
     long long n;
     int n_chroms;
+    int nJ;
     const int* chrom_lo;   // n_chroms + 1
     const float* vis;      // n (0 = gap bin)
     const signed char* sgn;
@@ -66,7 +66,7 @@ __device__ __forceinline__ uint32_t poisson(float lam, uint64_t h) {
     const float u1 = fmaxf(u01(h), 1e-7f), u2 = u01(mix64(h));
     const float z = sqrtf(-2.f * __logf(u1)) * __cosf(6.2831853f * u2);
     const float k = floorf(lam + sqrtf(lam) * z + 0.5f);
-    return k <= 0.f ? 0u : (k >= (float)kSynthCountMax ? kSynthCountMax : (uint32_t)k);
+    return k <= 0.f ? 0u : (k >= (float)kCntMax ? kCntMax : (uint32_t)k);
 }
 
 __device__ __forceinline__ uint32_t synth_count(const SynthDev& p, long long i, long long j) {
@@ -86,15 +86,14 @@ __device__ __forceinline__ uint32_t synth_count(const SynthDev& p, long long i, 
     return (mix64(h) & 3u) == 0u ? 2u : 1u;
 }
 
-// One wave per row.  PASS 0: chunks and upper pixels per row.  PASS 1: base
-// column and width k of each chunk (chunk index from row_chunk_start).
-// PASS 2: packed entries (k read back) and the per-row marginals.
+// PASS 0: cnt[w * nJ + J] = entries of row w in tile J; per-row stats.
+// PASS 1: write entries at tile_ent[t] + tile_rp[t][k] (t = tile_of[rb][J]).
 template <int PASS>
 __global__ __launch_bounds__(256) void k_synth_rows(SynthDev p, long long row_lo, long long nrows,
-                                                    int32_t* row_chunks, long long* row_upper,
-                                                    const long long* row_chunk_start, uint32_t* pay,
-                                                    uint32_t* hdr, double* diag,
-                                                    double* row_nnz2, double* row_sum2) {
+                                                    uint16_t* cnt, int32_t* row_work, long long* row_upper,
+                                                    double* diag, double* row_nnz2, double* row_sum2,
+                                                    const int32_t* tile_of, const long long* tile_ent,
+                                                    const uint32_t* tile_rp, uint32_t* pay) {
     const long long w = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     if (w >= nrows) return;
     const int lane = threadIdx.x & 63;
@@ -102,71 +101,55 @@ __global__ __launch_bounds__(256) void k_synth_rows(SynthDev p, long long row_lo
     const int c = p.chrom[r];
     const long long jlo = p.cis_only ? p.chrom_lo[c] : 0;
     const long long jhi = p.cis_only ? p.chrom_lo[c + 1] : p.n;
-    long long chunk = PASS > 0 ? row_chunk_start[w] : 0;
-    long long nchunks = 0, upper = 0, nnz = 0;
-    long long sum_lane = 0;
-    int fill = 0, kb = 0;
-    long long cbase = 0, clast = 0;
-    uint32_t cmax = 0;
+    const long long rb = w / kR;
+    const int k = (int)(w % kR);
     const unsigned long long lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    auto close_chunk = [&]() {
-        if (PASS == 1 && lane == 0) {
-            hdr[chunk] = make_hdr(cbase, nbits((uint32_t)(clast - cbase)));
+    long long upper = 0, nnz = 0, work = 0, sum_lane = 0;
+    int curJ = -1;
+    long long tcount = 0;   // entries of the current tile
+    long long pos = 0;      // PASS 1: next write position
+    auto flush = [&]() {
+        if (curJ < 0) return;
+        if (PASS == 0) {
+            if (lane == 0 && cnt) cnt[w * p.nJ + curJ] = (uint16_t)tcount;
+        } else {
+            const long long padded = (tcount + 3) & ~3LL;
+            for (long long q = tcount + lane; q < padded; q += 64) pay[pos - tcount + q] = 0u;
         }
-        if (PASS == 2)
-            for (int q = fill + lane; q < kChunk; q += 64) pay[(size_t)chunk * kChunk + slot_of(q)] = 0u;
-        ++chunk;
-        ++nchunks;
-        fill = 0;
-        cmax = 0;
+        work += (tcount + 3) & ~3LL;
     };
-    for (long long j0 = jlo; j0 < jhi; j0 += 64) {
+    for (long long j0 = jlo & ~63LL; j0 < jhi; j0 += 64) {
         const long long j = j0 + lane;
-        uint32_t k = 0;
-        if (j < jhi && j != r) k = synth_count(p, r, j);
-        unsigned long long mask = __ballot(k > 0);
+        const int J = (int)(j0 >> kWBits);
+        uint32_t kc = 0;
+        if (j >= jlo && j < jhi && j != r) kc = synth_count(p, r, j);
+        const unsigned long long mask = __ballot(kc > 0);
         if (mask == 0ull) continue;
-        nnz += __popcll(mask);
-        upper += __popcll(__ballot(k > 0 && j > r));
-        sum_lane += k;
-        while (mask) {
-            if (fill == 0) {
-                cbase = j0 + __builtin_ctzll(mask);
-                if (PASS == 2) kb = (int)(hdr[chunk] >> kHdrShift);
+        if (J != curJ) {
+            flush();
+            curJ = J;
+            tcount = 0;
+            if (PASS == 1) {
+                const int t = tile_of[rb * p.nJ + J];
+                pos = tile_ent[t] + tile_rp[(size_t)t * (kR + 1) + k];
             }
-            const bool in = (mask >> lane) & 1ull;
-            const int rank = __popcll(mask & lt_mask);
-            // inclusive prefix max of the counts of the remaining lanes
-            uint32_t pm = in ? k : 0u;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t t = __shfl_up(pm, o, 64);
-                if (lane >= o) pm = pm > t ? pm : t;
-            }
-            const uint32_t mx = pm > cmax ? pm : cmax;
-            const bool fit = in && rank < kChunk - fill &&
-                             nbits((uint32_t)(j - cbase)) + nbits(mx) <= 32;
-            const unsigned long long fm = __ballot(fit);
-            if (fm) {
-                const int top = 63 - __builtin_clzll(fm);
-                if (PASS == 2 && fit)
-                    pay[(size_t)chunk * kChunk + slot_of(fill + rank)] =
-                        (uint32_t)((unsigned long long)k << kb) | (uint32_t)(j - cbase);
-                cmax = __shfl(mx, top, 64);
-                clast = j0 + top;
-            }
-            fill += __popcll(fm);
-            mask &= ~fm;
-            if (mask != 0ull || fill == kChunk) close_chunk();
         }
+        const int rank = __popcll(mask & lt_mask);
+        if (PASS == 1 && kc > 0) pay[pos + rank] = (kc << kWBits) | ((uint32_t)j & kColMask);
+        const int nk = __popcll(mask);
+        tcount += nk;
+        pos += nk;
+        nnz += nk;
+        upper += __popcll(__ballot(kc > 0 && j > r));
+        sum_lane += kc;
     }
-    if (fill > 0) close_chunk();
+    flush();
     const long long s = wave_sum_ll(sum_lane);
     const uint32_t dg = p.ignore_diags == 0 ? synth_count(p, r, r) : 0u;
     if (lane == 0) {
-        if (row_chunks) row_chunks[w] = (int32_t)nchunks;
+        if (row_work) row_work[w] = (int32_t)work;
         if (row_upper) row_upper[w] = upper + (dg ? 1 : 0);
-        if (PASS == 2) {
+        if (diag) {
             diag[w] = (double)dg;
             row_nnz2[w] = (double)nnz + (dg ? 2.0 : 0.0);
             row_sum2[w] = (double)s + 2.0 * (double)dg;
@@ -197,7 +180,7 @@ void synth_setup(const hh_synth_params* p, SynthHost& h, hipStream_t s) {
         h.offsets.push_back(h.offsets.back() + p->chrom_nbins[c]);
     }
     const int64_t n = h.offsets.back();
-    HH_REQUIRE(n < kMaxBins, "too many bins (n_bins must be < 2^27)");
+    HH_REQUIRE(n < kMaxBins, "too many bins");
     std::vector<int> lo(h.offsets.begin(), h.offsets.end());
     std::vector<short> ch(n);
     for (int c = 0; c < p->n_chroms; ++c)
@@ -209,6 +192,7 @@ void synth_setup(const hh_synth_params* p, SynthHost& h, hipStream_t s) {
     SynthDev& d = h.dev;
     d.n = n;
     d.n_chroms = p->n_chroms;
+    d.nJ = (int)((n + kW - 1) / kW);
     d.chrom_lo = h.chrom_lo.p;
     d.vis = h.vis.p;
     d.sgn = h.sgn.p;
@@ -224,38 +208,41 @@ void synth_setup(const hh_synth_params* p, SynthHost& h, hipStream_t s) {
                        (float)p->vis_sigma, (float)p->gap_frac, p->comp_block, h.vis.p, h.sgn.p);
     HIP_CHECK(hipGetLastError());
 }
+
+inline dim3 row_grid(int64_t nrows) { return dim3((unsigned)((nrows * 64 + 255) / 256)); }
 }  // namespace
 
 extern "C" {
 
-int hh_synth_count(const hh_synth_params* p, int32_t* row_chunks, int64_t* row_nnz_upper, void* stream) {
+int hh_synth_count(const hh_synth_params* p, int32_t* row_work, int64_t* row_nnz_upper, void* stream) {
     return guard([&] {
-        HH_REQUIRE(row_chunks && row_nnz_upper, "null outputs");
+        HH_REQUIRE(row_work && row_nnz_upper, "null outputs");
         hipStream_t s = as_stream(stream);
         SynthHost h;
         synth_setup(p, h, s);
         const int64_t n = h.dev.n;
-        DBuf<int32_t> rc(n);
+        DBuf<int32_t> rw(n);
         DBuf<long long> ru(n);
-        hipLaunchKernelGGL((k_synth_rows<0>), dim3((unsigned)((n * 64 + 255) / 256)), dim3(256), 0, s, h.dev,
-                           0LL, (long long)n, rc.p, ru.p, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
+        hipLaunchKernelGGL((k_synth_rows<0>), row_grid(n), dim3(256), 0, s, h.dev, 0LL, (long long)n, nullptr, rw.p,
+                           ru.p, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
         HIP_CHECK(hipGetLastError());
-        rc.download(row_chunks, n, s);
+        rw.download(row_work, n, s);
         HIP_CHECK(hipMemcpyAsync(row_nnz_upper, ru.p, n * sizeof(int64_t), hipMemcpyDeviceToHost, s));
         HIP_CHECK(hipStreamSynchronize(s));
     });
 }
 
-int hh_synth_build(const hh_synth_params* p, const int32_t* row_chunks, int64_t row_lo, int64_t row_hi,
-                   void* stream, hh_matrix** out) {
+int hh_synth_build(const hh_synth_params* p, int64_t row_lo, int64_t row_hi, void* stream, hh_matrix** out) {
     return guard([&] {
-        HH_REQUIRE(row_chunks && out, "null");
+        HH_REQUIRE(out, "null");
         hipStream_t s = as_stream(stream);
         SynthHost h;
         synth_setup(p, h, s);
         const int64_t n = h.dev.n;
         HH_REQUIRE(0 <= row_lo && row_lo <= row_hi && row_hi <= n, "bad row range");
+        HH_REQUIRE(row_lo % kR == 0 && (row_hi % kR == 0 || row_hi == n), "shard rows must be aligned to 256-row blocks");
         const int64_t nloc = row_hi - row_lo;
+        const int nJ = h.dev.nJ;
         auto m = std::make_unique<hh_matrix>();
         HIP_CHECK(hipGetDevice(&m->device));
         m->n_bins = n;
@@ -265,51 +252,42 @@ int hh_synth_build(const hh_synth_params* p, const int32_t* row_chunks, int64_t 
         m->ignore_diags = p->ignore_diags;
         m->cis_only = p->cis_only ? 1 : 0;
         m->chrom_offsets = h.offsets;
-        std::vector<int64_t> rcl(nloc), start(nloc);
-        int64_t tot = 0;
-        for (int64_t r = 0; r < nloc; ++r) {
-            rcl[r] = row_chunks[row_lo + r];
-            start[r] = tot;
-            tot += rcl[r];
-        }
-        std::vector<uint16_t> bg = bin_groups(*m);
-        std::vector<uint16_t> rgroup(bg.begin() + row_lo, bg.begin() + row_hi);
-        HostLayer hl;
-        make_segments(rcl, rgroup, hl);
-        ChunkLayer& L = m->main;
-        L.n_chunks = tot;
-        L.n_segs = (int64_t)hl.seg_group.size();
-        L.pay.alloc((size_t)tot * kChunk);
-        L.hdr.alloc(tot);
-        L.seg_begin = to_device(hl.seg_begin, s);
-        L.row_seg = to_device(hl.row_seg, s);
-        L.seg_group = to_device(hl.seg_group, s);
-        m->row_group = to_device(rgroup, s);
         m->diag.alloc(nloc);
         m->row_nnz2.alloc(nloc);
         m->row_sum2.alloc(nloc);
-        DBuf<long long> dstart(nloc), rup(nloc);
-        std::vector<long long> st(start.begin(), start.end());
-        dstart.upload(st.data(), nloc, s);
-        if (nloc) {
-            const dim3 g((unsigned)((nloc * 64 + 255) / 256));
-            hipLaunchKernelGGL((k_synth_rows<1>), g, dim3(256), 0, s, h.dev, (long long)row_lo, (long long)nloc,
-                               nullptr, nullptr, dstart.p, nullptr, L.hdr.p, nullptr, nullptr, nullptr);
-            hipLaunchKernelGGL((k_synth_rows<2>), g, dim3(256), 0, s, h.dev, (long long)row_lo, (long long)nloc,
-                               nullptr, rup.p, dstart.p, L.pay.p, L.hdr.p, m->diag.p, m->row_nnz2.p,
-                               m->row_sum2.p);
-        }
+        DBuf<uint16_t> cnt((size_t)nloc * nJ);
+        cnt.zero(s);
+        DBuf<long long> rup(nloc);
+        if (nloc)
+            hipLaunchKernelGGL((k_synth_rows<0>), row_grid(nloc), dim3(256), 0, s, h.dev, (long long)row_lo,
+                               (long long)nloc, cnt.p, nullptr, rup.p, m->diag.p, m->row_nnz2.p, m->row_sum2.p,
+                               nullptr, nullptr, nullptr, nullptr);
         HIP_CHECK(hipGetLastError());
+        std::vector<uint16_t> hc((size_t)nloc * nJ);
+        cnt.download(hc.data(), hc.size(), s);
         std::vector<long long> up(nloc);
         rup.download(up.data(), nloc, s);
         HIP_CHECK(hipStreamSynchronize(s));
-        m->nnz_upper = std::accumulate(up.begin(), up.end(), 0LL);
-        std::vector<double> nz(nloc);
-        m->row_nnz2.download(nz.data(), nloc, s);
+        cnt.release();
+        std::vector<uint16_t> bg = bin_groups(*m);
+        std::vector<uint16_t> rgroup(bg.begin() + row_lo, bg.begin() + row_hi);
+        TilePlan P = plan_tiles(hc.data(), nloc, nJ, rgroup);
+        upload_plan(P, *m, s);
+        m->row_group = to_device(rgroup, s);
+        DBuf<int32_t> tof = to_device(P.tile_of, s);
+        m->pay.alloc(P.n_entries_padded);
+        if (nloc)
+            hipLaunchKernelGGL((k_synth_rows<1>), row_grid(nloc), dim3(256), 0, s, h.dev, (long long)row_lo,
+                               (long long)nloc, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, tof.p,
+                               m->tile_ent.p, m->tile_rp.p, m->pay.p);
+        HIP_CHECK(hipGetLastError());
+        std::vector<long long> wz(nloc + 1, 0);  // no wide entries (counts clamped)
+        m->wide_ptr = to_device(wz, s);
         HIP_CHECK(hipStreamSynchronize(s));
-        double ent = 0;
-        for (int64_t r = 0; r < nloc; ++r) ent += nz[r];
-        L.n_entries = (int64_t)ent;  // includes 2x diag indicator; diag is 0 when ignored
+        m->nnz_upper = std::accumulate(up.begin(), up.end(), 0LL);
+        int64_t ent = 0;
+        for (size_t i = 0; i < hc.size(); ++i) ent += hc[i];
+        m->n_entries = ent;
         *out = m.release();
     });
 }

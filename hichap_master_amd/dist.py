@@ -19,21 +19,27 @@ from __future__ import annotations
 import numpy as np
 
 
-def partition_rows(row_weight, world: int) -> np.ndarray:
-    """Contiguous row ranges with ~equal total weight (e.g. chunks per row).
-    Returns ``rank_rows[world + 1]``."""
+ROW_BLOCK = 256  # shards are whole 256-row blocks of the tiled layout
+
+
+def partition_rows(row_weight, world: int, align: int = ROW_BLOCK) -> np.ndarray:
+    """Contiguous row ranges with ~equal total weight (e.g. stored slots per
+    row), cut at multiples of ``align``.  Returns ``rank_rows[world + 1]``."""
     w = np.asarray(row_weight, dtype=np.float64)
     n = w.size
     if world <= 1 or n == 0:
         return np.array([0, n], dtype=np.int64)
-    cum = np.concatenate([[0.0], np.cumsum(w)])
+    nb = (n + align - 1) // align
+    wb = np.zeros(nb * align)
+    wb[:n] = w
+    cum = np.concatenate([[0.0], np.cumsum(wb.reshape(nb, align).sum(axis=1))])
     tot = cum[-1]
     cuts = [0]
     for r in range(1, world):
         c = int(np.searchsorted(cum, tot * r / world, side="left"))
-        cuts.append(min(max(c, cuts[-1]), n))
-    cuts.append(n)
-    return np.asarray(cuts, dtype=np.int64)
+        cuts.append(min(max(c, cuts[-1]), nb))
+    cuts.append(nb)
+    return np.minimum(np.asarray(cuts, dtype=np.int64) * align, n)
 
 
 class Exchange:

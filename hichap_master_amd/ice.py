@@ -69,17 +69,15 @@ class ContactMatrix:
         return cls(h, off)
 
     @classmethod
-    def synthetic(cls, chrom_nbins, row_range=None, row_chunks=None, stream=None, **kw):
-        """Generate a synthetic genome in HBM (see synth_params)."""
+    def synthetic(cls, chrom_nbins, row_range=None, stream=None, **kw):
+        """Generate a synthetic genome in HBM (see synth_params); rows
+        ``row_range`` (aligned to 256-row blocks) or all."""
         _lib.require_gpu()
         p, keep = synth_params(chrom_nbins, **kw)
         n = int(np.sum(chrom_nbins))
-        if row_chunks is None:
-            row_chunks, _ = synth_row_counts(chrom_nbins, stream=stream, **kw)
-        rc = np.ascontiguousarray(row_chunks, dtype=np.int32)
         lo, hi = (0, n) if row_range is None else (int(row_range[0]), int(row_range[1]))
         h = C.c_void_p()
-        call("hh_synth_build", C.byref(p), ptr(rc), lo, hi, stream, C.byref(h))
+        call("hh_synth_build", C.byref(p), lo, hi, stream, C.byref(h))
         off = np.concatenate([[0], np.cumsum(chrom_nbins)]).astype(np.int64)
         return cls(h, off)
 
@@ -125,8 +123,8 @@ def synth_params(chrom_nbins, A=30.0, decay=1.08, comp_strength=0.3, vis_sigma=0
 
 
 def synth_row_counts(chrom_nbins, stream=None, **kw):
-    """Pass 1 of the generator: per-row chunk counts and upper-triangle pixel
-    counts for every row (used to partition rows across ranks)."""
+    """Counting pass of the generator: per-row stored slots (work) and
+    upper-triangle pixel counts for every row (used to partition rows)."""
     _lib.require_gpu()
     p, keep = synth_params(chrom_nbins, **kw)
     n = int(np.sum(chrom_nbins))

@@ -44,13 +44,14 @@ int hh_synchronize(void* stream);
 int hh_tune(const char* key, int64_t value);
 
 /* ---------------------------------------------------- contact matrix
- * A contact matrix resident in HBM in the "pixel-chunk" layout:
+ * A contact matrix resident in HBM in the "tiled pixel" layout:
  * the symmetric matrix (both triangles of cooler's upper-triangle pixel table)
- * stored row by row for the rows [row_lo, row_hi) a rank owns, each row cut
- * into chunks of 256 entries packed as uint32 (count:16 | col - base:16) with
- * one int32 base column per chunk, plus an overflow layer for counts >= 2^16
- * and a per-row diagonal.  Static filters (ignore_diags, cis_only zero_trans,
- * zero counts) are applied at build time.
+ * for the rows [row_lo, row_hi) a rank owns, cut into 256-row blocks x
+ * 8192-column tiles; each tile stores its rows' entries as uint32
+ * (count << 13 | column offset), rows padded to 16 B, counts >= 2^19 in a
+ * small per-row wide list, plus a per-row diagonal.  Static filters
+ * (ignore_diags, cis_only zero_trans, zero counts) are applied at build time.
+ * Shards are whole 256-row blocks (row_lo % 256 == 0).
  */
 typedef struct hh_matrix hh_matrix;
 
@@ -59,10 +60,10 @@ typedef struct {
     int64_t row_lo, row_hi;/* rows held by this object                      */
     int64_t nnz_upper;     /* kept pixels with bin2 - bin1 >= ignore_diags   */
     int64_t n_entries;     /* symmetric off-diagonal entries stored          */
-    int64_t n_slots;       /* chunk slots (entries + padding)                */
-    int64_t n_chunks;
-    int64_t n_segments;
-    int64_t n_ovf_chunks;  /* chunks of the >= 2^16 overflow layer          */
+    int64_t n_slots;       /* stored uint32 slots (entries + row padding)    */
+    int64_t n_tiles;       /* nonempty (row-block, column-tile) pairs        */
+    int64_t n_units;       /* sweep work units                               */
+    int64_t n_wide;        /* entries with count >= 2^19 (wide list)         */
     int64_t device_bytes;  /* HBM held by the matrix                         */
     int32_t n_chroms;
     int32_t ignore_diags;
@@ -106,13 +107,13 @@ typedef struct {
     uint64_t seed;
 } hh_synth_params;
 
-/* Pass 1 over ALL rows: per-row chunk counts and upper-triangle pixel counts
- * (host arrays of n_bins). Used to partition rows across ranks. */
-int hh_synth_count(const hh_synth_params* p, int32_t* row_chunks, int64_t* row_nnz_upper,
+/* Counting pass over ALL rows: per-row stored slots (work) and upper-triangle
+ * pixel counts (host arrays of n_bins).  Used to partition rows across ranks. */
+int hh_synth_count(const hh_synth_params* p, int32_t* row_work, int64_t* row_nnz_upper,
                    void* stream);
-/* Pass 2: build rows [row_lo, row_hi) using the pass-1 chunk counts. */
-int hh_synth_build(const hh_synth_params* p, const int32_t* row_chunks, int64_t row_lo,
-                   int64_t row_hi, void* stream, hh_matrix** out);
+/* Build rows [row_lo, row_hi) (row_lo % 256 == 0). */
+int hh_synth_build(const hh_synth_params* p, int64_t row_lo, int64_t row_hi, void* stream,
+                   hh_matrix** out);
 
 /* ---------------------------------------------------------------- ICE
  * cooler's balance_cooler semantics (oracle/ice_ref.py). */

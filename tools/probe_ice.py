@@ -17,11 +17,11 @@ kw = dict(A=A, trans_density=td)
 t0 = time.time()
 rc, ru = ice.synth_row_counts(sizes, **kw)
 t1 = time.time()
-m = ice.ContactMatrix.synthetic(sizes, row_chunks=rc, **kw)
+m = ice.ContactMatrix.synthetic(sizes, **kw)
 t2 = time.time()
 inf = m.info()
 print(f"{name}: A={A:.1f} td={td:.3g} n={inf['n_bins']} nnz_upper={inf['nnz_upper']:.4g} entries={inf['n_entries']:.4g} "
-      f"slots={inf['n_slots']:.4g} fill={inf['n_entries']/max(inf['n_slots'],1):.3f} "
+      f"slots={inf['n_slots']:.4g} fill={inf['n_entries']/max(inf['n_slots'],1):.3f} tiles={inf['n_tiles']} units={inf['n_units']} "
       f"bytes={inf['device_bytes']/1e9:.2f}GB count={t1-t0:.2f}s build={t2-t1:.2f}s", flush=True)
 st = ice.IceState(m, ice.IceOptions(tol=0.0, max_iters=10**6, mad_max=0, min_nnz=0))
 def run(label):
@@ -30,18 +30,9 @@ def run(label):
     ms, n, it_ms = st.last_timing()
     sw = ms / n
     alg = 12.0 * inf["nnz_upper"]
-    real = 4.0 * inf["n_slots"] + 4.0 * inf["n_chunks"]
+    real = 4.0 * inf["n_slots"]
     print(f"  {label:28s} sweep {sw:.3f} ms  iter {it_ms/n:.3f} ms  it/s {1000*n/it_ms:.1f}  "
           f"alg {alg/sw/1e6:.0f} GB/s  real {real/sw/1e6:.0f} GB/s", flush=True)
 
-def tune(k, v):
-    _lib.call("hh_tune", k.encode(), v)
-
-for abl in (0, 1, 2):
-    tune("sweep_ablate", abl)
-    for pers in (0, 4, 8):
-        tune("sweep_persist", pers)
-        for U in (2, 4):
-            tune("sweep_unroll", U)
-            run(f"abl={abl} persist={pers} U={U}")
-tune("sweep_ablate", 0); tune("sweep_persist", 0); tune("sweep_unroll", 4)
+run("tiled")
+run("tiled")
