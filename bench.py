@@ -82,6 +82,8 @@ def main():
     ap.add_argument("--config", default="c4")
     ap.add_argument("--nnz", type=float, default=None)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--sharded", action="store_true",
+                    help="use the multi-GPU (all-gather) driver even at N=1 (path check)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -92,8 +94,10 @@ def main():
     from hichap_master_amd import _lib, dist, ice
     _lib.load()
     _lib.call("hh_set_device", local)
-    if world > 1:
+    if world > 1 or args.sharded:
         import torch.distributed as tdist
+        if "MASTER_ADDR" not in os.environ:
+            os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT="29531", RANK="0", WORLD_SIZE="1")
         tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     sizes, kw, label, target, tf = config(args.config, args.nnz)
@@ -110,11 +114,11 @@ def main():
     stream = torch.cuda.current_stream().cuda_stream
 
     def barrier():
-        if world > 1:
+        if torch.distributed.is_initialized():
             torch.distributed.barrier()
         torch.cuda.synchronize()
 
-    if world == 1:
+    if world == 1 and not args.sharded:
         # filters (untimed), then warmup + timed iterations in one C++ loop each
         st.marg_local(0, None, stream); st.filter_nnz(stream)
         st.marg_local(1, None, stream); st.filter_count_mad(stream)
@@ -136,7 +140,7 @@ def main():
         elapsed = time.perf_counter() - t_start
         sweep_ms, launches, iter_ms = float("nan"), 0, float("nan")
     tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-    if world > 1:
+    if torch.distributed.is_initialized():
         torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
     elapsed = float(tt.item())
 
@@ -157,7 +161,7 @@ def main():
                        "tiles": inf["n_tiles"], "units": inf["n_units"],
                        "hbm_bytes_matrix": inf["device_bytes"]},
         }
-        if world == 1 and launches:
+        if launches:
             sweep_avg = sweep_ms / launches / 1000.0
             achieved = ALG_BYTES_PER_PIXEL * inf["nnz_upper"] / sweep_avg / 1e9
             out["roofline"] = {"bound": "hbm", "kernel": "k_sweep_tiled", "achieved": achieved,
@@ -169,7 +173,7 @@ def main():
         if world == 1 and not args.no_cpu:
             out["cpu_baseline"] = cpu_baseline(sizes, kw, rc, nnz_total)
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if torch.distributed.is_initialized():
         torch.distributed.destroy_process_group()
 
 

@@ -53,7 +53,7 @@ __device__ __forceinline__ double tile_dot(const uint4 v, const double* __restri
 
 // NB row batches of a wave in flight together (loads of all of them issued
 // before any is consumed) so short rows still keep ~NB KiB per wave in flight.
-template <int G, int NB>
+template <int G, int NB, int ABL>
 __device__ __forceinline__ void tile_rows(const uint4* __restrict__ pay4, const uint32_t* __restrict__ rp,
                                           const double* __restrict__ bl, double* __restrict__ acc, int ra,
                                           int rb, int wave, int lane) {
@@ -83,7 +83,11 @@ __device__ __forceinline__ void tile_rows(const uint4* __restrict__ pay4, const 
             more = false;
 #pragma unroll
             for (int k = 0; k < NB; ++k) {
-                a[k] = tile_dot(v[k], bl, a[k]);
+                if (ABL == 1) {  // timing ablation: no LDS gathers
+                    a[k] += (double)(v[k].x + v[k].y + v[k].z + v[k].w);
+                } else {
+                    a[k] = tile_dot(v[k], bl, a[k]);
+                }
                 q[k] += G;
                 more |= q[k] < qe[k];
             }
@@ -99,11 +103,13 @@ __device__ __forceinline__ void tile_rows(const uint4* __restrict__ pay4, const 
     }
 }
 
+template <int NB, int ABL>
 __global__ __launch_bounds__(kSweepThreads) void k_sweep_tiled(TileDev T, const uint8_t* __restrict__ act,
                                                                 int n_units, const double* __restrict__ b,
                                                                 long long n_bins, double* __restrict__ part) {
     __shared__ __attribute__((aligned(16))) double bl[kW];
     __shared__ double acc[kR];
+    __shared__ uint32_t rps[kR + 1];
     const int u = blockIdx.x;
     if (u >= n_units) return;
     {
@@ -117,7 +123,9 @@ __global__ __launch_bounds__(kSweepThreads) void k_sweep_tiled(TileDev T, const 
     for (int t = T.u_tlo[u]; t < T.u_thi[u]; ++t) {
         const long long c0 = (long long)T.tile_J[t] * kW;
         __syncthreads();  // previous tile's LDS reads are done
-        if (c0 + kW <= n_bins) {
+        if (ABL == 2) {
+            // timing ablation: no staging
+        } else if (c0 + kW <= n_bins) {
             const double2* src = reinterpret_cast<const double2*>(b + c0);
             double2 v[kW / 2 / kSweepThreads];
 #pragma unroll
@@ -131,17 +139,21 @@ __global__ __launch_bounds__(kSweepThreads) void k_sweep_tiled(TileDev T, const 
         } else {
             for (int k = threadIdx.x; k < kW; k += kSweepThreads) bl[swz(k)] = c0 + k < n_bins ? b[c0 + k] : 0.0;
         }
+        {
+            const uint32_t* rpg = T.tile_rp + (size_t)t * (kR + 1);
+            for (int k = threadIdx.x; k <= kR; k += kSweepThreads) rps[k] = rpg[k];
+        }
         __syncthreads();
-        const uint32_t* rp = T.tile_rp + (size_t)t * (kR + 1);
+        const uint32_t* rp = rps;
         const uint4* pay4 = reinterpret_cast<const uint4*>(T.pay + T.tile_ent[t]);
         // lane-group width from the mean row length of the unit's rows in this tile
         const uint32_t tot = rp[rb] - rp[ra];
         const uint32_t mean4 = tot / (uint32_t)(4 * (rb - ra));  // uint4 per row
-        if (mean4 >= 48) tile_rows<64, 4>(pay4, rp, bl, acc, ra, rb, wave, lane);
-        else if (mean4 >= 24) tile_rows<32, 4>(pay4, rp, bl, acc, ra, rb, wave, lane);
-        else if (mean4 >= 12) tile_rows<16, 4>(pay4, rp, bl, acc, ra, rb, wave, lane);
-        else if (mean4 >= 6) tile_rows<8, 4>(pay4, rp, bl, acc, ra, rb, wave, lane);
-        else tile_rows<4, 4>(pay4, rp, bl, acc, ra, rb, wave, lane);
+        if (mean4 >= 48) tile_rows<64, NB, ABL>(pay4, rp, bl, acc, ra, rb, wave, lane);
+        else if (mean4 >= 24) tile_rows<32, NB, ABL>(pay4, rp, bl, acc, ra, rb, wave, lane);
+        else if (mean4 >= 12) tile_rows<16, NB, ABL>(pay4, rp, bl, acc, ra, rb, wave, lane);
+        else if (mean4 >= 6) tile_rows<8, NB, ABL>(pay4, rp, bl, acc, ra, rb, wave, lane);
+        else tile_rows<4, NB, ABL>(pay4, rp, bl, acc, ra, rb, wave, lane);
     }
     __syncthreads();
     for (int k = threadIdx.x; k < rb - ra; k += kSweepThreads) part[T.u_slot[u] + k] = acc[k];
@@ -343,10 +355,33 @@ struct hh_ice {
 
 namespace hh {
 
+// Tuning knobs (hh_tune; no effect on results except the ablations).
+static int g_sweep_nb = 4;
+static int g_sweep_ablate = 0;
+
+template <int NB, int ABL>
+static void launch_sweep(const hh_matrix* m, const uint8_t* act, const double* b, double* part, hipStream_t s) {
+    hipLaunchKernelGGL((k_sweep_tiled<NB, ABL>), dim3((unsigned)m->n_units), dim3(kSweepThreads), 0, s, m->dev(),
+                       act, (int)m->n_units, b, (long long)m->n_bins, part);
+}
+
+template <int ABL>
+static void launch_sweep_nb(const hh_matrix* m, const uint8_t* act, const double* b, double* part, hipStream_t s) {
+    switch (g_sweep_nb) {
+        case 1: launch_sweep<1, ABL>(m, act, b, part, s); break;
+        case 2: launch_sweep<2, ABL>(m, act, b, part, s); break;
+        case 8: launch_sweep<8, ABL>(m, act, b, part, s); break;
+        default: launch_sweep<4, ABL>(m, act, b, part, s); break;
+    }
+}
+
 static void sweep(const hh_matrix* m, const uint8_t* act, const double* b, double* part, hipStream_t s) {
     if (m->n_units == 0) return;
-    hipLaunchKernelGGL(k_sweep_tiled, dim3((unsigned)m->n_units), dim3(kSweepThreads), 0, s, m->dev(), act,
-                       (int)m->n_units, b, (long long)m->n_bins, part);
+    switch (g_sweep_ablate) {
+        case 1: launch_sweep_nb<1>(m, act, b, part, s); break;
+        case 2: launch_sweep_nb<2>(m, act, b, part, s); break;
+        default: launch_sweep_nb<0>(m, act, b, part, s); break;
+    }
     HIP_CHECK(hipGetLastError());
 }
 
@@ -390,8 +425,15 @@ int hh_tune(const char* key, int64_t value) {
     return guard([&] {
         HH_REQUIRE(key, "null key");
         const std::string k(key);
-        if (k == "none") {
-            (void)value;        } else {
+        if (k == "sweep_nb") {
+            HH_REQUIRE(value == 1 || value == 2 || value == 4 || value == 8, "sweep_nb must be 1, 2, 4 or 8");
+            g_sweep_nb = (int)value;
+        } else if (k == "sweep_ablate") {
+            HH_REQUIRE(value >= 0 && value <= 2, "sweep_ablate must be 0, 1 or 2");
+            g_sweep_ablate = (int)value;
+        } else if (k == "unit_entries") {
+            HH_REQUIRE(value == 0 || (value >= 4096 && value <= (1 << 24)), "unit_entries must be 0 (auto) or in [4096, 2^24]");
+            g_unit_entries = value;        } else {
             HH_THROW(HH_ERR_ARG, "unknown tuning key " + k);
         }
     });

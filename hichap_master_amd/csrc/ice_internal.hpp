@@ -27,7 +27,7 @@ constexpr int kWBits = 13;
 constexpr int kW = 1 << kWBits;         // columns per tile
 constexpr uint32_t kColMask = kW - 1;
 constexpr uint32_t kCntMax = (1u << (32 - kWBits)) - 1u;  // 2^19 - 1
-constexpr int64_t kUnitEntries = 1 << 17;                 // ~512 KiB of payload per unit
+extern int64_t g_unit_entries;                           // ~512 KiB of payload per unit (hh_tune)
 constexpr int64_t kMaxBins = (int64_t)1 << 30;
 
 inline int64_t pad4(int64_t x) { return (x + 3) & ~(int64_t)3; }

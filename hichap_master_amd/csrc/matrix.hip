@@ -10,6 +10,7 @@
 namespace hh {
 
 static thread_local std::string g_last_error;
+int64_t g_unit_entries = 0;  // 0 = auto (plan_tiles)
 void set_error(const std::string& msg) { g_last_error = msg; }
 
 TilePlan plan_tiles(const uint16_t* cnt, int64_t nloc, int32_t nJ, const std::vector<uint16_t>& row_group) {
@@ -43,7 +44,10 @@ TilePlan plan_tiles(const uint16_t* cnt, int64_t nloc, int32_t nJ, const std::ve
     }
     P.blk_tile_ptr[P.nrb] = (int32_t)P.tile_J.size();
     P.n_entries_padded = ent;
-    // units
+    // units: ~4 MiB of payload each on big matrices (measured best on C4),
+    // but at least ~4096 units so small matrices still fill 256 CUs.
+    const int64_t unit_cap = g_unit_entries > 0 ? g_unit_entries
+                                                : std::max<int64_t>(1 << 15, std::min<int64_t>(1 << 20, ent / 4096));
     auto emit = [&](int64_t rb, int32_t ta, int32_t tb, int32_t rlo, int32_t rhi) {
         const int64_t g0 = rb * kR + rlo, g1 = rb * kR + rhi - 1;
         P.u_tlo.push_back(ta);
@@ -65,13 +69,13 @@ TilePlan plan_tiles(const uint16_t* cnt, int64_t nloc, int32_t nJ, const std::ve
         for (int32_t t = ta; t < tb; ++t) {
             const uint32_t* trp = &P.tile_rp[(size_t)t * (kR + 1)];
             const int64_t sz = trp[kR];
-            if (sz > kUnitEntries) {
+            if (sz > unit_cap) {
                 if (cur < t) emit(rb, cur, t, 0, nr);
                 int32_t rlo = 0;
                 int64_t acc = 0;
                 for (int32_t k = 0; k < nr; ++k) {
                     const int64_t len = trp[k + 1] - trp[k];
-                    if (acc > 0 && acc + len > kUnitEntries) {
+                    if (acc > 0 && acc + len > unit_cap) {
                         emit(rb, t, t + 1, rlo, k);
                         rlo = k;
                         acc = 0;
@@ -82,7 +86,7 @@ TilePlan plan_tiles(const uint16_t* cnt, int64_t nloc, int32_t nJ, const std::ve
                 cur = t + 1;
                 cur_sz = 0;
             } else {
-                if (cur < t && cur_sz + sz > kUnitEntries) {
+                if (cur < t && cur_sz + sz > unit_cap) {
                     emit(rb, cur, t, 0, nr);
                     cur = t;
                     cur_sz = 0;

@@ -40,7 +40,10 @@ int hh_version(void);                 /* (major<<16)|(minor<<8)|patch */
 int hh_device_count(int32_t* n);
 int hh_set_device(int32_t device);
 int hh_synchronize(void* stream);
-/* Performance knobs (no effect on results): "sweep_unroll" in {1,2,4,8}. */
+/* Performance knobs: "sweep_nb" in {1,2,4,8} (row batches in flight per
+ * wave), "unit_entries" (work-unit size used by later matrix builds),
+ * "sweep_ablate" 0/1/2 (timing ablations only: 1 skips the LDS gathers,
+ * 2 skips the b staging; results are wrong while set). */
 int hh_tune(const char* key, int64_t value);
 
 /* ---------------------------------------------------- contact matrix
