@@ -45,6 +45,20 @@ def config(name, nnz=None):
     return sizes, dict(A=A, trans_density=td, comp_block=200, seed=20201015), label, target, tf
 
 
+def pmc_traffic(kernel="k_sweep_tiled"):
+    """HBM bytes per launch of the sweep kernel from the committed rocprofv3
+    PMC summary of this same command (tools/pmc_summary.py), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_c4_pmc.json")))
+    if not files:
+        return None, None
+    data = json.load(open(files[-1]))
+    for k, v in data.items():
+        if kernel in k:
+            return v["traffic_bytes"], os.path.relpath(files[-1], ROOT)
+    return None, None
+
+
 def cpu_baseline(sizes, kw, rc, nnz_total, budget_s=12.0):
     """Oracle (NumPy, cooler's bincount sweep) timed on the host on a bounded
     sample: the upper-triangle pixels of the first rows of the same matrix."""
@@ -161,12 +175,15 @@ def main():
                        "tiles": inf["n_tiles"], "units": inf["n_units"],
                        "hbm_bytes_matrix": inf["device_bytes"]},
         }
+        traffic, traffic_src = (pmc_traffic() if args.config == "c4" and args.nnz is None
+                                else (None, None))
         if launches:
             sweep_avg = sweep_ms / launches / 1000.0
             achieved = ALG_BYTES_PER_PIXEL * inf["nnz_upper"] / sweep_avg / 1e9
             out["roofline"] = {"bound": "hbm", "kernel": "k_sweep_tiled", "achieved": achieved,
                                "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS,
-                               "traffic": None,
+                               "traffic": traffic,
+                               "traffic_source": traffic_src,
                                "real_bytes_per_launch": 4.0 * inf["n_slots"] + 4.0 * 257 * inf["n_tiles"],
                                "sweep_ms_avg": sweep_avg * 1000.0,
                                "iter_ms_avg": iter_ms / launches}
