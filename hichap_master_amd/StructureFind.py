@@ -1,0 +1,333 @@
+"""StructureFind numeric cores on MI355X — same class / method names and
+arguments as ``HiCHap/StructureFind.py``:
+
+* ``Distance_Decay(M, G_array)``          StructureFind.py:201-271
+* ``Get_PCA(distance_bin, M, NG_array)``   :302-342
+* ``Select_PC_new(Cor_M, OE_M, pca)``      :374-423
+* ``Select_Allelic_PC(pcs, trad_pc)``      :446-460
+* ``Get_Gap(M)`` / ``Get_DI(M, Gap, w)``   :721-751 / :804-839
+* ``Gap_Filter(Gap, M)``                   :753-802
+
+The O(N^2) / O(N^2 n) work (column nonzeros, per-distance sums, O/E,
+Pearson correlation on fp64 MFMA, top-3 PCA, the masked sums of the PC
+selection, the windowed DI statistics) runs in HIP kernels; O(N) decisions
+(gap thresholds, bin counts, the selection rules) are host glue written with
+the reference's own NumPy expressions.  ``Get_PCA`` returns the correlation
+and O/E matrices as lazy device-backed arrays (``np.asarray`` materialises
+them) so the N x N products stay in HBM for ``Select_PC_new``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from ._lib import call, ptr
+
+PCA_TOL = 1e-13   # max entry change of the unit Ritz vectors between iterations
+PCA_MAX_ITERS = 2000
+
+
+class _Comp:
+    """Owns an ``hh_comp*`` (one chromosome's matrix in HBM)."""
+
+    def __init__(self, M):
+        _lib.require_gpu()
+        self.M = np.ascontiguousarray(M, dtype=np.float64)
+        if self.M.ndim != 2 or self.M.shape[0] != self.M.shape[1]:
+            raise ValueError("expected a square matrix")
+        self.N = self.M.shape[0]
+        h = C.c_void_p()
+        call("hh_comp_create", ptr(self.M), self.N, 0, None, C.byref(h))
+        self.h = h
+        self.decline = None
+        self.NG = None
+
+    def colnnz(self):
+        out = np.empty(self.N, np.int64)
+        call("hh_comp_colnnz", self.h, ptr(out), None)
+        return out
+
+    def diag_sums(self, gap_mask):
+        g = np.ascontiguousarray(gap_mask, dtype=np.uint8)
+        out = np.empty(self.N, np.float64)
+        call("hh_comp_diag_sums", self.h, ptr(g), ptr(out), None)
+        return out
+
+    def correlation(self, decline, NG):
+        self.decline = np.ascontiguousarray(decline, dtype=np.float64)
+        self.NG = np.ascontiguousarray(NG, dtype=np.int64)
+        call("hh_comp_correlation", self.h, ptr(self.decline), ptr(self.NG), self.NG.size, None)
+
+    def cor(self):
+        n = self.NG.size
+        out = np.empty((n, n), np.float64)
+        call("hh_comp_get_cor", self.h, ptr(out), None)
+        return out
+
+    def pca(self, k=3):
+        n = self.NG.size
+        comps = np.empty((k, n), np.float64)
+        ev = np.empty(k, np.float64)
+        it = C.c_int32(0)
+        call("hh_comp_pca", self.h, int(k), PCA_TOL, PCA_MAX_ITERS, ptr(comps), ptr(ev), C.byref(it), None)
+        return comps, ev, it.value
+
+    def select_stats(self, pcs, eps=1e-5):
+        p = np.ascontiguousarray(pcs, dtype=np.float64)
+        k = p.shape[0]
+        st = np.empty((k, 8), np.float64)
+        call("hh_comp_select_stats", self.h, ptr(p), int(k), float(eps), ptr(st), None)
+        return st
+
+    def __del__(self):
+        try:
+            if self.h:
+                call("hh_comp_free", self.h)
+                self.h = None
+        except Exception:
+            pass
+
+
+class DeviceCorrelation:
+    """Lazy n x n correlation matrix held in HBM (``np.asarray`` downloads)."""
+
+    def __init__(self, comp: _Comp):
+        self._c = comp
+        self.shape = (comp.NG.size, comp.NG.size)
+        self._host = None
+
+    def __array__(self, dtype=None, copy=None):
+        if self._host is None:
+            self._host = self._c.cor()
+        return self._host if dtype is None else self._host.astype(dtype)
+
+
+class DeviceOE:
+    """Lazy O/E matrix ``OE[:, NG]`` (N x n); ``[NG]`` gives the NG rows, the
+    form Select_PC_new receives (StructureFind.py:519)."""
+
+    def __init__(self, comp: _Comp, rows=None):
+        self._c = comp
+        self._rows = rows
+        n = comp.NG.size
+        self.shape = (comp.N if rows is None else len(rows), n)
+
+    def __getitem__(self, idx):
+        rows = np.arange(self._c.N)[idx] if self._rows is None else np.asarray(self._rows)[idx]
+        return DeviceOE(self._c, np.asarray(rows, dtype=np.int64))
+
+    def __array__(self, dtype=None, copy=None):
+        c = self._c
+        rows = np.arange(c.N) if self._rows is None else self._rows
+        sub = c.M[np.ix_(rows, c.NG)]
+        d = np.abs(rows[:, None] - c.NG[None, :])
+        out = np.zeros_like(sub)
+        nz = sub != 0
+        out[nz] = sub[nz] / c.decline[d[nz]]
+        return out if dtype is None else out.astype(dtype)
+
+
+class StructureFind(object):
+    """Numeric part of HiCHap's StructureFind (StructureFind.py:27)."""
+
+    def __init__(self, cooler_fil=None, Res=40000, Allelic=False, GapFile=None, Loop_ratio=0.6,
+                 Loop_strength=16):
+        self.cooler_fil = "{}::{}".format(cooler_fil, Res) if cooler_fil else None
+        self.Res = Res
+        self.Allelic = Allelic
+        self.Gap_file = GapFile
+        self.ratio = Loop_ratio
+        self.LoopStrength = Loop_strength
+        self._comp = None
+        self._comp_src = None
+
+    # ------------------------------------------------------ compartments
+    def Distance_Decay(self, M, G_array):
+        """Distance-decay expected counts (StructureFind.py:201-271).
+        Returns (distance_bin, G_array, NG_array)."""
+        comp = _Comp(M)
+        self._comp, self._comp_src = comp, M
+        size = comp.N
+        bin_arange = np.arange(size)
+        if G_array is None:
+            nonzero_mask = comp.colnnz() / float(size)
+            gap_mask = np.where(nonzero_mask <= 0.05, True, False)
+            G_array = bin_arange[gap_mask]
+            NG_array = bin_arange[~gap_mask]
+        else:
+            G_array = np.asarray(G_array)
+            gap_mask = np.zeros(size, dtype=bool)
+            gap_mask[G_array.astype(np.int64)] = True
+            NG_array = bin_arange[~gap_mask]
+        distance_bin = comp.diag_sums(gap_mask)
+        # bin counts per distance (the reference's loop :252-268, vectorised)
+        Gs = np.sort(np.asarray(G_array, dtype=np.int64))
+        dd = np.arange(size)
+        gap_num = (np.searchsorted(Gs, size - 1 - dd, side="right")
+                   + (Gs.size - np.searchsorted(Gs, dd, side="left")))
+        bin_num = np.asarray((size - dd), dtype=float) * 2 - gap_num
+        bin_num[0] = float(size - 0) - np.sum((0 <= Gs) & (Gs <= size - 1))
+        ok = bin_num > 0
+        distance_bin[ok] = distance_bin[ok] / bin_num[ok]
+        return distance_bin, G_array, NG_array
+
+    def Get_PCA(self, distance_bin, M, NG_array, SA=False):
+        """O/E, Pearson correlation and top-3 PCA (StructureFind.py:302-342).
+        Returns (pca_components[3 x n], Cor (lazy), OE[:, NG] (lazy))."""
+        if SA:
+            raise NotImplementedError("Sliding_Approach (SA=True) is not on the GPU path")
+        comp = self._comp if (self._comp is not None and self._comp_src is M) else None
+        if comp is None:
+            comp = _Comp(M)
+            self._comp, self._comp_src = comp, M
+        decline = distance_bin
+        decline[decline == 0] = decline[np.nonzero(decline)].min()
+        comp.correlation(decline, NG_array)
+        pcs, _, _ = comp.pca(3)
+        return pcs, DeviceCorrelation(comp), DeviceOE(comp)
+
+    def Select_PC_new(self, Cor_M, OE_M, pca):
+        """PC choice and A/B sign (StructureFind.py:374-423)."""
+        pca = np.asarray(pca)
+        if isinstance(Cor_M, DeviceCorrelation):
+            comp = Cor_M._c
+        else:
+            comp = _array_comp(np.asarray(Cor_M), np.asarray(OE_M))
+        st = comp.select_stats(pca[:3])
+        nums, values = 0, 0
+        for i in range(len(pca)):
+            minus = _means_minus(st[i], pca[i])
+            if minus > values:
+                values, nums = minus, i
+        pc = pca[nums]
+        with np.errstate(invalid="ignore", divide="ignore"):
+            values_a = st[nums, 4] / st[nums, 5]
+            values_b = st[nums, 6] / st[nums, 7]
+        if values_b > values_a:
+            pc = pc.copy() * -1
+        return pc
+
+    def Select_Allelic_PC(self, pca_components, Tranditional_PC, eps=0.7):
+        """Supervised PC choice for haplotype data (StructureFind.py:446-460)."""
+        PCC = [abs(np.corrcoef(pc, Tranditional_PC)[0][1]) for pc in pca_components]
+        if np.max(PCC) < eps:
+            print("    PCC too low for this chromosome, check it if possible!")
+        return pca_components[int(np.argmax(PCC))]
+
+    def compartment(self, M, Tranditional_PC=None):
+        """Per-chromosome body of Compartment() (StructureFind.py:509-527):
+        the selected PC at full length (zeros at gap bins)."""
+        M = np.asarray(M, dtype=np.float64)
+        distance_bin, Gap, NonGap = self.Distance_Decay(M=M, G_array=None)
+        pca, Cor_M, OE_M = self.Get_PCA(distance_bin=distance_bin, M=M, NG_array=NonGap)
+        out = np.zeros((M.shape[0],), dtype=float)
+        if Tranditional_PC is None:
+            out[NonGap] = self.Select_PC_new(Cor_M, OE_M[NonGap], pca)
+        else:
+            raw = np.zeros((len(pca), M.shape[0]))
+            raw[:, NonGap] = pca
+            out[NonGap] = self.Select_Allelic_PC(raw, Tranditional_PC)[NonGap]
+        return out
+
+
+    # --------------------------------------------------------------- TADs
+    def TAD_parameter_init(self, minTAD, maxTAD, state_num, window, test_type):
+        """Prior parameters of the TAD scan (StructureFind.py:709-718)."""
+        self.minTAD, self.maxTAD, self.state_num = minTAD, maxTAD, state_num
+        self.window, self.test_type = window, test_type
+
+    def Get_Gap(self, M):
+        """Gap columns for TAD calling (StructureFind.py:721-751)."""
+        _lib.require_gpu()
+        A = np.ascontiguousarray(M, dtype=np.float64)
+        N = A.shape[0]
+        g = np.empty(N, np.uint8)
+        call("hh_gap_scan", ptr(A), N, int(self.minTAD / self.Res), ptr(g), 0, None)
+        return np.nonzero(g)[0]
+
+    def Get_DI(self, M, Gap, window_bin):
+        """Directionality index (StructureFind.py:804-839)."""
+        _lib.require_gpu()
+        A = np.ascontiguousarray(M, dtype=np.float64)
+        N = A.shape[0]
+        g = np.zeros(N, np.uint8)
+        g[np.asarray(Gap, dtype=np.int64)] = 1
+        w = np.ascontiguousarray(np.broadcast_to(np.asarray(window_bin), (N,)), dtype=np.int32)
+        if self.test_type not in ("ttest", "chitest"):
+            return np.zeros(N)
+        di = np.empty(N, np.float64)
+        call("hh_di_scan", ptr(A), N, ptr(g), ptr(w), 0 if self.test_type == "ttest" else 1, ptr(di), 0, None)
+        return di
+
+    def Gap_Filter(self, Gap, M):
+        """Gap runs kept for HMM training (StructureFind.py:753-802): runs of
+        consecutive gap bins at least min(10, mean run length) long, plus the
+        first and last bin."""
+        Gap = np.asarray(Gap)
+        if Gap.shape[0] <= 1:
+            return []
+        runs = []
+        start = end = int(Gap[0])
+        L = Gap.shape[0]
+        for i in range(1, L):
+            step = Gap[i] - Gap[i - 1] == 1
+            if step and i == L - 1:
+                end = int(Gap[i]) + 1
+                runs.append((start, end))
+            elif step:
+                end = int(Gap[i]) + 1
+            else:
+                runs.append((start, end))
+                start, end = int(Gap[i]), int(Gap[i]) + 1
+        runs = sorted(set(runs))
+        mean_len = np.mean([e - s for s, e in runs])
+        kept = [r for r in runs if r[1] - r[0] >= min([10, mean_len])]
+        out = []
+        for s_, e_ in kept:
+            out.extend(range(s_, e_))
+        if 0 not in out:
+            out.insert(0, 0)
+        if np.shape(M)[0] - 1 not in out:
+            out.append(np.shape(M)[0] - 1)
+        return out
+
+    def di_scan(self, M, window=None):
+        """Data_preprocess's per-chromosome scan (:873-891): gap (with the
+        first and last bin) and DI."""
+        N = np.shape(M)[0]
+        gap = list(self.Get_Gap(M))
+        if 0 not in gap:
+            gap.insert(0, 0)
+        if N - 1 not in gap:
+            gap.append(N - 1)
+        gap = np.array(gap)
+        wb = int((self.window if window is None else window) / self.Res)
+        return gap, self.Get_DI(M, gap, np.ones(N, dtype=int) * wb)
+
+
+def _means_minus(st, pc):
+    """means_minus (StructureFind.py:375-402) from the device sums."""
+    loc = np.arange(len(pc))
+    la, lb = loc[pc > 0], loc[pc < 0]
+    if la.shape[0] == 0 or lb.shape[0] == 0:
+        return 0
+    size_a = la.max() - la.min()
+    size_b = lb.max() - lb.min()
+    lens = max(la.max(), lb.max()) - min(la.min(), lb.min())
+    n_ab = st[3]
+    mean_ab = st[2] / n_ab if n_ab else np.nan
+    if n_ab == 0 or mean_ab == 0 or mean_ab == -1 or size_a <= lens / 2 or size_b <= lens / 2:
+        return 0
+    return st[0] / st[1] - mean_ab
+
+
+def _array_comp(Cor, OE_ng):
+    """Select_PC_new on host arrays: upload O/E[NG,NG] as the matrix with a
+    unit decline and the given correlation."""
+    n = Cor.shape[0]
+    comp = _Comp(np.asarray(OE_ng, dtype=np.float64)[:, :n])
+    comp.correlation(np.ones(n), np.arange(n))
+    call("hh_comp_set_cor", comp.h, ptr(np.ascontiguousarray(Cor, dtype=np.float64)), None)
+    return comp

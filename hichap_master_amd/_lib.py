@@ -79,6 +79,19 @@ SIGNATURES = {
     "hh_ice_run": (C.c_int, [P, I32, P]),
     "hh_ice_finalize": (C.c_int, [P, P, P, P, P, P, P]),
     "hh_ice_last_sweep_timing": (C.c_int, [P, PF64, PI32, PF64]),
+    "hh_dense_rowstats": (C.c_int, [P, I32, I64, P, P, P, P, I32, P]),
+    "hh_dense_symvc": (C.c_int, [P, I32, I64, P, P, F64, F64, P, I32, P]),
+    "hh_comp_create": (C.c_int, [P, I64, I32, P, C.POINTER(P)]),
+    "hh_comp_free": (C.c_int, [P]),
+    "hh_comp_colnnz": (C.c_int, [P, P, P]),
+    "hh_comp_diag_sums": (C.c_int, [P, P, P, P]),
+    "hh_comp_correlation": (C.c_int, [P, P, P, I64, P]),
+    "hh_comp_get_cor": (C.c_int, [P, P, P]),
+    "hh_comp_set_cor": (C.c_int, [P, P, P]),
+    "hh_gap_scan": (C.c_int, [P, I64, I32, P, I32, P]),
+    "hh_di_scan": (C.c_int, [P, I64, P, P, I32, P, I32, P]),
+    "hh_comp_pca": (C.c_int, [P, I32, F64, I32, P, P, P, P]),
+    "hh_comp_select_stats": (C.c_int, [P, P, I32, F64, P, P]),
 }
 
 _lib = None

@@ -1,0 +1,792 @@
+// Compartment numerics of StructureFind (StructureFind.py:201-460) for one
+// chromosome's dense N x N raw contact matrix M (float64):
+//
+//   K6 k_colnnz / k_diag_part + k_diag_reduce
+//        column nonzero counts (gap columns, :216-220) and per-distance sums
+//        of nonzero entries whose column is not a gap (:222-249)
+//   K7 k_oe_colsum + k_oe_center   O/E = M / decline[|i-j|] on nonzeros
+//        (:323-329), columns NG only, centred by their means (np.cov)
+//      k_syrk   Cov = Zc^T Zc / (N - 1) on fp64 MFMA (v_mfma_f64_16x16x4)
+//      k_corr_norm   Cor = clip(Cov / sd_i / sd_j, -1, 1), NaN -> 0 (corrcoef)
+//   K8 top-k right singular vectors of the column-centred Cor (sklearn
+//        PCA(3).fit(Cor).components_, :338-340) by block subspace iteration
+//        with Rayleigh-Ritz: A V = Xc^T (Xc V), Xc = Cor - 1 mu^T, applied as
+//        two skinny products with Cor (k_cor_mul); b x b algebra on the host.
+//      k_select_stats  masked sums over Cor and O/E[NG, NG] that
+//        Select_PC_new's means_minus / select_ab need (:374-423).
+// All reductions are fixed-order (deterministic).
+#include <algorithm>
+#include <cmath>
+#include <limits>
+#include <numeric>
+
+#include "hh_common.hpp"
+
+namespace hh {
+
+constexpr int kCT = 64;        // tile edge for M / Cor passes
+constexpr int kSB = 16;        // subspace block size
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+// ------------------------------------------------------------------ K6
+__global__ __launch_bounds__(256) void k_colnnz(const double* __restrict__ M, long long N, int rows_per_block,
+                                                unsigned long long* __restrict__ nnz) {
+    const long long j = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (j >= N) return;
+    const long long r0 = (long long)blockIdx.y * rows_per_block;
+    const long long r1 = std::min<long long>(N, r0 + rows_per_block);
+    unsigned long long c = 0;
+    for (long long i = r0; i < r1; ++i) c += M[i * N + j] != 0.0;
+    atomicAdd(&nnz[j], c);  // integer: order-independent
+}
+
+// per tile (I, J) of the full grid: partial sums over local diagonals
+// delta = c - r in [-63, 63] of entries whose column is not a gap.
+__global__ __launch_bounds__(256) void k_diag_part(const double* __restrict__ M, long long N, long long nT,
+                                                   const uint8_t* __restrict__ gapcol, double* __restrict__ part) {
+    __shared__ double tile[kCT][kCT + 1];
+    const long long I = blockIdx.x / nT, J = blockIdx.x % nT;
+    const long long I0 = I * kCT, J0 = J * kCT;
+    for (int e = threadIdx.x; e < kCT * kCT; e += 256) {
+        const int r = e / kCT, c = e % kCT;
+        const long long gi = I0 + r, gj = J0 + c;
+        double v = 0.0;
+        if (gi < N && gj < N && !gapcol[gj]) v = M[gi * N + gj];
+        tile[r][c] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < 2 * kCT - 1) {
+        const int delta = (int)threadIdx.x - (kCT - 1);
+        double acc = 0.0;
+        for (int r = 0; r < kCT; ++r) {
+            const int c = r + delta;
+            if (c >= 0 && c < kCT) acc += tile[r][c];
+        }
+        part[(size_t)blockIdx.x * (2 * kCT - 1) + threadIdx.x] = acc;
+    }
+}
+
+// decline_raw[d] = sum over |i - j| = d: fixed order over (k = J - I, I).
+__global__ void k_diag_reduce(const double* __restrict__ part, long long N, long long nT, double* __restrict__ out) {
+    const long long d = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (d >= N) return;
+    double acc = 0.0;
+    // global offset g = j - i = 64 k + delta, delta in [-63, 63]; want g = +d and g = -d (d > 0)
+    for (int sgn = 1; sgn >= -1; sgn -= 2) {
+        if (sgn == -1 && d == 0) break;
+        const long long g = sgn * d;
+        const long long klo = (g - (kCT - 1) + (64LL * 4096) ) / kCT - 4096;  // ceil((g-63)/64)
+        for (long long k = klo; k <= klo + 2; ++k) {
+            const long long delta = g - k * kCT;
+            if (delta < -(kCT - 1) || delta > kCT - 1) continue;
+            for (long long I = 0; I < nT; ++I) {
+                const long long J = I + k;
+                if (J < 0 || J >= nT) continue;
+                acc += part[(size_t)(I * nT + J) * (2 * kCT - 1) + (delta + kCT - 1)];
+            }
+        }
+    }
+    out[d] = acc;
+}
+
+// ------------------------------------------------------------------ K7
+__device__ __forceinline__ double oe_value(const double* __restrict__ M, const double* __restrict__ dec,
+                                           long long N, long long i, long long j) {
+    const double m = M[i * N + j];
+    if (m == 0.0) return 0.0;
+    const long long d = i > j ? i - j : j - i;
+    return m / dec[d];
+}
+
+// partial column sums of O/E over row chunks: part[chunk][c]
+__global__ __launch_bounds__(256) void k_oe_colsum(const double* __restrict__ M, const double* __restrict__ dec,
+                                                   const long long* __restrict__ ng, long long N, long long n,
+                                                   int rows_per_chunk, double* __restrict__ part) {
+    const long long c = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (c >= n) return;
+    const long long j = ng[c];
+    const long long r0 = (long long)blockIdx.y * rows_per_chunk;
+    const long long r1 = std::min<long long>(N, r0 + rows_per_chunk);
+    double acc = 0.0;
+    for (long long i = r0; i < r1; ++i) acc += oe_value(M, dec, N, i, j);
+    part[(size_t)blockIdx.y * n + c] = acc;
+}
+
+__global__ void k_oe_mean(const double* __restrict__ part, long long n, int chunks, long long N,
+                          double* __restrict__ mu) {
+    const long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n) return;
+    double acc = 0.0;
+    for (int k = 0; k < chunks; ++k) acc += part[(size_t)k * n + c];
+    mu[c] = acc / (double)N;
+}
+
+// Zc[i][c] = OE(i, ng[c]) - mu[c]; rows >= N and columns >= n are zero padding.
+__global__ __launch_bounds__(256) void k_oe_center(const double* __restrict__ M, const double* __restrict__ dec,
+                                                   const long long* __restrict__ ng, const double* __restrict__ mu,
+                                                   long long N, long long n, long long Npad, long long ld,
+                                                   double* __restrict__ Z) {
+    const long long t = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (t >= Npad * ld) return;
+    const long long i = t / ld, c = t % ld;
+    double v = 0.0;
+    if (i < N && c < n) v = oe_value(M, dec, N, i, ng[c]) - mu[c];
+    Z[t] = v;
+}
+
+// Cov tile (bi, bj), bi <= bj, 64 x 64: 4 waves x (2 x 2) MFMA 16x16x4 f64 tiles.
+// LDS rows padded to 80 doubles so the 16-lane halves of a 32-lane LDS group
+// land on disjoint banks.
+constexpr int kLdS = 80;
+__global__ __launch_bounds__(256) void k_syrk(const double* __restrict__ Z, long long ld, long long Kpad,
+                                              long long nt, double scale, double* __restrict__ C, long long ldc) {
+    __shared__ __attribute__((aligned(16))) double As[16][kLdS];
+    __shared__ __attribute__((aligned(16))) double Bs[16][kLdS];
+    long long bi = 0, rem = blockIdx.x;
+    while (rem >= nt - bi) { rem -= nt - bi; ++bi; }
+    const long long bj = bi + rem;
+    const long long i0 = bi * 64, j0 = bj * 64;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int wr = (w >> 1) * 32, wc = (w & 1) * 32;
+    const bool diag = bi == bj;
+    d4 acc[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
+    const int lr = threadIdx.x / 16, lc = (threadIdx.x % 16) * 4;  // 16 rows x 64 cols, 4 doubles each
+    for (long long k0 = 0; k0 < Kpad; k0 += 16) {
+        const double* za = Z + (k0 + lr) * ld + i0 + lc;
+        const d4 va = *reinterpret_cast<const d4*>(za);
+        d4 vb = va;
+        if (!diag) vb = *reinterpret_cast<const d4*>(Z + (k0 + lr) * ld + j0 + lc);
+        __syncthreads();
+        *reinterpret_cast<d4*>(&As[lr][lc]) = va;
+        *reinterpret_cast<d4*>(&Bs[lr][lc]) = vb;
+        __syncthreads();
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const int kk = s * 4 + (lane >> 4);
+            double a[2], b[2];
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                a[t] = As[kk][wr + t * 16 + (lane & 15)];
+                b[t] = Bs[kk][wc + t * 16 + (lane & 15)];
+            }
+#pragma unroll
+            for (int ta = 0; ta < 2; ++ta)
+#pragma unroll
+                for (int tb = 0; tb < 2; ++tb)
+                    acc[ta][tb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ta], b[tb], acc[ta][tb], 0, 0, 0);
+        }
+    }
+    // C/D layout of v_mfma_f64_16x16x4_f64: col = lane & 15, row = (lane >> 4) + 4 * reg
+#pragma unroll
+    for (int ta = 0; ta < 2; ++ta)
+#pragma unroll
+        for (int tb = 0; tb < 2; ++tb)
+#pragma unroll
+            for (int reg = 0; reg < 4; ++reg) {
+                const long long gi = i0 + wr + ta * 16 + (lane >> 4) + 4 * reg;
+                const long long gj = j0 + wc + tb * 16 + (lane & 15);
+                const double v = acc[ta][tb][reg] * scale;
+                C[gi * ldc + gj] = v;
+                if (!diag) C[gj * ldc + gi] = v;
+            }
+}
+
+// numpy corrcoef: c /= sd[:, None]; c /= sd[None, :]; clip(-1, 1); then the
+// reference's NaN -> 0 (an inf cannot survive the clip).  Out of place.
+__global__ void k_corr_norm_oop(const double* __restrict__ Cov, long long n, long long ldc,
+                                double* __restrict__ Cor) {
+    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n * ldc) return;
+    const long long i = t / ldc, j = t % ldc;
+    double v = 0.0;
+    if (i < n && j < n) {
+        const double si = sqrt(Cov[i * ldc + i]), sj = sqrt(Cov[j * ldc + j]);
+        v = (Cov[i * ldc + j] / si) / sj;
+        if (v != v) v = 0.0;
+        else v = v < -1.0 ? -1.0 : (v > 1.0 ? 1.0 : v);
+    }
+    Cor[t] = v;
+}
+
+// ------------------------------------------------------------------ K8
+// out[i][0..B) = sum_j Cor[i][j] * V[j][0..B)   (V row-major n x B)
+// block: 16 rows; thread (row r = t/16, part q = t%16); columns in chunks of 256.
+__global__ __launch_bounds__(256) void k_cor_mul(const double* __restrict__ Cor, long long ldc, long long n,
+                                                 const double* __restrict__ V, double* __restrict__ out) {
+    __shared__ double Vs[256][kSB + 1];
+    const int r = threadIdx.x / 16, q = threadIdx.x % 16;
+    const long long i = (long long)blockIdx.x * 16 + r;
+    double acc[kSB];
+#pragma unroll
+    for (int b = 0; b < kSB; ++b) acc[b] = 0.0;
+    for (long long j0 = 0; j0 < n; j0 += 256) {
+        __syncthreads();
+        for (int e = threadIdx.x; e < 256 * kSB; e += 256) {
+            const int jj = e / kSB, b = e % kSB;
+            Vs[jj][b] = (j0 + jj < n) ? V[(j0 + jj) * kSB + b] : 0.0;
+        }
+        __syncthreads();
+        if (i < n) {
+#pragma unroll 4
+            for (int u = 0; u < 16; ++u) {
+                const int jj = q + 16 * u;
+                const long long j = j0 + jj;
+                const double c = j < n ? Cor[i * ldc + j] : 0.0;
+#pragma unroll
+                for (int b = 0; b < kSB; ++b) acc[b] = fma(c, Vs[jj][b], acc[b]);
+            }
+        }
+    }
+    // reduce over the 16 threads of the row (lanes 16r..16r+15 of a wave)
+#pragma unroll
+    for (int b = 0; b < kSB; ++b) {
+        double x = acc[b];
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+        acc[b] = x;
+    }
+    if (i < n && q == 0)
+#pragma unroll
+        for (int b = 0; b < kSB; ++b) out[i * kSB + b] = acc[b];
+}
+
+// Column means of Cor (over rows < n): mu[j] = sum_i Cor[i][j] / n (fixed order)
+__global__ void k_cor_colmean(const double* __restrict__ Cor, long long ldc, long long n, double* __restrict__ mu) {
+    const long long j = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    double acc = 0.0;
+    for (long long i = 0; i < n; ++i) acc += Cor[i * ldc + j];
+    mu[j] = acc / (double)n;
+}
+
+// Gram-type reduction: G[a][b] = sum_i X[i][a] * Y[i][b] (n x B each), block partials.
+__global__ __launch_bounds__(256) void k_gram_part(const double* __restrict__ X, const double* __restrict__ Y,
+                                                   long long n, int rows_per_block, double* __restrict__ part) {
+    // thread t = a * 16 + b
+    const int a = threadIdx.x / kSB, b = threadIdx.x % kSB;
+    const long long r0 = (long long)blockIdx.x * rows_per_block;
+    const long long r1 = std::min<long long>(n, r0 + rows_per_block);
+    double acc = 0.0;
+    for (long long i = r0; i < r1; ++i) acc = fma(X[i * kSB + a], Y[i * kSB + b], acc);
+    part[(size_t)blockIdx.x * kSB * kSB + threadIdx.x] = acc;
+}
+
+__global__ void k_gram_sum(const double* __restrict__ part, int nblk, double* __restrict__ G) {
+    const int t = threadIdx.x;
+    double acc = 0.0;
+    for (int k = 0; k < nblk; ++k) acc += part[(size_t)k * kSB * kSB + t];
+    G[t] = acc;
+}
+
+// Y = X * R (n x B times B x B) ; optionally out = X - 1 t^T or X - mu u^T
+__global__ void k_rot(const double* __restrict__ X, const double* __restrict__ R, long long n,
+                      double* __restrict__ Y) {
+    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n * kSB) return;
+    const long long i = t / kSB;
+    const int b = (int)(t % kSB);
+    double acc = 0.0;
+    for (int a = 0; a < kSB; ++a) acc = fma(X[i * kSB + a], R[a * kSB + b], acc);
+    Y[t] = acc;
+}
+
+// W -= x * y^T  (x: n-vector or nullptr = ones; y: B-vector)
+__global__ void k_rank1_sub(double* __restrict__ W, const double* __restrict__ x, const double* __restrict__ y,
+                            long long n) {
+    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n * kSB) return;
+    const long long i = t / kSB;
+    const int b = (int)(t % kSB);
+    W[t] -= (x ? x[i] : 1.0) * y[b];
+}
+
+// ------------------------------------------------------------------ select
+// Per PC k (<= 3): Cor sums {same, ab} with the means_minus masks and O/E
+// nonzero sums {aa, bb} for select_ab.  stats[blk][k][8].
+__global__ __launch_bounds__(256) void k_select_stats(const double* __restrict__ Cor, long long ldc, long long n,
+                                                      const double* __restrict__ M, long long N,
+                                                      const double* __restrict__ dec,
+                                                      const long long* __restrict__ ng,
+                                                      const int8_t* __restrict__ cls, int K, double eps,
+                                                      double* __restrict__ part) {
+    __shared__ double sh[16];
+    const long long i = blockIdx.x;  // one row of Cor / O/E[NG, NG]
+    double v[3][8];
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[k][q] = 0.0;
+    const long long gi = ng[i];
+    for (long long j = threadIdx.x; j < n; j += 256) {
+        const double c = Cor[i * ldc + j];
+        const double oe = oe_value(M, dec, N, gi, ng[j]);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            if (k >= K) break;
+            const int ci = cls[(size_t)k * n + i], cj = cls[(size_t)k * n + j];
+            if (ci != 0 && ci == cj) {
+                if (c > -1.0 && c < 1.0 - eps) { v[k][0] += c; v[k][1] += 1.0; }
+                if (oe != 0.0) {
+                    if (ci > 0) { v[k][4] += oe; v[k][5] += 1.0; }
+                    else { v[k][6] += oe; v[k][7] += 1.0; }
+                }
+            } else if (ci > 0 && cj < 0) {
+                if (c > -1.0 && c < 1.0) { v[k][2] += c; v[k][3] += 1.0; }
+            }
+        }
+    }
+    for (int k = 0; k < K; ++k)
+        for (int q = 0; q < 8; ++q) {
+            const double s = block_sum(v[k][q], sh);
+            if (threadIdx.x == 0) part[((size_t)i * 3 + k) * 8 + q] = s;
+        }
+}
+
+// ------------------------------------------------------------- host algebra
+// Cyclic Jacobi eigen-decomposition of a small symmetric matrix (row-major).
+static void jacobi_eig(int n, std::vector<double> A, std::vector<double>& evals, std::vector<double>& evecs) {
+    evecs.assign(n * n, 0.0);
+    for (int i = 0; i < n; ++i) evecs[i * n + i] = 1.0;
+    for (int sweep = 0; sweep < 100; ++sweep) {
+        double off = 0.0;
+        for (int p = 0; p < n; ++p)
+            for (int q = p + 1; q < n; ++q) off += A[p * n + q] * A[p * n + q];
+        if (off < 1e-300) break;
+        for (int p = 0; p < n; ++p)
+            for (int q = p + 1; q < n; ++q) {
+                const double apq = A[p * n + q];
+                if (std::fabs(apq) < 1e-300) continue;
+                const double app = A[p * n + p], aqq = A[q * n + q];
+                const double theta = (aqq - app) / (2.0 * apq);
+                const double t = (theta >= 0 ? 1.0 : -1.0) / (std::fabs(theta) + std::sqrt(theta * theta + 1.0));
+                const double c = 1.0 / std::sqrt(t * t + 1.0), s = t * c;
+                for (int k = 0; k < n; ++k) {
+                    const double akp = A[k * n + p], akq = A[k * n + q];
+                    A[k * n + p] = c * akp - s * akq;
+                    A[k * n + q] = s * akp + c * akq;
+                }
+                for (int k = 0; k < n; ++k) {
+                    const double apk = A[p * n + k], aqk = A[q * n + k];
+                    A[p * n + k] = c * apk - s * aqk;
+                    A[q * n + k] = s * apk + c * aqk;
+                }
+                for (int k = 0; k < n; ++k) {
+                    const double vkp = evecs[k * n + p], vkq = evecs[k * n + q];
+                    evecs[k * n + p] = c * vkp - s * vkq;
+                    evecs[k * n + q] = s * vkp + c * vkq;
+                }
+            }
+    }
+    evals.resize(n);
+    for (int i = 0; i < n; ++i) evals[i] = A[i * n + i];
+}
+
+// R^{-1} of the Cholesky factor of a small SPD matrix (G = R^T R), upper R.
+static bool chol_inv_upper(int n, const std::vector<double>& G, std::vector<double>& Rinv) {
+    std::vector<double> R(n * n, 0.0);
+    for (int j = 0; j < n; ++j) {
+        double d = G[j * n + j];
+        for (int k = 0; k < j; ++k) d -= R[k * n + j] * R[k * n + j];
+        if (!(d > 0)) return false;
+        R[j * n + j] = std::sqrt(d);
+        for (int i = j + 1; i < n; ++i) {
+            double s = G[j * n + i];
+            for (int k = 0; k < j; ++k) s -= R[k * n + j] * R[k * n + i];
+            R[j * n + i] = s / R[j * n + j];
+        }
+    }
+    Rinv.assign(n * n, 0.0);
+    for (int j = 0; j < n; ++j) {
+        Rinv[j * n + j] = 1.0 / R[j * n + j];
+        for (int i = j - 1; i >= 0; --i) {
+            double s = 0.0;
+            for (int k = i + 1; k <= j; ++k) s += R[i * n + k] * Rinv[k * n + j];
+            Rinv[i * n + j] = -s / R[i * n + i];
+        }
+    }
+    return true;
+}
+
+}  // namespace hh
+
+using namespace hh;
+
+struct hh_comp {
+    int device = 0;
+    long long N = 0;
+    DBuf<double> M;              // N x N (owned unless on_device)
+    const double* Mp = nullptr;
+    DBuf<double> dec;            // N
+    DBuf<long long> ng;          // n
+    long long n = 0, ld = 0;     // Cor leading dimension (n padded to 64)
+    DBuf<double> cor;            // ld x ld
+    int iters = 0;
+};
+
+namespace hh {
+
+static void gram(const double* X, const double* Y, long long n, std::vector<double>& G, hipStream_t s) {
+    const int rpb = 512;
+    const int nblk = (int)std::max<long long>(1, (n + rpb - 1) / rpb);
+    DBuf<double> part((size_t)nblk * kSB * kSB), dG(kSB * kSB);
+    hipLaunchKernelGGL(k_gram_part, dim3(nblk), dim3(256), 0, s, X, Y, n, rpb, part.p);
+    hipLaunchKernelGGL(k_gram_sum, dim3(1), dim3(kSB * kSB), 0, s, part.p, nblk, dG.p);
+    G.resize(kSB * kSB);
+    dG.download(G.data(), G.size(), s);
+    HIP_CHECK(hipStreamSynchronize(s));
+}
+
+// V <- V R^{-1} twice (CholQR2); returns false if V lost rank.
+static bool orthonormalize(DBuf<double>& V, DBuf<double>& tmp, long long n, hipStream_t s) {
+    for (int pass = 0; pass < 2; ++pass) {
+        std::vector<double> G, Rinv;
+        gram(V.p, V.p, n, G, s);
+        if (!chol_inv_upper(kSB, G, Rinv)) return false;
+        DBuf<double> dR = to_device(Rinv, s);
+        hipLaunchKernelGGL(k_rot, dim3((unsigned)((n * kSB + 255) / 256)), dim3(256), 0, s, V.p, dR.p, n, tmp.p);
+        HIP_CHECK(hipMemcpyAsync(V.p, tmp.p, n * kSB * sizeof(double), hipMemcpyDeviceToDevice, s));
+        HIP_CHECK(hipStreamSynchronize(s));
+    }
+    return true;
+}
+
+}  // namespace hh
+
+extern "C" {
+
+int hh_comp_create(const double* M, int64_t N, int32_t on_device, void* stream, hh_comp** out) {
+    return guard([&] {
+        HH_REQUIRE(M && N > 0 && out, "bad arguments");
+        auto c = std::make_unique<hh_comp>();
+        HIP_CHECK(hipGetDevice(&c->device));
+        c->N = N;
+        if (on_device) {
+            c->Mp = M;
+        } else {
+            c->M.alloc((size_t)N * N);
+            c->M.upload(M, (size_t)N * N, as_stream(stream));
+            c->Mp = c->M.p;
+        }
+        HIP_CHECK(hipStreamSynchronize(as_stream(stream)));
+        *out = c.release();
+    });
+}
+
+int hh_comp_free(hh_comp* c) {
+    return guard([&] { delete c; });
+}
+
+int hh_comp_colnnz(hh_comp* c, int64_t* nnz_col, void* stream) {
+    return guard([&] {
+        HH_REQUIRE(c && nnz_col, "null");
+        hipStream_t s = as_stream(stream);
+        const long long N = c->N;
+        DBuf<unsigned long long> d(N);
+        d.zero(s);
+        const int rpb = 256;
+        hipLaunchKernelGGL(k_colnnz, dim3((unsigned)((N + 255) / 256), (unsigned)((N + rpb - 1) / rpb)), dim3(256),
+                           0, s, c->Mp, N, rpb, d.p);
+        HIP_CHECK(hipGetLastError());
+        d.download(reinterpret_cast<unsigned long long*>(nnz_col), N, s);
+        HIP_CHECK(hipStreamSynchronize(s));
+    });
+}
+
+int hh_comp_diag_sums(hh_comp* c, const uint8_t* gapcol, double* sums, void* stream) {
+    return guard([&] {
+        HH_REQUIRE(c && gapcol && sums, "null");
+        hipStream_t s = as_stream(stream);
+        const long long N = c->N, nT = (N + kCT - 1) / kCT;
+        DBuf<uint8_t> g(N);
+        g.upload(gapcol, N, s);
+        DBuf<double> part((size_t)nT * nT * (2 * kCT - 1)), out(N);
+        hipLaunchKernelGGL(k_diag_part, dim3((unsigned)(nT * nT)), dim3(256), 0, s, c->Mp, N, nT, g.p, part.p);
+        hipLaunchKernelGGL(k_diag_reduce, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, part.p, N, nT, out.p);
+        HIP_CHECK(hipGetLastError());
+        out.download(sums, N, s);
+        HIP_CHECK(hipStreamSynchronize(s));
+    });
+}
+
+int hh_comp_correlation(hh_comp* c, const double* decline, const int64_t* ng, int64_t n, void* stream) {
+    return guard([&] {
+        HH_REQUIRE(c && decline && ng && n > 0 && n <= c->N, "bad arguments");
+        hipStream_t s = as_stream(stream);
+        const long long N = c->N;
+        c->n = n;
+        c->ld = (n + 63) / 64 * 64;
+        c->dec.alloc(N);
+        c->dec.upload(decline, N, s);
+        c->ng.alloc(n);
+        c->ng.upload(reinterpret_cast<const long long*>(ng), n, s);
+        // column means of O/E
+        const int rpc = 256;
+        const int chunks = (int)((N + rpc - 1) / rpc);
+        DBuf<double> part((size_t)chunks * n), mu(n);
+        hipLaunchKernelGGL(k_oe_colsum, dim3((unsigned)((n + 255) / 256), (unsigned)chunks), dim3(256), 0, s, c->Mp,
+                           c->dec.p, c->ng.p, N, (long long)n, rpc, part.p);
+        hipLaunchKernelGGL(k_oe_mean, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, part.p, (long long)n, chunks,
+                           N, mu.p);
+        // centred O/E, padded
+        const long long Npad = (N + 15) / 16 * 16;
+        DBuf<double> Z((size_t)Npad * c->ld);
+        hipLaunchKernelGGL(k_oe_center, dim3((unsigned)((Npad * c->ld + 255) / 256)), dim3(256), 0, s, c->Mp, c->dec.p,
+                           c->ng.p, mu.p, N, (long long)n, Npad, c->ld, Z.p);
+        // Cov = Z^T Z * (1 / (N - 1))  (np.cov: c *= true_divide(1, fact))
+        DBuf<double> cov((size_t)c->ld * c->ld);
+        const long long nt = c->ld / 64;
+        hipLaunchKernelGGL(k_syrk, dim3((unsigned)(nt * (nt + 1) / 2)), dim3(256), 0, s, Z.p, c->ld, Npad, nt,
+                           1.0 / (double)(N - 1), cov.p, c->ld);
+        Z.release();
+        c->cor.alloc((size_t)c->ld * c->ld);
+        hipLaunchKernelGGL(k_corr_norm_oop, dim3((unsigned)((c->ld * c->ld + 255) / 256)), dim3(256), 0, s, cov.p,
+                           (long long)n, c->ld, c->cor.p);
+        HIP_CHECK(hipGetLastError());
+        HIP_CHECK(hipStreamSynchronize(s));
+    });
+}
+
+int hh_comp_set_cor(hh_comp* c, const double* cor, void* stream) {
+    return guard([&] {
+        HH_REQUIRE(c && cor && c->cor.p, "call hh_comp_correlation first (sets n)");
+        hipStream_t s = as_stream(stream);
+        HIP_CHECK(hipMemcpy2DAsync(c->cor.p, c->ld * sizeof(double), cor, c->n * sizeof(double),
+                                   c->n * sizeof(double), c->n, hipMemcpyHostToDevice, s));
+        HIP_CHECK(hipStreamSynchronize(s));
+    });
+}
+
+int hh_comp_get_cor(hh_comp* c, double* cor, void* stream) {
+    return guard([&] {
+        HH_REQUIRE(c && cor && c->cor.p, "no correlation computed");
+        hipStream_t s = as_stream(stream);
+        HIP_CHECK(hipMemcpy2DAsync(cor, c->n * sizeof(double), c->cor.p, c->ld * sizeof(double),
+                                   c->n * sizeof(double), c->n, hipMemcpyDeviceToHost, s));
+        HIP_CHECK(hipStreamSynchronize(s));
+    });
+}
+
+int hh_comp_pca(hh_comp* c, int32_t k, double tol, int32_t max_iters, double* components, double* eigvals,
+                int32_t* iters_out, void* stream) {
+    return guard([&] {
+        HH_REQUIRE(c && components && c->cor.p && k >= 1 && k <= 8, "bad arguments");
+        hipStream_t s = as_stream(stream);
+        const long long n = c->n;
+        HH_REQUIRE(n >= kSB, "matrix smaller than the subspace block (16)");
+        DBuf<double> mu(n);
+        hipLaunchKernelGGL(k_cor_colmean, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, c->cor.p, c->ld, n, mu.p);
+        // deterministic start block
+        std::vector<double> v0((size_t)n * kSB);
+        for (long long i = 0; i < n; ++i)
+            for (int b = 0; b < kSB; ++b) v0[i * kSB + b] = (double)u01(mix64(0x5eedULL + i * kSB + b)) - 0.5;
+        DBuf<double> V = to_device(v0, s), W((size_t)n * kSB), W1((size_t)n * kSB), tmp((size_t)n * kSB);
+        HH_REQUIRE(orthonormalize(V, tmp, n, s), "start block rank deficient");
+        const unsigned gm = (unsigned)((n + 15) / 16), ge = (unsigned)((n * kSB + 255) / 256);
+        // mu and 1 as the first column of n x B blocks, so mu^T X and 1^T X are
+        // row 0 of a Gram product.
+        DBuf<double> mupad, onepad;
+        {
+            std::vector<double> muh(n), mp((size_t)n * kSB, 0.0), op((size_t)n * kSB, 0.0);
+            mu.download(muh.data(), n, s);
+            HIP_CHECK(hipStreamSynchronize(s));
+            for (long long i = 0; i < n; ++i) { mp[i * kSB] = muh[i]; op[i * kSB] = 1.0; }
+            mupad = to_device(mp, s);
+            onepad = to_device(op, s);
+        }
+        std::vector<double> prev((size_t)n * k, 0.0), cur((size_t)n * k);
+        std::vector<double> evals, evecs, G, Vh((size_t)n * kSB);
+        int it = 0;
+        bool done = false;
+        for (it = 1; it <= max_iters && !done; ++it) {
+            // A V = Xc^T (Xc V) with Xc = Cor - 1 mu^T (Cor symmetric):
+            // W1 = Cor V - 1 (mu^T V);  W = Cor W1 - mu (1^T W1)
+            hipLaunchKernelGGL(k_cor_mul, dim3(gm), dim3(256), 0, s, c->cor.p, c->ld, n, V.p, W1.p);
+            gram(mupad.p, V.p, n, G, s);
+            {
+                std::vector<double> t(G.begin(), G.begin() + kSB);
+                DBuf<double> dt = to_device(t, s);
+                hipLaunchKernelGGL(k_rank1_sub, dim3(ge), dim3(256), 0, s, W1.p, (const double*)nullptr, dt.p, n);
+                hipLaunchKernelGGL(k_cor_mul, dim3(gm), dim3(256), 0, s, c->cor.p, c->ld, n, W1.p, W.p);
+                gram(onepad.p, W1.p, n, G, s);
+                std::vector<double> u(G.begin(), G.begin() + kSB);
+                DBuf<double> du = to_device(u, s);
+                hipLaunchKernelGGL(k_rank1_sub, dim3(ge), dim3(256), 0, s, W.p, mu.p, du.p, n);
+                HIP_CHECK(hipStreamSynchronize(s));
+            }
+            // Rayleigh-Ritz: H = V^T W (V orthonormal), eig -> Y (descending)
+            gram(V.p, W.p, n, G, s);
+            std::vector<double> H(kSB * kSB);
+            for (int a = 0; a < kSB; ++a)
+                for (int b = 0; b < kSB; ++b) H[a * kSB + b] = 0.5 * (G[a * kSB + b] + G[b * kSB + a]);
+            jacobi_eig(kSB, H, evals, evecs);
+            std::vector<int> ord(kSB);
+            std::iota(ord.begin(), ord.end(), 0);
+            std::sort(ord.begin(), ord.end(), [&](int x, int y) { return evals[x] > evals[y]; });
+            std::vector<double> Y(kSB * kSB);
+            for (int a = 0; a < kSB; ++a)
+                for (int b = 0; b < kSB; ++b) Y[a * kSB + b] = evecs[a * kSB + ord[b]];
+            DBuf<double> dY = to_device(Y, s);
+            // Ritz vectors of this iteration: V Y
+            hipLaunchKernelGGL(k_rot, dim3(ge), dim3(256), 0, s, V.p, dY.p, n, tmp.p);
+            tmp.download(Vh.data(), Vh.size(), s);
+            HIP_CHECK(hipStreamSynchronize(s));
+            // convergence: largest entry change of the (unit, sign-aligned)
+            // top-k Ritz vectors between two iterations
+            double worst = 0.0;
+            for (int q = 0; q < k; ++q) {
+                double dot = 0.0, nn = 0.0;
+                for (long long i = 0; i < n; ++i) {
+                    cur[q * n + i] = Vh[i * kSB + q];
+                    dot += cur[q * n + i] * prev[q * n + i];
+                    nn += cur[q * n + i] * cur[q * n + i];
+                }
+                const double sg = dot < 0 ? -1.0 : 1.0, inv = 1.0 / std::sqrt(nn);
+                for (long long i = 0; i < n; ++i) {
+                    cur[q * n + i] *= inv;
+                    worst = std::max(worst, std::fabs(cur[q * n + i] - sg * prev[q * n + i]));
+                }
+            }
+            if (eigvals)
+                for (int q = 0; q < k; ++q) eigvals[q] = evals[ord[q]];
+            if (it > 1 && worst < tol) done = true;
+            prev = cur;
+            if (!done) {
+                // next block: orth(W Y)
+                hipLaunchKernelGGL(k_rot, dim3(ge), dim3(256), 0, s, W.p, dY.p, n, V.p);
+                HH_REQUIRE(orthonormalize(V, tmp, n, s), "subspace lost rank");
+            }
+        }
+        c->iters = it - 1;
+        if (iters_out) *iters_out = c->iters;
+        // unit norm + sklearn svd_flip(u_based_decision=False): max-|.| entry positive
+        for (int q = 0; q < k; ++q) {
+            double nn = 0.0;
+            long long am = 0;
+            for (long long i = 0; i < n; ++i) {
+                nn += cur[q * n + i] * cur[q * n + i];
+                if (std::fabs(cur[q * n + i]) > std::fabs(cur[q * n + am])) am = i;
+            }
+            const double sc = (cur[q * n + am] < 0 ? -1.0 : 1.0) / std::sqrt(nn);
+            for (long long i = 0; i < n; ++i) components[q * n + i] = cur[q * n + i] * sc;
+        }
+    });
+}
+
+int hh_comp_select_stats(hh_comp* c, const double* pcs, int32_t k, double eps, double* stats, void* stream) {
+    return guard([&] {
+        HH_REQUIRE(c && pcs && stats && c->cor.p && k >= 1 && k <= 3, "bad arguments");
+        hipStream_t s = as_stream(stream);
+        const long long n = c->n;
+        std::vector<int8_t> cls((size_t)k * n);
+        for (long long q = 0; q < (long long)k * n; ++q) cls[q] = pcs[q] > 0 ? 1 : (pcs[q] < 0 ? -1 : 0);
+        DBuf<int8_t> dcls = to_device(cls, s);
+        DBuf<double> part((size_t)n * 3 * 8);
+        hipLaunchKernelGGL(k_select_stats, dim3((unsigned)n), dim3(256), 0, s, c->cor.p, c->ld, n, c->Mp, c->N,
+                           c->dec.p, c->ng.p, dcls.p, (int)k, eps, part.p);
+        HIP_CHECK(hipGetLastError());
+        std::vector<double> h((size_t)n * 3 * 8);
+        part.download(h.data(), h.size(), s);
+        HIP_CHECK(hipStreamSynchronize(s));
+        for (int q = 0; q < k * 8; ++q) stats[q] = 0.0;
+        for (long long i = 0; i < n; ++i)
+            for (int q = 0; q < k; ++q)
+                for (int t = 0; t < 8; ++t) stats[q * 8 + t] += h[(i * 3 + q) * 8 + t];
+    });
+}
+
+}  // extern "C"
+
+// ================================================================== DI (K9)
+// StructureFind.Get_Gap (:721-751) and Get_DI (:804-839), one thread per
+// column (the windows are 2 x 15..60 bins; the matrix slice is tiny).
+namespace hh {
+__global__ void k_gap_scan(const double* __restrict__ M, long long N, int lb, uint8_t* __restrict__ gap) {
+    const long long j = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= N) return;
+    bool g = true;  // edges are gaps
+    if (lb <= j && j <= N - 1 - lb) {
+        int nz = 0;
+        for (long long r = j - lb; r < j + lb; ++r) nz += M[r * N + j] != 0.0;
+        g = (double)nz < 2.0 * lb * 0.8;
+    }
+    gap[j] = g ? 1 : 0;
+}
+
+__global__ void k_di(const double* __restrict__ M, long long N, const uint8_t* __restrict__ gap,
+                     const int* __restrict__ win, int test, double* __restrict__ di) {
+    const long long j = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= N) return;
+    const int w = win[j];
+    double v = 0.0;
+    if (!gap[j] && !(j < w || j > N - w - 1) && w >= 1) {
+        double su = 0.0, sd = 0.0;
+        for (int k = 1; k <= w; ++k) { su += M[(j - k) * N + j]; sd += M[(j + k) * N + j]; }
+        if (test == 0) {
+            const double um = su / w, dm = sd / w;
+            const double den = (double)w * (double)(w - 1);
+            double qu = 0.0, qd = 0.0;
+            for (int k = 1; k <= w; ++k) {
+                const double a = M[(j - k) * N + j] - um, b = M[(j + k) * N + j] - dm;
+                qu += a * a / den;
+                qd += b * b / den;
+            }
+            const double dsum = sqrt(qu + qd);
+            if (dsum != 0.0) v = (dm - um) / dsum;
+        } else {
+            const double e = (su + sd) / 2.0;
+            if (su != sd && e != 0.0)
+                v = (sd - su) / fabs(sd - su) * ((su - e) * (su - e) / e + (sd - e) * (sd - e) / e);
+        }
+    }
+    di[j] = v;
+}
+}  // namespace hh
+
+namespace {
+const double* stage_dense(const double* M, int64_t N, int32_t on_device, hh::DBuf<double>& buf, hipStream_t s) {
+    if (on_device) return M;
+    buf.alloc((size_t)N * N);
+    buf.upload(M, (size_t)N * N, s);
+    return buf.p;
+}
+}  // namespace
+
+extern "C" int hh_gap_scan(const double* M, int64_t N, int32_t lb, uint8_t* gap, int32_t on_device, void* stream) {
+    return guard([&] {
+        HH_REQUIRE(M && gap && N > 0 && lb >= 0, "bad arguments");
+        hipStream_t s = as_stream(stream);
+        DBuf<double> dM;
+        const double* pm = stage_dense(M, N, on_device, dM, s);
+        DBuf<uint8_t> dg(N);
+        hipLaunchKernelGGL(k_gap_scan, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, pm, (long long)N, lb, dg.p);
+        HIP_CHECK(hipGetLastError());
+        dg.download(gap, N, s);
+        HIP_CHECK(hipStreamSynchronize(s));
+    });
+}
+
+extern "C" int hh_di_scan(const double* M, int64_t N, const uint8_t* gap, const int32_t* window_bins, int32_t test,
+                          double* di, int32_t on_device, void* stream) {
+    return guard([&] {
+        HH_REQUIRE(M && window_bins && gap && di && N > 0, "bad arguments");
+        HH_REQUIRE(test == 0 || test == 1, "test must be 0 (ttest) or 1 (chitest)");
+        hipStream_t s = as_stream(stream);
+        DBuf<double> dM;
+        const double* pm = stage_dense(M, N, on_device, dM, s);
+        DBuf<int> dw(N);
+        dw.upload(window_bins, N, s);
+        DBuf<uint8_t> dg(N);
+        dg.upload(gap, N, s);
+        DBuf<double> dd(N);
+        hipLaunchKernelGGL(k_di, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, pm, (long long)N, dg.p, dw.p,
+                           test, dd.p);
+        HIP_CHECK(hipGetLastError());
+        dd.download(di, N, s);
+        HIP_CHECK(hipStreamSynchronize(s));
+    });
+}

@@ -1,0 +1,172 @@
+"""HiCHap's diploid bias correction on MI355X — same entry points as
+``HiCHap/matrixBuilding.py``.
+
+* ``TwoStepCorrection(TM, MM, PM)``            matrixBuilding.py:984-1023
+* ``IntraChromMatrixCorrection(Tra, Hap)``     matrixBuilding.py:1026-1041
+* ``GenomeWideMatrixCorrection(Bins_Pos, Hap_Bins_Pos, T_M, H_M)``  :857-901
+* ``Sort_Chromosomes(chro_lst)``               :388-406
+
+Every O(N^2) step runs in HIP kernels (``hh_dense_rowstats``: row sums and
+zero counts; ``hh_dense_symvc``: gap-aware symmetrisation + VC^(2/3) + mean
+rescale, fused).  What stays on the host is O(N) glue on per-row vectors,
+written with the same NumPy calls as the reference so the gap and alpha
+decisions are bit-identical (``np.percentile`` linear interpolation, the
+``max``/``==0`` fix-ups, true division of exact integer row sums).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from ._lib import call, ptr
+
+VC_EXPONENT = 2 / 3  # Correct_VC(X, 2/3) under `from __future__ import division` (:8, :1014)
+
+
+# ------------------------------------------------------------------ kernels
+def _as_dense(X):
+    X = np.asarray(X)
+    if X.ndim != 2 or X.shape[0] != X.shape[1]:
+        raise ValueError("expected a square matrix")
+    if np.issubdtype(X.dtype, np.integer) or X.dtype == np.bool_:
+        return np.ascontiguousarray(X, dtype=np.int64), 0
+    return np.ascontiguousarray(X, dtype=np.float64), 1
+
+
+def row_stats(X, lo=None, hi=None, stream=None):
+    """Per-row (sum, zero count) over columns [lo_i, hi_i) on the GPU."""
+    _lib.require_gpu()
+    A, dt = _as_dense(X)
+    N = A.shape[0]
+    s = np.empty(N, np.float64)
+    z = np.empty(N, np.int64)
+    l = None if lo is None else np.ascontiguousarray(lo, dtype=np.int64)
+    h = None if hi is None else np.ascontiguousarray(hi, dtype=np.int64)
+    call("hh_dense_rowstats", ptr(A), dt, N, ptr(l), ptr(h), ptr(s), ptr(z), 0, stream)
+    return s, z
+
+
+def sym_vc_rescale(X, alpha, gap_idx, raw_sum, exponent=VC_EXPONENT, stream=None):
+    """(mean(X)/mean(C)) * C, C = Correct_VC(Trans2symmetry(X/alpha[:,None], gap), exponent).
+    ``gap_idx`` None -> the sum form (no gap / Trans2symmetryLowRes)."""
+    _lib.require_gpu()
+    A, dt = _as_dense(X)
+    N = A.shape[0]
+    a = np.ascontiguousarray(alpha, dtype=np.float64)
+    g = None
+    if gap_idx is not None:
+        g = np.zeros(N, np.uint8)
+        g[np.asarray(gap_idx, dtype=np.int64)] = 1
+    out = np.empty((N, N), np.float64)
+    call("hh_dense_symvc", ptr(A), dt, N, ptr(a), ptr(g), float(exponent), float(raw_sum), ptr(out), 0, stream)
+    return out
+
+
+# --------------------------------------------------------------- host glue
+def _coverage(zeros, n):
+    """Coverage_M (:904-912): 1 - zeros / float(len(row))."""
+    return 1 - (np.asarray(zeros) / float(n))
+
+
+def _gap_from_coverage(cov):
+    """Gap_defined (:915-929) given the coverage vector."""
+    threshold = np.percentile(cov[np.nonzero(cov)], 25)
+    if threshold > 0.2:
+        threshold = 0.2
+    return np.nonzero(cov < threshold)[0].astype(np.int64)
+
+
+def _non_gap(N, gap):
+    """Non_Gap_Defined (:932-942)."""
+    keep = np.ones(N, dtype=bool)
+    keep[np.asarray(gap, dtype=np.int64)] = False
+    return np.nonzero(keep)[0]
+
+
+def _snp_alpha(m_sum, p_sum, t_sum, non_gap):
+    """SNP-density factor (:994-1005 / :878-886) on exact integer row sums."""
+    alpha = (m_sum + p_sum) / (t_sum + 1)
+    alpha /= np.max(alpha[non_gap])
+    alpha[alpha == 0] = 1
+    threshold = np.percentile(alpha[non_gap], 20)
+    alpha[alpha < threshold] = threshold
+    return alpha
+
+
+# ------------------------------------------------------------------- API
+def TwoStepCorrection(TM, MM, PM):
+    """Two-step correction of one chromosome's maternal / paternal matrices
+    (matrixBuilding.py:984-1023).  Returns (Nor_MM, Nor_PM, Gap_M, Gap_P)."""
+    N = np.asarray(TM).shape[0]
+    t_sum, _ = row_stats(TM)
+    m_sum, m_zero = row_stats(MM)
+    p_sum, p_zero = row_stats(PM)
+    Gap_M = _gap_from_coverage(_coverage(m_zero, N))
+    Gap_P = _gap_from_coverage(_coverage(p_zero, N))
+    non_gap = np.union1d(_non_gap(N, Gap_M), _non_gap(N, Gap_P))
+    alpha = _snp_alpha(m_sum, p_sum, t_sum, non_gap)
+    Nor_MM = sym_vc_rescale(MM, alpha, Gap_M if Gap_M.size else None, m_sum.sum())
+    Nor_PM = sym_vc_rescale(PM, alpha, Gap_P if Gap_P.size else None, p_sum.sum())
+    return Nor_MM, Nor_PM, Gap_M, Gap_P
+
+
+def IntraChromMatrixCorrection(Tra_Lib, Hap_Lib):
+    """Per-chromosome TwoStepCorrection (matrixBuilding.py:1026-1041)."""
+    Nor_Lib, Gap_Lib = {}, {}
+    for chro in Tra_Lib.keys():
+        Nor_MM, Nor_PM, Gap_M, Gap_P = TwoStepCorrection(Tra_Lib[chro], Hap_Lib["M" + chro], Hap_Lib["P" + chro])
+        Nor_Lib["M" + chro] = Nor_MM
+        Nor_Lib["P" + chro] = Nor_PM
+        Gap_Lib["M" + chro] = Gap_M
+        Gap_Lib["P" + chro] = Gap_P
+    return Nor_Lib, Gap_Lib
+
+
+def Sort_Chromosomes(chro_lst):
+    """Numeric labels ascending, then the rest sorted; leading 'c','h','r'
+    characters stripped as the reference's ``lstrip('chr')`` does (:388-406)."""
+    names = [i.lstrip("chr") for i in chro_lst]
+    num, txt = [], []
+    for i in names:
+        try:
+            num.append(int(i))
+        except ValueError:
+            txt.append(i)
+    return [str(j) for j in sorted(num)] + sorted(txt)
+
+
+def GenomeWideMatrixCorrection(Bins_Pos, Hap_Bins_Pos, T_M, H_M):
+    """Whole-genome diploid correction (matrixBuilding.py:857-901).
+
+    ``Bins_Pos[c] = (start, end)`` inclusive bin ranges of T_M;
+    ``Hap_Bins_Pos['M'+c]`` / ``['P'+c]`` the same in H_M (2n x 2n)."""
+    T_M = np.asarray(T_M)
+    H_M = np.asarray(H_M)
+    n, n2 = T_M.shape[0], H_M.shape[0]
+    t_lo, t_hi = np.zeros(n, np.int64), np.full(n, n, np.int64)
+    h_lo, h_hi = np.zeros(n2, np.int64), np.full(n2, n2, np.int64)
+    for c, (s, e) in Bins_Pos.items():
+        t_lo[s:e + 1], t_hi[s:e + 1] = s, e + 1
+        for h in ("M", "P"):
+            hs, he = Hap_Bins_Pos[h + c]
+            h_lo[hs:he + 1], h_hi[hs:he + 1] = hs, he + 1
+    t_sum, t_zero = row_stats(T_M, t_lo, t_hi)       # block-restricted (Tra_M = T_M[s:e+1, s:e+1])
+    h_sum, _ = row_stats(H_M, h_lo, h_hi)            # M_M / P_P diagonal blocks
+    h_full, _ = row_stats(H_M)                       # H_M.mean()
+    Beta = {}
+    for chro in Bins_Pos.keys():
+        s, e = Bins_Pos[chro]
+        ms, me = Hap_Bins_Pos["M" + chro]
+        ps, pe = Hap_Bins_Pos["P" + chro]
+        L = e - s + 1
+        cov = _coverage(t_zero[s:e + 1], L)
+        gap = np.nonzero(cov < 0.1)[0]              # Gap_definedLowRes (:742-753)
+        non_gap = _non_gap(L, gap)
+        Beta[chro] = _snp_alpha(h_sum[ms:me + 1], h_sum[ps:pe + 1], t_sum[s:e + 1], non_gap)
+    Alpha = []
+    for i in Sort_Chromosomes(list(Beta.keys())):
+        Alpha.extend(Beta[i])
+    Alpha += Alpha
+    return sym_vc_rescale(H_M, np.array(Alpha), None, h_full.sum())

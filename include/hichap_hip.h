@@ -176,6 +176,59 @@ int hh_ice_finalize(hh_ice* s, double* weights, double* scale, double* var, int3
 int hh_ice_last_sweep_timing(const hh_ice* s, double* sweep_ms_total, int32_t* sweep_launches,
                              double* iter_ms_total);
 
+/* ------------------------------------------ dense two-step correction
+ * Dense row-major N x N matrices; dtype 0 = int64, 1 = float64.  Host
+ * pointers (copied in/out) or, with on_device = 1, device pointers. */
+/* Per row i over columns [lo[i], hi[i]) (lo = hi = NULL: whole rows): sum
+ * (exact for int64) and number of zero entries.  Replaces the row loops of
+ * Coverage_M / Gap_defined / Gap_definedLowRes and the alpha row sums,
+ * matrixBuilding.py:742-753, :878-881, :904-929, :994-995. */
+int hh_dense_rowstats(const void* X, int32_t dtype, int64_t N, const int64_t* lo, const int64_t* hi,
+                      double* rowsum, int64_t* zeros, int32_t on_device, void* stream);
+/* out = (raw_sum / N^2) / mean(C) * C with C = Correct_VC(Y, exponent),
+ * Y = Trans2symmetry(X / alpha[:, None], gap) (gap = NULL: the sum form,
+ * Trans2symmetryLowRes).  raw_sum = sum(X) (MM.mean() * N^2).
+ * TwoStepCorrection :1007-1021, GenomeWideMatrixCorrection :894-899. */
+int hh_dense_symvc(const void* X, int32_t dtype, int64_t N, const double* alpha, const uint8_t* gap,
+                   double exponent, double raw_sum, double* out, int32_t on_device, void* stream);
+
+/* ---------------------------------------------------- compartment (one chrom)
+ * StructureFind.Distance_Decay / Get_PCA / Select_PC_new, StructureFind.py:201-423.
+ * M: dense N x N float64 raw contacts (cooler matrix(balance=False).fetch). */
+typedef struct hh_comp hh_comp;
+int hh_comp_create(const double* M, int64_t N, int32_t on_device, void* stream, hh_comp** out);
+int hh_comp_free(hh_comp* c);
+/* nnz_col[j] = number of nonzero entries of column j (gap columns, :216-220). */
+int hh_comp_colnnz(hh_comp* c, int64_t* nnz_col, void* stream);
+/* sums[d] = sum of nonzero M[i][j] with |i-j| = d whose column j is not a gap
+ * (gapcol[j] = 1) — the bincount of Distance_Decay before the bin_num division. */
+int hh_comp_diag_sums(hh_comp* c, const uint8_t* gapcol, double* sums, void* stream);
+/* O/E = M / decline[|i-j|] on nonzeros, columns ng[0..n); Pearson correlation
+ * of those columns (np.corrcoef(rowvar=False), NaN -> 0) kept on the device. */
+int hh_comp_correlation(hh_comp* c, const double* decline, const int64_t* ng, int64_t n, void* stream);
+int hh_comp_get_cor(hh_comp* c, double* cor, void* stream);
+/* Replace the device correlation (n x n from the last hh_comp_correlation). */
+int hh_comp_set_cor(hh_comp* c, const double* cor, void* stream);
+/* Top-k right singular vectors of the column-centred correlation (sklearn
+ * PCA(k).fit(Cor).components_, sign: max-|.| entry positive), k x n row-major,
+ * by block subspace iteration until 1 - |cos| < tol for each vector. */
+int hh_comp_pca(hh_comp* c, int32_t k, double tol, int32_t max_iters, double* components, double* eigvals,
+                int32_t* iters, void* stream);
+/* Per PC q < k (<= 3), 8 sums: [0,1] Cor same-sign pairs in (-1, 1-eps) sum,count;
+ * [2,3] Cor (pc_i > 0, pc_j < 0) pairs in (-1, 1) sum,count; [4,5] nonzero O/E
+ * over (+,+) sum,count; [6,7] over (-,-) — Select_PC_new's means_minus / select_ab. */
+int hh_comp_select_stats(hh_comp* c, const double* pcs, int32_t k, double eps, double* stats, void* stream);
+
+/* ------------------------------------------------------- TAD scan (DI)
+ * M dense N x N float64 (balanced, NaN -> 0, for traditional data).
+ * hh_gap_scan = StructureFind.Get_Gap (:721-751): gap[j] = 1 when column j
+ * has fewer than 2*lb*0.8 nonzeros in M[j-lb:j+lb, j], or is within lb of an
+ * edge.  hh_di_scan = Get_DI (:804-839): di[j] from the up / down windows of
+ * window_bins[j] bins (0 at gap[j] and edges); test 0 = t-test, 1 = chi2. */
+int hh_gap_scan(const double* M, int64_t N, int32_t lb, uint8_t* gap, int32_t on_device, void* stream);
+int hh_di_scan(const double* M, int64_t N, const uint8_t* gap, const int32_t* window_bins, int32_t test,
+               double* di, int32_t on_device, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,104 @@
+"""Compartment (decay, O/E, Pearson on fp64 MFMA, top-3 PCA, PC selection)
+and DI TAD scan on the GPU vs the reference's golden outputs and the oracle."""
+import numpy as np
+import pytest
+
+from hichap_master_amd import synth
+from oracle import structure_ref
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def SF():
+    from hichap_master_amd import _lib
+    from hichap_master_amd.StructureFind import StructureFind
+    _lib.require_gpu()
+    return StructureFind
+
+
+def _match_sign(a, b):
+    return a * np.sign(np.dot(a, b))
+
+
+@pytest.mark.parametrize("name", ["compartment_n150", "compartment_n260"])
+def test_compartment_matches_reference_golden(SF, golden, name):
+    g = golden(name)
+    sf = SF(Res=100000)
+    M = g["M"]
+    dec, G, NG = sf.Distance_Decay(M=M, G_array=None)
+    np.testing.assert_array_equal(G, g["G"])
+    np.testing.assert_array_equal(NG, g["NG"])
+    np.testing.assert_allclose(dec, g["decline"], rtol=1e-12, atol=0)
+    pcs, Cor, OE = sf.Get_PCA(distance_bin=dec.copy(), M=M, NG_array=NG)
+    np.testing.assert_allclose(np.asarray(Cor), g["Cor"], rtol=0, atol=1e-12)
+    np.testing.assert_allclose(np.asarray(OE), g["OE"], rtol=1e-12, atol=0)
+    for k in range(3):
+        np.testing.assert_allclose(_match_sign(pcs[k], g["pcs"][k]), g["pcs"][k], atol=1e-9)
+    pc = sf.Select_PC_new(Cor, OE[NG], pcs)
+    full = np.zeros(M.shape[0])
+    full[NG] = pc
+    np.testing.assert_allclose(full, g["pc"], atol=1e-9)
+    np.testing.assert_array_equal(np.sign(full), np.sign(g["pc"]))
+    # the whole per-chromosome body in one call
+    np.testing.assert_allclose(SF(Res=100000).compartment(M), g["pc"], atol=1e-9)
+    # haplotype selection (sign = solver convention: compare up to sign)
+    al = SF(Res=100000).compartment(M, Tranditional_PC=g["trad"])
+    np.testing.assert_allclose(_match_sign(al, g["allelic"]), g["allelic"], atol=1e-9)
+
+
+def test_select_pc_on_host_arrays(SF, golden):
+    g = golden("compartment_n150")
+    sf = SF(Res=100000)
+    NG = g["NG"]
+    pc = sf.Select_PC_new(g["Cor"], g["OE"][NG], g["pcs"])
+    ref, _ = structure_ref.select_pc(g["Cor"], g["OE"][NG], g["pcs"])
+    np.testing.assert_array_equal(pc, ref)
+
+
+@pytest.mark.parametrize("N", [700, 1500])
+def test_compartment_vs_oracle_larger(SF, N):
+    rng = np.random.default_rng(N)
+    M = synth.dense_chrom(N, rng, A=80.0, comp_len=(20, 60), gap_frac=0.03).astype(np.float64)
+    sf = SF(Res=25000)
+    dec, G, NG = sf.Distance_Decay(M=M, G_array=None)
+    d_ref, G_ref, NG_ref = structure_ref.distance_decay(M)
+    np.testing.assert_array_equal(NG, NG_ref)
+    np.testing.assert_allclose(dec, d_ref, rtol=1e-12)
+    pcs, Cor, OE = sf.Get_PCA(distance_bin=dec.copy(), M=M, NG_array=NG)
+    p_ref, C_ref, _ = structure_ref.get_pca(d_ref, M, NG_ref)
+    C = np.asarray(Cor)
+    np.testing.assert_allclose(C, C_ref, atol=1e-11)
+    np.testing.assert_allclose(C, C.T, atol=1e-15)  # corrcoef divides rows then columns: not bitwise symmetric
+    # PC1 always well separated; PC2/3 compared through the selected vector
+    np.testing.assert_allclose(_match_sign(pcs[0], p_ref[0]), p_ref[0], atol=1e-8)
+    full = sf.compartment(M)
+    ref_full, _, _, _ = structure_ref.compartment(M)
+    big = np.abs(ref_full) > 1e-6
+    np.testing.assert_array_equal(np.sign(full[big]), np.sign(ref_full[big]))
+    np.testing.assert_allclose(full, ref_full, atol=1e-7)
+
+
+@pytest.mark.parametrize("name,test", [("di_ttest_n220", "ttest"), ("di_chitest_n220", "chitest")])
+def test_di_matches_reference_golden(SF, golden, name, test):
+    g = golden(name)
+    sf = SF(Res=40000)
+    sf.TAD_parameter_init(200000, 4000000, 3, 600000, test)
+    gap, di = sf.di_scan(g["M"])
+    np.testing.assert_array_equal(gap, g["gap"])
+    np.testing.assert_allclose(di, g["DI"], rtol=1e-12, atol=1e-300)
+    np.testing.assert_array_equal(np.sign(di), np.sign(g["DI"]))
+    assert sf.Gap_Filter(gap, g["M"]) == list(g["gap_filtered"])
+
+
+def test_di_large_vs_oracle(SF):
+    rng = np.random.default_rng(9)
+    N = 3000
+    M = synth.dense_chrom(N, rng, A=30.0, gap_frac=0.03).astype(np.float64)
+    sf = SF(Res=10000)
+    sf.TAD_parameter_init(50000, 4000000, 3, 600000, "ttest")
+    gap, di = sf.di_scan(M)
+    gref = structure_ref.get_gap(M, 50000, 10000)
+    np.testing.assert_array_equal(gap, gref)
+    dref = structure_ref.get_di(M, gref, 60, "ttest")
+    np.testing.assert_allclose(di, dref, rtol=1e-11, atol=1e-300)
