@@ -241,24 +241,27 @@ class StructureFind(object):
     def Get_Gap(self, M):
         """Gap columns for TAD calling (StructureFind.py:721-751)."""
         _lib.require_gpu()
-        A = np.ascontiguousarray(M, dtype=np.float64)
-        N = A.shape[0]
+        lb = int(self.minTAD / self.Res)
+        band = column_band(M, lb)
+        N = band.shape[0]
         g = np.empty(N, np.uint8)
-        call("hh_gap_scan", ptr(A), N, int(self.minTAD / self.Res), ptr(g), 0, None)
+        call("hh_gap_scan", ptr(band), N, lb, lb, ptr(g), 0, None)
         return np.nonzero(g)[0]
 
     def Get_DI(self, M, Gap, window_bin):
         """Directionality index (StructureFind.py:804-839)."""
         _lib.require_gpu()
-        A = np.ascontiguousarray(M, dtype=np.float64)
-        N = A.shape[0]
+        N = np.shape(M)[0]
         g = np.zeros(N, np.uint8)
         g[np.asarray(Gap, dtype=np.int64)] = 1
         w = np.ascontiguousarray(np.broadcast_to(np.asarray(window_bin), (N,)), dtype=np.int32)
         if self.test_type not in ("ttest", "chitest"):
             return np.zeros(N)
+        B = int(max(w.max(), 0))
+        band = column_band(M, B)
         di = np.empty(N, np.float64)
-        call("hh_di_scan", ptr(A), N, ptr(g), ptr(w), 0 if self.test_type == "ttest" else 1, ptr(di), 0, None)
+        call("hh_di_scan", ptr(band), N, B, ptr(g), ptr(w), 0 if self.test_type == "ttest" else 1, ptr(di), 0,
+             None)
         return di
 
     def Gap_Filter(self, Gap, M):
@@ -305,6 +308,21 @@ class StructureFind(object):
         gap = np.array(gap)
         wb = int((self.window if window is None else window) / self.Res)
         return gap, self.Get_DI(M, gap, np.ones(N, dtype=int) * wb)
+
+
+def column_band(M, B):
+    """band[j, B + k] = M[j + k, j] for k in [-B, B] (0 outside): the part of
+    each column the gap / DI scans read, so N x N never crosses PCIe."""
+    M = np.asarray(M)
+    N = M.shape[0]
+    band = np.zeros((N, 2 * B + 1), dtype=np.float64)
+    for k in range(-min(B, N - 1), min(B, N - 1) + 1):
+        d = np.diagonal(M, offset=-k)  # M[t + k, t] (k >= 0) / M[t, t - k] (k < 0)
+        if k >= 0:
+            band[: N - k, B + k] = d
+        else:
+            band[-k:, B + k] = d
+    return band
 
 
 def _means_minus(st, pc):

@@ -88,8 +88,8 @@ SIGNATURES = {
     "hh_comp_correlation": (C.c_int, [P, P, P, I64, P]),
     "hh_comp_get_cor": (C.c_int, [P, P, P]),
     "hh_comp_set_cor": (C.c_int, [P, P, P]),
-    "hh_gap_scan": (C.c_int, [P, I64, I32, P, I32, P]),
-    "hh_di_scan": (C.c_int, [P, I64, P, P, I32, P, I32, P]),
+    "hh_gap_scan": (C.c_int, [P, I64, I32, I32, P, I32, P]),
+    "hh_di_scan": (C.c_int, [P, I64, I32, P, P, I32, P, I32, P]),
     "hh_comp_pca": (C.c_int, [P, I32, F64, I32, P, P, P, P]),
     "hh_comp_select_stats": (C.c_int, [P, P, I32, F64, P, P]),
 }

@@ -11,7 +11,9 @@
 //   K8 top-k right singular vectors of the column-centred Cor (sklearn
 //        PCA(3).fit(Cor).components_, :338-340) by block subspace iteration
 //        with Rayleigh-Ritz: A V = Xc^T (Xc V), Xc = Cor - 1 mu^T, applied as
-//        two skinny products with Cor (k_cor_mul); b x b algebra on the host.
+//        two skinny products with Cor on fp64 MFMA (k_cor_mul_part, split-K,
+//        + k_cor_mul_sum with the rank-1 centring fused); Gram products
+//        k_gram_part/k_gram_sum; b x b algebra (Jacobi, Cholesky) on the host.
 //      k_select_stats  masked sums over Cor and O/E[NG, NG] that
 //        Select_PC_new's means_minus / select_ab need (:374-423).
 // All reductions are fixed-order (deterministic).
@@ -214,73 +216,117 @@ __global__ void k_corr_norm_oop(const double* __restrict__ Cov, long long n, lon
 }
 
 // ------------------------------------------------------------------ K8
-// out[i][0..B) = sum_j Cor[i][j] * V[j][0..B)   (V row-major n x B)
-// block: 16 rows; thread (row r = t/16, part q = t%16); columns in chunks of 256.
-__global__ __launch_bounds__(256) void k_cor_mul(const double* __restrict__ Cor, long long ldc, long long n,
-                                                 const double* __restrict__ V, double* __restrict__ out) {
-    __shared__ double Vs[256][kSB + 1];
-    const int r = threadIdx.x / 16, q = threadIdx.x % 16;
-    const long long i = (long long)blockIdx.x * 16 + r;
-    double acc[kSB];
+// Y = Cor V (n x B, V row-major) on fp64 MFMA, split over K.  Cor is
+// symmetric, so the product is taken as Cor^T V: a lane's A operand is a
+// 32-B d4 of a Cor row (16 lanes cover 512 contiguous bytes), giving 4
+// MFMAs whose A-row r stands for output row i0 + 4 r + t.  A block = 64
+// output rows x 16 K-rows per step (wave w takes K-rows 4w..4w+3); the four
+// waves are reduced in LDS in wave order and each K split writes its own
+// partial, summed in split order by k_cor_mul_sum (deterministic).
+// Cor is ld x ld with zero padding, so only V needs a bound check.
+__global__ __launch_bounds__(256) void k_cor_mul_part(const double* __restrict__ Cor, long long ldc, long long n,
+                                                      const double* __restrict__ V, int ksteps,
+                                                      double* __restrict__ part) {
+    __shared__ double red[3][16 * 64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const long long i0 = (long long)blockIdx.x * 64;
+    const long long kbeg = (long long)blockIdx.y * ksteps * 16;
+    const int kr = 4 * w + (lane >> 4);
+    const int nsteps = (int)std::min<long long>(ksteps, (ldc - kbeg) / 16);
+    d4 acc[4];
 #pragma unroll
-    for (int b = 0; b < kSB; ++b) acc[b] = 0.0;
-    for (long long j0 = 0; j0 < n; j0 += 256) {
-        __syncthreads();
-        for (int e = threadIdx.x; e < 256 * kSB; e += 256) {
-            const int jj = e / kSB, b = e % kSB;
-            Vs[jj][b] = (j0 + jj < n) ? V[(j0 + jj) * kSB + b] : 0.0;
+    for (int t = 0; t < 4; ++t) acc[t] = d4{0.0, 0.0, 0.0, 0.0};
+    const double* cp = Cor + (kbeg + kr) * ldc + i0 + 4 * (lane & 15);
+    const double* vp = V + (kbeg + kr) * kSB + (lane & 15);
+    long long k = kbeg + kr;
+    int st = 0;
+    for (; st + 4 <= nsteps; st += 4) {  // 4 K-steps of loads in flight
+        d4 av[4];
+        double bv[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            av[u] = __builtin_nontemporal_load(reinterpret_cast<const d4*>(cp + u * 16 * ldc));
+            bv[u] = (k + 16 * u) < n ? vp[u * 16 * kSB] : 0.0;
         }
-        __syncthreads();
-        if (i < n) {
-#pragma unroll 4
-            for (int u = 0; u < 16; ++u) {
-                const int jj = q + 16 * u;
-                const long long j = j0 + jj;
-                const double c = j < n ? Cor[i * ldc + j] : 0.0;
 #pragma unroll
-                for (int b = 0; b < kSB; ++b) acc[b] = fma(c, Vs[jj][b], acc[b]);
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+                acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[u][t], bv[u], acc[t], 0, 0, 0);
+        cp += 64 * ldc;
+        vp += 64 * kSB;
+        k += 64;
+    }
+    for (; st < nsteps; ++st) {
+        const d4 av = __builtin_nontemporal_load(reinterpret_cast<const d4*>(cp));
+        const double bv = k < n ? *vp : 0.0;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[t], bv, acc[t], 0, 0, 0);
+        cp += 16 * ldc;
+        vp += 16 * kSB;
+        k += 16;
+    }
+    if (w > 0)
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int reg = 0; reg < 4; ++reg) red[w - 1][(t * 4 + reg) * 64 + lane] = acc[t][reg];
+    __syncthreads();
+    if (w == 0) {
+        double* out = part + ((long long)blockIdx.y * ldc + i0) * kSB;
+        // D layout: col = lane & 15, row = (lane >> 4) + 4 * reg  ->  output row 4 * row + t
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int reg = 0; reg < 4; ++reg) {
+                const int q = (t * 4 + reg) * 64 + lane;
+                const double v = ((acc[t][reg] + red[0][q]) + red[1][q]) + red[2][q];
+                out[(4 * ((lane >> 4) + 4 * reg) + t) * kSB + (lane & 15)] = v;
             }
-        }
     }
-    // reduce over the 16 threads of the row (lanes 16r..16r+15 of a wave)
-#pragma unroll
-    for (int b = 0; b < kSB; ++b) {
-        double x = acc[b];
-#pragma unroll
-        for (int o = 8; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
-        acc[b] = x;
-    }
-    if (i < n && q == 0)
-#pragma unroll
-        for (int b = 0; b < kSB; ++b) out[i * kSB + b] = acc[b];
 }
 
-// Column means of Cor (over rows < n): mu[j] = sum_i Cor[i][j] / n (fixed order)
-__global__ void k_cor_colmean(const double* __restrict__ Cor, long long ldc, long long n, double* __restrict__ mu) {
-    const long long j = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= n) return;
+// Y[i][b] = sum_s part[s][i][b] - x_i d_b   (x nullptr -> 1; d nullptr -> none)
+__global__ void k_cor_mul_sum(const double* __restrict__ part, int ks, long long ldc, long long n,
+                              const double* __restrict__ x, const double* __restrict__ d, double* __restrict__ Y) {
+    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n * kSB) return;
     double acc = 0.0;
-    for (long long i = 0; i < n; ++i) acc += Cor[i * ldc + j];
-    mu[j] = acc / (double)n;
+    for (int s = 0; s < ks; ++s) acc += part[(long long)s * ldc * kSB + t];
+    if (d) acc -= (x ? x[t / kSB] : 1.0) * d[t % kSB];
+    Y[t] = acc;
 }
 
-// Gram-type reduction: G[a][b] = sum_i X[i][a] * Y[i][b] (n x B each), block partials.
+// Gram-type reduction: G[a][b] = sum_i X[i][a] * Y[i][b] (n x B each).
+// Block partials over 256-row slabs staged through LDS (coalesced), then a
+// wave per entry sums the partials (fixed shuffle tree: deterministic).
+constexpr int kGramRows = 64;
 __global__ __launch_bounds__(256) void k_gram_part(const double* __restrict__ X, const double* __restrict__ Y,
-                                                   long long n, int rows_per_block, double* __restrict__ part) {
-    // thread t = a * 16 + b
+                                                   long long n, double* __restrict__ part) {
+    __shared__ double xs[64][kSB + 1], ys[64][kSB + 1];
     const int a = threadIdx.x / kSB, b = threadIdx.x % kSB;
-    const long long r0 = (long long)blockIdx.x * rows_per_block;
-    const long long r1 = std::min<long long>(n, r0 + rows_per_block);
+    const long long r0 = (long long)blockIdx.x * kGramRows;
     double acc = 0.0;
-    for (long long i = r0; i < r1; ++i) acc = fma(X[i * kSB + a], Y[i * kSB + b], acc);
+    for (int c = 0; c < kGramRows; c += 64) {
+        __syncthreads();
+        for (int e = threadIdx.x; e < 64 * kSB; e += 256) {
+            const long long i = r0 + c + e / kSB;
+            xs[e / kSB][e % kSB] = i < n ? X[i * kSB + e % kSB] : 0.0;
+            ys[e / kSB][e % kSB] = i < n ? Y[i * kSB + e % kSB] : 0.0;
+        }
+        __syncthreads();
+#pragma unroll 8
+        for (int r = 0; r < 64; ++r) acc = fma(xs[r][a], ys[r][b], acc);
+    }
     part[(size_t)blockIdx.x * kSB * kSB + threadIdx.x] = acc;
 }
 
-__global__ void k_gram_sum(const double* __restrict__ part, int nblk, double* __restrict__ G) {
-    const int t = threadIdx.x;
+__global__ __launch_bounds__(64) void k_gram_sum(const double* __restrict__ part, int nblk, double* __restrict__ G) {
+    const int e = blockIdx.x, l = threadIdx.x;
     double acc = 0.0;
-    for (int k = 0; k < nblk; ++k) acc += part[(size_t)k * kSB * kSB + t];
-    G[t] = acc;
+    for (int k = l; k < nblk; k += 64) acc += part[(size_t)k * kSB * kSB + e];
+    acc = wave_sum(acc);
+    if (l == 0) G[e] = acc;
 }
 
 // Y = X * R (n x B times B x B) ; optionally out = X - 1 t^T or X - mu u^T
@@ -293,16 +339,6 @@ __global__ void k_rot(const double* __restrict__ X, const double* __restrict__ R
     double acc = 0.0;
     for (int a = 0; a < kSB; ++a) acc = fma(X[i * kSB + a], R[a * kSB + b], acc);
     Y[t] = acc;
-}
-
-// W -= x * y^T  (x: n-vector or nullptr = ones; y: B-vector)
-__global__ void k_rank1_sub(double* __restrict__ W, const double* __restrict__ x, const double* __restrict__ y,
-                            long long n) {
-    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= n * kSB) return;
-    const long long i = t / kSB;
-    const int b = (int)(t % kSB);
-    W[t] -= (x ? x[i] : 1.0) * y[b];
 }
 
 // ------------------------------------------------------------------ select
@@ -430,27 +466,56 @@ struct hh_comp {
 
 namespace hh {
 
-static void gram(const double* X, const double* Y, long long n, std::vector<double>& G, hipStream_t s) {
-    const int rpb = 512;
-    const int nblk = (int)std::max<long long>(1, (n + rpb - 1) / rpb);
-    DBuf<double> part((size_t)nblk * kSB * kSB), dG(kSB * kSB);
-    hipLaunchKernelGGL(k_gram_part, dim3(nblk), dim3(256), 0, s, X, Y, n, rpb, part.p);
-    hipLaunchKernelGGL(k_gram_sum, dim3(1), dim3(kSB * kSB), 0, s, part.p, nblk, dG.p);
-    G.resize(kSB * kSB);
-    dG.download(G.data(), G.size(), s);
-    HIP_CHECK(hipStreamSynchronize(s));
-}
+// Small-matrix workspace of the subspace iteration (no allocation in the loop).
+struct PcaWork {
+    long long n = 0, ldc = 0;
+    int nblk = 0, ks = 1, ksteps = 1;
+    DBuf<double> part, G, R, mpart;
+    std::vector<double> hG;
+    PcaWork(long long n_, long long ldc_) : n(n_), ldc(ldc_) {
+        nblk = (int)std::max<long long>(1, (n + kGramRows - 1) / kGramRows);
+        part.alloc((size_t)nblk * kSB * kSB);
+        G.alloc(kSB * kSB);
+        R.alloc(kSB * kSB);
+        hG.resize(kSB * kSB);
+        // split K so that the product's blocks (24 KB LDS, 4 waves) are all
+        // resident at once (~6 per CU): no tail round
+        const long long rb = ldc / 64, steps = ldc / 16;
+        const long long want = std::max<long long>(1, std::min<long long>(32, 1280 / rb));
+        ksteps = (int)((steps + want - 1) / want);
+        ks = (int)((steps + ksteps - 1) / ksteps);
+        mpart.alloc((size_t)ks * ldc * kSB);
+    }
+    // G = X^T Y on the device (B x B), fixed-order reduction
+    void gram_dev(const double* X, const double* Y, hipStream_t s) {
+        hipLaunchKernelGGL(k_gram_part, dim3(nblk), dim3(256), 0, s, X, Y, n, part.p);
+        hipLaunchKernelGGL(k_gram_sum, dim3(kSB * kSB), dim3(64), 0, s, part.p, nblk, G.p);
+    }
+    // ... and hG = G on the host
+    void gram(const double* X, const double* Y, hipStream_t s) {
+        gram_dev(X, Y, s);
+        G.download(hG.data(), hG.size(), s);
+        HIP_CHECK(hipStreamSynchronize(s));
+    }
+    // Y = Cor V - x d^T, d = row 0 of the last gram_dev (d_use) or none
+    void cor_mul(const double* Cor, const double* V, const double* x, bool d_use, double* Y, hipStream_t s) {
+        hipLaunchKernelGGL(k_cor_mul_part, dim3((unsigned)(ldc / 64), (unsigned)ks), dim3(256), 0, s, Cor, ldc, n, V,
+                           ksteps, mpart.p);
+        hipLaunchKernelGGL(k_cor_mul_sum, dim3((unsigned)((n * kSB + 255) / 256)), dim3(256), 0, s, mpart.p, ks, ldc, n,
+                           x, d_use ? (const double*)G.p : nullptr, Y);
+    }
+    void put_small(const std::vector<double>& m, hipStream_t s) { R.upload(m.data(), m.size(), s); }
+};
 
 // V <- V R^{-1} twice (CholQR2); returns false if V lost rank.
-static bool orthonormalize(DBuf<double>& V, DBuf<double>& tmp, long long n, hipStream_t s) {
+static bool orthonormalize(PcaWork& w, DBuf<double>& V, DBuf<double>& tmp, long long n, hipStream_t s) {
     for (int pass = 0; pass < 2; ++pass) {
-        std::vector<double> G, Rinv;
-        gram(V.p, V.p, n, G, s);
-        if (!chol_inv_upper(kSB, G, Rinv)) return false;
-        DBuf<double> dR = to_device(Rinv, s);
-        hipLaunchKernelGGL(k_rot, dim3((unsigned)((n * kSB + 255) / 256)), dim3(256), 0, s, V.p, dR.p, n, tmp.p);
-        HIP_CHECK(hipMemcpyAsync(V.p, tmp.p, n * kSB * sizeof(double), hipMemcpyDeviceToDevice, s));
-        HIP_CHECK(hipStreamSynchronize(s));
+        std::vector<double> Rinv;
+        w.gram(V.p, V.p, s);
+        if (!chol_inv_upper(kSB, w.hG, Rinv)) return false;
+        w.put_small(Rinv, s);
+        hipLaunchKernelGGL(k_rot, dim3((unsigned)((n * kSB + 255) / 256)), dim3(256), 0, s, V.p, w.R.p, n, tmp.p);
+        std::swap(V.p, tmp.p);
     }
     return true;
 }
@@ -578,51 +643,46 @@ int hh_comp_pca(hh_comp* c, int32_t k, double tol, int32_t max_iters, double* co
         hipStream_t s = as_stream(stream);
         const long long n = c->n;
         HH_REQUIRE(n >= kSB, "matrix smaller than the subspace block (16)");
-        DBuf<double> mu(n);
-        hipLaunchKernelGGL(k_cor_colmean, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, c->cor.p, c->ld, n, mu.p);
+        PcaWork wk(n, c->ld);
+        // mu and 1 as the first column of n x B blocks, so mu^T X and 1^T X are
+        // row 0 of a Gram product; mu = column means of Cor = (Cor 1) / n.
+        DBuf<double> mu(n), mupad, onepad;
+        {
+            std::vector<double> op((size_t)n * kSB, 0.0), muh(n), mp((size_t)n * kSB, 0.0);
+            for (long long i = 0; i < n; ++i) op[i * kSB] = 1.0;
+            onepad = to_device(op, s);
+            DBuf<double> rs((size_t)n * kSB);
+            wk.cor_mul(c->cor.p, onepad.p, nullptr, false, rs.p, s);
+            std::vector<double> h((size_t)n * kSB);
+            rs.download(h.data(), h.size(), s);
+            HIP_CHECK(hipStreamSynchronize(s));
+            for (long long i = 0; i < n; ++i) { muh[i] = h[i * kSB] / (double)n; mp[i * kSB] = muh[i]; }
+            mu = to_device(muh, s);
+            mupad = to_device(mp, s);
+        }
         // deterministic start block
         std::vector<double> v0((size_t)n * kSB);
         for (long long i = 0; i < n; ++i)
             for (int b = 0; b < kSB; ++b) v0[i * kSB + b] = (double)u01(mix64(0x5eedULL + i * kSB + b)) - 0.5;
         DBuf<double> V = to_device(v0, s), W((size_t)n * kSB), W1((size_t)n * kSB), tmp((size_t)n * kSB);
-        HH_REQUIRE(orthonormalize(V, tmp, n, s), "start block rank deficient");
-        const unsigned gm = (unsigned)((n + 15) / 16), ge = (unsigned)((n * kSB + 255) / 256);
-        // mu and 1 as the first column of n x B blocks, so mu^T X and 1^T X are
-        // row 0 of a Gram product.
-        DBuf<double> mupad, onepad;
-        {
-            std::vector<double> muh(n), mp((size_t)n * kSB, 0.0), op((size_t)n * kSB, 0.0);
-            mu.download(muh.data(), n, s);
-            HIP_CHECK(hipStreamSynchronize(s));
-            for (long long i = 0; i < n; ++i) { mp[i * kSB] = muh[i]; op[i * kSB] = 1.0; }
-            mupad = to_device(mp, s);
-            onepad = to_device(op, s);
-        }
+        HH_REQUIRE(orthonormalize(wk, V, tmp, n, s), "start block rank deficient");
+        const unsigned ge = (unsigned)((n * kSB + 255) / 256);
         std::vector<double> prev((size_t)n * k, 0.0), cur((size_t)n * k);
-        std::vector<double> evals, evecs, G, Vh((size_t)n * kSB);
+        std::vector<double> evals, evecs, Vh((size_t)n * kSB);
         int it = 0;
         bool done = false;
         for (it = 1; it <= max_iters && !done; ++it) {
             // A V = Xc^T (Xc V) with Xc = Cor - 1 mu^T (Cor symmetric):
             // W1 = Cor V - 1 (mu^T V);  W = Cor W1 - mu (1^T W1)
-            hipLaunchKernelGGL(k_cor_mul, dim3(gm), dim3(256), 0, s, c->cor.p, c->ld, n, V.p, W1.p);
-            gram(mupad.p, V.p, n, G, s);
-            {
-                std::vector<double> t(G.begin(), G.begin() + kSB);
-                DBuf<double> dt = to_device(t, s);
-                hipLaunchKernelGGL(k_rank1_sub, dim3(ge), dim3(256), 0, s, W1.p, (const double*)nullptr, dt.p, n);
-                hipLaunchKernelGGL(k_cor_mul, dim3(gm), dim3(256), 0, s, c->cor.p, c->ld, n, W1.p, W.p);
-                gram(onepad.p, W1.p, n, G, s);
-                std::vector<double> u(G.begin(), G.begin() + kSB);
-                DBuf<double> du = to_device(u, s);
-                hipLaunchKernelGGL(k_rank1_sub, dim3(ge), dim3(256), 0, s, W.p, mu.p, du.p, n);
-                HIP_CHECK(hipStreamSynchronize(s));
-            }
+            wk.gram_dev(mupad.p, V.p, s);
+            wk.cor_mul(c->cor.p, V.p, nullptr, true, W1.p, s);
+            wk.gram_dev(onepad.p, W1.p, s);
+            wk.cor_mul(c->cor.p, W1.p, mu.p, true, W.p, s);
             // Rayleigh-Ritz: H = V^T W (V orthonormal), eig -> Y (descending)
-            gram(V.p, W.p, n, G, s);
+            wk.gram(V.p, W.p, s);
             std::vector<double> H(kSB * kSB);
             for (int a = 0; a < kSB; ++a)
-                for (int b = 0; b < kSB; ++b) H[a * kSB + b] = 0.5 * (G[a * kSB + b] + G[b * kSB + a]);
+                for (int b = 0; b < kSB; ++b) H[a * kSB + b] = 0.5 * (wk.hG[a * kSB + b] + wk.hG[b * kSB + a]);
             jacobi_eig(kSB, H, evals, evecs);
             std::vector<int> ord(kSB);
             std::iota(ord.begin(), ord.end(), 0);
@@ -630,9 +690,9 @@ int hh_comp_pca(hh_comp* c, int32_t k, double tol, int32_t max_iters, double* co
             std::vector<double> Y(kSB * kSB);
             for (int a = 0; a < kSB; ++a)
                 for (int b = 0; b < kSB; ++b) Y[a * kSB + b] = evecs[a * kSB + ord[b]];
-            DBuf<double> dY = to_device(Y, s);
+            wk.put_small(Y, s);
             // Ritz vectors of this iteration: V Y
-            hipLaunchKernelGGL(k_rot, dim3(ge), dim3(256), 0, s, V.p, dY.p, n, tmp.p);
+            hipLaunchKernelGGL(k_rot, dim3(ge), dim3(256), 0, s, V.p, wk.R.p, n, tmp.p);
             tmp.download(Vh.data(), Vh.size(), s);
             HIP_CHECK(hipStreamSynchronize(s));
             // convergence: largest entry change of the (unit, sign-aligned)
@@ -657,8 +717,8 @@ int hh_comp_pca(hh_comp* c, int32_t k, double tol, int32_t max_iters, double* co
             prev = cur;
             if (!done) {
                 // next block: orth(W Y)
-                hipLaunchKernelGGL(k_rot, dim3(ge), dim3(256), 0, s, W.p, dY.p, n, V.p);
-                HH_REQUIRE(orthonormalize(V, tmp, n, s), "subspace lost rank");
+                hipLaunchKernelGGL(k_rot, dim3(ge), dim3(256), 0, s, W.p, wk.R.p, n, V.p);
+                HH_REQUIRE(orthonormalize(wk, V, tmp, n, s), "subspace lost rank");
             }
         }
         c->iters = it - 1;
@@ -703,35 +763,39 @@ int hh_comp_select_stats(hh_comp* c, const double* pcs, int32_t k, double eps, d
 
 // ================================================================== DI (K9)
 // StructureFind.Get_Gap (:721-751) and Get_DI (:804-839), one thread per
-// column (the windows are 2 x 15..60 bins; the matrix slice is tiny).
+// column.  Both only read column j within +-B rows of the diagonal, so the
+// matrix crosses PCIe as a band: band[j][B + k] = M[j + k][j], k in [-B, B]
+// (N x (2B+1) instead of N x N: 24 MB instead of 5 GB for chr1 at 10 kb).
 namespace hh {
-__global__ void k_gap_scan(const double* __restrict__ M, long long N, int lb, uint8_t* __restrict__ gap) {
+__global__ void k_gap_scan(const double* __restrict__ band, long long N, int B, int lb, uint8_t* __restrict__ gap) {
     const long long j = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= N) return;
-    bool g = true;  // edges are gaps
+    const double* col = band + j * (2 * B + 1) + B;
+    bool g = true;  // within lb of an edge: gap
     if (lb <= j && j <= N - 1 - lb) {
         int nz = 0;
-        for (long long r = j - lb; r < j + lb; ++r) nz += M[r * N + j] != 0.0;
+        for (int k = -lb; k < lb; ++k) nz += col[k] != 0.0;  // rows j-lb .. j+lb-1
         g = (double)nz < 2.0 * lb * 0.8;
     }
     gap[j] = g ? 1 : 0;
 }
 
-__global__ void k_di(const double* __restrict__ M, long long N, const uint8_t* __restrict__ gap,
+__global__ void k_di(const double* __restrict__ band, long long N, int B, const uint8_t* __restrict__ gap,
                      const int* __restrict__ win, int test, double* __restrict__ di) {
     const long long j = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= N) return;
+    const double* col = band + j * (2 * B + 1) + B;
     const int w = win[j];
     double v = 0.0;
     if (!gap[j] && !(j < w || j > N - w - 1) && w >= 1) {
         double su = 0.0, sd = 0.0;
-        for (int k = 1; k <= w; ++k) { su += M[(j - k) * N + j]; sd += M[(j + k) * N + j]; }
+        for (int k = 1; k <= w; ++k) { su += col[-k]; sd += col[k]; }  // up reversed / down
         if (test == 0) {
             const double um = su / w, dm = sd / w;
             const double den = (double)w * (double)(w - 1);
             double qu = 0.0, qd = 0.0;
             for (int k = 1; k <= w; ++k) {
-                const double a = M[(j - k) * N + j] - um, b = M[(j + k) * N + j] - dm;
+                const double a = col[-k] - um, b = col[k] - dm;
                 qu += a * a / den;
                 qd += b * b / den;
             }
@@ -748,42 +812,47 @@ __global__ void k_di(const double* __restrict__ M, long long N, const uint8_t* _
 }  // namespace hh
 
 namespace {
-const double* stage_dense(const double* M, int64_t N, int32_t on_device, hh::DBuf<double>& buf, hipStream_t s) {
-    if (on_device) return M;
-    buf.alloc((size_t)N * N);
-    buf.upload(M, (size_t)N * N, s);
+const double* stage_band(const double* band, int64_t N, int32_t B, int32_t on_device, hh::DBuf<double>& buf,
+                         hipStream_t s) {
+    if (on_device) return band;
+    const size_t cnt = (size_t)N * (2 * B + 1);
+    buf.alloc(cnt);
+    buf.upload(band, cnt, s);
     return buf.p;
 }
 }  // namespace
 
-extern "C" int hh_gap_scan(const double* M, int64_t N, int32_t lb, uint8_t* gap, int32_t on_device, void* stream) {
+extern "C" int hh_gap_scan(const double* band, int64_t N, int32_t B, int32_t lb, uint8_t* gap, int32_t on_device,
+                           void* stream) {
     return guard([&] {
-        HH_REQUIRE(M && gap && N > 0 && lb >= 0, "bad arguments");
+        HH_REQUIRE(band && gap && N > 0 && lb >= 0 && B >= lb, "bad arguments (need 0 <= lb <= B)");
         hipStream_t s = as_stream(stream);
-        DBuf<double> dM;
-        const double* pm = stage_dense(M, N, on_device, dM, s);
+        DBuf<double> dB;
+        const double* pb = stage_band(band, N, B, on_device, dB, s);
         DBuf<uint8_t> dg(N);
-        hipLaunchKernelGGL(k_gap_scan, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, pm, (long long)N, lb, dg.p);
+        hipLaunchKernelGGL(k_gap_scan, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, pb, (long long)N, B, lb,
+                           dg.p);
         HIP_CHECK(hipGetLastError());
         dg.download(gap, N, s);
         HIP_CHECK(hipStreamSynchronize(s));
     });
 }
 
-extern "C" int hh_di_scan(const double* M, int64_t N, const uint8_t* gap, const int32_t* window_bins, int32_t test,
-                          double* di, int32_t on_device, void* stream) {
+extern "C" int hh_di_scan(const double* band, int64_t N, int32_t B, const uint8_t* gap, const int32_t* window_bins,
+                          int32_t test, double* di, int32_t on_device, void* stream) {
     return guard([&] {
-        HH_REQUIRE(M && window_bins && gap && di && N > 0, "bad arguments");
+        HH_REQUIRE(band && window_bins && gap && di && N > 0 && B >= 0, "bad arguments");
         HH_REQUIRE(test == 0 || test == 1, "test must be 0 (ttest) or 1 (chitest)");
+        for (int64_t j = 0; j < N; ++j) HH_REQUIRE(window_bins[j] <= B, "window larger than the band");
         hipStream_t s = as_stream(stream);
-        DBuf<double> dM;
-        const double* pm = stage_dense(M, N, on_device, dM, s);
+        DBuf<double> dB;
+        const double* pb = stage_band(band, N, B, on_device, dB, s);
         DBuf<int> dw(N);
         dw.upload(window_bins, N, s);
         DBuf<uint8_t> dg(N);
         dg.upload(gap, N, s);
         DBuf<double> dd(N);
-        hipLaunchKernelGGL(k_di, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, pm, (long long)N, dg.p, dw.p,
+        hipLaunchKernelGGL(k_di, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, pb, (long long)N, B, dg.p, dw.p,
                            test, dd.p);
         HIP_CHECK(hipGetLastError());
         dd.download(di, N, s);

@@ -220,14 +220,18 @@ int hh_comp_pca(hh_comp* c, int32_t k, double tol, int32_t max_iters, double* co
 int hh_comp_select_stats(hh_comp* c, const double* pcs, int32_t k, double eps, double* stats, void* stream);
 
 /* ------------------------------------------------------- TAD scan (DI)
- * M dense N x N float64 (balanced, NaN -> 0, for traditional data).
+ * Both scans read column j only within B rows of the diagonal, so the matrix
+ * is passed as a band: band[j * (2B+1) + B + k] = M[j + k][j], k in [-B, B]
+ * (0 outside the matrix); M balanced with NaN -> 0 for traditional data.
  * hh_gap_scan = StructureFind.Get_Gap (:721-751): gap[j] = 1 when column j
- * has fewer than 2*lb*0.8 nonzeros in M[j-lb:j+lb, j], or is within lb of an
- * edge.  hh_di_scan = Get_DI (:804-839): di[j] from the up / down windows of
- * window_bins[j] bins (0 at gap[j] and edges); test 0 = t-test, 1 = chi2. */
-int hh_gap_scan(const double* M, int64_t N, int32_t lb, uint8_t* gap, int32_t on_device, void* stream);
-int hh_di_scan(const double* M, int64_t N, const uint8_t* gap, const int32_t* window_bins, int32_t test,
-               double* di, int32_t on_device, void* stream);
+ * has fewer than 2*lb*0.8 nonzeros in M[j-lb:j+lb, j] or is within lb of an
+ * edge (lb <= B).  hh_di_scan = Get_DI (:804-839): di[j] from the up / down
+ * windows of window_bins[j] <= B bins (0 at gap[j] and edges); test 0 =
+ * t-test, 1 = chi-square. */
+int hh_gap_scan(const double* band, int64_t N, int32_t B, int32_t lb, uint8_t* gap, int32_t on_device,
+                void* stream);
+int hh_di_scan(const double* band, int64_t N, int32_t B, const uint8_t* gap, const int32_t* window_bins,
+               int32_t test, double* di, int32_t on_device, void* stream);
 
 #ifdef __cplusplus
 }

@@ -1,7 +1,8 @@
 """GPU probe: synthetic matrix generation + ICE sweep timing per variant."""
 import sys, time
 import numpy as np
-sys.path.insert(0, ".")
+import os
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from hichap_master_amd import ice, _lib, synth
 
 _lib.load(); _lib.require_gpu()
