@@ -243,7 +243,7 @@ class StructureFind(object):
         _lib.require_gpu()
         lb = int(self.minTAD / self.Res)
         band = column_band(M, lb)
-        N = band.shape[0]
+        N = band.shape[1]
         g = np.empty(N, np.uint8)
         call("hh_gap_scan", ptr(band), N, lb, lb, ptr(g), 0, None)
         return np.nonzero(g)[0]
@@ -311,17 +311,18 @@ class StructureFind(object):
 
 
 def column_band(M, B):
-    """band[j, B + k] = M[j + k, j] for k in [-B, B] (0 outside): the part of
-    each column the gap / DI scans read, so N x N never crosses PCIe."""
+    """band[B + k, j] = M[j + k, j] for k in [-B, B] (0 outside), diagonal-
+    major ((2B+1) x N): the part of each column the gap / DI scans read, so
+    N x N never crosses PCIe."""
     M = np.asarray(M)
     N = M.shape[0]
-    band = np.zeros((N, 2 * B + 1), dtype=np.float64)
+    band = np.zeros((2 * B + 1, N), dtype=np.float64)
     for k in range(-min(B, N - 1), min(B, N - 1) + 1):
         d = np.diagonal(M, offset=-k)  # M[t + k, t] (k >= 0) / M[t, t - k] (k < 0)
         if k >= 0:
-            band[: N - k, B + k] = d
+            band[B + k, : N - k] = d
         else:
-            band[-k:, B + k] = d
+            band[B + k, -k:] = d
     return band
 
 

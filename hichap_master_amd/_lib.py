@@ -81,6 +81,7 @@ SIGNATURES = {
     "hh_ice_last_sweep_timing": (C.c_int, [P, PF64, PI32, PF64]),
     "hh_dense_rowstats": (C.c_int, [P, I32, I64, P, P, P, P, I32, P]),
     "hh_dense_symvc": (C.c_int, [P, I32, I64, P, P, F64, F64, P, I32, P]),
+    "hh_twostep": (C.c_int, [P, P, P, I64, P, P, P, P, I32, P]),
     "hh_comp_create": (C.c_int, [P, I64, I32, P, C.POINTER(P)]),
     "hh_comp_free": (C.c_int, [P]),
     "hh_comp_colnnz": (C.c_int, [P, P, P]),

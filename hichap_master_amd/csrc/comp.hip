@@ -237,33 +237,34 @@ __global__ __launch_bounds__(256) void k_cor_mul_part(const double* __restrict__
 #pragma unroll
     for (int t = 0; t < 4; ++t) acc[t] = d4{0.0, 0.0, 0.0, 0.0};
     const double* cp = Cor + (kbeg + kr) * ldc + i0 + 4 * (lane & 15);
-    const double* vp = V + (kbeg + kr) * kSB + (lane & 15);
     long long k = kbeg + kr;
     int st = 0;
-    for (; st + 4 <= nsteps; st += 4) {  // 4 K-steps of loads in flight
-        d4 av[4];
-        double bv[4];
+    constexpr int U = 8;  // K-steps of loads in flight per wave
+    for (; st + U <= nsteps; st += U) {
+        d4 av[U];
+        double bv[U];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < U; ++u) {
             av[u] = __builtin_nontemporal_load(reinterpret_cast<const d4*>(cp + u * 16 * ldc));
-            bv[u] = (k + 16 * u) < n ? vp[u * 16 * kSB] : 0.0;
+            const long long kk = k + 16 * u;
+            const double x = V[(kk < n ? kk : n - 1) * kSB + (lane & 15)];  // clamped: no branch
+            bv[u] = kk < n ? x : 0.0;
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
+        for (int u = 0; u < U; ++u)
 #pragma unroll
             for (int t = 0; t < 4; ++t)
                 acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[u][t], bv[u], acc[t], 0, 0, 0);
-        cp += 64 * ldc;
-        vp += 64 * kSB;
-        k += 64;
+        cp += U * 16 * ldc;
+        k += U * 16;
     }
     for (; st < nsteps; ++st) {
         const d4 av = __builtin_nontemporal_load(reinterpret_cast<const d4*>(cp));
-        const double bv = k < n ? *vp : 0.0;
+        const double x = V[(k < n ? k : n - 1) * kSB + (lane & 15)];
+        const double bv = k < n ? x : 0.0;
 #pragma unroll
         for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[t], bv, acc[t], 0, 0, 0);
         cp += 16 * ldc;
-        vp += 16 * kSB;
         k += 16;
     }
     if (w > 0)
@@ -764,50 +765,69 @@ int hh_comp_select_stats(hh_comp* c, const double* pcs, int32_t k, double eps, d
 // ================================================================== DI (K9)
 // StructureFind.Get_Gap (:721-751) and Get_DI (:804-839), one thread per
 // column.  Both only read column j within +-B rows of the diagonal, so the
-// matrix crosses PCIe as a band: band[j][B + k] = M[j + k][j], k in [-B, B]
-// (N x (2B+1) instead of N x N: 24 MB instead of 5 GB for chr1 at 10 kb).
+// matrix crosses PCIe as a band, stored diagonal-major:
+// band[(B + k) * N + j] = M[j + k][j], k in [-B, B] (N x (2B+1) doubles:
+// 24 MB instead of 5 GB for chr1 at 10 kb); a wave's loads of one diagonal
+// are contiguous.
 namespace hh {
 __global__ void k_gap_scan(const double* __restrict__ band, long long N, int B, int lb, uint8_t* __restrict__ gap) {
     const long long j = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= N) return;
-    const double* col = band + j * (2 * B + 1) + B;
+    const double* col = band + (long long)B * N + j;  // col[k * N] = M[j + k][j]
     bool g = true;  // within lb of an edge: gap
     if (lb <= j && j <= N - 1 - lb) {
         int nz = 0;
-        for (int k = -lb; k < lb; ++k) nz += col[k] != 0.0;  // rows j-lb .. j+lb-1
+        for (int k = -lb; k < lb; ++k) nz += col[k * N] != 0.0;  // rows j-lb .. j+lb-1
         g = (double)nz < 2.0 * lb * 0.8;
     }
     gap[j] = g ? 1 : 0;
 }
 
-__global__ void k_di(const double* __restrict__ band, long long N, int B, const uint8_t* __restrict__ gap,
-                     const int* __restrict__ win, int test, double* __restrict__ di) {
-    const long long j = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= N) return;
-    const double* col = band + j * (2 * B + 1) + B;
-    const int w = win[j];
+// 8 lanes per column (lane q takes window offsets k = 1 + q + 8i); the
+// partial sums are combined by a fixed xor tree (deterministic).
+constexpr int kDiLanes = 8;
+__device__ __forceinline__ double di_lane_sum(double x) {
+    x += __shfl_xor(x, 1, 64);
+    x += __shfl_xor(x, 2, 64);
+    x += __shfl_xor(x, 4, 64);
+    return x;
+}
+__global__ __launch_bounds__(256) void k_di(const double* __restrict__ band, long long N, int B,
+                                            const uint8_t* __restrict__ gap, const int* __restrict__ win, int test,
+                                            double* __restrict__ di) {
+    const long long j = ((long long)blockIdx.x * blockDim.x + threadIdx.x) / kDiLanes;
+    const int q = threadIdx.x % kDiLanes;
+    const bool inb = j < N;
+    const long long jj = inb ? j : N - 1;  // whole lane groups stay in the shuffles
+    const double* col = band + (long long)B * N + jj;
+    const int w = win[jj];
+    const bool live = inb && !gap[jj] && !(jj < w || jj > N - w - 1) && w >= 1;
+    double su = 0.0, sd = 0.0;
+    if (live)
+        for (int k = 1 + q; k <= w; k += kDiLanes) { su += col[-k * N]; sd += col[k * N]; }
+    su = di_lane_sum(su);
+    sd = di_lane_sum(sd);
     double v = 0.0;
-    if (!gap[j] && !(j < w || j > N - w - 1) && w >= 1) {
-        double su = 0.0, sd = 0.0;
-        for (int k = 1; k <= w; ++k) { su += col[-k]; sd += col[k]; }  // up reversed / down
-        if (test == 0) {
-            const double um = su / w, dm = sd / w;
-            const double den = (double)w * (double)(w - 1);
-            double qu = 0.0, qd = 0.0;
-            for (int k = 1; k <= w; ++k) {
-                const double a = col[-k] - um, b = col[k] - dm;
+    if (test == 0) {
+        const double um = su / w, dm = sd / w;
+        const double den = (double)w * (double)(w - 1);
+        double qu = 0.0, qd = 0.0;
+        if (live)
+            for (int k = 1 + q; k <= w; k += kDiLanes) {
+                const double a = col[-k * N] - um, b = col[k * N] - dm;
                 qu += a * a / den;
                 qd += b * b / den;
             }
-            const double dsum = sqrt(qu + qd);
-            if (dsum != 0.0) v = (dm - um) / dsum;
-        } else {
-            const double e = (su + sd) / 2.0;
-            if (su != sd && e != 0.0)
-                v = (sd - su) / fabs(sd - su) * ((su - e) * (su - e) / e + (sd - e) * (sd - e) / e);
-        }
+        qu = di_lane_sum(qu);
+        qd = di_lane_sum(qd);
+        const double dsum = sqrt(qu + qd);
+        if (live && dsum != 0.0) v = (dm - um) / dsum;
+    } else if (live) {
+        const double e = (su + sd) / 2.0;
+        if (su != sd && e != 0.0)
+            v = (sd - su) / fabs(sd - su) * ((su - e) * (su - e) / e + (sd - e) * (sd - e) / e);
     }
-    di[j] = v;
+    if (inb && q == 0) di[j] = v;
 }
 }  // namespace hh
 
@@ -852,8 +872,8 @@ extern "C" int hh_di_scan(const double* band, int64_t N, int32_t B, const uint8_
         DBuf<uint8_t> dg(N);
         dg.upload(gap, N, s);
         DBuf<double> dd(N);
-        hipLaunchKernelGGL(k_di, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, pb, (long long)N, B, dg.p, dw.p,
-                           test, dd.p);
+        hipLaunchKernelGGL(k_di, dim3((unsigned)((N * kDiLanes + 255) / 256)), dim3(256), 0, s, pb, (long long)N, B,
+                           dg.p, dw.p, test, dd.p);
         HIP_CHECK(hipGetLastError());
         dd.download(di, N, s);
         HIP_CHECK(hipStreamSynchronize(s));

@@ -13,8 +13,11 @@
 //      three passes over symmetric 64x64 tile pairs (each element read once
 //      per pass): rowsum(Y) -> sum(C) -> write out.  Partial sums go to slabs
 //      reduced in a fixed order (bitwise deterministic, no float atomics).
+#include <algorithm>
 #include <cmath>
+#include <limits>
 #include <type_traits>
+#include <vector>
 
 #include "hh_common.hpp"
 
@@ -70,106 +73,147 @@ struct SymArgs {
     double scale;         // pass 3: mean(X) / mean(C)
 };
 
-// Loads S tile (I,J) and the transposed S tile (J,I) into LDS as tile[r][c]
-// (row r of I, column c of J) and tileT[r][c] = S[J0+c][I0+r].
+// Per-tile vectors staged once in LDS: alpha, gap flag and s for the 64
+// rows of I and of J (sentinel values past N).
+struct TileVecs {
+    double aI[kT], aJ[kT], sI[kT], sJ[kT];
+    uint8_t gI[kT], gJ[kT];
+};
+
+// Loads S tile (I,J) as st[r][c] = S[I0+r][J0+c] and the transposed tile as
+// stT[r][c] = S[J0+c][I0+r]; a wave reads one 512-B row per instruction.
 template <class T>
-__device__ __forceinline__ void load_pair(const T* __restrict__ X, const SymArgs& a, long long I0, long long J0,
-                                          double (*st)[kT + 1], double (*stT)[kT + 1]) {
-    for (int e = threadIdx.x; e < kT * kT; e += 256) {
-        const int r = e / kT, c = e % kT;
-        const long long gi = I0 + r, gj = J0 + c;
-        double v = 0.0, w = 0.0;
-        if (gi < a.N && gj < a.N) v = (double)X[gi * a.N + gj] / a.alpha[gi];
-        // transposed: read row J0+r, column I0+c  -> S[J0+r][I0+c], store at stT[c][r]
-        const long long ti = J0 + r, tj = I0 + c;
-        if (ti < a.N && tj < a.N) w = (double)X[ti * a.N + tj] / a.alpha[ti];
-        st[r][c] = v;
-        stT[c][r] = w;
+__device__ __forceinline__ void load_pair(const T* __restrict__ X, long long N, long long I0, long long J0,
+                                          const TileVecs& tv, double (*st)[kT + 1], double (*stT)[kT + 1]) {
+    const int c = threadIdx.x & (kT - 1), r0 = threadIdx.x >> 6;
+    // all 32 loads issued before the first use (memory-level parallelism:
+    // only 2 blocks fit a CU with 66 KB of LDS each)
+    T v[kT / 4], w[kT / 4];
+#pragma unroll
+    for (int k = 0; k < kT / 4; ++k) {
+        const int r = r0 + 4 * k;
+        const long long gi = I0 + r, gj = J0 + c, ti = J0 + r, tj = I0 + c;
+        // unconditional loads from clamped addresses (a guarded load becomes
+        // a branch with its own vmcnt(0) wait)
+        const bool okv = gi < N && gj < N, okw = ti < N && tj < N;
+        const T xv = X[okv ? gi * N + gj : 0], xw = X[okw ? ti * N + tj : 0];
+        v[k] = okv ? xv : T(0);
+        w[k] = okw ? xw : T(0);
+    }
+#pragma unroll
+    for (int k = 0; k < kT / 4; ++k) {
+        const int r = r0 + 4 * k;
+        st[r][c] = (double)v[k] / tv.aI[r];  // S = X / alpha[:, None] (true division)
+        stT[c][r] = (double)w[k] / tv.aJ[r];
     }
 }
 
-__device__ __forceinline__ double sym_value(const SymArgs& a, long long gi, long long gj, double sij, double sji) {
-    if (gi == gj) return sij;
-    if (!a.gap) return sij + sji;
-    if (a.gap[gi] && a.gap[gj]) return sij > sji ? sij : sji;  // np.maximum-like on non-NaN
+// Trans2symmetry element (i != j); d: on the diagonal
+__device__ __forceinline__ double sym_value(bool d, bool has_gap, bool gi, bool gj, double sij, double sji) {
+    if (d) return sij;
+    if (!has_gap) return sij + sji;
+    if (gi && gj) return sij > sji ? sij : sji;  // np.maximum-like on non-NaN
     return (sij + sji) / 2.0;
 }
 
 // PASS 1: partial row sums of Y.  part[pair][0..63] rows of I, [64..127] rows of J.
 // PASS 2: partial sum of C over tile (I,J) (+ mirrored (J,I) when I != J).
 // PASS 3: write out = scale * C for tiles (I,J) and (J,I).
+// Thread t: row r = t >> 2 and columns c = q + 4k (q = t & 3) for the
+// per-row work of passes 1-2; passes 1's column sums use the same split
+// transposed; pass 3 writes whole rows per wave.
 template <class T, int PASS>
 __global__ __launch_bounds__(256) void k_symvc(const T* __restrict__ X, SymArgs a, double* __restrict__ part,
                                                double* __restrict__ out) {
     __shared__ double st[kT][kT + 1];
     __shared__ double stT[kT][kT + 1];
-    __shared__ double red[kT * 2];
+    __shared__ TileVecs tv;
     __shared__ double sh[16];
-    // decode pair index -> (I, J)
     const long long p = blockIdx.x;
     long long I = 0, rem = p;
     while (rem >= a.nT - I) { rem -= a.nT - I; ++I; }
     const long long J = I + rem;
-    const long long I0 = I * kT, J0 = J * kT;
-    load_pair(X, a, I0, J0, st, stT);
+    const long long I0 = I * kT, J0 = J * kT, N = a.N;
+    const bool has_gap = a.gap != nullptr;
+    if (threadIdx.x < kT) {
+        const int r = threadIdx.x;
+        const long long gi = I0 + r, gj = J0 + r;
+        tv.aI[r] = gi < N ? a.alpha[gi] : 1.0;
+        tv.aJ[r] = gj < N ? a.alpha[gj] : 1.0;
+        tv.gI[r] = (has_gap && gi < N) ? a.gap[gi] : 0;
+        tv.gJ[r] = (has_gap && gj < N) ? a.gap[gj] : 0;
+        if (PASS > 1) {
+            tv.sI[r] = gi < N ? a.s[gi] : 1.0;
+            tv.sJ[r] = gj < N ? a.s[gj] : 1.0;
+        }
+    }
     __syncthreads();
+    load_pair(X, N, I0, J0, tv, st, stT);
+    __syncthreads();
+    const bool diag_tile = I == J;
+    const int lim_r = (int)std::min<long long>(kT, N - I0), lim_c = (int)std::min<long long>(kT, N - J0);
     if (PASS == 1) {
-        // thread t < 64: row sum of tile row t (over J); t in [64,128): column sum (rows of J)
-        const int t = threadIdx.x;
-        if (t < 2 * kT) {
-            double acc = 0.0;
-            if (t < kT) {
-                const long long gi = I0 + t;
-                for (int c = 0; c < kT; ++c) {
-                    const long long gj = J0 + c;
-                    if (gi < a.N && gj < a.N) acc += sym_value(a, gi, gj, st[t][c], stT[t][c]);
-                }
-            } else {
-                const int c = t - kT;
-                const long long gj = J0 + c;
-                for (int r = 0; r < kT; ++r) {
-                    const long long gi = I0 + r;
-                    if (gi < a.N && gj < a.N) acc += sym_value(a, gi, gj, st[r][c], stT[r][c]);
-                }
+        const int r = threadIdx.x >> 2, q = threadIdx.x & 3;
+        // row sum of I-row r over J columns
+        double acc = 0.0;
+        if (r < lim_r)
+#pragma unroll 4
+            for (int k = 0; k < kT / 4; ++k) {
+                const int c = q + 4 * k;
+                if (c < lim_c) acc += sym_value(diag_tile && r == c, has_gap, tv.gI[r], tv.gJ[c], st[r][c], stT[r][c]);
             }
-            part[p * (2 * kT) + t] = acc;
+        acc += __shfl_xor(acc, 1, 64);
+        acc += __shfl_xor(acc, 2, 64);
+        // column sum of J-column r (= row J0+r of Y) over I rows
+        double acc2 = 0.0;
+        if (r < lim_c)
+#pragma unroll 4
+            for (int k = 0; k < kT / 4; ++k) {
+                const int i = q + 4 * k;
+                if (i < lim_r)
+                    acc2 += sym_value(diag_tile && i == r, has_gap, tv.gI[i], tv.gJ[r], st[i][r], stT[i][r]);
+            }
+        acc2 += __shfl_xor(acc2, 1, 64);
+        acc2 += __shfl_xor(acc2, 2, 64);
+        if (q == 0) {
+            part[p * (2 * kT) + r] = acc;
+            part[p * (2 * kT) + kT + r] = acc2;
         }
     } else if (PASS == 2) {
+        const int r = threadIdx.x >> 2, q = threadIdx.x & 3;
         double acc = 0.0;
-        for (int e = threadIdx.x; e < kT * kT; e += 256) {
-            const int r = e / kT, c = e % kT;
-            const long long gi = I0 + r, gj = J0 + c;
-            if (gi < a.N && gj < a.N) {
-                const double y = sym_value(a, gi, gj, st[r][c], stT[r][c]);
-                const double v = y / (a.s[gj] * a.s[gi]);
-                acc += (I == J) ? v : 2.0 * v;
+        if (r < lim_r) {
+            const double si = tv.sI[r];
+#pragma unroll 4
+            for (int k = 0; k < kT / 4; ++k) {
+                const int c = q + 4 * k;
+                if (c < lim_c) {
+                    const double y = sym_value(diag_tile && r == c, has_gap, tv.gI[r], tv.gJ[c], st[r][c], stT[r][c]);
+                    acc += y / (tv.sJ[c] * si);
+                }
             }
         }
+        if (!diag_tile) acc *= 2.0;
         acc = block_sum(acc, sh);
         if (threadIdx.x == 0) part[p] = acc;
     } else {
-        // out[gi][gj] and out[gj][gi]
-        for (int e = threadIdx.x; e < kT * kT; e += 256) {
-            const int r = e / kT, c = e % kT;
-            const long long gi = I0 + r, gj = J0 + c;
-            if (gi < a.N && gj < a.N) {
-                const double y = sym_value(a, gi, gj, st[r][c], stT[r][c]);
-                out[gi * a.N + gj] = a.scale * (y / (a.s[gj] * a.s[gi]));
+        const int c = threadIdx.x & (kT - 1);
+        for (int r = threadIdx.x >> 6; r < lim_r; r += 4) {
+            if (c < lim_c) {
+                const double y = sym_value(diag_tile && r == c, has_gap, tv.gI[r], tv.gJ[c], st[r][c], stT[r][c]);
+                __builtin_nontemporal_store(a.scale * (y / (tv.sJ[c] * tv.sI[r])), &out[(I0 + r) * N + J0 + c]);
             }
         }
-        if (I != J) {
-            for (int e = threadIdx.x; e < kT * kT; e += 256) {
-                const int r = e / kT, c = e % kT;  // element (J0 + r, I0 + c)
-                const long long gi = J0 + r, gj = I0 + c;
-                if (gi < a.N && gj < a.N) {
-                    // Y[gi][gj] = Y[gj][gi] (symmetric): from tile (I,J) at [c][r]
-                    const double y = sym_value(a, gj, gi, st[c][r], stT[c][r]);
-                    out[gi * a.N + gj] = a.scale * (y / (a.s[gj] * a.s[gi]));
+        if (!diag_tile) {
+            // element (J0 + r, I0 + c) = Y[I0 + c][J0 + r] (Y symmetric)
+            for (int r = threadIdx.x >> 6; r < lim_c; r += 4) {
+                if (c < lim_r) {
+                    const double y = sym_value(false, has_gap, tv.gI[c], tv.gJ[r], st[c][r], stT[c][r]);
+                    __builtin_nontemporal_store(a.scale * (y / (tv.sI[c] * tv.sJ[r])), &out[(J0 + r) * N + I0 + c]);
                 }
             }
         }
     }
-    (void)red;
 }
 
 // rowsum(Y)_i from the pass-1 slab in a fixed order (J = 0 .. nT-1), then
@@ -225,9 +269,42 @@ static void symvc_run(const T* dX, long long N, const double* dalpha, const uint
     HIP_CHECK(hipStreamSynchronize(s));
 }
 
+// np.percentile(v, pct) with the default 'linear' method (NumPy 2.x:
+// virtual index (n-1)*q, floor/next clipped to the ends, _lerp's two-sided
+// form), so host-side gap and alpha decisions are bit-identical to the
+// reference's NumPy calls.
+static double np_percentile(std::vector<double> v, double pct) {
+    HH_REQUIRE(!v.empty(), "percentile of an empty array");
+    std::sort(v.begin(), v.end());
+    const long long n = (long long)v.size();
+    const double q = pct / 100.0;
+    const double vi = (double)(n - 1) * q;
+    long long prev = (long long)std::floor(vi), next = prev + 1;
+    if (vi >= (double)(n - 1)) prev = next = n - 1;
+    if (vi < 0) prev = next = 0;
+    const double gamma = vi - (vi >= (double)(n - 1) ? -1.0 : (double)prev);
+    const double a = v[prev], b = v[next], d = b - a;
+    return gamma >= 0.5 ? b - d * (1.0 - gamma) : a + d * gamma;
+}
+
+// Gap_defined (:915-929) from zero counts: cov = 1 - zeros / N
+static std::vector<uint8_t> gap_defined(const std::vector<long long>& zeros, long long N) {
+    std::vector<double> cov(N), nz;
+    for (long long i = 0; i < N; ++i) {
+        cov[i] = 1.0 - ((double)zeros[i] / (double)N);
+        if (cov[i] != 0.0) nz.push_back(cov[i]);
+    }
+    double th = np_percentile(nz, 25.0);
+    if (th > 0.2) th = 0.2;
+    std::vector<uint8_t> g(N);
+    for (long long i = 0; i < N; ++i) g[i] = cov[i] < th;
+    return g;
+}
+
 }  // namespace hh
 
 using namespace hh;
+
 
 extern "C" {
 
@@ -296,6 +373,80 @@ int hh_dense_symvc(const void* X, int32_t dtype, int64_t N, const double* alpha,
             HIP_CHECK(hipMemcpyAsync(out, po, bytes, hipMemcpyDeviceToHost, s));
             HIP_CHECK(hipStreamSynchronize(s));
         }
+    });
+}
+
+// TwoStepCorrection (matrixBuilding.py:984-1023) in one call: each matrix
+// crosses PCIe once; gap / alpha glue on the host with NumPy semantics.
+int hh_twostep(const int64_t* TM, const int64_t* MM, const int64_t* PM, int64_t N, double* nor_mm, double* nor_pm,
+               uint8_t* gap_m, uint8_t* gap_p, int32_t on_device, void* stream) {
+    return guard([&] {
+        HH_REQUIRE(TM && MM && PM && nor_mm && nor_pm && gap_m && gap_p && N > 0, "bad arguments");
+        hipStream_t s = as_stream(stream);
+        const size_t cnt = (size_t)N * N;
+        const long long* src[3] = {(const long long*)TM, (const long long*)MM, (const long long*)PM};
+        DBuf<long long> buf[3];
+        const long long* d[3];
+        for (int k = 0; k < 3; ++k) {
+            if (on_device) {
+                d[k] = src[k];
+            } else {
+                buf[k].alloc(cnt);
+                buf[k].upload(src[k], cnt, s);
+                d[k] = buf[k].p;
+            }
+        }
+        // row sums (exact) and zero counts
+        DBuf<double> dsum((size_t)3 * N);
+        DBuf<long long> dz((size_t)3 * N);
+        for (int k = 0; k < 3; ++k)
+            hipLaunchKernelGGL((k_rowstats<long long>), dim3((unsigned)N), dim3(256), 0, s, d[k], (long long)N,
+                               (const long long*)nullptr, (const long long*)nullptr, dsum.p + k * N, dz.p + k * N);
+        HIP_CHECK(hipGetLastError());
+        std::vector<double> sum((size_t)3 * N);
+        std::vector<long long> zeros((size_t)3 * N);
+        dsum.download(sum.data(), sum.size(), s);
+        dz.download(zeros.data(), zeros.size(), s);
+        HIP_CHECK(hipStreamSynchronize(s));
+        const std::vector<long long> zm(zeros.begin() + N, zeros.begin() + 2 * N), zp(zeros.begin() + 2 * N, zeros.end());
+        const std::vector<uint8_t> gm = gap_defined(zm, N), gp = gap_defined(zp, N);
+        // alpha over the union of non-gap bins (:994-1005)
+        std::vector<double> alpha(N), ng;
+        for (long long i = 0; i < N; ++i) alpha[i] = (sum[N + i] + sum[2 * N + i]) / (sum[i] + 1.0);
+        double mx = -std::numeric_limits<double>::infinity();
+        for (long long i = 0; i < N; ++i)
+            if (!gm[i] || !gp[i]) mx = std::max(mx, alpha[i]);
+        HH_REQUIRE(mx > -std::numeric_limits<double>::infinity(), "every bin is a gap");
+        for (long long i = 0; i < N; ++i) {
+            alpha[i] /= mx;
+            if (alpha[i] == 0.0) alpha[i] = 1.0;
+        }
+        for (long long i = 0; i < N; ++i)
+            if (!gm[i] || !gp[i]) ng.push_back(alpha[i]);
+        const double th = np_percentile(ng, 20.0);
+        for (long long i = 0; i < N; ++i)
+            if (alpha[i] < th) alpha[i] = th;
+        DBuf<double> dA = to_device(alpha, s);
+        bool any_m = false, any_p = false;
+        for (long long i = 0; i < N; ++i) { any_m |= gm[i] != 0; any_p |= gp[i] != 0; }
+        DBuf<uint8_t> dgm = to_device(gm, s), dgp = to_device(gp, s);
+        // exact integer totals (MM.mean() * N^2)
+        double raw[2];
+        for (int k = 0; k < 2; ++k) {
+            long long t = 0;  // row sums are exact integers
+            for (long long i = 0; i < N; ++i) t += (long long)sum[(k + 1) * N + i];
+            raw[k] = (double)t;
+        }
+        // outputs: on the host path TM's buffer holds Nor_MM, then MM's holds Nor_PM
+        double* out_m = on_device ? nor_mm : (double*)buf[0].p;
+        symvc_run(d[1], N, dA.p, any_m ? dgm.p : nullptr, 2.0 / 3.0, raw[0], out_m, s);
+        if (!on_device) HIP_CHECK(hipMemcpyAsync(nor_mm, out_m, cnt * 8, hipMemcpyDeviceToHost, s));
+        double* out_p = on_device ? nor_pm : (double*)buf[1].p;
+        symvc_run(d[2], N, dA.p, any_p ? dgp.p : nullptr, 2.0 / 3.0, raw[1], out_p, s);
+        if (!on_device) HIP_CHECK(hipMemcpyAsync(nor_pm, out_p, cnt * 8, hipMemcpyDeviceToHost, s));
+        HIP_CHECK(hipStreamSynchronize(s));
+        std::copy(gm.begin(), gm.end(), gap_m);
+        std::copy(gp.begin(), gp.end(), gap_p);
     });
 }
 

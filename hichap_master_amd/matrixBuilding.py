@@ -98,18 +98,22 @@ def _snp_alpha(m_sum, p_sum, t_sum, non_gap):
 # ------------------------------------------------------------------- API
 def TwoStepCorrection(TM, MM, PM):
     """Two-step correction of one chromosome's maternal / paternal matrices
-    (matrixBuilding.py:984-1023).  Returns (Nor_MM, Nor_PM, Gap_M, Gap_P)."""
-    N = np.asarray(TM).shape[0]
-    t_sum, _ = row_stats(TM)
-    m_sum, m_zero = row_stats(MM)
-    p_sum, p_zero = row_stats(PM)
-    Gap_M = _gap_from_coverage(_coverage(m_zero, N))
-    Gap_P = _gap_from_coverage(_coverage(p_zero, N))
-    non_gap = np.union1d(_non_gap(N, Gap_M), _non_gap(N, Gap_P))
-    alpha = _snp_alpha(m_sum, p_sum, t_sum, non_gap)
-    Nor_MM = sym_vc_rescale(MM, alpha, Gap_M if Gap_M.size else None, m_sum.sum())
-    Nor_PM = sym_vc_rescale(PM, alpha, Gap_P if Gap_P.size else None, p_sum.sum())
-    return Nor_MM, Nor_PM, Gap_M, Gap_P
+    (matrixBuilding.py:984-1023).  Returns (Nor_MM, Nor_PM, Gap_M, Gap_P).
+
+    One C-ABI call (``hh_twostep``): each matrix is uploaded once, the gap /
+    alpha glue runs in C++ with np.percentile semantics."""
+    _lib.require_gpu()
+    mats = [np.ascontiguousarray(X, dtype=np.int64) for X in (TM, MM, PM)]
+    N = mats[0].shape[0]
+    if any(X.ndim != 2 or X.shape != (N, N) for X in mats):
+        raise ValueError("TM, MM, PM must be square matrices of the same size")
+    Nor_MM = np.empty((N, N), np.float64)
+    Nor_PM = np.empty((N, N), np.float64)
+    gm = np.empty(N, np.uint8)
+    gp = np.empty(N, np.uint8)
+    call("hh_twostep", ptr(mats[0]), ptr(mats[1]), ptr(mats[2]), N, ptr(Nor_MM), ptr(Nor_PM), ptr(gm), ptr(gp), 0,
+         None)
+    return Nor_MM, Nor_PM, np.nonzero(gm)[0].astype(np.int64), np.nonzero(gp)[0].astype(np.int64)
 
 
 def IntraChromMatrixCorrection(Tra_Lib, Hap_Lib):

@@ -191,6 +191,12 @@ int hh_dense_rowstats(const void* X, int32_t dtype, int64_t N, const int64_t* lo
  * TwoStepCorrection :1007-1021, GenomeWideMatrixCorrection :894-899. */
 int hh_dense_symvc(const void* X, int32_t dtype, int64_t N, const double* alpha, const uint8_t* gap,
                    double exponent, double raw_sum, double* out, int32_t on_device, void* stream);
+/* TwoStepCorrection(TM, MM, PM) (matrixBuilding.py:984-1023) in one call:
+ * int64 N x N inputs, float64 N x N outputs (Nor_MM, Nor_PM), gap masks
+ * (gap_m[i] = 1 for i in Gap_M).  The gap / alpha glue runs on the host with
+ * np.percentile ('linear') semantics; each matrix crosses PCIe once. */
+int hh_twostep(const int64_t* TM, const int64_t* MM, const int64_t* PM, int64_t N, double* nor_mm, double* nor_pm,
+               uint8_t* gap_m, uint8_t* gap_p, int32_t on_device, void* stream);
 
 /* ---------------------------------------------------- compartment (one chrom)
  * StructureFind.Distance_Decay / Get_PCA / Select_PC_new, StructureFind.py:201-423.
@@ -221,8 +227,8 @@ int hh_comp_select_stats(hh_comp* c, const double* pcs, int32_t k, double eps, d
 
 /* ------------------------------------------------------- TAD scan (DI)
  * Both scans read column j only within B rows of the diagonal, so the matrix
- * is passed as a band: band[j * (2B+1) + B + k] = M[j + k][j], k in [-B, B]
- * (0 outside the matrix); M balanced with NaN -> 0 for traditional data.
+ * is passed as a diagonal-major band: band[(B + k) * N + j] = M[j + k][j],
+ * k in [-B, B] (0 outside the matrix); M balanced with NaN -> 0 for traditional data.
  * hh_gap_scan = StructureFind.Get_Gap (:721-751): gap[j] = 1 when column j
  * has fewer than 2*lb*0.8 nonzeros in M[j-lb:j+lb, j] or is within lb of an
  * edge (lb <= B).  hh_di_scan = Get_DI (:804-839): di[j] from the up / down

@@ -12,13 +12,13 @@ def test_sort_chromosomes(names):
 
 @pytest.mark.parametrize("N,B", [(1, 0), (5, 2), (5, 7), (40, 9)])
 def test_column_band_layout(N, B):
-    """band[j, B + k] = M[j + k, j] (0 outside): what hh_gap_scan / hh_di_scan read."""
+    """band[B + k, j] = M[j + k, j] (0 outside): what hh_gap_scan / hh_di_scan read."""
     import numpy as np
     from hichap_master_amd.StructureFind import column_band
     M = np.random.default_rng(N).random((N, N))
     band = column_band(M, B)
-    assert band.shape == (N, 2 * B + 1)
+    assert band.shape == (2 * B + 1, N)
     for j in range(N):
         for k in range(-B, B + 1):
             want = M[j + k, j] if 0 <= j + k < N else 0.0
-            assert band[j, B + k] == want
+            assert band[B + k, j] == want
