@@ -12,7 +12,14 @@ ranks (one process per GPU), one all-gather of the marginal per iteration
 over RCCL; total work fixed (strong scaling).  value = iterations/s of the
 whole job; nnz_iters_per_s = pixels x iterations / s.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c4|c2]
+--config c5: the per-chromosome compartment path (configs[4]): hg19
+autosomes at 25 kb as dense N x N float64 matrices generated in HBM, one
+step = Distance_Decay + Get_PCA (O/E, Pearson on fp64 MFMA, top-3 PCA) +
+Select_PC_new for all 22 autosomes; chromosomes dealt to ranks by LPT on N^3
+(no collective); value = chromosomes/s of the whole job; roofline on k_syrk
+(MFMA, fp64).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c4|c2|c5]
 """
 from __future__ import annotations
 
@@ -28,6 +35,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 PEAK_HBM_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
+PEAK_F64_MFMA_TFS = 78.6  # MI355X fp64 matrix spec (AMD datasheet; the guide has no fp64 row)
 ALG_BYTES_PER_PIXEL = 12.0  # int32 bin1 + int32 bin2 + fp32 count
 
 
@@ -88,6 +96,143 @@ def cpu_baseline(sizes, kw, rc, nnz_total, budget_s=12.0):
             "pixel_iters_per_s": pix_rate}
 
 
+C5_RES = 25000
+C5_STREAMS = int(os.environ.get("HH_C5_STREAMS", "4"))
+
+
+def c5_sizes():
+    from hichap_master_amd import synth
+    return synth.chrom_bins([synth.HG19[str(c)] for c in range(1, 23)], C5_RES)
+
+
+def c5_cpu_baseline(budget_chrom=20, seed=20201019):
+    """Oracle compartment (NumPy corrcoef + exact SVD, numpy's BLAS threads)
+    on the smallest autosome (chr21, hg19 25 kb) of the same synthetic model;
+    extrapolated to the 22 autosomes by sum(N^3) / N_sample^3."""
+    import torch
+    from hichap_master_amd import ice
+    from oracle import structure_ref
+    sizes = c5_sizes()
+    k = budget_chrom
+    Nk = sizes[k]
+    buf = torch.empty((Nk, Nk), dtype=torch.float64, device="cuda")
+    ice.synth_dense(sizes, k, buf.data_ptr(), **c5_synth_kw())
+    M = buf.cpu().numpy()
+    t0 = time.perf_counter()
+    structure_ref.compartment(M)
+    dt = time.perf_counter() - t0
+    cube = float(np.sum(np.asarray(sizes, dtype=float) ** 3))
+    total = dt * cube / float(Nk) ** 3
+    try:
+        from threadpoolctl import threadpool_info
+        threads = max([p.get("num_threads", 1) for p in threadpool_info() if p.get("user_api") == "blas"] or [1])
+    except Exception:
+        threads = int(os.environ.get("OMP_NUM_THREADS", "1"))
+    return {"value": len(sizes) / total, "unit": "chromosomes/s (22 hg19 autosomes at 25 kb, extrapolated)",
+            "cores": threads, "kind": "port",
+            "sample": f"oracle/structure_ref.compartment on chr21 (N={Nk}) of the same synthetic model: "
+                      f"{dt:.2f}s; x sum(N^3)/N^3 = {total:.1f}s for the autosome set "
+                      f"(numpy BLAS with {threads} threads)"}
+
+
+def c5_synth_kw():
+    return dict(A=120.0, trans_density=0.0, comp_block=80, ignore_diags=0, cis_only=True, gap_frac=0.02,
+                seed=20201019)
+
+
+def run_c5(args, world, rank, local):
+    import torch
+    from hichap_master_amd import _lib, dist, ice
+    from hichap_master_amd.StructureFind import StructureFind
+    sizes = c5_sizes()
+    keys = list(range(len(sizes)))
+    owner = dist.lpt_assign(np.asarray(sizes, dtype=float) ** 3, world)
+    mine = [k for k in keys if owner[k] == rank]
+    t0 = time.perf_counter()
+    mats = {}
+    for k in mine:
+        mats[k] = torch.empty((sizes[k], sizes[k]), dtype=torch.float64, device="cuda")
+        ice.synth_dense(sizes, k, mats[k].data_ptr(), **c5_synth_kw())
+    torch.cuda.synchronize()
+    gen_s = time.perf_counter() - t0
+    ng = {}
+    # chromosomes run concurrently on C5_STREAMS HIP streams (one host thread
+    # each; the C-ABI releases the GIL): the small chromosomes' PCA kernels are
+    # latency-bound, so overlapping them keeps the GPU busy.
+    from concurrent.futures import ThreadPoolExecutor
+    streams = [torch.cuda.Stream(device=local) for _ in range(C5_STREAMS)]
+    pool = ThreadPoolExecutor(max_workers=C5_STREAMS)
+
+    def one(k, st):
+        torch.cuda.set_device(local)  # the HIP current device is per host thread
+        _lib.call("hh_set_device", local)
+        with torch.cuda.stream(st):
+            sf = StructureFind(Res=C5_RES, stream=st.cuda_stream)
+            dec, G, NG = sf.Distance_Decay(M=mats[k], G_array=None)
+            pcs, Cor, OE = sf.Get_PCA(distance_bin=dec, M=mats[k], NG_array=NG)
+            sf.Select_PC_new(Cor, OE[NG], pcs)
+            ng[k] = NG.size
+
+    def step(nstreams=C5_STREAMS):
+        # largest first, dealt round-robin to the stream workers
+        order = sorted(mine, key=lambda k: -sizes[k])
+        lanes = [order[i::nstreams] for i in range(nstreams)]
+        futs = [pool.submit(lambda ks, st: [one(k, st) for k in ks], ks, st) for ks, st in zip(lanes, streams)]
+        for f in futs:
+            f.result()
+
+    def barrier():
+        if torch.distributed.is_initialized():
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier()
+    elapsed = time.perf_counter() - t_start
+    # per-kernel durations from one more pass with the streams serialised
+    # (concurrent streams share the CUs, so their event spans overlap)
+    _lib.call("hh_ktime_reset")
+    _lib.call("hh_ktime_enable", 1)
+    step(1)
+    torch.cuda.synchronize()
+    _lib.call("hh_ktime_enable", 0)
+    syrk_ms, syrk_n = _lib.ktime("k_syrk")
+    mul_ms, mul_n = _lib.ktime("k_cor_mul")
+    tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    if torch.distributed.is_initialized():
+        torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
+    elapsed = float(tt.item())
+    if rank == 0:
+        flops = sum(float(sizes[k]) * ng[k] * (ng[k] + 1) for k in mine)  # one (serialised) pass
+        achieved = flops / (syrk_ms / 1000.0) / 1e12 if syrk_ms > 0 else None
+        out = {
+            "metric": "compartment PCA chromosomes/sec (C5: hg19 autosomes at 25 kb, dense per-chrom)",
+            "value": len(sizes) * args.steps / elapsed, "unit": "chromosomes/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1000.0 * elapsed / args.steps,
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic dense per-chrom matrices generated in HBM (SURVEY.md §8(d) model)",
+            "config": {"workload": "hg19-autosomes-25kb-compartment", "n_chroms": len(sizes),
+                       "bins_total": int(np.sum(sizes)), "largest_N": int(max(sizes)),
+                       "parallelism": f"chromosomes LPT over {world} ranks" if world > 1 else "single GPU",
+                       "generate_s": round(gen_s, 2)},
+            "roofline": {"bound": "mfma", "kernel": "k_syrk", "achieved": achieved,
+                         "peak": PEAK_F64_MFMA_TFS, "unit": "TFLOP/s",
+                         "frac": (achieved / PEAK_F64_MFMA_TFS) if achieved else None, "traffic": None,
+                         "flops_per_step_rank0": flops,
+                         "kernel_timing": "HIP events (hh_ktime) over one extra serialised pass after the timed steps",
+                         "syrk_launches": syrk_n, "syrk_ms_avg": syrk_ms / max(syrk_n, 1),
+                         "cor_mul_launches": mul_n, "cor_mul_ms_avg": mul_ms / max(mul_n, 1)},
+        }
+        if world == 1 and not args.no_cpu:
+            out["cpu_baseline"] = c5_cpu_baseline()
+        print(json.dumps(out), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -114,6 +259,11 @@ def main():
             os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT="29531", RANK="0", WORLD_SIZE="1")
         tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
+    if args.config == "c5":
+        run_c5(args, world, rank, local)
+        if torch.distributed.is_initialized():
+            torch.distributed.destroy_process_group()
+        return
     sizes, kw, label, target, tf = config(args.config, args.nnz)
     n = int(np.sum(sizes))
     t0 = time.perf_counter()

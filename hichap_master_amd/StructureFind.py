@@ -32,38 +32,59 @@ PCA_MAX_ITERS = 2000
 class _Comp:
     """Owns an ``hh_comp*`` (one chromosome's matrix in HBM)."""
 
-    def __init__(self, M):
+    def __init__(self, M, stream=None):
         _lib.require_gpu()
-        self.M = np.ascontiguousarray(M, dtype=np.float64)
-        if self.M.ndim != 2 or self.M.shape[0] != self.M.shape[1]:
-            raise ValueError("expected a square matrix")
-        self.N = self.M.shape[0]
+        self.stream = stream  # HIP stream handle (int / c_void_p) or None = default
+        self._dev = None
+        self._host = None
+        if getattr(M, "is_cuda", False):  # a device-resident torch tensor: no copy
+            import torch
+            if M.dtype != torch.float64 or M.dim() != 2 or M.shape[0] != M.shape[1] or not M.is_contiguous():
+                raise ValueError("expected a contiguous square float64 device tensor")
+            self._dev = M
+            self.N = int(M.shape[0])
+            src, on_dev = C.c_void_p(M.data_ptr()), 1
+        else:
+            self._host = np.ascontiguousarray(M, dtype=np.float64)
+            if self._host.ndim != 2 or self._host.shape[0] != self._host.shape[1]:
+                raise ValueError("expected a square matrix")
+            self.N = self._host.shape[0]
+            src, on_dev = ptr(self._host), 0
         h = C.c_void_p()
-        call("hh_comp_create", ptr(self.M), self.N, 0, None, C.byref(h))
+        call("hh_comp_create", src, self.N, on_dev, self._s(), C.byref(h))
         self.h = h
         self.decline = None
         self.NG = None
 
+    def _s(self):
+        return None if self.stream is None else C.c_void_p(int(self.stream))
+
+    @property
+    def M(self):
+        if self._host is None:
+            self._host = self._dev.cpu().numpy()
+        return self._host
+
     def colnnz(self):
         out = np.empty(self.N, np.int64)
-        call("hh_comp_colnnz", self.h, ptr(out), None)
+        call("hh_comp_colnnz", self.h, ptr(out), self._s())
         return out
 
     def diag_sums(self, gap_mask):
         g = np.ascontiguousarray(gap_mask, dtype=np.uint8)
         out = np.empty(self.N, np.float64)
-        call("hh_comp_diag_sums", self.h, ptr(g), ptr(out), None)
+        call("hh_comp_diag_sums", self.h, ptr(g), ptr(out), self._s())
         return out
 
     def correlation(self, decline, NG):
         self.decline = np.ascontiguousarray(decline, dtype=np.float64)
         self.NG = np.ascontiguousarray(NG, dtype=np.int64)
-        call("hh_comp_correlation", self.h, ptr(self.decline), ptr(self.NG), self.NG.size, None)
+        call("hh_comp_correlation", self.h, ptr(self.decline), ptr(self.NG), self.NG.size, self._s())
 
     def cor(self):
         n = self.NG.size
         out = np.empty((n, n), np.float64)
-        call("hh_comp_get_cor", self.h, ptr(out), None)
+        call("hh_comp_get_cor", self.h, ptr(out), self._s())
         return out
 
     def pca(self, k=3):
@@ -71,14 +92,14 @@ class _Comp:
         comps = np.empty((k, n), np.float64)
         ev = np.empty(k, np.float64)
         it = C.c_int32(0)
-        call("hh_comp_pca", self.h, int(k), PCA_TOL, PCA_MAX_ITERS, ptr(comps), ptr(ev), C.byref(it), None)
+        call("hh_comp_pca", self.h, int(k), PCA_TOL, PCA_MAX_ITERS, ptr(comps), ptr(ev), C.byref(it), self._s())
         return comps, ev, it.value
 
     def select_stats(self, pcs, eps=1e-5):
         p = np.ascontiguousarray(pcs, dtype=np.float64)
         k = p.shape[0]
         st = np.empty((k, 8), np.float64)
-        call("hh_comp_select_stats", self.h, ptr(p), int(k), float(eps), ptr(st), None)
+        call("hh_comp_select_stats", self.h, ptr(p), int(k), float(eps), ptr(st), self._s())
         return st
 
     def __del__(self):
@@ -133,7 +154,7 @@ class StructureFind(object):
     """Numeric part of HiCHap's StructureFind (StructureFind.py:27)."""
 
     def __init__(self, cooler_fil=None, Res=40000, Allelic=False, GapFile=None, Loop_ratio=0.6,
-                 Loop_strength=16):
+                 Loop_strength=16, stream=None):
         self.cooler_fil = "{}::{}".format(cooler_fil, Res) if cooler_fil else None
         self.Res = Res
         self.Allelic = Allelic
@@ -142,12 +163,13 @@ class StructureFind(object):
         self.LoopStrength = Loop_strength
         self._comp = None
         self._comp_src = None
+        self.stream = stream  # HIP stream for the device calls (None = default stream)
 
     # ------------------------------------------------------ compartments
     def Distance_Decay(self, M, G_array):
         """Distance-decay expected counts (StructureFind.py:201-271).
         Returns (distance_bin, G_array, NG_array)."""
-        comp = _Comp(M)
+        comp = _Comp(M, self.stream)
         self._comp, self._comp_src = comp, M
         size = comp.N
         bin_arange = np.arange(size)
@@ -180,7 +202,7 @@ class StructureFind(object):
             raise NotImplementedError("Sliding_Approach (SA=True) is not on the GPU path")
         comp = self._comp if (self._comp is not None and self._comp_src is M) else None
         if comp is None:
-            comp = _Comp(M)
+            comp = _Comp(M, self.stream)
             self._comp, self._comp_src = comp, M
         decline = distance_bin
         decline[decline == 0] = decline[np.nonzero(decline)].min()
@@ -219,7 +241,8 @@ class StructureFind(object):
     def compartment(self, M, Tranditional_PC=None):
         """Per-chromosome body of Compartment() (StructureFind.py:509-527):
         the selected PC at full length (zeros at gap bins)."""
-        M = np.asarray(M, dtype=np.float64)
+        if not getattr(M, "is_cuda", False):
+            M = np.asarray(M, dtype=np.float64)
         distance_bin, Gap, NonGap = self.Distance_Decay(M=M, G_array=None)
         pca, Cor_M, OE_M = self.Get_PCA(distance_bin=distance_bin, M=M, NG_array=NonGap)
         out = np.zeros((M.shape[0],), dtype=float)

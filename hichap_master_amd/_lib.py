@@ -59,12 +59,16 @@ SIGNATURES = {
     "hh_set_device": (C.c_int, [I32]),
     "hh_synchronize": (C.c_int, [P]),
     "hh_tune": (C.c_int, [C.c_char_p, I64]),
+    "hh_ktime_enable": (C.c_int, [I32]),
+    "hh_ktime_query": (C.c_int, [C.c_char_p, P, P]),
+    "hh_ktime_reset": (C.c_int, []),
     "hh_matrix_from_pixels": (C.c_int, [P, P, P, I64, I64, P, I32, I32, I32, I64, I64, P, C.POINTER(P)]),
     "hh_matrix_free": (C.c_int, [P]),
     "hh_matrix_get_info": (C.c_int, [P, C.POINTER(MatrixInfo)]),
     "hh_matrix_export_upper": (C.c_int, [P, P, P, P, PI64]),
     "hh_synth_count": (C.c_int, [C.POINTER(SynthParams), P, P, P]),
     "hh_synth_build": (C.c_int, [C.POINTER(SynthParams), I64, I64, P, C.POINTER(P)]),
+    "hh_synth_dense": (C.c_int, [P, I32, P, P]),
     "hh_ice_balance": (C.c_int, [P, C.POINTER(IceOpts), P, P, P, P, P, PF64, P]),
     "hh_ice_create": (C.c_int, [P, C.POINTER(IceOpts), C.POINTER(P)]),
     "hh_ice_free": (C.c_int, [P]),
@@ -141,6 +145,15 @@ def ptr(a):
     return a.ctypes.data_as(C.c_void_p)
 
 
+def ktime(name: str):
+    """(total_ms, calls) of one kernel name recorded since hh_ktime_reset
+    while hh_ktime_enable(1) was on (measurement only)."""
+    t = C.c_double(0.0)
+    n = C.c_int64(0)
+    call("hh_ktime_query", name.encode(), C.byref(t), C.byref(n))
+    return t.value, n.value
+
+
 def device_count() -> int:
     n = C.c_int32(0)
     try:
@@ -150,6 +163,15 @@ def device_count() -> int:
     return int(n.value)
 
 
+_have_gpu = False
+
+
 def require_gpu():
+    """Raise unless a HIP device is visible (cached once found: the runtime's
+    device query costs ~1 ms)."""
+    global _have_gpu
+    if _have_gpu:
+        return
     if device_count() < 1:
         raise HipLibraryError(-101, "no HIP device visible: the HIP path has no CPU fallback")
+    _have_gpu = True

@@ -468,6 +468,57 @@ struct hh_comp {
 namespace hh {
 
 // Small-matrix workspace of the subspace iteration (no allocation in the loop).
+// G = R^T R (R upper) -> Rinv = R^{-1}, on the device (one wave, LDS;
+// cheaper than a host round trip).  Not positive definite -> *fail = 1 and
+// Rinv = I (keeps the iterate finite until the host sees the flag).
+__global__ __launch_bounds__(64) void k_chol_inv(const double* __restrict__ G, double* __restrict__ Rinv,
+                                                 int* __restrict__ fail) {
+    __shared__ double R[kSB][kSB + 1];
+    __shared__ int bad;
+    const int t = threadIdx.x;
+    if (t == 0) bad = 0;
+    if (t < kSB)
+        for (int i = 0; i < kSB; ++i) R[i][t] = 0.0;
+    __syncthreads();
+    for (int j = 0; j < kSB; ++j) {
+        if (t == j) {
+            double d = G[j * kSB + j];
+            for (int k = 0; k < j; ++k) d -= R[k][j] * R[k][j];
+            if (d > 0) R[j][j] = sqrt(d);
+            else { R[j][j] = 1.0; bad = 1; }
+        }
+        __syncthreads();
+        if (t > j && t < kSB) {
+            double x = G[j * kSB + t];
+            for (int k = 0; k < j; ++k) x -= R[k][j] * R[k][t];
+            R[j][t] = x / R[j][j];
+        }
+        __syncthreads();
+    }
+    if (t >= kSB) return;
+    if (bad) {
+        if (t == 0) *fail = 1;
+        for (int i = 0; i < kSB; ++i) Rinv[i * kSB + t] = i == t ? 1.0 : 0.0;
+        return;
+    }
+    // column t of R^{-1} by back substitution
+    double col[kSB];
+#pragma unroll
+    for (int i = 0; i < kSB; ++i) col[i] = 0.0;
+#pragma unroll
+    for (int i = kSB - 1; i >= 0; --i) {
+        if (i > t) continue;
+        if (i == t) { col[i] = 1.0 / R[i][i]; continue; }
+        double x = 0.0;
+#pragma unroll
+        for (int k = 0; k < kSB; ++k)
+            if (k > i && k <= t) x += R[i][k] * col[k];
+        col[i] = -x / R[i][i];
+    }
+#pragma unroll
+    for (int i = 0; i < kSB; ++i) Rinv[i * kSB + t] = col[i];
+}
+
 struct PcaWork {
     long long n = 0, ldc = 0;
     int nblk = 0, ks = 1, ksteps = 1;
@@ -500,13 +551,28 @@ struct PcaWork {
     }
     // Y = Cor V - x d^T, d = row 0 of the last gram_dev (d_use) or none
     void cor_mul(const double* Cor, const double* V, const double* x, bool d_use, double* Y, hipStream_t s) {
-        hipLaunchKernelGGL(k_cor_mul_part, dim3((unsigned)(ldc / 64), (unsigned)ks), dim3(256), 0, s, Cor, ldc, n, V,
-                           ksteps, mpart.p);
+        {
+            HH_KTIME("k_cor_mul", s);
+            hipLaunchKernelGGL(k_cor_mul_part, dim3((unsigned)(ldc / 64), (unsigned)ks), dim3(256), 0, s, Cor, ldc, n, V,
+                               ksteps, mpart.p);
+        }
         hipLaunchKernelGGL(k_cor_mul_sum, dim3((unsigned)((n * kSB + 255) / 256)), dim3(256), 0, s, mpart.p, ks, ldc, n,
                            x, d_use ? (const double*)G.p : nullptr, Y);
     }
     void put_small(const std::vector<double>& m, hipStream_t s) { R.upload(m.data(), m.size(), s); }
 };
+
+// V <- V R^{-1} `passes` times (CholQR / CholQR2) without leaving the device; rank loss is
+// reported through *fail (checked at the next host synchronisation).
+static void orthonormalize_dev(PcaWork& w, DBuf<double>& V, DBuf<double>& tmp, long long n, int* fail,
+                               hipStream_t s, int passes = 2) {
+    for (int pass = 0; pass < passes; ++pass) {
+        w.gram_dev(V.p, V.p, s);
+        hipLaunchKernelGGL(k_chol_inv, dim3(1), dim3(64), 0, s, w.G.p, w.R.p, fail);
+        hipLaunchKernelGGL(k_rot, dim3((unsigned)((n * kSB + 255) / 256)), dim3(256), 0, s, V.p, w.R.p, n, tmp.p);
+        std::swap(V.p, tmp.p);
+    }
+}
 
 // V <- V R^{-1} twice (CholQR2); returns false if V lost rank.
 static bool orthonormalize(PcaWork& w, DBuf<double>& V, DBuf<double>& tmp, long long n, hipStream_t s) {
@@ -544,7 +610,10 @@ int hh_comp_create(const double* M, int64_t N, int32_t on_device, void* stream, 
 }
 
 int hh_comp_free(hh_comp* c) {
-    return guard([&] { delete c; });
+    return guard([&] {
+        if (c) device_quiesce(c->device);
+        delete c;
+    });
 }
 
 int hh_comp_colnnz(hh_comp* c, int64_t* nnz_col, void* stream) {
@@ -606,8 +675,11 @@ int hh_comp_correlation(hh_comp* c, const double* decline, const int64_t* ng, in
         // Cov = Z^T Z * (1 / (N - 1))  (np.cov: c *= true_divide(1, fact))
         DBuf<double> cov((size_t)c->ld * c->ld);
         const long long nt = c->ld / 64;
-        hipLaunchKernelGGL(k_syrk, dim3((unsigned)(nt * (nt + 1) / 2)), dim3(256), 0, s, Z.p, c->ld, Npad, nt,
-                           1.0 / (double)(N - 1), cov.p, c->ld);
+        {
+            HH_KTIME("k_syrk", s);
+            hipLaunchKernelGGL(k_syrk, dim3((unsigned)(nt * (nt + 1) / 2)), dim3(256), 0, s, Z.p, c->ld, Npad, nt,
+                               1.0 / (double)(N - 1), cov.p, c->ld);
+        }
         Z.release();
         c->cor.alloc((size_t)c->ld * c->ld);
         hipLaunchKernelGGL(k_corr_norm_oop, dim3((unsigned)((c->ld * c->ld + 255) / 256)), dim3(256), 0, s, cov.p,
@@ -647,7 +719,7 @@ int hh_comp_pca(hh_comp* c, int32_t k, double tol, int32_t max_iters, double* co
         PcaWork wk(n, c->ld);
         // mu and 1 as the first column of n x B blocks, so mu^T X and 1^T X are
         // row 0 of a Gram product; mu = column means of Cor = (Cor 1) / n.
-        DBuf<double> mu(n), mupad, onepad;
+        DBuf<double> mu(n), mupad, onepad, nmu;
         {
             std::vector<double> op((size_t)n * kSB, 0.0), muh(n), mp((size_t)n * kSB, 0.0);
             for (long long i = 0; i < n; ++i) op[i * kSB] = 1.0;
@@ -657,9 +729,15 @@ int hh_comp_pca(hh_comp* c, int32_t k, double tol, int32_t max_iters, double* co
             std::vector<double> h((size_t)n * kSB);
             rs.download(h.data(), h.size(), s);
             HIP_CHECK(hipStreamSynchronize(s));
-            for (long long i = 0; i < n; ++i) { muh[i] = h[i * kSB] / (double)n; mp[i * kSB] = muh[i]; }
+            std::vector<double> nm(n);
+            for (long long i = 0; i < n; ++i) {
+                muh[i] = h[i * kSB] / (double)n;
+                mp[i * kSB] = muh[i];
+                nm[i] = (double)n * muh[i];
+            }
             mu = to_device(muh, s);
             mupad = to_device(mp, s);
+            nmu = to_device(nm, s);
         }
         // deterministic start block
         std::vector<double> v0((size_t)n * kSB);
@@ -670,17 +748,33 @@ int hh_comp_pca(hh_comp* c, int32_t k, double tol, int32_t max_iters, double* co
         const unsigned ge = (unsigned)((n * kSB + 255) / 256);
         std::vector<double> prev((size_t)n * k, 0.0), cur((size_t)n * k);
         std::vector<double> evals, evecs, Vh((size_t)n * kSB);
+        DBuf<int> fail(1);
+        fail.zero(s);
+        // Subspace iteration V <- orth(A V) on the device; every kCheck
+        // iterations a Rayleigh-Ritz step on the host extracts the Ritz
+        // vectors and tests convergence (the only host round trips).
+        constexpr int kCheck = 4;
         int it = 0;
         bool done = false;
         for (it = 1; it <= max_iters && !done; ++it) {
-            // A V = Xc^T (Xc V) with Xc = Cor - 1 mu^T (Cor symmetric):
-            // W1 = Cor V - 1 (mu^T V);  W = Cor W1 - mu (1^T W1)
+            // A V = Xc^T Xc V with Xc = Cor - 1 mu^T, Cor symmetric and
+            // Cor 1 = n mu:  A = Cor^2 - n mu mu^T, so
+            // W1 = Cor V;  W = Cor W1 - (n mu)(mu^T V)  (one Gram row, fused)
             wk.gram_dev(mupad.p, V.p, s);
-            wk.cor_mul(c->cor.p, V.p, nullptr, true, W1.p, s);
-            wk.gram_dev(onepad.p, W1.p, s);
-            wk.cor_mul(c->cor.p, W1.p, mu.p, true, W.p, s);
+            wk.cor_mul(c->cor.p, V.p, nullptr, false, W1.p, s);
+            wk.cor_mul(c->cor.p, W1.p, nmu.p, true, W.p, s);
+            if (it % kCheck != 0 && it != max_iters) {
+                // between checks one CholQR pass suffices (cond(A V) ~ l1/l16)
+                std::swap(V.p, W.p);
+                orthonormalize_dev(wk, V, tmp, n, fail.p, s, 1);
+                continue;
+            }
             // Rayleigh-Ritz: H = V^T W (V orthonormal), eig -> Y (descending)
             wk.gram(V.p, W.p, s);
+            int hfail = 0;
+            fail.download(&hfail, 1, s);
+            HIP_CHECK(hipStreamSynchronize(s));
+            HH_REQUIRE(!hfail, "subspace lost rank");
             std::vector<double> H(kSB * kSB);
             for (int a = 0; a < kSB; ++a)
                 for (int b = 0; b < kSB; ++b) H[a * kSB + b] = 0.5 * (wk.hG[a * kSB + b] + wk.hG[b * kSB + a]);
@@ -697,7 +791,7 @@ int hh_comp_pca(hh_comp* c, int32_t k, double tol, int32_t max_iters, double* co
             tmp.download(Vh.data(), Vh.size(), s);
             HIP_CHECK(hipStreamSynchronize(s));
             // convergence: largest entry change of the (unit, sign-aligned)
-            // top-k Ritz vectors between two iterations
+            // top-k Ritz vectors between two checks
             double worst = 0.0;
             for (int q = 0; q < k; ++q) {
                 double dot = 0.0, nn = 0.0;
@@ -714,12 +808,12 @@ int hh_comp_pca(hh_comp* c, int32_t k, double tol, int32_t max_iters, double* co
             }
             if (eigvals)
                 for (int q = 0; q < k; ++q) eigvals[q] = evals[ord[q]];
-            if (it > 1 && worst < tol) done = true;
+            if (it > kCheck && worst < tol) done = true;
             prev = cur;
             if (!done) {
                 // next block: orth(W Y)
                 hipLaunchKernelGGL(k_rot, dim3(ge), dim3(256), 0, s, W.p, wk.R.p, n, V.p);
-                HH_REQUIRE(orthonormalize(wk, V, tmp, n, s), "subspace lost rank");
+                orthonormalize_dev(wk, V, tmp, n, fail.p, s);
             }
         }
         c->iters = it - 1;
@@ -747,8 +841,11 @@ int hh_comp_select_stats(hh_comp* c, const double* pcs, int32_t k, double eps, d
         for (long long q = 0; q < (long long)k * n; ++q) cls[q] = pcs[q] > 0 ? 1 : (pcs[q] < 0 ? -1 : 0);
         DBuf<int8_t> dcls = to_device(cls, s);
         DBuf<double> part((size_t)n * 3 * 8);
-        hipLaunchKernelGGL(k_select_stats, dim3((unsigned)n), dim3(256), 0, s, c->cor.p, c->ld, n, c->Mp, c->N,
-                           c->dec.p, c->ng.p, dcls.p, (int)k, eps, part.p);
+        {
+            HH_KTIME("k_select_stats", s);
+            hipLaunchKernelGGL(k_select_stats, dim3((unsigned)n), dim3(256), 0, s, c->cor.p, c->ld, n, c->Mp, c->N,
+                               c->dec.p, c->ng.p, dcls.p, (int)k, eps, part.p);
+        }
         HIP_CHECK(hipGetLastError());
         std::vector<double> h((size_t)n * 3 * 8);
         part.download(h.data(), h.size(), s);
@@ -850,8 +947,11 @@ extern "C" int hh_gap_scan(const double* band, int64_t N, int32_t B, int32_t lb,
         DBuf<double> dB;
         const double* pb = stage_band(band, N, B, on_device, dB, s);
         DBuf<uint8_t> dg(N);
-        hipLaunchKernelGGL(k_gap_scan, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, pb, (long long)N, B, lb,
-                           dg.p);
+        {
+            HH_KTIME("k_gap_scan", s);
+            hipLaunchKernelGGL(k_gap_scan, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, pb, (long long)N, B, lb,
+                               dg.p);
+        }
         HIP_CHECK(hipGetLastError());
         dg.download(gap, N, s);
         HIP_CHECK(hipStreamSynchronize(s));
@@ -872,8 +972,11 @@ extern "C" int hh_di_scan(const double* band, int64_t N, int32_t B, const uint8_
         DBuf<uint8_t> dg(N);
         dg.upload(gap, N, s);
         DBuf<double> dd(N);
-        hipLaunchKernelGGL(k_di, dim3((unsigned)((N * kDiLanes + 255) / 256)), dim3(256), 0, s, pb, (long long)N, B,
-                           dg.p, dw.p, test, dd.p);
+        {
+            HH_KTIME("k_di", s);
+            hipLaunchKernelGGL(k_di, dim3((unsigned)((N * kDiLanes + 255) / 256)), dim3(256), 0, s, pb, (long long)N, B,
+                               dg.p, dw.p, test, dd.p);
+        }
         HIP_CHECK(hipGetLastError());
         dd.download(di, N, s);
         HIP_CHECK(hipStreamSynchronize(s));

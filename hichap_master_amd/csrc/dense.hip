@@ -253,18 +253,27 @@ static void symvc_run(const T* dX, long long N, const double* dalpha, const uint
     DBuf<double> tot(1);
     SymArgs a{N, nT, dalpha, dgap, nullptr, 1.0};
     HH_REQUIRE(npairs < (1LL << 31), "matrix too large");
-    hipLaunchKernelGGL((k_symvc<T, 1>), dim3((unsigned)npairs), dim3(256), 0, s, dX, a, part.p, nullptr);
+    {
+        HH_KTIME("k_symvc1", s);
+        hipLaunchKernelGGL((k_symvc<T, 1>), dim3((unsigned)npairs), dim3(256), 0, s, dX, a, part.p, nullptr);
+    }
     hipLaunchKernelGGL(k_symvc_rows, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, part.p, N, nT, exponent,
                        sv.p);
     a.s = sv.p;
-    hipLaunchKernelGGL((k_symvc<T, 2>), dim3((unsigned)npairs), dim3(256), 0, s, dX, a, part.p, nullptr);
+    {
+        HH_KTIME("k_symvc2", s);
+        hipLaunchKernelGGL((k_symvc<T, 2>), dim3((unsigned)npairs), dim3(256), 0, s, dX, a, part.p, nullptr);
+    }
     hipLaunchKernelGGL(k_slab_sum, dim3(1), dim3(256), 0, s, part.p, npairs, tot.p);
     double sumC = 0.0;
     HIP_CHECK(hipMemcpyAsync(&sumC, tot.p, sizeof(double), hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
     const double nn = (double)N * (double)N;
     a.scale = (raw_sum / nn) / (sumC / nn);
-    hipLaunchKernelGGL((k_symvc<T, 3>), dim3((unsigned)npairs), dim3(256), 0, s, dX, a, part.p, dout);
+    {
+        HH_KTIME("k_symvc3", s);
+        hipLaunchKernelGGL((k_symvc<T, 3>), dim3((unsigned)npairs), dim3(256), 0, s, dX, a, part.p, dout);
+    }
     HIP_CHECK(hipGetLastError());
     HIP_CHECK(hipStreamSynchronize(s));
 }
@@ -325,12 +334,15 @@ int hh_dense_rowstats(const void* X, int32_t dtype, int64_t N, const int64_t* lo
         if (lo) { dlo.alloc(N); dhi.alloc(N); dlo.upload((const long long*)lo, N, s); dhi.upload((const long long*)hi, N, s); }
         DBuf<double> dsum(N);
         DBuf<long long> dz(N);
-        if (dtype == 0)
-            hipLaunchKernelGGL((k_rowstats<long long>), dim3((unsigned)N), dim3(256), 0, s, (const long long*)px, (long long)N,
-                               dlo.p, dhi.p, dsum.p, dz.p);
-        else
-            hipLaunchKernelGGL((k_rowstats<double>), dim3((unsigned)N), dim3(256), 0, s, (const double*)px, (long long)N,
-                               dlo.p, dhi.p, dsum.p, dz.p);
+        {
+            HH_KTIME("k_rowstats", s);
+            if (dtype == 0)
+                hipLaunchKernelGGL((k_rowstats<long long>), dim3((unsigned)N), dim3(256), 0, s, (const long long*)px,
+                                   (long long)N, dlo.p, dhi.p, dsum.p, dz.p);
+            else
+                hipLaunchKernelGGL((k_rowstats<double>), dim3((unsigned)N), dim3(256), 0, s, (const double*)px,
+                                   (long long)N, dlo.p, dhi.p, dsum.p, dz.p);
+        }
         HIP_CHECK(hipGetLastError());
         dsum.download(rowsum, N, s);
         dz.download((long long*)zeros, N, s);
@@ -399,9 +411,11 @@ int hh_twostep(const int64_t* TM, const int64_t* MM, const int64_t* PM, int64_t 
         // row sums (exact) and zero counts
         DBuf<double> dsum((size_t)3 * N);
         DBuf<long long> dz((size_t)3 * N);
-        for (int k = 0; k < 3; ++k)
+        for (int k = 0; k < 3; ++k) {
+            HH_KTIME("k_rowstats", s);
             hipLaunchKernelGGL((k_rowstats<long long>), dim3((unsigned)N), dim3(256), 0, s, d[k], (long long)N,
                                (const long long*)nullptr, (const long long*)nullptr, dsum.p + k * N, dz.p + k * N);
+        }
         HIP_CHECK(hipGetLastError());
         std::vector<double> sum((size_t)3 * N);
         std::vector<long long> zeros((size_t)3 * N);

@@ -8,7 +8,10 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <memory>
+#include <mutex>
+#include <unordered_map>
 #include <stdexcept>
 #include <string>
 #include <utility>
@@ -64,7 +67,113 @@ int guard(F&& f) {
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
-// Owning device buffer.
+// Kernel timing registry (hh_ktime_*): when enabled, KTimeScope brackets a
+// launch with HIP events on its stream; hh_ktime_query sums the elapsed
+// times per kernel name.  Off by default (no events are created).
+struct KTimeRec {
+    const char* name;
+    hipEvent_t a, b;
+};
+inline bool g_ktime_on = false;
+inline std::mutex g_ktime_mu;
+inline std::vector<KTimeRec> g_ktime;
+struct KTimeScope {
+    KTimeRec r{nullptr, nullptr, nullptr};
+    hipStream_t s;
+    bool on;
+    KTimeScope(const char* name, hipStream_t s_) : s(s_), on(g_ktime_on) {
+        if (!on) return;
+        r.name = name;
+        HIP_CHECK(hipEventCreate(&r.a));
+        HIP_CHECK(hipEventCreate(&r.b));
+        HIP_CHECK(hipEventRecord(r.a, s));
+    }
+    ~KTimeScope() {
+        if (!on) return;
+        (void)hipEventRecord(r.b, s);
+        std::lock_guard<std::mutex> lk(g_ktime_mu);
+        g_ktime.push_back(r);
+    }
+};
+#define HH_KTIME(name, stream) ::hh::KTimeScope hh_kt_scope_(name, stream)
+
+// Device memory pool.  hipFree synchronises the device and costs ~0.2 ms per
+// call, which dominated per-chromosome loops (a few large buffers per call),
+// so released blocks are cached and reused (best fit within 2x).  Reuse is
+// stream-safe because every C-ABI entry point either synchronises its stream
+// before returning or keeps its buffers until a *_free that synchronises the
+// device first (hh_device_quiesce).
+struct PoolBlock {
+    size_t bytes;
+    int device;
+};
+inline std::mutex g_pool_mu;
+inline std::multimap<size_t, std::pair<int, void*>> g_pool_free;  // bytes -> (device, ptr)
+inline std::unordered_map<void*, PoolBlock> g_pool_live;
+inline size_t g_pool_cached = 0;
+constexpr size_t kPoolCacheCap = size_t(96) << 30;
+
+inline void pool_trim_locked(size_t keep) {
+    while (g_pool_cached > keep && !g_pool_free.empty()) {
+        auto it = std::prev(g_pool_free.end());  // largest first
+        int cur = 0;
+        (void)hipGetDevice(&cur);
+        (void)hipSetDevice(it->second.first);
+        (void)hipFree(it->second.second);
+        (void)hipSetDevice(cur);
+        g_pool_cached -= it->first;
+        g_pool_free.erase(it);
+    }
+}
+
+inline void* pool_alloc(size_t bytes) {
+    bytes = (bytes + 511) & ~size_t(511);
+    int dev = 0;
+    HIP_CHECK(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    for (auto it = g_pool_free.lower_bound(bytes); it != g_pool_free.end() && it->first <= 2 * bytes; ++it) {
+        if (it->second.first != dev) continue;
+        void* p = it->second.second;
+        g_pool_live[p] = PoolBlock{it->first, dev};
+        g_pool_cached -= it->first;
+        g_pool_free.erase(it);
+        return p;
+    }
+    void* p = nullptr;
+    hipError_t e = hipMalloc(&p, bytes);
+    if (e == hipErrorOutOfMemory) {
+        (void)hipGetLastError();
+        pool_trim_locked(0);
+        e = hipMalloc(&p, bytes);
+    }
+    if (e != hipSuccess)
+        throw Error(e == hipErrorOutOfMemory ? HH_ERR_OOM : HH_ERR_HIP,
+                    std::string("hipMalloc(") + std::to_string(bytes) + ") -> " + hipGetErrorString(e));
+    g_pool_live[p] = PoolBlock{bytes, dev};
+    return p;
+}
+
+inline void pool_free(void* p) {
+    if (!p) return;
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    auto it = g_pool_live.find(p);
+    if (it == g_pool_live.end()) return;
+    g_pool_free.emplace(it->second.bytes, std::make_pair(it->second.device, p));
+    g_pool_cached += it->second.bytes;
+    g_pool_live.erase(it);
+    if (g_pool_cached > kPoolCacheCap) pool_trim_locked(kPoolCacheCap / 2);
+}
+
+// Wait for all work on `device` (before releasing an object's buffers to the pool).
+inline void device_quiesce(int device) {
+    int cur = 0;
+    HIP_CHECK(hipGetDevice(&cur));
+    if (cur != device) HIP_CHECK(hipSetDevice(device));
+    HIP_CHECK(hipDeviceSynchronize());
+    if (cur != device) HIP_CHECK(hipSetDevice(cur));
+}
+
+// Owning device buffer (pooled).
 template <class T>
 struct DBuf {
     T* p = nullptr;
@@ -82,10 +191,10 @@ struct DBuf {
     void alloc(size_t count) {
         release();
         n = count;
-        if (count) HIP_CHECK(hipMalloc(&p, count * sizeof(T)));
+        if (count) p = static_cast<T*>(pool_alloc(count * sizeof(T)));
     }
     void release() {
-        if (p) (void)hipFree(p);
+        if (p) pool_free(p);
         p = nullptr;
         n = 0;
     }

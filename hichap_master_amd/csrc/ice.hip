@@ -507,7 +507,10 @@ int hh_ice_create(hh_matrix* m, const hh_ice_opts* o, hh_ice** out) {
 }
 
 int hh_ice_free(hh_ice* s) {
-    return guard([&] { delete s; });
+    return guard([&] {
+        if (s) device_quiesce(s->m->device);
+        delete s;
+    });
 }
 
 int hh_ice_n_groups(const hh_ice* s, int32_t* n) {

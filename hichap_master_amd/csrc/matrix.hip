@@ -135,6 +135,41 @@ extern "C" {
 const char* hh_last_error(void) { return g_last_error.c_str(); }
 int hh_version(void) { return (0 << 16) | (2 << 8) | 0; }
 
+int hh_ktime_enable(int32_t on) {
+    return guard([&] { hh::g_ktime_on = on != 0; });
+}
+
+int hh_ktime_query(const char* name, double* total_ms, int64_t* calls) {
+    return guard([&] {
+        HH_REQUIRE(name && total_ms && calls, "bad arguments");
+        std::lock_guard<std::mutex> lk(hh::g_ktime_mu);
+        double t = 0.0;
+        int64_t c = 0;
+        for (auto& r : hh::g_ktime) {
+            if (std::strcmp(r.name, name) != 0) continue;
+            HIP_CHECK(hipEventSynchronize(r.b));
+            float ms = 0.f;
+            HIP_CHECK(hipEventElapsedTime(&ms, r.a, r.b));
+            t += ms;
+            ++c;
+        }
+        *total_ms = t;
+        *calls = c;
+    });
+}
+
+int hh_ktime_reset(void) {
+    return guard([&] {
+        std::lock_guard<std::mutex> lk(hh::g_ktime_mu);
+        for (auto& r : hh::g_ktime) {
+            (void)hipEventSynchronize(r.b);
+            (void)hipEventDestroy(r.a);
+            (void)hipEventDestroy(r.b);
+        }
+        hh::g_ktime.clear();
+    });
+}
+
 int hh_device_count(int32_t* n) {
     return guard([&] {
         int c = 0;
@@ -291,7 +326,10 @@ int hh_matrix_from_pixels(const int64_t* bin1, const int64_t* bin2, const double
 }
 
 int hh_matrix_free(hh_matrix* m) {
-    return guard([&] { delete m; });
+    return guard([&] {
+        if (m) device_quiesce(m->device);
+        delete m;
+    });
 }
 
 int hh_matrix_get_info(const hh_matrix* m, hh_matrix_info* info) {

@@ -212,6 +212,20 @@ void synth_setup(const hh_synth_params* p, SynthHost& h, hipStream_t s) {
 inline dim3 row_grid(int64_t nrows) { return dim3((unsigned)((nrows * 64 + 255) / 256)); }
 }  // namespace
 
+namespace hh {
+// Dense cis block of one chromosome: out[i][j] = count(lo + i, lo + j).
+__global__ __launch_bounds__(256) void k_synth_dense(SynthDev p, long long lo, long long nc, double* __restrict__ out) {
+    const long long j = (long long)blockIdx.x * 64 + (threadIdx.x & 63);
+    const long long i0 = (long long)blockIdx.y * 16 + (threadIdx.x >> 6) * 4;
+    if (j >= nc) return;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const long long i = i0 + u;
+        if (i < nc) out[i * nc + j] = (double)synth_count(p, lo + i, lo + j);
+    }
+}
+}  // namespace hh
+
 extern "C" {
 
 int hh_synth_count(const hh_synth_params* p, int32_t* row_work, int64_t* row_nnz_upper, void* stream) {
@@ -289,6 +303,21 @@ int hh_synth_build(const hh_synth_params* p, int64_t row_lo, int64_t row_hi, voi
         for (size_t i = 0; i < hc.size(); ++i) ent += hc[i];
         m->n_entries = ent;
         *out = m.release();
+    });
+}
+
+int hh_synth_dense(const hh_synth_params* p, int32_t chrom, double* out, void* stream) {
+    return guard([&] {
+        HH_REQUIRE(p && out && 0 <= chrom && chrom < p->n_chroms, "bad arguments");
+        hipStream_t s = as_stream(stream);
+        SynthHost h;
+        synth_setup(p, h, s);
+        const long long lo = h.offsets[chrom], nc = h.offsets[chrom + 1] - lo;
+        if (nc > 0)
+            hipLaunchKernelGGL(k_synth_dense, dim3((unsigned)((nc + 63) / 64), (unsigned)((nc + 15) / 16)), dim3(256), 0,
+                               s, h.dev, lo, nc, out);
+        HIP_CHECK(hipGetLastError());
+        HIP_CHECK(hipStreamSynchronize(s));
     });
 }
 

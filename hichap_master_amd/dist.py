@@ -1,5 +1,9 @@
-"""Multi-GPU genome-wide ICE: one process per GPU, rows sharded, one
-all-gather of the per-bin marginal per iteration over RCCL (xGMI).
+"""Multi-GPU drivers: one process per GPU.
+
+Genome-wide ICE: rows sharded, one all-gather of the per-bin marginal per
+iteration over RCCL (xGMI).  Per-chromosome work (two-step correction,
+compartment PCA, DI scans): whole chromosomes dealt to ranks by LPT on their
+cost, no collective on the data path (``lpt_assign`` / ``run_chromosomes``).
 
 Each rank holds complete symmetric rows ``[rank_rows[r], rank_rows[r+1])`` of
 the pixel-chunk matrix, so the marginal of its own rows is exact locally; the
@@ -40,6 +44,38 @@ def partition_rows(row_weight, world: int, align: int = ROW_BLOCK) -> np.ndarray
         cuts.append(min(max(c, cuts[-1]), nb))
     cuts.append(nb)
     return np.minimum(np.asarray(cuts, dtype=np.int64) * align, n)
+
+
+def lpt_assign(costs, world: int) -> np.ndarray:
+    """Longest-processing-time-first: items in decreasing cost (ties by
+    index) each go to the least-loaded rank (ties by lowest rank).  Returns
+    ``owner[i]``; deterministic, so every rank computes the same plan."""
+    c = np.asarray(costs, dtype=np.float64)
+    owner = np.zeros(c.size, dtype=np.int64)
+    load = np.zeros(max(int(world), 1))
+    for i in sorted(range(c.size), key=lambda k: (-c[k], k)):
+        r = int(np.argmin(load))
+        owner[i] = r
+        load[r] += c[i]
+    return owner
+
+
+def run_chromosomes(fn, keys, costs, rank: int, world: int, gather: bool = False, group=None):
+    """Run ``fn(key)`` for this rank's share of ``keys`` (LPT on ``costs``).
+    Returns {key: result} for the local keys, or for every key on every rank
+    with ``gather=True`` (``all_gather_object``; meant for small results such
+    as PC vectors, not N x N matrices)."""
+    owner = lpt_assign(costs, world)
+    local = {k: fn(k) for k, o in zip(keys, owner) if o == rank}
+    if not gather or world == 1:
+        return local
+    import torch.distributed as tdist
+    parts = [None] * world
+    tdist.all_gather_object(parts, local, group=group)
+    out = {}
+    for p in parts:
+        out.update(p)
+    return {k: out[k] for k in keys}
 
 
 class Exchange:

@@ -122,6 +122,14 @@ def synth_params(chrom_nbins, A=30.0, decay=1.08, comp_strength=0.3, vis_sigma=0
     return p, arr  # keep `arr` alive while p is used
 
 
+def synth_dense(chrom_nbins, chrom, out_ptr, stream=None, **kw):
+    """Dense float64 cis block of chromosome ``chrom`` of the synthetic genome
+    written to device memory at ``out_ptr`` (N_c x N_c, row-major)."""
+    _lib.require_gpu()
+    p, keep = synth_params(chrom_nbins, **kw)
+    call("hh_synth_dense", C.byref(p), int(chrom), C.c_void_p(int(out_ptr)), stream)
+
+
 def synth_row_counts(chrom_nbins, stream=None, **kw):
     """Counting pass of the generator: per-row stored slots (work) and
     upper-triangle pixel counts for every row (used to partition rows)."""

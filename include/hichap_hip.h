@@ -45,6 +45,13 @@ int hh_synchronize(void* stream);
  * "sweep_ablate" 0/1/2 (timing ablations only: 1 skips the LDS gathers,
  * 2 skips the b staging; results are wrong while set). */
 int hh_tune(const char* key, int64_t value);
+/* Kernel timing (measurement only): while enabled, the dense-path launches
+ * (k_rowstats, k_symvc1..3, k_syrk, k_cor_mul, k_select_stats, k_di,
+ * k_gap_scan) are bracketed by HIP events on their stream; query returns the
+ * summed duration and launch count for one kernel name (synchronising). */
+int hh_ktime_enable(int32_t on);
+int hh_ktime_query(const char* name, double* total_ms, int64_t* calls);
+int hh_ktime_reset(void);
 
 /* ---------------------------------------------------- contact matrix
  * A contact matrix resident in HBM in the "tiled pixel" layout:
@@ -114,6 +121,10 @@ typedef struct {
  * pixel counts (host arrays of n_bins).  Used to partition rows across ranks. */
 int hh_synth_count(const hh_synth_params* p, int32_t* row_work, int64_t* row_nnz_upper,
                    void* stream);
+/* Dense cis block of chromosome `chrom` of the same synthetic genome as
+ * float64 counts into device memory out[N_c * N_c] (bench inputs for the
+ * per-chromosome compartment config C5; ignore_diags applies). */
+int hh_synth_dense(const hh_synth_params* p, int32_t chrom, double* out, void* stream);
 /* Build rows [row_lo, row_hi) (row_lo % 256 == 0). */
 int hh_synth_build(const hh_synth_params* p, int64_t row_lo, int64_t row_hi, void* stream,
                    hh_matrix** out);

@@ -68,3 +68,43 @@ def test_sharded_balance_gloo_matches_oracle(world):
         np.testing.assert_allclose(w, wr, rtol=1e-12, equal_nan=True)
     # the driver polls every 8 sweeps; converged groups stop updating
     assert its[0] == sr["iters"]
+
+
+def test_lpt_assign_greedy():
+    owner = dist.lpt_assign([10, 9, 8, 1, 1, 1], 2)
+    loads = [sum(c for c, o in zip([10, 9, 8, 1, 1, 1], owner) if o == r) for r in range(2)]
+    assert loads == [13, 17]  # 10 | 9, 8 | then the 1s to the lighter rank
+    assert list(dist.lpt_assign([5, 5, 5], 1)) == [0, 0, 0]
+    # hg19 autosomes at 25 kb, cost N^3 over 8 ranks: max load vs ideal (1.98e12 vs 1.27e12)
+    Ns = np.array(synth.chrom_bins([synth.HG19[str(c)] for c in range(1, 23)], 25000), dtype=float)
+    own = dist.lpt_assign(Ns ** 3, 8)
+    worst = max(float(np.sum(Ns[own == r] ** 3)) for r in range(8))
+    assert worst == float(Ns.max() ** 3) or worst < 1.6 * float(np.sum(Ns ** 3)) / 8
+
+
+def _chrom_worker(rank, world, port, outdir):
+    import torch.distributed as tdist
+    from oracle import hichap_ref
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    tdist.init_process_group("gloo", rank=rank, world_size=world)
+    rng = np.random.default_rng(5)
+    mats = {f"c{i}": synth.dense_chrom(n, rng, A=20.0) for i, n in enumerate([60, 90, 40, 75])}
+
+    def body(key):
+        TM = mats[key]
+        return hichap_ref.sort_chromosomes([key]), int(TM.sum())
+
+    res = dist.run_chromosomes(body, list(mats), [m.shape[0] ** 2 for m in mats.values()], rank, world,
+                               gather=True)
+    np.save(os.path.join(outdir, f"r{rank}.npy"), np.array([res[k][1] for k in mats]))
+    tdist.destroy_process_group()
+
+
+def test_run_chromosomes_gloo():
+    import torch.multiprocessing as mp
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_chrom_worker, args=(2, _free_port(), d), nprocs=2, start_method="spawn")
+        a, b = np.load(os.path.join(d, "r0.npy")), np.load(os.path.join(d, "r1.npy"))
+    rng = np.random.default_rng(5)
+    want = [int(synth.dense_chrom(n, rng, A=20.0).sum()) for n in [60, 90, 40, 75]]
+    assert list(a) == want and list(b) == want

@@ -179,3 +179,22 @@ def test_synthetic_generator_matches_oracle(ice):
     wr, sr = ice_ref.balance(b1, b2, c, int(off[-1]), off, max_iters=400)
     np.testing.assert_allclose(w, wr, rtol=1e-9, equal_nan=True)
     assert st["iters"] == sr["iters"]
+
+
+def test_synth_dense_block_matches_sparse_generator(ice):
+    """hh_synth_dense (C5 bench inputs) is the cis block of the same genome."""
+    import torch
+    sizes = [300, 260]
+    kw = dict(A=40.0, trans_density=0.0, comp_block=50, ignore_diags=0, cis_only=True, seed=7)
+    m = ice.ContactMatrix.synthetic(sizes, **kw)
+    b1, b2, c = m.export_upper()
+    off = np.concatenate([[0], np.cumsum(sizes)])
+    for k, n in enumerate(sizes):
+        buf = torch.zeros((n, n), dtype=torch.float64, device="cuda")
+        ice.synth_dense(sizes, k, buf.data_ptr(), **kw)
+        D = buf.cpu().numpy()
+        np.testing.assert_array_equal(D, D.T)
+        want = np.zeros((n, n))
+        sel = (b1 >= off[k]) & (b1 < off[k + 1])
+        want[b1[sel] - off[k], b2[sel] - off[k]] = c[sel]
+        np.testing.assert_array_equal(np.triu(D), want)

@@ -102,3 +102,14 @@ def test_di_large_vs_oracle(SF):
     np.testing.assert_array_equal(gap, gref)
     dref = structure_ref.get_di(M, gref, 60, "ttest")
     np.testing.assert_allclose(di, dref, rtol=1e-11, atol=1e-300)
+
+
+def test_compartment_device_tensor_input(SF):
+    """A device-resident torch tensor goes to the C-ABI without a host copy
+    and gives the same PC as the NumPy input."""
+    import torch
+    rng = np.random.default_rng(3)
+    M = synth.dense_chrom(600, rng, A=30.0, gap_frac=0.03).astype(np.float64)
+    a = SF(Res=100000).compartment(M)
+    b = SF(Res=100000).compartment(torch.from_numpy(M).cuda())
+    np.testing.assert_array_equal(a, b)
