@@ -321,7 +321,8 @@ def main():
                        "trans_fraction_target": tf, "resolution_bp": 10000 if args.config != "c1" else 40000,
                        "parallelism": f"rows sharded x{world}, RCCL all-gather of marginals" if world > 1
                        else "single GPU", "generate_s": round(gen_s, 2),
-                       "entries_stored": inf["n_entries"], "slots": inf["n_slots"],
+                       "entries_stored": inf["n_entries"], "slots_u32": inf["n_slots"],
+                       "slots_u16": inf["n_slots_narrow"], "payload_bytes": inf["payload_bytes"],
                        "tiles": inf["n_tiles"], "units": inf["n_units"],
                        "hbm_bytes_matrix": inf["device_bytes"]},
         }
@@ -330,11 +331,17 @@ def main():
         if launches:
             sweep_avg = sweep_ms / launches / 1000.0
             achieved = ALG_BYTES_PER_PIXEL * inf["nnz_upper"] / sweep_avg / 1e9
+            # bytes the layout actually streams: entries (uint16 + uint32) +
+            # both segments' row pointers (the b staging shows up in traffic)
+            real_b = float(inf["payload_bytes"]) + 8.0 * 513 * inf["n_tiles"]
             out["roofline"] = {"bound": "hbm", "kernel": "k_sweep_tiled", "achieved": achieved,
                                "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS,
                                "traffic": traffic,
                                "traffic_source": traffic_src,
-                               "real_bytes_per_launch": 4.0 * inf["n_slots"] + 4.0 * 257 * inf["n_tiles"],
+                               "real_bytes_per_launch": real_b,
+                               "real_GBps": real_b / sweep_avg / 1e9,
+                               "real_frac": real_b / sweep_avg / 1e9 / PEAK_HBM_GBS,
+                               "traffic_GBps": (traffic / sweep_avg / 1e9) if traffic else None,
                                "sweep_ms_avg": sweep_avg * 1000.0,
                                "iter_ms_avg": iter_ms / launches}
         if world == 1 and not args.no_cpu:

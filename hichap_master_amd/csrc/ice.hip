@@ -37,41 +37,80 @@ constexpr int kThreads = 256;
 constexpr int kSweepThreads = 512;
 constexpr int kSweepWaves = kSweepThreads / 64;
 
-// LDS image of the tile's bias values, XOR-rotated so that a wave reading
-// columns c, c+4, c+8, ... (one uint4 of 4 consecutive entries per lane on a
-// dense row) hits 32 distinct 8-byte bank slots: element e = 32h + l is kept
-// at 32h + ((l + h) mod 32).
-__device__ __forceinline__ uint32_t swz(uint32_t e) { return (e & ~31u) | ((e + (e >> 5)) & 31u); }
-
-__device__ __forceinline__ double tile_dot(const uint4 v, const double* __restrict__ bl, double a) {
-    a = fma((double)(v.x >> kWBits), bl[swz(v.x & kColMask)], a);
-    a = fma((double)(v.y >> kWBits), bl[swz(v.y & kColMask)], a);
-    a = fma((double)(v.z >> kWBits), bl[swz(v.z & kColMask)], a);
-    a = fma((double)(v.w >> kWBits), bl[swz(v.w & kColMask)], a);
-    return a;
+// Entry decode: the byte offset of the staged bias value is a field of the
+// entry (ice_internal.hpp), so an entry costs mask, shift, cvt, LDS read and
+// FMA.  All LDS reads of a uint4 are issued before the FMAs, into two
+// accumulators (even / odd entries; fixed order -> deterministic).
+__device__ __forceinline__ double lds_b(const double* bl, uint32_t byteoff) {
+    return *reinterpret_cast<const double*>(reinterpret_cast<const char*>(bl) + byteoff);
 }
 
-// NB row batches of a wave in flight together (loads of all of them issued
-// before any is consumed) so short rows still keep ~NB KiB per wave in flight.
-template <int G, int NB, int ABL>
+__device__ __forceinline__ void tile_dot(const uint4 v, const double* __restrict__ bl, double& a0, double& a1) {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    double x[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) x[i] = lds_b(bl, w[i] & 0xFFFFu);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < 4; i += 2) {
+        a0 = fma((double)(w[i] >> 16), x[i], a0);
+        a1 = fma((double)(w[i + 1] >> 16), x[i + 1], a1);
+    }
+}
+
+// 8 narrow entries (uint16 = byteoff | count) per uint4
+__device__ __forceinline__ void tile_dot16(const uint4 v, const double* __restrict__ bl, double& a0, double& a1) {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    double x[8];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        x[2 * i] = lds_b(bl, w[i] & 0xFFF8u);
+        x[2 * i + 1] = lds_b(bl, (w[i] >> 16) & 0xFFF8u);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        a0 = fma((double)(w[i] & 7u), x[2 * i], a0);
+        a1 = fma((double)((w[i] >> 16) & 7u), x[2 * i + 1], a1);
+    }
+}
+
+// 16-B payload load as one global_load_dwordx4 (a HIP uint4 copy under a
+// select is split into dword loads).  Unconditional: callers clamp the index
+// to a valid slot and zero the value of finished rows.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 ld16(const uint4* p) {
+    const u32x4 v = *reinterpret_cast<const u32x4*>(p);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+// Rows of one segment of a tile (EPV entries per uint4: 8 narrow uint16, 4
+// wide uint32).  Lane groups of G lanes take one row each, NB rows per group
+// at a time (their loads issued together).  acc[v] (v = row
+// index within the unit, + nr for the wide segment) is owned by one lane
+// group per tile -> fixed summation order.
+template <int G, int NB, int ABL, int EPV>
 __device__ __forceinline__ void tile_rows(const uint4* __restrict__ pay4, const uint32_t* __restrict__ rp,
                                           const double* __restrict__ bl, double* __restrict__ acc, int ra,
                                           int rb, int wave, int lane) {
     constexpr int RP = 64 / G;              // rows per wave step
     constexpr int S = kSweepWaves * RP;     // row distance between a wave's batches
+    constexpr int SH = EPV == 8 ? 3 : 2;
     const int gi = lane / G, li = lane % G;
+    const uint4 zero = make_uint4(0u, 0u, 0u, 0u);
     for (int r0 = ra + wave * RP; r0 < rb; r0 += NB * S) {
         uint32_t q[NB], qe[NB];
-        double a[NB];
+        double a[NB], a1[NB];
 #pragma unroll
         for (int k = 0; k < NB; ++k) {
             const int r = r0 + k * S + gi;
             q[k] = qe[k] = 0;
             if (r < rb) {
-                q[k] = (rp[r] >> 2) + li;
-                qe[k] = rp[r + 1] >> 2;
+                q[k] = (rp[r] >> SH) + li;
+                qe[k] = rp[r + 1] >> SH;
             }
             a[k] = 0.0;
+            a1[k] = 0.0;
         }
         bool more = false;
 #pragma unroll
@@ -79,14 +118,21 @@ __device__ __forceinline__ void tile_rows(const uint4* __restrict__ pay4, const 
         while (more) {
             uint4 v[NB];
 #pragma unroll
-            for (int k = 0; k < NB; ++k) v[k] = q[k] < qe[k] ? pay4[q[k]] : make_uint4(0u, 0u, 0u, 0u);
+            for (int k = 0; k < NB; ++k) {
+                const bool on = q[k] < qe[k];
+                const uint4 x = ld16(pay4 + (on ? q[k] : 0u));
+                v[k] = on ? x : zero;
+            }
+            __builtin_amdgcn_sched_barrier(0);  // all NB loads in flight before the first use
             more = false;
 #pragma unroll
             for (int k = 0; k < NB; ++k) {
                 if (ABL == 1) {  // timing ablation: no LDS gathers
                     a[k] += (double)(v[k].x + v[k].y + v[k].z + v[k].w);
+                } else if (EPV == 8) {
+                    tile_dot16(v[k], bl, a[k], a1[k]);
                 } else {
-                    a[k] = tile_dot(v[k], bl, a[k]);
+                    tile_dot(v[k], bl, a[k], a1[k]);
                 }
                 q[k] += G;
                 more |= q[k] < qe[k];
@@ -94,7 +140,7 @@ __device__ __forceinline__ void tile_rows(const uint4* __restrict__ pay4, const 
         }
 #pragma unroll
         for (int k = 0; k < NB; ++k) {
-            double x = a[k];
+            double x = a[k] + a1[k];
 #pragma unroll
             for (int o = G >> 1; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
             const int r = r0 + k * S + gi;
@@ -103,14 +149,108 @@ __device__ __forceinline__ void tile_rows(const uint4* __restrict__ pay4, const 
     }
 }
 
+// Sorted-band variant for units that cover whole row-blocks: the rows of a
+// band of the tile's length order (perm[lo..hi), all within a 2x length
+// range) go to lane groups of width G, so the rows a wave carries at once
+// have similar lengths and few lanes idle.
+template <int G, int NB, int ABL, int EPV>
+__device__ __forceinline__ void band_rows(const uint4* __restrict__ pay4, const uint32_t* __restrict__ rp,
+                                          const uint16_t* __restrict__ perm, int lo, int hi,
+                                          const double* __restrict__ bl, double* __restrict__ acc, int wave,
+                                          int lane) {
+    constexpr int RP = 64 / G;
+    constexpr int S = kSweepWaves * RP;
+    constexpr int SH = EPV == 8 ? 3 : 2;
+    const int gi = lane / G, li = lane % G;
+    const uint4 zero = make_uint4(0u, 0u, 0u, 0u);
+    for (int v0 = lo + wave * RP; v0 < hi; v0 += NB * S) {
+        uint32_t q[NB], qe[NB];
+        int row[NB];
+        double a[NB], a1[NB];
+#pragma unroll
+        for (int k = 0; k < NB; ++k) {
+            const int v = v0 + k * S + gi;
+            q[k] = qe[k] = 0;
+            row[k] = -1;
+            if (v < hi) {
+                const int r = perm[v];
+                row[k] = r;
+                q[k] = (rp[r] >> SH) + li;
+                qe[k] = rp[r + 1] >> SH;
+            }
+            a[k] = 0.0;
+            a1[k] = 0.0;
+        }
+        bool more = false;
+#pragma unroll
+        for (int k = 0; k < NB; ++k) more |= q[k] < qe[k];
+        while (more) {
+            uint4 v[NB];
+#pragma unroll
+            for (int k = 0; k < NB; ++k) {
+                const bool on = q[k] < qe[k];
+                const uint4 x = ld16(pay4 + (on ? q[k] : 0u));
+                v[k] = on ? x : zero;
+            }
+            __builtin_amdgcn_sched_barrier(0);  // all NB loads in flight before the first use
+            more = false;
+#pragma unroll
+            for (int k = 0; k < NB; ++k) {
+                if (ABL == 1) {
+                    a[k] += (double)(v[k].x + v[k].y + v[k].z + v[k].w);
+                } else if (EPV == 8) {
+                    tile_dot16(v[k], bl, a[k], a1[k]);
+                } else {
+                    tile_dot(v[k], bl, a[k], a1[k]);
+                }
+                q[k] += G;
+                more |= q[k] < qe[k];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < NB; ++k) {
+            double x = a[k] + a1[k];
+#pragma unroll
+            for (int o = G >> 1; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+            if (li == 0 && row[k] >= 0) acc[row[k]] += x;
+        }
+    }
+}
+
+template <int NB, int ABL, int EPV>
+__device__ __forceinline__ void sweep_bands(const uint16_t* band, const uint4* pay4, const uint32_t* rp,
+                                            const uint16_t* perm, const double* bl, double* acc, int wave,
+                                            int lane) {
+    if (band[1] > band[0]) band_rows<64, NB, ABL, EPV>(pay4, rp, perm, band[0], band[1], bl, acc, wave, lane);
+    if (band[2] > band[1]) band_rows<32, NB, ABL, EPV>(pay4, rp, perm, band[1], band[2], bl, acc, wave, lane);
+    if (band[3] > band[2]) band_rows<16, NB, ABL, EPV>(pay4, rp, perm, band[2], band[3], bl, acc, wave, lane);
+    if (band[4] > band[3]) band_rows<8, NB, ABL, EPV>(pay4, rp, perm, band[3], band[4], bl, acc, wave, lane);
+    if (band[5] > band[4]) band_rows<4, NB, ABL, EPV>(pay4, rp, perm, band[4], band[5], bl, acc, wave, lane);
+}
+
+template <int NB, int ABL, int EPV>
+__device__ __forceinline__ void sweep_rows(uint32_t mean, const uint4* pay4, const uint32_t* rp, const double* bl,
+                                           double* acc, int ra, int rb, int wave, int lane) {
+    if (mean >= 48) tile_rows<64, NB, ABL, EPV>(pay4, rp, bl, acc, ra, rb, wave, lane);
+    else if (mean >= 24) tile_rows<32, NB, ABL, EPV>(pay4, rp, bl, acc, ra, rb, wave, lane);
+    else if (mean >= 12) tile_rows<16, NB, ABL, EPV>(pay4, rp, bl, acc, ra, rb, wave, lane);
+    else if (mean >= 6) tile_rows<8, NB, ABL, EPV>(pay4, rp, bl, acc, ra, rb, wave, lane);
+    else tile_rows<4, NB, ABL, EPV>(pay4, rp, bl, acc, ra, rb, wave, lane);
+}
+
 template <int NB, int ABL>
-__global__ __launch_bounds__(kSweepThreads) void k_sweep_tiled(TileDev T, const uint8_t* __restrict__ act,
+__global__ __launch_bounds__(kSweepThreads, 4) void k_sweep_tiled(TileDev T, const uint8_t* __restrict__ act,
                                                                 int n_units, const double* __restrict__ b,
-                                                                long long n_bins, double* __restrict__ part) {
+                                                                long long n_bins, double* __restrict__ part,
+                                                                int flags) {
     __shared__ __attribute__((aligned(16))) double bl[kW];
-    __shared__ double acc[kR];
-    __shared__ uint32_t rps[kR + 1];
-    const int u = blockIdx.x;
+    __shared__ double acc2[2 * kR];  // narrow rows, then wide rows
+    __shared__ uint32_t rps[kR + 1], rpsn[kR + 1];
+    __shared__ uint16_t perm[2 * kR];
+    __shared__ uint16_t band[2 * kBandSlots];
+    // flags bit0: units sorted by column tile and dealt so that each XCD takes
+    // a contiguous range (measured slower on C4: kept as a knob only)
+    const int u = (flags & 1) ? T.u_order[xcd_remap(blockIdx.x, n_units)] : (int)blockIdx.x;
     if (u >= n_units) return;
     {
         bool on = false;
@@ -118,8 +258,9 @@ __global__ __launch_bounds__(kSweepThreads) void k_sweep_tiled(TileDev T, const 
         if (!on) return;
     }
     const int ra = T.u_rlo[u], rb = T.u_rhi[u];
+    const bool whole = T.u_whole[u] != 0;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    for (int k = threadIdx.x; k < rb - ra; k += kSweepThreads) acc[k] = 0.0;
+    for (int k = threadIdx.x; k < 2 * (rb - ra); k += kSweepThreads) acc2[k] = 0.0;
     for (int t = T.u_tlo[u]; t < T.u_thi[u]; ++t) {
         const long long c0 = (long long)T.tile_J[t] * kW;
         __syncthreads();  // previous tile's LDS reads are done
@@ -141,22 +282,35 @@ __global__ __launch_bounds__(kSweepThreads) void k_sweep_tiled(TileDev T, const 
         }
         {
             const uint32_t* rpg = T.tile_rp + (size_t)t * (kR + 1);
-            for (int k = threadIdx.x; k <= kR; k += kSweepThreads) rps[k] = rpg[k];
+            const uint32_t* rpgn = T.tile_rpn + (size_t)t * (kR + 1);
+            for (int k = threadIdx.x; k <= kR; k += kSweepThreads) {
+                rps[k] = rpg[k];
+                rpsn[k] = rpgn[k];
+            }
+            if (whole) {
+                const uint16_t* pg = T.tile_perm + (size_t)t * 2 * kR;
+                for (int k = threadIdx.x; k < 2 * kR; k += kSweepThreads) perm[k] = pg[k];
+                if (threadIdx.x < 2 * kBandSlots) band[threadIdx.x] = T.tile_band[(size_t)t * 2 * kBandSlots + threadIdx.x];
+            }
         }
         __syncthreads();
-        const uint32_t* rp = rps;
-        const uint4* pay4 = reinterpret_cast<const uint4*>(T.pay + T.tile_ent[t]);
-        // lane-group width from the mean row length of the unit's rows in this tile
-        const uint32_t tot = rp[rb] - rp[ra];
-        const uint32_t mean4 = tot / (uint32_t)(4 * (rb - ra));  // uint4 per row
-        if (mean4 >= 48) tile_rows<64, NB, ABL>(pay4, rp, bl, acc, ra, rb, wave, lane);
-        else if (mean4 >= 24) tile_rows<32, NB, ABL>(pay4, rp, bl, acc, ra, rb, wave, lane);
-        else if (mean4 >= 12) tile_rows<16, NB, ABL>(pay4, rp, bl, acc, ra, rb, wave, lane);
-        else if (mean4 >= 6) tile_rows<8, NB, ABL>(pay4, rp, bl, acc, ra, rb, wave, lane);
-        else tile_rows<4, NB, ABL>(pay4, rp, bl, acc, ra, rb, wave, lane);
+        const uint32_t totn = rpsn[rb] - rpsn[ra], totw = rps[rb] - rps[ra];
+        const uint4* payn4 = reinterpret_cast<const uint4*>(T.payn + T.tile_entn[t]);
+        const uint4* payw4 = reinterpret_cast<const uint4*>(T.pay + T.tile_ent[t]);
+        // narrow rows accumulate into acc2[0, nr), wide rows into acc2[nr, 2 nr):
+        // disjoint, so the two passes need no barrier between them.  Lane-group
+        // width from each segment's mean uint4 count per row.
+        const int nr = rb - ra;
+        if (whole) {  // ra == 0: acc2 index = row
+            if (totn) sweep_bands<NB, ABL, 8>(band, payn4, rpsn, perm, bl, acc2, wave, lane);
+            if (totw) sweep_bands<NB, ABL, 4>(band + kBandSlots, payw4, rps, perm + kR, bl, acc2 + nr, wave, lane);
+        } else {
+            if (totn) sweep_rows<NB, ABL, 8>(totn / 8 / (uint32_t)nr, payn4, rpsn, bl, acc2, ra, rb, wave, lane);
+            if (totw) sweep_rows<NB, ABL, 4>(totw / 4 / (uint32_t)nr, payw4, rps, bl, acc2 + nr, ra, rb, wave, lane);
+        }
     }
     __syncthreads();
-    for (int k = threadIdx.x; k < rb - ra; k += kSweepThreads) part[T.u_slot[u] + k] = acc[k];
+    for (int k = threadIdx.x; k < rb - ra; k += kSweepThreads) part[T.u_slot[u] + k] = acc2[k] + acc2[(rb - ra) + k];
 }
 
 // ---------------------------------------------------------------- K2
@@ -356,13 +510,14 @@ struct hh_ice {
 namespace hh {
 
 // Tuning knobs (hh_tune; no effect on results except the ablations).
-static int g_sweep_nb = 4;
+static int g_sweep_nb = 2;
 static int g_sweep_ablate = 0;
+static int g_sweep_flags = 0;  // bit0: XCD-ordered units
 
 template <int NB, int ABL>
 static void launch_sweep(const hh_matrix* m, const uint8_t* act, const double* b, double* part, hipStream_t s) {
     hipLaunchKernelGGL((k_sweep_tiled<NB, ABL>), dim3((unsigned)m->n_units), dim3(kSweepThreads), 0, s, m->dev(),
-                       act, (int)m->n_units, b, (long long)m->n_bins, part);
+                       act, (int)m->n_units, b, (long long)m->n_bins, part, g_sweep_flags);
 }
 
 template <int ABL>
@@ -433,7 +588,11 @@ int hh_tune(const char* key, int64_t value) {
             g_sweep_ablate = (int)value;
         } else if (k == "unit_entries") {
             HH_REQUIRE(value == 0 || (value >= 4096 && value <= (1 << 24)), "unit_entries must be 0 (auto) or in [4096, 2^24]");
-            g_unit_entries = value;        } else {
+            g_unit_entries = value;
+        } else if (k == "sweep_flags") {
+            HH_REQUIRE(value >= 0 && value <= 1, "sweep_flags in [0, 1]");
+            g_sweep_flags = (int)value;
+        } else {
             HH_THROW(HH_ERR_ARG, "unknown tuning key " + k);
         }
     });

@@ -2,12 +2,17 @@
 // DESIGN.md §3) and of its build plan.  Not part of the C-ABI.
 //
 // The symmetric matrix (both triangles of cooler's pixel table) is cut into
-// row-blocks of kR = 256 rows (global alignment: block = row / 256) and column
+// row-blocks of kR = 512 rows (global alignment: block = row / 256) and column
 // tiles of kW = 8192 columns.  A nonempty (row-block, tile) pair is a *tile*:
 // its entries are stored row by row (each row's list column-sorted and padded
-// to a multiple of 4 entries = 16 B), with kR + 1 row pointers.  An entry is
-// a uint32 = count << 13 | (col - tile_start); counts >= 2^19 go to a small
-// per-row "wide" list instead.  The sweep kernel stages the tile's 8192 bias
+// to 16 B), with kR + 1 row pointers.  Entries come in two widths, each a
+// row-structured segment of the tile with its own row pointers:
+//   narrow  uint16 = swz(c) << 3 | count, counts 1..7
+//           (~3/4 of a whole-genome matrix's pixels: far-cis and trans);
+//   wide    uint32 = count << 16 | swz(c) << 3, counts 8..65535,
+// with c = col - tile_start and swz the LDS bank rotation of the staged bias
+// slice, so swz(c) << 3 is the entry's byte offset in LDS: decoding is two
+// mask/shift ops.  Counts > 65535 go to a small per-row "wide list" instead.  The sweep kernel stages the tile's 8192 bias
 // values in LDS once and gathers from LDS, so the per-entry gathers never
 // touch the texture path.
 //
@@ -22,15 +27,33 @@
 
 namespace hh {
 
-constexpr int kR = 256;                 // rows per row-block
+constexpr int kR = 512;                 // rows per row-block
 constexpr int kWBits = 13;
 constexpr int kW = 1 << kWBits;         // columns per tile
 constexpr uint32_t kColMask = kW - 1;
-constexpr uint32_t kCntMax = (1u << (32 - kWBits)) - 1u;  // 2^19 - 1
+constexpr uint32_t kCntMax = 65535u;    // largest count stored in a tile (wide entry)
 extern int64_t g_unit_entries;                           // ~512 KiB of payload per unit (hh_tune)
 constexpr int64_t kMaxBins = (int64_t)1 << 30;
 
+constexpr uint32_t kNarrowMax = 7;                        // counts stored as uint16
 inline int64_t pad4(int64_t x) { return (x + 3) & ~(int64_t)3; }
+
+// LDS image of a tile's bias values, XOR-rotated so that a wave reading
+// columns c, c+4, c+8, ... (one uint4 per lane on a dense row) hits 32
+// distinct 8-byte bank slots: element e = 32h + l is kept at 32h + ((l + h) mod 32).
+__host__ __device__ __forceinline__ uint32_t swz(uint32_t e) { return (e & ~31u) | ((e + (e >> 5)) & 31u); }
+__host__ __device__ __forceinline__ uint32_t unswz(uint32_t s) { return (s & ~31u) | (((s & 31u) - (s >> 5)) & 31u); }
+// entry encodings (c = column offset in the tile)
+__host__ __device__ __forceinline__ uint16_t enc_narrow(uint32_t c, uint32_t count) {
+    return (uint16_t)((swz(c) << 3) | count);
+}
+__host__ __device__ __forceinline__ uint32_t enc_wide(uint32_t c, uint32_t count) { return (count << 16) | (swz(c) << 3); }
+__host__ __device__ __forceinline__ uint32_t dec_col(uint32_t byteoff) { return unswz((byteoff & 0xFFFFu) >> 3); }
+inline int64_t pad8(int64_t x) { return (x + 7) & ~(int64_t)7; }
+constexpr int kBands = 5;        // lane-group widths 64, 32, 16, 8, 4
+constexpr int kBandSlots = 8;    // kBands + 1 bounds, padded
+// minimum row length (uint4 per row) of band g
+__host__ __device__ constexpr uint32_t band_min(int g) { return g == 0 ? 48u : g == 1 ? 24u : g == 2 ? 12u : g == 3 ? 6u : 1u; }
 
 // Host plan + arrays of the tiled layout.
 struct TilePlan {
@@ -38,8 +61,15 @@ struct TilePlan {
     int64_t nrb = 0;       // local row-blocks
     int32_t nJ = 0;        // column tiles over the whole matrix
     std::vector<int32_t> tile_J;      // per tile
-    std::vector<int64_t> tile_ent;    // per tile: first entry (multiple of 4)
-    std::vector<uint32_t> tile_rp;    // per tile: kR + 1 row offsets (relative)
+    std::vector<int64_t> tile_ent;    // per tile: first wide entry (multiple of 4)
+    std::vector<uint32_t> tile_rp;    // per tile: kR + 1 wide row offsets (relative)
+    std::vector<int64_t> tile_entn;   // per tile: first narrow entry (multiple of 8)
+    std::vector<uint32_t> tile_rpn;   // per tile: kR + 1 narrow row offsets (relative)
+    // per tile and segment (narrow, wide): rows ordered by decreasing length
+    // (uint4 count, counting sort on min(len, 255), stable) and the bands of
+    // that order swept with lane groups of 64/32/16/8/4 (kBands + 1 bounds)
+    std::vector<uint16_t> tile_perm;  // per tile: 2 x kR
+    std::vector<uint16_t> tile_band;  // per tile: 2 x kBandSlots
     std::vector<int32_t> tile_rb;     // per tile: local row-block
     std::vector<int32_t> blk_tile_ptr;  // nrb + 1
     std::vector<int32_t> tile_of;     // nrb * nJ -> tile index or -1
@@ -47,19 +77,27 @@ struct TilePlan {
     std::vector<int32_t> u_tlo, u_thi, u_rb, u_rlo, u_rhi, u_slot;
     std::vector<uint16_t> u_glo, u_ghi;
     std::vector<int32_t> blk_unit_ptr;  // nrb + 1
-    int64_t n_entries_padded = 0;
+    std::vector<int32_t> u_order;       // sweep order: units sorted by first column tile
+    std::vector<uint8_t> u_whole;       // 1: the unit covers whole row-blocks (sorted-band sweep)
+    int64_t n_entries_padded = 0;     // wide slots
+    int64_t n_narrow_padded = 0;      // narrow slots
     int64_t n_part = 0;
 };
 
-// Build the plan from per-(local row, tile) entry counts (row-major,
-// nloc x nJ, unpadded).  row_group: ICE group per local row.
-TilePlan plan_tiles(const uint16_t* cnt, int64_t nloc, int32_t nJ, const std::vector<uint16_t>& row_group);
+// Build the plan from per-(local row, tile) wide and narrow entry counts
+// (row-major, nloc x nJ, unpadded; cntn may be null).  row_group: ICE group
+// per local row.  Units are sized in 4-byte payload words.
+TilePlan plan_tiles(const uint16_t* cntw, const uint16_t* cntn, int64_t nloc, int32_t nJ,
+                    const std::vector<uint16_t>& row_group);
 
 struct TileDev {
     const uint32_t* pay;
+    const uint16_t* payn;
     const int32_t* tile_J;
     const long long* tile_ent;
     const uint32_t* tile_rp;
+    const long long* tile_entn;
+    const uint32_t* tile_rpn;
     const int32_t* u_tlo;
     const int32_t* u_thi;
     const int32_t* u_rb;
@@ -69,6 +107,10 @@ struct TileDev {
     const uint16_t* u_glo;
     const uint16_t* u_ghi;
     const int32_t* blk_unit_ptr;
+    const int32_t* u_order;
+    const uint16_t* tile_perm;
+    const uint16_t* tile_band;
+    const uint8_t* u_whole;
 };
 
 }  // namespace hh
@@ -81,13 +123,16 @@ struct hh_matrix {
     int64_t nnz_upper = 0;
     int64_t n_entries = 0;        // stored off-diagonal entries (both triangles)
     int64_t n_tiles = 0, n_units = 0, n_part = 0, n_wide = 0, nJ = 0, nrb = 0;
-    int64_t n_slots = 0;          // padded entries in tiles
+    int64_t n_slots = 0;          // padded wide (uint32) entries in tiles
+    int64_t n_slots_narrow = 0;   // padded narrow (uint16) entries in tiles
     hh::DBuf<uint32_t> pay;
+    hh::DBuf<uint16_t> payn;
     hh::DBuf<int32_t> tile_J, tile_rb;
-    hh::DBuf<long long> tile_ent;
-    hh::DBuf<uint32_t> tile_rp;
-    hh::DBuf<int32_t> u_tlo, u_thi, u_rb, u_rlo, u_rhi, u_slot, blk_unit_ptr, blk_tile_ptr;
-    hh::DBuf<uint16_t> u_glo, u_ghi;
+    hh::DBuf<long long> tile_ent, tile_entn;
+    hh::DBuf<uint32_t> tile_rp, tile_rpn;
+    hh::DBuf<int32_t> u_tlo, u_thi, u_rb, u_rlo, u_rhi, u_slot, blk_unit_ptr, blk_tile_ptr, u_order;
+    hh::DBuf<uint16_t> u_glo, u_ghi, tile_perm, tile_band;
+    hh::DBuf<uint8_t> u_whole;
     hh::DBuf<long long> wide_ptr;  // local rows + 1
     hh::DBuf<int32_t> wide_col;
     hh::DBuf<double> wide_cnt;
@@ -97,14 +142,16 @@ struct hh_matrix {
     hh::DBuf<uint16_t> row_group; // local rows: ICE group id
     int64_t nloc() const { return row_hi - row_lo; }
     size_t device_bytes() const {
-        return pay.bytes() + tile_J.bytes() + tile_rb.bytes() + tile_ent.bytes() + tile_rp.bytes() +
-               u_tlo.bytes() * 6 + blk_unit_ptr.bytes() + blk_tile_ptr.bytes() + u_glo.bytes() * 2 +
+        return pay.bytes() + payn.bytes() + tile_entn.bytes() + tile_rpn.bytes() + tile_J.bytes() +
+               tile_rb.bytes() + tile_ent.bytes() + tile_rp.bytes() +
+               u_tlo.bytes() * 7 + blk_unit_ptr.bytes() + tile_perm.bytes() + tile_band.bytes() + u_whole.bytes() + blk_tile_ptr.bytes() + u_glo.bytes() * 2 +
                wide_ptr.bytes() + wide_col.bytes() + wide_cnt.bytes() + diag.bytes() + row_nnz2.bytes() +
                row_sum2.bytes() + row_group.bytes();
     }
     hh::TileDev dev() const {
-        return hh::TileDev{pay.p, tile_J.p, tile_ent.p, tile_rp.p, u_tlo.p, u_thi.p, u_rb.p, u_rlo.p,
-                           u_rhi.p, u_slot.p, u_glo.p, u_ghi.p, blk_unit_ptr.p};
+        return hh::TileDev{pay.p, payn.p, tile_J.p, tile_ent.p, tile_rp.p, tile_entn.p, tile_rpn.p, u_tlo.p,
+                           u_thi.p, u_rb.p, u_rlo.p, u_rhi.p, u_slot.p, u_glo.p, u_ghi.p, blk_unit_ptr.p,
+                           u_order.p, tile_perm.p, tile_band.p, u_whole.p};
     }
 };
 

@@ -13,7 +13,8 @@ static thread_local std::string g_last_error;
 int64_t g_unit_entries = 0;  // 0 = auto (plan_tiles)
 void set_error(const std::string& msg) { g_last_error = msg; }
 
-TilePlan plan_tiles(const uint16_t* cnt, int64_t nloc, int32_t nJ, const std::vector<uint16_t>& row_group) {
+TilePlan plan_tiles(const uint16_t* cntw, const uint16_t* cntn, int64_t nloc, int32_t nJ,
+                    const std::vector<uint16_t>& row_group) {
     TilePlan P;
     P.nloc = nloc;
     P.nJ = nJ;
@@ -21,33 +22,69 @@ TilePlan plan_tiles(const uint16_t* cnt, int64_t nloc, int32_t nJ, const std::ve
     P.tile_of.assign((size_t)P.nrb * nJ, -1);
     P.blk_tile_ptr.assign(P.nrb + 1, 0);
     P.blk_unit_ptr.assign(P.nrb + 1, 0);
-    int64_t ent = 0;
-    std::vector<uint32_t> rp(kR + 1);
+    int64_t ent = 0, entn = 0;
+    std::vector<uint32_t> rp(kR + 1), rpn(kR + 1);
     for (int64_t rb = 0; rb < P.nrb; ++rb) {
         P.blk_tile_ptr[rb] = (int32_t)P.tile_J.size();
         const int64_t r0 = rb * kR, r1 = std::min<int64_t>(nloc, r0 + kR);
         for (int32_t J = 0; J < nJ; ++J) {
-            rp[0] = 0;
+            rp[0] = rpn[0] = 0;
             for (int k = 0; k < kR; ++k) {
                 const int64_t r = r0 + k;
-                const uint32_t c = r < r1 ? (uint32_t)pad4(cnt[r * nJ + J]) : 0u;
-                rp[k + 1] = rp[k] + c;
+                const uint32_t cw = r < r1 ? (uint32_t)pad4(cntw[r * nJ + J]) : 0u;
+                const uint32_t cn = (r < r1 && cntn) ? (uint32_t)pad8(cntn[r * nJ + J]) : 0u;
+                rp[k + 1] = rp[k] + cw;
+                rpn[k + 1] = rpn[k] + cn;
             }
-            if (rp[kR] == 0) continue;
+            if (rp[kR] == 0 && rpn[kR] == 0) continue;
             P.tile_of[rb * nJ + J] = (int32_t)P.tile_J.size();
             P.tile_J.push_back(J);
             P.tile_ent.push_back(ent);
+            P.tile_entn.push_back(entn);
             P.tile_rb.push_back((int32_t)rb);
             P.tile_rp.insert(P.tile_rp.end(), rp.begin(), rp.end());
+            P.tile_rpn.insert(P.tile_rpn.end(), rpn.begin(), rpn.end());
+            // sorted-band order of both segments (narrow first)
+            for (int seg = 0; seg < 2; ++seg) {
+                const std::vector<uint32_t>& q = seg == 0 ? rpn : rp;
+                const int sh = seg == 0 ? 3 : 2;
+                uint32_t key[kR];
+                int hist[257] = {0};
+                for (int k = 0; k < kR; ++k) {
+                    const uint32_t len = (q[k + 1] - q[k]) >> sh;
+                    key[k] = 255u - std::min<uint32_t>(len, 255u);  // descending
+                    ++hist[key[k] + 1];
+                }
+                for (int k = 0; k < 256; ++k) hist[k + 1] += hist[k];
+                uint16_t perm[kR];
+                for (int k = 0; k < kR; ++k) perm[hist[key[k]]++] = (uint16_t)k;
+                P.tile_perm.insert(P.tile_perm.end(), perm, perm + kR);
+                uint16_t band[kBandSlots] = {0};
+                int pos = 0;
+                for (int g = 0; g < kBands; ++g) {
+                    while (pos < kR && ((q[perm[pos] + 1] - q[perm[pos]]) >> sh) >= band_min(g)) ++pos;
+                    band[g + 1] = (uint16_t)pos;
+                }
+                P.tile_band.insert(P.tile_band.end(), band, band + kBandSlots);
+            }
             ent += rp[kR];
+            entn += rpn[kR];
         }
     }
     P.blk_tile_ptr[P.nrb] = (int32_t)P.tile_J.size();
     P.n_entries_padded = ent;
+    P.n_narrow_padded = entn;
     // units: ~4 MiB of payload each on big matrices (measured best on C4),
     // but at least ~4096 units so small matrices still fill 256 CUs.
+    // Sizes in 4-byte payload words (a narrow entry is half a word).
+    const int64_t words = ent + entn / 2;
     const int64_t unit_cap = g_unit_entries > 0 ? g_unit_entries
-                                                : std::max<int64_t>(1 << 15, std::min<int64_t>(1 << 20, ent / 4096));
+                                                : std::max<int64_t>(1 << 15, std::min<int64_t>(1 << 20, words / 4096));
+    auto tile_words = [&](int32_t t, int k0, int k1) -> int64_t {
+        const uint32_t* a = &P.tile_rp[(size_t)t * (kR + 1)];
+        const uint32_t* b = &P.tile_rpn[(size_t)t * (kR + 1)];
+        return (int64_t)(a[k1] - a[k0]) + (int64_t)(b[k1] - b[k0]) / 2;
+    };
     auto emit = [&](int64_t rb, int32_t ta, int32_t tb, int32_t rlo, int32_t rhi) {
         const int64_t g0 = rb * kR + rlo, g1 = rb * kR + rhi - 1;
         P.u_tlo.push_back(ta);
@@ -56,6 +93,7 @@ TilePlan plan_tiles(const uint16_t* cnt, int64_t nloc, int32_t nJ, const std::ve
         P.u_rlo.push_back(rlo);
         P.u_rhi.push_back(rhi);
         P.u_slot.push_back((int32_t)P.n_part);
+        P.u_whole.push_back(rlo == 0 && rhi == (int32_t)(std::min<int64_t>(nloc, rb * kR + kR) - rb * kR) ? 1 : 0);
         P.u_glo.push_back(row_group[g0]);
         P.u_ghi.push_back(row_group[g1]);
         P.n_part += rhi - rlo;
@@ -67,14 +105,13 @@ TilePlan plan_tiles(const uint16_t* cnt, int64_t nloc, int32_t nJ, const std::ve
         int32_t cur = ta;
         int64_t cur_sz = 0;
         for (int32_t t = ta; t < tb; ++t) {
-            const uint32_t* trp = &P.tile_rp[(size_t)t * (kR + 1)];
-            const int64_t sz = trp[kR];
+            const int64_t sz = tile_words(t, 0, kR);
             if (sz > unit_cap) {
                 if (cur < t) emit(rb, cur, t, 0, nr);
                 int32_t rlo = 0;
                 int64_t acc = 0;
                 for (int32_t k = 0; k < nr; ++k) {
-                    const int64_t len = trp[k + 1] - trp[k];
+                    const int64_t len = tile_words(t, k, k + 1);
                     if (acc > 0 && acc + len > unit_cap) {
                         emit(rb, t, t + 1, rlo, k);
                         rlo = k;
@@ -97,6 +134,10 @@ TilePlan plan_tiles(const uint16_t* cnt, int64_t nloc, int32_t nJ, const std::ve
         if (cur < tb) emit(rb, cur, tb, 0, nr);
     }
     P.blk_unit_ptr[P.nrb] = (int32_t)P.u_tlo.size();
+    P.u_order.resize(P.u_tlo.size());
+    std::iota(P.u_order.begin(), P.u_order.end(), 0);
+    std::stable_sort(P.u_order.begin(), P.u_order.end(),
+                     [&](int32_t x, int32_t y) { return P.tile_J[P.u_tlo[x]] < P.tile_J[P.u_tlo[y]]; });
     if (P.n_part > INT32_MAX || P.tile_J.size() > (size_t)INT32_MAX) HH_THROW(HH_ERR_ARG, "plan too large");
     return P;
 }
@@ -108,11 +149,15 @@ void upload_plan(const TilePlan& P, hh_matrix& m, hipStream_t s) {
     m.n_units = (int64_t)P.u_tlo.size();
     m.n_part = P.n_part;
     m.n_slots = P.n_entries_padded;
+    m.n_slots_narrow = P.n_narrow_padded;
     m.tile_J = to_device(P.tile_J, s);
     m.tile_rb = to_device(P.tile_rb, s);
     std::vector<long long> te(P.tile_ent.begin(), P.tile_ent.end());
     m.tile_ent = to_device(te, s);
     m.tile_rp = to_device(P.tile_rp, s);
+    std::vector<long long> ten(P.tile_entn.begin(), P.tile_entn.end());
+    m.tile_entn = to_device(ten, s);
+    m.tile_rpn = to_device(P.tile_rpn, s);
     m.blk_tile_ptr = to_device(P.blk_tile_ptr, s);
     m.u_tlo = to_device(P.u_tlo, s);
     m.u_thi = to_device(P.u_thi, s);
@@ -123,6 +168,10 @@ void upload_plan(const TilePlan& P, hh_matrix& m, hipStream_t s) {
     m.u_glo = to_device(P.u_glo, s);
     m.u_ghi = to_device(P.u_ghi, s);
     m.blk_unit_ptr = to_device(P.blk_unit_ptr, s);
+    m.u_order = to_device(P.u_order, s);
+    m.tile_perm = to_device(P.tile_perm, s);
+    m.tile_band = to_device(P.tile_band, s);
+    m.u_whole = to_device(P.u_whole, s);
     HIP_CHECK(hipStreamSynchronize(s));  // the plan's host vectors may die after return
 }
 
@@ -196,7 +245,7 @@ int hh_matrix_from_pixels(const int64_t* bin1, const int64_t* bin2, const double
         HH_REQUIRE(n_bins < kMaxBins, "n_bins must be < 2^30");
         HH_REQUIRE(0 <= row_lo && row_lo <= row_hi && row_hi <= n_bins, "bad row range");
         HH_REQUIRE(row_lo % kR == 0 && (row_hi % kR == 0 || row_hi == n_bins),
-                   "shard rows must be aligned to 256-row blocks");
+                   "shard rows must be aligned to 512-row blocks");
         HH_REQUIRE(chrom_offsets[0] == 0 && chrom_offsets[n_chroms] == n_bins, "chrom_offsets must span [0, n_bins]");
         HH_REQUIRE(n_chroms < 65535, "too many chromosomes");
         HH_REQUIRE(ignore_diags >= 0, "ignore_diags must be >= 0");
@@ -274,28 +323,31 @@ int hh_matrix_from_pixels(const int64_t* bin1, const int64_t* bin2, const double
             std::stable_sort(tmp.begin(), tmp.end(), [](auto& x, auto& y) { return x.first < y.first; });
             for (int64_t k = lo; k < hi; ++k) { cols[k] = tmp[k - lo].first; vals[k] = tmp[k - lo].second; }
         }
-        // tile counts (entries with count > kCntMax go to the wide list)
+        // tile counts: narrow (count <= 7) and wide entries per (row, tile);
+        // counts > kCntMax go to the wide list
         const int32_t nJ = (int32_t)((n_bins + kW - 1) / kW);
-        std::vector<uint16_t> cnt((size_t)nloc * nJ, 0);
+        std::vector<uint16_t> cntw((size_t)nloc * nJ, 0), cntn((size_t)nloc * nJ, 0);
         std::vector<long long> wptr(nloc + 1, 0);
         for (int64_t r = 0; r < nloc; ++r) {
             for (int64_t k = deg[r]; k < deg[r + 1]; ++k) {
                 if (vals[k] > kCntMax) ++wptr[r + 1];
-                else ++cnt[(size_t)r * nJ + (cols[k] >> kWBits)];
+                else if (vals[k] <= kNarrowMax) ++cntn[(size_t)r * nJ + (cols[k] >> kWBits)];
+                else ++cntw[(size_t)r * nJ + (cols[k] >> kWBits)];
             }
         }
         for (int64_t r = 0; r < nloc; ++r) wptr[r + 1] += wptr[r];
         std::vector<uint16_t> bg = bin_groups(*m);
         std::vector<uint16_t> rgroup(bg.begin() + row_lo, bg.begin() + row_hi);
-        TilePlan P = plan_tiles(cnt.data(), nloc, nJ, rgroup);
-        // fill payload + wide list
+        TilePlan P = plan_tiles(cntw.data(), cntn.data(), nloc, nJ, rgroup);
+        // fill payloads + wide list
         std::vector<uint32_t> pay(P.n_entries_padded, 0u);
+        std::vector<uint16_t> payn(P.n_narrow_padded, 0u);
         std::vector<int32_t> wcol(wptr[nloc]);
         std::vector<double> wcnt(wptr[nloc]);
         for (int64_t r = 0; r < nloc; ++r) {
             const int64_t rb = r / kR, k = r % kR;
             int32_t curJ = -1;
-            int64_t pos = 0;
+            int64_t pos = 0, posn = 0;
             int64_t wp = wptr[r];
             for (int64_t q = deg[r]; q < deg[r + 1]; ++q) {
                 if (vals[q] > kCntMax) { wcol[wp] = cols[q]; wcnt[wp++] = vals[q]; continue; }
@@ -303,13 +355,16 @@ int hh_matrix_from_pixels(const int64_t* bin1, const int64_t* bin2, const double
                 if (J != curJ) {
                     const int32_t t = P.tile_of[rb * nJ + J];
                     pos = P.tile_ent[t] + P.tile_rp[(size_t)t * (kR + 1) + k];
+                    posn = P.tile_entn[t] + P.tile_rpn[(size_t)t * (kR + 1) + k];
                     curJ = J;
                 }
-                pay[pos++] = (vals[q] << kWBits) | ((uint32_t)cols[q] & kColMask);
+                if (vals[q] <= kNarrowMax) payn[posn++] = enc_narrow((uint32_t)cols[q] & kColMask, vals[q]);
+                else pay[pos++] = enc_wide((uint32_t)cols[q] & kColMask, vals[q]);
             }
         }
         upload_plan(P, *m, s);
         m->pay = to_device(pay, s);
+        m->payn = to_device(payn, s);
         m->wide_ptr = to_device(wptr, s);
         m->wide_col = to_device(wcol, s);
         m->wide_cnt = to_device(wcnt, s);
@@ -345,6 +400,8 @@ int hh_matrix_get_info(const hh_matrix* m, hh_matrix_info* info) {
         info->n_units = m->n_units;
         info->n_wide = m->n_wide;
         info->device_bytes = (int64_t)m->device_bytes();
+        info->n_slots_narrow = m->n_slots_narrow;
+        info->payload_bytes = 4 * m->n_slots + 2 * m->n_slots_narrow;
         info->n_chroms = m->n_chroms;
         info->ignore_diags = m->ignore_diags;
         info->cis_only = m->cis_only;
@@ -359,9 +416,13 @@ int hh_matrix_export_upper(const hh_matrix* m, int64_t* bin1, int64_t* bin2, dou
         HIP_CHECK(hipSetDevice(m->device));
         const int64_t nloc = m->nloc();
         HIP_CHECK(hipDeviceSynchronize());
-        std::vector<uint32_t> pay(m->pay.n), rp(m->tile_rp.n);
+        std::vector<uint32_t> pay(m->pay.n), rp(m->tile_rp.n), rpn(m->tile_rpn.n);
+        std::vector<uint16_t> payn(m->payn.n);
         std::vector<int32_t> tJ(m->tile_J.n), trb(m->tile_rb.n), wcol(m->wide_col.n);
-        std::vector<long long> tent(m->tile_ent.n), wptr(m->wide_ptr.n);
+        std::vector<long long> tent(m->tile_ent.n), tentn(m->tile_entn.n), wptr(m->wide_ptr.n);
+        m->payn.download(payn.data(), payn.size(), 0);
+        m->tile_rpn.download(rpn.data(), rpn.size(), 0);
+        m->tile_entn.download(tentn.data(), tentn.size(), 0);
         std::vector<double> wcnt(m->wide_cnt.n), diag(nloc);
         m->pay.download(pay.data(), pay.size(), 0);
         m->tile_rp.download(rp.data(), rp.size(), 0);
@@ -376,13 +437,20 @@ int hh_matrix_export_upper(const hh_matrix* m, int64_t* bin1, int64_t* bin2, dou
         std::vector<std::vector<std::pair<int64_t, double>>> rows(nloc);
         for (size_t t = 0; t < tJ.size(); ++t) {
             const uint32_t* trp = &rp[t * (kR + 1)];
+            const uint32_t* trpn = &rpn[t * (kR + 1)];
             for (int k = 0; k < kR; ++k) {
                 const int64_t r = (int64_t)trb[t] * kR + k;
                 for (uint32_t q = trp[k]; q < trp[k + 1]; ++q) {
                     const uint32_t e = pay[tent[t] + q];
-                    const uint32_t c = e >> kWBits;
+                    const uint32_t c = e >> 16;
                     if (!c) continue;
-                    rows[r].emplace_back((int64_t)tJ[t] * kW + (e & kColMask), (double)c);
+                    rows[r].emplace_back((int64_t)tJ[t] * kW + dec_col(e), (double)c);
+                }
+                for (uint32_t q = trpn[k]; q < trpn[k + 1]; ++q) {
+                    const uint32_t e = payn[tentn[t] + q];
+                    const uint32_t c = e & 7u;
+                    if (!c) continue;
+                    rows[r].emplace_back((int64_t)tJ[t] * kW + dec_col(e), (double)c);
                 }
             }
         }

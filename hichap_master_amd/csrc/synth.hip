@@ -4,7 +4,7 @@
 //
 // Model: cis lambda(i,j) = A (|i-j|+1)^-decay
 // (1 + c s_i s_j) v_i v_j, counts ~ Poisson(lambda) (inversion below 16,
-// normal approximation above; clamped to 2^19 - 1 so every entry fits a
+// normal approximation above; clamped to 65535 so every entry fits a
 // tile slot); trans pixels uniform with density p * v_i v_j, count 1 or 2.
 // Every draw is a pure function of (seed, min(i,j), max(i,j)), so row i's
 // lower half equals column i's upper half and every shard of every rank sees
@@ -86,14 +86,29 @@ __device__ __forceinline__ uint32_t synth_count(const SynthDev& p, long long i, 
     return (mix64(h) & 3u) == 0u ? 2u : 1u;
 }
 
-// PASS 0: cnt[w * nJ + J] = entries of row w in tile J; per-row stats.
-// PASS 1: write entries at tile_ent[t] + tile_rp[t][k] (t = tile_of[rb][J]).
+// PASS 0: cnt[w * nJ + J] / cntn[...] = wide / narrow entries of row w in
+//         tile J; per-row stats.
+// PASS 1: write entries at tile_ent[t] + tile_rp[t][k] (wide) and
+//         tile_entn[t] + tile_rpn[t][k] (narrow), t = tile_of[rb][J].
+struct SynthOut {
+    uint16_t* cnt;
+    uint16_t* cntn;
+    int32_t* row_work;
+    long long* row_upper;
+    double* diag;
+    double* row_nnz2;
+    double* row_sum2;
+    const int32_t* tile_of;
+    const long long* tile_ent;
+    const uint32_t* tile_rp;
+    const long long* tile_entn;
+    const uint32_t* tile_rpn;
+    uint32_t* pay;
+    uint16_t* payn;
+};
+
 template <int PASS>
-__global__ __launch_bounds__(256) void k_synth_rows(SynthDev p, long long row_lo, long long nrows,
-                                                    uint16_t* cnt, int32_t* row_work, long long* row_upper,
-                                                    double* diag, double* row_nnz2, double* row_sum2,
-                                                    const int32_t* tile_of, const long long* tile_ent,
-                                                    const uint32_t* tile_rp, uint32_t* pay) {
+__global__ __launch_bounds__(256) void k_synth_rows(SynthDev p, long long row_lo, long long nrows, SynthOut o) {
     const long long w = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     if (w >= nrows) return;
     const int lane = threadIdx.x & 63;
@@ -106,17 +121,21 @@ __global__ __launch_bounds__(256) void k_synth_rows(SynthDev p, long long row_lo
     const unsigned long long lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     long long upper = 0, nnz = 0, work = 0, sum_lane = 0;
     int curJ = -1;
-    long long tcount = 0;   // entries of the current tile
-    long long pos = 0;      // PASS 1: next write position
+    long long tw = 0, tn = 0;      // wide / narrow entries of the current tile
+    long long pos = 0, posn = 0;   // PASS 1: next write positions
     auto flush = [&]() {
         if (curJ < 0) return;
         if (PASS == 0) {
-            if (lane == 0 && cnt) cnt[w * p.nJ + curJ] = (uint16_t)tcount;
+            if (lane == 0 && o.cnt) {
+                o.cnt[w * p.nJ + curJ] = (uint16_t)tw;
+                o.cntn[w * p.nJ + curJ] = (uint16_t)tn;
+            }
         } else {
-            const long long padded = (tcount + 3) & ~3LL;
-            for (long long q = tcount + lane; q < padded; q += 64) pay[pos - tcount + q] = 0u;
+            const long long pw = (tw + 3) & ~3LL, pn = (tn + 7) & ~7LL;
+            for (long long q = tw + lane; q < pw; q += 64) o.pay[pos - tw + q] = 0u;
+            for (long long q = tn + lane; q < pn; q += 64) o.payn[posn - tn + q] = 0u;
         }
-        work += (tcount + 3) & ~3LL;
+        work += ((tw + 3) & ~3LL) + ((tn + 7) & ~7LL) / 2;  // 4-byte words
     };
     for (long long j0 = jlo & ~63LL; j0 < jhi; j0 += 64) {
         const long long j = j0 + lane;
@@ -128,18 +147,25 @@ __global__ __launch_bounds__(256) void k_synth_rows(SynthDev p, long long row_lo
         if (J != curJ) {
             flush();
             curJ = J;
-            tcount = 0;
+            tw = tn = 0;
             if (PASS == 1) {
-                const int t = tile_of[rb * p.nJ + J];
-                pos = tile_ent[t] + tile_rp[(size_t)t * (kR + 1) + k];
+                const int t = o.tile_of[rb * p.nJ + J];
+                pos = o.tile_ent[t] + o.tile_rp[(size_t)t * (kR + 1) + k];
+                posn = o.tile_entn[t] + o.tile_rpn[(size_t)t * (kR + 1) + k];
             }
         }
-        const int rank = __popcll(mask & lt_mask);
-        if (PASS == 1 && kc > 0) pay[pos + rank] = (kc << kWBits) | ((uint32_t)j & kColMask);
-        const int nk = __popcll(mask);
-        tcount += nk;
-        pos += nk;
-        nnz += nk;
+        const bool narrow = kc > 0 && kc <= kNarrowMax;
+        const unsigned long long mn = __ballot(narrow), mw = mask & ~mn;
+        if (PASS == 1) {
+            if (narrow) o.payn[posn + __popcll(mn & lt_mask)] = enc_narrow((uint32_t)j & kColMask, kc);
+            else if (kc > 0) o.pay[pos + __popcll(mw & lt_mask)] = enc_wide((uint32_t)j & kColMask, kc);
+        }
+        const int nn = __popcll(mn), nw = __popcll(mw);
+        tn += nn;
+        tw += nw;
+        posn += nn;
+        pos += nw;
+        nnz += nn + nw;
         upper += __popcll(__ballot(kc > 0 && j > r));
         sum_lane += kc;
     }
@@ -147,12 +173,12 @@ __global__ __launch_bounds__(256) void k_synth_rows(SynthDev p, long long row_lo
     const long long s = wave_sum_ll(sum_lane);
     const uint32_t dg = p.ignore_diags == 0 ? synth_count(p, r, r) : 0u;
     if (lane == 0) {
-        if (row_work) row_work[w] = (int32_t)work;
-        if (row_upper) row_upper[w] = upper + (dg ? 1 : 0);
-        if (diag) {
-            diag[w] = (double)dg;
-            row_nnz2[w] = (double)nnz + (dg ? 2.0 : 0.0);
-            row_sum2[w] = (double)s + 2.0 * (double)dg;
+        if (o.row_work) o.row_work[w] = (int32_t)work;
+        if (o.row_upper) o.row_upper[w] = upper + (dg ? 1 : 0);
+        if (o.diag) {
+            o.diag[w] = (double)dg;
+            o.row_nnz2[w] = (double)nnz + (dg ? 2.0 : 0.0);
+            o.row_sum2[w] = (double)s + 2.0 * (double)dg;
         }
     }
 }
@@ -237,8 +263,10 @@ int hh_synth_count(const hh_synth_params* p, int32_t* row_work, int64_t* row_nnz
         const int64_t n = h.dev.n;
         DBuf<int32_t> rw(n);
         DBuf<long long> ru(n);
-        hipLaunchKernelGGL((k_synth_rows<0>), row_grid(n), dim3(256), 0, s, h.dev, 0LL, (long long)n, nullptr, rw.p,
-                           ru.p, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
+        SynthOut o{};
+        o.row_work = rw.p;
+        o.row_upper = ru.p;
+        hipLaunchKernelGGL((k_synth_rows<0>), row_grid(n), dim3(256), 0, s, h.dev, 0LL, (long long)n, o);
         HIP_CHECK(hipGetLastError());
         rw.download(row_work, n, s);
         HIP_CHECK(hipMemcpyAsync(row_nnz_upper, ru.p, n * sizeof(int64_t), hipMemcpyDeviceToHost, s));
@@ -254,7 +282,7 @@ int hh_synth_build(const hh_synth_params* p, int64_t row_lo, int64_t row_hi, voi
         synth_setup(p, h, s);
         const int64_t n = h.dev.n;
         HH_REQUIRE(0 <= row_lo && row_lo <= row_hi && row_hi <= n, "bad row range");
-        HH_REQUIRE(row_lo % kR == 0 && (row_hi % kR == 0 || row_hi == n), "shard rows must be aligned to 256-row blocks");
+        HH_REQUIRE(row_lo % kR == 0 && (row_hi % kR == 0 || row_hi == n), "shard rows must be aligned to 512-row blocks");
         const int64_t nloc = row_hi - row_lo;
         const int nJ = h.dev.nJ;
         auto m = std::make_unique<hh_matrix>();
@@ -269,38 +297,59 @@ int hh_synth_build(const hh_synth_params* p, int64_t row_lo, int64_t row_hi, voi
         m->diag.alloc(nloc);
         m->row_nnz2.alloc(nloc);
         m->row_sum2.alloc(nloc);
-        DBuf<uint16_t> cnt((size_t)nloc * nJ);
+        DBuf<uint16_t> cnt((size_t)nloc * nJ), cntn((size_t)nloc * nJ);
         cnt.zero(s);
+        cntn.zero(s);
         DBuf<long long> rup(nloc);
-        if (nloc)
-            hipLaunchKernelGGL((k_synth_rows<0>), row_grid(nloc), dim3(256), 0, s, h.dev, (long long)row_lo,
-                               (long long)nloc, cnt.p, nullptr, rup.p, m->diag.p, m->row_nnz2.p, m->row_sum2.p,
-                               nullptr, nullptr, nullptr, nullptr);
+        {
+            SynthOut o{};
+            o.cnt = cnt.p;
+            o.cntn = cntn.p;
+            o.row_upper = rup.p;
+            o.diag = m->diag.p;
+            o.row_nnz2 = m->row_nnz2.p;
+            o.row_sum2 = m->row_sum2.p;
+            if (nloc)
+                hipLaunchKernelGGL((k_synth_rows<0>), row_grid(nloc), dim3(256), 0, s, h.dev, (long long)row_lo,
+                                   (long long)nloc, o);
+        }
         HIP_CHECK(hipGetLastError());
-        std::vector<uint16_t> hc((size_t)nloc * nJ);
+        std::vector<uint16_t> hc((size_t)nloc * nJ), hn((size_t)nloc * nJ);
         cnt.download(hc.data(), hc.size(), s);
+        cntn.download(hn.data(), hn.size(), s);
         std::vector<long long> up(nloc);
         rup.download(up.data(), nloc, s);
         HIP_CHECK(hipStreamSynchronize(s));
         cnt.release();
+        cntn.release();
         std::vector<uint16_t> bg = bin_groups(*m);
         std::vector<uint16_t> rgroup(bg.begin() + row_lo, bg.begin() + row_hi);
-        TilePlan P = plan_tiles(hc.data(), nloc, nJ, rgroup);
+        TilePlan P = plan_tiles(hc.data(), hn.data(), nloc, nJ, rgroup);
         upload_plan(P, *m, s);
         m->row_group = to_device(rgroup, s);
         DBuf<int32_t> tof = to_device(P.tile_of, s);
         m->pay.alloc(P.n_entries_padded);
-        if (nloc)
-            hipLaunchKernelGGL((k_synth_rows<1>), row_grid(nloc), dim3(256), 0, s, h.dev, (long long)row_lo,
-                               (long long)nloc, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, tof.p,
-                               m->tile_ent.p, m->tile_rp.p, m->pay.p);
+        m->payn.alloc(P.n_narrow_padded);
+        {
+            SynthOut o{};
+            o.tile_of = tof.p;
+            o.tile_ent = m->tile_ent.p;
+            o.tile_rp = m->tile_rp.p;
+            o.tile_entn = m->tile_entn.p;
+            o.tile_rpn = m->tile_rpn.p;
+            o.pay = m->pay.p;
+            o.payn = m->payn.p;
+            if (nloc)
+                hipLaunchKernelGGL((k_synth_rows<1>), row_grid(nloc), dim3(256), 0, s, h.dev, (long long)row_lo,
+                                   (long long)nloc, o);
+        }
         HIP_CHECK(hipGetLastError());
         std::vector<long long> wz(nloc + 1, 0);  // no wide entries (counts clamped)
         m->wide_ptr = to_device(wz, s);
         HIP_CHECK(hipStreamSynchronize(s));
         m->nnz_upper = std::accumulate(up.begin(), up.end(), 0LL);
         int64_t ent = 0;
-        for (size_t i = 0; i < hc.size(); ++i) ent += hc[i];
+        for (size_t i = 0; i < hc.size(); ++i) ent += (int64_t)hc[i] + hn[i];
         m->n_entries = ent;
         *out = m.release();
     });

@@ -23,7 +23,7 @@ from __future__ import annotations
 import numpy as np
 
 
-ROW_BLOCK = 256  # shards are whole 256-row blocks of the tiled layout
+ROW_BLOCK = 512  # shards are whole 512-row blocks of the tiled layout
 
 
 def partition_rows(row_weight, world: int, align: int = ROW_BLOCK) -> np.ndarray:

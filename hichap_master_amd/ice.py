@@ -71,7 +71,7 @@ class ContactMatrix:
     @classmethod
     def synthetic(cls, chrom_nbins, row_range=None, stream=None, **kw):
         """Generate a synthetic genome in HBM (see synth_params); rows
-        ``row_range`` (aligned to 256-row blocks) or all."""
+        ``row_range`` (aligned to 512-row blocks) or all."""
         _lib.require_gpu()
         p, keep = synth_params(chrom_nbins, **kw)
         n = int(np.sum(chrom_nbins))

@@ -56,12 +56,13 @@ int hh_ktime_reset(void);
 /* ---------------------------------------------------- contact matrix
  * A contact matrix resident in HBM in the "tiled pixel" layout:
  * the symmetric matrix (both triangles of cooler's upper-triangle pixel table)
- * for the rows [row_lo, row_hi) a rank owns, cut into 256-row blocks x
- * 8192-column tiles; each tile stores its rows' entries as uint32
- * (count << 13 | column offset), rows padded to 16 B, counts >= 2^19 in a
- * small per-row wide list, plus a per-row diagonal.  Static filters
+ * for the rows [row_lo, row_hi) a rank owns, cut into 512-row blocks x
+ * 8192-column tiles; each tile stores its rows' entries as uint16
+ * (count << 13 | column offset, counts 1..7) and uint32 (counts 8..2^19-1)
+ * segments, rows padded to 16 B, counts >= 2^19 in a small per-row wide
+ * list, plus a per-row diagonal.  Static filters
  * (ignore_diags, cis_only zero_trans, zero counts) are applied at build time.
- * Shards are whole 256-row blocks (row_lo % 256 == 0).
+ * Shards are whole 512-row blocks (row_lo % 512 == 0).
  */
 typedef struct hh_matrix hh_matrix;
 
@@ -75,6 +76,8 @@ typedef struct {
     int64_t n_units;       /* sweep work units                               */
     int64_t n_wide;        /* entries with count >= 2^19 (wide list)         */
     int64_t device_bytes;  /* HBM held by the matrix                         */
+    int64_t n_slots_narrow;/* stored uint16 slots (entries + row padding)    */
+    int64_t payload_bytes; /* entry bytes streamed per sweep (both widths)   */
     int32_t n_chroms;
     int32_t ignore_diags;
     int32_t cis_only;
@@ -125,7 +128,7 @@ int hh_synth_count(const hh_synth_params* p, int32_t* row_work, int64_t* row_nnz
  * float64 counts into device memory out[N_c * N_c] (bench inputs for the
  * per-chromosome compartment config C5; ignore_diags applies). */
 int hh_synth_dense(const hh_synth_params* p, int32_t chrom, double* out, void* stream);
-/* Build rows [row_lo, row_hi) (row_lo % 256 == 0). */
+/* Build rows [row_lo, row_hi) (row_lo % 512 == 0). */
 int hh_synth_build(const hh_synth_params* p, int64_t row_lo, int64_t row_hi, void* stream,
                    hh_matrix** out);
 

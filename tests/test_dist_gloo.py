@@ -15,7 +15,7 @@ def test_partition_rows_aligned_and_balanced():
     w = np.random.default_rng(0).integers(0, 100, size=5000)
     rr = dist.partition_rows(w, 4)
     assert rr[0] == 0 and rr[-1] == 5000
-    assert all(x % 256 == 0 for x in rr[1:-1])
+    assert all(x % dist.ROW_BLOCK == 0 for x in rr[1:-1])
     assert np.all(np.diff(rr) >= 0)
     loads = [w[a:b].sum() for a, b in zip(rr[:-1], rr[1:])]
     assert max(loads) < 1.35 * (w.sum() / 4)

@@ -165,13 +165,16 @@ def test_synthetic_generator_matches_oracle(ice):
     assert (b2 - b1 >= 1).all()
     # symmetric storage: every pixel appears in both rows -> entries = 2 * pixels
     assert inf["n_entries"] == 2 * b1.size
-    assert inf["n_slots"] >= inf["n_entries"] and inf["n_slots"] % 4 == 0
+    assert inf["n_slots"] + inf["n_slots_narrow"] >= inf["n_entries"]
+    assert inf["n_slots"] % 4 == 0 and inf["n_slots_narrow"] % 8 == 0
+    assert inf["payload_bytes"] == 4 * inf["n_slots"] + 2 * inf["n_slots_narrow"]
+    assert inf["n_slots_narrow"] > 0  # low counts are stored as uint16
     # shards see the same matrix
     rc, ru = ice.synth_row_counts(sizes, **kw)
     assert ru.sum() == b1.size
-    half = ice.ContactMatrix.synthetic(sizes, row_range=(0, 768), **kw)
+    half = ice.ContactMatrix.synthetic(sizes, row_range=(0, 1024), **kw)
     h1, h2, hc = half.export_upper()
-    sel = b1 < 768
+    sel = b1 < 1024
     np.testing.assert_array_equal(h1, b1[sel]); np.testing.assert_array_equal(h2, b2[sel])
     np.testing.assert_array_equal(hc, c[sel])
     off = m.chrom_offsets

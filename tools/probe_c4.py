@@ -31,6 +31,6 @@ for ue in units:
             ms, n, it_ms = st.last_timing()
             sw = ms / n
             print(f"  abl={abl} nb={nb}: sweep {sw:.3f} ms  it/s {1000*n/it_ms:.1f}  "
-                  f"alg {12.0*inf['nnz_upper']/sw/1e6:.0f} GB/s  real {4.0*inf['n_slots']/sw/1e6:.0f} GB/s", flush=True)
+                  f"alg {12.0*inf['nnz_upper']/sw/1e6:.0f} GB/s  real {inf['payload_bytes']/sw/1e6:.0f} GB/s", flush=True)
     tune("sweep_ablate", 0); tune("sweep_nb", 4)
     st.close(); m.close()

@@ -31,7 +31,7 @@ def run(label):
     ms, n, it_ms = st.last_timing()
     sw = ms / n
     alg = 12.0 * inf["nnz_upper"]
-    real = 4.0 * inf["n_slots"]
+    real = float(inf["payload_bytes"])
     print(f"  {label:28s} sweep {sw:.3f} ms  iter {it_ms/n:.3f} ms  it/s {1000*n/it_ms:.1f}  "
           f"alg {alg/sw/1e6:.0f} GB/s  real {real/sw/1e6:.0f} GB/s", flush=True)
 
