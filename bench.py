@@ -302,11 +302,35 @@ def main():
         dist.iterate(st, ex, args.steps)
         barrier()
         elapsed = time.perf_counter() - t_start
-        sweep_ms, launches, iter_ms = float("nan"), 0, float("nan")
+        # sweep-kernel timing: a few more iterations with the HIP-event
+        # registry on (after the timed region; events cost ~µs per launch)
+        n_prof = max(1, min(args.steps, 5))
+        _lib.call("hh_ktime_reset")
+        _lib.call("hh_ktime_enable", 1)
+        t_it = time.perf_counter()
+        dist.iterate(st, ex, n_prof)
+        torch.cuda.synchronize()
+        iter_ms = 1000.0 * (time.perf_counter() - t_it)
+        _lib.call("hh_ktime_enable", 0)
+        sweep_ms, launches = _lib.ktime("k_sweep_tiled")
+        _lib.call("hh_ktime_reset")
     tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
     if torch.distributed.is_initialized():
         torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
     elapsed = float(tt.item())
+
+    # the slowest rank's sweep bounds the iteration: report its shard
+    # a shard stores both triangles of its rows: its share of the 12 B/pixel
+    # algorithmic traffic is half its stored entries (= nnz_upper at N=1)
+    shard_pix = float(inf["nnz_upper"]) if world == 1 else 0.5 * float(inf["n_entries"])
+    shard = torch.tensor([sweep_ms / max(launches, 1), shard_pix,
+                          float(inf["payload_bytes"]) + 8.0 * 513 * inf["n_tiles"]],
+                         dtype=torch.float64, device="cuda")
+    if torch.distributed.is_initialized():
+        allsh = [torch.zeros_like(shard) for _ in range(world)]
+        torch.distributed.all_gather(allsh, shard)
+        shard = max(allsh, key=lambda t: float(t[0]))
+    shard_sweep_ms, shard_nnz, shard_real = (float(x) for x in shard.cpu())
 
     if rank == 0:
         its = args.steps / elapsed
@@ -329,11 +353,14 @@ def main():
         traffic, traffic_src = (pmc_traffic() if args.config == "c4" and args.nnz is None
                                 else (None, None))
         if launches:
-            sweep_avg = sweep_ms / launches / 1000.0
-            achieved = ALG_BYTES_PER_PIXEL * inf["nnz_upper"] / sweep_avg / 1e9
+            # per launch on the slowest rank (= the whole matrix at N=1)
+            sweep_avg = shard_sweep_ms / 1000.0
+            achieved = ALG_BYTES_PER_PIXEL * shard_nnz / sweep_avg / 1e9
             # bytes the layout actually streams: entries (uint16 + uint32) +
             # both segments' row pointers (the b staging shows up in traffic)
-            real_b = float(inf["payload_bytes"]) + 8.0 * 513 * inf["n_tiles"]
+            real_b = shard_real
+            if world > 1:
+                traffic = None  # the committed PMC summary is for the 1-GPU matrix
             out["roofline"] = {"bound": "hbm", "kernel": "k_sweep_tiled", "achieved": achieved,
                                "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS,
                                "traffic": traffic,
@@ -343,7 +370,9 @@ def main():
                                "real_frac": real_b / sweep_avg / 1e9 / PEAK_HBM_GBS,
                                "traffic_GBps": (traffic / sweep_avg / 1e9) if traffic else None,
                                "sweep_ms_avg": sweep_avg * 1000.0,
-                               "iter_ms_avg": iter_ms / launches}
+                               "iter_ms_avg": iter_ms / launches,
+                               "per_rank": "slowest rank's shard" if world > 1 else "whole matrix",
+                               "shard_nnz_upper": shard_nnz}
         if world == 1 and not args.no_cpu:
             out["cpu_baseline"] = cpu_baseline(sizes, kw, rc, nnz_total)
         print(json.dumps(out), flush=True)

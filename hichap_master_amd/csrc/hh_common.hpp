@@ -81,7 +81,7 @@ struct KTimeScope {
     KTimeRec r{nullptr, nullptr, nullptr};
     hipStream_t s;
     bool on;
-    KTimeScope(const char* name, hipStream_t s_) : s(s_), on(g_ktime_on) {
+    KTimeScope(const char* name, hipStream_t s_) : s(s_), on(g_ktime_on && name) {
         if (!on) return;
         r.name = name;
         HIP_CHECK(hipEventCreate(&r.a));

@@ -543,7 +543,10 @@ static void sweep(const hh_matrix* m, const uint8_t* act, const double* b, doubl
 static void marg_weighted(hh_ice* S, double* out, hipStream_t s, bool timed, int slot) {
     hh_matrix* m = S->m;
     if (timed) HIP_CHECK(hipEventRecord(S->ev[2 * slot], s));
-    sweep(m, S->act(), S->bias.p, S->part.p, s);
+    {
+        HH_KTIME(timed ? nullptr : "k_sweep_tiled", s);  // registry timing for the sharded driver
+        sweep(m, S->act(), S->bias.p, S->part.p, s);
+    }
     if (timed) HIP_CHECK(hipEventRecord(S->ev[2 * slot + 1], s));
     if (S->nloc == 0) return;
     hipLaunchKernelGGL(k_marg, dim3(nblocks(S->nloc, kThreads)), dim3(kThreads), 0, s, m->dev(), S->part.p,

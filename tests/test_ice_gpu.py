@@ -201,3 +201,31 @@ def test_synth_dense_block_matches_sparse_generator(ice):
         sel = (b1 >= off[k]) & (b1 < off[k + 1])
         want[b1[sel] - off[k], b2[sel] - off[k]] = c[sel]
         np.testing.assert_array_equal(np.triu(D), want)
+
+
+def test_balance_sharded_rccl_world1(ice):
+    """dist.balance_sharded over a real RCCL process group (world 1): the
+    all-gather path through torch.distributed "nccl" gives the full result."""
+    import socket
+    import torch
+    import torch.distributed as tdist
+    from hichap_master_amd import dist
+    b1, b2, c, off = _case(12, sizes=(600, 350))
+    n = int(off[-1])
+    w_full, st_full = ice.balance(b1, b2, c, n, off, max_iters=300)
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    tdist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                             device_id=torch.device("cuda", 0))
+    try:
+        rr = np.array([0, n], dtype=np.int64)
+        m = ice.ContactMatrix.from_pixels(b1, b2, c, n, off, row_range=(0, n))
+        st = ice.IceState(m, ice.IceOptions(max_iters=300))
+        ex = dist.Exchange(rr, torch.device("cuda", 0))
+        assert ex.fused
+        w, s_ = dist.balance_sharded(st, ex, max_iters=300)
+    finally:
+        tdist.destroy_process_group()
+    np.testing.assert_array_equal(w, w_full)
+    assert s_["iters"] == st_full["iters"]
