@@ -97,6 +97,17 @@ SIGNATURES = {
     "hh_di_scan": (C.c_int, [P, I64, I32, P, P, I32, P, I32, P]),
     "hh_comp_pca": (C.c_int, [P, I32, F64, I32, P, P, P, P]),
     "hh_comp_select_stats": (C.c_int, [P, P, I32, F64, P, P]),
+    "hh_binner_create": (C.c_int, [I32, C.c_char_p, P, I32, I32, C.POINTER(P)]),
+    "hh_binner_free": (C.c_int, [P]),
+    "hh_binner_add_target": (C.c_int, [P, I32, I32, P, P, I64, PI32]),
+    "hh_binner_feed": (C.c_int, [P, C.c_char_p, I64, P, I64, P]),
+    "hh_binner_feed_device": (C.c_int, [P, P, I64, P, P]),
+    "hh_binner_stats": (C.c_int, [P, P]),
+    "hh_binner_finish": (C.c_int, [P, P]),
+    "hh_binner_target_nnz": (C.c_int, [P, I32, PI64, PI64]),
+    "hh_binner_download": (C.c_int, [P, I32, P, P, P]),
+    "hh_binner_pixels_device": (C.c_int, [P, I32, P, P, P]),
+    "hh_synth_pairs_text": (C.c_int, [I32, C.c_char_p, P, I64, F64, F64, I32, C.c_uint64, I64, P, I64, PI64, P]),
 }
 
 _lib = None

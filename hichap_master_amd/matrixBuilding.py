@@ -174,3 +174,131 @@ def GenomeWideMatrixCorrection(Bins_Pos, Hap_Bins_Pos, T_M, H_M):
         Alpha.extend(Beta[i])
     Alpha += Alpha
     return sym_vc_rescale(H_M, np.array(Alpha), None, h_full.sum())
+
+
+# ---------------------------------------------------------- pair binning
+# Same entry points as the reference's matrix construction; the per-line
+# loops run on the GPU (hichap_master_amd.pairs, csrc/pairs.hip).
+def Load_Genome(genomeSize, chroms):
+    """{stripped chrom: length} for the chromosomes `chroms` accepts (:349-366)."""
+    from . import pairs
+    return pairs.load_genome(genomeSize, chroms)
+
+
+def Load_HaplotypeGenome(genomeSize, chroms):
+    """{'M'+c: l, 'P'+c: l} (:369-385)."""
+    g = Load_Genome(genomeSize, chroms)
+    out = {}
+    for c, l in g.items():
+        out["M" + c] = l
+        out["P" + c] = l
+    return out
+
+
+def Get_Chro_Bins(genomeSize, Resolution, chroms):
+    """({chrom: (first, last)} inclusive, n_bins) (:409-426)."""
+    from . import pairs
+    return pairs.chrom_bins(Load_Genome(genomeSize, chroms), Resolution)
+
+
+def Get_Chro_Bins_Haplotypes(genomeSize, Resolution, chroms):
+    """M chromosomes then P chromosomes (:429-454)."""
+    from . import pairs
+    return pairs.haplotype_bins(Load_Genome(genomeSize, chroms), Resolution)
+
+
+def _bin_sources(genome, chroms, passes, wholeRes, localRes, haplotype, local_halves):
+    """Run the GPU binner over `passes` = [(source, PairsFormat)], one whole
+    target per wholeRes and one intra-chromosome target per localRes."""
+    from . import pairs
+    B = pairs.PairBinner(genome, chroms)
+    try:
+        whole = {res: B.add_target(res, local=False, haplotype=haplotype) for res in wholeRes}
+        local = {res: B.add_target(res, local=True, haplotype=haplotype) for res in localRes}
+        for src, fmt in passes:
+            B.feed(src, fmt)
+        B.finish()
+        wp = {res: B.pixels(t) for res, t in whole.items()}
+        lp = {res: B.pixels(t) for res, t in local.items()}
+        return B.order, whole, local, wp, lp
+    finally:
+        B.close()
+
+
+def TraditionalMatrixBuilding(bed_IO, genomeSize, wholeRes, localRes, chroms):
+    """Traditional matrices from *_Valid.bed pairs (:528-614).
+
+    ``bed_IO``: a path, a list of paths (concatenated like `cat`), bytes, a
+    file object or an iterable of lines.  Returns ``(Whole_Lib, Local_Lib)``
+    in the reference's shape: ``Whole_Lib[res]`` = {chrom: upper-triangle
+    sparse, 'c1_c2': inter block sparse}, ``Local_Lib[res]`` = {chrom:
+    upper-triangle sparse}; sparse = structured (bin1, bin2, IF) arrays in
+    chromosome-local bins (WholeMatrixToSparseDict / IntraMatrixToSparseDict,
+    :457-525)."""
+    from . import pairs
+    genome = Load_Genome(genomeSize, chroms)
+    fmt = pairs.pairs_format(pairs.VALID_BED)
+    order, whole, local, wp, lp = _bin_sources(genome, chroms, [(bed_IO, fmt)], wholeRes, localRes, False, None)
+    Whole_Lib, Local_Lib = {}, {}
+    for res in wholeRes:
+        bins, _ = pairs.chrom_bins(genome, res)
+        Whole_Lib[res] = pairs.whole_sparse_dict(*wp[res], bins)
+    for res in localRes:
+        Local_Lib[res] = pairs.local_sparse_dict(*lp[res], local[res], order)
+    return Whole_Lib, Local_Lib
+
+
+def TraditionalMatrixInAllelic(bed_IO, genomeSize, wholeRes, localRes, chroms, dense=True):
+    """Traditional matrices of the haplotype pipeline from the allelic beds
+    (fields 0-3, no mark filter; :793-854).  Reference shape (dense=True):
+    ``Whole_Lib[res] = {'Bins': Bins, 'Matrix': int64 n x n}``,
+    ``Local_Lib[res][chrom]`` int64 N x N.  dense=False returns pixel tables
+    ``(bin1, bin2, count)`` (global bins for whole, local bins per chrom)."""
+    from . import pairs
+    genome = Load_Genome(genomeSize, chroms)
+    fmt = pairs.pairs_format(pairs.ALLELIC_BED)
+    order, whole, local, wp, lp = _bin_sources(genome, chroms, [(bed_IO, fmt)], wholeRes, localRes, False, None)
+    return _dense_libs(genome, order, whole, local, wp, lp, dense, haplotype=False)
+
+
+def _dense_libs(genome, order, whole, local, wp, lp, dense, haplotype):
+    from . import pairs
+    Whole_Lib, Local_Lib = {}, {}
+    for res, t in whole.items():
+        bins, total = (pairs.haplotype_bins if haplotype else pairs.chrom_bins)(genome, res)
+        b1, b2, c = wp[res]
+        Whole_Lib[res] = {"Bins": bins,
+                          "Matrix": pairs.dense_from_pixels(b1, b2, c, total) if dense else (b1, b2, c)}
+    for res, t in local.items():
+        b1, b2, c = lp[res]
+        b1 = np.asarray(b1, np.int64)
+        Local_Lib[res] = {}
+        halves = ("M", "P") if haplotype else ("",)
+        for h, prefix in enumerate(halves):
+            for k, chro in enumerate(order):
+                s0 = int(t.chrom_first[k]) + h * int(t.chrom_nbins.sum())
+                n = int(t.chrom_nbins[k])
+                lo, hi = np.searchsorted(b1, [s0, s0 + n], "left")
+                if dense:
+                    Local_Lib[res][prefix + chro] = pairs.dense_from_pixels(b1[lo:hi], b2[lo:hi], c[lo:hi], n, s0)
+                else:
+                    Local_Lib[res][prefix + chro] = (b1[lo:hi] - s0, np.asarray(b2[lo:hi], np.int64) - s0, c[lo:hi])
+    return Whole_Lib, Local_Lib
+
+
+def HaplotypeUnImputedBuilding(M_M, P_P, M_P, P_M, genomeSize, wholeRes, localRes, chroms, dense=True):
+    """The unimputed haplotype matrices of HaplotypeMatrixBuilding
+    (:1108-1240): M_M and P_P pairs with last field 'Both' (cis pairs also go
+    to the per-haplotype intra-chromosome matrices), M_P pairs as (M chrom1,
+    P chrom2) and P_M pairs as (P chrom1, M chrom2) in the 2n-bin whole-genome
+    layout.  Each argument is a pair source (path, list of paths, bytes, ...).
+    Returns ``(UnImputated_Whole_Lib, UnImputated_Local_Lib)`` in the
+    reference's dense shape (``Local_Lib[res]['M'+c]``, ``['P'+c]``)."""
+    from . import pairs
+    genome = Load_Genome(genomeSize, chroms)
+    passes = [(M_M, pairs.pairs_format(pairs.ALLELIC_BED, "Both", 0, 0)),
+              (P_P, pairs.pairs_format(pairs.ALLELIC_BED, "Both", 1, 1)),
+              (M_P, pairs.pairs_format(pairs.ALLELIC_BED, "", 0, 1)),
+              (P_M, pairs.pairs_format(pairs.ALLELIC_BED, "", 1, 0))]
+    order, whole, local, wp, lp = _bin_sources(genome, chroms, passes, wholeRes, localRes, True, None)
+    return _dense_libs(genome, order, whole, local, wp, lp, dense, haplotype=True)

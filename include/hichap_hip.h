@@ -18,6 +18,10 @@
  *   hh_compartment_*    StructureFind.Distance_Decay / Get_PCA / Select_PC_new,
  *                       StructureFind.py:201-423
  *   hh_di_scan          StructureFind.Get_Gap / Get_DI, StructureFind.py:721-839
+ *   hh_binner_*         the per-line pair binning loops of TraditionalMatrixBuilding
+ *                       (matrixBuilding.py:566-596), TraditionalMatrixInAllelic
+ *                       (:817-854) and HaplotypeMatrixBuilding's unimputed
+ *                       M_M / P_P / M_P / P_M passes (:1126-1240)
  */
 #ifndef HICHAP_HIP_H
 #define HICHAP_HIP_H
@@ -252,6 +256,65 @@ int hh_gap_scan(const double* band, int64_t N, int32_t B, int32_t lb, uint8_t* g
                 void* stream);
 int hh_di_scan(const double* band, int64_t N, int32_t B, const uint8_t* gap, const int32_t* window_bins,
                int32_t test, double* di, int32_t on_device, void* stream);
+
+/* ---------------------------------------------------------- pair binning
+ * Pair text (HiCHap *_Valid.bed: chrom/pos in fields 1, 6, 8, 13; allelic
+ * beds: fields 0-3 and a trailing mark) -> cooler pixel tables per target
+ * matrix: upper triangle (bin1 <= bin2), sorted by (bin1, bin2), count = number
+ * of pairs of the unordered bin pair — what the reference's dense
+ * `M[b1][b2] += 1; M[b2][b1] += 1` (once when b1 == b2) + np.triu + nonzero
+ * produce (matrixBuilding.py:457-525, :566-596).
+ * Lines follow Python's `line.strip().split()`; chromosome fields are
+ * `lstrip('chr')`-ed and looked up in the name table.  A line the reference
+ * would raise on (missing field, non-integer position, a name that passes the
+ * `chroms` filter but is not in genomeSize, a bin outside the matrix) fails the
+ * feed with HH_ERR_ARG naming the first such line (negative positions too:
+ * the reference's NumPy indexing would wrap them). */
+typedef struct hh_binner hh_binner;
+typedef struct {
+    int32_t col_chrom1, col_pos1, col_chrom2, col_pos2; /* 0-based fields      */
+    char mark[16];     /* non-empty: skip lines whose LAST field differs (`if
+                          line[-1] != 'Both': continue`, :1133)              */
+    int32_t hap1, hap2;/* haplotype half of chrom1 / chrom2 (0 = M or the
+                          traditional genome, 1 = P)                         */
+} hh_pairs_format;
+/* names: n_names NUL-terminated names back to back (after lstrip('chr'));
+ * name_ids[k] = chromosome index (Sort_Chromosomes order) or -2 for a name
+ * the `chroms` filter accepts but genomeSize lacks.  unknown_policy for names
+ * not in the table: 0 skip the line, 1 raise if the name is all digits
+ * ('#' in chroms), 2 raise (empty chroms list). */
+int hh_binner_create(int32_t n_chroms, const char* names, const int32_t* name_ids, int32_t n_names,
+                     int32_t unknown_policy, hh_binner** out);
+int hh_binner_free(hh_binner* b);
+/* One output matrix at resolution `res`: chrom_start[2 * n_chroms] = first
+ * global bin of chromosome c in haplotype h (index h * n_chroms + c; the
+ * traditional layout uses h = 0 only), chrom_nbins[c] = l // res + 1.
+ * local = 1: intra-chromosome matrices only (localRes; trans pairs dropped,
+ * per-chromosome bounds), bins still global (split per chromosome by the
+ * caller). */
+int hh_binner_add_target(hh_binner* b, int32_t res, int32_t local, const int64_t* chrom_start,
+                         const int32_t* chrom_nbins, int64_t n_bins, int32_t* index_out);
+/* Parse + bin host text (staged through pinned chunks of chunk_bytes, cut at
+ * line ends; 0 = 256 MB) or device-resident text.  Synchronous. */
+int hh_binner_feed(hh_binner* b, const char* text, int64_t nbytes, const hh_pairs_format* f, int64_t chunk_bytes,
+                   void* stream);
+int hh_binner_feed_device(hh_binner* b, const char* text, int64_t nbytes, const hh_pairs_format* f, void* stream);
+/* stats4: lines read, lines binned, skipped by the chromosome filter,
+ * skipped by the mark filter. */
+int hh_binner_stats(const hh_binner* b, int64_t* stats4);
+/* Sort + run-length encode every target (synchronous); then nnz per target. */
+int hh_binner_finish(hh_binner* b, void* stream);
+int hh_binner_target_nnz(const hh_binner* b, int32_t target, int64_t* nnz, int64_t* n_pairs);
+int hh_binner_download(const hh_binner* b, int32_t target, int32_t* bin1, int32_t* bin2, int32_t* count);
+/* Device pointers of a finished target (valid until hh_binner_free). */
+int hh_binner_pixels_device(const hh_binner* b, int32_t target, const int32_t** bin1, const int32_t** bin2,
+                            const int32_t** count);
+/* Synthetic pair text generated in device memory (bench input): format 0 =
+ * 15-column *_Valid.bed lines, 1 = allelic "chrom pos chrom pos mark".  out =
+ * NULL: size query into *nbytes. */
+int hh_synth_pairs_text(int32_t n_chroms, const char* names, const int64_t* lengths, int64_t n_lines,
+                        double cis_frac, double max_dist, int32_t format, uint64_t seed, int64_t line0, char* out,
+                        int64_t capacity, int64_t* nbytes, void* stream);
 
 #ifdef __cplusplus
 }
