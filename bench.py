@@ -233,6 +233,146 @@ def run_c5(args, world, rank, local):
         print(json.dumps(out), flush=True)
 
 
+PAIRS_WHOLE = [10000]            # whole-genome matrix at the C4 resolution
+PAIRS_LOCAL = [500000, 40000]    # HiCHap's default localRes (scripts/hichap:408)
+
+
+def pairs_genome():
+    from hichap_master_amd import synth
+    return {c: synth.HG19[c] for c in synth.HG19_ORDER}
+
+
+def synth_pairs_text(genome, n_lines, seed=20201016, fmt=0, line0=0):
+    """Synthetic *_Valid.bed text generated in HBM (hh_synth_pairs_text)."""
+    import ctypes as C
+    import torch
+    from hichap_master_amd._lib import call
+    names = b"".join(b"chr" + c.encode() + b"\0" for c in genome)
+    lens = np.array(list(genome.values()), dtype=np.int64)
+    nb = C.c_int64(0)
+    args = (len(genome), names, lens.ctypes.data_as(C.c_void_p), int(n_lines), 0.8, 1e8, fmt, seed, int(line0))
+    call("hh_synth_pairs_text", *args, None, 0, C.byref(nb), None)
+    buf = torch.empty(nb.value, dtype=torch.uint8, device="cuda")
+    call("hh_synth_pairs_text", *args, C.c_void_p(buf.data_ptr()), nb.value, C.byref(nb), None)
+    torch.cuda.synchronize()
+    return buf
+
+
+def pairs_cpu_baseline(genome, budget_s=10.0):
+    """Oracle (oracle/pairs_ref.py: the reference's per-line loop restated,
+    dict counts instead of dense += ) on a bounded sample of the same text."""
+    from oracle import pairs_ref
+    n = 4_000_000
+    text = bytes(synth_pairs_text(genome, n, line0=0).cpu().numpy()).decode()
+    lines = text.splitlines(keepends=True)
+    t0 = time.perf_counter()
+    done = 0
+    step = 200_000
+    while done < n and time.perf_counter() - t0 < budget_s:
+        pairs_ref.traditional_counts(lines[done:done + step], genome, ["#", "X"], PAIRS_WHOLE, PAIRS_LOCAL)
+        done += step
+    dt = time.perf_counter() - t0
+    return {"value": done / dt, "unit": "pairs/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/pairs_ref.traditional_counts (the reference's line loop, :566-596) on the first "
+                      f"{done} lines of the same synthetic text: {dt:.1f}s"}
+
+
+def run_pairs(args, world, rank, local):
+    """Pair binning: synthetic hg19 *_Valid.bed text
+    resident in HBM -> whole-genome 10 kb + intra-chromosome 500 kb / 40 kb
+    pixel tables.  A step = parse + bin + sort + RLE of every pair; ranks
+    bin disjoint line ranges of the same text (weak scaling, no collective:
+    merging per-rank tables is the reference's replicate merge)."""
+    import torch
+    from hichap_master_amd import _lib, pairs
+    genome = pairs_genome()
+    n_lines = int(args.pairs)
+    t0 = time.perf_counter()
+    text = synth_pairs_text(genome, n_lines, line0=rank * n_lines)
+    gen_s = time.perf_counter() - t0
+    fmt = pairs.pairs_format(pairs.VALID_BED)
+    stream = torch.cuda.current_stream().cuda_stream
+    if os.environ.get("HH_PARSE_ABLATE"):  # timing ablations only (results wrong)
+        _lib.call("hh_tune", b"parse_ablate", int(os.environ["HH_PARSE_ABLATE"]))
+    info = {}
+
+    def step():
+        B = pairs.PairBinner(genome, ["#", "X"], stream=stream)
+        ts = [B.add_target(r) for r in PAIRS_WHOLE] + [B.add_target(r, local=True) for r in PAIRS_LOCAL]
+        B.feed_device(text.data_ptr(), text.numel(), fmt)
+        B.finish()
+        info["st"] = B.stats()
+        info["nnz"] = []
+        for t in ts:
+            info["nnz"].append((t.res, t.local) + B.sizes(t))
+        B.close()
+
+    def barrier():
+        if torch.distributed.is_initialized():
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier()
+    elapsed = time.perf_counter() - t_start
+    _lib.call("hh_ktime_reset")
+    _lib.call("hh_ktime_enable", 1)
+    step()
+    torch.cuda.synchronize()
+    _lib.call("hh_ktime_enable", 0)
+    kt = {k: _lib.ktime(k) for k in ("k_parse_tile", "k_rs_hist", "k_rs_scatter")}
+    tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    if torch.distributed.is_initialized():
+        torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
+    elapsed = float(tt.item())
+    if rank == 0:
+        text_bytes = int(text.numel())
+        keys_total = sum(x[3] for x in info["nnz"])
+        # dominant-kernel roofline: the parse reads every text byte once and
+        # writes one 8 B key per pair and target; the radix scatter reads and
+        # writes 8 B per key per pass (+ the hist pass reads 8 B)
+        parse_ms, _ = kt["k_parse_tile"]
+        scat_ms, scat_n = kt["k_rs_scatter"]
+        hist_ms, _ = kt["k_rs_hist"]
+        parse_bytes = text_bytes + 8.0 * keys_total
+        passes_bytes = 24.0 * sum(x[3] * ((2 * (int(np.ceil(np.log2(max(2, _nbins(genome, x[0]))))) ) + 7) // 8)
+                                  for x in info["nnz"])
+        dom = "k_parse_tile" if parse_ms >= scat_ms + hist_ms else "k_rs_hist+k_rs_scatter"
+        if dom == "k_parse_tile":
+            achieved = parse_bytes / (parse_ms / 1000.0) / 1e9
+        else:
+            achieved = passes_bytes / ((scat_ms + hist_ms) / 1000.0) / 1e9
+        out = {
+            "metric": "pair binning pairs/sec (Valid.bed text in HBM -> cooler pixel tables)",
+            "value": world * n_lines * args.steps / elapsed, "unit": "pairs/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1000.0 * elapsed / args.steps,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int64",
+            "data": "synthetic hg19 *_Valid.bed text generated in HBM (15 columns, 80% cis, log-uniform distance)",
+            "config": {"workload": "hg19-validbed-pairs", "pairs_per_rank": n_lines, "text_bytes_per_rank": text_bytes,
+                       "whole_res": PAIRS_WHOLE, "local_res": PAIRS_LOCAL,
+                       "targets": [{"res": r, "local": bool(l), "pixels": nz, "pairs": npair}
+                                   for r, l, nz, npair in info["nnz"]],
+                       "stats": info["st"], "generate_s": round(gen_s, 2)},
+            "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                         "frac": achieved / PEAK_HBM_GBS, "traffic": None,
+                         "kernel_ms": {k: v[0] for k, v in kt.items()},
+                         "parse_alg_bytes": parse_bytes, "sort_alg_bytes": passes_bytes,
+                         "kernel_timing": "HIP events (hh_ktime) over one extra step after the timed steps"},
+        }
+        if world == 1 and not args.no_cpu:
+            out["cpu_baseline"] = pairs_cpu_baseline(genome)
+        print(json.dumps(out), flush=True)
+
+
+def _nbins(genome, res):
+    return sum(l // res + 1 for l in genome.values())
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -241,6 +381,7 @@ def main():
     ap.add_argument("--config", default="c4")
     ap.add_argument("--nnz", type=float, default=None)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--pairs", type=float, default=2e8, help="pairs per rank for --config pairs")
     ap.add_argument("--sharded", action="store_true",
                     help="use the multi-GPU (all-gather) driver even at N=1 (path check)")
     args = ap.parse_args()
@@ -259,8 +400,8 @@ def main():
             os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT="29531", RANK="0", WORLD_SIZE="1")
         tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
-    if args.config == "c5":
-        run_c5(args, world, rank, local)
+    if args.config in ("c5", "pairs"):
+        (run_c5 if args.config == "c5" else run_pairs)(args, world, rank, local)
         if torch.distributed.is_initialized():
             torch.distributed.destroy_process_group()
         return

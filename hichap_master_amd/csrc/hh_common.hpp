@@ -97,6 +97,11 @@ struct KTimeScope {
 };
 #define HH_KTIME(name, stream) ::hh::KTimeScope hh_kt_scope_(name, stream)
 
+// Timing ablations of the pair parser (hh_tune "parse_ablate"; results are
+// wrong while set): 1 stage text + masks only, 2 + line starts, 3 + parse
+// without binning.
+inline int g_parse_ablate = 0;
+
 // Device memory pool.  hipFree synchronises the device and costs ~0.2 ms per
 // call, which dominated per-chromosome loops (a few large buffers per call),
 // so released blocks are cached and reused (best fit within 2x).  Reuse is

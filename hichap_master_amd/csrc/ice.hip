@@ -592,6 +592,9 @@ int hh_tune(const char* key, int64_t value) {
         } else if (k == "unit_entries") {
             HH_REQUIRE(value == 0 || (value >= 4096 && value <= (1 << 24)), "unit_entries must be 0 (auto) or in [4096, 2^24]");
             g_unit_entries = value;
+        } else if (k == "parse_ablate") {
+            HH_REQUIRE(value >= 0 && value <= 3, "parse_ablate in [0, 3]");
+            g_parse_ablate = (int)value;
         } else if (k == "sweep_flags") {
             HH_REQUIRE(value >= 0 && value <= 1, "sweep_flags in [0, 1]");
             g_sweep_flags = (int)value;

@@ -12,12 +12,12 @@
 // matrix: parse -> key per pair -> LSD radix sort -> run-length encode.
 //
 // Pipeline per text chunk (device resident):
-//   k_nl_count / scan / k_nl_write   newline positions (4 KB tiles, uint4 loads)
-//   k_parse_bin                      one thread per line: whitespace fields
-//                                    (Python str.split semantics), 'chr'
-//                                    lstrip, chromosome hash lookup, int parse,
-//                                    pos // res + offset, per-target keys
-//                                    appended with wave-ballot compaction
+//   k_parse_tile   one block per 8 KB of text: the tile (+4 KB lookahead)
+//                  staged in LDS with coalesced 16 B loads, line starts found
+//                  in LDS (block scan), then one thread per line: whitespace
+//                  fields (Python str.split semantics), 'chr' lstrip,
+//                  chromosome hash lookup, int parse, pos // res + offset,
+//                  per-target keys appended with wave-ballot compaction
 // Per target at finish:
 //   k_rs_hist / scan / k_rs_scatter  stable LSD radix sort, 8-bit digits, LDS
 //                                    staging so each digit run is written
@@ -147,7 +147,7 @@ static void exclusive_scan(const T* in, U* out, long long n, unsigned long long*
     HIP_CHECK(hipGetLastError());
 }
 
-// ------------------------------------------------------------ newline scan
+// ------------------------------------------------------------ text access
 // Text is read as aligned 16-byte blocks: a 16 B-aligned block never crosses
 // a page, so the bytes around [0, nbytes) that share a block with a valid
 // byte are always mapped; they are masked out.
@@ -160,76 +160,53 @@ __device__ __forceinline__ unsigned byte_of(const uint4& v, int k) {
     return (w >> (8 * (k & 3))) & 0xffu;
 }
 
-// Newlines in the 16 bytes [pos0 + 16*j, ...) that are inside [0, nbytes),
-// relative to an aligned text start (text % 16 == 0 handled by the caller
-// passing the aligned base and the byte shift).
 struct TextView {
     const char* abase;   // text rounded down to 16 B
     long long shift;     // text - abase
     long long nbytes;
 };
 
-__device__ __forceinline__ int nl_mask16(const TextView& tv, long long blk, unsigned* mask) {
-    const uint4 v = load16(tv.abase, blk);
-    unsigned m = 0;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        const long long p = blk * 16 + k - tv.shift;  // text-relative position
-        if (p >= 0 && p < tv.nbytes && byte_of(v, k) == '\n') m |= 1u << k;
-    }
-    *mask = m;
-    return __popc(m);
-}
-
-__global__ __launch_bounds__(kScanThreads) void k_nl_count(TextView tv, long long nblk, unsigned* __restrict__ cnt) {
-    __shared__ unsigned long long sh[4];
-    const long long blk = (long long)blockIdx.x * kScanThreads + threadIdx.x;
-    unsigned m = 0;
-    const int c = blk < nblk ? nl_mask16(tv, blk, &m) : 0;
-    unsigned long long tot = 0;
-    (void)block_excl_scan_u64((unsigned long long)c, sh, &tot);
-    if (threadIdx.x == 0) cnt[blockIdx.x] = (unsigned)tot;
-}
-
-__global__ __launch_bounds__(kScanThreads) void k_nl_write(TextView tv, long long nblk,
-                                                           const unsigned long long* __restrict__ off,
-                                                           long long* __restrict__ nl) {
-    __shared__ unsigned long long sh[4];
-    const long long blk = (long long)blockIdx.x * kScanThreads + threadIdx.x;
-    unsigned m = 0;
-    const int c = blk < nblk ? nl_mask16(tv, blk, &m) : 0;
-    unsigned long long o = off[blockIdx.x] + block_excl_scan_u64((unsigned long long)c, sh, nullptr);
-    while (m) {
-        const int k = __ffs(m) - 1;
-        m &= m - 1;
-        nl[o++] = blk * 16 + k - tv.shift;
-    }
-}
-
 // ------------------------------------------------------------ line parsing
-struct NameEntry {  // open-addressing table of accepted / erroneous names
-    unsigned long long hash;  // 0 = empty slot
-    int32_t off, len;         // into the name bytes
-    int32_t id;               // >= 0 chromosome index; -2: reference raises (KeyError)
-    int32_t pad;
+// Chromosome name table: open addressing on a 32-bit hash of the name's
+// first 16 bytes (inline, zero padded) and its length.
+struct NameEntry {
+    uint32_t w[4];   // first 16 bytes of the name (little-endian words)
+    int32_t len;
+    int32_t id;      // >= 0 chromosome index; -2 reference raises (KeyError); -3 empty slot
+    int32_t off;     // all name bytes in `names` (compared past byte 16)
+    uint32_t hash;
 };
+constexpr int kEmptySlot = -3;
+
+__host__ __device__ __forceinline__ uint32_t name_hash(const uint32_t w[4], int len) {
+    uint32_t h = 0x9E3779B9u ^ (uint32_t)len;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        h ^= w[k] * 0x85EBCA6Bu;
+        h = ((h << 13) | (h >> 19)) * 5u + 0xE6546B64u;
+    }
+    h ^= h >> 16;
+    h *= 0x85EBCA6Bu;
+    h ^= h >> 13;
+    return h;
+}
 
 struct TargetDev {
     const long long* start;  // [2 * n_chroms] first global bin of chrom c in haplotype h
     const int32_t* nbins;    // [n_chroms] l // res + 1
     unsigned long long* keys;
-    unsigned long long* count;
+    unsigned long long* count;  // slots reserved (keys + sentinels)
+    unsigned long long* gaps;   // sentinel slots
     long long n_bins;
     long long res;
     int local;               // intra-chromosome matrix (localRes)
     int shift;               // key = min << shift | max
+    unsigned magic;          // division by res (div_res)
+    int msh;
 };
 
 struct ParseArgs {
     TextView tv;
-    const long long* nl;     // newline positions; line k = (nl[k-1]+1 .. nl[k])
-    long long n_lines;
-    long long line_base;     // global index of line 0 (error reports)
     const NameEntry* table;
     const char* names;
     int table_mask;
@@ -241,203 +218,550 @@ struct ParseArgs {
     int n_chroms;
     int n_targets;
     int has_whole, has_local;
-    unsigned long long* err;   // [0] min (line << 8 | code)
+    int ablate;                // g_parse_ablate (timing only)
+    unsigned long long* err;   // [0] min (line start byte << 8 | code)
     unsigned long long* stats; // [0] lines, [1] kept, [2] skipped (chromosome check), [3] skipped (mark)
     TargetDev t[kMaxTargets];
 };
 
 enum : int { kErrFields = 1, kErrInt = 2, kErrName = 3, kErrBin = 4 };
 
-struct Reader {  // 16-byte register cache over the text
+// Tile geometry of k_parse_tile: a block owns the lines that START in its
+// tile of aligned 16 B text blocks ([T0, T0 + TB), TB = 256..2560 blocks,
+// picked per feed so a tile holds ~230 lines); it stages the tile, the block
+// before it and 1 KB of lookahead (lines running further fall back to global
+// loads) in LDS with coalesced 16 B loads, plus each staged block's
+// whitespace / newline bitmasks.
+constexpr int kPLookBlk = 64;   // 1 KB
+constexpr int kPMaxSeg = 10;    // blocks per thread segment (TB <= 2560 = 40 KB)
+
+// Exact per-byte classes of one little-endian word, as 4-bit masks.
+__device__ __forceinline__ unsigned zero_bytes_hi(unsigned y) {  // 0x80 in each zero byte
+    return ~(((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y | 0x7F7F7F7Fu);
+}
+__device__ __forceinline__ unsigned hi_to_nibble(unsigned h) { return (((h >> 7) * 0x204081u) >> 21) & 0xFu; }
+
+__device__ __forceinline__ void word_classes(unsigned x, unsigned* ws, unsigned* nl) {
+    const unsigned n = zero_bytes_hi(x ^ 0x0A0A0A0Au);
+    const unsigned sp = zero_bytes_hi(x ^ 0x20202020u);
+    // bytes 9..13 (\t \n \v \f \r): (c | 0x80) - 9 has no inter-byte borrow
+    const unsigned r = (x | 0x80808080u) - 0x09090909u;
+    const unsigned lt5 = ~((r & 0x7F7F7F7Fu) + 0x7B7B7B7Bu) & 0x80808080u;
+    const unsigned rng = r & lt5 & ~x & 0x80808080u;
+    *ws = hi_to_nibble(sp | rng);
+    *nl = hi_to_nibble(n);
+}
+
+// Global 16-byte load for the rare out-of-window path.  Written as asm so the
+// compiler cannot merge it with the LDS path into one flat load (a flat load
+// waits on both the vector-memory and the LDS counters, serialising every LDS
+// read of the parse behind outstanding global traffic).
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 load16_global_sync(const char* p) {
+    u32x4_t v;
+    asm volatile("global_load_dwordx4 %0, %1, off\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+struct TileText {
+    const uint4* lds;      // text blocks [W0, W1)
+    const unsigned* msk;   // their masks: ws | nl << 16
+    long long W0, W1;
     const TextView* tv;
-    long long blk = -1;
-    uint4 v;
-    __device__ unsigned get(long long p) {  // p text-relative, in range
+    long long nblk_all;    // aligned blocks holding text bytes
+    __device__ uint4 blk(long long b) const {
+        if (b >= W0 && b < W1) return lds[b - W0];
+        if (b < 0 || b >= nblk_all) return make_uint4(0, 0, 0, 0);
+        return load16_global_sync(tv->abase + b * 16);
+    }
+    __device__ unsigned get(long long p) const {  // text-relative byte; past the end reads '\n'
+        if (p >= tv->nbytes) return '\n';
         const long long a = p + tv->shift;
-        const long long b = a >> 4;
-        if (b != blk) {
-            v = load16(tv->abase, b);
-            blk = b;
-        }
-        return byte_of(v, (int)(a & 15));
+        return byte_of(blk(a >> 4), (int)(a & 15));
     }
 };
 
-__device__ __forceinline__ bool is_ws(unsigned c) {
-    return c == ' ' || c == '\t' || c == '\n' || c == '\r' || c == 11 || c == 12;
+// ws | nl << 16 of aligned block b from its bytes; bytes past the end of the
+// text count as newline (and whitespace).
+__device__ __forceinline__ unsigned masks_of(const TextView& tv, uint4 v, long long b) {
+    unsigned w0, w1, w2, w3, n0, n1, n2, n3;
+    word_classes(v.x, &w0, &n0);
+    word_classes(v.y, &w1, &n1);
+    word_classes(v.z, &w2, &n2);
+    word_classes(v.w, &w3, &n3);
+    unsigned ws = w0 | w1 << 4 | w2 << 8 | w3 << 12;
+    unsigned nl = n0 | n1 << 4 | n2 << 8 | n3 << 12;
+    const long long lim = tv.shift + tv.nbytes - b * 16;  // valid bytes in this block
+    if (lim < 16) {
+        const unsigned past = lim <= 0 ? 0xffffu : (0xffffu << lim) & 0xffffu;
+        ws |= past;
+        nl |= past;
+    }
+    return ws | nl << 16;
 }
 
-__device__ __forceinline__ unsigned long long fnv1a_step(unsigned long long h, unsigned c) {
-    return (h ^ c) * 0x100000001B3ull;
+__device__ __forceinline__ unsigned block_mask(const TileText& T, long long b) {
+    if (b >= T.W0 && b < T.W1) return T.msk[b - T.W0];
+    return masks_of(*T.tv, T.blk(b), b);
 }
+
+// 16 text bytes starting at p (little-endian words).
+__device__ __forceinline__ void window16(const TileText& T, long long p, unsigned out[4]) {
+    const long long a = p + T.tv->shift;
+    const long long b = a >> 4;
+    const int o = (int)(a & 15);
+    const uint4 v0 = T.blk(b);
+    const uint4 v1 = o ? T.blk(b + 1) : make_uint4(0, 0, 0, 0);
+    const unsigned x[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+    const int ow = o >> 2, ob = o & 3;
+    unsigned y[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        const unsigned a0 = x[k], a1 = x[k + 1], a2 = x[k + 2];
+        const unsigned a3 = k + 3 < 8 ? x[k + 3] : 0u;
+        y[k] = ow == 0 ? a0 : ow == 1 ? a1 : ow == 2 ? a2 : a3;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) out[k] = ob ? __builtin_amdgcn_alignbyte(y[k + 1], y[k], ob) : y[k];
+}
+
+__device__ __forceinline__ unsigned wbyte(const unsigned w[4], int k) { return (w[k >> 2] >> (8 * (k & 3))) & 0xffu; }
 
 // Chromosome id of field [a, b) after lstrip('chr'); -1 = skip, -2 = raise.
-__device__ int lookup_chrom(const ParseArgs& A, Reader& rd, long long a, long long b, unsigned long long* hout,
-                            int* lout) {
-    while (a < b) {
-        const unsigned c = rd.get(a);
-        if (c == 'c' || c == 'h' || c == 'r') ++a; else break;
+__device__ int lookup_chrom(const ParseArgs& A, const TileText& T, long long a, long long b, int* key_len,
+                            uint32_t* key_hash) {
+    unsigned w[4];
+    // lstrip('chr'): leading 'c' / 'h' / 'r' bytes, 16 at a time
+    for (;;) {
+        const long long L = b - a;
+        if (L <= 0) break;
+        window16(T, a, w);
+        unsigned m = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const unsigned x = w[q];
+            m |= hi_to_nibble(zero_bytes_hi(x ^ 0x63636363u) | zero_bytes_hi(x ^ 0x68686868u) |
+                              zero_bytes_hi(x ^ 0x72727272u)) << (4 * q);
+        }
+        int k = __ffs(~m & 0x1ffffu) - 1;  // leading stripped bytes (<= 16)
+        if (k > L) k = (int)L;
+        a += k;
+        if (k < 16) break;
     }
-    unsigned long long h = 0xcbf29ce484222325ull;
-    bool digits = a < b;
-    for (long long p = a; p < b; ++p) {
-        const unsigned c = rd.get(p);
-        h = fnv1a_step(h, c);
-        digits = digits && c >= '0' && c <= '9';
-    }
-    if (h == 0) h = 1;
-    *hout = h;
-    *lout = (int)(b - a);
     const int len = (int)(b - a);
-    for (int k = 0, slot = (int)(h & A.table_mask);; ++k, slot = (slot + 1) & A.table_mask) {
-        const NameEntry e = A.table[slot];
-        if (e.hash == 0 || k > A.table_mask) break;
-        if (e.hash != h || e.len != len) continue;
+    window16(T, a, w);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {  // zero the bytes past the name
+        const int keep = len - 4 * q;
+        w[q] = keep >= 4 ? w[q] : keep <= 0 ? 0u : (w[q] & ((1u << (8 * keep)) - 1u));
+    }
+    const uint32_t h = name_hash(w, len);
+    *key_len = len;
+    *key_hash = h;
+    for (int k = 0, slot = (int)(h & A.table_mask); k <= A.table_mask; ++k, slot = (slot + 1) & A.table_mask) {
+        const NameEntry& e = A.table[slot];
+        const int id = e.id;
+        if (id == kEmptySlot) break;
+        if (e.hash != h || e.len != len || e.w[0] != w[0] || e.w[1] != w[1] || e.w[2] != w[2] || e.w[3] != w[3])
+            continue;
         bool eq = true;
-        for (int q = 0; q < len && eq; ++q) eq = (unsigned char)A.names[e.off + q] == rd.get(a + q);
-        if (eq) return e.id;
+        for (int q = 16; q < len && eq; ++q) eq = (unsigned char)A.names[e.off + q] == T.get(a + q);
+        if (eq) return id;
+    }
+    bool digits = len > 0;
+    for (long long p = a; p < b && digits; ++p) {
+        const unsigned c = T.get(p);
+        digits = c >= '0' && c <= '9';
     }
     if (A.unknown_policy == 2 || (A.unknown_policy == 1 && digits)) return -2;
     return -1;
 }
 
-// Python int() of an ASCII field: optional sign, then digits only.
-__device__ bool parse_int(Reader& rd, long long a, long long b, long long* out) {
+// Python int() of an ASCII field: optional sign, then 1..18 digits.
+// Digits are validated with SWAR byte classes on a 16-byte window and
+// accumulated by Horner steps in 32-bit (<= 9 digits; 64-bit beyond).
+__device__ bool parse_int(const TileText& T, long long a, long long b, long long* out) {
     bool neg = false;
     if (a < b) {
-        const unsigned c = rd.get(a);
+        const unsigned c = T.get(a);
         if (c == '+' || c == '-') { neg = c == '-'; ++a; }
     }
-    if (a >= b || b - a > 18) return false;
+    const long long L = b - a;
+    if (L <= 0 || L > 18) return false;
     long long v = 0;
-    for (long long p = a; p < b; ++p) {
-        const unsigned c = rd.get(p);
-        if (c < '0' || c > '9') return false;
-        v = v * 10 + (c - '0');
+    if (L <= 16) {
+        unsigned w[4];
+        window16(T, a, w);
+        const int n = (int)L;
+        unsigned dm = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const unsigned x = w[q];
+            const unsigned r = (x | 0x80808080u) - 0x30303030u;
+            const unsigned lt10 = ~((r & 0x7F7F7F7Fu) + 0x76767676u) & 0x80808080u;
+            dm |= hi_to_nibble(r & lt10 & ~x & 0x80808080u) << (4 * q);
+        }
+        const unsigned need = n >= 16 ? 0xFFFFu : ((1u << n) - 1u);
+        if ((dm & need) != need) return false;
+        unsigned lo = 0;
+#pragma unroll
+        for (int k = 0; k < 9; ++k)
+            if (k < n) lo = (lo << 3) + (lo << 1) + (wbyte(w, k) - '0');
+        v = lo;
+        for (int k = 9; k < n; ++k) v = v * 10 + (long long)(wbyte(w, k) - '0');
+    } else {
+        for (long long p = a; p < b; ++p) {
+            const unsigned c = T.get(p);
+            if (c < '0' || c > '9') return false;
+            v = v * 10 + (c - '0');
+        }
     }
     *out = neg ? -v : v;
     return true;
 }
 
-__global__ __launch_bounds__(kScanThreads) void k_parse_bin(ParseArgs A) {
-    __shared__ unsigned wcnt[4];
-    __shared__ unsigned long long bbase;
-    const long long li = (long long)blockIdx.x * kScanThreads + threadIdx.x;
-    const bool live = li < A.n_lines;
-    int status = 0;  // 0 none, 1 kept, 2 skip(check), 3 skip(mark), 4 error
-    int ecode = 0;
-    int id1 = -1, id2 = -1;
-    long long p1 = 0, p2 = 0;
-    bool same_name = false;
-    if (live) {
-        Reader rd{&A.tv};
-        const long long ls = li == 0 ? 0 : A.nl[li - 1] + 1;
-        const long long le = A.nl[li];
-        long long fa[4] = {-1, -1, -1, -1}, fb[4] = {0, 0, 0, 0};
-        const int want[4] = {A.f_c1, A.f_p1, A.f_c2, A.f_p2};
-        int maxf = max(max(A.f_c1, A.f_p1), max(A.f_c2, A.f_p2));
-        long long la = -1, lb = -1;  // last field
-        int nf = 0;
-        long long p = ls;
-        while (p < le) {
-            while (p < le && is_ws(rd.get(p))) ++p;
-            if (p >= le) break;
-            const long long a = p;
-            while (p < le && !is_ws(rd.get(p))) ++p;
+// Position of the k-th (0-based) set bit of a 16-bit mask (branch-free).
+__device__ __forceinline__ int kth_bit(unsigned m, int k) {
+    int pos = 0;
+    int c = __popc(m & 0xffu);
+    bool g = k >= c;
+    k -= g ? c : 0; m = g ? m >> 8 : m; pos += g ? 8 : 0;
+    c = __popc(m & 0xfu);
+    g = k >= c;
+    k -= g ? c : 0; m = g ? m >> 4 : m; pos += g ? 4 : 0;
+    c = __popc(m & 0x3u);
+    g = k >= c;
+    k -= g ? c : 0; m = g ? m >> 2 : m; pos += g ? 2 : 0;
+    g = k >= (int)(m & 1u);
+    return pos + (g ? 1 : 0);
+}
+
+struct LineOut {
+    int status;  // 0 none, 1 kept, 2 skip(check), 3 skip(mark), 4 error
+    int ecode;
+    int id1, id2;
+    long long p1, p2;
+    bool same_name;
+};
+
+// Field boundaries of the line starting at text position ls from the
+// blocks' whitespace masks (Python `line.strip().split()`), then the
+// reference's filters and int() parses.
+__device__ LineOut parse_line(const ParseArgs& A, const TileText& T, long long ls) {
+    LineOut o{1, 0, -1, -1, 0, 0, false};
+    long long fa[4] = {-1, -1, -1, -1}, fb[4] = {0, 0, 0, 0};
+    const int want[4] = {A.f_c1, A.f_p1, A.f_c2, A.f_p2};
+    const int maxf = max(max(A.f_c1, A.f_p1), max(A.f_c2, A.f_p2));
+    // One uniform pass over the line's blocks records, for each wanted field,
+    // the block (its base position and start / end mask) holding its start
+    // and its end; positions are resolved afterwards with kth_bit.  Lanes
+    // stay converged (no per-field branches inside the block loop).
+    long long sbase[4], ebase[4];
+    unsigned smask[4], emask[4];
+    int sk[4], ek[4];
 #pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (want[k] == nf) { fa[k] = a; fb[k] = p; }
-            la = a;
-            lb = p;
-            ++nf;
-            if (A.mark_len == 0 && nf > maxf) break;
+    for (int q = 0; q < 4; ++q) { sbase[q] = ebase[q] = 0; smask[q] = emask[q] = 0; sk[q] = ek[q] = -1; }
+    long long lsb = 0, leb = 0;  // last start / end block (mark mode)
+    unsigned lsm = 0, lem = 0;
+    int nf = 0;  // fields started
+    bool infield = false, done = false;
+    const long long a0 = ls + T.tv->shift;
+    long long b = a0 >> 4;
+    unsigned pre = (1u << (a0 & 15)) - 1u;  // bytes of the first block before the line
+    while (!done) {
+        const unsigned mk = block_mask(T, b);
+        const unsigned ws = (mk & 0xffffu) | pre;
+        const unsigned nl = (mk >> 16) & ~pre;
+        pre = 0;
+        const int endk = nl ? __ffs(nl) - 1 : 16;                 // the line's '\n' (or 16)
+        const unsigned live = endk == 16 ? 0xffffu : ((1u << endk) - 1u);
+        const unsigned nonws = ~ws & live;
+        const unsigned prev = ((nonws << 1) | (infield ? 1u : 0u)) & 0x1ffffu;
+        const unsigned st = nonws & ~prev;
+        const unsigned en = ~nonws & prev & (endk == 16 ? 0xffffu : ((2u << endk) - 1u));
+        const long long pos0 = b * 16 - T.tv->shift;
+        const int ns = __popc(st), ne = __popc(en);
+        const int e0 = infield ? nf - 1 : nf;  // field index of this block's first end
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int js = want[q] - nf, je = want[q] - e0;
+            const bool hs = js >= 0 && js < ns, he = je >= 0 && je < ne;
+            sbase[q] = hs ? pos0 : sbase[q];
+            smask[q] = hs ? st : smask[q];
+            sk[q] = hs ? js : sk[q];
+            ebase[q] = he ? pos0 : ebase[q];
+            emask[q] = he ? en : emask[q];
+            ek[q] = he ? je : ek[q];
         }
-        status = 1;
-        if (A.mark_len > 0) {  // `if line[-1] != 'Both': continue` (:1133)
-            if (nf == 0) {
-                status = 4; ecode = kErrFields;
-            } else {
-                bool eq = (lb - la) == A.mark_len;
-                for (int q = 0; q < A.mark_len && eq; ++q) eq = rd.get(la + q) == (unsigned char)A.mark[q];
-                if (!eq) status = 3;
+        lsb = st ? pos0 : lsb;
+        lsm = st ? st : lsm;
+        leb = en ? pos0 : leb;
+        lem = en ? en : lem;
+        nf += ns;
+        infield = (nonws >> 15) & 1u;
+        done = endk < 16 || (A.mark_len == 0 && nf - (infield ? 1 : 0) > maxf);
+        ++b;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        if (sk[q] >= 0 && ek[q] >= 0) {
+            fa[q] = sbase[q] + kth_bit(smask[q], sk[q]);
+            fb[q] = ebase[q] + kth_bit(emask[q], ek[q]);
+        }
+    }
+    long long la = -1, lb = -1;
+    if (nf > 0) {
+        la = lsb + 31 - __clz(lsm);
+        lb = leb + 31 - __clz(lem);
+    }
+    if (A.mark_len > 0) {  // `if line[-1] != 'Both': continue` (:1133)
+        if (nf == 0) {
+            o.status = 4; o.ecode = kErrFields;
+            return o;
+        }
+        bool eq = (lb - la) == A.mark_len;
+        for (int q = 0; q < A.mark_len && eq; ++q) eq = T.get(la + q) == (unsigned char)A.mark[q];
+        if (!eq) { o.status = 3; return o; }
+    }
+    if (fa[0] < 0 || fa[2] < 0) { o.status = 4; o.ecode = kErrFields; return o; }
+    int l1 = 0, l2 = 0;
+    uint32_t h1 = 0, h2 = 0;
+    o.id1 = lookup_chrom(A, T, fa[0], fb[0], &l1, &h1);
+    o.id2 = lookup_chrom(A, T, fa[2], fb[2], &l2, &h2);
+    if (o.id1 == -1 || o.id2 == -1) { o.status = 2; return o; }
+    if (o.id1 >= 0 && o.id2 >= 0) {
+        o.same_name = o.id1 == o.id2;
+    } else {  // an unknown name: compare the stripped names byte by byte
+        bool eq = l1 == l2 && h1 == h2;
+        const long long s1 = fb[0] - l1, s2 = fb[2] - l2;
+        for (int q = 0; q < l1 && eq; ++q) eq = T.get(s1 + q) == T.get(s2 + q);
+        o.same_name = eq;
+    }
+    const bool need_local = A.has_local && o.same_name && A.hap1 == A.hap2;
+    const bool need = A.has_whole || need_local;
+    if (o.id1 == -2 || o.id2 == -2) {
+        if (need) { o.status = 4; o.ecode = kErrName; }
+        else o.status = 2;  // never indexed by the reference: no effect
+        return o;
+    }
+    if (need) {
+        if (fa[1] < 0 || fa[3] < 0) { o.status = 4; o.ecode = kErrFields; }
+        else if (!parse_int(T, fa[1], fb[1], &o.p1) || !parse_int(T, fa[3], fb[3], &o.p2) || o.p1 < 0 || o.p2 < 0) {
+            o.status = 4; o.ecode = kErrInt;
+        }
+    }
+    return o;
+}
+
+// p // res with the target's round-up multiplier (Granlund-Montgomery:
+// l = ceil(log2 res), magic = floor(2^32 (2^l - res) / res) + 1; exact for
+// every 32-bit p; res == 1 -> msh = -1).
+__device__ __forceinline__ long long div_res(long long p, const TargetDev& T) {
+    if ((unsigned long long)p >= 0x100000000ull) return p / T.res;
+    const unsigned n = (unsigned)p;
+    if (T.msh < 0) return n;
+    const unsigned t = __umulhi(T.magic, n);
+    return (long long)((t + ((n - t) >> 1)) >> T.msh);
+}
+
+// Fused line split + parse + bin.  Persistent grid: block i parses tiles
+// i, i + G, ...; keys go to chunks of C slots of a target's key buffer that
+// the block reserves with one atomic each (a single shared cursor bumped per
+// round serialises ~1e6 same-address atomics); the unused tail of a block's
+// last chunk is filled with the all-ones sentinel, which sorts after every
+// key (keys use 2 * shift bits, bins < 2^shift - 1).
+__global__ __launch_bounds__(kScanThreads) void k_parse_tile(ParseArgs A, int TB, long long n_tiles, int C) {
+    extern __shared__ uint4 dyn[];
+    __shared__ unsigned starts[kScanThreads];
+    __shared__ unsigned long long sh[4];
+    __shared__ unsigned wcnt4[4][4];
+    __shared__ unsigned long long cbase[kMaxTargets];
+    __shared__ unsigned cused[kMaxTargets];
+    __shared__ unsigned long long nbase4[4];
+    const TextView& tv = A.tv;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const long long nblk_all = (tv.shift + tv.nbytes + 15) >> 4;
+    unsigned* msk = reinterpret_cast<unsigned*>(dyn + (TB + 1 + kPLookBlk));
+    if (tid < kMaxTargets) {
+        cbase[tid] = 0;
+        cused[tid] = (unsigned)C;  // no chunk yet
+    }
+    unsigned n_kept = 0, n_chr = 0, n_mark = 0, n_lines = 0;
+    for (long long tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+        const long long T0 = tile * TB;
+        const long long T1 = min(T0 + TB, nblk_all);
+        const long long W0 = max(0ll, T0 - 1);
+        const long long W1 = min(nblk_all, T1 + kPLookBlk);
+        const int nw = (int)(W1 - W0);
+        __syncthreads();  // previous tile's readers are done with dyn / msk / starts
+        for (int k = tid; k < nw; k += kScanThreads) {
+            const uint4 v = load16(tv.abase, W0 + k);
+            dyn[k] = v;
+            msk[k] = masks_of(tv, v, W0 + k);
+        }
+        __syncthreads();
+        const TileText T{dyn, msk, W0, W1, &tv, nblk_all};
+        if (A.ablate == 1) continue;
+        // line starts of this thread's segment as bitmasks: aligned coordinate a
+        // starts a line when a == shift (text position 0) or byte a - 1 is '\n'
+        const int SB = TB / kScanThreads;
+        const long long s0 = T0 + (long long)tid * SB;
+        unsigned m[kPMaxSeg];
+        unsigned cnt = 0;
+        unsigned carry = (s0 > 0 && s0 < T1) ? (msk[s0 - 1 - W0] >> 31) & 1u : 0u;
+#pragma unroll
+        for (int j = 0; j < kPMaxSeg; ++j) {
+            m[j] = 0;
+            if (j < SB && s0 + j < T1) {
+                const long long b = s0 + j;
+                const unsigned nl = msk[b - W0] >> 16;
+                unsigned st = ((nl << 1) | carry) & 0xffffu;
+                carry = (nl >> 15) & 1u;
+                // only real text positions start lines: [shift, shift + nbytes)
+                const long long lo = tv.shift - b * 16, hi = tv.shift + tv.nbytes - b * 16;
+                if (lo > 0) st &= lo >= 16 ? 0u : (0xffffu << lo) & 0xffffu;
+                if (lo >= 0 && lo < 16) st |= 1u << lo;  // text position 0
+                if (hi < 16) st &= hi <= 0 ? 0u : ((1u << hi) - 1u);
+                m[j] = st;
+                cnt += __popc(st);
             }
         }
-        if (status == 1 && (fa[0] < 0 || fa[2] < 0)) { status = 4; ecode = kErrFields; }
-        unsigned long long h1 = 0, h2 = 0;
-        int l1 = 0, l2 = 0;
-        if (status == 1) {
-            id1 = lookup_chrom(A, rd, fa[0], fb[0], &h1, &l1);
-            id2 = lookup_chrom(A, rd, fa[2], fb[2], &h2, &l2);
-            if (id1 == -1 || id2 == -1) status = 2;
-        }
-        if (status == 1) {
-            same_name = h1 == h2 && l1 == l2;  // c1 == c2 (names; id compare below for known ids)
-            if (id1 >= 0 && id2 >= 0) same_name = id1 == id2;
-            const bool need_local = A.has_local && same_name && A.hap1 == A.hap2;
-            const bool need = A.has_whole || need_local;
-            if (need && (id1 == -2 || id2 == -2)) { status = 4; ecode = kErrName; }
-            else if (id1 == -2 || id2 == -2) status = 2;  // never indexed by the reference: no effect
-            else if (need) {
-                if (fa[1] < 0 || fa[3] < 0) { status = 4; ecode = kErrFields; }
-                else if (!parse_int(rd, fa[1], fb[1], &p1) || !parse_int(rd, fa[3], fb[3], &p2) || p1 < 0 || p2 < 0) {
-                    status = 4; ecode = kErrInt;
+        unsigned long long total = 0;
+        const unsigned mybase = (unsigned)block_excl_scan_u64(cnt, sh, &total);
+        const int nlines = (int)total;
+        n_lines += nlines;
+        for (int base = 0; base < nlines; base += kScanThreads) {
+            // this round's line starts (indices [base, base + 256)) into LDS
+            if (mybase + cnt > (unsigned)base && mybase < (unsigned)base + kScanThreads) {
+                unsigned idx = mybase;
+#pragma unroll
+                for (int j = 0; j < kPMaxSeg; ++j) {
+                    unsigned x = m[j];
+                    while (x) {
+                        const int k = __ffs(x) - 1;
+                        x &= x - 1;
+                        if (idx >= (unsigned)base && idx < (unsigned)base + kScanThreads)
+                            starts[idx - base] = (unsigned)((s0 + j - T0) * 16 + k);
+                        ++idx;
+                    }
+                }
+            }
+            __syncthreads();
+            if (A.ablate == 2) continue;
+            const int li = base + tid;
+            LineOut L{0, 0, -1, -1, 0, 0, false};
+            long long ls = 0;
+            if (li < nlines) {
+                ls = T0 * 16 + starts[tid] - tv.shift;
+                L = parse_line(A, T, ls);
+                if (L.status == 4) atomicMin(A.err, (unsigned long long)ls << 8 | (unsigned)L.ecode);
+                n_kept += L.status == 1;
+                n_chr += L.status == 2;
+                n_mark += L.status == 3;
+            }
+            // keys of up to 4 targets per compaction phase (3 barriers)
+            for (int t0 = 0; t0 < (A.ablate == 3 ? 0 : A.n_targets); t0 += 4) {
+                bool ok[4];
+                unsigned long long key[4];
+                unsigned rk[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int t = t0 + u;
+                    ok[u] = false;
+                    key[u] = 0;
+                    if (t < A.n_targets && L.status == 1) {
+                        const TargetDev& TG = A.t[t];
+                        long long b1 = 0, b2 = 0;
+                        bool in_range = true;
+                        if (TG.local) {
+                            ok[u] = L.same_name && A.hap1 == A.hap2;
+                            if (ok[u]) {
+                                const long long q1 = div_res(L.p1, TG), q2 = div_res(L.p2, TG);
+                                in_range = q1 < TG.nbins[L.id1] && q2 < TG.nbins[L.id2];
+                                b1 = TG.start[A.hap1 * A.n_chroms + L.id1] + q1;
+                                b2 = TG.start[A.hap2 * A.n_chroms + L.id2] + q2;
+                            }
+                        } else {
+                            ok[u] = true;
+                            b1 = TG.start[A.hap1 * A.n_chroms + L.id1] + div_res(L.p1, TG);
+                            b2 = TG.start[A.hap2 * A.n_chroms + L.id2] + div_res(L.p2, TG);
+                            in_range = b1 < TG.n_bins && b2 < TG.n_bins;
+                        }
+                        if (!in_range) {
+                            atomicMin(A.err, (unsigned long long)ls << 8 | (unsigned)kErrBin);
+                            ok[u] = false;
+                        }
+                        if (ok[u]) {
+                            const unsigned long long lo = (unsigned long long)min(b1, b2),
+                                                     hi = (unsigned long long)max(b1, b2);
+                            key[u] = lo << TG.shift | hi;
+                        }
+                    }
+                    const unsigned long long mm = __ballot(ok[u]);
+                    rk[u] = __popcll(mm & ((1ull << lane) - 1ull));
+                    if (lane == 0) wcnt4[u][w] = (unsigned)__popcll(mm);
+                }
+                __syncthreads();
+                if (tid < 4 && t0 + tid < A.n_targets) {  // one lane per target reserves a chunk if needed
+                    const unsigned tot = wcnt4[tid][0] + wcnt4[tid][1] + wcnt4[tid][2] + wcnt4[tid][3];
+                    const unsigned room = (unsigned)C - cused[t0 + tid];
+                    if (tot > room) nbase4[tid] = atomicAdd(A.t[t0 + tid].count, (unsigned long long)C);
+                }
+                __syncthreads();
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int t = t0 + u;
+                    if (t < A.n_targets && ok[u]) {
+                        unsigned idx = rk[u];
+                        for (int k = 0; k < w; ++k) idx += wcnt4[u][k];
+                        const unsigned used = cused[t];
+                        const unsigned room = (unsigned)C - used;
+                        A.t[t].keys[idx < room ? cbase[t] + used + idx : nbase4[u] + (idx - room)] = key[u];
+                    }
+                }
+                __syncthreads();  // everyone has read cused / cbase / nbase4
+                if (tid < 4 && t0 + tid < A.n_targets) {
+                    const int t = t0 + tid;
+                    const unsigned tot = wcnt4[tid][0] + wcnt4[tid][1] + wcnt4[tid][2] + wcnt4[tid][3];
+                    const unsigned used = cused[t];
+                    const unsigned room = (unsigned)C - used;
+                    if (tot > room) {
+                        cbase[t] = nbase4[tid];
+                        cused[t] = tot - room;
+                    } else {
+                        cused[t] = used + tot;
+                    }
                 }
             }
         }
-        if (status == 4) atomicMin(A.err, (unsigned long long)(A.line_base + li) << 8 | (unsigned)ecode);
     }
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    __syncthreads();
+    // sentinel-fill the unused tail of each target's last chunk
     for (int t = 0; t < A.n_targets; ++t) {
-        const TargetDev& T = A.t[t];
-        bool ok = false;
-        unsigned long long key = 0;
-        if (status == 1) {
-            long long b1, b2;
-            bool in_range;
-            if (T.local) {
-                ok = same_name && A.hap1 == A.hap2;
-                const long long s1 = p1 / T.res, s2 = p2 / T.res;
-                in_range = ok ? (s1 < T.nbins[id1] && s2 < T.nbins[id2]) : true;
-                b1 = ok ? T.start[A.hap1 * A.n_chroms + id1] + s1 : 0;
-                b2 = ok ? T.start[A.hap2 * A.n_chroms + id2] + s2 : 0;
-            } else {
-                ok = true;
-                b1 = T.start[A.hap1 * A.n_chroms + id1] + p1 / T.res;
-                b2 = T.start[A.hap2 * A.n_chroms + id2] + p2 / T.res;
-                in_range = b1 < T.n_bins && b2 < T.n_bins;
-            }
-            if (!in_range) {
-                atomicMin(A.err, (unsigned long long)(A.line_base + li) << 8 | (unsigned)kErrBin);
-                ok = false;
-            }
-            if (ok) {
-                const unsigned long long lo = (unsigned long long)min(b1, b2), hi = (unsigned long long)max(b1, b2);
-                key = lo << T.shift | hi;
-            }
-        }
-        const unsigned long long m = __ballot(ok);
-        const unsigned rk = __popcll(m & ((1ull << lane) - 1ull));
-        if (lane == 0) wcnt[w] = (unsigned)__popcll(m);
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            const unsigned tot = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
-            bbase = tot ? atomicAdd(T.count, (unsigned long long)tot) : 0ull;
-        }
-        __syncthreads();
-        unsigned before = 0;
-        for (int k = 0; k < w; ++k) before += wcnt[k];
-        if (ok) T.keys[bbase + before + rk] = key;
-        __syncthreads();
+        const unsigned used = cused[t];
+        const unsigned gap = (unsigned)C - used;
+        for (unsigned k = tid; k < gap; k += kScanThreads) A.t[t].keys[cbase[t] + used + k] = ~0ull;
+        if (tid == 0 && gap) atomicAdd(A.t[t].gaps, (unsigned long long)gap);
     }
-    // line statistics (one atomic per wave and kind)
-    const unsigned long long m0 = __ballot(live), m1 = __ballot(status == 1), m2 = __ballot(status == 2),
-                             m3 = __ballot(status == 3);
+    // line statistics: one atomic per wave and kind
+    const unsigned long long c1 = wave_sum_ll(n_kept), c2 = wave_sum_ll(n_chr), c3 = wave_sum_ll(n_mark);
     if (lane == 0) {
-        if (m0) atomicAdd(A.stats + 0, (unsigned long long)__popcll(m0));
-        if (m1) atomicAdd(A.stats + 1, (unsigned long long)__popcll(m1));
-        if (m2) atomicAdd(A.stats + 2, (unsigned long long)__popcll(m2));
-        if (m3) atomicAdd(A.stats + 3, (unsigned long long)__popcll(m3));
+        if (w == 0 && n_lines) atomicAdd(A.stats + 0, (unsigned long long)n_lines);
+        if (c1) atomicAdd(A.stats + 1, c1);
+        if (c2) atomicAdd(A.stats + 2, c2);
+        if (c3) atomicAdd(A.stats + 3, c3);
     }
+}
+
+// Lines before byte `upto` of a chunk (error reports only).
+__global__ void k_count_nl(TextView tv, long long upto, unsigned long long* __restrict__ out) {
+    unsigned long long c = 0;
+    for (long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x; p < upto; p += (long long)gridDim.x * blockDim.x) {
+        const long long a = p + tv.shift;
+        c += byte_of(load16(tv.abase, a >> 4), (int)(a & 15)) == '\n';
+    }
+    c = wave_sum_ll((long long)c);
+    if ((threadIdx.x & 63) == 0 && c) atomicAdd(out, c);
 }
 
 // ------------------------------------------------------------ radix sort
@@ -663,12 +987,16 @@ using namespace hh;
 struct hh_binner {
     struct Target {
         int32_t res = 0, local = 0, shift = 0;
+        uint32_t magic = 0;  // division by res: see div_res
+        int32_t msh = -1;
         int64_t n_bins = 0;
         DBuf<long long> start;
         DBuf<int32_t> nbins;
         DBuf<unsigned long long> keys;
-        DBuf<unsigned long long> count;  // device counter
-        int64_t n_keys = 0;              // host mirror after sync
+        DBuf<unsigned long long> count;  // device: slots reserved (keys + sentinels)
+        DBuf<unsigned long long> gaps;   // device: sentinel slots
+        int64_t n_keys = 0;              // host mirror of count after each feed
+        int64_t n_gaps = 0;              // host mirror of gaps
         // results of finish
         bool done = false;
         int64_t nnz = 0;
@@ -696,12 +1024,6 @@ struct hh_binner {
 
 namespace hh {
 
-static unsigned long long host_fnv(const char* s, int n) {
-    unsigned long long h = 0xcbf29ce484222325ull;
-    for (int k = 0; k < n; ++k) h = (h ^ (unsigned char)s[k]) * 0x100000001B3ull;
-    return h == 0 ? 1 : h;
-}
-
 static void ensure_keys(hh_binner::Target& T, int64_t need, hipStream_t s) {
     if ((int64_t)T.keys.n >= need) return;
     const int64_t cap = std::max<int64_t>(need, (int64_t)(T.keys.n * 3 / 2) + (1 << 20));
@@ -712,20 +1034,29 @@ static void ensure_keys(hh_binner::Target& T, int64_t need, hipStream_t s) {
     T.keys = std::move(nk);
 }
 
-static void raise_parse_error(hh_binner* B, hipStream_t s) {
+// First erroneous line of the chunk just parsed (byte offset from the error
+// word) -> 1-based line number in the whole feed; raises.
+static void raise_parse_error(hh_binner* B, const TextView& tv, int64_t lines_before, hipStream_t s) {
     unsigned long long e = 0;
     HIP_CHECK(hipMemcpyAsync(&e, B->err.p, sizeof(e), hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
     if (e == ~0ull) return;
-    const long long line = (long long)(e >> 8);
+    const long long at = (long long)(e >> 8);
     const int code = (int)(e & 0xff);
+    DBuf<unsigned long long> nl(1);
+    nl.zero(s);
+    if (at > 0)
+        hipLaunchKernelGGL(k_count_nl, dim3((unsigned)std::min<long long>(4096, (at + 255) / 256)), dim3(256), 0, s, tv,
+                           at, nl.p);
+    unsigned long long before = 0;
+    HIP_CHECK(hipMemcpyAsync(&before, nl.p, sizeof(before), hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipMemsetAsync(B->err.p, 0xff, sizeof(unsigned long long), s));
+    HIP_CHECK(hipStreamSynchronize(s));
     const char* what = code == kErrFields ? "missing field (IndexError in the reference)"
                        : code == kErrInt  ? "position is not a non-negative integer (ValueError in the reference)"
                        : code == kErrName ? "chromosome passes the chroms filter but is not in genomeSize (KeyError in the reference)"
                                           : "bin outside the matrix (IndexError in the reference)";
-    // reset so the object stays usable for inspection; the caller discards it
-    HIP_CHECK(hipMemsetAsync(B->err.p, 0xff, sizeof(unsigned long long), s));
-    HH_THROW(HH_ERR_ARG, "pair line " + std::to_string(line + 1) + ": " + what);
+    HH_THROW(HH_ERR_ARG, "pair line " + std::to_string(lines_before + (long long)before + 1) + ": " + what);
 }
 
 // Parse one device-resident text chunk that starts at a line start.
@@ -735,29 +1066,8 @@ static void feed_device(hh_binner* B, const char* text, int64_t nbytes, const hh
     tv.abase = reinterpret_cast<const char*>(reinterpret_cast<uintptr_t>(text) & ~uintptr_t(15));
     tv.shift = text - tv.abase;
     tv.nbytes = nbytes;
-    const long long nblk = (tv.shift + nbytes + 15) / 16;
-    const long long ntile = (nblk + kScanThreads - 1) / kScanThreads;
-    DBuf<unsigned> cnt(ntile);
-    DBuf<unsigned long long> off(ntile), tot(1);
-    hipLaunchKernelGGL(k_nl_count, dim3((unsigned)ntile), dim3(kScanThreads), 0, s, tv, nblk, cnt.p);
-    exclusive_scan<unsigned, unsigned long long>(cnt.p, off.p, ntile, tot.p, s);
-    unsigned long long n_nl = 0;
-    char last = 0;
-    HIP_CHECK(hipMemcpyAsync(&n_nl, tot.p, sizeof(n_nl), hipMemcpyDeviceToHost, s));
-    HIP_CHECK(hipMemcpyAsync(&last, text + nbytes - 1, 1, hipMemcpyDeviceToHost, s));
-    HIP_CHECK(hipStreamSynchronize(s));
-    const long long n_lines = (long long)n_nl + (last != '\n' ? 1 : 0);
-    DBuf<long long> nl(n_lines);
-    hipLaunchKernelGGL(k_nl_write, dim3((unsigned)ntile), dim3(kScanThreads), 0, s, tv, nblk, off.p, nl.p);
-    if (last != '\n') {  // final line without a newline: it ends at nbytes
-        const long long endp = nbytes;
-        HIP_CHECK(hipMemcpyAsync(nl.p + n_nl, &endp, sizeof(endp), hipMemcpyHostToDevice, s));
-    }
     ParseArgs A{};
     A.tv = tv;
-    A.nl = nl.p;
-    A.n_lines = n_lines;
-    A.line_base = B->lines_seen;
     A.table = B->table.p;
     A.names = B->names.p;
     A.table_mask = B->table_mask;
@@ -766,34 +1076,74 @@ static void feed_device(hh_binner* B, const char* text, int64_t nbytes, const hh
     A.f_p1 = f->col_pos1;
     A.f_c2 = f->col_chrom2;
     A.f_p2 = f->col_pos2;
+    HH_REQUIRE(std::min(std::min(A.f_c1, A.f_p1), std::min(A.f_c2, A.f_p2)) >= 0, "negative field index");
     A.mark_len = (int)strnlen(f->mark, sizeof(f->mark));
+    HH_REQUIRE(A.mark_len < (int)sizeof(f->mark), "mark must be NUL-terminated (<= 15 bytes)");
     std::memcpy(A.mark, f->mark, sizeof(A.mark));
     A.hap1 = f->hap1;
     A.hap2 = f->hap2;
+    HH_REQUIRE((A.hap1 == 0 || A.hap1 == 1) && (A.hap2 == 0 || A.hap2 == 1), "hap1/hap2 in {0, 1}");
     A.n_chroms = B->n_chroms;
     A.n_targets = (int)B->t.size();
     A.err = B->err.p;
     A.stats = B->stats.p;
+    A.ablate = g_parse_ablate;
+    // tile size: ~230 lines per 256-thread block, from the mean line length
+    // of the first 64 KB (multiples of 256 aligned blocks, 4..40 KB)
+    const int64_t ns = std::min<int64_t>(nbytes, 65536);
+    std::vector<char> sample(ns);
+    HIP_CHECK(hipMemcpyAsync(sample.data(), text, ns, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    const int64_t nnl = std::count(sample.begin(), sample.end(), '\n');
+    const double mean_len = nnl ? (double)ns / (double)nnl : (double)ns;
+    int TB = (int)std::lround(230.0 * mean_len / 16.0 / kScanThreads) * kScanThreads;
+    TB = std::min(std::max(TB, kScanThreads), kPMaxSeg * kScanThreads);
+    const long long nblk_all = (tv.shift + nbytes + 15) >> 4;
+    const long long n_tiles = (nblk_all + TB - 1) / TB;
+    // persistent grid (4 blocks per CU) and key-chunk size: ~1/16 of a
+    // block's expected lines, 256..4096 slots
+    int dev = 0, n_cu = 256;
+    HIP_CHECK(hipGetDevice(&dev));
+    HIP_CHECK(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
+    const long long grid = std::max<long long>(1, std::min<long long>(n_tiles, 4ll * n_cu));
+    const double lines_per_block = (double)nbytes / mean_len / (double)grid;
+    int C = 256;
+    while (C < 4096 && 2.0 * C * 16.0 <= lines_per_block) C <<= 1;
+    // a line that yields a key has > max field index fields, each a byte plus
+    // a separator: bounds the keys this chunk can append to any target
+    const int maxf = std::max(std::max(A.f_c1, A.f_p1), std::max(A.f_c2, A.f_p2));
+    const int64_t max_keys = (nbytes + 1) / (2 * (maxf + 1)) + 1;
     for (size_t k = 0; k < B->t.size(); ++k) {
         auto& T = B->t[k];
         HH_REQUIRE(!T.done, "hh_binner_feed after hh_binner_finish");
-        ensure_keys(T, T.n_keys + n_lines, s);
+        // every chunk a block opens is filled except its last: keys + grid * C
+        ensure_keys(T, T.n_keys + max_keys + grid * (int64_t)C, s);
         A.has_whole |= T.local == 0;
         A.has_local |= T.local != 0;
-        A.t[k] = TargetDev{T.start.p, T.nbins.p, T.keys.p, T.count.p, (long long)T.n_bins, (long long)T.res,
-                           T.local, T.shift};
+        A.t[k] = TargetDev{T.start.p, T.nbins.p, T.keys.p, T.count.p, T.gaps.p, (long long)T.n_bins,
+                           (long long)T.res, T.local, T.shift, T.magic, T.msh};
     }
-    if (n_lines)
-        hipLaunchKernelGGL(k_parse_bin, dim3(grid_of(n_lines, kScanThreads)), dim3(kScanThreads), 0, s, A);
+    const int64_t lines_before = B->lines_seen;
+    const size_t lds = (size_t)(TB + 1 + kPLookBlk) * (sizeof(uint4) + sizeof(unsigned));
+    {
+        HH_KTIME("k_parse_tile", s);
+        hipLaunchKernelGGL(k_parse_tile, dim3((unsigned)grid), dim3(kScanThreads), lds, s, A, TB, n_tiles, C);
+    }
     HIP_CHECK(hipGetLastError());
-    B->lines_seen += n_lines;
-    // key counts back to the host (sizes the next chunk's capacity check)
-    std::vector<unsigned long long> c(B->t.size());
-    for (size_t k = 0; k < B->t.size(); ++k)
-        HIP_CHECK(hipMemcpyAsync(&c[k], B->t[k].count.p, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    // slot / gap counts and lines back to the host (capacity of the next feed)
+    std::vector<unsigned long long> c(2 * B->t.size() + 1);
+    for (size_t k = 0; k < B->t.size(); ++k) {
+        HIP_CHECK(hipMemcpyAsync(&c[2 * k], B->t[k].count.p, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+        HIP_CHECK(hipMemcpyAsync(&c[2 * k + 1], B->t[k].gaps.p, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    }
+    HIP_CHECK(hipMemcpyAsync(&c.back(), B->stats.p, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
-    for (size_t k = 0; k < B->t.size(); ++k) B->t[k].n_keys = (int64_t)c[k];
-    raise_parse_error(B, s);
+    for (size_t k = 0; k < B->t.size(); ++k) {
+        B->t[k].n_keys = (int64_t)c[2 * k];
+        B->t[k].n_gaps = (int64_t)c[2 * k + 1];
+    }
+    B->lines_seen = (int64_t)c.back();
+    raise_parse_error(B, tv, lines_before, s);
 }
 
 static void sort_keys(DBuf<unsigned long long>& keys, int64_t n, int bits, hipStream_t s) {
@@ -805,11 +1155,17 @@ static void sort_keys(DBuf<unsigned long long>& keys, int64_t n, int bits, hipSt
     unsigned long long* b = tmp.p;
     int passes = 0;
     for (int shift = 0; shift < bits; shift += 8, ++passes) {
-        hipLaunchKernelGGL(k_rs_hist, dim3((unsigned)tiles), dim3(kScanThreads), 0, s, a, (long long)n, shift,
-                           tiles, hist.p);
+        {
+            HH_KTIME("k_rs_hist", s);
+            hipLaunchKernelGGL(k_rs_hist, dim3((unsigned)tiles), dim3(kScanThreads), 0, s, a, (long long)n, shift,
+                               tiles, hist.p);
+        }
         exclusive_scan<unsigned, unsigned>(hist.p, off.p, 256 * tiles, nullptr, s);
-        hipLaunchKernelGGL(k_rs_scatter, dim3((unsigned)tiles), dim3(kScanThreads), 0, s, a, b, (long long)n, shift,
-                           tiles, off.p);
+        {
+            HH_KTIME("k_rs_scatter", s);
+            hipLaunchKernelGGL(k_rs_scatter, dim3((unsigned)tiles), dim3(kScanThreads), 0, s, a, b, (long long)n,
+                               shift, tiles, off.p);
+        }
         HIP_CHECK(hipGetLastError());
         std::swap(a, b);
     }
@@ -845,18 +1201,21 @@ int hh_binner_create(int32_t n_chroms, const char* names, const int32_t* name_id
         int cap = 16;
         while (cap < 4 * std::max(n_names, 1)) cap <<= 1;
         std::vector<NameEntry> tab(cap);
-        for (auto& e : tab) e = NameEntry{0, 0, 0, 0, 0};
+        for (auto& e : tab) e = NameEntry{{0, 0, 0, 0}, 0, kEmptySlot, 0, 0};
         for (int k = 0; k < n_names; ++k) {
-            const unsigned long long h = host_fnv(bytes.data() + span[k].first, span[k].second);
-            int slot = (int)(h & (cap - 1));
+            NameEntry ne{{0, 0, 0, 0}, span[k].second, name_ids[k], span[k].first, 0};
+            for (int q = 0; q < std::min(16, span[k].second); ++q)
+                ne.w[q >> 2] |= (uint32_t)(unsigned char)bytes[span[k].first + q] << (8 * (q & 3));
+            ne.hash = name_hash(ne.w, ne.len);
+            int slot = (int)(ne.hash & (uint32_t)(cap - 1));
             for (;;) {
                 auto& e = tab[slot];
-                if (e.hash == 0) {
-                    e = NameEntry{h, span[k].first, span[k].second, name_ids[k], 0};
+                if (e.id == kEmptySlot) {
+                    e = ne;
                     break;
                 }
-                HH_REQUIRE(!(e.hash == h && e.len == span[k].second &&
-                             std::memcmp(bytes.data() + e.off, bytes.data() + span[k].first, e.len) == 0),
+                HH_REQUIRE(!(e.len == ne.len &&
+                             std::memcmp(bytes.data() + e.off, bytes.data() + ne.off, e.len) == 0),
                            "duplicate chromosome name");
                 slot = (slot + 1) & (cap - 1);
             }
@@ -896,8 +1255,14 @@ int hh_binner_add_target(hh_binner* B, int32_t res, int32_t local, const int64_t
         T.local = local ? 1 : 0;
         T.n_bins = n_bins;
         int sh = 1;
-        while ((int64_t(1) << sh) < n_bins) ++sh;
+        while ((int64_t(1) << sh) <= n_bins) ++sh;  // bins < 2^sh - 1: the all-ones key is free
         T.shift = sh;
+        if (res > 1) {
+            int l = 0;
+            while ((int64_t(1) << l) < res) ++l;
+            T.magic = (uint32_t)(((unsigned __int128)1 << 32) * ((uint64_t(1) << l) - (uint64_t)res) / (uint64_t)res + 1);
+            T.msh = l - 1;
+        }
         hipStream_t s = 0;
         std::vector<long long> st(chrom_start, chrom_start + 2 * B->n_chroms);
         std::vector<int32_t> nb(chrom_nbins, chrom_nbins + B->n_chroms);
@@ -907,6 +1272,8 @@ int hh_binner_add_target(hh_binner* B, int32_t res, int32_t local, const int64_t
         T.nbins = to_device(nb, s);
         T.count.alloc(1);
         T.count.zero(s);
+        T.gaps.alloc(1);
+        T.gaps.zero(s);
         HIP_CHECK(hipStreamSynchronize(s));
         *index_out = (int32_t)B->t.size();
         B->t.push_back(std::move(T));
@@ -973,12 +1340,10 @@ int hh_binner_finish(hh_binner* B, void* stream) {
         hipStream_t s = as_stream(stream);
         for (auto& T : B->t) {
             if (T.done) continue;
-            const int64_t n = T.n_keys;
-            HH_REQUIRE(n < (int64_t(1) << 32) - 1, "more than 2^32 pairs in one matrix");
-            {
-                HH_KTIME("k_rs_sort", s);
-                sort_keys(T.keys, n, 2 * T.shift, s);
-            }
+            const int64_t n_all = T.n_keys;  // keys + sentinels (sorted last)
+            HH_REQUIRE(n_all < (int64_t(1) << 32) - 1, "more than 2^32 pairs in one matrix");
+            sort_keys(T.keys, n_all, 2 * T.shift, s);
+            const int64_t n = T.n_keys - T.n_gaps;
             DBuf<unsigned> head(std::max<int64_t>(n, 1)), idx(std::max<int64_t>(n, 1));
             DBuf<unsigned long long> tot(1);
             unsigned long long nu = 0;
@@ -1012,7 +1377,7 @@ int hh_binner_target_nnz(const hh_binner* B, int32_t target, int64_t* nnz, int64
         HH_REQUIRE(B && target >= 0 && target < (int)B->t.size(), "bad target");
         const auto& T = B->t[target];
         if (nnz) *nnz = T.done ? T.nnz : -1;
-        if (n_pairs) *n_pairs = T.n_keys;
+        if (n_pairs) *n_pairs = T.n_keys - T.n_gaps;
     });
 }
 

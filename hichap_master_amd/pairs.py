@@ -251,9 +251,13 @@ class PairBinner:
         self.finished = True
 
     def n_pairs(self, t: Target) -> int:
+        return self.sizes(t)[1]
+
+    def sizes(self, t: Target):
+        """(pixels, pairs) of a target (pixels = -1 before finish)."""
         a, b = C.c_int64(0), C.c_int64(0)
         call("hh_binner_target_nnz", self._h, t.index, C.byref(a), C.byref(b))
-        return int(b.value)
+        return int(a.value), int(b.value)
 
     def pixels(self, t: Target):
         """(bin1, bin2, count) int32 host arrays of a finished target, sorted
