@@ -62,7 +62,8 @@ int hh_ktime_reset(void);
  * the symmetric matrix (both triangles of cooler's upper-triangle pixel table)
  * for the rows [row_lo, row_hi) a rank owns, cut into 512-row blocks x
  * 8192-column tiles; each tile stores its rows' entries as uint16
- * (count << 13 | column offset, counts 1..7) and uint32 (counts 8..2^19-1)
+ * (swizzled LDS byte offset << 3 | count, counts 1..7) and uint32 (count << 16 |
+ * offset, counts 8..65535)
  * segments, rows padded to 16 B, counts >= 2^19 in a small per-row wide
  * list, plus a per-row diagonal.  Static filters
  * (ignore_diags, cis_only zero_trans, zero counts) are applied at build time.
