@@ -107,6 +107,11 @@ SIGNATURES = {
     "hh_binner_target_nnz": (C.c_int, [P, I32, PI64, PI64]),
     "hh_binner_download": (C.c_int, [P, I32, P, P, P]),
     "hh_binner_pixels_device": (C.c_int, [P, I32, P, P, P]),
+    "hh_hiccups_create": (C.c_int, [P, P, P, I64, I32, I32, I32, P, C.POINTER(P)]),
+    "hh_hiccups_free": (C.c_int, [P]),
+    "hh_hiccups_set_pixels": (C.c_int, [P, P, P, I64, P]),
+    "hh_hiccups_width": (C.c_int, [P, I32, PI64, P]),
+    "hh_hiccups_results": (C.c_int, [P, P, P, P, P, P, P]),
     "hh_synth_pairs_text": (C.c_int, [I32, C.c_char_p, P, I64, F64, F64, I32, C.c_uint64, I64, P, I64, PI64, P]),
 }
 

@@ -18,6 +18,8 @@
  *   hh_compartment_*    StructureFind.Distance_Decay / Get_PCA / Select_PC_new,
  *                       StructureFind.py:201-423
  *   hh_di_scan          StructureFind.Get_Gap / Get_DI, StructureFind.py:721-839
+ *   hh_hiccups_*        StructureFind.pcaller neighbourhood sums (HICCUPS loops),
+ *                       StructureFind.py:1631-1830
  *   hh_binner_*         the per-line pair binning loops of TraditionalMatrixBuilding
  *                       (matrixBuilding.py:566-596), TraditionalMatrixInAllelic
  *                       (:817-854) and HaplotypeMatrixBuilding's unimputed
@@ -64,7 +66,7 @@ int hh_ktime_reset(void);
  * 8192-column tiles; each tile stores its rows' entries as uint16
  * (swizzled LDS byte offset << 3 | count, counts 1..7) and uint32 (count << 16 |
  * offset, counts 8..65535)
- * segments, rows padded to 16 B, counts >= 2^19 in a small per-row wide
+ * segments, rows padded to 16 B, counts > 65535 in a small per-row wide
  * list, plus a per-row diagonal.  Static filters
  * (ignore_diags, cis_only zero_trans, zero counts) are applied at build time.
  * Shards are whole 512-row blocks (row_lo % 512 == 0).
@@ -316,6 +318,27 @@ int hh_binner_pixels_device(const hh_binner* b, int32_t target, const int32_t** 
 int hh_synth_pairs_text(int32_t n_chroms, const char* names, const int64_t* lengths, int64_t n_lines,
                         double cis_frac, double max_dist, int32_t format, uint64_t seed, int64_t line0, char* out,
                         int64_t capacity, int64_t* nbytes, void* stream);
+
+/* ------------------------------------------------ HICCUPS loop calling
+ * The neighbourhood sums of StructureFind.pcaller (StructureFind.py:1631-1830)
+ * for one chromosome.  Bands are row-major N x num (num = maxapart / res +
+ * maxww + 1; band[r][d] = M[r][r + d], 0 past the matrix): Hb raw counts with
+ * the main diagonal zeroed, Cb balanced counts on diagonals ww..num-1 (0
+ * elsewhere); Eall[d] = expected on diagonal d (0 for d < ww). */
+typedef struct hh_hiccups hh_hiccups;
+int hh_hiccups_create(const double* Hb, const double* Cb, const double* Eall, int64_t N, int32_t num, int32_t pw,
+                      int32_t on_device, void* stream, hh_hiccups** out);
+int hh_hiccups_free(hh_hiccups* h);
+/* Candidate pixels (row <= col, col - row < num); resets every pixel to pending. */
+int hh_hiccups_set_pixels(hh_hiccups* h, const int32_t* row, const int32_t* col, int64_t n, void* stream);
+/* One window width w (>= pw): every pending pixel whose lower-left raw reads
+ * reach 16 gets its donut / lower-left balanced and expected sums and is
+ * assigned; *newly_valid = how many (the caller applies the reference's
+ * stop rule: fewer than 10 % of the pending pixels). */
+int hh_hiccups_width(hh_hiccups* h, int32_t w, int64_t* newly_valid, void* stream);
+/* Per pixel: donut / lower-left sums of the balanced (sK, sY) and expected
+ * (eK, eY) bands at its width; width[i] = that w (0 = never assigned). */
+int hh_hiccups_results(hh_hiccups* h, double* sK, double* sY, double* eK, double* eY, uint8_t* width, void* stream);
 
 #ifdef __cplusplus
 }
