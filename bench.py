@@ -373,6 +373,141 @@ def _nbins(genome, res):
     return sum(l // res + 1 for l in genome.values())
 
 
+LOOPS_RES = 10000
+
+
+def loops_band(N, res, seed=20201018, depth=60.0):
+    """Synthetic raw band (N x num) of one chromosome: power-law decay,
+    log-normal visibility, planted loop pixels, 1 % empty bins; weights =
+    1 / sqrt(row sum) (NaN for empty bins).  Band-only: no N x N matrix."""
+    from hichap_master_amd import loops
+    p = loops.peaks_parameter(res)
+    num = p["maxapart"] // res + p["maxww"] + 1
+    rng = np.random.default_rng(seed)
+    vis = rng.lognormal(0, 0.2, N)
+    d = np.arange(num)[None, :]
+    r = np.arange(N)[:, None]
+    inside = (r + d) < N
+    lam = depth * (d + 1.0) ** -1.0 * vis[:, None] * vis[np.minimum(r + d, N - 1)]
+    for _ in range(N // 40):
+        a = int(rng.integers(5, N - num))
+        b = int(rng.integers(p["ww"] + 2, num - 4))
+        lam[a - 1:a + 2, b - 1:b + 2] *= 4.0
+    Hb = np.where(inside, rng.poisson(lam), 0)
+    gaps = rng.choice(N, size=N // 100, replace=False)
+    Hb[gaps, :] = 0
+    for g in gaps:  # column g of the band matrix
+        rows = np.arange(max(0, g - num + 1), g + 1)
+        Hb[rows, g - rows] = 0
+    rs = Hb.sum(1).astype(float)
+    w = np.where(rs > 0, 1.0 / np.sqrt(np.maximum(rs, 1.0)), np.nan)
+    return Hb, w, num
+
+
+def loops_dense_from_band(Hb):
+    N, num = Hb.shape
+    H = np.zeros((N, N), dtype=np.int64)
+    r = np.repeat(np.arange(N), num)
+    c = r + np.tile(np.arange(num), N)
+    ok = c < N
+    H[r[ok], c[ok]] = Hb.ravel()[ok]
+    H[c[ok], r[ok]] = Hb.ravel()[ok]
+    return H
+
+
+def run_loops(args, world, rank, local):
+    """HICCUPS on hg19 chr1 at 10 kb: one step = the
+    window-widening loop (donut / lower-left sums of every candidate pixel,
+    one launch per width, the reference's stop rule) over bands resident in
+    HBM.  Ranks run independent chromosomes (weak scaling, no collective)."""
+    import torch
+    from hichap_master_amd import _lib, loops, synth
+    N = synth.chrom_bins([synth.HG19["1"]], LOOPS_RES)[0]
+    t0 = time.perf_counter()
+    Hb, w, num = loops_band(N, LOOPS_RES, seed=20201018 + rank)
+    H = loops_dense_from_band(Hb)
+    t_wall = time.perf_counter()
+    D, L, widths = loops.pcaller(H, w, LOOPS_RES, return_widths=True)   # whole chromosome, host glue included
+    wall_s = time.perf_counter() - t_wall
+    B = loops.bands(H, w, LOOPS_RES)
+    del H
+    xi, yi = loops.candidates(B)
+    nb = loops.Neighbourhood(B)
+    nb.set_pixels(xi, yi)
+    gen_s = time.perf_counter() - t0
+
+    def step():
+        nb.reset()
+        nb.widen()
+
+    def barrier():
+        if torch.distributed.is_initialized():
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier()
+    elapsed = time.perf_counter() - t_start
+    _lib.call("hh_ktime_reset")
+    _lib.call("hh_ktime_enable", 1)
+    step()
+    torch.cuda.synchronize()
+    _lib.call("hh_ktime_enable", 0)
+    k_ms, k_n = _lib.ktime("k_hiccups_width")
+    nb.close()
+    tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    if torch.distributed.is_initialized():
+        torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
+    elapsed = float(tt.item())
+    if rank == 0:
+        n = int(xi.size)
+        prefix_bytes = 3.0 * N * (num + 1) * 8.0  # the three prefix arrays, read once per launch at best
+        k_avg = k_ms / max(k_n, 1) / 1000.0
+        achieved = prefix_bytes / k_avg / 1e9 if k_avg > 0 else None
+        out = {
+            "metric": "HICCUPS candidate pixels/sec (window-widening neighbourhood sums, hg19 chr1 10 kb)",
+            "value": world * n * args.steps / elapsed, "unit": "pixels/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": 1000.0 * elapsed / args.steps, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic chr1 band (power-law decay, planted loops) generated on the host",
+            "config": {"workload": "hg19-chr1-10kb-hiccups", "bins": int(N), "band_diagonals": int(num),
+                       "candidates": n, "widths": widths, "calls": len(D),
+                       "pcaller_wall_s_incl_host_glue": round(wall_s, 3), "setup_s": round(gen_s, 2),
+                       "parallelism": f"independent chromosomes x{world}" if world > 1 else "single GPU"},
+            "roofline": {"bound": "hbm", "kernel": "k_hiccups_width", "achieved": achieved, "peak": PEAK_HBM_GBS,
+                         "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS if achieved else None, "traffic": None,
+                         "launches_per_step": k_n, "kernel_ms_avg": k_avg * 1000.0,
+                         "alg_bytes_per_launch": prefix_bytes,
+                         "note": "gather-bound (L2/MALL): ~150 prefix lookups per pixel per width"},
+        }
+        if world == 1 and not args.no_cpu:
+            out["cpu_baseline"] = loops_cpu_baseline()
+        print(json.dumps(out), flush=True)
+
+
+def loops_cpu_baseline(budget_s=12.0):
+    """Oracle (oracle/loops_ref.py: the reference's window loop restated with
+    dense-band gathers per offset) on a 1500-bin piece of the same model."""
+    from hichap_master_amd import loops
+    from oracle import loops_ref
+    Hb, w, num = loops_band(8000, LOOPS_RES, seed=7)
+    H = loops_dense_from_band(Hb)
+    P = loops_ref.prepare(H, w, LOOPS_RES)
+    xi, yi = loops_ref.candidates(P)
+    t0 = time.perf_counter()
+    loops_ref.neighbourhood(P, xi, yi)
+    dt = time.perf_counter() - t0
+    return {"value": xi.size / dt, "unit": "pixels/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/loops_ref.neighbourhood on an 8000-bin chromosome of the same model "
+                      f"({xi.size} candidates) in {dt:.1f}s (NumPy; the reference's own scipy.sparse "
+                      f"shifted-diagonal sums are slower still)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -400,8 +535,8 @@ def main():
             os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT="29531", RANK="0", WORLD_SIZE="1")
         tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
-    if args.config in ("c5", "pairs"):
-        (run_c5 if args.config == "c5" else run_pairs)(args, world, rank, local)
+    if args.config in ("c5", "pairs", "loops"):
+        {"c5": run_c5, "pairs": run_pairs, "loops": run_loops}[args.config](args, world, rank, local)
         if torch.distributed.is_initialized():
             torch.distributed.destroy_process_group()
         return

@@ -111,6 +111,7 @@ SIGNATURES = {
     "hh_hiccups_free": (C.c_int, [P]),
     "hh_hiccups_set_pixels": (C.c_int, [P, P, P, I64, P]),
     "hh_hiccups_width": (C.c_int, [P, I32, PI64, P]),
+    "hh_hiccups_reset": (C.c_int, [P, P]),
     "hh_hiccups_results": (C.c_int, [P, P, P, P, P, P, P]),
     "hh_synth_pairs_text": (C.c_int, [I32, C.c_char_p, P, I64, F64, F64, I32, C.c_uint64, I64, P, I64, PI64, P]),
 }

@@ -211,6 +211,16 @@ int hh_hiccups_set_pixels(hh_hiccups* h, const int32_t* row, const int32_t* col,
     });
 }
 
+int hh_hiccups_reset(hh_hiccups* h, void* stream) {
+    return guard([&] {
+        HH_REQUIRE(h, "null");
+        hipStream_t s = as_stream(stream);
+        h->state.zero(s);
+        for (DBuf<double>* b : {&h->sK, &h->sY, &h->eK, &h->eY}) b->zero(s);
+        HIP_CHECK(hipStreamSynchronize(s));
+    });
+}
+
 int hh_hiccups_width(hh_hiccups* h, int32_t w, int64_t* newly_valid, void* stream) {
     return guard([&] {
         HH_REQUIRE(h && newly_valid && w >= 1 && w <= 255, "bad arguments");

@@ -128,14 +128,17 @@ class Neighbourhood:
              int(B["num"]), int(B["pw"]), 0, stream, C.byref(h))
         self._h = h
 
-    def run(self, xi, yi):
-        """The widening loop; returns (S, E, valid, widths) like the oracle."""
-        B = self.B
-        n = xi.size
+    def set_pixels(self, xi, yi):
+        self.n = int(xi.size)
         r32 = np.ascontiguousarray(xi, dtype=np.int32)
         c32 = np.ascontiguousarray(yi, dtype=np.int32)
-        call("hh_hiccups_set_pixels", self._h, ptr(r32), ptr(c32), n, self.stream)
-        pending = n
+        call("hh_hiccups_set_pixels", self._h, ptr(r32), ptr(c32), self.n, self.stream)
+
+    def widen(self):
+        """The widening loop over the current pixels (all pending); returns
+        [(w, newly valid, ratio)] with the reference's stop rule."""
+        B = self.B
+        pending = self.n
         widths = []
         for w in range(B["ww"], B["maxww"] + 1):
             if pending == 0:
@@ -147,6 +150,16 @@ class Neighbourhood:
             widths.append((w, int(nv.value), ratio))
             if ratio < 0.1:
                 break
+        return widths
+
+    def reset(self):
+        call("hh_hiccups_reset", self._h, self.stream)
+
+    def run(self, xi, yi):
+        """The widening loop; returns (S, E, valid, widths) like the oracle."""
+        self.set_pixels(xi, yi)
+        widths = self.widen()
+        n = self.n
         sK, sY, eK, eY = (np.empty(n) for _ in range(4))
         wid = np.empty(n, np.uint8)
         call("hh_hiccups_results", self._h, ptr(sK), ptr(sY), ptr(eK), ptr(eY), ptr(wid), self.stream)

@@ -331,6 +331,8 @@ int hh_hiccups_create(const double* Hb, const double* Cb, const double* Eall, in
 int hh_hiccups_free(hh_hiccups* h);
 /* Candidate pixels (row <= col, col - row < num); resets every pixel to pending. */
 int hh_hiccups_set_pixels(hh_hiccups* h, const int32_t* row, const int32_t* col, int64_t n, void* stream);
+/* Every pixel back to pending (same pixels; repeated runs). */
+int hh_hiccups_reset(hh_hiccups* h, void* stream);
 /* One window width w (>= pw): every pending pixel whose lower-left raw reads
  * reach 16 gets its donut / lower-left balanced and expected sums and is
  * assigned; *newly_valid = how many (the caller applies the reference's
