@@ -492,7 +492,7 @@ def run_loops(args, world, rank, local):
 
 def loops_cpu_baseline(budget_s=12.0):
     """Oracle (oracle/loops_ref.py: the reference's window loop restated with
-    dense-band gathers per offset) on a 1500-bin piece of the same model."""
+    dense-band gathers per offset) on an 8000-bin piece of the same model."""
     from hichap_master_amd import loops
     from oracle import loops_ref
     Hb, w, num = loops_band(8000, LOOPS_RES, seed=7)
