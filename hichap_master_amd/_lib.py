@@ -101,6 +101,9 @@ SIGNATURES = {
     "hh_binner_free": (C.c_int, [P]),
     "hh_binner_add_target": (C.c_int, [P, I32, I32, P, P, I64, PI32]),
     "hh_binner_feed": (C.c_int, [P, C.c_char_p, I64, P, I64, P]),
+    "hh_binner_add_impute_target": (C.c_int, [P, I32, I32, P, P, I64, P, I32, I64, F64, PI32]),
+    "hh_binner_last_reached": (C.c_int, [P, PI64, PI32]),
+    "hh_binner_set_stale": (C.c_int, [P, I32, I64, I32]),
     "hh_binner_feed_device": (C.c_int, [P, P, I64, P, P]),
     "hh_binner_stats": (C.c_int, [P, P]),
     "hh_binner_finish": (C.c_int, [P, P]),

@@ -24,6 +24,7 @@
 //                                    contiguously
 //   k_rle_*                          unique pixels + counts
 #include <algorithm>
+#include <cmath>
 #include <cstring>
 
 #include "hh_common.hpp"
@@ -200,9 +201,19 @@ struct TargetDev {
     long long n_bins;
     long long res;
     int local;               // intra-chromosome matrix (localRes)
-    int shift;               // key = min << shift | max
+    int shift;               // key = min << shift | max (ordered: row << shift | col)
     unsigned magic;          // division by res (div_res)
     int msh;
+    // imputation targets (mode 1; HaplotypeMatrixBuilding :1251-1494)
+    int ordered;             // keys keep (row, col) as incremented (asymmetric matrix)
+    int imp_s;               // L = Imputation_region // res
+    const long long* rowpref;  // unimputed whole matrix, per-row prefix sums, n_bins x (n_bins + 1)
+    const int* disc_j0;      // disc row i of the (2L+1)^2 window covers columns [j0, j1]
+    const int* disc_j1;
+    long long imin;
+    double ratio;
+    long long pp_sum;        // the P pass's stale M_M_sub neighbourhood sum (:1445)
+    int pp_ok;
 };
 
 struct ParseArgs {
@@ -218,13 +229,19 @@ struct ParseArgs {
     int n_chroms;
     int n_targets;
     int has_whole, has_local;
+    int mode;                  // 0 binning, 1 imputation (single-allele lines)
+    int mark2_len;             // imputation: last field == mark2 ('R1') selects the R1 branch
+    char mark2[16];
+    unsigned long long byte_base;  // bytes fed before this chunk (line order across chunks)
+    unsigned long long* lastq;     // max (global line-start byte + 1) << 8 | target of M-pass lines
+                                   // that reached the neighbourhood step (the stale M_M_sub)
     int ablate;                // g_parse_ablate (timing only)
     unsigned long long* err;   // [0] min (line start byte << 8 | code)
     unsigned long long* stats; // [0] lines, [1] kept, [2] skipped (chromosome check), [3] skipped (mark)
     TargetDev t[kMaxTargets];
 };
 
-enum : int { kErrFields = 1, kErrInt = 2, kErrName = 3, kErrBin = 4 };
+enum : int { kErrFields = 1, kErrInt = 2, kErrName = 3, kErrBin = 4, kErrStale = 5 };
 
 // Tile geometry of k_parse_tile: a block owns the lines that START in its
 // tile of aligned 16 B text blocks ([T0, T0 + TB), TB = 256..2560 blocks,
@@ -442,13 +459,14 @@ struct LineOut {
     int id1, id2;
     long long p1, p2;
     bool same_name;
+    bool r1;     // imputation: last field == mark2
 };
 
 // Field boundaries of the line starting at text position ls from the
 // blocks' whitespace masks (Python `line.strip().split()`), then the
 // reference's filters and int() parses.
 __device__ LineOut parse_line(const ParseArgs& A, const TileText& T, long long ls) {
-    LineOut o{1, 0, -1, -1, 0, 0, false};
+    LineOut o{1, 0, -1, -1, 0, 0, false, false};
     long long fa[4] = {-1, -1, -1, -1}, fb[4] = {0, 0, 0, 0};
     const int want[4] = {A.f_c1, A.f_p1, A.f_c2, A.f_p2};
     const int maxf = max(max(A.f_c1, A.f_p1), max(A.f_c2, A.f_p2));
@@ -514,14 +532,19 @@ __device__ LineOut parse_line(const ParseArgs& A, const TileText& T, long long l
         la = lsb + 31 - __clz(lsm);
         lb = leb + 31 - __clz(lem);
     }
-    if (A.mark_len > 0) {  // `if line[-1] != 'Both': continue` (:1133)
+    if (A.mark_len > 0) {  // `if line[-1] != 'Both': continue` (:1133); imputation: `== 'Both'` (:1273)
         if (nf == 0) {
             o.status = 4; o.ecode = kErrFields;
             return o;
         }
         bool eq = (lb - la) == A.mark_len;
         for (int q = 0; q < A.mark_len && eq; ++q) eq = T.get(la + q) == (unsigned char)A.mark[q];
-        if (!eq) { o.status = 3; return o; }
+        if (eq == (A.mode == 1)) { o.status = 3; return o; }
+        if (A.mode == 1) {
+            bool e2 = (lb - la) == A.mark2_len;
+            for (int q = 0; q < A.mark2_len && e2; ++q) e2 = T.get(la + q) == (unsigned char)A.mark2[q];
+            o.r1 = e2;
+        }
     }
     if (fa[0] < 0 || fa[2] < 0) { o.status = 4; o.ecode = kErrFields; return o; }
     int l1 = 0, l2 = 0;
@@ -564,6 +587,84 @@ __device__ __forceinline__ long long div_res(long long p, const TargetDev& T) {
     return (long long)((t + ((n - t) >> 1)) >> T.msh);
 }
 
+// Neighbourhood sum of the unimputed whole matrix over GetNeighborhoodIndex's
+// disc (:721-738) in the window with top-left (r0, c0): per disc row, one
+// difference of row prefix sums.
+__device__ long long disc_sum(const TargetDev& T, long long r0, long long c0) {
+    long long sum = 0;
+    const long long w = T.n_bins + 1;
+    for (int i = 0; i <= 2 * T.imp_s; ++i) {
+        const int j0 = T.disc_j0[i], j1 = T.disc_j1[i];
+        if (j1 < j0) continue;
+        const long long* P = T.rowpref + (r0 + i) * w;
+        sum += P[c0 + j1 + 1] - P[c0 + j0];
+    }
+    return sum;
+}
+
+// Imputation of one single-allele line into one target (:1270-1490): sets
+// *ok / *key (ordered cell); *reached = the line got to the neighbourhood
+// step (it rebinds M_M_sub in the M pass); returns an error code or 0.
+__device__ int impute_key(const ParseArgs& A, const TargetDev& T, const LineOut& L, bool* ok,
+                          unsigned long long* key, bool* reached) {
+    *ok = false;
+    *reached = false;
+    const int n = A.n_chroms, hap = A.hap1;
+    const long long q1 = div_res(L.p1, T), q2 = div_res(L.p2, T);
+    long long row, col;
+    if (L.same_name) {  // intra-chromosome: ordered count, R1 (bin1, bin2) else (bin2, bin1)
+        if (T.local) {
+            if (q1 >= T.nbins[L.id1] || q2 >= T.nbins[L.id2]) return kErrBin;
+            const long long base = T.start[hap * n + L.id1];
+            row = base + (L.r1 ? q1 : q2);
+            col = base + (L.r1 ? q2 : q1);
+        } else {
+            const long long b1 = T.start[hap * n + L.id1] + q1, b2 = T.start[hap * n + L.id2] + q2;
+            if (b1 >= T.n_bins || b2 >= T.n_bins) return kErrBin;
+            row = L.r1 ? b1 : b2;
+            col = L.r1 ? b2 : b1;
+        }
+    } else {
+        if (T.local) return 0;  // inter-chromosome lines only impute the whole matrix
+        const long long s = T.imp_s, N2 = T.n_bins;
+        long long x, mb, pb;    // the allele's own bin, the partner's M / P copies
+        if (L.r1) {
+            x = q1 + T.start[hap * n + L.id1];
+            mb = q2 + T.start[L.id2];
+            pb = q2 + T.start[n + L.id2];
+        } else {                // :1347-1349 (pos2 with chrom1's offset, pos1 with chrom2's)
+            x = q2 + T.start[hap * n + L.id1];
+            mb = q1 + T.start[L.id2];
+            pb = q1 + T.start[n + L.id2];
+        }
+        if (x < s || mb < s || pb < s || x + s + 1 > N2 || mb + s + 1 > N2 || pb + s + 1 > N2) return 0;
+        *reached = true;
+        long long own, other, r_own, c_own, r_oth, c_oth;
+        if (L.r1) {
+            if (hap == 0) own = disc_sum(T, x - s, mb - s);
+            else if (!T.pp_ok) return kErrStale;
+            else own = T.pp_sum;                       // stale M_M_sub (:1445)
+            other = disc_sum(T, x - s, pb - s);
+            r_own = x; c_own = mb; r_oth = x; c_oth = pb;   // the P pass also adds to M_bin2 (:1451)
+        } else if (hap == 0) {
+            own = disc_sum(T, mb - s, x - s);
+            other = disc_sum(T, pb - s, x - s);
+            r_own = x; c_own = mb; r_oth = x; c_oth = pb;
+        } else {
+            own = disc_sum(T, pb - s, x - s);
+            other = disc_sum(T, mb - s, x - s);
+            r_own = pb; c_own = x; r_oth = mb; c_oth = x;
+        }
+        const double tot = (double)(own + other);
+        if (own >= T.imin && (double)own / tot > T.ratio) { row = r_own; col = c_own; }
+        else if (other >= T.imin && (double)other / tot > T.ratio) { row = r_oth; col = c_oth; }
+        else return 0;
+    }
+    *ok = true;
+    *key = (unsigned long long)row << T.shift | (unsigned long long)col;
+    return 0;
+}
+
 // Fused line split + parse + bin.  Persistent grid: block i parses tiles
 // i, i + G, ...; keys go to chunks of C slots of a target's key buffer that
 // the block reserves with one atomic each (a single shared cursor bumped per
@@ -578,6 +679,7 @@ __global__ __launch_bounds__(kScanThreads) void k_parse_tile(ParseArgs A, int TB
     __shared__ unsigned long long cbase[kMaxTargets];
     __shared__ unsigned cused[kMaxTargets];
     __shared__ unsigned long long nbase4[4];
+    __shared__ unsigned long long blk_lastq;
     const TextView& tv = A.tv;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const long long nblk_all = (tv.shift + tv.nbytes + 15) >> 4;
@@ -586,6 +688,7 @@ __global__ __launch_bounds__(kScanThreads) void k_parse_tile(ParseArgs A, int TB
         cbase[tid] = 0;
         cused[tid] = (unsigned)C;  // no chunk yet
     }
+    if (tid == 0) blk_lastq = 0;
     unsigned n_kept = 0, n_chr = 0, n_mark = 0, n_lines = 0;
     for (long long tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
         const long long T0 = tile * TB;
@@ -649,7 +752,7 @@ __global__ __launch_bounds__(kScanThreads) void k_parse_tile(ParseArgs A, int TB
             __syncthreads();
             if (A.ablate == 2) continue;
             const int li = base + tid;
-            LineOut L{0, 0, -1, -1, 0, 0, false};
+            LineOut L{0, 0, -1, -1, 0, 0, false, false};
             long long ls = 0;
             if (li < nlines) {
                 ls = T0 * 16 + starts[tid] - tv.shift;
@@ -669,7 +772,13 @@ __global__ __launch_bounds__(kScanThreads) void k_parse_tile(ParseArgs A, int TB
                     const int t = t0 + u;
                     ok[u] = false;
                     key[u] = 0;
-                    if (t < A.n_targets && L.status == 1) {
+                    if (t < A.n_targets && L.status == 1 && A.mode == 1) {
+                        bool reached = false;
+                        const int e = impute_key(A, A.t[t], L, &ok[u], &key[u], &reached);
+                        if (e) atomicMin(A.err, (unsigned long long)ls << 8 | (unsigned)e);
+                        if (reached && A.hap1 == 0)
+                            atomicMax(&blk_lastq, (A.byte_base + (unsigned long long)ls + 1ull) << 8 | (unsigned)t);
+                    } else if (t < A.n_targets && L.status == 1) {
                         const TargetDev& TG = A.t[t];
                         long long b1 = 0, b2 = 0;
                         bool in_range = true;
@@ -743,6 +852,7 @@ __global__ __launch_bounds__(kScanThreads) void k_parse_tile(ParseArgs A, int TB
         for (unsigned k = tid; k < gap; k += kScanThreads) A.t[t].keys[cbase[t] + used + k] = ~0ull;
         if (tid == 0 && gap) atomicAdd(A.t[t].gaps, (unsigned long long)gap);
     }
+    if (tid == 0 && blk_lastq) atomicMax(A.lastq, blk_lastq);
     // line statistics: one atomic per wave and kind
     const unsigned long long c1 = wave_sum_ll(n_kept), c2 = wave_sum_ll(n_chr), c3 = wave_sum_ll(n_mark);
     if (lane == 0) {
@@ -979,6 +1089,29 @@ __global__ void k_synth_write(SynthPairsDev P, long long n, const unsigned long 
     emit_line(P, i, e);
 }
 
+// P[r][0] = 0, P[r][k] = sum_{c < k} M[r][c] (int64, one wave per row).
+__global__ __launch_bounds__(256) void k_row_prefix_i64(const long long* __restrict__ M, long long n,
+                                                        long long* __restrict__ P) {
+    const long long r = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (r >= n) return;
+    long long carry = 0;
+    long long* out = P + r * (n + 1);
+    if (lane == 0) out[0] = 0;
+    for (long long c0 = 0; c0 < n; c0 += 64) {
+        const long long c = c0 + lane;
+        long long v = c < n ? M[r * n + c] : 0;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const long long t = __shfl_up(v, o, 64);
+            if (lane >= o) v += t;
+        }
+        v += carry;
+        if (c < n) out[c + 1] = v;
+        carry = __shfl(v, 63, 64);
+    }
+}
+
 }  // namespace hh
 
 using namespace hh;
@@ -1001,6 +1134,12 @@ struct hh_binner {
         bool done = false;
         int64_t nnz = 0;
         DBuf<int32_t> bin1, bin2, cnt;
+        // imputation
+        int32_t ordered = 0, imp_s = 0, pp_ok = 0;
+        int64_t imin = 0, pp_sum = 0;
+        double ratio = 0.0;
+        DBuf<long long> rowpref;
+        DBuf<int32_t> disc_j0, disc_j1;
     };
     int device = 0;
     int32_t n_chroms = 0;
@@ -1012,6 +1151,8 @@ struct hh_binner {
     DBuf<unsigned long long> err;    // [1]
     DBuf<unsigned long long> stats;  // [4]
     int64_t lines_seen = 0;
+    int64_t bytes_seen = 0;
+    DBuf<unsigned long long> lastq;  // see ParseArgs::lastq
     // host staging for hh_binner_feed
     PinnedBuf<char> pin[2];
     DBuf<char> dtext[2];
@@ -1055,6 +1196,7 @@ static void raise_parse_error(hh_binner* B, const TextView& tv, int64_t lines_be
     const char* what = code == kErrFields ? "missing field (IndexError in the reference)"
                        : code == kErrInt  ? "position is not a non-negative integer (ValueError in the reference)"
                        : code == kErrName ? "chromosome passes the chroms filter but is not in genomeSize (KeyError in the reference)"
+                       : code == kErrStale ? "no stale M_M_sub neighbourhood for the P pass (NameError / IndexError in the reference)"
                                           : "bin outside the matrix (IndexError in the reference)";
     HH_THROW(HH_ERR_ARG, "pair line " + std::to_string(lines_before + (long long)before + 1) + ": " + what);
 }
@@ -1082,6 +1224,14 @@ static void feed_device(hh_binner* B, const char* text, int64_t nbytes, const hh
     std::memcpy(A.mark, f->mark, sizeof(A.mark));
     A.hap1 = f->hap1;
     A.hap2 = f->hap2;
+    A.mode = f->mode;
+    HH_REQUIRE(A.mode == 0 || A.mode == 1, "mode in {0 (binning), 1 (imputation)}");
+    A.mark2_len = (int)strnlen(f->mark2, sizeof(f->mark2));
+    HH_REQUIRE(A.mark2_len < (int)sizeof(f->mark2), "mark2 must be NUL-terminated (<= 15 bytes)");
+    std::memcpy(A.mark2, f->mark2, sizeof(A.mark2));
+    HH_REQUIRE(A.mode == 0 || (A.mark_len > 0 && A.hap1 == A.hap2), "imputation needs mark ('Both') and hap1 == hap2");
+    A.byte_base = (unsigned long long)B->bytes_seen;
+    A.lastq = B->lastq.p;
     HH_REQUIRE((A.hap1 == 0 || A.hap1 == 1) && (A.hap2 == 0 || A.hap2 == 1), "hap1/hap2 in {0, 1}");
     A.n_chroms = B->n_chroms;
     A.n_targets = (int)B->t.size();
@@ -1120,8 +1270,10 @@ static void feed_device(hh_binner* B, const char* text, int64_t nbytes, const hh
         ensure_keys(T, T.n_keys + max_keys + grid * (int64_t)C, s);
         A.has_whole |= T.local == 0;
         A.has_local |= T.local != 0;
+        HH_REQUIRE((A.mode == 1) == (T.ordered != 0), "imputation targets take imputation feeds only");
         A.t[k] = TargetDev{T.start.p, T.nbins.p, T.keys.p, T.count.p, T.gaps.p, (long long)T.n_bins,
-                           (long long)T.res, T.local, T.shift, T.magic, T.msh};
+                           (long long)T.res, T.local, T.shift, T.magic, T.msh, T.ordered, T.imp_s, T.rowpref.p,
+                           T.disc_j0.p, T.disc_j1.p, (long long)T.imin, T.ratio, (long long)T.pp_sum, T.pp_ok};
     }
     const int64_t lines_before = B->lines_seen;
     const size_t lds = (size_t)(TB + 1 + kPLookBlk) * (sizeof(uint4) + sizeof(unsigned));
@@ -1143,6 +1295,7 @@ static void feed_device(hh_binner* B, const char* text, int64_t nbytes, const hh
         B->t[k].n_gaps = (int64_t)c[2 * k + 1];
     }
     B->lines_seen = (int64_t)c.back();
+    B->bytes_seen += nbytes;
     raise_parse_error(B, tv, lines_before, s);
 }
 
@@ -1229,6 +1382,8 @@ int hh_binner_create(int32_t n_chroms, const char* names, const int32_t* name_id
         HIP_CHECK(hipMemsetAsync(B->err.p, 0xff, sizeof(unsigned long long), s));
         B->stats.alloc(4);
         B->stats.zero(s);
+        B->lastq.alloc(1);
+        B->lastq.zero(s);
         HIP_CHECK(hipStreamSynchronize(s));
         *out = B.release();
     });
@@ -1277,6 +1432,65 @@ int hh_binner_add_target(hh_binner* B, int32_t res, int32_t local, const int64_t
         HIP_CHECK(hipStreamSynchronize(s));
         *index_out = (int32_t)B->t.size();
         B->t.push_back(std::move(T));
+    });
+}
+
+int hh_binner_add_impute_target(hh_binner* B, int32_t res, int32_t local, const int64_t* chrom_start,
+                                const int32_t* chrom_nbins, int64_t n_bins, const int64_t* unimputed, int32_t L,
+                                int64_t imin, double ratio, int32_t* index_out) {
+    int rc = hh_binner_add_target(B, res, local, chrom_start, chrom_nbins, n_bins, index_out);
+    if (rc) return rc;
+    return guard([&] {
+        auto& T = B->t[*index_out];
+        T.ordered = 1;
+        if (local) return;
+        HH_REQUIRE(unimputed && L >= 1 && 2 * (int64_t)L + 1 <= n_bins, "whole imputation target needs the unimputed matrix and 1 <= L");
+        T.imp_s = L;
+        T.imin = imin;
+        T.ratio = ratio;
+        // GetNeighborhoodIndex (:721-732): cells of the (2L+1)^2 window with
+        // sqrt((i-(L+1))^2 + (j-(L+1))^2) < sqrt(L), as column intervals per row
+        std::vector<int32_t> j0(2 * L + 1, 1), j1(2 * L + 1, 0);
+        for (int i = 0; i <= 2 * L; ++i) {
+            int lo = -1, hi = -2;
+            for (int j = 0; j <= 2 * L; ++j) {
+                const double d2 = (double)((i - (L + 1)) * (i - (L + 1)) + (j - (L + 1)) * (j - (L + 1)));
+                if (std::sqrt(d2) < std::sqrt((double)L)) {
+                    if (lo < 0) lo = j;
+                    HH_REQUIRE(hi < 0 || hi == j - 1, "disc row not contiguous");
+                    hi = j;
+                }
+            }
+            if (lo >= 0) { j0[i] = lo; j1[i] = hi; }
+        }
+        hipStream_t s = 0;
+        T.disc_j0 = to_device(j0, s);
+        T.disc_j1 = to_device(j1, s);
+        DBuf<long long> dm((size_t)n_bins * n_bins);
+        dm.upload(reinterpret_cast<const long long*>(unimputed), (size_t)n_bins * n_bins, s);
+        T.rowpref.alloc((size_t)n_bins * (n_bins + 1));
+        hipLaunchKernelGGL(k_row_prefix_i64, dim3((unsigned)((n_bins + 3) / 4)), dim3(256), 0, s, dm.p, (long long)n_bins,
+                           T.rowpref.p);
+        HIP_CHECK(hipGetLastError());
+        HIP_CHECK(hipStreamSynchronize(s));
+    });
+}
+
+int hh_binner_set_stale(hh_binner* B, int32_t target, int64_t pp_sum, int32_t ok) {
+    return guard([&] {
+        HH_REQUIRE(B && target >= 0 && target < (int)B->t.size(), "bad target");
+        B->t[target].pp_sum = pp_sum;
+        B->t[target].pp_ok = ok ? 1 : 0;
+    });
+}
+
+int hh_binner_last_reached(const hh_binner* B, int64_t* byte_offset, int32_t* target) {
+    return guard([&] {
+        HH_REQUIRE(B && byte_offset && target, "null");
+        unsigned long long v = 0;
+        HIP_CHECK(hipMemcpy(&v, B->lastq.p, sizeof(v), hipMemcpyDeviceToHost));
+        *byte_offset = v ? (int64_t)(v >> 8) - 1 : -1;
+        *target = v ? (int32_t)(v & 0xff) : -1;
     });
 }
 

@@ -16,6 +16,7 @@ decisions are bit-identical (``np.percentile`` linear interpolation, the
 from __future__ import annotations
 
 import ctypes as C
+import os
 
 import numpy as np
 
@@ -302,3 +303,118 @@ def HaplotypeUnImputedBuilding(M_M, P_P, M_P, P_M, genomeSize, wholeRes, localRe
               (P_M, pairs.pairs_format(pairs.ALLELIC_BED, "", 1, 0))]
     order, whole, local, wp, lp = _bin_sources(genome, chroms, passes, wholeRes, localRes, True, None)
     return _dense_libs(genome, order, whole, local, wp, lp, dense, haplotype=True)
+
+
+def _materialise(source):
+    """Paths stay paths (read in blocks, seekable); anything else -> bytes."""
+    import os
+    if isinstance(source, (bytes, bytearray, memoryview, str, os.PathLike)):
+        return source
+    if isinstance(source, (list, tuple)) and source and all(isinstance(x, (str, os.PathLike)) and os.path.isfile(x)
+                                                            for x in source):
+        return list(source)
+    from . import pairs
+    return b"".join(pairs._iter_blocks(source, pairs.CHUNK_BYTES))
+
+
+def HaplotypeImputation(M_M, P_P, genomeSize, wholeRes, localRes, chroms, Imputation_region, Imputation_min,
+                        Imputation_ratio, UnImputated_Whole_Lib, UnImputated_Local_Lib):
+    """The imputation passes of HaplotypeMatrixBuilding (:1251-1494) on the
+    GPU: single-allele ('R1' / 'R2') lines of the M_M then P_P beds; intra-
+    chromosome ones add an ordered count, inter-chromosome ones are imputed
+    to the M or P copy whose neighbourhood (GetNeighborhoodIndex disc) in the
+    unimputed whole matrix dominates.  The reference's quirks are kept: R2
+    lines take chrom1's offset for pos2 (:1347-1349); the P pass's R1 branch
+    sums the stale M_M_sub of the M pass's last line to reach that step and
+    adds to chrom2's M copy (:1445-1451).  Returns (Imputated_Whole_Lib,
+    Imputated_Local_Lib) in the reference's dense shapes."""
+    from . import pairs
+    genome = Load_Genome(genomeSize, chroms)
+    M_M, P_P = _materialise(M_M), _materialise(P_P)
+    B = pairs.PairBinner(genome, chroms)
+    try:
+        whole = {}
+        for res in wholeRes:
+            whole[res] = B.add_impute_target(res, False, UnImputated_Whole_Lib[res]["Matrix"],
+                                             int(Imputation_region // res), Imputation_min, Imputation_ratio)
+        local = {res: B.add_impute_target(res, True) for res in localRes}
+        fm = pairs.pairs_format(pairs.ALLELIC_BED, "Both", 0, 0, mode=1, mark2="R1")
+        fp = pairs.pairs_format(pairs.ALLELIC_BED, "Both", 1, 1, mode=1, mark2="R1")
+        B.feed(M_M, fm)
+        # the stale M_M_sub the P pass sums (NameError / IndexError where the reference has none)
+        off, t = B.last_reached()
+        stale = None
+        if off >= 0:
+            f = pairs.line_at(M_M, off).decode().strip().split()
+            rl = next(r for r, tt in whole.items() if tt.index == t)
+            hb, _ = pairs.haplotype_bins(genome, rl)
+            s = int(Imputation_region // rl)
+            c1, c2 = f[0].lstrip("chr"), f[2].lstrip("chr")
+            p1, p2 = int(f[1]) // rl, int(f[3]) // rl
+            U = UnImputated_Whole_Lib[rl]["Matrix"]
+            if f[-1] == "R1":
+                a, mb = p1 + hb["M" + c1][0], p2 + hb["M" + c2][0]
+                stale = U[a - s:a + s + 1, mb - s:mb + s + 1]
+            else:
+                b, mb = p2 + hb["M" + c1][0], p1 + hb["M" + c2][0]
+                stale = U[mb - s:mb + s + 1, b - s:b + s + 1]
+        for res, tt in whole.items():
+            ok, pp = False, 0
+            if stale is not None:
+                ii, jj = pairs.neighborhood_index(int(Imputation_region // res))
+                try:
+                    pp, ok = int(np.asarray(stale)[ii, jj].sum()), True
+                except IndexError:
+                    ok = False
+            B.set_stale(tt, pp, ok)
+        B.feed(P_P, fp)
+        B.finish()
+        IW, IL = {}, {}
+        for res, tt in whole.items():
+            r, c, v = B.pixels(tt)
+            M = np.array(UnImputated_Whole_Lib[res]["Matrix"], dtype=np.int64, copy=True)
+            np.add.at(M, (r.astype(np.int64), c.astype(np.int64)), v.astype(np.int64))
+            IW[res] = {"Bins": UnImputated_Whole_Lib[res]["Bins"], "Matrix": M}
+        order = B.order
+        for res, tt in local.items():
+            r, c, v = B.pixels(tt)
+            r = r.astype(np.int64)
+            IL[res] = {}
+            half = int(tt.chrom_nbins.sum())
+            for h, pre in enumerate("MP"):
+                for k, chro in enumerate(order):
+                    s0 = int(tt.chrom_first[k]) + h * half
+                    n = int(tt.chrom_nbins[k])
+                    lo, hi = np.searchsorted(r, [s0, s0 + n], "left")
+                    M = np.array(UnImputated_Local_Lib[res][pre + chro], dtype=np.int64, copy=True)
+                    np.add.at(M, (r[lo:hi] - s0, c[lo:hi].astype(np.int64) - s0), v[lo:hi].astype(np.int64))
+                    IL[res][pre + chro] = M
+        return IW, IL
+    finally:
+        B.close()
+
+
+def HaplotypeMatrixBuilding(BedFiles, genomeSize, wholeRes, localRes, Imputation_region, Imputation_min,
+                            Imputation_ratio, chroms):
+    """The matrix part of HaplotypeMatrixBuilding (:1044-1494) on the GPU.
+    BedFiles = {'Bi_Allelic', 'M_M', 'P_P', 'M_P', 'P_M': source}; returns the
+    reference's DataSets dict: Tradition_Whole / _Local (all five beds,
+    :1080-1095), UnImputated_Whole / _Local and Imputated_Whole / _Local."""
+    from . import pairs
+    srcs = {k: _materialise(v) for k, v in BedFiles.items()}
+    # the traditional pass reads `cat` of the five beds in sorted file-name order (:1062, :1080-1089)
+    everything = [v for k in sorted(srcs) for v in ([srcs[k]] if not isinstance(srcs[k], list) else srcs[k])]
+    if all(isinstance(v, (str, os.PathLike)) for v in everything):
+        trad_src = everything
+    else:
+        trad_src = b"".join(b"".join(pairs._iter_blocks(v, pairs.CHUNK_BYTES)) for v in everything)
+    DataSets = {}
+    TW, TL = TraditionalMatrixInAllelic(trad_src, genomeSize, wholeRes, localRes, chroms)
+    DataSets["Tradition_Whole"], DataSets["Tradition_Local"] = TW, TL
+    UW, UL = HaplotypeUnImputedBuilding(srcs["M_M"], srcs["P_P"], srcs["M_P"], srcs["P_M"], genomeSize, wholeRes,
+                                        localRes, chroms)
+    DataSets["UnImputated_Whole"], DataSets["UnImputated_Local"] = UW, UL
+    IW, IL = HaplotypeImputation(srcs["M_M"], srcs["P_P"], genomeSize, wholeRes, localRes, chroms,
+                                 Imputation_region, Imputation_min, Imputation_ratio, UW, UL)
+    DataSets["Imputated_Whole"], DataSets["Imputated_Local"] = IW, IL
+    return DataSets

@@ -34,7 +34,8 @@ CHUNK_BYTES = 256 << 20
 
 class PairsFormat(C.Structure):
     _fields_ = [("col_chrom1", C.c_int32), ("col_pos1", C.c_int32), ("col_chrom2", C.c_int32),
-                ("col_pos2", C.c_int32), ("mark", C.c_char * 16), ("hap1", C.c_int32), ("hap2", C.c_int32)]
+                ("col_pos2", C.c_int32), ("mark", C.c_char * 16), ("hap1", C.c_int32), ("hap2", C.c_int32),
+                ("mode", C.c_int32), ("mark2", C.c_char * 16)]
 
 
 # field layouts of the reference's pair files
@@ -42,11 +43,11 @@ VALID_BED = (1, 6, 8, 13)     # TraditionalMatrixBuilding :577-588
 ALLELIC_BED = (0, 1, 2, 3)    # TraditionalMatrixInAllelic :824-836, haplotype passes :1135-1142
 
 
-def pairs_format(cols=VALID_BED, mark="", hap1=0, hap2=0) -> PairsFormat:
-    m = mark.encode()
-    if len(m) > 15:
+def pairs_format(cols=VALID_BED, mark="", hap1=0, hap2=0, mode=0, mark2="") -> PairsFormat:
+    m, m2 = mark.encode(), mark2.encode()
+    if len(m) > 15 or len(m2) > 15:
         raise ValueError("mark longer than 15 bytes")
-    return PairsFormat(cols[0], cols[1], cols[2], cols[3], m, int(hap1), int(hap2))
+    return PairsFormat(cols[0], cols[1], cols[2], cols[3], m, int(hap1), int(hap2), int(mode), m2)
 
 
 # ----------------------------------------------------------- genome / bins
@@ -222,6 +223,39 @@ class PairBinner:
         self.targets.append(t)
         return t
 
+    def add_impute_target(self, res: int, local: bool, unimputed=None, L: int = 0, imin: int = 2,
+                          ratio: float = 0.9) -> Target:
+        """An imputation target (haplotype layout, ordered cells); whole
+        targets take the dense unimputed whole matrix at this resolution."""
+        res = int(res)
+        nb = np.array([self.genome[c] // res + 1 for c in self.order], dtype=np.int64)
+        first = np.concatenate([[0], np.cumsum(nb)[:-1]]).astype(np.int64)
+        total = int(nb.sum())
+        start = np.concatenate([first, first + total])
+        n_bins = 2 * total
+        um = None
+        if not local:
+            um = np.ascontiguousarray(unimputed, dtype=np.int64)
+            if um.shape != (n_bins, n_bins):
+                raise ValueError(f"unimputed matrix must be {n_bins} x {n_bins}")
+        idx = C.c_int32(-1)
+        call("hh_binner_add_impute_target", self._h, res, int(bool(local)), ptr(start), ptr(nb.astype(np.int32)),
+             n_bins, ptr(um), int(L), int(imin), float(ratio), C.byref(idx))
+        t = Target(res, bool(local), True, idx.value)
+        t.n_bins, t.chrom_first, t.chrom_nbins = n_bins, first, nb
+        self.targets.append(t)
+        return t
+
+    def last_reached(self):
+        """(byte offset in the fed stream, target index) of the last M-pass
+        line that reached the imputation neighbourhood step, or (-1, -1)."""
+        off, t = C.c_int64(0), C.c_int32(0)
+        call("hh_binner_last_reached", self._h, C.byref(off), C.byref(t))
+        return int(off.value), int(t.value)
+
+    def set_stale(self, t: Target, pp_sum: int, ok: bool):
+        call("hh_binner_set_stale", self._h, t.index, int(pp_sum), int(bool(ok)))
+
     def feed(self, source, fmt: PairsFormat, chunk_bytes: int = CHUNK_BYTES):
         """Parse + bin a pair source (see _iter_blocks); lines are split at
         newlines across blocks and files exactly like `cat file1 file2 |`."""
@@ -281,6 +315,44 @@ class PairBinner:
             self.close()
         except Exception:
             pass
+
+
+def neighborhood_index(L):
+    """GetNeighborhoodIndex (matrixBuilding.py:721-732): the disc around
+    (L+1, L+1) -- not the window centre -- of radius sqrt(L)."""
+    import math
+    center = L + 1
+    ii, jj = [], []
+    for i in range(L * 2 + 1):
+        for j in range(L * 2 + 1):
+            if math.sqrt((i - center) ** 2 + (j - center) ** 2) < math.sqrt(L):
+                ii.append(i)
+                jj.append(j)
+    return ii, jj
+
+
+def line_at(source, offset):
+    """The text line starting at `offset` of a source's `cat` stream (bytes,
+    a path or a list of paths)."""
+    if isinstance(source, (bytes, bytearray, memoryview)):
+        b = bytes(source)
+        e = b.find(b"\n", offset)
+        return b[offset:] if e < 0 else b[offset:e]
+    paths = [source] if isinstance(source, (str, os.PathLike)) else list(source)
+    out = b""
+    for p in paths:
+        size = os.path.getsize(p)
+        if offset >= size and not out:
+            offset -= size
+            continue
+        with open(p, "rb") as f:
+            f.seek(offset)
+            chunk = f.readline()
+        out += chunk
+        offset = 0
+        if chunk.endswith(b"\n"):
+            break
+    return out.rstrip(b"\n")
 
 
 # ------------------------------------------------------ reference shapes

@@ -280,6 +280,10 @@ typedef struct {
                           line[-1] != 'Both': continue`, :1133)              */
     int32_t hap1, hap2;/* haplotype half of chrom1 / chrom2 (0 = M or the
                           traditional genome, 1 = P)                         */
+    int32_t mode;      /* 0 binning; 1 imputation (HaplotypeMatrixBuilding
+                          :1251-1494): lines whose last field == mark are
+                          skipped, last field == mark2 selects the R1 branch  */
+    char mark2[16];
 } hh_pairs_format;
 /* names: n_names NUL-terminated names back to back (after lstrip('chr'));
  * name_ids[k] = chromosome index (Sort_Chromosomes order) or -2 for a name
@@ -297,6 +301,20 @@ int hh_binner_free(hh_binner* b);
  * caller). */
 int hh_binner_add_target(hh_binner* b, int32_t res, int32_t local, const int64_t* chrom_start,
                          const int32_t* chrom_nbins, int64_t n_bins, int32_t* index_out);
+/* An imputation target (ordered cells: the imputed matrices are asymmetric).
+ * Whole (local = 0): `unimputed` = the unimputed whole matrix (host, n_bins x
+ * n_bins int64, haplotype layout), L = Imputation_region // res, the
+ * Imputation_min / _ratio tests.  Feeds in mode 1: first the M_M text
+ * (hap 0), then — after hh_binner_set_stale — the P_P text (hap 1). */
+int hh_binner_add_impute_target(hh_binner* b, int32_t res, int32_t local, const int64_t* chrom_start,
+                                const int32_t* chrom_nbins, int64_t n_bins, const int64_t* unimputed, int32_t L,
+                                int64_t imin, double ratio, int32_t* index_out);
+/* The M pass's last line (byte offset in the concatenated feeds) that reached
+ * the neighbourhood step, and at which target (-1 / -1: none): the caller
+ * rebuilds the reference's stale M_M_sub from it and sets the P pass's sum
+ * per whole target (ok = 0: the reference raises there). */
+int hh_binner_last_reached(const hh_binner* b, int64_t* byte_offset, int32_t* target);
+int hh_binner_set_stale(hh_binner* b, int32_t target, int64_t pp_sum, int32_t ok);
 /* Parse + bin host text (staged through pinned chunks of chunk_bytes, cut at
  * line ends; 0 = 256 MB) or device-resident text.  Synchronous. */
 int hh_binner_feed(hh_binner* b, const char* text, int64_t nbytes, const hh_pairs_format* f, int64_t chunk_bytes,
