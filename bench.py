@@ -524,6 +524,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # path checks on a 1-GPU box only: every rank on one device, gloo exchange
+    local = int(os.environ.get("HH_DEVICE", local))
+    backend = os.environ.get("HH_DIST_BACKEND", "nccl")
     import torch
     torch.cuda.set_device(local)
     from hichap_master_amd import _lib, dist, ice
@@ -533,7 +536,10 @@ def main():
         import torch.distributed as tdist
         if "MASTER_ADDR" not in os.environ:
             os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT="29531", RANK="0", WORLD_SIZE="1")
-        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            tdist.init_process_group(backend)
 
     if args.config in ("c5", "pairs", "loops"):
         {"c5": run_c5, "pairs": run_pairs, "loops": run_loops}[args.config](args, world, rank, local)
