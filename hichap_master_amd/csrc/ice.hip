@@ -315,11 +315,88 @@ __global__ __launch_bounds__(kSweepThreads, 4) void k_sweep_tiled(TileDev T, con
 
 // ---------------------------------------------------------------- K2
 // marg_r = b_r * (sum of the row's unit partials + wide entries + 2 diag b_r)
+// K1b: the dense diagonal band.  One block per (256-row block, 2048-slot
+// chunk): the chunk's bias window (rows + slots + 1 columns) is staged in LDS
+// with one double of padding per 16, so the 64 lanes of a wave -- each
+// reading 16 consecutive slots of a row from one uint4 -- hit distinct banks;
+// a row's 2048 slots are two fully coalesced uint4 loads per lane (two rows in
+// flight per wave), the counts convert in registers and FMA against LDS.
+// Fixed per-lane order + xor-tree wave reduction: deterministic.
+constexpr int kBandThreads = 512;
+constexpr int kBandWin = kBandRows + kBandChunk + 1;
+__device__ __forceinline__ int bpad(int k) { return k + (k >> 4); }
+
+__device__ __forceinline__ double band_dot16(const uint4 v, const double* __restrict__ bl, int base, double acc) {
+    const unsigned x[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const unsigned c = (x[k >> 2] >> (8 * (k & 3))) & 0xffu;
+        acc = fma((double)c, bl[bpad(base + k)], acc);
+    }
+    return acc;
+}
+
+__global__ __launch_bounds__(kBandThreads) void k_sweep_band(const uint8_t* __restrict__ band, int W, long long nloc,
+                                                             long long row_lo, long long n_bins,
+                                                             const uint8_t* __restrict__ act,
+                                                             const uint16_t* __restrict__ row_group,
+                                                             const double* __restrict__ b,
+                                                             double* __restrict__ bpart) {
+    __shared__ double bl[kBandWin + kBandWin / 16 + 1];
+    const long long r0 = (long long)blockIdx.x * kBandRows;
+    const int chunk = blockIdx.y;
+    const int s0 = chunk * kBandChunk, s1 = min(s0 + kBandChunk, 2 * W);
+    const int nr = (int)min((long long)kBandRows, nloc - r0);
+    const int crosses = (s0 < W && s1 > W) ? 1 : 0;  // the chunk skips the main diagonal
+    const long long g0 = row_lo + r0 + band_diag(s0, W);
+    const int len = nr + (s1 - s0) + crosses;
+    for (int k = threadIdx.x; k < len; k += kBandThreads) {
+        // the band multiplies implicit zeros too: a NaN bias (an empty group
+        // in cis-only mode, whose bins no stored pixel touches) must read 0
+        const long long c = g0 + k;
+        const double v = (c >= 0 && c < n_bins) ? b[c] : 0.0;
+        bl[bpad(k)] = v == v ? v : 0.0;
+    }
+    __syncthreads();
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    constexpr int NW = kBandThreads / 64;
+    for (int rr = wave; rr < nr; rr += 2 * NW) {
+        const int rr2 = rr + NW;
+        const bool two = rr2 < nr;
+        const bool a1 = act[row_group[r0 + rr]] != 0, a2 = two && act[row_group[r0 + rr2]] != 0;
+        const uint8_t* row1 = band + (r0 + rr) * (long long)(2 * W);
+        const uint8_t* row2 = band + (r0 + rr2) * (long long)(2 * W);
+        double acc1 = 0.0, acc2 = 0.0;
+        for (int sb = s0 + lane * 16; sb < s1; sb += 64 * 16 * 2) {
+            const int sc = sb + 64 * 16;
+            const bool hc = sc < s1;
+            uint4 v1 = make_uint4(0, 0, 0, 0), v2 = v1, w1 = v1, w2 = v1;
+            if (a1) v1 = *reinterpret_cast<const uint4*>(row1 + sb);
+            if (a1 && hc) w1 = *reinterpret_cast<const uint4*>(row1 + sc);
+            if (a2) v2 = *reinterpret_cast<const uint4*>(row2 + sb);
+            if (a2 && hc) w2 = *reinterpret_cast<const uint4*>(row2 + sc);
+            const int adj = (sb >= W) ? crosses : 0, adjc = (sc >= W) ? crosses : 0;
+            acc1 = band_dot16(v1, bl, rr + (sb - s0) + adj, acc1);
+            acc2 = band_dot16(v2, bl, rr2 + (sb - s0) + adj, acc2);
+            if (hc) {
+                acc1 = band_dot16(w1, bl, rr + (sc - s0) + adjc, acc1);
+                acc2 = band_dot16(w2, bl, rr2 + (sc - s0) + adjc, acc2);
+            }
+        }
+        acc1 = wave_sum(acc1);
+        acc2 = wave_sum(acc2);
+        if (lane == 0) {
+            if (a1) bpart[(long long)chunk * nloc + r0 + rr] = acc1;
+            if (a2) bpart[(long long)chunk * nloc + r0 + rr2] = acc2;
+        }
+    }
+}
+
 __global__ void k_marg(TileDev T, const double* __restrict__ part, const long long* __restrict__ wide_ptr,
                        const int32_t* __restrict__ wide_col, const double* __restrict__ wide_cnt,
                        const double* __restrict__ diag, const uint16_t* __restrict__ row_group,
                        const uint8_t* __restrict__ act, const double* __restrict__ b, long long row_lo,
-                       int nloc, double* __restrict__ out) {
+                       int nloc, const double* __restrict__ bpart, int nch, double* __restrict__ out) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nloc) return;
     if (act[row_group[i]] == 0) return;
@@ -329,6 +406,7 @@ __global__ void k_marg(TileDev T, const double* __restrict__ part, const long lo
         const int lo = T.u_rlo[u], hi = T.u_rhi[u];
         if (rl >= lo && rl < hi) s += part[T.u_slot[u] + rl - lo];
     }
+    for (int c = 0; c < nch; ++c) s += bpart[(long long)c * nloc + i];  // dense band chunks, fixed order
     for (long long q = wide_ptr[i]; q < wide_ptr[i + 1]; ++q) s = fma(wide_cnt[q], b[wide_col[q]], s);
     const double br = b[row_lo + i];
     out[i] = br * fma(2.0 * diag[i], br, s);
@@ -484,6 +562,8 @@ struct hh_ice {
     int32_t n_tiles = 0;
     DBuf<int32_t> tile_lo, tile_hi, tile_group, group_tile_ptr;
     DBuf<double> bias, marg, part, tile_cnt, tile_sum, tile_sq;
+    DBuf<double> bpart;  // dense band partials: n_band_chunks x nloc
+    int32_t nch = 0;
     DBuf<uint8_t> active;  // 2 x G (parity double buffer)
     DBuf<double> g_var, g_mean;
     DBuf<int32_t> g_iters;
@@ -540,18 +620,28 @@ static void sweep(const hh_matrix* m, const uint8_t* act, const double* b, doubl
     HIP_CHECK(hipGetLastError());
 }
 
+static void sweep_band(hh_ice* S, hipStream_t s) {
+    const hh_matrix* m = S->m;
+    if (!S->nch || !S->nloc) return;
+    const dim3 g((unsigned)((S->nloc + kBandRows - 1) / kBandRows), (unsigned)S->nch);
+    hipLaunchKernelGGL(k_sweep_band, g, dim3(kBandThreads), 0, s, m->band.p, (int)m->band_w, (long long)S->nloc,
+                       (long long)m->row_lo, (long long)m->n_bins, S->act(), m->row_group.p, S->bias.p, S->bpart.p);
+    HIP_CHECK(hipGetLastError());
+}
+
 static void marg_weighted(hh_ice* S, double* out, hipStream_t s, bool timed, int slot) {
     hh_matrix* m = S->m;
     if (timed) HIP_CHECK(hipEventRecord(S->ev[2 * slot], s));
     {
-        HH_KTIME(timed ? nullptr : "k_sweep_tiled", s);  // registry timing for the sharded driver
+        HH_KTIME(timed ? nullptr : "k_sweep_tiled", s);  // registry timing for the sharded driver (tiles + band)
         sweep(m, S->act(), S->bias.p, S->part.p, s);
+        sweep_band(S, s);
     }
     if (timed) HIP_CHECK(hipEventRecord(S->ev[2 * slot + 1], s));
     if (S->nloc == 0) return;
     hipLaunchKernelGGL(k_marg, dim3(nblocks(S->nloc, kThreads)), dim3(kThreads), 0, s, m->dev(), S->part.p,
                        m->wide_ptr.p, m->wide_col.p, m->wide_cnt.p, m->diag.p, m->row_group.p, S->act(),
-                       S->bias.p, (long long)m->row_lo, (int)S->nloc, out);
+                       S->bias.p, (long long)m->row_lo, (int)S->nloc, S->bpart.p, (int)S->nch, out);
     HIP_CHECK(hipGetLastError());
 }
 
@@ -595,6 +685,10 @@ int hh_tune(const char* key, int64_t value) {
         } else if (k == "parse_ablate") {
             HH_REQUIRE(value >= 0 && value <= 3, "parse_ablate in [0, 3]");
             g_parse_ablate = (int)value;
+        } else if (k == "band_w") {
+            HH_REQUIRE(value >= -1 && value <= kBandMaxW && (value <= 0 || value % 16 == 0),
+                       "band_w: -1 (auto), 0 (off) or a multiple of 16 <= 16384");
+            g_band_w = value;
         } else if (k == "sweep_flags") {
             HH_REQUIRE(value >= 0 && value <= 1, "sweep_flags in [0, 1]");
             g_sweep_flags = (int)value;
@@ -648,6 +742,9 @@ int hh_ice_create(hh_matrix* m, const hh_ice_opts* o, hh_ice** out) {
         S->marg.alloc(S->n);
         S->marg.zero(s);
         S->part.alloc(std::max<int64_t>(m->n_part, 1));
+        S->nch = m->band_w > 0 ? (int32_t)((2 * (int64_t)m->band_w + kBandChunk - 1) / kBandChunk) : 0;
+        S->bpart.alloc(std::max<int64_t>((int64_t)S->nch * S->nloc, 1));
+
         S->tile_cnt.alloc(std::max(S->n_tiles, 1));
         S->tile_sum.alloc(std::max(S->n_tiles, 1));
         S->tile_sq.alloc(std::max(S->n_tiles, 1));

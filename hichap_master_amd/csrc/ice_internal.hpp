@@ -36,6 +36,24 @@ extern int64_t g_unit_entries;                           // ~512 KiB of payload 
 constexpr int64_t kMaxBins = (int64_t)1 << 30;
 
 constexpr uint32_t kNarrowMax = 7;                        // counts stored as uint16
+
+// Dense diagonal band: the pixels with 1 <= |col - row| <= W
+// and count <= 255 are stored as uint8 counts with implicit columns, row r's
+// slots [0, 2W) = diagonals -W..-1, 1..W; W is a multiple of 16 chosen from
+// the data (the diagonals whose occupancy is >= kBandDensity), 0 = no band.
+// Everything else (farther, trans, larger counts) stays in the tiles.
+constexpr int kBandRows = 256;      // rows per band work block
+constexpr int kBandChunk = 2048;    // band slots per work block
+constexpr int kBandMaxW = 16384;
+constexpr uint32_t kBandMaxCnt = 255u;
+constexpr double kBandDensity = 0.5;
+extern int64_t g_band_w;            // hh_tune("band_w"): -1 auto, 0 off, > 0 forced (multiple of 16)
+__host__ __device__ __forceinline__ int64_t band_slot(int64_t d, int64_t W) { return d < 0 ? d + W : d + W - 1; }
+__host__ __device__ __forceinline__ int64_t band_diag(int64_t s, int64_t W) { return s < W ? s - W : s - W + 1; }
+// W from the occupancy of diagonals 1..kBandMaxW (occ[d] / (n - d)): the
+// longest prefix of diagonals from ignore_diags on whose occupancy stays >=
+// kBandDensity, rounded down to a multiple of 16 (or the forced value).
+int32_t choose_band_w(const std::vector<double>& occupancy, int ignore_diags);
 inline int64_t pad4(int64_t x) { return (x + 3) & ~(int64_t)3; }
 
 // LDS image of a tile's bias values, XOR-rotated so that a wave reading
@@ -125,6 +143,9 @@ struct hh_matrix {
     int64_t n_tiles = 0, n_units = 0, n_part = 0, n_wide = 0, nJ = 0, nrb = 0;
     int64_t n_slots = 0;          // padded wide (uint32) entries in tiles
     int64_t n_slots_narrow = 0;   // padded narrow (uint16) entries in tiles
+    int32_t band_w = 0;           // dense band half-width (0 = no band)
+    int64_t n_band = 0;           // nonzero entries held by the band
+    hh::DBuf<uint8_t> band;       // local rows x 2 * band_w
     hh::DBuf<uint32_t> pay;
     hh::DBuf<uint16_t> payn;
     hh::DBuf<int32_t> tile_J, tile_rb;
@@ -146,7 +167,7 @@ struct hh_matrix {
                tile_rb.bytes() + tile_ent.bytes() + tile_rp.bytes() +
                u_tlo.bytes() * 7 + blk_unit_ptr.bytes() + tile_perm.bytes() + tile_band.bytes() + u_whole.bytes() + blk_tile_ptr.bytes() + u_glo.bytes() * 2 +
                wide_ptr.bytes() + wide_col.bytes() + wide_cnt.bytes() + diag.bytes() + row_nnz2.bytes() +
-               row_sum2.bytes() + row_group.bytes();
+               row_sum2.bytes() + row_group.bytes() + band.bytes();
     }
     hh::TileDev dev() const {
         return hh::TileDev{pay.p, payn.p, tile_J.p, tile_ent.p, tile_rp.p, tile_entn.p, tile_rpn.p, u_tlo.p,

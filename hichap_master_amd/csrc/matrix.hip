@@ -11,6 +11,15 @@ namespace hh {
 
 static thread_local std::string g_last_error;
 int64_t g_unit_entries = 0;  // 0 = auto (plan_tiles)
+int64_t g_band_w = -1;       // -1 = auto (choose_band_w)
+
+int32_t choose_band_w(const std::vector<double>& occ, int ignore_diags) {
+    if (g_band_w >= 0) return (int32_t)std::min<int64_t>(g_band_w, kBandMaxW) & ~15;
+    int64_t d = std::max(1, ignore_diags);
+    if (d > 1) return 0;  // diagonal 1 dropped: no dense neighbourhood to exploit
+    while (d < (int64_t)occ.size() && occ[d] >= kBandDensity) ++d;
+    return (int32_t)((d - 1) & ~15LL);
+}
 void set_error(const std::string& msg) { g_last_error = msg; }
 
 TilePlan plan_tiles(const uint16_t* cntw, const uint16_t* cntn, int64_t nloc, int32_t nJ,
@@ -301,6 +310,25 @@ int hh_matrix_from_pixels(const int64_t* bin1, const int64_t* bin2, const double
             if (inb) { ++deg[b - row_lo + 1]; rnnz[b - row_lo] += 1.0; rsum[b - row_lo] += c; }
         }
         for (int64_t r = 0; r < nloc; ++r) deg[r + 1] += deg[r];
+        // dense band width from the diagonals' occupancy over the WHOLE matrix
+        // (identical for every shard: the band decomposition fixes the
+        // summation order, so it must not depend on the row range)
+        int32_t W = 0;
+        {
+            std::vector<double> occ(kBandMaxW + 2, 0.0);
+            for (int64_t i = 0; i < nnz; ++i) {
+                int64_t a, b;
+                uint32_t c;
+                if (!keep(i, a, b, c) || a == b || b - a > kBandMaxW + 1) continue;
+                occ[b - a] += 1.0;
+            }
+            for (int64_t d = 1; d < (int64_t)occ.size(); ++d) occ[d] = d < n_bins ? occ[d] / (double)(n_bins - d) : 0.0;
+            W = choose_band_w(occ, ignore_diags);
+        }
+        auto in_band = [&](int64_t r_glob, int64_t col, uint32_t v) {
+            const int64_t d = col - r_glob;
+            return W > 0 && v <= kBandMaxCnt && d != 0 && d >= -W && d <= W;
+        };
         // pass 2: symmetric CSR rows
         std::vector<int32_t> cols(deg[nloc]);
         std::vector<uint32_t> vals(deg[nloc]);
@@ -328,8 +356,15 @@ int hh_matrix_from_pixels(const int64_t* bin1, const int64_t* bin2, const double
         const int32_t nJ = (int32_t)((n_bins + kW - 1) / kW);
         std::vector<uint16_t> cntw((size_t)nloc * nJ, 0), cntn((size_t)nloc * nJ, 0);
         std::vector<long long> wptr(nloc + 1, 0);
+        std::vector<uint8_t> band((size_t)nloc * 2 * W, 0);
+        int64_t n_band = 0;
         for (int64_t r = 0; r < nloc; ++r) {
             for (int64_t k = deg[r]; k < deg[r + 1]; ++k) {
+                if (in_band(row_lo + r, cols[k], vals[k])) {
+                    band[(size_t)r * 2 * W + band_slot(cols[k] - (row_lo + r), W)] = (uint8_t)vals[k];
+                    ++n_band;
+                    continue;
+                }
                 if (vals[k] > kCntMax) ++wptr[r + 1];
                 else if (vals[k] <= kNarrowMax) ++cntn[(size_t)r * nJ + (cols[k] >> kWBits)];
                 else ++cntw[(size_t)r * nJ + (cols[k] >> kWBits)];
@@ -350,6 +385,7 @@ int hh_matrix_from_pixels(const int64_t* bin1, const int64_t* bin2, const double
             int64_t pos = 0, posn = 0;
             int64_t wp = wptr[r];
             for (int64_t q = deg[r]; q < deg[r + 1]; ++q) {
+                if (in_band(row_lo + r, cols[q], vals[q])) continue;
                 if (vals[q] > kCntMax) { wcol[wp] = cols[q]; wcnt[wp++] = vals[q]; continue; }
                 const int32_t J = cols[q] >> kWBits;
                 if (J != curJ) {
@@ -373,6 +409,9 @@ int hh_matrix_from_pixels(const int64_t* bin1, const int64_t* bin2, const double
         m->row_nnz2 = to_device(rnnz, s);
         m->row_sum2 = to_device(rsum, s);
         m->row_group = to_device(rgroup, s);
+        m->band_w = W;
+        m->n_band = n_band;
+        m->band = to_device(band, s);
         m->nnz_upper = nnz_upper;
         m->n_entries = deg[nloc];
         HIP_CHECK(hipStreamSynchronize(s));  // host vectors die here
@@ -401,7 +440,10 @@ int hh_matrix_get_info(const hh_matrix* m, hh_matrix_info* info) {
         info->n_wide = m->n_wide;
         info->device_bytes = (int64_t)m->device_bytes();
         info->n_slots_narrow = m->n_slots_narrow;
-        info->payload_bytes = 4 * m->n_slots + 2 * m->n_slots_narrow;
+        info->payload_bytes = 4 * m->n_slots + 2 * m->n_slots_narrow + (int64_t)m->band.n;
+        info->band_w = m->band_w;
+        info->pad_ = 0;
+        info->n_band = m->n_band;
         info->n_chroms = m->n_chroms;
         info->ignore_diags = m->ignore_diags;
         info->cis_only = m->cis_only;
@@ -456,6 +498,17 @@ int hh_matrix_export_upper(const hh_matrix* m, int64_t* bin1, int64_t* bin2, dou
         }
         for (int64_t r = 0; r < nloc; ++r)
             for (long long q = wptr[r]; q < wptr[r + 1]; ++q) rows[r].emplace_back(wcol[q], wcnt[q]);
+        if (m->band_w > 0) {
+            const int64_t W = m->band_w;
+            std::vector<uint8_t> band(m->band.n);
+            m->band.download(band.data(), band.size(), 0);
+            HIP_CHECK(hipDeviceSynchronize());
+            for (int64_t r = 0; r < nloc; ++r)
+                for (int64_t sl = 0; sl < 2 * W; ++sl) {
+                    const uint8_t v = band[(size_t)r * 2 * W + sl];
+                    if (v) rows[r].emplace_back(m->row_lo + r + band_diag(sl, W), (double)v);
+                }
+        }
         int64_t cnt = 0;
         const int64_t cap = *nnz_inout;
         auto emit = [&](int64_t i, int64_t j, double v) {

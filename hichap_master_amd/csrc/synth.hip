@@ -33,6 +33,7 @@ struct SynthDev {
     float A, decay, comp, trans;
     int ignore_diags, cis_only;
     unsigned long long seed;
+    int band_w;            // dense band half-width (0 = none)
 };
 
 __global__ void k_synth_bins(SynthDev p, float vis_sigma, float gap_frac, int comp_block,
@@ -105,6 +106,8 @@ struct SynthOut {
     const uint32_t* tile_rpn;
     uint32_t* pay;
     uint16_t* payn;
+    uint8_t* band;         // PASS 1: local rows x 2 * band_w
+    int32_t* row_band;     // PASS 0: band entries per row
 };
 
 template <int PASS>
@@ -119,7 +122,7 @@ __global__ __launch_bounds__(256) void k_synth_rows(SynthDev p, long long row_lo
     const long long rb = w / kR;
     const int k = (int)(w % kR);
     const unsigned long long lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    long long upper = 0, nnz = 0, work = 0, sum_lane = 0;
+    long long upper = 0, nnz = 0, work = 0, sum_lane = 0, nb_lane = 0, nbu_lane = 0;
     int curJ = -1;
     long long tw = 0, tn = 0;      // wide / narrow entries of the current tile
     long long pos = 0, posn = 0;   // PASS 1: next write positions
@@ -142,6 +145,16 @@ __global__ __launch_bounds__(256) void k_synth_rows(SynthDev p, long long row_lo
         const int J = (int)(j0 >> kWBits);
         uint32_t kc = 0;
         if (j >= jlo && j < jhi && j != r) kc = synth_count(p, r, j);
+        // dense band: |j - r| <= W and count <= 255 (implicit column)
+        const long long dj = j - r;
+        const bool inband = kc > 0 && p.band_w > 0 && kc <= kBandMaxCnt && dj >= -p.band_w && dj <= p.band_w;
+        if (inband) {  // per-lane counters (the tile counters below are wave-uniform)
+            if (PASS == 1) o.band[w * 2 * p.band_w + band_slot(dj, p.band_w)] = (uint8_t)kc;
+            nb_lane += 1;
+            nbu_lane += dj > 0 ? 1 : 0;
+            sum_lane += kc;
+            kc = 0;
+        }
         const unsigned long long mask = __ballot(kc > 0);
         if (mask == 0ull) continue;
         if (J != curJ) {
@@ -171,8 +184,14 @@ __global__ __launch_bounds__(256) void k_synth_rows(SynthDev p, long long row_lo
     }
     flush();
     const long long s = wave_sum_ll(sum_lane);
+    // band entries were counted per lane; tile entries per wave (ballots)
+    const long long nband = wave_sum_ll(nb_lane);
+    nnz += nband;
+    upper += wave_sum_ll(nbu_lane);
+    work += (long long)p.band_w / 2;  // 2W bytes per row, in 4-byte words
     const uint32_t dg = p.ignore_diags == 0 ? synth_count(p, r, r) : 0u;
     if (lane == 0) {
+        if (o.row_band) o.row_band[w] = (int32_t)nband;
         if (o.row_work) o.row_work[w] = (int32_t)work;
         if (o.row_upper) o.row_upper[w] = upper + (dg ? 1 : 0);
         if (o.diag) {
@@ -196,6 +215,8 @@ struct SynthHost {
     SynthDev dev{};
     std::vector<int64_t> offsets;
 };
+
+int32_t synth_band_w(const hh_synth_params* p, const std::vector<int64_t>& offsets);
 
 void synth_setup(const hh_synth_params* p, SynthHost& h, hipStream_t s) {
     HH_REQUIRE(p && p->chrom_nbins && p->n_chroms > 0 && p->n_chroms < 32767, "bad synth params");
@@ -230,12 +251,46 @@ void synth_setup(const hh_synth_params* p, SynthHost& h, hipStream_t s) {
     d.ignore_diags = p->ignore_diags;
     d.cis_only = p->cis_only ? 1 : 0;
     d.seed = p->seed;
+    d.band_w = synth_band_w(p, h.offsets);
     hipLaunchKernelGGL(k_synth_bins, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, d,
                        (float)p->vis_sigma, (float)p->gap_frac, p->comp_block, h.vis.p, h.sgn.p);
     HIP_CHECK(hipGetLastError());
 }
 
 inline dim3 row_grid(int64_t nrows) { return dim3((unsigned)((nrows * 64 + 255) / 256)); }
+
+// Dense-band width of the synthetic model: expected occupancy of diagonal d =
+// P(count > 0) averaged over visibility / compartment draws (the generator's
+// distributions, a fixed host sample) x the share of rows whose partner bin
+// is cis and not a gap.  Only performance depends on it.
+int32_t synth_band_w(const hh_synth_params* p, const std::vector<int64_t>& offsets) {
+    const int S = 2048;
+    std::vector<double> x(S);
+    uint64_t st = 0x9E3779B97F4A7C15ull ^ p->seed;
+    auto uni = [&]() { st = mix64(st); return ((double)(st >> 11) + 0.5) * (1.0 / 9007199254740992.0); };
+    for (int k = 0; k < S; ++k) {
+        const double z1 = std::sqrt(-2.0 * std::log(uni())) * std::cos(6.283185307179586 * uni());
+        const double z2 = std::sqrt(-2.0 * std::log(uni())) * std::cos(6.283185307179586 * uni());
+        x[k] = std::exp(p->vis_sigma * z1) * std::exp(p->vis_sigma * z2);
+    }
+    const int64_t n = offsets.back();
+    std::vector<double> occ(kBandMaxW + 2, 0.0);
+    for (int64_t d = 1; d < (int64_t)occ.size() && d < n; ++d) {
+        double cis = 0.0;
+        for (size_t c = 0; c + 1 < offsets.size(); ++c) cis += (double)std::max<int64_t>(0, offsets[c + 1] - offsets[c] - d);
+        cis /= (double)(n - d);
+        const double same = std::max(0.0, 1.0 - (double)d / (double)p->comp_block);
+        const double lam0 = p->A * std::pow((double)d + 1.0, -p->decay);
+        double e = 0.0;
+        for (int k = 0; k < S; ++k) {
+            const double lp = lam0 * (1.0 + p->comp_strength) * x[k], lm = lam0 * (1.0 - p->comp_strength) * x[k];
+            const double pp = same + 0.5 * (1.0 - same);
+            e += pp * (1.0 - std::exp(-lp)) + (1.0 - pp) * (1.0 - std::exp(-lm));
+        }
+        occ[d] = e / S * cis * (1.0 - p->gap_frac) * (1.0 - p->gap_frac);
+    }
+    return choose_band_w(occ, p->ignore_diags);
+}
 }  // namespace
 
 namespace hh {
@@ -301,11 +356,13 @@ int hh_synth_build(const hh_synth_params* p, int64_t row_lo, int64_t row_hi, voi
         cnt.zero(s);
         cntn.zero(s);
         DBuf<long long> rup(nloc);
+        DBuf<int32_t> rband(std::max<int64_t>(nloc, 1));
         {
             SynthOut o{};
             o.cnt = cnt.p;
             o.cntn = cntn.p;
             o.row_upper = rup.p;
+            o.row_band = rband.p;
             o.diag = m->diag.p;
             o.row_nnz2 = m->row_nnz2.p;
             o.row_sum2 = m->row_sum2.p;
@@ -319,6 +376,8 @@ int hh_synth_build(const hh_synth_params* p, int64_t row_lo, int64_t row_hi, voi
         cntn.download(hn.data(), hn.size(), s);
         std::vector<long long> up(nloc);
         rup.download(up.data(), nloc, s);
+        std::vector<int32_t> hb(nloc);
+        rband.download(hb.data(), nloc, s);
         HIP_CHECK(hipStreamSynchronize(s));
         cnt.release();
         cntn.release();
@@ -330,8 +389,12 @@ int hh_synth_build(const hh_synth_params* p, int64_t row_lo, int64_t row_hi, voi
         DBuf<int32_t> tof = to_device(P.tile_of, s);
         m->pay.alloc(P.n_entries_padded);
         m->payn.alloc(P.n_narrow_padded);
+        m->band_w = h.dev.band_w;
+        m->band.alloc((size_t)nloc * 2 * m->band_w);
+        m->band.zero(s);
         {
             SynthOut o{};
+            o.band = m->band.p;
             o.tile_of = tof.p;
             o.tile_ent = m->tile_ent.p;
             o.tile_rp = m->tile_rp.p;
@@ -350,7 +413,10 @@ int hh_synth_build(const hh_synth_params* p, int64_t row_lo, int64_t row_hi, voi
         m->nnz_upper = std::accumulate(up.begin(), up.end(), 0LL);
         int64_t ent = 0;
         for (size_t i = 0; i < hc.size(); ++i) ent += (int64_t)hc[i] + hn[i];
-        m->n_entries = ent;
+        int64_t nb = 0;
+        for (int64_t r = 0; r < nloc; ++r) nb += hb[r];
+        m->n_band = nb;
+        m->n_entries = ent + nb;
         *out = m.release();
     });
 }

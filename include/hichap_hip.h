@@ -46,7 +46,8 @@ int hh_version(void);                 /* (major<<16)|(minor<<8)|patch */
 int hh_device_count(int32_t* n);
 int hh_set_device(int32_t device);
 int hh_synchronize(void* stream);
-/* Performance knobs: "sweep_nb" in {1,2,4,8} (row batches in flight per
+/* Performance knobs: "band_w" (-1 auto, 0 no dense band, > 0 forced
+ * multiple of 16; for matrices built afterwards), "sweep_nb" in {1,2,4,8} (row batches in flight per
  * wave), "unit_entries" (work-unit size used by later matrix builds),
  * "sweep_ablate" 0/1/2 (timing ablations only: 1 skips the LDS gathers,
  * 2 skips the b staging; results are wrong while set). */
@@ -67,7 +68,9 @@ int hh_ktime_reset(void);
  * (swizzled LDS byte offset << 3 | count, counts 1..7) and uint32 (count << 16 |
  * offset, counts 8..65535)
  * segments, rows padded to 16 B, counts > 65535 in a small per-row wide
- * list, plus a per-row diagonal.  Static filters
+ * list, plus a per-row diagonal.  Pixels near the diagonal (|col - row| <= W,
+ * count <= 255, W chosen from the data's diagonal occupancy) live in a dense
+ * uint8 band with implicit columns instead of the tiles.  Static filters
  * (ignore_diags, cis_only zero_trans, zero counts) are applied at build time.
  * Shards are whole 512-row blocks (row_lo % 512 == 0).
  */
@@ -84,11 +87,15 @@ typedef struct {
     int64_t n_wide;        /* entries with count >= 2^19 (wide list)         */
     int64_t device_bytes;  /* HBM held by the matrix                         */
     int64_t n_slots_narrow;/* stored uint16 slots (entries + row padding)    */
-    int64_t payload_bytes; /* entry bytes streamed per sweep (both widths)   */
+    int64_t payload_bytes; /* entry bytes streamed per sweep (both widths and
+                              the dense band)                                */
     int32_t n_chroms;
     int32_t ignore_diags;
     int32_t cis_only;
     int32_t device;
+    int32_t band_w;        /* dense diagonal band half-width W (0 = none)    */
+    int32_t pad_;
+    int64_t n_band;        /* nonzero entries held by the band               */
 } hh_matrix_info;
 
 /* Build from cooler's pixel table (upper triangle bin1 <= bin2; any order,

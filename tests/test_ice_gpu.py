@@ -165,9 +165,10 @@ def test_synthetic_generator_matches_oracle(ice):
     assert (b2 - b1 >= 1).all()
     # symmetric storage: every pixel appears in both rows -> entries = 2 * pixels
     assert inf["n_entries"] == 2 * b1.size
-    assert inf["n_slots"] + inf["n_slots_narrow"] >= inf["n_entries"]
+    assert inf["n_slots"] + inf["n_slots_narrow"] + inf["n_band"] >= inf["n_entries"]
     assert inf["n_slots"] % 4 == 0 and inf["n_slots_narrow"] % 8 == 0
-    assert inf["payload_bytes"] == 4 * inf["n_slots"] + 2 * inf["n_slots_narrow"]
+    band_bytes = 2 * inf["band_w"] * (inf["row_hi"] - inf["row_lo"])
+    assert inf["payload_bytes"] == 4 * inf["n_slots"] + 2 * inf["n_slots_narrow"] + band_bytes
     assert inf["n_slots_narrow"] > 0  # low counts are stored as uint16
     # shards see the same matrix
     rc, ru = ice.synth_row_counts(sizes, **kw)
@@ -229,3 +230,36 @@ def test_balance_sharded_rccl_world1(ice):
         tdist.destroy_process_group()
     np.testing.assert_array_equal(w, w_full)
     assert s_["iters"] == st_full["iters"]
+
+
+@pytest.mark.parametrize("band_w", [0, 16, 64, -1])
+def test_dense_band_widths(ice, band_w):
+    """The dense diagonal band (any width, or none) holds exactly the pixels
+    it claims: export round trip, and weights equal the oracle's."""
+    from hichap_master_amd import _lib
+    b1, b2, c, off = _case(31, sizes=(700, 500), A=60.0, trans=0.02)
+    c = c.copy()
+    c[::97] = 300  # counts > 255 near the diagonal go to the tiles
+    n = int(off[-1])
+    _lib.call("hh_tune", b"band_w", band_w)
+    try:
+        m = ice.ContactMatrix.from_pixels(b1, b2, c, n, off)
+        inf = m.info()
+        if band_w > 0:
+            assert inf["band_w"] == band_w
+        if band_w == 0:
+            assert inf["band_w"] == 0 and inf["n_band"] == 0
+        if band_w == -1:
+            assert inf["band_w"] > 0 and inf["n_band"] > 0  # dense near the diagonal at A=60
+        e1, e2, ec = m.export_upper()
+        f1, f2, fc = _filtered_upper(b1, b2, c, off, 1, False)
+        np.testing.assert_array_equal(e1, f1)
+        np.testing.assert_array_equal(e2, f2)
+        np.testing.assert_array_equal(ec, fc)
+        w, st = ice.balance_matrix(m)
+        m.close()
+    finally:
+        _lib.call("hh_tune", b"band_w", -1)
+    w_ref, st_ref = ice_ref.balance(b1, b2, c, n, off)
+    assert st["iters"] == st_ref["iters"]
+    np.testing.assert_allclose(w, w_ref, rtol=1e-9, equal_nan=True)

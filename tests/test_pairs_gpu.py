@@ -284,3 +284,42 @@ def test_ice_on_binned_pixels(mb):
     w_ref, st_ref = ice_ref.balance(e1, e2, ec.astype(np.float64), int(off[-1]), off)
     assert st["iters"] == st_ref["iters"]
     np.testing.assert_allclose(w, w_ref, rtol=1e-9, equal_nan=True)
+
+
+def test_long_lines_and_unaligned_device_text(mb):
+    """Lines far longer than a tile's 1 KB lookahead (fields read through the
+    global fallback), and device text starting at an unaligned address."""
+    import torch
+    from hichap_master_amd import pairs
+    rng = np.random.default_rng(21)
+    names = ["chr1", "chr2", "chr3", "chrX", "chrY"]
+    out = []
+    for k in range(3000):
+        c1, c2 = names[rng.integers(5)], names[rng.integers(5)]
+        p1, p2 = int(rng.integers(0, 15_000_000)), int(rng.integers(0, 15_000_000))
+        pad = "x" * int(rng.choice([1, 50, 3000, 9000], p=[0.6, 0.3, 0.07, 0.03]))
+        sep = " " * int(rng.integers(1, 4))
+        out.append(sep.join([f"R{k}{pad}", c1, "+", str(p1), "0", "0", str(p1), "0", c2, "-", str(p2), "0", "0",
+                             str(p2), "0" + pad]) + "\n")
+    text = "".join(out).encode()
+    lines = text.decode().splitlines(keepends=True)
+    whole, local = pairs_ref.traditional_counts(lines, GENOME, ["#", "X"], [500_000], [250_000])
+    for shift in (0, 3, 13):
+        buf = torch.zeros(len(text) + 32, dtype=torch.uint8, device="cuda")
+        buf[shift:shift + len(text)] = torch.frombuffer(bytearray(text), dtype=torch.uint8).cuda()
+        B = pairs.PairBinner(GENOME, ["#", "X"])
+        tw = B.add_target(500_000)
+        tl = B.add_target(250_000, local=True)
+        B.feed_device(buf.data_ptr() + shift, len(text), pairs.pairs_format(pairs.VALID_BED))
+        b1, b2, c = B.pixels(tw)
+        e1, e2, ec = pairs_ref.counter_to_pixels(whole[500_000])
+        np.testing.assert_array_equal(b1, e1)
+        np.testing.assert_array_equal(b2, e2)
+        np.testing.assert_array_equal(c, ec)
+        lsd = pairs.local_sparse_dict(*B.pixels(tl), tl, pairs.sort_chromosomes(GENOME))
+        for chro in lsd:
+            e1, e2, ec = pairs_ref.counter_to_pixels(local[250_000][chro])
+            np.testing.assert_array_equal(lsd[chro]["bin2"], e2)
+            np.testing.assert_array_equal(lsd[chro]["IF"], ec.astype(np.float64))
+        assert B.stats()["lines"] == 3000
+        B.close()
