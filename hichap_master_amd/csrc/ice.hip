@@ -36,6 +36,7 @@ constexpr int kThreads = 256;
 // which only that wave touches -> fixed summation order (deterministic).
 constexpr int kSweepThreads = 512;
 constexpr int kSweepWaves = kSweepThreads / 64;
+constexpr int kFlatU = 4;  // uint4 per lane per step in flat segments
 
 // Entry decode: the byte offset of the staged bias value is a field of the
 // entry (ice_internal.hpp), so an entry costs mask, shift, cvt, LDS read and
@@ -217,6 +218,175 @@ __device__ __forceinline__ void band_rows(const uint4* __restrict__ pay4, const 
     }
 }
 
+// Flat (merge-path) sweep of a whole tile segment whose rows are all short
+// (plan_tiles marks it).  The segment's payload is one
+// contiguous uint4 array; fbe[0..nfr] are the entry offsets of its nonempty
+// rows (row ids fr[i], in row order; fbe[nfr] = end).  Each wave takes the
+// rows starting in its eighth of the array; per step every lane streams U
+// consecutive uint4 (64 * U fully used uint4 per wave in flight, no idle
+// lanes, no per-row setup chain), finds the row of its first uint4 by a
+// short search over fbe, and walks its run closing rows at their starts:
+//   * a row that starts and ends inside the run is added to acc by the lane;
+//   * the part of a row before the run's first start ("head") flows left
+//     through a segmented suffix scan over lanes to the lane where the row
+//     started ("tail"), which adds tail + heads; lane 0 adds a head whose row
+//     started in an earlier step.
+// A row's acc is touched only by its wave, in program order; every sum is a
+// fixed tree of the tile content -> deterministic.
+template <int EPV>
+__device__ __forceinline__ double flat_dot(const uint4 v, const double* __restrict__ bl) {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    if constexpr (EPV == 8) {
+        double g[8];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            g[2 * i] = lds_b(bl, w[i] & 0xFFF8u);
+            g[2 * i + 1] = lds_b(bl, (w[i] >> 16) & 0xFFF8u);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        double a = 0.0, c = 0.0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            a = fma((double)(w[i] & 7u), g[2 * i], a);
+            c = fma((double)((w[i] >> 16) & 7u), g[2 * i + 1], c);
+        }
+        return a + c;
+    } else {
+        double g[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) g[i] = lds_b(bl, w[i] & 0xFFFFu);
+        __builtin_amdgcn_sched_barrier(0);
+        double a = 0.0, c = 0.0;
+#pragma unroll
+        for (int i = 0; i < 4; i += 2) {
+            a = fma((double)(w[i] >> 16), g[i], a);
+            c = fma((double)(w[i + 1] >> 16), g[i + 1], c);
+        }
+        return a + c;
+    }
+}
+
+// U consecutive uint4 of the lane's run starting at s (zeros past qb).
+template <int U>
+__device__ __forceinline__ void flat_load(const uint4* __restrict__ pay4, uint32_t s, uint32_t qa, uint32_t qb,
+                                          uint4 (&v)[U]) {
+    const uint4 zero = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+        const bool on = s + k < qb;
+        const uint4 x = ld16(pay4 + (on ? s + k : qa));
+        v[k] = on ? x : zero;
+    }
+}
+
+// One step of a wave over uint4 [q0, q0 + 64 U) of its range [.., qb): v
+// holds the lane's run [s, s + U), s = q0 + lane U.  ic = the row holding
+// q0 - 1 (q0 at the first step); rows [.., i1) belong to the wave; fst =
+// uint4 starts of the segment's nonempty rows (fst[nfr] = end), fr = their ids.
+template <int U, int ABL, int EPV>
+__device__ __forceinline__ void flat_step(const uint4 (&v)[U], uint32_t q0, uint32_t qb, int& ic, int i1,
+                                          const uint16_t* __restrict__ fst, const uint16_t* __restrict__ fr,
+                                          int nfr, const double* __restrict__ bl, double* __restrict__ acc,
+                                          int lane) {
+    const uint32_t s = q0 + (uint32_t)lane * U;
+    const bool act = s < qb;
+    // row of s: the largest i with start <= s; at most lane U + 1 rows
+    // start in (q0 - 1, s] (rows are nonempty)
+    int lo = ic, hi = min(i1 - 1, ic + lane * U + 1);
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if ((uint32_t)fst[mid] <= s) lo = mid; else hi = mid - 1;
+    }
+    const bool head = (uint32_t)fst[lo] < s;  // the run starts inside row lo
+    uint32_t nb[U], rid[U];                 // starts of rows lo+1.., ids of rows lo..
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+        nb[k] = fst[min(lo + 1 + k, nfr)];
+        rid[k] = fr[min(lo + k, nfr - 1)];
+    }
+    double x = 0.0, h = 0.0, cv[U];
+    uint32_t cr[U];
+    bool inhead = head;
+    int j = 0;  // row starts passed inside the run
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+        cv[k] = 0.0;
+        cr[k] = 0xFFFFFFFFu;
+        if (k > 0) {
+            uint32_t nxt = nb[0], crow = rid[0];
+#pragma unroll
+            for (int jj = 1; jj < k; ++jj)
+                if (j == jj) {
+                    nxt = nb[jj];
+                    crow = rid[jj];
+                }
+            if (s + k == nxt && s + k < qb) {
+                if (inhead) {
+                    h = x;
+                    inhead = false;
+                } else if (U <= 4) {
+                    cv[k] = x;
+                    cr[k] = crow;
+                } else {
+                    acc[crow] += x;  // long runs: write at once (registers)
+                }
+                x = 0.0;
+                ++j;
+            }
+        }
+        x += ABL == 1 ? (double)(v[k].x + v[k].y + v[k].z + v[k].w) : flat_dot<EPV>(v[k], bl);
+    }
+    uint32_t orow = rid[0];
+#pragma unroll
+    for (int jj = 1; jj < U; ++jj)
+        if (j == jj) orow = rid[jj];
+    if (inhead) h = x;
+    const bool tail = act && !inhead;
+    // rows that start and end inside the run (independent read-modify-writes)
+    if (U <= 4) {
+        double old[U];
+#pragma unroll
+        for (int k = 1; k < U; ++k) old[k] = cr[k] != 0xFFFFFFFFu ? acc[cr[k]] : 0.0;
+#pragma unroll
+        for (int k = 1; k < U; ++k)
+            if (cr[k] != 0xFFFFFFFFu) acc[cr[k]] = old[k] + cv[k];
+    }
+    // heads flow left: H_l = h_l + pass_l * H_{l+1}
+    double H = act ? h : 0.0;
+    int F = (!act || inhead) ? 1 : 0;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const double Hn = __shfl_down(H, o, 64);
+        const int Fn = __shfl_down(F, o, 64);
+        if (lane + o < 64 && F) {
+            H += Hn;
+            F = Fn;
+        }
+    }
+    const double Hr = __shfl_down(H, 1, 64);
+    if (tail) acc[orow] += x + (lane < 63 ? Hr : 0.0);
+    if (lane == 0 && head) acc[rid[0]] += H;
+    ic = __shfl(lo + j, 63, 64);
+}
+
+// A wave's rows [i0, i1) = uint4 [qa, qb) of one segment, the first step's
+// run already loaded into v (its loads were issued before the tile's LDS
+// staging, so they fly while the block stages).
+template <int U, int ABL, int EPV>
+__device__ __forceinline__ void flat_seg(const uint4* __restrict__ pay4, uint4 (&v)[U], uint32_t qa, uint32_t qb,
+                                         int i0, int i1, const uint16_t* __restrict__ fst,
+                                         const uint16_t* __restrict__ fr, int nfr, const double* __restrict__ bl,
+                                         double* __restrict__ acc, int lane) {
+    if (i0 >= i1) return;
+    int ic = i0;
+    for (uint32_t q0 = qa;;) {
+        flat_step<U, ABL, EPV>(v, q0, qb, ic, i1, fst, fr, nfr, bl, acc, lane);
+        q0 += 64u * U;
+        if (q0 >= qb) break;
+        flat_load<U>(pay4, q0 + (uint32_t)lane * U, qa, qb, v);
+    }
+}
+
 template <int NB, int ABL, int EPV>
 __device__ __forceinline__ void sweep_bands(const uint16_t* band, const uint4* pay4, const uint32_t* rp,
                                             const uint16_t* perm, const double* bl, double* acc, int wave,
@@ -238,20 +408,42 @@ __device__ __forceinline__ void sweep_rows(uint32_t mean, const uint4* pay4, con
     else tile_rows<4, NB, ABL, EPV>(pay4, rp, bl, acc, ra, rb, wave, lane);
 }
 
+// The tile's 8192 bias values -> LDS (rotated image), coalesced 16-B loads
+// in R rounds (R > 1: fewer registers in flight).
+template <int R = 1>
+__device__ __forceinline__ void stage_bias(double* __restrict__ bl, const double* __restrict__ b, long long c0,
+                                           long long n_bins) {
+    if (c0 + kW <= n_bins) {
+        constexpr int NV = kW / 2 / kSweepThreads / R;
+        const double2* src = reinterpret_cast<const double2*>(b + c0);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            double2 v[NV];
+#pragma unroll
+            for (int k = 0; k < NV; ++k) v[k] = src[threadIdx.x + (r * NV + k) * kSweepThreads];
+#pragma unroll
+            for (int k = 0; k < NV; ++k) {
+                const uint32_t e = 2u * (threadIdx.x + (r * NV + k) * kSweepThreads);
+                bl[swz(e)] = v[k].x;
+                bl[swz(e + 1)] = v[k].y;
+            }
+        }
+    } else {
+        for (int k = threadIdx.x; k < kW; k += kSweepThreads) bl[swz(k)] = c0 + k < n_bins ? b[c0 + k] : 0.0;
+    }
+}
+
 template <int NB, int ABL>
 __global__ __launch_bounds__(kSweepThreads, 4) void k_sweep_tiled(TileDev T, const uint8_t* __restrict__ act,
-                                                                int n_units, const double* __restrict__ b,
-                                                                long long n_bins, double* __restrict__ part,
-                                                                int flags) {
+                                                                int n_list, const double* __restrict__ b,
+                                                                long long n_bins, double* __restrict__ part) {
     __shared__ __attribute__((aligned(16))) double bl[kW];
     __shared__ double acc2[2 * kR];  // narrow rows, then wide rows
     __shared__ uint32_t rps[kR + 1], rpsn[kR + 1];
     __shared__ uint16_t perm[2 * kR];
     __shared__ uint16_t band[2 * kBandSlots];
-    // flags bit0: units sorted by column tile and dealt so that each XCD takes
-    // a contiguous range (measured slower on C4: kept as a knob only)
-    const int u = (flags & 1) ? T.u_order[xcd_remap(blockIdx.x, n_units)] : (int)blockIdx.x;
-    if (u >= n_units) return;
+    if ((int)blockIdx.x >= n_list) return;
+    const int u = T.u_order[blockIdx.x];  // the tiled-kernel units lead the launch list
     {
         bool on = false;
         for (int g = T.u_glo[u]; g <= T.u_ghi[u]; ++g) on |= act[g] != 0;
@@ -264,22 +456,7 @@ __global__ __launch_bounds__(kSweepThreads, 4) void k_sweep_tiled(TileDev T, con
     for (int t = T.u_tlo[u]; t < T.u_thi[u]; ++t) {
         const long long c0 = (long long)T.tile_J[t] * kW;
         __syncthreads();  // previous tile's LDS reads are done
-        if (ABL == 2) {
-            // timing ablation: no staging
-        } else if (c0 + kW <= n_bins) {
-            const double2* src = reinterpret_cast<const double2*>(b + c0);
-            double2 v[kW / 2 / kSweepThreads];
-#pragma unroll
-            for (int k = 0; k < kW / 2 / kSweepThreads; ++k) v[k] = src[threadIdx.x + k * kSweepThreads];
-#pragma unroll
-            for (int k = 0; k < kW / 2 / kSweepThreads; ++k) {
-                const uint32_t e = 2u * (threadIdx.x + k * kSweepThreads);
-                bl[swz(e)] = v[k].x;
-                bl[swz(e + 1)] = v[k].y;
-            }
-        } else {
-            for (int k = threadIdx.x; k < kW; k += kSweepThreads) bl[swz(k)] = c0 + k < n_bins ? b[c0 + k] : 0.0;
-        }
+        if (ABL != 2) stage_bias(bl, b, c0, n_bins);  // ABL 2: timing ablation, no staging
         {
             const uint32_t* rpg = T.tile_rp + (size_t)t * (kR + 1);
             const uint32_t* rpgn = T.tile_rpn + (size_t)t * (kR + 1);
@@ -311,6 +488,61 @@ __global__ __launch_bounds__(kSweepThreads, 4) void k_sweep_tiled(TileDev T, con
     }
     __syncthreads();
     for (int k = threadIdx.x; k < rb - ra; k += kSweepThreads) part[T.u_slot[u] + k] = acc2[k] + acc2[(rb - ra) + k];
+}
+
+// K1c: the flat tiles (whole row-blocks whose rows are all short).  Per
+// tile the latency chain is kept to two hops: each wave's row / uint4 range
+// (tile_fw, scalar loads prefetched one tile ahead) lets it issue the loads
+// of its first narrow and wide runs at once, while the block copies the bias
+// slice and the tile's flat record (compacted row starts + row ids) into LDS
+// in one pass; then the waves sweep both segments with flat_seg.
+template <int U, int ABL>
+__global__ __launch_bounds__(kSweepThreads, 4) void k_sweep_flat(TileDev T, const uint8_t* __restrict__ act,
+                                                               int n_list, int list_off,
+                                                               const double* __restrict__ b, long long n_bins,
+                                                               double* __restrict__ part) {
+    static_assert(kSweepWaves == kFlatWaves, "one plan split per wave");
+    constexpr int UW = 2;  // wide runs: few wide entries in flat tiles
+    __shared__ __attribute__((aligned(16))) double bl[kW];
+    __shared__ double acc2[2 * kR];  // narrow rows, then wide rows
+    __shared__ __attribute__((aligned(16))) uint16_t rec[kFrecU4 * 8];
+    if ((int)blockIdx.x >= n_list) return;
+    const int u = T.u_order[list_off + blockIdx.x];
+    {
+        bool on = false;
+        for (int g = T.u_glo[u]; g <= T.u_ghi[u]; ++g) on |= act[g] != 0;
+        if (!on) return;
+    }
+    const int nr = T.u_rhi[u];  // whole row-block: rows [0, nr)
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint16_t* fstn = rec;
+    const uint16_t* fstw = rec + (kR + 1);
+    const uint16_t* fidn = rec + 2 * (kR + 1);
+    const uint16_t* fidw = fidn + kR;
+    for (int k = threadIdx.x; k < 2 * nr; k += kSweepThreads) acc2[k] = 0.0;
+    const int t0 = T.u_tlo[u], t1 = T.u_thi[u];
+    for (int t = t0; t < t1; ++t) {
+        const uint32_t* fw = T.tile_fw + (size_t)t * kFlatMeta;
+        const uint32_t* fwn = fw + 2 * wave;
+        const uint32_t* fww = fw + 2 * (kFlatWaves + 1) + 2 * wave;
+        const uint32_t qan = fwn[0], qbn = fwn[2], qaw = fww[0], qbw = fww[2];
+        const int i0n = (int)fwn[1], i1n = (int)fwn[3], i0w = (int)fww[1], i1w = (int)fww[3];
+        const int nfn = (int)fw[2 * kFlatWaves + 1], nfw = (int)fww[2 * (kFlatWaves - wave) + 1];
+        const uint4* payn4 = reinterpret_cast<const uint4*>(T.payn + T.tile_entn[t]);
+        const uint4* payw4 = reinterpret_cast<const uint4*>(T.pay + T.tile_ent[t]);
+        uint4 v[U], vw[UW];
+        if (i0n < i1n) flat_load<U>(payn4, qan + (uint32_t)lane * U, qan, qbn, v);
+        if (i0w < i1w) flat_load<UW>(payw4, qaw + (uint32_t)lane * UW, qaw, qbw, vw);
+        const uint4* rg = T.frec + (size_t)T.tile_frec[t] * kFrecU4;
+        __syncthreads();  // previous tile's LDS reads are done
+        if (ABL != 2) stage_bias<U >= 8 ? 2 : 1>(bl, b, (long long)T.tile_J[t] * kW, n_bins);
+        for (int k = threadIdx.x; k < kFrecU4; k += kSweepThreads) reinterpret_cast<uint4*>(rec)[k] = rg[k];
+        __syncthreads();
+        flat_seg<U, ABL, 8>(payn4, v, qan, qbn, i0n, i1n, fstn, fidn, nfn, bl, acc2, lane);
+        flat_seg<UW, ABL, 4>(payw4, vw, qaw, qbw, i0w, i1w, fstw, fidw, nfw, bl, acc2 + nr, lane);
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < nr; k += kSweepThreads) part[T.u_slot[u] + k] = acc2[k] + acc2[nr + k];
 }
 
 // ---------------------------------------------------------------- K2
@@ -576,8 +808,14 @@ struct hh_ice {
     std::vector<hipEvent_t> ev;
     double sweep_ms = 0.0, iter_ms = 0.0;
     int32_t sweep_launches = 0;
+    // side stream for the dense-band sweep, run beside the tile sweep
+    hipStream_t side = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
     ~hh_ice() {
         for (auto e : ev) (void)hipEventDestroy(e);
+        if (fork) (void)hipEventDestroy(fork);
+        if (join) (void)hipEventDestroy(join);
+        if (side) (void)hipStreamDestroy(side);
     }
     bool full() const { return m->row_lo == 0 && m->row_hi == m->n_bins; }
     TileArgs ta() {
@@ -592,12 +830,17 @@ namespace hh {
 // Tuning knobs (hh_tune; no effect on results except the ablations).
 static int g_sweep_nb = 2;
 static int g_sweep_ablate = 0;
-static int g_sweep_flags = 0;  // bit0: XCD-ordered units
+static int g_band_concurrent = 0;  // dense-band sweep on a side stream, beside the tiles
 
 template <int NB, int ABL>
 static void launch_sweep(const hh_matrix* m, const uint8_t* act, const double* b, double* part, hipStream_t s) {
-    hipLaunchKernelGGL((k_sweep_tiled<NB, ABL>), dim3((unsigned)m->n_units), dim3(kSweepThreads), 0, s, m->dev(),
-                       act, (int)m->n_units, b, (long long)m->n_bins, part, g_sweep_flags);
+    const int n_tiled = (int)(m->n_units - m->n_units_flat), n_flat = (int)m->n_units_flat;
+    if (n_tiled)
+        hipLaunchKernelGGL((k_sweep_tiled<NB, ABL>), dim3((unsigned)n_tiled), dim3(kSweepThreads), 0, s, m->dev(),
+                           act, n_tiled, b, (long long)m->n_bins, part);
+    if (n_flat)
+        hipLaunchKernelGGL((k_sweep_flat<kFlatU, ABL>), dim3((unsigned)n_flat), dim3(kSweepThreads), 0, s, m->dev(),
+                           act, n_flat, n_tiled, b, (long long)m->n_bins, part);
 }
 
 template <int ABL>
@@ -634,8 +877,21 @@ static void marg_weighted(hh_ice* S, double* out, hipStream_t s, bool timed, int
     if (timed) HIP_CHECK(hipEventRecord(S->ev[2 * slot], s));
     {
         HH_KTIME(timed ? nullptr : "k_sweep_tiled", s);  // registry timing for the sharded driver (tiles + band)
-        sweep(m, S->act(), S->bias.p, S->part.p, s);
-        sweep_band(S, s);
+        // the two sweeps write disjoint partials (part / bpart): the band
+        // kernel runs on a side stream so its blocks fill the CUs the tile
+        // kernel leaves idle (both are HBM-bound; neither saturates alone)
+        const bool conc = g_band_concurrent && S->nch && S->nloc && m->n_units;
+        if (conc) {
+            HIP_CHECK(hipEventRecord(S->fork, s));
+            HIP_CHECK(hipStreamWaitEvent(S->side, S->fork, 0));
+            sweep_band(S, S->side);
+            HIP_CHECK(hipEventRecord(S->join, S->side));
+            sweep(m, S->act(), S->bias.p, S->part.p, s);
+            HIP_CHECK(hipStreamWaitEvent(s, S->join, 0));
+        } else {
+            sweep(m, S->act(), S->bias.p, S->part.p, s);
+            sweep_band(S, s);
+        }
     }
     if (timed) HIP_CHECK(hipEventRecord(S->ev[2 * slot + 1], s));
     if (S->nloc == 0) return;
@@ -679,6 +935,9 @@ int hh_tune(const char* key, int64_t value) {
         } else if (k == "sweep_ablate") {
             HH_REQUIRE(value >= 0 && value <= 2, "sweep_ablate must be 0, 1 or 2");
             g_sweep_ablate = (int)value;
+        } else if (k == "flat_max") {
+            HH_REQUIRE(value >= 0 && value <= 255, "flat_max in [0, 255]");
+            g_flat_max = value;
         } else if (k == "unit_entries") {
             HH_REQUIRE(value == 0 || (value >= 4096 && value <= (1 << 24)), "unit_entries must be 0 (auto) or in [4096, 2^24]");
             g_unit_entries = value;
@@ -689,9 +948,9 @@ int hh_tune(const char* key, int64_t value) {
             HH_REQUIRE(value >= -1 && value <= kBandMaxW && (value <= 0 || value % 16 == 0),
                        "band_w: -1 (auto), 0 (off) or a multiple of 16 <= 16384");
             g_band_w = value;
-        } else if (k == "sweep_flags") {
-            HH_REQUIRE(value >= 0 && value <= 1, "sweep_flags in [0, 1]");
-            g_sweep_flags = (int)value;
+        } else if (k == "band_concurrent") {
+            HH_REQUIRE(value == 0 || value == 1, "band_concurrent in {0, 1}");
+            g_band_concurrent = (int)value;
         } else {
             HH_THROW(HH_ERR_ARG, "unknown tuning key " + k);
         }
@@ -744,6 +1003,9 @@ int hh_ice_create(hh_matrix* m, const hh_ice_opts* o, hh_ice** out) {
         S->part.alloc(std::max<int64_t>(m->n_part, 1));
         S->nch = m->band_w > 0 ? (int32_t)((2 * (int64_t)m->band_w + kBandChunk - 1) / kBandChunk) : 0;
         S->bpart.alloc(std::max<int64_t>((int64_t)S->nch * S->nloc, 1));
+        HIP_CHECK(hipStreamCreateWithFlags(&S->side, hipStreamNonBlocking));
+        HIP_CHECK(hipEventCreateWithFlags(&S->fork, hipEventDisableTiming));
+        HIP_CHECK(hipEventCreateWithFlags(&S->join, hipEventDisableTiming));
 
         S->tile_cnt.alloc(std::max(S->n_tiles, 1));
         S->tile_sum.alloc(std::max(S->n_tiles, 1));

@@ -69,7 +69,23 @@ __host__ __device__ __forceinline__ uint32_t enc_wide(uint32_t c, uint32_t count
 __host__ __device__ __forceinline__ uint32_t dec_col(uint32_t byteoff) { return unswz((byteoff & 0xFFFFu) >> 3); }
 inline int64_t pad8(int64_t x) { return (x + 7) & ~(int64_t)7; }
 constexpr int kBands = 5;        // lane-group widths 64, 32, 16, 8, 4
-constexpr int kBandSlots = 8;    // kBands + 1 bounds, padded
+constexpr int kBandSlots = 8;    // kBands + 1 bounds, then the flat flag and row count
+// Flat tiles: when no row of either segment of a tile is
+// longer than g_flat_max uint4, the tile goes to k_sweep_flat, which streams
+// each segment as one flat uint4 array (lane-major runs, rows found by search
+// over the compacted row starts, segmented reduction across lanes) instead of
+// lane groups per row; its perms then list the nonempty rows in row order.
+// Units hold only flat or only non-flat tiles.
+constexpr int kFlatWaves = 8;    // waves of a flat-kernel block (= kSweepThreads / 64)
+constexpr int kFlatMeta = 2 * 2 * (kFlatWaves + 1);
+// per flat tile, one record staged into LDS in one copy: uint16 starts (in
+// uint4) of the nonempty rows of both segments, kR + 1 each (padded with the
+// segment's uint4 count), then uint16 row ids, kR each; 16-B padded
+constexpr int kFrecHalf = 2 * (kR + 1) + 2 * kR;
+constexpr int kFrecU4 = (kFrecHalf * 2 + 15) / 16;
+constexpr int kFlatFlag = 6;     // band slot: 1 = flat segment
+constexpr int kFlatRows = 7;     // band slot: number of nonempty rows
+extern int64_t g_flat_max;       // hh_tune("flat_max"), build time
 // minimum row length (uint4 per row) of band g
 __host__ __device__ constexpr uint32_t band_min(int g) { return g == 0 ? 48u : g == 1 ? 24u : g == 2 ? 12u : g == 3 ? 6u : 1u; }
 
@@ -88,6 +104,12 @@ struct TilePlan {
     // that order swept with lane groups of 64/32/16/8/4 (kBands + 1 bounds)
     std::vector<uint16_t> tile_perm;  // per tile: 2 x kR
     std::vector<uint16_t> tile_band;  // per tile: 2 x kBandSlots
+    // per flat tile and segment: the 8 waves' split of the nonempty rows,
+    // kFlatWaves + 1 pairs (first uint4, first compact row index); the last
+    // pair is (segment uint4 count, number of nonempty rows)
+    std::vector<uint32_t> tile_fw;    // per tile: kFlatMeta words
+    std::vector<int32_t> tile_frec;   // per tile: index of its flat record, -1
+    std::vector<uint16_t> frec;       // flat records, kFrecU4 * 8 halves each
     std::vector<int32_t> tile_rb;     // per tile: local row-block
     std::vector<int32_t> blk_tile_ptr;  // nrb + 1
     std::vector<int32_t> tile_of;     // nrb * nJ -> tile index or -1
@@ -95,8 +117,12 @@ struct TilePlan {
     std::vector<int32_t> u_tlo, u_thi, u_rb, u_rlo, u_rhi, u_slot;
     std::vector<uint16_t> u_glo, u_ghi;
     std::vector<int32_t> blk_unit_ptr;  // nrb + 1
-    std::vector<int32_t> u_order;       // sweep order: units sorted by first column tile
+    std::vector<int32_t> u_order;       // launch lists: tiled-kernel units, then flat-kernel units
     std::vector<uint8_t> u_whole;       // 1: the unit covers whole row-blocks (sorted-band sweep)
+    std::vector<uint8_t> tile_flat;     // per tile: 1 = flat (every nonempty segment flat)
+    std::vector<uint8_t> u_flat;        // per unit: 1 = swept by the flat kernel
+    int64_t n_units_flat = 0;
+    int64_t payload_bytes_flat = 0;     // payload of the flat units' tiles
     int64_t n_entries_padded = 0;     // wide slots
     int64_t n_narrow_padded = 0;      // narrow slots
     int64_t n_part = 0;
@@ -128,6 +154,9 @@ struct TileDev {
     const int32_t* u_order;
     const uint16_t* tile_perm;
     const uint16_t* tile_band;
+    const uint32_t* tile_fw;
+    const int32_t* tile_frec;
+    const uint4* frec;
     const uint8_t* u_whole;
 };
 
@@ -141,6 +170,8 @@ struct hh_matrix {
     int64_t nnz_upper = 0;
     int64_t n_entries = 0;        // stored off-diagonal entries (both triangles)
     int64_t n_tiles = 0, n_units = 0, n_part = 0, n_wide = 0, nJ = 0, nrb = 0;
+    int64_t n_units_flat = 0;     // units swept by k_sweep_flat (the last entries of u_order)
+    int64_t payload_bytes_flat = 0;
     int64_t n_slots = 0;          // padded wide (uint32) entries in tiles
     int64_t n_slots_narrow = 0;   // padded narrow (uint16) entries in tiles
     int32_t band_w = 0;           // dense band half-width (0 = no band)
@@ -153,6 +184,9 @@ struct hh_matrix {
     hh::DBuf<uint32_t> tile_rp, tile_rpn;
     hh::DBuf<int32_t> u_tlo, u_thi, u_rb, u_rlo, u_rhi, u_slot, blk_unit_ptr, blk_tile_ptr, u_order;
     hh::DBuf<uint16_t> u_glo, u_ghi, tile_perm, tile_band;
+    hh::DBuf<uint32_t> tile_fw;
+    hh::DBuf<int32_t> tile_frec;
+    hh::DBuf<uint16_t> frec;
     hh::DBuf<uint8_t> u_whole;
     hh::DBuf<long long> wide_ptr;  // local rows + 1
     hh::DBuf<int32_t> wide_col;
@@ -165,14 +199,15 @@ struct hh_matrix {
     size_t device_bytes() const {
         return pay.bytes() + payn.bytes() + tile_entn.bytes() + tile_rpn.bytes() + tile_J.bytes() +
                tile_rb.bytes() + tile_ent.bytes() + tile_rp.bytes() +
-               u_tlo.bytes() * 7 + blk_unit_ptr.bytes() + tile_perm.bytes() + tile_band.bytes() + u_whole.bytes() + blk_tile_ptr.bytes() + u_glo.bytes() * 2 +
+               u_tlo.bytes() * 7 + blk_unit_ptr.bytes() + tile_perm.bytes() + tile_band.bytes() + u_whole.bytes() + tile_fw.bytes() + tile_frec.bytes() + frec.bytes() + blk_tile_ptr.bytes() + u_glo.bytes() * 2 +
                wide_ptr.bytes() + wide_col.bytes() + wide_cnt.bytes() + diag.bytes() + row_nnz2.bytes() +
                row_sum2.bytes() + row_group.bytes() + band.bytes();
     }
     hh::TileDev dev() const {
         return hh::TileDev{pay.p, payn.p, tile_J.p, tile_ent.p, tile_rp.p, tile_entn.p, tile_rpn.p, u_tlo.p,
                            u_thi.p, u_rb.p, u_rlo.p, u_rhi.p, u_slot.p, u_glo.p, u_ghi.p, blk_unit_ptr.p,
-                           u_order.p, tile_perm.p, tile_band.p, u_whole.p};
+                           u_order.p, tile_perm.p, tile_band.p, tile_fw.p, tile_frec.p,
+                           reinterpret_cast<const uint4*>(frec.p), u_whole.p};
     }
 };
 

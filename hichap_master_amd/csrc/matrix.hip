@@ -12,6 +12,7 @@ namespace hh {
 static thread_local std::string g_last_error;
 int64_t g_unit_entries = 0;  // 0 = auto (plan_tiles)
 int64_t g_band_w = -1;       // -1 = auto (choose_band_w)
+int64_t g_flat_max = 64;     // longest row (uint4) of a flat tile segment; 0 = no flat segments
 
 int32_t choose_band_w(const std::vector<double>& occ, int ignore_diags) {
     if (g_band_w >= 0) return (int32_t)std::min<int64_t>(g_band_w, kBandMaxW) & ~15;
@@ -53,7 +54,14 @@ TilePlan plan_tiles(const uint16_t* cntw, const uint16_t* cntn, int64_t nloc, in
             P.tile_rb.push_back((int32_t)rb);
             P.tile_rp.insert(P.tile_rp.end(), rp.begin(), rp.end());
             P.tile_rpn.insert(P.tile_rpn.end(), rpn.begin(), rpn.end());
-            // sorted-band order of both segments (narrow first)
+            // per segment (narrow first): rows by decreasing length (uint4
+            // count, counting sort on min(len, 255), stable) and the bands of
+            // that order; a tile whose nonempty segments have only short rows
+            // (<= g_flat_max uint4) is *flat*: its perms list the nonempty rows
+            // in row order instead (band[kFlatFlag] = 1, band[kFlatRows] = count)
+            uint16_t perm[2][kR];
+            uint16_t band[2][kBandSlots] = {{0}};
+            uint32_t maxlen[2];
             for (int seg = 0; seg < 2; ++seg) {
                 const std::vector<uint32_t>& q = seg == 0 ? rpn : rp;
                 const int sh = seg == 0 ? 3 : 2;
@@ -65,16 +73,65 @@ TilePlan plan_tiles(const uint16_t* cntw, const uint16_t* cntn, int64_t nloc, in
                     ++hist[key[k] + 1];
                 }
                 for (int k = 0; k < 256; ++k) hist[k + 1] += hist[k];
-                uint16_t perm[kR];
-                for (int k = 0; k < kR; ++k) perm[hist[key[k]]++] = (uint16_t)k;
-                P.tile_perm.insert(P.tile_perm.end(), perm, perm + kR);
-                uint16_t band[kBandSlots] = {0};
+                for (int k = 0; k < kR; ++k) perm[seg][hist[key[k]]++] = (uint16_t)k;
                 int pos = 0;
                 for (int g = 0; g < kBands; ++g) {
-                    while (pos < kR && ((q[perm[pos] + 1] - q[perm[pos]]) >> sh) >= band_min(g)) ++pos;
-                    band[g + 1] = (uint16_t)pos;
+                    while (pos < kR && ((q[perm[seg][pos] + 1] - q[perm[seg][pos]]) >> sh) >= band_min(g)) ++pos;
+                    band[seg][g + 1] = (uint16_t)pos;
                 }
-                P.tile_band.insert(P.tile_band.end(), band, band + kBandSlots);
+                maxlen[seg] = 255u - key[perm[seg][0]];
+            }
+            const bool flat = g_flat_max > 0 && maxlen[0] <= (uint32_t)g_flat_max &&
+                              maxlen[1] <= (uint32_t)g_flat_max && (rpn[kR] >> 3) < 65536u && (rp[kR] >> 2) < 65536u;
+            uint32_t fw[kFlatMeta] = {0};
+            if (flat) {
+                for (int seg = 0; seg < 2; ++seg) {
+                    const std::vector<uint32_t>& q = seg == 0 ? rpn : rp;
+                    const int sh = seg == 0 ? 3 : 2;
+                    int nfr = 0;
+                    uint32_t st[kR + 1];  // uint4 starts of the nonempty rows, then the end
+                    for (int k = 0; k < kR; ++k)
+                        if (q[k + 1] > q[k]) {
+                            st[nfr] = q[k] >> sh;
+                            perm[seg][nfr++] = (uint16_t)k;
+                        }
+                    for (int k = nfr; k < kR; ++k) perm[seg][k] = 0;
+                    const uint32_t Q = q[kR] >> sh;
+                    st[nfr] = Q;
+                    band[seg][kFlatFlag] = nfr > 0 ? 1 : 0;
+                    band[seg][kFlatRows] = (uint16_t)nfr;
+                    // wave w takes the rows starting in [Q w / 8, Q (w + 1) / 8)
+                    uint32_t* f = fw + seg * 2 * (kFlatWaves + 1);
+                    for (int w = 0; w <= kFlatWaves; ++w) {
+                        const uint32_t tq = (uint32_t)(((uint64_t)Q * w) / kFlatWaves);
+                        const int i = (int)(std::lower_bound(st, st + nfr, tq) - st);
+                        f[2 * w] = st[i];
+                        f[2 * w + 1] = (uint32_t)i;
+                    }
+                }
+            }
+            P.tile_fw.insert(P.tile_fw.end(), fw, fw + kFlatMeta);
+            if (flat) {
+                P.tile_frec.push_back((int32_t)(P.frec.size() / (kFrecU4 * 8)));
+                const size_t base = P.frec.size();
+                P.frec.resize(base + kFrecU4 * 8, 0);
+                uint16_t* rec = &P.frec[base];
+                for (int seg = 0; seg < 2; ++seg) {
+                    const std::vector<uint32_t>& q = seg == 0 ? rpn : rp;
+                    const int sh = seg == 0 ? 3 : 2;
+                    const int nfr = band[seg][kFlatRows];
+                    uint16_t* st = rec + seg * (kR + 1);
+                    uint16_t* id = rec + 2 * (kR + 1) + seg * kR;
+                    for (int i = 0; i <= kR; ++i) st[i] = (uint16_t)(i < nfr ? q[perm[seg][i]] >> sh : q[kR] >> sh);
+                    for (int i = 0; i < kR; ++i) id[i] = perm[seg][i];
+                }
+            } else {
+                P.tile_frec.push_back(-1);
+            }
+            P.tile_flat.push_back(flat ? 1 : 0);
+            for (int seg = 0; seg < 2; ++seg) {
+                P.tile_perm.insert(P.tile_perm.end(), perm[seg], perm[seg] + kR);
+                P.tile_band.insert(P.tile_band.end(), band[seg], band[seg] + kBandSlots);
             }
             ent += rp[kR];
             entn += rpn[kR];
@@ -105,6 +162,7 @@ TilePlan plan_tiles(const uint16_t* cntw, const uint16_t* cntn, int64_t nloc, in
         P.u_whole.push_back(rlo == 0 && rhi == (int32_t)(std::min<int64_t>(nloc, rb * kR + kR) - rb * kR) ? 1 : 0);
         P.u_glo.push_back(row_group[g0]);
         P.u_ghi.push_back(row_group[g1]);
+        P.u_flat.push_back(P.u_whole.back() && P.tile_flat[ta] ? 1 : 0);
         P.n_part += rhi - rlo;
     };
     for (int64_t rb = 0; rb < P.nrb; ++rb) {
@@ -132,7 +190,8 @@ TilePlan plan_tiles(const uint16_t* cntw, const uint16_t* cntn, int64_t nloc, in
                 cur = t + 1;
                 cur_sz = 0;
             } else {
-                if (cur < t && cur_sz + sz > unit_cap) {
+                // a unit is all flat tiles or none (two sweep kernels)
+                if (cur < t && (cur_sz + sz > unit_cap || P.tile_flat[t] != P.tile_flat[cur])) {
                     emit(rb, cur, t, 0, nr);
                     cur = t;
                     cur_sz = 0;
@@ -143,10 +202,16 @@ TilePlan plan_tiles(const uint16_t* cntw, const uint16_t* cntn, int64_t nloc, in
         if (cur < tb) emit(rb, cur, tb, 0, nr);
     }
     P.blk_unit_ptr[P.nrb] = (int32_t)P.u_tlo.size();
-    P.u_order.resize(P.u_tlo.size());
-    std::iota(P.u_order.begin(), P.u_order.end(), 0);
-    std::stable_sort(P.u_order.begin(), P.u_order.end(),
-                     [&](int32_t x, int32_t y) { return P.tile_J[P.u_tlo[x]] < P.tile_J[P.u_tlo[y]]; });
+    // launch lists: the tiled-kernel units, then the flat-kernel units
+    P.n_units_flat = 0;
+    for (size_t u = 0; u < P.u_tlo.size(); ++u)
+        if (!P.u_flat[u]) P.u_order.push_back((int32_t)u);
+    for (size_t u = 0; u < P.u_tlo.size(); ++u)
+        if (P.u_flat[u]) {
+            P.u_order.push_back((int32_t)u);
+            ++P.n_units_flat;
+            for (int32_t t = P.u_tlo[u]; t < P.u_thi[u]; ++t) P.payload_bytes_flat += 4 * tile_words(t, 0, kR);
+        }
     if (P.n_part > INT32_MAX || P.tile_J.size() > (size_t)INT32_MAX) HH_THROW(HH_ERR_ARG, "plan too large");
     return P;
 }
@@ -156,6 +221,8 @@ void upload_plan(const TilePlan& P, hh_matrix& m, hipStream_t s) {
     m.nrb = P.nrb;
     m.n_tiles = (int64_t)P.tile_J.size();
     m.n_units = (int64_t)P.u_tlo.size();
+    m.n_units_flat = P.n_units_flat;
+    m.payload_bytes_flat = P.payload_bytes_flat;
     m.n_part = P.n_part;
     m.n_slots = P.n_entries_padded;
     m.n_slots_narrow = P.n_narrow_padded;
@@ -180,6 +247,9 @@ void upload_plan(const TilePlan& P, hh_matrix& m, hipStream_t s) {
     m.u_order = to_device(P.u_order, s);
     m.tile_perm = to_device(P.tile_perm, s);
     m.tile_band = to_device(P.tile_band, s);
+    m.tile_fw = to_device(P.tile_fw, s);
+    m.tile_frec = to_device(P.tile_frec, s);
+    m.frec = to_device(P.frec, s);
     m.u_whole = to_device(P.u_whole, s);
     HIP_CHECK(hipStreamSynchronize(s));  // the plan's host vectors may die after return
 }
@@ -442,8 +512,9 @@ int hh_matrix_get_info(const hh_matrix* m, hh_matrix_info* info) {
         info->n_slots_narrow = m->n_slots_narrow;
         info->payload_bytes = 4 * m->n_slots + 2 * m->n_slots_narrow + (int64_t)m->band.n;
         info->band_w = m->band_w;
-        info->pad_ = 0;
+        info->n_units_flat = (int32_t)m->n_units_flat;
         info->n_band = m->n_band;
+        info->payload_bytes_flat = m->payload_bytes_flat;
         info->n_chroms = m->n_chroms;
         info->ignore_diags = m->ignore_diags;
         info->cis_only = m->cis_only;

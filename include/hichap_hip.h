@@ -47,7 +47,10 @@ int hh_device_count(int32_t* n);
 int hh_set_device(int32_t device);
 int hh_synchronize(void* stream);
 /* Performance knobs: "band_w" (-1 auto, 0 no dense band, > 0 forced
- * multiple of 16; for matrices built afterwards), "sweep_nb" in {1,2,4,8} (row batches in flight per
+ * multiple of 16; for matrices built afterwards), "flat_max" (0..255: longest
+ * row, in 16-B payload words, of a tile swept by the flat kernel; 0 = none;
+ * later builds), "band_concurrent" 0/1 (dense-band sweep on a side stream),
+ * "sweep_nb" in {1,2,4,8} (row batches in flight per
  * wave), "unit_entries" (work-unit size used by later matrix builds),
  * "sweep_ablate" 0/1/2 (timing ablations only: 1 skips the LDS gathers,
  * 2 skips the b staging; results are wrong while set). */
@@ -94,8 +97,9 @@ typedef struct {
     int32_t cis_only;
     int32_t device;
     int32_t band_w;        /* dense diagonal band half-width W (0 = none)    */
-    int32_t pad_;
+    int32_t n_units_flat;  /* work units swept by the flat (short-row) kernel */
     int64_t n_band;        /* nonzero entries held by the band               */
+    int64_t payload_bytes_flat; /* part of payload_bytes in flat-kernel tiles */
 } hh_matrix_info;
 
 /* Build from cooler's pixel table (upper triangle bin1 <= bin2; any order,

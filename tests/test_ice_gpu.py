@@ -113,44 +113,57 @@ def test_invalid_counts_rejected(ice):
         ice.ContactMatrix.from_pixels([0, 1], [5, 60], [1, 2], 10, [0, 10])
 
 
-def test_sharded_equals_full_bitwise(ice):
-    """Two row shards on one GPU with a manual gather == the one-shard run."""
+def _sharded_weights(ice, b1, b2, c, off, rr, max_iters=300):
+    """Row shards on one GPU with a manual marginal gather (the sharded
+    driver's exchange, without a process group)."""
     import torch
-    from hichap_master_amd import dist
-    b1, b2, c, off = _case(8, sizes=(500, 400))
     n = int(off[-1])
-    opts = ice.IceOptions(max_iters=300)
-    w_full, st_full = ice.balance(b1, b2, c, n, off, max_iters=300)
-    rr = dist.partition_rows(np.bincount(b1, minlength=n) + np.bincount(b2, minlength=n), 2)
-    shards = [ice.ContactMatrix.from_pixels(b1, b2, c, n, off, row_range=(rr[k], rr[k + 1])) for k in range(2)]
+    opts = ice.IceOptions(max_iters=max_iters)
+    W = len(rr) - 1
+    shards = [ice.ContactMatrix.from_pixels(b1, b2, c, n, off, row_range=(rr[k], rr[k + 1])) for k in range(W)]
     states = [ice.IceState(m, opts) for m in shards]
     maxlen = int(np.max(np.diff(rr)))
-    loc = [torch.zeros(maxlen, dtype=torch.float64, device="cuda") for _ in range(2)]
-    gat = torch.zeros(2 * maxlen, dtype=torch.float64, device="cuda")
+    loc = [torch.zeros(maxlen, dtype=torch.float64, device="cuda") for _ in range(W)]
+    gat = torch.zeros(W * maxlen, dtype=torch.float64, device="cuda")
     s = torch.cuda.current_stream().cuda_stream
 
     def exchange(mode):
-        for k in range(2):
+        for k in range(W):
             states[k].marg_local(mode, loc[k], s)
-        for k in range(2):
+        for k in range(W):
             gat[k * maxlen:(k + 1) * maxlen].copy_(loc[k])
-        for k in range(2):
-            states[k].set_marg(gat, 2, maxlen, rr, s)
+        for k in range(W):
+            states[k].set_marg(gat, W, maxlen, rr, s)
     exchange(0)
     for st_ in states:
         st_.filter_nnz(s)
     exchange(1)
     for st_ in states:
         st_.filter_count_mad(s)
-    for it in range(300):
+    for it in range(max_iters):
         exchange(2)
         for st_ in states:
             st_.update(s)
         if it % 8 == 7 and states[0].active_groups(s) == 0:
             break
-    w0, s0 = states[0].finalize(s)
-    w1, s1 = states[1].finalize(s)
-    np.testing.assert_array_equal(w0, w1)
+    res = [st_.finalize(s) for st_ in states]
+    for st_ in states:
+        st_.close()
+    for m in shards:
+        m.close()
+    for w, _ in res[1:]:
+        np.testing.assert_array_equal(w, res[0][0])
+    return res[0]
+
+
+def test_sharded_equals_full_bitwise(ice):
+    """Two row shards on one GPU with a manual gather == the one-shard run."""
+    from hichap_master_amd import dist
+    b1, b2, c, off = _case(8, sizes=(500, 400))
+    n = int(off[-1])
+    w_full, st_full = ice.balance(b1, b2, c, n, off, max_iters=300)
+    rr = dist.partition_rows(np.bincount(b1, minlength=n) + np.bincount(b2, minlength=n), 2)
+    w0, s0 = _sharded_weights(ice, b1, b2, c, off, rr)
     np.testing.assert_array_equal(w0, w_full)
     assert s0["iters"] == st_full["iters"]
 
@@ -263,3 +276,31 @@ def test_dense_band_widths(ice, band_w):
     w_ref, st_ref = ice_ref.balance(b1, b2, c, n, off)
     assert st["iters"] == st_ref["iters"]
     np.testing.assert_allclose(w, w_ref, rtol=1e-9, equal_nan=True)
+
+
+@pytest.mark.parametrize("flat_max", [0, 2, 24, 255])
+def test_flat_tiles(ice, flat_max):
+    """Tiles whose rows are all short go to the flat (merge-path) sweep kernel;
+    any threshold (none, few, most, all tiles flat) gives the oracle's weights,
+    and a 3-shard run is bitwise equal to the whole-matrix run."""
+    from hichap_master_amd import _lib
+    b1, b2, c, off = _case(41, sizes=(9000, 7000, 600), A=3.0, trans=0.0005)
+    n = int(off[-1])
+    _lib.call("hh_tune", b"flat_max", flat_max)
+    try:
+        m = ice.ContactMatrix.from_pixels(b1, b2, c, n, off)
+        inf = m.info()
+        if flat_max == 0:
+            assert inf["n_units_flat"] == 0
+        if flat_max == 255:
+            assert inf["n_units_flat"] > 0
+        w, st = ice.balance_matrix(m, ice.IceOptions(max_iters=300))
+        m.close()
+        ws, sts = _sharded_weights(ice, b1, b2, c, off, np.array([0, 4096, 11264, n]))
+    finally:
+        _lib.call("hh_tune", b"flat_max", 64)
+    w_ref, st_ref = ice_ref.balance(b1, b2, c, n, off, max_iters=300)
+    assert st["iters"] == st_ref["iters"]
+    np.testing.assert_allclose(w, w_ref, rtol=1e-9, equal_nan=True)
+    np.testing.assert_array_equal(ws, w)
+    assert sts["iters"] == st["iters"]

@@ -1,0 +1,45 @@
+"""GPU probe on the C4 synthetic matrix: ICE sweep time under run-time knob
+settings (hh_tune), one matrix build.  Usage:
+    python tools/probe_knobs.py "band_concurrent=0" "band_concurrent=1,sweep_nb=1" ...
+Build-time knobs (band_w, unit_entries) may be given with --build k=v,..."""
+import argparse
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from hichap_master_amd import ice, _lib, synth  # noqa: E402
+
+
+def tune(spec):
+    for kv in filter(None, spec.split(",")):
+        k, v = kv.split("=")
+        _lib.call("hh_tune", k.encode(), int(v))
+
+
+ap = argparse.ArgumentParser()
+ap.add_argument("settings", nargs="+")
+ap.add_argument("--build", default="")
+ap.add_argument("--nnz", type=float, default=5e9)
+ap.add_argument("--iters", type=int, default=10)
+a = ap.parse_args()
+_lib.load(); _lib.require_gpu()
+sizes = synth.genome_bins(10000, diploid=True)
+A, td = synth.calibrate(sizes, a.nnz, 0.2)
+tune(a.build)
+t0 = time.time()
+m = ice.ContactMatrix.synthetic(sizes, A=A, trans_density=td)
+inf = m.info()
+print(f"build {time.time()-t0:.1f}s band_w={inf['band_w']} units={inf['n_units']} "
+      f"payload {inf['payload_bytes']/1e9:.2f} GB (flat {inf['payload_bytes_flat']/1e9:.2f} GB in "
+      f"{inf['n_units_flat']} units, band {2 * inf['band_w'] * (inf['row_hi'] - inf['row_lo']) / 1e9:.2f} GB) "
+      f"tiles {inf['n_tiles']}", flush=True)
+st = ice.IceState(m, ice.IceOptions(tol=0.0, max_iters=10**6, mad_max=0, min_nnz=0))
+for rep in range(2):
+    for spec in a.settings:
+        tune(spec)
+        st.run(2)
+        st.run(a.iters)
+        ms, n, it_ms = st.last_timing()
+        print(f"[{rep}] {spec}: sweep {ms/n:.3f} ms  iter {it_ms/n:.3f} ms", flush=True)
+st.close(); m.close()
