@@ -575,6 +575,7 @@ __global__ __launch_bounds__(kBandThreads) void k_sweep_band(const uint8_t* __re
                                                              const double* __restrict__ b,
                                                              double* __restrict__ bpart) {
     __shared__ double bl[kBandWin + kBandWin / 16 + 1];
+    __shared__ uint8_t ract[kBandRows];  // active flag per row (no dependent global loads in the row loop)
     const long long r0 = (long long)blockIdx.x * kBandRows;
     const int chunk = blockIdx.y;
     const int s0 = chunk * kBandChunk, s1 = min(s0 + kBandChunk, 2 * W);
@@ -589,13 +590,14 @@ __global__ __launch_bounds__(kBandThreads) void k_sweep_band(const uint8_t* __re
         const double v = (c >= 0 && c < n_bins) ? b[c] : 0.0;
         bl[bpad(k)] = v == v ? v : 0.0;
     }
+    for (int k = threadIdx.x; k < nr; k += kBandThreads) ract[k] = act[row_group[r0 + k]] != 0;
     __syncthreads();
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     constexpr int NW = kBandThreads / 64;
     for (int rr = wave; rr < nr; rr += 2 * NW) {
         const int rr2 = rr + NW;
         const bool two = rr2 < nr;
-        const bool a1 = act[row_group[r0 + rr]] != 0, a2 = two && act[row_group[r0 + rr2]] != 0;
+        const bool a1 = ract[rr] != 0, a2 = two && ract[rr2] != 0;
         const uint8_t* row1 = band + (r0 + rr) * (long long)(2 * W);
         const uint8_t* row2 = band + (r0 + rr2) * (long long)(2 * W);
         double acc1 = 0.0, acc2 = 0.0;
@@ -876,7 +878,7 @@ static void marg_weighted(hh_ice* S, double* out, hipStream_t s, bool timed, int
     hh_matrix* m = S->m;
     if (timed) HIP_CHECK(hipEventRecord(S->ev[2 * slot], s));
     {
-        HH_KTIME(timed ? nullptr : "k_sweep_tiled", s);  // registry timing for the sharded driver (tiles + band)
+        HH_KTIME(timed ? nullptr : "ice_sweep", s);  // registry timing for the sharded driver (tiled + flat + band)
         // the two sweeps write disjoint partials (part / bpart): the band
         // kernel runs on a side stream so its blocks fill the CUs the tile
         // kernel leaves idle (both are HBM-bound; neither saturates alone)
