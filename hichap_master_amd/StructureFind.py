@@ -7,6 +7,8 @@ arguments as ``HiCHap/StructureFind.py``:
 * ``Select_Allelic_PC(pcs, trad_pc)``      :446-460
 * ``Get_Gap(M)`` / ``Get_DI(M, Gap, w)``   :721-751 / :804-839
 * ``Gap_Filter(Gap, M)``                   :753-802
+* ``Data_preprocess`` / ``viterbipath`` / ``BoundaryCall`` /
+  ``BoundaryFilter`` / ``BoundaryToDomain``  :842-1342 (``tads.py``)
 
 The O(N^2) / O(N^2 n) work (column nonzeros, per-distance sums, O/E,
 Pearson correlation on fp64 MFMA, top-3 PCA, the masked sums of the PC
@@ -24,6 +26,7 @@ import numpy as np
 
 from . import _lib
 from ._lib import call, ptr
+from .tads import GaussianMixtureHMM, TADCalling  # noqa: F401  (TAD HMM + boundary rules)
 
 PCA_TOL = 1e-13   # max entry change of the unit Ritz vectors between iterations
 PCA_MAX_ITERS = 2000
@@ -150,8 +153,9 @@ class DeviceOE:
         return out if dtype is None else out.astype(dtype)
 
 
-class StructureFind(object):
-    """Numeric part of HiCHap's StructureFind (StructureFind.py:27)."""
+class StructureFind(TADCalling):
+    """Numeric part of HiCHap's StructureFind (StructureFind.py:27); the TAD
+    HMM / boundary-rule methods come from ``tads.TADCalling``."""
 
     def __init__(self, cooler_fil=None, Res=40000, Allelic=False, GapFile=None, Loop_ratio=0.6,
                  Loop_strength=16, stream=None):

@@ -96,6 +96,7 @@ SIGNATURES = {
     "hh_comp_set_cor": (C.c_int, [P, P, P]),
     "hh_gap_scan": (C.c_int, [P, I64, I32, I32, P, I32, P]),
     "hh_di_scan": (C.c_int, [P, I64, I32, P, P, I32, P, I32, P]),
+    "hh_viterbi_gmm": (C.c_int, [P, I64, I32, I32, P, P, P, P, P, P, P]),
     "hh_comp_pca": (C.c_int, [P, I32, F64, I32, P, P, P, P]),
     "hh_comp_select_stats": (C.c_int, [P, P, I32, F64, P, P]),
     "hh_binner_create": (C.c_int, [I32, C.c_char_p, P, I32, I32, C.POINTER(P)]),

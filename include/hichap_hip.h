@@ -18,6 +18,8 @@
  *   hh_compartment_*    StructureFind.Distance_Decay / Get_PCA / Select_PC_new,
  *                       StructureFind.py:201-423
  *   hh_di_scan          StructureFind.Get_Gap / Get_DI, StructureFind.py:721-839
+ *   hh_viterbi_gmm      StructureFind.viterbipath (ghmm model.viterbi),
+ *                       StructureFind.py:1113-1123 (host code)
  *   hh_hiccups_*        StructureFind.pcaller neighbourhood sums (HICCUPS loops),
  *                       StructureFind.py:1631-1830
  *   hh_binner_*         the per-line pair binning loops of TraditionalMatrixBuilding
@@ -270,6 +272,17 @@ int hh_gap_scan(const double* band, int64_t N, int32_t B, int32_t lb, uint8_t* g
                 void* stream);
 int hh_di_scan(const double* band, int64_t N, int32_t B, const uint8_t* gap, const int32_t* window_bins,
                int32_t test, double* di, int32_t on_device, void* stream);
+
+/* ------------------------------------------------- TAD HMM (host code)
+ * Viterbi path of a continuous HMM with Gaussian-mixture emissions, ghmm's
+ * `model.viterbi(EmissionSequence)` as StructureFind.viterbipath calls it
+ * (:1113-1123): S states, M components per state; A (S x S, row-major) and pi
+ * are probabilities, mean / var / weight are S x M (var = variance, ghmm's
+ * GaussianMixtureDistribution parameters).  Log space, a_ij = 0 -> -inf, ties
+ * to the lowest state.  path[t] = state of obs[t]; *logp = log joint
+ * probability of the path.  Runs on the host (no GPU needed). */
+int hh_viterbi_gmm(const double* obs, int64_t n, int32_t S, int32_t M, const double* A, const double* pi,
+                   const double* mean, const double* var, const double* weight, int32_t* path, double* logp);
 
 /* ---------------------------------------------------------- pair binning
  * Pair text (HiCHap *_Valid.bed: chrom/pos in fields 1, 6, 8, 13; allelic
