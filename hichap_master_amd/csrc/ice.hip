@@ -36,7 +36,7 @@ constexpr int kThreads = 256;
 // which only that wave touches -> fixed summation order (deterministic).
 constexpr int kSweepThreads = 512;
 constexpr int kSweepWaves = kSweepThreads / 64;
-constexpr int kFlatU = 4;  // uint4 per lane per step in flat segments
+constexpr int kFlatU = 8;  // uint4 per lane per step in flat narrow segments
 
 // Entry decode: the byte offset of the staged bias value is a field of the
 // entry (ice_internal.hpp), so an entry costs mask, shift, cvt, LDS read and
@@ -369,6 +369,83 @@ __device__ __forceinline__ void flat_step(const uint4 (&v)[U], uint32_t q0, uint
     ic = __shfl(lo + j, 63, 64);
 }
 
+// flat_step with the accumulator indexed by compact row (the row's index in
+// fst), not by row id: every nonempty row's first write is a plain store by
+// the lane holding its start (a row that starts and ends in the run, or the
+// tail + heads of one that continues), later steps add through lane 0 -- so
+// no row ids, no stash and no read-modify-write inside the walk (registers
+// for U = 8).  accc[i] is mapped to the row accumulator after the segment.
+template <int U, int ABL, int EPV>
+__device__ __forceinline__ void flat_step_c(const uint4 (&v)[U], uint32_t q0, uint32_t qb, int& ic, int i1,
+                                            const uint16_t* __restrict__ fst, int nfr,
+                                            const double* __restrict__ bl, double* __restrict__ accc, int lane) {
+    const uint32_t s = q0 + (uint32_t)lane * U;
+    const bool act = s < qb;
+    int lo = ic, hi = min(i1 - 1, ic + lane * U + 1);
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if ((uint32_t)fst[mid] <= s) lo = mid; else hi = mid - 1;
+    }
+    const bool head = (uint32_t)fst[lo] < s;
+    uint32_t nb[U];
+#pragma unroll
+    for (int k = 0; k < U - 1; ++k) nb[k] = fst[min(lo + 1 + k, nfr)];
+    double x = 0.0, h = 0.0;
+    bool inhead = head;
+    int j = 0;
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+        if (k > 0) {
+            uint32_t nxt = nb[0];
+#pragma unroll
+            for (int jj = 1; jj < k; ++jj)
+                if (j == jj) nxt = nb[jj];
+            if (s + k == nxt && s + k < qb) {
+                if (inhead) {
+                    h = x;
+                    inhead = false;
+                } else {
+                    accc[lo + j] = x;  // started and ended in this run
+                }
+                x = 0.0;
+                ++j;
+            }
+        }
+        x += ABL == 1 ? (double)(v[k].x + v[k].y + v[k].z + v[k].w) : flat_dot<EPV>(v[k], bl);
+    }
+    if (inhead) h = x;
+    const bool tail = act && !inhead;
+    double H = act ? h : 0.0;
+    int F = (!act || inhead) ? 1 : 0;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const double Hn = __shfl_down(H, o, 64);
+        const int Fn = __shfl_down(F, o, 64);
+        if (lane + o < 64 && F) {
+            H += Hn;
+            F = Fn;
+        }
+    }
+    const double Hr = __shfl_down(H, 1, 64);
+    if (tail) accc[lo + j] = x + (lane < 63 ? Hr : 0.0);  // the row's first write
+    if (lane == 0 && head) accc[lo] += H;                 // continues a row of an earlier step
+    ic = __shfl(lo + j, 63, 64);
+}
+
+template <int U, int ABL, int EPV>
+__device__ __forceinline__ void flat_seg_c(const uint4* __restrict__ pay4, uint4 (&v)[U], uint32_t qa, uint32_t qb,
+                                           int i0, int i1, const uint16_t* __restrict__ fst, int nfr,
+                                           const double* __restrict__ bl, double* __restrict__ accc, int lane) {
+    if (i0 >= i1) return;
+    int ic = i0;
+    for (uint32_t q0 = qa;;) {
+        flat_step_c<U, ABL, EPV>(v, q0, qb, ic, i1, fst, nfr, bl, accc, lane);
+        q0 += 64u * U;
+        if (q0 >= qb) break;
+        flat_load<U>(pay4, q0 + (uint32_t)lane * U, qa, qb, v);
+    }
+}
+
 // A wave's rows [i0, i1) = uint4 [qa, qb) of one segment, the first step's
 // run already loaded into v (its loads were issued before the tile's LDS
 // staging, so they fly while the block stages).
@@ -491,11 +568,13 @@ __global__ __launch_bounds__(kSweepThreads, 4) void k_sweep_tiled(TileDev T, con
 }
 
 // K1c: the flat tiles (whole row-blocks whose rows are all short).  Per
-// tile the latency chain is kept to two hops: each wave's row / uint4 range
-// (tile_fw, scalar loads prefetched one tile ahead) lets it issue the loads
-// of its first narrow and wide runs at once, while the block copies the bias
-// slice and the tile's flat record (compacted row starts + row ids) into LDS
-// in one pass; then the waves sweep both segments with flat_seg.
+// tile the latency chain is kept to one hop: each wave's row / uint4 range
+// (tile_fw, read one tile ahead) lets it issue the loads of its whole narrow
+// run (U = 8 uint4 per lane: one step covers the typical tile) and its first
+// wide run at once, while the block copies the bias slice and the tile's flat
+// record (compacted row starts + row ids) into LDS in one pass; the narrow
+// segment accumulates by compact row (flat_step_c), the few wide rows by row
+// id, and after a barrier the compact sums are added to their rows.
 template <int U, int ABL>
 __global__ __launch_bounds__(kSweepThreads, 4) void k_sweep_flat(TileDev T, const uint8_t* __restrict__ act,
                                                                int n_list, int list_off,
@@ -504,7 +583,8 @@ __global__ __launch_bounds__(kSweepThreads, 4) void k_sweep_flat(TileDev T, cons
     static_assert(kSweepWaves == kFlatWaves, "one plan split per wave");
     constexpr int UW = 2;  // wide runs: few wide entries in flat tiles
     __shared__ __attribute__((aligned(16))) double bl[kW];
-    __shared__ double acc2[2 * kR];  // narrow rows, then wide rows
+    __shared__ double acc[kR];    // row sums (narrow + wide)
+    __shared__ double accc[kR];   // narrow sums by compact row
     __shared__ __attribute__((aligned(16))) uint16_t rec[kFrecU4 * 8];
     if ((int)blockIdx.x >= n_list) return;
     const int u = T.u_order[list_off + blockIdx.x];
@@ -519,7 +599,7 @@ __global__ __launch_bounds__(kSweepThreads, 4) void k_sweep_flat(TileDev T, cons
     const uint16_t* fstw = rec + (kR + 1);
     const uint16_t* fidn = rec + 2 * (kR + 1);
     const uint16_t* fidw = fidn + kR;
-    for (int k = threadIdx.x; k < 2 * nr; k += kSweepThreads) acc2[k] = 0.0;
+    for (int k = threadIdx.x; k < nr; k += kSweepThreads) acc[k] = 0.0;
     const int t0 = T.u_tlo[u], t1 = T.u_thi[u];
     for (int t = t0; t < t1; ++t) {
         const uint32_t* fw = T.tile_fw + (size_t)t * kFlatMeta;
@@ -527,22 +607,24 @@ __global__ __launch_bounds__(kSweepThreads, 4) void k_sweep_flat(TileDev T, cons
         const uint32_t* fww = fw + 2 * (kFlatWaves + 1) + 2 * wave;
         const uint32_t qan = fwn[0], qbn = fwn[2], qaw = fww[0], qbw = fww[2];
         const int i0n = (int)fwn[1], i1n = (int)fwn[3], i0w = (int)fww[1], i1w = (int)fww[3];
-        const int nfn = (int)fw[2 * kFlatWaves + 1], nfw = (int)fww[2 * (kFlatWaves - wave) + 1];
+        const int nfn = (int)fw[2 * kFlatWaves + 1], nfw = (int)fw[2 * (kFlatWaves + 1) + 2 * kFlatWaves + 1];
         const uint4* payn4 = reinterpret_cast<const uint4*>(T.payn + T.tile_entn[t]);
         const uint4* payw4 = reinterpret_cast<const uint4*>(T.pay + T.tile_ent[t]);
         uint4 v[U], vw[UW];
         if (i0n < i1n) flat_load<U>(payn4, qan + (uint32_t)lane * U, qan, qbn, v);
         if (i0w < i1w) flat_load<UW>(payw4, qaw + (uint32_t)lane * UW, qaw, qbw, vw);
         const uint4* rg = T.frec + (size_t)T.tile_frec[t] * kFrecU4;
-        __syncthreads();  // previous tile's LDS reads are done
-        if (ABL != 2) stage_bias<U >= 8 ? 2 : 1>(bl, b, (long long)T.tile_J[t] * kW, n_bins);
+        __syncthreads();  // previous tile's LDS reads (and its mapping) are done
+        if (ABL != 2) stage_bias(bl, b, (long long)T.tile_J[t] * kW, n_bins);
         for (int k = threadIdx.x; k < kFrecU4; k += kSweepThreads) reinterpret_cast<uint4*>(rec)[k] = rg[k];
         __syncthreads();
-        flat_seg<U, ABL, 8>(payn4, v, qan, qbn, i0n, i1n, fstn, fidn, nfn, bl, acc2, lane);
-        flat_seg<UW, ABL, 4>(payw4, vw, qaw, qbw, i0w, i1w, fstw, fidw, nfw, bl, acc2 + nr, lane);
+        flat_seg_c<U, ABL, 8>(payn4, v, qan, qbn, i0n, i1n, fstn, nfn, bl, accc, lane);
+        flat_seg<UW, ABL, 4>(payw4, vw, qaw, qbw, i0w, i1w, fstw, fidw, nfw, bl, acc, lane);
+        __syncthreads();  // compact narrow sums complete; wide row sums written
+        for (int k = threadIdx.x; k < nfn; k += kSweepThreads) acc[fidn[k]] += accc[k];
     }
     __syncthreads();
-    for (int k = threadIdx.x; k < nr; k += kSweepThreads) part[T.u_slot[u] + k] = acc2[k] + acc2[nr + k];
+    for (int k = threadIdx.x; k < nr; k += kSweepThreads) part[T.u_slot[u] + k] = acc[k];
 }
 
 // ---------------------------------------------------------------- K2
@@ -560,10 +642,16 @@ __device__ __forceinline__ int bpad(int k) { return k + (k >> 4); }
 
 __device__ __forceinline__ double band_dot16(const uint4 v, const double* __restrict__ bl, int base, double acc) {
     const unsigned x[4] = {v.x, v.y, v.z, v.w};
+    // bpad(base + k) = p0 + k before the window's next 16-boundary, p0 + k + 1
+    // after it: one select per element, the k offset folds into the LDS read
+    const uint32_t a0 = (uint32_t)bpad(base) * 8u, a1 = a0 + 8u;
+    const int split = 16 - (base & 15);
+    const char* lds = reinterpret_cast<const char*>(bl);
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
         const unsigned c = (x[k >> 2] >> (8 * (k & 3))) & 0xffu;
-        acc = fma((double)c, bl[bpad(base + k)], acc);
+        const uint32_t a = (k < split ? a0 : a1) + 8u * k;
+        acc = fma((double)c, *reinterpret_cast<const double*>(lds + a), acc);
     }
     return acc;
 }

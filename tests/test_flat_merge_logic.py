@@ -22,7 +22,10 @@ def plan_split(fst, nfr, Q):
     return out
 
 
-def flat_seg(pay, fst, fr, nfr, acc, qa, qb, i0, i1, U):
+def flat_seg(pay, fst, fr, nfr, acc, qa, qb, i0, i1, U, compact=None):
+    """compact: None (row-id accumulation, flat_step) or a dict of compact
+    row -> sum (flat_step_c: every row's first write must be a plain store
+    by the lane holding its start, later ones adds by lane 0)."""
     if i0 >= i1:
         return
     ic, q0 = i0, qa
@@ -49,16 +52,25 @@ def flat_seg(pay, fst, fr, nfr, acc, qa, qb, i0, i1, U):
                     if inhead:
                         h, inhead = x, False
                     else:
-                        done.append((rid[j], x))
+                        done.append((lo + j if compact is not None else rid[j], x))
                     x, j = 0.0, j + 1
                 x += d[k]
             if inhead:
                 h = x
+            c = compact is not None
             L.append(dict(act=act, h=h if act else 0.0, F=(not act) or inhead, x=x,
-                          tail=act and not inhead, orow=rid[j], done=done, head=head, rid0=rid[0], last=lo + j))
+                          tail=act and not inhead, orow=(lo + j) if c else rid[j], done=done, head=head,
+                          rid0=lo if c else rid[0], last=lo + j))
+        def store(r, v):
+            if compact is None:
+                acc[r] += v
+            else:
+                assert r not in compact, "a compact row's first write must be its only store"
+                compact[r] = v
+
         for ln in L:
             for r, v in ln["done"]:
-                acc[r] += v
+                store(r, v)
         H = [ln["h"] for ln in L]
         F = [ln["F"] for ln in L]
         o = 1
@@ -71,15 +83,19 @@ def flat_seg(pay, fst, fr, nfr, acc, qa, qb, i0, i1, U):
             o <<= 1
         for lane, ln in enumerate(L):
             if ln["tail"]:
-                acc[ln["orow"]] += ln["x"] + (H[lane + 1] if lane < 63 else 0.0)
+                store(ln["orow"], ln["x"] + (H[lane + 1] if lane < 63 else 0.0))
         if L[0]["head"]:
-            acc[L[0]["rid0"]] += H[0]
+            if compact is None:
+                acc[L[0]["rid0"]] += H[0]
+            else:
+                assert L[0]["rid0"] in compact, "a continued row was stored before"
+                compact[L[0]["rid0"]] += H[0]
         ic = L[63]["last"]
         q0 += 64 * U
 
 
-@pytest.mark.parametrize("U", [2, 4])
-def test_flat_rows_bookkeeping(U):
+@pytest.mark.parametrize("U,compact", [(2, False), (4, False), (2, True), (8, True)])
+def test_flat_rows_bookkeeping(U, compact):
     rng = np.random.default_rng(7 + U)
     for _ in range(25):
         nrows = 512
@@ -100,8 +116,13 @@ def test_flat_rows_bookkeeping(U):
         fst[:nfr] = rp[nz]
         split = plan_split(fst, nfr, Q)
         acc = np.zeros(nrows)
+        cmp = {} if compact else None
         for w in range(NW):
             (qa, i0), (qb, i1) = split[w], split[w + 1]
-            flat_seg(pay, fst, fr, nfr, acc, qa, qb, i0, i1, U)
+            flat_seg(pay, fst, fr, nfr, acc, qa, qb, i0, i1, U, cmp)
+        if compact:
+            assert sorted(cmp) == list(range(nfr))  # every nonempty row written
+            for i, v in cmp.items():
+                acc[fr[i]] += v
         ref = np.array([pay[rp[r]:rp[r + 1]].sum() for r in range(nrows)])
         np.testing.assert_allclose(acc, ref, rtol=1e-12, atol=1e-12)
