@@ -594,28 +594,45 @@ __global__ __launch_bounds__(kSweepThreads, 4) void k_sweep_flat(TileDev T, cons
         if (!on) return;
     }
     const int nr = T.u_rhi[u];  // whole row-block: rows [0, nr)
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const uint16_t* fstn = rec;
     const uint16_t* fstw = rec + (kR + 1);
     const uint16_t* fidn = rec + 2 * (kR + 1);
     const uint16_t* fidw = fidn + kR;
     for (int k = threadIdx.x; k < nr; k += kSweepThreads) acc[k] = 0.0;
     const int t0 = T.u_tlo[u], t1 = T.u_thi[u];
-    for (int t = t0; t < t1; ++t) {
+    // a flat unit's tiles have consecutive flat records (plan order)
+    const uint4* rg0 = T.frec + (size_t)T.tile_frec[t0] * kFrecU4;
+    // the wave's split of tile t (wave-uniform scalars)
+    struct Meta {
+        uint32_t qan, qbn, qaw, qbw;
+        int i0n, i1n, i0w, i1w, nfn, nfw, J;
+        long long entn, ent;
+    };
+    auto meta = [&](int t) {
         const uint32_t* fw = T.tile_fw + (size_t)t * kFlatMeta;
         const uint32_t* fwn = fw + 2 * wave;
         const uint32_t* fww = fw + 2 * (kFlatWaves + 1) + 2 * wave;
-        const uint32_t qan = fwn[0], qbn = fwn[2], qaw = fww[0], qbw = fww[2];
-        const int i0n = (int)fwn[1], i1n = (int)fwn[3], i0w = (int)fww[1], i1w = (int)fww[3];
-        const int nfn = (int)fw[2 * kFlatWaves + 1], nfw = (int)fw[2 * (kFlatWaves + 1) + 2 * kFlatWaves + 1];
-        const uint4* payn4 = reinterpret_cast<const uint4*>(T.payn + T.tile_entn[t]);
-        const uint4* payw4 = reinterpret_cast<const uint4*>(T.pay + T.tile_ent[t]);
+        Meta m;
+        m.qan = fwn[0], m.qbn = fwn[2], m.qaw = fww[0], m.qbw = fww[2];
+        m.i0n = (int)fwn[1], m.i1n = (int)fwn[3], m.i0w = (int)fww[1], m.i1w = (int)fww[3];
+        m.nfn = (int)fw[2 * kFlatWaves + 1], m.nfw = (int)fw[2 * (kFlatWaves + 1) + 2 * kFlatWaves + 1];
+        m.J = T.tile_J[t];
+        m.entn = T.tile_entn[t], m.ent = T.tile_ent[t];
+        return m;
+    };
+    for (int t = t0; t < t1; ++t) {
+        const Meta cm = meta(t);
+        const uint32_t qan = cm.qan, qbn = cm.qbn, qaw = cm.qaw, qbw = cm.qbw;
+        const int i0n = cm.i0n, i1n = cm.i1n, i0w = cm.i0w, i1w = cm.i1w, nfn = cm.nfn, nfw = cm.nfw;
+        const uint4* payn4 = reinterpret_cast<const uint4*>(T.payn + cm.entn);
+        const uint4* payw4 = reinterpret_cast<const uint4*>(T.pay + cm.ent);
         uint4 v[U], vw[UW];
         if (i0n < i1n) flat_load<U>(payn4, qan + (uint32_t)lane * U, qan, qbn, v);
         if (i0w < i1w) flat_load<UW>(payw4, qaw + (uint32_t)lane * UW, qaw, qbw, vw);
-        const uint4* rg = T.frec + (size_t)T.tile_frec[t] * kFrecU4;
+        const uint4* rg = rg0 + (size_t)(t - t0) * kFrecU4;
         __syncthreads();  // previous tile's LDS reads (and its mapping) are done
-        if (ABL != 2) stage_bias(bl, b, (long long)T.tile_J[t] * kW, n_bins);
+        if (ABL != 2) stage_bias(bl, b, (long long)cm.J * kW, n_bins);
         for (int k = threadIdx.x; k < kFrecU4; k += kSweepThreads) reinterpret_cast<uint4*>(rec)[k] = rg[k];
         __syncthreads();
         flat_seg_c<U, ABL, 8>(payn4, v, qan, qbn, i0n, i1n, fstn, nfn, bl, accc, lane);
