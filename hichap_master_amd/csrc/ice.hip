@@ -647,29 +647,42 @@ __global__ __launch_bounds__(kSweepThreads, 4) void k_sweep_flat(TileDev T, cons
 // ---------------------------------------------------------------- K2
 // marg_r = b_r * (sum of the row's unit partials + wide entries + 2 diag b_r)
 // K1b: the dense diagonal band.  One block per (256-row block, 2048-slot
-// chunk): the chunk's bias window (rows + slots + 1 columns) is staged in LDS
-// with one double of padding per 16, so the 64 lanes of a wave -- each
-// reading 16 consecutive slots of a row from one uint4 -- hit distinct banks;
-// a row's 2048 slots are two fully coalesced uint4 loads per lane (two rows in
-// flight per wave), the counts convert in registers and FMA against LDS.
-// Fixed per-lane order + xor-tree wave reduction: deterministic.
+// chunk).  Row r is read in 16-slot groups shifted back by m = r & 15, so the
+// bias column of group l's slot k is (r - m) + s0 + 16 l + k - W: the window
+// index (r & ~15) + 16 l + k is 16-aligned per lane and the padded LDS
+// address (one double of padding per 16, conflict-free for the 64 lanes'
+// stride-17 reads) is p0 + k -- an immediate offset, no address arithmetic
+// per count.  A lane's 16 shifted counts are the last m bytes of the
+// previous uint4 and the first 16 - m of its own (two coalesced 16-B loads,
+// the second an L1 hit; one alignbyte per dword, the dword choice is
+// wave-uniform).  Two rows in flight per wave, counts converted in
+// registers, fixed per-lane order + xor-tree wave reduction: deterministic.
 constexpr int kBandThreads = 512;
-constexpr int kBandWin = kBandRows + kBandChunk + 1;
+constexpr int kBandWin = kBandRows + kBandChunk;
 __device__ __forceinline__ int bpad(int k) { return k + (k >> 4); }
 
-__device__ __forceinline__ double band_dot16(const uint4 v, const double* __restrict__ bl, int base, double acc) {
-    const unsigned x[4] = {v.x, v.y, v.z, v.w};
-    // bpad(base + k) = p0 + k before the window's next 16-boundary, p0 + k + 1
-    // after it: one select per element, the k offset folds into the LDS read
-    const uint32_t a0 = (uint32_t)bpad(base) * 8u, a1 = a0 + 8u;
-    const int split = 16 - (base & 15);
-    const char* lds = reinterpret_cast<const char*>(bl);
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        const unsigned c = (x[k >> 2] >> (8 * (k & 3))) & 0xffu;
-        const uint32_t a = (k < split ? a0 : a1) + 8u * k;
-        acc = fma((double)c, *reinterpret_cast<const double*>(lds + a), acc);
+// bytes [16 - m, 32 - m) of prev ++ own (m in [0, 16), wave-uniform; the
+// first byte is in dword q = (16 - m) / 4 in 0..4)
+__device__ __forceinline__ uint4 band_shift(const uint4 prev, const uint4 own, int m) {
+    const uint32_t d[8] = {prev.x, prev.y, prev.z, prev.w, own.x, own.y, own.z, own.w};
+    const int q = (16 - m) >> 2, r = (16 - m) & 3;
+    uint32_t o[5];
+    switch (q) {  // uniform branch
+        case 0: o[0] = d[0], o[1] = d[1], o[2] = d[2], o[3] = d[3], o[4] = d[4]; break;
+        case 1: o[0] = d[1], o[1] = d[2], o[2] = d[3], o[3] = d[4], o[4] = d[5]; break;
+        case 2: o[0] = d[2], o[1] = d[3], o[2] = d[4], o[3] = d[5], o[4] = d[6]; break;
+        case 3: o[0] = d[3], o[1] = d[4], o[2] = d[5], o[3] = d[6], o[4] = d[7]; break;
+        default: o[0] = d[4], o[1] = d[5], o[2] = d[6], o[3] = d[7], o[4] = 0u; break;  // q = 4 (m = 0)
     }
+    if (r == 0) return make_uint4(o[0], o[1], o[2], o[3]);
+    return make_uint4(__builtin_amdgcn_alignbyte(o[1], o[0], r), __builtin_amdgcn_alignbyte(o[2], o[1], r),
+                      __builtin_amdgcn_alignbyte(o[3], o[2], r), __builtin_amdgcn_alignbyte(o[4], o[3], r));
+}
+
+__device__ __forceinline__ double band_dot16(const uint4 v, const double* __restrict__ b0, double acc) {
+    const unsigned x[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 16; ++k) acc = fma((double)((x[k >> 2] >> (8 * (k & 3))) & 0xffu), b0[k], acc);
     return acc;
 }
 
@@ -683,11 +696,11 @@ __global__ __launch_bounds__(kBandThreads) void k_sweep_band(const uint8_t* __re
     __shared__ uint8_t ract[kBandRows];  // active flag per row (no dependent global loads in the row loop)
     const long long r0 = (long long)blockIdx.x * kBandRows;
     const int chunk = blockIdx.y;
-    const int s0 = chunk * kBandChunk, s1 = min(s0 + kBandChunk, 2 * W);
+    const int stride = (int)band_stride(W);
+    const int s0 = chunk * kBandChunk, s1 = min(s0 + kBandChunk, stride);
     const int nr = (int)min((long long)kBandRows, nloc - r0);
-    const int crosses = (s0 < W && s1 > W) ? 1 : 0;  // the chunk skips the main diagonal
-    const long long g0 = row_lo + r0 + band_diag(s0, W);
-    const int len = nr + (s1 - s0) + crosses;
+    const long long g0 = row_lo + r0 + s0 - W;  // bias column of window index 0
+    const int len = ((nr + 15) & ~15) + (s1 - s0);
     for (int k = threadIdx.x; k < len; k += kBandThreads) {
         // the band multiplies implicit zeros too: a NaN bias (an empty group
         // in cis-only mode, whose bins no stored pixel touches) must read 0
@@ -697,36 +710,42 @@ __global__ __launch_bounds__(kBandThreads) void k_sweep_band(const uint8_t* __re
     }
     for (int k = threadIdx.x; k < nr; k += kBandThreads) ract[k] = act[row_group[r0 + k]] != 0;
     __syncthreads();
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     constexpr int NW = kBandThreads / 64;
+    const uint4 zero = make_uint4(0u, 0u, 0u, 0u);
     for (int rr = wave; rr < nr; rr += 2 * NW) {
         const int rr2 = rr + NW;
-        const bool two = rr2 < nr;
-        const bool a1 = ract[rr] != 0, a2 = two && ract[rr2] != 0;
-        const uint8_t* row1 = band + (r0 + rr) * (long long)(2 * W);
-        const uint8_t* row2 = band + (r0 + rr2) * (long long)(2 * W);
-        double acc1 = 0.0, acc2 = 0.0;
-        for (int sb = s0 + lane * 16; sb < s1; sb += 64 * 16 * 2) {
-            const int sc = sb + 64 * 16;
-            const bool hc = sc < s1;
-            uint4 v1 = make_uint4(0, 0, 0, 0), v2 = v1, w1 = v1, w2 = v1;
-            if (a1) v1 = *reinterpret_cast<const uint4*>(row1 + sb);
-            if (a1 && hc) w1 = *reinterpret_cast<const uint4*>(row1 + sc);
-            if (a2) v2 = *reinterpret_cast<const uint4*>(row2 + sb);
-            if (a2 && hc) w2 = *reinterpret_cast<const uint4*>(row2 + sc);
-            const int adj = (sb >= W) ? crosses : 0, adjc = (sc >= W) ? crosses : 0;
-            acc1 = band_dot16(v1, bl, rr + (sb - s0) + adj, acc1);
-            acc2 = band_dot16(v2, bl, rr2 + (sb - s0) + adj, acc2);
-            if (hc) {
-                acc1 = band_dot16(w1, bl, rr + (sc - s0) + adjc, acc1);
-                acc2 = band_dot16(w2, bl, rr2 + (sc - s0) + adjc, acc2);
+        const bool a[2] = {ract[rr] != 0, rr2 < nr && ract[rr2] != 0};
+        const int rows[2] = {rr, rr2};
+        uint4 own[2][2], prev[2][2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const uint8_t* row = band + (r0 + rows[i]) * (long long)stride;
+#pragma unroll
+            for (int g = 0; g < 2; ++g) {
+                const int sb = s0 + 16 * (lane + 64 * g);
+                const bool on = a[i] && sb < s1, onp = on && sb >= 16;
+                const uint4 x = ld16(reinterpret_cast<const uint4*>(on ? row + sb : band));
+                const uint4 y = ld16(reinterpret_cast<const uint4*>(onp ? row + sb - 16 : band));
+                own[i][g] = on ? x : zero;
+                prev[i][g] = onp ? y : zero;
             }
         }
-        acc1 = wave_sum(acc1);
-        acc2 = wave_sum(acc2);
-        if (lane == 0) {
-            if (a1) bpart[(long long)chunk * nloc + r0 + rr] = acc1;
-            if (a2) bpart[(long long)chunk * nloc + r0 + rr2] = acc2;
+        double acc[2] = {0.0, 0.0};
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int m = rows[i] & 15, base = rows[i] & ~15;
+#pragma unroll
+            for (int g = 0; g < 2; ++g) {
+                const int l = lane + 64 * g;
+                if (s0 + 16 * l < s1)
+                    acc[i] = band_dot16(band_shift(prev[i][g], own[i][g], m), bl + bpad(base + 16 * l), acc[i]);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const double t = wave_sum(acc[i]);
+            if (lane == 0 && a[i]) bpart[(long long)chunk * nloc + r0 + rows[i]] = t;
         }
     }
 }
@@ -1108,7 +1127,7 @@ int hh_ice_create(hh_matrix* m, const hh_ice_opts* o, hh_ice** out) {
         S->marg.alloc(S->n);
         S->marg.zero(s);
         S->part.alloc(std::max<int64_t>(m->n_part, 1));
-        S->nch = m->band_w > 0 ? (int32_t)((2 * (int64_t)m->band_w + kBandChunk - 1) / kBandChunk) : 0;
+        S->nch = m->band_w > 0 ? (int32_t)((band_stride(m->band_w) + kBandChunk - 1) / kBandChunk) : 0;
         S->bpart.alloc(std::max<int64_t>((int64_t)S->nch * S->nloc, 1));
         HIP_CHECK(hipStreamCreateWithFlags(&S->side, hipStreamNonBlocking));
         HIP_CHECK(hipEventCreateWithFlags(&S->fork, hipEventDisableTiming));

@@ -38,8 +38,8 @@ constexpr int64_t kMaxBins = (int64_t)1 << 30;
 constexpr uint32_t kNarrowMax = 7;                        // counts stored as uint16
 
 // Dense diagonal band: the pixels with 1 <= |col - row| <= W
-// and count <= 255 are stored as uint8 counts with implicit columns, row r's
-// slots [0, 2W) = diagonals -W..-1, 1..W; W is a multiple of 16 chosen from
+// and count <= 255 are stored as uint8 counts with implicit columns (slots
+// below); W is a multiple of 16 chosen from
 // the data (the diagonals whose occupancy is >= kBandDensity), 0 = no band.
 // Everything else (farther, trans, larger counts) stays in the tiles.
 constexpr int kBandRows = 256;      // rows per band work block
@@ -48,8 +48,13 @@ constexpr int kBandMaxW = 16384;
 constexpr uint32_t kBandMaxCnt = 255u;
 constexpr double kBandDensity = 0.5;
 extern int64_t g_band_w;            // hh_tune("band_w"): -1 auto, 0 off, > 0 forced (multiple of 16)
-__host__ __device__ __forceinline__ int64_t band_slot(int64_t d, int64_t W) { return d < 0 ? d + W : d + W - 1; }
-__host__ __device__ __forceinline__ int64_t band_diag(int64_t s, int64_t W) { return s < W ? s - W : s - W + 1; }
+// row r's band slots: s = d + W for diagonals d in [-W, W] (slot W, the main
+// diagonal, stays 0), then zero padding: a row is band_stride(W) = 2W + 16
+// bytes (a multiple of 16; the padding lets the sweep read 16-slot groups
+// shifted by the row's alignment without a bounds case)
+__host__ __device__ __forceinline__ int64_t band_slot(int64_t d, int64_t W) { return d + W; }
+__host__ __device__ __forceinline__ int64_t band_diag(int64_t s, int64_t W) { return s - W; }
+__host__ __device__ __forceinline__ int64_t band_stride(int64_t W) { return W > 0 ? 2 * W + 16 : 0; }
 // W from the occupancy of diagonals 1..kBandMaxW (occ[d] / (n - d)): the
 // longest prefix of diagonals from ignore_diags on whose occupancy stays >=
 // kBandDensity, rounded down to a multiple of 16 (or the forced value).

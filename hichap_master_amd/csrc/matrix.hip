@@ -426,12 +426,12 @@ int hh_matrix_from_pixels(const int64_t* bin1, const int64_t* bin2, const double
         const int32_t nJ = (int32_t)((n_bins + kW - 1) / kW);
         std::vector<uint16_t> cntw((size_t)nloc * nJ, 0), cntn((size_t)nloc * nJ, 0);
         std::vector<long long> wptr(nloc + 1, 0);
-        std::vector<uint8_t> band((size_t)nloc * 2 * W, 0);
+        std::vector<uint8_t> band((size_t)nloc * band_stride(W), 0);
         int64_t n_band = 0;
         for (int64_t r = 0; r < nloc; ++r) {
             for (int64_t k = deg[r]; k < deg[r + 1]; ++k) {
                 if (in_band(row_lo + r, cols[k], vals[k])) {
-                    band[(size_t)r * 2 * W + band_slot(cols[k] - (row_lo + r), W)] = (uint8_t)vals[k];
+                    band[(size_t)r * band_stride(W) + band_slot(cols[k] - (row_lo + r), W)] = (uint8_t)vals[k];
                     ++n_band;
                     continue;
                 }
@@ -575,8 +575,8 @@ int hh_matrix_export_upper(const hh_matrix* m, int64_t* bin1, int64_t* bin2, dou
             m->band.download(band.data(), band.size(), 0);
             HIP_CHECK(hipDeviceSynchronize());
             for (int64_t r = 0; r < nloc; ++r)
-                for (int64_t sl = 0; sl < 2 * W; ++sl) {
-                    const uint8_t v = band[(size_t)r * 2 * W + sl];
+                for (int64_t sl = 0; sl < band_stride(W); ++sl) {
+                    const uint8_t v = band[(size_t)r * band_stride(W) + sl];
                     if (v) rows[r].emplace_back(m->row_lo + r + band_diag(sl, W), (double)v);
                 }
         }

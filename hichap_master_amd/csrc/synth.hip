@@ -149,7 +149,7 @@ __global__ __launch_bounds__(256) void k_synth_rows(SynthDev p, long long row_lo
         const long long dj = j - r;
         const bool inband = kc > 0 && p.band_w > 0 && kc <= kBandMaxCnt && dj >= -p.band_w && dj <= p.band_w;
         if (inband) {  // per-lane counters (the tile counters below are wave-uniform)
-            if (PASS == 1) o.band[w * 2 * p.band_w + band_slot(dj, p.band_w)] = (uint8_t)kc;
+            if (PASS == 1) o.band[w * band_stride(p.band_w) + band_slot(dj, p.band_w)] = (uint8_t)kc;
             nb_lane += 1;
             nbu_lane += dj > 0 ? 1 : 0;
             sum_lane += kc;
@@ -390,7 +390,7 @@ int hh_synth_build(const hh_synth_params* p, int64_t row_lo, int64_t row_hi, voi
         m->pay.alloc(P.n_entries_padded);
         m->payn.alloc(P.n_narrow_padded);
         m->band_w = h.dev.band_w;
-        m->band.alloc((size_t)nloc * 2 * m->band_w);
+        m->band.alloc((size_t)nloc * band_stride(m->band_w));
         m->band.zero(s);
         {
             SynthOut o{};

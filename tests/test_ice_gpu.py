@@ -180,7 +180,7 @@ def test_synthetic_generator_matches_oracle(ice):
     assert inf["n_entries"] == 2 * b1.size
     assert inf["n_slots"] + inf["n_slots_narrow"] + inf["n_band"] >= inf["n_entries"]
     assert inf["n_slots"] % 4 == 0 and inf["n_slots_narrow"] % 8 == 0
-    band_bytes = 2 * inf["band_w"] * (inf["row_hi"] - inf["row_lo"])
+    band_bytes = (2 * inf["band_w"] + 16 if inf["band_w"] else 0) * (inf["row_hi"] - inf["row_lo"])
     assert inf["payload_bytes"] == 4 * inf["n_slots"] + 2 * inf["n_slots_narrow"] + band_bytes
     assert inf["n_slots_narrow"] > 0  # low counts are stored as uint16
     # shards see the same matrix
