@@ -686,6 +686,7 @@ __device__ __forceinline__ double band_dot16(const uint4 v, const double* __rest
     return acc;
 }
 
+template <int ABL>
 __global__ __launch_bounds__(kBandThreads) void k_sweep_band(const uint8_t* __restrict__ band, int W, long long nloc,
                                                              long long row_lo, long long n_bins,
                                                              const uint8_t* __restrict__ act,
@@ -738,7 +739,9 @@ __global__ __launch_bounds__(kBandThreads) void k_sweep_band(const uint8_t* __re
 #pragma unroll
             for (int g = 0; g < 2; ++g) {
                 const int l = lane + 64 * g;
-                if (s0 + 16 * l < s1)
+                if (ABL == 1)  // timing ablation: stream only
+                    acc[i] += (double)(own[i][g].x + own[i][g].y + own[i][g].z + own[i][g].w + prev[i][g].x);
+                else if (s0 + 16 * l < s1)
                     acc[i] = band_dot16(band_shift(prev[i][g], own[i][g], m), bl + bpad(base + 16 * l), acc[i]);
             }
         }
@@ -993,7 +996,8 @@ static void sweep_band(hh_ice* S, hipStream_t s) {
     const hh_matrix* m = S->m;
     if (!S->nch || !S->nloc) return;
     const dim3 g((unsigned)((S->nloc + kBandRows - 1) / kBandRows), (unsigned)S->nch);
-    hipLaunchKernelGGL(k_sweep_band, g, dim3(kBandThreads), 0, s, m->band.p, (int)m->band_w, (long long)S->nloc,
+    auto kern = g_sweep_ablate == 1 ? k_sweep_band<1> : k_sweep_band<0>;  // 1: timing ablation (stream only)
+    hipLaunchKernelGGL(kern, g, dim3(kBandThreads), 0, s, m->band.p, (int)m->band_w, (long long)S->nloc,
                        (long long)m->row_lo, (long long)m->n_bins, S->act(), m->row_group.p, S->bias.p, S->bpart.p);
     HIP_CHECK(hipGetLastError());
 }
