@@ -29,7 +29,8 @@ class MatrixInfo(C.Structure):
         "n_bins", "row_lo", "row_hi", "nnz_upper", "n_entries", "n_slots", "n_tiles",
         "n_units", "n_wide", "device_bytes", "n_slots_narrow", "payload_bytes")] + [
         (n, C.c_int32) for n in ("n_chroms", "ignore_diags", "cis_only", "device", "band_w", "n_units_flat")] + [
-        ("n_band", C.c_int64), ("payload_bytes_flat", C.c_int64)]
+        ("n_band", C.c_int64), ("payload_bytes_flat", C.c_int64)] + [
+        (n, C.c_int32) for n in ("band_w4", "pad2_")]
 
 
 class SynthParams(C.Structure):

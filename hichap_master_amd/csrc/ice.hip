@@ -646,26 +646,36 @@ __global__ __launch_bounds__(kSweepThreads, 4) void k_sweep_flat(TileDev T, cons
 
 // ---------------------------------------------------------------- K2
 // marg_r = b_r * (sum of the row's unit partials + wide entries + 2 diag b_r)
-// K1b: the dense diagonal band.  One block per (256-row block, 2048-slot
-// chunk).  Row r is read in 16-slot groups shifted back by m = r & 15, so the
-// bias column of group l's slot k is (r - m) + s0 + 16 l + k - W: the window
-// index (r & ~15) + 16 l + k is 16-aligned per lane and the padded LDS
-// address (one double of padding per 16, conflict-free for the 64 lanes'
-// stride-17 reads) is p0 + k -- an immediate offset, no address arithmetic
-// per count.  A lane's 16 shifted counts are the last m bytes of the
-// previous uint4 and the first 16 - m of its own (two coalesced 16-B loads,
-// the second an L1 hit; one alignbyte per dword, the dword choice is
-// wave-uniform).  Two rows in flight per wave, counts converted in
-// registers, fixed per-lane order + xor-tree wave reduction: deterministic.
+// K1b: the dense diagonal bands (uint8 counts near the diagonal, 4-bit
+// counts beyond).  A band segment is a per-row run of slots s = 0, 1, ... for
+// the diagonals d = dlo + s (zero padding at the end).  One block per
+// (256-row block, 2048-byte chunk of the segment).  Row r is read in 16-byte
+// groups (G = 128 / BITS slots) shifted back by m = r mod G, so the bias
+// column of group l's slot k is (r - m) + dlo + s0 + G l + k: the window
+// index (r & ~(G-1)) + G l + k is G-aligned per lane and the padded LDS
+// address (one double of padding per G, conflict-free for the 64 lanes'
+// stride-(G+1) reads) is p0 + k -- an immediate offset, no address
+// arithmetic per count.  A lane's G shifted counts come from the previous
+// and its own 16 bytes (two coalesced loads, the second an L1 hit; one
+// alignbit per dword, the dword choice is wave-uniform).  Two rows in flight
+// per wave, fixed per-lane order + xor-tree wave reduction: deterministic.
 constexpr int kBandThreads = 512;
-constexpr int kBandWin = kBandRows + kBandChunk;
-__device__ __forceinline__ int bpad(int k) { return k + (k >> 4); }
+constexpr int kBandChunkB = kBandChunk;  // bytes of a segment per block
+template <int BITS>
+struct BandGeo {
+    static constexpr int G = 128 / BITS;                 // slots per 16-byte group
+    static constexpr int CS = kBandChunkB * 8 / BITS;    // slots per chunk
+    static constexpr int WIN = kBandRows + CS;           // window values
+    static constexpr int LDS = WIN + WIN / G + 1;
+};
+template <int G>
+__device__ __forceinline__ int bpadg(int k) { return k + k / G; }
 
-// bytes [16 - m, 32 - m) of prev ++ own (m in [0, 16), wave-uniform; the
-// first byte is in dword q = (16 - m) / 4 in 0..4)
+// bits [128 - BITS m, 256 - BITS m) of prev ++ own (m < G, wave-uniform)
+template <int BITS>
 __device__ __forceinline__ uint4 band_shift(const uint4 prev, const uint4 own, int m) {
     const uint32_t d[8] = {prev.x, prev.y, prev.z, prev.w, own.x, own.y, own.z, own.w};
-    const int q = (16 - m) >> 2, r = (16 - m) & 3;
+    const int B = 128 - BITS * m, q = B >> 5, r = B & 31;
     uint32_t o[5];
     switch (q) {  // uniform branch
         case 0: o[0] = d[0], o[1] = d[1], o[2] = d[2], o[3] = d[3], o[4] = d[4]; break;
@@ -675,80 +685,99 @@ __device__ __forceinline__ uint4 band_shift(const uint4 prev, const uint4 own, i
         default: o[0] = d[4], o[1] = d[5], o[2] = d[6], o[3] = d[7], o[4] = 0u; break;  // q = 4 (m = 0)
     }
     if (r == 0) return make_uint4(o[0], o[1], o[2], o[3]);
-    return make_uint4(__builtin_amdgcn_alignbyte(o[1], o[0], r), __builtin_amdgcn_alignbyte(o[2], o[1], r),
-                      __builtin_amdgcn_alignbyte(o[3], o[2], r), __builtin_amdgcn_alignbyte(o[4], o[3], r));
+    return make_uint4(__builtin_amdgcn_alignbit(o[1], o[0], r), __builtin_amdgcn_alignbit(o[2], o[1], r),
+                      __builtin_amdgcn_alignbit(o[3], o[2], r), __builtin_amdgcn_alignbit(o[4], o[3], r));
 }
 
-__device__ __forceinline__ double band_dot16(const uint4 v, const double* __restrict__ b0, double acc) {
+template <int BITS>
+__device__ __forceinline__ double band_dot(const uint4 v, const double* __restrict__ b0, double acc) {
     const unsigned x[4] = {v.x, v.y, v.z, v.w};
+    constexpr int G = 128 / BITS, PER = 32 / BITS;
+    constexpr unsigned MASK = (1u << BITS) - 1u;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) acc = fma((double)((x[k >> 2] >> (8 * (k & 3))) & 0xffu), b0[k], acc);
+    for (int k = 0; k < G; ++k) acc = fma((double)((x[k / PER] >> (BITS * (k % PER))) & MASK), b0[k], acc);
     return acc;
 }
 
-template <int ABL>
-__global__ __launch_bounds__(kBandThreads) void k_sweep_band(const uint8_t* __restrict__ band, int W, long long nloc,
+template <int BITS, int ABL>
+__global__ __launch_bounds__(kBandThreads) void k_sweep_band(const uint8_t* __restrict__ seg, long long row_stride,
+                                                             int seg_bytes, long long dlo, long long nloc,
                                                              long long row_lo, long long n_bins,
                                                              const uint8_t* __restrict__ act,
                                                              const uint16_t* __restrict__ row_group,
                                                              const double* __restrict__ b,
                                                              double* __restrict__ bpart) {
-    __shared__ double bl[kBandWin + kBandWin / 16 + 1];
+    using Geo = BandGeo<BITS>;
+    constexpr int G = Geo::G;
+    __shared__ double bl[Geo::LDS];
     __shared__ uint8_t ract[kBandRows];  // active flag per row (no dependent global loads in the row loop)
     const long long r0 = (long long)blockIdx.x * kBandRows;
     const int chunk = blockIdx.y;
-    const int stride = (int)band_stride(W);
-    const int s0 = chunk * kBandChunk, s1 = min(s0 + kBandChunk, stride);
+    const int c0 = chunk * kBandChunkB, c1 = min(c0 + kBandChunkB, seg_bytes);  // bytes
+    const int s0 = c0 * 8 / BITS, s1 = c1 * 8 / BITS;                              // slots
     const int nr = (int)min((long long)kBandRows, nloc - r0);
-    const long long g0 = row_lo + r0 + s0 - W;  // bias column of window index 0
-    const int len = ((nr + 15) & ~15) + (s1 - s0);
+    const long long g0 = row_lo + r0 + dlo + s0;  // bias column of window index 0
+    const int len = ((nr + G - 1) & ~(G - 1)) + (s1 - s0);
     for (int k = threadIdx.x; k < len; k += kBandThreads) {
         // the band multiplies implicit zeros too: a NaN bias (an empty group
         // in cis-only mode, whose bins no stored pixel touches) must read 0
         const long long c = g0 + k;
         const double v = (c >= 0 && c < n_bins) ? b[c] : 0.0;
-        bl[bpad(k)] = v == v ? v : 0.0;
+        bl[bpadg<G>(k)] = v == v ? v : 0.0;
     }
     for (int k = threadIdx.x; k < nr; k += kBandThreads) ract[k] = act[row_group[r0 + k]] != 0;
     __syncthreads();
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     constexpr int NW = kBandThreads / 64;
+    constexpr int RJ = 2;       // rows of a G-aligned row group handled together: they share the window
+    constexpr int RPG = G / NW; // rows of a G-group per wave
+    static_assert(G % NW == 0 && RPG % RJ == 0, "whole rows per wave and group");
     const uint4 zero = make_uint4(0u, 0u, 0u, 0u);
-    for (int rr = wave; rr < nr; rr += 2 * NW) {
-        const int rr2 = rr + NW;
-        const bool a[2] = {ract[rr] != 0, rr2 < nr && ract[rr2] != 0};
-        const int rows[2] = {rr, rr2};
-        uint4 own[2][2], prev[2][2];
+    for (int gh = 0; gh < (nr + G - 1) / G * (RPG / RJ); ++gh) {
+        // rows gb + wave + NW (j0 + j) (shift m = wave + NW (j0 + j), uniform):
+        // the window values of a lane's slot group are read from LDS once for
+        // the RJ rows
+        const int gb = (gh / (RPG / RJ)) * G, j0 = (gh % (RPG / RJ)) * RJ;
+        bool a[RJ];
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const uint8_t* row = band + (r0 + rows[i]) * (long long)stride;
+        for (int j = 0; j < RJ; ++j) {
+            const int r = gb + wave + NW * (j0 + j);
+            a[j] = r < nr && ract[r] != 0;
+        }
+        double acc[RJ];
 #pragma unroll
-            for (int g = 0; g < 2; ++g) {
-                const int sb = s0 + 16 * (lane + 64 * g);
-                const bool on = a[i] && sb < s1, onp = on && sb >= 16;
-                const uint4 x = ld16(reinterpret_cast<const uint4*>(on ? row + sb : band));
-                const uint4 y = ld16(reinterpret_cast<const uint4*>(onp ? row + sb - 16 : band));
-                own[i][g] = on ? x : zero;
-                prev[i][g] = onp ? y : zero;
+        for (int j = 0; j < RJ; ++j) acc[j] = 0.0;
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+            const int l = lane + 64 * g;
+            const int cb = c0 + 16 * l;
+            uint4 own[RJ], prev[RJ];
+#pragma unroll
+            for (int j = 0; j < RJ; ++j) {
+                const uint8_t* row = seg + (r0 + gb + wave + NW * (j0 + j)) * row_stride;
+                const bool on = a[j] && cb < c1, onp = on && cb >= 16;
+                const uint4 x = ld16(reinterpret_cast<const uint4*>(on ? row + cb : seg));
+                const uint4 y = ld16(reinterpret_cast<const uint4*>(onp ? row + cb - 16 : seg));
+                own[j] = on ? x : zero;
+                prev[j] = onp ? y : zero;
+            }
+            if (ABL == 1) {  // timing ablation: stream only
+#pragma unroll
+                for (int j = 0; j < RJ; ++j) acc[j] += (double)(own[j].x + own[j].y + own[j].z + own[j].w + prev[j].x);
+            } else if (cb < c1) {
+                double w[G];
+                const double* b0 = bl + bpadg<G>(gb + G * l);
+#pragma unroll
+                for (int k = 0; k < G; ++k) w[k] = b0[k];
+#pragma unroll
+                for (int j = 0; j < RJ; ++j)
+                    acc[j] = band_dot<BITS>(band_shift<BITS>(prev[j], own[j], wave + NW * (j0 + j)), w, acc[j]);
             }
         }
-        double acc[2] = {0.0, 0.0};
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int m = rows[i] & 15, base = rows[i] & ~15;
-#pragma unroll
-            for (int g = 0; g < 2; ++g) {
-                const int l = lane + 64 * g;
-                if (ABL == 1)  // timing ablation: stream only
-                    acc[i] += (double)(own[i][g].x + own[i][g].y + own[i][g].z + own[i][g].w + prev[i][g].x);
-                else if (s0 + 16 * l < s1)
-                    acc[i] = band_dot16(band_shift(prev[i][g], own[i][g], m), bl + bpad(base + 16 * l), acc[i]);
-            }
-        }
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const double t = wave_sum(acc[i]);
-            if (lane == 0 && a[i]) bpart[(long long)chunk * nloc + r0 + rows[i]] = t;
+        for (int j = 0; j < RJ; ++j) {
+            const double t = wave_sum(acc[j]);
+            if (lane == 0 && a[j]) bpart[(long long)chunk * nloc + r0 + gb + wave + NW * (j0 + j)] = t;
         }
     }
 }
@@ -995,11 +1024,24 @@ static void sweep(const hh_matrix* m, const uint8_t* act, const double* b, doubl
 static void sweep_band(hh_ice* S, hipStream_t s) {
     const hh_matrix* m = S->m;
     if (!S->nch || !S->nloc) return;
-    const dim3 g((unsigned)((S->nloc + kBandRows - 1) / kBandRows), (unsigned)S->nch);
-    auto kern = g_sweep_ablate == 1 ? k_sweep_band<1> : k_sweep_band<0>;  // 1: timing ablation (stream only)
-    hipLaunchKernelGGL(kern, g, dim3(kBandThreads), 0, s, m->band.p, (int)m->band_w, (long long)S->nloc,
-                       (long long)m->row_lo, (long long)m->n_bins, S->act(), m->row_group.p, S->bias.p, S->bpart.p);
-    HIP_CHECK(hipGetLastError());
+    const unsigned rb = (unsigned)((S->nloc + kBandRows - 1) / kBandRows);
+    const long long W8 = m->band_w, W4 = m->band_w4;
+    int ch = 0;  // first bpart chunk of the segment
+    auto launch = [&](auto kern, const uint8_t* seg, long long stride, long long bytes, long long dlo) {
+        const int nc = (int)((bytes + kBandChunkB - 1) / kBandChunkB);
+        hipLaunchKernelGGL(kern, dim3(rb, (unsigned)nc), dim3(kBandThreads), 0, s, seg, stride, (int)bytes, dlo,
+                           (long long)S->nloc, (long long)m->row_lo, (long long)m->n_bins, S->act(), m->row_group.p,
+                           S->bias.p, S->bpart.p + (long long)ch * S->nloc);
+        HIP_CHECK(hipGetLastError());
+        ch += nc;
+    };
+    const bool abl = g_sweep_ablate == 1;  // timing ablation (stream only)
+    if (W8 > 0) launch(abl ? k_sweep_band<8, 1> : k_sweep_band<8, 0>, m->band.p, band_stride(W8), band_stride(W8), -W8);
+    if (W4 > W8) {
+        const long long st = band4_stride(W8, W4), sg = band4_seg(W8, W4);
+        launch(abl ? k_sweep_band<4, 1> : k_sweep_band<4, 0>, m->band4.p, st, sg, -W4);
+        launch(abl ? k_sweep_band<4, 1> : k_sweep_band<4, 0>, m->band4.p + sg, st, sg, W8 + 1);
+    }
 }
 
 static void marg_weighted(hh_ice* S, double* out, hipStream_t s, bool timed, int slot) {
@@ -1065,6 +1107,9 @@ int hh_tune(const char* key, int64_t value) {
         } else if (k == "sweep_ablate") {
             HH_REQUIRE(value >= 0 && value <= 2, "sweep_ablate must be 0, 1 or 2");
             g_sweep_ablate = (int)value;
+        } else if (k == "band4") {
+            HH_REQUIRE(value == 0 || value == 1, "band4 in {0, 1}");
+            g_band4 = value;
         } else if (k == "flat_max") {
             HH_REQUIRE(value >= 0 && value <= 255, "flat_max in [0, 255]");
             g_flat_max = value;
@@ -1132,6 +1177,8 @@ int hh_ice_create(hh_matrix* m, const hh_ice_opts* o, hh_ice** out) {
         S->marg.zero(s);
         S->part.alloc(std::max<int64_t>(m->n_part, 1));
         S->nch = m->band_w > 0 ? (int32_t)((band_stride(m->band_w) + kBandChunk - 1) / kBandChunk) : 0;
+        if (m->band_w4 > m->band_w)
+            S->nch += 2 * (int32_t)((band4_seg(m->band_w, m->band_w4) + kBandChunk - 1) / kBandChunk);
         S->bpart.alloc(std::max<int64_t>((int64_t)S->nch * S->nloc, 1));
         HIP_CHECK(hipStreamCreateWithFlags(&S->side, hipStreamNonBlocking));
         HIP_CHECK(hipEventCreateWithFlags(&S->fork, hipEventDisableTiming));

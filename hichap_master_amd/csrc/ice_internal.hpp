@@ -48,6 +48,33 @@ constexpr int kBandMaxW = 16384;
 constexpr uint32_t kBandMaxCnt = 255u;
 constexpr double kBandDensity = 0.5;
 extern int64_t g_band_w;            // hh_tune("band_w"): -1 auto, 0 off, > 0 forced (multiple of 16)
+// Nibble band: beyond the uint8 band, the diagonals
+// W8 < |d| <= W4 whose counts are <= 15 are stored as 4-bit counts with
+// implicit columns, in two segments per row (negative, positive diagonals),
+// each K = W4 - W8 slots (a multiple of 32) + 32 slots of zero padding.
+// W8 shrinks to where counts > 15 become rare (< kBand8Big of a diagonal's
+// pixels), W4 reaches the occupancy break-even of 4-bit slots vs 2-byte tile
+// entries (kBand4Density).  Larger counts there stay in the tiles.
+constexpr uint32_t kBand4MaxCnt = 15u;
+constexpr double kBand4Density = 0.25;
+constexpr double kBand8Big = 0.05;
+extern int64_t g_band4;             // hh_tune("band4"): 1 nibble band on (default), 0 off
+struct BandWidths {
+    int32_t w8 = 0, w4 = 0;         // uint8 band |d| <= w8; nibble band w8 < |d| <= w4 (w4 == w8: none)
+};
+// occ[d] = occupancy of diagonal d, big[d] = share of its pixels with count > 15
+BandWidths choose_band_widths(const std::vector<double>& occ, const std::vector<double>& big, int ignore_diags);
+__host__ __device__ __forceinline__ int64_t band4_seg(int64_t w8, int64_t w4) { return w4 > w8 ? (w4 - w8) / 2 + 16 : 0; }
+__host__ __device__ __forceinline__ int64_t band4_stride(int64_t w8, int64_t w4) { return 2 * band4_seg(w8, w4); }
+// nibble index of diagonal d (w8 < |d| <= w4) within a row's band4 bytes:
+// segment 0 (d < 0) slot d + w4, segment 1 (d > 0) slot d - w8 - 1
+__host__ __device__ __forceinline__ int64_t band4_nibble(int64_t d, int64_t w8, int64_t w4) {
+    return d < 0 ? d + w4 : 2 * band4_seg(w8, w4) + (d - w8 - 1);
+}
+__host__ __device__ __forceinline__ bool in_band4(int64_t d, uint32_t v, int64_t w8, int64_t w4) {
+    const int64_t a = d < 0 ? -d : d;
+    return v > 0 && v <= kBand4MaxCnt && a > w8 && a <= w4;
+}
 // row r's band slots: s = d + W for diagonals d in [-W, W] (slot W, the main
 // diagonal, stays 0), then zero padding: a row is band_stride(W) = 2W + 16
 // bytes (a multiple of 16; the padding lets the sweep read 16-slot groups
@@ -179,9 +206,11 @@ struct hh_matrix {
     int64_t payload_bytes_flat = 0;
     int64_t n_slots = 0;          // padded wide (uint32) entries in tiles
     int64_t n_slots_narrow = 0;   // padded narrow (uint16) entries in tiles
-    int32_t band_w = 0;           // dense band half-width (0 = no band)
-    int64_t n_band = 0;           // nonzero entries held by the band
-    hh::DBuf<uint8_t> band;       // local rows x 2 * band_w
+    int32_t band_w = 0;           // uint8 band half-width W8 (0 = no band)
+    int32_t band_w4 = 0;          // nibble band outer width W4 (== band_w: none)
+    int64_t n_band = 0;           // nonzero entries held by the bands
+    hh::DBuf<uint8_t> band;       // local rows x band_stride(W8)
+    hh::DBuf<uint8_t> band4;      // local rows x band4_stride(W8, W4)
     hh::DBuf<uint32_t> pay;
     hh::DBuf<uint16_t> payn;
     hh::DBuf<int32_t> tile_J, tile_rb;
@@ -206,7 +235,7 @@ struct hh_matrix {
                tile_rb.bytes() + tile_ent.bytes() + tile_rp.bytes() +
                u_tlo.bytes() * 7 + blk_unit_ptr.bytes() + tile_perm.bytes() + tile_band.bytes() + u_whole.bytes() + tile_fw.bytes() + tile_frec.bytes() + frec.bytes() + blk_tile_ptr.bytes() + u_glo.bytes() * 2 +
                wide_ptr.bytes() + wide_col.bytes() + wide_cnt.bytes() + diag.bytes() + row_nnz2.bytes() +
-               row_sum2.bytes() + row_group.bytes() + band.bytes();
+               row_sum2.bytes() + row_group.bytes() + band.bytes() + band4.bytes();
     }
     hh::TileDev dev() const {
         return hh::TileDev{pay.p, payn.p, tile_J.p, tile_ent.p, tile_rp.p, tile_entn.p, tile_rpn.p, u_tlo.p,

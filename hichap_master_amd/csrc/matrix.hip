@@ -14,12 +14,35 @@ int64_t g_unit_entries = 0;  // 0 = auto (plan_tiles)
 int64_t g_band_w = -1;       // -1 = auto (choose_band_w)
 int64_t g_flat_max = 64;     // longest row (uint4) of a flat tile segment; 0 = no flat segments
 
+int64_t g_band4 = 1;         // nibble band on
+
 int32_t choose_band_w(const std::vector<double>& occ, int ignore_diags) {
     if (g_band_w >= 0) return (int32_t)std::min<int64_t>(g_band_w, kBandMaxW) & ~15;
     int64_t d = std::max(1, ignore_diags);
     if (d > 1) return 0;  // diagonal 1 dropped: no dense neighbourhood to exploit
     while (d < (int64_t)occ.size() && occ[d] >= kBandDensity) ++d;
     return (int32_t)((d - 1) & ~15LL);
+}
+
+BandWidths choose_band_widths(const std::vector<double>& occ, const std::vector<double>& big, int ignore_diags) {
+    BandWidths bw;
+    bw.w8 = bw.w4 = choose_band_w(occ, ignore_diags);
+    if (g_band_w >= 0 || !g_band4 || std::max(1, ignore_diags) > 1) return bw;
+    // outer edge: occupancy >= kBand4Density from diagonal 1 on
+    int64_t d4 = 1;
+    while (d4 < (int64_t)occ.size() && occ[d4] >= kBand4Density) ++d4;
+    --d4;
+    // inner edge: past the last diagonal where counts > 15 are common
+    int64_t d8 = 0;
+    for (int64_t d = 1; d <= d4 && d < (int64_t)big.size(); ++d)
+        if (big[d] >= kBand8Big) d8 = d;
+    int64_t w8 = (d8 + 15) & ~15LL;
+    if (w8 > bw.w8) w8 = bw.w8;  // no uint8 slots below their own break-even
+    const int64_t k = (d4 - w8) & ~31LL;
+    if (k < 32) return bw;       // no nibble band: the uint8 band as before
+    bw.w8 = (int32_t)w8;
+    bw.w4 = (int32_t)(w8 + k);
+    return bw;
 }
 void set_error(const std::string& msg) { g_last_error = msg; }
 
@@ -383,22 +406,29 @@ int hh_matrix_from_pixels(const int64_t* bin1, const int64_t* bin2, const double
         // dense band width from the diagonals' occupancy over the WHOLE matrix
         // (identical for every shard: the band decomposition fixes the
         // summation order, so it must not depend on the row range)
-        int32_t W = 0;
+        int32_t W = 0, W4 = 0;
         {
-            std::vector<double> occ(kBandMaxW + 2, 0.0);
+            std::vector<double> occ(kBandMaxW + 2, 0.0), big(kBandMaxW + 2, 0.0);
             for (int64_t i = 0; i < nnz; ++i) {
                 int64_t a, b;
                 uint32_t c;
                 if (!keep(i, a, b, c) || a == b || b - a > kBandMaxW + 1) continue;
                 occ[b - a] += 1.0;
+                if (c > kBand4MaxCnt) big[b - a] += 1.0;
             }
-            for (int64_t d = 1; d < (int64_t)occ.size(); ++d) occ[d] = d < n_bins ? occ[d] / (double)(n_bins - d) : 0.0;
-            W = choose_band_w(occ, ignore_diags);
+            for (int64_t d = 1; d < (int64_t)occ.size(); ++d) {
+                big[d] = occ[d] > 0 ? big[d] / occ[d] : 0.0;
+                occ[d] = d < n_bins ? occ[d] / (double)(n_bins - d) : 0.0;
+            }
+            const BandWidths bw = choose_band_widths(occ, big, ignore_diags);
+            W = bw.w8;
+            W4 = bw.w4;
         }
         auto in_band = [&](int64_t r_glob, int64_t col, uint32_t v) {
             const int64_t d = col - r_glob;
             return W > 0 && v <= kBandMaxCnt && d != 0 && d >= -W && d <= W;
         };
+        auto in_nib = [&](int64_t r_glob, int64_t col, uint32_t v) { return in_band4(col - r_glob, v, W, W4); };
         // pass 2: symmetric CSR rows
         std::vector<int32_t> cols(deg[nloc]);
         std::vector<uint32_t> vals(deg[nloc]);
@@ -427,11 +457,18 @@ int hh_matrix_from_pixels(const int64_t* bin1, const int64_t* bin2, const double
         std::vector<uint16_t> cntw((size_t)nloc * nJ, 0), cntn((size_t)nloc * nJ, 0);
         std::vector<long long> wptr(nloc + 1, 0);
         std::vector<uint8_t> band((size_t)nloc * band_stride(W), 0);
+        std::vector<uint8_t> band4((size_t)nloc * band4_stride(W, W4), 0);
         int64_t n_band = 0;
         for (int64_t r = 0; r < nloc; ++r) {
             for (int64_t k = deg[r]; k < deg[r + 1]; ++k) {
                 if (in_band(row_lo + r, cols[k], vals[k])) {
                     band[(size_t)r * band_stride(W) + band_slot(cols[k] - (row_lo + r), W)] = (uint8_t)vals[k];
+                    ++n_band;
+                    continue;
+                }
+                if (in_nib(row_lo + r, cols[k], vals[k])) {
+                    const int64_t nib = band4_nibble(cols[k] - (row_lo + r), W, W4);
+                    band4[(size_t)r * band4_stride(W, W4) + (nib >> 1)] |= (uint8_t)(vals[k] << (4 * (nib & 1)));
                     ++n_band;
                     continue;
                 }
@@ -455,7 +492,7 @@ int hh_matrix_from_pixels(const int64_t* bin1, const int64_t* bin2, const double
             int64_t pos = 0, posn = 0;
             int64_t wp = wptr[r];
             for (int64_t q = deg[r]; q < deg[r + 1]; ++q) {
-                if (in_band(row_lo + r, cols[q], vals[q])) continue;
+                if (in_band(row_lo + r, cols[q], vals[q]) || in_nib(row_lo + r, cols[q], vals[q])) continue;
                 if (vals[q] > kCntMax) { wcol[wp] = cols[q]; wcnt[wp++] = vals[q]; continue; }
                 const int32_t J = cols[q] >> kWBits;
                 if (J != curJ) {
@@ -480,8 +517,10 @@ int hh_matrix_from_pixels(const int64_t* bin1, const int64_t* bin2, const double
         m->row_sum2 = to_device(rsum, s);
         m->row_group = to_device(rgroup, s);
         m->band_w = W;
+        m->band_w4 = W4;
         m->n_band = n_band;
         m->band = to_device(band, s);
+        m->band4 = to_device(band4, s);
         m->nnz_upper = nnz_upper;
         m->n_entries = deg[nloc];
         HIP_CHECK(hipStreamSynchronize(s));  // host vectors die here
@@ -510,7 +549,9 @@ int hh_matrix_get_info(const hh_matrix* m, hh_matrix_info* info) {
         info->n_wide = m->n_wide;
         info->device_bytes = (int64_t)m->device_bytes();
         info->n_slots_narrow = m->n_slots_narrow;
-        info->payload_bytes = 4 * m->n_slots + 2 * m->n_slots_narrow + (int64_t)m->band.n;
+        info->payload_bytes = 4 * m->n_slots + 2 * m->n_slots_narrow + (int64_t)m->band.n + (int64_t)m->band4.n;
+        info->band_w4 = m->band_w4;
+        info->pad2_ = 0;
         info->band_w = m->band_w;
         info->n_units_flat = (int32_t)m->n_units_flat;
         info->n_band = m->n_band;
@@ -578,6 +619,19 @@ int hh_matrix_export_upper(const hh_matrix* m, int64_t* bin1, int64_t* bin2, dou
                 for (int64_t sl = 0; sl < band_stride(W); ++sl) {
                     const uint8_t v = band[(size_t)r * band_stride(W) + sl];
                     if (v) rows[r].emplace_back(m->row_lo + r + band_diag(sl, W), (double)v);
+                }
+        }
+        if (m->band_w4 > m->band_w) {
+            const int64_t W8 = m->band_w, W4 = m->band_w4, st = band4_stride(W8, W4);
+            std::vector<uint8_t> b4(m->band4.n);
+            m->band4.download(b4.data(), b4.size(), 0);
+            HIP_CHECK(hipDeviceSynchronize());
+            for (int64_t r = 0; r < nloc; ++r)
+                for (int64_t d = -W4; d <= W4; ++d) {
+                    if (d >= -W8 && d <= W8) continue;
+                    const int64_t nib = band4_nibble(d, W8, W4);
+                    const uint32_t v = (b4[(size_t)r * st + (nib >> 1)] >> (4 * (nib & 1))) & 15u;
+                    if (v) rows[r].emplace_back(m->row_lo + r + d, (double)v);
                 }
         }
         int64_t cnt = 0;

@@ -33,7 +33,8 @@ struct SynthDev {
     float A, decay, comp, trans;
     int ignore_diags, cis_only;
     unsigned long long seed;
-    int band_w;            // dense band half-width (0 = none)
+    int band_w;            // uint8 band half-width W8 (0 = none)
+    int band_w4;           // nibble band outer width W4 (== band_w: none)
 };
 
 __global__ void k_synth_bins(SynthDev p, float vis_sigma, float gap_frac, int comp_block,
@@ -106,7 +107,8 @@ struct SynthOut {
     const uint32_t* tile_rpn;
     uint32_t* pay;
     uint16_t* payn;
-    uint8_t* band;         // PASS 1: local rows x 2 * band_w
+    uint8_t* band;         // PASS 1: local rows x band_stride(W8)
+    uint32_t* band4;       // PASS 1: local rows x band4_stride(W8, W4) bytes (zeroed; nibbles OR-ed in)
     int32_t* row_band;     // PASS 0: band entries per row
 };
 
@@ -148,8 +150,16 @@ __global__ __launch_bounds__(256) void k_synth_rows(SynthDev p, long long row_lo
         // dense band: |j - r| <= W and count <= 255 (implicit column)
         const long long dj = j - r;
         const bool inband = kc > 0 && p.band_w > 0 && kc <= kBandMaxCnt && dj >= -p.band_w && dj <= p.band_w;
-        if (inband) {  // per-lane counters (the tile counters below are wave-uniform)
-            if (PASS == 1) o.band[w * band_stride(p.band_w) + band_slot(dj, p.band_w)] = (uint8_t)kc;
+        const bool innib = !inband && in_band4(dj, kc, p.band_w, p.band_w4);
+        if (inband || innib) {  // per-lane counters (the tile counters below are wave-uniform)
+            if (PASS == 1) {
+                if (inband) {
+                    o.band[w * band_stride(p.band_w) + band_slot(dj, p.band_w)] = (uint8_t)kc;
+                } else {  // adjacent lanes share bytes: OR the nibble into the zeroed word
+                    const long long nib = w * 2 * band4_stride(p.band_w, p.band_w4) + band4_nibble(dj, p.band_w, p.band_w4);
+                    atomicOr(o.band4 + (nib >> 3), kc << (4 * (nib & 7)));
+                }
+            }
             nb_lane += 1;
             nbu_lane += dj > 0 ? 1 : 0;
             sum_lane += kc;
@@ -188,7 +198,7 @@ __global__ __launch_bounds__(256) void k_synth_rows(SynthDev p, long long row_lo
     const long long nband = wave_sum_ll(nb_lane);
     nnz += nband;
     upper += wave_sum_ll(nbu_lane);
-    work += (long long)p.band_w / 2;  // 2W bytes per row, in 4-byte words
+    work += ((long long)p.band_w + band4_stride(p.band_w, p.band_w4) / 2) / 2;  // band bytes per row, in 4-byte words
     const uint32_t dg = p.ignore_diags == 0 ? synth_count(p, r, r) : 0u;
     if (lane == 0) {
         if (o.row_band) o.row_band[w] = (int32_t)nband;
@@ -216,7 +226,7 @@ struct SynthHost {
     std::vector<int64_t> offsets;
 };
 
-int32_t synth_band_w(const hh_synth_params* p, const std::vector<int64_t>& offsets);
+BandWidths synth_band_w(const hh_synth_params* p, const std::vector<int64_t>& offsets);
 
 void synth_setup(const hh_synth_params* p, SynthHost& h, hipStream_t s) {
     HH_REQUIRE(p && p->chrom_nbins && p->n_chroms > 0 && p->n_chroms < 32767, "bad synth params");
@@ -251,7 +261,11 @@ void synth_setup(const hh_synth_params* p, SynthHost& h, hipStream_t s) {
     d.ignore_diags = p->ignore_diags;
     d.cis_only = p->cis_only ? 1 : 0;
     d.seed = p->seed;
-    d.band_w = synth_band_w(p, h.offsets);
+    {
+        const BandWidths bw = synth_band_w(p, h.offsets);
+        d.band_w = bw.w8;
+        d.band_w4 = bw.w4;
+    }
     hipLaunchKernelGGL(k_synth_bins, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, d,
                        (float)p->vis_sigma, (float)p->gap_frac, p->comp_block, h.vis.p, h.sgn.p);
     HIP_CHECK(hipGetLastError());
@@ -263,7 +277,7 @@ inline dim3 row_grid(int64_t nrows) { return dim3((unsigned)((nrows * 64 + 255) 
 // P(count > 0) averaged over visibility / compartment draws (the generator's
 // distributions, a fixed host sample) x the share of rows whose partner bin
 // is cis and not a gap.  Only performance depends on it.
-int32_t synth_band_w(const hh_synth_params* p, const std::vector<int64_t>& offsets) {
+BandWidths synth_band_w(const hh_synth_params* p, const std::vector<int64_t>& offsets) {
     const int S = 2048;
     std::vector<double> x(S);
     uint64_t st = 0x9E3779B97F4A7C15ull ^ p->seed;
@@ -274,22 +288,36 @@ int32_t synth_band_w(const hh_synth_params* p, const std::vector<int64_t>& offse
         x[k] = std::exp(p->vis_sigma * z1) * std::exp(p->vis_sigma * z2);
     }
     const int64_t n = offsets.back();
-    std::vector<double> occ(kBandMaxW + 2, 0.0);
+    std::vector<double> occ(kBandMaxW + 2, 0.0), big(kBandMaxW + 2, 0.0);
+    // P(X > 15) / P(X > 0) for X ~ Poisson(lam)
+    auto tail15 = [](double lam) {
+        if (lam > 60.0) return 1.0;
+        double term = std::exp(-lam), cdf = term;
+        for (int k = 1; k <= 15; ++k) {
+            term *= lam / k;
+            cdf += term;
+        }
+        const double nz = 1.0 - std::exp(-lam);
+        return nz > 0 ? std::max(0.0, 1.0 - cdf) / nz : 0.0;
+    };
     for (int64_t d = 1; d < (int64_t)occ.size() && d < n; ++d) {
         double cis = 0.0;
         for (size_t c = 0; c + 1 < offsets.size(); ++c) cis += (double)std::max<int64_t>(0, offsets[c + 1] - offsets[c] - d);
         cis /= (double)(n - d);
         const double same = std::max(0.0, 1.0 - (double)d / (double)p->comp_block);
         const double lam0 = p->A * std::pow((double)d + 1.0, -p->decay);
-        double e = 0.0;
-        for (int k = 0; k < S; ++k) {
+        double e = 0.0, bg = 0.0;
+        for (int k = 0; k < S; k += (d < 64 ? 1 : 8)) {
             const double lp = lam0 * (1.0 + p->comp_strength) * x[k], lm = lam0 * (1.0 - p->comp_strength) * x[k];
             const double pp = same + 0.5 * (1.0 - same);
-            e += pp * (1.0 - std::exp(-lp)) + (1.0 - pp) * (1.0 - std::exp(-lm));
+            const double op = 1.0 - std::exp(-lp), om = 1.0 - std::exp(-lm);
+            e += pp * op + (1.0 - pp) * om;
+            bg += pp * op * tail15(lp) + (1.0 - pp) * om * tail15(lm);
         }
-        occ[d] = e / S * cis * (1.0 - p->gap_frac) * (1.0 - p->gap_frac);
+        big[d] = e > 0 ? bg / e : 0.0;
+        occ[d] = e / (d < 64 ? S : (S + 7) / 8) * cis * (1.0 - p->gap_frac) * (1.0 - p->gap_frac);
     }
-    return choose_band_w(occ, p->ignore_diags);
+    return choose_band_widths(occ, big, p->ignore_diags);
 }
 }  // namespace
 
@@ -390,11 +418,15 @@ int hh_synth_build(const hh_synth_params* p, int64_t row_lo, int64_t row_hi, voi
         m->pay.alloc(P.n_entries_padded);
         m->payn.alloc(P.n_narrow_padded);
         m->band_w = h.dev.band_w;
+        m->band_w4 = h.dev.band_w4;
         m->band.alloc((size_t)nloc * band_stride(m->band_w));
         m->band.zero(s);
+        m->band4.alloc((size_t)nloc * band4_stride(m->band_w, m->band_w4));
+        m->band4.zero(s);
         {
             SynthOut o{};
             o.band = m->band.p;
+            o.band4 = reinterpret_cast<uint32_t*>(m->band4.p);
             o.tile_of = tof.p;
             o.tile_ent = m->tile_ent.p;
             o.tile_rp = m->tile_rp.p;

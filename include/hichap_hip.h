@@ -49,7 +49,8 @@ int hh_device_count(int32_t* n);
 int hh_set_device(int32_t device);
 int hh_synchronize(void* stream);
 /* Performance knobs: "band_w" (-1 auto, 0 no dense band, > 0 forced
- * multiple of 16; for matrices built afterwards), "flat_max" (0..255: longest
+ * multiple of 16; for matrices built afterwards), "band4" 0/1 (the 4-bit
+ * band; later builds), "flat_max" (0..255: longest
  * row, in 16-B payload words, of a tile swept by the flat kernel; 0 = none;
  * later builds), "band_concurrent" 0/1 (dense-band sweep on a side stream),
  * "sweep_nb" in {1,2,4,8} (row batches in flight per
@@ -73,9 +74,10 @@ int hh_ktime_reset(void);
  * (swizzled LDS byte offset << 3 | count, counts 1..7) and uint32 (count << 16 |
  * offset, counts 8..65535)
  * segments, rows padded to 16 B, counts > 65535 in a small per-row wide
- * list, plus a per-row diagonal.  Pixels near the diagonal (|col - row| <= W,
- * count <= 255, W chosen from the data's diagonal occupancy) live in a dense
- * uint8 band with implicit columns instead of the tiles.  Static filters
+ * list, plus a per-row diagonal.  Pixels near the diagonal (|col - row| <= W8,
+ * count <= 255) live in a dense uint8 band with implicit columns, and those
+ * with W8 < |col - row| <= W4 and count <= 15 in a dense 4-bit band, instead
+ * of the tiles (W8, W4 chosen from the data's diagonal occupancy and counts).  Static filters
  * (ignore_diags, cis_only zero_trans, zero counts) are applied at build time.
  * Shards are whole 512-row blocks (row_lo % 512 == 0).
  */
@@ -98,10 +100,12 @@ typedef struct {
     int32_t ignore_diags;
     int32_t cis_only;
     int32_t device;
-    int32_t band_w;        /* dense diagonal band half-width W (0 = none)    */
+    int32_t band_w;        /* uint8 diagonal band half-width W8 (0 = none)   */
     int32_t n_units_flat;  /* work units swept by the flat (short-row) kernel */
     int64_t n_band;        /* nonzero entries held by the band               */
     int64_t payload_bytes_flat; /* part of payload_bytes in flat-kernel tiles */
+    int32_t band_w4;       /* nibble band outer width (== band_w: none)      */
+    int32_t pad2_;
 } hh_matrix_info;
 
 /* Build from cooler's pixel table (upper triangle bin1 <= bin2; any order,

@@ -180,7 +180,10 @@ def test_synthetic_generator_matches_oracle(ice):
     assert inf["n_entries"] == 2 * b1.size
     assert inf["n_slots"] + inf["n_slots_narrow"] + inf["n_band"] >= inf["n_entries"]
     assert inf["n_slots"] % 4 == 0 and inf["n_slots_narrow"] % 8 == 0
-    band_bytes = (2 * inf["band_w"] + 16 if inf["band_w"] else 0) * (inf["row_hi"] - inf["row_lo"])
+    rows = inf["row_hi"] - inf["row_lo"]
+    band_bytes = (2 * inf["band_w"] + 16 if inf["band_w"] else 0) * rows
+    if inf["band_w4"] > inf["band_w"]:  # 4-bit band: two segments of (W4 - W8) / 2 + 16 bytes
+        band_bytes += (inf["band_w4"] - inf["band_w"] + 32) * rows
     assert inf["payload_bytes"] == 4 * inf["n_slots"] + 2 * inf["n_slots_narrow"] + band_bytes
     assert inf["n_slots_narrow"] > 0  # low counts are stored as uint16
     # shards see the same matrix
@@ -245,25 +248,33 @@ def test_balance_sharded_rccl_world1(ice):
     assert s_["iters"] == st_full["iters"]
 
 
-@pytest.mark.parametrize("band_w", [0, 16, 64, -1])
-def test_dense_band_widths(ice, band_w):
-    """The dense diagonal band (any width, or none) holds exactly the pixels
-    it claims: export round trip, and weights equal the oracle's."""
+@pytest.mark.parametrize("band_w,band4", [(0, 1), (16, 1), (64, 1), (-1, 0), (-1, 1)])
+def test_dense_band_widths(ice, band_w, band4):
+    """The dense diagonal bands (uint8 of any width or none; the 4-bit band
+    beyond it, on or off) hold exactly the pixels they claim: export round
+    trip (counts > 255 near the diagonal and > 15 in the 4-bit range go to
+    the tiles), and weights equal the oracle's."""
     from hichap_master_amd import _lib
-    b1, b2, c, off = _case(31, sizes=(700, 500), A=60.0, trans=0.02)
+    b1, b2, c, off = _case(31, sizes=(1400, 900), A=60.0, trans=0.02)
     c = c.copy()
-    c[::97] = 300  # counts > 255 near the diagonal go to the tiles
+    c[::97] = 300   # counts > 255 near the diagonal go to the tiles
+    c[5::89] = 16   # ... and counts > 15 in the 4-bit range
     n = int(off[-1])
     _lib.call("hh_tune", b"band_w", band_w)
+    _lib.call("hh_tune", b"band4", band4)
     try:
         m = ice.ContactMatrix.from_pixels(b1, b2, c, n, off)
         inf = m.info()
         if band_w > 0:
-            assert inf["band_w"] == band_w
+            assert inf["band_w"] == band_w and inf["band_w4"] == band_w
         if band_w == 0:
-            assert inf["band_w"] == 0 and inf["n_band"] == 0
+            assert inf["band_w"] == 0 and inf["band_w4"] == 0 and inf["n_band"] == 0
         if band_w == -1:
-            assert inf["band_w"] > 0 and inf["n_band"] > 0  # dense near the diagonal at A=60
+            assert inf["n_band"] > 0  # dense near the diagonal at A=60
+            if band4:
+                assert inf["band_w4"] > inf["band_w"] and (inf["band_w4"] - inf["band_w"]) % 32 == 0
+            else:
+                assert inf["band_w4"] == inf["band_w"] > 0
         e1, e2, ec = m.export_upper()
         f1, f2, fc = _filtered_upper(b1, b2, c, off, 1, False)
         np.testing.assert_array_equal(e1, f1)
@@ -273,6 +284,7 @@ def test_dense_band_widths(ice, band_w):
         m.close()
     finally:
         _lib.call("hh_tune", b"band_w", -1)
+        _lib.call("hh_tune", b"band4", 1)
     w_ref, st_ref = ice_ref.balance(b1, b2, c, n, off)
     assert st["iters"] == st_ref["iters"]
     np.testing.assert_allclose(w, w_ref, rtol=1e-9, equal_nan=True)

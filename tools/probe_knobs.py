@@ -30,9 +30,10 @@ tune(a.build)
 t0 = time.time()
 m = ice.ContactMatrix.synthetic(sizes, A=A, trans_density=td)
 inf = m.info()
-print(f"build {time.time()-t0:.1f}s band_w={inf['band_w']} units={inf['n_units']} "
+print(f"build {time.time()-t0:.1f}s band_w={inf['band_w']} band_w4={inf['band_w4']} units={inf['n_units']} "
       f"payload {inf['payload_bytes']/1e9:.2f} GB (flat {inf['payload_bytes_flat']/1e9:.2f} GB in "
-      f"{inf['n_units_flat']} units, band {(2 * inf['band_w'] + 16) * (inf['row_hi'] - inf['row_lo']) / 1e9:.2f} GB) "
+      f"{inf['n_units_flat']} units, band {(2 * inf['band_w'] + 16) * (inf['row_hi'] - inf['row_lo']) / 1e9:.2f} GB, band4 "
+      f"{(inf['band_w4'] - inf['band_w'] + 32) * (inf['band_w4'] > inf['band_w']) * (inf['row_hi'] - inf['row_lo']) / 1e9:.2f} GB) "
       f"tiles {inf['n_tiles']}", flush=True)
 st = ice.IceState(m, ice.IceOptions(tol=0.0, max_iters=10**6, mad_max=0, min_nnz=0))
 for rep in range(2):
