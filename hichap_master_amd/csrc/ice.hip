@@ -671,22 +671,16 @@ struct BandGeo {
 template <int G>
 __device__ __forceinline__ int bpadg(int k) { return k + k / G; }
 
-// bits [128 - BITS m, 256 - BITS m) of prev ++ own (m < G, wave-uniform)
-template <int BITS>
-__device__ __forceinline__ uint4 band_shift(const uint4 prev, const uint4 own, int m) {
-    const uint32_t d[8] = {prev.x, prev.y, prev.z, prev.w, own.x, own.y, own.z, own.w};
-    const int B = 128 - BITS * m, q = B >> 5, r = B & 31;
-    uint32_t o[5];
-    switch (q) {  // uniform branch
-        case 0: o[0] = d[0], o[1] = d[1], o[2] = d[2], o[3] = d[3], o[4] = d[4]; break;
-        case 1: o[0] = d[1], o[1] = d[2], o[2] = d[3], o[3] = d[4], o[4] = d[5]; break;
-        case 2: o[0] = d[2], o[1] = d[3], o[2] = d[4], o[3] = d[5], o[4] = d[6]; break;
-        case 3: o[0] = d[3], o[1] = d[4], o[2] = d[5], o[3] = d[6], o[4] = d[7]; break;
-        default: o[0] = d[4], o[1] = d[5], o[2] = d[6], o[3] = d[7], o[4] = 0u; break;  // q = 4 (m = 0)
-    }
-    if (r == 0) return make_uint4(o[0], o[1], o[2], o[3]);
-    return make_uint4(__builtin_amdgcn_alignbit(o[1], o[0], r), __builtin_amdgcn_alignbit(o[2], o[1], r),
-                      __builtin_amdgcn_alignbit(o[3], o[2], r), __builtin_amdgcn_alignbit(o[4], o[3], r));
+// bits [128 - BITS m, 256 - BITS m) of prev ++ own (m < G, wave-uniform):
+// output dword i = alignbit(d[q + i + 1], d[q + i], r) with B = 128 - BITS m,
+// q = B / 32, r = B % 32.  Q is a template parameter so each case reads its
+// source registers directly (a runtime dword choice costs a v_mov per dword).
+template <int Q>
+__device__ __forceinline__ uint4 band_shift_q(const uint4 prev, const uint4 own, int r) {
+    const uint32_t d[9] = {prev.x, prev.y, prev.z, prev.w, own.x, own.y, own.z, own.w, 0u};
+    if (r == 0) return make_uint4(d[Q], d[Q + 1], d[Q + 2], d[Q + 3]);
+    return make_uint4(__builtin_amdgcn_alignbit(d[Q + 1], d[Q], r), __builtin_amdgcn_alignbit(d[Q + 2], d[Q + 1], r),
+                      __builtin_amdgcn_alignbit(d[Q + 3], d[Q + 2], r), __builtin_amdgcn_alignbit(d[Q + 4], d[Q + 3], r));
 }
 
 template <int BITS>
@@ -697,6 +691,20 @@ __device__ __forceinline__ double band_dot(const uint4 v, const double* __restri
 #pragma unroll
     for (int k = 0; k < G; ++k) acc = fma((double)((x[k / PER] >> (BITS * (k % PER))) & MASK), b0[k], acc);
     return acc;
+}
+
+// acc + the dot of the row's m-shifted counts with the lane's window values
+template <int BITS, int G>
+__device__ __forceinline__ double band_dot_shifted(const uint4 prev, const uint4 own, int m, const double (&w)[G],
+                                                   double acc) {
+    const int B = 128 - BITS * m, r = B & 31;
+    switch (B >> 5) {  // wave-uniform
+        case 0: return band_dot<BITS>(band_shift_q<0>(prev, own, r), w, acc);
+        case 1: return band_dot<BITS>(band_shift_q<1>(prev, own, r), w, acc);
+        case 2: return band_dot<BITS>(band_shift_q<2>(prev, own, r), w, acc);
+        case 3: return band_dot<BITS>(band_shift_q<3>(prev, own, r), w, acc);
+        default: return band_dot<BITS>(band_shift_q<4>(prev, own, 0), w, acc);  // m = 0
+    }
 }
 
 template <int BITS, int ABL>
@@ -771,7 +779,7 @@ __global__ __launch_bounds__(kBandThreads) void k_sweep_band(const uint8_t* __re
                 for (int k = 0; k < G; ++k) w[k] = b0[k];
 #pragma unroll
                 for (int j = 0; j < RJ; ++j)
-                    acc[j] = band_dot<BITS>(band_shift<BITS>(prev[j], own[j], wave + NW * (j0 + j)), w, acc[j]);
+                    acc[j] = band_dot_shifted<BITS, G>(prev[j], own[j], wave + NW * (j0 + j), w, acc[j]);
             }
         }
 #pragma unroll
