@@ -1115,6 +1115,9 @@ int hh_tune(const char* key, int64_t value) {
         } else if (k == "sweep_ablate") {
             HH_REQUIRE(value >= 0 && value <= 2, "sweep_ablate must be 0, 1 or 2");
             g_sweep_ablate = (int)value;
+        } else if (k == "band4_density_pct" || k == "band8_big_pct") {
+            HH_REQUIRE(value >= 1 && value <= 100, "percent in [1, 100]");
+            (k == "band4_density_pct" ? g_band4_density : g_band8_big) = (double)value / 100.0;
         } else if (k == "band4") {
             HH_REQUIRE(value == 0 || value == 1, "band4 in {0, 1}");
             g_band4 = value;

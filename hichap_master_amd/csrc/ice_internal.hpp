@@ -52,12 +52,12 @@ extern int64_t g_band_w;            // hh_tune("band_w"): -1 auto, 0 off, > 0 fo
 // W8 < |d| <= W4 whose counts are <= 15 are stored as 4-bit counts with
 // implicit columns, in two segments per row (negative, positive diagonals),
 // each K = W4 - W8 slots (a multiple of 32) + 32 slots of zero padding.
-// W8 shrinks to where counts > 15 become rare (< kBand8Big of a diagonal's
-// pixels), W4 reaches the occupancy break-even of 4-bit slots vs 2-byte tile
-// entries (kBand4Density).  Larger counts there stay in the tiles.
+// W8 shrinks to where counts > 15 become rare (< g_band8_big of a diagonal's
+// pixels), W4 reaches the occupancy break-even of 4-bit slots vs
+// 2-byte tile entries (g_band4_density).  Larger counts there stay in the tiles.
 constexpr uint32_t kBand4MaxCnt = 15u;
-constexpr double kBand4Density = 0.25;
-constexpr double kBand8Big = 0.05;
+extern double g_band4_density;      // hh_tune("band4_density_pct"), default 25 %
+extern double g_band8_big;          // hh_tune("band8_big_pct"), default 5 %
 extern int64_t g_band4;             // hh_tune("band4"): 1 nibble band on (default), 0 off
 struct BandWidths {
     int32_t w8 = 0, w4 = 0;         // uint8 band |d| <= w8; nibble band w8 < |d| <= w4 (w4 == w8: none)

@@ -15,6 +15,8 @@ int64_t g_band_w = -1;       // -1 = auto (choose_band_w)
 int64_t g_flat_max = 64;     // longest row (uint4) of a flat tile segment; 0 = no flat segments
 
 int64_t g_band4 = 1;         // nibble band on
+double g_band4_density = 0.25;
+double g_band8_big = 0.05;
 
 int32_t choose_band_w(const std::vector<double>& occ, int ignore_diags) {
     if (g_band_w >= 0) return (int32_t)std::min<int64_t>(g_band_w, kBandMaxW) & ~15;
@@ -28,14 +30,14 @@ BandWidths choose_band_widths(const std::vector<double>& occ, const std::vector<
     BandWidths bw;
     bw.w8 = bw.w4 = choose_band_w(occ, ignore_diags);
     if (g_band_w >= 0 || !g_band4 || std::max(1, ignore_diags) > 1) return bw;
-    // outer edge: occupancy >= kBand4Density from diagonal 1 on
+    // outer edge: occupancy >= g_band4_density from diagonal 1 on
     int64_t d4 = 1;
-    while (d4 < (int64_t)occ.size() && occ[d4] >= kBand4Density) ++d4;
+    while (d4 < (int64_t)occ.size() && occ[d4] >= g_band4_density) ++d4;
     --d4;
     // inner edge: past the last diagonal where counts > 15 are common
     int64_t d8 = 0;
     for (int64_t d = 1; d <= d4 && d < (int64_t)big.size(); ++d)
-        if (big[d] >= kBand8Big) d8 = d;
+        if (big[d] >= g_band8_big) d8 = d;
     int64_t w8 = (d8 + 15) & ~15LL;
     if (w8 > bw.w8) w8 = bw.w8;  // no uint8 slots below their own break-even
     const int64_t k = (d4 - w8) & ~31LL;

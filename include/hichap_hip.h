@@ -50,7 +50,8 @@ int hh_set_device(int32_t device);
 int hh_synchronize(void* stream);
 /* Performance knobs: "band_w" (-1 auto, 0 no dense band, > 0 forced
  * multiple of 16; for matrices built afterwards), "band4" 0/1 (the 4-bit
- * band; later builds), "flat_max" (0..255: longest
+ * band; later builds), "band4_density_pct" / "band8_big_pct" (its width
+ * thresholds, defaults 25 / 5; later builds), "flat_max" (0..255: longest
  * row, in 16-B payload words, of a tile swept by the flat kernel; 0 = none;
  * later builds), "band_concurrent" 0/1 (dense-band sweep on a side stream),
  * "sweep_nb" in {1,2,4,8} (row batches in flight per
