@@ -16,15 +16,16 @@ def load(path, counter):
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] == counter:
             acc[r["Kernel_Name"]].append(float(r["Counter_Value"]))
-    return {k: sum(v) / len(v) for k, v in acc.items()}
+    return {k: sum(v) / len(v) for k, v in acc.items()}, {k: len(v) for k, v in acc.items()}
 
 
 def main(fetch_csv, write_csv, out):
-    f, w = load(fetch_csv, "FETCH_SIZE"), load(write_csv, "WRITE_SIZE")
+    (f, nf), (w, _) = load(fetch_csv, "FETCH_SIZE"), load(write_csv, "WRITE_SIZE")
     res = {}
     for k in sorted(set(f) | set(w)):
         fb, wb = f.get(k, 0.0) * 1024.0, w.get(k, 0.0) * 1024.0
-        res[k] = {"fetch_size_bytes": fb, "write_size_bytes": wb, "traffic_bytes": 2.0 * fb + wb}
+        res[k] = {"fetch_size_bytes": fb, "write_size_bytes": wb, "traffic_bytes": 2.0 * fb + wb,
+                  "dispatches": nf.get(k, 0)}
     json.dump(res, open(out, "w"), indent=1)
     for k, v in res.items():
         if "sweep" in k:
