@@ -44,9 +44,17 @@ def config(name, nnz=None):
     if name == "c4":
         sizes = synth.genome_bins(10000, diploid=True)
         target, tf, label = nnz or 5e9, 0.2, "hg19-10kb-diploid-wholegenome"
+    elif name == "c3":
+        sizes = synth.genome_bins(40000)
+        # hg19 at 40 kb has only 1.42e8 cis pixels (sum n(n+1)/2, 2 % gaps), so
+        # the ~8e8 nnz of BASELINE C3 needs ~85 % trans contacts
+        target, tf, label = nnz or 8e8, 0.85, "hg19-40kb-wholegenome"
     elif name == "c2":
         sizes = [synth.chrom_bins([synth.HG19["1"]], 10000)[0]]
         target, tf, label = nnz or 5e7, 0.0, "hg19-chr1-10kb"
+    elif name == "c1":
+        sizes = [5000]
+        target, tf, label = nnz or 2e6, 0.0, "single-chrom-40kb-5000-bins"
     else:
         raise SystemExit(f"unknown config {name}")
     A, td = synth.calibrate(sizes, target, tf)
@@ -75,7 +83,7 @@ def pmc_traffic(kernels=SWEEP_KERNELS):
     return tot, os.path.relpath(files[-1], ROOT)
 
 
-def cpu_baseline(sizes, kw, rc, nnz_total, budget_s=12.0):
+def cpu_baseline(sizes, kw, rc, nnz_total, label, budget_s=12.0):
     """Oracle (NumPy, cooler's bincount sweep) timed on the host on a bounded
     sample: the upper-triangle pixels of the first rows of the same matrix."""
     from hichap_master_amd import ice
@@ -83,7 +91,7 @@ def cpu_baseline(sizes, kw, rc, nnz_total, budget_s=12.0):
     n = int(np.sum(sizes))
     per_row = max(nnz_total / n, 1.0)
     rows = int(min(n, max(64, 2.5e7 / per_row)))
-    rows = min(n, (rows + 255) // 256 * 256)
+    rows = min(n, (rows + 511) // 512 * 512)  # shards are whole 512-row blocks
     m = ice.ContactMatrix.synthetic(sizes, row_range=(0, rows), **kw)
     b1, b2, c = m.export_upper()
     m.close()
@@ -96,7 +104,7 @@ def cpu_baseline(sizes, kw, rc, nnz_total, budget_s=12.0):
             break
     dt = time.perf_counter() - t0
     pix_rate = b1.size * iters / dt
-    return {"value": pix_rate / nnz_total, "unit": "ICE iterations/s (whole C4 matrix, extrapolated)",
+    return {"value": pix_rate / nnz_total, "unit": f"ICE iterations/s (whole {label} matrix, extrapolated)",
             "cores": 1, "kind": "port",
             "sample": f"oracle/ice_ref.sweep_rate (numpy bincount, cooler restatement) on the "
                       f"{b1.size} upper pixels of rows [0,{rows}) of the same matrix, {iters} sweeps "
@@ -632,8 +640,8 @@ def main():
             "data": "synthetic (SURVEY.md §8(d) model generated in HBM; no real Hi-C data offline)",
             "nnz_iters_per_s": nnz_total * its,
             "config": {"workload": label, "n_bins": n, "nnz_upper": nnz_total,
-                       "trans_fraction_target": tf, "resolution_bp": 10000 if args.config != "c1" else 40000,
-                       "parallelism": f"rows sharded x{world}, RCCL all-gather of marginals" if world > 1
+                       "trans_fraction_target": tf, "resolution_bp": 40000 if args.config in ("c1", "c3") else 10000,
+                       "parallelism": f"rows sharded x{world}, {'RCCL' if backend == 'nccl' else backend} all-gather of marginals" if world > 1
                        else "single GPU", "generate_s": round(gen_s, 2),
                        "entries_stored": inf["n_entries"], "slots_u32": inf["n_slots"],
                        "slots_u16": inf["n_slots_narrow"], "payload_bytes": inf["payload_bytes"],
@@ -668,7 +676,7 @@ def main():
                                        "because the HBM layout streams ~3.6 B/pixel (DESIGN.md 3); "
                                        "traffic_GBps / peak is the physical HBM utilisation"}
         if world == 1 and not args.no_cpu:
-            out["cpu_baseline"] = cpu_baseline(sizes, kw, rc, nnz_total)
+            out["cpu_baseline"] = cpu_baseline(sizes, kw, rc, nnz_total, label)
         print(json.dumps(out), flush=True)
     if torch.distributed.is_initialized():
         torch.distributed.destroy_process_group()
