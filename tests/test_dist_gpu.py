@@ -1,0 +1,71 @@
+"""Multi-process sharded ICE on the GPU: world_size-2 runs of
+hichap_master_amd.dist.balance_sharded with the HIP backend (IceState over a
+row shard each), both ranks on cuda:0 with the gloo exchange (RCCL refuses two
+ranks on one device; the RCCL path is covered at world 1 in test_ice_gpu.py
+and at N>1 by the driver's scaling bench).  Every rank's weights equal the
+one-process HIP run bitwise and the oracle within the ICE tolerance."""
+import os
+import socket
+import tempfile
+
+import numpy as np
+import pytest
+
+from hichap_master_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, case, cis_only, outdir):
+    import torch
+    import torch.distributed as tdist
+    from hichap_master_amd import _lib, dist, ice
+    torch.cuda.set_device(0)
+    _lib.load()
+    _lib.call("hh_set_device", 0)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    tdist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        b1, b2, c, off = case
+        n = int(off[-1])
+        rr = dist.partition_rows(np.bincount(b1, minlength=n) + np.bincount(b2, minlength=n), world)
+        m = ice.ContactMatrix.from_pixels(b1, b2, c, n, off, cis_only=cis_only, row_range=(rr[rank], rr[rank + 1]))
+        st = ice.IceState(m, ice.IceOptions(max_iters=400, cis_only=cis_only))
+        ex = dist.Exchange(rr, torch.device("cuda", 0))
+        assert not ex.fused
+        w, s_ = dist.balance_sharded(st, ex, max_iters=400)
+        torch.cuda.synchronize()
+        st.close()
+        m.close()
+        np.save(os.path.join(outdir, f"w{rank}.npy"), w)
+        np.save(os.path.join(outdir, f"it{rank}.npy"), np.atleast_1d(s_["iters"]))
+    finally:
+        tdist.destroy_process_group()
+
+
+@pytest.mark.parametrize("cis_only", [False, True])
+def test_balance_sharded_two_processes(cis_only):
+    import torch.multiprocessing as mp
+    from hichap_master_amd import _lib, ice
+    from oracle import ice_ref
+    _lib.require_gpu()
+    rng = np.random.default_rng(21)
+    case = synth.coo_genome([900, 700, 400], rng, A=25.0, trans_density=0.01)
+    b1, b2, c, off = case
+    n = int(off[-1])
+    w_full, st_full = ice.balance(b1, b2, c, n, off, cis_only=cis_only, max_iters=400)
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_worker, args=(2, _free_port(), case, cis_only, d), nprocs=2, start_method="spawn")
+        ws = [np.load(os.path.join(d, f"w{r}.npy")) for r in range(2)]
+        its = [np.load(os.path.join(d, f"it{r}.npy")) for r in range(2)]
+    wr, sr = ice_ref.balance(b1, b2, c, n, off, cis_only=cis_only, max_iters=400)
+    for w, it in zip(ws, its):
+        np.testing.assert_array_equal(w, w_full)
+        np.testing.assert_allclose(w, wr, rtol=1e-9, equal_nan=True)
+        np.testing.assert_array_equal(it, np.atleast_1d(st_full["iters"]))
