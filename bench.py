@@ -112,6 +112,34 @@ def cpu_baseline(sizes, kw, rc, nnz_total, label, budget_s=12.0):
             "pixel_iters_per_s": pix_rate}
 
 
+def tad_scan_bench(m, st, stream, reps=5, res=10000, min_tad=200000, window=600000):
+    """C2's TAD step after ICE: the gap + DI scan of the balanced chromosome
+    (StructureFind.Data_preprocess :853-891 with HiCHap's defaults, minTAD
+    200 kb and a 600 kb window) fed from the pixel table already in HBM
+    (hh_tad_scan_pixels, on_device): band build + gap + DI, N x N never built."""
+    import torch
+    from hichap_master_amd._lib import call, ptr
+    w, _ = st.finalize(stream)
+    b1, b2, c = m.export_upper()
+    n = int(m.info()["n_bins"])
+    dev = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    d1, d2, dc, dw = dev(b1), dev(b2), dev(c.astype(np.float64)), dev(w)
+    lb, wb = min_tad // res, window // res
+    win = np.full(n, wb, np.int32)
+    gap = np.empty(n, np.uint8)
+    di = np.empty(n, np.float64)
+    ts = []
+    for _ in range(reps + 1):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        call("hh_tad_scan_pixels", ptr(d1), ptr(d2), ptr(dc), b1.size, ptr(dw), n, 0, n, lb, ptr(win), 0,
+             ptr(gap), ptr(di), 1, stream)
+        ts.append(time.perf_counter() - t0)
+    return {"ms": 1000.0 * float(np.median(ts[1:])), "pixels": int(b1.size), "bins": n, "band_halfwidth": wb,
+            "gap_bins": int(gap.sum()), "nonzero_di": int(np.count_nonzero(di)),
+            "what": "hh_tad_scan_pixels on device pixels + ICE weights: balanced band, Get_Gap, Get_DI (ttest)"}
+
+
 C5_RES = 25000
 C5_STREAMS = int(os.environ.get("HH_C5_STREAMS", "4"))
 
@@ -612,6 +640,7 @@ def main():
         _lib.call("hh_ktime_enable", 0)
         sweep_ms, launches = _lib.ktime("ice_sweep")
         _lib.call("hh_ktime_reset")
+    tad = tad_scan_bench(m, st, stream) if args.config == "c2" and world == 1 and not args.sharded else None
     tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
     if torch.distributed.is_initialized():
         torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
@@ -675,6 +704,8 @@ def main():
                                "note": "achieved = SURVEY 8(d) algorithmic 12 B/pixel / sweep time; frac > 1 "
                                        "because the HBM layout streams ~3.6 B/pixel (DESIGN.md 3); "
                                        "traffic_GBps / peak is the physical HBM utilisation"}
+        if tad is not None:
+            out["tad_scan"] = tad
         if world == 1 and not args.no_cpu:
             out["cpu_baseline"] = cpu_baseline(sizes, kw, rc, nnz_total, label)
         print(json.dumps(out), flush=True)

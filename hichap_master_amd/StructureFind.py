@@ -336,6 +336,33 @@ class StructureFind(TADCalling):
         wb = int((self.window if window is None else window) / self.Res)
         return gap, self.Get_DI(M, gap, np.ones(N, dtype=int) * wb)
 
+    def di_scan_pixels(self, bin1, bin2, count, weight, lo, N, window=None):
+        """``di_scan`` of one chromosome straight from cooler's pixel table
+        (Data_preprocess :853-854 fetches the balanced dense matrix and
+        applies np.nan_to_num; pass ``weight=None`` for the allelic
+        ``balance=False`` path, :858-865): the band the scans read is built on
+        the device, so the N x N matrix never exists.  ``bin1 <= bin2`` are
+        global bin ids of unique pixels, the chromosome is bins [lo, lo + N).
+        Returns (gap with the first / last bin, DI) like ``di_scan``."""
+        _lib.require_gpu()
+        b1 = np.ascontiguousarray(bin1, dtype=np.int64)
+        b2 = np.ascontiguousarray(bin2, dtype=np.int64)
+        c = np.ascontiguousarray(count, dtype=np.float64)
+        if not (b1.shape == b2.shape == c.shape):
+            raise ValueError("bin1, bin2 and count must have the same length")
+        w = None if weight is None else np.ascontiguousarray(weight, dtype=np.float64)
+        lb = int(self.minTAD / self.Res)
+        wb = int((self.window if window is None else window) / self.Res)
+        if self.test_type not in ("ttest", "chitest"):
+            raise ValueError(f"unknown test type {self.test_type!r}")
+        win = np.full(int(N), wb, dtype=np.int32)
+        g = np.empty(int(N), np.uint8)
+        di = np.empty(int(N), np.float64)
+        call("hh_tad_scan_pixels", ptr(b1), ptr(b2), ptr(c), b1.size, None if w is None else ptr(w),
+             0 if w is None else w.size, int(lo), int(N), lb, ptr(win), 0 if self.test_type == "ttest" else 1,
+             ptr(g), ptr(di), 0, None)
+        return np.nonzero(g)[0], di
+
 
 def column_band(M, B):
     """band[B + k, j] = M[j + k, j] for k in [-B, B] (0 outside), diagonal-

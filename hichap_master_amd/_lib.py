@@ -97,6 +97,8 @@ SIGNATURES = {
     "hh_comp_set_cor": (C.c_int, [P, P, P]),
     "hh_gap_scan": (C.c_int, [P, I64, I32, I32, P, I32, P]),
     "hh_di_scan": (C.c_int, [P, I64, I32, P, P, I32, P, I32, P]),
+    "hh_band_from_pixels": (C.c_int, [P, P, P, I64, P, I64, I64, I64, I32, P, I32, P]),
+    "hh_tad_scan_pixels": (C.c_int, [P, P, P, I64, P, I64, I64, I64, I32, P, I32, P, P, I32, P]),
     "hh_viterbi_gmm": (C.c_int, [P, I64, I32, I32, P, P, P, P, P, P, P]),
     "hh_comp_pca": (C.c_int, [P, I32, F64, I32, P, P, P, P]),
     "hh_comp_select_stats": (C.c_int, [P, P, I32, F64, P, P]),

@@ -982,3 +982,124 @@ extern "C" int hh_di_scan(const double* band, int64_t N, int32_t B, const uint8_
         HIP_CHECK(hipStreamSynchronize(s));
     });
 }
+
+// ============================================ balanced band from pixels (K10)
+// cooler's `matrix(balance=True).fetch(chrom)` followed by np.nan_to_num
+// (StructureFind.Data_preprocess :853-854; allelic data: balance=False,
+// :858-865), restricted to the band the gap / DI scans read: one thread per
+// pixel of the (upper-triangle, unique) pixel table; a pixel of the
+// chromosome [lo, lo + N) within B of the diagonal writes M[i][j] and M[j][i]
+// with value count * w[bin1] * w[bin2] (cooler's product order; NaN -> 0).
+// Every band cell has at most one writer: no atomics, deterministic.
+namespace hh {
+__global__ void k_band_from_pixels(const int64_t* __restrict__ b1, const int64_t* __restrict__ b2,
+                                   const double* __restrict__ cnt, long long nnz, const double* __restrict__ w,
+                                   long long lo, long long N, int B, double* __restrict__ band) {
+    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nnz) return;
+    const long long p = b1[t], q = b2[t];
+    const long long i = (p < q ? p : q) - lo, j = (p < q ? q : p) - lo;
+    if (i < 0 || j >= N) return;
+    const long long d = j - i;
+    if (d > B) return;
+    double v = cnt[t];
+    if (w) {
+        v = v * w[p] * w[q];
+        if (v != v) v = 0.0;
+    }
+    band[(long long)(B - d) * N + j] = v;            // M[i][j]: column j, k = -d
+    if (d) band[(long long)(B + d) * N + i] = v;     // M[j][i]: column i, k = +d
+}
+}  // namespace hh
+
+namespace {
+// stage the pixel table (and weights) on the device unless already there,
+// then build the zeroed (2B+1) x N band at `band` (device)
+void band_from_pixels_dev(const int64_t* bin1, const int64_t* bin2, const double* count, int64_t nnz,
+                          const double* weight, int64_t n_weight, int64_t lo, int64_t N, int32_t B, int32_t on_device,
+                          double* band, hipStream_t s) {
+    DBuf<int64_t> d1, d2;
+    DBuf<double> dc, dw;
+    const int64_t *p1 = bin1, *p2 = bin2;
+    const double *pc = count, *pw = weight;
+    if (!on_device && nnz > 0) {
+        d1.alloc(nnz); d1.upload(bin1, nnz, s); p1 = d1.p;
+        d2.alloc(nnz); d2.upload(bin2, nnz, s); p2 = d2.p;
+        dc.alloc(nnz); dc.upload(count, nnz, s); pc = dc.p;
+        if (weight) { dw.alloc(n_weight); dw.upload(weight, n_weight, s); pw = dw.p; }
+    }
+    HIP_CHECK(hipMemsetAsync(band, 0, sizeof(double) * (size_t)N * (2 * B + 1), s));
+    if (nnz > 0) {
+        HH_KTIME("k_band_from_pixels", s);
+        hipLaunchKernelGGL(hh::k_band_from_pixels, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s, p1, p2, pc,
+                           (long long)nnz, pw, (long long)lo, (long long)N, B, band);
+    }
+    HIP_CHECK(hipGetLastError());
+    HIP_CHECK(hipStreamSynchronize(s));  // staged inputs are freed on return
+}
+
+void check_pixels_args(const int64_t* bin1, const int64_t* bin2, const double* count, int64_t nnz,
+                       const double* weight, int64_t n_weight, int64_t lo, int64_t N, int32_t B, int32_t on_device) {
+    HH_REQUIRE(nnz >= 0 && N > 0 && B >= 0 && lo >= 0, "bad arguments");
+    HH_REQUIRE(nnz == 0 || (bin1 && bin2 && count), "null pixel arrays");
+    HH_REQUIRE(!weight || lo + N <= n_weight, "weights do not cover the chromosome");
+    HH_REQUIRE((double)N * (2.0 * B + 1.0) < 4e9, "band too large");
+    (void)on_device;
+}
+}  // namespace
+
+extern "C" int hh_band_from_pixels(const int64_t* bin1, const int64_t* bin2, const double* count, int64_t nnz,
+                                   const double* weight, int64_t n_weight, int64_t lo, int64_t N, int32_t B,
+                                   double* band, int32_t on_device, void* stream) {
+    return guard([&] {
+        check_pixels_args(bin1, bin2, count, nnz, weight, n_weight, lo, N, B, on_device);
+        HH_REQUIRE(band, "null band");
+        hipStream_t s = as_stream(stream);
+        if (on_device) {
+            band_from_pixels_dev(bin1, bin2, count, nnz, weight, n_weight, lo, N, B, 1, band, s);
+            return;
+        }
+        DBuf<double> db((size_t)N * (2 * B + 1));
+        band_from_pixels_dev(bin1, bin2, count, nnz, weight, n_weight, lo, N, B, 0, db.p, s);
+        db.download(band, db.n, s);
+        HIP_CHECK(hipStreamSynchronize(s));
+    });
+}
+
+extern "C" int hh_tad_scan_pixels(const int64_t* bin1, const int64_t* bin2, const double* count, int64_t nnz,
+                                  const double* weight, int64_t n_weight, int64_t lo, int64_t N, int32_t lb,
+                                  const int32_t* window_bins, int32_t test, uint8_t* gap, double* di,
+                                  int32_t on_device, void* stream) {
+    return guard([&] {
+        HH_REQUIRE(window_bins && gap && di && lb >= 0, "bad arguments");
+        HH_REQUIRE(test == 0 || test == 1, "test must be 0 (ttest) or 1 (chitest)");
+        int32_t B = lb;
+        for (int64_t j = 0; j < N; ++j) B = std::max(B, window_bins[j]);
+        check_pixels_args(bin1, bin2, count, nnz, weight, n_weight, lo, N, B, on_device);
+        hipStream_t s = as_stream(stream);
+        DBuf<double> db((size_t)N * (2 * B + 1));
+        band_from_pixels_dev(bin1, bin2, count, nnz, weight, n_weight, lo, N, B, on_device, db.p, s);
+        DBuf<uint8_t> dg(N);
+        {
+            HH_KTIME("k_gap_scan", s);
+            hipLaunchKernelGGL(hh::k_gap_scan, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, db.p, (long long)N,
+                               B, lb, dg.p);
+        }
+        HIP_CHECK(hipGetLastError());
+        // Data_preprocess (:876-884): the first and last bins join the gap
+        HIP_CHECK(hipMemsetAsync(dg.p, 1, 1, s));
+        HIP_CHECK(hipMemsetAsync(dg.p + N - 1, 1, 1, s));
+        DBuf<int> dw(N);
+        dw.upload(window_bins, N, s);
+        DBuf<double> dd(N);
+        {
+            HH_KTIME("k_di", s);
+            hipLaunchKernelGGL(hh::k_di, dim3((unsigned)((N * hh::kDiLanes + 255) / 256)), dim3(256), 0, s, db.p,
+                               (long long)N, B, dg.p, dw.p, test, dd.p);
+        }
+        HIP_CHECK(hipGetLastError());
+        dg.download(gap, N, s);
+        dd.download(di, N, s);
+        HIP_CHECK(hipStreamSynchronize(s));
+    });
+}

@@ -277,6 +277,27 @@ int hh_gap_scan(const double* band, int64_t N, int32_t B, int32_t lb, uint8_t* g
                 void* stream);
 int hh_di_scan(const double* band, int64_t N, int32_t B, const uint8_t* gap, const int32_t* window_bins,
                int32_t test, double* di, int32_t on_device, void* stream);
+/* The same scans fed from cooler's pixel table instead of a dense matrix:
+ * StructureFind.Data_preprocess (:853-854) loads each chromosome as
+ * cooler.matrix(balance=True).fetch(chrom) + np.nan_to_num (allelic data:
+ * balance=False, :858-865) and scans it.  hh_band_from_pixels builds that
+ * matrix's band on the device, band[(B + k) * N + j] = M[j + k][j] for the
+ * chromosome's bins [lo, lo + N), from the unique upper-triangle pixels
+ * (bin1 <= bin2, global bin ids): value count * weight[bin1] * weight[bin2]
+ * with NaN -> 0, or the raw count when weight is NULL (n_weight >= lo + N).
+ * on_device: bin1/bin2/count/weight/band are device pointers; otherwise host
+ * pointers (the band is returned to the host).  hh_tad_scan_pixels = band of
+ * width B = max(lb, max window_bins) + hh_gap_scan + the first / last bin
+ * joining the gap (Data_preprocess :876-884) + hh_di_scan in one call, the
+ * pixel table crossing PCIe once (not at all with on_device); gap, di and
+ * window_bins are host arrays of N. */
+int hh_band_from_pixels(const int64_t* bin1, const int64_t* bin2, const double* count, int64_t nnz,
+                        const double* weight, int64_t n_weight, int64_t lo, int64_t N, int32_t B, double* band,
+                        int32_t on_device, void* stream);
+int hh_tad_scan_pixels(const int64_t* bin1, const int64_t* bin2, const double* count, int64_t nnz,
+                       const double* weight, int64_t n_weight, int64_t lo, int64_t N, int32_t lb,
+                       const int32_t* window_bins, int32_t test, uint8_t* gap, double* di, int32_t on_device,
+                       void* stream);
 
 /* ------------------------------------------------- TAD HMM (host code)
  * Viterbi path of a continuous HMM with Gaussian-mixture emissions, ghmm's

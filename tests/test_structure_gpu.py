@@ -113,3 +113,60 @@ def test_compartment_device_tensor_input(SF):
     a = SF(Res=100000).compartment(M)
     b = SF(Res=100000).compartment(torch.from_numpy(M).cuda())
     np.testing.assert_array_equal(a, b)
+
+
+def _balanced_dense(b1, b2, c, w, lo, N):
+    """cooler.matrix(balance=True).fetch(chrom) + np.nan_to_num (Data_preprocess
+    :853-854) in NumPy: count * w[bin1] * w[bin2], symmetric."""
+    sel = (b1 >= lo) & (b1 < lo + N) & (b2 >= lo) & (b2 < lo + N)
+    i, j = b1[sel] - lo, b2[sel] - lo
+    v = c[sel].astype(np.float64)
+    if w is not None:
+        v = v * w[b1[sel]] * w[b2[sel]]
+    M = np.zeros((N, N))
+    M[i, j] = v
+    M[j, i] = v
+    return np.nan_to_num(M)
+
+
+@pytest.mark.parametrize("balanced,test", [(True, "ttest"), (True, "chitest"), (False, "ttest")])
+def test_tad_scan_from_pixels(SF, balanced, test):
+    """di_scan_pixels (device band from the pixel table + ICE weights) equals
+    di_scan on the dense balanced matrix bitwise, and the oracle."""
+    from hichap_master_amd import ice
+    from hichap_master_amd._lib import call, ptr
+    from hichap_master_amd.StructureFind import column_band
+    rng = np.random.default_rng(31)
+    b1, b2, c, off = synth.coo_genome([900, 1200], rng, A=30.0, trans_density=0.01)
+    n = int(off[-1])
+    w = ice.balance(b1, b2, c, n, off, max_iters=300)[0] if balanced else None
+    sf = SF(Res=10000)
+    sf.TAD_parameter_init(50000, 4000000, 3, 300000, test)
+    for k in range(2):
+        lo, N = int(off[k]), int(off[k + 1] - off[k])
+        M = _balanced_dense(b1, b2, c, w, lo, N)
+        gap, di = sf.di_scan_pixels(b1, b2, c, w, lo, N)
+        gd, dd = sf.di_scan(M)
+        np.testing.assert_array_equal(gap, gd)
+        np.testing.assert_array_equal(di, dd)
+        gref = list(structure_ref.get_gap(M, 50000, 10000))
+        gref = sorted(set(gref) | {0, N - 1})
+        np.testing.assert_array_equal(gap, gref)
+        dref = structure_ref.get_di(M, np.array(gref), 30, test)
+        np.testing.assert_allclose(di, dref, rtol=1e-11, atol=1e-300)
+        # the band itself, host mode
+        B = 30
+        band = np.empty((2 * B + 1, N))
+        cf = np.ascontiguousarray(c, dtype=np.float64)
+        call("hh_band_from_pixels", ptr(b1), ptr(b2), ptr(cf), b1.size,
+             None if w is None else ptr(w), 0 if w is None else n, lo, N, B, ptr(band), 0, None)
+        np.testing.assert_array_equal(band, column_band(M, B))
+
+
+def test_tad_scan_from_pixels_empty(SF):
+    sf = SF(Res=10000)
+    sf.TAD_parameter_init(50000, 4000000, 3, 300000, "ttest")
+    e = np.zeros(0, np.int64)
+    gap, di = sf.di_scan_pixels(e, e, np.zeros(0), None, 0, 200)
+    np.testing.assert_array_equal(gap, np.arange(200))
+    assert not di.any()

@@ -1,0 +1,3 @@
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 300 python -u bench.py --config c2 --steps 200 > gpurun_out/r1v8_c2_bench.log 2>&1
