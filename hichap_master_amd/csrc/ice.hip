@@ -790,20 +790,60 @@ __global__ __launch_bounds__(kBandThreads) void k_sweep_band(const uint8_t* __re
     }
 }
 
-__global__ void k_marg(TileDev T, const double* __restrict__ part, const long long* __restrict__ wide_ptr,
-                       const int32_t* __restrict__ wide_col, const double* __restrict__ wide_cnt,
-                       const double* __restrict__ diag, const uint16_t* __restrict__ row_group,
-                       const uint8_t* __restrict__ act, const double* __restrict__ b, long long row_lo,
-                       int nloc, const double* __restrict__ bpart, int nch, double* __restrict__ out) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nloc) return;
-    if (act[row_group[i]] == 0) return;
-    const int rbk = i / kR, rl = i % kR;
+// One block per row-block (thread = row): the block's unit descriptors are
+// staged in LDS in batches (every row used to re-read them from global
+// memory, one dependent chain per unit), the partial loads are issued
+// unconditionally from a clamped index and selected, so a batch's loads fly
+// together.  Summation order per row is unchanged (units in order, then band
+// chunks, wide entries, diagonal): bitwise the same marginals.
+constexpr int kMargThreads = kR;
+constexpr int kMargU = 256;  // unit descriptors per LDS batch
+__global__ __launch_bounds__(kMargThreads) void k_marg(TileDev T, const double* __restrict__ part,
+                                                       const long long* __restrict__ wide_ptr,
+                                                       const int32_t* __restrict__ wide_col,
+                                                       const double* __restrict__ wide_cnt,
+                                                       const double* __restrict__ diag,
+                                                       const uint16_t* __restrict__ row_group,
+                                                       const uint8_t* __restrict__ act, const double* __restrict__ b,
+                                                       long long row_lo, int nloc, const double* __restrict__ bpart,
+                                                       int nch, double* __restrict__ out) {
+    __shared__ int su_lo[kMargU], su_n[kMargU], su_slot[kMargU];
+    const int rbk = blockIdx.x, rl = threadIdx.x;
+    const int i = rbk * kR + rl;
+    const bool live = i < nloc && act[row_group[i < nloc ? i : 0]] != 0;
+    const int u0 = T.blk_unit_ptr[rbk], u1 = T.blk_unit_ptr[rbk + 1];
     double s = 0.0;
-    for (int u = T.blk_unit_ptr[rbk]; u < T.blk_unit_ptr[rbk + 1]; ++u) {
-        const int lo = T.u_rlo[u], hi = T.u_rhi[u];
-        if (rl >= lo && rl < hi) s += part[T.u_slot[u] + rl - lo];
+    for (int ub = u0; ub < u1; ub += kMargU) {
+        const int cnt = min(kMargU, u1 - ub);
+        __syncthreads();
+        if (rl < cnt) {
+            su_lo[rl] = T.u_rlo[ub + rl];
+            su_n[rl] = T.u_rhi[ub + rl] - T.u_rlo[ub + rl];
+            su_slot[rl] = T.u_slot[ub + rl];
+        }
+        __syncthreads();
+        if (live) {
+            int k = 0;
+            for (; k + 8 <= cnt; k += 8) {
+                double x[8];
+                bool in[8];
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const int o = rl - su_lo[k + q];
+                    in[q] = (unsigned)o < (unsigned)su_n[k + q];
+                    x[q] = part[su_slot[k + q] + (in[q] ? o : 0)];
+                }
+#pragma unroll
+                for (int q = 0; q < 8; ++q)
+                    if (in[q]) s += x[q];
+            }
+            for (; k < cnt; ++k) {
+                const int o = rl - su_lo[k];
+                if ((unsigned)o < (unsigned)su_n[k]) s += part[su_slot[k] + o];
+            }
+        }
     }
+    if (!live) return;
     for (int c = 0; c < nch; ++c) s += bpart[(long long)c * nloc + i];  // dense band chunks, fixed order
     for (long long q = wide_ptr[i]; q < wide_ptr[i + 1]; ++q) s = fma(wide_cnt[q], b[wide_col[q]], s);
     const double br = b[row_lo + i];
@@ -1075,7 +1115,7 @@ static void marg_weighted(hh_ice* S, double* out, hipStream_t s, bool timed, int
     }
     if (timed) HIP_CHECK(hipEventRecord(S->ev[2 * slot + 1], s));
     if (S->nloc == 0) return;
-    hipLaunchKernelGGL(k_marg, dim3(nblocks(S->nloc, kThreads)), dim3(kThreads), 0, s, m->dev(), S->part.p,
+    hipLaunchKernelGGL(k_marg, dim3(nblocks(S->nloc, kR)), dim3(kMargThreads), 0, s, m->dev(), S->part.p,
                        m->wide_ptr.p, m->wide_col.p, m->wide_cnt.p, m->diag.p, m->row_group.p, S->act(),
                        S->bias.p, (long long)m->row_lo, (int)S->nloc, S->bpart.p, (int)S->nch, out);
     HIP_CHECK(hipGetLastError());
