@@ -39,6 +39,24 @@ PEAK_F64_MFMA_TFS = 78.6  # MI355X fp64 matrix spec (AMD datasheet; the guide ha
 ALG_BYTES_PER_PIXEL = 12.0  # int32 bin1 + int32 bin2 + fp32 count
 
 
+def measure_shard_sweep_ms(st, nloc, stream, n=5):
+    """Average sweep time of this rank's shard (HIP-event registry), for the
+    partition refinement; leaves the registry off and empty."""
+    import torch
+    from hichap_master_amd import _lib
+    out = torch.zeros(max(int(nloc), 1), dtype=torch.float64, device="cuda")
+    st.marg_local(2, out, stream)
+    _lib.call("hh_ktime_reset")
+    _lib.call("hh_ktime_enable", 1)
+    for _ in range(n):
+        st.marg_local(2, out, stream)
+    torch.cuda.synchronize()
+    _lib.call("hh_ktime_enable", 0)
+    t, k = _lib.ktime("ice_sweep")
+    _lib.call("hh_ktime_reset")
+    return t / max(k, 1)
+
+
 def config(name, nnz=None):
     from hichap_master_amd import synth
     if name == "c4":
@@ -596,12 +614,31 @@ def main():
     rc, ru = ice.synth_row_counts(sizes, **kw)
     rank_rows = dist.partition_rows(rc, world)
     m = ice.ContactMatrix.synthetic(sizes, row_range=(rank_rows[rank], rank_rows[rank + 1]), **kw)
-    gen_s = time.perf_counter() - t0
-    inf = m.info()
-    nnz_total = int(ru.sum())
     opts = ice.IceOptions(tol=0.0, max_iters=1 << 30)
     st = ice.IceState(m, opts)
     stream = torch.cuda.current_stream().cuda_stream
+    if world > 1:
+        # small shards: the dense-band sweep on a side stream fills the tile
+        # kernels' tails (-6 % per shard at N=8, tools/probe_shards.py)
+        _lib.call("hh_tune", b"band_concurrent", 1)
+        if not os.environ.get("HH_NO_REFINE"):
+            # setup, untimed: one measured refinement of the row partition
+            # (payload bytes mis-price rows whose bytes sweep at different rates)
+            ms = torch.tensor([measure_shard_sweep_ms(st, rank_rows[rank + 1] - rank_rows[rank], stream)],
+                              dtype=torch.float64, device="cuda")
+            allms = [torch.zeros_like(ms) for _ in range(world)]
+            torch.distributed.all_gather(allms, ms)
+            cost = [float(x.item()) for x in allms]
+            rr2 = dist.partition_rows(dist.refine_weights(rc, rank_rows, cost), world)
+            if not np.array_equal(rr2, rank_rows):
+                st.close()
+                m.close()
+                rank_rows = rr2
+                m = ice.ContactMatrix.synthetic(sizes, row_range=(rank_rows[rank], rank_rows[rank + 1]), **kw)
+                st = ice.IceState(m, opts)
+    gen_s = time.perf_counter() - t0
+    inf = m.info()
+    nnz_total = int(ru.sum())
 
     def barrier():
         if torch.distributed.is_initialized():
@@ -670,7 +707,7 @@ def main():
             "nnz_iters_per_s": nnz_total * its,
             "config": {"workload": label, "n_bins": n, "nnz_upper": nnz_total,
                        "trans_fraction_target": tf, "resolution_bp": 40000 if args.config in ("c1", "c3") else 10000,
-                       "parallelism": f"rows sharded x{world}, {'RCCL' if backend == 'nccl' else backend} all-gather of marginals" if world > 1
+                       "parallelism": f"rows sharded x{world} (measured-cost partition), {'RCCL' if backend == 'nccl' else backend} all-gather of marginals" if world > 1
                        else "single GPU", "generate_s": round(gen_s, 2),
                        "entries_stored": inf["n_entries"], "slots_u32": inf["n_slots"],
                        "slots_u16": inf["n_slots_narrow"], "payload_bytes": inf["payload_bytes"],

@@ -46,6 +46,24 @@ def partition_rows(row_weight, world: int, align: int = ROW_BLOCK) -> np.ndarray
     return np.minimum(np.asarray(cuts, dtype=np.int64) * align, n)
 
 
+def refine_weights(row_weight, rank_rows, shard_cost) -> np.ndarray:
+    """Per-row weights rescaled so each shard's rows carry its measured cost
+    (e.g. sweep ms): w'_i = w_i * cost_r / W_r for the rows of shard r (W_r =
+    the shard's total weight).  Stored payload alone mis-prices rows whose
+    bytes sweep at different rates (4-bit band slots are VALU-bound, sparse
+    flat tiles latency-bound); one measured refinement of ``partition_rows``
+    levels the slowest rank.  A shard with zero weight keeps its weights."""
+    w = np.asarray(row_weight, dtype=np.float64)
+    rr = np.asarray(rank_rows, dtype=np.int64)
+    cost = np.asarray(shard_cost, dtype=np.float64)
+    out = w.copy()
+    for r in range(rr.size - 1):
+        W = w[rr[r]:rr[r + 1]].sum()
+        if W > 0 and cost[r] > 0:
+            out[rr[r]:rr[r + 1]] *= cost[r] / W
+    return out
+
+
 def lpt_assign(costs, world: int) -> np.ndarray:
     """Longest-processing-time-first: items in decreasing cost (ties by
     index) each go to the least-loaded rank (ties by lowest rank).  Returns

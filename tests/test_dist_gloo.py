@@ -108,3 +108,21 @@ def test_run_chromosomes_gloo():
     rng = np.random.default_rng(5)
     want = [int(synth.dense_chrom(n, rng, A=20.0).sum()) for n in [60, 90, 40, 75]]
     assert list(a) == want and list(b) == want
+
+
+def test_refine_weights_levels_measured_cost():
+    """A shard measured slower per unit weight gets fewer rows next time."""
+    w = np.ones(8192)
+    rr = dist.partition_rows(w, 2)
+    assert list(rr) == [0, 4096, 8192]
+    # rows of the second half sweep 3x slower per weight unit
+    w2 = dist.refine_weights(w, rr, [1.0, 3.0])
+    np.testing.assert_allclose(w2[:4096].sum(), 1.0)
+    np.testing.assert_allclose(w2[4096:].sum(), 3.0)
+    rr2 = dist.partition_rows(w2, 2)
+    assert rr2[1] > 4096 and rr2[1] % dist.ROW_BLOCK == 0
+    cost = [w2[a:b].sum() for a, b in zip(rr2[:-1], rr2[1:])]
+    assert max(cost) < 1.15 * (sum(cost) / 2)
+    # zero-weight shard untouched, equal costs keep the partition
+    np.testing.assert_array_equal(dist.refine_weights(np.zeros(10), [0, 5, 10], [1.0, 1.0]), np.zeros(10))
+    np.testing.assert_array_equal(dist.partition_rows(dist.refine_weights(w, rr, [2.0, 2.0]), 2), rr)

@@ -2,8 +2,10 @@
 hichap_master_amd.dist.balance_sharded with the HIP backend (IceState over a
 row shard each), both ranks on cuda:0 with the gloo exchange (RCCL refuses two
 ranks on one device; the RCCL path is covered at world 1 in test_ice_gpu.py
-and at N>1 by the driver's scaling bench).  Every rank's weights equal the
-one-process HIP run bitwise and the oracle within the ICE tolerance."""
+and at N>1 by the driver's scaling bench), with the dense-band sweep on a
+side stream as bench.py runs shards.  Every rank's weights equal the
+one-process HIP run (default stream order) bitwise and the oracle within the
+ICE tolerance."""
 import os
 import socket
 import tempfile
@@ -29,6 +31,7 @@ def _worker(rank, world, port, case, cis_only, outdir):
     torch.cuda.set_device(0)
     _lib.load()
     _lib.call("hh_set_device", 0)
+    _lib.call("hh_tune", b"band_concurrent", 1)  # as bench.py runs N > 1 shards
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     tdist.init_process_group("gloo", rank=rank, world_size=world)
     try:

@@ -370,3 +370,19 @@ def test_saturated_counts_match_oracle(ice):
     assert st["iters"] == sr["iters"] == 60 and not st["converged"]
     np.testing.assert_allclose(st["var"], sr["var"], rtol=1e-9)
     np.testing.assert_allclose(w, wr, rtol=1e-9, equal_nan=True)
+
+
+def test_band_concurrent_bitwise(ice):
+    """The dense-band sweep on a side stream (hh_tune band_concurrent, used for
+    N > 1 shards) writes its own partials: weights bitwise equal."""
+    from hichap_master_amd import _lib
+    b1, b2, c, off = _case(17, sizes=(1500, 900), A=60.0)
+    n = int(off[-1])
+    w0, s0 = ice.balance(b1, b2, c, n, off, max_iters=300)
+    _lib.call("hh_tune", b"band_concurrent", 1)
+    try:
+        w1, s1 = ice.balance(b1, b2, c, n, off, max_iters=300)
+    finally:
+        _lib.call("hh_tune", b"band_concurrent", 0)
+    np.testing.assert_array_equal(w1, w0)
+    assert s1["iters"] == s0["iters"]
