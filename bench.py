@@ -624,18 +624,28 @@ def main():
         if not os.environ.get("HH_NO_REFINE"):
             # setup, untimed: one measured refinement of the row partition
             # (payload bytes mis-price rows whose bytes sweep at different rates)
-            ms = torch.tensor([measure_shard_sweep_ms(st, rank_rows[rank + 1] - rank_rows[rank], stream)],
-                              dtype=torch.float64, device="cuda")
-            allms = [torch.zeros_like(ms) for _ in range(world)]
-            torch.distributed.all_gather(allms, ms)
-            cost = [float(x.item()) for x in allms]
-            rr2 = dist.partition_rows(dist.refine_weights(rc, rank_rows, cost), world)
-            if not np.array_equal(rr2, rank_rows):
+            def costs():
+                ms = torch.tensor([measure_shard_sweep_ms(st, rank_rows[rank + 1] - rank_rows[rank], stream)],
+                                  dtype=torch.float64, device="cuda")
+                allms = [torch.zeros_like(ms) for _ in range(world)]
+                torch.distributed.all_gather(allms, ms)
+                return [float(x.item()) for x in allms]
+
+            def rebuild(rr):
+                nonlocal m, st, rank_rows
                 st.close()
                 m.close()
-                rank_rows = rr2
+                rank_rows = rr
                 m = ice.ContactMatrix.synthetic(sizes, row_range=(rank_rows[rank], rank_rows[rank + 1]), **kw)
                 st = ice.IceState(m, opts)
+
+            cost = costs()
+            rr0 = rank_rows
+            rr2 = dist.partition_rows(dist.refine_weights(rc, rank_rows, cost), world)
+            if not np.array_equal(rr2, rank_rows):
+                rebuild(rr2)
+                if max(costs()) > max(cost):  # measured worse (noise): keep the payload partition
+                    rebuild(rr0)
     gen_s = time.perf_counter() - t0
     inf = m.info()
     nnz_total = int(ru.sum())
