@@ -327,10 +327,11 @@ def test_full_size_balanced_marginals(ice, res, target, diploid):
     host from the exported pixels of the first 4096 rows and the returned
     weights, are 1 within the convergence tolerance -- a size-independent
     property covering the band, tiled and flat sweeps at their production
-    shapes.  (C3's spec -- 8e8 pixels at 40 kb with 20 % trans -- saturates
-    the generator's calibration (A = 1e6, every cis pixel dense) and that
-    matrix does not converge under cooler's algorithm either: the oracle and
-    the GPU agree to 1e-15 on it, tools/probe_conv_small.py.)"""
+    shapes.  (C3's 8e8 pixels at 40 kb with 20 % trans saturates the
+    generator's calibration (A = 1e6, every cis pixel dense) and that matrix
+    does not converge under cooler's algorithm either: the oracle and the GPU
+    agree to 1e-15 on it, tools/probe_conv_small.py.  bench.py's C3 therefore
+    uses 85 % trans: test_config_size_balanced_marginals.)"""
     sizes = synth.genome_bins(res, diploid=diploid)
     A, td = synth.calibrate(sizes, target, 0.2)
     kw = dict(A=A, trans_density=td, comp_block=200, seed=20201015)
@@ -386,3 +387,51 @@ def test_band_concurrent_bitwise(ice):
         _lib.call("hh_tune", b"band_concurrent", 0)
     np.testing.assert_array_equal(w1, w0)
     assert s1["iters"] == s0["iters"]
+
+
+def test_c1_config_matches_oracle(ice):
+    """BASELINE C1 at its own size (one chromosome, 5 000 bins at 40 kb,
+    ~2e6 pixels, cooler's 200-iteration cap): GPU == oracle."""
+    sizes = [5000]
+    A, td = synth.calibrate(sizes, 2e6, 0.0)
+    kw = dict(A=A, trans_density=td, comp_block=200, seed=20201015)
+    m = ice.ContactMatrix.synthetic(sizes, **kw)
+    b1, b2, c = m.export_upper()
+    assert 1.5e6 < b1.size < 2.5e6
+    w, st = ice.balance_matrix(m, ice.IceOptions(max_iters=200))
+    m.close()
+    wr, sr = ice_ref.balance(b1, b2, c, 5000, np.array([0, 5000]), max_iters=200)
+    assert st["iters"] == sr["iters"] and st["converged"] == sr["converged"]
+    np.testing.assert_allclose(w, wr, rtol=1e-9, equal_nan=True)
+
+
+@pytest.mark.parametrize("cfg", ["c2", "c3"])
+def test_config_size_balanced_marginals(ice, cfg):
+    """BASELINE C2 (hg19 chr1 at 10 kb, 5e7 pixels, cis only) and C3 (hg19
+    whole genome at 40 kb, 8e8 pixels, 85 % trans) at full size: ICE
+    converges and the balanced marginals of the first 4096 rows, recomputed
+    on the host from the exported pixels, are 1 within tolerance."""
+    if cfg == "c2":
+        sizes = synth.chrom_bins([synth.HG19["1"]], 10000)
+        A, td = synth.calibrate(sizes, 5e7, 0.0)
+    else:
+        sizes = synth.genome_bins(40000)
+        A, td = synth.calibrate(sizes, 8e8, 0.85)
+    kw = dict(A=A, trans_density=td, comp_block=200, seed=20201015)
+    m = ice.ContactMatrix.synthetic(sizes, **kw)
+    w, st = ice.balance_matrix(m, ice.IceOptions(max_iters=4000))
+    m.close()
+    assert st["converged"] and st["var"] < 1e-5, (st["var"], st["iters"])
+    rows = 4096
+    ms = ice.ContactMatrix.synthetic(sizes, row_range=(0, rows), **kw)
+    b1, b2, c = ms.export_upper()
+    ms.close()
+    wz = np.nan_to_num(w)
+    contrib = c * wz[b1] * wz[b2]
+    marg = np.bincount(b1, contrib, minlength=rows + 1)[:rows] + \
+        np.bincount(np.minimum(b2, rows), contrib, minlength=rows + 1)[:rows]
+    ok = ~np.isnan(w[:rows])
+    assert ok.sum() > rows // 2
+    mr = marg[ok]
+    assert abs(mr.mean() - 1.0) < 5e-3, mr.mean()
+    assert mr.var() < 1e-4, mr.var()
