@@ -137,57 +137,72 @@ __global__ __launch_bounds__(256) void k_oe_center(const double* __restrict__ M,
     Z[t] = v;
 }
 
-// Cov tile (bi, bj), bi <= bj, 64 x 64: 4 waves x (2 x 2) MFMA 16x16x4 f64 tiles.
-// LDS rows padded to 80 doubles so the 16-lane halves of a 32-lane LDS group
-// land on disjoint banks.
-constexpr int kLdS = 80;
-__global__ __launch_bounds__(256) void k_syrk(const double* __restrict__ Z, long long ld, long long Kpad,
+// Cov tile (bi, bj), bi <= bj, 128 x 128: 4 waves x (4 x 4) MFMA 16x16x4 f64
+// tiles (64 x 64 per wave: 16 flops per byte staged, twice the 64 x 64
+// tile's, which was bound by the L2 -> CU stream at 0.59 of the fp64 matrix
+// peak).  K steps of 16 rows; the next step's global loads are issued before
+// the current step's MFMAs (register double buffer), one LDS buffer.  LDS rows
+// padded to 144 doubles (= 16 mod 32) so the two 16-lane row groups of a
+// 32-lane LDS pass land on disjoint banks.
+constexpr int kSyT = 128;
+constexpr int kLdS = kSyT + 16;
+__global__ __launch_bounds__(256, 2) void k_syrk(const double* __restrict__ Z, long long ld, long long Kpad,
                                               long long nt, double scale, double* __restrict__ C, long long ldc) {
     __shared__ __attribute__((aligned(16))) double As[16][kLdS];
     __shared__ __attribute__((aligned(16))) double Bs[16][kLdS];
     long long bi = 0, rem = blockIdx.x;
     while (rem >= nt - bi) { rem -= nt - bi; ++bi; }
     const long long bj = bi + rem;
-    const long long i0 = bi * 64, j0 = bj * 64;
+    const long long i0 = bi * kSyT, j0 = bj * kSyT;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int wr = (w >> 1) * 32, wc = (w & 1) * 32;
+    const int wr = (w >> 1) * 64, wc = (w & 1) * 64;
     const bool diag = bi == bj;
-    d4 acc[2][2];
+    d4 acc[4][4];
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+    for (int a = 0; a < 4; ++a)
 #pragma unroll
-        for (int b = 0; b < 2; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
-    const int lr = threadIdx.x / 16, lc = (threadIdx.x % 16) * 4;  // 16 rows x 64 cols, 4 doubles each
+        for (int b = 0; b < 4; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
+    // 16 rows x 128 cols per operand: thread -> rows lr, lr + 8; 4 doubles at lc
+    const int lr = threadIdx.x / 32, lc = (threadIdx.x % 32) * 4;
+    d4 va[2], vb[2];
+    auto load = [&](long long k0) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            va[h] = *reinterpret_cast<const d4*>(Z + (k0 + lr + 8 * h) * ld + i0 + lc);
+            vb[h] = diag ? va[h] : *reinterpret_cast<const d4*>(Z + (k0 + lr + 8 * h) * ld + j0 + lc);
+        }
+    };
+    load(0);
     for (long long k0 = 0; k0 < Kpad; k0 += 16) {
-        const double* za = Z + (k0 + lr) * ld + i0 + lc;
-        const d4 va = *reinterpret_cast<const d4*>(za);
-        d4 vb = va;
-        if (!diag) vb = *reinterpret_cast<const d4*>(Z + (k0 + lr) * ld + j0 + lc);
+        __syncthreads();  // previous step's LDS reads are done
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            *reinterpret_cast<d4*>(&As[lr + 8 * h][lc]) = va[h];
+            *reinterpret_cast<d4*>(&Bs[lr + 8 * h][lc]) = vb[h];
+        }
         __syncthreads();
-        *reinterpret_cast<d4*>(&As[lr][lc]) = va;
-        *reinterpret_cast<d4*>(&Bs[lr][lc]) = vb;
-        __syncthreads();
+        if (k0 + 16 < Kpad) load(k0 + 16);
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
             const int kk = s * 4 + (lane >> 4);
-            double a[2], b[2];
+            double a[4], b[4];
 #pragma unroll
-            for (int t = 0; t < 2; ++t) {
+            for (int t = 0; t < 4; ++t) {
                 a[t] = As[kk][wr + t * 16 + (lane & 15)];
                 b[t] = Bs[kk][wc + t * 16 + (lane & 15)];
             }
 #pragma unroll
-            for (int ta = 0; ta < 2; ++ta)
+            for (int ta = 0; ta < 4; ++ta)
 #pragma unroll
-                for (int tb = 0; tb < 2; ++tb)
+                for (int tb = 0; tb < 4; ++tb)
                     acc[ta][tb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ta], b[tb], acc[ta][tb], 0, 0, 0);
         }
     }
     // C/D layout of v_mfma_f64_16x16x4_f64: col = lane & 15, row = (lane >> 4) + 4 * reg
 #pragma unroll
-    for (int ta = 0; ta < 2; ++ta)
+    for (int ta = 0; ta < 4; ++ta)
 #pragma unroll
-        for (int tb = 0; tb < 2; ++tb)
+        for (int tb = 0; tb < 4; ++tb)
 #pragma unroll
             for (int reg = 0; reg < 4; ++reg) {
                 const long long gi = i0 + wr + ta * 16 + (lane >> 4) + 4 * reg;
@@ -460,7 +475,7 @@ struct hh_comp {
     const double* Mp = nullptr;
     DBuf<double> dec;            // N
     DBuf<long long> ng;          // n
-    long long n = 0, ld = 0;     // Cor leading dimension (n padded to 64)
+    long long n = 0, ld = 0;     // Cor leading dimension (n padded to 128)
     DBuf<double> cor;            // ld x ld
     int iters = 0;
 };
@@ -654,7 +669,7 @@ int hh_comp_correlation(hh_comp* c, const double* decline, const int64_t* ng, in
         hipStream_t s = as_stream(stream);
         const long long N = c->N;
         c->n = n;
-        c->ld = (n + 63) / 64 * 64;
+        c->ld = (n + kSyT - 1) / kSyT * kSyT;  // whole k_syrk tiles (a multiple of 64 for the other kernels)
         c->dec.alloc(N);
         c->dec.upload(decline, N, s);
         c->ng.alloc(n);
@@ -674,7 +689,7 @@ int hh_comp_correlation(hh_comp* c, const double* decline, const int64_t* ng, in
                            c->ng.p, mu.p, N, (long long)n, Npad, c->ld, Z.p);
         // Cov = Z^T Z * (1 / (N - 1))  (np.cov: c *= true_divide(1, fact))
         DBuf<double> cov((size_t)c->ld * c->ld);
-        const long long nt = c->ld / 64;
+        const long long nt = c->ld / kSyT;
         {
             HH_KTIME("k_syrk", s);
             hipLaunchKernelGGL(k_syrk, dim3((unsigned)(nt * (nt + 1) / 2)), dim3(256), 0, s, Z.p, c->ld, Npad, nt,
