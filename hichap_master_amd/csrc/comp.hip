@@ -218,7 +218,7 @@ __global__ __launch_bounds__(256, 2) void k_syrk(const double* __restrict__ Z, l
 __global__ void k_corr_norm_oop(const double* __restrict__ Cov, long long n, long long ldc,
                                 double* __restrict__ Cor) {
     const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= n * ldc) return;
+    if (t >= ldc * ldc) return;  // the padding rows too: the split-K products read them (x 0)
     const long long i = t / ldc, j = t % ldc;
     double v = 0.0;
     if (i < n && j < n) {
