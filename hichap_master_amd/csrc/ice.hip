@@ -1015,10 +1015,12 @@ struct hh_ice {
     double sweep_ms = 0.0, iter_ms = 0.0;
     int32_t sweep_launches = 0;
     // side stream for the dense-band sweep, run beside the tile sweep
-    hipStream_t side = nullptr;
-    hipEvent_t fork = nullptr, join = nullptr;
+    hipStream_t side = nullptr, side2 = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr, join2 = nullptr;
     ~hh_ice() {
         for (auto e : ev) (void)hipEventDestroy(e);
+        if (join2) (void)hipEventDestroy(join2);
+        if (side2) (void)hipStreamDestroy(side2);
         if (fork) (void)hipEventDestroy(fork);
         if (join) (void)hipEventDestroy(join);
         if (side) (void)hipStreamDestroy(side);
@@ -1036,35 +1038,45 @@ namespace hh {
 // Tuning knobs (hh_tune; no effect on results except the ablations).
 static int g_sweep_nb = 2;
 static int g_sweep_ablate = 0;
-static int g_band_concurrent = 0;  // dense-band sweep on a side stream, beside the tiles
+// Default: three streams per sweep -- band kernels (side), tiled kernel (side2),
+// flat kernel (main) -- so each kernel's ramp and tail overlap the others'
+// (C4: 4.80 -> 4.69 ms; the band beside tiled+flat on one stream alone was
+// +2 %, profiles/r1v8_knobs_split.log).  All write disjoint partials.
+static int g_band_concurrent = 1;  // dense-band sweep on a side stream, beside the tiles
+static int g_split_tiles = 1;      // with band_concurrent: tiled kernel on a second side stream
 
 template <int NB, int ABL>
-static void launch_sweep(const hh_matrix* m, const uint8_t* act, const double* b, double* part, hipStream_t s) {
+static void launch_sweep(const hh_matrix* m, const uint8_t* act, const double* b, double* part, hipStream_t s,
+                         hipStream_t s_tiled) {
     const int n_tiled = (int)(m->n_units - m->n_units_flat), n_flat = (int)m->n_units_flat;
     if (n_tiled)
-        hipLaunchKernelGGL((k_sweep_tiled<NB, ABL>), dim3((unsigned)n_tiled), dim3(kSweepThreads), 0, s, m->dev(),
-                           act, n_tiled, b, (long long)m->n_bins, part);
+        hipLaunchKernelGGL((k_sweep_tiled<NB, ABL>), dim3((unsigned)n_tiled), dim3(kSweepThreads), 0, s_tiled,
+                           m->dev(), act, n_tiled, b, (long long)m->n_bins, part);
     if (n_flat)
         hipLaunchKernelGGL((k_sweep_flat<kFlatU, ABL>), dim3((unsigned)n_flat), dim3(kSweepThreads), 0, s, m->dev(),
                            act, n_flat, n_tiled, b, (long long)m->n_bins, part);
 }
 
 template <int ABL>
-static void launch_sweep_nb(const hh_matrix* m, const uint8_t* act, const double* b, double* part, hipStream_t s) {
+static void launch_sweep_nb(const hh_matrix* m, const uint8_t* act, const double* b, double* part, hipStream_t s,
+                            hipStream_t st) {
     switch (g_sweep_nb) {
-        case 1: launch_sweep<1, ABL>(m, act, b, part, s); break;
-        case 2: launch_sweep<2, ABL>(m, act, b, part, s); break;
-        case 8: launch_sweep<8, ABL>(m, act, b, part, s); break;
-        default: launch_sweep<4, ABL>(m, act, b, part, s); break;
+        case 1: launch_sweep<1, ABL>(m, act, b, part, s, st); break;
+        case 2: launch_sweep<2, ABL>(m, act, b, part, s, st); break;
+        case 8: launch_sweep<8, ABL>(m, act, b, part, s, st); break;
+        default: launch_sweep<4, ABL>(m, act, b, part, s, st); break;
     }
 }
 
-static void sweep(const hh_matrix* m, const uint8_t* act, const double* b, double* part, hipStream_t s) {
+// s_tiled: stream of the tiled kernel (= s, or a side stream joined by the caller)
+static void sweep(const hh_matrix* m, const uint8_t* act, const double* b, double* part, hipStream_t s,
+                  hipStream_t s_tiled = nullptr) {
     if (m->n_units == 0) return;
+    if (!s_tiled) s_tiled = s;
     switch (g_sweep_ablate) {
-        case 1: launch_sweep_nb<1>(m, act, b, part, s); break;
-        case 2: launch_sweep_nb<2>(m, act, b, part, s); break;
-        default: launch_sweep_nb<0>(m, act, b, part, s); break;
+        case 1: launch_sweep_nb<1>(m, act, b, part, s, s_tiled); break;
+        case 2: launch_sweep_nb<2>(m, act, b, part, s, s_tiled); break;
+        default: launch_sweep_nb<0>(m, act, b, part, s, s_tiled); break;
     }
     HIP_CHECK(hipGetLastError());
 }
@@ -1106,7 +1118,12 @@ static void marg_weighted(hh_ice* S, double* out, hipStream_t s, bool timed, int
             HIP_CHECK(hipStreamWaitEvent(S->side, S->fork, 0));
             sweep_band(S, S->side);
             HIP_CHECK(hipEventRecord(S->join, S->side));
-            sweep(m, S->act(), S->bias.p, S->part.p, s);
+            if (g_split_tiles) HIP_CHECK(hipStreamWaitEvent(S->side2, S->fork, 0));
+            sweep(m, S->act(), S->bias.p, S->part.p, s, g_split_tiles ? S->side2 : s);
+            if (g_split_tiles) {
+                HIP_CHECK(hipEventRecord(S->join2, S->side2));
+                HIP_CHECK(hipStreamWaitEvent(s, S->join2, 0));
+            }
             HIP_CHECK(hipStreamWaitEvent(s, S->join, 0));
         } else {
             sweep(m, S->act(), S->bias.p, S->part.p, s);
@@ -1174,6 +1191,9 @@ int hh_tune(const char* key, int64_t value) {
             HH_REQUIRE(value >= -1 && value <= kBandMaxW && (value <= 0 || value % 16 == 0),
                        "band_w: -1 (auto), 0 (off) or a multiple of 16 <= 16384");
             g_band_w = value;
+        } else if (k == "split_tiles") {
+            HH_REQUIRE(value == 0 || value == 1, "split_tiles in {0, 1}");
+            g_split_tiles = (int)value;
         } else if (k == "band_concurrent") {
             HH_REQUIRE(value == 0 || value == 1, "band_concurrent in {0, 1}");
             g_band_concurrent = (int)value;
@@ -1234,6 +1254,8 @@ int hh_ice_create(hh_matrix* m, const hh_ice_opts* o, hh_ice** out) {
         HIP_CHECK(hipStreamCreateWithFlags(&S->side, hipStreamNonBlocking));
         HIP_CHECK(hipEventCreateWithFlags(&S->fork, hipEventDisableTiming));
         HIP_CHECK(hipEventCreateWithFlags(&S->join, hipEventDisableTiming));
+        HIP_CHECK(hipStreamCreateWithFlags(&S->side2, hipStreamNonBlocking));
+        HIP_CHECK(hipEventCreateWithFlags(&S->join2, hipEventDisableTiming));
 
         S->tile_cnt.alloc(std::max(S->n_tiles, 1));
         S->tile_sum.alloc(std::max(S->n_tiles, 1));

@@ -373,18 +373,22 @@ def test_saturated_counts_match_oracle(ice):
     np.testing.assert_allclose(w, wr, rtol=1e-9, equal_nan=True)
 
 
-def test_band_concurrent_bitwise(ice):
-    """The dense-band sweep on a side stream (hh_tune band_concurrent, used for
-    N > 1 shards) writes its own partials: weights bitwise equal."""
+@pytest.mark.parametrize("conc,split", [(1, 0), (0, 0)])
+def test_band_concurrent_bitwise(ice, conc, split):
+    """Sweep kernels on one stream, or the band sweep / tiled kernel on side
+    streams (hh_tune band_concurrent / split_tiles; default 1 / 1): each
+    kernel writes its own partials, so the weights are bitwise equal."""
     from hichap_master_amd import _lib
     b1, b2, c, off = _case(17, sizes=(1500, 900), A=60.0)
     n = int(off[-1])
-    w0, s0 = ice.balance(b1, b2, c, n, off, max_iters=300)
-    _lib.call("hh_tune", b"band_concurrent", 1)
+    w0, s0 = ice.balance(b1, b2, c, n, off, max_iters=300)  # defaults: three streams
+    _lib.call("hh_tune", b"band_concurrent", conc)
+    _lib.call("hh_tune", b"split_tiles", split)
     try:
         w1, s1 = ice.balance(b1, b2, c, n, off, max_iters=300)
     finally:
-        _lib.call("hh_tune", b"band_concurrent", 0)
+        _lib.call("hh_tune", b"band_concurrent", 1)
+        _lib.call("hh_tune", b"split_tiles", 1)
     np.testing.assert_array_equal(w1, w0)
     assert s1["iters"] == s0["iters"]
 
