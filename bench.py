@@ -735,7 +735,7 @@ def main():
             real_b = shard_real
             if world > 1:
                 traffic = None  # the committed PMC summary is for the 1-GPU matrix
-            out["roofline"] = {"bound": "hbm", "kernel": "ice sweep = k_sweep_tiled + k_sweep_flat + k_sweep_band<8> + 2 x k_sweep_band<4>",
+            out["roofline"] = {"bound": "hbm", "kernel": "ice sweep span: k_sweep_flat | k_sweep_tiled | k_sweep_band<8> + 2 x k_sweep_band<4> on three streams (HIP events around the sweep; rocprof per-sweep span: tools/sweep_span.py)",
                                "achieved": achieved,
                                "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS,
                                "traffic": traffic,
