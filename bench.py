@@ -618,9 +618,8 @@ def main():
     st = ice.IceState(m, opts)
     stream = torch.cuda.current_stream().cuda_stream
     if world > 1:
-        # small shards: the dense-band sweep on a side stream fills the tile
-        # kernels' tails (-6 % per shard at N=8, tools/probe_shards.py)
-        _lib.call("hh_tune", b"band_concurrent", 1)
+        # (the sweep's three streams are the library default for shards of
+        # >= 1 GB payload: C4 at N=8 has 1.85 GB per shard)
         if not os.environ.get("HH_NO_REFINE"):
             # setup, untimed: one measured refinement of the row partition
             # (payload bytes mis-price rows whose bytes sweep at different rates)

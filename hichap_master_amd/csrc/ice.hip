@@ -1044,6 +1044,9 @@ static int g_sweep_ablate = 0;
 // +2 %, profiles/r1v8_knobs_split.log).  All write disjoint partials.
 static int g_band_concurrent = 1;  // dense-band sweep on a side stream, beside the tiles
 static int g_split_tiles = 1;      // with band_concurrent: tiled kernel on a second side stream
+// below this payload the fork / join costs more than the overlap gains (C2,
+// 0.2 GB: 4 620 -> 4 300 it/s with three streams; N=8 C4 shards, 1.85 GB, gain)
+static int64_t g_conc_min_bytes = 1LL << 30;
 
 template <int NB, int ABL>
 static void launch_sweep(const hh_matrix* m, const uint8_t* act, const double* b, double* part, hipStream_t s,
@@ -1112,7 +1115,9 @@ static void marg_weighted(hh_ice* S, double* out, hipStream_t s, bool timed, int
         // the two sweeps write disjoint partials (part / bpart): the band
         // kernel runs on a side stream so its blocks fill the CUs the tile
         // kernel leaves idle (both are HBM-bound; neither saturates alone)
-        const bool conc = g_band_concurrent && S->nch && S->nloc && m->n_units;
+        const bool conc = g_band_concurrent && S->nch && S->nloc && m->n_units &&
+                          4 * m->n_slots + 2 * m->n_slots_narrow + (int64_t)m->band.n + (int64_t)m->band4.n >=
+                              g_conc_min_bytes;
         if (conc) {
             HIP_CHECK(hipEventRecord(S->fork, s));
             HIP_CHECK(hipStreamWaitEvent(S->side, S->fork, 0));
@@ -1191,6 +1196,9 @@ int hh_tune(const char* key, int64_t value) {
             HH_REQUIRE(value >= -1 && value <= kBandMaxW && (value <= 0 || value % 16 == 0),
                        "band_w: -1 (auto), 0 (off) or a multiple of 16 <= 16384");
             g_band_w = value;
+        } else if (k == "conc_min_bytes") {
+            HH_REQUIRE(value >= 0, "conc_min_bytes >= 0");
+            g_conc_min_bytes = value;
         } else if (k == "split_tiles") {
             HH_REQUIRE(value == 0 || value == 1, "split_tiles in {0, 1}");
             g_split_tiles = (int)value;

@@ -31,7 +31,7 @@ def _worker(rank, world, port, case, cis_only, outdir):
     torch.cuda.set_device(0)
     _lib.load()
     _lib.call("hh_set_device", 0)
-    _lib.call("hh_tune", b"band_concurrent", 1)  # as bench.py runs N > 1 shards
+    _lib.call("hh_tune", b"conc_min_bytes", 0)  # three sweep streams even on this small shard
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     tdist.init_process_group("gloo", rank=rank, world_size=world)
     try:

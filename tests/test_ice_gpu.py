@@ -373,22 +373,26 @@ def test_saturated_counts_match_oracle(ice):
     np.testing.assert_allclose(w, wr, rtol=1e-9, equal_nan=True)
 
 
-@pytest.mark.parametrize("conc,split", [(1, 0), (0, 0)])
+@pytest.mark.parametrize("conc,split", [(1, 0), (1, 1)])
 def test_band_concurrent_bitwise(ice, conc, split):
     """Sweep kernels on one stream, or the band sweep / tiled kernel on side
-    streams (hh_tune band_concurrent / split_tiles; default 1 / 1): each
-    kernel writes its own partials, so the weights are bitwise equal."""
+    streams (hh_tune band_concurrent / split_tiles, default on for matrices of
+    >= conc_min_bytes of payload; forced here on a small one): each kernel
+    writes its own partials, so the weights are bitwise equal."""
     from hichap_master_amd import _lib
     b1, b2, c, off = _case(17, sizes=(1500, 900), A=60.0)
     n = int(off[-1])
-    w0, s0 = ice.balance(b1, b2, c, n, off, max_iters=300)  # defaults: three streams
-    _lib.call("hh_tune", b"band_concurrent", conc)
-    _lib.call("hh_tune", b"split_tiles", split)
+    _lib.call("hh_tune", b"band_concurrent", 0)
     try:
+        w0, s0 = ice.balance(b1, b2, c, n, off, max_iters=300)  # one stream
+        _lib.call("hh_tune", b"band_concurrent", conc)
+        _lib.call("hh_tune", b"split_tiles", split)
+        _lib.call("hh_tune", b"conc_min_bytes", 0)
         w1, s1 = ice.balance(b1, b2, c, n, off, max_iters=300)
     finally:
         _lib.call("hh_tune", b"band_concurrent", 1)
         _lib.call("hh_tune", b"split_tiles", 1)
+        _lib.call("hh_tune", b"conc_min_bytes", 1 << 30)
     np.testing.assert_array_equal(w1, w0)
     assert s1["iters"] == s0["iters"]
 
