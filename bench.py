@@ -159,7 +159,7 @@ def tad_scan_bench(m, st, stream, reps=5, res=10000, min_tad=200000, window=6000
 
 
 C5_RES = 25000
-C5_STREAMS = int(os.environ.get("HH_C5_STREAMS", "4"))
+C5_STREAMS = int(os.environ.get("HH_C5_STREAMS", "8"))
 
 
 def c5_sizes():
@@ -217,7 +217,7 @@ def run_c5(args, world, rank, local):
         ice.synth_dense(sizes, k, mats[k].data_ptr(), **c5_synth_kw())
     torch.cuda.synchronize()
     gen_s = time.perf_counter() - t0
-    ng = {}
+    ng, prods, conv, phases = {}, {}, {}, {}
     # chromosomes run concurrently on C5_STREAMS HIP streams (one host thread
     # each; the C-ABI releases the GIL): the small chromosomes' PCA kernels are
     # latency-bound, so overlapping them keeps the GPU busy.
@@ -229,11 +229,19 @@ def run_c5(args, world, rank, local):
         torch.cuda.set_device(local)  # the HIP current device is per host thread
         _lib.call("hh_set_device", local)
         with torch.cuda.stream(st):
+            t_a = time.perf_counter()
             sf = StructureFind(Res=C5_RES, stream=st.cuda_stream)
             dec, G, NG = sf.Distance_Decay(M=mats[k], G_array=None)
+            t_b = time.perf_counter()
             pcs, Cor, OE = sf.Get_PCA(distance_bin=dec, M=mats[k], NG_array=NG)
+            t_c = time.perf_counter()
             sf.Select_PC_new(Cor, OE[NG], pcs)
+            t_d = time.perf_counter()
+            for key, v in (("decay", t_b - t_a), ("get_pca", t_c - t_b), ("select", t_d - t_c)):
+                phases[key] = phases.get(key, 0.0) + v
             ng[k] = NG.size
+            prods[k] = sf.pca_status["products"]
+            conv[k] = sf.pca_status["converged"]
 
     def step(nstreams=C5_STREAMS):
         # largest first, dealt round-robin to the stream workers
@@ -258,6 +266,12 @@ def run_c5(args, world, rank, local):
     elapsed = time.perf_counter() - t_start
     # per-kernel durations from one more pass with the streams serialised
     # (concurrent streams share the CUs, so their event spans overlap)
+    phases.clear()
+    t_ser = time.perf_counter()
+    step(1)
+    torch.cuda.synchronize()
+    serial_ms = 1000.0 * (time.perf_counter() - t_ser)
+    serial_phases = {k: round(1000.0 * v, 2) for k, v in phases.items()}
     _lib.call("hh_ktime_reset")
     _lib.call("hh_ktime_enable", 1)
     step(1)
@@ -271,7 +285,19 @@ def run_c5(args, world, rank, local):
     elapsed = float(tt.item())
     if rank == 0:
         flops = sum(float(sizes[k]) * ng[k] * (ng[k] + 1) for k in mine)  # one (serialised) pass
-        achieved = flops / (syrk_ms / 1000.0) / 1e12 if syrk_ms > 0 else None
+        syrk_tfs = flops / (syrk_ms / 1000.0) / 1e12 if syrk_ms > 0 else None
+        # Cor . V products: HBM-bound stream of the padded ld x ld correlation
+        ld = {k: (ng[k] + 127) // 128 * 128 for k in mine}
+        mul_bytes = sum(8.0 * ld[k] * ld[k] * prods[k] for k in mine)
+        mul_gbs = mul_bytes / (mul_ms / 1000.0) / 1e9 if mul_ms > 0 else None
+        syrk_side = {"bound": "mfma", "kernel": "k_syrk", "achieved": syrk_tfs, "peak": PEAK_F64_MFMA_TFS,
+                     "unit": "TFLOP/s", "frac": (syrk_tfs / PEAK_F64_MFMA_TFS) if syrk_tfs else None,
+                     "total_ms": syrk_ms, "launches": syrk_n, "flops": flops}
+        mul_side = {"bound": "hbm", "kernel": "k_cor_mul_part (+ k_cor_mul_sum)", "achieved": mul_gbs,
+                    "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": (mul_gbs / PEAK_HBM_GBS) if mul_gbs else None,
+                    "total_ms": mul_ms, "launches": mul_n, "alg_bytes": mul_bytes,
+                    "alg_bytes_note": "8 B x ld^2 (the padded correlation) per Cor.V product"}
+        dom, other = (mul_side, syrk_side) if mul_ms > syrk_ms else (syrk_side, mul_side)
         out = {
             "metric": "compartment PCA chromosomes/sec (C5: hg19 autosomes at 25 kb, dense per-chrom)",
             "value": len(sizes) * args.steps / elapsed, "unit": "chromosomes/s", "n_gpus": world,
@@ -281,14 +307,13 @@ def run_c5(args, world, rank, local):
             "config": {"workload": "hg19-autosomes-25kb-compartment", "n_chroms": len(sizes),
                        "bins_total": int(np.sum(sizes)), "largest_N": int(max(sizes)),
                        "parallelism": f"chromosomes LPT over {world} ranks" if world > 1 else "single GPU",
-                       "generate_s": round(gen_s, 2)},
-            "roofline": {"bound": "mfma", "kernel": "k_syrk", "achieved": achieved,
-                         "peak": PEAK_F64_MFMA_TFS, "unit": "TFLOP/s",
-                         "frac": (achieved / PEAK_F64_MFMA_TFS) if achieved else None, "traffic": None,
-                         "flops_per_step_rank0": flops,
-                         "kernel_timing": "HIP events (hh_ktime) over one extra serialised pass after the timed steps",
-                         "syrk_launches": syrk_n, "syrk_ms_avg": syrk_ms / max(syrk_n, 1),
-                         "cor_mul_launches": mul_n, "cor_mul_ms_avg": mul_ms / max(mul_n, 1)},
+                       "generate_s": round(gen_s, 2),
+                       "pca_products_per_chrom": {int(k) + 1: int(prods[k]) for k in sorted(mine)},
+                       "pca_all_converged": bool(all(conv[k] for k in mine)),
+                       "serial_step_ms": round(serial_ms, 2), "serial_phase_ms": serial_phases},
+            "roofline": dict(dom, traffic=None,
+                             kernel_timing="HIP events (hh_ktime) over one extra serialised pass after the timed steps",
+                             other_kernel=other),
         }
         if world == 1 and not args.no_cpu:
             out["cpu_baseline"] = c5_cpu_baseline()
@@ -594,6 +619,9 @@ def main():
     from hichap_master_amd import _lib, dist, ice
     _lib.load()
     _lib.call("hh_set_device", local)
+    for key in ("pca_p", "pca_method"):  # eigensolver knobs (measurement)
+        if os.environ.get("HH_" + key.upper()):
+            _lib.call("hh_tune", key.encode(), int(os.environ["HH_" + key.upper()]))
     if world > 1 or args.sharded:
         import torch.distributed as tdist
         if "MASTER_ADDR" not in os.environ:

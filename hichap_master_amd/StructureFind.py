@@ -21,6 +21,7 @@ them) so the N x N products stay in HBM for ``Select_PC_new``.
 from __future__ import annotations
 
 import ctypes as C
+import warnings
 
 import numpy as np
 
@@ -91,11 +92,23 @@ class _Comp:
         return out
 
     def pca(self, k=3):
+        """Top-k PCA components of the correlation (block Krylov on the
+        device, hh_comp_pca).  Warns (RuntimeWarning) when the eigensolver
+        stopped at its product budget without meeting PCA_TOL; the status is
+        kept in ``self.pca_status``."""
         n = self.NG.size
         comps = np.empty((k, n), np.float64)
         ev = np.empty(k, np.float64)
         it = C.c_int32(0)
         call("hh_comp_pca", self.h, int(k), PCA_TOL, PCA_MAX_ITERS, ptr(comps), ptr(ev), C.byref(it), self._s())
+        conv, prods, cyc, meth = (C.c_int32(0) for _ in range(4))
+        call("hh_comp_pca_status", self.h, C.byref(conv), C.byref(prods), C.byref(cyc), C.byref(meth))
+        self.pca_status = {"converged": bool(conv.value), "products": prods.value, "cycles": cyc.value,
+                           "method": "krylov" if meth.value == 1 else "subspace", "eigvals": ev.copy()}
+        if not conv.value:
+            warnings.warn(f"compartment PCA did not converge to {PCA_TOL:g} within its budget "
+                          f"({prods.value} correlation products, {self.pca_status['method']}); "
+                          f"the top eigenvalues may be (nearly) degenerate", RuntimeWarning, stacklevel=3)
         return comps, ev, it.value
 
     def select_stats(self, pcs, eps=1e-5):
@@ -212,6 +225,7 @@ class StructureFind(TADCalling):
         decline[decline == 0] = decline[np.nonzero(decline)].min()
         comp.correlation(decline, NG_array)
         pcs, _, _ = comp.pca(3)
+        self.pca_status = comp.pca_status
         return pcs, DeviceCorrelation(comp), DeviceOE(comp)
 
     def Select_PC_new(self, Cor_M, OE_M, pca):

@@ -102,6 +102,8 @@ SIGNATURES = {
     "hh_viterbi_gmm": (C.c_int, [P, I64, I32, I32, P, P, P, P, P, P, P]),
     "hh_comp_pca": (C.c_int, [P, I32, F64, I32, P, P, P, P]),
     "hh_comp_select_stats": (C.c_int, [P, P, I32, F64, P, P]),
+    "hh_comp_pca_status": (C.c_int, [P, PI32, PI32, PI32, PI32]),
+    "hh_sym_topk": (C.c_int, [P, I32, I32, P, P]),
     "hh_binner_create": (C.c_int, [I32, C.c_char_p, P, I32, I32, C.POINTER(P)]),
     "hh_binner_free": (C.c_int, [P]),
     "hh_binner_add_target": (C.c_int, [P, I32, I32, P, P, I64, PI32]),

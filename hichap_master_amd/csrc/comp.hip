@@ -18,6 +18,7 @@
 //        Select_PC_new's means_minus / select_ab need (:374-423).
 // All reductions are fixed-order (deterministic).
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <limits>
 #include <numeric>
@@ -478,6 +479,8 @@ struct hh_comp {
     long long n = 0, ld = 0;     // Cor leading dimension (n padded to 128)
     DBuf<double> cor;            // ld x ld
     int iters = 0;
+    // last hh_comp_pca: converged flag, Cor products, Krylov cycles, method
+    int pca_converged = 0, pca_products = 0, pca_cycles = 0, pca_method = 0;
 };
 
 namespace hh {
@@ -589,6 +592,435 @@ static void orthonormalize_dev(PcaWork& w, DBuf<double>& V, DBuf<double>& tmp, l
     }
 }
 
+// ------------------------------------------------------- Krylov PCA (K8)
+// Explicit-restart block Krylov on Cor with a Rayleigh-Ritz step for
+// A = Xc^T Xc (Xc = Cor - 1 mu^T, the matrix sklearn's PCA factors):
+//   cycle: Q_0 = [1/sqrt(n) | top-15 Ritz vectors], Q_{j+1} from Cor Q_j
+//   (j < P) by two-pass block Gram-Schmidt with shifted Cholesky-QR3 inside
+//   the block (stable down to rank deficiency, unlike CholQR2), so that
+//   Cor Q = Q_+ T exactly (T from the Gram-Schmidt coefficients and R
+//   factors).  Because 1/sqrt(n) is column 0 of Q_0, Xc Q = (I - q0 q0^T)
+//   Cor Q = Q_+ S with S = T minus its row 0: A's projection is S^T S (no
+//   squared cancellation), eigen-decomposed on the host.  The Krylov space of
+//   Cor of degree 2k contains A's of degree k, so a cycle of P products does
+//   the work of P / 2 subspace iterations with optimal polynomial weights:
+//   ~45 Cor products per chromosome instead of ~200.
+
+// G = X_k^T Y for nb blocks X_k (n x 16 each, contiguous): part[k][blk][a][b]
+__global__ __launch_bounds__(256) void k_gram_mp(const double* __restrict__ X, int nb, const double* __restrict__ Y,
+                                                 long long n, int nblk, double* __restrict__ part) {
+    __shared__ double xs[64][kSB + 1], ys[64][kSB + 1];
+    const int a = threadIdx.x / kSB, b = threadIdx.x % kSB;
+    const int xb = blockIdx.y;
+    const double* Xk = X + (size_t)xb * n * kSB;
+    const long long r0 = (long long)blockIdx.x * kGramRows;
+    for (int e = threadIdx.x; e < 64 * kSB; e += 256) {
+        const long long i = r0 + e / kSB;
+        xs[e / kSB][e % kSB] = i < n ? Xk[i * kSB + e % kSB] : 0.0;
+        ys[e / kSB][e % kSB] = i < n ? Y[i * kSB + e % kSB] : 0.0;
+    }
+    __syncthreads();
+    double acc = 0.0;
+#pragma unroll 8
+    for (int r = 0; r < 64; ++r) acc = fma(xs[r][a], ys[r][b], acc);
+    part[((size_t)xb * nblk + blockIdx.x) * kSB * kSB + threadIdx.x] = acc;
+}
+
+// G[k][e] = sum over row blocks of part[k][.][e]; fixed tree
+__global__ __launch_bounds__(64) void k_gram_ms(const double* __restrict__ part, int nblk, double* __restrict__ G) {
+    const int e = blockIdx.x % (kSB * kSB), k = blockIdx.x / (kSB * kSB), l = threadIdx.x;
+    const double* p = part + (size_t)k * nblk * kSB * kSB;
+    double acc = 0.0;
+    for (int r = l; r < nblk; r += 64) acc += p[(size_t)r * kSB * kSB + e];
+    acc = wave_sum(acc);
+    if (l == 0) G[(size_t)k * kSB * kSB + e] = acc;
+}
+
+// out = base - sum_k X_k C_k (base != null) or sum_k X_k C_k (base == null);
+// C = nb stacked 16 x 16 blocks (row k*16 + a)
+__global__ void k_comb_mp(const double* __restrict__ base, const double* __restrict__ X, int nb,
+                          const double* __restrict__ Cm, long long n, double* __restrict__ out) {
+    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n * kSB) return;
+    const long long i = t / kSB;
+    const int b = (int)(t % kSB);
+    double acc = 0.0;
+    for (int k = 0; k < nb; ++k) {
+        const double* xr = X + ((size_t)k * n + i) * kSB;
+        const double* c = Cm + (size_t)k * kSB * kSB + b;
+#pragma unroll
+        for (int a = 0; a < kSB; ++a) acc = fma(xr[a], c[a * kSB], acc);
+    }
+    out[t] = base ? base[t] - acc : acc;
+}
+
+// out = (in - sum_k Q_k Cm_k) Rinv for 64 rows per block (Cm == null: no
+// subtraction; Rinv == null: identity), plus per-block Gram partials of the
+// output: gpart[blk] = out_blk^T out_blk and, when qpart != null,
+// qpart[k][blk] = Q_k,blk^T out_blk (k < nb) — the next step's reductions
+// without another pass over the rows.  256 threads = 16 rows x 16 columns per
+// sub-step; LDS: the 64-row tile, Cm, Rinv.
+constexpr int kApplyRows = 64;
+__global__ __launch_bounds__(256) void k_apply(const double* __restrict__ in, const double* __restrict__ Q, int nb,
+                                               const double* __restrict__ Cm, const double* __restrict__ Rinv,
+                                               long long n, double* __restrict__ out, double* __restrict__ gpart,
+                                               double* __restrict__ qpart, int nblk) {
+    __shared__ double ts[kApplyRows][kSB + 1], os_[kApplyRows][kSB + 1];
+    __shared__ double cm[8 * kSB * kSB], ri[kSB * kSB];
+    const int t = threadIdx.x, rr = t / kSB, b = t % kSB;
+    const long long r0 = (long long)blockIdx.x * kApplyRows;
+    if (Cm)
+        for (int e = t; e < nb * kSB * kSB; e += 256) cm[e] = Cm[e];
+    if (Rinv) ri[t] = Rinv[t];
+    for (int e = t; e < kApplyRows * kSB; e += 256) {
+        const long long i = r0 + e / kSB;
+        ts[e / kSB][e % kSB] = i < n ? in[i * kSB + e % kSB] : 0.0;
+    }
+    __syncthreads();
+    if (Cm) {
+        double acc[kApplyRows / 16];
+#pragma unroll
+        for (int q = 0; q < kApplyRows / 16; ++q) acc[q] = ts[rr + 16 * q][b];
+        for (int k = 0; k < nb; ++k) {
+            const double* Qk = Q + (size_t)k * n * kSB;
+#pragma unroll
+            for (int q = 0; q < kApplyRows / 16; ++q) {
+                const long long i = r0 + rr + 16 * q;
+                if (i >= n) continue;
+                const double* qr = Qk + i * kSB;
+                double s = 0.0;
+#pragma unroll
+                for (int a = 0; a < kSB; ++a) s = fma(qr[a], cm[(k * kSB + a) * kSB + b], s);
+                acc[q] -= s;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < kApplyRows / 16; ++q) ts[rr + 16 * q][b] = acc[q];
+        __syncthreads();
+    }
+#pragma unroll
+    for (int q = 0; q < kApplyRows / 16; ++q) {
+        const int r = rr + 16 * q;
+        double v = ts[r][b];
+        if (Rinv) {
+            v = 0.0;
+#pragma unroll
+            for (int a = 0; a < kSB; ++a) v = fma(ts[r][a], ri[a * kSB + b], v);
+        }
+        const long long i = r0 + r;
+        if (i >= n) v = 0.0;
+        os_[r][b] = v;
+        if (i < n) out[i * kSB + b] = v;
+    }
+    __syncthreads();
+    if (gpart) {
+        const int a = t / kSB;
+        double acc = 0.0;
+#pragma unroll 8
+        for (int r = 0; r < kApplyRows; ++r) acc = fma(os_[r][a], os_[r][b], acc);
+        gpart[(size_t)blockIdx.x * kSB * kSB + t] = acc;
+    }
+    if (qpart) {
+        const int a = t / kSB;
+        const long long rmax = n - r0;  // rows of this block inside the matrix
+        for (int k = 0; k < nb; ++k) {
+            const double* Qk = Q + ((size_t)k * n + r0) * kSB + a;
+            double acc = 0.0;
+#pragma unroll 16
+            for (int r = 0; r < kApplyRows; ++r) {
+                const double q = r < rmax ? Qk[(size_t)r * kSB] : 0.0;
+                acc = fma(q, os_[r][b], acc);
+            }
+            qpart[((size_t)k * nblk + blockIdx.x) * kSB * kSB + t] = acc;
+        }
+    }
+}
+
+// G = sum of nblk Gram partials (fixed order), then Cholesky G (+ shift I) =
+// R^T R and R^{-1}, all in LDS (the 16 dependent steps never touch global
+// memory).  shift_scale > 0: shift = shift_scale * trace(G) (shifted
+// CholeskyQR, Fukaya et al.: 11 (m n + n (n + 1)) u ||X||^2, the trace
+// bounding ||X||^2).  Not positive definite -> *fail = 1, R = Rinv = I.
+__global__ __launch_bounds__(1024) void k_reduce_chol(const double* __restrict__ gpart, int nblk, double shift_scale,
+                                                      double* __restrict__ Rout, double* __restrict__ Rinv,
+                                                      int* __restrict__ fail) {
+    __shared__ double G[kSB][kSB + 1], R[kSB][kSB + 1], X[kSB][kSB + 1], P4[4][kSB * kSB];
+    __shared__ double shift;
+    __shared__ int bad;
+    const int tt = threadIdx.x, t = tt & 255, part = tt >> 8, a = t / kSB, b = t % kSB;
+    // four fixed quarters of the partials, each summed in order with 8
+    // independent loads in flight, then combined in quarter order
+    {
+        const int q0 = (int)((long long)nblk * part / 4), q1 = (int)((long long)nblk * (part + 1) / 4);
+        double acc = 0.0;
+        int r = q0;
+        for (; r + 8 <= q1; r += 8) {
+            double v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = gpart[(size_t)(r + u) * kSB * kSB + t];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) acc += v[u];
+        }
+        for (; r < q1; ++r) acc += gpart[(size_t)r * kSB * kSB + t];
+        P4[part][t] = acc;
+    }
+    __syncthreads();
+    const bool w = tt < 256;  // the 16 x 16 algebra: threads 0..255; all reach every barrier
+    if (w) {
+        G[a][b] = ((P4[0][t] + P4[1][t]) + P4[2][t]) + P4[3][t];
+        R[a][b] = 0.0;
+    }
+    __syncthreads();
+    if (tt == 0) {
+        bad = 0;
+        double tr = 0.0;
+        for (int i = 0; i < kSB; ++i) tr += G[i][i];
+        shift = shift_scale > 0 ? shift_scale * tr : 0.0;
+    }
+    __syncthreads();
+    if (w && a == b) G[a][a] += shift;
+    __syncthreads();
+    // right-looking: step j: R[j][j] = sqrt(G[j][j]); R[j][c] = G[j][c] / R[j][j];
+    // G[p][q] -= R[j][p] R[j][q] for p, q > j
+    for (int j = 0; j < kSB; ++j) {
+        const double d = G[j][j];
+        const bool okd = d > 0;
+        const double rjj = okd ? sqrt(d) : 1.0;
+        if (tt == 0 && !okd) bad = 1;
+        if (w && a == j && b >= j) R[j][b] = b == j ? rjj : G[j][b] / rjj;
+        __syncthreads();
+        if (w && a > j && b > j) G[a][b] -= R[j][a] * R[j][b];
+        __syncthreads();
+    }
+    // R^{-1} by back substitution, column b per thread group (16 x 16 threads)
+    if (w) X[a][b] = 0.0;
+    __syncthreads();
+    for (int i = kSB - 1; i >= 0; --i) {
+        if (w && a == i) {
+            double s = i == b ? 1.0 : 0.0;
+            for (int k = i + 1; k < kSB; ++k) s -= R[i][k] * X[k][b];
+            X[i][b] = s / R[i][i];
+        }
+        __syncthreads();
+    }
+    if (!w) return;
+    if (bad) {
+        if (t == 0) *fail = 1;
+        Rinv[t] = a == b ? 1.0 : 0.0;
+        Rout[t] = a == b ? 1.0 : 0.0;
+        return;
+    }
+    Rinv[t] = X[a][b];
+    Rout[t] = R[a][b];
+}
+
+// start block [1/sqrt(n) | X[:, 0..14]]
+__global__ void k_start_block(const double* __restrict__ X, long long n, double* __restrict__ out) {
+    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n * kSB) return;
+    const long long i = t / kSB;
+    const int b = (int)(t % kSB);
+    out[t] = b == 0 ? 1.0 / sqrt((double)n) : X[i * kSB + b - 1];
+}
+
+// ---------------------------------------------- small symmetric eigen (host)
+// Householder tridiagonalisation T = Q^T A Q (Golub & Van Loan 8.3.1; A full
+// m x m row-major, destroyed), Q kept as reflectors (v_k, beta_k).
+struct Tridiag {
+    int m = 0;
+    std::vector<double> d, e, V, beta;  // e[i] = T[i+1][i]
+};
+static void tridiagonalize(int m, std::vector<double>& A, Tridiag& T) {
+    T.m = m;
+    T.V.assign((size_t)m * m, 0.0);
+    T.beta.assign(m, 0.0);
+    std::vector<double> p(m), w(m);
+    for (int k = 0; k + 2 < m; ++k) {
+        double sig = 0.0;
+        for (int i = k + 2; i < m; ++i) sig += A[(size_t)i * m + k] * A[(size_t)i * m + k];
+        if (sig == 0.0) continue;
+        const double x0 = A[(size_t)(k + 1) * m + k];
+        const double mu = std::sqrt(x0 * x0 + sig);
+        const double v0 = x0 <= 0 ? x0 - mu : -sig / (x0 + mu);
+        const double beta = 2.0 * v0 * v0 / (sig + v0 * v0);
+        double* v = &T.V[(size_t)k * m];
+        v[k + 1] = 1.0;
+        for (int i = k + 2; i < m; ++i) v[i] = A[(size_t)i * m + k] / v0;
+        T.beta[k] = beta;
+        // A22 <- P A22 P, P = I - beta v v^T:  p = beta A22 v,
+        // w = p - (beta / 2)(p^T v) v,  A22 -= v w^T + w v^T
+        double pv = 0.0;
+        for (int i = k + 1; i < m; ++i) {
+            double s = 0.0;
+            const double* ai = &A[(size_t)i * m];
+            for (int j = k + 1; j < m; ++j) s += ai[j] * v[j];
+            p[i] = beta * s;
+            pv += p[i] * v[i];
+        }
+        for (int i = k + 1; i < m; ++i) w[i] = p[i] - 0.5 * beta * pv * v[i];
+        for (int i = k + 1; i < m; ++i) {
+            double* ai = &A[(size_t)i * m];
+            for (int j = k + 1; j < m; ++j) ai[j] -= v[i] * w[j] + w[i] * v[j];
+        }
+        A[(size_t)(k + 1) * m + k] = mu;
+        A[(size_t)k * m + k + 1] = mu;
+        for (int i = k + 2; i < m; ++i) A[(size_t)i * m + k] = A[(size_t)k * m + i] = 0.0;
+    }
+    T.d.resize(m);
+    T.e.assign(m, 0.0);
+    for (int i = 0; i < m; ++i) T.d[i] = A[(size_t)i * m + i];
+    for (int i = 0; i + 1 < m; ++i) T.e[i] = A[(size_t)(i + 1) * m + i];
+}
+
+// eigenvalues of the symmetric tridiagonal (d, e) by implicit-shift QL
+static std::vector<double> tridiag_eigvals(std::vector<double> d, std::vector<double> e) {
+    const int m = (int)d.size();
+    for (int l = 0; l < m; ++l) {
+        for (int iter = 0; iter < 60; ++iter) {
+            int mm = l;
+            for (; mm < m - 1; ++mm) {
+                const double dd = std::fabs(d[mm]) + std::fabs(d[mm + 1]);
+                if (std::fabs(e[mm]) <= std::numeric_limits<double>::epsilon() * dd) break;
+            }
+            if (mm == l) break;
+            double g = (d[l + 1] - d[l]) / (2.0 * e[l]);
+            double r = std::hypot(g, 1.0);
+            g = d[mm] - d[l] + e[l] / (g + (g >= 0 ? r : -r));
+            double s = 1.0, c = 1.0, p = 0.0;
+            int i = mm - 1;
+            bool underflow = false;
+            for (; i >= l; --i) {
+                const double f = s * e[i], b = c * e[i];
+                r = std::hypot(f, g);
+                e[i + 1] = r;
+                if (r == 0.0) {
+                    d[i + 1] -= p;
+                    e[mm] = 0.0;
+                    underflow = true;
+                    break;
+                }
+                s = f / r;
+                c = g / r;
+                g = d[i + 1] - p;
+                r = (d[i] - g) * s + 2.0 * c * b;
+                p = s * r;
+                d[i + 1] = g + p;
+                g = c * r - b;
+            }
+            if (underflow) continue;
+            d[l] -= p;
+            e[l] = g;
+            e[mm] = 0.0;
+        }
+    }
+    return d;
+}
+
+// eigenvector of the tridiagonal for eigenvalue lam: inverse iteration with
+// a Gaussian elimination with partial pivoting (two superdiagonals)
+static void tridiag_invit(const Tridiag& T, double lam, double tnorm, uint64_t seed, std::vector<double>& x) {
+    const int m = T.m;
+    const double pert = std::max(tnorm, 1e-300) * 1e-14;
+    const double sh = lam + pert;
+    // rows: (sub a_i, diag b_i, sup c_i) of T - sh I
+    std::vector<double> l(m, 0.0), u0(m), u1(m, 0.0), u2(m, 0.0);
+    std::vector<char> piv(m, 0);
+    {
+        // LU with partial pivoting of the tridiagonal
+        std::vector<double> b(m), c(m, 0.0), a(m, 0.0);
+        for (int i = 0; i < m; ++i) b[i] = T.d[i] - sh;
+        for (int i = 0; i + 1 < m; ++i) c[i] = a[i + 1] = T.e[i];
+        // current row i holds (u0 = diag, u1 = sup, u2 = sup2)
+        double cd = b[0], cs = m > 1 ? c[0] : 0.0, cs2 = 0.0;
+        for (int i = 0; i < m; ++i) {
+            if (i == m - 1) {
+                u0[i] = cd == 0.0 ? pert : cd;
+                u1[i] = u2[i] = 0.0;
+                break;
+            }
+            const double na = a[i + 1], nb = b[i + 1], nc = i + 2 < m ? c[i + 1] : 0.0;
+            if (std::fabs(na) > std::fabs(cd)) {  // swap rows i and i+1
+                piv[i] = 1;
+                u0[i] = na; u1[i] = nb; u2[i] = nc;
+                const double f = cd / na;
+                l[i] = f;
+                cd = cs - f * nb;
+                cs = cs2 - f * nc;
+                cs2 = 0.0;
+            } else {
+                if (cd == 0.0) cd = pert;
+                u0[i] = cd; u1[i] = cs; u2[i] = cs2;
+                const double f = na / cd;
+                l[i] = f;
+                cd = nb - f * cs;
+                cs = nc - f * cs2;
+                cs2 = 0.0;
+            }
+        }
+    }
+    x.assign(m, 0.0);
+    for (int i = 0; i < m; ++i) x[i] = 1.0 + 0.1 * ((double)u01(mix64(seed + (uint64_t)i)) - 0.5);
+    for (int it = 0; it < 3; ++it) {
+        // forward: apply the row operations
+        for (int i = 0; i + 1 < m; ++i) {
+            if (piv[i]) std::swap(x[i], x[i + 1]);
+            x[i + 1] -= l[i] * x[i];
+        }
+        // back substitution with U
+        for (int i = m - 1; i >= 0; --i) {
+            double s = x[i];
+            if (i + 1 < m) s -= u1[i] * x[i + 1];
+            if (i + 2 < m) s -= u2[i] * x[i + 2];
+            x[i] = s / u0[i];
+        }
+        double nn = 0.0;
+        for (double v : x) nn += v * v;
+        nn = 1.0 / std::sqrt(nn);
+        for (double& v : x) v *= nn;
+    }
+}
+
+// top-k eigenpairs (descending) of the symmetric m x m matrix H
+static void sym_topk(int m, std::vector<double> H, int k, std::vector<double>& evals, std::vector<double>& evecs) {
+    Tridiag T;
+    tridiagonalize(m, H, T);
+    std::vector<double> ev = tridiag_eigvals(T.d, T.e);
+    std::sort(ev.begin(), ev.end(), std::greater<double>());
+    double tnorm = 0.0;
+    for (int i = 0; i < m; ++i)
+        tnorm = std::max(tnorm, std::fabs(T.d[i]) + (i ? std::fabs(T.e[i - 1]) : 0.0) + std::fabs(T.e[i]));
+    evals.assign(ev.begin(), ev.begin() + k);
+    evecs.assign((size_t)m * k, 0.0);  // column q of an m x k row-major matrix
+    std::vector<std::vector<double>> ys(k);
+    for (int q = 0; q < k; ++q) {
+        tridiag_invit(T, ev[q], tnorm, 0x7e57ULL * (q + 1), ys[q]);
+        // two Gram-Schmidt passes against the previous vectors (clusters)
+        for (int pass = 0; pass < 2; ++pass)
+            for (int r = 0; r < q; ++r) {
+                double dot = 0.0;
+                for (int i = 0; i < m; ++i) dot += ys[q][i] * ys[r][i];
+                for (int i = 0; i < m; ++i) ys[q][i] -= dot * ys[r][i];
+            }
+        double nn = 0.0;
+        for (double v : ys[q]) nn += v * v;
+        nn = 1.0 / std::sqrt(nn);
+        for (double& v : ys[q]) v *= nn;
+        // back-transform: x = P_0 P_1 ... P_{m-3} y
+        std::vector<double>& x = ys[q];
+        std::vector<double> y = x;
+        for (int kk = m - 3; kk >= 0; --kk) {
+            if (T.beta[kk] == 0.0) continue;
+            const double* v = &T.V[(size_t)kk * m];
+            double dot = 0.0;
+            for (int i = kk + 1; i < m; ++i) dot += v[i] * y[i];
+            dot *= T.beta[kk];
+            for (int i = kk + 1; i < m; ++i) y[i] -= dot * v[i];
+        }
+        for (int i = 0; i < m; ++i) evecs[(size_t)i * k + q] = y[i];
+    }
+}
+
 // V <- V R^{-1} twice (CholQR2); returns false if V lost rank.
 static bool orthonormalize(PcaWork& w, DBuf<double>& V, DBuf<double>& tmp, long long n, hipStream_t s) {
     for (int pass = 0; pass < 2; ++pass) {
@@ -598,6 +1030,286 @@ static bool orthonormalize(PcaWork& w, DBuf<double>& V, DBuf<double>& tmp, long 
         w.put_small(Rinv, s);
         hipLaunchKernelGGL(k_rot, dim3((unsigned)((n * kSB + 255) / 256)), dim3(256), 0, s, V.p, w.R.p, n, tmp.p);
         std::swap(V.p, tmp.p);
+    }
+    return true;
+}
+
+// PCA statistics of the last hh_comp_pca (hh_comp_pca_status)
+struct PcaStatus {
+    int converged = 0, products = 0, cycles = 0, method = 0;
+    double residual[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // ||A x - theta x|| of the last checked Ritz vectors
+    double bound = 0.0;                              // max_q ||r_q|| / gap_q (angle bound)
+};
+
+// Block Krylov PCA (see the K8 comment above).  Returns false when the
+// method cannot run (basis larger than the matrix, start block rank
+// deficient); the caller then falls back to subspace iteration.
+static bool pca_krylov(PcaWork& wk, const double* cor, long long n, int k, double tol, int max_products, int P,
+                       double* components, double* eigvals, PcaStatus& st, hipStream_t s) {
+    constexpr int B = kSB, BB = kSB * kSB;
+    if (P < 2 || (long long)(P + 1) * B > n) return false;
+    const int nblk = (int)((n + kGramRows - 1) / kGramRows);
+    const unsigned ge = (unsigned)((n * B + 255) / 256);
+    const double eps = std::numeric_limits<double>::epsilon();
+    const double shift_scale = 11.0 * ((double)n * B + (double)B * (B + 1)) * eps;
+    DBuf<double> Q((size_t)P * n * B), W((size_t)n * B), T1((size_t)n * B), T2((size_t)n * B), X((size_t)n * B);
+    const int nap = (int)((n + kApplyRows - 1) / kApplyRows);  // k_apply blocks
+    DBuf<double> part((size_t)P * nblk * BB), gpart((size_t)nap * BB), qpart((size_t)P * nap * BB), rinv(BB);
+    // small outputs of one cycle, per block j: c1 [P], c2 [P], R x 6, G
+    const int slot = (2 * P + 7) * BB;
+    DBuf<double> smalls((size_t)P * slot + 3 * BB);  // + the restart block's R factors
+    double* restartR = smalls.p + (size_t)P * slot;
+    DBuf<int> fail(P * 8 + 8);  // per block j: slots j * 8 + 0..5; restart: P * 8 + 0..2
+    DBuf<double> Ydev((size_t)P * B * B);
+    std::vector<double> hs((size_t)P * slot + 3 * BB);
+    std::vector<int> hf(P * 8 + 8);
+    auto gram = [&](const double* Xs, int nb, const double* Y, double* out) {
+        hipLaunchKernelGGL(k_gram_mp, dim3((unsigned)nblk, (unsigned)nb), dim3(256), 0, s, Xs, nb, Y, n, nblk, part.p);
+        hipLaunchKernelGGL(k_gram_ms, dim3((unsigned)(nb * BB)), dim3(64), 0, s, part.p, nblk, out);
+    };
+    auto apply = [&](const double* in, int nb, const double* Cm, const double* Ri, double* out, bool g, bool qg) {
+        hipLaunchKernelGGL(k_apply, dim3((unsigned)nap), dim3(256), 0, s, in, Q.p, nb, Cm, Ri, n, out,
+                           g ? gpart.p : nullptr, qg ? qpart.p : nullptr, nap);
+    };
+    auto chol = [&](bool shifted, double* Rout, int* fl) {
+        hipLaunchKernelGGL(k_reduce_chol, dim3(1), dim3(1024), 0, s, gpart.p, nap, shifted ? shift_scale : 0.0, Rout,
+                           rinv.p, fl);
+    };
+    // shifted CholeskyQR3 of the block whose Gram partials are in gpart (its
+    // rows in `in`): out = in R^{-1}, R factors to R3[0..2]; qg: the final
+    // pass also leaves Q_k^T out partials in qpart (the next reduction)
+    auto scholqr3 = [&](const double* in, double* out, double* R3, int* fl, int nbq) {
+        const double* cur = in;
+        // passes 0 and 1 shifted: a direction the Gram-Schmidt step left at
+        // rounding level (a deflated Krylov direction) comes out of the two
+        // shifted passes with kappa ~ 1e3-1e5 instead of 1e8, so the plain
+        // third pass cannot break down (its noise direction is a valid new
+        // basis vector; the outer second Gram-Schmidt pass re-orthogonalises it)
+        for (int pass = 0; pass < 3; ++pass) {
+            chol(pass < 2, R3 + pass * BB, fl + pass);
+            double* dst = pass == 2 ? out : (cur == T1.p ? T2.p : T1.p);
+            apply(cur, nbq, nullptr, rinv.p, dst, pass < 2, pass == 2 && nbq > 0);
+            cur = dst;
+        }
+    };
+    auto qreduce = [&](int nb, double* out) {  // c = sum of the qpart partials
+        hipLaunchKernelGGL(k_gram_ms, dim3((unsigned)(nb * BB)), dim3(64), 0, s, qpart.p, nap, out);
+    };
+    fail.zero(s);
+    // start block: [1 / sqrt(n) | deterministic pseudo-random columns]
+    {
+        std::vector<double> v0((size_t)n * B);
+        for (long long i = 0; i < n; ++i)
+            for (int b = 0; b < B; ++b)
+                v0[i * B + b] = b == 0 ? 1.0 / std::sqrt((double)n) : (double)u01(mix64(0x5eedULL + i * B + b)) - 0.5;
+        X.upload(v0.data(), v0.size(), s);
+        apply(X.p, 0, nullptr, nullptr, W.p, true, false);
+        scholqr3(W.p, Q.p, restartR, fail.p + P * 8, 0);
+    }
+    std::vector<double> cur((size_t)n * k), Xh((size_t)n * B);
+    double last_bound = 1e300;
+    int products = 0, cycles = 0;
+    bool done = false;
+    while (!done && products + P <= max_products) {
+        int pe = P;  // blocks of this cycle's basis
+        HIP_CHECK(hipMemsetAsync(fail.p, 0, sizeof(int) * P * 8, s));
+        for (int j = 0; j < P; ++j) {
+            double* sl = smalls.p + (size_t)j * slot;
+            double *c1 = sl, *c2 = sl + (size_t)P * BB, *R = sl + (size_t)2 * P * BB, *G = sl + (size_t)(2 * P + 6) * BB;
+            double* Qj = Q.p + (size_t)j * n * B;
+            wk.cor_mul(cor, Qj, nullptr, false, W.p, s);
+            ++products;
+            const int nb = j + 1;
+            if (j < P - 1) {
+                // pass A: W1 = W - Qa c1 = Q1 RA;  pass B: W2 = Q1 - Qa c2 = Q_{j+1} RB
+                gram(Q.p, nb, W.p, c1);
+                apply(W.p, nb, c1, nullptr, X.p, true, false);
+                scholqr3(X.p, W.p, R, fail.p + j * 8, nb);      // Q1 -> W, Qa^T Q1 partials
+                qreduce(nb, c2);
+                apply(W.p, nb, c2, nullptr, X.p, true, false);
+                scholqr3(X.p, Q.p + (size_t)(j + 1) * n * B, R + 3 * BB, fail.p + j * 8 + 3, 0);
+            } else {
+                // last product: CGS2 coefficients + Gram of the residual
+                gram(Q.p, nb, W.p, c1);
+                apply(W.p, nb, c1, nullptr, X.p, false, true);
+                qreduce(nb, c2);
+                apply(X.p, nb, c2, nullptr, W.p, true, false);
+                hipLaunchKernelGGL(k_gram_ms, dim3((unsigned)BB), dim3(64), 0, s, gpart.p, nap, G);
+            }
+        }
+        smalls.download(hs.data(), hs.size(), s);
+        fail.download(hf.data(), hf.size(), s);
+        const auto c0 = std::chrono::steady_clock::now();
+        HIP_CHECK(hipStreamSynchronize(s));
+        const auto c1 = std::chrono::steady_clock::now();
+        const double t_w = std::chrono::duration<double, std::milli>(c1 - c0).count();
+        if (hf[P * 8] || hf[P * 8 + 1] || hf[P * 8 + 2]) return false;  // start block rank deficient
+        for (int j = 0; j + 1 < P; ++j) {
+            bool bad = false;
+            for (int q = 0; q < 6; ++q) bad |= hf[j * 8 + q] != 0;
+            if (bad) { pe = j + 1; break; }
+        }
+        if (pe < 2) return false;  // deflated at the first expansion
+        // T (m + B) x m, column block j = [c_j (rows 0 .. (j+1)B); R_j (next B rows)]
+        const int m = pe * B;
+        // St = S^T (m x (m + B)): row a = coordinates of column a of Xc Q
+        const int ldS = m + B;
+        std::vector<double> St((size_t)m * ldS, 0.0);
+        std::vector<int> slen(m, 0);  // nonzero rows of column a
+        auto mm16 = [&](const double* A, const double* Bm, double* C) {  // C = A Bm (16 x 16)
+            for (int a = 0; a < B; ++a)
+                for (int b = 0; b < B; ++b) {
+                    double acc = 0.0;
+                    for (int q = 0; q < B; ++q) acc += A[a * B + q] * Bm[q * B + b];
+                    C[a * B + b] = acc;
+                }
+        };
+        std::vector<double> RA(BB), RB(BB), tmp(BB), tmp2(BB);
+        std::vector<double> extraG;  // Gram of the residual block (last block)
+        int last = -1;
+        for (int j = 0; j < pe; ++j) {
+            const double* sl = hs.data() + (size_t)j * slot;
+            const double *c1 = sl, *c2 = sl + (size_t)P * BB, *R = sl + (size_t)2 * P * BB,
+                         *G = sl + (size_t)(2 * P + 6) * BB;
+            const int nb = j + 1;
+            const bool is_last = (j == P - 1);
+            if (!is_last && j == pe - 1) {
+                // deflated next block: cycle ends here, ignore this product
+                break;
+            }
+            if (!is_last) {
+                mm16(R + BB, R, tmp.data());        // R2 R1
+                mm16(R + 2 * BB, tmp.data(), RA.data());  // R3 R2 R1
+                mm16(R + 4 * BB, R + 3 * BB, tmp.data());
+                mm16(R + 5 * BB, tmp.data(), RB.data());
+                // coef = c1 + c2 RA ; R_j = RB RA
+                for (int r = 0; r < nb * B; ++r)
+                    for (int b = 0; b < B; ++b) {
+                        double acc = c1[r * B + b];
+                        for (int q = 0; q < B; ++q) acc += c2[r * B + q] * RA[q * B + b];
+                        St[(size_t)(j * B + b) * ldS + r] = acc;
+                    }
+                mm16(RB.data(), RA.data(), tmp2.data());
+                for (int a = 0; a < B; ++a)
+                    for (int b = 0; b < B; ++b) St[(size_t)(j * B + b) * ldS + (j + 1) * B + a] = tmp2[a * B + b];
+                for (int b = 0; b < B; ++b) slen[j * B + b] = (j + 2) * B;
+                last = j;
+            } else {
+                for (int r = 0; r < nb * B; ++r)
+                    for (int b = 0; b < B; ++b) St[(size_t)(j * B + b) * ldS + r] = c1[r * B + b] + c2[r * B + b];
+                for (int b = 0; b < B; ++b) slen[j * B + b] = (j + 1) * B;
+                extraG.assign(G, G + BB);
+                last = j;
+            }
+        }
+        const int mb = (last + 1) * B;  // basis columns used by Rayleigh-Ritz
+        // Xc Q = Q_+ S with row 0 (the 1/sqrt(n) coordinate) removed
+        for (int c = 0; c < m; ++c) St[(size_t)c * ldS] = 0.0;
+        std::vector<double> H((size_t)mb * mb, 0.0);
+        for (int a = 0; a < mb; ++a) {
+            const double* sa = &St[(size_t)a * ldS];
+            for (int b = a; b < mb; ++b) {
+                const double* sb = &St[(size_t)b * ldS];
+                const int L = std::min(slen[a], slen[b]);
+                double acc = 0.0;
+                for (int r = 0; r < L; ++r) acc += sa[r] * sb[r];
+                H[(size_t)a * mb + b] = H[(size_t)b * mb + a] = acc;
+            }
+        }
+        if (!extraG.empty()) {
+            const int o = last * B;
+            for (int a = 0; a < B; ++a)
+                for (int b = 0; b < B; ++b) H[(size_t)(o + a) * mb + o + b] += 0.5 * (extraG[a * B + b] + extraG[b * B + a]);
+        }
+        const auto c2 = std::chrono::steady_clock::now();
+        std::vector<double> ev, Y;
+        sym_topk(mb, H, B, ev, Y);
+        const auto c3 = std::chrono::steady_clock::now();
+        const double t_h = std::chrono::duration<double, std::milli>(c2 - c1).count();
+        const double t_e = std::chrono::duration<double, std::milli>(c3 - c2).count();
+        // Ritz vectors X = Qa Y (top B), uploaded as nb stacked 16 x 16 blocks
+        Ydev.upload(Y.data(), (size_t)mb * B, s);
+        hipLaunchKernelGGL(k_comb_mp, dim3(ge), dim3(256), 0, s, nullptr, Q.p, last + 1, Ydev.p, n, X.p);
+        X.download(Xh.data(), Xh.size(), s);
+        HIP_CHECK(hipStreamSynchronize(s));
+        ++cycles;
+        for (int q = 0; q < k; ++q) {
+            double nn = 0.0;
+            for (long long i = 0; i < n; ++i) nn += Xh[i * B + q] * Xh[i * B + q];
+            const double inv = 1.0 / std::sqrt(nn);
+            for (long long i = 0; i < n; ++i) cur[q * n + i] = Xh[i * B + q] * inv;
+        }
+        if (eigvals)
+            for (int q = 0; q < k; ++q) eigvals[q] = ev[q];
+        // Convergence from residuals of the PREVIOUS cycle's Ritz vectors:
+        // they are columns 1..k of this cycle's start block, x_q = Q_0 (R e_{q+1})
+        // (R = the restart's CholQR factors), and A x_q lies in span(Q_0, Q_1, Q_2)
+        // (A = Cor P Cor), so r_q = A x_q - theta x_q = Q (H e - theta e) exactly:
+        // ||r_q|| with no cancellation, and sin(x_q, v_q) <= ||r_q|| / gap_q.
+        // Done when that bound is < tol for every q < k, or when it has
+        // stopped shrinking (< 2x per cycle) below 1e3 tol: the rounding floor
+        // of the products (a degenerate gap never gets there: not converged).
+        if (cycles > 1 && last >= 2) {
+            const double* Rr = hs.data() + (size_t)P * slot;
+            std::vector<double> tmpR(BB), Rt(BB);
+            mm16(Rr + BB, Rr, tmpR.data());
+            mm16(Rr + 2 * BB, tmpR.data(), Rt.data());
+            double bound = 0.0;
+            for (int q = 0; q < k; ++q) {
+                std::vector<double> e(mb, 0.0), He(mb, 0.0);
+                for (int a = 0; a < B; ++a) e[a] = Rt[a * B + q + 1];
+                for (int a = 0; a < mb; ++a) {
+                    double acc = 0.0;
+                    for (int c = 0; c < B; ++c) acc += H[(size_t)a * mb + c] * e[c];
+                    He[a] = acc;
+                }
+                double ee = 0.0, eHe = 0.0;
+                for (int a = 0; a < mb; ++a) { ee += e[a] * e[a]; eHe += e[a] * He[a]; }
+                const double theta = eHe / ee;
+                double rr = 0.0;
+                for (int a = 0; a < mb; ++a) rr += (He[a] - theta * e[a]) * (He[a] - theta * e[a]);
+                const double res = std::sqrt(rr / ee);
+                double gap = std::fabs(ev[q] - ev[q + 1]);
+                if (q > 0) gap = std::min(gap, std::fabs(ev[q - 1] - ev[q]));
+                bound = std::max(bound, gap > 0 ? res / gap : 1e300);
+                st.residual[q] = res;
+            }
+            st.bound = bound;
+            if (g_pca_debug)
+                fprintf(stderr, "[pca] n=%lld cycle=%d products=%d pe=%d bound=%.3e res=%.3e %.3e %.3e ev=%.6g %.6g %.6g %.6g"
+                        " host_ms H=%.3f eig=%.3f gpu_wait_ms=%.3f\n",
+                        n, cycles, products, pe, bound, st.residual[0], st.residual[1], st.residual[2], ev[0], ev[1],
+                        ev[2], ev[3], t_h, t_e, t_w);
+            // this cycle's vectors are better than the checked ones by about
+            // the last contraction factor: stop when the predicted bound is met
+            const double predicted = last_bound < 1e300 ? bound * std::min(1.0, bound / last_bound) : bound;
+            if (predicted < tol || (bound < 1e3 * tol && bound > 0.5 * last_bound)) {
+                done = true;
+                st.converged = 1;
+            }
+            last_bound = bound;
+        }
+        if (!done) {
+            hipLaunchKernelGGL(k_start_block, dim3(ge), dim3(256), 0, s, X.p, n, T2.p);
+            HIP_CHECK(hipMemsetAsync(fail.p + P * 8, 0, sizeof(int) * 8, s));
+            apply(T2.p, 0, nullptr, nullptr, W.p, true, false);
+            scholqr3(W.p, Q.p, restartR, fail.p + P * 8, 0);
+        }
+    }
+    if (!done) st.converged = 0;
+    st.products = products;
+    st.cycles = cycles;
+    st.method = 1;
+    // unit norm + sklearn svd_flip(u_based_decision=False): max-|.| entry positive
+    for (int q = 0; q < k; ++q) {
+        double nn = 0.0;
+        long long am = 0;
+        for (long long i = 0; i < n; ++i) {
+            nn += cur[q * n + i] * cur[q * n + i];
+            if (std::fabs(cur[q * n + i]) > std::fabs(cur[q * n + am])) am = i;
+        }
+        const double sc = (cur[q * n + am] < 0 ? -1.0 : 1.0) / std::sqrt(nn);
+        for (long long i = 0; i < n; ++i) components[q * n + i] = cur[q * n + i] * sc;
     }
     return true;
 }
@@ -732,6 +1444,18 @@ int hh_comp_pca(hh_comp* c, int32_t k, double tol, int32_t max_iters, double* co
         const long long n = c->n;
         HH_REQUIRE(n >= kSB, "matrix smaller than the subspace block (16)");
         PcaWork wk(n, c->ld);
+        if (g_pca_method == 1) {
+            PcaStatus st;
+            if (pca_krylov(wk, c->cor.p, n, k, tol, 2 * max_iters, g_pca_p, components, eigvals, st, s)) {
+                c->iters = st.products;
+                c->pca_converged = st.converged;
+                c->pca_products = st.products;
+                c->pca_cycles = st.cycles;
+                c->pca_method = 1;
+                if (iters_out) *iters_out = st.products;
+                return;
+            }
+        }
         // mu and 1 as the first column of n x B blocks, so mu^T X and 1^T X are
         // row 0 of a Gram product; mu = column means of Cor = (Cor 1) / n.
         DBuf<double> mu(n), mupad, onepad, nmu;
@@ -832,6 +1556,10 @@ int hh_comp_pca(hh_comp* c, int32_t k, double tol, int32_t max_iters, double* co
             }
         }
         c->iters = it - 1;
+        c->pca_converged = done ? 1 : 0;
+        c->pca_products = 2 * c->iters + 1;
+        c->pca_cycles = c->iters;
+        c->pca_method = 0;
         if (iters_out) *iters_out = c->iters;
         // unit norm + sklearn svd_flip(u_based_decision=False): max-|.| entry positive
         for (int q = 0; q < k; ++q) {
@@ -844,6 +1572,31 @@ int hh_comp_pca(hh_comp* c, int32_t k, double tol, int32_t max_iters, double* co
             const double sc = (cur[q * n + am] < 0 ? -1.0 : 1.0) / std::sqrt(nn);
             for (long long i = 0; i < n; ++i) components[q * n + i] = cur[q * n + i] * sc;
         }
+    });
+}
+
+int hh_sym_topk(const double* H, int32_t m, int32_t k, double* evals, double* evecs) {
+    return guard([&] {
+        HH_REQUIRE(H && evals && evecs && m >= 1 && k >= 1 && k <= m, "bad arguments");
+        std::vector<double> A(H, H + (size_t)m * m), ev, Y;
+        if (m == 1) {
+            evals[0] = A[0];
+            evecs[0] = 1.0;
+            return;
+        }
+        sym_topk(m, A, k, ev, Y);
+        std::copy(ev.begin(), ev.end(), evals);
+        std::copy(Y.begin(), Y.end(), evecs);
+    });
+}
+
+int hh_comp_pca_status(const hh_comp* c, int32_t* converged, int32_t* products, int32_t* cycles, int32_t* method) {
+    return guard([&] {
+        HH_REQUIRE(c, "null");
+        if (converged) *converged = c->pca_converged;
+        if (products) *products = c->pca_products;
+        if (cycles) *cycles = c->pca_cycles;
+        if (method) *method = c->pca_method;
     });
 }
 

@@ -102,6 +102,12 @@ struct KTimeScope {
 // without binning.
 inline int g_parse_ablate = 0;
 
+// Compartment PCA eigensolver (hh_tune "pca_method" 0 = block subspace
+// iteration, 1 = block Krylov; "pca_p" = Cor products per Krylov cycle).
+inline int g_pca_method = 1;
+inline int g_pca_p = 8;
+inline int g_pca_debug = 0;  // hh_tune "pca_debug": per-cycle trace on stderr
+
 // Device memory pool.  hipFree synchronises the device and costs ~0.2 ms per
 // call, which dominated per-chromosome loops (a few large buffers per call),
 // so released blocks are cached and reused (best fit within 2x).  Reuse is

@@ -1202,6 +1202,14 @@ int hh_tune(const char* key, int64_t value) {
         } else if (k == "split_tiles") {
             HH_REQUIRE(value == 0 || value == 1, "split_tiles in {0, 1}");
             g_split_tiles = (int)value;
+        } else if (k == "pca_method") {
+            HH_REQUIRE(value == 0 || value == 1, "pca_method in {0, 1}");
+            g_pca_method = (int)value;
+        } else if (k == "pca_debug") {
+            g_pca_debug = (int)value;
+        } else if (k == "pca_p") {
+            HH_REQUIRE(value >= 2 && value <= 8, "pca_p in [2, 8]");
+            g_pca_p = (int)value;
         } else if (k == "band_concurrent") {
             HH_REQUIRE(value == 0 || value == 1, "band_concurrent in {0, 1}");
             g_band_concurrent = (int)value;

@@ -255,10 +255,27 @@ int hh_comp_get_cor(hh_comp* c, double* cor, void* stream);
 /* Replace the device correlation (n x n from the last hh_comp_correlation). */
 int hh_comp_set_cor(hh_comp* c, const double* cor, void* stream);
 /* Top-k right singular vectors of the column-centred correlation (sklearn
- * PCA(k).fit(Cor).components_, sign: max-|.| entry positive), k x n row-major,
- * by block subspace iteration until 1 - |cos| < tol for each vector. */
+ * PCA(k).fit(Cor).components_, sign: max-|.| entry positive), k x n row-major.
+ * Default method (hh_tune "pca_method" 1): explicit-restart block Krylov on
+ * Cor (16 columns, hh_tune "pca_p" products per cycle) with a Rayleigh-Ritz
+ * step for the centred matrix; stops when the top-k Ritz vectors'
+ * a-posteriori angle bound max ||A x - theta x|| / gap is < tol, or has
+ * stopped shrinking below 1e3 tol (the rounding floor; a degenerate gap never
+ * gets there), after at most 2 * max_iters Cor products.  Method 0
+ * (and the fallback when the basis would not fit, n < 16 (pca_p + 1)): block
+ * subspace iteration, max_iters iterations.  *iters = Cor products (Krylov)
+ * or iterations (subspace).  Not converging is not an error: query
+ * hh_comp_pca_status. */
 int hh_comp_pca(hh_comp* c, int32_t k, double tol, int32_t max_iters, double* components, double* eigvals,
                 int32_t* iters, void* stream);
+/* Outcome of the last hh_comp_pca: converged (1/0), Cor products, Krylov
+ * cycles (subspace: iterations), method (1 Krylov, 0 subspace). */
+int hh_comp_pca_status(const hh_comp* c, int32_t* converged, int32_t* products, int32_t* cycles, int32_t* method);
+/* Host helper (no GPU): top-k eigenpairs, descending, of a symmetric m x m
+ * matrix (Householder tridiagonalisation, implicit QL eigenvalues, inverse
+ * iteration) — the Rayleigh-Ritz solver of the Krylov PCA; evecs m x k
+ * row-major. */
+int hh_sym_topk(const double* H, int32_t m, int32_t k, double* evals, double* evecs);
 /* Per PC q < k (<= 3), 8 sums: [0,1] Cor same-sign pairs in (-1, 1-eps) sum,count;
  * [2,3] Cor (pc_i > 0, pc_j < 0) pairs in (-1, 1) sum,count; [4,5] nonzero O/E
  * over (+,+) sum,count; [6,7] over (-,-) — Select_PC_new's means_minus / select_ab. */

@@ -22,3 +22,13 @@ def golden():
     def load(name):
         return dict(np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False))
     return load
+
+
+def pytest_sessionstart(session):
+    """Measurement knobs passed through the environment (HH_PCA_P,
+    HH_PCA_METHOD) apply to GPU test runs too."""
+    for key in ("pca_p", "pca_method"):
+        v = os.environ.get("HH_" + key.upper())
+        if v:
+            from hichap_master_amd._lib import call
+            call("hh_tune", key.encode(), int(v))

@@ -1,0 +1,193 @@
+"""C5 at its own size (BASELINE configs[4]: hg19 autosomes at 25 kb, dense
+per chromosome) and the compartment eigensolver's edge cases.
+
+chr21 / chr22 (N = 1 926 / 2 053) run the whole compartment path against the
+oracle (exact SVD); chr1 (N = 9 971) is checked by sampled correlation columns
+against NumPy's corrcoef of the same O/E columns and by eigen-residuals of the
+returned components — the oracle's dense SVD of 9 971^2 would take minutes.
+Reference: StructureFind.py:201-271 (Distance_Decay), :302-342 (Get_PCA),
+:374-423 (Select_PC_new)."""
+import warnings
+
+import numpy as np
+import pytest
+
+from oracle import structure_ref
+
+pytestmark = pytest.mark.gpu
+
+C5_RES = 25000
+
+
+def _c5_sizes():
+    from hichap_master_amd import synth
+    return synth.chrom_bins([synth.HG19[str(c)] for c in range(1, 23)], C5_RES)
+
+
+def _c5_kw():
+    # the bench's C5 generator parameters (bench.c5_synth_kw)
+    return dict(A=120.0, trans_density=0.0, comp_block=80, ignore_diags=0, cis_only=True, gap_frac=0.02,
+                seed=20201019)
+
+
+def _c5_matrix(k):
+    import torch
+    from hichap_master_amd import _lib, ice
+    _lib.require_gpu()
+    sizes = _c5_sizes()
+    buf = torch.empty((sizes[k], sizes[k]), dtype=torch.float64, device="cuda")
+    ice.synth_dense(sizes, k, buf.data_ptr(), **_c5_kw())
+    torch.cuda.synchronize()
+    return buf
+
+
+def _match_sign(a, b):
+    return a * np.sign(np.dot(a, b))
+
+
+@pytest.mark.parametrize("chrom", [21, 22])
+def test_c5_small_autosomes_vs_oracle(chrom):
+    from hichap_master_amd.StructureFind import StructureFind
+    dM = _c5_matrix(chrom - 1)
+    M = dM.cpu().numpy()
+    assert M.shape[0] == _c5_sizes()[chrom - 1]
+    sf = StructureFind(Res=C5_RES)
+    dec, G, NG = sf.Distance_Decay(M=dM, G_array=None)
+    d_ref, G_ref, NG_ref = structure_ref.distance_decay(M)
+    np.testing.assert_array_equal(NG, NG_ref)
+    np.testing.assert_allclose(dec, d_ref, rtol=1e-12)
+    pcs, Cor, OE = sf.Get_PCA(distance_bin=dec.copy(), M=dM, NG_array=NG)
+    st = sf.pca_status
+    assert st["converged"] and st["method"] == "krylov"
+    assert st["products"] <= 60, st
+    p_ref, C_ref, _ = structure_ref.get_pca(d_ref, M, NG_ref)
+    np.testing.assert_allclose(np.asarray(Cor), C_ref, atol=1e-11)
+    # PC1 to 1e-11; PC2 / PC3 as far as their eigen-gap allows
+    np.testing.assert_allclose(_match_sign(pcs[0], p_ref[0]), p_ref[0], atol=1e-11)
+    X = C_ref - C_ref.mean(axis=0)
+    s = np.linalg.svd(X, compute_uv=False)
+    lam = s ** 2
+    for q in (1, 2):
+        gap = min(lam[q - 1] - lam[q], lam[q] - lam[q + 1]) / lam[0]
+        np.testing.assert_allclose(_match_sign(pcs[q], p_ref[q]), p_ref[q], atol=max(1e-11, 1e-14 / gap))
+    np.testing.assert_allclose(st["eigvals"], lam[:3], rtol=1e-12)
+    full = sf.compartment(dM)
+    ref_full, k_ref, _, _ = structure_ref.compartment(M)
+    big = np.abs(ref_full) > 1e-8
+    np.testing.assert_array_equal(np.sign(full[big]), np.sign(ref_full[big]))
+    np.testing.assert_allclose(full, ref_full, atol=1e-10)
+
+
+def test_c5_chr1_spot_checks():
+    """chr1 at 25 kb (N = 9 971): sampled Cor entries vs NumPy corrcoef of the
+    same O/E columns; top-3 components orthonormal with eigen-residuals
+    |A v - lambda v| / lambda_1 < 1e-11 (A = Xc^T Xc, Xc = Cor - mean)."""
+    from hichap_master_amd.StructureFind import StructureFind
+    dM = _c5_matrix(0)
+    N = dM.shape[0]
+    assert N == 9971
+    sf = StructureFind(Res=C5_RES)
+    dec, G, NG = sf.Distance_Decay(M=dM, G_array=None)
+    pcs, Cor, OE = sf.Get_PCA(distance_bin=dec.copy(), M=dM, NG_array=NG)
+    st = sf.pca_status
+    assert st["converged"] and st["products"] <= 72, st
+    M = dM.cpu().numpy()
+    del dM
+    C = np.asarray(Cor)
+    n = NG.size
+    rng = np.random.default_rng(1)
+    sel = np.sort(rng.choice(n, size=48, replace=False))
+    dd = dec.copy()
+    dd[dd == 0] = dd[np.nonzero(dd)].min()
+    cols = M[:, NG[sel]]
+    dist = np.abs(np.arange(N)[:, None] - NG[sel][None, :])
+    oe = np.where(cols != 0, cols / dd[dist], 0.0)
+    Cs = structure_ref.pearson_columns(oe)
+    np.testing.assert_allclose(C[np.ix_(sel, sel)], Cs, atol=1e-11)
+    mu = C.mean(axis=0)
+    lam = st["eigvals"]
+    for q in range(3):
+        v = pcs[q]
+        Xv = C @ v - (mu @ v)                          # Xc v = Cor v - 1 (mu . v)
+        Av = C.T @ Xv - mu * Xv.sum()                    # Xc^T w = Cor w - mu (1 . w)
+        assert np.linalg.norm(Av - lam[q] * v) / lam[0] < 1e-11, q
+    np.testing.assert_allclose(pcs @ pcs.T, np.eye(3), atol=1e-12)
+    assert lam[0] > lam[1] > lam[2] > 0
+
+
+def _comp_with_cor(Cor):
+    """An hh_comp whose device correlation is ``Cor`` (n x n)."""
+    from hichap_master_amd.StructureFind import _Comp
+    from hichap_master_amd._lib import call, ptr
+    n = Cor.shape[0]
+    comp = _Comp(np.eye(n))
+    comp.correlation(np.ones(n), np.arange(n))
+    call("hh_comp_set_cor", comp.h, ptr(np.ascontiguousarray(Cor)), None)
+    return comp
+
+
+def _planted(n, s, seed):
+    """Symmetric matrix with zero column means and eigenvalues s (rest 0.01):
+    Xc = Cor, so the PCA components are its top eigenvectors."""
+    rng = np.random.default_rng(seed)
+    Z = rng.standard_normal((n, n))
+    Z -= Z.mean(axis=0)
+    U, _ = np.linalg.qr(Z)
+    U = U[:, : n - 1]  # orthonormal, orthogonal to 1
+    vals = np.full(n - 1, 0.01)
+    vals[: len(s)] = s
+    return (U * vals) @ U.T, U[:, : len(s)]
+
+
+def test_pca_planted_spectrum_exact():
+    Cor, U = _planted(700, [9.0, 6.0, 4.0, 2.0, 1.5], seed=3)
+    comp = _comp_with_cor(Cor)
+    pcs, ev, _ = comp.pca(3)
+    assert comp.pca_status["converged"]
+    for q in range(3):
+        np.testing.assert_allclose(_match_sign(pcs[q], U[:, q]), U[:, q], atol=1e-12)
+    np.testing.assert_allclose(ev, np.array([9.0, 6.0, 4.0]) ** 2, rtol=1e-12)
+
+
+def test_pca_near_degenerate_warns():
+    """lambda_3 == lambda_4: the third component is not determined, the solver
+    must say it did not converge — PC1 / PC2 are still exact."""
+    from hichap_master_amd import StructureFind as SFm
+    Cor, U = _planted(400, [9.0, 6.0, 4.0, 4.0, 1.0], seed=5)
+    comp = _comp_with_cor(Cor)
+    old = SFm.PCA_MAX_ITERS
+    SFm.PCA_MAX_ITERS = 100
+    try:
+        with warnings.catch_warnings(record=True) as rec:
+            warnings.simplefilter("always")
+            pcs, ev, _ = comp.pca(3)
+    finally:
+        SFm.PCA_MAX_ITERS = old
+    assert not comp.pca_status["converged"]
+    assert any(issubclass(w.category, RuntimeWarning) for w in rec)
+    for q in range(2):
+        np.testing.assert_allclose(_match_sign(pcs[q], U[:, q]), U[:, q], atol=1e-11)
+    # the third lies in the degenerate plane
+    r = pcs[2] - U[:, 2:4] @ (U[:, 2:4].T @ pcs[2])
+    assert np.linalg.norm(r) < 1e-10
+
+
+def test_pca_krylov_matches_subspace_iteration():
+    from hichap_master_amd import synth
+    from hichap_master_amd._lib import call
+    from hichap_master_amd.StructureFind import StructureFind
+    rng = np.random.default_rng(44)
+    M = synth.dense_chrom(1200, rng, A=90.0, comp_len=(30, 80), gap_frac=0.02).astype(np.float64)
+    out = {}
+    for meth in (0, 1):
+        call("hh_tune", b"pca_method", meth)
+        try:
+            sf = StructureFind(Res=25000)
+            dec, G, NG = sf.Distance_Decay(M=M, G_array=None)
+            pcs, Cor, OE = sf.Get_PCA(distance_bin=dec.copy(), M=M, NG_array=NG)
+            out[meth] = (pcs, sf.pca_status)
+        finally:
+            call("hh_tune", b"pca_method", 1)
+    assert out[1][1]["method"] == "krylov" and out[0][1]["method"] == "subspace"
+    assert out[1][1]["products"] < out[0][1]["products"] / 2
+    np.testing.assert_allclose(_match_sign(out[1][0][0], out[0][0][0]), out[0][0][0], atol=1e-11)
