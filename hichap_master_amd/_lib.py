@@ -65,6 +65,7 @@ SIGNATURES = {
     "hh_ktime_query": (C.c_int, [C.c_char_p, P, P]),
     "hh_ktime_reset": (C.c_int, []),
     "hh_matrix_from_pixels": (C.c_int, [P, P, P, I64, I64, P, I32, I32, I32, I64, I64, P, C.POINTER(P)]),
+    "hh_matrix_from_pixels_device": (C.c_int, [P, P, P, I64, I64, P, I32, I32, I32, I64, I64, P, C.POINTER(P)]),
     "hh_matrix_free": (C.c_int, [P]),
     "hh_matrix_get_info": (C.c_int, [P, C.POINTER(MatrixInfo)]),
     "hh_matrix_export_upper": (C.c_int, [P, P, P, P, PI64]),

@@ -1205,6 +1205,9 @@ int hh_tune(const char* key, int64_t value) {
         } else if (k == "pca_method") {
             HH_REQUIRE(value == 0 || value == 1, "pca_method in {0, 1}");
             g_pca_method = (int)value;
+        } else if (k == "host_build") {
+            HH_REQUIRE(value == 0 || value == 1, "host_build in {0, 1}");
+            g_host_build = value;
         } else if (k == "pca_debug") {
             g_pca_debug = (int)value;
         } else if (k == "pca_p") {

@@ -256,4 +256,16 @@ inline std::vector<uint16_t> bin_groups(const hh_matrix& m) {
 }
 // Upload the plan arrays (not the payload) into m.
 void upload_plan(const TilePlan& P, hh_matrix& m, hipStream_t s);
+// Device helpers shared with the pair binner (pairs.hip): stable LSD radix
+// sort of n 64-bit keys on their low `bits` bits (synchronous), exclusive
+// scan of n int64 values (*total_dev = the sum, may be null; asynchronous).
+void dev_sort_u64(DBuf<unsigned long long>& keys, int64_t n, int bits, hipStream_t s);
+void dev_excl_scan_i64(const long long* in, long long* out, long long n, unsigned long long* total_dev, hipStream_t s);
+// Device build from a host pixel table (build.hip); false = not a sorted
+// upper-triangle table (nothing built).  g_host_build forces the host builder.
+bool build_from_host_pixels_on_device(const int64_t* bin1, const int64_t* bin2, const double* count, int64_t nnz,
+                                      int64_t n_bins, const int64_t* chrom_offsets, int32_t n_chroms,
+                                      int32_t ignore_diags, int32_t cis_only, int64_t row_lo, int64_t row_hi,
+                                      hipStream_t s, hh_matrix** out);
+extern int64_t g_host_build;
 }  // namespace hh

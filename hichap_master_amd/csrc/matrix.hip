@@ -13,6 +13,7 @@ static thread_local std::string g_last_error;
 int64_t g_unit_entries = 0;  // 0 = auto (plan_tiles)
 int64_t g_band_w = -1;       // -1 = auto (choose_band_w)
 int64_t g_flat_max = 64;     // longest row (uint4) of a flat tile segment; 0 = no flat segments
+int64_t g_host_build = 0;    // hh_tune("host_build"): 1 = host builder for every pixel table
 
 int64_t g_band4 = 1;         // nibble band on
 double g_band4_density = 0.25;
@@ -344,6 +345,12 @@ int hh_matrix_from_pixels(const int64_t* bin1, const int64_t* bin2, const double
                           int32_t ignore_diags, int32_t cis_only, int64_t row_lo, int64_t row_hi,
                           void* stream, hh_matrix** out) {
     return guard([&] {
+        // cooler's sorted upper-triangle table: built on the device (build.hip);
+        // any other order (or g_host_build): the host builder below
+        if (!g_host_build &&
+            build_from_host_pixels_on_device(bin1, bin2, count, nnz, n_bins, chrom_offsets, n_chroms, ignore_diags,
+                                             cis_only, row_lo, row_hi, as_stream(stream), out))
+            return;
         HH_REQUIRE(out && n_bins > 0 && nnz >= 0 && n_chroms > 0 && chrom_offsets, "bad arguments");
         HH_REQUIRE(nnz == 0 || (bin1 && bin2 && count), "null pixel arrays");
         HH_REQUIRE(n_bins < kMaxBins, "n_bins must be < 2^30");
@@ -394,6 +401,9 @@ int hh_matrix_from_pixels(const int64_t* bin1, const int64_t* bin2, const double
             const bool ina = a >= row_lo && a < row_hi, inb = b >= row_lo && b < row_hi;
             if (a == b) {
                 if (ina) {
+                    if (diag[a - row_lo] != 0.0)
+                        HH_THROW(HH_ERR_ARG, "duplicate pixel (" + std::to_string(a) + ", " + std::to_string(b) +
+                                                 "): cooler's pixel table has unique (bin1, bin2)");
                     diag[a - row_lo] += c;
                     rnnz[a - row_lo] += 2.0;
                     rsum[a - row_lo] += 2.0 * c;
@@ -447,11 +457,20 @@ int hh_matrix_from_pixels(const int64_t* bin1, const int64_t* bin2, const double
         std::vector<std::pair<int32_t, uint32_t>> tmp;
         for (int64_t r = 0; r < nloc; ++r) {
             const int64_t lo = deg[r], hi = deg[r + 1];
-            if (std::is_sorted(cols.begin() + lo, cols.begin() + hi)) continue;
-            tmp.clear();
-            for (int64_t k = lo; k < hi; ++k) tmp.emplace_back(cols[k], vals[k]);
-            std::stable_sort(tmp.begin(), tmp.end(), [](auto& x, auto& y) { return x.first < y.first; });
-            for (int64_t k = lo; k < hi; ++k) { cols[k] = tmp[k - lo].first; vals[k] = tmp[k - lo].second; }
+            if (!std::is_sorted(cols.begin() + lo, cols.begin() + hi)) {
+                tmp.clear();
+                for (int64_t k = lo; k < hi; ++k) tmp.emplace_back(cols[k], vals[k]);
+                std::stable_sort(tmp.begin(), tmp.end(), [](auto& x, auto& y) { return x.first < y.first; });
+                for (int64_t k = lo; k < hi; ++k) { cols[k] = tmp[k - lo].first; vals[k] = tmp[k - lo].second; }
+            }
+            // a repeated (bin1, bin2) would be counted twice by the filters'
+            // marginals but once by the dense bands: reject it (cooler's
+            // pixel table is unique)
+            for (int64_t k = lo + 1; k < hi; ++k)
+                if (cols[k] == cols[k - 1])
+                    HH_THROW(HH_ERR_ARG, "duplicate pixel (" + std::to_string(std::min<int64_t>(row_lo + r, cols[k])) +
+                                             ", " + std::to_string(std::max<int64_t>(row_lo + r, cols[k])) +
+                                             "): cooler's pixel table has unique (bin1, bin2)");
         }
         // tile counts: narrow (count <= 7) and wide entries per (row, tile);
         // counts > kCntMax go to the wide list

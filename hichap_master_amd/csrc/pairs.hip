@@ -1326,6 +1326,12 @@ static void sort_keys(DBuf<unsigned long long>& keys, int64_t n, int bits, hipSt
     HIP_CHECK(hipStreamSynchronize(s));  // tmp / hist are released to the pool
 }
 
+// Shared with the device matrix build (build.hip, ice_internal.hpp).
+void dev_sort_u64(DBuf<unsigned long long>& keys, int64_t n, int bits, hipStream_t s) { sort_keys(keys, n, bits, s); }
+void dev_excl_scan_i64(const long long* in, long long* out, long long n, unsigned long long* total_dev, hipStream_t s) {
+    exclusive_scan<long long, long long>(in, out, n, total_dev, s);
+}
+
 }  // namespace hh
 
 extern "C" {

@@ -9,8 +9,12 @@ Each rank holds complete symmetric rows ``[rank_rows[r], rank_rows[r+1])`` of
 the pixel-chunk matrix, so the marginal of its own rows is exact locally; the
 only exchange per iteration is an all-gather of those marginals (n_bins x 8 B
 in total: 4.9 MB for the diploid 10 kb genome).  Every rank then runs the
-identical variance / bias update on the full vector.  With
-fixed-tree reductions the weights are bitwise independent of the world size.
+identical variance / bias update on the full vector.  Every
+reduction is a fixed tree, so the weights are bitwise reproducible for a fixed
+unit plan; the work-unit size adapts to each shard's payload, which regroups a
+row's partial sums, so runs with different world sizes agree to ~1e-15
+relative rather than bitwise (bitwise whenever the unit plan is the same, e.g.
+small matrices at the unit-size floor, or a pinned hh_tune("unit_entries")).
 
 The driver is written against a small backend protocol (``marg_local``,
 ``set_marg``, ``filter_nnz``, ``filter_count_mad``, ``update``,

@@ -69,6 +69,33 @@ class ContactMatrix:
         return cls(h, off)
 
     @classmethod
+    def from_device_pixels(cls, bin1, bin2, count, n_bins, chrom_offsets, ignore_diags=1, cis_only=False,
+                           row_range=None, stream=None, nnz=None):
+        """Build from a pixel table already in HBM (cooler order: sorted by
+        (bin1, bin2), bin1 <= bin2, unique; int32 ids and counts) — e.g. the
+        output of ``PairBinner`` — with no host round trip.  ``bin1`` /
+        ``bin2`` / ``count`` are int32 torch tensors or raw device pointers
+        (then ``nnz`` is required)."""
+        _lib.require_gpu()
+        def dptr(x):
+            if hasattr(x, "data_ptr"):
+                import torch
+                if x.dtype != torch.int32 or not x.is_cuda or not x.is_contiguous():
+                    raise ValueError("expected contiguous int32 device tensors")
+                return C.c_void_p(x.data_ptr()), int(x.numel())
+            return C.c_void_p(int(x)), None
+        (p1, n1), (p2, n2), (pc, n3) = dptr(bin1), dptr(bin2), dptr(count)
+        n = nnz if nnz is not None else n1
+        if n is None or (n1 is not None and not (n1 == n2 == n3 == n)):
+            raise ValueError("bin1, bin2 and count must have the same length (nnz)")
+        off = np.ascontiguousarray(chrom_offsets, dtype=np.int64)
+        lo, hi = (0, int(n_bins)) if row_range is None else (int(row_range[0]), int(row_range[1]))
+        h = C.c_void_p()
+        call("hh_matrix_from_pixels_device", p1, p2, pc, int(n), int(n_bins), ptr(off), off.size - 1,
+             int(ignore_diags), int(bool(cis_only)), lo, hi, stream, C.byref(h))
+        return cls(h, off)
+
+    @classmethod
     def synthetic(cls, chrom_nbins, row_range=None, stream=None, **kw):
         """Generate a synthetic genome in HBM (see synth_params); rows
         ``row_range`` (aligned to 512-row blocks) or all."""

@@ -224,8 +224,11 @@ def significance(B, xi, yi, S, E, valid):
         fold = Ov / Ev
         pv = np.ones(x.size)
         qv = np.ones(x.size)
-        if Ev.size:
-            edges = lambda_chunks(Ev)
+        edges = lambda_chunks(Ev) if Ev.size else []
+        # no chunk at all when every expected value is below 2**(-2/3)
+        # (numbin <= 0): the reference's lambdachunk Pool is empty, so p and q
+        # stay 1 and nothing is called (StructureFind.py:1617-1629, :1866-1880)
+        if edges:
             rvs = np.array([e[1] for e in edges], dtype=np.float64)
             lvs = np.array([e[0] for e in edges], dtype=np.float64)
             ci = np.searchsorted(rvs, Ev, side="right")        # first rv > E

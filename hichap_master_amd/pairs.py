@@ -305,6 +305,37 @@ class PairBinner:
         call("hh_binner_download", self._h, t.index, ptr(b1), ptr(b2), ptr(c))
         return b1, b2, c
 
+    def pixels_device(self, t: Target):
+        """(bin1_ptr, bin2_ptr, count_ptr, nnz): device pointers of a finished
+        target's int32 pixel table (valid until close())."""
+        if not self.finished:
+            self.finish()
+        nnz, npairs = C.c_int64(0), C.c_int64(0)
+        call("hh_binner_target_nnz", self._h, t.index, C.byref(nnz), C.byref(npairs))
+        p1, p2, pc = C.c_void_p(), C.c_void_p(), C.c_void_p()
+        call("hh_binner_pixels_device", self._h, t.index, C.byref(p1), C.byref(p2), C.byref(pc))
+        return p1.value or 0, p2.value or 0, pc.value or 0, int(nnz.value)
+
+    def chrom_offsets(self, t: Target) -> np.ndarray:
+        """cooler ``indexes/chrom_offset`` of a target's bin layout (haplotype:
+        the M chromosomes then the P chromosomes)."""
+        nb = np.asarray(t.chrom_nbins, dtype=np.int64)
+        if t.haplotype:
+            nb = np.concatenate([nb, nb])
+        return np.concatenate([[0], np.cumsum(nb)]).astype(np.int64)
+
+    def contact_matrix(self, t: Target, ignore_diags=1, cis_only=None, row_range=None):
+        """The target's pixel table straight into an HBM-resident
+        ``ice.ContactMatrix`` (no host round trip): bin -> cooler -> balance
+        of TraditionalMatrixConstruction (matrixBuilding.py:617-714) without
+        the cooler file.  ``cis_only`` defaults to the target being local
+        (HiCHap balances localRes coolers with --cis-only, :713)."""
+        from .ice import ContactMatrix
+        p1, p2, pc, nnz = self.pixels_device(t)
+        cis = t.local if cis_only is None else bool(cis_only)
+        return ContactMatrix.from_device_pixels(p1, p2, pc, t.n_bins, self.chrom_offsets(t), ignore_diags, cis,
+                                                row_range=row_range, stream=self.stream, nnz=nnz)
+
     def close(self):
         if getattr(self, "_h", None):
             call("hh_binner_free", self._h)

@@ -109,8 +109,9 @@ typedef struct {
     int32_t pad2_;
 } hh_matrix_info;
 
-/* Build from cooler's pixel table (upper triangle bin1 <= bin2; any order,
- * sorted input is fastest).  Counts must be non-negative integers < 2^32
+/* Build from cooler's pixel table (host arrays; any order: a sorted
+ * upper-triangle table is uploaded and built on the device, anything else is
+ * built on the host; duplicate (bin1, bin2) pixels fail with HH_ERR_ARG).  Counts must be non-negative integers < 2^32
  * (cooler `count`, int32 in HiCHap's traditional coolers, matrixBuilding.py:196).
  * chrom_offsets[n_chroms+1] = cooler `indexes/chrom_offset`. Rows outside
  * [row_lo, row_hi) are not stored (a shard for multi-GPU genome-wide ICE). */
@@ -118,6 +119,19 @@ int hh_matrix_from_pixels(const int64_t* bin1, const int64_t* bin2, const double
                           int64_t nnz, int64_t n_bins, const int64_t* chrom_offsets,
                           int32_t n_chroms, int32_t ignore_diags, int32_t cis_only,
                           int64_t row_lo, int64_t row_hi, void* stream, hh_matrix** out);
+/* The same from a DEVICE pixel table in cooler's own order — sorted by
+ * (bin1, bin2), bin1 <= bin2, unique — with int32 ids and counts (cooler's
+ * `count` dtype for HiCHap's traditional coolers; what hh_binner_pixels_device
+ * hands out).  Built entirely on the device (filters, symmetric rows by a
+ * radix sort of the lower half, tile counts, payload); the layout equals
+ * hh_matrix_from_pixels'.  A table out of order, with a duplicate pixel, a
+ * negative count or an id out of range fails with HH_ERR_ARG naming the first
+ * offending pixel.  hh_matrix_from_pixels itself takes this path whenever its
+ * host table is sorted upper-triangle (uploading it once), and builds on the
+ * host otherwise (hh_tune "host_build" 1 forces the host builder). */
+int hh_matrix_from_pixels_device(const int32_t* bin1, const int32_t* bin2, const int32_t* count, int64_t nnz,
+                                 int64_t n_bins, const int64_t* chrom_offsets, int32_t n_chroms, int32_t ignore_diags,
+                                 int32_t cis_only, int64_t row_lo, int64_t row_hi, void* stream, hh_matrix** out);
 int hh_matrix_free(hh_matrix* m);
 int hh_matrix_get_info(const hh_matrix* m, hh_matrix_info* info);
 /* Copy the stored upper-triangle pixels (bin1 <= bin2, bin1 in the local rows

@@ -90,6 +90,20 @@ def test_no_candidates(lp):
     assert D == {} and L == {}
 
 
+def test_low_coverage_band_calls_nothing(lp):
+    """Every expected value below 2**(-2/3): the reference's lambdachunk has no
+    chunk, p = q = 1 and nothing is called (this used to raise)."""
+    rng = np.random.default_rng(12)
+    N = 300
+    up = np.triu(rng.poisson(0.04, size=(N, N)), 1)
+    H = (up + up.T).astype(np.int64)
+    B = lp.bands(H, np.ones(N), 40000)
+    xi, yi = lp.candidates(B)
+    assert xi.size > 0
+    D, L = lp.pcaller(H, np.ones(N), 40000)
+    assert D == {} and L == {}
+
+
 def test_call_peaks_writes_reference_format(lp, golden, tmp_path):
     g = golden("loops_trad_n360")
     out = tmp_path / "loops.txt"
