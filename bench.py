@@ -84,21 +84,23 @@ SWEEP_KERNELS = ("k_sweep_tiled", "k_sweep_flat", "k_sweep_band")  # band: <8> o
 
 def pmc_traffic(kernels=SWEEP_KERNELS):
     """HBM bytes per ICE sweep (the three sweep kernels, one launch each)
-    from the committed rocprofv3 PMC summary of this same command
-    (tools/pmc_summary.py), or None."""
+    from the newest committed rocprofv3 PMC summary of the C4 bench
+    (tools/pmc_summary.py), its metadata (commit, the layout's real bytes per
+    sweep) and the file name; (None, None, None) without one."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_c4_pmc.json")))
     if not files:
-        return None, None
+        return None, None, None
     data = json.load(open(files[-1]))
-    hits = [v for k, v in data.items() if any(name in k for name in kernels)]
+    meta = data.get("_meta", {})
+    hits = [v for k, v in data.items() if k != "_meta" and any(name in k for name in kernels)]
     if not hits:
-        return None, None
+        return None, None, None
     # per sweep: a kernel launched k times per sweep (the 4-bit band's two
     # segments) has k times as many dispatches as the once-per-sweep kernels
     base = min(v.get("dispatches", 1) or 1 for v in hits)
     tot = sum(v["traffic_bytes"] * (v.get("dispatches", base) or base) / base for v in hits)
-    return tot, os.path.relpath(files[-1], ROOT)
+    return tot, meta, os.path.relpath(files[-1], ROOT)
 
 
 def cpu_baseline(sizes, kw, rc, nnz_total, label, budget_s=12.0):
@@ -595,6 +597,134 @@ def loops_cpu_baseline(budget_s=12.0):
                       f"shifted-diagonal sums are slower still)"}
 
 
+def run_dropin(args, world, rank, local):
+    """The drop-in path as a HiCHap user reaches it: cooler's
+    pixel table on the HOST (int32 bin1 / bin2 / count, sorted, as
+    ``cooler.Cooler(uri).pixels()`` holds it) -> upload -> device layout build
+    -> filters -> ICE, each phase timed.  Workload: C3 (hg19 40 kb whole
+    genome, 8e8 pixels; the synthetic matrix's pixel table is exported once to
+    the host first, untimed).  A step = the whole chain; ICE runs cooler's
+    defaults (tol 1e-5, max 200 iterations) unless --fixed-iters."""
+    import torch
+    from hichap_master_amd import ice
+    sizes, kw, label, target, tf = config("c3", args.nnz)
+    n = int(np.sum(sizes))
+    m = ice.ContactMatrix.synthetic(sizes, **kw)
+    b1, b2, c = m.export_upper()
+    m.close()
+    off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    hb1, hb2, hc = (np.ascontiguousarray(x, dtype=np.int32) for x in (b1, b2, c))
+    del b1, b2, c
+    nnz = hb1.size
+    opts = ice.IceOptions(max_iters=args.iters, tol=0.0 if args.fixed_iters else 1e-5)
+    stream = torch.cuda.current_stream().cuda_stream
+    phases = {}
+
+    def step():
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        d = [torch.from_numpy(x).to("cuda", non_blocking=False) for x in (hb1, hb2, hc)]
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        mm = ice.ContactMatrix.from_device_pixels(d[0], d[1], d[2], n, off, stream=stream)
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        del d
+        w, st = ice.balance_matrix(mm, opts, stream)
+        t3 = time.perf_counter()
+        mm.close()
+        for k, v in (("upload_s", t1 - t0), ("build_s", t2 - t1), ("filters_and_ice_s", t3 - t2),
+                     ("ice_sweeps_s", st["sweep_seconds"])):
+            phases.setdefault(k, []).append(v)
+        phases.setdefault("iters", []).append(st["iters"])
+        return w
+
+    for _ in range(args.warmup):
+        step()
+    phases.clear()
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    elapsed = time.perf_counter() - t_start
+    if rank == 0:
+        med = {k: float(np.median(v)) for k, v in phases.items()}
+        up_bytes = 12.0 * nnz
+        out = {
+            "metric": "cooler-balance drop-in: host pixel table -> weights (C3, hg19 40 kb whole genome)",
+            "value": args.steps / elapsed, "unit": "balanced matrices/s", "n_gpus": 1, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": 1000.0 * elapsed / args.steps, "higher_is_better": True,
+            "scaling": "replicas", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic C3 pixel table (SURVEY.md §8(d) model) exported to host int32 arrays",
+            "config": {"workload": label + "-host-pixel-table", "n_bins": n, "pixels": int(nnz),
+                       "ice": "tol 0 (fixed iterations)" if args.fixed_iters else "cooler defaults (tol 1e-5)",
+                       "max_iters": args.iters},
+            "phases_median": med,
+            "upload_GBps": up_bytes / med["upload_s"] / 1e9,
+            "build_pixels_per_s": nnz / med["build_s"],
+            "note": "upload = pageable host int32 -> HBM (PCIe); build = hh_matrix_from_pixels_device "
+                    "(validate, filters, lower-half radix sort, tiles/bands); filters_and_ice = hh_ice_balance",
+        }
+        print(json.dumps(out), flush=True)
+
+
+def run_e2e(args, world, rank, local):
+    """pairs -> weights with nothing on the host: synthetic *_Valid.bed text in
+    HBM -> PairBinner (whole-genome target at --res) -> ContactMatrix (device
+    build from the binner's table) -> ICE (cooler defaults).  The chain of
+    TraditionalMatrixConstruction + `cooler balance` (matrixBuilding.py:617-714)
+    without the cooler file.  A step = the whole chain."""
+    import torch
+    from hichap_master_amd import ice, pairs
+    genome = pairs_genome()
+    n_lines = int(args.pairs)
+    text = synth_pairs_text(genome, n_lines, line0=rank * n_lines)
+    fmt = pairs.pairs_format(pairs.VALID_BED)
+    stream = torch.cuda.current_stream().cuda_stream
+    opts = ice.IceOptions(max_iters=args.iters, tol=1e-5)
+    phases, info = {}, {}
+
+    def step():
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        B = pairs.PairBinner(genome, ["#", "X"], stream=stream)
+        t = B.add_target(args.res)
+        B.feed_device(text.data_ptr(), text.numel(), fmt)
+        B.finish()
+        t1 = time.perf_counter()
+        mm = B.contact_matrix(t)
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        w, st = ice.balance_matrix(mm, opts, stream)
+        t3 = time.perf_counter()
+        info.update(pixels=B.sizes(t)[0], bins=t.n_bins, iters=st["iters"], converged=st["converged"],
+                    payload_bytes=mm.info()["payload_bytes"])
+        mm.close()
+        B.close()
+        for k, v in (("bin_s", t1 - t0), ("build_s", t2 - t1), ("filters_and_ice_s", t3 - t2),
+                     ("ice_sweeps_s", st["sweep_seconds"])):
+            phases.setdefault(k, []).append(v)
+
+    for _ in range(args.warmup):
+        step()
+    phases.clear()
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    elapsed = time.perf_counter() - t_start
+    if rank == 0:
+        out = {
+            "metric": "pairs -> ICE weights end to end (Valid.bed text in HBM, whole genome)",
+            "value": n_lines * args.steps / elapsed, "unit": "pairs/s", "n_gpus": 1, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": 1000.0 * elapsed / args.steps, "higher_is_better": True,
+            "scaling": "replicas", "vs_baseline": None, "dtype": "int64/f64",
+            "data": "synthetic hg19 *_Valid.bed text generated in HBM",
+            "config": {"workload": f"hg19-validbed-{args.res // 1000}kb-wholegenome-balance", "pairs": n_lines,
+                       "res": args.res, **info},
+            "phases_median": {k: float(np.median(v)) for k, v in phases.items()},
+        }
+        print(json.dumps(out), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -604,6 +734,9 @@ def main():
     ap.add_argument("--nnz", type=float, default=None)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--pairs", type=float, default=2e8, help="pairs per rank for --config pairs")
+    ap.add_argument("--iters", type=int, default=200, help="ICE iteration cap for --config dropin / e2e")
+    ap.add_argument("--fixed-iters", action="store_true", help="dropin: tol 0 (exactly --iters iterations)")
+    ap.add_argument("--res", type=int, default=10000, help="whole-genome resolution for --config e2e")
     ap.add_argument("--sharded", action="store_true",
                     help="use the multi-GPU (all-gather) driver even at N=1 (path check)")
     args = ap.parse_args()
@@ -631,8 +764,9 @@ def main():
         else:
             tdist.init_process_group(backend)
 
-    if args.config in ("c5", "pairs", "loops"):
-        {"c5": run_c5, "pairs": run_pairs, "loops": run_loops}[args.config](args, world, rank, local)
+    if args.config in ("c5", "pairs", "loops", "dropin", "e2e"):
+        {"c5": run_c5, "pairs": run_pairs, "loops": run_loops, "dropin": run_dropin,
+         "e2e": run_e2e}[args.config](args, world, rank, local)
         if torch.distributed.is_initialized():
             torch.distributed.destroy_process_group()
         return
@@ -751,37 +885,50 @@ def main():
                        "tiles": inf["n_tiles"], "units": inf["n_units"],
                        "hbm_bytes_matrix": inf["device_bytes"]},
         }
-        traffic, traffic_src = (pmc_traffic() if args.config == "c4" and args.nnz is None
-                                else (None, None))
+        traffic, meta, traffic_src = (pmc_traffic() if args.config == "c4" and args.nnz is None
+                                      else (None, None, None))
         if launches:
             # per launch on the slowest rank (= the whole matrix at N=1)
             sweep_avg = shard_sweep_ms / 1000.0
-            achieved = ALG_BYTES_PER_PIXEL * shard_nnz / sweep_avg / 1e9
+            alg_gbps = ALG_BYTES_PER_PIXEL * shard_nnz / sweep_avg / 1e9
             # bytes the layout actually streams: entries (uint16 + uint32) +
             # both segments' row pointers (the b staging shows up in traffic)
             real_b = shard_real
-            if world > 1:
-                traffic = None  # the committed PMC summary is for the 1-GPU matrix
+            if traffic and world > 1:
+                # the PMC summary is of the whole matrix: scale its
+                # traffic-per-payload-byte ratio to this shard's payload
+                full_real = (meta or {}).get("real_bytes_per_sweep")
+                traffic = traffic / full_real * real_b if full_real else None
+                traffic_src = f"{traffic_src} (scaled by shard payload)" if traffic else None
+            phys = traffic if traffic else real_b
+            achieved = phys / sweep_avg / 1e9
             out["roofline"] = {"bound": "hbm", "kernel": "ice sweep span: k_sweep_flat | k_sweep_tiled | k_sweep_band<8> + 2 x k_sweep_band<4> on three streams (HIP events around the sweep; rocprof per-sweep span: tools/sweep_span.py)",
                                "achieved": achieved,
                                "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS,
+                               "bytes_per_launch": phys,
+                               "bytes_source": "PMC traffic" if traffic else "layout payload (no PMC summary)",
                                "traffic": traffic,
                                "traffic_source": traffic_src,
+                               "traffic_profile_commit": (meta or {}).get("commit"),
                                "real_bytes_per_launch": real_b,
                                "real_GBps": real_b / sweep_avg / 1e9,
                                "real_frac": real_b / sweep_avg / 1e9 / PEAK_HBM_GBS,
-                               "traffic_GBps": (traffic / sweep_avg / 1e9) if traffic else None,
+                               "alg_effective_GBps": alg_gbps,
+                               "alg_bytes_per_launch": ALG_BYTES_PER_PIXEL * shard_nnz,
                                "sweep_ms_avg": sweep_avg * 1000.0,
                                "iter_ms_avg": iter_ms / launches,
                                "per_rank": "slowest rank's shard" if world > 1 else "whole matrix",
                                "shard_nnz_upper": shard_nnz,
-                               "note": "achieved = SURVEY 8(d) algorithmic 12 B/pixel / sweep time; frac > 1 "
-                                       "because the HBM layout streams ~3.6 B/pixel (DESIGN.md 3); "
-                                       "traffic_GBps / peak is the physical HBM utilisation"}
+                               "note": "achieved / frac = physical HBM bytes per sweep (PMC traffic, else the "
+                                       "layout's payload) / sweep time; alg_effective_GBps = SURVEY 8(d)'s "
+                                       "12 B/pixel / sweep time (> peak: the layout streams ~3 B/pixel, DESIGN.md 3)"}
         if tad is not None:
             out["tad_scan"] = tad
         if world == 1 and not args.no_cpu:
             out["cpu_baseline"] = cpu_baseline(sizes, kw, rc, nnz_total, label)
+            # vs_baseline stays null (BASELINE.md publishes no number for this
+            # metric); the ratio to the measured CPU baseline is reported here
+            out["vs_cpu_baseline"] = its / out["cpu_baseline"]["value"]
         print(json.dumps(out), flush=True)
     if torch.distributed.is_initialized():
         torch.distributed.destroy_process_group()

@@ -60,6 +60,7 @@ SIGNATURES = {
     "hh_device_count": (C.c_int, [PI32]),
     "hh_set_device": (C.c_int, [I32]),
     "hh_synchronize": (C.c_int, [P]),
+    "hh_device_copy": (C.c_int, [P, P, I64, P]),
     "hh_tune": (C.c_int, [C.c_char_p, I64]),
     "hh_ktime_enable": (C.c_int, [I32]),
     "hh_ktime_query": (C.c_int, [C.c_char_p, P, P]),
@@ -118,6 +119,13 @@ SIGNATURES = {
     "hh_binner_target_nnz": (C.c_int, [P, I32, PI64, PI64]),
     "hh_binner_download": (C.c_int, [P, I32, P, P, P]),
     "hh_binner_pixels_device": (C.c_int, [P, I32, P, P, P]),
+    "hh_gw_create": (C.c_int, [P, P, P, I64, P, P, P, I64, I64, P, I32, P, C.POINTER(P)]),
+    "hh_gw_create_device": (C.c_int, [P, P, P, I64, P, P, P, I64, I64, P, I32, P, C.POINTER(P)]),
+    "hh_gw_free": (C.c_int, [P]),
+    "hh_gw_stats": (C.c_int, [P, P, P, P, PI64]),
+    "hh_gw_correct": (C.c_int, [P, P, F64, PI64, P]),
+    "hh_gw_result": (C.c_int, [P, P, P, P, P]),
+    "hh_gw_result_device": (C.c_int, [P, P, P, P]),
     "hh_hiccups_create": (C.c_int, [P, P, P, I64, I32, I32, I32, P, C.POINTER(P)]),
     "hh_hiccups_free": (C.c_int, [P]),
     "hh_hiccups_set_pixels": (C.c_int, [P, P, P, I64, P]),

@@ -1,0 +1,544 @@
+// Sparse GenomeWideMatrixCorrection (matrixBuilding.py:857-901) for whole-
+// genome diploid matrices too large for the reference's dense 2n x 2n NumPy
+// arrays (10 kb diploid: 607 282^2 fp64 = 2.9 TB).  Inputs are the pixel
+// tables HiCHap's matrix construction produces: the traditional whole-genome
+// table T (cooler order: bin1 <= bin2, sorted, unique; n bins) and the
+// imputed haplotype matrix H as ordered cells (row, col, count) sorted by
+// (row, col) — H is asymmetric (R1/R2 imputation, :1290-1301) — on the
+// 2n-bin layout M chromosomes then P chromosomes (:429-454).
+//
+//   hh_gw_create   validate, H row pointers, a radix sort of H's off-diagonal
+//                  cells by column (column lists), and the exact integer row
+//                  statistics the alpha step needs: T row sums / nonzeros
+//                  within each chromosome's block (Tra_M, Gap_definedLowRes),
+//                  H row sums within the same-chromosome same-haplotype block
+//                  (M_M / P_P), sum(H)
+//   (host glue)    alpha per chromosome with NumPy's percentile semantics
+//                  (hichap_master_amd.matrixBuilding, as for the dense path)
+//   hh_gw_correct  S = H / Alpha[:, None]; Y = Trans2symmetryLowRes(S) (Y_ij =
+//                  S_ij + S_ji off the diagonal, :770-777) as an upper-triangle
+//                  table: every (r, c >= r) of H's row plus every lower cell
+//                  (i > r, r) without a partner, merged in column order by
+//                  binary searches; Correct_VC(Y, 2/3) (:780-790) with the
+//                  symmetric marginal rowsum(Y)_r = rowsum(S)_r +
+//                  off-diagonal colsum(S)_r; mean rescale (:897-899).
+// Every sum is a fixed-order reduction (integer ones exact): deterministic.
+#include <algorithm>
+#include <cmath>
+#include <numeric>
+
+#include "ice_internal.hpp"
+
+namespace hh {
+
+template <class Id, class Cnt>
+__global__ __launch_bounds__(256) void k_gw_check(const Id* __restrict__ r_in, const Id* __restrict__ c_in,
+                                                  const Cnt* __restrict__ v_in, long long nnz, long long nb,
+                                                  int upper, int32_t* __restrict__ R, int32_t* __restrict__ Cc,
+                                                  uint32_t* __restrict__ V, unsigned long long* __restrict__ errs) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nnz) return;
+    const long long a = (long long)r_in[i], b = (long long)c_in[i];
+    const double v = (double)v_in[i];
+    int code = 0;
+    if (a < 0 || b < 0 || a >= nb || b >= nb) code = 1;
+    else if (upper && a > b) code = 2;
+    else if (i > 0) {
+        const long long pa = (long long)r_in[i - 1], pb = (long long)c_in[i - 1];
+        if (pa > a || (pa == a && pb > b)) code = 3;
+        else if (pa == a && pb == b) code = 4;
+    }
+    if (!code && (!(v >= 0.0) || v != floor(v) || v >= 4294967296.0)) code = 5;
+    if (code) {
+        atomicMin(errs + code - 1, (unsigned long long)i);
+        R[i] = Cc[i] = 0;
+        V[i] = 0u;
+        return;
+    }
+    R[i] = (int32_t)a;
+    Cc[i] = (int32_t)b;
+    V[i] = (uint32_t)v;
+}
+
+// ptr[r] = first i with A[i] >= r, r in [0, nr] (A sorted)
+__global__ void k_px_rowptr_gw(const int32_t* __restrict__ A, long long nnz, long long nr, long long* __restrict__ ptr) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i > nnz) return;
+    const long long lo = i == 0 ? -1 : (long long)A[i - 1];
+    const long long hi = i == nnz ? nr : (long long)A[i];
+    for (long long r = lo + 1; r <= hi; ++r) ptr[r] = i;
+}
+
+// the same from the high bits of sorted keys
+__global__ void k_px_keyptr_gw(const unsigned long long* __restrict__ keys, long long n, int ib, long long nr,
+                               long long* __restrict__ ptr) {
+    const long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k > n) return;
+    const long long lo = k == 0 ? -1 : (long long)(keys[k - 1] >> ib);
+    const long long hi = k == n ? nr : (long long)(keys[k] >> ib);
+    for (long long r = lo + 1; r <= hi; ++r) ptr[r] = k;
+}
+
+// T row statistics within each chromosome block (both ends of an upper pixel,
+// the diagonal once): exact integer sums / counts
+__global__ void k_gw_tstats(const int32_t* __restrict__ a, const int32_t* __restrict__ b,
+                            const uint32_t* __restrict__ v, long long nnz, const int32_t* __restrict__ chrom_of,
+                            unsigned long long* __restrict__ rsum, unsigned long long* __restrict__ rnz) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nnz) return;
+    const int32_t x = a[i], y = b[i];
+    const uint32_t c = v[i];
+    if (c == 0u || chrom_of[x] != chrom_of[y]) return;
+    atomicAdd(rsum + x, (unsigned long long)c);
+    atomicAdd(rnz + x, 1ull);
+    if (x != y) {
+        atomicAdd(rsum + y, (unsigned long long)c);
+        atomicAdd(rnz + y, 1ull);
+    }
+}
+
+// H row sums within the same-chromosome same-haplotype block, and sum(H)
+__global__ void k_gw_hstats(const int32_t* __restrict__ r, const int32_t* __restrict__ c,
+                            const uint32_t* __restrict__ v, long long nnz, const int32_t* __restrict__ block_of,
+                            unsigned long long* __restrict__ bsum, unsigned long long* __restrict__ total) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    unsigned long long t = 0;
+    if (i < nnz) {
+        const uint32_t x = v[i];
+        t = x;
+        if (x && block_of[r[i]] == block_of[c[i]]) atomicAdd(bsum + r[i], (unsigned long long)x);
+    }
+    t = (unsigned long long)wave_sum_ll((long long)t);
+    if ((threadIdx.x & 63) == 0 && t) atomicAdd(total, t);
+}
+
+// off-diagonal cells keyed by column: (col << ib) | index
+__global__ __launch_bounds__(256) void k_gw_colkeys(const int32_t* __restrict__ r, const int32_t* __restrict__ c,
+                                                    long long nnz, int ib, unsigned long long* __restrict__ keys,
+                                                    unsigned long long* __restrict__ n_keys) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool take = i < nnz && r[i] != c[i];
+    const unsigned long long m = __ballot(take);
+    if (!m) return;
+    const int lane = threadIdx.x & 63;
+    unsigned long long base = 0;
+    if (lane == 63 - __clzll(m)) base = atomicAdd(n_keys, (unsigned long long)__popcll(m));
+    base = __shfl(base, 63 - __clzll(m), 64);
+    if (take) keys[base + __popcll(m & ((1ull << lane) - 1ull))] = ((unsigned long long)c[i] << ib) | (unsigned long long)i;
+}
+
+__device__ __forceinline__ long long lower_bound_i32(const int32_t* a, long long lo, long long hi, int32_t x) {
+    while (lo < hi) {
+        const long long mid = (lo + hi) >> 1;
+        if (a[mid] < x) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+// first key position in [lo, hi) of the column list whose cell row >= x
+__device__ __forceinline__ long long lower_bound_keyrow(const unsigned long long* keys, unsigned long long imask,
+                                                        const int32_t* R, long long lo, long long hi, int32_t x) {
+    while (lo < hi) {
+        const long long mid = (lo + hi) >> 1;
+        if (R[(long long)(keys[mid] & imask)] < x) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+struct GwDev {
+    const int32_t* R;
+    const int32_t* C;
+    const uint32_t* V;
+    const long long* hptr;      // N2 + 1 row pointers of H
+    const unsigned long long* keys;  // off-diagonal cells sorted by (col, row)
+    const long long* cptr;      // N2 + 1 column-list pointers
+    unsigned long long imask;
+    int ib;
+    long long N2;
+    const double* alpha;        // N2
+    long long* ustart;          // per row: first cell with col >= row
+    long long* lstart;          // per column r: first list entry with row > r
+};
+
+// per row r (one wave): rowsum(S)_r and the off-diagonal column sum of S in
+// column r, in list order (fixed xor-tree per chunk): the symmetric marginal
+// of Y; u/l starts for the merge
+__global__ __launch_bounds__(256) void k_gw_marg(GwDev g, double exponent, double* __restrict__ s_out) {
+    const long long r = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (r >= g.N2) return;
+    const int lane = threadIdx.x & 63;
+    const long long h0 = g.hptr[r], h1 = g.hptr[r + 1];
+    double acc = 0.0;
+    const double ar = g.alpha[r];
+    for (long long q0 = h0; q0 < h1; q0 += 64) {
+        const long long q = q0 + lane;
+        double x = q < h1 ? (double)g.V[q] / ar : 0.0;
+        acc += wave_sum(x);
+    }
+    const long long c0 = g.cptr[r], c1 = g.cptr[r + 1];
+    double acc2 = 0.0;
+    for (long long q0 = c0; q0 < c1; q0 += 64) {
+        const long long q = q0 + lane;
+        double x = 0.0;
+        if (q < c1) {
+            const long long k = (long long)(g.keys[q] & g.imask);
+            x = (double)g.V[k] / g.alpha[g.R[k]];
+        }
+        acc2 += wave_sum(x);
+    }
+    if (lane == 0) {
+        const double m = acc + acc2;
+        double sv = pow(m, exponent);
+        if (sv == 0.0) sv = 1.0;
+        s_out[r] = sv;
+        g.ustart[r] = lower_bound_i32(g.C, h0, h1, (int32_t)r);
+        g.lstart[r] = lower_bound_keyrow(g.keys, g.imask, g.R, c0, c1, (int32_t)(r + 1));
+    }
+}
+
+// orphan flags over the column-sorted list: entry (i, r), i > r, whose
+// partner (r, i) is not a cell of H
+__global__ void k_gw_orphans(GwDev g, long long nkeys, long long* __restrict__ flag) {
+    const long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= nkeys) return;
+    const long long k = (long long)(g.keys[q] & g.imask);
+    const long long r = (long long)(g.keys[q] >> g.ib);  // the column
+    const int32_t i = g.R[k];
+    long long f = 0;
+    if (i > r) {
+        const long long h0 = g.ustart[r], h1 = g.hptr[r + 1];
+        const long long p = lower_bound_i32(g.C, h0, h1, i);
+        f = (p < h1 && g.C[p] == i) ? 0 : 1;
+    }
+    flag[q] = f;
+}
+
+__global__ void k_gw_rowlen(GwDev g, const long long* __restrict__ oprefix, long long* __restrict__ len) {
+    const long long r = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= g.N2) return;
+    len[r] = (g.hptr[r + 1] - g.ustart[r]) + (oprefix[g.cptr[r + 1]] - oprefix[g.lstart[r]]);
+}
+
+// upper cells (r, c >= r) of H: Y = S_rc + S_cr (partner found in column r's list)
+__global__ void k_gw_write_upper(GwDev g, const long long* __restrict__ oprefix, const long long* __restrict__ row_off,
+                                 const double* __restrict__ s, int32_t* __restrict__ ob1, int32_t* __restrict__ ob2,
+                                 double* __restrict__ ov) {
+    const long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= g.hptr[g.N2]) return;
+    const int32_t r = g.R[k], c = g.C[k];
+    if (c < r) return;
+    double y = (double)g.V[k] / g.alpha[r];
+    long long before = 0;  // orphans of row r with column < c
+    if (c > r) {
+        const long long l0 = g.lstart[r], l1 = g.cptr[(long long)r + 1];
+        const long long p = lower_bound_keyrow(g.keys, g.imask, g.R, l0, l1, c);
+        if (p < l1) {
+            const long long kk = (long long)(g.keys[p] & g.imask);
+            if (g.R[kk] == c) y += (double)g.V[kk] / g.alpha[c];
+        }
+        before = oprefix[p] - oprefix[l0];
+    }
+    const long long pos = row_off[r] + (k - g.ustart[r]) + before;
+    ob1[pos] = r;
+    ob2[pos] = c;
+    ov[pos] = y / (s[c] * s[r]);  // Correct_VC: x / (s2[None, :] * s1[:, None])
+}
+
+// lower cells (i, r), i > r, without a partner: Y_ri = S_ir alone
+__global__ void k_gw_write_orphans(GwDev g, long long nkeys, const long long* __restrict__ flag,
+                                   const long long* __restrict__ oprefix, const long long* __restrict__ row_off,
+                                   const double* __restrict__ s, int32_t* __restrict__ ob1,
+                                   int32_t* __restrict__ ob2, double* __restrict__ ov) {
+    const long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= nkeys || !flag[q]) return;
+    const long long k = (long long)(g.keys[q] & g.imask);
+    const long long r = (long long)(g.keys[q] >> g.ib);
+    const int32_t i = g.R[k];
+    const long long u0 = g.ustart[r], u1 = g.hptr[r + 1];
+    const long long before = lower_bound_i32(g.C, u0, u1, i) - u0;  // upper cells of row r with col < i
+    const long long pos = row_off[r] + (oprefix[q] - oprefix[g.lstart[r]]) + before;
+    const double y = (double)g.V[k] / g.alpha[i];
+    ob1[pos] = (int32_t)r;
+    ob2[pos] = i;
+    ov[pos] = y / (s[i] * s[r]);
+}
+
+// sum of the full symmetric C from its upper table: per block, fixed order
+__global__ __launch_bounds__(256) void k_gw_csum(const int32_t* __restrict__ b1, const int32_t* __restrict__ b2,
+                                                 const double* __restrict__ v, long long n, long long per,
+                                                 double* __restrict__ part) {
+    __shared__ double sh[16];
+    const long long lo = (long long)blockIdx.x * per, hi = std::min<long long>(n, lo + per);
+    double acc = 0.0;
+    for (long long q = lo + threadIdx.x; q < hi; q += 256) acc += (b1[q] == b2[q] ? 1.0 : 2.0) * v[q];
+    acc = block_sum(acc, sh);
+    if (threadIdx.x == 0) part[blockIdx.x] = acc;
+}
+
+__global__ void k_gw_scale(double* __restrict__ v, long long n, double rf) {
+    const long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q < n) v[q] = rf * v[q];
+}
+
+}  // namespace hh
+
+using namespace hh;
+
+struct hh_gw {
+    int device = 0;
+    int64_t n = 0, N2 = 0, t_nnz = 0, h_nnz = 0, n_keys = 0;
+    DBuf<int32_t> tA, tB, R, C;
+    DBuf<uint32_t> tV, V;
+    DBuf<long long> hptr, cptr;
+    DBuf<unsigned long long> keys;
+    int ib = 1;
+    std::vector<unsigned long long> t_rowsum, t_nnz_row, h_blocksum;
+    unsigned long long h_total = 0;
+    // result (upper-triangle table of Nor)
+    DBuf<int32_t> ob1, ob2;
+    DBuf<double> ov;
+    int64_t out_nnz = -1;
+};
+
+namespace {
+
+const char* kErrWhat[5] = {"bin id out of range", "bin1 > bin2 in the traditional table (not upper triangle)",
+                           "cells not sorted by (row, col)", "duplicate cell", "counts must be non-negative integers < 2^32"};
+
+template <class Id, class Cnt>
+void gw_check(const Id* r, const Id* c, const Cnt* v, int64_t nnz, int64_t nb, int upper, DBuf<int32_t>& R,
+              DBuf<int32_t>& Cc, DBuf<uint32_t>& V, const char* what, hipStream_t s) {
+    R.alloc(std::max<int64_t>(nnz, 1));
+    Cc.alloc(std::max<int64_t>(nnz, 1));
+    V.alloc(std::max<int64_t>(nnz, 1));
+    DBuf<unsigned long long> err(5);
+    HIP_CHECK(hipMemsetAsync(err.p, 0xff, 5 * sizeof(unsigned long long), s));
+    if (nnz > 0)
+        hipLaunchKernelGGL((k_gw_check<Id, Cnt>), dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s, r, c, v,
+                           (long long)nnz, (long long)nb, upper, R.p, Cc.p, V.p, err.p);
+    HIP_CHECK(hipGetLastError());
+    unsigned long long he[5];
+    err.download(he, 5, s);
+    HIP_CHECK(hipStreamSynchronize(s));
+    int code = -1;
+    unsigned long long at = ~0ull;
+    for (int q = 0; q < 5; ++q)
+        if (he[q] < at) { at = he[q]; code = q; }
+    if (code >= 0) HH_THROW(HH_ERR_ARG, std::string(what) + ": " + kErrWhat[code] + " at entry " + std::to_string(at));
+}
+
+template <class Id, class Cnt>
+void gw_create(hh_gw& G, const Id* t1, const Id* t2, const Cnt* tv, int64_t t_nnz, const Id* hr, const Id* hc,
+               const Cnt* hv, int64_t h_nnz, int64_t n, const int64_t* chrom_offsets, int32_t n_chroms,
+               hipStream_t s) {
+    HH_REQUIRE(n > 0 && n_chroms > 0 && chrom_offsets && t_nnz >= 0 && h_nnz >= 0, "bad arguments");
+    HH_REQUIRE(chrom_offsets[0] == 0 && chrom_offsets[n_chroms] == n, "chrom_offsets must span [0, n]");
+    HH_REQUIRE(2 * n < kMaxBins, "too many bins");
+    G.n = n;
+    G.N2 = 2 * n;
+    G.t_nnz = t_nnz;
+    G.h_nnz = h_nnz;
+    std::vector<int32_t> chrom_of(n), block_of(2 * n);
+    for (int c = 0; c < n_chroms; ++c) {
+        HH_REQUIRE(chrom_offsets[c] <= chrom_offsets[c + 1], "chrom_offsets not monotone");
+        for (int64_t b = chrom_offsets[c]; b < chrom_offsets[c + 1]; ++b) {
+            chrom_of[b] = c;
+            block_of[b] = c;                 // M copy of chromosome c
+            block_of[n + b] = n_chroms + c;  // P copy
+        }
+    }
+    gw_check(t1, t2, tv, t_nnz, n, 1, G.tA, G.tB, G.tV, "traditional table", s);
+    gw_check(hr, hc, hv, h_nnz, 2 * n, 0, G.R, G.C, G.V, "haplotype cells", s);
+    DBuf<int32_t> dch = to_device(chrom_of, s), dblk = to_device(block_of, s);
+    DBuf<unsigned long long> trs(n), tnz(n), hbs(2 * n), htot(1);
+    trs.zero(s);
+    tnz.zero(s);
+    hbs.zero(s);
+    htot.zero(s);
+    if (t_nnz > 0)
+        hipLaunchKernelGGL(k_gw_tstats, dim3((unsigned)((t_nnz + 255) / 256)), dim3(256), 0, s, G.tA.p, G.tB.p, G.tV.p,
+                           (long long)t_nnz, dch.p, trs.p, tnz.p);
+    if (h_nnz > 0)
+        hipLaunchKernelGGL(k_gw_hstats, dim3((unsigned)((h_nnz + 255) / 256)), dim3(256), 0, s, G.R.p, G.C.p, G.V.p,
+                           (long long)h_nnz, dblk.p, hbs.p, htot.p);
+    HIP_CHECK(hipGetLastError());
+    G.t_rowsum.resize(n);
+    G.t_nnz_row.resize(n);
+    G.h_blocksum.resize(2 * n);
+    trs.download(G.t_rowsum.data(), n, s);
+    tnz.download(G.t_nnz_row.data(), n, s);
+    hbs.download(G.h_blocksum.data(), 2 * n, s);
+    htot.download(&G.h_total, 1, s);
+    // H row pointers and column lists
+    G.hptr.alloc(2 * n + 1);
+    if (h_nnz > 0)
+        hipLaunchKernelGGL(k_px_rowptr_gw, dim3((unsigned)((h_nnz + 1 + 255) / 256)), dim3(256), 0, s, G.R.p,
+                           (long long)h_nnz, (long long)(2 * n), G.hptr.p);
+    else
+        HIP_CHECK(hipMemsetAsync(G.hptr.p, 0, (2 * n + 1) * sizeof(long long), s));
+    G.ib = 1;
+    while (G.ib < 63 && ((int64_t)1 << G.ib) < std::max<int64_t>(h_nnz, 2)) ++G.ib;
+    int cbits = 1;
+    while (cbits < 40 && ((int64_t)1 << cbits) < 2 * n) ++cbits;
+    HH_REQUIRE(G.ib + cbits <= 64, "haplotype matrix too large for 64-bit column keys");
+    DBuf<unsigned long long> nk(1);
+    nk.zero(s);
+    G.keys.alloc(std::max<int64_t>(h_nnz, 1));
+    if (h_nnz > 0)
+        hipLaunchKernelGGL(k_gw_colkeys, dim3((unsigned)((h_nnz + 255) / 256)), dim3(256), 0, s, G.R.p, G.C.p,
+                           (long long)h_nnz, G.ib, G.keys.p, nk.p);
+    unsigned long long hn = 0;
+    nk.download(&hn, 1, s);
+    HIP_CHECK(hipStreamSynchronize(s));
+    G.n_keys = (int64_t)hn;
+    dev_sort_u64(G.keys, G.n_keys, G.ib + cbits, s);
+    G.cptr.alloc(2 * n + 1);
+    hipLaunchKernelGGL(k_px_keyptr_gw, dim3((unsigned)((hn + 1 + 255) / 256)), dim3(256), 0, s, G.keys.p,
+                       (long long)hn, G.ib, (long long)(2 * n), G.cptr.p);
+    HIP_CHECK(hipGetLastError());
+    HIP_CHECK(hipStreamSynchronize(s));
+}
+
+}  // namespace
+
+extern "C" {
+
+int hh_gw_create(const int64_t* t_bin1, const int64_t* t_bin2, const double* t_count, int64_t t_nnz,
+                 const int64_t* h_row, const int64_t* h_col, const double* h_count, int64_t h_nnz, int64_t n,
+                 const int64_t* chrom_offsets, int32_t n_chroms, void* stream, hh_gw** out) {
+    return guard([&] {
+        HH_REQUIRE(out, "null");
+        HH_REQUIRE((t_nnz == 0 || (t_bin1 && t_bin2 && t_count)) && (h_nnz == 0 || (h_row && h_col && h_count)),
+                   "null arrays");
+        hipStream_t s = as_stream(stream);
+        auto G = std::make_unique<hh_gw>();
+        HIP_CHECK(hipGetDevice(&G->device));
+        DBuf<long long> a(std::max<int64_t>(t_nnz, 1)), b(std::max<int64_t>(t_nnz, 1)), r(std::max<int64_t>(h_nnz, 1)),
+            c(std::max<int64_t>(h_nnz, 1));
+        DBuf<double> tv(std::max<int64_t>(t_nnz, 1)), hv(std::max<int64_t>(h_nnz, 1));
+        a.upload(reinterpret_cast<const long long*>(t_bin1), t_nnz, s);
+        b.upload(reinterpret_cast<const long long*>(t_bin2), t_nnz, s);
+        tv.upload(t_count, t_nnz, s);
+        r.upload(reinterpret_cast<const long long*>(h_row), h_nnz, s);
+        c.upload(reinterpret_cast<const long long*>(h_col), h_nnz, s);
+        hv.upload(h_count, h_nnz, s);
+        gw_create<long long, double>(*G, a.p, b.p, tv.p, t_nnz, r.p, c.p, hv.p, h_nnz, n, chrom_offsets, n_chroms, s);
+        *out = G.release();
+    });
+}
+
+int hh_gw_create_device(const int32_t* t_bin1, const int32_t* t_bin2, const int32_t* t_count, int64_t t_nnz,
+                        const int32_t* h_row, const int32_t* h_col, const int32_t* h_count, int64_t h_nnz, int64_t n,
+                        const int64_t* chrom_offsets, int32_t n_chroms, void* stream, hh_gw** out) {
+    return guard([&] {
+        HH_REQUIRE(out, "null");
+        auto G = std::make_unique<hh_gw>();
+        HIP_CHECK(hipGetDevice(&G->device));
+        gw_create<int32_t, int32_t>(*G, t_bin1, t_bin2, t_count, t_nnz, h_row, h_col, h_count, h_nnz, n,
+                                    chrom_offsets, n_chroms, as_stream(stream));
+        *out = G.release();
+    });
+}
+
+int hh_gw_free(hh_gw* g) {
+    return guard([&] {
+        if (g) device_quiesce(g->device);
+        delete g;
+    });
+}
+
+int hh_gw_stats(const hh_gw* g, int64_t* t_rowsum, int64_t* t_nnz_row, int64_t* h_blocksum, int64_t* h_total) {
+    return guard([&] {
+        HH_REQUIRE(g, "null");
+        if (t_rowsum) for (int64_t i = 0; i < g->n; ++i) t_rowsum[i] = (int64_t)g->t_rowsum[i];
+        if (t_nnz_row) for (int64_t i = 0; i < g->n; ++i) t_nnz_row[i] = (int64_t)g->t_nnz_row[i];
+        if (h_blocksum) for (int64_t i = 0; i < g->N2; ++i) h_blocksum[i] = (int64_t)g->h_blocksum[i];
+        if (h_total) *h_total = (int64_t)g->h_total;
+    });
+}
+
+int hh_gw_correct(hh_gw* g, const double* alpha, double exponent, int64_t* out_nnz, void* stream) {
+    return guard([&] {
+        HH_REQUIRE(g && alpha && out_nnz, "null");
+        hipStream_t s = as_stream(stream);
+        const int64_t N2 = g->N2, nk = g->n_keys;
+        DBuf<double> dal(N2), sv(N2);
+        dal.upload(alpha, N2, s);
+        DBuf<long long> ustart(N2), lstart(N2);
+        GwDev d{g->R.p, g->C.p, g->V.p, g->hptr.p, g->keys.p, g->cptr.p,
+                g->ib >= 64 ? ~0ull : ((1ull << g->ib) - 1ull), g->ib, (long long)N2, dal.p, ustart.p, lstart.p};
+        hipLaunchKernelGGL(k_gw_marg, dim3((unsigned)((N2 * 64 + 255) / 256)), dim3(256), 0, s, d, exponent, sv.p);
+        DBuf<long long> flag(nk + 1), opre(nk + 1);
+        if (nk > 0)
+            hipLaunchKernelGGL(k_gw_orphans, dim3((unsigned)((nk + 255) / 256)), dim3(256), 0, s, d, (long long)nk,
+                               flag.p);
+        HIP_CHECK(hipMemsetAsync(flag.p + nk, 0, sizeof(long long), s));
+        dev_excl_scan_i64(flag.p, opre.p, nk + 1, nullptr, s);
+        DBuf<long long> len(N2 + 1), roff(N2 + 1);
+        hipLaunchKernelGGL(k_gw_rowlen, dim3((unsigned)((N2 + 255) / 256)), dim3(256), 0, s, d, opre.p, len.p);
+        HIP_CHECK(hipMemsetAsync(len.p + N2, 0, sizeof(long long), s));
+        dev_excl_scan_i64(len.p, roff.p, N2 + 1, nullptr, s);
+        long long total = 0;
+        HIP_CHECK(hipMemcpyAsync(&total, roff.p + N2, sizeof(long long), hipMemcpyDeviceToHost, s));
+        HIP_CHECK(hipStreamSynchronize(s));
+        g->ob1.alloc(std::max<long long>(total, 1));
+        g->ob2.alloc(std::max<long long>(total, 1));
+        g->ov.alloc(std::max<long long>(total, 1));
+        if (g->h_nnz > 0)
+            hipLaunchKernelGGL(k_gw_write_upper, dim3((unsigned)((g->h_nnz + 255) / 256)), dim3(256), 0, s, d, opre.p,
+                               roff.p, sv.p, g->ob1.p, g->ob2.p, g->ov.p);
+        if (nk > 0)
+            hipLaunchKernelGGL(k_gw_write_orphans, dim3((unsigned)((nk + 255) / 256)), dim3(256), 0, s, d,
+                               (long long)nk, flag.p, opre.p, roff.p, sv.p, g->ob1.p, g->ob2.p, g->ov.p);
+        HIP_CHECK(hipGetLastError());
+        // R_F = H.mean() / C.mean() over the full 2n x 2n matrices (:897-899)
+        const long long per = 1 << 16;
+        const long long nbk = std::max<long long>(1, (total + per - 1) / per);
+        DBuf<double> part(nbk);
+        part.zero(s);
+        if (total > 0)
+            hipLaunchKernelGGL(k_gw_csum, dim3((unsigned)nbk), dim3(256), 0, s, g->ob1.p, g->ob2.p, g->ov.p,
+                               (long long)total, per, part.p);
+        std::vector<double> hp(nbk);
+        part.download(hp.data(), nbk, s);
+        HIP_CHECK(hipStreamSynchronize(s));
+        double csum = 0.0;
+        for (double x : hp) csum += x;
+        const double NN = (double)N2 * (double)N2;
+        const double rf = ((double)g->h_total / NN) / (csum / NN);
+        if (total > 0)
+            hipLaunchKernelGGL(k_gw_scale, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, g->ov.p,
+                               (long long)total, rf);
+        HIP_CHECK(hipGetLastError());
+        HIP_CHECK(hipStreamSynchronize(s));
+        g->out_nnz = total;
+        *out_nnz = total;
+    });
+}
+
+int hh_gw_result(const hh_gw* g, int64_t* bin1, int64_t* bin2, double* value, void* stream) {
+    return guard([&] {
+        HH_REQUIRE(g && g->out_nnz >= 0, "call hh_gw_correct first");
+        hipStream_t s = as_stream(stream);
+        const int64_t m = g->out_nnz;
+        std::vector<int32_t> a(m), b(m);
+        g->ob1.download(a.data(), m, s);
+        g->ob2.download(b.data(), m, s);
+        if (value) g->ov.download(value, m, s);
+        HIP_CHECK(hipStreamSynchronize(s));
+        if (bin1) for (int64_t i = 0; i < m; ++i) bin1[i] = a[i];
+        if (bin2) for (int64_t i = 0; i < m; ++i) bin2[i] = b[i];
+    });
+}
+
+int hh_gw_result_device(const hh_gw* g, const int32_t** bin1, const int32_t** bin2, const double** value) {
+    return guard([&] {
+        HH_REQUIRE(g && g->out_nnz >= 0, "call hh_gw_correct first");
+        if (bin1) *bin1 = g->ob1.p;
+        if (bin2) *bin2 = g->ob2.p;
+        if (value) *value = g->ov.p;
+    });
+}
+
+}  // extern "C"

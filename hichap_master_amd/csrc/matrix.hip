@@ -340,6 +340,13 @@ int hh_synchronize(void* stream) {
     return guard([&] { HIP_CHECK(hipStreamSynchronize(as_stream(stream))); });
 }
 
+int hh_device_copy(void* dst, const void* src, int64_t bytes, void* stream) {
+    return guard([&] {
+        HH_REQUIRE(bytes >= 0 && (bytes == 0 || (dst && src)), "bad arguments");
+        if (bytes) HIP_CHECK(hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyDeviceToDevice, as_stream(stream)));
+    });
+}
+
 int hh_matrix_from_pixels(const int64_t* bin1, const int64_t* bin2, const double* count, int64_t nnz,
                           int64_t n_bins, const int64_t* chrom_offsets, int32_t n_chroms,
                           int32_t ignore_diags, int32_t cis_only, int64_t row_lo, int64_t row_hi,

@@ -177,6 +177,91 @@ def GenomeWideMatrixCorrection(Bins_Pos, Hap_Bins_Pos, T_M, H_M):
     return sym_vc_rescale(H_M, np.array(Alpha), None, h_full.sum())
 
 
+def _gw_layout(Bins_Pos, Hap_Bins_Pos):
+    """chrom_offsets of T's layout (chromosomes in bin order) and a check that
+    H is the M copies then the P copies of the same layout (:429-454)."""
+    items = sorted(Bins_Pos.items(), key=lambda kv: kv[1][0])
+    off = [0]
+    for c, (s, e) in items:
+        if s != off[-1]:
+            raise ValueError("Bins_Pos must tile [0, n) contiguously")
+        off.append(e + 1)
+    n = off[-1]
+    for c, (s, e) in items:
+        if tuple(Hap_Bins_Pos["M" + c]) != (s, e) or tuple(Hap_Bins_Pos["P" + c]) != (n + s, n + e):
+            raise ValueError("Hap_Bins_Pos must be the M copies then the P copies of Bins_Pos' layout")
+    return np.asarray(off, dtype=np.int64), [c for c, _ in items]
+
+
+def GenomeWideMatrixCorrectionSparse(Bins_Pos, Hap_Bins_Pos, T_pixels, H_cells, exponent=VC_EXPONENT,
+                                     stream=None, device_result=False):
+    """GenomeWideMatrixCorrection (matrixBuilding.py:857-901) on pixel tables:
+    the whole-genome diploid matrices at 10 kb are 607 282 x 607 282, which the
+    reference's dense form cannot hold.
+
+    ``T_pixels`` = (bin1, bin2, count): cooler's upper-triangle table of T_M
+    (sorted by (bin1, bin2)); ``H_cells`` = (row, col, count): every nonzero
+    cell of the asymmetric imputed H_M (sorted by (row, col)).  Either may be
+    host arrays or int32 device tensors (then both must be).  Returns the
+    upper triangle of the corrected matrix as (bin1, bin2, value), cooler
+    order — the table NPZ2Cooler writes for it (:1613, :1628-1633).  The alpha
+    step runs here with the reference's NumPy expressions on exact integer row
+    sums computed on the GPU (hh_gw_stats)."""
+    _lib.require_gpu()
+    off, order = _gw_layout(Bins_Pos, Hap_Bins_Pos)
+    n = int(off[-1])
+    h = C.c_void_p()
+    on_dev = hasattr(H_cells[0], "data_ptr")
+    if on_dev:
+        def dp(x):
+            return C.c_void_p(x.data_ptr())
+        call("hh_gw_create_device", dp(T_pixels[0]), dp(T_pixels[1]), dp(T_pixels[2]), int(T_pixels[0].numel()),
+             dp(H_cells[0]), dp(H_cells[1]), dp(H_cells[2]), int(H_cells[0].numel()), n, ptr(off), len(order),
+             stream, C.byref(h))
+    else:
+        t = [np.ascontiguousarray(x, dtype=dt) for x, dt in zip(T_pixels, (np.int64, np.int64, np.float64))]
+        hc = [np.ascontiguousarray(x, dtype=dt) for x, dt in zip(H_cells, (np.int64, np.int64, np.float64))]
+        call("hh_gw_create", ptr(t[0]), ptr(t[1]), ptr(t[2]), t[0].size, ptr(hc[0]), ptr(hc[1]), ptr(hc[2]),
+             hc[0].size, n, ptr(off), len(order), stream, C.byref(h))
+    try:
+        t_sum = np.empty(n, np.int64)
+        t_nz = np.empty(n, np.int64)
+        h_bs = np.empty(2 * n, np.int64)
+        h_tot = C.c_int64(0)
+        call("hh_gw_stats", h, ptr(t_sum), ptr(t_nz), ptr(h_bs), C.byref(h_tot))
+        Beta = {}
+        for c, (s, e) in Bins_Pos.items():
+            L = e - s + 1
+            cov = _coverage(L - t_nz[s:e + 1], L)
+            gap = np.nonzero(cov < 0.1)[0]              # Gap_definedLowRes (:742-753)
+            Beta[c] = _snp_alpha(h_bs[s:e + 1], h_bs[n + s:n + e + 1], t_sum[s:e + 1], _non_gap(L, gap))
+        Alpha = []
+        for i in Sort_Chromosomes(list(Beta.keys())):
+            Alpha.extend(Beta[i])
+        Alpha += Alpha
+        Alpha = np.ascontiguousarray(Alpha, dtype=np.float64)
+        m = C.c_int64(0)
+        call("hh_gw_correct", h, ptr(Alpha), float(exponent), C.byref(m), stream)
+        m = int(m.value)
+        if device_result:  # int32 / int32 / float64 device tensors (e.g. for ice / cooler writing on GPU)
+            import torch
+            p1, p2, pv = C.c_void_p(), C.c_void_p(), C.c_void_p()
+            call("hh_gw_result_device", h, C.byref(p1), C.byref(p2), C.byref(pv))
+            out = [torch.empty(m, dtype=dt, device="cuda") for dt in (torch.int32, torch.int32, torch.float64)]
+            for t, p in zip(out, (p1, p2, pv)):
+                if m:
+                    call("hh_device_copy", C.c_void_p(t.data_ptr()), p, t.element_size() * m, stream)
+            call("hh_synchronize", stream)
+            return tuple(out)
+        b1 = np.empty(m, np.int64)
+        b2 = np.empty(m, np.int64)
+        v = np.empty(m, np.float64)
+        call("hh_gw_result", h, ptr(b1), ptr(b2), ptr(v), stream)
+        return b1, b2, v
+    finally:
+        call("hh_gw_free", h)
+
+
 # ---------------------------------------------------------- pair binning
 # Same entry points as the reference's matrix construction; the per-line
 # loops run on the GPU (hichap_master_amd.pairs, csrc/pairs.hip).

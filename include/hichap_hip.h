@@ -48,6 +48,8 @@ int hh_version(void);                 /* (major<<16)|(minor<<8)|patch */
 int hh_device_count(int32_t* n);
 int hh_set_device(int32_t device);
 int hh_synchronize(void* stream);
+/* device-to-device copy of `bytes` on `stream` (asynchronous) */
+int hh_device_copy(void* dst, const void* src, int64_t bytes, void* stream);
 /* Performance knobs: "band_w" (-1 auto, 0 no dense band, > 0 forced
  * multiple of 16; for matrices built afterwards), "band4" 0/1 (the 4-bit
  * band; later builds), "band4_density_pct" / "band8_big_pct" (its width
@@ -250,6 +252,41 @@ int hh_dense_symvc(const void* X, int32_t dtype, int64_t N, const double* alpha,
  * np.percentile ('linear') semantics; each matrix crosses PCIe once. */
 int hh_twostep(const int64_t* TM, const int64_t* MM, const int64_t* PM, int64_t N, double* nor_mm, double* nor_pm,
                uint8_t* gap_m, uint8_t* gap_p, int32_t on_device, void* stream);
+
+/* ------------------------------------ sparse genome-wide correction
+ * GenomeWideMatrixCorrection (matrixBuilding.py:857-901) on pixel tables
+ * instead of dense 2n x 2n matrices.  T: the traditional whole-genome table
+ * (cooler order: bin1 <= bin2, sorted, unique) on n bins, chrom_offsets[n_chroms
+ * + 1] its chromosome layout; H: every nonzero cell (row, col, count) of the
+ * imputed haplotype matrix, sorted by (row, col), unique, on 2n bins laid out
+ * as the M copies of the chromosomes then the P copies (Get_Chro_Bins_Haplotypes
+ * :429-454).  hh_gw_create validates both and computes the alpha step's exact
+ * integer statistics; the caller computes alpha (NumPy percentile semantics,
+ * :878-893) and hh_gw_correct does S = H / Alpha[:, None], the sum
+ * symmetrisation (:770-777), Correct_VC(., exponent) and the mean rescale
+ * (:894-899), leaving the upper triangle of the result (cooler order, what
+ * NPZ2Cooler stores) on the device.  Counts are integers < 2^32. */
+typedef struct hh_gw hh_gw;
+int hh_gw_create(const int64_t* t_bin1, const int64_t* t_bin2, const double* t_count, int64_t t_nnz,
+                 const int64_t* h_row, const int64_t* h_col, const double* h_count, int64_t h_nnz, int64_t n,
+                 const int64_t* chrom_offsets, int32_t n_chroms, void* stream, hh_gw** out);
+/* the same from device int32 tables (the binner's outputs) */
+int hh_gw_create_device(const int32_t* t_bin1, const int32_t* t_bin2, const int32_t* t_count, int64_t t_nnz,
+                        const int32_t* h_row, const int32_t* h_col, const int32_t* h_count, int64_t h_nnz, int64_t n,
+                        const int64_t* chrom_offsets, int32_t n_chroms, void* stream, hh_gw** out);
+int hh_gw_free(hh_gw* g);
+/* host arrays: t_rowsum[n], t_nnz_row[n] = sum / nonzero count of T's row
+ * within its chromosome block (the diagonal once); h_blocksum[2n] = sum of H's
+ * row within its same-chromosome same-haplotype block (M_M / P_P); *h_total =
+ * sum(H).  Any pointer may be NULL. */
+int hh_gw_stats(const hh_gw* g, int64_t* t_rowsum, int64_t* t_nnz_row, int64_t* h_blocksum, int64_t* h_total);
+/* alpha[2n] (host): the concatenated, duplicated SNP-density factors;
+ * exponent: 2/3.  *out_nnz = upper-triangle pixels of the result. */
+int hh_gw_correct(hh_gw* g, const double* alpha, double exponent, int64_t* out_nnz, void* stream);
+/* the result to host arrays of out_nnz (any may be NULL), or its device
+ * pointers (valid until hh_gw_free or the next hh_gw_correct) */
+int hh_gw_result(const hh_gw* g, int64_t* bin1, int64_t* bin2, double* value, void* stream);
+int hh_gw_result_device(const hh_gw* g, const int32_t** bin1, const int32_t** bin2, const double** value);
 
 /* ---------------------------------------------------- compartment (one chrom)
  * StructureFind.Distance_Decay / Get_PCA / Select_PC_new, StructureFind.py:201-423.

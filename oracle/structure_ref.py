@@ -188,3 +188,69 @@ def get_di(M, gap, w, test_type="ttest"):
                 val = float(ds - us) / abs(ds - us) * ((us - e) ** 2 / e + (ds - e) ** 2 / e)
         DI[j] = val
     return DI
+
+
+# ----------------------------------------------- banded restatement (large N)
+def band_from_pixels(bin1, bin2, count, weight, lo, N, B):
+    """Diagonal-major band of one chromosome's balanced matrix from cooler's
+    pixel table: band[B + k, j] = M[j + k, j] for |k| <= B, M = count * w[bin1]
+    * w[bin2] with NaN -> 0 (Data_preprocess :853-854; weight None = raw)."""
+    b1 = np.asarray(bin1, dtype=np.int64) - lo
+    b2 = np.asarray(bin2, dtype=np.int64) - lo
+    v = np.asarray(count, dtype=np.float64)
+    sel = (b1 >= 0) & (b2 < N) & (np.abs(b2 - b1) <= B)
+    i, j, v = b1[sel], b2[sel], v[sel]
+    if weight is not None:
+        w = np.asarray(weight, dtype=np.float64)
+        v = v * w[i + lo] * w[j + lo]
+        v[np.isnan(v)] = 0.0
+    band = np.zeros((2 * B + 1, N))
+    d = j - i
+    band[B - d, j] = v      # M[i][j] = M[j - d][j]
+    band[B + d, i] = v      # M[j][i] = M[i + d][i]
+    return band
+
+
+def get_gap_band(band, B, lb):
+    """Get_Gap (StructureFind.py:721-751) on the band, plus the first / last
+    bin (Data_preprocess :875-883): column i is a gap when fewer than
+    2 lb 0.8 of M[i - lb : i + lb, i] are nonzero, or within lb of an edge."""
+    N = band.shape[1]
+    nz = np.zeros(N, dtype=np.int64)
+    for k in range(-lb, lb):
+        nz += band[B + k] != 0
+    gap = np.ones(N, dtype=bool)
+    inner = np.arange(lb, N - lb)
+    gap[inner] = nz[inner] < 2 * lb * 0.8
+    gap[0] = gap[N - 1] = True
+    return np.nonzero(gap)[0].astype(np.int64)
+
+
+def get_di_band(band, B, gap, w, test_type="ttest"):
+    """Get_DI (StructureFind.py:804-839) on the band: up = M[j-w:j, j] reversed
+    (band rows B-1 .. B-w), down = M[j+1:j+w+1, j] (rows B+1 .. B+w); the same
+    per-column arithmetic as get_di."""
+    N = band.shape[1]
+    g = np.zeros(N, dtype=bool)
+    g[np.asarray(gap, dtype=np.int64)] = True
+    DI = np.zeros(N)
+    for j in range(N):
+        if g[j] or j < w or j > N - w - 1:
+            continue
+        up = band[B - 1:B - w - 1:-1, j] if B - w - 1 >= 0 else band[B - 1::-1, j][:w]
+        down = band[B + 1:B + w + 1, j]
+        val = 0.0
+        if test_type == "ttest":
+            um, dm = up.mean(), down.mean()
+            ud = np.sum((up - um) ** 2 / (up.size * (up.size - 1)))
+            dd = np.sum((down - dm) ** 2 / (down.size * (down.size - 1)))
+            den = np.sqrt(ud + dd)
+            if den != 0:
+                val = (dm - um) / den
+        else:
+            us, ds = up.sum(), down.sum()
+            e = float(us + ds) / 2.0
+            if us != ds and e != 0:
+                val = float(ds - us) / abs(ds - us) * ((us - e) ** 2 / e + (ds - e) ** 2 / e)
+        DI[j] = val
+    return DI

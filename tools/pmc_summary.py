@@ -19,18 +19,23 @@ def load(path, counter):
     return {k: sum(v) / len(v) for k, v in acc.items()}, {k: len(v) for k, v in acc.items()}
 
 
-def main(fetch_csv, write_csv, out):
+def main(fetch_csv, write_csv, out, commit=None, real_bytes_per_sweep=None):
+    """Optional metadata: the commit the profiled build came from and the
+    layout's payload bytes per sweep (bench.py scales traffic to shards by it)."""
     (f, nf), (w, _) = load(fetch_csv, "FETCH_SIZE"), load(write_csv, "WRITE_SIZE")
     res = {}
+    if commit or real_bytes_per_sweep:
+        res["_meta"] = {"commit": commit,
+                        "real_bytes_per_sweep": float(real_bytes_per_sweep) if real_bytes_per_sweep else None}
     for k in sorted(set(f) | set(w)):
         fb, wb = f.get(k, 0.0) * 1024.0, w.get(k, 0.0) * 1024.0
         res[k] = {"fetch_size_bytes": fb, "write_size_bytes": wb, "traffic_bytes": 2.0 * fb + wb,
                   "dispatches": nf.get(k, 0)}
     json.dump(res, open(out, "w"), indent=1)
     for k, v in res.items():
-        if "sweep" in k:
+        if "sweep" in k and k != "_meta":
             print(k[:60], v)
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:4])
+    main(*sys.argv[1:6])
