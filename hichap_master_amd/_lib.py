@@ -73,6 +73,9 @@ SIGNATURES = {
     "hh_synth_count": (C.c_int, [C.POINTER(SynthParams), P, P, P]),
     "hh_synth_build": (C.c_int, [C.POINTER(SynthParams), I64, I64, P, C.POINTER(P)]),
     "hh_synth_dense": (C.c_int, [P, I32, P, P]),
+    "hh_synth_pixels": (C.c_int, [C.POINTER(SynthParams), I32, P, C.POINTER(P)]),
+    "hh_pixels_get": (C.c_int, [P, P, P, P, PI64]),
+    "hh_pixels_free": (C.c_int, [P]),
     "hh_ice_balance": (C.c_int, [P, C.POINTER(IceOpts), P, P, P, P, P, PF64, P]),
     "hh_ice_create": (C.c_int, [P, C.POINTER(IceOpts), C.POINTER(P)]),
     "hh_ice_free": (C.c_int, [P]),

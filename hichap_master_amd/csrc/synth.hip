@@ -35,6 +35,7 @@ struct SynthDev {
     unsigned long long seed;
     int band_w;            // uint8 band half-width W8 (0 = none)
     int band_w4;           // nibble band outer width W4 (== band_w: none)
+    int ordered;           // 1: independent draws for (i, j) and (j, i) (asymmetric cells)
 };
 
 __global__ void k_synth_bins(SynthDev p, float vis_sigma, float gap_frac, int comp_block,
@@ -77,7 +78,8 @@ __device__ __forceinline__ uint32_t synth_count(const SynthDev& p, long long i, 
     const long long lo = i < j ? i : j, hi = i < j ? j : i;
     const long long d = hi - lo;
     if (d < p.ignore_diags) return 0u;
-    const uint64_t h = mix64(p.seed ^ mix64((uint64_t)lo * 0x100000001B3ull + (uint64_t)hi));
+    const uint64_t h = p.ordered ? mix64(p.seed ^ mix64((uint64_t)i * 0x100000001B3ull + (uint64_t)j + 0x0DDull))
+                                 : mix64(p.seed ^ mix64((uint64_t)lo * 0x100000001B3ull + (uint64_t)hi));
     if (p.chrom[i] == p.chrom[j]) {
         const float lam = p.A * exp2f(-p.decay * __log2f((float)d + 1.f)) *
                           (1.f + p.comp * (float)(p.sgn[i] * p.sgn[j])) * vi * vj;
@@ -216,6 +218,12 @@ __global__ __launch_bounds__(256) void k_synth_rows(SynthDev p, long long row_lo
 
 using namespace hh;
 
+struct hh_pixels {
+    int device = 0;
+    int64_t nnz = 0;
+    DBuf<int32_t> b1, b2, cnt;
+};
+
 namespace {
 struct SynthHost {
     DBuf<int> chrom_lo;
@@ -333,6 +341,40 @@ __global__ __launch_bounds__(256) void k_synth_dense(SynthDev p, long long lo, l
         if (i < nc) out[i * nc + j] = (double)synth_count(p, lo + i, lo + j);
     }
 }
+// Pixel table of the same model, one wave per row: PASS 0 counts the row's
+// cells (upper triangle j >= i, or every j when p.ordered), PASS 1 writes
+// them at the row's offset in (row, col) order.
+template <int PASS>
+__global__ __launch_bounds__(256) void k_synth_cells(SynthDev p, long long* __restrict__ row_cnt,
+                                                     const long long* __restrict__ row_off,
+                                                     int32_t* __restrict__ b1, int32_t* __restrict__ b2,
+                                                     int32_t* __restrict__ cnt) {
+    const long long r = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (r >= p.n) return;
+    const int lane = threadIdx.x & 63;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    const int c = p.chrom[r];
+    const long long jlo0 = p.cis_only ? p.chrom_lo[c] : 0, jhi = p.cis_only ? p.chrom_lo[c + 1] : p.n;
+    const long long jlo = p.ordered ? jlo0 : (r > jlo0 ? r : jlo0);
+    long long pos = PASS == 1 ? row_off[r] : 0, tot = 0;
+    for (long long j0 = jlo & ~63LL; j0 < jhi; j0 += 64) {
+        const long long j = j0 + lane;
+        uint32_t kc = 0;
+        if (j >= jlo && j < jhi) kc = (j == r) ? (p.ignore_diags == 0 ? synth_count(p, r, j) : 0u) : synth_count(p, r, j);
+        const unsigned long long m = __ballot(kc > 0);
+        if (!m) continue;
+        if (PASS == 1 && kc) {
+            const long long q = pos + __popcll(m & lt);
+            b1[q] = (int32_t)r;
+            b2[q] = (int32_t)j;
+            cnt[q] = (int32_t)kc;
+        }
+        pos += __popcll(m);
+        tot += __popcll(m);
+    }
+    if (PASS == 0 && lane == 0) row_cnt[r] = tot;
+}
+
 }  // namespace hh
 
 extern "C" {
@@ -450,6 +492,53 @@ int hh_synth_build(const hh_synth_params* p, int64_t row_lo, int64_t row_hi, voi
         m->n_band = nb;
         m->n_entries = ent + nb;
         *out = m.release();
+    });
+}
+
+int hh_synth_pixels(const hh_synth_params* p, int32_t ordered, void* stream, hh_pixels** out) {
+    return guard([&] {
+        HH_REQUIRE(out, "null");
+        hipStream_t s = as_stream(stream);
+        SynthHost h;
+        synth_setup(p, h, s);
+        h.dev.ordered = ordered ? 1 : 0;
+        const int64_t n = h.dev.n;
+        auto P = std::make_unique<hh_pixels>();
+        HIP_CHECK(hipGetDevice(&P->device));
+        DBuf<long long> rc(n + 1), off(n + 1);
+        hipLaunchKernelGGL((k_synth_cells<0>), row_grid(n), dim3(256), 0, s, h.dev, rc.p, (const long long*)nullptr,
+                           (int32_t*)nullptr, (int32_t*)nullptr, (int32_t*)nullptr);
+        HIP_CHECK(hipMemsetAsync(rc.p + n, 0, sizeof(long long), s));
+        dev_excl_scan_i64(rc.p, off.p, n + 1, nullptr, s);
+        long long tot = 0;
+        HIP_CHECK(hipMemcpyAsync(&tot, off.p + n, sizeof(long long), hipMemcpyDeviceToHost, s));
+        HIP_CHECK(hipStreamSynchronize(s));
+        P->nnz = tot;
+        P->b1.alloc(std::max<long long>(tot, 1));
+        P->b2.alloc(std::max<long long>(tot, 1));
+        P->cnt.alloc(std::max<long long>(tot, 1));
+        hipLaunchKernelGGL((k_synth_cells<1>), row_grid(n), dim3(256), 0, s, h.dev, (long long*)nullptr, off.p,
+                           P->b1.p, P->b2.p, P->cnt.p);
+        HIP_CHECK(hipGetLastError());
+        HIP_CHECK(hipStreamSynchronize(s));
+        *out = P.release();
+    });
+}
+
+int hh_pixels_get(const hh_pixels* P, const int32_t** bin1, const int32_t** bin2, const int32_t** count, int64_t* nnz) {
+    return guard([&] {
+        HH_REQUIRE(P, "null");
+        if (bin1) *bin1 = P->b1.p;
+        if (bin2) *bin2 = P->b2.p;
+        if (count) *count = P->cnt.p;
+        if (nnz) *nnz = P->nnz;
+    });
+}
+
+int hh_pixels_free(hh_pixels* P) {
+    return guard([&] {
+        if (P) device_quiesce(P->device);
+        delete P;
     });
 }
 

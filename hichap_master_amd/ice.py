@@ -149,6 +149,47 @@ def synth_params(chrom_nbins, A=30.0, decay=1.08, comp_strength=0.3, vis_sigma=0
     return p, arr  # keep `arr` alive while p is used
 
 
+class DevArray:
+    """A device buffer view (pointer, length, dtype) with the torch-like
+    ``data_ptr()`` / ``numel()`` the table-driven entry points accept."""
+
+    def __init__(self, p, n, owner=None):
+        self._p, self._n, self._owner = int(p or 0), int(n), owner
+
+    def data_ptr(self):
+        return self._p
+
+    def numel(self):
+        return self._n
+
+
+class SynthPixels:
+    """Synthetic pixel table in HBM (hh_synth_pixels): cooler's upper-triangle
+    table, or with ``ordered`` every cell of an asymmetric matrix."""
+
+    def __init__(self, chrom_nbins, ordered=False, stream=None, **kw):
+        _lib.require_gpu()
+        p, keep = synth_params(chrom_nbins, **kw)
+        h = C.c_void_p()
+        call("hh_synth_pixels", C.byref(p), int(bool(ordered)), stream, C.byref(h))
+        self._h = h
+        p1, p2, pc, n = C.c_void_p(), C.c_void_p(), C.c_void_p(), C.c_int64(0)
+        call("hh_pixels_get", h, C.byref(p1), C.byref(p2), C.byref(pc), C.byref(n))
+        self.nnz = int(n.value)
+        self.bin1, self.bin2, self.count = (DevArray(x.value, self.nnz, self) for x in (p1, p2, pc))
+
+    def close(self):
+        if self._h:
+            call("hh_pixels_free", self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def synth_dense(chrom_nbins, chrom, out_ptr, stream=None, **kw):
     """Dense float64 cis block of chromosome ``chrom`` of the synthetic genome
     written to device memory at ``out_ptr`` (N_c x N_c, row-major)."""
@@ -291,5 +332,5 @@ class IceState:
             pass
 
 
-__all__ = ["IceOptions", "ContactMatrix", "IceState", "balance", "balance_matrix",
+__all__ = ["IceOptions", "ContactMatrix", "IceState", "SynthPixels", "DevArray", "balance", "balance_matrix",
            "cooler_balance_cmd", "synth_row_counts", "synth_params", "asdict"]

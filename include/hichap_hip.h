@@ -169,6 +169,15 @@ int hh_synth_count(const hh_synth_params* p, int32_t* row_work, int64_t* row_nnz
  * float64 counts into device memory out[N_c * N_c] (bench inputs for the
  * per-chromosome compartment config C5; ignore_diags applies). */
 int hh_synth_dense(const hh_synth_params* p, int32_t chrom, double* out, void* stream);
+/* The model's pixel table in HBM (bench inputs of the table-driven paths):
+ * cooler's upper-triangle table sorted by (bin1, bin2), or with ordered = 1
+ * every nonzero cell (i, j) sorted by (i, j) with independent draws for (i, j)
+ * and (j, i) (an asymmetric matrix like HiCHap's imputed haplotype matrices).
+ * int32 ids and counts, owned by the hh_pixels handle. */
+typedef struct hh_pixels hh_pixels;
+int hh_synth_pixels(const hh_synth_params* p, int32_t ordered, void* stream, hh_pixels** out);
+int hh_pixels_get(const hh_pixels* P, const int32_t** bin1, const int32_t** bin2, const int32_t** count, int64_t* nnz);
+int hh_pixels_free(hh_pixels* P);
 /* Build rows [row_lo, row_hi) (row_lo % 512 == 0). */
 int hh_synth_build(const hh_synth_params* p, int64_t row_lo, int64_t row_hi, void* stream,
                    hh_matrix** out);
