@@ -883,6 +883,7 @@ def main():
             torch.distributed.barrier()
         torch.cuda.synchronize()
 
+    dist_impl = "single"
     if world == 1 and not args.sharded:
         # filters (untimed), then warmup + timed iterations in one C++ loop each
         st.marg_local(0, None, stream); st.filter_nnz(stream)
@@ -895,12 +896,28 @@ def main():
         elapsed = time.perf_counter() - t_start
         sweep_ms, launches, iter_ms = st.last_timing()
     else:
-        ex = dist.Exchange(rank_rows, torch.device("cuda", local))
-        dist.run_filters(st, ex)
-        dist.iterate(st, ex, args.warmup)
+        # the iteration loop in C++ (hh_ice_run_sharded) with the library's
+        # own RCCL communicator; HH_DIST_IMPL=torch keeps the Python loop with
+        # torch.distributed's all-gather (also the fallback if RCCL init fails)
+        impl = os.environ.get("HH_DIST_IMPL", "capi")
+        cx = None
+        if impl == "capi":
+            try:
+                cx = dist.CapiExchange(rank_rows, world, rank, backend=backend)
+            except Exception as e:  # noqa: BLE001
+                print(f"[bench] C-ABI exchange unavailable ({e}); using torch.distributed", file=sys.stderr)
+                impl = "torch"
+        if impl == "capi":
+            run = lambda k: dist.iterate_capi(st, cx, k, stream)
+            dist.filters_capi(st, cx, stream)
+        else:
+            ex = dist.Exchange(rank_rows, torch.device("cuda", local))
+            run = lambda k: dist.iterate(st, ex, k)
+            dist.run_filters(st, ex)
+        run(args.warmup)
         barrier()
         t_start = time.perf_counter()
-        dist.iterate(st, ex, args.steps)
+        run(args.steps)
         barrier()
         elapsed = time.perf_counter() - t_start
         # sweep-kernel timing: a few more iterations with the HIP-event
@@ -909,12 +926,15 @@ def main():
         _lib.call("hh_ktime_reset")
         _lib.call("hh_ktime_enable", 1)
         t_it = time.perf_counter()
-        dist.iterate(st, ex, n_prof)
+        run(n_prof)
         torch.cuda.synchronize()
         iter_ms = 1000.0 * (time.perf_counter() - t_it)
         _lib.call("hh_ktime_enable", 0)
         sweep_ms, launches = _lib.ktime("ice_sweep")
         _lib.call("hh_ktime_reset")
+        dist_impl = impl
+        if cx is not None:
+            cx.close()
     tad = tad_scan_bench(m, st, stream) if args.config == "c2" and world == 1 and not args.sharded else None
     tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
     if torch.distributed.is_initialized():
@@ -945,7 +965,7 @@ def main():
             "nnz_iters_per_s": nnz_total * its,
             "config": {"workload": label, "n_bins": n, "nnz_upper": nnz_total,
                        "trans_fraction_target": tf, "resolution_bp": 40000 if args.config in ("c1", "c3") else 10000,
-                       "parallelism": f"rows sharded x{world} (measured-cost partition), {'RCCL' if backend == 'nccl' else backend} all-gather of marginals" if world > 1
+                       "parallelism": f"rows sharded x{world} (measured-cost partition), {'RCCL' if backend == 'nccl' else backend} all-gather of marginals, loop in {'C++ (hh_ice_run_sharded)' if dist_impl == 'capi' else 'Python'}" if world > 1
                        else "single GPU", "generate_s": round(gen_s, 2),
                        "entries_stored": inf["n_entries"], "slots_u32": inf["n_slots"],
                        "slots_u16": inf["n_slots_narrow"], "payload_bytes": inf["payload_bytes"],

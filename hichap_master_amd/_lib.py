@@ -90,6 +90,13 @@ SIGNATURES = {
     "hh_ice_run": (C.c_int, [P, I32, P]),
     "hh_ice_finalize": (C.c_int, [P, P, P, P, P, P, P]),
     "hh_ice_last_sweep_timing": (C.c_int, [P, PF64, PI32, PF64]),
+    "hh_comm_unique_id": (C.c_int, [P]),
+    "hh_comm_init": (C.c_int, [P, I32, I32, C.POINTER(P)]),
+    "hh_comm_free": (C.c_int, [P]),
+    "hh_comm_allgather": (C.c_int, [P, I64, P, P, P]),
+    "hh_ice_balance_sharded": (C.c_int, [P, C.POINTER(IceOpts), I32, I32, P, P, P, P, P, P, P, P, PF64, P]),
+    "hh_ice_filters_sharded": (C.c_int, [P, I32, P, P, P, P]),
+    "hh_ice_run_sharded": (C.c_int, [P, I32, P, P, P, I32, P]),
     "hh_dense_rowstats": (C.c_int, [P, I32, I64, P, P, P, P, I32, P]),
     "hh_dense_symvc": (C.c_int, [P, I32, I64, P, P, F64, F64, P, I32, P]),
     "hh_twostep": (C.c_int, [P, P, P, I64, P, P, P, P, I32, P]),

@@ -170,3 +170,121 @@ def balance_sharded(backend, ex: Exchange, max_iters: int, check_every: int = 8)
         if backend.active_groups(s) == 0:
             break
     return backend.finalize(s)
+
+
+# ----------------------------------------------------------- C-ABI driver
+# The same sharded ICE with the iteration loop in C++ (hh_ice_*_sharded):
+# the exchange is a C function pointer, the library's RCCL all-gather
+# (hh_comm_allgather over a communicator it owns) or, for CPU-side path checks
+# (gloo), a Python callback.
+
+def _cb_type():
+    import ctypes as C
+    return C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p)
+
+
+class CapiExchange:
+    """(function pointer, user) pair for hh_ice_*_sharded.
+
+    ``backend="nccl"``: the library owns an RCCL communicator; rank 0 makes
+    the ncclUniqueId and ``torch.distributed`` broadcasts it (any other means
+    would do for a non-Python caller).  ``"gloo"``: a Python callback
+    all-gathering through host memory (path checks with every rank on one
+    GPU, where RCCL refuses duplicate devices)."""
+
+    def __init__(self, rank_rows, world, rank, backend="nccl", group=None):
+        import ctypes as C
+        from . import _lib
+        self.rank_rows = np.ascontiguousarray(rank_rows, dtype=np.int64)
+        self.world, self.rank = int(world), int(rank)
+        self._comm = None
+        self._cb = None
+        lib = _lib.load()
+        if self.world == 1:
+            self.fn, self.user = None, None
+        elif backend == "nccl":
+            import torch.distributed as tdist
+            uid = C.create_string_buffer(128)
+            if self.rank == 0:
+                _lib.call("hh_comm_unique_id", uid)
+            obj = [bytes(uid.raw) if self.rank == 0 else None]
+            tdist.broadcast_object_list(obj, src=0, group=group)
+            uid = C.create_string_buffer(obj[0], 128)
+            h = C.c_void_p()
+            _lib.call("hh_comm_init", uid, self.world, self.rank, C.byref(h))
+            self._comm = h
+            self.fn = C.cast(lib.hh_comm_allgather, C.c_void_p)
+            self.user = h
+        else:
+            self._cb = _python_allgather(self.world, group)
+            self.fn = C.cast(self._cb, C.c_void_p)
+            self.user = None
+
+    def close(self):
+        if self._comm is not None:
+            from ._lib import call
+            call("hh_comm_free", self._comm)
+            self._comm = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def _python_allgather(world, group=None):
+    """An hh_allgather_fn over torch.distributed's CPU path (gloo)."""
+    import ctypes as C
+    import torch
+    import torch.distributed as tdist
+    from ._lib import call
+
+    def cb(send, count, recv, user, stream):
+        try:
+            st = C.c_void_p(stream) if stream else None
+            buf = torch.empty(int(count), dtype=torch.float64, device="cuda")
+            call("hh_device_copy", C.c_void_p(buf.data_ptr()), C.c_void_p(send), 8 * int(count), st)
+            call("hh_synchronize", st)
+            cpu = buf.cpu()
+            parts = [torch.empty_like(cpu) for _ in range(world)]
+            tdist.all_gather(parts, cpu, group=group)
+            g = torch.cat(parts).cuda()
+            torch.cuda.synchronize()
+            call("hh_device_copy", C.c_void_p(recv), C.c_void_p(g.data_ptr()), 8 * int(count) * world, st)
+            call("hh_synchronize", st)
+            return 0
+        except Exception:  # never raise through C
+            return -2
+    return _cb_type()(cb)
+
+
+def balance_capi(m, opts, ex: CapiExchange, stream=None):
+    """Filters + ICE to convergence on this rank's shard, loop in C++
+    (hh_ice_balance_sharded).  Returns (weights, stats), identical on every
+    rank."""
+    import ctypes as C
+    from .ice import _stats
+    from ._lib import call, ptr
+    inf = m.info()
+    G = inf["n_chroms"] if inf["cis_only"] else 1
+    w = np.empty(inf["n_bins"], np.float64)
+    scale, var = np.empty(G), np.empty(G)
+    iters, conv = np.empty(G, np.int32), np.empty(G, np.int32)
+    secs = C.c_double(0)
+    call("hh_ice_balance_sharded", m.handle, C.byref(opts.c_opts()), ex.world, ex.rank, ptr(ex.rank_rows),
+         ex.fn, ex.user, ptr(w), ptr(scale), ptr(var), ptr(iters), ptr(conv), C.byref(secs), stream)
+    st = _stats(opts, scale, var, iters, conv, inf["cis_only"])
+    st["sweep_seconds"] = secs.value
+    return w, st
+
+
+def filters_capi(st, ex: CapiExchange, stream=None):
+    from ._lib import call, ptr
+    call("hh_ice_filters_sharded", st._h, ex.world, ptr(ex.rank_rows), ex.fn, ex.user, stream)
+
+
+def iterate_capi(st, ex: CapiExchange, n: int, stream=None):
+    """``n`` ICE iterations enqueued from C++ (one call, no host polling)."""
+    from ._lib import call, ptr
+    call("hh_ice_run_sharded", st._h, ex.world, ptr(ex.rank_rows), ex.fn, ex.user, int(n), stream)

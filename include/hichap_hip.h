@@ -240,6 +240,36 @@ int hh_ice_finalize(hh_ice* s, double* weights, double* scale, double* var, int3
 int hh_ice_last_sweep_timing(const hh_ice* s, double* sweep_ms_total, int32_t* sweep_launches,
                              double* iter_ms_total);
 
+/* ------------------------------------------------ sharded ICE in C
+ * Genome-wide ICE over world processes (one GPU each), each holding the
+ * matrix rows rank_rows[rank] .. rank_rows[rank + 1] (whole 512-row blocks):
+ * per iteration one all-gather of the local marginals, then the identical
+ * update everywhere, iterations enqueued from C++ (no caller code in the
+ * loop).  The exchange is a callback: `allgather(send, count, recv, user,
+ * stream)` must gather `count` doubles from every rank (device buffers,
+ * rank order) into recv[world * count] on `stream` and return 0.  The
+ * library's RCCL transport: hh_comm_unique_id on one rank (128 bytes, shared
+ * by the caller's own means), hh_comm_init on every rank, then pass
+ * hh_comm_allgather with user = the hh_comm. */
+typedef int (*hh_allgather_fn)(const double* send, int64_t count, double* recv, void* user, void* stream);
+typedef struct hh_comm hh_comm;
+int hh_comm_unique_id(uint8_t* id128);
+int hh_comm_init(const uint8_t* id128, int32_t world, int32_t rank, hh_comm** out);
+int hh_comm_free(hh_comm* c);
+int hh_comm_allgather(const double* send, int64_t count, double* recv, void* comm, void* stream);
+/* The whole balance (filters, iterations to convergence, finalize) on this
+ * rank's shard `m`; outputs as hh_ice_balance (weights for every bin, identical
+ * on every rank). */
+int hh_ice_balance_sharded(hh_matrix* m, const hh_ice_opts* o, int32_t world, int32_t rank, const int64_t* rank_rows,
+                           hh_allgather_fn allgather, void* user, double* weights, double* scale, double* var,
+                           int32_t* iters, int32_t* converged, double* sweep_seconds, void* stream);
+/* Pieces of it on an hh_ice (bench / fixed iteration counts): the two
+ * filters, and n iterations without convergence polling. */
+int hh_ice_filters_sharded(hh_ice* s, int32_t world, const int64_t* rank_rows, hh_allgather_fn allgather, void* user,
+                           void* stream);
+int hh_ice_run_sharded(hh_ice* s, int32_t world, const int64_t* rank_rows, hh_allgather_fn allgather, void* user,
+                       int32_t n, void* stream);
+
 /* ------------------------------------------ dense two-step correction
  * Dense row-major N x N matrices; dtype 0 = int64, 1 = float64.  Host
  * pointers (copied in/out) or, with on_device = 1, device pointers. */

@@ -24,7 +24,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, case, cis_only, outdir):
+def _worker(rank, world, port, case, cis_only, outdir, impl="python"):
     import torch
     import torch.distributed as tdist
     from hichap_master_amd import _lib, dist, ice
@@ -39,12 +39,19 @@ def _worker(rank, world, port, case, cis_only, outdir):
         n = int(off[-1])
         rr = dist.partition_rows(np.bincount(b1, minlength=n) + np.bincount(b2, minlength=n), world)
         m = ice.ContactMatrix.from_pixels(b1, b2, c, n, off, cis_only=cis_only, row_range=(rr[rank], rr[rank + 1]))
-        st = ice.IceState(m, ice.IceOptions(max_iters=400, cis_only=cis_only))
-        ex = dist.Exchange(rr, torch.device("cuda", 0))
-        assert not ex.fused
-        w, s_ = dist.balance_sharded(st, ex, max_iters=400)
+        opts = ice.IceOptions(max_iters=400, cis_only=cis_only)
+        if impl == "capi":
+            # the loop in C++ (hh_ice_balance_sharded), exchange = a gloo callback
+            cx = dist.CapiExchange(rr, world, rank, backend="gloo")
+            w, s_ = dist.balance_capi(m, opts, cx, torch.cuda.current_stream().cuda_stream)
+            cx.close()
+        else:
+            st = ice.IceState(m, opts)
+            ex = dist.Exchange(rr, torch.device("cuda", 0))
+            assert not ex.fused
+            w, s_ = dist.balance_sharded(st, ex, max_iters=400)
+            st.close()
         torch.cuda.synchronize()
-        st.close()
         m.close()
         np.save(os.path.join(outdir, f"w{rank}.npy"), w)
         np.save(os.path.join(outdir, f"it{rank}.npy"), np.atleast_1d(s_["iters"]))
@@ -52,8 +59,8 @@ def _worker(rank, world, port, case, cis_only, outdir):
         tdist.destroy_process_group()
 
 
-@pytest.mark.parametrize("cis_only", [False, True])
-def test_balance_sharded_two_processes(cis_only):
+@pytest.mark.parametrize("cis_only,impl", [(False, "python"), (True, "python"), (False, "capi"), (True, "capi")])
+def test_balance_sharded_two_processes(cis_only, impl):
     import torch.multiprocessing as mp
     from hichap_master_amd import _lib, ice
     from oracle import ice_ref
@@ -64,7 +71,7 @@ def test_balance_sharded_two_processes(cis_only):
     n = int(off[-1])
     w_full, st_full = ice.balance(b1, b2, c, n, off, cis_only=cis_only, max_iters=400)
     with tempfile.TemporaryDirectory() as d:
-        mp.start_processes(_worker, args=(2, _free_port(), case, cis_only, d), nprocs=2, start_method="spawn")
+        mp.start_processes(_worker, args=(2, _free_port(), case, cis_only, d, impl), nprocs=2, start_method="spawn")
         ws = [np.load(os.path.join(d, f"w{r}.npy")) for r in range(2)]
         its = [np.load(os.path.join(d, f"it{r}.npy")) for r in range(2)]
     wr, sr = ice_ref.balance(b1, b2, c, n, off, cis_only=cis_only, max_iters=400)
@@ -72,3 +79,33 @@ def test_balance_sharded_two_processes(cis_only):
         np.testing.assert_array_equal(w, w_full)
         np.testing.assert_allclose(w, wr, rtol=1e-9, equal_nan=True)
         np.testing.assert_array_equal(it, np.atleast_1d(st_full["iters"]))
+
+
+def test_library_rccl_communicator_world1():
+    """hh_comm_* (the library-owned RCCL communicator) at world 1 on the box's
+    one GPU, and the C++ sharded balance at world 1 equal to hh_ice_balance."""
+    import ctypes as C
+    import torch
+    from hichap_master_amd import _lib, dist, ice
+    _lib.require_gpu()
+    uid = C.create_string_buffer(128)
+    _lib.call("hh_comm_unique_id", uid)
+    h = C.c_void_p()
+    _lib.call("hh_comm_init", uid, 1, 0, C.byref(h))
+    x = torch.arange(1000, dtype=torch.float64, device="cuda")
+    y = torch.zeros_like(x)
+    s = torch.cuda.current_stream().cuda_stream
+    _lib.call("hh_comm_allgather", C.c_void_p(x.data_ptr()), 1000, C.c_void_p(y.data_ptr()), h, C.c_void_p(s))
+    torch.cuda.synchronize()
+    assert torch.equal(x, y)
+    _lib.call("hh_comm_free", h)
+    rng = np.random.default_rng(5)
+    b1, b2, c, off = synth.coo_genome([800, 600], rng, A=25.0, trans_density=0.01)
+    n = int(off[-1])
+    m = ice.ContactMatrix.from_pixels(b1, b2, c, n, off)
+    opts = ice.IceOptions(max_iters=300)
+    w1, s1 = ice.balance_matrix(m, opts)
+    cx = dist.CapiExchange([0, n], 1, 0)
+    w2, s2 = dist.balance_capi(m, opts, cx)
+    np.testing.assert_array_equal(w1, w2)
+    assert s1["iters"] == s2["iters"]
