@@ -2,7 +2,7 @@
 arguments as ``HiCHap/StructureFind.py``:
 
 * ``Distance_Decay(M, G_array)``          StructureFind.py:201-271
-* ``Get_PCA(distance_bin, M, NG_array)``   :302-342
+* ``Get_PCA(distance_bin, M, NG_array, SA)`` :302-342 (SA: Sliding_Approach :274-299)
 * ``Select_PC_new(Cor_M, OE_M, pca)``      :374-423
 * ``Select_Allelic_PC(pcs, trad_pc)``      :446-460
 * ``Get_Gap(M)`` / ``Get_DI(M, Gap, w)``   :721-751 / :804-839
@@ -59,6 +59,8 @@ class _Comp:
         self.h = h
         self.decline = None
         self.NG = None
+        self.sa = False
+        self._sa_host = None
 
     def _s(self):
         return None if self.stream is None else C.c_void_p(int(self.stream))
@@ -79,6 +81,23 @@ class _Comp:
         out = np.empty(self.N, np.float64)
         call("hh_comp_diag_sums", self.h, ptr(g), ptr(out), self._s())
         return out
+
+    def sliding_oe(self, decline, step):
+        """Sliding_Approach O/E on the device (None: back to the plain O/E)."""
+        if decline is None:
+            call("hh_comp_sliding_oe", self.h, None, 0, self._s())
+            self.sa = False
+            return
+        self.decline = np.ascontiguousarray(decline, dtype=np.float64)
+        call("hh_comp_sliding_oe", self.h, ptr(self.decline), int(step), self._s())
+        self.sa = True
+        self._sa_host = None
+
+    def sa_matrix(self):
+        if self._sa_host is None:
+            self._sa_host = np.empty((self.N, self.N), np.float64)
+            call("hh_comp_get_sliding_oe", self.h, ptr(self._sa_host), self._s())
+        return self._sa_host
 
     def correlation(self, decline, NG):
         self.decline = np.ascontiguousarray(decline, dtype=np.float64)
@@ -158,6 +177,9 @@ class DeviceOE:
     def __array__(self, dtype=None, copy=None):
         c = self._c
         rows = np.arange(c.N) if self._rows is None else self._rows
+        if c.sa:
+            out = c.sa_matrix()[np.ix_(rows, c.NG)]
+            return out if dtype is None else out.astype(dtype)
         sub = c.M[np.ix_(rows, c.NG)]
         d = np.abs(rows[:, None] - c.NG[None, :])
         out = np.zeros_like(sub)
@@ -214,15 +236,21 @@ class StructureFind(TADCalling):
 
     def Get_PCA(self, distance_bin, M, NG_array, SA=False):
         """O/E, Pearson correlation and top-3 PCA (StructureFind.py:302-342).
-        Returns (pca_components[3 x n], Cor (lazy), OE[:, NG] (lazy))."""
-        if SA:
-            raise NotImplementedError("Sliding_Approach (SA=True) is not on the GPU path")
+        Returns (pca_components[3 x n], Cor (lazy), OE[:, NG] (lazy)).
+        ``SA=True`` uses the Sliding_Approach O/E (:274-299, window 600 kb)."""
         comp = self._comp if (self._comp is not None and self._comp_src is M) else None
         if comp is None:
             comp = _Comp(M, self.stream)
             self._comp, self._comp_src = comp, M
         decline = distance_bin
         decline[decline == 0] = decline[np.nonzero(decline)].min()
+        if SA:
+            step = 600000 // self.Res // 2
+            if step < 1:  # the reference reads decline[N], decline[N + 1] here
+                raise IndexError(f"Sliding_Approach window 600000 // Res {self.Res} // 2 = 0 bins")
+            comp.sliding_oe(decline, step)
+        elif comp.sa:
+            comp.sliding_oe(None, 0)
         comp.correlation(decline, NG_array)
         pcs, _, _ = comp.pca(3)
         self.pca_status = comp.pca_status

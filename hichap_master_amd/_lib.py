@@ -104,6 +104,8 @@ SIGNATURES = {
     "hh_comp_free": (C.c_int, [P]),
     "hh_comp_colnnz": (C.c_int, [P, P, P]),
     "hh_comp_diag_sums": (C.c_int, [P, P, P, P]),
+    "hh_comp_sliding_oe": (C.c_int, [P, P, I32, P]),
+    "hh_comp_get_sliding_oe": (C.c_int, [P, P, P]),
     "hh_comp_correlation": (C.c_int, [P, P, P, I64, P]),
     "hh_comp_get_cor": (C.c_int, [P, P, P]),
     "hh_comp_set_cor": (C.c_int, [P, P, P]),

@@ -102,6 +102,43 @@ __device__ __forceinline__ double oe_value(const double* __restrict__ M, const d
     return m / dec[d];
 }
 
+// Sliding_Approach O/E (StructureFind.py:274-299), two passes over M:
+// Hs[i][j] = sum_{|dj| <= step} M[i][j + dj] for the interior columns, then
+// OE[i][j] = sum_{|di| <= step} Hs[i + di][j] / E(|i - j|) inside the
+// [step, N - step - 1]^2 square, with the reference's 3-2-1 weighted expected
+// sum E = 3 d[i-j] + 2 d[i-j-1] + 2 d[i-j+1] + d[i-j-2] + d[i-j+2] (|.|,
+// left to right); M / d[|i - j|] on the border.  The box sum's order differs
+// from NumPy's slice sum by rounding only.
+__global__ __launch_bounds__(256) void k_sa_hsum(const double* __restrict__ M, long long N, int step,
+                                                 double* __restrict__ Hs) {
+    const long long t = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (t >= N * N) return;
+    const long long i = t / N, j = t % N;
+    if (j < step || j > N - step - 1) return;
+    const double* row = M + i * N + j;
+    double acc = 0.0;
+    for (int dj = -step; dj <= step; ++dj) acc += row[dj];
+    Hs[t] = acc;
+}
+
+__global__ __launch_bounds__(256) void k_sa_oe(const double* __restrict__ M, const double* __restrict__ Hs,
+                                               const double* __restrict__ dec, long long N, int step,
+                                               double* __restrict__ OE) {
+    const long long t = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (t >= N * N) return;
+    const long long i = t / N, j = t % N;
+    const long long dd = i - j;
+    auto d = [&](long long x) { return dec[x < 0 ? -x : x]; };
+    if (i < step || j < step || i > N - step - 1 || j > N - step - 1) {
+        OE[t] = M[t] / d(dd);
+        return;
+    }
+    double o = 0.0;
+    for (int di = -step; di <= step; ++di) o += Hs[t + (long long)di * N];
+    const double e = 3.0 * d(dd) + 2.0 * d(dd - 1) + 2.0 * d(dd + 1) + d(dd - 2) + d(dd + 2);
+    OE[t] = o / e;
+}
+
 // partial column sums of O/E over row chunks: part[chunk][c]
 __global__ __launch_bounds__(256) void k_oe_colsum(const double* __restrict__ M, const double* __restrict__ dec,
                                                    const long long* __restrict__ ng, long long N, long long n,
@@ -479,6 +516,8 @@ struct hh_comp {
     long long n = 0, ld = 0;     // Cor leading dimension (n padded to 128)
     DBuf<double> cor;            // ld x ld
     int iters = 0;
+    DBuf<double> sa;             // N x N Sliding_Approach O/E (hh_comp_sliding_oe), used when sa_on
+    int sa_on = 0;
     // last hh_comp_pca: converged flag, Cor products, Krylov cycles, method
     int pca_converged = 0, pca_products = 0, pca_cycles = 0, pca_method = 0;
 };
@@ -1375,6 +1414,39 @@ int hh_comp_diag_sums(hh_comp* c, const uint8_t* gapcol, double* sums, void* str
     });
 }
 
+int hh_comp_sliding_oe(hh_comp* c, const double* decline, int32_t step, void* stream) {
+    return guard([&] {
+        HH_REQUIRE(c, "null");
+        if (!decline) {  // back to the plain O/E
+            c->sa_on = 0;
+            c->sa.release();
+            return;
+        }
+        const long long N = c->N;
+        // step 0 reads d[N] / d[N + 1] in the reference (IndexError there)
+        HH_REQUIRE(step >= 1, "Sliding_Approach needs step = window // Res // 2 >= 1");
+        hipStream_t s = as_stream(stream);
+        DBuf<double> dec(N), Hs((size_t)N * N);
+        dec.upload(decline, N, s);
+        c->sa.alloc((size_t)N * N);
+        const unsigned g = (unsigned)((N * N + 255) / 256);
+        hipLaunchKernelGGL(k_sa_hsum, dim3(g), dim3(256), 0, s, c->Mp, N, (int)step, Hs.p);
+        hipLaunchKernelGGL(k_sa_oe, dim3(g), dim3(256), 0, s, c->Mp, Hs.p, dec.p, N, (int)step, c->sa.p);
+        HIP_CHECK(hipGetLastError());
+        HIP_CHECK(hipStreamSynchronize(s));
+        c->sa_on = 1;
+    });
+}
+
+int hh_comp_get_sliding_oe(hh_comp* c, double* oe, void* stream) {
+    return guard([&] {
+        HH_REQUIRE(c && oe && c->sa_on, "no Sliding_Approach O/E computed");
+        hipStream_t s = as_stream(stream);
+        c->sa.download(oe, (size_t)c->N * c->N, s);
+        HIP_CHECK(hipStreamSynchronize(s));
+    });
+}
+
 int hh_comp_correlation(hh_comp* c, const double* decline, const int64_t* ng, int64_t n, void* stream) {
     return guard([&] {
         HH_REQUIRE(c && decline && ng && n > 0 && n <= c->N, "bad arguments");
@@ -1383,21 +1455,28 @@ int hh_comp_correlation(hh_comp* c, const double* decline, const int64_t* ng, in
         c->n = n;
         c->ld = (n + kSyT - 1) / kSyT * kSyT;  // whole k_syrk tiles (a multiple of 64 for the other kernels)
         c->dec.alloc(N);
-        c->dec.upload(decline, N, s);
+        if (c->sa_on) {  // the O/E is already materialised: oe_value(sa, 1) = sa
+            std::vector<double> ones(N, 1.0);
+            c->dec.upload(ones.data(), N, s);
+            HIP_CHECK(hipStreamSynchronize(s));
+        } else {
+            c->dec.upload(decline, N, s);
+        }
+        const double* Msrc = c->sa_on ? c->sa.p : c->Mp;
         c->ng.alloc(n);
         c->ng.upload(reinterpret_cast<const long long*>(ng), n, s);
         // column means of O/E
         const int rpc = 256;
         const int chunks = (int)((N + rpc - 1) / rpc);
         DBuf<double> part((size_t)chunks * n), mu(n);
-        hipLaunchKernelGGL(k_oe_colsum, dim3((unsigned)((n + 255) / 256), (unsigned)chunks), dim3(256), 0, s, c->Mp,
+        hipLaunchKernelGGL(k_oe_colsum, dim3((unsigned)((n + 255) / 256), (unsigned)chunks), dim3(256), 0, s, Msrc,
                            c->dec.p, c->ng.p, N, (long long)n, rpc, part.p);
         hipLaunchKernelGGL(k_oe_mean, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, part.p, (long long)n, chunks,
                            N, mu.p);
         // centred O/E, padded
         const long long Npad = (N + 15) / 16 * 16;
         DBuf<double> Z((size_t)Npad * c->ld);
-        hipLaunchKernelGGL(k_oe_center, dim3((unsigned)((Npad * c->ld + 255) / 256)), dim3(256), 0, s, c->Mp, c->dec.p,
+        hipLaunchKernelGGL(k_oe_center, dim3((unsigned)((Npad * c->ld + 255) / 256)), dim3(256), 0, s, Msrc, c->dec.p,
                            c->ng.p, mu.p, N, (long long)n, Npad, c->ld, Z.p);
         // Cov = Z^T Z * (1 / (N - 1))  (np.cov: c *= true_divide(1, fact))
         DBuf<double> cov((size_t)c->ld * c->ld);
@@ -1611,7 +1690,8 @@ int hh_comp_select_stats(hh_comp* c, const double* pcs, int32_t k, double eps, d
         DBuf<double> part((size_t)n * 3 * 8);
         {
             HH_KTIME("k_select_stats", s);
-            hipLaunchKernelGGL(k_select_stats, dim3((unsigned)n), dim3(256), 0, s, c->cor.p, c->ld, n, c->Mp, c->N,
+            const double* Msrc = c->sa_on ? c->sa.p : c->Mp;
+            hipLaunchKernelGGL(k_select_stats, dim3((unsigned)n), dim3(256), 0, s, c->cor.p, c->ld, n, Msrc, c->N,
                                c->dec.p, c->ng.p, dcls.p, (int)k, eps, part.p);
         }
         HIP_CHECK(hipGetLastError());

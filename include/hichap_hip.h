@@ -338,8 +338,17 @@ int hh_comp_colnnz(hh_comp* c, int64_t* nnz_col, void* stream);
 /* sums[d] = sum of nonzero M[i][j] with |i-j| = d whose column j is not a gap
  * (gapcol[j] = 1) — the bincount of Distance_Decay before the bin_num division. */
 int hh_comp_diag_sums(hh_comp* c, const uint8_t* gapcol, double* sums, void* stream);
-/* O/E = M / decline[|i-j|] on nonzeros, columns ng[0..n); Pearson correlation
- * of those columns (np.corrcoef(rowvar=False), NaN -> 0) kept on the device. */
+/* Get_PCA(SA=True): the Sliding_Approach O/E (StructureFind.py:274-299,
+ * step = 600000 // Res // 2 >= 1) materialised on the device (N x N): box
+ * sum of M over the (2 step + 1)^2 window / the 3-2-1 weighted expected sum
+ * inside [step, N - step - 1]^2, M / decline[|i-j|] on the border.  Later
+ * hh_comp_correlation / hh_comp_select_stats use it in place of the plain
+ * O/E; decline = NULL switches back. */
+int hh_comp_sliding_oe(hh_comp* c, const double* decline, int32_t step, void* stream);
+int hh_comp_get_sliding_oe(hh_comp* c, double* oe, void* stream);
+/* O/E = M / decline[|i-j|] on nonzeros (or the Sliding_Approach O/E), columns
+ * ng[0..n); Pearson correlation of those columns (np.corrcoef(rowvar=False),
+ * NaN -> 0) kept on the device. */
 int hh_comp_correlation(hh_comp* c, const double* decline, const int64_t* ng, int64_t n, void* stream);
 int hh_comp_get_cor(hh_comp* c, double* cor, void* stream);
 /* Replace the device correlation (n x n from the last hh_comp_correlation). */

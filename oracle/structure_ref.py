@@ -58,6 +58,35 @@ def oe_matrix(M, decline):
     return OE
 
 
+def sliding_oe(M, decline, step):
+    """Sliding_Approach (StructureFind.py:274-299): inside
+    [step, N-step-1]^2 the (2 step+1)^2 box sum of M over the 3-2-1 weighted
+    expected sum of five diagonals; M / decline[|i-j|] on the border.
+    ``decline`` already has the zero fix of Get_PCA :321.  Vectorised: box
+    sums from a 2-D cumulative sum (rounding-level difference only)."""
+    M = np.asarray(M, dtype=np.float64)
+    dec = np.asarray(decline, dtype=np.float64)
+    N = M.shape[0]
+    if step < 1:
+        raise IndexError("Sliding_Approach with step 0 reads decline[N]")
+    idx = np.arange(N)
+    dd = idx[:, None] - idx[None, :]
+    OE = M / dec[np.abs(dd)]
+    lo, hi = step, N - step - 1
+    if hi >= lo:
+        P = np.zeros((N + 1, N + 1))
+        P[1:, 1:] = M.cumsum(0).cumsum(1)
+        a = np.arange(lo, hi + 1)
+        r0, r1 = a[:, None] - step, a[:, None] + step + 1
+        c0, c1 = a[None, :] - step, a[None, :] + step + 1
+        O = P[r1, c1] - P[r0, c1] - P[r1, c0] + P[r0, c0]
+        d = dd[lo:hi + 1, lo:hi + 1]
+        E = (3 * dec[np.abs(d)] + 2 * dec[np.abs(d - 1)] + 2 * dec[np.abs(d + 1)] + dec[np.abs(d - 2)]
+             + dec[np.abs(d + 2)])
+        OE[lo:hi + 1, lo:hi + 1] = O / E
+    return OE
+
+
 def pearson_columns(X):
     """np.corrcoef(X, rowvar=False) with NaN→0, inf→1 (Get_PCA :335-337)."""
     with np.errstate(invalid="ignore", divide="ignore"):
@@ -81,9 +110,15 @@ def top_components(C, k=3):
     return V
 
 
-def get_pca(decline, M, NG):
-    """Get_PCA (StructureFind.py:302-342), SA=False. Returns (pcs, Cor, OE[:, NG])."""
-    OE = oe_matrix(M, decline)[:, NG]
+def get_pca(decline, M, NG, SA=False, res=None):
+    """Get_PCA (StructureFind.py:302-342). Returns (pcs, Cor, OE[:, NG]);
+    SA=True: Sliding_Approach with window 600 kb at resolution ``res``."""
+    if SA:
+        dec = np.array(decline, dtype=np.float64)
+        dec[dec == 0] = dec[np.nonzero(dec)].min()
+        OE = sliding_oe(M, dec, 600000 // res // 2)[:, NG]
+    else:
+        OE = oe_matrix(M, decline)[:, NG]
     C = pearson_columns(OE)
     return top_components(C, 3), C, OE
 

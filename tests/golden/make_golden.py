@@ -40,7 +40,7 @@ MB_FUNCS = [
 ]
 SF_METHODS = [
     "Distance_Decay", "Get_PCA", "Select_PC_new", "Select_Allelic_PC", "Get_Gap", "Gap_Filter",
-    "Get_DI",
+    "Get_DI", "Sliding_Approach",
 ]
 
 
@@ -153,6 +153,23 @@ def gen_compartment(ref, rng, N):
                 pcs=np.asarray(pca), Cor=Cor, OE=OE, pc=full, trad=trad, allelic=allelic)
 
 
+def gen_compartment_sa(ref, rng, N, res):
+    """Get_PCA(SA=True): the Sliding_Approach O/E (StructureFind.py:274-299,
+    window 600 kb -> step = 600000 // res // 2) feeding corrcoef + PCA(3) +
+    Select_PC_new."""
+    M = synth.dense_chrom(N, rng, A=60.0, comp_len=(8, 30)).astype(np.float64)
+    sf = ref["RefSF"]()
+    sf.Res = res
+    dec, G, NG = sf.Distance_Decay(M=M.copy(), G_array=None)
+    dec0 = dec.copy()
+    pca, Cor, OE = sf.Get_PCA(distance_bin=dec.copy(), M=M, NG_array=NG, SA=True)
+    pc = sf.Select_PC_new(Cor, OE[NG], pca)
+    full = np.zeros(N)
+    full[NG] = pc
+    return dict(M=M, res=np.int64(res), decline=dec0, NG=np.asarray(NG, np.int64), pcs=np.asarray(pca),
+                Cor=Cor, OE=OE, pc=full)
+
+
 def gen_di(ref, rng, N, test_type, res=40000, min_tad=200000, window=600000):
     M = synth.dense_chrom(N, rng, A=30.0, gap_frac=0.04).astype(np.float64)
     # balanced-like float matrix with NaN->0 as Data_preprocess does
@@ -176,6 +193,19 @@ def gen_di(ref, rng, N, test_type, res=40000, min_tad=200000, window=600000):
                 lb=np.int64(int(min_tad / res)), gap_filtered=np.asarray(filt, np.int64))
 
 
+def main_sa():
+    """Only the Sliding_Approach cases (own seed: the other fixtures keep
+    their bytes)."""
+    ref = load_reference()
+    rng = np.random.default_rng(20201020)
+    out = {"compartment_sa_n120": gen_compartment_sa(ref, rng, 120, 100000),
+           "compartment_sa_n150": gen_compartment_sa(ref, rng, 150, 50000)}
+    for name, d in out.items():
+        path = os.path.join(HERE, name + ".npz")
+        np.savez_compressed(path, **d)
+        print("wrote", path, {k: np.shape(v) for k, v in d.items()})
+
+
 def main():
     ref = load_reference()
     out = {}
@@ -195,4 +225,5 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    import sys
+    main_sa() if sys.argv[1:] == ["sa"] else main()

@@ -66,3 +66,44 @@ def test_di_oracle(golden, name, test):
     np.testing.assert_array_equal(gap, g["gap"])
     di = structure_ref.get_di(g["M"], gap, int(g["window_bins"]), test)
     np.testing.assert_allclose(di, g["DI"], rtol=1e-12, atol=1e-300)
+
+
+def _sliding_loop(M, dec, step):
+    """Literal restatement of Sliding_Approach's double loop (:285-297)."""
+    N = M.shape[0]
+    out = np.zeros(M.shape)
+    for i in range(N):
+        for j in range(N):
+            if i < step or j < step or i > N - step - 1 or j > N - step - 1:
+                out[i][j] = M[i][j] / dec[abs(i - j)]
+            else:
+                o = M[i - step:i + step + 1, j - step:j + step + 1].sum()
+                e = (3 * dec[abs(i - j)] + 2 * dec[abs(i - j - 1)] + 2 * dec[abs(i - j + 1)] + dec[abs(i - j - 2)]
+                     + dec[abs(i - j + 2)])
+                out[i][j] = o / e
+    return out
+
+
+@pytest.mark.parametrize("N,step", [(30, 2), (9, 4), (7, 4), (25, 1)])
+def test_sliding_oe_vectorised_equals_loop(N, step):
+    rng = np.random.default_rng(N + step)
+    M = rng.poisson(3.0, size=(N, N)).astype(np.float64) + rng.random((N, N))
+    M = M + M.T
+    dec = rng.random(N) + 0.5
+    np.testing.assert_allclose(structure_ref.sliding_oe(M, dec, step), _sliding_loop(M, dec, step), rtol=1e-13)
+    with pytest.raises(IndexError):
+        structure_ref.sliding_oe(M, dec, 0)
+
+
+@pytest.mark.parametrize("name", ["compartment_sa_n120", "compartment_sa_n150"])
+def test_compartment_sliding_approach_oracle(golden, name):
+    """Get_PCA(SA=True) golden (make_golden.py main_sa, the reference run)."""
+    g = golden(name)
+    pcs, C, OE = structure_ref.get_pca(g["decline"], g["M"], g["NG"], SA=True, res=int(g["res"]))
+    np.testing.assert_allclose(OE, g["OE"], rtol=1e-12, atol=0)
+    np.testing.assert_allclose(C, g["Cor"], rtol=0, atol=1e-12)
+    for k in range(3):
+        s = np.sign(np.dot(pcs[k], g["pcs"][k]))
+        np.testing.assert_allclose(s * pcs[k], g["pcs"][k], atol=1e-9)
+    pc, _ = structure_ref.select_pc(C, OE[g["NG"]], pcs)
+    np.testing.assert_allclose(pc, g["pc"][g["NG"]], atol=1e-9)

@@ -170,3 +170,41 @@ def test_tad_scan_from_pixels_empty(SF):
     gap, di = sf.di_scan_pixels(e, e, np.zeros(0), None, 0, 200)
     np.testing.assert_array_equal(gap, np.arange(200))
     assert not di.any()
+
+
+@pytest.mark.parametrize("name", ["compartment_sa_n120", "compartment_sa_n150"])
+def test_sliding_approach_matches_reference_golden(SF, golden, name):
+    """Get_PCA(SA=True): Sliding_Approach O/E (StructureFind.py:274-299) on the
+    device, against the reference's own output."""
+    g = golden(name)
+    sf = SF(Res=int(g["res"]))
+    M = g["M"]
+    dec, G, NG = sf.Distance_Decay(M=M, G_array=None)
+    np.testing.assert_array_equal(NG, g["NG"])
+    pcs, Cor, OE = sf.Get_PCA(distance_bin=dec.copy(), M=M, NG_array=NG, SA=True)
+    np.testing.assert_allclose(np.asarray(OE), g["OE"], rtol=1e-12, atol=0)
+    np.testing.assert_allclose(np.asarray(Cor), g["Cor"], rtol=0, atol=1e-12)
+    for k in range(3):
+        np.testing.assert_allclose(_match_sign(pcs[k], g["pcs"][k]), g["pcs"][k], atol=1e-9)
+    pc = sf.Select_PC_new(Cor, OE[NG], pcs)
+    np.testing.assert_allclose(pc, g["pc"][NG], atol=1e-9)
+    np.testing.assert_array_equal(np.sign(pc), np.sign(g["pc"][NG]))
+    # the same matrix object back on the plain O/E
+    dec2, _, NG2 = sf.Distance_Decay(M=M, G_array=None)
+    _, Cor2, OE2 = sf.Get_PCA(distance_bin=dec2.copy(), M=M, NG_array=NG2)
+    ref = structure_ref.get_pca(dec2, M, NG2)
+    np.testing.assert_allclose(np.asarray(OE2), ref[2], rtol=1e-12)
+
+
+def test_sliding_approach_vs_oracle_larger_and_errors(SF):
+    rng = np.random.default_rng(5)
+    M = synth.dense_chrom(900, rng, A=80.0, comp_len=(20, 60), gap_frac=0.03).astype(np.float64)
+    sf = SF(Res=20000)  # step 15
+    dec, G, NG = sf.Distance_Decay(M=M, G_array=None)
+    pcs, Cor, OE = sf.Get_PCA(distance_bin=dec.copy(), M=M, NG_array=NG, SA=True)
+    p_ref, C_ref, OE_ref = structure_ref.get_pca(dec, M, NG, SA=True, res=20000)
+    np.testing.assert_allclose(np.asarray(OE), OE_ref, rtol=1e-12)
+    np.testing.assert_allclose(np.asarray(Cor), C_ref, atol=1e-11)
+    np.testing.assert_allclose(_match_sign(pcs[0], p_ref[0]), p_ref[0], atol=1e-8)
+    with pytest.raises(IndexError):
+        SF(Res=400000).Get_PCA(distance_bin=dec.copy(), M=M, NG_array=NG, SA=True)
