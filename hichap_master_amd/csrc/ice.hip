@@ -510,17 +510,33 @@ __device__ __forceinline__ void stage_bias(double* __restrict__ bl, const double
     }
 }
 
+// LDS of the three sweep bodies (one kernel each, or all three in one launch
+// for small matrices: k_sweep_all, a union of the three)
+struct TiledLds {
+    double bl[kW];
+    double acc2[2 * kR];  // narrow rows, then wide rows
+    uint32_t rps[kR + 1], rpsn[kR + 1];
+    uint16_t perm[2 * kR];
+    uint16_t band[2 * kBandSlots];
+};
+struct FlatLds {
+    double bl[kW];
+    double acc[kR];    // row sums (narrow + wide)
+    double accc[kR];   // narrow sums by compact row
+    uint16_t rec[kFrecU4 * 8];
+};
+
+// One tiled-kernel work unit u.
 template <int NB, int ABL>
-__global__ __launch_bounds__(kSweepThreads, 4) void k_sweep_tiled(TileDev T, const uint8_t* __restrict__ act,
-                                                                int n_list, const double* __restrict__ b,
-                                                                long long n_bins, double* __restrict__ part) {
-    __shared__ __attribute__((aligned(16))) double bl[kW];
-    __shared__ double acc2[2 * kR];  // narrow rows, then wide rows
-    __shared__ uint32_t rps[kR + 1], rpsn[kR + 1];
-    __shared__ uint16_t perm[2 * kR];
-    __shared__ uint16_t band[2 * kBandSlots];
-    if ((int)blockIdx.x >= n_list) return;
-    const int u = T.u_order[blockIdx.x];  // the tiled-kernel units lead the launch list
+__device__ __forceinline__ void sweep_tiled_unit(const TileDev& T, const uint8_t* __restrict__ act, int u,
+                                                 const double* __restrict__ b, long long n_bins,
+                                                 double* __restrict__ part, TiledLds& L) {
+    double* __restrict__ bl = L.bl;
+    double* __restrict__ acc2 = L.acc2;
+    uint32_t* __restrict__ rps = L.rps;
+    uint32_t* __restrict__ rpsn = L.rpsn;
+    uint16_t* __restrict__ perm = L.perm;
+    uint16_t* __restrict__ band = L.band;
     {
         bool on = false;
         for (int g = T.u_glo[u]; g <= T.u_ghi[u]; ++g) on |= act[g] != 0;
@@ -567,6 +583,15 @@ __global__ __launch_bounds__(kSweepThreads, 4) void k_sweep_tiled(TileDev T, con
     for (int k = threadIdx.x; k < rb - ra; k += kSweepThreads) part[T.u_slot[u] + k] = acc2[k] + acc2[(rb - ra) + k];
 }
 
+template <int NB, int ABL>
+__global__ __launch_bounds__(kSweepThreads, 4) void k_sweep_tiled(TileDev T, const uint8_t* __restrict__ act,
+                                                                int n_list, const double* __restrict__ b,
+                                                                long long n_bins, double* __restrict__ part) {
+    __shared__ __attribute__((aligned(16))) TiledLds L;
+    if ((int)blockIdx.x >= n_list) return;
+    sweep_tiled_unit<NB, ABL>(T, act, T.u_order[blockIdx.x], b, n_bins, part, L);  // tiled units lead the list
+}
+
 // K1c: the flat tiles (whole row-blocks whose rows are all short).  Per
 // tile the latency chain is kept to one hop: each wave's row / uint4 range
 // (tile_fw, read one tile ahead) lets it issue the loads of its whole narrow
@@ -576,18 +601,15 @@ __global__ __launch_bounds__(kSweepThreads, 4) void k_sweep_tiled(TileDev T, con
 // segment accumulates by compact row (flat_step_c), the few wide rows by row
 // id, and after a barrier the compact sums are added to their rows.
 template <int U, int ABL>
-__global__ __launch_bounds__(kSweepThreads, 4) void k_sweep_flat(TileDev T, const uint8_t* __restrict__ act,
-                                                               int n_list, int list_off,
-                                                               const double* __restrict__ b, long long n_bins,
-                                                               double* __restrict__ part) {
+__device__ __forceinline__ void sweep_flat_unit(const TileDev& T, const uint8_t* __restrict__ act, int u,
+                                                const double* __restrict__ b, long long n_bins,
+                                                double* __restrict__ part, FlatLds& L) {
     static_assert(kSweepWaves == kFlatWaves, "one plan split per wave");
     constexpr int UW = 2;  // wide runs: few wide entries in flat tiles
-    __shared__ __attribute__((aligned(16))) double bl[kW];
-    __shared__ double acc[kR];    // row sums (narrow + wide)
-    __shared__ double accc[kR];   // narrow sums by compact row
-    __shared__ __attribute__((aligned(16))) uint16_t rec[kFrecU4 * 8];
-    if ((int)blockIdx.x >= n_list) return;
-    const int u = T.u_order[list_off + blockIdx.x];
+    double* __restrict__ bl = L.bl;
+    double* __restrict__ acc = L.acc;
+    double* __restrict__ accc = L.accc;
+    uint16_t* __restrict__ rec = L.rec;
     {
         bool on = false;
         for (int g = T.u_glo[u]; g <= T.u_ghi[u]; ++g) on |= act[g] != 0;
@@ -644,6 +666,16 @@ __global__ __launch_bounds__(kSweepThreads, 4) void k_sweep_flat(TileDev T, cons
     for (int k = threadIdx.x; k < nr; k += kSweepThreads) part[T.u_slot[u] + k] = acc[k];
 }
 
+template <int U, int ABL>
+__global__ __launch_bounds__(kSweepThreads, 4) void k_sweep_flat(TileDev T, const uint8_t* __restrict__ act,
+                                                               int n_list, int list_off,
+                                                               const double* __restrict__ b, long long n_bins,
+                                                               double* __restrict__ part) {
+    __shared__ __attribute__((aligned(16))) FlatLds L;
+    if ((int)blockIdx.x >= n_list) return;
+    sweep_flat_unit<U, ABL>(T, act, T.u_order[list_off + blockIdx.x], b, n_bins, part, L);
+}
+
 // ---------------------------------------------------------------- K2
 // marg_r = b_r * (sum of the row's unit partials + wide entries + 2 diag b_r)
 // K1b: the dense diagonal bands (uint8 counts near the diagonal, 4-bit
@@ -661,11 +693,11 @@ __global__ __launch_bounds__(kSweepThreads, 4) void k_sweep_flat(TileDev T, cons
 // per wave, fixed per-lane order + xor-tree wave reduction: deterministic.
 constexpr int kBandThreads = 512;
 constexpr int kBandChunkB = kBandChunk;  // bytes of a segment per block
-template <int BITS>
+template <int BITS, int ROWS>
 struct BandGeo {
     static constexpr int G = 128 / BITS;                 // slots per 16-byte group
     static constexpr int CS = kBandChunkB * 8 / BITS;    // slots per chunk
-    static constexpr int WIN = kBandRows + CS;           // window values
+    static constexpr int WIN = ROWS + CS;                // window values
     static constexpr int LDS = WIN + WIN / G + 1;
 };
 template <int G>
@@ -707,24 +739,39 @@ __device__ __forceinline__ double band_dot_shifted(const uint4 prev, const uint4
     }
 }
 
-template <int BITS, int ABL>
-__global__ __launch_bounds__(kBandThreads) void k_sweep_band(const uint8_t* __restrict__ seg, long long row_stride,
-                                                             int seg_bytes, long long dlo, long long nloc,
-                                                             long long row_lo, long long n_bins,
-                                                             const uint8_t* __restrict__ act,
-                                                             const uint16_t* __restrict__ row_group,
-                                                             const double* __restrict__ b,
-                                                             double* __restrict__ bpart) {
-    using Geo = BandGeo<BITS>;
+// The band segments of one sweep (uint8 band; 4-bit band, negative and
+// positive diagonals): slot s of a segment row <-> diagonal dlo + s; its nc
+// chunks are grid rows [y0, y0 + nc) and write bpart chunks [ch, ch + nc).
+struct BandSeg {
+    const uint8_t* seg;
+    long long stride, dlo;
+    int bytes, nc, ch, bits;
+};
+struct BandSegs {
+    BandSeg s[3];
+    int n;
+};
+
+// One (ROWS-row block, 2048-byte chunk) of one segment.  ROWS = 256 on big
+// matrices; 64 when the grid would not fill the chip (a wave walks ROWS / 8
+// rows in sequence: on a single chromosome the 256-row chain, not the bytes,
+// set the time).  A row's partial does not depend on ROWS (lane -> slot and
+// the summation order are fixed by the row alone): bitwise the same sweep.
+template <int BITS, int ABL, int ROWS>
+__device__ __forceinline__ void band_block(const BandSeg& P, int rblk, int chunk, double* __restrict__ bl,
+                                           uint8_t* __restrict__ ract, long long nloc, long long row_lo,
+                                           long long n_bins, const uint8_t* __restrict__ act,
+                                           const uint16_t* __restrict__ row_group, const double* __restrict__ b,
+                                           double* __restrict__ bpart) {
+    using Geo = BandGeo<BITS, ROWS>;
     constexpr int G = Geo::G;
-    __shared__ double bl[Geo::LDS];
-    __shared__ uint8_t ract[kBandRows];  // active flag per row (no dependent global loads in the row loop)
-    const long long r0 = (long long)blockIdx.x * kBandRows;
-    const int chunk = blockIdx.y;
-    const int c0 = chunk * kBandChunkB, c1 = min(c0 + kBandChunkB, seg_bytes);  // bytes
-    const int s0 = c0 * 8 / BITS, s1 = c1 * 8 / BITS;                              // slots
-    const int nr = (int)min((long long)kBandRows, nloc - r0);
-    const long long g0 = row_lo + r0 + dlo + s0;  // bias column of window index 0
+    const uint8_t* __restrict__ seg = P.seg;
+    const long long row_stride = P.stride;
+    const long long r0 = (long long)rblk * ROWS;
+    const int c0 = chunk * kBandChunkB, c1 = min(c0 + kBandChunkB, P.bytes);  // bytes
+    const int s0 = c0 * 8 / BITS, s1 = c1 * 8 / BITS;                          // slots
+    const int nr = (int)min((long long)ROWS, nloc - r0);
+    const long long g0 = row_lo + r0 + P.dlo + s0;  // bias column of window index 0
     const int len = ((nr + G - 1) & ~(G - 1)) + (s1 - s0);
     for (int k = threadIdx.x; k < len; k += kBandThreads) {
         // the band multiplies implicit zeros too: a NaN bias (an empty group
@@ -739,8 +786,9 @@ __global__ __launch_bounds__(kBandThreads) void k_sweep_band(const uint8_t* __re
     constexpr int NW = kBandThreads / 64;
     constexpr int RJ = 2;       // rows of a G-aligned row group handled together: they share the window
     constexpr int RPG = G / NW; // rows of a G-group per wave
-    static_assert(G % NW == 0 && RPG % RJ == 0, "whole rows per wave and group");
+    static_assert(G % NW == 0 && RPG % RJ == 0 && ROWS % G == 0, "whole rows per wave and group");
     const uint4 zero = make_uint4(0u, 0u, 0u, 0u);
+    double* __restrict__ out = bpart + (long long)(P.ch + chunk) * nloc;
     for (int gh = 0; gh < (nr + G - 1) / G * (RPG / RJ); ++gh) {
         // rows gb + wave + NW (j0 + j) (shift m = wave + NW (j0 + j), uniform):
         // the window values of a lane's slot group are read from LDS once for
@@ -785,8 +833,77 @@ __global__ __launch_bounds__(kBandThreads) void k_sweep_band(const uint8_t* __re
 #pragma unroll
         for (int j = 0; j < RJ; ++j) {
             const double t = wave_sum(acc[j]);
-            if (lane == 0 && a[j]) bpart[(long long)chunk * nloc + r0 + gb + wave + NW * (j0 + j)] = t;
+            if (lane == 0 && a[j]) out[r0 + gb + wave + NW * (j0 + j)] = t;
         }
+    }
+}
+
+// All band segments of a sweep in one launch (grid.y = their chunks, uint8
+// first): the three used to run back to back, each with its own ramp and
+// tail.  Registers / LDS are the larger (4-bit) body's.
+template <int ROWS>
+struct BandLds {
+    static constexpr int L8 = BandGeo<8, ROWS>::LDS, L4 = BandGeo<4, ROWS>::LDS;
+    double bl[L8 > L4 ? L8 : L4];
+    uint8_t ract[ROWS];  // active flag per row (no dependent global loads in the row loop)
+};
+
+// grid row y of the band launch -> segment and its chunk
+template <int ABL, int ROWS>
+__device__ __forceinline__ void band_any(const BandSegs& S, int rblk, int y, BandLds<ROWS>& L, long long nloc,
+                                         long long row_lo, long long n_bins, const uint8_t* __restrict__ act,
+                                         const uint16_t* __restrict__ row_group, const double* __restrict__ b,
+                                         double* __restrict__ bpart) {
+    int k = 0;
+    while (k + 1 < S.n && y >= S.s[k].nc) {
+        y -= S.s[k].nc;
+        ++k;
+    }
+    const BandSeg P = S.s[k];
+    if (P.bits == 8)
+        band_block<8, ABL, ROWS>(P, rblk, y, L.bl, L.ract, nloc, row_lo, n_bins, act, row_group, b, bpart);
+    else
+        band_block<4, ABL, ROWS>(P, rblk, y, L.bl, L.ract, nloc, row_lo, n_bins, act, row_group, b, bpart);
+}
+
+template <int ABL, int ROWS>
+__global__ __launch_bounds__(kBandThreads) void k_sweep_bands(BandSegs S, long long nloc, long long row_lo,
+                                                              long long n_bins, const uint8_t* __restrict__ act,
+                                                              const uint16_t* __restrict__ row_group,
+                                                              const double* __restrict__ b,
+                                                              double* __restrict__ bpart) {
+    __shared__ BandLds<ROWS> L;
+    band_any<ABL, ROWS>(S, blockIdx.x, blockIdx.y, L, nloc, row_lo, n_bins, act, row_group, b, bpart);
+}
+
+// Small matrices (one chromosome, a shard of a few hundred MB): the whole
+// sweep -- tiled units, band blocks, flat units -- as ONE launch.  Each body
+// is latency-bound there (few blocks, each a short dependent chain), and run
+// as three kernels their ramps and tails add up; in one grid the blocks of
+// all three share the CUs.  Same bodies, same partials: bitwise the same.
+static_assert(kBandThreads == kSweepThreads, "one block shape");
+template <int NB, int U, int ABL>
+__global__ __launch_bounds__(kSweepThreads, 4) void k_sweep_all(TileDev T, const uint8_t* __restrict__ act,
+                                                              int n_tiled, int n_band, BandSegs S, int band_rb,
+                                                              long long nloc, long long row_lo,
+                                                              const uint16_t* __restrict__ row_group,
+                                                              const double* __restrict__ b, long long n_bins,
+                                                              double* __restrict__ part,
+                                                              double* __restrict__ bpart) {
+    __shared__ __attribute__((aligned(16))) union Lds {
+        TiledLds t;
+        FlatLds f;
+        BandLds<64> band;
+    } L;
+    // grid: [tiled units | band blocks (n_band = band_rb x chunks) | flat units]
+    const int x = blockIdx.x;
+    if (x < n_tiled) {
+        sweep_tiled_unit<NB, ABL>(T, act, T.u_order[x], b, n_bins, part, L.t);
+    } else if (x < n_tiled + n_band) {
+        const int y = x - n_tiled;
+        band_any<ABL, 64>(S, y % band_rb, y / band_rb, L.band, nloc, row_lo, n_bins, act, row_group, b, bpart);
+    } else {
+        sweep_flat_unit<U, ABL>(T, act, T.u_order[x - n_band], b, n_bins, part, L.f);  // flat units follow the tiled
     }
 }
 
@@ -1047,6 +1164,10 @@ static int g_split_tiles = 1;      // with band_concurrent: tiled kernel on a se
 // below this payload the fork / join costs more than the overlap gains (C2,
 // 0.2 GB: 4 620 -> 4 300 it/s with three streams; N=8 C4 shards, 1.85 GB, gain)
 static int64_t g_conc_min_bytes = 1LL << 30;
+static int g_band_rows = 0;   // rows per band block: 0 = auto (64 or 256)
+static int g_band_fused = 1;  // the band segments in one launch
+static int g_sweep_single = -1;  // whole sweep in one launch: -1 auto (below g_single_max_bytes), 0 off, 1 on
+static int64_t g_single_max_bytes = 1LL << 30;
 
 template <int NB, int ABL>
 static void launch_sweep(const hh_matrix* m, const uint8_t* act, const double* b, double* part, hipStream_t s,
@@ -1084,27 +1205,69 @@ static void sweep(const hh_matrix* m, const uint8_t* act, const double* b, doubl
     HIP_CHECK(hipGetLastError());
 }
 
+// The matrix's band segments; returns their total chunk count.
+static int band_segs(const hh_matrix* m, BandSegs& segs) {
+    const long long W8 = m->band_w, W4 = m->band_w4;
+    segs = BandSegs{};
+    int ch = 0;  // first bpart chunk of the segment
+    auto add = [&](const uint8_t* seg, long long stride, long long bytes, long long dlo, int bits) {
+        const int nc = (int)((bytes + kBandChunkB - 1) / kBandChunkB);
+        segs.s[segs.n++] = BandSeg{seg, stride, dlo, (int)bytes, nc, ch, bits};
+        ch += nc;
+    };
+    if (W8 > 0) add(m->band.p, band_stride(W8), band_stride(W8), -W8, 8);
+    if (W4 > W8) {
+        const long long st = band4_stride(W8, W4), sg = band4_seg(W8, W4);
+        add(m->band4.p, st, sg, -W4, 4);
+        add(m->band4.p + sg, st, sg, W8 + 1, 4);
+    }
+    return ch;
+}
+
 static void sweep_band(hh_ice* S, hipStream_t s) {
     const hh_matrix* m = S->m;
     if (!S->nch || !S->nloc) return;
-    const unsigned rb = (unsigned)((S->nloc + kBandRows - 1) / kBandRows);
-    const long long W8 = m->band_w, W4 = m->band_w4;
-    int ch = 0;  // first bpart chunk of the segment
-    auto launch = [&](auto kern, const uint8_t* seg, long long stride, long long bytes, long long dlo) {
-        const int nc = (int)((bytes + kBandChunkB - 1) / kBandChunkB);
-        hipLaunchKernelGGL(kern, dim3(rb, (unsigned)nc), dim3(kBandThreads), 0, s, seg, stride, (int)bytes, dlo,
-                           (long long)S->nloc, (long long)m->row_lo, (long long)m->n_bins, S->act(), m->row_group.p,
-                           S->bias.p, S->bpart.p + (long long)ch * S->nloc);
-        HIP_CHECK(hipGetLastError());
-        ch += nc;
-    };
+    BandSegs segs;
+    const int ch = band_segs(m, segs);
+    // 64-row blocks when 256-row blocks would give under ~4 per CU
+    const int rows = g_band_rows ? g_band_rows : (((S->nloc + 255) / 256) * ch < 1024 ? 64 : 256);
     const bool abl = g_sweep_ablate == 1;  // timing ablation (stream only)
-    if (W8 > 0) launch(abl ? k_sweep_band<8, 1> : k_sweep_band<8, 0>, m->band.p, band_stride(W8), band_stride(W8), -W8);
-    if (W4 > W8) {
-        const long long st = band4_stride(W8, W4), sg = band4_seg(W8, W4);
-        launch(abl ? k_sweep_band<4, 1> : k_sweep_band<4, 0>, m->band4.p, st, sg, -W4);
-        launch(abl ? k_sweep_band<4, 1> : k_sweep_band<4, 0>, m->band4.p + sg, st, sg, W8 + 1);
+    auto launch = [&](const BandSegs& L, int nc) {
+        const unsigned rb = (unsigned)((S->nloc + rows - 1) / rows);
+        auto kern = rows == 64 ? (abl ? k_sweep_bands<1, 64> : k_sweep_bands<0, 64>)
+                               : (abl ? k_sweep_bands<1, 256> : k_sweep_bands<0, 256>);
+        hipLaunchKernelGGL(kern, dim3(rb, (unsigned)nc), dim3(kBandThreads), 0, s, L, (long long)S->nloc,
+                           (long long)m->row_lo, (long long)m->n_bins, S->act(), m->row_group.p, S->bias.p,
+                           S->bpart.p);
+        HIP_CHECK(hipGetLastError());
+    };
+    if (g_band_fused) {
+        launch(segs, ch);
+    } else {
+        for (int k = 0; k < segs.n; ++k) {
+            BandSegs one{};
+            one.s[0] = segs.s[k];
+            one.n = 1;
+            launch(one, segs.s[k].nc);
+        }
     }
+}
+
+// The whole sweep as one k_sweep_all launch (small matrices).
+static void sweep_single(hh_ice* S, hipStream_t s) {
+    const hh_matrix* m = S->m;
+    BandSegs segs;
+    const int ch = (S->nch && S->nloc) ? band_segs(m, segs) : (segs = BandSegs{}, 0);
+    const int band_rb = (int)((S->nloc + 63) / 64);
+    const int n_tiled = (int)(m->n_units - m->n_units_flat), n_flat = (int)m->n_units_flat;
+    const long long n_band = ch ? (long long)band_rb * ch : 0;
+    const long long grid = n_tiled + n_band + n_flat;
+    if (!grid) return;
+    HH_REQUIRE(grid < (1LL << 31), "sweep grid too large for one launch");
+    hipLaunchKernelGGL((k_sweep_all<2, kFlatU, 0>), dim3((unsigned)grid), dim3(kSweepThreads), 0, s, m->dev(),
+                       S->act(), n_tiled, (int)n_band, segs, band_rb, (long long)S->nloc, (long long)m->row_lo,
+                       m->row_group.p, S->bias.p, (long long)m->n_bins, S->part.p, S->bpart.p);
+    HIP_CHECK(hipGetLastError());
 }
 
 static void marg_weighted(hh_ice* S, double* out, hipStream_t s, bool timed, int slot) {
@@ -1115,10 +1278,13 @@ static void marg_weighted(hh_ice* S, double* out, hipStream_t s, bool timed, int
         // the two sweeps write disjoint partials (part / bpart): the band
         // kernel runs on a side stream so its blocks fill the CUs the tile
         // kernel leaves idle (both are HBM-bound; neither saturates alone)
-        const bool conc = g_band_concurrent && S->nch && S->nloc && m->n_units &&
-                          4 * m->n_slots + 2 * m->n_slots_narrow + (int64_t)m->band.n + (int64_t)m->band4.n >=
-                              g_conc_min_bytes;
-        if (conc) {
+        const int64_t bytes = 4 * m->n_slots + 2 * m->n_slots_narrow + (int64_t)m->band.n + (int64_t)m->band4.n;
+        const bool conc = g_band_concurrent && S->nch && S->nloc && m->n_units && bytes >= g_conc_min_bytes;
+        const bool single = g_sweep_ablate == 0 && g_sweep_nb == 2 &&
+                            (g_sweep_single == 1 || (g_sweep_single == -1 && bytes < g_single_max_bytes));
+        if (single) {
+            sweep_single(S, s);
+        } else if (conc) {
             HIP_CHECK(hipEventRecord(S->fork, s));
             HIP_CHECK(hipStreamWaitEvent(S->side, S->fork, 0));
             sweep_band(S, S->side);
@@ -1213,6 +1379,18 @@ int hh_tune(const char* key, int64_t value) {
         } else if (k == "pca_p") {
             HH_REQUIRE(value >= 2 && value <= 8, "pca_p in [2, 8]");
             g_pca_p = (int)value;
+        } else if (k == "band_rows") {
+            HH_REQUIRE(value == 0 || value == 64 || value == 256, "band_rows in {0 (auto), 64, 256}");
+            g_band_rows = (int)value;
+        } else if (k == "sweep_single") {
+            HH_REQUIRE(value >= -1 && value <= 1, "sweep_single in {-1 (auto), 0, 1}");
+            g_sweep_single = (int)value;
+        } else if (k == "single_max_bytes") {
+            HH_REQUIRE(value >= 0, "single_max_bytes >= 0");
+            g_single_max_bytes = value;
+        } else if (k == "band_fused") {
+            HH_REQUIRE(value == 0 || value == 1, "band_fused in {0, 1}");
+            g_band_fused = (int)value;
         } else if (k == "band_concurrent") {
             HH_REQUIRE(value == 0 || value == 1, "band_concurrent in {0, 1}");
             g_band_concurrent = (int)value;

@@ -42,7 +42,7 @@ constexpr uint32_t kNarrowMax = 7;                        // counts stored as ui
 // below); W is a multiple of 16 chosen from
 // the data (the diagonals whose occupancy is >= kBandDensity), 0 = no band.
 // Everything else (farther, trans, larger counts) stays in the tiles.
-constexpr int kBandRows = 256;      // rows per band work block
+// band work blocks: 64 or 256 rows (ice.hip sweep_band)
 constexpr int kBandChunk = 2048;    // band slots per work block
 constexpr int kBandMaxW = 16384;
 constexpr uint32_t kBandMaxCnt = 255u;

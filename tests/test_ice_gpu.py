@@ -443,3 +443,52 @@ def test_config_size_balanced_marginals(ice, cfg):
     mr = marg[ok]
     assert abs(mr.mean() - 1.0) < 5e-3, mr.mean()
     assert mr.var() < 1e-4, mr.var()
+
+
+def test_closed_forms(ice):
+    """The analytic known answers of tests/test_oracle_ice.py through the HIP
+    path: 2 bins (one sweep, var 0, w = 1/sqrt(a)), 3 bins (w0 = sqrt(c/2ab)
+    ...), and an all-masked genome-wide matrix (weights NaN, var 0)."""
+    from tests.test_oracle_ice import _three_bin
+    for a in (1, 7, 123456):
+        w, st = ice.balance([0, 0, 1], [0, 1, 1], [5, a, 9], 2, [0, 2], min_nnz=0, mad_max=0)
+        np.testing.assert_allclose(w, 1 / np.sqrt(a), rtol=1e-15)
+        assert st["iters"] == 1 and st["var"] == 0.0 and st["scale"] == a
+    for abc in ((1, 2, 3), (10, 1, 1), (5, 40, 17)):
+        (b1, b2, c), w_exact = _three_bin(*abc)
+        w, st = ice.balance(b1, b2, c.astype(np.int64), 3, [0, 3], min_nnz=0, mad_max=0, tol=1e-20,
+                            max_iters=5000)
+        np.testing.assert_allclose(w, w_exact, rtol=1e-8)
+    rng = np.random.default_rng(9)
+    b1, b2, c, off = synth.coo_genome([40, 30], rng, A=5.0, trans_density=0.0)
+    w, st = ice.balance(b1, b2, c, int(off[-1]), off, min_nnz=10 ** 6)
+    assert np.isnan(w).all() and st["var"] == 0.0 and np.isnan(st["scale"])
+
+
+@pytest.mark.parametrize("cis_only", [False, True])
+def test_sweep_launch_shapes_bitwise(ice, cis_only):
+    """The sweep's launch shapes -- one k_sweep_all launch (small matrices),
+    band segments fused or one launch each, 64- or 256-row band blocks --
+    produce the same partials: bitwise the same weights and iterations."""
+    from hichap_master_amd import _lib
+    b1, b2, c, off = _case(23, sizes=(1700, 1100, 600), A=60.0, trans=0.02)
+    n = int(off[-1])
+    knobs = ("sweep_single", "band_fused", "band_rows", "flat_max")
+    default = {"sweep_single": -1, "band_fused": 1, "band_rows": 0, "flat_max": None}
+    shapes = [dict(sweep_single=0, band_fused=0, band_rows=256), dict(sweep_single=1),
+              dict(sweep_single=0, band_fused=1, band_rows=64), dict(sweep_single=0, band_fused=0, band_rows=64)]
+    try:
+        ref = None
+        for sh in shapes:
+            for k in knobs[:3]:
+                _lib.call("hh_tune", k.encode(), sh.get(k, default[k]))
+            w, st = ice.balance(b1, b2, c, n, off, cis_only=cis_only, max_iters=300)
+            if ref is None:
+                ref = (w, st)
+            np.testing.assert_array_equal(w, ref[0])
+            np.testing.assert_array_equal(np.atleast_1d(st["iters"]), np.atleast_1d(ref[1]["iters"]))
+    finally:
+        for k in knobs[:3]:
+            _lib.call("hh_tune", k.encode(), default[k])
+    wr, _ = ice_ref.balance(b1, b2, c, n, off, cis_only=cis_only, max_iters=300)
+    np.testing.assert_allclose(ref[0], wr, rtol=1e-9, equal_nan=True)

@@ -75,3 +75,40 @@ def test_cis_only_ignores_trans():
     w2, st2 = ice_ref.balance(b1[cis], b2[cis], c[cis], n, off, cis_only=True, max_iters=1000)
     np.testing.assert_allclose(w, w2, rtol=1e-12, equal_nan=True)
     assert len(st["scale"]) == 2 and st["chrom_converged"].all()
+
+
+# ---- closed forms (exact small cases, all-masked genome-wide)
+def _three_bin(a, b, c):
+    """3 bins, zero diagonal, A01 = a, A02 = b, A12 = c.  Equal row sums s of
+    w_i w_j A_ij force w0 w1 a = w0 w2 b = w1 w2 c = s / 2; rescaled to
+    marginals 1 (s = 1): w0 = sqrt(c / 2ab), w1 = sqrt(b / 2ac), w2 = sqrt(a / 2bc)."""
+    pix = (np.array([0, 0, 1]), np.array([1, 2, 2]), np.array([a, b, c], dtype=np.float64))
+    w = np.sqrt(np.array([c / (2 * a * b), b / (2 * a * c), a / (2 * b * c)]))
+    return pix, w
+
+
+def test_two_bin_closed_form():
+    """One off-diagonal pixel of count a: marginals equal after one sweep,
+    var 0, weights 1 / sqrt(a) (rescaled), scale a."""
+    for a in (1.0, 7.0, 123456.0):
+        w, st = ice_ref.balance(np.array([0, 0, 1]), np.array([0, 1, 1]), np.array([5.0, a, 9.0]), 2, [0, 2],
+                                min_nnz=0, mad_max=0)
+        np.testing.assert_allclose(w, 1 / np.sqrt(a), rtol=1e-15)
+        assert st["iters"] == 1 and st["var"] == 0.0 and st["scale"] == a
+
+
+@pytest.mark.parametrize("abc", [(1.0, 2.0, 3.0), (10.0, 1.0, 1.0), (5.0, 40.0, 17.0)])
+def test_three_bin_closed_form(abc):
+    (b1, b2, c), w_exact = _three_bin(*abc)
+    w, st = ice_ref.balance(b1, b2, c, 3, [0, 3], min_nnz=0, mad_max=0, tol=1e-20, max_iters=20000)
+    np.testing.assert_allclose(w, w_exact, rtol=1e-8)
+
+
+def test_all_masked_genome_wide():
+    """Every bin fails min_nnz: cooler's all-zero-marginal exit (weights all
+    NaN, var 0, scale NaN, converged after one sweep)."""
+    rng = np.random.default_rng(9)
+    b1, b2, c, off = synth.coo_genome([40, 30], rng, A=5.0, trans_density=0.0)
+    n = int(off[-1])
+    w, st = ice_ref.balance(b1, b2, c, n, off, min_nnz=10 ** 6)
+    assert np.isnan(w).all() and st["var"] == 0.0 and np.isnan(st["scale"]) and st["iters"] == 1

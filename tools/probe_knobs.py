@@ -22,13 +22,24 @@ ap.add_argument("settings", nargs="+")
 ap.add_argument("--build", default="")
 ap.add_argument("--nnz", type=float, default=5e9)
 ap.add_argument("--iters", type=int, default=10)
+ap.add_argument("--config", default="", help="a bench.py config (c2, c3, ...) instead of C4")
+ap.add_argument("--shard", default="", help="k/N: build only shard k of N (equal 512-row blocks)")
 a = ap.parse_args()
 _lib.load(); _lib.require_gpu()
-sizes = synth.genome_bins(10000, diploid=True)
-A, td = synth.calibrate(sizes, a.nnz, 0.2)
+if a.config:
+    from bench import config
+    sizes, kw = config(a.config)[:2]
+else:
+    sizes = synth.genome_bins(10000, diploid=True)
+    A, td = synth.calibrate(sizes, a.nnz, 0.2)
+    kw = dict(A=A, trans_density=td)
 tune(a.build)
 t0 = time.time()
-m = ice.ContactMatrix.synthetic(sizes, A=A, trans_density=td)
+if a.shard:
+    k, N = map(int, a.shard.split("/"))
+    nrb = (int(sum(sizes)) + 511) // 512
+    kw["row_range"] = (min(int(sum(sizes)), k * nrb // N * 512), min(int(sum(sizes)), (k + 1) * nrb // N * 512))
+m = ice.ContactMatrix.synthetic(sizes, **kw)
 inf = m.info()
 print(f"build {time.time()-t0:.1f}s band_w={inf['band_w']} band_w4={inf['band_w4']} units={inf['n_units']} "
       f"payload {inf['payload_bytes']/1e9:.2f} GB (flat {inf['payload_bytes_flat']/1e9:.2f} GB in "
@@ -36,9 +47,23 @@ print(f"build {time.time()-t0:.1f}s band_w={inf['band_w']} band_w4={inf['band_w4
       f"{(inf['band_w4'] - inf['band_w'] + 32) * (inf['band_w4'] > inf['band_w']) * (inf['row_hi'] - inf['row_lo']) / 1e9:.2f} GB) "
       f"tiles {inf['n_tiles']}", flush=True)
 st = ice.IceState(m, ice.IceOptions(tol=0.0, max_iters=10**6, mad_max=0, min_nnz=0))
+def run_shard(n):
+    """A shard cannot use hh_ice_run: one-rank sharded loop, wall time."""
+    import ctypes as C
+    import numpy as np
+    rr = np.array([0, int(sum(sizes))], np.int64)
+    _lib.call("hh_ice_run_sharded", st._h, 1, _lib.ptr(rr), None, None, int(n), None)
+
+
 for rep in range(2):
     for spec in a.settings:
         tune(spec)
+        if a.shard:
+            run_shard(2)
+            t0 = time.perf_counter()
+            run_shard(a.iters)
+            print(f"[{rep}] {spec}: shard iter {(time.perf_counter() - t0) * 1e3 / a.iters:.3f} ms (wall)", flush=True)
+            continue
         st.run(2)
         st.run(a.iters)
         ms, n, it_ms = st.last_timing()
