@@ -33,6 +33,12 @@ PCA_TOL = 1e-13   # max entry change of the unit Ritz vectors between iterations
 PCA_MAX_ITERS = 2000
 
 
+def py2_float_str(v):
+    """Python 2 ``str(float)``: '%.12g', with '.0' on integral values."""
+    t = "%.12g" % float(v)
+    return t + ".0" if t.lstrip("-").isdigit() else t
+
+
 class _Comp:
     """Owns an ``hh_comp*`` (one chromosome's matrix in HBM)."""
 
@@ -300,6 +306,77 @@ class StructureFind(TADCalling):
             out[NonGap] = self.Select_Allelic_PC(raw, Tranditional_PC)[NonGap]
         return out
 
+
+    # ------------------------------------------------- cooler-driven steps
+    def _chroms_and_matrices(self, balance_traditional):
+        """The per-chromosome dense matrices the reference fetches from its
+        cooler (StructureFind.py:499-513, :848-865): traditional data with
+        ``balance_traditional`` (NaN -> 0 when balanced), haplotype data raw,
+        chromosomes filtered by the Allelic prefix."""
+        from .coolio import Cooler
+        if not self.cooler_fil:
+            raise ValueError("no cooler file (StructureFind(cooler_fil=..., Res=...))")
+        with Cooler(self.cooler_fil) as c:
+            if self.Allelic is False:
+                chroms = list(c.chromnames)
+            elif self.Allelic in ("Maternal", "Paternal"):
+                chroms = [x for x in c.chromnames if x.startswith(self.Allelic[0])]
+            else:
+                raise ValueError(f"Unknown key word {self.Allelic}, only Maternal, Paternal, False allowed")
+            bal = balance_traditional and self.Allelic is False
+            out = {}
+            for chro in chroms:
+                M = c.matrix(balance=bal).fetch(chro)
+                out[chro] = np.nan_to_num(M) if bal else M
+        return chroms, out
+
+    @staticmethod
+    def Loading_Tranditional_PC(fil):
+        """``chrom value`` lines -> {chrom: PC array} (StructureFind.py:426-443)."""
+        d = {}
+        with open(fil) as f:
+            for line in f:
+                parts = line.split()
+                if parts:
+                    d.setdefault(parts[0], []).append(parts[-1])
+        return {k: np.array(v, dtype=float) for k, v in d.items()}
+
+    def Compartment(self, SA=False, Tranditional_PC_file=None, Matrix_Dict=None):
+        """Compartment() (StructureFind.py:491-554): raw matrices from the
+        cooler (or ``Matrix_Dict``), one selected PC per chromosome in
+        ``Compartment_Dict`` (zeros at gap bins); haplotype data also keep
+        the three raw PCs in ``RawPCA``."""
+        if Matrix_Dict is None:
+            chroms, Matrix_Dict = self._chroms_and_matrices(False)
+        else:
+            chroms = list(Matrix_Dict)
+        trad = self.Loading_Tranditional_PC(Tranditional_PC_file) if self.Allelic is not False else None
+        self.chroms, self.Matrix_Dict = chroms, Matrix_Dict
+        self.Compartment_Dict, self.RawPCA = {}, {}
+        for chro in chroms:
+            M = np.asarray(Matrix_Dict[chro], dtype=np.float64)
+            distance_bin, Gap, NonGap = self.Distance_Decay(M=M, G_array=None)
+            pca, Cor_M, OE_M = self.Get_PCA(distance_bin=distance_bin, M=M, NG_array=NonGap, SA=SA)
+            out = np.zeros(M.shape[0], dtype=float)
+            if self.Allelic is False:
+                out[NonGap] = self.Select_PC_new(Cor_M, OE_M[NonGap], pca)
+            else:
+                raw = np.zeros((len(pca), M.shape[0]))
+                raw[:, NonGap] = pca
+                self.RawPCA[chro] = raw
+                out[NonGap] = self.Select_Allelic_PC(raw, trad[chro[1:]])[NonGap]
+            self.Compartment_Dict[chro] = out
+        return self.Compartment_Dict
+
+    def OutPut_PC_To_txt(self, out):
+        """``chrom<TAB>value`` per bin (StructureFind.py:557-576; haplotype
+        chromosomes without their M/P prefix), values as Python 2's
+        ``str(float)`` prints them (12 significant digits)."""
+        with open(out, "w") as f:
+            for chro, pc in self.Compartment_Dict.items():
+                name = chro if self.Allelic is False else chro[1:]
+                for v in pc:
+                    f.write(f"{name}\t{py2_float_str(v)}\n")
 
     # --------------------------------------------------------------- TADs
     def TAD_parameter_init(self, minTAD, maxTAD, state_num, window, test_type):

@@ -1,0 +1,986 @@
+"""Minimal HDF5 reader / writer for cooler files.
+
+h5py / libhdf5 are absent from this image and from the GPU box, so the
+cooler drop-in (``coolio.py``: ``cooler balance`` as matrixBuilding.py:708
+invokes it, and the ``Cooler(...).matrix().fetch()`` reads of
+StructureFind.py:513 / :853 / :2006) reads and writes the HDF5 file format
+itself, restated from the published HDF5 File Format Specification 3.0.
+
+PARITY UNPINNED: there is no HDF5 file in /root/reference and no HDF5
+implementation here to check against; tests/test_h5.py checks round trips of
+this module's own writer, the reader on hand-assembled structures of the
+forms libhdf5 writes (chunked + shuffle + deflate datasets, v1 B-trees,
+variable-length string attributes in the global heap, enum types, v2 object
+headers with link messages), and the in-place append.
+
+Read support: superblock v0/v1/v2/v3; object headers v1 and v2 (with
+continuation blocks); old-style (symbol table) and compact new-style (link
+message) groups; contiguous / compact / chunked (v1 B-tree, layout v3; v4
+single-chunk) datasets with shuffle / deflate filters (fletcher32 checksums
+are stripped, not verified; v2 metadata checksums are not verified);
+fixed-point, floating-point, fixed and variable-length string, enum and
+bitfield types; attributes (v1-v3).
+
+Write support: a new file from an in-memory tree (superblock v0, v1 object
+headers, symbol-table groups, contiguous datasets) -- the layout libhdf5
+produces with its default "earliest" format bounds -- and, on an existing
+file, adding or replacing one dataset in a symbol-table group in place
+(``append_dataset``: what ``cooler balance --force`` does to ``bins/weight``).
+"""
+from __future__ import annotations
+
+import struct
+import zlib
+
+import numpy as np
+
+SIG = b"\x89HDF\r\n\x1a\n"
+UNDEF = 0xFFFFFFFFFFFFFFFF
+
+
+class H5Error(ValueError):
+    pass
+
+
+def _pad8(n):
+    return (n + 7) & ~7
+
+
+# ------------------------------------------------------------------ types
+class VlenStr:
+    """Marker for a variable-length string datatype (elements are global
+    heap references)."""
+
+    def __init__(self, charset):
+        self.charset = charset
+
+
+class H5Type:
+    """A parsed datatype: ``dtype`` (numpy) plus ``vlen_str`` / ``enum``."""
+
+    def __init__(self, dtype, vlen_str=None, enum=None, size=None):
+        self.dtype = dtype
+        self.vlen_str = vlen_str
+        self.enum = enum  # {name: value}
+        self.size = size if size is not None else (dtype.itemsize if dtype is not None else 16)
+
+
+def _parse_dtype(buf, p):
+    """Datatype message at buf[p:]; returns (H5Type, bytes consumed)."""
+    b0 = buf[p]
+    cls, ver = b0 & 0x0F, b0 >> 4
+    bits = buf[p + 1] | (buf[p + 2] << 8) | (buf[p + 3] << 16)
+    size = struct.unpack_from("<I", buf, p + 4)[0]
+    q = p + 8
+    order = ">" if bits & 1 else "<"
+    if cls == 0:  # fixed-point
+        signed = bool(bits & 0x08)
+        if size not in (1, 2, 4, 8):
+            raise H5Error(f"fixed-point size {size}")
+        dt = np.dtype(f"{order}{'i' if signed else 'u'}{size}")
+        return H5Type(dt), 8 + 4
+    if cls == 1:  # floating point
+        if size not in (2, 4, 8):
+            raise H5Error(f"float size {size}")
+        return H5Type(np.dtype(f"{order}f{size}")), 8 + 12
+    if cls == 3:  # fixed-length string
+        return H5Type(np.dtype(f"S{size}")), 8
+    if cls == 4:  # bitfield
+        return H5Type(np.dtype(f"{order}u{size}") if size in (1, 2, 4, 8) else np.dtype(f"V{size}")), 8 + 4
+    if cls == 5:  # opaque: tag follows, NUL-padded to 8
+        taglen = bits & 0xFF
+        return H5Type(np.dtype(f"V{size}")), 8 + taglen
+    if cls == 8:  # enum
+        nmem = bits & 0xFFFF
+        base, nb = _parse_dtype(buf, q)
+        q += nb
+        names = []
+        for _ in range(nmem):
+            e = bytes(buf).index(b"\0", q)
+            nm = bytes(buf[q:e]).decode()
+            names.append(nm)
+            # v1/v2: each name NUL-terminated and padded to a multiple of 8
+            q = q + _pad8(len(nm) + 1) if ver < 3 else e + 1
+        vals = np.frombuffer(bytes(buf[q:q + nmem * base.size]), dtype=base.dtype)
+        q += nmem * base.size
+        return H5Type(base.dtype, enum=dict(zip(names, vals.tolist())), size=base.size), q - p
+    if cls == 9:  # variable-length
+        vtype, charset = bits & 0x0F, (bits >> 8) & 0x0F
+        base, nb = _parse_dtype(buf, q)
+        if vtype == 1:
+            return H5Type(None, vlen_str=VlenStr(charset), size=16), 8 + nb
+        return H5Type(None, size=16), 8 + nb  # sequences: unsupported payloads
+    raise H5Error(f"datatype class {cls} not supported")
+
+
+def _parse_dataspace(buf, p):
+    ver, rank, flags = buf[p], buf[p + 1], buf[p + 2]
+    if ver == 1:
+        q = p + 8
+        kind = 1 if rank else 0
+    elif ver == 2:
+        kind = buf[p + 3]
+        q = p + 4
+    else:
+        raise H5Error(f"dataspace version {ver}")
+    dims = struct.unpack_from(f"<{rank}Q", buf, q) if rank else ()
+    if kind == 2:  # null dataspace
+        return None
+    return tuple(int(d) for d in dims)
+
+
+# ------------------------------------------------------------------ reader
+class _Msg:
+    __slots__ = ("type", "data", "addr")
+
+    def __init__(self, t, data, addr):
+        self.type, self.data, self.addr = t, data, addr
+
+
+class File:
+    """An HDF5 file opened read-only (``mode='r'``) or for in-place dataset
+    appends (``mode='r+'``)."""
+
+    def __init__(self, path, mode="r"):
+        if mode not in ("r", "r+"):
+            raise ValueError("mode must be 'r' or 'r+'")
+        self.path = path
+        self.mode = mode
+        self.f = open(path, "rb" if mode == "r" else "r+b")
+        self._gheap = {}
+        self._superblock()
+        self.root = Group(self, self.root_addr, "/")
+
+    # -- low level
+    def read(self, addr, n):
+        self.f.seek(self.base + addr)
+        b = self.f.read(n)
+        if len(b) != n:
+            raise H5Error(f"short read at {addr}")
+        return b
+
+    def _off(self, buf, p):
+        return struct.unpack_from("<Q" if self.so == 8 else "<I", buf, p)[0]
+
+    def _len(self, buf, p):
+        return struct.unpack_from("<Q" if self.sl == 8 else "<I", buf, p)[0]
+
+    def _superblock(self):
+        self.f.seek(0, 2)
+        size = self.f.tell()
+        at = 0
+        while True:
+            self.f.seek(at)
+            if self.f.read(8) == SIG:
+                break
+            at = 512 if at == 0 else at * 2
+            if at >= size:
+                raise H5Error("not an HDF5 file")
+        self.sb_at = at
+        self.f.seek(at)
+        hdr = self.f.read(256)
+        ver = hdr[8]
+        self.sb_version = ver
+        if ver in (0, 1):
+            self.so, self.sl = hdr[13], hdr[14]
+            self.leaf_k, self.int_k = struct.unpack_from("<HH", hdr, 16)
+            p = 24 + (4 if ver == 1 else 0)
+            self.base = self._off(hdr, p)
+            self.eof_pos = at + p + 2 * self.so
+            self.eof = self._off(hdr, p + 2 * self.so)
+            ent = p + 4 * self.so
+            self.root_addr = self._off(hdr, ent + self.so)
+        elif ver in (2, 3):
+            self.so, self.sl = hdr[9], hdr[10]
+            p = 12
+            self.base = self._off(hdr, p)
+            self.eof_pos = at + p + 2 * self.so
+            self.eof = self._off(hdr, p + 2 * self.so)
+            self.root_addr = self._off(hdr, p + 3 * self.so)
+            self.leaf_k, self.int_k = 4, 16
+        else:
+            raise H5Error(f"superblock version {ver}")
+        if self.so != 8 or self.sl != 8:
+            raise H5Error("only 8-byte offsets / lengths are supported")
+
+    def messages(self, addr):
+        """All header messages of the object header at ``addr``."""
+        head = self.read(addr, 16)
+        out = []
+        if head[:4] == b"OHDR":
+            flags = head[5]
+            p = 6 + (16 if flags & 0x20 else 0) + (4 if flags & 0x10 else 0)
+            w = 1 << (flags & 3)
+            pre = self.read(addr, p + w)
+            size0 = int.from_bytes(pre[p:p + w], "little")
+            blocks = [(addr + p + w, size0)]
+            tracked = bool(flags & 0x04)
+            while blocks:
+                a, n = blocks.pop(0)
+                buf = self.read(a, n)
+                q = 0
+                hdr = 4 + (2 if tracked else 0)
+                while q + hdr <= n:
+                    t, sz, fl = buf[q], struct.unpack_from("<H", buf, q + 1)[0], buf[q + 3]
+                    q += hdr
+                    if q + sz > n:
+                        break
+                    data = buf[q:q + sz]
+                    if t == 0x10:
+                        ca, cl = self._off(data, 0), self._len(data, 8)
+                        blocks.append((ca + 4, cl - 8))  # "OCHK" ... checksum
+                    elif t != 0:
+                        out.append(_Msg(t, data, a + q))
+                    q += sz
+            return out
+        ver = head[0]
+        if ver != 1:
+            raise H5Error(f"object header version {ver}")
+        nmsg = struct.unpack_from("<H", head, 2)[0]
+        size = struct.unpack_from("<I", head, 8)[0]
+        blocks = [(addr + 16, size)]
+        while blocks and len(out) < nmsg:
+            a, n = blocks.pop(0)
+            buf = self.read(a, n)
+            q = 0
+            while q + 8 <= n:
+                t, sz = struct.unpack_from("<HH", buf, q)
+                data = buf[q + 8:q + 8 + sz]
+                if t == 0x10:
+                    blocks.append((self._off(data, 0), self._len(data, 8)))
+                elif t != 0:
+                    out.append(_Msg(t, data, a + q + 8))
+                q += 8 + sz
+        return out
+
+    def gheap_object(self, coll, idx):
+        if coll not in self._gheap:
+            head = self.read(coll, 16)
+            if head[:4] != b"GCOL":
+                raise H5Error("bad global heap collection")
+            size = self._len(head, 8)
+            buf = self.read(coll, size)
+            objs = {}
+            q = 16
+            while q + 16 <= size:
+                i, _rc = struct.unpack_from("<HH", buf, q)
+                n = self._len(buf, q + 8)
+                if i == 0:
+                    break
+                objs[i] = bytes(buf[q + 16:q + 16 + n])
+                q += 16 + _pad8(n)
+            self._gheap[coll] = objs
+        return self._gheap[coll][idx]
+
+    def local_heap(self, addr):
+        h = self.read(addr, 32)
+        if h[:4] != b"HEAP":
+            raise H5Error("bad local heap")
+        size, free, data = self._len(h, 8), self._len(h, 16), self._off(h, 24)
+        return size, free, data
+
+    def close(self):
+        self.f.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __getitem__(self, path):
+        return self.root[path]
+
+    def __contains__(self, path):
+        try:
+            self.root[path]
+            return True
+        except KeyError:
+            return False
+
+
+def _decode_attr_values(fobj, typ, shape, raw):
+    n = int(np.prod(shape)) if shape else 1
+    if typ.vlen_str is not None:
+        vals = []
+        for k in range(n):
+            ln, coll, idx = struct.unpack_from("<IQI", raw, 16 * k)
+            vals.append(fobj.gheap_object(coll, idx)[:ln].decode("utf-8", "replace") if coll else "")
+        arr = np.array(vals, dtype=object)
+    else:
+        arr = np.frombuffer(bytes(raw[:n * typ.dtype.itemsize]), dtype=typ.dtype).copy()
+        if typ.enum is not None and set(typ.enum) == {"FALSE", "TRUE"}:
+            arr = arr.astype(bool)
+        elif arr.dtype.kind == "S":
+            arr = np.array([x.rstrip(b"\0").decode("utf-8", "replace") for x in arr], dtype=object)
+    if not shape:
+        v = arr[0]
+        return v.item() if hasattr(v, "item") else v
+    return arr.reshape(shape)
+
+
+def _parse_attribute(fobj, data):
+    ver = data[0]
+    if ver == 1:
+        nsz, dsz, ssz = struct.unpack_from("<HHH", data, 2)
+        p = 8
+        name = bytes(data[p:p + nsz]).split(b"\0")[0].decode()
+        p += _pad8(nsz)
+        typ, _ = _parse_dtype(data, p)
+        p += _pad8(dsz)
+        shape = _parse_dataspace(data, p)
+        p += _pad8(ssz)
+    elif ver in (2, 3):
+        if data[1] & 0x3:
+            raise H5Error("shared attribute datatype / dataspace not supported")
+        nsz, dsz, ssz = struct.unpack_from("<HHH", data, 2)
+        p = 8 + (1 if ver == 3 else 0)
+        name = bytes(data[p:p + nsz]).split(b"\0")[0].decode()
+        p += nsz
+        typ, _ = _parse_dtype(data, p)
+        p += dsz
+        shape = _parse_dataspace(data, p)
+        p += ssz
+    else:
+        raise H5Error(f"attribute version {ver}")
+    if shape is None:
+        return name, None
+    return name, _decode_attr_values(fobj, typ, shape, data[p:])
+
+
+class _Node:
+    def __init__(self, fobj, addr, name):
+        self.file = fobj
+        self.addr = addr
+        self.name = name
+        self._msgs = fobj.messages(addr)
+
+    @property
+    def attrs(self):
+        out = {}
+        for m in self._msgs:
+            if m.type == 0x0C:
+                k, v = _parse_attribute(self.file, m.data)
+                out[k] = v
+        return out
+
+
+class Group(_Node):
+    def _links(self):
+        f = self.file
+        links = {}
+        for m in self._msgs:
+            if m.type == 0x11:  # symbol table
+                bt, heap = f._off(m.data, 0), f._off(m.data, 8)
+                size, _, hdata = f.local_heap(heap)
+                seg = f.read(hdata, size)
+                for name_off, obj in _group_btree_entries(f, bt):
+                    links[_heap_name(seg, name_off)] = obj
+            elif m.type == 0x06:  # link message (compact new-style group)
+                d = m.data
+                flags = d[1]
+                p = 2
+                ltype = 0
+                if flags & 0x08:
+                    ltype = d[p]
+                    p += 1
+                if flags & 0x04:
+                    p += 8
+                if flags & 0x10:
+                    p += 1
+                w = 1 << (flags & 3)
+                nlen = int.from_bytes(d[p:p + w], "little")
+                p += w
+                name = bytes(d[p:p + nlen]).decode()
+                p += nlen
+                if ltype == 0:
+                    links[name] = f._off(d, p)
+            elif m.type == 0x02:  # link info: dense storage if a fractal heap address is set
+                d = m.data
+                p = 2 + (8 if d[1] & 1 else 0)
+                if f._off(d, p) != UNDEF:
+                    raise H5Error("dense link storage (fractal heap) not supported")
+        return links
+
+    def keys(self):
+        return list(self._links().keys())
+
+    def __contains__(self, name):
+        try:
+            self[name]
+            return True
+        except KeyError:
+            return False
+
+    def __getitem__(self, path):
+        parts = [p for p in path.split("/") if p]
+        node = self
+        for p in parts:
+            links = node._links()
+            if p not in links:
+                raise KeyError(path)
+            addr = links[p]
+            msgs = node.file.messages(addr)
+            types = {m.type for m in msgs}
+            full = (node.name.rstrip("/") + "/" + p)
+            node = Dataset(node.file, addr, full) if 0x08 in types else Group(node.file, addr, full)
+        return node
+
+
+def _heap_name(seg, off):
+    """NUL-terminated name at ``off`` of a local heap data segment."""
+    return bytes(seg[off:seg.index(b"\0", off)]).decode()
+
+
+def _group_btree_entries(f, addr):
+    """(name offset, object header address) of every SNOD entry under the
+    group B-tree at ``addr`` (depth first, key order)."""
+    head = f.read(addr, 24)
+    if head[:4] != b"TREE" or head[4] != 0:
+        raise H5Error("bad group B-tree node")
+    level, n = head[5], struct.unpack_from("<H", head, 6)[0]
+    body = f.read(addr + 24, (2 * n + 1) * 8)
+    out = []
+    for i in range(n):
+        child = f._off(body, 8 + 16 * i)
+        if level > 0:
+            out.extend(_group_btree_entries(f, child))
+        else:
+            sn = f.read(child, 8)
+            if sn[:4] != b"SNOD":
+                raise H5Error("bad symbol table node")
+            ns = struct.unpack_from("<H", sn, 6)[0]
+            ents = f.read(child + 8, 40 * ns)
+            for k in range(ns):
+                out.append((f._off(ents, 40 * k), f._off(ents, 40 * k + 8)))
+    return out
+
+
+class Dataset(_Node):
+    def __init__(self, fobj, addr, name):
+        super().__init__(fobj, addr, name)
+        self.filters = []
+        self.layout = None
+        for m in self._msgs:
+            if m.type == 0x01:
+                self.shape = _parse_dataspace(m.data, 0)
+            elif m.type == 0x03:
+                self.type, _ = _parse_dtype(m.data, 0)
+            elif m.type == 0x08:
+                self.layout = self._parse_layout(m.data)
+            elif m.type == 0x0B:
+                self.filters = _parse_filters(m.data)
+        if self.layout is None:
+            raise H5Error("dataset without a layout message")
+        self.dtype = self.type.dtype
+
+    def _parse_layout(self, d):
+        f = self.file
+        ver = d[0]
+        if ver == 3:
+            cls = d[1]
+            if cls == 0:
+                n = struct.unpack_from("<H", d, 2)[0]
+                return ("compact", bytes(d[4:4 + n]))
+            if cls == 1:
+                return ("contiguous", f._off(d, 2), f._len(d, 10))
+            if cls == 2:
+                r = d[2]
+                bt = f._off(d, 3)
+                dims = struct.unpack_from(f"<{r}I", d, 11)
+                return ("chunked", bt, dims)
+        elif ver in (1, 2):
+            r, cls = d[1], d[2]
+            p = 8
+            addr = None
+            if cls != 0:
+                addr = f._off(d, p)
+                p += 8
+            dims = struct.unpack_from(f"<{r}I", d, p)
+            p += 4 * r
+            if cls == 0:
+                n = struct.unpack_from("<I", d, p)[0]
+                return ("compact", bytes(d[p + 4:p + 4 + n]))
+            if cls == 1:
+                return ("contiguous", addr, None)
+            return ("chunked", addr, dims)
+        elif ver == 4:
+            cls = d[1]
+            if cls == 0:
+                n = struct.unpack_from("<H", d, 2)[0]
+                return ("compact", bytes(d[4:4 + n]))
+            if cls == 1:
+                return ("contiguous", f._off(d, 2), f._len(d, 10))
+            if cls == 2:
+                flags, r, w = d[2], d[3], d[4]
+                dims = [int.from_bytes(d[5 + w * k:5 + w * (k + 1)], "little") for k in range(r)]
+                p = 5 + w * r
+                itype = d[p]
+                p += 1
+                if itype == 1:  # single chunk
+                    if flags & 0x02:
+                        fsize = f._len(d, p)
+                        mask = struct.unpack_from("<I", d, p + 8)[0]
+                        return ("single", f._off(d, p + 12), dims, fsize, mask)
+                    return ("single", f._off(d, p), dims, None, 0)
+                raise H5Error(f"chunk index type {itype} not supported")
+        raise H5Error(f"layout version {ver} not supported")
+
+    @property
+    def size(self):
+        return int(np.prod(self.shape)) if self.shape else 1
+
+    def _elem(self):
+        return self.type.size
+
+    def _decode(self, raw, n):
+        if self.type.vlen_str is not None:
+            out = []
+            for k in range(n):
+                ln, coll, idx = struct.unpack_from("<IQI", raw, 16 * k)
+                out.append(self.file.gheap_object(coll, idx)[:ln].decode("utf-8", "replace") if coll else "")
+            return np.array(out, dtype=object)
+        return np.frombuffer(raw, dtype=self.dtype, count=n)
+
+    def _unfilter(self, raw, mask):
+        for k in range(len(self.filters) - 1, -1, -1):
+            fid, cv = self.filters[k]
+            if mask & (1 << k):
+                continue
+            if fid == 1:
+                raw = zlib.decompress(raw)
+            elif fid == 2:
+                s = cv[0] if cv else self._elem()
+                n = len(raw) // s
+                a = np.frombuffer(raw[:n * s], dtype=np.uint8).reshape(s, n)
+                raw = a.T.tobytes() + raw[n * s:]
+            elif fid == 3:  # fletcher32: the trailing checksum is dropped, not verified
+                raw = raw[:-4]
+            else:
+                raise H5Error(f"filter {fid} not supported")
+        return raw
+
+    def read(self, start=None, stop=None):
+        """Elements [start, stop) of a 1-D dataset (the whole dataset by
+        default; any rank when no range is given)."""
+        shape = self.shape or ()
+        n = self.size
+        one_d = len(shape) == 1
+        if (start is not None or stop is not None) and not one_d:
+            raise ValueError("ranges only for 1-D datasets")
+        lo = 0 if start is None else max(0, int(start))
+        hi = n if stop is None else min(n, int(stop))
+        if hi <= lo:
+            return self._decode(b"", 0) if self.type.vlen_str is None else np.array([], dtype=object)
+        es = self._elem()
+        lay = self.layout
+        if lay[0] == "compact":
+            raw = lay[1][lo * es:hi * es]
+        elif lay[0] == "contiguous":
+            addr = lay[1]
+            raw = b"\0" * ((hi - lo) * es) if addr == UNDEF else self.file.read(addr + lo * es, (hi - lo) * es)
+        elif lay[0] == "single":
+            _, addr, dims, fsize, mask = lay
+            nbytes = fsize if fsize is not None else int(np.prod(dims)) * es
+            raw = self._unfilter(self.file.read(addr, nbytes), mask)[lo * es:hi * es]
+        else:
+            raw = self._read_chunked(lo, hi, shape)
+        out = self._decode(raw, hi - lo)
+        if one_d or not shape:
+            return out if shape else out.reshape(())
+        return out.reshape(shape)
+
+    def _read_chunked(self, lo, hi, shape):
+        _, bt, dims = self.layout
+        es = self._elem()
+        rank = len(shape)
+        cdims = dims[:rank]
+        if rank == 1:
+            out = bytearray((hi - lo) * es)
+            c = cdims[0]
+            for off, size, mask, addr in _chunk_entries(self.file, bt, rank + 1):
+                s0 = off[0]
+                if s0 + c <= lo or s0 >= hi or addr == UNDEF:
+                    continue
+                raw = self._unfilter(self.file.read(addr, size), mask)
+                a, b = max(lo, s0), min(hi, s0 + c, shape[0])
+                out[(a - lo) * es:(b - lo) * es] = raw[(a - s0) * es:(b - s0) * es]
+            return bytes(out)
+        full = np.zeros(shape, dtype=np.dtype(f"V{es}"))
+        for off, size, mask, addr in _chunk_entries(self.file, bt, rank + 1):
+            if addr == UNDEF:
+                continue
+            raw = self._unfilter(self.file.read(addr, size), mask)
+            blk = np.frombuffer(raw[:int(np.prod(cdims)) * es], dtype=full.dtype).reshape(cdims)
+            sl = tuple(slice(o, min(o + c, s)) for o, c, s in zip(off, cdims, shape))
+            full[sl] = blk[tuple(slice(0, x.stop - x.start) for x in sl)]
+        return full.tobytes()
+
+
+def _parse_filters(d):
+    ver, n = d[0], d[1]
+    out = []
+    p = 8 if ver == 1 else 2
+    for _ in range(n):
+        fid = struct.unpack_from("<H", d, p)[0]
+        p += 2
+        nlen = 0
+        if ver == 1 or fid >= 256:
+            nlen = struct.unpack_from("<H", d, p)[0]
+            p += 2
+        _flags, ncv = struct.unpack_from("<HH", d, p)
+        p += 4
+        p += _pad8(nlen) if ver == 1 else nlen
+        cv = list(struct.unpack_from(f"<{ncv}I", d, p))
+        p += 4 * ncv
+        if ver == 1 and ncv % 2:
+            p += 4
+        out.append((fid, cv))
+    return out
+
+
+def _chunk_entries(f, addr, ndims):
+    """(chunk offsets, stored size, filter mask, address) of every chunk under
+    the v1 chunk B-tree at ``addr``."""
+    head = f.read(addr, 24)
+    if head[:4] != b"TREE" or head[4] != 1:
+        raise H5Error("bad chunk B-tree node")
+    level, n = head[5], struct.unpack_from("<H", head, 6)[0]
+    ks = 8 + 8 * ndims
+    body = f.read(addr + 24, n * (ks + 8) + ks)
+    out = []
+    for i in range(n):
+        k = i * (ks + 8)
+        size, mask = struct.unpack_from("<II", body, k)
+        off = struct.unpack_from(f"<{ndims}Q", body, k + 8)
+        child = f._off(body, k + ks)
+        if level > 0:
+            out.extend(_chunk_entries(f, child, ndims))
+        else:
+            out.append((off[:-1], size, mask, child))
+    return out
+
+
+def open_file(path, mode="r"):
+    return File(path, mode)
+
+
+# ------------------------------------------------------------------ writer
+def _dt_fixed(dt):
+    dt = np.dtype(dt)
+    b0 = (0x08 if dt.kind == "i" else 0) | (1 if dt.byteorder == ">" else 0)
+    return bytes([0x10, b0, 0, 0]) + struct.pack("<IHH", dt.itemsize, 0, 8 * dt.itemsize)
+
+
+def _dt_float(dt):
+    dt = np.dtype(dt)
+    if dt.itemsize == 8:
+        return bytes([0x11, 0x20, 63, 0]) + struct.pack("<IHHBBBBI", 8, 0, 64, 52, 11, 0, 52, 1023)
+    if dt.itemsize == 4:
+        return bytes([0x11, 0x20, 31, 0]) + struct.pack("<IHHBBBBI", 4, 0, 32, 23, 8, 0, 23, 127)
+    raise H5Error("float width")
+
+
+def _dt_string(n):
+    return bytes([0x13, 0x01, 0, 0]) + struct.pack("<I", n)  # NUL-padded ASCII (numpy 'S')
+
+
+def _dt_enum(base, members):
+    """Enum over an integer base type; members = [(name, value)]."""
+    body = _dt_fixed(base)
+    for name, _ in members:
+        nb = name.encode() + b"\0"
+        body += nb + b"\0" * (_pad8(len(nb)) - len(nb))
+    body += np.asarray([v for _, v in members], dtype=base).tobytes()
+    n = len(members)
+    return bytes([0x18, n & 0xFF, (n >> 8) & 0xFF, 0]) + struct.pack("<I", np.dtype(base).itemsize) + body
+
+
+BOOL_ENUM = [("FALSE", 0), ("TRUE", 1)]  # h5py's encoding of numpy bool
+
+
+def _encode_values(value):
+    """(datatype message bytes, dims or None for scalar, raw data) for an
+    attribute / dataset value."""
+    if isinstance(value, (bool, np.bool_)) or (isinstance(value, np.ndarray) and value.dtype == bool):
+        arr = np.asarray(value, dtype=np.int8)
+        return _dt_enum(np.int8, BOOL_ENUM), (arr.shape or None), arr.tobytes()
+    if isinstance(value, str):
+        b = value.encode()
+        n = max(len(b), 1)
+        return _dt_string(n), None, b.ljust(n, b"\0")
+    if isinstance(value, bytes):
+        n = max(len(value), 1)
+        return _dt_string(n), None, value.ljust(n, b"\0")
+    if isinstance(value, (list, tuple)) and value and all(isinstance(x, str) for x in value):
+        value = np.array([x.encode() for x in value])
+    arr = np.asarray(value)
+    if arr.dtype.kind == "U":
+        arr = np.char.encode(arr, "utf-8")
+    if arr.dtype.kind == "S":
+        n = max(arr.dtype.itemsize, 1)
+        arr = arr.astype(f"S{n}")
+        return _dt_string(n), (arr.shape or None), arr.tobytes()
+    if arr.dtype.kind in "iu":
+        arr = arr.astype(arr.dtype.newbyteorder("<"))
+        return _dt_fixed(arr.dtype), (arr.shape or None), arr.tobytes()
+    if arr.dtype.kind == "f":
+        arr = arr.astype("<f8" if arr.dtype.itemsize == 8 else "<f4")
+        return _dt_float(arr.dtype), (arr.shape or None), arr.tobytes()
+    raise H5Error(f"cannot store value of dtype {arr.dtype}")
+
+
+def _dataspace(dims):
+    if dims is None:
+        return bytes([1, 0, 0, 0]) + b"\0" * 4
+    r = len(dims)
+    return bytes([1, r, 1, 0]) + b"\0" * 4 + struct.pack(f"<{r}Q", *dims) + struct.pack(f"<{r}Q", *dims)
+
+
+def _msg(t, data):
+    data = data + b"\0" * (_pad8(len(data)) - len(data))
+    return struct.pack("<HHB3x", t, len(data), 0) + data
+
+
+def _attr_msg(name, value):
+    dt, dims, raw = _encode_values(value)
+    nb = name.encode() + b"\0"
+    ds = _dataspace(dims)
+    body = struct.pack("<BBHHH", 1, 0, len(nb), len(dt), len(ds))
+    body += nb + b"\0" * (_pad8(len(nb)) - len(nb))
+    body += dt + b"\0" * (_pad8(len(dt)) - len(dt))
+    body += ds + b"\0" * (_pad8(len(ds)) - len(ds))
+    return _msg(0x0C, body + raw)
+
+
+def _object_header(msgs):
+    body = b"".join(msgs)
+    if len(body) < 24:  # room for a later message; libhdf5 never writes smaller headers
+        body += struct.pack("<HHB3x", 0, 24 - len(body) - 8, 0) + b"\0" * (24 - len(body) - 8)
+        nmsg = len(msgs) + 1
+    else:
+        nmsg = len(msgs)
+    return struct.pack("<BBHII", 1, 0, nmsg, 1, len(body)) + b"\0" * 4 + body
+
+
+def _dataset_header(arr, attrs, data_addr, enum=None):
+    dt, dims, raw = _encode_values(arr)
+    if enum is not None:  # integer data stored with an enum type (cooler's bins/chrom)
+        dt = _dt_enum(np.asarray(arr).dtype, enum)
+    if dims is None:
+        dims = (1,) if np.ndim(arr) == 0 else np.shape(arr)
+    msgs = [_msg(0x01, _dataspace(tuple(np.shape(arr)) or None)), _msg(0x03, dt),
+            _msg(0x05, bytes([2, 2, 0, 0])),
+            _msg(0x08, bytes([3, 1]) + struct.pack("<QQ", data_addr if raw else UNDEF, len(raw)))]
+    for k, v in (attrs or {}).items():
+        msgs.append(_attr_msg(k, v))
+    return _object_header(msgs), raw
+
+
+class _W:
+    """Sequential file image under construction."""
+
+    def __init__(self):
+        self.parts = []
+        self.pos = 0
+
+    def alloc(self, n):
+        a = self.pos
+        self.pos += _pad8(n)
+        return a
+
+    def put(self, addr, data):
+        self.parts.append((addr, data))
+
+
+def _heap_block(names, spare=256):
+    """Local heap data segment: "" at offset 0, then the names; a free block
+    of ``spare`` bytes at the end (room for in-place additions)."""
+    data = b"\0" * 8
+    offs = {}
+    for nm in names:
+        offs[nm] = len(data)
+        nb = nm.encode() + b"\0"
+        data += nb + b"\0" * (_pad8(len(nb)) - len(nb))
+    free_at = len(data)
+    data += struct.pack("<QQ", 1, spare) + b"\0" * (spare - 16)  # next free = 1 (none), size
+    return data, offs, free_at
+
+
+def write_file(path, tree):
+    """Write a new HDF5 file.  ``tree`` is a nested dict: a dict value is a
+    group, a numpy array (or scalar / string list) a dataset; the special key
+    ``"@attrs"`` holds a node's attributes (``{"@attrs": {...}, "@data": arr}``
+    gives a dataset with attributes; ``"@enum": [(name, value)]`` stores
+    integer data with that enum type)."""
+    W = _W()
+    W.alloc(96)  # superblock v0 + root symbol table entry
+
+    def build_group(node):
+        attrs = node.get("@attrs", {})
+        names = sorted(k for k in node if not k.startswith("@"))
+        if len(names) > 8 * 32:
+            raise H5Error("more than 256 links in one group")
+        children = {}
+        for nm in names:
+            v = node[nm]
+            if isinstance(v, dict) and "@data" not in v:
+                children[nm] = build_group(v)
+            else:
+                data, a = (v["@data"], v.get("@attrs", {})) if isinstance(v, dict) else (v, {})
+                en = v.get("@enum") if isinstance(v, dict) else None
+                data = np.asarray(data) if not isinstance(data, str) else data
+                hdr, raw = _dataset_header(data, a, 0, en)
+                ha = W.alloc(len(hdr))
+                da = W.alloc(len(raw)) if raw else UNDEF
+                hdr, raw = _dataset_header(data, a, da, en)
+                W.put(ha, hdr)
+                if raw:
+                    W.put(da, raw)
+                children[nm] = ha
+        heap, offs, free_at = _heap_block(names)
+        heap_hdr = W.alloc(32)
+        heap_data = W.alloc(len(heap))
+        W.put(heap_hdr, b"HEAP" + bytes([0, 0, 0, 0]) + struct.pack("<QQQ", len(heap), free_at, heap_data))
+        W.put(heap_data, heap)
+        # symbol table nodes of up to 8 entries, one level of B-tree (<= 32 of them)
+        chunks = [names[i:i + 8] for i in range(0, len(names), 8)] or [[]]
+        snods = []
+        for ch in chunks:
+            a = W.alloc(8 + 40 * 8)
+            body = b"SNOD" + bytes([1, 0]) + struct.pack("<H", len(ch))
+            for nm in ch:
+                body += struct.pack("<QQII16x", offs[nm], children[nm], 0, 0)
+            body += b"\0" * (8 + 40 * 8 - len(body))
+            W.put(a, body)
+            snods.append((a, ch))
+        bt = W.alloc(24 + 33 * 8 + 32 * 8)
+        body = b"TREE" + bytes([0, 0]) + struct.pack("<HQQ", len(snods), UNDEF, UNDEF)
+        body += struct.pack("<Q", 0)
+        for a, ch in snods:
+            body += struct.pack("<QQ", a, offs[ch[-1]] if ch else 0)
+        body += b"\0" * (24 + 33 * 8 + 32 * 8 - len(body))
+        W.put(bt, body)
+        msgs = [_msg(0x11, struct.pack("<QQ", bt, heap_hdr))] + [_attr_msg(k, v) for k, v in attrs.items()]
+        hdr = _object_header(msgs)
+        ga = W.alloc(len(hdr))
+        W.put(ga, hdr)
+        return ga
+
+    root = build_group(tree)
+    eof = W.pos
+    sb = SIG + bytes([0, 0, 0, 0, 0, 8, 8, 0]) + struct.pack("<HHI", 4, 16, 0)
+    sb += struct.pack("<QQQQ", 0, UNDEF, eof, UNDEF)
+    sb += struct.pack("<QQII16x", 0, root, 0, 0)
+    W.put(0, sb)
+    with open(path, "wb") as f:
+        f.truncate(eof)
+        for a, d in W.parts:
+            f.seek(a)
+            f.write(d)
+
+
+# -------------------------------------------------- in-place dataset append
+def append_dataset(path, group, name, data, attrs=None):
+    """Add (or replace) dataset ``group/name`` in an existing file, in place:
+    the new object header and data go to the end of the file; the group's
+    symbol table gets the link (name added to its local heap, which moves to
+    the end of the file when its free space is too small).  A replaced
+    dataset's old storage is left unreferenced, as libhdf5 does."""
+    F = File(path, "r+")
+    try:
+        if F.sb_version > 1:
+            raise H5Error("in-place append supports version 0/1 superblocks (no checksum update)")
+        g = F[group] if group not in ("", "/") else F.root
+        st = [m for m in g._msgs if m.type == 0x11]
+        if not st:
+            raise H5Error("in-place append needs an old-style (symbol table) group")
+        bt, heap = F._off(st[0].data, 0), F._off(st[0].data, 8)
+        end = _pad8(F.eof)
+
+        def put(addr, b):
+            F.f.seek(F.base + addr)
+            F.f.write(b)
+
+        arr = np.asarray(data) if not isinstance(data, str) else data
+        hdr, raw = _dataset_header(arr, attrs, 0)
+        ha = end
+        da = _pad8(ha + len(hdr))
+        hdr, raw = _dataset_header(arr, attrs, da if raw else UNDEF)
+        put(ha, hdr)
+        if raw:
+            put(da, raw)
+        end = _pad8(da + len(raw)) if raw else _pad8(ha + len(hdr))
+
+        head = F.read(bt, 24)
+        if head[:4] != b"TREE" or head[5] != 0:
+            raise H5Error("in-place append supports one-level group B-trees")
+        n = struct.unpack_from("<H", head, 6)[0]
+        body = bytearray(F.read(bt + 24, (2 * n + 1) * 8))
+        size, free, hdata = F.local_heap(heap)
+        seg = bytearray(F.read(hdata, size))
+        # existing link: repoint it
+        for i in range(n):
+            sn = F._off(body, 8 + 16 * i)
+            ns = struct.unpack_from("<H", F.read(sn, 8), 6)[0]
+            ents = F.read(sn + 8, 40 * ns)
+            for k in range(ns):
+                if _heap_name(seg, F._off(ents, 40 * k)) == name:
+                    put(sn + 8 + 40 * k + 8, struct.pack("<Q", ha))
+                    put(F.eof_pos, struct.pack("<Q", end))
+                    return
+        # new name -> local heap
+        nb = name.encode() + b"\0"
+        need = _pad8(len(nb))
+        off = None
+        prev, cur = None, free
+        while cur not in (1, UNDEF) and cur < size:
+            nxt, bsz = struct.unpack_from("<QQ", seg, cur)
+            if bsz >= need and (bsz == need or bsz - need >= 16):
+                off = cur
+                rest = cur + need
+                if bsz > need:
+                    struct.pack_into("<QQ", seg, rest, nxt, bsz - need)
+                    link = rest
+                else:
+                    link = nxt
+                if prev is None:
+                    free = link
+                else:
+                    struct.pack_into("<Q", seg, prev, link)
+                break
+            prev, cur = cur, nxt
+        if off is None:  # grow: move the data segment to the end of the file
+            off = size
+            seg += nb + b"\0" * (need - len(nb))
+            spare = 256
+            fb = len(seg)
+            seg += struct.pack("<QQ", free if free not in (UNDEF,) else 1, spare) + b"\0" * (spare - 16)
+            free = fb
+            size = len(seg)
+            hdata = end
+            end = _pad8(hdata + size)
+        seg[off:off + need] = nb + b"\0" * (need - len(nb))
+        put(hdata, bytes(seg))
+        put(heap + 8, struct.pack("<QQQ", size, free, hdata))
+        # symbol table node: the child whose key range holds the name
+        names_at = lambda o: _heap_name(seg, o)
+        ci = n - 1
+        for i in range(n):
+            if name <= names_at(F._off(body, 16 * (i + 1))):
+                ci = i
+                break
+        sn = F._off(body, 8 + 16 * ci)
+        snh = F.read(sn, 8)
+        ns = struct.unpack_from("<H", snh, 6)[0]
+        if ns >= 2 * F.leaf_k:
+            raise H5Error("symbol table node full (in-place append does not split nodes)")
+        ents = [F.read(sn + 8 + 40 * k, 40) for k in range(ns)]
+        pos = sum(1 for e in ents if names_at(F._off(e, 0)) < name)
+        ents.insert(pos, struct.pack("<QQII16x", off, ha, 0, 0))
+        put(sn, snh[:6] + struct.pack("<H", ns + 1) + b"".join(ents))
+        if name > names_at(F._off(body, 16 * (ci + 1))):
+            put(bt + 24 + 16 * (ci + 1), struct.pack("<Q", off))
+        put(F.eof_pos, struct.pack("<Q", end))
+    finally:
+        F.close()

@@ -134,13 +134,16 @@ class TADCalling:
 
     # ------------------------------------------------------- preprocessing
     def Data_preprocess(self, Matrix_Dict=None):
-        """StructureFind.py:842-915 on in-memory matrices (the reference
-        fetches them from its cooler: balanced with NaN -> 0 for traditional
-        data, raw for haplotype data).  Sets Gap_all, DI_dict, DI_all_train."""
+        """StructureFind.py:842-915: the per-chromosome matrices from the
+        cooler (coolio: balanced with NaN -> 0 for traditional data, raw for
+        haplotype data) or given in memory.  Sets Gap_all, DI_dict,
+        DI_all_train."""
+        if Matrix_Dict is None and getattr(self, "cooler_fil", None):
+            _, Matrix_Dict = self._chroms_and_matrices(True)  # balanced, NaN -> 0 (:853-854)
         if Matrix_Dict is None:
             Matrix_Dict = getattr(self, "Matrix_Dict", None)
         if Matrix_Dict is None:
-            raise ValueError("Data_preprocess needs the per-chromosome matrices (cooler is not read here)")
+            raise ValueError("Data_preprocess needs a cooler file or the per-chromosome matrices")
         window_bin = int(self.window / self.Res)
         width = 7
         Gap_all, DI_dict, DI_all_train = {}, {}, {}
