@@ -1234,8 +1234,9 @@ static void sweep_band(hh_ice* S, hipStream_t s) {
     const bool abl = g_sweep_ablate == 1;  // timing ablation (stream only)
     auto launch = [&](const BandSegs& L, int nc) {
         const unsigned rb = (unsigned)((S->nloc + rows - 1) / rows);
-        auto kern = rows == 64 ? (abl ? k_sweep_bands<1, 64> : k_sweep_bands<0, 64>)
-                               : (abl ? k_sweep_bands<1, 256> : k_sweep_bands<0, 256>);
+        auto kern = rows == 64    ? (abl ? k_sweep_bands<1, 64> : k_sweep_bands<0, 64>)
+                    : rows == 128 ? (abl ? k_sweep_bands<1, 128> : k_sweep_bands<0, 128>)
+                                  : (abl ? k_sweep_bands<1, 256> : k_sweep_bands<0, 256>);
         hipLaunchKernelGGL(kern, dim3(rb, (unsigned)nc), dim3(kBandThreads), 0, s, L, (long long)S->nloc,
                            (long long)m->row_lo, (long long)m->n_bins, S->act(), m->row_group.p, S->bias.p,
                            S->bpart.p);
@@ -1355,6 +1356,9 @@ int hh_tune(const char* key, int64_t value) {
         } else if (k == "unit_entries") {
             HH_REQUIRE(value == 0 || (value >= 4096 && value <= (1 << 24)), "unit_entries must be 0 (auto) or in [4096, 2^24]");
             g_unit_entries = value;
+        } else if (k == "tile_cost") {
+            HH_REQUIRE(value >= 0 && value <= (1 << 20), "tile_cost in [0, 2^20] payload words");
+            g_tile_cost = value;
         } else if (k == "parse_ablate") {
             HH_REQUIRE(value >= 0 && value <= 3, "parse_ablate in [0, 3]");
             g_parse_ablate = (int)value;
@@ -1380,7 +1384,8 @@ int hh_tune(const char* key, int64_t value) {
             HH_REQUIRE(value >= 2 && value <= 8, "pca_p in [2, 8]");
             g_pca_p = (int)value;
         } else if (k == "band_rows") {
-            HH_REQUIRE(value == 0 || value == 64 || value == 256, "band_rows in {0 (auto), 64, 256}");
+            HH_REQUIRE(value == 0 || value == 64 || value == 128 || value == 256,
+                       "band_rows in {0 (auto), 64, 128, 256}");
             g_band_rows = (int)value;
         } else if (k == "sweep_single") {
             HH_REQUIRE(value >= -1 && value <= 1, "sweep_single in {-1 (auto), 0, 1}");

@@ -11,6 +11,7 @@ namespace hh {
 
 static thread_local std::string g_last_error;
 int64_t g_unit_entries = 0;  // 0 = auto (plan_tiles)
+int64_t g_tile_cost = 32768; // payload-word equivalent of one tile's fixed cost in the unit split (C4 shard 8/8: 0.79 -> 0.65 ms/iter)
 int64_t g_band_w = -1;       // -1 = auto (choose_band_w)
 int64_t g_flat_max = 64;     // longest row (uint4) of a flat tile segment; 0 = no flat segments
 int64_t g_host_build = 0;    // hh_tune("host_build"): 1 = host builder for every pixel table
@@ -198,7 +199,9 @@ TilePlan plan_tiles(const uint16_t* cntw, const uint16_t* cntn, int64_t nloc, in
         int32_t cur = ta;
         int64_t cur_sz = 0;
         for (int32_t t = ta; t < tb; ++t) {
-            const int64_t sz = tile_words(t, 0, kR);
+            // a tile's fixed cost (staging, the per-tile latency chain) counts
+            // toward the unit's size: runs of tiny trans tiles stay short
+            const int64_t sz = tile_words(t, 0, kR) + g_tile_cost;
             if (sz > unit_cap) {
                 if (cur < t) emit(rb, cur, t, 0, nr);
                 int32_t rlo = 0;
