@@ -964,6 +964,9 @@ def main():
             "data": "synthetic (SURVEY.md §8(d) model generated in HBM; no real Hi-C data offline)",
             "nnz_iters_per_s": nnz_total * its,
             "config": {"workload": label, "n_bins": n, "nnz_upper": nnz_total,
+                       **({"config_note": "trans fraction 0.85, not SURVEY 8(d)'s ~0.2: hg19 at 40 kb has only "
+                                          "1.42e8 cis pixels, so BASELINE C3's 8e8 nnz needs ~85 % trans"}
+                          if args.config == "c3" else {}),
                        "trans_fraction_target": tf, "resolution_bp": 40000 if args.config in ("c1", "c3") else 10000,
                        "parallelism": f"rows sharded x{world} (measured-cost partition), {'RCCL' if backend == 'nccl' else backend} all-gather of marginals, loop in {'C++ (hh_ice_run_sharded)' if dist_impl == 'capi' else 'Python'}" if world > 1
                        else "single GPU", "generate_s": round(gen_s, 2),
