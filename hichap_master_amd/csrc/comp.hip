@@ -1135,9 +1135,10 @@ static bool pca_krylov(PcaWork& wk, const double* cor, long long n, int k, doubl
         hipLaunchKernelGGL(k_gram_ms, dim3((unsigned)(nb * BB)), dim3(64), 0, s, qpart.p, nap, out);
     };
     fail.zero(s);
-    // start block: [1 / sqrt(n) | deterministic pseudo-random columns]
+    // start block: [1 / sqrt(n) | deterministic pseudo-random columns]; the
+    // host source of the upload lives until the first cycle's synchronise
+    std::vector<double> v0((size_t)n * B);
     {
-        std::vector<double> v0((size_t)n * B);
         for (long long i = 0; i < n; ++i)
             for (int b = 0; b < B; ++b)
                 v0[i * B + b] = b == 0 ? 1.0 / std::sqrt((double)n) : (double)u01(mix64(0x5eedULL + i * B + b)) - 0.5;
@@ -1335,6 +1336,9 @@ static bool pca_krylov(PcaWork& wk, const double* cor, long long n, int k, doubl
             scholqr3(W.p, Q.p, restartR, fail.p + P * 8, 0);
         }
     }
+    // a budget-exhausted run leaves a restart block enqueued: drain the
+    // stream before this function's buffers go back to the pool
+    HIP_CHECK(hipStreamSynchronize(s));
     if (!done) st.converged = 0;
     st.products = products;
     st.cycles = cycles;

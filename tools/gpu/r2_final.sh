@@ -16,7 +16,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/k
 cp $(find /tmp/k2 -name "*kernel_stats.csv" | head -1) $O/r2_c2_kernel_stats.csv
 timeout -k 10 300 python3 -u bench.py --config c3 --steps 50 --warmup 5 > $O/r2_c3_bench.log 2>&1 || exit 1
 timeout -k 10 300 python3 -u bench.py --config c5 --steps 5 --warmup 1 > $O/r2_c5_bench.log 2>&1 || exit 1
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/k5 -o c5 -- python3 -u bench.py --config c5 --steps 3 --warmup 1 --no-cpu > $O/r2_c5_prof.log 2>&1 || exit 1
+HH_C5_STREAMS=1 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/k5 -o c5 -- python3 -u bench.py --config c5 --steps 3 --warmup 1 --no-cpu > $O/r2_c5_prof.log 2>&1 || exit 1
 cp $(find /tmp/k5 -name "*kernel_stats.csv" | head -1) $O/r2_c5_kernel_stats.csv
 timeout -k 10 300 python3 -u bench.py --config dropin --steps 3 --warmup 1 > $O/r2_dropin_bench.log 2>&1 || exit 1
 timeout -k 10 300 python3 -u bench.py --config e2e --steps 3 --warmup 1 > $O/r2_e2e_bench.log 2>&1 || exit 1
