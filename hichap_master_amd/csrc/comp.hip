@@ -700,17 +700,83 @@ __global__ void k_comb_mp(const double* __restrict__ base, const double* __restr
 // without another pass over the rows.  256 threads = 16 rows x 16 columns per
 // sub-step; LDS: the 64-row tile, Cm, Rinv.
 constexpr int kApplyRows = 64;
-__global__ __launch_bounds__(256) void k_apply(const double* __restrict__ in, const double* __restrict__ Q, int nb,
-                                               const double* __restrict__ Cm, const double* __restrict__ Rinv,
-                                               long long n, double* __restrict__ out, double* __restrict__ gpart,
-                                               double* __restrict__ qpart, int nblk) {
+// CHOL: Rinv is not an input but the inverse Cholesky factor of the Gram
+// matrix whose nin per-block partials are in gin (+ shift_scale * trace on
+// the diagonal): every block reduces the partials in the same fixed order and
+// factors the 16 x 16 matrix itself, so a separate one-block reduce + Cholesky
+// launch and its serialisation disappear from each CholeskyQR pass (block 0 writes
+// R and the breakdown flag for the host).  gin must not be gpart.
+// shift_scale > 0: shifted CholeskyQR (Fukaya et al.), shift = 11 (m n +
+// n (n + 1)) u ||X||^2 with the trace bounding ||X||^2.  Not positive
+// definite -> *fail = 1, R = R^{-1} = I.
+template <bool CHOL>
+__global__ __launch_bounds__(256) void k_apply_t(const double* __restrict__ in, const double* __restrict__ Q, int nb,
+                                                 const double* __restrict__ Cm, const double* __restrict__ Rinv,
+                                                 long long n, double* __restrict__ out, double* __restrict__ gpart,
+                                                 double* __restrict__ qpart, int nblk, const double* __restrict__ gin,
+                                                 int nin, double shift_scale, double* __restrict__ Rout,
+                                                 int* __restrict__ fail) {
     __shared__ double ts[kApplyRows][kSB + 1], os_[kApplyRows][kSB + 1];
     __shared__ double cm[8 * kSB * kSB], ri[kSB * kSB];
     const int t = threadIdx.x, rr = t / kSB, b = t % kSB;
     const long long r0 = (long long)blockIdx.x * kApplyRows;
     if (Cm)
         for (int e = t; e < nb * kSB * kSB; e += 256) cm[e] = Cm[e];
-    if (Rinv) ri[t] = Rinv[t];
+    if (CHOL) {
+        // ts / os_ double as scratch for the 16 x 16 algebra before the rows
+        // are staged: G in ts[0..15], R in os_[0..15], R^{-1} in ts[16..31]
+        double acc = 0.0;
+        int r = 0;
+        for (; r + 8 <= nin; r += 8) {
+            double v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = gin[(size_t)(r + u) * kSB * kSB + t];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) acc += v[u];
+        }
+        for (; r < nin; ++r) acc += gin[(size_t)r * kSB * kSB + t];
+        ts[rr][b] = acc;
+        os_[rr][b] = 0.0;
+        ts[16 + rr][b] = 0.0;
+        __syncthreads();
+        __shared__ double shift;
+        __shared__ int bad;
+        if (t == 0) {
+            double tr = 0.0;
+            for (int i = 0; i < kSB; ++i) tr += ts[i][i];
+            shift = shift_scale > 0 ? shift_scale * tr : 0.0;
+            bad = 0;
+        }
+        __syncthreads();
+        if (rr == b) ts[rr][rr] += shift;
+        __syncthreads();
+        for (int j = 0; j < kSB; ++j) {
+            const double d = ts[j][j];
+            const bool okd = d > 0;
+            const double rjj = okd ? sqrt(d) : 1.0;
+            if (t == 0 && !okd) bad = 1;
+            if (rr == j && b >= j) os_[j][b] = b == j ? rjj : ts[j][b] / rjj;
+            __syncthreads();
+            if (rr > j && b > j) ts[rr][b] -= os_[j][rr] * os_[j][b];
+            __syncthreads();
+        }
+        for (int i = kSB - 1; i >= 0; --i) {
+            if (rr == i) {
+                double v = i == b ? 1.0 : 0.0;
+                for (int k = i + 1; k < kSB; ++k) v -= os_[i][k] * ts[16 + k][b];
+                ts[16 + i][b] = v / os_[i][i];
+            }
+            __syncthreads();
+        }
+        ri[t] = bad ? (rr == b ? 1.0 : 0.0) : ts[16 + rr][b];
+        if (blockIdx.x == 0) {
+            Rout[t] = bad ? (rr == b ? 1.0 : 0.0) : os_[rr][b];
+            if (t == 0 && bad) *fail = 1;
+        }
+        __syncthreads();  // scratch reads done before the rows are staged
+    } else if (Rinv) {
+        ri[t] = Rinv[t];
+    }
     for (int e = t; e < kApplyRows * kSB; e += 256) {
         const long long i = r0 + e / kSB;
         ts[e / kSB][e % kSB] = i < n ? in[i * kSB + e % kSB] : 0.0;
@@ -742,7 +808,7 @@ __global__ __launch_bounds__(256) void k_apply(const double* __restrict__ in, co
     for (int q = 0; q < kApplyRows / 16; ++q) {
         const int r = rr + 16 * q;
         double v = ts[r][b];
-        if (Rinv) {
+        if (CHOL || Rinv) {
             v = 0.0;
 #pragma unroll
             for (int a = 0; a < kSB; ++a) v = fma(ts[r][a], ri[a * kSB + b], v);
@@ -774,84 +840,6 @@ __global__ __launch_bounds__(256) void k_apply(const double* __restrict__ in, co
             qpart[((size_t)k * nblk + blockIdx.x) * kSB * kSB + t] = acc;
         }
     }
-}
-
-// G = sum of nblk Gram partials (fixed order), then Cholesky G (+ shift I) =
-// R^T R and R^{-1}, all in LDS (the 16 dependent steps never touch global
-// memory).  shift_scale > 0: shift = shift_scale * trace(G) (shifted
-// CholeskyQR, Fukaya et al.: 11 (m n + n (n + 1)) u ||X||^2, the trace
-// bounding ||X||^2).  Not positive definite -> *fail = 1, R = Rinv = I.
-__global__ __launch_bounds__(1024) void k_reduce_chol(const double* __restrict__ gpart, int nblk, double shift_scale,
-                                                      double* __restrict__ Rout, double* __restrict__ Rinv,
-                                                      int* __restrict__ fail) {
-    __shared__ double G[kSB][kSB + 1], R[kSB][kSB + 1], X[kSB][kSB + 1], P4[4][kSB * kSB];
-    __shared__ double shift;
-    __shared__ int bad;
-    const int tt = threadIdx.x, t = tt & 255, part = tt >> 8, a = t / kSB, b = t % kSB;
-    // four fixed quarters of the partials, each summed in order with 8
-    // independent loads in flight, then combined in quarter order
-    {
-        const int q0 = (int)((long long)nblk * part / 4), q1 = (int)((long long)nblk * (part + 1) / 4);
-        double acc = 0.0;
-        int r = q0;
-        for (; r + 8 <= q1; r += 8) {
-            double v[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) v[u] = gpart[(size_t)(r + u) * kSB * kSB + t];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) acc += v[u];
-        }
-        for (; r < q1; ++r) acc += gpart[(size_t)r * kSB * kSB + t];
-        P4[part][t] = acc;
-    }
-    __syncthreads();
-    const bool w = tt < 256;  // the 16 x 16 algebra: threads 0..255; all reach every barrier
-    if (w) {
-        G[a][b] = ((P4[0][t] + P4[1][t]) + P4[2][t]) + P4[3][t];
-        R[a][b] = 0.0;
-    }
-    __syncthreads();
-    if (tt == 0) {
-        bad = 0;
-        double tr = 0.0;
-        for (int i = 0; i < kSB; ++i) tr += G[i][i];
-        shift = shift_scale > 0 ? shift_scale * tr : 0.0;
-    }
-    __syncthreads();
-    if (w && a == b) G[a][a] += shift;
-    __syncthreads();
-    // right-looking: step j: R[j][j] = sqrt(G[j][j]); R[j][c] = G[j][c] / R[j][j];
-    // G[p][q] -= R[j][p] R[j][q] for p, q > j
-    for (int j = 0; j < kSB; ++j) {
-        const double d = G[j][j];
-        const bool okd = d > 0;
-        const double rjj = okd ? sqrt(d) : 1.0;
-        if (tt == 0 && !okd) bad = 1;
-        if (w && a == j && b >= j) R[j][b] = b == j ? rjj : G[j][b] / rjj;
-        __syncthreads();
-        if (w && a > j && b > j) G[a][b] -= R[j][a] * R[j][b];
-        __syncthreads();
-    }
-    // R^{-1} by back substitution, column b per thread group (16 x 16 threads)
-    if (w) X[a][b] = 0.0;
-    __syncthreads();
-    for (int i = kSB - 1; i >= 0; --i) {
-        if (w && a == i) {
-            double s = i == b ? 1.0 : 0.0;
-            for (int k = i + 1; k < kSB; ++k) s -= R[i][k] * X[k][b];
-            X[i][b] = s / R[i][i];
-        }
-        __syncthreads();
-    }
-    if (!w) return;
-    if (bad) {
-        if (t == 0) *fail = 1;
-        Rinv[t] = a == b ? 1.0 : 0.0;
-        Rout[t] = a == b ? 1.0 : 0.0;
-        return;
-    }
-    Rinv[t] = X[a][b];
-    Rout[t] = R[a][b];
 }
 
 // start block [1/sqrt(n) | X[:, 0..14]]
@@ -1093,7 +1081,10 @@ static bool pca_krylov(PcaWork& wk, const double* cor, long long n, int k, doubl
     const double shift_scale = 11.0 * ((double)n * B + (double)B * (B + 1)) * eps;
     DBuf<double> Q((size_t)P * n * B), W((size_t)n * B), T1((size_t)n * B), T2((size_t)n * B), X((size_t)n * B);
     const int nap = (int)((n + kApplyRows - 1) / kApplyRows);  // k_apply blocks
-    DBuf<double> part((size_t)P * nblk * BB), gpart((size_t)nap * BB), qpart((size_t)P * nap * BB), rinv(BB);
+    DBuf<double> part((size_t)P * nblk * BB), gpart((size_t)nap * BB), gpart2((size_t)nap * BB),
+        qpart((size_t)P * nap * BB);
+    double* gcur = gpart.p;  // Gram partials of the last apply that made them
+    double* galt = gpart2.p;
     // small outputs of one cycle, per block j: c1 [P], c2 [P], R x 6, G
     const int slot = (2 * P + 7) * BB;
     DBuf<double> smalls((size_t)P * slot + 3 * BB);  // + the restart block's R factors
@@ -1107,12 +1098,17 @@ static bool pca_krylov(PcaWork& wk, const double* cor, long long n, int k, doubl
         hipLaunchKernelGGL(k_gram_ms, dim3((unsigned)(nb * BB)), dim3(64), 0, s, part.p, nblk, out);
     };
     auto apply = [&](const double* in, int nb, const double* Cm, const double* Ri, double* out, bool g, bool qg) {
-        hipLaunchKernelGGL(k_apply, dim3((unsigned)nap), dim3(256), 0, s, in, Q.p, nb, Cm, Ri, n, out,
-                           g ? gpart.p : nullptr, qg ? qpart.p : nullptr, nap);
+        hipLaunchKernelGGL(k_apply_t<false>, dim3((unsigned)nap), dim3(256), 0, s, in, Q.p, nb, Cm, Ri, n, out,
+                           g ? gcur : nullptr, qg ? qpart.p : nullptr, nap, nullptr, 0, 0.0, nullptr, nullptr);
     };
-    auto chol = [&](bool shifted, double* Rout, int* fl) {
-        hipLaunchKernelGGL(k_reduce_chol, dim3(1), dim3(1024), 0, s, gpart.p, nap, shifted ? shift_scale : 0.0, Rout,
-                           rinv.p, fl);
+    // out = in R^{-1}, R = chol(the Gram of `in` from gcur (+ shift)), in one
+    // launch; new Gram partials (g) go to the other buffer
+    auto apply_chol = [&](const double* in, int nbq, double* out, bool g, bool qg, bool shifted, double* Rout,
+                          int* fl) {
+        hipLaunchKernelGGL(k_apply_t<true>, dim3((unsigned)nap), dim3(256), 0, s, in, Q.p, nbq, nullptr, nullptr, n,
+                           out, g ? galt : nullptr, qg ? qpart.p : nullptr, nap, gcur, nap,
+                           shifted ? shift_scale : 0.0, Rout, fl);
+        if (g) std::swap(gcur, galt);
     };
     // shifted CholeskyQR3 of the block whose Gram partials are in gpart (its
     // rows in `in`): out = in R^{-1}, R factors to R3[0..2]; qg: the final
@@ -1125,9 +1121,8 @@ static bool pca_krylov(PcaWork& wk, const double* cor, long long n, int k, doubl
         // third pass cannot break down (its noise direction is a valid new
         // basis vector; the outer second Gram-Schmidt pass re-orthogonalises it)
         for (int pass = 0; pass < 3; ++pass) {
-            chol(pass < 2, R3 + pass * BB, fl + pass);
             double* dst = pass == 2 ? out : (cur == T1.p ? T2.p : T1.p);
-            apply(cur, nbq, nullptr, rinv.p, dst, pass < 2, pass == 2 && nbq > 0);
+            apply_chol(cur, nbq, dst, pass < 2, pass == 2 && nbq > 0, pass < 2, R3 + pass * BB, fl + pass);
             cur = dst;
         }
     };
@@ -1174,7 +1169,7 @@ static bool pca_krylov(PcaWork& wk, const double* cor, long long n, int k, doubl
                 apply(W.p, nb, c1, nullptr, X.p, false, true);
                 qreduce(nb, c2);
                 apply(X.p, nb, c2, nullptr, W.p, true, false);
-                hipLaunchKernelGGL(k_gram_ms, dim3((unsigned)BB), dim3(64), 0, s, gpart.p, nap, G);
+                hipLaunchKernelGGL(k_gram_ms, dim3((unsigned)BB), dim3(64), 0, s, gcur, nap, G);
             }
         }
         smalls.download(hs.data(), hs.size(), s);

@@ -203,15 +203,34 @@ class CapiExchange:
         if self.world == 1:
             self.fn, self.user = None, None
         elif backend == "nccl":
+            import torch
             import torch.distributed as tdist
+            # every rank reaches every collective below whatever fails, and
+            # all ranks raise together (a caller can then fall back as one)
             uid = C.create_string_buffer(128)
+            err = None
             if self.rank == 0:
-                _lib.call("hh_comm_unique_id", uid)
-            obj = [bytes(uid.raw) if self.rank == 0 else None]
+                try:
+                    _lib.call("hh_comm_unique_id", uid)
+                except Exception as e:  # noqa: BLE001
+                    err = e
+            obj = [bytes(uid.raw) if self.rank == 0 and err is None else None]
             tdist.broadcast_object_list(obj, src=0, group=group)
+            if obj[0] is None:
+                raise RuntimeError(f"ncclGetUniqueId failed on rank 0: {err}")
             uid = C.create_string_buffer(obj[0], 128)
             h = C.c_void_p()
-            _lib.call("hh_comm_init", uid, self.world, self.rank, C.byref(h))
+            try:
+                _lib.call("hh_comm_init", uid, self.world, self.rank, C.byref(h))
+                ok = 1
+            except Exception as e:  # noqa: BLE001
+                err, ok = e, 0
+            flag = torch.tensor([ok], dtype=torch.int32, device="cuda")
+            tdist.all_reduce(flag, op=tdist.ReduceOp.MIN, group=group)
+            if int(flag.item()) == 0:
+                if ok:
+                    _lib.call("hh_comm_free", h)
+                raise RuntimeError(f"RCCL communicator init failed on a rank ({err})")
             self._comm = h
             self.fn = C.cast(lib.hh_comm_allgather, C.c_void_p)
             self.user = h

@@ -232,3 +232,39 @@ def test_not_hdf5(tmp_path):
     p.write_bytes(b"plain text" * 100)
     with pytest.raises(h5.H5Error):
         h5.File(str(p))
+
+
+def test_reader_2d_chunked_with_unallocated_chunk(tmp_path):
+    """A 5 x 7 float64 dataset in 3 x 4 chunks (edge chunks partial), deflate
+    only, one chunk never written (absent from the B-tree: reads as 0)."""
+    x = np.arange(35, dtype="<f8").reshape(5, 7) / 7
+    img = _Img()
+    img.put(b"\0" * 48)
+    entries = []
+    for r0 in (0, 3):
+        for c0 in (0, 4):
+            if (r0, c0) == (3, 4):
+                x[3:, 4:] = 0.0
+                continue
+            blk = np.zeros((3, 4), "<f8")
+            part = x[r0:r0 + 3, c0:c0 + 4]
+            blk[:part.shape[0], :part.shape[1]] = part
+            raw = zlib.compress(blk.tobytes())
+            entries.append((r0, c0, len(raw), img.put(raw)))
+    bt = b"TREE" + bytes([1, 0]) + struct.pack("<HQQ", len(entries), UNDEF, UNDEF)
+    for r0, c0, size, addr in entries:
+        bt += struct.pack("<IIQQQ", size, 0, r0, c0, 0) + struct.pack("<Q", addr)
+    bt += struct.pack("<IIQQQ", 0, 0, 5, 7, 0)
+    bt_at = img.put(bt)
+    dspace = bytes([2, 2, 0, 1]) + struct.pack("<QQ", 5, 7)
+    f8 = bytes([0x11, 0x20, 63, 0]) + struct.pack("<IHHBBBBI", 8, 0, 64, 52, 11, 0, 52, 1023)
+    layout = bytes([3, 2, 3]) + struct.pack("<Q", bt_at) + struct.pack("<III", 3, 4, 8)
+    filt = bytes([2, 1]) + struct.pack("<HHHI", 1, 0, 1, 4)
+    ds_at = img.put(_ohdr_v2([(0x01, dspace), (0x03, f8), (0x08, layout), (0x0B, filt)]))
+    link = bytes([1, 0x00, 1]) + b"m" + struct.pack("<Q", ds_at)
+    root_at = img.put(_ohdr_v2([(0x06, link)]))
+    img.patch(0, h5.SIG + bytes([2, 8, 8, 0]) + struct.pack("<QQQQ", 0, UNDEF, len(img.b), root_at) + b"\0" * 4)
+    p = tmp_path / "m.h5"
+    p.write_bytes(bytes(img.b))
+    with h5.File(str(p)) as f:
+        np.testing.assert_array_equal(f["m"].read(), x)
