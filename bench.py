@@ -819,7 +819,7 @@ def main():
     from hichap_master_amd import _lib, dist, ice
     _lib.load()
     _lib.call("hh_set_device", local)
-    for key in ("pca_p", "pca_method"):  # eigensolver knobs (measurement)
+    for key in ("pca_p", "pca_method", "build_debug"):  # eigensolver / build-trace knobs (measurement)
         if os.environ.get("HH_" + key.upper()):
             _lib.call("hh_tune", key.encode(), int(os.environ["HH_" + key.upper()]))
     if world > 1 or args.sharded:
@@ -992,7 +992,10 @@ def main():
                 traffic_src = f"{traffic_src} (scaled by shard payload)" if traffic else None
             phys = traffic if traffic else real_b
             achieved = phys / sweep_avg / 1e9
-            out["roofline"] = {"bound": "hbm", "kernel": "ice sweep span: k_sweep_flat | k_sweep_tiled | k_sweep_band<8> + 2 x k_sweep_band<4> on three streams (HIP events around the sweep; rocprof per-sweep span: tools/sweep_span.py)",
+            out["roofline"] = {"bound": "hbm", "kernel": ("ice sweep span: k_sweep_flat | k_sweep_tiled | k_sweep_bands (uint8 + 2 x 4-bit segments) on three streams"
+                                         if inf["payload_bytes"] >= (1 << 30) else
+                                         "ice sweep: k_sweep_all (tiled + band + flat bodies in one launch)")
+                               + " (HIP events around the sweep; rocprof per-sweep span: tools/sweep_span.py)",
                                "achieved": achieved,
                                "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS,
                                "bytes_per_launch": phys,

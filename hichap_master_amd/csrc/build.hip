@@ -28,6 +28,9 @@
 #include <cmath>
 #include <numeric>
 
+#include <chrono>
+#include <cstdio>
+
 #include "ice_internal.hpp"
 
 namespace hh {
@@ -100,26 +103,53 @@ __global__ void k_px_keyptr(const unsigned long long* __restrict__ keys, long lo
 }
 
 // lower-half keys of the local rows (order fixed later by the sort)
+// One block per kLowChunk pixels: count the block's lower-half keys, ONE
+// atomic per block for its output range (one per wave was 12.5 M same-address
+// atomics at C3: 150 ms), then write them in pixel order within the block.
+// The order across blocks does not matter: the keys are unique and sorted next.
+constexpr int kLowItems = 16;
+constexpr int kLowChunk = 256 * kLowItems;
 __global__ __launch_bounds__(256) void k_px_lowkeys(const int32_t* __restrict__ A, const int32_t* __restrict__ B,
                                                     const uint32_t* __restrict__ kc, long long nnz, long long row_lo,
                                                     long long row_hi, int ib, unsigned long long* __restrict__ keys,
                                                     unsigned long long* __restrict__ n_keys) {
-    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    bool take = false;
-    long long b = 0;
-    if (i < nnz) {
-        b = B[i];
-        take = kc[i] != 0u && A[i] < b && b >= row_lo && b < row_hi;
+    __shared__ unsigned wcnt[kLowItems][4];
+    __shared__ unsigned long long base_sh;
+    const long long c0 = (long long)blockIdx.x * kLowChunk;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    unsigned long long mk[kLowItems];
+#pragma unroll
+    for (int k = 0; k < kLowItems; ++k) {
+        const long long i = c0 + (long long)k * 256 + threadIdx.x;
+        bool take = false;
+        if (i < nnz) {
+            const long long b = B[i];
+            take = kc[i] != 0u && A[i] < b && b >= row_lo && b < row_hi;
+        }
+        mk[k] = __ballot(take);
+        if (lane == 0) wcnt[k][wave] = (unsigned)__popcll(mk[k]);
     }
-    const unsigned long long m = __ballot(take);
-    if (!m) return;
-    const int lane = threadIdx.x & 63;
-    unsigned long long base = 0;
-    if (lane == 63 - __clzll(m)) base = atomicAdd(n_keys, (unsigned long long)__popcll(m));
-    base = __shfl(base, 63 - __clzll(m), 64);
-    if (take)
-        keys[base + __popcll(m & ((1ull << lane) - 1ull))] =
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned tot = 0;
+        for (int k = 0; k < kLowItems; ++k)
+            for (int w = 0; w < 4; ++w) {
+                const unsigned c = wcnt[k][w];
+                wcnt[k][w] = tot;  // exclusive offset within the block
+                tot += c;
+            }
+        base_sh = tot ? atomicAdd(n_keys, (unsigned long long)tot) : 0ull;
+    }
+    __syncthreads();
+    const unsigned long long base = base_sh;
+#pragma unroll
+    for (int k = 0; k < kLowItems; ++k) {
+        if (!((mk[k] >> lane) & 1ull)) continue;
+        const long long i = c0 + (long long)k * 256 + threadIdx.x;
+        const long long b = B[i];
+        keys[base + wcnt[k][wave] + __popcll(mk[k] & ((1ull << lane) - 1ull))] =
             ((unsigned long long)(b - row_lo) << ib) | (unsigned long long)i;
+    }
 }
 
 struct PxRows {
@@ -315,6 +345,15 @@ void build_from_device_pixels(const Id* b1, const Id* b2, const Cnt* cnt, int64_
     HH_REQUIRE(chrom_offsets[0] == 0 && chrom_offsets[n_chroms] == n_bins, "chrom_offsets must span [0, n_bins]");
     HH_REQUIRE(n_chroms < 65535, "too many chromosomes");
     HH_REQUIRE(ignore_diags >= 0, "ignore_diags must be >= 0");
+    // hh_tune("build_debug", 1): phase times on stderr (synchronises per phase)
+    auto t_last = std::chrono::steady_clock::now();
+    auto phase = [&](const char* what) {
+        if (!g_build_debug) return;
+        HIP_CHECK(hipStreamSynchronize(s));
+        const auto t = std::chrono::steady_clock::now();
+        fprintf(stderr, "[build] %-24s %8.3f ms\n", what, std::chrono::duration<double, std::milli>(t - t_last).count());
+        t_last = t;
+    };
     auto m = std::make_unique<hh_matrix>();
     HIP_CHECK(hipGetDevice(&m->device));
     m->n_bins = n_bins;
@@ -351,6 +390,7 @@ void build_from_device_pixels(const Id* b1, const Id* b2, const Cnt* cnt, int64_
     std::vector<unsigned> hocc(occ_max + 1), hbig(occ_max + 1);
     docc.download(hocc.data(), hocc.size(), s);
     dbig.download(hbig.data(), hbig.size(), s);
+    phase("check");
     HIP_CHECK(hipStreamSynchronize(s));
     {
         static const char* what[5] = {"bin id out of range", "bin1 > bin2 (not an upper-triangle pixel table)",
@@ -379,6 +419,7 @@ void build_from_device_pixels(const Id* b1, const Id* b2, const Cnt* cnt, int64_
         W = bw.w8;
         W4 = bw.w4;
     }
+    phase("bands chosen");
     // ---- row structure: upper rows from the sorted table, lower rows sorted
     DBuf<long long> up_ptr(n_bins + 1);
     if (nnz > 0)
@@ -395,12 +436,15 @@ void build_from_device_pixels(const Id* b1, const Id* b2, const Cnt* cnt, int64_
     nkeys.zero(s);
     DBuf<unsigned long long> keys(std::max<int64_t>(nnz, 1));
     if (nnz > 0)
-        hipLaunchKernelGGL(k_px_lowkeys, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s, dA.p, dB.p, dkc.p,
+        hipLaunchKernelGGL(k_px_lowkeys, dim3((unsigned)((nnz + kLowChunk - 1) / kLowChunk)), dim3(256), 0, s, dA.p,
+                           dB.p, dkc.p,
                            (long long)nnz, (long long)row_lo, (long long)row_hi, ib, keys.p, nkeys.p);
     unsigned long long hn = 0;
     nkeys.download(&hn, 1, s);
     HIP_CHECK(hipStreamSynchronize(s));
+    phase("lower keys");
     dev_sort_u64(keys, (int64_t)hn, ib + rbits, s);
+    phase("radix sort");
     DBuf<long long> lo_ptr(nloc + 1);
     hipLaunchKernelGGL(k_px_keyptr, dim3((unsigned)((hn + 1 + 255) / 256)), dim3(256), 0, s, keys.p, (long long)hn, ib,
                        (long long)nloc, lo_ptr.p);
@@ -439,6 +483,7 @@ void build_from_device_pixels(const Id* b1, const Id* b2, const Cnt* cnt, int64_
     const dim3 rgrid((unsigned)((nloc * 64 + 255) / 256));
     if (nloc) hipLaunchKernelGGL((k_px_rows<0>), rgrid, dim3(256), 0, s, P);
     HIP_CHECK(hipGetLastError());
+    phase("pass 0");
     std::vector<uint16_t> hc((size_t)nloc * nJ), hnarrow((size_t)nloc * nJ);
     cnt_w.download(hc.data(), hc.size(), s);
     cnt_n.download(hnarrow.data(), hnarrow.size(), s);
@@ -451,10 +496,13 @@ void build_from_device_pixels(const Id* b1, const Id* b2, const Cnt* cnt, int64_
     HIP_CHECK(hipStreamSynchronize(s));
     cnt_w.release();
     cnt_n.release();
+    phase("download counts");
     std::vector<uint16_t> bg = bin_groups(*m);
     std::vector<uint16_t> rgroup(bg.begin() + row_lo, bg.begin() + row_hi);
     TilePlan TP = plan_tiles(hc.data(), hnarrow.data(), nloc, nJ, rgroup);
+    phase("plan_tiles (host)");
     upload_plan(TP, *m, s);
+    phase("upload plan");
     m->row_group = to_device(rgroup, s);
     DBuf<int32_t> tof = to_device(TP.tile_of, s);
     m->pay.alloc(TP.n_entries_padded);
@@ -471,6 +519,7 @@ void build_from_device_pixels(const Id* b1, const Id* b2, const Cnt* cnt, int64_
     m->wide_col.alloc(std::max<long long>(wptr[nloc], 1));
     m->wide_cnt.alloc(std::max<long long>(wptr[nloc], 1));
     m->n_wide = wptr[nloc];
+    phase("alloc + zero");
     // ---- PASS 1: write
     P.tile_of = tof.p;
     P.tile_ent = m->tile_ent.p;
@@ -487,6 +536,7 @@ void build_from_device_pixels(const Id* b1, const Id* b2, const Cnt* cnt, int64_
     if (nloc) hipLaunchKernelGGL((k_px_rows<1>), rgrid, dim3(256), 0, s, P);
     HIP_CHECK(hipGetLastError());
     HIP_CHECK(hipStreamSynchronize(s));  // scratch buffers return to the pool
+    phase("pass 1");
     int64_t nb = 0, ent = 0, up = 0;
     for (int64_t r = 0; r < nloc; ++r) {
         nb += hb[r];

@@ -79,52 +79,131 @@ __global__ void k_px_keyptr_gw(const unsigned long long* __restrict__ keys, long
     for (long long r = lo + 1; r <= hi; ++r) ptr[r] = k;
 }
 
+// Wave-segmented integer sums: lanes hold (key, val) with keys non-decreasing
+// across the wave (a sorted table's rows); each key's segment sum goes out
+// in one atomic from its last lane (was one same-address atomic per lane:
+// 64-way serialised on a sorted table).  Integer sums: order-free, exact.
+__device__ __forceinline__ void seg_add_u64(long long key, unsigned long long val, unsigned long long* __restrict__ out) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const unsigned long long vu = __shfl_up(val, o, 64);
+        const long long ku = __shfl_up(key, o, 64);
+        if (lane >= o && ku == key) val += vu;
+    }
+    const long long kd = __shfl_down(key, 1, 64);
+    if ((lane == 63 || kd != key) && val) atomicAdd(out + key, val);
+}
+
+// Grid-stride kernels with a fixed grid: a block's scalar total is reduced
+// once and added with one atomic per block.
+constexpr int kGwStatBlocks = 2048;
+
 // T row statistics within each chromosome block (both ends of an upper pixel,
-// the diagonal once): exact integer sums / counts
-__global__ void k_gw_tstats(const int32_t* __restrict__ a, const int32_t* __restrict__ b,
-                            const uint32_t* __restrict__ v, long long nnz, const int32_t* __restrict__ chrom_of,
-                            unsigned long long* __restrict__ rsum, unsigned long long* __restrict__ rnz) {
-    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nnz) return;
-    const int32_t x = a[i], y = b[i];
-    const uint32_t c = v[i];
-    if (c == 0u || chrom_of[x] != chrom_of[y]) return;
-    atomicAdd(rsum + x, (unsigned long long)c);
-    atomicAdd(rnz + x, 1ull);
-    if (x != y) {
-        atomicAdd(rsum + y, (unsigned long long)c);
-        atomicAdd(rnz + y, 1ull);
+// the diagonal once): exact integer sums / counts.  The table is sorted by
+// bin1: the bin1 end is a segmented sum, the bin2 end an atomic per pixel
+// (distinct columns within a wave).
+__global__ __launch_bounds__(256) void k_gw_tstats(const int32_t* __restrict__ a, const int32_t* __restrict__ b,
+                                                   const uint32_t* __restrict__ v, long long nnz,
+                                                   const int32_t* __restrict__ chrom_of,
+                                                   unsigned long long* __restrict__ rsum,
+                                                   unsigned long long* __restrict__ rnz) {
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    const long long start = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long long end = (nnz + 63) / 64 * 64;  // whole waves iterate together
+    for (long long i = start; i < end; i += stride) {
+        long long x = 0x7fffffffLL;
+        unsigned long long c = 0, one = 0;
+        if (i < nnz) {
+            x = a[i];
+            const int32_t y = b[i];
+            const uint32_t cc = v[i];
+            if (cc != 0u && chrom_of[x] == chrom_of[y]) {
+                c = cc;
+                one = 1;
+                if (x != y) {
+                    atomicAdd(rsum + y, (unsigned long long)cc);
+                    atomicAdd(rnz + y, 1ull);
+                }
+            }
+        }
+        seg_add_u64(x, c, rsum);
+        seg_add_u64(x, one, rnz);
     }
 }
 
-// H row sums within the same-chromosome same-haplotype block, and sum(H)
-__global__ void k_gw_hstats(const int32_t* __restrict__ r, const int32_t* __restrict__ c,
-                            const uint32_t* __restrict__ v, long long nnz, const int32_t* __restrict__ block_of,
-                            unsigned long long* __restrict__ bsum, unsigned long long* __restrict__ total) {
-    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+// H row sums within the same-chromosome same-haplotype block (H sorted by
+// row: segmented), and sum(H)
+__global__ __launch_bounds__(256) void k_gw_hstats(const int32_t* __restrict__ r, const int32_t* __restrict__ c,
+                                                   const uint32_t* __restrict__ v, long long nnz,
+                                                   const int32_t* __restrict__ block_of,
+                                                   unsigned long long* __restrict__ bsum,
+                                                   unsigned long long* __restrict__ total) {
+    __shared__ unsigned long long wsum[4];
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    const long long start = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long long end = (nnz + 63) / 64 * 64;
     unsigned long long t = 0;
-    if (i < nnz) {
-        const uint32_t x = v[i];
-        t = x;
-        if (x && block_of[r[i]] == block_of[c[i]]) atomicAdd(bsum + r[i], (unsigned long long)x);
+    for (long long i = start; i < end; i += stride) {
+        long long row = 0x7fffffffLL;
+        unsigned long long x = 0;
+        if (i < nnz) {
+            row = r[i];
+            const uint32_t xx = v[i];
+            t += xx;
+            if (xx && block_of[row] == block_of[c[i]]) x = xx;
+        }
+        seg_add_u64(row, x, bsum);
     }
     t = (unsigned long long)wave_sum_ll((long long)t);
-    if ((threadIdx.x & 63) == 0 && t) atomicAdd(total, t);
+    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = t;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned long long bt = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+        if (bt) atomicAdd(total, bt);
+    }
 }
 
-// off-diagonal cells keyed by column: (col << ib) | index
+// off-diagonal cells keyed by column: (col << ib) | index.  One block per
+// kColChunk cells and ONE atomic per block for its output range (one per
+// wave was ~23 M same-address atomics at 10 kb diploid); the keys are unique
+// and sorted next, so the order across blocks does not matter.
+constexpr int kColItems = 16;
+constexpr int kColChunk = 256 * kColItems;
 __global__ __launch_bounds__(256) void k_gw_colkeys(const int32_t* __restrict__ r, const int32_t* __restrict__ c,
                                                     long long nnz, int ib, unsigned long long* __restrict__ keys,
                                                     unsigned long long* __restrict__ n_keys) {
-    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    const bool take = i < nnz && r[i] != c[i];
-    const unsigned long long m = __ballot(take);
-    if (!m) return;
-    const int lane = threadIdx.x & 63;
-    unsigned long long base = 0;
-    if (lane == 63 - __clzll(m)) base = atomicAdd(n_keys, (unsigned long long)__popcll(m));
-    base = __shfl(base, 63 - __clzll(m), 64);
-    if (take) keys[base + __popcll(m & ((1ull << lane) - 1ull))] = ((unsigned long long)c[i] << ib) | (unsigned long long)i;
+    __shared__ unsigned wcnt[kColItems][4];
+    __shared__ unsigned long long base_sh;
+    const long long c0 = (long long)blockIdx.x * kColChunk;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    unsigned long long mk[kColItems];
+#pragma unroll
+    for (int k = 0; k < kColItems; ++k) {
+        const long long i = c0 + (long long)k * 256 + threadIdx.x;
+        mk[k] = __ballot(i < nnz && r[i] != c[i]);
+        if (lane == 0) wcnt[k][wave] = (unsigned)__popcll(mk[k]);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned tot = 0;
+        for (int k = 0; k < kColItems; ++k)
+            for (int w = 0; w < 4; ++w) {
+                const unsigned n = wcnt[k][w];
+                wcnt[k][w] = tot;
+                tot += n;
+            }
+        base_sh = tot ? atomicAdd(n_keys, (unsigned long long)tot) : 0ull;
+    }
+    __syncthreads();
+    const unsigned long long base = base_sh;
+#pragma unroll
+    for (int k = 0; k < kColItems; ++k) {
+        if (!((mk[k] >> lane) & 1ull)) continue;
+        const long long i = c0 + (long long)k * 256 + threadIdx.x;
+        keys[base + wcnt[k][wave] + __popcll(mk[k] & ((1ull << lane) - 1ull))] =
+            ((unsigned long long)c[i] << ib) | (unsigned long long)i;
+    }
 }
 
 __device__ __forceinline__ long long lower_bound_i32(const int32_t* a, long long lo, long long hi, int32_t x) {
@@ -356,12 +435,13 @@ void gw_create(hh_gw& G, const Id* t1, const Id* t2, const Cnt* tv, int64_t t_nn
     tnz.zero(s);
     hbs.zero(s);
     htot.zero(s);
+    auto sgrid = [](int64_t nnz) { return dim3((unsigned)std::min<int64_t>(kGwStatBlocks, (nnz + 255) / 256)); };
     if (t_nnz > 0)
-        hipLaunchKernelGGL(k_gw_tstats, dim3((unsigned)((t_nnz + 255) / 256)), dim3(256), 0, s, G.tA.p, G.tB.p, G.tV.p,
-                           (long long)t_nnz, dch.p, trs.p, tnz.p);
+        hipLaunchKernelGGL(k_gw_tstats, sgrid(t_nnz), dim3(256), 0, s, G.tA.p, G.tB.p, G.tV.p, (long long)t_nnz, dch.p,
+                           trs.p, tnz.p);
     if (h_nnz > 0)
-        hipLaunchKernelGGL(k_gw_hstats, dim3((unsigned)((h_nnz + 255) / 256)), dim3(256), 0, s, G.R.p, G.C.p, G.V.p,
-                           (long long)h_nnz, dblk.p, hbs.p, htot.p);
+        hipLaunchKernelGGL(k_gw_hstats, sgrid(h_nnz), dim3(256), 0, s, G.R.p, G.C.p, G.V.p, (long long)h_nnz, dblk.p,
+                           hbs.p, htot.p);
     HIP_CHECK(hipGetLastError());
     G.t_rowsum.resize(n);
     G.t_nnz_row.resize(n);
@@ -386,7 +466,8 @@ void gw_create(hh_gw& G, const Id* t1, const Id* t2, const Cnt* tv, int64_t t_nn
     nk.zero(s);
     G.keys.alloc(std::max<int64_t>(h_nnz, 1));
     if (h_nnz > 0)
-        hipLaunchKernelGGL(k_gw_colkeys, dim3((unsigned)((h_nnz + 255) / 256)), dim3(256), 0, s, G.R.p, G.C.p,
+        hipLaunchKernelGGL(k_gw_colkeys, dim3((unsigned)((h_nnz + kColChunk - 1) / kColChunk)), dim3(256), 0, s,
+                           G.R.p, G.C.p,
                            (long long)h_nnz, G.ib, G.keys.p, nk.p);
     unsigned long long hn = 0;
     nk.download(&hn, 1, s);

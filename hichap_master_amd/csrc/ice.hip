@@ -1378,6 +1378,8 @@ int hh_tune(const char* key, int64_t value) {
         } else if (k == "host_build") {
             HH_REQUIRE(value == 0 || value == 1, "host_build in {0, 1}");
             g_host_build = value;
+        } else if (k == "build_debug") {
+            g_build_debug = value;
         } else if (k == "pca_debug") {
             g_pca_debug = (int)value;
         } else if (k == "pca_p") {

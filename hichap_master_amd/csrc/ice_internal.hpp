@@ -269,4 +269,5 @@ bool build_from_host_pixels_on_device(const int64_t* bin1, const int64_t* bin2, 
                                       int32_t ignore_diags, int32_t cis_only, int64_t row_lo, int64_t row_hi,
                                       hipStream_t s, hh_matrix** out);
 extern int64_t g_host_build;
+extern int64_t g_build_debug;  // hh_tune("build_debug"): device-build phase times on stderr
 }  // namespace hh

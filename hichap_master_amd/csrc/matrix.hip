@@ -2,8 +2,12 @@
 // layout (ice_internal.hpp): tile/unit planning shared with the
 // on-device generator (synth.hip), host fill + upload, and export for checks.
 #include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstdio>
 #include <cmath>
 #include <numeric>
+#include <thread>
 
 #include "ice_internal.hpp"
 
@@ -14,6 +18,7 @@ int64_t g_unit_entries = 0;  // 0 = auto (plan_tiles)
 int64_t g_tile_cost = 32768; // payload-word equivalent of one tile's fixed cost in the unit split (C4 shard 8/8: 0.79 -> 0.65 ms/iter)
 int64_t g_band_w = -1;       // -1 = auto (choose_band_w)
 int64_t g_flat_max = 64;     // longest row (uint4) of a flat tile segment; 0 = no flat segments
+int64_t g_build_debug = 0;
 int64_t g_host_build = 0;    // hh_tune("host_build"): 1 = host builder for every pixel table
 
 int64_t g_band4 = 1;         // nibble band on
@@ -50,6 +55,131 @@ BandWidths choose_band_widths(const std::vector<double>& occ, const std::vector<
 }
 void set_error(const std::string& msg) { g_last_error = msg; }
 
+namespace {
+// The tiles of one row-block (plan_tiles' per-block work, entry offsets
+// relative to the block's first tile).
+struct BlockTiles {
+    std::vector<int32_t> J;
+    std::vector<int64_t> ent, entn;
+    std::vector<uint32_t> rp, rpn, fw;
+    std::vector<uint16_t> perm, band, frec;
+    std::vector<int32_t> frec_of;  // per tile: flat record index within the block, -1
+    std::vector<uint8_t> flat;
+    int64_t ent_total = 0, entn_total = 0;
+};
+
+void plan_block(const uint16_t* cntw, const uint16_t* cntn, int64_t nloc, int32_t nJ, int64_t rb, BlockTiles& B) {
+    std::vector<uint32_t> rp(kR + 1), rpn(kR + 1);
+    const int64_t r0 = rb * kR, r1 = std::min<int64_t>(nloc, r0 + kR);
+    // the block's counts transposed to tile-major (one pass over its rows)
+    std::vector<uint16_t> tw((size_t)nJ * kR, 0), tn((size_t)nJ * kR, 0);
+    for (int64_t r = r0; r < r1; ++r)
+        for (int32_t J = 0; J < nJ; ++J) {
+            tw[(size_t)J * kR + (r - r0)] = cntw[r * nJ + J];
+            if (cntn) tn[(size_t)J * kR + (r - r0)] = cntn[r * nJ + J];
+        }
+    int64_t ent = 0, entn = 0;
+    for (int32_t J = 0; J < nJ; ++J) {
+        const uint16_t* cw_ = &tw[(size_t)J * kR];
+        const uint16_t* cn_ = &tn[(size_t)J * kR];
+        rp[0] = rpn[0] = 0;
+        for (int k = 0; k < kR; ++k) {
+            rp[k + 1] = rp[k] + (uint32_t)pad4(cw_[k]);
+            rpn[k + 1] = rpn[k] + (uint32_t)pad8(cn_[k]);
+        }
+        if (rp[kR] == 0 && rpn[kR] == 0) continue;
+        B.J.push_back(J);
+        B.ent.push_back(ent);
+        B.entn.push_back(entn);
+        B.rp.insert(B.rp.end(), rp.begin(), rp.end());
+        B.rpn.insert(B.rpn.end(), rpn.begin(), rpn.end());
+        // per segment (narrow first): rows by decreasing length (uint4
+        // count, counting sort on min(len, 255), stable) and the bands of
+        // that order; a tile whose nonempty segments have only short rows
+        // (<= g_flat_max uint4) is *flat*: its perms list the nonempty rows
+        // in row order instead (band[kFlatFlag] = 1, band[kFlatRows] = count)
+        uint16_t perm[2][kR];
+        uint16_t band[2][kBandSlots] = {{0}};
+        uint32_t maxlen[2];
+        for (int seg = 0; seg < 2; ++seg) {
+            const std::vector<uint32_t>& q = seg == 0 ? rpn : rp;
+            const int sh = seg == 0 ? 3 : 2;
+            uint32_t key[kR];
+            int hist[257] = {0};
+            for (int k = 0; k < kR; ++k) {
+                const uint32_t len = (q[k + 1] - q[k]) >> sh;
+                key[k] = 255u - std::min<uint32_t>(len, 255u);  // descending
+                ++hist[key[k] + 1];
+            }
+            for (int k = 0; k < 256; ++k) hist[k + 1] += hist[k];
+            for (int k = 0; k < kR; ++k) perm[seg][hist[key[k]]++] = (uint16_t)k;
+            int pos = 0;
+            for (int g = 0; g < kBands; ++g) {
+                while (pos < kR && ((q[perm[seg][pos] + 1] - q[perm[seg][pos]]) >> sh) >= band_min(g)) ++pos;
+                band[seg][g + 1] = (uint16_t)pos;
+            }
+            maxlen[seg] = 255u - key[perm[seg][0]];
+        }
+        const bool flat = g_flat_max > 0 && maxlen[0] <= (uint32_t)g_flat_max &&
+                          maxlen[1] <= (uint32_t)g_flat_max && (rpn[kR] >> 3) < 65536u && (rp[kR] >> 2) < 65536u;
+        uint32_t fw[kFlatMeta] = {0};
+        if (flat) {
+            for (int seg = 0; seg < 2; ++seg) {
+                const std::vector<uint32_t>& q = seg == 0 ? rpn : rp;
+                const int sh = seg == 0 ? 3 : 2;
+                int nfr = 0;
+                uint32_t st[kR + 1];  // uint4 starts of the nonempty rows, then the end
+                for (int k = 0; k < kR; ++k)
+                    if (q[k + 1] > q[k]) {
+                        st[nfr] = q[k] >> sh;
+                        perm[seg][nfr++] = (uint16_t)k;
+                    }
+                for (int k = nfr; k < kR; ++k) perm[seg][k] = 0;
+                const uint32_t Q = q[kR] >> sh;
+                st[nfr] = Q;
+                band[seg][kFlatFlag] = nfr > 0 ? 1 : 0;
+                band[seg][kFlatRows] = (uint16_t)nfr;
+                // wave w takes the rows starting in [Q w / 8, Q (w + 1) / 8)
+                uint32_t* f = fw + seg * 2 * (kFlatWaves + 1);
+                for (int w = 0; w <= kFlatWaves; ++w) {
+                    const uint32_t tq = (uint32_t)(((uint64_t)Q * w) / kFlatWaves);
+                    const int i = (int)(std::lower_bound(st, st + nfr, tq) - st);
+                    f[2 * w] = st[i];
+                    f[2 * w + 1] = (uint32_t)i;
+                }
+            }
+        }
+        B.fw.insert(B.fw.end(), fw, fw + kFlatMeta);
+        if (flat) {
+            B.frec_of.push_back((int32_t)(B.frec.size() / (kFrecU4 * 8)));
+            const size_t base = B.frec.size();
+            B.frec.resize(base + kFrecU4 * 8, 0);
+            uint16_t* rec = &B.frec[base];
+            for (int seg = 0; seg < 2; ++seg) {
+                const std::vector<uint32_t>& q = seg == 0 ? rpn : rp;
+                const int sh = seg == 0 ? 3 : 2;
+                const int nfr = band[seg][kFlatRows];
+                uint16_t* st = rec + seg * (kR + 1);
+                uint16_t* id = rec + 2 * (kR + 1) + seg * kR;
+                for (int i = 0; i <= kR; ++i) st[i] = (uint16_t)(i < nfr ? q[perm[seg][i]] >> sh : q[kR] >> sh);
+                for (int i = 0; i < kR; ++i) id[i] = perm[seg][i];
+            }
+        } else {
+            B.frec_of.push_back(-1);
+        }
+        B.flat.push_back(flat ? 1 : 0);
+        for (int seg = 0; seg < 2; ++seg) {
+            B.perm.insert(B.perm.end(), perm[seg], perm[seg] + kR);
+            B.band.insert(B.band.end(), band[seg], band[seg] + kBandSlots);
+        }
+        ent += rp[kR];
+        entn += rpn[kR];
+    }
+    B.ent_total = ent;
+    B.entn_total = entn;
+}
+}  // namespace
+
 TilePlan plan_tiles(const uint16_t* cntw, const uint16_t* cntn, int64_t nloc, int32_t nJ,
                     const std::vector<uint16_t>& row_group) {
     TilePlan P;
@@ -59,112 +189,72 @@ TilePlan plan_tiles(const uint16_t* cntw, const uint16_t* cntn, int64_t nloc, in
     P.tile_of.assign((size_t)P.nrb * nJ, -1);
     P.blk_tile_ptr.assign(P.nrb + 1, 0);
     P.blk_unit_ptr.assign(P.nrb + 1, 0);
+    // row-blocks planned in parallel (independent), concatenated in order:
+    // the plan is identical to the serial one
+    std::vector<BlockTiles> blocks((size_t)P.nrb);
+    const auto tp0 = std::chrono::steady_clock::now();
+    {
+        const int nt = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)std::thread::hardware_concurrency(),
+                                                                     (int64_t)16, P.nrb}));
+        std::atomic<int64_t> next{0};
+        auto work = [&] {
+            for (int64_t rb; (rb = next.fetch_add(1)) < P.nrb;) plan_block(cntw, cntn, nloc, nJ, rb, blocks[rb]);
+        };
+        std::vector<std::thread> th;
+        for (int t = 1; t < nt; ++t) th.emplace_back(work);
+        work();
+        for (auto& t : th) t.join();
+    }
+    const auto tp1 = std::chrono::steady_clock::now();
+    // concatenation in block order (its cost is first-touch page faults of
+    // the ~6 KB per tile of plan arrays, not the copies: a parallel copy
+    // measured the same 45 ms at 22 572 tiles)
+    size_t nt_all = 0, nfrec = 0;
+    for (const auto& B : blocks) {
+        nt_all += B.J.size();
+        nfrec += B.frec.size();
+    }
+    P.tile_J.reserve(nt_all);
+    P.tile_ent.reserve(nt_all);
+    P.tile_entn.reserve(nt_all);
+    P.tile_rb.reserve(nt_all);
+    P.tile_rp.reserve(nt_all * (kR + 1));
+    P.tile_rpn.reserve(nt_all * (kR + 1));
+    P.tile_fw.reserve(nt_all * kFlatMeta);
+    P.tile_perm.reserve(nt_all * 2 * kR);
+    P.tile_band.reserve(nt_all * 2 * kBandSlots);
+    P.tile_frec.reserve(nt_all);
+    P.tile_flat.reserve(nt_all);
+    P.frec.reserve(nfrec);
     int64_t ent = 0, entn = 0;
-    std::vector<uint32_t> rp(kR + 1), rpn(kR + 1);
     for (int64_t rb = 0; rb < P.nrb; ++rb) {
+        BlockTiles& B = blocks[rb];
         P.blk_tile_ptr[rb] = (int32_t)P.tile_J.size();
-        const int64_t r0 = rb * kR, r1 = std::min<int64_t>(nloc, r0 + kR);
-        for (int32_t J = 0; J < nJ; ++J) {
-            rp[0] = rpn[0] = 0;
-            for (int k = 0; k < kR; ++k) {
-                const int64_t r = r0 + k;
-                const uint32_t cw = r < r1 ? (uint32_t)pad4(cntw[r * nJ + J]) : 0u;
-                const uint32_t cn = (r < r1 && cntn) ? (uint32_t)pad8(cntn[r * nJ + J]) : 0u;
-                rp[k + 1] = rp[k] + cw;
-                rpn[k + 1] = rpn[k] + cn;
-            }
-            if (rp[kR] == 0 && rpn[kR] == 0) continue;
-            P.tile_of[rb * nJ + J] = (int32_t)P.tile_J.size();
-            P.tile_J.push_back(J);
-            P.tile_ent.push_back(ent);
-            P.tile_entn.push_back(entn);
+        const int32_t frec0 = (int32_t)(P.frec.size() / (kFrecU4 * 8));
+        for (size_t i = 0; i < B.J.size(); ++i) {
+            P.tile_of[rb * nJ + B.J[i]] = (int32_t)P.tile_J.size();
+            P.tile_J.push_back(B.J[i]);
+            P.tile_ent.push_back(ent + B.ent[i]);
+            P.tile_entn.push_back(entn + B.entn[i]);
             P.tile_rb.push_back((int32_t)rb);
-            P.tile_rp.insert(P.tile_rp.end(), rp.begin(), rp.end());
-            P.tile_rpn.insert(P.tile_rpn.end(), rpn.begin(), rpn.end());
-            // per segment (narrow first): rows by decreasing length (uint4
-            // count, counting sort on min(len, 255), stable) and the bands of
-            // that order; a tile whose nonempty segments have only short rows
-            // (<= g_flat_max uint4) is *flat*: its perms list the nonempty rows
-            // in row order instead (band[kFlatFlag] = 1, band[kFlatRows] = count)
-            uint16_t perm[2][kR];
-            uint16_t band[2][kBandSlots] = {{0}};
-            uint32_t maxlen[2];
-            for (int seg = 0; seg < 2; ++seg) {
-                const std::vector<uint32_t>& q = seg == 0 ? rpn : rp;
-                const int sh = seg == 0 ? 3 : 2;
-                uint32_t key[kR];
-                int hist[257] = {0};
-                for (int k = 0; k < kR; ++k) {
-                    const uint32_t len = (q[k + 1] - q[k]) >> sh;
-                    key[k] = 255u - std::min<uint32_t>(len, 255u);  // descending
-                    ++hist[key[k] + 1];
-                }
-                for (int k = 0; k < 256; ++k) hist[k + 1] += hist[k];
-                for (int k = 0; k < kR; ++k) perm[seg][hist[key[k]]++] = (uint16_t)k;
-                int pos = 0;
-                for (int g = 0; g < kBands; ++g) {
-                    while (pos < kR && ((q[perm[seg][pos] + 1] - q[perm[seg][pos]]) >> sh) >= band_min(g)) ++pos;
-                    band[seg][g + 1] = (uint16_t)pos;
-                }
-                maxlen[seg] = 255u - key[perm[seg][0]];
-            }
-            const bool flat = g_flat_max > 0 && maxlen[0] <= (uint32_t)g_flat_max &&
-                              maxlen[1] <= (uint32_t)g_flat_max && (rpn[kR] >> 3) < 65536u && (rp[kR] >> 2) < 65536u;
-            uint32_t fw[kFlatMeta] = {0};
-            if (flat) {
-                for (int seg = 0; seg < 2; ++seg) {
-                    const std::vector<uint32_t>& q = seg == 0 ? rpn : rp;
-                    const int sh = seg == 0 ? 3 : 2;
-                    int nfr = 0;
-                    uint32_t st[kR + 1];  // uint4 starts of the nonempty rows, then the end
-                    for (int k = 0; k < kR; ++k)
-                        if (q[k + 1] > q[k]) {
-                            st[nfr] = q[k] >> sh;
-                            perm[seg][nfr++] = (uint16_t)k;
-                        }
-                    for (int k = nfr; k < kR; ++k) perm[seg][k] = 0;
-                    const uint32_t Q = q[kR] >> sh;
-                    st[nfr] = Q;
-                    band[seg][kFlatFlag] = nfr > 0 ? 1 : 0;
-                    band[seg][kFlatRows] = (uint16_t)nfr;
-                    // wave w takes the rows starting in [Q w / 8, Q (w + 1) / 8)
-                    uint32_t* f = fw + seg * 2 * (kFlatWaves + 1);
-                    for (int w = 0; w <= kFlatWaves; ++w) {
-                        const uint32_t tq = (uint32_t)(((uint64_t)Q * w) / kFlatWaves);
-                        const int i = (int)(std::lower_bound(st, st + nfr, tq) - st);
-                        f[2 * w] = st[i];
-                        f[2 * w + 1] = (uint32_t)i;
-                    }
-                }
-            }
-            P.tile_fw.insert(P.tile_fw.end(), fw, fw + kFlatMeta);
-            if (flat) {
-                P.tile_frec.push_back((int32_t)(P.frec.size() / (kFrecU4 * 8)));
-                const size_t base = P.frec.size();
-                P.frec.resize(base + kFrecU4 * 8, 0);
-                uint16_t* rec = &P.frec[base];
-                for (int seg = 0; seg < 2; ++seg) {
-                    const std::vector<uint32_t>& q = seg == 0 ? rpn : rp;
-                    const int sh = seg == 0 ? 3 : 2;
-                    const int nfr = band[seg][kFlatRows];
-                    uint16_t* st = rec + seg * (kR + 1);
-                    uint16_t* id = rec + 2 * (kR + 1) + seg * kR;
-                    for (int i = 0; i <= kR; ++i) st[i] = (uint16_t)(i < nfr ? q[perm[seg][i]] >> sh : q[kR] >> sh);
-                    for (int i = 0; i < kR; ++i) id[i] = perm[seg][i];
-                }
-            } else {
-                P.tile_frec.push_back(-1);
-            }
-            P.tile_flat.push_back(flat ? 1 : 0);
-            for (int seg = 0; seg < 2; ++seg) {
-                P.tile_perm.insert(P.tile_perm.end(), perm[seg], perm[seg] + kR);
-                P.tile_band.insert(P.tile_band.end(), band[seg], band[seg] + kBandSlots);
-            }
-            ent += rp[kR];
-            entn += rpn[kR];
+            P.tile_frec.push_back(B.frec_of[i] < 0 ? -1 : frec0 + B.frec_of[i]);
         }
+        P.tile_rp.insert(P.tile_rp.end(), B.rp.begin(), B.rp.end());
+        P.tile_rpn.insert(P.tile_rpn.end(), B.rpn.begin(), B.rpn.end());
+        P.tile_fw.insert(P.tile_fw.end(), B.fw.begin(), B.fw.end());
+        P.tile_perm.insert(P.tile_perm.end(), B.perm.begin(), B.perm.end());
+        P.tile_band.insert(P.tile_band.end(), B.band.begin(), B.band.end());
+        P.tile_flat.insert(P.tile_flat.end(), B.flat.begin(), B.flat.end());
+        P.frec.insert(P.frec.end(), B.frec.begin(), B.frec.end());
+        ent += B.ent_total;
+        entn += B.entn_total;
+        B = BlockTiles();  // free as we go
     }
     P.blk_tile_ptr[P.nrb] = (int32_t)P.tile_J.size();
+    if (g_build_debug)
+        fprintf(stderr, "[plan] %zu tiles: blocks %.3f ms, concat %.3f ms\n", nt_all,
+                std::chrono::duration<double, std::milli>(tp1 - tp0).count(),
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tp1).count());
     P.n_entries_padded = ent;
     P.n_narrow_padded = entn;
     // units: ~4 MiB of payload each on big matrices (measured best on C4),
