@@ -725,14 +725,16 @@ __global__ __launch_bounds__(256) void k_apply_t(const double* __restrict__ in, 
     if (CHOL) {
         // ts / os_ double as scratch for the 16 x 16 algebra before the rows
         // are staged: G in ts[0..15], R in os_[0..15], R^{-1} in ts[16..31]
+        // 32 loads in flight per thread: the grid is < 1 block per CU here,
+        // so registers are free and the dependent round trips are the cost
         double acc = 0.0;
         int r = 0;
-        for (; r + 8 <= nin; r += 8) {
-            double v[8];
+        for (; r + 32 <= nin; r += 32) {
+            double v[32];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) v[u] = gin[(size_t)(r + u) * kSB * kSB + t];
+            for (int u = 0; u < 32; ++u) v[u] = gin[(size_t)(r + u) * kSB * kSB + t];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) acc += v[u];
+            for (int u = 0; u < 32; ++u) acc += v[u];
         }
         for (; r < nin; ++r) acc += gin[(size_t)r * kSB * kSB + t];
         ts[rr][b] = acc;
