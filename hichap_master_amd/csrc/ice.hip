@@ -715,28 +715,32 @@ __device__ __forceinline__ uint4 band_shift_q(const uint4 prev, const uint4 own,
                       __builtin_amdgcn_alignbit(d[Q + 3], d[Q + 2], r), __builtin_amdgcn_alignbit(d[Q + 4], d[Q + 3], r));
 }
 
+// the row's counts shifted back by m slots (its 16-byte group aligned to the
+// window)
 template <int BITS>
-__device__ __forceinline__ double band_dot(const uint4 v, const double* __restrict__ b0, double acc) {
-    const unsigned x[4] = {v.x, v.y, v.z, v.w};
-    constexpr int G = 128 / BITS, PER = 32 / BITS;
-    constexpr unsigned MASK = (1u << BITS) - 1u;
-#pragma unroll
-    for (int k = 0; k < G; ++k) acc = fma((double)((x[k / PER] >> (BITS * (k % PER))) & MASK), b0[k], acc);
-    return acc;
-}
-
-// acc + the dot of the row's m-shifted counts with the lane's window values
-template <int BITS, int G>
-__device__ __forceinline__ double band_dot_shifted(const uint4 prev, const uint4 own, int m, const double (&w)[G],
-                                                   double acc) {
+__device__ __forceinline__ uint4 band_shifted(const uint4 prev, const uint4 own, int m) {
     const int B = 128 - BITS * m, r = B & 31;
     switch (B >> 5) {  // wave-uniform
-        case 0: return band_dot<BITS>(band_shift_q<0>(prev, own, r), w, acc);
-        case 1: return band_dot<BITS>(band_shift_q<1>(prev, own, r), w, acc);
-        case 2: return band_dot<BITS>(band_shift_q<2>(prev, own, r), w, acc);
-        case 3: return band_dot<BITS>(band_shift_q<3>(prev, own, r), w, acc);
-        default: return band_dot<BITS>(band_shift_q<4>(prev, own, 0), w, acc);  // m = 0
+        case 0: return band_shift_q<0>(prev, own, r);
+        case 1: return band_shift_q<1>(prev, own, r);
+        case 2: return band_shift_q<2>(prev, own, r);
+        case 3: return band_shift_q<3>(prev, own, r);
+        default: return band_shift_q<4>(prev, own, 0);  // m = 0
     }
+}
+
+// acc + the dot of half H of a shifted group (dwords 2H, 2H + 1: slots
+// [H G/2, (H + 1) G/2)) with those slots' window values: the window is held
+// in registers half at a time (G = 32 doubles for the 4-bit band was 64
+// VGPRs), same summation order as one pass over the G slots
+template <int BITS, int H>
+__device__ __forceinline__ double band_dot_half(const uint4 v, const double* __restrict__ wh, double acc) {
+    const unsigned x[2] = {H == 0 ? v.x : v.z, H == 0 ? v.y : v.w};
+    constexpr int G2 = 64 / BITS, PER = 32 / BITS;
+    constexpr unsigned MASK = (1u << BITS) - 1u;
+#pragma unroll
+    for (int k = 0; k < G2; ++k) acc = fma((double)((x[k / PER] >> (BITS * (k % PER))) & MASK), wh[k], acc);
+    return acc;
 }
 
 // The band segments of one sweep (uint8 band; 4-bit band, negative and
@@ -821,13 +825,24 @@ __device__ __forceinline__ void band_block(const BandSeg& P, int rblk, int chunk
 #pragma unroll
                 for (int j = 0; j < RJ; ++j) acc[j] += (double)(own[j].x + own[j].y + own[j].z + own[j].w + prev[j].x);
             } else if (cb < c1) {
-                double w[G];
+                uint4 sh[RJ];
+#pragma unroll
+                for (int j = 0; j < RJ; ++j) sh[j] = band_shifted<BITS>(prev[j], own[j], wave + NW * (j0 + j));
                 const double* b0 = bl + bpadg<G>(gb + G * l);
+                {
+                    double w[G / 2];
 #pragma unroll
-                for (int k = 0; k < G; ++k) w[k] = b0[k];
+                    for (int k = 0; k < G / 2; ++k) w[k] = b0[k];
 #pragma unroll
-                for (int j = 0; j < RJ; ++j)
-                    acc[j] = band_dot_shifted<BITS, G>(prev[j], own[j], wave + NW * (j0 + j), w, acc[j]);
+                    for (int j = 0; j < RJ; ++j) acc[j] = band_dot_half<BITS, 0>(sh[j], w, acc[j]);
+                }
+                {
+                    double w[G / 2];
+#pragma unroll
+                    for (int k = 0; k < G / 2; ++k) w[k] = b0[G / 2 + k];
+#pragma unroll
+                    for (int j = 0; j < RJ; ++j) acc[j] = band_dot_half<BITS, 1>(sh[j], w, acc[j]);
+                }
             }
         }
 #pragma unroll
@@ -867,7 +882,7 @@ __device__ __forceinline__ void band_any(const BandSegs& S, int rblk, int y, Ban
 }
 
 template <int ABL, int ROWS>
-__global__ __launch_bounds__(kBandThreads) void k_sweep_bands(BandSegs S, long long nloc, long long row_lo,
+__global__ __launch_bounds__(kBandThreads, 4) void k_sweep_bands(BandSegs S, long long nloc, long long row_lo,
                                                               long long n_bins, const uint8_t* __restrict__ act,
                                                               const uint16_t* __restrict__ row_group,
                                                               const double* __restrict__ b,
