@@ -720,11 +720,19 @@ __global__ __launch_bounds__(256) void k_apply_t(const double* __restrict__ in, 
     __shared__ double cm[8 * kSB * kSB], ri[kSB * kSB];
     const int t = threadIdx.x, rr = t / kSB, b = t % kSB;
     const long long r0 = (long long)blockIdx.x * kApplyRows;
+    constexpr int PER = kApplyRows * kSB / 256;  // row values staged per thread
+    double pre[PER];
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {  // issued first: they fly during the reduction / factorisation
+        const int e = t + 256 * q;
+        const long long i = r0 + e / kSB;
+        pre[q] = i < n ? in[i * kSB + e % kSB] : 0.0;
+    }
     if (Cm)
         for (int e = t; e < nb * kSB * kSB; e += 256) cm[e] = Cm[e];
     if (CHOL) {
-        // ts / os_ double as scratch for the 16 x 16 algebra before the rows
-        // are staged: G in ts[0..15], R in os_[0..15], R^{-1} in ts[16..31]
+        // ts doubles as scratch for the 16 x 16 Gram matrix before the rows
+        // are staged; R goes to ri.
         // 32 loads in flight per thread: the grid is < 1 block per CU here,
         // so registers are free and the dependent round trips are the cost
         double acc = 0.0;
@@ -738,50 +746,53 @@ __global__ __launch_bounds__(256) void k_apply_t(const double* __restrict__ in, 
         }
         for (; r < nin; ++r) acc += gin[(size_t)r * kSB * kSB + t];
         ts[rr][b] = acc;
-        os_[rr][b] = 0.0;
-        ts[16 + rr][b] = 0.0;
         __syncthreads();
-        __shared__ double shift;
-        __shared__ int bad;
-        if (t == 0) {
-            double tr = 0.0;
-            for (int i = 0; i < kSB; ++i) tr += ts[i][i];
-            shift = shift_scale > 0 ? shift_scale * tr : 0.0;
-            bad = 0;
-        }
-        __syncthreads();
-        if (rr == b) ts[rr][rr] += shift;
-        __syncthreads();
+        double tr = 0.0;
+#pragma unroll
+        for (int i = 0; i < kSB; ++i) tr += ts[i][i];
+        const double shift = shift_scale > 0 ? shift_scale * tr : 0.0;
+        // right-looking Cholesky inside each wave, registers + shuffles (no
+        // block barriers): lane l holds column c = l % 16 of rows
+        // (l / 16) + 4 q, q = 0..3; every wave computes the same R, wave 0
+        // publishes it
+        const int lane = t & 63, c = lane & 15, a0 = lane >> 4;
+        double g[4], rrow[kSB];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) g[q] = ts[a0 + 4 * q][c] + (a0 + 4 * q == c ? shift : 0.0);
+        bool okall = true;
+#pragma unroll
         for (int j = 0; j < kSB; ++j) {
-            const double d = ts[j][j];
+            const double d = __shfl(g[j >> 2], (j & 3) * 16 + j, 64);
             const bool okd = d > 0;
+            okall = okall && okd;
             const double rjj = okd ? sqrt(d) : 1.0;
-            if (t == 0 && !okd) bad = 1;
-            if (rr == j && b >= j) os_[j][b] = b == j ? rjj : ts[j][b] / rjj;
-            __syncthreads();
-            if (rr > j && b > j) ts[rr][b] -= os_[j][rr] * os_[j][b];
-            __syncthreads();
-        }
-        for (int i = kSB - 1; i >= 0; --i) {
-            if (rr == i) {
-                double v = i == b ? 1.0 : 0.0;
-                for (int k = i + 1; k < kSB; ++k) v -= os_[i][k] * ts[16 + k][b];
-                ts[16 + i][b] = v / os_[i][i];
+            const double gjc = __shfl(g[j >> 2], (j & 3) * 16 + c, 64);
+            const double rjc = c == j ? rjj : (c > j ? gjc / rjj : 0.0);
+            rrow[j] = rjc;  // R[j][c]
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int a = a0 + 4 * q;
+                const double rja = __shfl(rjc, a, 64);  // R[j][a]
+                if (a > j && c > j) g[q] -= rja * rjc;
             }
-            __syncthreads();
         }
-        ri[t] = bad ? (rr == b ? 1.0 : 0.0) : ts[16 + rr][b];
-        if (blockIdx.x == 0) {
-            Rout[t] = bad ? (rr == b ? 1.0 : 0.0) : os_[rr][b];
-            if (t == 0 && bad) *fail = 1;
+        if (t < kSB) {  // wave 0, lanes 0..15: column c = t
+#pragma unroll
+            for (int j = 0; j < kSB; ++j) {
+                const double rv = okall ? rrow[j] : (j == c ? 1.0 : 0.0);
+                ri[j * kSB + c] = rv;  // R (upper), row-major
+                if (blockIdx.x == 0) Rout[j * kSB + c] = rv;
+            }
+            if (t == 0 && blockIdx.x == 0 && !okall) *fail = 1;
         }
-        __syncthreads();  // scratch reads done before the rows are staged
+        __syncthreads();  // R published; scratch reads done before the rows are staged
     } else if (Rinv) {
         ri[t] = Rinv[t];
     }
-    for (int e = t; e < kApplyRows * kSB; e += 256) {
-        const long long i = r0 + e / kSB;
-        ts[e / kSB][e % kSB] = i < n ? in[i * kSB + e % kSB] : 0.0;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const int e = t + 256 * q;
+        ts[e / kSB][e % kSB] = pre[q];
     }
     __syncthreads();
     if (Cm) {
@@ -806,19 +817,41 @@ __global__ __launch_bounds__(256) void k_apply_t(const double* __restrict__ in, 
         for (int q = 0; q < kApplyRows / 16; ++q) ts[rr + 16 * q][b] = acc[q];
         __syncthreads();
     }
+    if (CHOL) {
+        // out_row = row R^{-1}: forward substitution x R = row, one thread
+        // per row (no R^{-1}, none of its 16 barrier steps)
+        if (t < kApplyRows) {
+            const long long i = r0 + t;
+            double x[kSB];
 #pragma unroll
-    for (int q = 0; q < kApplyRows / 16; ++q) {
-        const int r = rr + 16 * q;
-        double v = ts[r][b];
-        if (CHOL || Rinv) {
-            v = 0.0;
+            for (int c = 0; c < kSB; ++c) {
+                double v = ts[t][c];
 #pragma unroll
-            for (int a = 0; a < kSB; ++a) v = fma(ts[r][a], ri[a * kSB + b], v);
+                for (int a = 0; a < c; ++a) v -= x[a] * ri[a * kSB + c];
+                x[c] = v / ri[c * kSB + c];
+            }
+#pragma unroll
+            for (int c = 0; c < kSB; ++c) {
+                const double v = i < n ? x[c] : 0.0;
+                os_[t][c] = v;
+                if (i < n) out[i * kSB + c] = v;
+            }
         }
-        const long long i = r0 + r;
-        if (i >= n) v = 0.0;
-        os_[r][b] = v;
-        if (i < n) out[i * kSB + b] = v;
+    } else {
+#pragma unroll
+        for (int q = 0; q < kApplyRows / 16; ++q) {
+            const int r = rr + 16 * q;
+            double v = ts[r][b];
+            if (Rinv) {
+                v = 0.0;
+#pragma unroll
+                for (int a = 0; a < kSB; ++a) v = fma(ts[r][a], ri[a * kSB + b], v);
+            }
+            const long long i = r0 + r;
+            if (i >= n) v = 0.0;
+            os_[r][b] = v;
+            if (i < n) out[i * kSB + b] = v;
+        }
     }
     __syncthreads();
     if (gpart) {
