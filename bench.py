@@ -847,8 +847,8 @@ def main():
     st = ice.IceState(m, opts)
     stream = torch.cuda.current_stream().cuda_stream
     if world > 1:
-        # (the sweep's three streams are the library default for shards of
-        # >= 1 GB payload: C4 at N=8 has 1.85 GB per shard)
+        # (shards below 8 GB of payload sweep on one stream, the library
+        # default: C4 at N=8 has 1.6-1.9 GB per shard)
         if not os.environ.get("HH_NO_REFINE"):
             # setup, untimed: one measured refinement of the row partition
             # (payload bytes mis-price rows whose bytes sweep at different rates)
@@ -992,8 +992,11 @@ def main():
                 traffic_src = f"{traffic_src} (scaled by shard payload)" if traffic else None
             phys = traffic if traffic else real_b
             achieved = phys / sweep_avg / 1e9
+            pb = inf["payload_bytes"]
             out["roofline"] = {"bound": "hbm", "kernel": ("ice sweep span: k_sweep_flat | k_sweep_tiled | k_sweep_bands (uint8 + 2 x 4-bit segments) on three streams"
-                                         if inf["payload_bytes"] >= (1 << 30) else
+                                         if pb >= (8 << 30) else
+                                         "ice sweep: k_sweep_tiled, k_sweep_flat, k_sweep_bands (uint8 + 2 x 4-bit segments) on one stream"
+                                         if pb >= (1 << 30) else
                                          "ice sweep: k_sweep_all (tiled + band + flat bodies in one launch)")
                                + " (HIP events around the sweep; rocprof per-sweep span: tools/sweep_span.py)",
                                "achieved": achieved,

@@ -1176,9 +1176,11 @@ static int g_sweep_ablate = 0;
 // +2 %, profiles/r1v8_knobs_split.log).  All write disjoint partials.
 static int g_band_concurrent = 1;  // dense-band sweep on a side stream, beside the tiles
 static int g_split_tiles = 1;      // with band_concurrent: tiled kernel on a second side stream
-// below this payload the fork / join costs more than the overlap gains (C2,
-// 0.2 GB: 4 620 -> 4 300 it/s with three streams; N=8 C4 shards, 1.85 GB, gain)
-static int64_t g_conc_min_bytes = 1LL << 30;
+// below this payload the fork / join costs more than the overlap gains.
+// Round 2, with the band kernel at 8 waves per SIMD: one stream is 4-5 %
+// faster for C3 (3.0 GB) and the N = 8 C4 shards (1.6-1.9 GB), three streams
+// 0.3 % faster for the whole C4 matrix (14.8 GB; profiles/r2_conc_probe.log)
+static int64_t g_conc_min_bytes = 8LL << 30;
 static int g_band_rows = 0;   // rows per band block: 0 = auto (64 or 256)
 static int g_band_fused = 1;  // the band segments in one launch
 static int g_sweep_single = -1;  // whole sweep in one launch: -1 auto (below g_single_max_bytes), 0 off, 1 on

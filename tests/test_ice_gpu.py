@@ -392,7 +392,7 @@ def test_band_concurrent_bitwise(ice, conc, split):
     finally:
         _lib.call("hh_tune", b"band_concurrent", 1)
         _lib.call("hh_tune", b"split_tiles", 1)
-        _lib.call("hh_tune", b"conc_min_bytes", 1 << 30)
+        _lib.call("hh_tune", b"conc_min_bytes", 8 << 30)
     np.testing.assert_array_equal(w1, w0)
     assert s1["iters"] == s0["iters"]
 
