@@ -103,18 +103,19 @@ __global__ void k_px_keyptr(const unsigned long long* __restrict__ keys, long lo
 }
 
 // lower-half keys of the local rows (order fixed later by the sort)
-// One block per kLowChunk pixels: count the block's lower-half keys, ONE
-// atomic per block for its output range (one per wave was 12.5 M same-address
-// atomics at C3: 150 ms), then write them in pixel order within the block.
-// The order across blocks does not matter: the keys are unique and sorted next.
+// One block per kLowChunk pixels.  PASS 0: the block's number of lower-half
+// keys -> cnt[block]; PASS 1: the keys at base[block] (exclusive scan of the
+// counts) in pixel order.  The key array is then in index order, so the sort
+// only has to order the row bits (stable LSD: ties keep index order) -- 3
+// radix passes instead of 6-7 -- and no same-address atomics are involved.
 constexpr int kLowItems = 16;
 constexpr int kLowChunk = 256 * kLowItems;
+template <int PASS>
 __global__ __launch_bounds__(256) void k_px_lowkeys(const int32_t* __restrict__ A, const int32_t* __restrict__ B,
                                                     const uint32_t* __restrict__ kc, long long nnz, long long row_lo,
                                                     long long row_hi, int ib, unsigned long long* __restrict__ keys,
-                                                    unsigned long long* __restrict__ n_keys) {
+                                                    long long* __restrict__ cnt_or_base) {
     __shared__ unsigned wcnt[kLowItems][4];
-    __shared__ unsigned long long base_sh;
     const long long c0 = (long long)blockIdx.x * kLowChunk;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     unsigned long long mk[kLowItems];
@@ -138,10 +139,11 @@ __global__ __launch_bounds__(256) void k_px_lowkeys(const int32_t* __restrict__ 
                 wcnt[k][w] = tot;  // exclusive offset within the block
                 tot += c;
             }
-        base_sh = tot ? atomicAdd(n_keys, (unsigned long long)tot) : 0ull;
+        if (PASS == 0) cnt_or_base[blockIdx.x] = tot;
     }
+    if (PASS == 0) return;
     __syncthreads();
-    const unsigned long long base = base_sh;
+    const unsigned long long base = (unsigned long long)cnt_or_base[blockIdx.x];
 #pragma unroll
     for (int k = 0; k < kLowItems; ++k) {
         if (!((mk[k] >> lane) & 1ull)) continue;
@@ -432,18 +434,24 @@ void build_from_device_pixels(const Id* b1, const Id* b2, const Cnt* cnt, int64_
     int rbits = 1;
     while (rbits < 40 && ((int64_t)1 << rbits) < std::max<int64_t>(nloc, 2)) ++rbits;
     HH_REQUIRE(ib + rbits <= 64, "pixel table too large for the 64-bit lower-half keys");
-    DBuf<unsigned long long> nkeys(1);
-    nkeys.zero(s);
     DBuf<unsigned long long> keys(std::max<int64_t>(nnz, 1));
-    if (nnz > 0)
-        hipLaunchKernelGGL(k_px_lowkeys, dim3((unsigned)((nnz + kLowChunk - 1) / kLowChunk)), dim3(256), 0, s, dA.p,
-                           dB.p, dkc.p,
-                           (long long)nnz, (long long)row_lo, (long long)row_hi, ib, keys.p, nkeys.p);
     unsigned long long hn = 0;
-    nkeys.download(&hn, 1, s);
-    HIP_CHECK(hipStreamSynchronize(s));
+    if (nnz > 0) {
+        const long long nblk = (nnz + kLowChunk - 1) / kLowChunk;
+        DBuf<long long> bcnt(nblk + 1), bbase(nblk + 1);
+        DBuf<unsigned long long> ntot(1);
+        HIP_CHECK(hipMemsetAsync(bcnt.p + nblk, 0, sizeof(long long), s));
+        hipLaunchKernelGGL(k_px_lowkeys<0>, dim3((unsigned)nblk), dim3(256), 0, s, dA.p, dB.p, dkc.p, (long long)nnz,
+                           (long long)row_lo, (long long)row_hi, ib, keys.p, bcnt.p);
+        dev_excl_scan_i64(bcnt.p, bbase.p, nblk + 1, ntot.p, s);
+        hipLaunchKernelGGL(k_px_lowkeys<1>, dim3((unsigned)nblk), dim3(256), 0, s, dA.p, dB.p, dkc.p, (long long)nnz,
+                           (long long)row_lo, (long long)row_hi, ib, keys.p, bbase.p);
+        HIP_CHECK(hipGetLastError());
+        ntot.download(&hn, 1, s);
+        HIP_CHECK(hipStreamSynchronize(s));
+    }
     phase("lower keys");
-    dev_sort_u64(keys, (int64_t)hn, ib + rbits, s);
+    dev_sort_u64(keys, (int64_t)hn, rbits, s, ib);  // keys in index order: only the row bits
     phase("radix sort");
     DBuf<long long> lo_ptr(nloc + 1);
     hipLaunchKernelGGL(k_px_keyptr, dim3((unsigned)((hn + 1 + 255) / 256)), dim3(256), 0, s, keys.p, (long long)hn, ib,

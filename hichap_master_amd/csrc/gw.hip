@@ -165,16 +165,16 @@ __global__ __launch_bounds__(256) void k_gw_hstats(const int32_t* __restrict__ r
 }
 
 // off-diagonal cells keyed by column: (col << ib) | index.  One block per
-// kColChunk cells and ONE atomic per block for its output range (one per
-// wave was ~23 M same-address atomics at 10 kb diploid); the keys are unique
-// and sorted next, so the order across blocks does not matter.
+// kColChunk cells; PASS 0 counts the block's keys, PASS 1 writes them at the
+// scanned base in cell order, so the keys arrive in index order and the sort
+// orders only the column bits (stable: 3 radix passes instead of 7).
 constexpr int kColItems = 16;
 constexpr int kColChunk = 256 * kColItems;
+template <int PASS>
 __global__ __launch_bounds__(256) void k_gw_colkeys(const int32_t* __restrict__ r, const int32_t* __restrict__ c,
                                                     long long nnz, int ib, unsigned long long* __restrict__ keys,
-                                                    unsigned long long* __restrict__ n_keys) {
+                                                    long long* __restrict__ cnt_or_base) {
     __shared__ unsigned wcnt[kColItems][4];
-    __shared__ unsigned long long base_sh;
     const long long c0 = (long long)blockIdx.x * kColChunk;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     unsigned long long mk[kColItems];
@@ -193,10 +193,11 @@ __global__ __launch_bounds__(256) void k_gw_colkeys(const int32_t* __restrict__ 
                 wcnt[k][w] = tot;
                 tot += n;
             }
-        base_sh = tot ? atomicAdd(n_keys, (unsigned long long)tot) : 0ull;
+        if (PASS == 0) cnt_or_base[blockIdx.x] = tot;
     }
+    if (PASS == 0) return;
     __syncthreads();
-    const unsigned long long base = base_sh;
+    const unsigned long long base = (unsigned long long)cnt_or_base[blockIdx.x];
 #pragma unroll
     for (int k = 0; k < kColItems; ++k) {
         if (!((mk[k] >> lane) & 1ull)) continue;
@@ -462,18 +463,24 @@ void gw_create(hh_gw& G, const Id* t1, const Id* t2, const Cnt* tv, int64_t t_nn
     int cbits = 1;
     while (cbits < 40 && ((int64_t)1 << cbits) < 2 * n) ++cbits;
     HH_REQUIRE(G.ib + cbits <= 64, "haplotype matrix too large for 64-bit column keys");
-    DBuf<unsigned long long> nk(1);
-    nk.zero(s);
     G.keys.alloc(std::max<int64_t>(h_nnz, 1));
-    if (h_nnz > 0)
-        hipLaunchKernelGGL(k_gw_colkeys, dim3((unsigned)((h_nnz + kColChunk - 1) / kColChunk)), dim3(256), 0, s,
-                           G.R.p, G.C.p,
-                           (long long)h_nnz, G.ib, G.keys.p, nk.p);
     unsigned long long hn = 0;
-    nk.download(&hn, 1, s);
-    HIP_CHECK(hipStreamSynchronize(s));
+    if (h_nnz > 0) {
+        const long long nblk = (h_nnz + kColChunk - 1) / kColChunk;
+        DBuf<long long> bcnt(nblk + 1), bbase(nblk + 1);
+        DBuf<unsigned long long> ntot(1);
+        HIP_CHECK(hipMemsetAsync(bcnt.p + nblk, 0, sizeof(long long), s));
+        hipLaunchKernelGGL(k_gw_colkeys<0>, dim3((unsigned)nblk), dim3(256), 0, s, G.R.p, G.C.p, (long long)h_nnz,
+                           G.ib, G.keys.p, bcnt.p);
+        dev_excl_scan_i64(bcnt.p, bbase.p, nblk + 1, ntot.p, s);
+        hipLaunchKernelGGL(k_gw_colkeys<1>, dim3((unsigned)nblk), dim3(256), 0, s, G.R.p, G.C.p, (long long)h_nnz,
+                           G.ib, G.keys.p, bbase.p);
+        HIP_CHECK(hipGetLastError());
+        ntot.download(&hn, 1, s);
+        HIP_CHECK(hipStreamSynchronize(s));
+    }
     G.n_keys = (int64_t)hn;
-    dev_sort_u64(G.keys, G.n_keys, G.ib + cbits, s);
+    dev_sort_u64(G.keys, G.n_keys, cbits, s, G.ib);  // keys in index order: only the column bits
     G.cptr.alloc(2 * n + 1);
     hipLaunchKernelGGL(k_px_keyptr_gw, dim3((unsigned)((hn + 1 + 255) / 256)), dim3(256), 0, s, G.keys.p,
                        (long long)hn, G.ib, (long long)(2 * n), G.cptr.p);

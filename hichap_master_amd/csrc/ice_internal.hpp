@@ -260,7 +260,9 @@ void upload_plan(const TilePlan& P, hh_matrix& m, hipStream_t s);
 // Device helpers shared with the pair binner (pairs.hip): stable LSD radix
 // sort of n 64-bit keys on their low `bits` bits (synchronous), exclusive
 // scan of n int64 values (*total_dev = the sum, may be null; asynchronous).
-void dev_sort_u64(DBuf<unsigned long long>& keys, int64_t n, int bits, hipStream_t s);
+// stable LSD radix sort of the key bits [lo_bit, lo_bit + bits) (keys whose
+// lower bits are already in order -- an index -- need only the upper ones)
+void dev_sort_u64(DBuf<unsigned long long>& keys, int64_t n, int bits, hipStream_t s, int lo_bit = 0);
 void dev_excl_scan_i64(const long long* in, long long* out, long long n, unsigned long long* total_dev, hipStream_t s);
 // Device build from a host pixel table (build.hip); false = not a sorted
 // upper-triangle table (nothing built).  g_host_build forces the host builder.

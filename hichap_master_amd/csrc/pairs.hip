@@ -1299,7 +1299,7 @@ static void feed_device(hh_binner* B, const char* text, int64_t nbytes, const hh
     raise_parse_error(B, tv, lines_before, s);
 }
 
-static void sort_keys(DBuf<unsigned long long>& keys, int64_t n, int bits, hipStream_t s) {
+static void sort_keys(DBuf<unsigned long long>& keys, int64_t n, int bits, hipStream_t s, int lo_bit = 0) {
     if (n <= 1) return;
     const long long tiles = (n + kScanTile - 1) / kScanTile;
     DBuf<unsigned long long> tmp(n);
@@ -1307,7 +1307,7 @@ static void sort_keys(DBuf<unsigned long long>& keys, int64_t n, int bits, hipSt
     unsigned long long* a = keys.p;
     unsigned long long* b = tmp.p;
     int passes = 0;
-    for (int shift = 0; shift < bits; shift += 8, ++passes) {
+    for (int shift = lo_bit; shift < lo_bit + bits; shift += 8, ++passes) {
         {
             HH_KTIME("k_rs_hist", s);
             hipLaunchKernelGGL(k_rs_hist, dim3((unsigned)tiles), dim3(kScanThreads), 0, s, a, (long long)n, shift,
@@ -1327,7 +1327,9 @@ static void sort_keys(DBuf<unsigned long long>& keys, int64_t n, int bits, hipSt
 }
 
 // Shared with the device matrix build (build.hip, ice_internal.hpp).
-void dev_sort_u64(DBuf<unsigned long long>& keys, int64_t n, int bits, hipStream_t s) { sort_keys(keys, n, bits, s); }
+void dev_sort_u64(DBuf<unsigned long long>& keys, int64_t n, int bits, hipStream_t s, int lo_bit) {
+    sort_keys(keys, n, bits, s, lo_bit);
+}
 void dev_excl_scan_i64(const long long* in, long long* out, long long n, unsigned long long* total_dev, hipStream_t s) {
     exclusive_scan<long long, long long>(in, out, n, total_dev, s);
 }
