@@ -916,6 +916,8 @@ def append_dataset(path, group, name, data, attrs=None):
         if head[:4] != b"TREE" or head[5] != 0:
             raise H5Error("in-place append supports one-level group B-trees")
         n = struct.unpack_from("<H", head, 6)[0]
+        if n == 0:
+            raise H5Error("in-place append into a group without a symbol table node")
         body = bytearray(F.read(bt + 24, (2 * n + 1) * 8))
         size, free, hdata = F.local_heap(heap)
         seg = bytearray(F.read(hdata, size))
