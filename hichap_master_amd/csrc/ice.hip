@@ -777,7 +777,7 @@ __device__ __forceinline__ void band_block(const BandSeg& P, int rblk, int chunk
     const int nr = (int)min((long long)ROWS, nloc - r0);
     const long long g0 = row_lo + r0 + P.dlo + s0;  // bias column of window index 0
     const int len = ((nr + G - 1) & ~(G - 1)) + (s1 - s0);
-    for (int k = threadIdx.x; k < len; k += kBandThreads) {
+    for (int k = threadIdx.x; k < (ABL == 2 ? 0 : len); k += kBandThreads) {  // ABL 2: no staging (timing)
         // the band multiplies implicit zeros too: a NaN bias (an empty group
         // in cis-only mode, whose bins no stored pixel touches) must read 0
         const long long c = g0 + k;
@@ -904,7 +904,8 @@ __global__ __launch_bounds__(kSweepThreads, 4) void k_sweep_all(TileDev T, const
                                                               const uint16_t* __restrict__ row_group,
                                                               const double* __restrict__ b, long long n_bins,
                                                               double* __restrict__ part,
-                                                              double* __restrict__ bpart) {
+                                                              double* __restrict__ bpart,
+                                                              unsigned long long* __restrict__ trace) {
     __shared__ __attribute__((aligned(16))) union Lds {
         TiledLds t;
         FlatLds f;
@@ -912,6 +913,7 @@ __global__ __launch_bounds__(kSweepThreads, 4) void k_sweep_all(TileDev T, const
     } L;
     // grid: [tiled units | band blocks (n_band = band_rb x chunks) | flat units]
     const int x = blockIdx.x;
+    const unsigned long long t0 = trace ? wall_clock64() : 0ull;
     if (x < n_tiled) {
         sweep_tiled_unit<NB, ABL>(T, act, T.u_order[x], b, n_bins, part, L.t);
     } else if (x < n_tiled + n_band) {
@@ -919,6 +921,14 @@ __global__ __launch_bounds__(kSweepThreads, 4) void k_sweep_all(TileDev T, const
         band_any<ABL, 64>(S, y % band_rb, y / band_rb, L.band, nloc, row_lo, n_bins, act, row_group, b, bpart);
     } else {
         sweep_flat_unit<U, ABL>(T, act, T.u_order[x - n_band], b, n_bins, part, L.f);  // flat units follow the tiled
+    }
+    if (trace) {  // diagnostic block timeline (hh_tune "sweep_trace"): start, end, CU of each block
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            trace[3 * (size_t)x] = t0;
+            trace[3 * (size_t)x + 1] = wall_clock64();
+            trace[3 * (size_t)x + 2] = (unsigned long long)__smid();
+        }
     }
 }
 
@@ -1185,6 +1195,9 @@ static int g_band_rows = 0;   // rows per band block: 0 = auto (64 or 256)
 static int g_band_fused = 1;  // the band segments in one launch
 static int g_sweep_single = -1;  // whole sweep in one launch: -1 auto (below g_single_max_bytes), 0 off, 1 on
 static int64_t g_single_max_bytes = 1LL << 30;
+// diagnostic: per-block timeline of the last single-launch sweep (hh_sweep_trace)
+static unsigned long long* g_trace = nullptr;
+static int64_t g_trace_cap = 0, g_trace_n = 0;
 
 template <int NB, int ABL>
 static void launch_sweep(const hh_matrix* m, const uint8_t* act, const double* b, double* part, hipStream_t s,
@@ -1282,9 +1295,14 @@ static void sweep_single(hh_ice* S, hipStream_t s) {
     const long long grid = n_tiled + n_band + n_flat;
     if (!grid) return;
     HH_REQUIRE(grid < (1LL << 31), "sweep grid too large for one launch");
-    hipLaunchKernelGGL((k_sweep_all<2, kFlatU, 0>), dim3((unsigned)grid), dim3(kSweepThreads), 0, s, m->dev(),
-                       S->act(), n_tiled, (int)n_band, segs, band_rb, (long long)S->nloc, (long long)m->row_lo,
-                       m->row_group.p, S->bias.p, (long long)m->n_bins, S->part.p, S->bpart.p);
+    unsigned long long* trace = grid <= g_trace_cap ? g_trace : nullptr;
+    if (trace) g_trace_n = grid;
+    auto kern = g_sweep_ablate == 1   ? k_sweep_all<2, kFlatU, 1>
+                : g_sweep_ablate == 2 ? k_sweep_all<2, kFlatU, 2>
+                                      : k_sweep_all<2, kFlatU, 0>;  // ablations: timing diagnostics only
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kSweepThreads), 0, s, m->dev(), S->act(), n_tiled,
+                       (int)n_band, segs, band_rb, (long long)S->nloc, (long long)m->row_lo, m->row_group.p,
+                       S->bias.p, (long long)m->n_bins, S->part.p, S->bpart.p, trace);
     HIP_CHECK(hipGetLastError());
 }
 
@@ -1298,7 +1316,7 @@ static void marg_weighted(hh_ice* S, double* out, hipStream_t s, bool timed, int
         // kernel leaves idle (both are HBM-bound; neither saturates alone)
         const int64_t bytes = 4 * m->n_slots + 2 * m->n_slots_narrow + (int64_t)m->band.n + (int64_t)m->band4.n;
         const bool conc = g_band_concurrent && S->nch && S->nloc && m->n_units && bytes >= g_conc_min_bytes;
-        const bool single = g_sweep_ablate == 0 && g_sweep_nb == 2 &&
+        const bool single = g_sweep_nb == 2 &&
                             (g_sweep_single == 1 || (g_sweep_single == -1 && bytes < g_single_max_bytes));
         if (single) {
             sweep_single(S, s);
@@ -1406,6 +1424,13 @@ int hh_tune(const char* key, int64_t value) {
             HH_REQUIRE(value == 0 || value == 64 || value == 128 || value == 256,
                        "band_rows in {0 (auto), 64, 128, 256}");
             g_band_rows = (int)value;
+        } else if (k == "sweep_trace") {
+            HH_REQUIRE(value >= 0 && value < (1LL << 31), "sweep_trace: block capacity >= 0");
+            if (g_trace) HIP_CHECK(hipFree(g_trace));
+            g_trace = nullptr;
+            g_trace_cap = g_trace_n = 0;
+            if (value) HIP_CHECK(hipMalloc(&g_trace, (size_t)value * 3 * sizeof(unsigned long long)));
+            g_trace_cap = value;
         } else if (k == "sweep_single") {
             HH_REQUIRE(value >= -1 && value <= 1, "sweep_single in {-1 (auto), 0, 1}");
             g_sweep_single = (int)value;
@@ -1662,6 +1687,18 @@ int hh_ice_last_sweep_timing(const hh_ice* S, double* sweep_ms_total, int32_t* s
         if (sweep_ms_total) *sweep_ms_total = S->sweep_ms;
         if (sweep_launches) *sweep_launches = S->sweep_launches;
         if (iter_ms_total) *iter_ms_total = S->iter_ms;
+    });
+}
+
+int hh_sweep_trace(uint64_t* out, int64_t cap, int64_t* n) {
+    return guard([&] {
+        HH_REQUIRE(n, "null");
+        *n = g_trace_n;
+        if (out && g_trace && g_trace_n) {
+            HH_REQUIRE(cap >= 3 * g_trace_n, "sweep_trace: out holds 3 x blocks words");
+            HIP_CHECK(hipDeviceSynchronize());
+            HIP_CHECK(hipMemcpy(out, g_trace, (size_t)g_trace_n * 3 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+        }
     });
 }
 

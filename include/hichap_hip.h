@@ -59,8 +59,14 @@ int hh_device_copy(void* dst, const void* src, int64_t bytes, void* stream);
  * "sweep_nb" in {1,2,4,8} (row batches in flight per
  * wave), "unit_entries" (work-unit size used by later matrix builds),
  * "sweep_ablate" 0/1/2 (timing ablations only: 1 skips the LDS gathers,
- * 2 skips the b staging; results are wrong while set). */
+ * 2 skips the b staging; results are wrong while set), "sweep_trace" n
+ * (diagnostic: record start / end wall clock and CU of each block of the
+ * single-launch sweep when its grid has <= n blocks; 0 frees the buffer). */
 int hh_tune(const char* key, int64_t value);
+/* The last traced single-launch sweep: *n blocks; out (cap >= 3 n words) gets
+ * (start, end, cu) per block in grid order (tiled units | band blocks | flat
+ * units), wall-clock ticks (100 MHz).  Diagnostic, synchronising. */
+int hh_sweep_trace(uint64_t* out, int64_t cap, int64_t* n);
 /* Kernel timing (measurement only): while enabled, the dense-path launches
  * (k_rowstats, k_symvc1..3, k_syrk, k_cor_mul, k_select_stats, k_di,
  * k_gap_scan) are bracketed by HIP events on their stream; query returns the
