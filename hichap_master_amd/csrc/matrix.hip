@@ -264,10 +264,11 @@ TilePlan plan_tiles(const uint16_t* cntw, const uint16_t* cntn, int64_t nloc, in
     const int64_t unit_cap = g_unit_entries > 0 ? g_unit_entries
                                                 : std::max<int64_t>(1 << 15, std::min<int64_t>(1 << 20, words / 4096));
     // the per-tile cost only where the units are small (shards, single
-    // chromosomes): at the 4 MiB unit cap (whole C4) it changes no time but
-    // splits the flat units 3x, and each unit re-stages its bias slices
-    // (flat-kernel PMC traffic 7.05 -> 7.96 GB per sweep)
-    const int64_t tile_cost = unit_cap < (1 << 20) ? g_tile_cost : 0;
+    // chromosomes, C3, C4 shards): on the whole C4 matrix (unit cap 446 K
+    // words) it changes no time but splits the flat units 3x, and each unit
+    // re-stages its bias slices (flat-kernel PMC traffic 7.05 -> 7.96 GB per
+    // sweep, profiles/r2_tile_cost_ab.log for the time)
+    const int64_t tile_cost = unit_cap < (3 << 17) ? g_tile_cost : 0;
     auto tile_words = [&](int32_t t, int k0, int k1) -> int64_t {
         const uint32_t* a = &P.tile_rp[(size_t)t * (kR + 1)];
         const uint32_t* b = &P.tile_rpn[(size_t)t * (kR + 1)];
