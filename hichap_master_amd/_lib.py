@@ -172,6 +172,11 @@ def load(path: str = LIB_PATH):
         fn.restype = res
         fn.argtypes = args
     _lib = lib
+    # measurement knobs for a whole process (A/B runs of tests and benches):
+    # HH_TUNE="key=value,key=value" -> hh_tune at load
+    for kv in filter(None, os.environ.get("HH_TUNE", "").split(",")):
+        k, v = kv.split("=")
+        call("hh_tune", k.strip().encode(), int(v))
     return lib
 
 
