@@ -8,10 +8,14 @@
 //                sum(count * b[col]) in fp64 -> part[seg]          [HBM bound]
 //   K2 k_marg    per local row: marg = b_r * (sum_seg part + 2 * diag * b_r)
 //                (cooler's bincount(bin1) + bincount(bin2))
-//   K3 k_stats1  per tile of 1024 bins: nonzero count and sum
-//      k_stats2  per tile: sum of squared deviations from the group mean
-//      k_update  per tile: b /= marg/mean (marg==0 -> 1); first tile of the
-//                group records var/mean/iters and the next active flag.
+//   K3 stats     per stats tile (a 512-row block cut at group boundaries):
+//                nonzero count and sum -- fused into k_marg when one GPU
+//                holds every row (else k_stats1 on the gathered vector); the
+//                last block to finish reduces them per group (count, sum)
+//      k_update  per stats tile: b /= marg/mean (marg==0 -> 1) and the tile's
+//                sum of squared deviations; the last block to finish reduces
+//                those per group and records var/mean/iters and the next
+//                active flag (2 launches after the sweep instead of 4).
 // All reductions use fixed trees -> bitwise deterministic, and independent of
 // how rows are sharded across GPUs.
 #include <algorithm>
@@ -22,7 +26,6 @@
 #include "ice_internal.hpp"
 
 namespace hh {
-constexpr int kTile = 1024;
 constexpr int kThreads = 256;
 
 // ---------------------------------------------------------------- K1
@@ -940,6 +943,95 @@ __global__ __launch_bounds__(kSweepThreads, 4) void k_sweep_all(TileDev T, const
 // chunks, wide entries, diagonal): bitwise the same marginals.
 constexpr int kMargThreads = kR;
 constexpr int kMargU = 256;  // unit descriptors per LDS batch
+
+// Stats tiles: the 512-row blocks cut at group boundaries, in row order
+// (tile_lo sorted); blk_tile_ptr[B] = first tile of global row-block B.
+struct TileArgs {
+    const int32_t* tile_lo;
+    const int32_t* tile_hi;
+    const int32_t* tile_group;
+    const int32_t* group_tile_ptr;
+    const int32_t* blk_tile_ptr;
+    double* tile_cnt;
+    double* tile_sum;
+    double* tile_sq;
+    double* g_cnt;  // per group, from the stats tail
+    double* g_sum;
+    unsigned* counter;  // [2]: last-block-done counters (stats, update)
+};
+
+struct GroupState {
+    double* var;
+    double* mean;
+    int32_t* iters;
+    uint8_t* empty;
+};
+
+// One stats tile's nonzero count and sum; thread = row (block start +
+// threadIdx.x), x = that row's marginal.  The same per-thread values and
+// tree in k_marg (fused) and k_stats1 -> bitwise the same tile sums.
+__device__ __forceinline__ void tile_stats(const TileArgs& ta, int t, long long row, double x, double* sh) {
+    const bool in = row >= ta.tile_lo[t] && row < ta.tile_hi[t] && x != 0.0;
+    const double c = block_sum(in ? 1.0 : 0.0, sh);
+    const double s = block_sum(in ? x : 0.0, sh);
+    if (threadIdx.x == 0) {
+        ta.tile_cnt[t] = c;
+        ta.tile_sum[t] = s;
+    }
+}
+
+// Sum of v[t0..t1) by one wave in a fixed order (lane-strided, then the
+// xor tree): the same bits wherever it is evaluated.
+__device__ __forceinline__ double wave_range_sum(const double* v, int t0, int t1) {
+    const int lane = threadIdx.x & 63;
+    double a = 0.0;
+#pragma unroll 4
+    for (int t = t0 + lane; t < t1; t += 64) a += v[t];
+    return wave_sum(a);
+}
+
+// Last-block-done: every block bumps counter[k] after a release fence (the
+// values the tail reads were stored by thread 0); the block that sees
+// gridDim.x - 1 returns true (after an acquire fence) and resets the counter
+// for the next launch.  No block waits on another.
+__device__ __forceinline__ bool last_block(unsigned* counter, int* flag) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        *flag = atomicAdd(counter, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!*flag) return false;
+    __threadfence();
+    if (threadIdx.x == 0) atomicExch(counter, 0u);
+    return true;
+}
+
+// Stats tail (last block): per active group, one wave: count and sum over the
+// group's tiles -> g_cnt / g_sum.
+__device__ __forceinline__ void stats_tail(const TileArgs& ta, const uint8_t* act, int G) {
+    const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    for (int g = w; g < G; g += nw) {
+        if (act[g] == 0) continue;
+        const int t0 = ta.group_tile_ptr[g], t1 = ta.group_tile_ptr[g + 1];
+        const double c = wave_range_sum(ta.tile_cnt, t0, t1);
+        const double s = wave_range_sum(ta.tile_sum, t0, t1);
+        if ((threadIdx.x & 63) == 0) {
+            ta.g_cnt[g] = c;
+            ta.g_sum[g] = s;
+        }
+    }
+}
+
+// One block per row-block (thread = row): the block's unit descriptors are
+// staged in LDS in batches (every row used to re-read them from global
+// memory, one dependent chain per unit), the partial loads are issued
+// unconditionally from a clamped index and selected, so a batch's loads fly
+// together.  Summation order per row is unchanged (units in order, then band
+// chunks, wide entries, diagonal): bitwise the same marginals.  With
+// `stats` (one GPU holds every row, out = the full marginal vector) the
+// block also writes its stats tiles' count / sum, and the last block the
+// per-group totals (k_stats1's work, without its launch).
 __global__ __launch_bounds__(kMargThreads) void k_marg(TileDev T, const double* __restrict__ part,
                                                        const long long* __restrict__ wide_ptr,
                                                        const int32_t* __restrict__ wide_col,
@@ -948,8 +1040,11 @@ __global__ __launch_bounds__(kMargThreads) void k_marg(TileDev T, const double* 
                                                        const uint16_t* __restrict__ row_group,
                                                        const uint8_t* __restrict__ act, const double* __restrict__ b,
                                                        long long row_lo, int nloc, const double* __restrict__ bpart,
-                                                       int nch, double* __restrict__ out) {
+                                                       int nch, double* __restrict__ out, TileArgs ta, int G,
+                                                       int stats) {
     __shared__ int su_lo[kMargU], su_n[kMargU], su_slot[kMargU];
+    __shared__ double sh[16];
+    __shared__ int flag;
     const int rbk = blockIdx.x, rl = threadIdx.x;
     const int i = rbk * kR + rl;
     const bool live = i < nloc && act[row_group[i < nloc ? i : 0]] != 0;
@@ -985,11 +1080,19 @@ __global__ __launch_bounds__(kMargThreads) void k_marg(TileDev T, const double* 
             }
         }
     }
-    if (!live) return;
-    for (int c = 0; c < nch; ++c) s += bpart[(long long)c * nloc + i];  // dense band chunks, fixed order
-    for (long long q = wide_ptr[i]; q < wide_ptr[i + 1]; ++q) s = fma(wide_cnt[q], b[wide_col[q]], s);
-    const double br = b[row_lo + i];
-    out[i] = br * fma(2.0 * diag[i], br, s);
+    double v = 0.0;
+    if (live) {
+        for (int c = 0; c < nch; ++c) s += bpart[(long long)c * nloc + i];  // dense band chunks, fixed order
+        for (long long q = wide_ptr[i]; q < wide_ptr[i + 1]; ++q) s = fma(wide_cnt[q], b[wide_col[q]], s);
+        const double br = b[row_lo + i];
+        v = br * fma(2.0 * diag[i], br, s);
+        out[i] = v;
+    }
+    if (!stats) return;
+    const int B = (int)(row_lo / kR) + rbk;
+    for (int t = ta.blk_tile_ptr[B]; t < ta.blk_tile_ptr[B + 1]; ++t)
+        if (act[ta.tile_group[t]] != 0) tile_stats(ta, t, row_lo + i, v, sh);
+    if (last_block(ta.counter, &flag)) stats_tail(ta, act, G);
 }
 
 __global__ void k_scatter(const double* __restrict__ g, int world, long long maxlen,
@@ -1008,112 +1111,77 @@ __global__ void k_filter_lt(const double* __restrict__ marg, long long n, double
     if (i < n && marg[i] < thr) bias[i] = 0.0;
 }
 
-struct TileArgs {
-    const int32_t* tile_lo;
-    const int32_t* tile_hi;
-    const int32_t* tile_group;
-    const int32_t* group_tile_ptr;
-    double* tile_cnt;
-    double* tile_sum;
-    double* tile_sq;
-};
-
-__global__ __launch_bounds__(kThreads) void k_stats1(TileArgs ta, const uint8_t* __restrict__ act,
-                                                     const double* __restrict__ marg) {
+// k_marg's stats part on the full (gathered) marginal vector: one block per
+// stats tile, thread = row of the tile's 512-row block.
+__global__ __launch_bounds__(kR) void k_stats1(TileArgs ta, const uint8_t* __restrict__ act,
+                                               const double* __restrict__ marg, int G) {
     __shared__ double sh[16];
+    __shared__ int flag;
     const int t = blockIdx.x;
-    if (act[ta.tile_group[t]] == 0) return;
-    double c = 0.0, s = 0.0;
-    for (int i = ta.tile_lo[t] + threadIdx.x; i < ta.tile_hi[t]; i += kThreads) {
-        const double x = marg[i];
-        if (x != 0.0) { c += 1.0; s += x; }
+    if (act[ta.tile_group[t]] != 0) {
+        const long long row = (long long)(ta.tile_lo[t] / kR) * kR + threadIdx.x;
+        const bool in = row >= ta.tile_lo[t] && row < ta.tile_hi[t];
+        tile_stats(ta, t, row, in ? marg[row] : 0.0, sh);
     }
-    c = block_sum(c, sh);
-    s = block_sum(s, sh);
-    if (threadIdx.x == 0) { ta.tile_cnt[t] = c; ta.tile_sum[t] = s; }
+    if (last_block(ta.counter, &flag)) stats_tail(ta, act, G);
 }
 
-// Group totals over the group's tiles in a fixed order (every block of the
-// group computes the identical value).
-__device__ __forceinline__ void group_totals(const TileArgs& ta, int g, double* sh, double& cnt,
-                                             double& sum, double* sq) {
-    const int t0 = ta.group_tile_ptr[g], t1 = ta.group_tile_ptr[g + 1];
-    double c = 0.0, s = 0.0, q = 0.0;
-    for (int t = t0 + threadIdx.x; t < t1; t += kThreads) {
-        c += ta.tile_cnt[t];
-        s += ta.tile_sum[t];
-        if (sq) q += ta.tile_sq[t];
-    }
-    cnt = block_sum(c, sh);
-    sum = block_sum(s, sh);
-    if (sq) *sq = block_sum(q, sh);
-}
-
-__global__ __launch_bounds__(kThreads) void k_stats2(TileArgs ta, const uint8_t* __restrict__ act,
-                                                     const double* __restrict__ marg) {
+// One block per stats tile: b /= marg/mean with the group mean from the stats
+// tail, and the tile's sum of squared deviations; the last block reduces those
+// per group (one wave each) and records var / mean / iters / the next flag
+// (cooler: bias updated, then `var < tol` tested).
+__global__ __launch_bounds__(kR) void k_update(TileArgs ta, const uint8_t* __restrict__ act,
+                                               uint8_t* __restrict__ nxt, const double* __restrict__ marg,
+                                               double* __restrict__ bias, GroupState gs, double tol,
+                                               int max_iters, int G) {
     __shared__ double sh[16];
+    __shared__ int flag;
     const int t = blockIdx.x;
     const int g = ta.tile_group[t];
-    if (act[g] == 0) return;
-    double cnt, sum;
-    group_totals(ta, g, sh, cnt, sum, nullptr);
-    const double mean = sum / cnt;
-    double q = 0.0;
-    for (int i = ta.tile_lo[t] + threadIdx.x; i < ta.tile_hi[t]; i += kThreads) {
-        const double x = marg[i];
-        if (x != 0.0) { const double d = x - mean; q = fma(d, d, q); }
-    }
-    q = block_sum(q, sh);
-    if (threadIdx.x == 0) ta.tile_sq[t] = q;
-}
-
-struct GroupState {
-    double* var;
-    double* mean;
-    int32_t* iters;
-    uint8_t* empty;
-};
-
-__global__ __launch_bounds__(kThreads) void k_update(TileArgs ta, const uint8_t* __restrict__ act,
-                                                     uint8_t* __restrict__ nxt,
-                                                     const double* __restrict__ marg,
-                                                     double* __restrict__ bias, GroupState gs,
-                                                     double tol, int max_iters) {
-    __shared__ double sh[16];
-    const int t = blockIdx.x;
-    const int g = ta.tile_group[t];
-    const bool first = t == ta.group_tile_ptr[g];
-    if (act[g] == 0) {
-        if (first && threadIdx.x == 0) nxt[g] = 0;
-        return;
-    }
-    double cnt, sum, sq;
-    group_totals(ta, g, sh, cnt, sum, &sq);
-    const int lo = ta.tile_lo[t], hi = ta.tile_hi[t];
-    if (cnt == 0.0) {  // no nonzero marginal: cooler sets the group's bias to NaN
-        for (int i = lo + threadIdx.x; i < hi; i += kThreads) bias[i] = __builtin_nan("");
-        if (first && threadIdx.x == 0) {
-            gs.empty[g] = 1;
-            gs.var[g] = 0.0;
-            gs.mean[g] = __builtin_nan("");
-            gs.iters[g] += 1;
-            nxt[g] = 0;
+    if (act[g] != 0) {
+        const double cnt = ta.g_cnt[g], sum = ta.g_sum[g];
+        const long long row = ta.tile_lo[t] + threadIdx.x;
+        const bool in = row < ta.tile_hi[t];
+        double q = 0.0;
+        if (cnt == 0.0) {  // no nonzero marginal: cooler sets the group's bias to NaN
+            if (in) bias[row] = __builtin_nan("");
+        } else if (in) {
+            const double mean = sum / cnt;
+            const double x = marg[row];
+            double m = x / mean;
+            if (m == 0.0) m = 1.0;
+            bias[row] /= m;
+            if (x != 0.0) {
+                const double d = x - mean;
+                q = d * d;
+            }
         }
-        return;
+        q = block_sum(q, sh);
+        if (threadIdx.x == 0) ta.tile_sq[t] = q;
     }
-    const double mean = sum / cnt;
-    const double var = sq / cnt;
-    for (int i = lo + threadIdx.x; i < hi; i += kThreads) {
-        double m = marg[i] / mean;
-        if (m == 0.0) m = 1.0;
-        bias[i] /= m;
-    }
-    if (first && threadIdx.x == 0) {
-        gs.var[g] = var;
-        gs.mean[g] = mean;
-        const int it = gs.iters[g] + 1;
-        gs.iters[g] = it;
-        nxt[g] = (var < tol || it >= max_iters) ? 0 : 1;
+    if (!last_block(ta.counter + 1, &flag)) return;
+    const int w = threadIdx.x >> 6, nw = blockDim.x >> 6, lane = threadIdx.x & 63;
+    for (int gg = w; gg < G; gg += nw) {
+        if (act[gg] == 0) {
+            if (lane == 0) nxt[gg] = 0;
+            continue;
+        }
+        const double cnt = ta.g_cnt[gg];
+        const double sq = wave_range_sum(ta.tile_sq, ta.group_tile_ptr[gg], ta.group_tile_ptr[gg + 1]);
+        if (lane != 0) continue;
+        const int it = gs.iters[gg] + 1;
+        gs.iters[gg] = it;
+        if (cnt == 0.0) {
+            gs.empty[gg] = 1;
+            gs.var[gg] = 0.0;
+            gs.mean[gg] = __builtin_nan("");
+            nxt[gg] = 0;
+        } else {
+            const double var = sq / cnt;
+            gs.var[gg] = var;
+            gs.mean[gg] = ta.g_sum[gg] / cnt;
+            nxt[gg] = (var < tol || it >= max_iters) ? 0 : 1;
+        }
     }
 }
 
@@ -1140,8 +1208,10 @@ struct hh_ice {
     int32_t G = 1;
     std::vector<int64_t> glo, ghi;
     int32_t n_tiles = 0;
-    DBuf<int32_t> tile_lo, tile_hi, tile_group, group_tile_ptr;
-    DBuf<double> bias, marg, part, tile_cnt, tile_sum, tile_sq;
+    DBuf<int32_t> tile_lo, tile_hi, tile_group, group_tile_ptr, blk_tile_ptr;
+    DBuf<double> bias, marg, part, tile_cnt, tile_sum, tile_sq, g_cnt, g_sum;
+    DBuf<unsigned> counter;   // last-block-done counters of the stats / update tails
+    bool stats_fresh = false; // tile + group stats of the current marginals already made (fused k_marg)
     DBuf<double> bpart;  // dense band partials: n_band_chunks x nloc
     int32_t nch = 0;
     DBuf<uint8_t> active;  // 2 x G (parity double buffer)
@@ -1169,7 +1239,8 @@ struct hh_ice {
     }
     bool full() const { return m->row_lo == 0 && m->row_hi == m->n_bins; }
     TileArgs ta() {
-        return TileArgs{tile_lo.p, tile_hi.p, tile_group.p, group_tile_ptr.p, tile_cnt.p, tile_sum.p, tile_sq.p};
+        return TileArgs{tile_lo.p, tile_hi.p, tile_group.p, group_tile_ptr.p, blk_tile_ptr.p, tile_cnt.p,
+                        tile_sum.p, tile_sq.p, g_cnt.p, g_sum.p, counter.p};
     }
     uint8_t* act() { return active.p + (iters_done & 1) * G; }
     uint8_t* nxt() { return active.p + (1 - (iters_done & 1)) * G; }
@@ -1193,6 +1264,7 @@ static int g_split_tiles = 1;      // with band_concurrent: tiled kernel on a se
 static int64_t g_conc_min_bytes = 8LL << 30;
 static int g_band_rows = 0;   // rows per band block: 0 = auto (64 or 256)
 static int g_band_fused = 1;  // the band segments in one launch
+static int g_fuse_stats = 1;    // stats tile sums in k_marg's tail on one GPU (0: separate k_stats1 launch)
 static int g_sweep_single = -1;  // whole sweep in one launch: -1 auto (below g_single_max_bytes), 0 off, 1 on
 static int64_t g_single_max_bytes = 1LL << 30;
 // diagnostic: per-block timeline of the last single-launch sweep (hh_sweep_trace)
@@ -1338,23 +1410,30 @@ static void marg_weighted(hh_ice* S, double* out, hipStream_t s, bool timed, int
         }
     }
     if (timed) HIP_CHECK(hipEventRecord(S->ev[2 * slot + 1], s));
+    S->stats_fresh = false;
     if (S->nloc == 0) return;
+    // stats fused into k_marg when this GPU holds every row and `out` is the
+    // marginal vector update() reads (k_stats1's tile sums, bitwise)
+    const int stats = g_fuse_stats && S->full() && out == S->marg.p && S->n_tiles > 0;
     hipLaunchKernelGGL(k_marg, dim3(nblocks(S->nloc, kR)), dim3(kMargThreads), 0, s, m->dev(), S->part.p,
                        m->wide_ptr.p, m->wide_col.p, m->wide_cnt.p, m->diag.p, m->row_group.p, S->act(),
-                       S->bias.p, (long long)m->row_lo, (int)S->nloc, S->bpart.p, (int)S->nch, out);
+                       S->bias.p, (long long)m->row_lo, (int)S->nloc, S->bpart.p, (int)S->nch, out, S->ta(),
+                       (int)S->G, stats);
     HIP_CHECK(hipGetLastError());
+    S->stats_fresh = stats != 0;
 }
 
 static void update(hh_ice* S, hipStream_t s) {
     TileArgs ta = S->ta();
     if (S->n_tiles) {
-        hipLaunchKernelGGL(k_stats1, dim3(S->n_tiles), dim3(kThreads), 0, s, ta, S->act(), S->marg.p);
-        hipLaunchKernelGGL(k_stats2, dim3(S->n_tiles), dim3(kThreads), 0, s, ta, S->act(), S->marg.p);
+        if (!S->stats_fresh)
+            hipLaunchKernelGGL(k_stats1, dim3(S->n_tiles), dim3(kR), 0, s, ta, S->act(), S->marg.p, (int)S->G);
         GroupState gs{S->g_var.p, S->g_mean.p, S->g_iters.p, S->g_empty.p};
-        hipLaunchKernelGGL(k_update, dim3(S->n_tiles), dim3(kThreads), 0, s, ta, S->act(), S->nxt(),
-                           S->marg.p, S->bias.p, gs, S->o.tol, S->o.max_iters);
+        hipLaunchKernelGGL(k_update, dim3(S->n_tiles), dim3(kR), 0, s, ta, S->act(), S->nxt(), S->marg.p,
+                           S->bias.p, gs, S->o.tol, S->o.max_iters, (int)S->G);
         HIP_CHECK(hipGetLastError());
     }
+    S->stats_fresh = false;
     // groups without tiles never run; keep their flag cleared in the next buffer
     S->iters_done += 1;
 }
@@ -1404,6 +1483,9 @@ int hh_tune(const char* key, int64_t value) {
         } else if (k == "conc_min_bytes") {
             HH_REQUIRE(value >= 0, "conc_min_bytes >= 0");
             g_conc_min_bytes = value;
+        } else if (k == "fuse_stats") {
+            HH_REQUIRE(value == 0 || value == 1, "fuse_stats in {0, 1}");
+            g_fuse_stats = (int)value;
         } else if (k == "split_tiles") {
             HH_REQUIRE(value == 0 || value == 1, "split_tiles in {0, 1}");
             g_split_tiles = (int)value;
@@ -1474,19 +1556,33 @@ int hh_ice_create(hh_matrix* m, const hh_ice_opts* o, hh_ice** out) {
         std::vector<int32_t> tlo, thi, tg, gtp(S->G + 1, 0);
         for (int g = 0; g < S->G; ++g) {
             gtp[g] = (int32_t)tlo.size();
-            for (int64_t b = S->glo[g]; b < S->ghi[g]; b += kTile) {
+            // stats tiles: the group's rows cut at 512-row block boundaries
+            for (int64_t b = S->glo[g]; b < S->ghi[g];) {
+                const int64_t e = std::min<int64_t>((b / kR + 1) * kR, S->ghi[g]);
                 tlo.push_back((int32_t)b);
-                thi.push_back((int32_t)std::min<int64_t>(b + kTile, S->ghi[g]));
+                thi.push_back((int32_t)e);
                 tg.push_back(g);
+                b = e;
             }
         }
         gtp[S->G] = (int32_t)tlo.size();
         S->n_tiles = (int32_t)tlo.size();
+        const int64_t nblk = (S->n + kR - 1) / kR;
+        std::vector<int32_t> btp(nblk + 1, 0);
+        for (size_t t = 0, B = 0; B <= (size_t)nblk; ++B) {  // tiles are in row order
+            while (t < tlo.size() && tlo[t] < (int64_t)B * kR) ++t;
+            btp[B] = (int32_t)t;
+        }
         hipStream_t s = 0;
         S->tile_lo = to_device(tlo, s);
         S->tile_hi = to_device(thi, s);
         S->tile_group = to_device(tg, s);
         S->group_tile_ptr = to_device(gtp, s);
+        S->blk_tile_ptr = to_device(btp, s);
+        S->g_cnt.alloc(S->G);
+        S->g_sum.alloc(S->G);
+        S->counter.alloc(2);
+        S->counter.zero(s);
         S->bias.alloc(S->n);
         std::vector<double> ones(S->n, 1.0);
         S->bias.upload(ones.data(), S->n, s);
@@ -1547,6 +1643,7 @@ int hh_ice_marg_local(hh_ice* S, int32_t mode, double* marg_local, void* stream)
         if (mode == 2) {
             marg_weighted(S, out, s, false, 0);
         } else {
+            S->stats_fresh = false;
             const DBuf<double>& src = mode == 0 ? S->m->row_nnz2 : S->m->row_sum2;
             if (S->nloc)
                 HIP_CHECK(hipMemcpyAsync(out, src.p, S->nloc * sizeof(double), hipMemcpyDeviceToDevice, s));
@@ -1568,6 +1665,7 @@ int hh_ice_set_marg(hh_ice* S, const double* gathered, int32_t world, int64_t ma
             std::vector<long long> ll(rr.begin(), rr.end());
             S->rank_rows = to_device(ll, s);
         }
+        S->stats_fresh = false;
         const long long tot = (long long)world * maxlen;
         if (tot)
             hipLaunchKernelGGL(k_scatter, dim3(nblocks(tot, kThreads)), dim3(kThreads), 0, s, gathered, world,
