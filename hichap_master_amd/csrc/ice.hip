@@ -754,9 +754,14 @@ struct BandSeg {
     long long stride, dlo;
     int bytes, nc, ch, bits;
 };
+constexpr int kMaxBandChunks = 64;
 struct BandSegs {
     BandSeg s[3];
     int n;
+    // grid row -> bpart chunk (heaviest chunks dispatched first: full 4-bit
+    // chunks, full uint8 chunks, then the partial last chunks, so the light
+    // blocks form the launch's tail; the chunk -> partial mapping is unchanged)
+    uint8_t ord[kMaxBandChunks];
 };
 
 // One (ROWS-row block, 2048-byte chunk) of one segment.  ROWS = 256 on big
@@ -872,16 +877,14 @@ __device__ __forceinline__ void band_any(const BandSegs& S, int rblk, int y, Ban
                                          long long row_lo, long long n_bins, const uint8_t* __restrict__ act,
                                          const uint16_t* __restrict__ row_group, const double* __restrict__ b,
                                          double* __restrict__ bpart) {
+    const int c = S.ord[y];
     int k = 0;
-    while (k + 1 < S.n && y >= S.s[k].nc) {
-        y -= S.s[k].nc;
-        ++k;
-    }
+    while (k + 1 < S.n && c >= S.s[k + 1].ch) ++k;
     const BandSeg P = S.s[k];
     if (P.bits == 8)
-        band_block<8, ABL, ROWS>(P, rblk, y, L.bl, L.ract, nloc, row_lo, n_bins, act, row_group, b, bpart);
+        band_block<8, ABL, ROWS>(P, rblk, c - P.ch, L.bl, L.ract, nloc, row_lo, n_bins, act, row_group, b, bpart);
     else
-        band_block<4, ABL, ROWS>(P, rblk, y, L.bl, L.ract, nloc, row_lo, n_bins, act, row_group, b, bpart);
+        band_block<4, ABL, ROWS>(P, rblk, c - P.ch, L.bl, L.ract, nloc, row_lo, n_bins, act, row_group, b, bpart);
 }
 
 template <int ABL, int ROWS>
@@ -1264,6 +1267,7 @@ static int g_split_tiles = 1;      // with band_concurrent: tiled kernel on a se
 static int64_t g_conc_min_bytes = 8LL << 30;
 static int g_band_rows = 0;   // rows per band block: 0 = auto (64 or 256)
 static int g_band_fused = 1;  // the band segments in one launch
+static int g_band_lpt = 1;      // band chunks dispatched heaviest first (0: uint8 first, index order)
 static int g_fuse_stats = 1;    // stats tile sums in k_marg's tail on one GPU (0: separate k_stats1 launch)
 static int g_sweep_single = -1;  // whole sweep in one launch: -1 auto (below g_single_max_bytes), 0 off, 1 on
 static int64_t g_single_max_bytes = 1LL << 30;
@@ -1308,6 +1312,19 @@ static void sweep(const hh_matrix* m, const uint8_t* act, const double* b, doubl
 }
 
 // The matrix's band segments; returns their total chunk count.
+// Dispatch order of the band chunks: by work (counts in the chunk) descending,
+// ties by index (g_band_lpt 0: index order, uint8 first).
+static void band_order(BandSegs& segs, int ch) {
+    std::vector<std::pair<long long, int>> w;
+    for (int k = 0; k < segs.n; ++k)
+        for (int c = 0; c < segs.s[k].nc; ++c) {
+            const long long bytes = std::min<long long>(kBandChunkB, segs.s[k].bytes - (long long)c * kBandChunkB);
+            w.push_back({g_band_lpt ? -bytes * (8 / segs.s[k].bits) : 0, segs.s[k].ch + c});
+        }
+    std::stable_sort(w.begin(), w.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+    for (int y = 0; y < ch; ++y) segs.ord[y] = (uint8_t)w[y].second;
+}
+
 static int band_segs(const hh_matrix* m, BandSegs& segs) {
     const long long W8 = m->band_w, W4 = m->band_w4;
     segs = BandSegs{};
@@ -1323,6 +1340,8 @@ static int band_segs(const hh_matrix* m, BandSegs& segs) {
         add(m->band4.p, st, sg, -W4, 4);
         add(m->band4.p + sg, st, sg, W8 + 1, 4);
     }
+    HH_REQUIRE(ch <= kMaxBandChunks, "too many band chunks");
+    band_order(segs, ch);
     return ch;
 }
 
@@ -1351,6 +1370,7 @@ static void sweep_band(hh_ice* S, hipStream_t s) {
             BandSegs one{};
             one.s[0] = segs.s[k];
             one.n = 1;
+            for (int y = 0; y < segs.s[k].nc; ++y) one.ord[y] = (uint8_t)(segs.s[k].ch + y);
             launch(one, segs.s[k].nc);
         }
     }
@@ -1483,6 +1503,9 @@ int hh_tune(const char* key, int64_t value) {
         } else if (k == "conc_min_bytes") {
             HH_REQUIRE(value >= 0, "conc_min_bytes >= 0");
             g_conc_min_bytes = value;
+        } else if (k == "band_lpt") {
+            HH_REQUIRE(value == 0 || value == 1, "band_lpt in {0, 1}");
+            g_band_lpt = (int)value;
         } else if (k == "fuse_stats") {
             HH_REQUIRE(value == 0 || value == 1, "fuse_stats in {0, 1}");
             g_fuse_stats = (int)value;

@@ -2,7 +2,7 @@
 rank's shard on this one GPU in turn (dist.partition_rows, as bench.py does)
 and time its sweep (HIP-event registry, 'ice_sweep').  Prints per-rank sweep
 ms and max/mean; the slowest rank bounds an N-GPU iteration.
-  python tools/probe_shards.py [worlds=2,4,8] [refine=0|1]
+  python tools/probe_shards.py [2,4,8] [1]     (world sizes; second argument 1 = refine)
 HH_TUNE="key=value,..." sets hh_tune knobs first.  refine=1: re-partition
 once with per-row weights scaled by each shard's measured time per weight
 (dist.refine_weights) and measure again."""
