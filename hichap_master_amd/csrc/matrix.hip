@@ -15,6 +15,7 @@ namespace hh {
 
 static thread_local std::string g_last_error;
 int64_t g_unit_entries = 0;  // 0 = auto (plan_tiles)
+int64_t g_unit_lpt = 1;      // launch lists by unit cost class, largest first (0: row order)
 int64_t g_tile_cost = 32768; // payload-word equivalent of one tile's fixed cost in the unit split (C4 shard 8/8: 0.79 -> 0.65 ms/iter)
 int64_t g_band_w = -1;       // -1 = auto (choose_band_w)
 int64_t g_flat_max = 64;     // longest row (uint4) of a flat tile segment; 0 = no flat segments
@@ -337,6 +338,21 @@ TilePlan plan_tiles(const uint16_t* cntw, const uint16_t* cntn, int64_t nloc, in
             ++P.n_units_flat;
             for (int32_t t = P.u_tlo[u]; t < P.u_thi[u]; ++t) P.payload_bytes_flat += 4 * tile_words(t, 0, kR);
         }
+    if (g_unit_lpt) {
+        // each list by cost class (bit length of words + per-tile cost),
+        // largest first, row order within a class: the remainder units of the
+        // row-blocks form the launch's tail.  Dispatch order only: a row's
+        // partials are summed in unit-index order (k_marg), bitwise the same.
+        auto cls = [&](int32_t u) {
+            int64_t c = (int64_t)(P.u_thi[u] - P.u_tlo[u]) * tile_cost;
+            for (int32_t t = P.u_tlo[u]; t < P.u_thi[u]; ++t) c += tile_words(t, P.u_rlo[u], P.u_rhi[u]);
+            return 64 - __builtin_clzll((unsigned long long)c | 1ull);
+        };
+        const auto mid = P.u_order.end() - P.n_units_flat;
+        auto by = [&](int32_t a, int32_t b) { return cls(a) > cls(b); };
+        std::stable_sort(P.u_order.begin(), mid, by);
+        std::stable_sort(mid, P.u_order.end(), by);
+    }
     if (P.n_part > INT32_MAX || P.tile_J.size() > (size_t)INT32_MAX) HH_THROW(HH_ERR_ARG, "plan too large");
     return P;
 }
