@@ -1491,7 +1491,7 @@ int hh_tune(const char* key, int64_t value) {
             HH_REQUIRE(value == 0 || (value >= 4096 && value <= (1 << 24)), "unit_entries must be 0 (auto) or in [4096, 2^24]");
             g_unit_entries = value;
         } else if (k == "unit_lpt") {
-            HH_REQUIRE(value == 0 || value == 1, "unit_lpt in {0, 1}");
+            HH_REQUIRE(value >= 0 && value <= 2, "unit_lpt in {0, 1, 2}");
             g_unit_lpt = value;
         } else if (k == "tile_cost") {
             HH_REQUIRE(value >= 0 && value <= (1 << 20), "tile_cost in [0, 2^20] payload words");

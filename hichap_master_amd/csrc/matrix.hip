@@ -343,13 +343,15 @@ TilePlan plan_tiles(const uint16_t* cntw, const uint16_t* cntn, int64_t nloc, in
         // largest first, row order within a class: the remainder units of the
         // row-blocks form the launch's tail.  Dispatch order only: a row's
         // partials are summed in unit-index order (k_marg), bitwise the same.
-        auto cls = [&](int32_t u) {
+        // (g_unit_lpt 2: by exact cost, largest first)
+        std::vector<int64_t> key(P.u_tlo.size());
+        for (size_t u = 0; u < key.size(); ++u) {
             int64_t c = (int64_t)(P.u_thi[u] - P.u_tlo[u]) * tile_cost;
             for (int32_t t = P.u_tlo[u]; t < P.u_thi[u]; ++t) c += tile_words(t, P.u_rlo[u], P.u_rhi[u]);
-            return 64 - __builtin_clzll((unsigned long long)c | 1ull);
-        };
+            key[u] = g_unit_lpt == 2 ? c : 64 - __builtin_clzll((unsigned long long)c | 1ull);
+        }
         const auto mid = P.u_order.end() - P.n_units_flat;
-        auto by = [&](int32_t a, int32_t b) { return cls(a) > cls(b); };
+        auto by = [&](int32_t a, int32_t b) { return key[a] > key[b]; };
         std::stable_sort(P.u_order.begin(), mid, by);
         std::stable_sort(mid, P.u_order.end(), by);
     }
