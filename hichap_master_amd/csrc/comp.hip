@@ -179,19 +179,38 @@ __global__ __launch_bounds__(256) void k_oe_center(const double* __restrict__ M,
 // tiles (64 x 64 per wave: 16 flops per byte staged, twice the 64 x 64
 // tile's, which was bound by the L2 -> CU stream at 0.59 of the fp64 matrix
 // peak).  K steps of 16 rows; the next step's global loads are issued before
-// the current step's MFMAs (register double buffer), one LDS buffer.  LDS rows
+// the current step's MFMAs (register double buffer), one LDS buffer (two LDS
+// buffers with one barrier per step measured 46.4 vs 49.5 TF/s).  LDS rows
 // padded to 144 doubles (= 16 mod 32) so the two 16-lane row groups of a
 // 32-lane LDS pass land on disjoint banks.
+// Split K (SPLIT): block x = split * ntile + tile takes K rows [split * kc,
+// (split + 1) * kc) and writes its raw partial tile; k_syrk_reduce sums the
+// splits in order.  The host splits when a chromosome's triangle of tiles
+// would leave most of the chip idle for its last round (chr21: 105 tiles on
+// 512 block slots).
 constexpr int kSyT = 128;
 constexpr int kLdS = kSyT + 16;
+constexpr int kSyTile = kSyT * kSyT;
+__device__ __forceinline__ void syrk_tile_ij(long long t, long long nt, long long& bi, long long& bj) {
+    long long b = 0, rem = t;
+    while (rem >= nt - b) { rem -= nt - b; ++b; }
+    bi = b;
+    bj = b + rem;
+}
+
+template <bool SPLIT>
 __global__ __launch_bounds__(256, 2) void k_syrk(const double* __restrict__ Z, long long ld, long long Kpad,
-                                              long long nt, double scale, double* __restrict__ C, long long ldc) {
+                                              long long nt, long long kc, double scale, double* __restrict__ C,
+                                              long long ldc, double* __restrict__ P) {
     __shared__ __attribute__((aligned(16))) double As[16][kLdS];
     __shared__ __attribute__((aligned(16))) double Bs[16][kLdS];
-    long long bi = 0, rem = blockIdx.x;
-    while (rem >= nt - bi) { rem -= nt - bi; ++bi; }
-    const long long bj = bi + rem;
+    const long long ntile = nt * (nt + 1) / 2;
+    const long long tile = SPLIT ? blockIdx.x % ntile : blockIdx.x;
+    const long long split = SPLIT ? blockIdx.x / ntile : 0;
+    long long bi, bj;
+    syrk_tile_ij(tile, nt, bi, bj);
     const long long i0 = bi * kSyT, j0 = bj * kSyT;
+    const long long kb = split * kc, ke = min(kb + kc, Kpad);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int wr = (w >> 1) * 64, wc = (w & 1) * 64;
     const bool diag = bi == bj;
@@ -210,8 +229,8 @@ __global__ __launch_bounds__(256, 2) void k_syrk(const double* __restrict__ Z, l
             vb[h] = diag ? va[h] : *reinterpret_cast<const d4*>(Z + (k0 + lr + 8 * h) * ld + j0 + lc);
         }
     };
-    load(0);
-    for (long long k0 = 0; k0 < Kpad; k0 += 16) {
+    if (kb < ke) load(kb);
+    for (long long k0 = kb; k0 < ke; k0 += 16) {
         __syncthreads();  // previous step's LDS reads are done
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
@@ -219,7 +238,7 @@ __global__ __launch_bounds__(256, 2) void k_syrk(const double* __restrict__ Z, l
             *reinterpret_cast<d4*>(&Bs[lr + 8 * h][lc]) = vb[h];
         }
         __syncthreads();
-        if (k0 + 16 < Kpad) load(k0 + 16);
+        if (k0 + 16 < ke) load(k0 + 16);
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
             const int kk = s * 4 + (lane >> 4);
@@ -243,12 +262,34 @@ __global__ __launch_bounds__(256, 2) void k_syrk(const double* __restrict__ Z, l
         for (int tb = 0; tb < 4; ++tb)
 #pragma unroll
             for (int reg = 0; reg < 4; ++reg) {
-                const long long gi = i0 + wr + ta * 16 + (lane >> 4) + 4 * reg;
-                const long long gj = j0 + wc + tb * 16 + (lane & 15);
-                const double v = acc[ta][tb][reg] * scale;
-                C[gi * ldc + gj] = v;
-                if (!diag) C[gj * ldc + gi] = v;
+                const int li = wr + ta * 16 + (lane >> 4) + 4 * reg;
+                const int lj = wc + tb * 16 + (lane & 15);
+                if (SPLIT) {
+                    P[(size_t)blockIdx.x * kSyTile + li * kSyT + lj] = acc[ta][tb][reg];
+                } else {
+                    const double v = acc[ta][tb][reg] * scale;
+                    C[(i0 + li) * ldc + j0 + lj] = v;
+                    if (!diag) C[(j0 + lj) * ldc + i0 + li] = v;
+                }
             }
+}
+
+// Split-K partial tiles -> Cov (both triangles): splits summed in order, then
+// scaled (deterministic).  One thread per element of the tile triangle.
+__global__ __launch_bounds__(256) void k_syrk_reduce(const double* __restrict__ P, int nsplit, long long nt,
+                                                     double scale, double* __restrict__ C, long long ldc) {
+    const long long ntile = nt * (nt + 1) / 2;
+    const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= ntile * kSyTile) return;
+    const long long tile = e / kSyTile;
+    const int li = (int)(e % kSyTile) / kSyT, lj = (int)(e % kSyT);
+    double v = 0.0;
+    for (int k = 0; k < nsplit; ++k) v += P[((size_t)k * ntile + tile) * kSyTile + (e % kSyTile)];
+    v *= scale;
+    long long bi, bj;
+    syrk_tile_ij(tile, nt, bi, bj);
+    C[(bi * kSyT + li) * ldc + bj * kSyT + lj] = v;
+    if (bi != bj) C[(bj * kSyT + lj) * ldc + bi * kSyT + li] = v;
 }
 
 // numpy corrcoef: c /= sd[:, None]; c /= sd[None, :]; clip(-1, 1); then the
@@ -1481,6 +1522,32 @@ int hh_comp_get_sliding_oe(hh_comp* c, double* oe, void* stream) {
     });
 }
 
+// K splits for the Cov triangle, by a cost model in units of one round of
+// full-K tiles on the 2-blocks-per-CU slots: ceil(tiles s / slots) / s for the
+// split launch plus the reduction pass, which streams (s + 2) partial-tile
+// sizes per tile (128 KB each at ~4 TB/s, against a round of ~0.23 us x K on
+// fp64 MFMA): ~0.14 (s + 2) tiles / K.  Splits <= 8, >= 256 K rows each.  The
+// triangle's last round is what it buys back: chr21 at 25 kb has 105 tiles
+// for 512 slots (s = 4), chr1 2701 (5.3 rounds -> s = 2, 5.5 + 0.15).
+static int syrk_splits(long long ntile, long long Kpad) {
+    if (g_syrk_split > 0) return (int)std::min<long long>(g_syrk_split, std::max<long long>(1, Kpad / 16));
+    if (g_syrk_split == 0) return 1;
+    int dev = 0, n_cu = 256;
+    HIP_CHECK(hipGetDevice(&dev));
+    HIP_CHECK(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
+    const long long slots = 2LL * n_cu;
+    int best = 1;
+    double best_t = (double)((ntile + slots - 1) / slots);
+    for (int k = 2; k <= 8 && Kpad / k >= 256; ++k) {
+        const double t = (double)((ntile * k + slots - 1) / slots) / k + 0.14 * (k + 2) * ntile / (double)Kpad;
+        if (t < 0.97 * best_t) {
+            best_t = t;
+            best = k;
+        }
+    }
+    return best;
+}
+
 int hh_comp_correlation(hh_comp* c, const double* decline, const int64_t* ng, int64_t n, void* stream) {
     return guard([&] {
         HH_REQUIRE(c && decline && ng && n > 0 && n <= c->N, "bad arguments");
@@ -1514,13 +1581,26 @@ int hh_comp_correlation(hh_comp* c, const double* decline, const int64_t* ng, in
                            c->ng.p, mu.p, N, (long long)n, Npad, c->ld, Z.p);
         // Cov = Z^T Z * (1 / (N - 1))  (np.cov: c *= true_divide(1, fact))
         DBuf<double> cov((size_t)c->ld * c->ld);
-        const long long nt = c->ld / kSyT;
+        const long long nt = c->ld / kSyT, ntile = nt * (nt + 1) / 2;
+        const int ns = syrk_splits(ntile, Npad);
+        const long long kc = (Npad / 16 + ns - 1) / ns * 16;
+        const double scale = 1.0 / (double)(N - 1);
+        // (P and Z stay allocated until the stream is synchronised below: a
+        // pooled block released earlier could be handed to another thread's
+        // stream while these kernels still use it)
+        DBuf<double> P(ns > 1 ? (size_t)ns * ntile * kSyTile : 0);
         {
-            HH_KTIME("k_syrk", s);
-            hipLaunchKernelGGL(k_syrk, dim3((unsigned)(nt * (nt + 1) / 2)), dim3(256), 0, s, Z.p, c->ld, Npad, nt,
-                               1.0 / (double)(N - 1), cov.p, c->ld);
+            HH_KTIME("k_syrk", s);  // (split K: the reduction is inside the timed span)
+            if (ns == 1) {
+                hipLaunchKernelGGL(k_syrk<false>, dim3((unsigned)ntile), dim3(256), 0, s, Z.p, c->ld, Npad, nt,
+                                   Npad, scale, cov.p, c->ld, nullptr);
+            } else {
+                hipLaunchKernelGGL(k_syrk<true>, dim3((unsigned)(ns * ntile)), dim3(256), 0, s, Z.p, c->ld, Npad,
+                                   nt, kc, scale, nullptr, c->ld, P.p);
+                hipLaunchKernelGGL(k_syrk_reduce, dim3((unsigned)((ntile * kSyTile + 255) / 256)), dim3(256), 0, s,
+                                   P.p, ns, nt, scale, cov.p, c->ld);
+            }
         }
-        Z.release();
         c->cor.alloc((size_t)c->ld * c->ld);
         hipLaunchKernelGGL(k_corr_norm_oop, dim3((unsigned)((c->ld * c->ld + 255) / 256)), dim3(256), 0, s, cov.p,
                            (long long)n, c->ld, c->cor.p);

@@ -105,6 +105,7 @@ inline int g_parse_ablate = 0;
 // Compartment PCA eigensolver (hh_tune "pca_method" 0 = block subspace
 // iteration, 1 = block Krylov; "pca_p" = Cor products per Krylov cycle).
 inline int g_pca_method = 1;
+inline int g_syrk_split = -1;  // Cov K splits (hh_tune "syrk_split"): -1 auto, 0 never, n > 0 forced
 inline int g_pca_p = 8;
 inline int g_pca_debug = 0;  // hh_tune "pca_debug": per-cycle trace on stderr
 

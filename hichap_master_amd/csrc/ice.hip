@@ -1506,6 +1506,9 @@ int hh_tune(const char* key, int64_t value) {
         } else if (k == "conc_min_bytes") {
             HH_REQUIRE(value >= 0, "conc_min_bytes >= 0");
             g_conc_min_bytes = value;
+        } else if (k == "syrk_split") {
+            HH_REQUIRE(value >= -1 && value <= 64, "syrk_split in [-1, 64]");
+            g_syrk_split = (int)value;
         } else if (k == "band_lpt") {
             HH_REQUIRE(value == 0 || value == 1, "band_lpt in {0, 1}");
             g_band_lpt = (int)value;
