@@ -154,14 +154,24 @@ __global__ __launch_bounds__(256) void k_px_lowkeys(const int32_t* __restrict__ 
     }
 }
 
+// Sorted lower-half keys -> packed (column | count << 32), in place, once:
+// the two row passes then read the lower half contiguously instead of each
+// gathering A[i] and kc[i] at random (C3: 8e8 x 2 random 4-byte reads per pass).
+__global__ void k_px_lowgather(unsigned long long* __restrict__ keys, long long n, unsigned long long imask,
+                               const int32_t* __restrict__ A, const uint32_t* __restrict__ kc) {
+    const long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= n) return;
+    const long long i = (long long)(keys[q] & imask);
+    keys[q] = (unsigned long long)(uint32_t)A[i] | ((unsigned long long)kc[i] << 32);
+}
+
 struct PxRows {
     const int32_t* A;
     const int32_t* B;
     const uint32_t* kc;
     const long long* up_ptr;            // n_bins + 1 (global rows)
-    const unsigned long long* lkeys;    // sorted lower keys
+    const unsigned long long* lkeys;    // lower half, row-sorted, packed (column | count << 32)
     const long long* lo_ptr;            // nloc + 1
-    unsigned long long imask;           // (1 << ib) - 1
     long long row_lo, nloc;
     int nJ, band_w, band_w4;
     // PASS 0
@@ -282,19 +292,14 @@ __global__ __launch_bounds__(256) void k_px_rows(PxRows p) {
             mask &= ~run;
         }
     };
-    // lower half: columns < r, from the sorted keys
+    // lower half: columns < r, the sorted keys replaced by their packed
+    // (column, count) (k_px_lowgather): contiguous, no per-pass gathers
     const long long l0 = p.lo_ptr[w], l1 = p.lo_ptr[w + 1];
     for (long long q0 = l0; q0 < l1; q0 += 64) {
         const long long q = q0 + lane;
-        long long col = 0;
-        uint32_t v = 0;
         const bool valid = q < l1;
-        if (valid) {
-            const long long i = (long long)(p.lkeys[q] & p.imask);
-            col = p.A[i];
-            v = p.kc[i];
-        }
-        chunk(col, v, valid);
+        const unsigned long long x = valid ? p.lkeys[q] : 0ull;
+        chunk((long long)(uint32_t)x, (uint32_t)(x >> 32), valid);
     }
     // upper half: columns >= r, the row's run of the table
     const long long u0 = p.up_ptr[r], u1 = p.up_ptr[r + 1];
@@ -456,7 +461,11 @@ void build_from_device_pixels(const Id* b1, const Id* b2, const Cnt* cnt, int64_
     DBuf<long long> lo_ptr(nloc + 1);
     hipLaunchKernelGGL(k_px_keyptr, dim3((unsigned)((hn + 1 + 255) / 256)), dim3(256), 0, s, keys.p, (long long)hn, ib,
                        (long long)nloc, lo_ptr.p);
+    if (hn)
+        hipLaunchKernelGGL(k_px_lowgather, dim3((unsigned)((hn + 255) / 256)), dim3(256), 0, s, keys.p, (long long)hn,
+                           ib >= 64 ? ~0ull : ((1ull << ib) - 1ull), dA.p, dkc.p);
     HIP_CHECK(hipGetLastError());
+    phase("lower gather");
     // ---- PASS 0: per-(row, tile) counts and row statistics
     m->diag.alloc(nloc);
     m->row_nnz2.alloc(nloc);
@@ -473,7 +482,6 @@ void build_from_device_pixels(const Id* b1, const Id* b2, const Cnt* cnt, int64_
     P.up_ptr = up_ptr.p;
     P.lkeys = keys.p;
     P.lo_ptr = lo_ptr.p;
-    P.imask = ib >= 64 ? ~0ull : ((1ull << ib) - 1ull);
     P.row_lo = row_lo;
     P.nloc = nloc;
     P.nJ = nJ;
