@@ -8,14 +8,16 @@
 //                sum(count * b[col]) in fp64 -> part[seg]          [HBM bound]
 //   K2 k_marg    per local row: marg = b_r * (sum_seg part + 2 * diag * b_r)
 //                (cooler's bincount(bin1) + bincount(bin2))
-//   K3 stats     per stats tile (a 512-row block cut at group boundaries):
-//                nonzero count and sum -- fused into k_marg when one GPU
-//                holds every row (else k_stats1 on the gathered vector); the
-//                last block to finish reduces them per group (count, sum)
-//      k_update  per stats tile: b /= marg/mean (marg==0 -> 1) and the tile's
-//                sum of squared deviations; the last block to finish reduces
-//                those per group and records var/mean/iters and the next
-//                active flag (2 launches after the sweep instead of 4).
+//   K3 stats     per stats tile (a 512-row block cut at group boundaries).
+//                Few tiles (<= 128, single chromosomes): nonzero count and sum
+//                fused into k_marg when one GPU holds every row (else
+//                k_stats1 on the gathered vector), the last block to finish
+//                reduces them per group; k_update: b /= marg/mean (marg==0
+//                -> 1) and the tile's squared deviations, its last block
+//                records var/mean/iters and the next active flag (2 launches
+//                after the sweep).  Many tiles: k_stats1, k_stats2,
+//                k_update_big, every block re-reducing its group's tile sums
+//                (no device-scope fences / one-wave tails over ~1 200 tiles).
 // All reductions use fixed trees -> bitwise deterministic, and independent of
 // how rows are sharded across GPUs.
 #include <algorithm>
@@ -1116,6 +1118,7 @@ __global__ void k_filter_lt(const double* __restrict__ marg, long long n, double
 
 // k_marg's stats part on the full (gathered) marginal vector: one block per
 // stats tile, thread = row of the tile's 512-row block.
+template <bool TAIL>
 __global__ __launch_bounds__(kR) void k_stats1(TileArgs ta, const uint8_t* __restrict__ act,
                                                const double* __restrict__ marg, int G) {
     __shared__ double sh[16];
@@ -1126,7 +1129,91 @@ __global__ __launch_bounds__(kR) void k_stats1(TileArgs ta, const uint8_t* __res
         const bool in = row >= ta.tile_lo[t] && row < ta.tile_hi[t];
         tile_stats(ta, t, row, in ? marg[row] : 0.0, sh);
     }
-    if (last_block(ta.counter, &flag)) stats_tail(ta, act, G);
+    if (TAIL && last_block(ta.counter, &flag)) stats_tail(ta, act, G);
+}
+
+// Large matrices (many stats tiles): no last-block tails -- their device-scope
+// fences and one-wave reductions over ~1 200 tiles cost ~45 us per C4
+// iteration -- but every block re-reduces its group's tile sums (block-wide,
+// fixed order; the same function in k_stats2 and k_update_big -> the same
+// mean), as in round 1: k_marg, k_stats1<false>, k_stats2, k_update_big.
+__device__ __forceinline__ void group_totals_block(const TileArgs& ta, int g, double* sh, double& cnt, double& sum,
+                                                   double* sq) {
+    const int t0 = ta.group_tile_ptr[g], t1 = ta.group_tile_ptr[g + 1];
+    double c = 0.0, s = 0.0, q = 0.0;
+    for (int t = t0 + threadIdx.x; t < t1; t += blockDim.x) {
+        c += ta.tile_cnt[t];
+        s += ta.tile_sum[t];
+        if (sq) q += ta.tile_sq[t];
+    }
+    cnt = block_sum(c, sh);
+    sum = block_sum(s, sh);
+    if (sq) *sq = block_sum(q, sh);
+}
+
+__global__ __launch_bounds__(kR) void k_stats2(TileArgs ta, const uint8_t* __restrict__ act,
+                                               const double* __restrict__ marg) {
+    __shared__ double sh[16];
+    const int t = blockIdx.x;
+    const int g = ta.tile_group[t];
+    if (act[g] == 0) return;
+    double cnt, sum;
+    group_totals_block(ta, g, sh, cnt, sum, nullptr);
+    const double mean = sum / cnt;
+    const long long row = ta.tile_lo[t] + threadIdx.x;
+    double q = 0.0;
+    if (row < ta.tile_hi[t]) {
+        const double x = marg[row];
+        if (x != 0.0) {
+            const double d = x - mean;
+            q = d * d;
+        }
+    }
+    q = block_sum(q, sh);
+    if (threadIdx.x == 0) ta.tile_sq[t] = q;
+}
+
+__global__ __launch_bounds__(kR) void k_update_big(TileArgs ta, const uint8_t* __restrict__ act,
+                                                   uint8_t* __restrict__ nxt, const double* __restrict__ marg,
+                                                   double* __restrict__ bias, GroupState gs, double tol,
+                                                   int max_iters) {
+    __shared__ double sh[16];
+    const int t = blockIdx.x;
+    const int g = ta.tile_group[t];
+    const bool first = t == ta.group_tile_ptr[g];
+    if (act[g] == 0) {
+        if (first && threadIdx.x == 0) nxt[g] = 0;
+        return;
+    }
+    double cnt, sum, sq;
+    group_totals_block(ta, g, sh, cnt, sum, &sq);
+    const long long row = ta.tile_lo[t] + threadIdx.x;
+    const bool in = row < ta.tile_hi[t];
+    if (cnt == 0.0) {  // no nonzero marginal: cooler sets the group's bias to NaN
+        if (in) bias[row] = __builtin_nan("");
+        if (first && threadIdx.x == 0) {
+            gs.empty[g] = 1;
+            gs.var[g] = 0.0;
+            gs.mean[g] = __builtin_nan("");
+            gs.iters[g] += 1;
+            nxt[g] = 0;
+        }
+        return;
+    }
+    const double mean = sum / cnt;
+    if (in) {
+        double m = marg[row] / mean;
+        if (m == 0.0) m = 1.0;
+        bias[row] /= m;
+    }
+    if (first && threadIdx.x == 0) {
+        const double var = sq / cnt;
+        gs.var[g] = var;
+        gs.mean[g] = mean;
+        const int it = gs.iters[g] + 1;
+        gs.iters[g] = it;
+        nxt[g] = (var < tol || it >= max_iters) ? 0 : 1;
+    }
 }
 
 // One block per stats tile: b /= marg/mean with the group mean from the stats
@@ -1204,6 +1291,12 @@ static inline unsigned nblocks(long long n, int t) { return (unsigned)((n + t - 
 
 using namespace hh;
 
+namespace hh {
+// the stats mode switch (hh_ice::small_stats): C2 (49 tiles) fused, C3 (149) / C4 (1 187) not
+static int g_fuse_stats = -1;
+constexpr int kFuseMaxTiles = 128;
+}  // namespace hh
+
 struct hh_ice {
     hh_matrix* m = nullptr;
     hh_ice_opts o{};
@@ -1245,6 +1338,10 @@ struct hh_ice {
         return TileArgs{tile_lo.p, tile_hi.p, tile_group.p, group_tile_ptr.p, blk_tile_ptr.p, tile_cnt.p,
                         tile_sum.p, tile_sq.p, g_cnt.p, g_sum.p, counter.p};
     }
+    // stats mode: few tiles -> fused k_marg stats + last-block tails (2
+    // launches after the sweep); many -> 4 launches, no tails (hh_tune
+    // "fuse_stats": -1 auto, 0 never, 1 always)
+    bool small_stats() const { return hh::g_fuse_stats > 0 || (hh::g_fuse_stats < 0 && n_tiles <= hh::kFuseMaxTiles); }
     uint8_t* act() { return active.p + (iters_done & 1) * G; }
     uint8_t* nxt() { return active.p + (1 - (iters_done & 1)) * G; }
 };
@@ -1268,7 +1365,6 @@ static int64_t g_conc_min_bytes = 8LL << 30;
 static int g_band_rows = 0;   // rows per band block: 0 = auto (64 or 256)
 static int g_band_fused = 1;  // the band segments in one launch
 static int g_band_lpt = 1;      // band chunks dispatched heaviest first (0: uint8 first, index order)
-static int g_fuse_stats = 1;    // stats tile sums in k_marg's tail on one GPU (0: separate k_stats1 launch)
 static int g_sweep_single = -1;  // whole sweep in one launch: -1 auto (below g_single_max_bytes), 0 off, 1 on
 static int64_t g_single_max_bytes = 1LL << 30;
 // diagnostic: per-block timeline of the last single-launch sweep (hh_sweep_trace)
@@ -1434,7 +1530,7 @@ static void marg_weighted(hh_ice* S, double* out, hipStream_t s, bool timed, int
     if (S->nloc == 0) return;
     // stats fused into k_marg when this GPU holds every row and `out` is the
     // marginal vector update() reads (k_stats1's tile sums, bitwise)
-    const int stats = g_fuse_stats && S->full() && out == S->marg.p && S->n_tiles > 0;
+    const int stats = S->small_stats() && S->full() && out == S->marg.p && S->n_tiles > 0;
     hipLaunchKernelGGL(k_marg, dim3(nblocks(S->nloc, kR)), dim3(kMargThreads), 0, s, m->dev(), S->part.p,
                        m->wide_ptr.p, m->wide_col.p, m->wide_cnt.p, m->diag.p, m->row_group.p, S->act(),
                        S->bias.p, (long long)m->row_lo, (int)S->nloc, S->bpart.p, (int)S->nch, out, S->ta(),
@@ -1446,11 +1542,20 @@ static void marg_weighted(hh_ice* S, double* out, hipStream_t s, bool timed, int
 static void update(hh_ice* S, hipStream_t s) {
     TileArgs ta = S->ta();
     if (S->n_tiles) {
-        if (!S->stats_fresh)
-            hipLaunchKernelGGL(k_stats1, dim3(S->n_tiles), dim3(kR), 0, s, ta, S->act(), S->marg.p, (int)S->G);
         GroupState gs{S->g_var.p, S->g_mean.p, S->g_iters.p, S->g_empty.p};
-        hipLaunchKernelGGL(k_update, dim3(S->n_tiles), dim3(kR), 0, s, ta, S->act(), S->nxt(), S->marg.p,
-                           S->bias.p, gs, S->o.tol, S->o.max_iters, (int)S->G);
+        if (S->small_stats()) {
+            if (!S->stats_fresh)
+                hipLaunchKernelGGL(k_stats1<true>, dim3(S->n_tiles), dim3(kR), 0, s, ta, S->act(), S->marg.p,
+                                   (int)S->G);
+            hipLaunchKernelGGL(k_update, dim3(S->n_tiles), dim3(kR), 0, s, ta, S->act(), S->nxt(), S->marg.p,
+                               S->bias.p, gs, S->o.tol, S->o.max_iters, (int)S->G);
+        } else {
+            hipLaunchKernelGGL(k_stats1<false>, dim3(S->n_tiles), dim3(kR), 0, s, ta, S->act(), S->marg.p,
+                               (int)S->G);
+            hipLaunchKernelGGL(k_stats2, dim3(S->n_tiles), dim3(kR), 0, s, ta, S->act(), S->marg.p);
+            hipLaunchKernelGGL(k_update_big, dim3(S->n_tiles), dim3(kR), 0, s, ta, S->act(), S->nxt(), S->marg.p,
+                               S->bias.p, gs, S->o.tol, S->o.max_iters);
+        }
         HIP_CHECK(hipGetLastError());
     }
     S->stats_fresh = false;
@@ -1493,6 +1598,9 @@ int hh_tune(const char* key, int64_t value) {
         } else if (k == "unit_lpt") {
             HH_REQUIRE(value >= 0 && value <= 2, "unit_lpt in {0, 1, 2}");
             g_unit_lpt = value;
+        } else if (k == "unit_lpt_lists") {
+            HH_REQUIRE(value >= 0 && value <= 3, "unit_lpt_lists in [0, 3]");
+            g_unit_lpt_lists = value;
         } else if (k == "tile_cost") {
             HH_REQUIRE(value >= 0 && value <= (1 << 20), "tile_cost in [0, 2^20] payload words");
             g_tile_cost = value;
@@ -1513,7 +1621,7 @@ int hh_tune(const char* key, int64_t value) {
             HH_REQUIRE(value == 0 || value == 1, "band_lpt in {0, 1}");
             g_band_lpt = (int)value;
         } else if (k == "fuse_stats") {
-            HH_REQUIRE(value == 0 || value == 1, "fuse_stats in {0, 1}");
+            HH_REQUIRE(value >= -1 && value <= 1, "fuse_stats in {-1, 0, 1}");
             g_fuse_stats = (int)value;
         } else if (k == "split_tiles") {
             HH_REQUIRE(value == 0 || value == 1, "split_tiles in {0, 1}");

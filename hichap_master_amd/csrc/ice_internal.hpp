@@ -33,6 +33,7 @@ constexpr int kW = 1 << kWBits;         // columns per tile
 constexpr uint32_t kColMask = kW - 1;
 constexpr uint32_t kCntMax = 65535u;    // largest count stored in a tile (wide entry)
 extern int64_t g_unit_lpt;                               // launch lists largest cost class first (hh_tune)
+extern int64_t g_unit_lpt_lists;                         // which launch lists unit_lpt orders (bit 0 tiled, bit 1 flat)
 extern int64_t g_tile_cost;                              // per-tile cost in the unit split (hh_tune)
 extern int64_t g_unit_entries;                           // ~512 KiB of payload per unit (hh_tune)
 constexpr int64_t kMaxBins = (int64_t)1 << 30;

@@ -16,6 +16,7 @@ namespace hh {
 static thread_local std::string g_last_error;
 int64_t g_unit_entries = 0;  // 0 = auto (plan_tiles)
 int64_t g_unit_lpt = 1;      // launch lists by unit cost class, largest first (0: row order)
+int64_t g_unit_lpt_lists = 1; // which lists: 1 tiled, 2 flat, 3 both (flat too: C4 sweep +1 %, profiles/r2b_modes_ab.log)
 int64_t g_tile_cost = 32768; // payload-word equivalent of one tile's fixed cost in the unit split (C4 shard 8/8: 0.79 -> 0.65 ms/iter)
 int64_t g_band_w = -1;       // -1 = auto (choose_band_w)
 int64_t g_flat_max = 64;     // longest row (uint4) of a flat tile segment; 0 = no flat segments
@@ -352,8 +353,8 @@ TilePlan plan_tiles(const uint16_t* cntw, const uint16_t* cntn, int64_t nloc, in
         }
         const auto mid = P.u_order.end() - P.n_units_flat;
         auto by = [&](int32_t a, int32_t b) { return key[a] > key[b]; };
-        std::stable_sort(P.u_order.begin(), mid, by);
-        std::stable_sort(mid, P.u_order.end(), by);
+        if (g_unit_lpt_lists & 1) std::stable_sort(P.u_order.begin(), mid, by);
+        if (g_unit_lpt_lists & 2) std::stable_sort(mid, P.u_order.end(), by);
     }
     if (P.n_part > INT32_MAX || P.tile_J.size() > (size_t)INT32_MAX) HH_THROW(HH_ERR_ARG, "plan too large");
     return P;

@@ -492,3 +492,30 @@ def test_sweep_launch_shapes_bitwise(ice, cis_only):
             _lib.call("hh_tune", k.encode(), default[k])
     wr, _ = ice_ref.balance(b1, b2, c, n, off, cis_only=cis_only, max_iters=300)
     np.testing.assert_allclose(ref[0], wr, rtol=1e-9, equal_nan=True)
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("cis_only", [False, True])
+def test_stats_modes(ice, mode, cis_only):
+    """Both ICE stats paths (hh_tune fuse_stats: 1 = stats fused into k_marg +
+    last-block tails, 0 = k_stats1 / k_stats2 / k_update_big as used for
+    matrices of > 128 stats tiles) against the oracle, with the same iteration
+    counts, and sharded == one shard bitwise within each mode."""
+    from hichap_master_amd import _lib, dist
+    b1, b2, c, off = _case(12, sizes=(600, 450, 300))
+    n = int(off[-1])
+    _lib.call("hh_tune", b"fuse_stats", mode)
+    try:
+        w, st = ice.balance(b1, b2, c, n, off, cis_only=cis_only, max_iters=400)
+        wr, sr = ice_ref.balance(b1, b2, c, n, off, cis_only=cis_only, max_iters=400)
+        np.testing.assert_array_equal(np.isnan(w), np.isnan(wr))
+        np.testing.assert_allclose(w, wr, rtol=1e-9, equal_nan=True)
+        np.testing.assert_array_equal(st["iters"], sr["iters"])
+        np.testing.assert_allclose(st["var"], sr["var"], rtol=1e-6, atol=1e-15)
+        if not cis_only:
+            rr = dist.partition_rows(np.bincount(b1, minlength=n) + np.bincount(b2, minlength=n), 2)
+            w0, s0 = _sharded_weights(ice, b1, b2, c, off, rr)
+            np.testing.assert_array_equal(w0, w)
+            assert s0["iters"] == st["iters"]
+    finally:
+        _lib.call("hh_tune", b"fuse_stats", -1)
