@@ -875,55 +875,29 @@ __global__ void k_count_nl(TextView tv, long long upto, unsigned long long* __re
 }
 
 // ------------------------------------------------------------ radix sort
+// Digit histogram of one 4096-key tile: each wave counts its 1 024 keys by
+// ballot matching into wave-private LDS counters (no LDS atomics: a skewed
+// digit -- the high bits of a row index -- serialised them), then the four
+// waves' counts are summed.
 __global__ __launch_bounds__(kScanThreads) void k_rs_hist(const unsigned long long* __restrict__ keys, long long n,
                                                           int shift, long long n_tiles, unsigned* __restrict__ hist) {
-    __shared__ unsigned h[256];
-    h[threadIdx.x] = 0;
-    __syncthreads();
-    const long long base = (long long)blockIdx.x * kScanTile;
-#pragma unroll
-    for (int r = 0; r < kScanItems; ++r) {
-        const long long i = base + (long long)r * kScanThreads + threadIdx.x;
-        if (i < n) atomicAdd(&h[(keys[i] >> shift) & 0xff], 1u);
-    }
-    __syncthreads();
-    hist[(long long)threadIdx.x * n_tiles + blockIdx.x] = h[threadIdx.x];
-}
-
-// Stable scatter of one 4096-key tile: local ranks from wave ballots (the 8
-// digit bits matched across the wave), staged in LDS in digit order, then
-// written digit run by digit run.
-__global__ __launch_bounds__(kScanThreads) void k_rs_scatter(const unsigned long long* __restrict__ in,
-                                                             unsigned long long* __restrict__ out, long long n,
-                                                             int shift, long long n_tiles,
-                                                             const unsigned* __restrict__ hist_off) {
-    __shared__ unsigned long long stage[kScanTile];
-    __shared__ unsigned cnt[256], start[256], run[256], gofs_lo[256];
-    __shared__ unsigned wc[4][256];
-    __shared__ unsigned long long sh[4];
+    constexpr int NW = kScanThreads / 64;
+    constexpr int PER = kScanTile / NW;
+    __shared__ unsigned wcnt[NW][256];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const long long base = (long long)blockIdx.x * kScanTile;
-    const int nvalid = (int)min((long long)kScanTile, n - base);
-    cnt[tid] = 0;
-    run[tid] = 0;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) wc[k][tid] = 0;
-    __syncthreads();
+    for (int k = 0; k < NW; ++k) wcnt[k][tid] = 0;
+    const long long base = (long long)blockIdx.x * kScanTile;
     unsigned long long kv[kScanItems];
 #pragma unroll
     for (int r = 0; r < kScanItems; ++r) {
-        const int j = r * kScanThreads + tid;
-        kv[r] = j < nvalid ? in[base + j] : 0ull;
-        if (j < nvalid) atomicAdd(&cnt[(kv[r] >> shift) & 0xff], 1u);
+        const long long i = base + w * PER + r * 64 + lane;
+        kv[r] = i < n ? keys[i] : 0ull;
     }
-    __syncthreads();
-    start[tid] = (unsigned)block_excl_scan_u64(cnt[tid], sh, nullptr);
-    gofs_lo[tid] = hist_off[(long long)tid * n_tiles + blockIdx.x];
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < kScanItems; ++r) {
-        const int j = r * kScanThreads + tid;
-        const bool v = j < nvalid;
+        const bool v = base + w * PER + r * 64 + lane < n;
         const unsigned d = (unsigned)((kv[r] >> shift) & 0xff);
         unsigned long long m = __ballot(v);
 #pragma unroll
@@ -931,19 +905,86 @@ __global__ __launch_bounds__(kScanThreads) void k_rs_scatter(const unsigned long
             const unsigned long long bb = __ballot((d >> b) & 1u);
             m &= ((d >> b) & 1u) ? bb : ~bb;
         }
-        const unsigned wr = (unsigned)__popcll(m & ((1ull << lane) - 1ull));
-        if (v && lane == 63 - __clzll(m)) wc[w][d] = (unsigned)__popcll(m);
-        __syncthreads();
-        if (v) {
-            unsigned before = run[d];
-            for (int k = 0; k < w; ++k) before += wc[k][d];
-            stage[start[d] + before + wr] = kv[r];
-        }
-        __syncthreads();
-        run[tid] += wc[0][tid] + wc[1][tid] + wc[2][tid] + wc[3][tid];
-        wc[0][tid] = wc[1][tid] = wc[2][tid] = wc[3][tid] = 0;
-        __syncthreads();
+        if (v && lane == 63 - __clzll(m)) wcnt[w][d] += (unsigned)__popcll(m);
     }
+    __syncthreads();
+    unsigned tot = 0;
+#pragma unroll
+    for (int k = 0; k < NW; ++k) tot += wcnt[k][tid];
+    hist[(long long)tid * n_tiles + blockIdx.x] = tot;
+}
+
+// Stable scatter of one 4096-key tile.  Each wave owns 1 024 consecutive keys
+// (16 steps of 64) and ranks them with ballots (the 8 digit bits matched
+// across the wave) against wave-private digit counters in LDS -- no block
+// barrier inside the ranking loop (round 1: three per step, 48 per tile).
+// Then one scan over (digit, wave) places the waves' runs in key order, the
+// tile is staged in LDS in digit order and written digit run by digit run.
+__global__ __launch_bounds__(kScanThreads) void k_rs_scatter(const unsigned long long* __restrict__ in,
+                                                             unsigned long long* __restrict__ out, long long n,
+                                                             int shift, long long n_tiles,
+                                                             const unsigned* __restrict__ hist_off) {
+    constexpr int NW = kScanThreads / 64;
+    constexpr int PER = kScanTile / NW;  // keys per wave
+    static_assert(PER == 64 * kScanItems, "a wave's run is kScanItems steps of 64 keys");
+    __shared__ unsigned long long stage[kScanTile];
+    __shared__ unsigned wcnt[NW][256];
+    __shared__ unsigned start[256], gofs_lo[256];
+    __shared__ unsigned long long sh[4];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const long long base = (long long)blockIdx.x * kScanTile;
+    const int nvalid = (int)min((long long)kScanTile, n - base);
+#pragma unroll
+    for (int k = 0; k < NW; ++k) wcnt[k][tid] = 0;
+    unsigned long long kv[kScanItems];
+#pragma unroll
+    for (int r = 0; r < kScanItems; ++r) {
+        const int j = w * PER + r * 64 + lane;
+        kv[r] = j < nvalid ? in[base + j] : 0ull;
+    }
+    __syncthreads();
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    unsigned rk[kScanItems];
+#pragma unroll
+    for (int r = 0; r < kScanItems; ++r) {
+        const bool v = w * PER + r * 64 + lane < nvalid;
+        const unsigned d = (unsigned)((kv[r] >> shift) & 0xff);
+        unsigned long long m = __ballot(v);
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            const unsigned long long bb = __ballot((d >> b) & 1u);
+            m &= ((d >> b) & 1u) ? bb : ~bb;
+        }
+        // wave-private counter: every lane reads it before the leader (the
+        // highest matching lane) writes it; a wave's LDS ops are in order
+        const unsigned prior = wcnt[w][d];
+        rk[r] = prior + (unsigned)__popcll(m & lt);
+        if (v && lane == 63 - __clzll(m)) wcnt[w][d] = prior + (unsigned)__popcll(m);
+    }
+    __syncthreads();
+    unsigned tot = 0;
+#pragma unroll
+    for (int k = 0; k < NW; ++k) tot += wcnt[k][tid];
+    const unsigned st = (unsigned)block_excl_scan_u64(tot, sh, nullptr);
+    start[tid] = st;
+    gofs_lo[tid] = hist_off[(long long)tid * n_tiles + blockIdx.x];
+    {
+        unsigned acc = st;  // wave w's first slot for digit tid: start + the earlier waves' counts
+#pragma unroll
+        for (int k = 0; k < NW; ++k) {
+            const unsigned c = wcnt[k][tid];
+            wcnt[k][tid] = acc;
+            acc += c;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kScanItems; ++r) {
+        const bool v = w * PER + r * 64 + lane < nvalid;
+        const unsigned d = (unsigned)((kv[r] >> shift) & 0xff);
+        if (v) stage[wcnt[w][d] + rk[r]] = kv[r];
+    }
+    __syncthreads();
     for (int j = tid; j < nvalid; j += kScanThreads) {
         const unsigned long long key = stage[j];
         const unsigned d = (unsigned)((key >> shift) & 0xff);
