@@ -215,26 +215,38 @@ __device__ __forceinline__ long long lower_bound_i32(const int32_t* a, long long
     }
     return lo;
 }
-// first key position in [lo, hi) of the column list whose cell row >= x
-__device__ __forceinline__ long long lower_bound_keyrow(const unsigned long long* keys, unsigned long long imask,
-                                                        const int32_t* R, long long lo, long long hi, int32_t x) {
+// first position in [lo, hi) of the column list whose cell row >= x
+__device__ __forceinline__ long long lower_bound_keyrow(const unsigned long long* lrv, long long lo, long long hi,
+                                                        int32_t x) {
     while (lo < hi) {
         const long long mid = (lo + hi) >> 1;
-        if (R[(long long)(keys[mid] & imask)] < x) lo = mid + 1;
+        if ((int32_t)(uint32_t)lrv[mid] < x) lo = mid + 1;
         else hi = mid;
     }
     return lo;
 }
+
+// The column-sorted keys replaced, in place and once, by their cells' (row,
+// count) packed as row | count << 32 (the column is the list segment,
+// cptr): the kernels below used to gather R[k] and V[k] at random through
+// the keys, each of them again.
+__global__ void k_gw_pack(unsigned long long* __restrict__ keys, long long n, unsigned long long imask,
+                          const int32_t* __restrict__ R, const uint32_t* __restrict__ V) {
+    const long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= n) return;
+    const long long k = (long long)(keys[q] & imask);
+    keys[q] = (unsigned long long)(uint32_t)R[k] | ((unsigned long long)V[k] << 32);
+}
+__device__ __forceinline__ int32_t lrv_row(unsigned long long x) { return (int32_t)(uint32_t)x; }
+__device__ __forceinline__ double lrv_val(unsigned long long x) { return (double)(uint32_t)(x >> 32); }
 
 struct GwDev {
     const int32_t* R;
     const int32_t* C;
     const uint32_t* V;
     const long long* hptr;      // N2 + 1 row pointers of H
-    const unsigned long long* keys;  // off-diagonal cells sorted by (col, row)
+    const unsigned long long* lrv;   // off-diagonal cells sorted by (col, row): (row, count) packed
     const long long* cptr;      // N2 + 1 column-list pointers
-    unsigned long long imask;
-    int ib;
     long long N2;
     const double* alpha;        // N2
     long long* ustart;          // per row: first cell with col >= row
@@ -262,8 +274,8 @@ __global__ __launch_bounds__(256) void k_gw_marg(GwDev g, double exponent, doubl
         const long long q = q0 + lane;
         double x = 0.0;
         if (q < c1) {
-            const long long k = (long long)(g.keys[q] & g.imask);
-            x = (double)g.V[k] / g.alpha[g.R[k]];
+            const unsigned long long e = g.lrv[q];
+            x = lrv_val(e) / g.alpha[lrv_row(e)];
         }
         acc2 += wave_sum(x);
     }
@@ -273,25 +285,27 @@ __global__ __launch_bounds__(256) void k_gw_marg(GwDev g, double exponent, doubl
         if (sv == 0.0) sv = 1.0;
         s_out[r] = sv;
         g.ustart[r] = lower_bound_i32(g.C, h0, h1, (int32_t)r);
-        g.lstart[r] = lower_bound_keyrow(g.keys, g.imask, g.R, c0, c1, (int32_t)(r + 1));
+        g.lstart[r] = lower_bound_keyrow(g.lrv, c0, c1, (int32_t)(r + 1));
     }
 }
 
 // orphan flags over the column-sorted list: entry (i, r), i > r, whose
 // partner (r, i) is not a cell of H
-__global__ void k_gw_orphans(GwDev g, long long nkeys, long long* __restrict__ flag) {
-    const long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= nkeys) return;
-    const long long k = (long long)(g.keys[q] & g.imask);
-    const long long r = (long long)(g.keys[q] >> g.ib);  // the column
-    const int32_t i = g.R[k];
-    long long f = 0;
-    if (i > r) {
-        const long long h0 = g.ustart[r], h1 = g.hptr[r + 1];
-        const long long p = lower_bound_i32(g.C, h0, h1, i);
-        f = (p < h1 && g.C[p] == i) ? 0 : 1;
+// (one wave per column r of the list)
+__global__ void k_gw_orphans(GwDev g, long long* __restrict__ flag) {
+    const long long r = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (r >= g.N2) return;
+    const int lane = threadIdx.x & 63;
+    const long long h0 = g.ustart[r], h1 = g.hptr[r + 1];
+    for (long long q = g.cptr[r] + lane; q < g.cptr[r + 1]; q += 64) {
+        const int32_t i = lrv_row(g.lrv[q]);
+        long long f = 0;
+        if (i > r) {
+            const long long p = lower_bound_i32(g.C, h0, h1, i);
+            f = (p < h1 && g.C[p] == i) ? 0 : 1;
+        }
+        flag[q] = f;
     }
-    flag[q] = f;
 }
 
 __global__ void k_gw_rowlen(GwDev g, const long long* __restrict__ oprefix, long long* __restrict__ len) {
@@ -312,10 +326,10 @@ __global__ void k_gw_write_upper(GwDev g, const long long* __restrict__ oprefix,
     long long before = 0;  // orphans of row r with column < c
     if (c > r) {
         const long long l0 = g.lstart[r], l1 = g.cptr[(long long)r + 1];
-        const long long p = lower_bound_keyrow(g.keys, g.imask, g.R, l0, l1, c);
+        const long long p = lower_bound_keyrow(g.lrv, l0, l1, c);
         if (p < l1) {
-            const long long kk = (long long)(g.keys[p] & g.imask);
-            if (g.R[kk] == c) y += (double)g.V[kk] / g.alpha[c];
+            const unsigned long long e = g.lrv[p];
+            if (lrv_row(e) == c) y += lrv_val(e) / g.alpha[c];
         }
         before = oprefix[p] - oprefix[l0];
     }
@@ -326,22 +340,26 @@ __global__ void k_gw_write_upper(GwDev g, const long long* __restrict__ oprefix,
 }
 
 // lower cells (i, r), i > r, without a partner: Y_ri = S_ir alone
-__global__ void k_gw_write_orphans(GwDev g, long long nkeys, const long long* __restrict__ flag,
-                                   const long long* __restrict__ oprefix, const long long* __restrict__ row_off,
-                                   const double* __restrict__ s, int32_t* __restrict__ ob1,
-                                   int32_t* __restrict__ ob2, double* __restrict__ ov) {
-    const long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= nkeys || !flag[q]) return;
-    const long long k = (long long)(g.keys[q] & g.imask);
-    const long long r = (long long)(g.keys[q] >> g.ib);
-    const int32_t i = g.R[k];
+// (one wave per column r of the list)
+__global__ void k_gw_write_orphans(GwDev g, const long long* __restrict__ flag, const long long* __restrict__ oprefix,
+                                   const long long* __restrict__ row_off, const double* __restrict__ s,
+                                   int32_t* __restrict__ ob1, int32_t* __restrict__ ob2, double* __restrict__ ov) {
+    const long long r = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (r >= g.N2) return;
+    const int lane = threadIdx.x & 63;
     const long long u0 = g.ustart[r], u1 = g.hptr[r + 1];
-    const long long before = lower_bound_i32(g.C, u0, u1, i) - u0;  // upper cells of row r with col < i
-    const long long pos = row_off[r] + (oprefix[q] - oprefix[g.lstart[r]]) + before;
-    const double y = (double)g.V[k] / g.alpha[i];
-    ob1[pos] = (int32_t)r;
-    ob2[pos] = i;
-    ov[pos] = y / (s[i] * s[r]);
+    const long long obase = row_off[r] - oprefix[g.lstart[r]];
+    for (long long q = g.cptr[r] + lane; q < g.cptr[r + 1]; q += 64) {
+        if (!flag[q]) continue;
+        const unsigned long long e = g.lrv[q];
+        const int32_t i = lrv_row(e);
+        const long long before = lower_bound_i32(g.C, u0, u1, i) - u0;  // upper cells of row r with col < i
+        const long long pos = obase + oprefix[q] + before;
+        const double y = lrv_val(e) / g.alpha[i];
+        ob1[pos] = (int32_t)r;
+        ob2[pos] = i;
+        ov[pos] = y / (s[i] * s[r]);
+    }
 }
 
 // sum of the full symmetric C from its upper table: per block, fixed order
@@ -371,7 +389,7 @@ struct hh_gw {
     DBuf<int32_t> tA, tB, R, C;
     DBuf<uint32_t> tV, V;
     DBuf<long long> hptr, cptr;
-    DBuf<unsigned long long> keys;
+    DBuf<unsigned long long> keys;  // column-sorted cells, (row, count) packed after hh_gw_create
     int ib = 1;
     std::vector<unsigned long long> t_rowsum, t_nnz_row, h_blocksum;
     unsigned long long h_total = 0;
@@ -484,6 +502,9 @@ void gw_create(hh_gw& G, const Id* t1, const Id* t2, const Cnt* tv, int64_t t_nn
     G.cptr.alloc(2 * n + 1);
     hipLaunchKernelGGL(k_px_keyptr_gw, dim3((unsigned)((hn + 1 + 255) / 256)), dim3(256), 0, s, G.keys.p,
                        (long long)hn, G.ib, (long long)(2 * n), G.cptr.p);
+    if (hn)
+        hipLaunchKernelGGL(k_gw_pack, dim3((unsigned)((hn + 255) / 256)), dim3(256), 0, s, G.keys.p, (long long)hn,
+                           G.ib >= 64 ? ~0ull : ((1ull << G.ib) - 1ull), G.R.p, G.V.p);
     HIP_CHECK(hipGetLastError());
     HIP_CHECK(hipStreamSynchronize(s));
 }
@@ -554,13 +575,11 @@ int hh_gw_correct(hh_gw* g, const double* alpha, double exponent, int64_t* out_n
         DBuf<double> dal(N2), sv(N2);
         dal.upload(alpha, N2, s);
         DBuf<long long> ustart(N2), lstart(N2);
-        GwDev d{g->R.p, g->C.p, g->V.p, g->hptr.p, g->keys.p, g->cptr.p,
-                g->ib >= 64 ? ~0ull : ((1ull << g->ib) - 1ull), g->ib, (long long)N2, dal.p, ustart.p, lstart.p};
+        GwDev d{g->R.p, g->C.p, g->V.p, g->hptr.p, g->keys.p, g->cptr.p, (long long)N2, dal.p, ustart.p, lstart.p};
         hipLaunchKernelGGL(k_gw_marg, dim3((unsigned)((N2 * 64 + 255) / 256)), dim3(256), 0, s, d, exponent, sv.p);
         DBuf<long long> flag(nk + 1), opre(nk + 1);
         if (nk > 0)
-            hipLaunchKernelGGL(k_gw_orphans, dim3((unsigned)((nk + 255) / 256)), dim3(256), 0, s, d, (long long)nk,
-                               flag.p);
+            hipLaunchKernelGGL(k_gw_orphans, dim3((unsigned)((N2 * 64 + 255) / 256)), dim3(256), 0, s, d, flag.p);
         HIP_CHECK(hipMemsetAsync(flag.p + nk, 0, sizeof(long long), s));
         dev_excl_scan_i64(flag.p, opre.p, nk + 1, nullptr, s);
         DBuf<long long> len(N2 + 1), roff(N2 + 1);
@@ -577,8 +596,8 @@ int hh_gw_correct(hh_gw* g, const double* alpha, double exponent, int64_t* out_n
             hipLaunchKernelGGL(k_gw_write_upper, dim3((unsigned)((g->h_nnz + 255) / 256)), dim3(256), 0, s, d, opre.p,
                                roff.p, sv.p, g->ob1.p, g->ob2.p, g->ov.p);
         if (nk > 0)
-            hipLaunchKernelGGL(k_gw_write_orphans, dim3((unsigned)((nk + 255) / 256)), dim3(256), 0, s, d,
-                               (long long)nk, flag.p, opre.p, roff.p, sv.p, g->ob1.p, g->ob2.p, g->ov.p);
+            hipLaunchKernelGGL(k_gw_write_orphans, dim3((unsigned)((N2 * 64 + 255) / 256)), dim3(256), 0, s, d,
+                               flag.p, opre.p, roff.p, sv.p, g->ob1.p, g->ob2.p, g->ov.p);
         HIP_CHECK(hipGetLastError());
         // R_F = H.mean() / C.mean() over the full 2n x 2n matrices (:897-899)
         const long long per = 1 << 16;
