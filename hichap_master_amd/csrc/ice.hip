@@ -648,6 +648,13 @@ __device__ __forceinline__ void sweep_flat_unit(const TileDev& T, const uint8_t*
         m.entn = T.tile_entn[t], m.ent = T.tile_ent[t];
         return m;
     };
+    // The compact narrow sums of tile t are added to their rows after the
+    // barrier that opens tile t + 1, beside its staging (row ids read from
+    // tile t's record in global memory, an L2 hit: the LDS copy is being
+    // replaced): two barriers per tile instead of three.
+    const bool defer = T.flat_defer != 0;
+    int nfn_prev = 0;
+    const uint16_t* fidn_prev = nullptr;
     for (int t = t0; t < t1; ++t) {
         const Meta cm = meta(t);
         const uint32_t qan = cm.qan, qbn = cm.qbn, qaw = cm.qaw, qbw = cm.qbw;
@@ -658,15 +665,23 @@ __device__ __forceinline__ void sweep_flat_unit(const TileDev& T, const uint8_t*
         if (i0n < i1n) flat_load<U>(payn4, qan + (uint32_t)lane * U, qan, qbn, v);
         if (i0w < i1w) flat_load<UW>(payw4, qaw + (uint32_t)lane * UW, qaw, qbw, vw);
         const uint4* rg = rg0 + (size_t)(t - t0) * kFrecU4;
-        __syncthreads();  // previous tile's LDS reads (and its mapping) are done
+        __syncthreads();  // previous tile's walk (LDS reads, accc / acc writes) is done
+        for (int k = threadIdx.x; k < nfn_prev; k += kSweepThreads) acc[fidn_prev[k]] += accc[k];
         if (ABL != 2) stage_bias(bl, b, (long long)cm.J * kW, n_bins);
         for (int k = threadIdx.x; k < kFrecU4; k += kSweepThreads) reinterpret_cast<uint4*>(rec)[k] = rg[k];
         __syncthreads();
         flat_seg_c<U, ABL, 8>(payn4, v, qan, qbn, i0n, i1n, fstn, nfn, bl, accc, lane);
         flat_seg<UW, ABL, 4>(payw4, vw, qaw, qbw, i0w, i1w, fstw, fidw, nfw, bl, acc, lane);
-        __syncthreads();  // compact narrow sums complete; wide row sums written
-        for (int k = threadIdx.x; k < nfn; k += kSweepThreads) acc[fidn[k]] += accc[k];
+        if (defer) {
+            nfn_prev = nfn;
+            fidn_prev = reinterpret_cast<const uint16_t*>(rg) + 2 * (kR + 1);
+        } else {  // round-1 order: a third barrier, merge from the LDS record
+            __syncthreads();
+            for (int k = threadIdx.x; k < nfn; k += kSweepThreads) acc[fidn[k]] += accc[k];
+        }
     }
+    __syncthreads();  // the last tile's compact sums complete
+    for (int k = threadIdx.x; k < nfn_prev; k += kSweepThreads) acc[fidn_prev[k]] += accc[k];
     __syncthreads();
     for (int k = threadIdx.x; k < nr; k += kSweepThreads) part[T.u_slot[u] + k] = acc[k];
 }
@@ -1595,6 +1610,9 @@ int hh_tune(const char* key, int64_t value) {
         } else if (k == "unit_entries") {
             HH_REQUIRE(value == 0 || (value >= 4096 && value <= (1 << 24)), "unit_entries must be 0 (auto) or in [4096, 2^24]");
             g_unit_entries = value;
+        } else if (k == "flat_defer") {
+            HH_REQUIRE(value == 0 || value == 1, "flat_defer in {0, 1}");
+            g_flat_defer = (int)value;
         } else if (k == "unit_lpt") {
             HH_REQUIRE(value >= 0 && value <= 2, "unit_lpt in {0, 1, 2}");
             g_unit_lpt = value;

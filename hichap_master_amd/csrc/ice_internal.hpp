@@ -193,7 +193,10 @@ struct TileDev {
     const int32_t* tile_frec;
     const uint4* frec;
     const uint8_t* u_whole;
+    int flat_defer;  // flat kernel: merge a tile's compact sums after the next tile's barrier (hh_tune "flat_defer")
 };
+
+extern int g_flat_defer;
 
 }  // namespace hh
 
@@ -244,7 +247,7 @@ struct hh_matrix {
         return hh::TileDev{pay.p, payn.p, tile_J.p, tile_ent.p, tile_rp.p, tile_entn.p, tile_rpn.p, u_tlo.p,
                            u_thi.p, u_rb.p, u_rlo.p, u_rhi.p, u_slot.p, u_glo.p, u_ghi.p, blk_unit_ptr.p,
                            u_order.p, tile_perm.p, tile_band.p, tile_fw.p, tile_frec.p,
-                           reinterpret_cast<const uint4*>(frec.p), u_whole.p};
+                           reinterpret_cast<const uint4*>(frec.p), u_whole.p, hh::g_flat_defer};
     }
 };
 

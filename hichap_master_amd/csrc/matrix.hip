@@ -15,6 +15,7 @@ namespace hh {
 
 static thread_local std::string g_last_error;
 int64_t g_unit_entries = 0;  // 0 = auto (plan_tiles)
+int g_flat_defer = 1;
 int64_t g_unit_lpt = 1;      // launch lists by unit cost class, largest first (0: row order)
 int64_t g_unit_lpt_lists = 1; // which lists: 1 tiled, 2 flat, 3 both (flat too: C4 sweep +1 %, profiles/r2b_modes_ab.log)
 int64_t g_tile_cost = 32768; // payload-word equivalent of one tile's fixed cost in the unit split (C4 shard 8/8: 0.79 -> 0.65 ms/iter)
