@@ -7,7 +7,10 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <new>
+#include <sys/mman.h>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -222,12 +225,55 @@ struct DBuf {
     }
 };
 
-template <class T>
-DBuf<T> to_device(const std::vector<T>& v, hipStream_t s) {
+template <class T, class A>
+DBuf<T> to_device(const std::vector<T, A>& v, hipStream_t s) {
     DBuf<T> d(v.size());
     d.upload(v.data(), v.size(), s);
     return d;
 }
+
+// Host allocator for the big tile-plan arrays (~6 KB per tile, 140 MB at
+// 22 572 tiles): blocks of >= 2 MiB are anonymous mappings advised as
+// transparent huge pages, so filling them takes a few hundred 2 MiB faults
+// instead of ~35 000 4 KiB ones (the plan concatenation was first-touch bound).
+template <class T>
+struct HugeAlloc {
+    using value_type = T;
+    static constexpr size_t kHuge = size_t(2) << 20;
+    HugeAlloc() = default;
+    template <class U>
+    HugeAlloc(const HugeAlloc<U>&) {}
+    static size_t rounded(size_t b) { return (b + kHuge - 1) & ~(kHuge - 1); }
+    T* allocate(size_t n) {
+        const size_t b = n * sizeof(T);
+        if (b >= kHuge) {
+            void* p = mmap(nullptr, rounded(b), PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+            if (p == MAP_FAILED) throw std::bad_alloc();
+            (void)madvise(p, rounded(b), MADV_HUGEPAGE);
+            return static_cast<T*>(p);
+        }
+        void* p = std::malloc(b ? b : 1);
+        if (!p) throw std::bad_alloc();
+        return static_cast<T*>(p);
+    }
+    void deallocate(T* p, size_t n) {
+        const size_t b = n * sizeof(T);
+        if (b >= kHuge) (void)munmap(p, rounded(b));
+        else std::free(p);
+    }
+    // default-initialise (no zero fill): resize() does not touch the pages,
+    // so threads can fault them in while they copy
+    template <class U>
+    void construct(U* p) noexcept { ::new ((void*)p) U; }
+    template <class U, class... Args>
+    void construct(U* p, Args&&... a) { ::new ((void*)p) U(std::forward<Args>(a)...); }
+    template <class U>
+    bool operator==(const HugeAlloc<U>&) const { return true; }
+    template <class U>
+    bool operator!=(const HugeAlloc<U>&) const { return false; }
+};
+template <class T>
+using HVec = std::vector<T, HugeAlloc<T>>;
 
 // Pinned host buffer.
 template <class T>

@@ -131,20 +131,20 @@ struct TilePlan {
     int32_t nJ = 0;        // column tiles over the whole matrix
     std::vector<int32_t> tile_J;      // per tile
     std::vector<int64_t> tile_ent;    // per tile: first wide entry (multiple of 4)
-    std::vector<uint32_t> tile_rp;    // per tile: kR + 1 wide row offsets (relative)
+    HVec<uint32_t> tile_rp;    // per tile: kR + 1 wide row offsets (relative)
     std::vector<int64_t> tile_entn;   // per tile: first narrow entry (multiple of 8)
-    std::vector<uint32_t> tile_rpn;   // per tile: kR + 1 narrow row offsets (relative)
+    HVec<uint32_t> tile_rpn;   // per tile: kR + 1 narrow row offsets (relative)
     // per tile and segment (narrow, wide): rows ordered by decreasing length
     // (uint4 count, counting sort on min(len, 255), stable) and the bands of
     // that order swept with lane groups of 64/32/16/8/4 (kBands + 1 bounds)
-    std::vector<uint16_t> tile_perm;  // per tile: 2 x kR
-    std::vector<uint16_t> tile_band;  // per tile: 2 x kBandSlots
+    HVec<uint16_t> tile_perm;  // per tile: 2 x kR
+    HVec<uint16_t> tile_band;  // per tile: 2 x kBandSlots
     // per flat tile and segment: the 8 waves' split of the nonempty rows,
     // kFlatWaves + 1 pairs (first uint4, first compact row index); the last
     // pair is (segment uint4 count, number of nonempty rows)
-    std::vector<uint32_t> tile_fw;    // per tile: kFlatMeta words
+    HVec<uint32_t> tile_fw;    // per tile: kFlatMeta words
     std::vector<int32_t> tile_frec;   // per tile: index of its flat record, -1
-    std::vector<uint16_t> frec;       // flat records, kFrecU4 * 8 halves each
+    HVec<uint16_t> frec;       // flat records, kFrecU4 * 8 halves each
     std::vector<int32_t> tile_rb;     // per tile: local row-block
     std::vector<int32_t> blk_tile_ptr;  // nrb + 1
     std::vector<int32_t> tile_of;     // nrb * nJ -> tile index or -1

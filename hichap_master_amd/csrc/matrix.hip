@@ -209,31 +209,64 @@ TilePlan plan_tiles(const uint16_t* cntw, const uint16_t* cntn, int64_t nloc, in
         for (auto& t : th) t.join();
     }
     const auto tp1 = std::chrono::steady_clock::now();
-    // concatenation in block order (its cost is first-touch page faults of
-    // the ~6 KB per tile of plan arrays, not the copies: a parallel copy
-    // measured the same 45 ms at 22 572 tiles)
+    // concatenation in block order.  Its cost was first-touch page faults of
+    // the ~6 KB per tile of plan arrays (45 ms at 22 572 tiles, a parallel
+    // copy into 4 KiB pages no faster): the big arrays now live on
+    // THP-advised mappings (HVec), are sized without being touched, and the
+    // blocks are copied into them by the planning threads.
     size_t nt_all = 0, nfrec = 0;
-    for (const auto& B : blocks) {
-        nt_all += B.J.size();
+    std::vector<size_t> t_off((size_t)P.nrb + 1, 0), f_off((size_t)P.nrb + 1, 0);
+    for (int64_t rb = 0; rb < P.nrb; ++rb) {
+        const BlockTiles& B = blocks[rb];
+        const size_t k = B.J.size();
+        if (B.rp.size() != k * (kR + 1) || B.rpn.size() != k * (kR + 1) || B.fw.size() != k * kFlatMeta ||
+            B.perm.size() != k * 2 * kR || B.band.size() != k * 2 * kBandSlots || B.flat.size() != k)
+            HH_THROW(HH_ERR_STATE, "tile plan: inconsistent per-block array sizes");
+        t_off[rb] = nt_all;
+        f_off[rb] = nfrec;
+        nt_all += k;
         nfrec += B.frec.size();
     }
+    t_off[P.nrb] = nt_all;
+    f_off[P.nrb] = nfrec;
     P.tile_J.reserve(nt_all);
     P.tile_ent.reserve(nt_all);
     P.tile_entn.reserve(nt_all);
     P.tile_rb.reserve(nt_all);
-    P.tile_rp.reserve(nt_all * (kR + 1));
-    P.tile_rpn.reserve(nt_all * (kR + 1));
-    P.tile_fw.reserve(nt_all * kFlatMeta);
-    P.tile_perm.reserve(nt_all * 2 * kR);
-    P.tile_band.reserve(nt_all * 2 * kBandSlots);
     P.tile_frec.reserve(nt_all);
     P.tile_flat.reserve(nt_all);
-    P.frec.reserve(nfrec);
+    P.tile_rp.resize(nt_all * (kR + 1));
+    P.tile_rpn.resize(nt_all * (kR + 1));
+    P.tile_fw.resize(nt_all * kFlatMeta);
+    P.tile_perm.resize(nt_all * 2 * kR);
+    P.tile_band.resize(nt_all * 2 * kBandSlots);
+    P.frec.resize(nfrec);
+    {
+        const int nt = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)std::thread::hardware_concurrency(),
+                                                                     (int64_t)16, P.nrb}));
+        std::atomic<int64_t> next{0};
+        auto copy = [&] {
+            for (int64_t rb; (rb = next.fetch_add(1)) < P.nrb;) {
+                const BlockTiles& B = blocks[rb];
+                const size_t t0 = t_off[rb];
+                std::copy(B.rp.begin(), B.rp.end(), P.tile_rp.begin() + t0 * (kR + 1));
+                std::copy(B.rpn.begin(), B.rpn.end(), P.tile_rpn.begin() + t0 * (kR + 1));
+                std::copy(B.fw.begin(), B.fw.end(), P.tile_fw.begin() + t0 * kFlatMeta);
+                std::copy(B.perm.begin(), B.perm.end(), P.tile_perm.begin() + t0 * 2 * kR);
+                std::copy(B.band.begin(), B.band.end(), P.tile_band.begin() + t0 * 2 * kBandSlots);
+                std::copy(B.frec.begin(), B.frec.end(), P.frec.begin() + f_off[rb]);
+            }
+        };
+        std::vector<std::thread> th;
+        for (int t = 1; t < nt; ++t) th.emplace_back(copy);
+        copy();
+        for (auto& t : th) t.join();
+    }
     int64_t ent = 0, entn = 0;
     for (int64_t rb = 0; rb < P.nrb; ++rb) {
         BlockTiles& B = blocks[rb];
         P.blk_tile_ptr[rb] = (int32_t)P.tile_J.size();
-        const int32_t frec0 = (int32_t)(P.frec.size() / (kFrecU4 * 8));
+        const int32_t frec0 = (int32_t)(f_off[rb] / (kFrecU4 * 8));
         for (size_t i = 0; i < B.J.size(); ++i) {
             P.tile_of[rb * nJ + B.J[i]] = (int32_t)P.tile_J.size();
             P.tile_J.push_back(B.J[i]);
@@ -242,13 +275,7 @@ TilePlan plan_tiles(const uint16_t* cntw, const uint16_t* cntn, int64_t nloc, in
             P.tile_rb.push_back((int32_t)rb);
             P.tile_frec.push_back(B.frec_of[i] < 0 ? -1 : frec0 + B.frec_of[i]);
         }
-        P.tile_rp.insert(P.tile_rp.end(), B.rp.begin(), B.rp.end());
-        P.tile_rpn.insert(P.tile_rpn.end(), B.rpn.begin(), B.rpn.end());
-        P.tile_fw.insert(P.tile_fw.end(), B.fw.begin(), B.fw.end());
-        P.tile_perm.insert(P.tile_perm.end(), B.perm.begin(), B.perm.end());
-        P.tile_band.insert(P.tile_band.end(), B.band.begin(), B.band.end());
         P.tile_flat.insert(P.tile_flat.end(), B.flat.begin(), B.flat.end());
-        P.frec.insert(P.frec.end(), B.frec.begin(), B.frec.end());
         ent += B.ent_total;
         entn += B.entn_total;
         B = BlockTiles();  // free as we go
