@@ -1102,7 +1102,16 @@ __global__ __launch_bounds__(kMargThreads) void k_marg(TileDev T, const double* 
     }
     double v = 0.0;
     if (live) {
-        for (int c = 0; c < nch; ++c) s += bpart[(long long)c * nloc + i];  // dense band chunks, fixed order
+        // dense band chunks, fixed order; loads issued 8 at a time
+        int c = 0;
+        for (; c + 8 <= nch; c += 8) {
+            double x[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) x[q] = bpart[(long long)(c + q) * nloc + i];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) s += x[q];
+        }
+        for (; c < nch; ++c) s += bpart[(long long)c * nloc + i];
         for (long long q = wide_ptr[i]; q < wide_ptr[i + 1]; ++q) s = fma(wide_cnt[q], b[wide_col[q]], s);
         const double br = b[row_lo + i];
         v = br * fma(2.0 * diag[i], br, s);
