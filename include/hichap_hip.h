@@ -61,7 +61,14 @@ int hh_device_copy(void* dst, const void* src, int64_t bytes, void* stream);
  * "sweep_ablate" 0/1/2 (timing ablations only: 1 skips the LDS gathers,
  * 2 skips the b staging; results are wrong while set), "sweep_trace" n
  * (diagnostic: record start / end wall clock and CU of each block of the
- * single-launch sweep when its grid has <= n blocks; 0 frees the buffer). */
+ * single-launch sweep when its grid has <= n blocks; 0 frees the buffer),
+ * "fuse_stats" -1/0/1 (ICE statistics fused into k_marg + last-block tails:
+ * auto = up to 128 stats tiles), "band_lpt" 0/1 (band chunks dispatched
+ * heaviest first), "unit_lpt" 0/1/2 and "unit_lpt_lists" 1..3 (work-unit
+ * launch lists by cost; later builds), "flat_defer" 0/1 (flat sweep merges a
+ * tile's compact sums after the next tile's barrier), "syrk_split" -1 / 0 /
+ * n (K splits of the compartment correlation GEMM: auto, never, forced).
+ * None of them changes a result bit except the ablations. */
 int hh_tune(const char* key, int64_t value);
 /* The last traced single-launch sweep: *n blocks; out (cap >= 3 n words) gets
  * (start, end, cu) per block in grid order (tiled units | band blocks | flat
