@@ -68,7 +68,8 @@ int hh_device_copy(void* dst, const void* src, int64_t bytes, void* stream);
  * launch lists by cost; later builds), "flat_defer" 0/1 (flat sweep merges a
  * tile's compact sums after the next tile's barrier), "syrk_split" -1 / 0 /
  * n (K splits of the compartment correlation GEMM: auto, never, forced).
- * None of them changes a result bit except the ablations. */
+ * fuse_stats / syrk_split change reduction orders (last bits); the ablations
+ * give wrong results; the others leave every bit unchanged. */
 int hh_tune(const char* key, int64_t value);
 /* The last traced single-launch sweep: *n blocks; out (cap >= 3 n words) gets
  * (start, end, cu) per block in grid order (tiled units | band blocks | flat
