@@ -40,6 +40,8 @@ struct PxErr {
     int code;                  // of that pixel: 1 range, 2 bin1 > bin2, 3 unsorted, 4 duplicate, 5 count
 };
 
+constexpr int kOccCopies = 64;
+
 template <class Id, class Cnt>
 __global__ __launch_bounds__(256) void k_px_check(const Id* __restrict__ b1, const Id* __restrict__ b2,
                                                   const Cnt* __restrict__ cnt, long long nnz, long long n_bins,
@@ -77,9 +79,26 @@ __global__ __launch_bounds__(256) void k_px_check(const Id* __restrict__ b1, con
     B[i] = (int32_t)b;
     const long long d = b - a;
     if (c && d >= 1 && d <= occ_max) {
-        atomicAdd(occ + d, 1u);
-        if (c > kBand4MaxCnt) atomicAdd(big + d, 1u);
+        // one of kOccCopies histogram copies per block: every row hits the
+        // same near-diagonal counters, so one copy serialised ~n_bins atomics
+        // per address (k_occ_reduce sums the copies)
+        const long long o = (long long)(blockIdx.x % kOccCopies) * (occ_max + 1) + d;
+        atomicAdd(occ + o, 1u);
+        if (c > kBand4MaxCnt) atomicAdd(big + o, 1u);
     }
+}
+
+__global__ void k_occ_reduce(const unsigned* __restrict__ occ, const unsigned* __restrict__ big, int len,
+                             unsigned* __restrict__ occ_out, unsigned* __restrict__ big_out) {
+    const int d = blockIdx.x * blockDim.x + threadIdx.x;
+    if (d >= len) return;
+    unsigned a = 0, b = 0;
+    for (int k = 0; k < kOccCopies; ++k) {
+        a += occ[(long long)k * len + d];
+        b += big[(long long)k * len + d];
+    }
+    occ_out[d] = a;
+    big_out[d] = b;
 }
 
 // ptr[r] = first i with A[i] >= r, r in [0, n_bins]  (A sorted, nnz >= 1)
@@ -383,14 +402,17 @@ void build_from_device_pixels(const Id* b1, const Id* b2, const Cnt* cnt, int64_
     DBuf<int32_t> dA(std::max<int64_t>(nnz, 1)), dB(std::max<int64_t>(nnz, 1));
     DBuf<uint32_t> dkc(std::max<int64_t>(nnz, 1));
     DBuf<unsigned> docc(occ_max + 1), dbig(occ_max + 1);
+    DBuf<unsigned> docc_c((size_t)kOccCopies * (occ_max + 1)), dbig_c((size_t)kOccCopies * (occ_max + 1));
     DBuf<unsigned long long> derr(5);
-    docc.zero(s);
-    dbig.zero(s);
+    docc_c.zero(s);
+    dbig_c.zero(s);
     HIP_CHECK(hipMemsetAsync(derr.p, 0xff, 5 * sizeof(unsigned long long), s));
     if (nnz > 0)
         hipLaunchKernelGGL((k_px_check<Id, Cnt>), dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s, b1, b2, cnt,
-                           (long long)nnz, (long long)n_bins, dch.p, ignore_diags, cis_only, dA.p, dB.p, dkc.p, docc.p,
-                           dbig.p, occ_max, derr.p);
+                           (long long)nnz, (long long)n_bins, dch.p, ignore_diags, cis_only, dA.p, dB.p, dkc.p, docc_c.p,
+                           dbig_c.p, occ_max, derr.p);
+    hipLaunchKernelGGL(k_occ_reduce, dim3((unsigned)((occ_max + 1 + 255) / 256)), dim3(256), 0, s, docc_c.p, dbig_c.p,
+                       occ_max + 1, docc.p, dbig.p);
     HIP_CHECK(hipGetLastError());
     std::vector<unsigned long long> herr(5);
     derr.download(herr.data(), 5, s);
