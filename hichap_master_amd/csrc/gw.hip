@@ -103,14 +103,23 @@ constexpr int kGwStatBlocks = 2048;
 // the diagonal once): exact integer sums / counts.  The table is sorted by
 // bin1: the bin1 end is a segmented sum, the bin2 end an atomic per pixel
 // (distinct columns within a wave).
+// PACK: the bin2 end as ONE atomic per pixel, (count << 24) + 1 into rpk
+// (the host splits it: sum in the high 40 bits, nonzeros in the low 24), and
+// the table's count total in *total so the host can verify that no sum
+// reached 2^40 (else it reruns unpacked).  Needs n_bins < 2^24.
+template <bool PACK>
 __global__ __launch_bounds__(256) void k_gw_tstats(const int32_t* __restrict__ a, const int32_t* __restrict__ b,
                                                    const uint32_t* __restrict__ v, long long nnz,
                                                    const int32_t* __restrict__ chrom_of,
                                                    unsigned long long* __restrict__ rsum,
-                                                   unsigned long long* __restrict__ rnz) {
+                                                   unsigned long long* __restrict__ rnz,
+                                                   unsigned long long* __restrict__ rpk,
+                                                   unsigned long long* __restrict__ total) {
+    __shared__ unsigned long long wsum[4];
     const long long stride = (long long)gridDim.x * blockDim.x;
     const long long start = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     const long long end = (nnz + 63) / 64 * 64;  // whole waves iterate together
+    unsigned long long t = 0;
     for (long long i = start; i < end; i += stride) {
         long long x = 0x7fffffffLL;
         unsigned long long c = 0, one = 0;
@@ -118,17 +127,31 @@ __global__ __launch_bounds__(256) void k_gw_tstats(const int32_t* __restrict__ a
             x = a[i];
             const int32_t y = b[i];
             const uint32_t cc = v[i];
+            if (PACK) t += cc;
             if (cc != 0u && chrom_of[x] == chrom_of[y]) {
                 c = cc;
                 one = 1;
                 if (x != y) {
-                    atomicAdd(rsum + y, (unsigned long long)cc);
-                    atomicAdd(rnz + y, 1ull);
+                    if (PACK) {
+                        atomicAdd(rpk + y, ((unsigned long long)cc << 24) | 1ull);
+                    } else {
+                        atomicAdd(rsum + y, (unsigned long long)cc);
+                        atomicAdd(rnz + y, 1ull);
+                    }
                 }
             }
         }
         seg_add_u64(x, c, rsum);
         seg_add_u64(x, one, rnz);
+    }
+    if (PACK) {
+        t = (unsigned long long)wave_sum_ll((long long)t);
+        if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = t;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const unsigned long long bt = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+            if (bt) atomicAdd(total, bt);
+        }
     }
 }
 
@@ -455,9 +478,18 @@ void gw_create(hh_gw& G, const Id* t1, const Id* t2, const Cnt* tv, int64_t t_nn
     hbs.zero(s);
     htot.zero(s);
     auto sgrid = [](int64_t nnz) { return dim3((unsigned)std::min<int64_t>(kGwStatBlocks, (nnz + 255) / 256)); };
-    if (t_nnz > 0)
-        hipLaunchKernelGGL(k_gw_tstats, sgrid(t_nnz), dim3(256), 0, s, G.tA.p, G.tB.p, G.tV.p, (long long)t_nnz, dch.p,
-                           trs.p, tnz.p);
+    const bool tpack = n < (1LL << 24);
+    DBuf<unsigned long long> tpk(tpack ? n : 1), ttot(1);
+    if (tpack) tpk.zero(s);
+    ttot.zero(s);
+    if (t_nnz > 0) {
+        if (tpack)
+            hipLaunchKernelGGL(k_gw_tstats<true>, sgrid(t_nnz), dim3(256), 0, s, G.tA.p, G.tB.p, G.tV.p,
+                               (long long)t_nnz, dch.p, trs.p, tnz.p, tpk.p, ttot.p);
+        else
+            hipLaunchKernelGGL(k_gw_tstats<false>, sgrid(t_nnz), dim3(256), 0, s, G.tA.p, G.tB.p, G.tV.p,
+                               (long long)t_nnz, dch.p, trs.p, tnz.p, nullptr, nullptr);
+    }
     if (h_nnz > 0)
         hipLaunchKernelGGL(k_gw_hstats, sgrid(h_nnz), dim3(256), 0, s, G.R.p, G.C.p, G.V.p, (long long)h_nnz, dblk.p,
                            hbs.p, htot.p);
@@ -469,6 +501,28 @@ void gw_create(hh_gw& G, const Id* t1, const Id* t2, const Cnt* tv, int64_t t_nn
     tnz.download(G.t_nnz_row.data(), n, s);
     hbs.download(G.h_blocksum.data(), 2 * n, s);
     htot.download(&G.h_total, 1, s);
+    if (tpack && t_nnz > 0) {
+        unsigned long long tt = 0;
+        ttot.download(&tt, 1, s);
+        std::vector<unsigned long long> pk(n);
+        tpk.download(pk.data(), n, s);
+        HIP_CHECK(hipStreamSynchronize(s));
+        if (tt < (1ull << 40)) {  // no column sum can have carried into bit 64
+            for (int64_t y = 0; y < n; ++y) {
+                G.t_rowsum[y] += pk[y] >> 24;
+                G.t_nnz_row[y] += pk[y] & 0xffffffull;
+            }
+        } else {  // counts too large for the packed field: the two-atomic pass
+            trs.zero(s);
+            tnz.zero(s);
+            hipLaunchKernelGGL(k_gw_tstats<false>, sgrid(t_nnz), dim3(256), 0, s, G.tA.p, G.tB.p, G.tV.p,
+                               (long long)t_nnz, dch.p, trs.p, tnz.p, nullptr, nullptr);
+            HIP_CHECK(hipGetLastError());
+            trs.download(G.t_rowsum.data(), n, s);
+            tnz.download(G.t_nnz_row.data(), n, s);
+            HIP_CHECK(hipStreamSynchronize(s));
+        }
+    }
     // H row pointers and column lists
     G.hptr.alloc(2 * n + 1);
     if (h_nnz > 0)
