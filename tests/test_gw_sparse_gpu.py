@@ -76,6 +76,25 @@ def test_matches_oracle_with_orphans_and_diagonal(mb, seed):
     _check_upper(b1, b2, v, dense, 1e-12)
 
 
+def test_huge_t_counts_unpacked_path(mb):
+    """T counts near 2^32 (count total > 2^40): the packed one-atomic column
+    statistics cannot hold the sums, so hh_gw_create reruns them unpacked;
+    the result still equals the oracle and the dense path."""
+    rng = np.random.default_rng(5)
+    sizes = [60, 40]
+    n = sum(sizes)
+    T = np.triu(rng.poisson(2.0, size=(n, n)) * (rng.random((n, n)) < 0.5)).astype(np.int64)
+    T = np.where(T > 0, 3_000_000_000 + T, 0)
+    T = T + np.triu(T, 1).T
+    assert T.max() < 2**32 and np.triu(T).sum() > 2**40
+    H = rng.poisson(0.8, size=(2 * n, 2 * n)) * (rng.random((2 * n, 2 * n)) < 0.3)
+    bins, hbins = _layout(["1", "2"], sizes)
+    tp, hc = _tables(T, H)
+    b1, b2, v = mb.GenomeWideMatrixCorrectionSparse(bins, hbins, tp, hc)
+    ref = hichap_ref.genome_wide_correction(bins, hbins, T, H)
+    _check_upper(b1, b2, v, ref, 1e-12)
+
+
 def test_device_tables_and_errors(mb):
     import torch
     from hichap_master_amd._lib import HipLibraryError
