@@ -1121,7 +1121,7 @@ __global__ __launch_bounds__(kMargThreads) void k_marg(TileDev T, const double* 
     const int B = (int)(row_lo / kR) + rbk;
     for (int t = ta.blk_tile_ptr[B]; t < ta.blk_tile_ptr[B + 1]; ++t)
         if (act[ta.tile_group[t]] != 0) tile_stats(ta, t, row_lo + i, v, sh);
-    if (last_block(ta.counter, &flag)) stats_tail(ta, act, G);
+    if (stats == 1 && last_block(ta.counter, &flag)) stats_tail(ta, act, G);  // 2: tile sums only (big mode)
 }
 
 __global__ void k_scatter(const double* __restrict__ g, int world, long long maxlen,
@@ -1363,9 +1363,10 @@ struct hh_ice {
                         tile_sum.p, tile_sq.p, g_cnt.p, g_sum.p, counter.p};
     }
     // stats mode: few tiles -> fused k_marg stats + last-block tails (2
-    // launches after the sweep); many -> 4 launches, no tails (hh_tune
-    // "fuse_stats": -1 auto, 0 never, 1 always)
-    bool small_stats() const { return hh::g_fuse_stats > 0 || (hh::g_fuse_stats < 0 && n_tiles <= hh::kFuseMaxTiles); }
+    // launches after the sweep); many -> tile sums in k_marg, k_stats2,
+    // k_update_big, no tails (hh_tune "fuse_stats": -1 auto, 0 never fused:
+    // k_stats1 launched, 1 always the small mode, 2 always the big mode)
+    bool small_stats() const { return hh::g_fuse_stats == 1 || (hh::g_fuse_stats < 0 && n_tiles <= hh::kFuseMaxTiles); }
     uint8_t* act() { return active.p + (iters_done & 1) * G; }
     uint8_t* nxt() { return active.p + (1 - (iters_done & 1)) * G; }
 };
@@ -1554,7 +1555,11 @@ static void marg_weighted(hh_ice* S, double* out, hipStream_t s, bool timed, int
     if (S->nloc == 0) return;
     // stats fused into k_marg when this GPU holds every row and `out` is the
     // marginal vector update() reads (k_stats1's tile sums, bitwise)
-    const int stats = S->small_stats() && S->full() && out == S->marg.p && S->n_tiles > 0;
+    // 1: tile sums + the last-block group tail (few tiles); 2: tile sums only
+    // (k_stats1's work without its launch; k_stats2 / k_update_big reduce)
+    const int stats = (g_fuse_stats != 0 && S->full() && out == S->marg.p && S->n_tiles > 0)
+                          ? (S->small_stats() ? 1 : 2)
+                          : 0;
     hipLaunchKernelGGL(k_marg, dim3(nblocks(S->nloc, kR)), dim3(kMargThreads), 0, s, m->dev(), S->part.p,
                        m->wide_ptr.p, m->wide_col.p, m->wide_cnt.p, m->diag.p, m->row_group.p, S->act(),
                        S->bias.p, (long long)m->row_lo, (int)S->nloc, S->bpart.p, (int)S->nch, out, S->ta(),
@@ -1574,8 +1579,9 @@ static void update(hh_ice* S, hipStream_t s) {
             hipLaunchKernelGGL(k_update, dim3(S->n_tiles), dim3(kR), 0, s, ta, S->act(), S->nxt(), S->marg.p,
                                S->bias.p, gs, S->o.tol, S->o.max_iters, (int)S->G);
         } else {
-            hipLaunchKernelGGL(k_stats1<false>, dim3(S->n_tiles), dim3(kR), 0, s, ta, S->act(), S->marg.p,
-                               (int)S->G);
+            if (!S->stats_fresh)
+                hipLaunchKernelGGL(k_stats1<false>, dim3(S->n_tiles), dim3(kR), 0, s, ta, S->act(), S->marg.p,
+                                   (int)S->G);
             hipLaunchKernelGGL(k_stats2, dim3(S->n_tiles), dim3(kR), 0, s, ta, S->act(), S->marg.p);
             hipLaunchKernelGGL(k_update_big, dim3(S->n_tiles), dim3(kR), 0, s, ta, S->act(), S->nxt(), S->marg.p,
                                S->bias.p, gs, S->o.tol, S->o.max_iters);
@@ -1648,7 +1654,7 @@ int hh_tune(const char* key, int64_t value) {
             HH_REQUIRE(value == 0 || value == 1, "band_lpt in {0, 1}");
             g_band_lpt = (int)value;
         } else if (k == "fuse_stats") {
-            HH_REQUIRE(value >= -1 && value <= 1, "fuse_stats in {-1, 0, 1}");
+            HH_REQUIRE(value >= -1 && value <= 2, "fuse_stats in {-1, 0, 1, 2}");
             g_fuse_stats = (int)value;
         } else if (k == "split_tiles") {
             HH_REQUIRE(value == 0 || value == 1, "split_tiles in {0, 1}");

@@ -494,13 +494,14 @@ def test_sweep_launch_shapes_bitwise(ice, cis_only):
     np.testing.assert_allclose(ref[0], wr, rtol=1e-9, equal_nan=True)
 
 
-@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("mode", [0, 1, 2])
 @pytest.mark.parametrize("cis_only", [False, True])
 def test_stats_modes(ice, mode, cis_only):
-    """Both ICE stats paths (hh_tune fuse_stats: 1 = stats fused into k_marg +
-    last-block tails, 0 = k_stats1 / k_stats2 / k_update_big as used for
-    matrices of > 128 stats tiles) against the oracle, with the same iteration
-    counts, and sharded == one shard bitwise within each mode."""
+    """The ICE stats paths (hh_tune fuse_stats: 1 = stats fused into k_marg +
+    last-block tails, 2 = tile sums in k_marg then k_stats2 / k_update_big as
+    used for matrices of > 128 stats tiles, 0 = never fused: k_stats1
+    launched) against the oracle, with the same iteration counts, and
+    sharded == one shard bitwise within each mode."""
     from hichap_master_amd import _lib, dist
     b1, b2, c, off = _case(12, sizes=(600, 450, 300))
     n = int(off[-1])
