@@ -62,8 +62,9 @@ int hh_device_copy(void* dst, const void* src, int64_t bytes, void* stream);
  * 2 skips the b staging; results are wrong while set), "sweep_trace" n
  * (diagnostic: record start / end wall clock and CU of each block of the
  * single-launch sweep when its grid has <= n blocks; 0 frees the buffer),
- * "fuse_stats" -1/0/1 (ICE statistics fused into k_marg + last-block tails:
- * auto = up to 128 stats tiles), "band_lpt" 0/1 (band chunks dispatched
+ * "fuse_stats" -1/0/1/2 (ICE statistics: -1 auto, 0 never fused into k_marg,
+ * 1 fused + last-block tails (auto up to 128 stats tiles), 2 tile sums in
+ * k_marg + block-wide group reductions (auto above)), "band_lpt" 0/1 (band chunks dispatched
  * heaviest first), "unit_lpt" 0/1/2 and "unit_lpt_lists" 1..3 (work-unit
  * launch lists by cost; later builds), "flat_defer" 0/1 (flat sweep merges a
  * tile's compact sums after the next tile's barrier), "syrk_split" -1 / 0 /
