@@ -1519,6 +1519,22 @@ static void sweep_single(hh_ice* S, hipStream_t s) {
     HIP_CHECK(hipGetLastError());
 }
 
+// The three-stream sweep's side streams and events, created on first use
+// (matrices below conc_min_bytes never need them; stream creation per
+// hh_ice_create cost the small balances ~ms).
+static void ensure_side_streams(hh_ice* S) {
+    if (S->side) return;
+    int cur = 0;
+    HIP_CHECK(hipGetDevice(&cur));
+    if (cur != S->m->device) HIP_CHECK(hipSetDevice(S->m->device));
+    HIP_CHECK(hipStreamCreateWithFlags(&S->side, hipStreamNonBlocking));
+    HIP_CHECK(hipEventCreateWithFlags(&S->fork, hipEventDisableTiming));
+    HIP_CHECK(hipEventCreateWithFlags(&S->join, hipEventDisableTiming));
+    HIP_CHECK(hipStreamCreateWithFlags(&S->side2, hipStreamNonBlocking));
+    HIP_CHECK(hipEventCreateWithFlags(&S->join2, hipEventDisableTiming));
+    if (cur != S->m->device) HIP_CHECK(hipSetDevice(cur));
+}
+
 static void marg_weighted(hh_ice* S, double* out, hipStream_t s, bool timed, int slot) {
     hh_matrix* m = S->m;
     if (timed) HIP_CHECK(hipEventRecord(S->ev[2 * slot], s));
@@ -1534,6 +1550,7 @@ static void marg_weighted(hh_ice* S, double* out, hipStream_t s, bool timed, int
         if (single) {
             sweep_single(S, s);
         } else if (conc) {
+            ensure_side_streams(S);
             HIP_CHECK(hipEventRecord(S->fork, s));
             HIP_CHECK(hipStreamWaitEvent(S->side, S->fork, 0));
             sweep_band(S, S->side);
@@ -1763,11 +1780,7 @@ int hh_ice_create(hh_matrix* m, const hh_ice_opts* o, hh_ice** out) {
         if (m->band_w4 > m->band_w)
             S->nch += 2 * (int32_t)((band4_seg(m->band_w, m->band_w4) + kBandChunk - 1) / kBandChunk);
         S->bpart.alloc(std::max<int64_t>((int64_t)S->nch * S->nloc, 1));
-        HIP_CHECK(hipStreamCreateWithFlags(&S->side, hipStreamNonBlocking));
-        HIP_CHECK(hipEventCreateWithFlags(&S->fork, hipEventDisableTiming));
-        HIP_CHECK(hipEventCreateWithFlags(&S->join, hipEventDisableTiming));
-        HIP_CHECK(hipStreamCreateWithFlags(&S->side2, hipStreamNonBlocking));
-        HIP_CHECK(hipEventCreateWithFlags(&S->join2, hipEventDisableTiming));
+        // (the side streams of the three-stream sweep are made on first use)
 
         S->tile_cnt.alloc(std::max(S->n_tiles, 1));
         S->tile_sum.alloc(std::max(S->n_tiles, 1));
