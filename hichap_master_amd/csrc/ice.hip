@@ -2016,16 +2016,23 @@ int hh_ice_finalize(hh_ice* S, double* weights, double* scale, double* var, int3
 int hh_ice_balance(hh_matrix* m, const hh_ice_opts* o, double* weights, double* scale, double* var,
                    int32_t* iters, int32_t* converged, double* sweep_seconds, void* stream) {
     hh_ice* S = nullptr;
+    const auto tc0 = std::chrono::steady_clock::now();
+    auto ms_since = [](std::chrono::steady_clock::time_point a) {
+        return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count();
+    };
     int rc = hh_ice_create(m, o, &S);
     if (rc) return rc;
+    if (g_build_debug) fprintf(stderr, "[ice] create %.3f ms\n", ms_since(tc0));
     rc = guard([&] {
         HH_REQUIRE(S->full(), "hh_ice_balance needs a matrix holding every row");
         auto ok = [](int r) { if (r) throw Error(r, hh_last_error()); };
+        const auto tf0 = std::chrono::steady_clock::now();
         ok(hh_ice_marg_local(S, 0, nullptr, stream));
         ok(hh_ice_filter_nnz(S, stream));
         ok(hh_ice_marg_local(S, 1, nullptr, stream));
         ok(hh_ice_filter_count_mad(S, stream));
         HIP_CHECK(hipStreamSynchronize(as_stream(stream)));
+        if (g_build_debug) fprintf(stderr, "[ice] filters %.3f ms\n", ms_since(tf0));
         const auto t0 = std::chrono::steady_clock::now();
         while (S->iters_done < S->o.max_iters) {
             const int k = std::min(S->o.check_every, S->o.max_iters - S->iters_done);
@@ -2041,8 +2048,11 @@ int hh_ice_balance(hh_matrix* m, const hh_ice_opts* o, double* weights, double* 
         const auto t1 = std::chrono::steady_clock::now();
         if (sweep_seconds) *sweep_seconds = std::chrono::duration<double>(t1 - t0).count();
         ok(hh_ice_finalize(S, weights, scale, var, iters, converged, stream));
+        if (g_build_debug) fprintf(stderr, "[ice] finalize %.3f ms\n", ms_since(t1));
     });
+    const auto tx0 = std::chrono::steady_clock::now();
     hh_ice_free(S);
+    if (g_build_debug) fprintf(stderr, "[ice] free %.3f ms (balance total %.3f ms)\n", ms_since(tx0), ms_since(tc0));
     return rc;
 }
 
