@@ -196,7 +196,7 @@ def balance_cooler(uri, ignore_diags=1, cis_only=False, mad_max=5, min_nnz=10, m
 def _bins_arrays(chromsizes, binsize):
     names, starts, ends, cids = [], [], [], []
     for k, (nm, L) in enumerate(chromsizes):
-        s = np.arange(0, L, binsize, dtype=np.int64)
+        s = np.arange(0, L, binsize, dtype=np.int32)  # cooler COORD_DTYPE
         starts.append(s)
         ends.append(np.minimum(s + binsize, L))
         cids.append(np.full(s.size, k, dtype=np.int32))

@@ -1,30 +1,33 @@
 """Minimal HDF5 reader / writer for cooler files.
 
-h5py / libhdf5 are absent from this image and from the GPU box, so the
-cooler drop-in (``coolio.py``: ``cooler balance`` as matrixBuilding.py:708
-invokes it, and the ``Cooler(...).matrix().fetch()`` reads of
-StructureFind.py:513 / :853 / :2006) reads and writes the HDF5 file format
-itself, restated from the published HDF5 File Format Specification 3.0.
+h5py is absent from this image and from the GPU box, so the cooler drop-in
+(``coolio.py``: ``cooler balance`` as matrixBuilding.py:708 invokes it, and the
+``Cooler(...).matrix().fetch()`` reads of StructureFind.py:513 / :853 / :2006)
+reads and writes the HDF5 file format itself, restated from the published
+HDF5 File Format Specification 3.0.
 
-PARITY UNPINNED: there is no HDF5 file in /root/reference and no HDF5
-implementation here to check against; tests/test_h5.py checks round trips of
-this module's own writer, the reader on hand-assembled structures of the
-forms libhdf5 writes (chunked + shuffle + deflate datasets, v1 B-trees,
-variable-length string attributes in the global heap, enum types, v2 object
-headers with link messages), and the in-place append.
+PINNED at the file-format level against the real libhdf5 (1.10.6, present in
+/opt/conda of the build container only; tests/test_h5_libhdf5.py): coolers
+written by libhdf5 with h5py's default ("earliest") and with libver "latest"
+format bounds are read exactly as libhdf5 reads them, and libhdf5 (its
+listing, h5dump, h5repack + h5diff) reads every file this module writes or
+appends to.  cooler's own schema handling stays unpinned (cooler is absent).
 
 Read support: superblock v0/v1/v2/v3; object headers v1 and v2 (with
-continuation blocks); old-style (symbol table) and compact new-style (link
-message) groups; contiguous / compact / chunked (v1 B-tree, layout v3; v4
-single-chunk) datasets with shuffle / deflate filters (fletcher32 checksums
-are stripped, not verified; v2 metadata checksums are not verified);
-fixed-point, floating-point, fixed and variable-length string, enum and
-bitfield types; attributes (v1-v3).
+continuation blocks); old-style (symbol table) groups, new-style groups with
+compact (link messages) or dense (fractal heap + v2 B-tree) link storage;
+compact and dense attribute storage; contiguous / compact / chunked datasets
+(v1 B-tree; layout v4 single-chunk, implicit, fixed-array and
+extensible-array indexes, unpaged) with shuffle / deflate filters (fletcher32
+checksums are stripped, not verified; v2 metadata checksums are not
+verified); fixed-point, floating-point, fixed and variable-length string,
+enum and bitfield types; attributes (v1-v3).  Anything else raises H5Error.
 
 Write support: a new file from an in-memory tree (superblock v0, v1 object
-headers, symbol-table groups, contiguous datasets) -- the layout libhdf5
-produces with its default "earliest" format bounds -- and, on an existing
-file, adding or replacing one dataset in a symbol-table group in place
+headers, symbol-table groups, contiguous datasets, str attributes as
+variable-length UTF-8 in a global heap) -- the layout libhdf5 produces with
+its default "earliest" format bounds, as h5py writes -- and, on an existing
+v0/v1 file, adding or replacing one dataset in a symbol-table group in place
 (``append_dataset``: what ``cooler balance --force`` does to ``bins/weight``).
 """
 from __future__ import annotations
@@ -299,7 +302,7 @@ class File:
             return False
 
 
-def _decode_attr_values(fobj, typ, shape, raw):
+def _decode_attr_values(fobj, typ, shape, raw, raw_enum=False):
     n = int(np.prod(shape)) if shape else 1
     if typ.vlen_str is not None:
         vals = []
@@ -309,7 +312,9 @@ def _decode_attr_values(fobj, typ, shape, raw):
         arr = np.array(vals, dtype=object)
     else:
         arr = np.frombuffer(bytes(raw[:n * typ.dtype.itemsize]), dtype=typ.dtype).copy()
-        if typ.enum is not None and set(typ.enum) == {"FALSE", "TRUE"}:
+        if raw_enum:  # raw values: enum integers, fixed strings as padded bytes
+            pass
+        elif typ.enum is not None and set(typ.enum) == {"FALSE", "TRUE"}:
             arr = arr.astype(bool)
         elif arr.dtype.kind == "S":
             arr = np.array([x.rstrip(b"\0").decode("utf-8", "replace") for x in arr], dtype=object)
@@ -319,7 +324,8 @@ def _decode_attr_values(fobj, typ, shape, raw):
     return arr.reshape(shape)
 
 
-def _parse_attribute(fobj, data):
+def _parse_attribute(fobj, data, raw_enum=False):
+    """(name, H5Type, shape, value) of an attribute message (versions 1-3)."""
     ver = data[0]
     if ver == 1:
         nsz, dsz, ssz = struct.unpack_from("<HHH", data, 2)
@@ -344,8 +350,8 @@ def _parse_attribute(fobj, data):
     else:
         raise H5Error(f"attribute version {ver}")
     if shape is None:
-        return name, None
-    return name, _decode_attr_values(fobj, typ, shape, data[p:])
+        return name, typ, None, None
+    return name, typ, shape, _decode_attr_values(fobj, typ, shape, data[p:], raw_enum)
 
 
 class _Node:
@@ -355,13 +361,38 @@ class _Node:
         self.name = name
         self._msgs = fobj.messages(addr)
 
+    def _attr_messages(self):
+        """Raw attribute messages: compact (in the object header) and dense
+        (attribute info message -> fractal heap objects indexed by a v2
+        B-tree of names, libver >= 1.8 with more than 8 attributes)."""
+        out = []
+        f = self.file
+        for m in self._msgs:
+            if m.type == 0x0C:
+                out.append(m.data)
+            elif m.type == 0x15:
+                d = m.data
+                p = 2 + (2 if d[1] & 1 else 0)
+                heap, names = f._off(d, p), f._off(d, p + 8)
+                if heap == UNDEF or names == UNDEF:
+                    continue
+                fh = _FractalHeap(f, heap)
+                for rec in _btree2_records(f, names, 8):
+                    if rec[8] & 0x02:
+                        raise H5Error("shared attribute messages not supported")
+                    out.append(fh.get(rec[:8]))
+        return out
+
+    def attr_items(self):
+        """[(name, H5Type, shape, value)] with enum values as their integers."""
+        return [_parse_attribute(self.file, d, raw_enum=True) for d in self._attr_messages()]
+
     @property
     def attrs(self):
         out = {}
-        for m in self._msgs:
-            if m.type == 0x0C:
-                k, v = _parse_attribute(self.file, m.data)
-                out[k] = v
+        for d in self._attr_messages():
+            k, _, _, v = _parse_attribute(self.file, d)
+            out[k] = v
         return out
 
 
@@ -377,29 +408,19 @@ class Group(_Node):
                 for name_off, obj in _group_btree_entries(f, bt):
                     links[_heap_name(seg, name_off)] = obj
             elif m.type == 0x06:  # link message (compact new-style group)
-                d = m.data
-                flags = d[1]
-                p = 2
-                ltype = 0
-                if flags & 0x08:
-                    ltype = d[p]
-                    p += 1
-                if flags & 0x04:
-                    p += 8
-                if flags & 0x10:
-                    p += 1
-                w = 1 << (flags & 3)
-                nlen = int.from_bytes(d[p:p + w], "little")
-                p += w
-                name = bytes(d[p:p + nlen]).decode()
-                p += nlen
-                if ltype == 0:
-                    links[name] = f._off(d, p)
+                name, obj = _parse_link(f, m.data)
+                if obj is not None:
+                    links[name] = obj
             elif m.type == 0x02:  # link info: dense storage if a fractal heap address is set
                 d = m.data
                 p = 2 + (8 if d[1] & 1 else 0)
-                if f._off(d, p) != UNDEF:
-                    raise H5Error("dense link storage (fractal heap) not supported")
+                heap, names = f._off(d, p), f._off(d, p + 8)
+                if heap != UNDEF:
+                    fh = _FractalHeap(f, heap)
+                    for rec in _btree2_records(f, names, 5):
+                        name, obj = _parse_link(f, fh.get(rec[4:4 + fh.id_len]))
+                        if obj is not None:
+                            links[name] = obj
         return links
 
     def keys(self):
@@ -425,6 +446,157 @@ class Group(_Node):
             full = (node.name.rstrip("/") + "/" + p)
             node = Dataset(node.file, addr, full) if 0x08 in types else Group(node.file, addr, full)
         return node
+
+
+def _parse_link(f, d):
+    """(name, object header address or None for soft / external links) of a
+    link message."""
+    flags = d[1]
+    p = 2
+    ltype = 0
+    if flags & 0x08:
+        ltype = d[p]
+        p += 1
+    if flags & 0x04:
+        p += 8
+    if flags & 0x10:
+        p += 1
+    w = 1 << (flags & 3)
+    nlen = int.from_bytes(d[p:p + w], "little")
+    p += w
+    name = bytes(d[p:p + nlen]).decode()
+    p += nlen
+    return name, (f._off(d, p) if ltype == 0 else None)
+
+
+def _enc_size(x):
+    """Bytes libhdf5 uses to encode values up to ``x`` (H5VM_limit_enc_size)."""
+    return (max(int(x), 1).bit_length() - 1) // 8 + 1
+
+
+class _FractalHeap:
+    """Managed (and tiny) objects of a fractal heap (format spec III.G):
+    doubling-table direct blocks under a root direct or indirect block."""
+
+    def __init__(self, f, addr):
+        h = f.read(addr, 160)
+        if h[:4] != b"FRHP" or h[4] != 0:
+            raise H5Error("bad fractal heap header")
+        self.f = f
+        self.id_len, filt_len = struct.unpack_from("<HH", h, 5)
+        self.flags = h[9]
+        max_man = struct.unpack_from("<I", h, 10)[0]
+        p = 14 + 12 * 8  # next huge id, huge B-tree, free space, fs manager, 8 counters
+        self.width = struct.unpack_from("<H", h, p)[0]
+        self.start, self.max_direct = struct.unpack_from("<QQ", h, p + 2)
+        self.max_heap_bits, _start_rows = struct.unpack_from("<HH", h, p + 18)
+        self.root = f._off(h, p + 22)
+        self.cur_rows = struct.unpack_from("<H", h, p + 30)[0]
+        if filt_len:
+            raise H5Error("filtered fractal heap not supported")
+        self.off_size = (self.max_heap_bits + 7) // 8
+        self.len_size = min(_enc_size(self.max_direct), _enc_size(max_man))
+        self.max_drows = (self.max_direct.bit_length() - 1) - (self.start.bit_length() - 1) + 2
+        self.first_row_bits = (self.start.bit_length() - 1) + (self.width.bit_length() - 1)
+
+    def _row_size(self, r):
+        return self.start if r == 0 else self.start << (r - 1)
+
+    def _dblock_hdr(self):
+        return 5 + 8 + self.off_size + (4 if self.flags & 0x02 else 0)
+
+    def get(self, hid):
+        hid = bytes(hid)
+        b0 = hid[0]
+        if b0 >> 6 != 0:
+            raise H5Error("fractal heap ID version")
+        kind = (b0 >> 4) & 3
+        if kind == 2:  # tiny: the object is in the ID
+            n = (b0 & 0x0F) + 1
+            return hid[1:1 + n]
+        if kind != 0:
+            raise H5Error("huge fractal heap objects not supported")
+        off = int.from_bytes(hid[1:1 + self.off_size], "little")
+        ln = int.from_bytes(hid[1 + self.off_size:1 + self.off_size + self.len_size], "little")
+        if self.cur_rows == 0:  # root is a direct block at heap offset 0
+            return self.f.read(self.root + off, ln)
+        return self._from_iblock(self.root, 0, self.cur_rows, off, ln)
+
+    def _from_iblock(self, addr, boff, nrows, off, ln):
+        f = self.f
+        nd = min(nrows, self.max_drows) * self.width
+        ni = max(nrows - self.max_drows, 0) * self.width
+        hdr = 5 + 8 + self.off_size
+        body = f.read(addr + hdr, 8 * (nd + ni))
+        rel = off - boff
+        row_off = 0
+        for r in range(nrows):
+            size = self._row_size(r)
+            if rel < row_off + self.width * size:
+                c = (rel - row_off) // size
+                k = r * self.width + c
+                child = f._off(body, 8 * k)
+                if child == UNDEF:
+                    raise H5Error("fractal heap object in an unallocated block")
+                cstart = boff + row_off + c * size
+                if r < self.max_drows:
+                    return f.read(child + (off - cstart), ln)
+                crows = (size.bit_length() - 1) - self.first_row_bits + 1
+                return self._from_iblock(child, cstart, crows, off, ln)
+            row_off += self.width * size
+        raise H5Error("fractal heap offset out of range")
+
+
+def _btree2_records(f, addr, want_type):
+    """Every record (raw bytes) of the v2 B-tree at ``addr`` (spec III.A.2)."""
+    h = f.read(addr, 38)
+    if h[:4] != b"BTHD" or h[4] != 0:
+        raise H5Error("bad v2 B-tree header")
+    btype = h[5]
+    if btype != want_type:
+        raise H5Error(f"v2 B-tree type {btype}, expected {want_type}")
+    node_size, rec_size, depth = struct.unpack_from("<IHH", h, 6)
+    root = f._off(h, 16)
+    nroot = struct.unpack_from("<H", h, 24)[0]
+    # per-level capacities and the byte widths of child record counts
+    pre = 10  # signature, version, type, checksum
+    max_nrec = [(node_size - pre) // rec_size]
+    cum = [max_nrec[0]]
+    nsz = [_enc_size(max_nrec[0])]
+    csz = [_enc_size(cum[0])]
+    for u in range(1, depth + 1):
+        ptr = 8 + nsz[u - 1] + (csz[u - 1] if u > 1 else 0)
+        m = (node_size - pre - ptr) // (rec_size + ptr)
+        max_nrec.append(m)
+        cum.append((m + 1) * cum[u - 1] + m)
+        nsz.append(_enc_size(m))
+        csz.append(_enc_size(cum[u]))
+    out = []
+
+    def node(a, nrec, level):
+        if a == UNDEF or nrec == 0 and level == 0:
+            return
+        sig = b"BTLF" if level == 0 else b"BTIN"
+        b = f.read(a, node_size)
+        if b[:4] != sig:
+            raise H5Error("bad v2 B-tree node")
+        recs = [bytes(b[6 + k * rec_size:6 + (k + 1) * rec_size]) for k in range(nrec)]
+        if level == 0:
+            out.extend(recs)
+            return
+        p = 6 + nrec * rec_size
+        w = nsz[level - 1]
+        cw = csz[level - 1] if level > 1 else 0
+        for k in range(nrec + 1):
+            ca = f._off(b, p)
+            cn = int.from_bytes(b[p + 8:p + 8 + w], "little")
+            p += 8 + w + cw
+            node(ca, cn, level - 1)
+            if k < nrec:
+                out.append(recs[k])
+
+    node(root, nroot, depth)
+    return out
 
 
 def _heap_name(seg, off):
@@ -523,6 +695,12 @@ class Dataset(_Node):
                         mask = struct.unpack_from("<I", d, p + 8)[0]
                         return ("single", f._off(d, p + 12), dims, fsize, mask)
                     return ("single", f._off(d, p), dims, None, 0)
+                if itype == 2:  # implicit: unfiltered chunks back to back
+                    return ("indexed", f._off(d, p), dims, ("implicit",))
+                if itype == 3:  # fixed array
+                    return ("indexed", f._off(d, p + 1), dims, ("farray", d[p]))
+                if itype == 4:  # extensible array (one unlimited dimension)
+                    return ("indexed", f._off(d, p + 5), dims, ("earray",) + tuple(d[p:p + 5]))
                 raise H5Error(f"chunk index type {itype} not supported")
         raise H5Error(f"layout version {ver} not supported")
 
@@ -579,10 +757,6 @@ class Dataset(_Node):
         elif lay[0] == "contiguous":
             addr = lay[1]
             raw = b"\0" * ((hi - lo) * es) if addr == UNDEF else self.file.read(addr + lo * es, (hi - lo) * es)
-        elif lay[0] == "single":
-            _, addr, dims, fsize, mask = lay
-            nbytes = fsize if fsize is not None else int(np.prod(dims)) * es
-            raw = self._unfilter(self.file.read(addr, nbytes), mask)[lo * es:hi * es]
         else:
             raw = self._read_chunked(lo, hi, shape)
         out = self._decode(raw, hi - lo)
@@ -590,15 +764,48 @@ class Dataset(_Node):
             return out if shape else out.reshape(())
         return out.reshape(shape)
 
+    def _chunks(self):
+        """(element offsets, stored size, filter mask, address) of every
+        allocated chunk, whatever the chunk index."""
+        lay = self.layout
+        rank = len(self.shape or ())
+        es = self._elem()
+        if lay[0] == "chunked":  # layout v1-v3: v1 B-tree
+            return _chunk_entries(self.file, lay[1], rank + 1)
+        dims = lay[2]
+        cdims = tuple(dims[:rank])
+        full = int(np.prod(cdims)) * es
+        if lay[0] == "single":
+            _, addr, _, fsize, mask = lay
+            return [((0,) * rank, fsize if fsize is not None else full, mask, addr)]
+        kind, addr = lay[3], lay[1]
+        grid = [-(-int(s) // int(c)) for s, c in zip(self.shape, cdims)]
+        nchunks = int(np.prod(grid)) if grid else 1
+        if kind[0] == "implicit":
+            ents = [(addr + k * full, full, 0) for k in range(nchunks)] if addr != UNDEF else []
+        elif kind[0] == "farray":
+            ents = _farray_entries(self.file, addr, nchunks, full)
+        else:
+            if rank != 1:
+                raise H5Error("extensible array chunk index on more than one dimension")
+            ents = _earray_entries(self.file, addr, nchunks, full)
+        out = []
+        for k, (a, size, mask) in enumerate(ents):
+            if a == UNDEF:
+                continue
+            idx = np.unravel_index(k, grid) if rank > 1 else (k,)
+            out.append((tuple(int(i) * c for i, c in zip(idx, cdims)), size, mask, a))
+        return out
+
     def _read_chunked(self, lo, hi, shape):
-        _, bt, dims = self.layout
+        dims = self.layout[2]
         es = self._elem()
         rank = len(shape)
         cdims = dims[:rank]
         if rank == 1:
             out = bytearray((hi - lo) * es)
             c = cdims[0]
-            for off, size, mask, addr in _chunk_entries(self.file, bt, rank + 1):
+            for off, size, mask, addr in self._chunks():
                 s0 = off[0]
                 if s0 + c <= lo or s0 >= hi or addr == UNDEF:
                     continue
@@ -607,7 +814,7 @@ class Dataset(_Node):
                 out[(a - lo) * es:(b - lo) * es] = raw[(a - s0) * es:(b - s0) * es]
             return bytes(out)
         full = np.zeros(shape, dtype=np.dtype(f"V{es}"))
-        for off, size, mask, addr in _chunk_entries(self.file, bt, rank + 1):
+        for off, size, mask, addr in self._chunks():
             if addr == UNDEF:
                 continue
             raw = self._unfilter(self.file.read(addr, size), mask)
@@ -658,6 +865,98 @@ def _chunk_entries(f, addr, ndims):
             out.extend(_chunk_entries(f, child, ndims))
         else:
             out.append((off[:-1], size, mask, child))
+    return out
+
+
+def _chunk_elements(buf, p, n, esize, full):
+    """n chunk index elements at buf[p:]: the address, then (filtered
+    chunks) the stored size and the filter mask."""
+    out = []
+    for k in range(n):
+        q = p + k * esize
+        a = struct.unpack_from("<Q", buf, q)[0]
+        if esize == 8:
+            out.append((a, full, 0))
+        else:
+            sw = esize - 12
+            size = int.from_bytes(buf[q + 8:q + 8 + sw], "little")
+            out.append((a, size, struct.unpack_from("<I", buf, q + 8 + sw)[0]))
+    return out
+
+
+def _farray_entries(f, addr, n, full):
+    """Chunk entries of a fixed array index (spec III.H.1), unpaged."""
+    h = f.read(addr, 28)
+    if h[:4] != b"FAHD":
+        raise H5Error("bad fixed array header")
+    esize, page_bits = h[6], h[7]
+    nmax = struct.unpack_from("<Q", h, 8)[0]
+    dblk = f._off(h, 16)
+    if nmax > (1 << page_bits):
+        raise H5Error("paged fixed array chunk index not supported")
+    if dblk == UNDEF:
+        return []
+    b = f.read(dblk, 14 + esize * nmax)
+    if b[:4] != b"FADB":
+        raise H5Error("bad fixed array data block")
+    return _chunk_elements(b, 14, min(n, nmax), esize, full)
+
+
+def _earray_entries(f, addr, n, full):
+    """Chunk entries of an extensible array index (spec III.H.2): elements
+    in the index block, then data blocks grouped in super blocks (the first
+    super blocks' data blocks addressed from the index block), unpaged."""
+    h = f.read(addr, 70)
+    if h[:4] != b"EAHD":
+        raise H5Error("bad extensible array header")
+    esize, max_bits, iblk_el, dblk_min, sblk_min_ptrs, page_bits = h[6:12]
+    iblk = f._off(h, 12 + 6 * 8)
+    if iblk == UNDEF:
+        return []
+    off_size = (max_bits + 7) // 8
+    nsblks = 1 + max_bits - (dblk_min.bit_length() - 1)
+    ib_nsblks = 2 * (sblk_min_ptrs.bit_length() - 1)
+    ndblk_addrs = 2 * (sblk_min_ptrs - 1)
+    nsblk_addrs = nsblks - ib_nsblks
+    b = f.read(iblk, 14 + iblk_el * esize + 8 * (ndblk_addrs + nsblk_addrs))
+    if b[:4] != b"EAIB":
+        raise H5Error("bad extensible array index block")
+    out = _chunk_elements(b, 14, min(n, iblk_el), esize, full)
+    p = 14 + iblk_el * esize
+    dblk_addrs = [f._off(b, p + 8 * k) for k in range(ndblk_addrs)]
+    sblk_addrs = [f._off(b, p + 8 * (ndblk_addrs + k)) for k in range(nsblk_addrs)]
+    page = 1 << page_bits
+    di = 0
+    for s_ in range(nsblks):
+        if len(out) >= n:
+            break
+        ndb = 1 << (s_ // 2)
+        dn = (1 << ((s_ + 1) // 2)) * dblk_min
+        if dn > page:
+            raise H5Error("paged extensible array data blocks not supported")
+        if s_ < ib_nsblks:
+            addrs = dblk_addrs[di:di + ndb]
+            di += ndb
+        else:
+            sa = sblk_addrs[s_ - ib_nsblks]
+            if sa == UNDEF:
+                addrs = [UNDEF] * ndb
+            else:
+                sb = f.read(sa, 14 + off_size + 8 * ndb)
+                if sb[:4] != b"EASB":
+                    raise H5Error("bad extensible array super block")
+                addrs = [f._off(sb, 14 + off_size + 8 * k) for k in range(ndb)]
+        for a in addrs:
+            m = min(dn, n - len(out))
+            if m <= 0:
+                break
+            if a == UNDEF:
+                out.extend([(UNDEF, 0, 0)] * m)
+                continue
+            db = f.read(a, 14 + off_size + dn * esize)
+            if db[:4] != b"EADB":
+                raise H5Error("bad extensible array data block")
+            out.extend(_chunk_elements(db, 14 + off_size, m, esize, full))
     return out
 
 
@@ -742,8 +1041,39 @@ def _msg(t, data):
     return struct.pack("<HHB3x", t, len(data), 0) + data
 
 
-def _attr_msg(name, value):
-    dt, dims, raw = _encode_values(value)
+def _dt_vlen_utf8():
+    """Variable-length UTF-8 string (h5py's str), base type unsigned 8-bit."""
+    return bytes([0x19, 0x01, 0x01, 0x00]) + struct.pack("<I", 16) + _dt_fixed(np.uint8)
+
+
+class _GlobalHeap:
+    """One global heap collection holding the variable-length string
+    attribute values of a new file (libhdf5's GCOL: >= 4096 bytes, objects
+    8-aligned, free space as object 0)."""
+
+    def __init__(self, strings):
+        self.index = {}
+        body = b""
+        for k, st in enumerate(dict.fromkeys(strings)):
+            b = st.encode("utf-8")
+            self.index[st] = (k + 1, len(b))
+            body += struct.pack("<HH4xQ", k + 1, 0, len(b)) + b + b"\0" * (_pad8(len(b)) - len(b))
+        used = 16 + len(body)
+        self.size = max(4096, _pad8(used + 16))
+        self.image = b"GCOL" + bytes([1, 0, 0, 0]) + struct.pack("<Q", self.size) + body
+        self.image += struct.pack("<HH4xQ", 0, 0, self.size - used) + b"\0" * (self.size - used - 16)
+        self.addr = None
+
+    def ref(self, st):
+        idx, ln = self.index[st]
+        return struct.pack("<IQI", ln, self.addr, idx)
+
+
+def _attr_msg(name, value, gheap=None):
+    if isinstance(value, str) and gheap is not None:
+        dt, dims, raw = _dt_vlen_utf8(), None, gheap.ref(value)
+    else:
+        dt, dims, raw = _encode_values(value)
     nb = name.encode() + b"\0"
     ds = _dataspace(dims)
     body = struct.pack("<BBHHH", 1, 0, len(nb), len(dt), len(ds))
@@ -763,7 +1093,7 @@ def _object_header(msgs):
     return struct.pack("<BBHII", 1, 0, nmsg, 1, len(body)) + b"\0" * 4 + body
 
 
-def _dataset_header(arr, attrs, data_addr, enum=None):
+def _dataset_header(arr, attrs, data_addr, enum=None, gheap=None):
     dt, dims, raw = _encode_values(arr)
     if enum is not None:  # integer data stored with an enum type (cooler's bins/chrom)
         dt = _dt_enum(np.asarray(arr).dtype, enum)
@@ -773,7 +1103,7 @@ def _dataset_header(arr, attrs, data_addr, enum=None):
             _msg(0x05, bytes([2, 2, 0, 0])),
             _msg(0x08, bytes([3, 1]) + struct.pack("<QQ", data_addr if raw else UNDEF, len(raw)))]
     for k, v in (attrs or {}).items():
-        msgs.append(_attr_msg(k, v))
+        msgs.append(_attr_msg(k, v, gheap))
     return _object_header(msgs), raw
 
 
@@ -807,20 +1137,39 @@ def _heap_block(names, spare=256):
     return data, offs, free_at
 
 
+SNOD_FILL = 4  # entries per symbol table node written (capacity 2 * leaf_k = 8)
+
+
+def _str_attrs(node, out):
+    for v in node.get("@attrs", {}).values():
+        if isinstance(v, str):
+            out.append(v)
+    for k, v in node.items():
+        if not k.startswith("@") and isinstance(v, dict):
+            _str_attrs(v, out)
+    return out
+
+
 def write_file(path, tree):
     """Write a new HDF5 file.  ``tree`` is a nested dict: a dict value is a
     group, a numpy array (or scalar / string list) a dataset; the special key
     ``"@attrs"`` holds a node's attributes (``{"@attrs": {...}, "@data": arr}``
     gives a dataset with attributes; ``"@enum": [(name, value)]`` stores
-    integer data with that enum type)."""
+    integer data with that enum type).  String attributes are stored as h5py
+    stores Python ``str``: variable-length UTF-8 in a global heap."""
     W = _W()
     W.alloc(96)  # superblock v0 + root symbol table entry
+    strings = _str_attrs(tree, [])
+    gheap = _GlobalHeap(strings) if strings else None
+    if gheap is not None:
+        gheap.addr = W.alloc(gheap.size)
+        W.put(gheap.addr, gheap.image)
 
     def build_group(node):
         attrs = node.get("@attrs", {})
         names = sorted(k for k in node if not k.startswith("@"))
-        if len(names) > 8 * 32:
-            raise H5Error("more than 256 links in one group")
+        if len(names) > SNOD_FILL * 32:
+            raise H5Error(f"more than {SNOD_FILL * 32} links in one group")
         children = {}
         for nm in names:
             v = node[nm]
@@ -830,10 +1179,10 @@ def write_file(path, tree):
                 data, a = (v["@data"], v.get("@attrs", {})) if isinstance(v, dict) else (v, {})
                 en = v.get("@enum") if isinstance(v, dict) else None
                 data = np.asarray(data) if not isinstance(data, str) else data
-                hdr, raw = _dataset_header(data, a, 0, en)
+                hdr, raw = _dataset_header(data, a, 0, en, gheap)
                 ha = W.alloc(len(hdr))
                 da = W.alloc(len(raw)) if raw else UNDEF
-                hdr, raw = _dataset_header(data, a, da, en)
+                hdr, raw = _dataset_header(data, a, da, en, gheap)
                 W.put(ha, hdr)
                 if raw:
                     W.put(da, raw)
@@ -843,8 +1192,10 @@ def write_file(path, tree):
         heap_data = W.alloc(len(heap))
         W.put(heap_hdr, b"HEAP" + bytes([0, 0, 0, 0]) + struct.pack("<QQQ", len(heap), free_at, heap_data))
         W.put(heap_data, heap)
-        # symbol table nodes of up to 8 entries, one level of B-tree (<= 32 of them)
-        chunks = [names[i:i + 8] for i in range(0, len(names), 8)] or [[]]
+        # symbol table nodes filled to half their capacity of 8 entries (as
+        # libhdf5's splits leave them; room for in-place appends), one level of
+        # B-tree (<= 32 of them)
+        chunks = [names[i:i + SNOD_FILL] for i in range(0, len(names), SNOD_FILL)] or [[]]
         snods = []
         for ch in chunks:
             a = W.alloc(8 + 40 * 8)
@@ -861,7 +1212,7 @@ def write_file(path, tree):
             body += struct.pack("<QQ", a, offs[ch[-1]] if ch else 0)
         body += b"\0" * (24 + 33 * 8 + 32 * 8 - len(body))
         W.put(bt, body)
-        msgs = [_msg(0x11, struct.pack("<QQ", bt, heap_hdr))] + [_attr_msg(k, v) for k, v in attrs.items()]
+        msgs = [_msg(0x11, struct.pack("<QQ", bt, heap_hdr))] + [_attr_msg(k, v, gheap) for k, v in attrs.items()]
         hdr = _object_header(msgs)
         ga = W.alloc(len(hdr))
         W.put(ga, hdr)
@@ -884,9 +1235,17 @@ def write_file(path, tree):
 def append_dataset(path, group, name, data, attrs=None):
     """Add (or replace) dataset ``group/name`` in an existing file, in place:
     the new object header and data go to the end of the file; the group's
-    symbol table gets the link (name added to its local heap, which moves to
-    the end of the file when its free space is too small).  A replaced
-    dataset's old storage is left unreferenced, as libhdf5 does."""
+    symbol table gets the link (name added to its local heap, whose data
+    segment moves to the end of the file when its free space is too small;
+    a full symbol table node is split as libhdf5 splits it).  A replaced
+    dataset's old storage is left unreferenced, as libhdf5 does.
+
+    Write order: everything new is written past the old end of file, then the
+    end-of-file address, then the existing structures are re-pointed (local
+    heap, symbol table node, B-tree node), so an interruption between two
+    writes leaves a readable file (new objects unreferenced, or the dataset
+    linked).  A torn write inside one block is not protected against: like
+    libhdf5 without SWMR, this is not crash-safe in general."""
     F = File(path, "r+")
     try:
         if F.sb_version > 1:
@@ -896,22 +1255,6 @@ def append_dataset(path, group, name, data, attrs=None):
         if not st:
             raise H5Error("in-place append needs an old-style (symbol table) group")
         bt, heap = F._off(st[0].data, 0), F._off(st[0].data, 8)
-        end = _pad8(F.eof)
-
-        def put(addr, b):
-            F.f.seek(F.base + addr)
-            F.f.write(b)
-
-        arr = np.asarray(data) if not isinstance(data, str) else data
-        hdr, raw = _dataset_header(arr, attrs, 0)
-        ha = end
-        da = _pad8(ha + len(hdr))
-        hdr, raw = _dataset_header(arr, attrs, da if raw else UNDEF)
-        put(ha, hdr)
-        if raw:
-            put(da, raw)
-        end = _pad8(da + len(raw)) if raw else _pad8(ha + len(hdr))
-
         head = F.read(bt, 24)
         if head[:4] != b"TREE" or head[5] != 0:
             raise H5Error("in-place append supports one-level group B-trees")
@@ -921,15 +1264,41 @@ def append_dataset(path, group, name, data, attrs=None):
         body = bytearray(F.read(bt + 24, (2 * n + 1) * 8))
         size, free, hdata = F.local_heap(heap)
         seg = bytearray(F.read(hdata, size))
-        # existing link: repoint it
+        end = _pad8(F.eof)
+        tail = []          # (addr, bytes) past the old end of file
+        relink = []        # (addr, bytes) re-pointing existing structures, in order
+
+        arr = np.asarray(data) if not isinstance(data, str) else data
+        hdr, raw = _dataset_header(arr, attrs, 0)
+        ha = end
+        da = _pad8(ha + len(hdr))
+        hdr, raw = _dataset_header(arr, attrs, da if raw else UNDEF)
+        tail.append((ha, hdr))
+        if raw:
+            tail.append((da, raw))
+        end = _pad8(da + len(raw)) if raw else _pad8(ha + len(hdr))
+
+        def commit():
+            def put(addr, b):
+                F.f.seek(F.base + addr)
+                F.f.write(b)
+            for a, b in tail:
+                put(a, b)
+            F.f.flush()
+            put(F.eof_pos, struct.pack("<Q", end))
+            F.f.flush()
+            for a, b in relink:
+                put(a, b)
+
+        # existing link: re-point it
         for i in range(n):
             sn = F._off(body, 8 + 16 * i)
             ns = struct.unpack_from("<H", F.read(sn, 8), 6)[0]
             ents = F.read(sn + 8, 40 * ns)
             for k in range(ns):
                 if _heap_name(seg, F._off(ents, 40 * k)) == name:
-                    put(sn + 8 + 40 * k + 8, struct.pack("<Q", ha))
-                    put(F.eof_pos, struct.pack("<Q", end))
+                    relink.append((sn + 8 + 40 * k + 8, struct.pack("<Q", ha)))
+                    commit()
                     return
         # new name -> local heap
         nb = name.encode() + b"\0"
@@ -952,7 +1321,8 @@ def append_dataset(path, group, name, data, attrs=None):
                     struct.pack_into("<Q", seg, prev, link)
                 break
             prev, cur = cur, nxt
-        if off is None:  # grow: move the data segment to the end of the file
+        moved = off is None
+        if moved:  # grow: the data segment moves to the end of the file
             off = size
             seg += nb + b"\0" * (need - len(nb))
             spare = 256
@@ -963,8 +1333,8 @@ def append_dataset(path, group, name, data, attrs=None):
             hdata = end
             end = _pad8(hdata + size)
         seg[off:off + need] = nb + b"\0" * (need - len(nb))
-        put(hdata, bytes(seg))
-        put(heap + 8, struct.pack("<QQQ", size, free, hdata))
+        (tail if moved else relink).append((hdata, bytes(seg)))
+        relink.append((heap + 8, struct.pack("<QQQ", size, free, hdata)))
         # symbol table node: the child whose key range holds the name
         names_at = lambda o: _heap_name(seg, o)
         ci = n - 1
@@ -975,14 +1345,37 @@ def append_dataset(path, group, name, data, attrs=None):
         sn = F._off(body, 8 + 16 * ci)
         snh = F.read(sn, 8)
         ns = struct.unpack_from("<H", snh, 6)[0]
-        if ns >= 2 * F.leaf_k:
-            raise H5Error("symbol table node full (in-place append does not split nodes)")
         ents = [F.read(sn + 8 + 40 * k, 40) for k in range(ns)]
         pos = sum(1 for e in ents if names_at(F._off(e, 0)) < name)
         ents.insert(pos, struct.pack("<QQII16x", off, ha, 0, 0))
-        put(sn, snh[:6] + struct.pack("<H", ns + 1) + b"".join(ents))
-        if name > names_at(F._off(body, 16 * (ci + 1))):
-            put(bt + 24 + 16 * (ci + 1), struct.pack("<Q", off))
-        put(F.eof_pos, struct.pack("<Q", end))
+        cap = 2 * F.leaf_k
+        if len(ents) <= cap:
+            relink.append((sn, snh[:6] + struct.pack("<H", len(ents)) + b"".join(ents)))
+            if name > names_at(F._off(body, 16 * (ci + 1))):
+                relink.append((bt + 24 + 16 * (ci + 1), struct.pack("<Q", off)))
+        else:  # split: the upper half goes to a new node past the end of file
+            if n + 1 > 2 * F.int_k:
+                raise H5Error("group B-tree node full (in-place append does not split B-tree nodes)")
+            half = (len(ents) + 1) // 2
+            left, right = ents[:half], ents[half:]
+            na = end
+            end = _pad8(na + 8 + 40 * cap)
+            node = b"SNOD" + bytes([1, 0]) + struct.pack("<H", len(right)) + b"".join(right)
+            tail.append((na, node + b"\0" * (8 + 40 * cap - len(node))))
+            # B-tree: child ci keeps keys (k_ci, last of left); the new child
+            # gets (last of left, k_ci+1) -- or the new name if it is the last
+            lk = F._off(left[-1], 0)
+            keys = [F._off(body, 16 * i) for i in range(n + 1)]
+            kids = [F._off(body, 8 + 16 * i) for i in range(n)]
+            if name > names_at(keys[ci + 1]):
+                keys[ci + 1] = off
+            keys.insert(ci + 1, lk)
+            kids.insert(ci + 1, na)
+            nbody = struct.pack("<Q", keys[0]) + b"".join(struct.pack("<QQ", kids[i], keys[i + 1])
+                                                          for i in range(n + 1))
+            relink.append((bt, head[:6] + struct.pack("<H", n + 1) + head[8:]))
+            relink.append((bt + 24, nbody))
+            relink.append((sn, snh[:6] + struct.pack("<H", len(left)) + b"".join(left) + b"\0" * (40 * (cap - len(left)))))
+        commit()
     finally:
         F.close()

@@ -32,6 +32,7 @@ def _worker(rank, world, port, case, cis_only, outdir, impl="python"):
     _lib.load()
     _lib.call("hh_set_device", 0)
     _lib.call("hh_tune", b"conc_min_bytes", 0)  # three sweep streams even on this small shard
+    _lib.call("hh_tune", b"sweep_single", 0)    # (the single launch is checked first: off)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     tdist.init_process_group("gloo", rank=rank, world_size=world)
     try:

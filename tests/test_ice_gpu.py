@@ -383,6 +383,9 @@ def test_band_concurrent_bitwise(ice, conc, split):
     b1, b2, c, off = _case(17, sizes=(1500, 900), A=60.0)
     n = int(off[-1])
     _lib.call("hh_tune", b"band_concurrent", 0)
+    # the single-launch sweep (auto below 1 GB) is checked before the
+    # concurrent one: switch it off so side / side2 really run
+    _lib.call("hh_tune", b"sweep_single", 0)
     try:
         w0, s0 = ice.balance(b1, b2, c, n, off, max_iters=300)  # one stream
         _lib.call("hh_tune", b"band_concurrent", conc)
@@ -393,6 +396,7 @@ def test_band_concurrent_bitwise(ice, conc, split):
         _lib.call("hh_tune", b"band_concurrent", 1)
         _lib.call("hh_tune", b"split_tiles", 1)
         _lib.call("hh_tune", b"conc_min_bytes", 8 << 30)
+        _lib.call("hh_tune", b"sweep_single", -1)
     np.testing.assert_array_equal(w1, w0)
     assert s1["iters"] == s0["iters"]
 
