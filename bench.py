@@ -19,7 +19,10 @@ Select_PC_new for all 22 autosomes; chromosomes dealt to ranks by LPT on N^3
 (no collective); value = chromosomes/s of the whole job; roofline on k_syrk
 (MFMA, fp64).
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c4|c2|c5]
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c4|c4h|c3|c2|c1|c5|gw|dropin|e2e|pairs|loops]
+
+--config c4h: the same metric on the haploid traditional 10 kb matrix (303 641 bins,
+5e9 pixels), the one HiCHap's `cooler balance` runs on (matrixBuilding.py:1537).
 """
 from __future__ import annotations
 
@@ -62,6 +65,13 @@ def config(name, nnz=None):
     if name == "c4":
         sizes = synth.genome_bins(10000, diploid=True)
         target, tf, label = nnz or 5e9, 0.2, "hg19-10kb-diploid-wholegenome"
+    elif name == "c4h":
+        # the haploid traditional T matrix HiCHap actually balances genome-wide
+        # at 10 kb (matrixBuilding.py:1536-1538, :1760-1762): 3.04e5 bins
+        # hg19 haploid at 10 kb has only 2.36e9 cis pairs in all, so 5e9
+        # pixels need >= 53 % trans (0.6: A = 3.2e4, cis 85 % dense)
+        sizes = synth.genome_bins(10000)
+        target, tf, label = nnz or 5e9, 0.6, "hg19-10kb-haploid-wholegenome"
     elif name == "c3":
         sizes = synth.genome_bins(40000)
         # hg19 at 40 kb has only 1.42e8 cis pixels (sum n(n+1)/2, 2 % gaps), so
@@ -101,6 +111,31 @@ def pmc_traffic(kernels=SWEEP_KERNELS):
     base = min(v.get("dispatches", 1) or 1 for v in hits)
     tot = sum(v["traffic_bytes"] * (v.get("dispatches", base) or base) / base for v in hits)
     return tot, meta, os.path.relpath(files[-1], ROOT)
+
+
+def host_info():
+    """The CPU every cpu_baseline ran on: model name and how many logical CPUs
+    the machine has / this process may use (a GPU box shares its host)."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = os.cpu_count()
+    return {"host_cpu_model": model, "host_nproc": os.cpu_count(), "host_cpus_usable": usable,
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+
+
+def with_host(d):
+    d.update(host_info())
+    return d
 
 
 def cpu_baseline(sizes, kw, rc, nnz_total, label, budget_s=12.0):
@@ -318,7 +353,7 @@ def run_c5(args, world, rank, local):
                              other_kernel=other),
         }
         if world == 1 and not args.no_cpu:
-            out["cpu_baseline"] = c5_cpu_baseline()
+            out["cpu_baseline"] = with_host(c5_cpu_baseline())
         print(json.dumps(out), flush=True)
 
 
@@ -454,7 +489,7 @@ def run_pairs(args, world, rank, local):
                          "kernel_timing": "HIP events (hh_ktime) over one extra step after the timed steps"},
         }
         if world == 1 and not args.no_cpu:
-            out["cpu_baseline"] = pairs_cpu_baseline(genome)
+            out["cpu_baseline"] = with_host(pairs_cpu_baseline(genome))
         print(json.dumps(out), flush=True)
 
 
@@ -575,7 +610,7 @@ def run_loops(args, world, rank, local):
                          "note": "gather-bound (L2/MALL): ~150 prefix lookups per pixel per width"},
         }
         if world == 1 and not args.no_cpu:
-            out["cpu_baseline"] = loops_cpu_baseline()
+            out["cpu_baseline"] = with_host(loops_cpu_baseline())
         print(json.dumps(out), flush=True)
 
 
@@ -967,6 +1002,10 @@ def main():
                        **({"config_note": "trans fraction 0.85, not SURVEY 8(d)'s ~0.2: hg19 at 40 kb has only "
                                           "1.42e8 cis pixels, so BASELINE C3's 8e8 nnz needs ~85 % trans"}
                           if args.config == "c3" else {}),
+                       **({"config_note": "haploid traditional T matrix (303 641 bins): the one HiCHap balances "
+                                          "genome-wide at 10 kb, matrixBuilding.py:1536-1538; trans fraction 0.6: "
+                                          "it has only 2.36e9 cis pairs, so 5e9 pixels need >= 53 % trans"}
+                          if args.config == "c4h" else {}),
                        "trans_fraction_target": tf, "resolution_bp": 40000 if args.config in ("c1", "c3") else 10000,
                        "parallelism": f"rows sharded x{world} (measured-cost partition), {'RCCL' if backend == 'nccl' else backend} all-gather of marginals, loop in {'C++ (hh_ice_run_sharded)' if dist_impl == 'capi' else 'Python'}" if world > 1
                        else "single GPU", "generate_s": round(gen_s, 2),
@@ -1021,7 +1060,7 @@ def main():
         if tad is not None:
             out["tad_scan"] = tad
         if world == 1 and not args.no_cpu:
-            out["cpu_baseline"] = cpu_baseline(sizes, kw, rc, nnz_total, label)
+            out["cpu_baseline"] = with_host(cpu_baseline(sizes, kw, rc, nnz_total, label))
             # vs_baseline stays null (BASELINE.md publishes no number for this
             # metric); the ratio to the measured CPU baseline is reported here
             out["vs_cpu_baseline"] = its / out["cpu_baseline"]["value"]

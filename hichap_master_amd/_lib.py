@@ -96,6 +96,7 @@ SIGNATURES = {
     "hh_comm_free": (C.c_int, [P]),
     "hh_comm_allgather": (C.c_int, [P, I64, P, P, P]),
     "hh_ice_balance_sharded": (C.c_int, [P, C.POINTER(IceOpts), I32, I32, P, P, P, P, P, P, P, P, PF64, P]),
+    "hh_ice_balance_cis_local": (C.c_int, [P, C.POINTER(IceOpts), I32, I64, P, P, P, P, P, P, P, PF64, P]),
     "hh_ice_filters_sharded": (C.c_int, [P, I32, P, P, P, P]),
     "hh_ice_run_sharded": (C.c_int, [P, I32, P, P, P, I32, P]),
     "hh_dense_rowstats": (C.c_int, [P, I32, I64, P, P, P, P, I32, P]),

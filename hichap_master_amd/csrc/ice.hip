@@ -22,6 +22,7 @@
 // how rows are sharded across GPUs.
 #include <algorithm>
 #include <chrono>
+#include <functional>
 #include <cmath>
 #include <limits>
 
@@ -1618,6 +1619,47 @@ static void check_opts(const hh_ice_opts* o) {
 
 }  // namespace hh
 
+// MIN-count and MAD-max filters (cooler balance_cooler): per-chromosome median
+// normalisation of the raw marginal, then a log-MAD cutoff over the whole
+// genome.  O(n) host work with numpy's median semantics; run once per balance.
+// `gather` (may be null) turns this matrix's normalised marginals into the
+// genome's (the cis-only-by-chromosome sharding: every rank holds whole
+// chromosomes, so the per-chromosome medians are local and only the
+// genome-wide median of the logs needs the other ranks' values).
+static void filter_count_mad(hh_ice* S, hipStream_t s,
+                             const std::function<std::vector<double>(const std::vector<double>&)>& gather) {
+    if (S->o.min_count != 0.0)
+        hipLaunchKernelGGL(k_filter_lt, dim3(nblocks(S->n, kThreads)), dim3(kThreads), 0, s, S->marg.p,
+                           (long long)S->n, S->o.min_count, S->bias.p);
+    HIP_CHECK(hipGetLastError());
+    if (S->o.mad_max <= 0) return;
+    std::vector<double> marg(S->n), bias(S->n);
+    S->marg.download(marg.data(), S->n, s);
+    S->bias.download(bias.data(), S->n, s);
+    HIP_CHECK(hipStreamSynchronize(s));
+    const auto& off = S->m->chrom_offsets;
+    std::vector<double> pos;
+    for (int c = 0; c < S->m->n_chroms; ++c) {
+        pos.clear();
+        for (int64_t i = off[c]; i < off[c + 1]; ++i)
+            if (marg[i] > 0) pos.push_back(marg[i]);
+        const double med = np_median(pos);
+        for (int64_t i = off[c]; i < off[c + 1]; ++i) marg[i] = marg[i] / med;
+    }
+    const std::vector<double> all = gather ? gather(marg) : marg;
+    std::vector<double> logm;
+    for (double x : all)
+        if (x > 0) logm.push_back(std::log(x));
+    const double med = np_median(logm);
+    std::vector<double> dev(logm.size());
+    for (size_t k = 0; k < logm.size(); ++k) dev[k] = std::fabs(logm[k] - med);
+    const double cutoff = std::exp(med - S->o.mad_max * np_median(dev));
+    for (int64_t i = 0; i < S->n; ++i)
+        if (marg[i] < cutoff) bias[i] = 0.0;
+    S->bias.upload(bias.data(), S->n, s);
+    HIP_CHECK(hipStreamSynchronize(s));
+}
+
 extern "C" {
 
 int hh_tune(const char* key, int64_t value) {
@@ -1870,39 +1912,7 @@ int hh_ice_filter_nnz(hh_ice* S, void* stream) {
 int hh_ice_filter_count_mad(hh_ice* S, void* stream) {
     return guard([&] {
         HH_REQUIRE(S, "null");
-        hipStream_t s = as_stream(stream);
-        if (S->o.min_count != 0.0)
-            hipLaunchKernelGGL(k_filter_lt, dim3(nblocks(S->n, kThreads)), dim3(kThreads), 0, s, S->marg.p,
-                               (long long)S->n, S->o.min_count, S->bias.p);
-        HIP_CHECK(hipGetLastError());
-        if (S->o.mad_max <= 0) return;
-        // MAD-max filter (cooler balance_cooler): per-chromosome median
-        // normalisation of the raw marginal, then a log-MAD cutoff.  O(n) host
-        // work with numpy's median semantics; run once per balance.
-        std::vector<double> marg(S->n), bias(S->n);
-        S->marg.download(marg.data(), S->n, s);
-        S->bias.download(bias.data(), S->n, s);
-        HIP_CHECK(hipStreamSynchronize(s));
-        const auto& off = S->m->chrom_offsets;
-        std::vector<double> pos;
-        for (int c = 0; c < S->m->n_chroms; ++c) {
-            pos.clear();
-            for (int64_t i = off[c]; i < off[c + 1]; ++i)
-                if (marg[i] > 0) pos.push_back(marg[i]);
-            const double med = np_median(pos);
-            for (int64_t i = off[c]; i < off[c + 1]; ++i) marg[i] = marg[i] / med;
-        }
-        std::vector<double> logm;
-        for (double x : marg)
-            if (x > 0) logm.push_back(std::log(x));
-        const double med = np_median(logm);
-        std::vector<double> dev(logm.size());
-        for (size_t k = 0; k < logm.size(); ++k) dev[k] = std::fabs(logm[k] - med);
-        const double cutoff = std::exp(med - S->o.mad_max * np_median(dev));
-        for (int64_t i = 0; i < S->n; ++i)
-            if (marg[i] < cutoff) bias[i] = 0.0;
-        S->bias.upload(bias.data(), S->n, s);
-        HIP_CHECK(hipStreamSynchronize(s));
+        filter_count_mad(S, as_stream(stream), nullptr);
     });
 }
 
@@ -2053,6 +2063,66 @@ int hh_ice_balance(hh_matrix* m, const hh_ice_opts* o, double* weights, double* 
     const auto tx0 = std::chrono::steady_clock::now();
     hh_ice_free(S);
     if (g_build_debug) fprintf(stderr, "[ice] free %.3f ms (balance total %.3f ms)\n", ms_since(tx0), ms_since(tc0));
+    return rc;
+}
+
+// --cis-only ICE over world processes without a collective in the
+// iterations: each rank holds whole chromosomes as a
+// compact matrix (its chromosomes' bins renumbered consecutively), whose ICE
+// groups (one per chromosome) converge independently; the one exchange is an
+// all-gather of the per-chromosome-normalised raw marginals for the
+// genome-wide MAD cutoff (padded with zeros to max_local_bins, which the
+// cutoff ignores as cooler ignores zero marginals).
+int hh_ice_balance_cis_local(hh_matrix* m, const hh_ice_opts* o, int32_t world, int64_t max_local_bins,
+                             hh_allgather_fn allgather, void* user, double* weights, double* scale, double* var,
+                             int32_t* iters, int32_t* converged, double* sweep_seconds, void* stream) {
+    hh_ice* S = nullptr;
+    int rc = guard([&] {
+        HH_REQUIRE(m && o && world >= 1 && (world == 1 || allgather), "bad arguments");
+        HH_REQUIRE(m->cis_only, "hh_ice_balance_cis_local balances cis-only matrices");
+        HH_REQUIRE(max_local_bins >= m->n_bins, "max_local_bins is below this rank's bins");
+    });
+    if (rc) return rc;
+    rc = hh_ice_create(m, o, &S);
+    if (rc) return rc;
+    rc = guard([&] {
+        HH_REQUIRE(S->full(), "the local matrix must hold every one of its rows");
+        hipStream_t s = as_stream(stream);
+        auto ok = [](int r) { if (r) throw Error(r, hh_last_error()); };
+        ok(hh_ice_marg_local(S, 0, nullptr, stream));
+        ok(hh_ice_filter_nnz(S, stream));
+        ok(hh_ice_marg_local(S, 1, nullptr, stream));
+        auto gather = [&](const std::vector<double>& loc) {
+            if (world == 1) return loc;
+            DBuf<double> send, recv;
+            send.alloc(std::max<int64_t>(max_local_bins, 1));
+            send.zero(s);
+            if (!loc.empty()) send.upload(loc.data(), (int64_t)loc.size(), s);
+            recv.alloc((size_t)world * std::max<int64_t>(max_local_bins, 1));
+            const int r = allgather(send.p, std::max<int64_t>(max_local_bins, 1), recv.p, user, stream);
+            if (r) HH_THROW(r < 0 ? r : HH_ERR_HIP, std::string("all-gather callback failed: ") + hh_last_error());
+            std::vector<double> all((size_t)world * std::max<int64_t>(max_local_bins, 1));
+            recv.download(all.data(), (int64_t)all.size(), s);
+            HIP_CHECK(hipStreamSynchronize(s));
+            return all;
+        };
+        filter_count_mad(S, s, gather);
+        const auto t0 = std::chrono::steady_clock::now();
+        while (S->iters_done < S->o.max_iters) {
+            const int k = std::min(S->o.check_every, S->o.max_iters - S->iters_done);
+            for (int j = 0; j < k; ++j) {
+                marg_weighted(S, S->marg.p, s, false, 0);
+                update(S, s);
+            }
+            int32_t na = 0;
+            ok(hh_ice_active_groups(S, &na, stream));
+            if (na == 0) break;
+        }
+        if (sweep_seconds)
+            *sweep_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        ok(hh_ice_finalize(S, weights, scale, var, iters, converged, stream));
+    });
+    hh_ice_free(S);
     return rc;
 }
 

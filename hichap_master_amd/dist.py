@@ -307,3 +307,111 @@ def iterate_capi(st, ex: CapiExchange, n: int, stream=None):
     """``n`` ICE iterations enqueued from C++ (one call, no host polling)."""
     from ._lib import call, ptr
     call("hh_ice_run_sharded", st._h, ex.world, ptr(ex.rank_rows), ex.fn, ex.user, int(n), stream)
+
+
+# ------------------------------------------- --cis-only, chromosomes by LPT
+# SURVEY.md §8(e) row 1: `cooler balance --cis-only` (matrixBuilding.py:713,
+# :1542, :1766) needs no collective in its iterations: every chromosome is
+# its own ICE group, so whole chromosomes are dealt to ranks (LPT on their
+# cis pixels) and each rank balances a compact matrix of its own
+# chromosomes.  The one exchange is cooler's genome-wide MAD cutoff over the
+# per-chromosome-normalised raw marginals (hh_ice_balance_cis_local); the
+# weights are gathered once at the end.
+
+def cis_plan(bin1, bin2, chrom_offsets, world: int):
+    """``(owner[chrom], cis pixels per chrom)``: LPT on cis pixels."""
+    off = np.asarray(chrom_offsets, dtype=np.int64)
+    nc = off.size - 1
+    c1 = np.searchsorted(off, np.asarray(bin1), side="right") - 1
+    c2 = np.searchsorted(off, np.asarray(bin2), side="right") - 1
+    cost = np.bincount(c1[c1 == c2], minlength=nc).astype(np.float64)
+    return lpt_assign(cost, world), cost
+
+
+def local_genome(bin1, bin2, count, chrom_offsets, chroms):
+    """The cis pixels of ``chroms`` (ascending chromosome indices) renumbered
+    into a compact genome: ``(b1, b2, count, local_offsets)``."""
+    off = np.asarray(chrom_offsets, dtype=np.int64)
+    chroms = np.asarray(sorted(chroms), dtype=np.int64)
+    sizes = np.diff(off)[chroms]
+    loff = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    shift = np.zeros(off.size - 1, dtype=np.int64)
+    shift[chroms] = loff[:-1] - off[chroms]
+    keep = np.zeros(off.size - 1, dtype=bool)
+    keep[chroms] = True
+    b1 = np.asarray(bin1, dtype=np.int64)
+    b2 = np.asarray(bin2, dtype=np.int64)
+    c1 = np.searchsorted(off, b1, side="right") - 1
+    c2 = np.searchsorted(off, b2, side="right") - 1
+    sel = (c1 == c2) & keep[np.clip(c1, 0, off.size - 2)]
+    sh = shift[c1[sel]]
+    return b1[sel] + sh, b2[sel] + sh, np.asarray(count)[sel], loff
+
+
+def balance_cis_capi(m_local, opts, ex: CapiExchange, max_local_bins: int, stream=None):
+    """hh_ice_balance_cis_local on this rank's compact matrix: ``(weights of
+    the local bins, per-local-chromosome scale, var, iters, converged,
+    sweep seconds)``."""
+    import ctypes as C
+    from ._lib import call, ptr
+    inf = m_local.info()
+    G = inf["n_chroms"]
+    w = np.empty(inf["n_bins"], np.float64)
+    scale, var = np.empty(G), np.empty(G)
+    iters, conv = np.empty(G, np.int32), np.empty(G, np.int32)
+    secs = C.c_double(0)
+    call("hh_ice_balance_cis_local", m_local.handle, C.byref(opts.c_opts()), ex.world, int(max_local_bins),
+         ex.fn, ex.user, ptr(w), ptr(scale), ptr(var), ptr(iters), ptr(conv), C.byref(secs), stream)
+    return w, scale, var, iters, conv, secs.value
+
+
+def balance_cis_sharded(bin1, bin2, count, n_bins, chrom_offsets, rank: int, world: int, opts, ex: CapiExchange,
+                        group=None, stream=None):
+    """`cooler balance --cis-only` over ``world`` ranks, chromosomes by LPT,
+    no collective in the iterations.  Returns ``(weights, stats)`` for the
+    whole genome on every rank (as ``ice.balance`` with ``cis_only=True``)."""
+    from .ice import ContactMatrix, _stats
+    off = np.asarray(chrom_offsets, dtype=np.int64)
+    owner, _ = cis_plan(bin1, bin2, off, world)
+    sizes = np.diff(off)
+    max_local = max(int(sizes[owner == r].sum()) for r in range(world))
+    mine = np.flatnonzero(owner == rank)
+    loc = None
+    if mine.size:
+        b1, b2, c, loff = local_genome(bin1, bin2, count, off, mine)
+        m = ContactMatrix.from_pixels(b1, b2, c, int(loff[-1]), loff, opts.ignore_diags, True, stream=stream)
+        try:
+            loc = balance_cis_capi(m, opts, ex, max_local, stream)
+        finally:
+            m.close()
+    elif world > 1:  # a rank without chromosomes still joins the MAD exchange
+        b1, b2, c, loff = np.zeros(0, np.int64), np.zeros(0, np.int64), np.zeros(0), np.array([0, 1])
+        m = ContactMatrix.from_pixels(b1, b2, c, 1, loff, opts.ignore_diags, True, stream=stream)
+        try:
+            balance_cis_capi(m, opts, ex, max_local, stream)
+        finally:
+            m.close()
+    parts = [(mine, loc)]
+    if world > 1:
+        import torch.distributed as tdist
+        parts = [None] * world
+        tdist.all_gather_object(parts, (mine, loc), group=group)
+    nc = off.size - 1
+    w = np.full(int(n_bins), np.nan)
+    scale, var = np.full(nc, np.nan), np.full(nc, np.nan)
+    iters, conv = np.zeros(nc, np.int32), np.zeros(nc, np.int32)
+    secs = 0.0
+    for chroms, res in parts:
+        if res is None:
+            continue
+        wl, sc, vr, it, cv, t = res
+        p = 0
+        for k, ch in enumerate(chroms):
+            n = int(sizes[ch])
+            w[off[ch]:off[ch] + n] = wl[p:p + n]
+            p += n
+            scale[ch], var[ch], iters[ch], conv[ch] = sc[k], vr[k], it[k], cv[k]
+        secs = max(secs, t)
+    st = _stats(opts, scale, var, iters, conv, True)
+    st["sweep_seconds"] = secs
+    return w, st

@@ -278,6 +278,17 @@ int hh_comm_allgather(const double* send, int64_t count, double* recv, void* com
 int hh_ice_balance_sharded(hh_matrix* m, const hh_ice_opts* o, int32_t world, int32_t rank, const int64_t* rank_rows,
                            hh_allgather_fn allgather, void* user, double* weights, double* scale, double* var,
                            int32_t* iters, int32_t* converged, double* sweep_seconds, void* stream);
+/* `cooler balance --cis-only` (matrixBuilding.py:713, :1542, :1766) over world
+ * processes with no collective in the iterations:
+ * every rank holds whole chromosomes (dealt by LPT on their pixels) as a
+ * compact cis-only matrix `m` -- its chromosomes' bins renumbered
+ * consecutively -- whose per-chromosome ICE groups converge independently.
+ * The one exchange is `allgather` of max_local_bins doubles per rank (the
+ * per-chromosome-normalised raw marginals, zero padded) for cooler's
+ * genome-wide MAD cutoff.  Outputs cover this rank's bins and chromosomes. */
+int hh_ice_balance_cis_local(hh_matrix* m, const hh_ice_opts* o, int32_t world, int64_t max_local_bins,
+                             hh_allgather_fn allgather, void* user, double* weights, double* scale, double* var,
+                             int32_t* iters, int32_t* converged, double* sweep_seconds, void* stream);
 /* Pieces of it on an hh_ice (bench / fixed iteration counts): the two
  * filters, and n iterations without convergence polling. */
 int hh_ice_filters_sharded(hh_ice* s, int32_t world, const int64_t* rank_rows, hh_allgather_fn allgather, void* user,

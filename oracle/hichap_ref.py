@@ -130,3 +130,81 @@ def genome_wide_correction(bins_pos, hap_bins_pos, T_M, H_M):
     Y = symmetrize_sum(H_M / alpha[:, None])
     C = correct_vc(Y)
     return (H_M.mean() / C.mean()) * C
+
+
+def genome_wide_correction_sparse(bins_pos, hap_bins_pos, T_pixels, H_cells):
+    """GenomeWideMatrixCorrection (matrixBuilding.py:857-901) restated on
+    pixel tables, for whole-genome diploid sizes the dense form cannot hold
+    (10 kb: 607 282^2 x 8 B = 2.9 TB).  ``T_pixels`` = cooler's upper-triangle
+    table of T_M, ``H_cells`` = the nonzero ordered cells of the asymmetric
+    H_M.  Same arithmetic as :func:`genome_wide_correction`: block row sums of
+    T (Gap_definedLowRes coverage, :742-753) and of the M_M / P_P blocks of H
+    (:878-886, exact integers), Alpha in Sort_Chromosomes order and duplicated
+    (:887-892), S = H / Alpha[:, None], the sum symmetrisation
+    (Trans2symmetryLowRes, :770-777: Y_ij = S_ij + S_ji, diagonal kept),
+    Correct_VC(Y, 2/3) (:780-790) and the mean rescale (:897-899).  Returns
+    the upper triangle (bin1, bin2, value), sorted and unique (cooler order)."""
+    t1, t2, tv = (np.asarray(x) for x in T_pixels)
+    t1, t2, tv = t1.astype(np.int64), t2.astype(np.int64), tv.astype(np.int64)
+    hr, hc, hv = (np.asarray(x) for x in H_cells)
+    hr, hc, hv = hr.astype(np.int64), hc.astype(np.int64), hv.astype(np.int64)
+    names = list(bins_pos)
+    n = max(e for _, e in bins_pos.values()) + 1
+    N2 = 2 * n
+    chrom_of = np.full(n, -1, np.int64)
+    for k, c in enumerate(names):
+        s, e = bins_pos[c]
+        chrom_of[s:e + 1] = k
+    # T row sums / nonzeros within each chromosome block (both triangles, diagonal once)
+    cis = chrom_of[t1] == chrom_of[t2]
+    off = cis & (t1 != t2)
+    tsum = np.bincount(t1[cis], tv[cis], minlength=n) + np.bincount(t2[off], tv[off], minlength=n)
+    tsum = np.rint(tsum).astype(np.int64)
+    nzc, nzo = cis & (tv != 0), off & (tv != 0)
+    tnz = np.bincount(t1[nzc], minlength=n) + np.bincount(t2[nzo], minlength=n)
+    # H row sums within the M_M / P_P block of the row's chromosome copy
+    block_of = np.full(N2, -1, np.int64)
+    for k, c in enumerate(names):
+        for h, key in ((0, "M" + c), (1, "P" + c)):
+            s, e = hap_bins_pos[key]
+            block_of[s:e + 1] = 2 * k + h
+    same = block_of[hr] == block_of[hc]
+    hbs = np.rint(np.bincount(hr[same], hv[same], minlength=N2)).astype(np.int64)  # exact below 2^53
+    alphas = {}
+    for c in names:
+        s, e = bins_pos[c]
+        L = e - s + 1
+        cov = 1 - (L - tnz[s:e + 1]) / float(L)
+        gap = np.nonzero(cov < 0.1)[0]
+        ms, me = hap_bins_pos["M" + c]
+        ps, pe = hap_bins_pos["P" + c]
+        alpha = (hbs[ms:me + 1] + hbs[ps:pe + 1]) / (tsum[s:e + 1] + 1)
+        alpha = alpha.astype(np.float64)
+        ng = non_gap(L, gap)
+        alpha /= np.max(alpha[ng])
+        alpha[alpha == 0] = 1
+        thr = np.percentile(alpha[ng], 20)
+        alpha[alpha < thr] = thr
+        alphas[c] = alpha
+    Alpha = np.concatenate([alphas[c] for c in sort_chromosomes(names)])
+    Alpha = np.concatenate([Alpha, Alpha])
+    S = hv / Alpha[hr]
+    # Y upper table: S_rc at key (min, max); partners add, the diagonal stays single
+    lo, hi = np.minimum(hr, hc), np.maximum(hr, hc)
+    key = lo * N2 + hi
+    o = np.argsort(key, kind="stable")
+    ks, vs = key[o], S[o]
+    first = np.concatenate([[True], ks[1:] != ks[:-1]]) if ks.size else np.zeros(0, bool)
+    idx = np.flatnonzero(first)
+    ukey = ks[idx]
+    Y = np.add.reduceat(vs, idx) if ks.size else np.zeros(0)
+    b1, b2 = ukey // N2, ukey % N2
+    offd = b1 != b2
+    rs = np.bincount(b1, Y, minlength=N2) + np.bincount(b2[offd], Y[offd], minlength=N2)
+    sv = rs ** VC_EXPONENT
+    sv[sv == 0] = 1
+    C = Y / (sv[b2] * sv[b1])
+    csum = np.sum(np.where(offd, 2.0, 1.0) * C)
+    NN = float(N2) * float(N2)
+    rf = (float(hv.sum()) / NN) / (csum / NN)
+    return b1, b2, rf * C

@@ -126,3 +126,32 @@ def test_refine_weights_levels_measured_cost():
     # zero-weight shard untouched, equal costs keep the partition
     np.testing.assert_array_equal(dist.refine_weights(np.zeros(10), [0, 5, 10], [1.0, 1.0]), np.zeros(10))
     np.testing.assert_array_equal(dist.partition_rows(dist.refine_weights(w, rr, [2.0, 2.0]), 2), rr)
+
+
+def test_cis_plan_local_genome_reassembles():
+    """--cis-only by chromosome (dist.cis_plan / local_genome): LPT owners,
+    compact renumbering; the oracle's per-rank balances of the local genomes
+    (MAD off: its cutoff is the one genome-wide step, exchanged on the GPU
+    path) reassemble the whole-genome --cis-only result exactly."""
+    from hichap_master_amd import dist, synth
+    from oracle import ice_ref
+    rng = np.random.default_rng(4)
+    b1, b2, c, off = synth.coo_genome([300, 250, 200, 150, 100], rng, A=20.0, trans_density=0.02)
+    n = int(off[-1])
+    w_full, st_full = ice_ref.balance(b1, b2, c, n, off, cis_only=True, mad_max=0, max_iters=300)
+    for world in (1, 2, 3):
+        owner, cost = dist.cis_plan(b1, b2, off, world)
+        assert sorted(set(owner.tolist())) == list(range(min(world, len(cost))))
+        w = np.full(n, np.nan)
+        for r in range(world):
+            mine = np.flatnonzero(owner == r)
+            lb1, lb2, lc, loff = dist.local_genome(b1, b2, c, off, mine)
+            assert (lb1 <= lb2).all() and lb2.max() < loff[-1]
+            wl, _ = ice_ref.balance(lb1, lb2, lc, int(loff[-1]), loff, cis_only=True, mad_max=0, max_iters=300)
+            p = 0
+            for ch in mine:
+                k = int(off[ch + 1] - off[ch])
+                w[off[ch]:off[ch + 1]] = wl[p:p + k]
+                p += k
+        np.testing.assert_array_equal(np.isnan(w), np.isnan(w_full))
+        np.testing.assert_allclose(w, w_full, rtol=1e-13, equal_nan=True)

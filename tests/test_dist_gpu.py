@@ -1,11 +1,13 @@
-"""Multi-process sharded ICE on the GPU: world_size-2 runs of
-hichap_master_amd.dist.balance_sharded with the HIP backend (IceState over a
-row shard each), both ranks on cuda:0 with the gloo exchange (RCCL refuses two
-ranks on one device; the RCCL path is covered at world 1 in test_ice_gpu.py
-and at N>1 by the driver's scaling bench), with the dense-band sweep on a
-side stream as bench.py runs shards.  Every rank's weights equal the
-one-process HIP run (default stream order) bitwise and the oracle within the
-ICE tolerance."""
+"""Multi-process sharded ICE on the GPU.  World-size-2 runs of
+hichap_master_amd.dist.balance_sharded / balance_capi (row shards) and
+balance_cis_sharded (--cis-only, whole chromosomes per rank, no collective in
+the iterations) with both ranks on cuda:0 and the gloo exchange (RCCL refuses
+two ranks on one device), the sweep's side streams forced on: every rank's
+weights equal the one-process HIP run (bitwise for row shards; 1e-12 for the
+compact per-rank chromosome numbering) and the oracle within the ICE
+tolerance.  test_rccl_every_gpu spawns one rank per GPU over the library's own
+RCCL communicator on any box with >= 2 GPUs (skipped on a 1-GPU box); RCCL at
+world 1 is covered by test_library_rccl_communicator_world1."""
 import os
 import socket
 import tempfile
@@ -39,9 +41,18 @@ def _worker(rank, world, port, case, cis_only, outdir, impl="python"):
         b1, b2, c, off = case
         n = int(off[-1])
         rr = dist.partition_rows(np.bincount(b1, minlength=n) + np.bincount(b2, minlength=n), world)
-        m = ice.ContactMatrix.from_pixels(b1, b2, c, n, off, cis_only=cis_only, row_range=(rr[rank], rr[rank + 1]))
         opts = ice.IceOptions(max_iters=400, cis_only=cis_only)
-        if impl == "capi":
+        if impl != "cis":
+            m = ice.ContactMatrix.from_pixels(b1, b2, c, n, off, cis_only=cis_only,
+                                              row_range=(rr[rank], rr[rank + 1]))
+        if impl == "cis":
+            # chromosomes by LPT, no collective in the iterations (gloo callback
+            # for the one MAD exchange)
+            cx = dist.CapiExchange([0, n], world, rank, backend="gloo")
+            w, s_ = dist.balance_cis_sharded(b1, b2, c, n, off, rank, world,
+                                             ice.IceOptions(max_iters=400, cis_only=True), cx)
+            cx.close()
+        elif impl == "capi":
             # the loop in C++ (hh_ice_balance_sharded), exchange = a gloo callback
             cx = dist.CapiExchange(rr, world, rank, backend="gloo")
             w, s_ = dist.balance_capi(m, opts, cx, torch.cuda.current_stream().cuda_stream)
@@ -53,14 +64,16 @@ def _worker(rank, world, port, case, cis_only, outdir, impl="python"):
             w, s_ = dist.balance_sharded(st, ex, max_iters=400)
             st.close()
         torch.cuda.synchronize()
-        m.close()
+        if impl != "cis":
+            m.close()
         np.save(os.path.join(outdir, f"w{rank}.npy"), w)
         np.save(os.path.join(outdir, f"it{rank}.npy"), np.atleast_1d(s_["iters"]))
     finally:
         tdist.destroy_process_group()
 
 
-@pytest.mark.parametrize("cis_only,impl", [(False, "python"), (True, "python"), (False, "capi"), (True, "capi")])
+@pytest.mark.parametrize("cis_only,impl", [(False, "python"), (True, "python"), (False, "capi"), (True, "capi"),
+                                            (True, "cis")])
 def test_balance_sharded_two_processes(cis_only, impl):
     import torch.multiprocessing as mp
     from hichap_master_amd import _lib, ice
@@ -77,9 +90,14 @@ def test_balance_sharded_two_processes(cis_only, impl):
         its = [np.load(os.path.join(d, f"it{r}.npy")) for r in range(2)]
     wr, sr = ice_ref.balance(b1, b2, c, n, off, cis_only=cis_only, max_iters=400)
     for w, it in zip(ws, its):
-        np.testing.assert_array_equal(w, w_full)
+        if impl == "cis":  # compact per-rank numbering: same sums up to the row-block grouping
+            np.testing.assert_array_equal(np.isnan(w), np.isnan(w_full))
+            np.testing.assert_allclose(w, w_full, rtol=1e-12, equal_nan=True)
+        else:
+            np.testing.assert_array_equal(w, w_full)
         np.testing.assert_allclose(w, wr, rtol=1e-9, equal_nan=True)
         np.testing.assert_array_equal(it, np.atleast_1d(st_full["iters"]))
+    np.testing.assert_array_equal(ws[0], ws[1])
 
 
 def test_library_rccl_communicator_world1():
@@ -110,3 +128,66 @@ def test_library_rccl_communicator_world1():
     w2, s2 = dist.balance_capi(m, opts, cx)
     np.testing.assert_array_equal(w1, w2)
     assert s1["iters"] == s2["iters"]
+
+
+def _rccl_worker(rank, world, port, case, outdir):
+    """One rank per GPU over the library's own RCCL communicator (xGMI):
+    genome-wide row shards (hh_ice_balance_sharded, one ncclAllGather of the
+    marginals per iteration) and --cis-only by chromosome
+    (hh_ice_balance_cis_local, no collective in the iterations)."""
+    import torch
+    import torch.distributed as tdist
+    from hichap_master_amd import _lib, dist, ice
+    torch.cuda.set_device(rank)
+    _lib.load()
+    _lib.call("hh_set_device", rank)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    tdist.init_process_group("gloo", rank=rank, world_size=world)  # bootstrap for the ncclUniqueId only
+    try:
+        b1, b2, c, off = case
+        n = int(off[-1])
+        rr = dist.partition_rows(np.bincount(b1, minlength=n) + np.bincount(b2, minlength=n), world)
+        cx = dist.CapiExchange(rr, world, rank, backend="nccl")
+        m = ice.ContactMatrix.from_pixels(b1, b2, c, n, off, row_range=(rr[rank], rr[rank + 1]))
+        w, s_ = dist.balance_capi(m, ice.IceOptions(max_iters=400), cx, torch.cuda.current_stream().cuda_stream)
+        m.close()
+        wc, sc = dist.balance_cis_sharded(b1, b2, c, n, off, rank, world,
+                                          ice.IceOptions(max_iters=400, cis_only=True), cx)
+        torch.cuda.synchronize()
+        cx.close()
+        np.save(os.path.join(outdir, f"w{rank}.npy"), w)
+        np.save(os.path.join(outdir, f"wc{rank}.npy"), wc)
+        np.save(os.path.join(outdir, f"it{rank}.npy"), np.array([s_["iters"]]))
+        np.save(os.path.join(outdir, f"itc{rank}.npy"), np.atleast_1d(sc["iters"]))
+    finally:
+        tdist.destroy_process_group()
+
+
+def test_rccl_every_gpu():
+    """RCCL at world = every GPU of the box (skipped below 2: RCCL refuses
+    two ranks on one device): the genome-wide sharded balance is bitwise the
+    one-GPU run (small matrix: the unit plan sits at its floor, so shards
+    sum every row in the same order) and the chromosome-dealt --cis-only run
+    equals the one-GPU --cis-only run to 1e-12 with the same iterations."""
+    import torch
+    import torch.multiprocessing as mp
+    from hichap_master_amd import _lib, ice
+    _lib.require_gpu()
+    world = min(torch.cuda.device_count(), 8)
+    if world < 2:
+        pytest.skip("one GPU on this box: RCCL at world > 1 needs >= 2 devices")
+    rng = np.random.default_rng(33)
+    case = synth.coo_genome([1100, 900, 700, 500, 300], rng, A=25.0, trans_density=0.01)
+    b1, b2, c, off = case
+    n = int(off[-1])
+    w_full, st_full = ice.balance(b1, b2, c, n, off, max_iters=400)
+    wc_full, stc_full = ice.balance(b1, b2, c, n, off, cis_only=True, max_iters=400)
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_rccl_worker, args=(world, _free_port(), case, d), nprocs=world, start_method="spawn")
+        for r in range(world):
+            np.testing.assert_array_equal(np.load(os.path.join(d, f"w{r}.npy")), w_full)
+            assert int(np.load(os.path.join(d, f"it{r}.npy"))[0]) == st_full["iters"]
+            wc = np.load(os.path.join(d, f"wc{r}.npy"))
+            np.testing.assert_array_equal(np.isnan(wc), np.isnan(wc_full))
+            np.testing.assert_allclose(wc, wc_full, rtol=1e-12, equal_nan=True)
+            np.testing.assert_array_equal(np.load(os.path.join(d, f"itc{r}.npy")), stc_full["iters"])
