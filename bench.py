@@ -807,6 +807,9 @@ def run_gw(args, world, rank, local):
     elapsed = time.perf_counter() - t_start
     if rank == 0:
         in_bytes = 12.0 * (T.nnz + H.nnz)
+        out_bytes = 16.0 * info["out_nnz"]  # int32 bin1 + int32 bin2 + fp64 value
+        step_s = elapsed / args.steps
+        alg = in_bytes + out_bytes
         out = {
             "metric": "sparse GenomeWideMatrixCorrection, hg19 10 kb diploid (T table + imputed H cells -> corrected table)",
             "value": args.steps / elapsed, "unit": "corrections/s", "n_gpus": 1, "steps": args.steps,
@@ -816,13 +819,133 @@ def run_gw(args, world, rank, local):
             "config": {"workload": "hg19-10kb-diploid-genomewide-correction", "n_bins_T": n, "n_bins_H": 2 * n,
                        "T_pixels": T.nnz, "H_cells": H.nnz, "out_pixels": info["out_nnz"],
                        "generate_s": round(gen_s, 2)},
-            "input_GBps": in_bytes / (elapsed / args.steps) / 1e9,
+            "input_GBps": in_bytes / step_s / 1e9,
             "cells_per_s": H.nnz * args.steps / elapsed,
+            "roofline": {"bound": "hbm", "kernel": "the whole correction (hh_gw_create + hh_gw_correct: ~25 kernels, "
+                                                   "per-kernel times in profiles/*gw_kernel_stats.csv)",
+                         "achieved": alg / step_s / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                         "frac": alg / step_s / 1e9 / PEAK_HBM_GBS, "traffic": None,
+                         "alg_bytes_per_launch": alg,
+                         "alg_bytes_note": "12 B per T pixel and H cell read (int32 ids, int32 count) + 16 B per "
+                                           "corrected upper cell written (int32 bin1, bin2, fp64 value)"},
             "note": "dense reference form: 607282^2 x 8 B = 2.9 TB per matrix (infeasible)",
         }
+        if not args.no_cpu:
+            out["cpu_baseline"] = with_host(gw_cpu_baseline(bins, hap, H.nnz))
+            out["vs_cpu_baseline"] = out["value"] / out["cpu_baseline"]["value"]
         print(json.dumps(out), flush=True)
     T.close()
     H.close()
+
+
+def gw_cpu_baseline(bins, hap, h_full, depth=2e8, seed=20201023):
+    """The pixel-table oracle (oracle/hichap_ref.genome_wide_correction_sparse,
+    NumPy, 1 core) on the same 10 kb diploid layout at reduced depth (~2e8 T
+    pixels + ~2e8 H cells, generated on the GPU and copied to the host; at
+    much lower depth whole chromosomes fall under Gap_definedLowRes's 0.1
+    coverage and the reference's alpha step raises), as corrections/s
+    extrapolated by H cells."""
+    import ctypes as C
+    import torch
+    from hichap_master_amd import ice, synth
+    from hichap_master_amd._lib import call
+    from oracle import hichap_ref
+    nb = synth.genome_bins(10000)
+    At, tdt = synth.calibrate(nb, depth, 0.2)
+    Ah, tdh = synth.calibrate(nb + nb, depth / 2.0, 0.2)
+    T = ice.SynthPixels(nb, ordered=False, A=At, trans_density=tdt, comp_block=200, ignore_diags=0, seed=seed)
+    H = ice.SynthPixels(nb + nb, ordered=True, A=Ah, trans_density=tdh, comp_block=200, ignore_diags=0,
+                        seed=seed + 1)
+
+    def host(a):
+        t = torch.empty(a.numel(), dtype=torch.int32, device="cuda")
+        if a.numel():
+            call("hh_device_copy", C.c_void_p(t.data_ptr()), C.c_void_p(a.data_ptr()), 4 * a.numel(), None)
+        call("hh_synchronize", None)
+        return t.cpu().numpy()
+
+    tp = tuple(host(x) for x in (T.bin1, T.bin2, T.count))
+    hc = tuple(host(x) for x in (H.bin1, H.bin2, H.count))
+    hn = H.nnz
+    T.close()
+    H.close()
+    t0 = time.perf_counter()
+    hichap_ref.genome_wide_correction_sparse(bins, hap, tp, hc)
+    dt = time.perf_counter() - t0
+    return {"value": (hn / dt) / h_full, "unit": "corrections/s (full-depth matrix, extrapolated by H cells)",
+            "cores": 1, "kind": "port",
+            "sample": f"oracle/hichap_ref.genome_wide_correction_sparse (NumPy) on the 10 kb diploid layout at "
+                      f"{tp[0].size} T pixels + {hn} H cells: {dt:.1f} s = {hn / dt:.3g} H cells/s",
+            "cells_per_s": hn / dt}
+
+
+def run_twostep(args, world, rank, local):
+    """TwoStepCorrection (matrixBuilding.py:984-1023) at HiCHap's default
+    localRes: hg19 chr1 at 40 kb (N = 6 232), synthetic T / imputed M, P.
+    A step = the whole correction on device-resident int64 matrices (gaps,
+    alpha, gap-aware symmetrisation, VC^(2/3), mean rescale; no host round
+    trip).  Also timed: the host-array call (3 uploads + 2 downloads of
+    N^2 x 8 B) and the cell-fed call (pixel tables in, upper tables out)."""
+    import torch
+    from hichap_master_amd import matrixBuilding as mb, synth
+    N = 249250621 // 40000 + 1
+    rng = np.random.default_rng(20201024)
+    TM = synth.dense_chrom(N, rng, A=60.0)
+    MM, PM = synth.haplotype_pair(TM, rng, drop_rows=120)
+    dev = [torch.from_numpy(X).cuda() for X in (TM, MM, PM)]
+    torch.cuda.synchronize()
+    for _ in range(args.warmup):
+        mb.TwoStepCorrection(*dev)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = mb.TwoStepCorrection(*dev)
+        del out
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    step = elapsed / args.steps
+    # the host-array form and the cell-fed form (a few calls each)
+    def wall(fn, k=3):
+        fn()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(k):
+            fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t) / k
+    host_s = wall(lambda: mb.TwoStepCorrection(TM, MM, PM))
+    i, j = np.nonzero(np.triu(TM))
+    tp = (i, j, TM[i, j])
+    cells = []
+    for X in (MM, PM):
+        r, c = np.nonzero(X)
+        cells.append((r, c, X[r, c]))
+    cells_s = wall(lambda: mb.TwoStepCorrectionPixels(N, tp, cells[0], cells[1]))
+    alg = 3 * 8.0 * N * N + 2 * 8.0 * N * N  # SURVEY 8(d): 3 int64 reads + 2 fp64 writes
+    if rank == 0:
+        out = {"metric": "TwoStepCorrection, hg19 chr1 at 40 kb (N = 6232), device-resident",
+               "value": 1.0 / step, "unit": "chromosomes/s", "n_gpus": 1, "steps": args.steps,
+               "warmup": args.warmup, "ms_per_step": 1000.0 * step, "higher_is_better": True,
+               "scaling": "replicas", "vs_baseline": None, "dtype": "int64 in, f64 out",
+               "data": "synthetic (synth.dense_chrom + haplotype_pair)",
+               "config": {"workload": "twostep-chr1-40kb", "N": N, "nnz_T_upper": int(i.size),
+                          "cells_MM": int(cells[0][0].size), "cells_PM": int(cells[1][0].size)},
+               "roofline": {"bound": "hbm", "kernel": "hh_twostep (k_rowstats x3, k_symvc passes x2 matrices)",
+                            "achieved": alg / step / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                            "frac": alg / step / 1e9 / PEAK_HBM_GBS, "traffic": None,
+                            "alg_bytes_per_launch": alg},
+               "host_arrays_ms": 1000.0 * host_s, "cells_in_upper_out_ms": 1000.0 * cells_s,
+               "note": "host_arrays_ms: numpy N x N in / out (PCIe: 1.55 GB per call); cells_in_upper_out_ms: "
+                       "pixel tables in, corrected upper tables out (TwoStepCorrectionPixels)"}
+        if not args.no_cpu:
+            from oracle import hichap_ref
+            t = time.perf_counter()
+            hichap_ref.two_step_correction(TM, MM, PM)
+            dt = time.perf_counter() - t
+            out["cpu_baseline"] = with_host({"value": 1.0 / dt, "unit": "chromosomes/s", "cores": 1, "kind": "port",
+                                             "sample": f"oracle/hichap_ref.two_step_correction (vectorised NumPy) "
+                                                       f"on the same chromosome: {dt:.2f} s"})
+        print(json.dumps(out), flush=True)
 
 
 def main():
@@ -866,9 +989,9 @@ def main():
         else:
             tdist.init_process_group(backend)
 
-    if args.config in ("c5", "pairs", "loops", "dropin", "e2e", "gw"):
+    if args.config in ("c5", "pairs", "loops", "dropin", "e2e", "gw", "twostep"):
         {"c5": run_c5, "pairs": run_pairs, "loops": run_loops, "dropin": run_dropin,
-         "e2e": run_e2e, "gw": run_gw}[args.config](args, world, rank, local)
+         "e2e": run_e2e, "gw": run_gw, "twostep": run_twostep}[args.config](args, world, rank, local)
         if torch.distributed.is_initialized():
             torch.distributed.destroy_process_group()
         return

@@ -341,6 +341,32 @@ class StructureFind(TADCalling):
                     d.setdefault(parts[0], []).append(parts[-1])
         return {k: np.array(v, dtype=float) for k, v in d.items()}
 
+    def _gaps(self):
+        """The haplotype gap lists (CallPeaks :1985-1991): ``GapFile`` as a
+        dict {str(Res): {chrom: gap}} / {chrom: gap}, or an .npz path read
+        without unpickling (a pickled npz raises: pass the dict)."""
+        G = self.Gap_file
+        if G is None:
+            raise ValueError("Gap file needed for haplotype-resolved loop calling ...")
+        if isinstance(G, (str, bytes)):
+            with np.load(G, allow_pickle=False) as z:
+                G = {k: z[k] for k in z.files}
+        if str(self.Res) in G:
+            G = G[str(self.Res)]
+            G = G[()] if hasattr(G, "shape") and G.shape == () else G
+        return G
+
+    def CallPeaks(self, outfil, Allelic=False):
+        """HICCUPS loop calling from the cooler (StructureFind.py:1954-2043):
+        raw, balanced and weight read from ``cooler_fil::Res`` itself
+        (:2006-2010) as pixel bands -- no dense N x N -- then
+        hichap_master_amd.loops on the GPU; writes the reference's file."""
+        from . import loops
+        gaps = None if Allelic is False else self._gaps()
+        out = loops.call_peaks_cooler(self.cooler_fil, outfil, self.Res, Allelic, gaps)
+        self.chroms = list(out)
+        return out
+
     def Compartment(self, SA=False, Tranditional_PC_file=None, Matrix_Dict=None):
         """Compartment() (StructureFind.py:491-554): raw matrices from the
         cooler (or ``Matrix_Dict``), one selected PC per chromosome in

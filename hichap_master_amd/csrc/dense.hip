@@ -19,7 +19,7 @@
 #include <type_traits>
 #include <vector>
 
-#include "hh_common.hpp"
+#include "ice_internal.hpp"  // hh_common.hpp + dev_excl_scan_i64
 
 namespace hh {
 
@@ -310,6 +310,65 @@ static std::vector<uint8_t> gap_defined(const std::vector<long long>& zeros, lon
     return g;
 }
 
+// Dense N x N int64 from cells (row, col, count) with ids shifted by
+// `offset` (pairs.dense_from_pixels / the reference's per-line dense `+=`
+// result, matrixBuilding.py:554, :567-570, :1290-1301): out[r][c] = v, and
+// out[c][r] = v for an upper-triangle (symmetric) table.  Cells are unique
+// (cooler's tables, the binner's run-length output), so no two threads write
+// one element.
+__global__ void k_dense_scatter(const long long* __restrict__ r, const long long* __restrict__ c,
+                                const long long* __restrict__ v, long long nnz, long long N, long long offset,
+                                int sym, long long* __restrict__ out, unsigned long long* __restrict__ bad) {
+    const long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= nnz) return;
+    const long long a = r[k] - offset, b = c[k] - offset;
+    if (a < 0 || b < 0 || a >= N || b >= N || (sym && a > b)) {
+        atomicMin(bad, (unsigned long long)k);
+        return;
+    }
+    out[a * N + b] = v[k];
+    if (sym) out[b * N + a] = v[k];
+}
+
+// Upper-triangle nonzeros of a dense fp64 N x N matrix in row-major (cooler)
+// order -- the np.triu(...).nonzero() table NPZ2Cooler writes for the
+// corrected matrices (matrixBuilding.py:1613, :1628-1633).  PASS 0: per-row
+// counts (one block per row); PASS 1: write at the scanned row offsets, the
+// block's 256-wide chunks in order (ballot compaction keeps column order).
+template <int PASS>
+__global__ __launch_bounds__(256) void k_upper_nz(const double* __restrict__ X, long long N,
+                                                  long long* __restrict__ cnt_or_off, int32_t* __restrict__ ob1,
+                                                  int32_t* __restrict__ ob2, double* __restrict__ ov) {
+    __shared__ long long wtot[4];
+    __shared__ long long base_sh;
+    const long long i = blockIdx.x;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const double* row = X + i * N;
+    long long base = PASS ? cnt_or_off[i] : 0;
+    for (long long j0 = i; j0 < N; j0 += 256) {
+        const long long j = j0 + threadIdx.x;
+        const double x = j < N ? row[j] : 0.0;
+        const unsigned long long m = __ballot(x != 0.0);
+        if (lane == 0) wtot[wave] = __popcll(m);
+        __syncthreads();
+        long long before = 0, tot = 0;
+        for (int w = 0; w < 4; ++w) {
+            if (w < wave) before += wtot[w];
+            tot += wtot[w];
+        }
+        if (PASS == 1 && x != 0.0) {
+            const long long pos = base + before + __popcll(m & ((1ull << lane) - 1ull));
+            ob1[pos] = (int32_t)i;
+            ob2[pos] = (int32_t)j;
+            ov[pos] = x;
+        }
+        base += tot;
+        __syncthreads();
+    }
+    if (PASS == 0 && threadIdx.x == 0) cnt_or_off[i] = base;
+    (void)base_sh;
+}
+
 }  // namespace hh
 
 using namespace hh;
@@ -461,6 +520,73 @@ int hh_twostep(const int64_t* TM, const int64_t* MM, const int64_t* PM, int64_t 
         HIP_CHECK(hipStreamSynchronize(s));
         std::copy(gm.begin(), gm.end(), gap_m);
         std::copy(gp.begin(), gp.end(), gap_p);
+    });
+}
+
+int hh_dense_from_cells(const int64_t* row, const int64_t* col, const int64_t* count, int64_t nnz, int64_t N,
+                        int64_t offset, int32_t symmetric, int32_t on_device, int64_t* out, void* stream) {
+    return guard([&] {
+        HH_REQUIRE(out && N > 0 && nnz >= 0 && (nnz == 0 || (row && col && count)), "bad arguments");
+        hipStream_t s = as_stream(stream);
+        DBuf<long long> buf[3];
+        const long long* d[3] = {(const long long*)row, (const long long*)col, (const long long*)count};
+        if (!on_device)
+            for (int k = 0; k < 3; ++k) {
+                buf[k].alloc(std::max<int64_t>(nnz, 1));
+                buf[k].upload(d[k], nnz, s);
+                d[k] = buf[k].p;
+            }
+        HIP_CHECK(hipMemsetAsync(out, 0, (size_t)N * N * sizeof(long long), s));
+        DBuf<unsigned long long> bad(1);
+        HIP_CHECK(hipMemsetAsync(bad.p, 0xff, sizeof(unsigned long long), s));
+        if (nnz)
+            hipLaunchKernelGGL(k_dense_scatter, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s, d[0], d[1], d[2],
+                               (long long)nnz, (long long)N, (long long)offset, symmetric, (long long*)out, bad.p);
+        HIP_CHECK(hipGetLastError());
+        unsigned long long hb = 0;
+        bad.download(&hb, 1, s);
+        HIP_CHECK(hipStreamSynchronize(s));
+        if (hb != ~0ull)
+            HH_THROW(HH_ERR_ARG, std::string(symmetric ? "pixel " : "cell ") + std::to_string(hb) +
+                                     " outside the matrix" + (symmetric ? " or below the diagonal" : ""));
+    });
+}
+
+// two calls: the count (caller sizes device buffers), then the write (which
+// recounts: one more read of X, ~80 us at N = 6 232, against a host round trip)
+static void upper_offsets(const double* X, int64_t N, DBuf<long long>& off, unsigned long long* m, hipStream_t s) {
+    DBuf<long long> cnt(N + 1);
+    off.alloc(N + 1);
+    HIP_CHECK(hipMemsetAsync(cnt.p + N, 0, sizeof(long long), s));
+    hipLaunchKernelGGL(k_upper_nz<0>, dim3((unsigned)N), dim3(256), 0, s, X, (long long)N, cnt.p, (int32_t*)nullptr,
+                       (int32_t*)nullptr, (double*)nullptr);
+    DBuf<unsigned long long> tot(1);
+    dev_excl_scan_i64(cnt.p, off.p, N + 1, tot.p, s);
+    tot.download(m, 1, s);
+    HIP_CHECK(hipStreamSynchronize(s));
+}
+
+int hh_dense_upper_count(const double* X, int64_t N, int64_t* nnz, void* stream) {
+    return guard([&] {
+        HH_REQUIRE(X && N > 0 && nnz, "bad arguments");
+        DBuf<long long> off;
+        unsigned long long m = 0;
+        upper_offsets(X, N, off, &m, as_stream(stream));
+        *nnz = (int64_t)m;
+    });
+}
+
+int hh_dense_upper_write(const double* X, int64_t N, int32_t* bin1, int32_t* bin2, double* value, void* stream) {
+    return guard([&] {
+        HH_REQUIRE(X && N > 0 && bin1 && bin2 && value, "bad arguments");
+        hipStream_t s = as_stream(stream);
+        DBuf<long long> off;
+        unsigned long long m = 0;
+        upper_offsets(X, N, off, &m, s);
+        hipLaunchKernelGGL(k_upper_nz<1>, dim3((unsigned)N), dim3(256), 0, s, X, (long long)N, off.p, bin1, bin2,
+                           value);
+        HIP_CHECK(hipGetLastError());
+        HIP_CHECK(hipStreamSynchronize(s));
     });
 }
 

@@ -53,19 +53,49 @@ def biases_from_weights(weights):
     return biases
 
 
-def bands(H_raw, weights, res, allelic=False, params=None):
-    """Raw / balanced bands, expected per diagonal and biases (:2003-2032)."""
-    from sklearn import isotonic
+def band_width(res, params=None):
+    """``num`` of CallPeaks (:2020): diagonals 0 .. maxapart // res + maxww."""
     p = params or peaks_parameter(res)
-    ww, maxww, maxapart = p["ww"], p["maxww"], p["maxapart"]
-    H = np.asarray(H_raw)
-    N = H.shape[0]
-    num = maxapart // res + maxww + 1
+    return p["maxapart"] // res + p["maxww"] + 1
+
+
+def raw_band_from_pixels(bin1, bin2, count, lo, N, num):
+    """raw[r, d] = H[r, r + d] (d < num) of chromosome bins [lo, lo + N)
+    straight from cooler's upper-triangle pixel table (global ids, unique
+    pixels): the band CallPeaks reads from ``matrix(balance=False).fetch``
+    (:2006), without the N x N matrix."""
+    b1 = np.asarray(bin1, dtype=np.int64) - lo
+    b2 = np.asarray(bin2, dtype=np.int64) - lo
+    c = np.asarray(count)
+    d = b2 - b1
+    k = (b1 >= 0) & (b1 < N) & (b2 < N) & (d >= 0) & (d < num)
+    raw = np.zeros((N, num), dtype=c.dtype if c.dtype.kind in "iu" else np.float64)
+    raw[b1[k], d[k]] = c[k]
+    return raw
+
+
+def bands(H_raw, weights, res, allelic=False, params=None, raw=None):
+    """Raw / balanced bands, expected per diagonal and biases (:2003-2032),
+    from the dense raw matrix or (``raw``, ``H_raw=None``) from its band."""
+    p = params or peaks_parameter(res)
+    num = band_width(res, p)
+    if raw is None:
+        H = np.asarray(H_raw)
+        N = H.shape[0]
+        r = np.arange(N)[:, None]
+        d = np.arange(num)[None, :]
+        raw = np.where((r + d) < N, H[r, np.minimum(r + d, N - 1)], 0)
+    return _bands_from_raw(np.asarray(raw), weights, res, allelic, p)
+
+
+def _bands_from_raw(raw, weights, res, allelic, p):
+    from sklearn import isotonic
+    ww = p["ww"]
+    N, num = raw.shape
     r = np.arange(N)[:, None]
     d = np.arange(num)[None, :]
     inside = (r + d) < N
     cc = np.minimum(r + d, N - 1)
-    raw = np.where(inside, H[r, cc], 0)
     if not allelic:
         w = np.asarray(weights, dtype=np.float64)
         # cH = nan_to_num(H * w_i * w_j), evaluated on the band in the same order
@@ -267,7 +297,10 @@ def significance(B, xi, yi, S, E, valid):
 
 def pcaller(H_raw, weights, res, allelic=False, gap=None, stream=None, return_widths=False):
     """One chromosome of StructureFind.CallPeaks: (Donuts, LL) as the reference."""
-    B = bands(H_raw, weights, res, allelic)
+    return _pcaller_bands(bands(H_raw, weights, res, allelic), gap, stream, return_widths)
+
+
+def _pcaller_bands(B, gap=None, stream=None, return_widths=False):
     xi, yi = candidates(B, gap)
     nb = Neighbourhood(B, stream)
     try:
@@ -281,6 +314,42 @@ def pcaller(H_raw, weights, res, allelic=False, gap=None, stream=None, return_wi
 LINE_FORMAT = "%s\t%d\t%d\t%.4g\t%.4g\t%.4g\t%.4g\t%.4g\t%.4g\t%.4g\n"
 HEAD = "\t".join(["chromLabel", "loc_1", "loc_2", "IF", "D-Enrichment", "D-pvalue", "D-qvalue",
                   "LL-Enrichment", "LL-pvalue", "LL-qvalue"]) + "\n"
+
+
+def call_peaks_cooler(cooler_uri, outfil, res, allelic=False, gaps=None):
+    """CallPeaks (:1954-2043) reading the cooler itself, as the reference
+    does (:2003-2015): per chromosome the raw band from the pixel table
+    (``matrix(balance=False)``), the balanced band from the same pixels and
+    ``bins/weight`` (``matrix(balance=True)`` + nan_to_num, biases
+    ``1 / weight``), allelic data raw with its gap list; no N x N matrix.
+    ``allelic``: False, 'Maternal' or 'Paternal' (chromosomes by prefix)."""
+    from .coolio import Cooler
+    out = {}
+    with Cooler(cooler_uri) as c:
+        if allelic is False:
+            chroms = list(c.chromnames)
+        elif allelic in ("Maternal", "Paternal"):
+            chroms = [x for x in c.chromnames if x.startswith(allelic[0])]
+            if gaps is None:
+                raise ValueError("Gap file needed for haplotype-resolved loop calling ...")
+        else:
+            raise ValueError(f"Unkonwn key word {allelic}, Only Maternal, Paternal, False allowed")
+        w_all = c.weights() if allelic is False else None
+        num = band_width(res)
+        with open(outfil, "w") as f:
+            f.write(HEAD)
+            for chro in chroms:
+                lo, hi = c.extent(chro)
+                b1, b2, v = c.pixel_rows(lo, hi)
+                raw = raw_band_from_pixels(b1, b2, v, lo, hi - lo, num)
+                w = None if w_all is None else w_all[lo:hi]
+                B = bands(None, w, res, allelic is not False, raw=raw)
+                D, L = _pcaller_bands(B, None if allelic is False else gaps[chro])
+                out[chro] = (D, L)
+                label = chro if allelic is False else chro[1:]
+                for pos in sorted(D):
+                    f.write(LINE_FORMAT % ((label,) + pos + tuple(D[pos]) + tuple(L[pos][1:])))
+    return out
 
 
 def call_peaks(matrices, res, outfil, allelic=False, gaps=None):
@@ -299,5 +368,5 @@ def call_peaks(matrices, res, outfil, allelic=False, gaps=None):
     return out
 
 
-__all__ = ["peaks_parameter", "bands", "candidates", "Neighbourhood", "significance", "pcaller", "call_peaks",
+__all__ = ["peaks_parameter", "bands", "band_width", "raw_band_from_pixels", "call_peaks_cooler", "candidates", "Neighbourhood", "significance", "pcaller", "call_peaks",
            "lambda_chunks", "biases_from_weights"]

@@ -104,6 +104,8 @@ def TwoStepCorrection(TM, MM, PM):
     One C-ABI call (``hh_twostep``): each matrix is uploaded once, the gap /
     alpha glue runs in C++ with np.percentile semantics."""
     _lib.require_gpu()
+    if all(hasattr(X, "data_ptr") for X in (TM, MM, PM)):
+        return _twostep_device(TM, MM, PM)
     mats = [np.ascontiguousarray(X, dtype=np.int64) for X in (TM, MM, PM)]
     N = mats[0].shape[0]
     if any(X.ndim != 2 or X.shape != (N, N) for X in mats):
@@ -115,6 +117,87 @@ def TwoStepCorrection(TM, MM, PM):
     call("hh_twostep", ptr(mats[0]), ptr(mats[1]), ptr(mats[2]), N, ptr(Nor_MM), ptr(Nor_PM), ptr(gm), ptr(gp), 0,
          None)
     return Nor_MM, Nor_PM, np.nonzero(gm)[0].astype(np.int64), np.nonzero(gp)[0].astype(np.int64)
+
+
+def _twostep_device(TM, MM, PM, stream=None):
+    """TwoStepCorrection on int64 device tensors: no host round trip; returns
+    (Nor_MM, Nor_PM) as float64 device tensors and the gap index arrays."""
+    import torch
+    N = int(TM.shape[0])
+    for X in (TM, MM, PM):
+        if tuple(X.shape) != (N, N) or X.dtype != torch.int64 or not X.is_cuda or not X.is_contiguous():
+            raise ValueError("TM, MM, PM must be contiguous int64 N x N device tensors")
+    nm = torch.empty((N, N), dtype=torch.float64, device=TM.device)
+    npm = torch.empty((N, N), dtype=torch.float64, device=TM.device)
+    gm = np.empty(N, np.uint8)
+    gp = np.empty(N, np.uint8)
+    dp = lambda t: C.c_void_p(t.data_ptr())
+    call("hh_twostep", dp(TM), dp(MM), dp(PM), N, dp(nm), dp(npm), ptr(gm), ptr(gp), 1, stream)
+    return nm, npm, np.nonzero(gm)[0].astype(np.int64), np.nonzero(gp)[0].astype(np.int64)
+
+
+def dense_from_cells_device(cells, N, offset=0, symmetric=False, stream=None):
+    """Dense int64 N x N device tensor from (row, col, count) cells (host
+    arrays or int64 device tensors) -- the reference's dense matrices
+    (:554, :567-570, :1290-1301) built on the GPU so only cells cross PCIe.
+    ``symmetric``: an upper-triangle table mirrored (T); else ordered cells
+    (the asymmetric imputed MM / PM)."""
+    import torch
+    out = torch.empty((int(N), int(N)), dtype=torch.int64, device="cuda")
+    on_dev = hasattr(cells[0], "data_ptr")
+    if on_dev:
+        arrs = [x.to(torch.int64).contiguous() for x in cells]
+        ps = [C.c_void_p(x.data_ptr()) for x in arrs]
+        n = int(arrs[0].numel())
+    else:
+        arrs = [np.ascontiguousarray(x, dtype=np.int64) for x in cells]
+        ps = [ptr(x) for x in arrs]
+        n = int(arrs[0].size)
+    call("hh_dense_from_cells", ps[0], ps[1], ps[2], n, int(N), int(offset), int(bool(symmetric)), int(on_dev),
+         C.c_void_p(out.data_ptr()), stream)
+    return out
+
+
+def upper_table_device(X, stream=None):
+    """np.triu(X).nonzero() of a dense fp64 device matrix as (bin1, bin2,
+    value) int32 / int32 / float64 device tensors in cooler order -- what
+    NPZ2Cooler writes for a corrected matrix (:1613, :1628-1633)."""
+    import torch
+    N = int(X.shape[0])
+    m = C.c_int64(0)
+    call("hh_dense_upper_count", C.c_void_p(X.data_ptr()), N, C.byref(m), stream)
+    out = [torch.empty(max(int(m.value), 1), dtype=dt, device=X.device)
+           for dt in (torch.int32, torch.int32, torch.float64)]
+    call("hh_dense_upper_write", C.c_void_p(X.data_ptr()), N, *(C.c_void_p(t.data_ptr()) for t in out), stream)
+    return tuple(t[:int(m.value)] for t in out)
+
+
+def TwoStepCorrectionPixels(N, T_pixels, MM_cells, PM_cells, offset=0, output="upper", stream=None):
+    """TwoStepCorrection (:984-1023) fed by the tables the matrix
+    construction produces -- T as an upper-triangle pixel table, the imputed
+    MM / PM as ordered cells (asymmetric, :1290-1301) -- with the dense
+    matrices built and corrected on the GPU: only the cells cross PCIe, not
+    3 x N^2 x 8 B in and 2 x N^2 x 8 B out.  ``output="upper"``: the
+    corrected matrices' upper-triangle tables (bin1, bin2, value) as host
+    arrays -- the triu COO NPZ2Cooler stores (:1613, :1628-1633);
+    ``"device"``: dense float64 device tensors.  Returns (Nor_MM, Nor_PM,
+    Gap_M, Gap_P)."""
+    _lib.require_gpu()
+    TM = dense_from_cells_device(T_pixels, N, offset, True, stream)
+    MM = dense_from_cells_device(MM_cells, N, offset, False, stream)
+    PM = dense_from_cells_device(PM_cells, N, offset, False, stream)
+    nm, npm, gm, gp = _twostep_device(TM, MM, PM, stream)
+    del TM, MM, PM
+    if output == "device":
+        return nm, npm, gm, gp
+    if output != "upper":
+        raise ValueError("output must be 'upper' or 'device'")
+    res = []
+    for X in (nm, npm):
+        b1, b2, v = upper_table_device(X, stream)
+        res.append((b1.cpu().numpy().astype(np.int64) + offset, b2.cpu().numpy().astype(np.int64) + offset,
+                    v.cpu().numpy()))
+    return res[0], res[1], gm, gp
 
 
 def IntraChromMatrixCorrection(Tra_Lib, Hap_Lib):

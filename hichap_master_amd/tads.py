@@ -139,7 +139,7 @@ class TADCalling:
         haplotype data) or given in memory.  Sets Gap_all, DI_dict,
         DI_all_train."""
         if Matrix_Dict is None and getattr(self, "cooler_fil", None):
-            _, Matrix_Dict = self._chroms_and_matrices(True)  # balanced, NaN -> 0 (:853-854)
+            return self._data_preprocess_pixels()
         if Matrix_Dict is None:
             Matrix_Dict = getattr(self, "Matrix_Dict", None)
         if Matrix_Dict is None:
@@ -163,6 +163,39 @@ class TADCalling:
                                                      Gap_desity_t)
         self.DI_all_train, self.DI_dict, self.Gap_all = DI_all_train, DI_dict, Gap_all
         self.Matrix_Dict, self.chroms = Matrix_Dict, list(Matrix_Dict.keys())
+
+    def _data_preprocess_pixels(self):
+        """Data_preprocess from the cooler (StructureFind.py:842-915) on its
+        pixel table: per chromosome the gap / DI scans run on a band built on
+        the GPU from the pixels and ``bins/weight`` (balanced, NaN -> 0, for
+        traditional data :853-854; raw for haplotype data :858-865) -- the
+        N x N matrix the reference fetches (5 GB for chr1 at 10 kb) never
+        exists; bitwise the dense path's gap and DI (``di_scan_pixels``).
+        ``Matrix_Dict`` becomes a lazy {chrom: dense} view for Plot_TAD."""
+        from .coolio import Cooler
+        with Cooler(self.cooler_fil) as c:
+            if self.Allelic is False:
+                chroms = list(c.chromnames)
+            elif self.Allelic in ("Maternal", "Paternal"):
+                chroms = [x for x in c.chromnames if x.startswith(self.Allelic[0])]
+            else:
+                raise ValueError(f"Unkonwn key word {self.Allelic}, Only Maternal, Paternal, False allowed")
+            w = c.weights() if self.Allelic is False else None
+            width = 7
+            Gap_all, DI_dict, DI_all_train = {}, {}, {}
+            for chro in chroms:
+                lo, hi = c.extent(chro)
+                N = hi - lo
+                b1, b2, v = c.pixel_rows(lo, hi)
+                keep = b2 < hi
+                Gap, DI_sub = self.di_scan_pixels(b1[keep], b2[keep], v[keep], w, lo, N)
+                Gap_desity_t = float(Gap.size) / N / 2.0
+                Gap_all[chro] = Gap
+                DI_dict[chro] = DI_sub
+                DI_all_train[chro] = self.train_segments(Gap, self.Gap_Filter(Gap, None), DI_sub, width,
+                                                         Gap_desity_t)
+        self.DI_all_train, self.DI_dict, self.Gap_all = DI_all_train, DI_dict, Gap_all
+        self.Matrix_Dict, self.chroms = _LazyMatrices(self.cooler_fil, chroms, self.Allelic is False), chroms
 
     @staticmethod
     def train_segments(Gap, Gap_fitered, DI_sub, width, Gap_desity_t):
@@ -326,3 +359,37 @@ class TADCalling:
         self.BoundaryFilter()
         self.BoundaryToDomain()
         return self.Domain_dict
+
+
+class _LazyMatrices(dict):
+    """{chrom: dense matrix} fetched from the cooler on first access (only
+    Plot_TAD reads Matrix_Dict after Data_preprocess, StructureFind.py:1354)."""
+
+    def __init__(self, uri, chroms, balance):
+        super().__init__()
+        self._uri, self._order, self._bal = uri, list(chroms), balance
+
+    def __getitem__(self, chro):
+        if not dict.__contains__(self, chro):
+            if chro not in self._order:
+                raise KeyError(chro)
+            from .coolio import Cooler
+            with Cooler(self._uri) as c:
+                M = c.matrix(balance=self._bal).fetch(chro)
+            dict.__setitem__(self, chro, np.nan_to_num(M) if self._bal else M)
+        return dict.__getitem__(self, chro)
+
+    def keys(self):
+        return list(self._order)
+
+    def __iter__(self):
+        return iter(self._order)
+
+    def __len__(self):
+        return len(self._order)
+
+    def __contains__(self, chro):
+        return chro in self._order
+
+    def items(self):
+        return [(k, self[k]) for k in self._order]

@@ -315,6 +315,21 @@ int hh_dense_symvc(const void* X, int32_t dtype, int64_t N, const double* alpha,
  * int64 N x N inputs, float64 N x N outputs (Nor_MM, Nor_PM), gap masks
  * (gap_m[i] = 1 for i in Gap_M).  The gap / alpha glue runs on the host with
  * np.percentile ('linear') semantics; each matrix crosses PCIe once. */
+/* Dense N x N int64 (device `out`, zeroed first) from cells (row, col, count)
+ * whose ids are shifted by `offset`: out[r][c] = count, and out[c][r] too for
+ * an upper-triangle table (symmetric = 1).  The reference's dense matrices
+ * from its per-line loops (matrixBuilding.py:554, :567-570, :1290-1301), built
+ * on the device from the binner's tables so only the cells cross PCIe.
+ * Cells must be unique; out-of-range ids (or bin1 > bin2 when symmetric)
+ * are an error.  on_device = 1: row / col / count are device pointers. */
+int hh_dense_from_cells(const int64_t* row, const int64_t* col, const int64_t* count, int64_t nnz, int64_t N,
+                        int64_t offset, int32_t symmetric, int32_t on_device, int64_t* out, void* stream);
+/* Upper-triangle nonzeros of a dense fp64 N x N device matrix in cooler
+ * order, the np.triu(M).nonzero() table NPZ2Cooler writes for the corrected
+ * matrices (matrixBuilding.py:1613, :1628-1633): hh_dense_upper_count, then
+ * hh_dense_upper_write into caller-sized device buffers. */
+int hh_dense_upper_count(const double* X, int64_t N, int64_t* nnz, void* stream);
+int hh_dense_upper_write(const double* X, int64_t N, int32_t* bin1, int32_t* bin2, double* value, void* stream);
 int hh_twostep(const int64_t* TM, const int64_t* MM, const int64_t* PM, int64_t N, double* nor_mm, double* nor_pm,
                uint8_t* gap_m, uint8_t* gap_p, int32_t on_device, void* stream);
 

@@ -1,0 +1,110 @@
+"""The file-driven drivers on cooler pixels (no dense N x N):
+
+* ``StructureFind(cooler_fil, Res).Data_preprocess()`` (StructureFind.py:842-915)
+  runs the gap / DI scans on bands built on the GPU from the pixel table and
+  ``bins/weight`` -- bitwise the in-memory path on the dense matrices the
+  reference fetches (balanced + nan_to_num for traditional data, raw for
+  haplotype data);
+* ``StructureFind(cooler_fil, Res).CallPeaks(outfil, Allelic)`` (:1954-2060)
+  reads raw, balanced and weight from the cooler itself as pixel bands --
+  the same output file as ``loops.call_peaks`` on the dense fetches."""
+import numpy as np
+import pytest
+
+from hichap_master_amd import coolio
+
+pytestmark = pytest.mark.gpu
+
+
+def _chrom_pixels(rng, N, depth, loops=True):
+    i = np.arange(N)
+    d = np.abs(i[:, None] - i[None, :])
+    lam = depth * (d + 1.0) ** -1.05 * rng.lognormal(0, 0.2, N)[:, None]
+    lam = np.triu(lam) + np.triu(lam, 1).T
+    if loops:
+        for _ in range(N // 25):
+            a = int(rng.integers(5, N - 80))
+            b = a + int(rng.integers(6, 60))
+            lam[a - 1:a + 2, b - 1:b + 2] *= 4.0
+    # TAD-like blocks so the DI has structure
+    for s in range(0, N, 40):
+        lam[s:s + 40, s:s + 40] *= 2.0
+    H = np.triu(rng.poisson(np.triu(lam)))
+    gaps = rng.choice(N, size=max(N // 80, 1), replace=False)
+    H[gaps, :] = 0
+    H[:, gaps] = 0
+    r, c = np.nonzero(H)
+    return r, c, H[r, c].astype(np.int32), np.sort(gaps)
+
+
+def _cooler(tmp_path, res, names, sizes, seed=3, depth=40.0):
+    rng = np.random.default_rng(seed)
+    chromsizes = [(nm, N * res - res // 2) for nm, N in zip(names, sizes)]  # last bin partial
+    b1, b2, cnt, gaps, off = [], [], [], {}, 0
+    for nm, N in zip(names, sizes):
+        r, c, v, g = _chrom_pixels(rng, N, depth)
+        b1.append(r + off)
+        b2.append(c + off)
+        cnt.append(v)
+        gaps[nm] = g
+        off += N
+    path = str(tmp_path / "sample.cool")
+    coolio.create_cooler(path, {res: (chromsizes, np.concatenate(b1), np.concatenate(b2), np.concatenate(cnt))})
+    uri = f"{path}::{res}"
+    coolio.balance_cooler(uri, ignore_diags=1, cis_only=True)
+    return path, uri, gaps
+
+
+@pytest.mark.parametrize("allelic", [False, "Maternal"])
+def test_data_preprocess_from_pixels_equals_dense(tmp_path, allelic):
+    from hichap_master_amd.StructureFind import StructureFind
+    res = 40000
+    names = ["chr1", "chr2"] if allelic is False else ["M1", "P1", "M2"]
+    sizes = [700, 450] if allelic is False else [600, 600, 380]
+    path, uri, _ = _cooler(tmp_path, res, names, sizes)
+    a = StructureFind(path, res, Allelic=allelic)
+    a.TAD_parameter_init(200000, 4000000, 3, 600000, "ttest")
+    a.Data_preprocess()  # from the cooler: pixel bands, no dense matrix
+    b = StructureFind(None, res, Allelic=allelic)
+    b.cooler_fil = uri
+    b.TAD_parameter_init(200000, 4000000, 3, 600000, "ttest")
+    b.Allelic = allelic
+    chroms, dense = b._chroms_and_matrices(True)  # what the reference fetches (:853-865)
+    b.Data_preprocess(dense)
+    assert a.chroms == chroms == list(b.DI_dict)
+    for ch in chroms:
+        np.testing.assert_array_equal(a.Gap_all[ch], b.Gap_all[ch])
+        np.testing.assert_array_equal(a.DI_dict[ch], b.DI_dict[ch])
+        assert list(a.DI_all_train[ch]) == list(b.DI_all_train[ch])
+        for k in a.DI_all_train[ch]:
+            np.testing.assert_array_equal(a.DI_all_train[ch][k], b.DI_all_train[ch][k])
+        np.testing.assert_array_equal(a.Matrix_Dict[ch], dense[ch])  # the lazy plotting view
+
+
+def _read_calls(p):
+    with open(p) as f:
+        return f.read()
+
+
+@pytest.mark.parametrize("allelic", [False, "Maternal"])
+def test_callpeaks_from_cooler_equals_dense(tmp_path, allelic):
+    from hichap_master_amd import loops
+    from hichap_master_amd.StructureFind import StructureFind
+    res = 20000
+    names = ["chr1", "chr2"] if allelic is False else ["M1", "P1", "M2"]
+    sizes = [700, 500] if allelic is False else [600, 600, 400]
+    path, uri, gaps = _cooler(tmp_path, res, names, sizes, seed=9)
+    sf = StructureFind(path, res, Allelic=allelic, GapFile={str(res): gaps} if allelic else None)
+    out_pix = str(tmp_path / "pix.loops")
+    res_pix = sf.CallPeaks(out_pix, Allelic=allelic)
+    # the dense form: the matrices the reference fetches (:2006-2015)
+    with coolio.Cooler(uri) as c:
+        chroms = list(c.chromnames) if allelic is False else [x for x in c.chromnames if x.startswith("M")]
+        mats = {ch: (c.matrix(balance=False).fetch(ch), c.bins().fetch(ch)["weight"].to_numpy()) for ch in chroms}
+    out_dense = str(tmp_path / "dense.loops")
+    res_dense = loops.call_peaks(mats, res, out_dense, allelic=allelic is not False,
+                                 gaps=gaps if allelic else None)
+    assert _read_calls(out_pix) == _read_calls(out_dense)
+    assert sum(len(D) for D, _ in res_pix.values()) > 0
+    for ch in chroms:
+        assert sorted(res_pix[ch][0]) == sorted(res_dense[ch][0])

@@ -133,3 +133,87 @@ def test_default_wholeres_matches_dense(mb):
     ref = hichap_ref.genome_wide_correction(bins, hap, T, H)
     np.testing.assert_allclose(v, ref[b1, b2], rtol=1e-11)
     assert b1.size == np.count_nonzero(np.triu(ref))
+
+
+def _gw_10kb(t_target, h_target):
+    """The bench's 10 kb diploid layout (hg19, 2n = 607 282 bins) with
+    synthetic T (upper table) and imputed H (ordered cells) in HBM
+    (bench.py --config gw at a chosen depth)."""
+    from hichap_master_amd import ice, synth
+    names = synth.HG19_ORDER
+    nb = synth.genome_bins(10000)
+    n = int(np.sum(nb))
+    At, tdt = synth.calibrate(nb, t_target, 0.2)
+    Ah, tdh = synth.calibrate(nb + nb, h_target / 2.0, 0.2)
+    T = ice.SynthPixels(nb, ordered=False, A=At, trans_density=tdt, comp_block=200, ignore_diags=0, seed=20201021)
+    H = ice.SynthPixels(nb + nb, ordered=True, A=Ah, trans_density=tdh, comp_block=200, ignore_diags=0,
+                        seed=20201022)
+    off = np.concatenate([[0], np.cumsum(nb)])
+    bins = {c: (int(off[k]), int(off[k + 1]) - 1) for k, c in enumerate(names)}
+    hap = {}
+    for c in names:
+        hap["M" + c] = bins[c]
+        hap["P" + c] = (n + bins[c][0], n + bins[c][1])
+    return bins, hap, T, H, 2 * n
+
+
+def _host(a):
+    import ctypes as C
+    import torch
+    from hichap_master_amd._lib import call
+    t = torch.empty(a.numel(), dtype=torch.int32, device="cuda")
+    if a.numel():
+        call("hh_device_copy", C.c_void_p(t.data_ptr()), C.c_void_p(a.data_ptr()), 4 * a.numel(), None)
+    call("hh_synchronize", None)
+    return t.cpu().numpy()
+
+
+def test_10kb_diploid_layout_matches_sparse_oracle(mb):
+    """a4 at its real layout (10 kb diploid, 607 282 bins: every chromosome
+    block, the 2n-bin M / P halves, Sort_Chromosomes order) at reduced depth
+    (~2e8 T pixels + ~2e8 H cells): the GPU's corrected upper table equals
+    the pixel-table oracle (same cells, values to 1e-11)."""
+    bins, hap, T, H, N2 = _gw_10kb(2e8, 2e8)
+    try:
+        assert T.nnz > 1e8 and H.nnz > 1e8
+        b1, b2, v = (x.cpu().numpy() for x in
+                     mb.GenomeWideMatrixCorrectionSparse(bins, hap, (T.bin1, T.bin2, T.count),
+                                                         (H.bin1, H.bin2, H.count), device_result=True))
+        tp = tuple(_host(x) for x in (T.bin1, T.bin2, T.count))
+        hc = tuple(_host(x) for x in (H.bin1, H.bin2, H.count))
+    finally:
+        T.close()
+        H.close()
+    r1, r2, rv = hichap_ref.genome_wide_correction_sparse(bins, hap, tp, hc)
+    np.testing.assert_array_equal(b1, r1)
+    np.testing.assert_array_equal(b2, r2)
+    np.testing.assert_allclose(v, rv, rtol=1e-11, atol=0)
+
+
+def test_bench_size_invariants(mb):
+    """bench.py --config gw's size (1.5e9 T pixels + 1.5e9 H cells): the
+    corrected table is sorted and unique upper-triangle (cooler order), and
+    the mean rescale's invariant holds, sum(Nor) over the full symmetric
+    matrix == sum(H) (matrixBuilding.py:897-899), to 1e-9."""
+    import torch
+    bins, hap, T, H, N2 = _gw_10kb(1.5e9, 1.5e9)
+    try:
+        b1, b2, v = mb.GenomeWideMatrixCorrectionSparse(bins, hap, (T.bin1, T.bin2, T.count),
+                                                        (H.bin1, H.bin2, H.count), device_result=True)
+        import ctypes as C
+        from hichap_master_amd._lib import call
+        hcnt = torch.empty(H.count.numel(), dtype=torch.int32, device="cuda")
+        call("hh_device_copy", C.c_void_p(hcnt.data_ptr()), C.c_void_p(H.count.data_ptr()), 4 * H.count.numel(), None)
+        call("hh_synchronize", None)
+        hsum = float(hcnt.to(torch.int64).sum().item())
+        del hcnt
+    finally:
+        T.close()
+        H.close()
+    assert b1.numel() > 1e9
+    assert bool((b1 <= b2).all())
+    key = b1.to(torch.int64) * N2 + b2.to(torch.int64)
+    assert bool((key[1:] > key[:-1]).all())
+    del key
+    tot = float((torch.where(b1 == b2, 1.0, 2.0).to(torch.float64) * v).sum().item())
+    assert abs(tot - hsum) <= 1e-9 * hsum, (tot, hsum)

@@ -69,3 +69,59 @@ def test_intra_chrom_dict_api(mb):
     ref = hichap_ref.two_step_correction(tra["X"], hap["MX"], hap["PX"])
     np.testing.assert_allclose(nor["PX"], ref[1], rtol=1e-11)
     np.testing.assert_array_equal(gaps["MX"], ref[2])
+
+
+@pytest.mark.parametrize("N,drop", [(6232, 120), (4813, 60)])
+def test_twostep_real_sizes_vs_oracle(mb, N, drop):
+    """TwoStepCorrection at HiCHap's own sizes: chr1 at the default localRes
+    40 kb (N = 249 250 621 // 40 000 + 1 = 6 232) and chr21 at 10 kb
+    (N = 48 129 895 // 10 000 + 1 = 4 813), against the oracle."""
+    rng = np.random.default_rng(N)
+    TM = synth.dense_chrom(N, rng, A=60.0)
+    MM, PM = synth.haplotype_pair(TM, rng, drop_rows=drop)
+    got = mb.TwoStepCorrection(TM, MM, PM)
+    ref = hichap_ref.two_step_correction(TM, MM, PM)
+    np.testing.assert_array_equal(got[2], ref[2])
+    np.testing.assert_array_equal(got[3], ref[3])
+    for a, b in zip(got[:2], ref[:2]):
+        np.testing.assert_allclose(a, b, rtol=1e-11, atol=0)
+    np.testing.assert_allclose(got[1].sum(), PM.sum(), rtol=1e-9)
+
+
+def test_twostep_from_cells_and_device(mb):
+    """The PCIe-free forms: dense matrices built on the GPU from the tables
+    (T upper pixels, MM / PM ordered cells, global ids) and corrected there,
+    returned as upper tables or device tensors -- bitwise the host-array
+    TwoStepCorrection (same kernels on the same matrices)."""
+    import torch
+    N, off = 1500, 1000
+    rng = np.random.default_rng(77)
+    TM = synth.dense_chrom(N, rng, A=60.0)
+    MM, PM = synth.haplotype_pair(TM, rng, drop_rows=30)
+    want = mb.TwoStepCorrection(TM, MM, PM)
+    i, j = np.nonzero(np.triu(TM))
+    tp = (i + off, j + off, TM[i, j])
+    cells = []
+    for X in (MM, PM):
+        r, c = np.nonzero(X)
+        cells.append((r + off, c + off, X[r, c]))
+    um, up, gm, gp = mb.TwoStepCorrectionPixels(N, tp, cells[0], cells[1], offset=off)
+    np.testing.assert_array_equal(gm, want[2])
+    np.testing.assert_array_equal(gp, want[3])
+    for (b1, b2, v), D in ((um, want[0]), (up, want[1])):
+        r, c = np.nonzero(np.triu(D))
+        np.testing.assert_array_equal(b1, r + off)
+        np.testing.assert_array_equal(b2, c + off)
+        np.testing.assert_array_equal(v, D[r, c])
+    dev = [torch.from_numpy(X).cuda() for X in (TM, MM, PM)]
+    nm, npm, gm2, gp2 = mb.TwoStepCorrection(*dev)
+    np.testing.assert_array_equal(nm.cpu().numpy(), want[0])
+    np.testing.assert_array_equal(npm.cpu().numpy(), want[1])
+    np.testing.assert_array_equal(gm2, want[2])
+    # device cells too
+    tcells = [torch.from_numpy(np.asarray(x, np.int64)).cuda() for x in tp]
+    D = mb.dense_from_cells_device(tcells, N, off, symmetric=True)
+    np.testing.assert_array_equal(D.cpu().numpy(), TM)
+    from hichap_master_amd._lib import HipLibraryError
+    with pytest.raises(HipLibraryError, match="outside"):
+        mb.dense_from_cells_device((np.array([off + N]), np.array([off]), np.array([1])), N, off)
