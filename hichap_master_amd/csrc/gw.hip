@@ -25,39 +25,52 @@
 // Every sum is a fixed-order reduction (integer ones exact): deterministic.
 #include <algorithm>
 #include <cmath>
+#include <memory>
 #include <numeric>
+#include <type_traits>
 
 #include "ice_internal.hpp"
 
 namespace hh {
 
-template <class Id, class Cnt>
+template <class Id, class Cnt, bool COPY>
 __global__ __launch_bounds__(256) void k_gw_check(const Id* __restrict__ r_in, const Id* __restrict__ c_in,
                                                   const Cnt* __restrict__ v_in, long long nnz, long long nb,
                                                   int upper, int32_t* __restrict__ R, int32_t* __restrict__ Cc,
-                                                  uint32_t* __restrict__ V, unsigned long long* __restrict__ errs) {
+                                                  uint32_t* __restrict__ V, unsigned long long* __restrict__ errs,
+                                                  unsigned* __restrict__ vmax) {
     const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nnz) return;
-    const long long a = (long long)r_in[i], b = (long long)c_in[i];
-    const double v = (double)v_in[i];
-    int code = 0;
-    if (a < 0 || b < 0 || a >= nb || b >= nb) code = 1;
-    else if (upper && a > b) code = 2;
-    else if (i > 0) {
-        const long long pa = (long long)r_in[i - 1], pb = (long long)c_in[i - 1];
-        if (pa > a || (pa == a && pb > b)) code = 3;
-        else if (pa == a && pb == b) code = 4;
+    unsigned mx = 0u;
+    if (i < nnz) {
+        const long long a = (long long)r_in[i], b = (long long)c_in[i];
+        const double v = (double)v_in[i];
+        int code = 0;
+        if (a < 0 || b < 0 || a >= nb || b >= nb) code = 1;
+        else if (upper && a > b) code = 2;
+        else if (i > 0) {
+            const long long pa = (long long)r_in[i - 1], pb = (long long)c_in[i - 1];
+            if (pa > a || (pa == a && pb > b)) code = 3;
+            else if (pa == a && pb == b) code = 4;
+        }
+        if (!code && (!(v >= 0.0) || v != floor(v) || v >= 4294967296.0)) code = 5;
+        if (code) {
+            atomicMin(errs + code - 1, (unsigned long long)i);
+            if (COPY) {
+                R[i] = Cc[i] = 0;
+                V[i] = 0u;
+            }
+        } else {
+            mx = (unsigned)v;
+            if (COPY) {
+                R[i] = (int32_t)a;
+                Cc[i] = (int32_t)b;
+                V[i] = (uint32_t)v;
+            }
+        }
     }
-    if (!code && (!(v >= 0.0) || v != floor(v) || v >= 4294967296.0)) code = 5;
-    if (code) {
-        atomicMin(errs + code - 1, (unsigned long long)i);
-        R[i] = Cc[i] = 0;
-        V[i] = 0u;
-        return;
-    }
-    R[i] = (int32_t)a;
-    Cc[i] = (int32_t)b;
-    V[i] = (uint32_t)v;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mx = max(mx, (unsigned)__shfl_xor((int)mx, o, 64));
+    if ((threadIdx.x & 63) == 0 && mx) atomicMax(vmax, mx);
 }
 
 // ptr[r] = first i with A[i] >= r, r in [0, nr] (A sorted)
@@ -193,8 +206,13 @@ __global__ __launch_bounds__(256) void k_gw_hstats(const int32_t* __restrict__ r
 // orders only the column bits (stable: 3 radix passes instead of 7).
 constexpr int kColItems = 16;
 constexpr int kColChunk = 256 * kColItems;
+// FMT 1 (ids < 2^20, counts < 2^24): the key IS the packed cell, col << 44 |
+// row << 24 | count, and the sort orders its column bits (the cells arrive in
+// row order, the sort is stable): no index, no gather afterwards.  FMT 0:
+// col << ib | index, then k_gw_pack.
 template <int PASS>
 __global__ __launch_bounds__(256) void k_gw_colkeys(const int32_t* __restrict__ r, const int32_t* __restrict__ c,
+                                                    const uint32_t* __restrict__ v, int fmt,
                                                     long long nnz, int ib, unsigned long long* __restrict__ keys,
                                                     long long* __restrict__ cnt_or_base) {
     __shared__ unsigned wcnt[kColItems][4];
@@ -226,8 +244,20 @@ __global__ __launch_bounds__(256) void k_gw_colkeys(const int32_t* __restrict__ 
         if (!((mk[k] >> lane) & 1ull)) continue;
         const long long i = c0 + (long long)k * 256 + threadIdx.x;
         keys[base + wcnt[k][wave] + __popcll(mk[k] & ((1ull << lane) - 1ull))] =
-            ((unsigned long long)c[i] << ib) | (unsigned long long)i;
+            fmt ? ((unsigned long long)c[i] << 44) | ((unsigned long long)r[i] << 24) | (unsigned long long)v[i]
+                : ((unsigned long long)c[i] << ib) | (unsigned long long)i;
     }
+}
+
+// column-list entry -> (row, count): FMT 0 row | count << 32 (after
+// k_gw_pack), FMT 1 the packed sort key col << 44 | row << 24 | count
+template <int FMT>
+__device__ __forceinline__ int32_t lrv_row(unsigned long long x) {
+    return FMT ? (int32_t)((x >> 24) & 0xFFFFFull) : (int32_t)(uint32_t)x;
+}
+template <int FMT>
+__device__ __forceinline__ double lrv_val(unsigned long long x) {
+    return FMT ? (double)(uint32_t)(x & 0xFFFFFFull) : (double)(uint32_t)(x >> 32);
 }
 
 __device__ __forceinline__ long long lower_bound_i32(const int32_t* a, long long lo, long long hi, int32_t x) {
@@ -239,11 +269,12 @@ __device__ __forceinline__ long long lower_bound_i32(const int32_t* a, long long
     return lo;
 }
 // first position in [lo, hi) of the column list whose cell row >= x
+template <int FMT>
 __device__ __forceinline__ long long lower_bound_keyrow(const unsigned long long* lrv, long long lo, long long hi,
                                                         int32_t x) {
     while (lo < hi) {
         const long long mid = (lo + hi) >> 1;
-        if ((int32_t)(uint32_t)lrv[mid] < x) lo = mid + 1;
+        if (lrv_row<FMT>(lrv[mid]) < x) lo = mid + 1;
         else hi = mid;
     }
     return lo;
@@ -260,8 +291,6 @@ __global__ void k_gw_pack(unsigned long long* __restrict__ keys, long long n, un
     const long long k = (long long)(keys[q] & imask);
     keys[q] = (unsigned long long)(uint32_t)R[k] | ((unsigned long long)V[k] << 32);
 }
-__device__ __forceinline__ int32_t lrv_row(unsigned long long x) { return (int32_t)(uint32_t)x; }
-__device__ __forceinline__ double lrv_val(unsigned long long x) { return (double)(uint32_t)(x >> 32); }
 
 struct GwDev {
     const int32_t* R;
@@ -279,6 +308,7 @@ struct GwDev {
 // per row r (one wave): rowsum(S)_r and the off-diagonal column sum of S in
 // column r, in list order (fixed xor-tree per chunk): the symmetric marginal
 // of Y; u/l starts for the merge
+template <int FMT>
 __global__ __launch_bounds__(256) void k_gw_marg(GwDev g, double exponent, double* __restrict__ s_out) {
     const long long r = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     if (r >= g.N2) return;
@@ -298,7 +328,7 @@ __global__ __launch_bounds__(256) void k_gw_marg(GwDev g, double exponent, doubl
         double x = 0.0;
         if (q < c1) {
             const unsigned long long e = g.lrv[q];
-            x = lrv_val(e) / g.alpha[lrv_row(e)];
+            x = lrv_val<FMT>(e) / g.alpha[lrv_row<FMT>(e)];
         }
         acc2 += wave_sum(x);
     }
@@ -308,109 +338,137 @@ __global__ __launch_bounds__(256) void k_gw_marg(GwDev g, double exponent, doubl
         if (sv == 0.0) sv = 1.0;
         s_out[r] = sv;
         g.ustart[r] = lower_bound_i32(g.C, h0, h1, (int32_t)r);
-        g.lstart[r] = lower_bound_keyrow(g.lrv, c0, c1, (int32_t)(r + 1));
+        g.lstart[r] = lower_bound_keyrow<FMT>(g.lrv, c0, c1, (int32_t)(r + 1));
     }
 }
 
-// orphan flags over the column-sorted list: entry (i, r), i > r, whose
-// partner (r, i) is not a cell of H
-// (one wave per column r of the list)
-__global__ void k_gw_orphans(GwDev g, long long* __restrict__ flag) {
+// Row r of the corrected upper table, by a wave-level merge of two sorted
+// lists: A = H's cells (r, c >= r) (columns ascending) and B = the cells
+// (i, r), i > r, of column r's list (rows ascending; their transposes land
+// in row r).  The output row is the union by column: Y = S_rc + S_cr where
+// both exist (Trans2symmetryLowRes, :770-777), else the one present; C =
+// Y / (s_c s_r) (Correct_VC, :780-790).  Per window of 64 elements of each
+// list, lane l finds by merge path how many of the first l + 1 merged
+// elements come from A (ties: A first, so a B element directly follows its
+// A partner); 63 merged elements are consumed per window (64 when element
+// 62 and its partner 63 form a pair), a B element tied to the preceding A
+// element is absorbed.  PASS 0: per row the union's length and its share of
+// sum(C) over the full symmetric matrix (row order, fixed tree); PASS 1:
+// write (r, c, rf C) at the row's offset.  O(|A| + |B|) with coalesced
+// loads (was a binary search per element in three kernels plus two flag /
+// prefix arrays over every column-list entry).
+constexpr int kMergeInf = 0x7fffffff;
+template <int FMT, int PASS>
+__global__ __launch_bounds__(256) void k_gw_merge(GwDev g, const double* __restrict__ s, double rf,
+                                                  long long* __restrict__ len_or_off, double* __restrict__ rowc,
+                                                  int32_t* __restrict__ ob1, int32_t* __restrict__ ob2,
+                                                  double* __restrict__ ov) {
     const long long r = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     if (r >= g.N2) return;
     const int lane = threadIdx.x & 63;
-    const long long h0 = g.ustart[r], h1 = g.hptr[r + 1];
-    for (long long q = g.cptr[r] + lane; q < g.cptr[r + 1]; q += 64) {
-        const int32_t i = lrv_row(g.lrv[q]);
-        long long f = 0;
-        if (i > r) {
-            const long long p = lower_bound_i32(g.C, h0, h1, i);
-            f = (p < h1 && g.C[p] == i) ? 0 : 1;
+    long long ia = g.ustart[r];
+    const long long a1 = g.hptr[r + 1];
+    long long ib = g.lstart[r];
+    const long long b1 = g.cptr[r + 1];
+    const double ar = g.alpha[r], sr = s[r];
+    long long pos = PASS ? len_or_off[r] : 0;
+    double csum = 0.0;
+    while (ia < a1 || ib < b1) {
+        // windows (padded with +inf keys)
+        const bool ina = ia + lane < a1, inb = ib + lane < b1;
+        const int ka = ina ? g.C[ia + lane] : kMergeInf;
+        const double va = ina ? (double)g.V[ia + lane] / ar : 0.0;
+        int kb = kMergeInf;
+        double vb = 0.0;
+        if (inb) {
+            const unsigned long long e = g.lrv[ib + lane];
+            kb = lrv_row<FMT>(e);
+            vb = lrv_val<FMT>(e) / g.alpha[kb];
         }
-        flag[q] = f;
-    }
-}
-
-__global__ void k_gw_rowlen(GwDev g, const long long* __restrict__ oprefix, long long* __restrict__ len) {
-    const long long r = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= g.N2) return;
-    len[r] = (g.hptr[r + 1] - g.ustart[r]) + (oprefix[g.cptr[r + 1]] - oprefix[g.lstart[r]]);
-}
-
-// upper cells (r, c >= r) of H: Y = S_rc + S_cr (partner found in column r's list)
-__global__ void k_gw_write_upper(GwDev g, const long long* __restrict__ oprefix, const long long* __restrict__ row_off,
-                                 const double* __restrict__ s, int32_t* __restrict__ ob1, int32_t* __restrict__ ob2,
-                                 double* __restrict__ ov) {
-    const long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= g.hptr[g.N2]) return;
-    const int32_t r = g.R[k], c = g.C[k];
-    if (c < r) return;
-    double y = (double)g.V[k] / g.alpha[r];
-    long long before = 0;  // orphans of row r with column < c
-    if (c > r) {
-        const long long l0 = g.lstart[r], l1 = g.cptr[(long long)r + 1];
-        const long long p = lower_bound_keyrow(g.lrv, l0, l1, c);
-        if (p < l1) {
-            const unsigned long long e = g.lrv[p];
-            if (lrv_row(e) == c) y += lrv_val(e) / g.alpha[c];
+        // merge path: x = number of A elements among the first d = lane + 1
+        // merged ones; A[x - 1] <= B[d - x] (A wins ties)
+        const int d = lane + 1;
+        int lo = d > 64 ? d - 64 : 0, hi = d < 64 ? d : 64;
+        while (__any(lo < hi)) {
+            const int mid = (lo + hi) >> 1;
+            const int am = __shfl(ka, min(mid, 63), 64);
+            const int bm = __shfl(kb, min(max(d - 1 - mid, 0), 63), 64);
+            if (lo < hi) {
+                if (am <= bm) lo = mid + 1;  // A[mid] is among the first d
+                else hi = mid;
+            }
         }
-        before = oprefix[p] - oprefix[l0];
+        const int x = lo;                         // A elements in the first lane + 1
+        const int xp = lane ? __shfl_up(x, 1, 64) : 0;  // ... in the first lane
+        const bool fromA = x > xp;
+        const int src = fromA ? xp : lane - xp;   // index in that window
+        // every lane takes part in every shuffle (a lane reading from a lane
+        // outside the active mask of a divergent shuffle gets nothing)
+        const int srcl = min(src, 63);
+        const int key_a = __shfl(ka, srcl, 64), key_b = __shfl(kb, srcl, 64);
+        const double val_a = __shfl(va, srcl, 64), val_b = __shfl(vb, srcl, 64);
+        const int key = fromA ? key_a : key_b;
+        const double val = fromA ? val_a : val_b;
+        // the next merged element (tie partner?)
+        const int key_n = __shfl_down(key, 1, 64);
+        const bool fromA_n = __shfl_down(fromA ? 1 : 0, 1, 64) != 0;
+        const double val_n = __shfl_down(val, 1, 64);
+        const bool pair_next = lane < 63 && fromA && !fromA_n && key_n == key && key != kMergeInf;
+        const bool pair_prev = __shfl_up(pair_next ? 1 : 0, 1, 64) != 0 && lane > 0;
+        // consume 63 elements, or 64 when 62-63 is a pair
+        const int M = __shfl(pair_next ? 1 : 0, 62, 64) ? 64 : 63;
+        const bool live = lane < M && key != kMergeInf;
+        const bool emit = live && !pair_prev;
+        const double y = val + (pair_next ? val_n : 0.0);
+        const double cv = emit ? y / (s[emit ? key : 0] * sr) : 0.0;
+        const unsigned long long em = __ballot(emit);
+        if (PASS == 0) {
+            csum += (key == r ? 1.0 : 2.0) * cv;
+        } else if (emit) {
+            const long long q = pos + __popcll(em & ((1ull << lane) - 1ull));
+            ob1[q] = (int32_t)r;
+            ob2[q] = key;
+            ov[q] = rf * cv;
+        }
+        pos += __popcll(em);
+        const int xa = __shfl(x, M - 1, 64);  // A elements among the M consumed
+        ia += xa;
+        ib += M - xa;
     }
-    const long long pos = row_off[r] + (k - g.ustart[r]) + before;
-    ob1[pos] = r;
-    ob2[pos] = c;
-    ov[pos] = y / (s[c] * s[r]);  // Correct_VC: x / (s2[None, :] * s1[:, None])
+    if (PASS == 0) {
+        csum = wave_sum(csum);
+        if (lane == 0) {
+            len_or_off[r] = pos;
+            rowc[r] = csum;
+        }
+    }
 }
 
-// lower cells (i, r), i > r, without a partner: Y_ri = S_ir alone
-// (one wave per column r of the list)
-__global__ void k_gw_write_orphans(GwDev g, const long long* __restrict__ flag, const long long* __restrict__ oprefix,
-                                   const long long* __restrict__ row_off, const double* __restrict__ s,
-                                   int32_t* __restrict__ ob1, int32_t* __restrict__ ob2, double* __restrict__ ov) {
-    const long long r = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    if (r >= g.N2) return;
-    const int lane = threadIdx.x & 63;
-    const long long u0 = g.ustart[r], u1 = g.hptr[r + 1];
-    const long long obase = row_off[r] - oprefix[g.lstart[r]];
-    for (long long q = g.cptr[r] + lane; q < g.cptr[r + 1]; q += 64) {
-        if (!flag[q]) continue;
-        const unsigned long long e = g.lrv[q];
-        const int32_t i = lrv_row(e);
-        const long long before = lower_bound_i32(g.C, u0, u1, i) - u0;  // upper cells of row r with col < i
-        const long long pos = obase + oprefix[q] + before;
-        const double y = lrv_val(e) / g.alpha[i];
-        ob1[pos] = (int32_t)r;
-        ob2[pos] = i;
-        ov[pos] = y / (s[i] * s[r]);
-    }
-}
-
-// sum of the full symmetric C from its upper table: per block, fixed order
-__global__ __launch_bounds__(256) void k_gw_csum(const int32_t* __restrict__ b1, const int32_t* __restrict__ b2,
-                                                 const double* __restrict__ v, long long n, long long per,
-                                                 double* __restrict__ part) {
+// sum of per-row values in blocks of `per` rows (fixed tree per block)
+__global__ __launch_bounds__(256) void k_gw_rowsum_blocks(const double* __restrict__ v, long long n, long long per,
+                                                          double* __restrict__ part) {
     __shared__ double sh[16];
     const long long lo = (long long)blockIdx.x * per, hi = std::min<long long>(n, lo + per);
     double acc = 0.0;
-    for (long long q = lo + threadIdx.x; q < hi; q += 256) acc += (b1[q] == b2[q] ? 1.0 : 2.0) * v[q];
+    for (long long q = lo + threadIdx.x; q < hi; q += 256) acc += v[q];
     acc = block_sum(acc, sh);
     if (threadIdx.x == 0) part[blockIdx.x] = acc;
-}
-
-__global__ void k_gw_scale(double* __restrict__ v, long long n, double rf) {
-    const long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (q < n) v[q] = rf * v[q];
 }
 
 }  // namespace hh
 
 using namespace hh;
 
+namespace { struct GwScratch; }
 struct hh_gw {
     int device = 0;
+    std::shared_ptr<GwScratch> scratch;  // between hh_gw_correct_count and _write
     int64_t n = 0, N2 = 0, t_nnz = 0, h_nnz = 0, n_keys = 0;
-    DBuf<int32_t> tA, tB, R, C;
+    DBuf<int32_t> tA, tB, R, C;  // converted copies (host / int64 tables); device int32 tables are used in place
     DBuf<uint32_t> tV, V;
+    const int32_t *tAp = nullptr, *tBp = nullptr, *Rp = nullptr, *Cp = nullptr;
+    const uint32_t *tVp = nullptr, *Vp = nullptr;
+    int fmt = 0;  // column-list entry format (k_gw_colkeys)
     DBuf<long long> hptr, cptr;
     DBuf<unsigned long long> keys;  // column-sorted cells, (row, count) packed after hh_gw_create
     int ib = 1;
@@ -427,26 +485,36 @@ namespace {
 const char* kErrWhat[5] = {"bin id out of range", "bin1 > bin2 in the traditional table (not upper triangle)",
                            "cells not sorted by (row, col)", "duplicate cell", "counts must be non-negative integers < 2^32"};
 
-template <class Id, class Cnt>
-void gw_check(const Id* r, const Id* c, const Cnt* v, int64_t nnz, int64_t nb, int upper, DBuf<int32_t>& R,
-              DBuf<int32_t>& Cc, DBuf<uint32_t>& V, const char* what, hipStream_t s) {
-    R.alloc(std::max<int64_t>(nnz, 1));
-    Cc.alloc(std::max<int64_t>(nnz, 1));
-    V.alloc(std::max<int64_t>(nnz, 1));
+// Validate a table (range, order, uniqueness, counts); COPY: convert it into
+// int32 / uint32 device arrays (host or int64 tables), else it is used in
+// place (int32 device tables).  Returns the largest count.
+template <class Id, class Cnt, bool COPY>
+unsigned gw_check(const Id* r, const Id* c, const Cnt* v, int64_t nnz, int64_t nb, int upper, DBuf<int32_t>& R,
+                  DBuf<int32_t>& Cc, DBuf<uint32_t>& V, const char* what, hipStream_t s) {
+    if (COPY) {
+        R.alloc(std::max<int64_t>(nnz, 1));
+        Cc.alloc(std::max<int64_t>(nnz, 1));
+        V.alloc(std::max<int64_t>(nnz, 1));
+    }
     DBuf<unsigned long long> err(5);
+    DBuf<unsigned> vmax(1);
+    vmax.zero(s);
     HIP_CHECK(hipMemsetAsync(err.p, 0xff, 5 * sizeof(unsigned long long), s));
     if (nnz > 0)
-        hipLaunchKernelGGL((k_gw_check<Id, Cnt>), dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s, r, c, v,
-                           (long long)nnz, (long long)nb, upper, R.p, Cc.p, V.p, err.p);
+        hipLaunchKernelGGL((k_gw_check<Id, Cnt, COPY>), dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s, r, c, v,
+                           (long long)nnz, (long long)nb, upper, R.p, Cc.p, V.p, err.p, vmax.p);
     HIP_CHECK(hipGetLastError());
     unsigned long long he[5];
+    unsigned mx = 0;
     err.download(he, 5, s);
+    vmax.download(&mx, 1, s);
     HIP_CHECK(hipStreamSynchronize(s));
     int code = -1;
     unsigned long long at = ~0ull;
     for (int q = 0; q < 5; ++q)
         if (he[q] < at) { at = he[q]; code = q; }
     if (code >= 0) HH_THROW(HH_ERR_ARG, std::string(what) + ": " + kErrWhat[code] + " at entry " + std::to_string(at));
+    return mx;
 }
 
 template <class Id, class Cnt>
@@ -469,8 +537,17 @@ void gw_create(hh_gw& G, const Id* t1, const Id* t2, const Cnt* tv, int64_t t_nn
             block_of[n + b] = n_chroms + c;  // P copy
         }
     }
-    gw_check(t1, t2, tv, t_nnz, n, 1, G.tA, G.tB, G.tV, "traditional table", s);
-    gw_check(hr, hc, hv, h_nnz, 2 * n, 0, G.R, G.C, G.V, "haplotype cells", s);
+    constexpr bool COPY = !(std::is_same<Id, int32_t>::value && std::is_same<Cnt, int32_t>::value);
+    gw_check<Id, Cnt, COPY>(t1, t2, tv, t_nnz, n, 1, G.tA, G.tB, G.tV, "traditional table", s);
+    const unsigned hmax = gw_check<Id, Cnt, COPY>(hr, hc, hv, h_nnz, 2 * n, 0, G.R, G.C, G.V, "haplotype cells", s);
+    if (COPY) {
+        G.tAp = G.tA.p, G.tBp = G.tB.p, G.tVp = G.tV.p, G.Rp = G.R.p, G.Cp = G.C.p, G.Vp = G.V.p;
+    } else {  // validated int32 device tables, read in place (counts >= 0: as uint32)
+        G.tAp = reinterpret_cast<const int32_t*>(t1), G.tBp = reinterpret_cast<const int32_t*>(t2);
+        G.tVp = reinterpret_cast<const uint32_t*>(tv);
+        G.Rp = reinterpret_cast<const int32_t*>(hr), G.Cp = reinterpret_cast<const int32_t*>(hc);
+        G.Vp = reinterpret_cast<const uint32_t*>(hv);
+    }
     DBuf<int32_t> dch = to_device(chrom_of, s), dblk = to_device(block_of, s);
     DBuf<unsigned long long> trs(n), tnz(n), hbs(2 * n), htot(1);
     trs.zero(s);
@@ -484,14 +561,14 @@ void gw_create(hh_gw& G, const Id* t1, const Id* t2, const Cnt* tv, int64_t t_nn
     ttot.zero(s);
     if (t_nnz > 0) {
         if (tpack)
-            hipLaunchKernelGGL(k_gw_tstats<true>, sgrid(t_nnz), dim3(256), 0, s, G.tA.p, G.tB.p, G.tV.p,
+            hipLaunchKernelGGL(k_gw_tstats<true>, sgrid(t_nnz), dim3(256), 0, s, G.tAp, G.tBp, G.tVp,
                                (long long)t_nnz, dch.p, trs.p, tnz.p, tpk.p, ttot.p);
         else
-            hipLaunchKernelGGL(k_gw_tstats<false>, sgrid(t_nnz), dim3(256), 0, s, G.tA.p, G.tB.p, G.tV.p,
+            hipLaunchKernelGGL(k_gw_tstats<false>, sgrid(t_nnz), dim3(256), 0, s, G.tAp, G.tBp, G.tVp,
                                (long long)t_nnz, dch.p, trs.p, tnz.p, nullptr, nullptr);
     }
     if (h_nnz > 0)
-        hipLaunchKernelGGL(k_gw_hstats, sgrid(h_nnz), dim3(256), 0, s, G.R.p, G.C.p, G.V.p, (long long)h_nnz, dblk.p,
+        hipLaunchKernelGGL(k_gw_hstats, sgrid(h_nnz), dim3(256), 0, s, G.Rp, G.Cp, G.Vp, (long long)h_nnz, dblk.p,
                            hbs.p, htot.p);
     HIP_CHECK(hipGetLastError());
     G.t_rowsum.resize(n);
@@ -515,7 +592,7 @@ void gw_create(hh_gw& G, const Id* t1, const Id* t2, const Cnt* tv, int64_t t_nn
         } else {  // counts too large for the packed field: the two-atomic pass
             trs.zero(s);
             tnz.zero(s);
-            hipLaunchKernelGGL(k_gw_tstats<false>, sgrid(t_nnz), dim3(256), 0, s, G.tA.p, G.tB.p, G.tV.p,
+            hipLaunchKernelGGL(k_gw_tstats<false>, sgrid(t_nnz), dim3(256), 0, s, G.tAp, G.tBp, G.tVp,
                                (long long)t_nnz, dch.p, trs.p, tnz.p, nullptr, nullptr);
             HIP_CHECK(hipGetLastError());
             trs.download(G.t_rowsum.data(), n, s);
@@ -526,14 +603,20 @@ void gw_create(hh_gw& G, const Id* t1, const Id* t2, const Cnt* tv, int64_t t_nn
     // H row pointers and column lists
     G.hptr.alloc(2 * n + 1);
     if (h_nnz > 0)
-        hipLaunchKernelGGL(k_px_rowptr_gw, dim3((unsigned)((h_nnz + 1 + 255) / 256)), dim3(256), 0, s, G.R.p,
+        hipLaunchKernelGGL(k_px_rowptr_gw, dim3((unsigned)((h_nnz + 1 + 255) / 256)), dim3(256), 0, s, G.Rp,
                            (long long)h_nnz, (long long)(2 * n), G.hptr.p);
     else
         HIP_CHECK(hipMemsetAsync(G.hptr.p, 0, (2 * n + 1) * sizeof(long long), s));
-    G.ib = 1;
-    while (G.ib < 63 && ((int64_t)1 << G.ib) < std::max<int64_t>(h_nnz, 2)) ++G.ib;
     int cbits = 1;
     while (cbits < 40 && ((int64_t)1 << cbits) < 2 * n) ++cbits;
+    // packed keys (col | row | count) when ids fit 20 bits and counts 24
+    G.fmt = (2 * n <= (1LL << 20) && hmax < (1u << 24)) ? 1 : 0;
+    if (G.fmt) {
+        G.ib = 44;
+    } else {
+        G.ib = 1;
+        while (G.ib < 63 && ((int64_t)1 << G.ib) < std::max<int64_t>(h_nnz, 2)) ++G.ib;
+    }
     HH_REQUIRE(G.ib + cbits <= 64, "haplotype matrix too large for 64-bit column keys");
     G.keys.alloc(std::max<int64_t>(h_nnz, 1));
     unsigned long long hn = 0;
@@ -542,11 +625,11 @@ void gw_create(hh_gw& G, const Id* t1, const Id* t2, const Cnt* tv, int64_t t_nn
         DBuf<long long> bcnt(nblk + 1), bbase(nblk + 1);
         DBuf<unsigned long long> ntot(1);
         HIP_CHECK(hipMemsetAsync(bcnt.p + nblk, 0, sizeof(long long), s));
-        hipLaunchKernelGGL(k_gw_colkeys<0>, dim3((unsigned)nblk), dim3(256), 0, s, G.R.p, G.C.p, (long long)h_nnz,
-                           G.ib, G.keys.p, bcnt.p);
+        hipLaunchKernelGGL(k_gw_colkeys<0>, dim3((unsigned)nblk), dim3(256), 0, s, G.Rp, G.Cp, G.Vp, G.fmt,
+                           (long long)h_nnz, G.ib, G.keys.p, bcnt.p);
         dev_excl_scan_i64(bcnt.p, bbase.p, nblk + 1, ntot.p, s);
-        hipLaunchKernelGGL(k_gw_colkeys<1>, dim3((unsigned)nblk), dim3(256), 0, s, G.R.p, G.C.p, (long long)h_nnz,
-                           G.ib, G.keys.p, bbase.p);
+        hipLaunchKernelGGL(k_gw_colkeys<1>, dim3((unsigned)nblk), dim3(256), 0, s, G.Rp, G.Cp, G.Vp, G.fmt,
+                           (long long)h_nnz, G.ib, G.keys.p, bbase.p);
         HIP_CHECK(hipGetLastError());
         ntot.download(&hn, 1, s);
         HIP_CHECK(hipStreamSynchronize(s));
@@ -556,9 +639,9 @@ void gw_create(hh_gw& G, const Id* t1, const Id* t2, const Cnt* tv, int64_t t_nn
     G.cptr.alloc(2 * n + 1);
     hipLaunchKernelGGL(k_px_keyptr_gw, dim3((unsigned)((hn + 1 + 255) / 256)), dim3(256), 0, s, G.keys.p,
                        (long long)hn, G.ib, (long long)(2 * n), G.cptr.p);
-    if (hn)
+    if (hn && !G.fmt)
         hipLaunchKernelGGL(k_gw_pack, dim3((unsigned)((hn + 255) / 256)), dim3(256), 0, s, G.keys.p, (long long)hn,
-                           G.ib >= 64 ? ~0ull : ((1ull << G.ib) - 1ull), G.R.p, G.V.p);
+                           G.ib >= 64 ? ~0ull : ((1ull << G.ib) - 1ull), G.Rp, G.Vp);
     HIP_CHECK(hipGetLastError());
     HIP_CHECK(hipStreamSynchronize(s));
 }
@@ -621,60 +704,111 @@ int hh_gw_stats(const hh_gw* g, int64_t* t_rowsum, int64_t* t_nnz_row, int64_t* 
     });
 }
 
+}  // extern "C"
+
+namespace {
+
+// marginals, VC factors, merge count pass and sum(C): everything up to the
+// write; returns the output size, leaves s / offsets / rf in the scratch
+struct GwScratch {
+    DBuf<double> dal, sv, rowc;
+    DBuf<long long> ustart, lstart, len, roff;
+    double rf = 0.0;
+    long long total = 0;
+};
+
+template <int FMT>
+void gw_prepare(hh_gw* g, const double* alpha, double exponent, GwScratch& W, hipStream_t s) {
+    const int64_t N2 = g->N2;
+    W.dal.alloc(N2);
+    W.sv.alloc(N2);
+    W.rowc.alloc(N2);
+    W.dal.upload(alpha, N2, s);
+    W.ustart.alloc(N2);
+    W.lstart.alloc(N2);
+    W.len.alloc(N2 + 1);
+    W.roff.alloc(N2 + 1);
+    GwDev d{g->Rp, g->Cp, g->Vp, g->hptr.p, g->keys.p, g->cptr.p, (long long)N2, W.dal.p, W.ustart.p, W.lstart.p};
+    const unsigned wg = (unsigned)((N2 * 64 + 255) / 256);
+    hipLaunchKernelGGL(k_gw_marg<FMT>, dim3(wg), dim3(256), 0, s, d, exponent, W.sv.p);
+    hipLaunchKernelGGL((k_gw_merge<FMT, 0>), dim3(wg), dim3(256), 0, s, d, W.sv.p, 0.0, W.len.p, W.rowc.p,
+                       (int32_t*)nullptr, (int32_t*)nullptr, (double*)nullptr);
+    HIP_CHECK(hipMemsetAsync(W.len.p + N2, 0, sizeof(long long), s));
+    DBuf<unsigned long long> tot(1);
+    dev_excl_scan_i64(W.len.p, W.roff.p, N2 + 1, tot.p, s);
+    // sum(C) over the full matrix: row shares in row order, fixed tree
+    const long long per = 1 << 14;
+    const long long nbk = std::max<long long>(1, (N2 + per - 1) / per);
+    DBuf<double> part(nbk);
+    hipLaunchKernelGGL(k_gw_rowsum_blocks, dim3((unsigned)nbk), dim3(256), 0, s, W.rowc.p, (long long)N2, per, part.p);
+    HIP_CHECK(hipGetLastError());
+    std::vector<double> hp(nbk);
+    unsigned long long m = 0;
+    part.download(hp.data(), nbk, s);
+    tot.download(&m, 1, s);
+    HIP_CHECK(hipStreamSynchronize(s));
+    double csum = 0.0;
+    for (double x : hp) csum += x;
+    const double NN = (double)N2 * (double)N2;
+    W.rf = ((double)g->h_total / NN) / (csum / NN);  // R_F = H.mean() / C.mean() (:897-899)
+    W.total = (long long)m;
+}
+
+template <int FMT>
+void gw_write(hh_gw* g, GwScratch& W, int32_t* b1, int32_t* b2, double* v, hipStream_t s) {
+    const int64_t N2 = g->N2;
+    GwDev d{g->Rp, g->Cp, g->Vp, g->hptr.p, g->keys.p, g->cptr.p, (long long)N2, W.dal.p, W.ustart.p, W.lstart.p};
+    const unsigned wg = (unsigned)((N2 * 64 + 255) / 256);
+    if (W.total > 0)
+        hipLaunchKernelGGL((k_gw_merge<FMT, 1>), dim3(wg), dim3(256), 0, s, d, W.sv.p, W.rf, W.roff.p,
+                           (double*)nullptr, b1, b2, v);
+    HIP_CHECK(hipGetLastError());
+    HIP_CHECK(hipStreamSynchronize(s));
+}
+
+}  // namespace
+
+extern "C" {
+
 int hh_gw_correct(hh_gw* g, const double* alpha, double exponent, int64_t* out_nnz, void* stream) {
     return guard([&] {
         HH_REQUIRE(g && alpha && out_nnz, "null");
         hipStream_t s = as_stream(stream);
-        const int64_t N2 = g->N2, nk = g->n_keys;
-        DBuf<double> dal(N2), sv(N2);
-        dal.upload(alpha, N2, s);
-        DBuf<long long> ustart(N2), lstart(N2);
-        GwDev d{g->R.p, g->C.p, g->V.p, g->hptr.p, g->keys.p, g->cptr.p, (long long)N2, dal.p, ustart.p, lstart.p};
-        hipLaunchKernelGGL(k_gw_marg, dim3((unsigned)((N2 * 64 + 255) / 256)), dim3(256), 0, s, d, exponent, sv.p);
-        DBuf<long long> flag(nk + 1), opre(nk + 1);
-        if (nk > 0)
-            hipLaunchKernelGGL(k_gw_orphans, dim3((unsigned)((N2 * 64 + 255) / 256)), dim3(256), 0, s, d, flag.p);
-        HIP_CHECK(hipMemsetAsync(flag.p + nk, 0, sizeof(long long), s));
-        dev_excl_scan_i64(flag.p, opre.p, nk + 1, nullptr, s);
-        DBuf<long long> len(N2 + 1), roff(N2 + 1);
-        hipLaunchKernelGGL(k_gw_rowlen, dim3((unsigned)((N2 + 255) / 256)), dim3(256), 0, s, d, opre.p, len.p);
-        HIP_CHECK(hipMemsetAsync(len.p + N2, 0, sizeof(long long), s));
-        dev_excl_scan_i64(len.p, roff.p, N2 + 1, nullptr, s);
-        long long total = 0;
-        HIP_CHECK(hipMemcpyAsync(&total, roff.p + N2, sizeof(long long), hipMemcpyDeviceToHost, s));
-        HIP_CHECK(hipStreamSynchronize(s));
-        g->ob1.alloc(std::max<long long>(total, 1));
-        g->ob2.alloc(std::max<long long>(total, 1));
-        g->ov.alloc(std::max<long long>(total, 1));
-        if (g->h_nnz > 0)
-            hipLaunchKernelGGL(k_gw_write_upper, dim3((unsigned)((g->h_nnz + 255) / 256)), dim3(256), 0, s, d, opre.p,
-                               roff.p, sv.p, g->ob1.p, g->ob2.p, g->ov.p);
-        if (nk > 0)
-            hipLaunchKernelGGL(k_gw_write_orphans, dim3((unsigned)((N2 * 64 + 255) / 256)), dim3(256), 0, s, d,
-                               flag.p, opre.p, roff.p, sv.p, g->ob1.p, g->ob2.p, g->ov.p);
-        HIP_CHECK(hipGetLastError());
-        // R_F = H.mean() / C.mean() over the full 2n x 2n matrices (:897-899)
-        const long long per = 1 << 16;
-        const long long nbk = std::max<long long>(1, (total + per - 1) / per);
-        DBuf<double> part(nbk);
-        part.zero(s);
-        if (total > 0)
-            hipLaunchKernelGGL(k_gw_csum, dim3((unsigned)nbk), dim3(256), 0, s, g->ob1.p, g->ob2.p, g->ov.p,
-                               (long long)total, per, part.p);
-        std::vector<double> hp(nbk);
-        part.download(hp.data(), nbk, s);
-        HIP_CHECK(hipStreamSynchronize(s));
-        double csum = 0.0;
-        for (double x : hp) csum += x;
-        const double NN = (double)N2 * (double)N2;
-        const double rf = ((double)g->h_total / NN) / (csum / NN);
-        if (total > 0)
-            hipLaunchKernelGGL(k_gw_scale, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, g->ov.p,
-                               (long long)total, rf);
-        HIP_CHECK(hipGetLastError());
-        HIP_CHECK(hipStreamSynchronize(s));
-        g->out_nnz = total;
-        *out_nnz = total;
+        GwScratch W;
+        if (g->fmt) gw_prepare<1>(g, alpha, exponent, W, s);
+        else gw_prepare<0>(g, alpha, exponent, W, s);
+        g->ob1.alloc(std::max<long long>(W.total, 1));
+        g->ob2.alloc(std::max<long long>(W.total, 1));
+        g->ov.alloc(std::max<long long>(W.total, 1));
+        if (g->fmt) gw_write<1>(g, W, g->ob1.p, g->ob2.p, g->ov.p, s);
+        else gw_write<0>(g, W, g->ob1.p, g->ob2.p, g->ov.p, s);
+        g->out_nnz = W.total;
+        *out_nnz = W.total;
+    });
+}
+
+// The same in two calls so the caller can own the output: the count (and
+// everything before the write, kept in the handle), then the write into
+// caller-sized device buffers (no copy of a 20 GB result at 10 kb diploid).
+int hh_gw_correct_count(hh_gw* g, const double* alpha, double exponent, int64_t* out_nnz, void* stream) {
+    return guard([&] {
+        HH_REQUIRE(g && alpha && out_nnz, "null");
+        hipStream_t s = as_stream(stream);
+        g->scratch = std::make_shared<GwScratch>();
+        if (g->fmt) gw_prepare<1>(g, alpha, exponent, *g->scratch, s);
+        else gw_prepare<0>(g, alpha, exponent, *g->scratch, s);
+        *out_nnz = g->scratch->total;
+    });
+}
+
+int hh_gw_correct_write(hh_gw* g, int32_t* bin1, int32_t* bin2, double* value, void* stream) {
+    return guard([&] {
+        HH_REQUIRE(g && g->scratch, "call hh_gw_correct_count first");
+        HH_REQUIRE(g->scratch->total == 0 || (bin1 && bin2 && value), "null output buffers");
+        hipStream_t s = as_stream(stream);
+        if (g->fmt) gw_write<1>(g, *g->scratch, bin1, bin2, value, s);
+        else gw_write<0>(g, *g->scratch, bin1, bin2, value, s);
+        g->scratch.reset();
     });
 }
 

@@ -697,6 +697,113 @@ __global__ __launch_bounds__(kSweepThreads, 4) void k_sweep_flat(TileDev T, cons
     sweep_flat_unit<U, ABL>(T, act, T.u_order[list_off + blockIdx.x], b, n_bins, part, L);
 }
 
+// K1c' (round 3): the flat tiles swept by column tile.  A block takes a
+// group of up to kFlatGroup flat tiles sharing one column tile J (different
+// row-blocks), stages b[J] once, and each of its 8 waves then walks whole
+// tiles on its own -- the next tile of the group from an LDS counter, the
+// tile's flat record in a per-wave LDS slot, its row sums in a per-wave LDS
+// accumulator, written out as that tile's unit partials.  No block barrier
+// per tile: the waves' load / walk / write chains drift apart and overlap
+// (the round-2 kernel ran one tile at a time per block with two barriers per
+// tile and re-staged 64 KB of b for every ~100 KB of sparse payload).  Per
+// tile the walk is the round-2 one with the whole tile as the wave's range,
+// so a row's sum is a fixed function of the tile: deterministic, and the
+// same wherever the tile is swept.
+struct FlatWLds {
+    double bl[kW];
+    uint16_t rec[kFlatWaves][kFrecU4 * 8];
+    double acc[kFlatWaves][kR];
+    int next;
+};
+
+__device__ __forceinline__ void wave_lds_sync() {
+    // one wave's LDS writes before its later LDS reads (the LDS queue is in
+    // order per wave; this orders the compiler and waits for the writes)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int U, int ABL>
+__global__ __launch_bounds__(kSweepThreads, 2) void k_sweep_flatw(TileDev T, const uint8_t* __restrict__ act,
+                                                                const double* __restrict__ b, long long n_bins,
+                                                                double* __restrict__ part) {
+    static_assert(kSweepWaves == kFlatWaves, "one LDS slot per wave");
+    constexpr int UW = 2;
+    __shared__ __attribute__((aligned(16))) FlatWLds L;
+    const int k0 = T.fg_ptr[blockIdx.x], nk = T.fg_ptr[blockIdx.x + 1] - k0;
+    {
+        bool on = false;  // block-uniform: any active tile in the group
+        for (int k = 0; k < nk && !on; ++k) {
+            const int u = T.fg_unit[k0 + k];
+            for (int g = T.u_glo[u]; g <= T.u_ghi[u]; ++g) on |= act[g] != 0;
+        }
+        if (!on) return;
+    }
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int J = T.tile_J[T.u_tlo[T.fg_unit[k0]]];
+    if (threadIdx.x == 0) L.next = 0;
+    if (ABL != 2) stage_bias(L.bl, b, (long long)J * kW, n_bins);
+    __syncthreads();
+    const double* __restrict__ bl = L.bl;
+    uint16_t* __restrict__ rec = L.rec[wave];
+    double* __restrict__ acc = L.acc[wave];
+    const uint16_t* fstn = rec;
+    const uint16_t* fstw = rec + (kR + 1);
+    const uint16_t* fidn = rec + 2 * (kR + 1);
+    const uint16_t* fidw = fidn + kR;
+    for (;;) {
+        int k = 0;
+        if (lane == 0) k = atomicAdd(&L.next, 1);
+        k = __builtin_amdgcn_readfirstlane(__shfl(k, 0, 64));
+        if (k >= nk) break;
+        const int u = T.fg_unit[k0 + k];
+        bool on = false;
+        for (int g = T.u_glo[u]; g <= T.u_ghi[u]; ++g) on |= act[g] != 0;
+        if (!on) continue;  // a converged group's rows: k_marg never reads them
+        const int t = T.u_tlo[u], nr = T.u_rhi[u];
+        const uint32_t* fw = T.tile_fw + (size_t)t * kFlatMeta;
+        const uint32_t qbn = fw[2 * kFlatWaves];
+        const int nfn = (int)fw[2 * kFlatWaves + 1];
+        const uint32_t* fww = fw + 2 * (kFlatWaves + 1);
+        const uint32_t qbw = fww[2 * kFlatWaves];
+        const int nfw = (int)fww[2 * kFlatWaves + 1];
+        const uint4* payn4 = reinterpret_cast<const uint4*>(T.payn + T.tile_entn[t]);
+        const uint4* payw4 = reinterpret_cast<const uint4*>(T.pay + T.tile_ent[t]);
+        uint4 v[U], vw[UW];
+        if (nfn) flat_load<U>(payn4, (uint32_t)lane * U, 0u, qbn, v);
+        if (nfw) flat_load<UW>(payw4, (uint32_t)lane * UW, 0u, qbw, vw);
+        const uint4* rg = T.frec + (size_t)T.tile_frec[t] * kFrecU4;
+        for (int q = lane; q < kFrecU4; q += 64) reinterpret_cast<uint4*>(rec)[q] = rg[q];
+        wave_lds_sync();
+        flat_seg_c<U, ABL, 8>(payn4, v, 0u, qbn, 0, nfn, fstn, nfn, bl, acc, lane);
+        wave_lds_sync();
+        // compact narrow sums -> rows (zeros for rows without narrow entries)
+        constexpr int PL = kR / 64;
+        double cv[PL];
+        int cid[PL];
+#pragma unroll
+        for (int q = 0; q < PL; ++q) {
+            const int i = lane + 64 * q;
+            cv[q] = i < nfn ? acc[i] : 0.0;
+            cid[q] = i < nfn ? (int)fidn[i] : -1;
+        }
+        wave_lds_sync();
+#pragma unroll
+        for (int q = 0; q < PL; ++q) acc[lane + 64 * q] = 0.0;
+        wave_lds_sync();
+#pragma unroll
+        for (int q = 0; q < PL; ++q)
+            if (cid[q] >= 0) acc[cid[q]] = cv[q];
+        wave_lds_sync();
+        flat_seg<UW, ABL, 4>(payw4, vw, 0u, qbw, 0, nfw, fstw, fidw, nfw, bl, acc, lane);
+        wave_lds_sync();
+        double* __restrict__ out = part + T.u_slot[u];
+        for (int r = lane; r < nr; r += 64) out[r] = acc[r];
+        wave_lds_sync();  // this tile's LDS reads before the next tile's writes
+    }
+}
+
 // ---------------------------------------------------------------- K2
 // marg_r = b_r * (sum of the row's unit partials + wide entries + 2 diag b_r)
 // K1b: the dense diagonal bands (uint8 counts near the diagonal, 4-bit
@@ -1376,6 +1483,7 @@ namespace hh {
 
 // Tuning knobs (hh_tune; no effect on results except the ablations).
 static int g_sweep_nb = 2;
+static int g_flatw_u = 8;  // uint4 per lane per step in k_sweep_flatw (8 or 16)
 static int g_sweep_ablate = 0;
 // Default: three streams per sweep -- band kernels (side), tiled kernel (side2),
 // flat kernel (main) -- so each kernel's ramp and tail overlap the others'
@@ -1404,9 +1512,17 @@ static void launch_sweep(const hh_matrix* m, const uint8_t* act, const double* b
     if (n_tiled)
         hipLaunchKernelGGL((k_sweep_tiled<NB, ABL>), dim3((unsigned)n_tiled), dim3(kSweepThreads), 0, s_tiled,
                            m->dev(), act, n_tiled, b, (long long)m->n_bins, part);
-    if (n_flat)
+    if (n_flat && m->n_fgroups) {
+        if (g_flatw_u == 16)
+            hipLaunchKernelGGL((k_sweep_flatw<16, ABL>), dim3((unsigned)m->n_fgroups), dim3(kSweepThreads), 0, s,
+                               m->dev(), act, b, (long long)m->n_bins, part);
+        else
+            hipLaunchKernelGGL((k_sweep_flatw<kFlatU, ABL>), dim3((unsigned)m->n_fgroups), dim3(kSweepThreads), 0, s,
+                               m->dev(), act, b, (long long)m->n_bins, part);
+    } else if (n_flat) {
         hipLaunchKernelGGL((k_sweep_flat<kFlatU, ABL>), dim3((unsigned)n_flat), dim3(kSweepThreads), 0, s, m->dev(),
                            act, n_flat, n_tiled, b, (long long)m->n_bins, part);
+    }
 }
 
 template <int ABL>
@@ -1678,6 +1794,12 @@ int hh_tune(const char* key, int64_t value) {
         } else if (k == "band4") {
             HH_REQUIRE(value == 0 || value == 1, "band4 in {0, 1}");
             g_band4 = value;
+        } else if (k == "flat_cols") {
+            HH_REQUIRE(value == 0 || value == 1, "flat_cols in {0, 1}");
+            g_flat_cols = value;
+        } else if (k == "flatw_u") {
+            HH_REQUIRE(value == 8 || value == 16, "flatw_u in {8, 16}");
+            g_flatw_u = (int)value;
         } else if (k == "flat_max") {
             HH_REQUIRE(value >= 0 && value <= 255, "flat_max in [0, 255]");
             g_flat_max = value;

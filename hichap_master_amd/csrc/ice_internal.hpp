@@ -121,6 +121,13 @@ constexpr int kFrecU4 = (kFrecHalf * 2 + 15) / 16;
 constexpr int kFlatFlag = 6;     // band slot: 1 = flat segment
 constexpr int kFlatRows = 7;     // band slot: number of nonempty rows
 extern int64_t g_flat_max;       // hh_tune("flat_max"), build time
+// Column-grouped flat sweep (hh_tune "flat_cols", build time):
+// every flat tile is its own work unit (one partial per row per flat tile),
+// and the flat tiles of one column tile J are swept together in groups of up
+// to kFlatGroup by one block that stages b[J] once, each wave walking whole
+// tiles on its own (no block barrier per tile).
+extern int64_t g_flat_cols;
+constexpr int kFlatGroup = 16;
 // minimum row length (uint4 per row) of band g
 __host__ __device__ constexpr uint32_t band_min(int g) { return g == 0 ? 48u : g == 1 ? 24u : g == 2 ? 12u : g == 3 ? 6u : 1u; }
 
@@ -156,6 +163,7 @@ struct TilePlan {
     std::vector<uint8_t> u_whole;       // 1: the unit covers whole row-blocks (sorted-band sweep)
     std::vector<uint8_t> tile_flat;     // per tile: 1 = flat (every nonempty segment flat)
     std::vector<uint8_t> u_flat;        // per unit: 1 = swept by the flat kernel
+    std::vector<int32_t> fg_ptr, fg_unit;  // flat groups (g_flat_cols): units of group g = fg_unit[fg_ptr[g] ..)
     int64_t n_units_flat = 0;
     int64_t payload_bytes_flat = 0;     // payload of the flat units' tiles
     int64_t n_entries_padded = 0;     // wide slots
@@ -193,6 +201,8 @@ struct TileDev {
     const int32_t* tile_frec;
     const uint4* frec;
     const uint8_t* u_whole;
+    const int32_t* fg_ptr;
+    const int32_t* fg_unit;
     int flat_defer;  // flat kernel: merge a tile's compact sums after the next tile's barrier (hh_tune "flat_defer")
 };
 
@@ -228,6 +238,8 @@ struct hh_matrix {
     hh::DBuf<int32_t> tile_frec;
     hh::DBuf<uint16_t> frec;
     hh::DBuf<uint8_t> u_whole;
+    hh::DBuf<int32_t> fg_ptr, fg_unit;  // column groups of the flat units (g_flat_cols)
+    int64_t n_fgroups = 0;
     hh::DBuf<long long> wide_ptr;  // local rows + 1
     hh::DBuf<int32_t> wide_col;
     hh::DBuf<double> wide_cnt;
@@ -240,6 +252,7 @@ struct hh_matrix {
         return pay.bytes() + payn.bytes() + tile_entn.bytes() + tile_rpn.bytes() + tile_J.bytes() +
                tile_rb.bytes() + tile_ent.bytes() + tile_rp.bytes() +
                u_tlo.bytes() * 7 + blk_unit_ptr.bytes() + tile_perm.bytes() + tile_band.bytes() + u_whole.bytes() + tile_fw.bytes() + tile_frec.bytes() + frec.bytes() + blk_tile_ptr.bytes() + u_glo.bytes() * 2 +
+               fg_ptr.bytes() + fg_unit.bytes() +
                wide_ptr.bytes() + wide_col.bytes() + wide_cnt.bytes() + diag.bytes() + row_nnz2.bytes() +
                row_sum2.bytes() + row_group.bytes() + band.bytes() + band4.bytes();
     }
@@ -247,7 +260,7 @@ struct hh_matrix {
         return hh::TileDev{pay.p, payn.p, tile_J.p, tile_ent.p, tile_rp.p, tile_entn.p, tile_rpn.p, u_tlo.p,
                            u_thi.p, u_rb.p, u_rlo.p, u_rhi.p, u_slot.p, u_glo.p, u_ghi.p, blk_unit_ptr.p,
                            u_order.p, tile_perm.p, tile_band.p, tile_fw.p, tile_frec.p,
-                           reinterpret_cast<const uint4*>(frec.p), u_whole.p, hh::g_flat_defer};
+                           reinterpret_cast<const uint4*>(frec.p), u_whole.p, fg_ptr.p, fg_unit.p, hh::g_flat_defer};
     }
 };
 

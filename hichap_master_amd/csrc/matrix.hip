@@ -18,6 +18,7 @@ int64_t g_unit_entries = 0;  // 0 = auto (plan_tiles)
 int g_flat_defer = 1;
 int64_t g_unit_lpt = 1;      // launch lists by unit cost class, largest first (0: row order)
 int64_t g_unit_lpt_lists = 1; // which lists: 1 tiled, 2 flat, 3 both (flat too: C4 sweep +1 %, profiles/r2b_modes_ab.log)
+int64_t g_flat_cols = 1;       // flat tiles as single-tile units swept in column groups (ice.hip k_sweep_flatw)
 int64_t g_tile_cost = 32768; // payload-word equivalent of one tile's fixed cost in the unit split (C4 shard 8/8: 0.79 -> 0.65 ms/iter)
 int64_t g_band_w = -1;       // -1 = auto (choose_band_w)
 int64_t g_flat_max = 64;     // longest row (uint4) of a flat tile segment; 0 = no flat segments
@@ -142,10 +143,13 @@ void plan_block(const uint16_t* cntw, const uint16_t* cntn, int64_t nloc, int32_
                 st[nfr] = Q;
                 band[seg][kFlatFlag] = nfr > 0 ? 1 : 0;
                 band[seg][kFlatRows] = (uint16_t)nfr;
-                // wave w takes the rows starting in [Q w / 8, Q (w + 1) / 8)
+                // wave w takes the rows starting in [Q w / 8, Q (w + 1) / 8);
+                // with the column-grouped sweep one wave walks the whole tile
+                // (k_sweep_flatw), and the one-launch sweep's flat body must
+                // sum each row in that same order: wave 0 takes every row
                 uint32_t* f = fw + seg * 2 * (kFlatWaves + 1);
                 for (int w = 0; w <= kFlatWaves; ++w) {
-                    const uint32_t tq = (uint32_t)(((uint64_t)Q * w) / kFlatWaves);
+                    const uint32_t tq = g_flat_cols ? (w == 0 ? 0u : Q) : (uint32_t)(((uint64_t)Q * w) / kFlatWaves);
                     const int i = (int)(std::lower_bound(st, st + nfr, tq) - st);
                     f[2 * w] = st[i];
                     f[2 * w + 1] = (uint32_t)i;
@@ -344,6 +348,12 @@ TilePlan plan_tiles(const uint16_t* cntw, const uint16_t* cntn, int64_t nloc, in
                 emit(rb, t, t + 1, rlo, nr);
                 cur = t + 1;
                 cur_sz = 0;
+            } else if (g_flat_cols && P.tile_flat[t]) {
+                // column-grouped flat sweep: every flat tile its own unit
+                if (cur < t) emit(rb, cur, t, 0, nr);
+                emit(rb, t, t + 1, 0, nr);
+                cur = t + 1;
+                cur_sz = 0;
             } else {
                 // a unit is all flat tiles or none (two sweep kernels)
                 if (cur < t && (cur_sz + sz > unit_cap || P.tile_flat[t] != P.tile_flat[cur])) {
@@ -367,6 +377,37 @@ TilePlan plan_tiles(const uint16_t* cntw, const uint16_t* cntn, int64_t nloc, in
             ++P.n_units_flat;
             for (int32_t t = P.u_tlo[u]; t < P.u_thi[u]; ++t) P.payload_bytes_flat += 4 * tile_words(t, 0, kR);
         }
+    if (g_flat_cols && P.n_units_flat) {
+        // flat groups: the flat units ordered by (column tile, row-block), cut
+        // into runs of <= kFlatGroup with one column tile; groups dispatched
+        // by payload, largest first (a group's partials do not depend on it)
+        std::vector<int32_t> fu;
+        for (size_t u = 0; u < P.u_tlo.size(); ++u)
+            if (P.u_flat[u]) fu.push_back((int32_t)u);
+        std::stable_sort(fu.begin(), fu.end(), [&](int32_t a, int32_t b) {
+            const int32_t ja = P.tile_J[P.u_tlo[a]], jb = P.tile_J[P.u_tlo[b]];
+            return ja != jb ? ja < jb : P.u_rb[a] < P.u_rb[b];
+        });
+        std::vector<std::pair<int64_t, std::pair<int32_t, int32_t>>> groups;  // (-words, [lo, hi) in fu)
+        for (size_t a = 0; a < fu.size();) {
+            size_t e = a;
+            int64_t w = 0;
+            const int32_t J = P.tile_J[P.u_tlo[fu[a]]];
+            while (e < fu.size() && e - a < (size_t)kFlatGroup && P.tile_J[P.u_tlo[fu[e]]] == J) {
+                w += tile_words(P.u_tlo[fu[e]], 0, kR);
+                ++e;
+            }
+            groups.push_back({-w, {(int32_t)a, (int32_t)e}});
+            a = e;
+        }
+        std::stable_sort(groups.begin(), groups.end(),
+                         [](const auto& x, const auto& y) { return x.first < y.first; });
+        P.fg_ptr.assign(1, 0);
+        for (const auto& g : groups) {
+            for (int32_t k = g.second.first; k < g.second.second; ++k) P.fg_unit.push_back(fu[k]);
+            P.fg_ptr.push_back((int32_t)P.fg_unit.size());
+        }
+    }
     if (g_unit_lpt) {
         // each list by cost class (bit length of words + per-tile cost),
         // largest first, row order within a class: the remainder units of the
@@ -423,6 +464,11 @@ void upload_plan(const TilePlan& P, hh_matrix& m, hipStream_t s) {
     m.tile_frec = to_device(P.tile_frec, s);
     m.frec = to_device(P.frec, s);
     m.u_whole = to_device(P.u_whole, s);
+    m.n_fgroups = P.fg_ptr.empty() ? 0 : (int64_t)P.fg_ptr.size() - 1;
+    if (m.n_fgroups) {
+        m.fg_ptr = to_device(P.fg_ptr, s);
+        m.fg_unit = to_device(P.fg_unit, s);
+    }
     HIP_CHECK(hipStreamSynchronize(s));  // the plan's host vectors may die after return
 }
 

@@ -324,18 +324,15 @@ def GenomeWideMatrixCorrectionSparse(Bins_Pos, Hap_Bins_Pos, T_pixels, H_cells, 
         Alpha += Alpha
         Alpha = np.ascontiguousarray(Alpha, dtype=np.float64)
         m = C.c_int64(0)
+        if device_result:  # int32 / int32 / float64 device tensors, written in place by the library
+            import torch
+            call("hh_gw_correct_count", h, ptr(Alpha), float(exponent), C.byref(m), stream)
+            m = int(m.value)
+            out = [torch.empty(max(m, 1), dtype=dt, device="cuda") for dt in (torch.int32, torch.int32, torch.float64)]
+            call("hh_gw_correct_write", h, *(C.c_void_p(t.data_ptr()) for t in out), stream)
+            return tuple(t[:m] for t in out)
         call("hh_gw_correct", h, ptr(Alpha), float(exponent), C.byref(m), stream)
         m = int(m.value)
-        if device_result:  # int32 / int32 / float64 device tensors (e.g. for ice / cooler writing on GPU)
-            import torch
-            p1, p2, pv = C.c_void_p(), C.c_void_p(), C.c_void_p()
-            call("hh_gw_result_device", h, C.byref(p1), C.byref(p2), C.byref(pv))
-            out = [torch.empty(m, dtype=dt, device="cuda") for dt in (torch.int32, torch.int32, torch.float64)]
-            for t, p in zip(out, (p1, p2, pv)):
-                if m:
-                    call("hh_device_copy", C.c_void_p(t.data_ptr()), p, t.element_size() * m, stream)
-            call("hh_synchronize", stream)
-            return tuple(out)
         b1 = np.empty(m, np.int64)
         b2 = np.empty(m, np.int64)
         v = np.empty(m, np.float64)

@@ -192,7 +192,7 @@ class TADCalling:
                 Gap_desity_t = float(Gap.size) / N / 2.0
                 Gap_all[chro] = Gap
                 DI_dict[chro] = DI_sub
-                DI_all_train[chro] = self.train_segments(Gap, self.Gap_Filter(Gap, None), DI_sub, width,
+                DI_all_train[chro] = self.train_segments(Gap, self.Gap_Filter(Gap, np.empty((N, 0))), DI_sub, width,
                                                          Gap_desity_t)
         self.DI_all_train, self.DI_dict, self.Gap_all = DI_all_train, DI_dict, Gap_all
         self.Matrix_Dict, self.chroms = _LazyMatrices(self.cooler_fil, chroms, self.Allelic is False), chroms

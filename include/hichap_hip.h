@@ -363,6 +363,12 @@ int hh_gw_stats(const hh_gw* g, int64_t* t_rowsum, int64_t* t_nnz_row, int64_t* 
 /* alpha[2n] (host): the concatenated, duplicated SNP-density factors;
  * exponent: 2/3.  *out_nnz = upper-triangle pixels of the result. */
 int hh_gw_correct(hh_gw* g, const double* alpha, double exponent, int64_t* out_nnz, void* stream);
+/* hh_gw_correct in two calls, the output owned by the caller: the count
+ * (marginals, VC factors, merge count pass, the mean rescale factor; state
+ * kept in the handle), then the write of the upper table into device
+ * buffers of out_nnz elements. */
+int hh_gw_correct_count(hh_gw* g, const double* alpha, double exponent, int64_t* out_nnz, void* stream);
+int hh_gw_correct_write(hh_gw* g, int32_t* bin1, int32_t* bin2, double* value, void* stream);
 /* the result to host arrays of out_nnz (any may be NULL), or its device
  * pointers (valid until hh_gw_free or the next hh_gw_correct) */
 int hh_gw_result(const hh_gw* g, int64_t* bin1, int64_t* bin2, double* value, void* stream);

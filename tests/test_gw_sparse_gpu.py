@@ -217,3 +217,22 @@ def test_bench_size_invariants(mb):
     del key
     tot = float((torch.where(b1 == b2, 1.0, 2.0).to(torch.float64) * v).sum().item())
     assert abs(tot - hsum) <= 1e-9 * hsum, (tot, hsum)
+
+
+def test_large_h_counts_index_keys(mb):
+    """An H count >= 2^24 does not fit the packed (col | row | count) column
+    keys: the column lists fall back to index keys + k_gw_pack; same result
+    as the oracle and the dense path."""
+    rng = np.random.default_rng(11)
+    sizes = [50, 35]
+    n = sum(sizes)
+    T = np.triu(rng.poisson(2.0, size=(n, n)) * (rng.random((n, n)) < 0.5))
+    T = T + np.triu(T, 1).T
+    H = (rng.poisson(0.8, size=(2 * n, 2 * n)) * (rng.random((2 * n, 2 * n)) < 0.3)).astype(np.int64)
+    H[3, 100] = 2**24 + 5
+    H[120, 7] = 2**31
+    bins, hbins = _layout(["1", "2"], sizes)
+    tp, hc = _tables(T, H)
+    b1, b2, v = mb.GenomeWideMatrixCorrectionSparse(bins, hbins, tp, hc)
+    ref = hichap_ref.genome_wide_correction(bins, hbins, T, H)
+    _check_upper(b1, b2, v, ref, 1e-12)
