@@ -39,9 +39,11 @@ __global__ __launch_bounds__(256) void k_gw_check(const Id* __restrict__ r_in, c
                                                   int upper, int32_t* __restrict__ R, int32_t* __restrict__ Cc,
                                                   uint32_t* __restrict__ V, unsigned long long* __restrict__ errs,
                                                   unsigned* __restrict__ vmax) {
-    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    // grid-stride, one max atomic per block (one per wave was 23M same-address
+    // atomics on a 1.5e9-cell table: 266 ms)
     unsigned mx = 0u;
-    if (i < nnz) {
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < nnz;
+         i += (long long)gridDim.x * blockDim.x) {
         const long long a = (long long)r_in[i], b = (long long)c_in[i];
         const double v = (double)v_in[i];
         int code = 0;
@@ -60,7 +62,7 @@ __global__ __launch_bounds__(256) void k_gw_check(const Id* __restrict__ r_in, c
                 V[i] = 0u;
             }
         } else {
-            mx = (unsigned)v;
+            mx = max(mx, (unsigned)v);
             if (COPY) {
                 R[i] = (int32_t)a;
                 Cc[i] = (int32_t)b;
@@ -70,7 +72,13 @@ __global__ __launch_bounds__(256) void k_gw_check(const Id* __restrict__ r_in, c
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) mx = max(mx, (unsigned)__shfl_xor((int)mx, o, 64));
-    if ((threadIdx.x & 63) == 0 && mx) atomicMax(vmax, mx);
+    __shared__ unsigned wm[4];
+    if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = mx;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        mx = max(max(wm[0], wm[1]), max(wm[2], wm[3]));
+        if (mx) atomicMax(vmax, mx);
+    }
 }
 
 // ptr[r] = first i with A[i] >= r, r in [0, nr] (A sorted)
@@ -399,7 +407,8 @@ __global__ __launch_bounds__(256) void k_gw_merge(GwDev g, const double* __restr
             }
         }
         const int x = lo;                         // A elements in the first lane + 1
-        const int xp = lane ? __shfl_up(x, 1, 64) : 0;  // ... in the first lane
+        const int xu = __shfl_up(x, 1, 64);       // (every lane shuffles)
+        const int xp = lane ? xu : 0;             // ... in the first lane
         const bool fromA = x > xp;
         const int src = fromA ? xp : lane - xp;   // index in that window
         // every lane takes part in every shuffle (a lane reading from a lane
@@ -414,7 +423,8 @@ __global__ __launch_bounds__(256) void k_gw_merge(GwDev g, const double* __restr
         const bool fromA_n = __shfl_down(fromA ? 1 : 0, 1, 64) != 0;
         const double val_n = __shfl_down(val, 1, 64);
         const bool pair_next = lane < 63 && fromA && !fromA_n && key_n == key && key != kMergeInf;
-        const bool pair_prev = __shfl_up(pair_next ? 1 : 0, 1, 64) != 0 && lane > 0;
+        const int pn_up = __shfl_up(pair_next ? 1 : 0, 1, 64);
+        const bool pair_prev = pn_up != 0 && lane > 0;
         // consume 63 elements, or 64 when 62-63 is a pair
         const int M = __shfl(pair_next ? 1 : 0, 62, 64) ? 64 : 63;
         const bool live = lane < M && key != kMergeInf;
@@ -501,7 +511,7 @@ unsigned gw_check(const Id* r, const Id* c, const Cnt* v, int64_t nnz, int64_t n
     vmax.zero(s);
     HIP_CHECK(hipMemsetAsync(err.p, 0xff, 5 * sizeof(unsigned long long), s));
     if (nnz > 0)
-        hipLaunchKernelGGL((k_gw_check<Id, Cnt, COPY>), dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s, r, c, v,
+        hipLaunchKernelGGL((k_gw_check<Id, Cnt, COPY>), dim3((unsigned)std::max<long long>(1, std::min<long long>((nnz + 255) / 256, 16384))), dim3(256), 0, s, r, c, v,
                            (long long)nnz, (long long)nb, upper, R.p, Cc.p, V.p, err.p, vmax.p);
     HIP_CHECK(hipGetLastError());
     unsigned long long he[5];

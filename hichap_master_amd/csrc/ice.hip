@@ -452,6 +452,46 @@ __device__ __forceinline__ void flat_seg_c(const uint4* __restrict__ pay4, uint4
     }
 }
 
+// flat_seg_c / flat_seg with the next step's run loaded before the current
+// step is walked (two runs in registers: the one-wave-per-tile kernel has
+// the VGPRs for it); the same steps in the same order, bitwise the same sums
+template <int U, int ABL, int EPV>
+__device__ __forceinline__ void flat_seg_c_pipe(const uint4* __restrict__ pay4, uint4 (&v)[U], uint32_t qa, uint32_t qb,
+                                                int i0, int i1, const uint16_t* __restrict__ fst, int nfr,
+                                                const double* __restrict__ bl, double* __restrict__ accc, int lane) {
+    if (i0 >= i1) return;
+    int ic = i0;
+    for (uint32_t q0 = qa;;) {
+        const uint32_t qn = q0 + 64u * U;
+        uint4 vn[U];
+        if (qn < qb) flat_load<U>(pay4, qn + (uint32_t)lane * U, qa, qb, vn);
+        flat_step_c<U, ABL, EPV>(v, q0, qb, ic, i1, fst, nfr, bl, accc, lane);
+        if (qn >= qb) break;
+#pragma unroll
+        for (int k = 0; k < U; ++k) v[k] = vn[k];
+        q0 = qn;
+    }
+}
+
+template <int U, int ABL, int EPV>
+__device__ __forceinline__ void flat_seg_pipe(const uint4* __restrict__ pay4, uint4 (&v)[U], uint32_t qa, uint32_t qb,
+                                              int i0, int i1, const uint16_t* __restrict__ fst,
+                                              const uint16_t* __restrict__ fr, int nfr, const double* __restrict__ bl,
+                                              double* __restrict__ acc, int lane) {
+    if (i0 >= i1) return;
+    int ic = i0;
+    for (uint32_t q0 = qa;;) {
+        const uint32_t qn = q0 + 64u * U;
+        uint4 vn[U];
+        if (qn < qb) flat_load<U>(pay4, qn + (uint32_t)lane * U, qa, qb, vn);
+        flat_step<U, ABL, EPV>(v, q0, qb, ic, i1, fst, fr, nfr, bl, acc, lane);
+        if (qn >= qb) break;
+#pragma unroll
+        for (int k = 0; k < U; ++k) v[k] = vn[k];
+        q0 = qn;
+    }
+}
+
 // A wave's rows [i0, i1) = uint4 [qa, qb) of one segment, the first step's
 // run already loaded into v (its loads were issued before the tile's LDS
 // staging, so they fly while the block stages).
@@ -724,7 +764,7 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-template <int U, int ABL>
+template <int U, int ABL, int PIPE = 2>
 __global__ __launch_bounds__(kSweepThreads, 2) void k_sweep_flatw(TileDev T, const uint8_t* __restrict__ act,
                                                                 const double* __restrict__ b, long long n_bins,
                                                                 double* __restrict__ part) {
@@ -752,31 +792,42 @@ __global__ __launch_bounds__(kSweepThreads, 2) void k_sweep_flatw(TileDev T, con
     const uint16_t* fstw = rec + (kR + 1);
     const uint16_t* fidn = rec + 2 * (kR + 1);
     const uint16_t* fidw = fidn + kR;
+    struct Tw {
+        int u, t, nr, nfn, nfw;
+        uint32_t qbn, qbw;
+        const uint4 *payn4, *payw4;
+    };
+    // the group's next active tile (LDS counter), false when none is left
+    auto grab = [&](Tw& x) -> bool {
+        for (;;) {
+            int k = 0;
+            if (lane == 0) k = atomicAdd(&L.next, 1);
+            k = __builtin_amdgcn_readfirstlane(__shfl(k, 0, 64));
+            if (k >= nk) return false;
+            const int u = T.fg_unit[k0 + k];
+            bool on = false;
+            for (int g = T.u_glo[u]; g <= T.u_ghi[u]; ++g) on |= act[g] != 0;
+            if (!on) continue;  // a converged group's rows: k_marg never reads them
+            const int t = T.u_tlo[u];
+            const uint32_t* fw = T.tile_fw + (size_t)t * kFlatMeta;
+            const uint32_t* fww = fw + 2 * (kFlatWaves + 1);
+            x = Tw{u, t, T.u_rhi[u], (int)fw[2 * kFlatWaves + 1], (int)fww[2 * kFlatWaves + 1], fw[2 * kFlatWaves],
+                   fww[2 * kFlatWaves], reinterpret_cast<const uint4*>(T.payn + T.tile_entn[t]),
+                   reinterpret_cast<const uint4*>(T.pay + T.tile_ent[t])};
+            return true;
+        }
+    };
+    Tw cur;
+    if (!grab(cur)) return;
+    uint4 v[U], vw[UW];
+    if (cur.nfn) flat_load<U>(cur.payn4, (uint32_t)lane * U, 0u, cur.qbn, v);
+    if (cur.nfw) flat_load<UW>(cur.payw4, (uint32_t)lane * UW, 0u, cur.qbw, vw);
     for (;;) {
-        int k = 0;
-        if (lane == 0) k = atomicAdd(&L.next, 1);
-        k = __builtin_amdgcn_readfirstlane(__shfl(k, 0, 64));
-        if (k >= nk) break;
-        const int u = T.fg_unit[k0 + k];
-        bool on = false;
-        for (int g = T.u_glo[u]; g <= T.u_ghi[u]; ++g) on |= act[g] != 0;
-        if (!on) continue;  // a converged group's rows: k_marg never reads them
-        const int t = T.u_tlo[u], nr = T.u_rhi[u];
-        const uint32_t* fw = T.tile_fw + (size_t)t * kFlatMeta;
-        const uint32_t qbn = fw[2 * kFlatWaves];
-        const int nfn = (int)fw[2 * kFlatWaves + 1];
-        const uint32_t* fww = fw + 2 * (kFlatWaves + 1);
-        const uint32_t qbw = fww[2 * kFlatWaves];
-        const int nfw = (int)fww[2 * kFlatWaves + 1];
-        const uint4* payn4 = reinterpret_cast<const uint4*>(T.payn + T.tile_entn[t]);
-        const uint4* payw4 = reinterpret_cast<const uint4*>(T.pay + T.tile_ent[t]);
-        uint4 v[U], vw[UW];
-        if (nfn) flat_load<U>(payn4, (uint32_t)lane * U, 0u, qbn, v);
-        if (nfw) flat_load<UW>(payw4, (uint32_t)lane * UW, 0u, qbw, vw);
-        const uint4* rg = T.frec + (size_t)T.tile_frec[t] * kFrecU4;
+        const uint4* rg = T.frec + (size_t)T.tile_frec[cur.t] * kFrecU4;
         for (int q = lane; q < kFrecU4; q += 64) reinterpret_cast<uint4*>(rec)[q] = rg[q];
         wave_lds_sync();
-        flat_seg_c<U, ABL, 8>(payn4, v, 0u, qbn, 0, nfn, fstn, nfn, bl, acc, lane);
+        if (PIPE) flat_seg_c_pipe<U, ABL, 8>(cur.payn4, v, 0u, cur.qbn, 0, cur.nfn, fstn, cur.nfn, bl, acc, lane);
+        else flat_seg_c<U, ABL, 8>(cur.payn4, v, 0u, cur.qbn, 0, cur.nfn, fstn, cur.nfn, bl, acc, lane);
         wave_lds_sync();
         // compact narrow sums -> rows (zeros for rows without narrow entries)
         constexpr int PL = kR / 64;
@@ -785,8 +836,8 @@ __global__ __launch_bounds__(kSweepThreads, 2) void k_sweep_flatw(TileDev T, con
 #pragma unroll
         for (int q = 0; q < PL; ++q) {
             const int i = lane + 64 * q;
-            cv[q] = i < nfn ? acc[i] : 0.0;
-            cid[q] = i < nfn ? (int)fidn[i] : -1;
+            cv[q] = i < cur.nfn ? acc[i] : 0.0;
+            cid[q] = i < cur.nfn ? (int)fidn[i] : -1;
         }
         wave_lds_sync();
 #pragma unroll
@@ -796,11 +847,32 @@ __global__ __launch_bounds__(kSweepThreads, 2) void k_sweep_flatw(TileDev T, con
         for (int q = 0; q < PL; ++q)
             if (cid[q] >= 0) acc[cid[q]] = cv[q];
         wave_lds_sync();
-        flat_seg<UW, ABL, 4>(payw4, vw, 0u, qbw, 0, nfw, fstw, fidw, nfw, bl, acc, lane);
+        if (PIPE) flat_seg_pipe<UW, ABL, 4>(cur.payw4, vw, 0u, cur.qbw, 0, cur.nfw, fstw, fidw, cur.nfw, bl, acc, lane);
+        else flat_seg<UW, ABL, 4>(cur.payw4, vw, 0u, cur.qbw, 0, cur.nfw, fstw, fidw, cur.nfw, bl, acc, lane);
         wave_lds_sync();
-        double* __restrict__ out = part + T.u_slot[u];
-        for (int r = lane; r < nr; r += 64) out[r] = acc[r];
+        // PIPE 2: the next tile's first runs are in flight while this tile's
+        // row sums go out
+        Tw nxt;
+        bool more = false;
+        if (PIPE == 2) {
+            more = grab(nxt);
+            if (more) {
+                if (nxt.nfn) flat_load<U>(nxt.payn4, (uint32_t)lane * U, 0u, nxt.qbn, v);
+                if (nxt.nfw) flat_load<UW>(nxt.payw4, (uint32_t)lane * UW, 0u, nxt.qbw, vw);
+            }
+        }
+        double* __restrict__ out = part + T.u_slot[cur.u];
+        for (int r = lane; r < cur.nr; r += 64) out[r] = acc[r];
         wave_lds_sync();  // this tile's LDS reads before the next tile's writes
+        if (PIPE != 2) {
+            more = grab(nxt);
+            if (more) {
+                if (nxt.nfn) flat_load<U>(nxt.payn4, (uint32_t)lane * U, 0u, nxt.qbn, v);
+                if (nxt.nfw) flat_load<UW>(nxt.payw4, (uint32_t)lane * UW, 0u, nxt.qbw, vw);
+            }
+        }
+        if (!more) break;
+        cur = nxt;
     }
 }
 
@@ -894,7 +966,15 @@ struct BandSegs {
 // rows in sequence: on a single chromosome the 256-row chain, not the bytes,
 // set the time).  A row's partial does not depend on ROWS (lane -> slot and
 // the summation order are fixed by the row alone): bitwise the same sweep.
-template <int BITS, int ABL, int ROWS>
+// lane l <- lane l - 1 (lane 0 <- 0): DPP wave_shr:1, no LDS
+__device__ __forceinline__ uint4 dpp_shr1(const uint4 v) {
+    return make_uint4(__builtin_amdgcn_update_dpp(0u, v.x, 0x138, 0xF, 0xF, false),
+                      __builtin_amdgcn_update_dpp(0u, v.y, 0x138, 0xF, 0xF, false),
+                      __builtin_amdgcn_update_dpp(0u, v.z, 0x138, 0xF, 0xF, false),
+                      __builtin_amdgcn_update_dpp(0u, v.w, 0x138, 0xF, 0xF, false));
+}
+
+template <int BITS, int ABL, int ROWS, bool DPP = true>
 __device__ __forceinline__ void band_block(const BandSeg& P, int rblk, int chunk, double* __restrict__ bl,
                                            uint8_t* __restrict__ ract, long long nloc, long long row_lo,
                                            long long n_bins, const uint8_t* __restrict__ act,
@@ -940,6 +1020,7 @@ __device__ __forceinline__ void band_block(const BandSeg& P, int rblk, int chunk
         double acc[RJ];
 #pragma unroll
         for (int j = 0; j < RJ; ++j) acc[j] = 0.0;
+        uint4 last[RJ];  // lane 63's bytes of the first half (the second half's lane 0 prev)
 #pragma unroll
         for (int g = 0; g < 2; ++g) {
             const int l = lane + 64 * g;
@@ -950,9 +1031,29 @@ __device__ __forceinline__ void band_block(const BandSeg& P, int rblk, int chunk
                 const uint8_t* row = seg + (r0 + gb + wave + NW * (j0 + j)) * row_stride;
                 const bool on = a[j] && cb < c1, onp = on && cb >= 16;
                 const uint4 x = ld16(reinterpret_cast<const uint4*>(on ? row + cb : seg));
-                const uint4 y = ld16(reinterpret_cast<const uint4*>(onp ? row + cb - 16 : seg));
                 own[j] = on ? x : zero;
-                prev[j] = onp ? y : zero;
+                if (DPP) {
+                    // the previous 16 bytes are lane l - 1's: one DPP shift per
+                    // dword instead of a second (L1-hit) load per lane; lane 0
+                    // loads the chunk's preceding group (first half) or takes
+                    // lane 63's of the first half
+                    uint4 y = dpp_shr1(own[j]);
+                    if (g == 0) {
+                        if (lane == 0 && onp) y = ld16(reinterpret_cast<const uint4*>(row + cb - 16));
+                    } else if (lane == 0) {
+                        y = last[j];
+                    }
+                    prev[j] = onp ? y : zero;
+                } else {
+                    const uint4 y = ld16(reinterpret_cast<const uint4*>(onp ? row + cb - 16 : seg));
+                    prev[j] = onp ? y : zero;
+                }
+            }
+            if (DPP && g == 0) {
+#pragma unroll
+                for (int j = 0; j < RJ; ++j)
+                    last[j] = make_uint4(__builtin_amdgcn_readlane(own[j].x, 63), __builtin_amdgcn_readlane(own[j].y, 63),
+                                         __builtin_amdgcn_readlane(own[j].z, 63), __builtin_amdgcn_readlane(own[j].w, 63));
             }
             if (ABL == 1) {  // timing ablation: stream only
 #pragma unroll
@@ -997,7 +1098,7 @@ struct BandLds {
 };
 
 // grid row y of the band launch -> segment and its chunk
-template <int ABL, int ROWS>
+template <int ABL, int ROWS, bool DPP = true>
 __device__ __forceinline__ void band_any(const BandSegs& S, int rblk, int y, BandLds<ROWS>& L, long long nloc,
                                          long long row_lo, long long n_bins, const uint8_t* __restrict__ act,
                                          const uint16_t* __restrict__ row_group, const double* __restrict__ b,
@@ -1007,19 +1108,19 @@ __device__ __forceinline__ void band_any(const BandSegs& S, int rblk, int y, Ban
     while (k + 1 < S.n && c >= S.s[k + 1].ch) ++k;
     const BandSeg P = S.s[k];
     if (P.bits == 8)
-        band_block<8, ABL, ROWS>(P, rblk, c - P.ch, L.bl, L.ract, nloc, row_lo, n_bins, act, row_group, b, bpart);
+        band_block<8, ABL, ROWS, DPP>(P, rblk, c - P.ch, L.bl, L.ract, nloc, row_lo, n_bins, act, row_group, b, bpart);
     else
-        band_block<4, ABL, ROWS>(P, rblk, c - P.ch, L.bl, L.ract, nloc, row_lo, n_bins, act, row_group, b, bpart);
+        band_block<4, ABL, ROWS, DPP>(P, rblk, c - P.ch, L.bl, L.ract, nloc, row_lo, n_bins, act, row_group, b, bpart);
 }
 
-template <int ABL, int ROWS>
+template <int ABL, int ROWS, bool DPP = true>
 __global__ __launch_bounds__(kBandThreads, 4) void k_sweep_bands(BandSegs S, long long nloc, long long row_lo,
                                                               long long n_bins, const uint8_t* __restrict__ act,
                                                               const uint16_t* __restrict__ row_group,
                                                               const double* __restrict__ b,
                                                               double* __restrict__ bpart) {
     __shared__ BandLds<ROWS> L;
-    band_any<ABL, ROWS>(S, blockIdx.x, blockIdx.y, L, nloc, row_lo, n_bins, act, row_group, b, bpart);
+    band_any<ABL, ROWS, DPP>(S, blockIdx.x, blockIdx.y, L, nloc, row_lo, n_bins, act, row_group, b, bpart);
 }
 
 // Small matrices (one chromosome, a shard of a few hundred MB): the whole
@@ -1483,7 +1584,11 @@ namespace hh {
 
 // Tuning knobs (hh_tune; no effect on results except the ablations).
 static int g_sweep_nb = 2;
-static int g_flatw_u = 8;  // uint4 per lane per step in k_sweep_flatw (8 or 16)
+static int g_flatw_u = 8;     // uint4 per lane per step in k_sweep_flatw (8 or 16)
+static int g_band_dpp = 0;    // band sweep: a lane's previous 16 bytes by DPP shift (0: a second load;
+                              // measured 4.34 vs 4.44 ms C4 sweep, profiles/r3_band_dpp_ab.log)
+static int g_flatw_pipe = 2;  // k_sweep_flatw: 1 = the next run's loads before the current step's walk,
+                              // 2 = and the next tile's first runs before the current tile's row sums go out
 static int g_sweep_ablate = 0;
 // Default: three streams per sweep -- band kernels (side), tiled kernel (side2),
 // flat kernel (main) -- so each kernel's ramp and tail overlap the others'
@@ -1513,12 +1618,12 @@ static void launch_sweep(const hh_matrix* m, const uint8_t* act, const double* b
         hipLaunchKernelGGL((k_sweep_tiled<NB, ABL>), dim3((unsigned)n_tiled), dim3(kSweepThreads), 0, s_tiled,
                            m->dev(), act, n_tiled, b, (long long)m->n_bins, part);
     if (n_flat && m->n_fgroups) {
-        if (g_flatw_u == 16)
-            hipLaunchKernelGGL((k_sweep_flatw<16, ABL>), dim3((unsigned)m->n_fgroups), dim3(kSweepThreads), 0, s,
-                               m->dev(), act, b, (long long)m->n_bins, part);
-        else
-            hipLaunchKernelGGL((k_sweep_flatw<kFlatU, ABL>), dim3((unsigned)m->n_fgroups), dim3(kSweepThreads), 0, s,
-                               m->dev(), act, b, (long long)m->n_bins, part);
+        auto kern = g_flatw_u == 16 ? (g_flatw_pipe == 2 ? k_sweep_flatw<16, ABL, 2>
+                                       : g_flatw_pipe == 1 ? k_sweep_flatw<16, ABL, 1> : k_sweep_flatw<16, ABL, 0>)
+                    : (g_flatw_pipe == 2 ? k_sweep_flatw<kFlatU, ABL, 2>
+                       : g_flatw_pipe == 1 ? k_sweep_flatw<kFlatU, ABL, 1> : k_sweep_flatw<kFlatU, ABL, 0>);
+        hipLaunchKernelGGL(kern, dim3((unsigned)m->n_fgroups), dim3(kSweepThreads), 0, s, m->dev(), act, b,
+                           (long long)m->n_bins, part);
     } else if (n_flat) {
         hipLaunchKernelGGL((k_sweep_flat<kFlatU, ABL>), dim3((unsigned)n_flat), dim3(kSweepThreads), 0, s, m->dev(),
                            act, n_flat, n_tiled, b, (long long)m->n_bins, part);
@@ -1595,7 +1700,8 @@ static void sweep_band(hh_ice* S, hipStream_t s) {
         const unsigned rb = (unsigned)((S->nloc + rows - 1) / rows);
         auto kern = rows == 64    ? (abl ? k_sweep_bands<1, 64> : k_sweep_bands<0, 64>)
                     : rows == 128 ? (abl ? k_sweep_bands<1, 128> : k_sweep_bands<0, 128>)
-                                  : (abl ? k_sweep_bands<1, 256> : k_sweep_bands<0, 256>);
+                                  : (abl ? k_sweep_bands<1, 256>
+                                         : (g_band_dpp ? k_sweep_bands<0, 256, true> : k_sweep_bands<0, 256, false>));
         hipLaunchKernelGGL(kern, dim3(rb, (unsigned)nc), dim3(kBandThreads), 0, s, L, (long long)S->nloc,
                            (long long)m->row_lo, (long long)m->n_bins, S->act(), m->row_group.p, S->bias.p,
                            S->bpart.p);
@@ -1797,6 +1903,12 @@ int hh_tune(const char* key, int64_t value) {
         } else if (k == "flat_cols") {
             HH_REQUIRE(value == 0 || value == 1, "flat_cols in {0, 1}");
             g_flat_cols = value;
+        } else if (k == "flatw_pipe") {
+            HH_REQUIRE(value >= 0 && value <= 2, "flatw_pipe in {0, 1, 2}");
+            g_flatw_pipe = (int)value;
+        } else if (k == "band_dpp") {
+            HH_REQUIRE(value == 0 || value == 1, "band_dpp in {0, 1}");
+            g_band_dpp = (int)value;
         } else if (k == "flatw_u") {
             HH_REQUIRE(value == 8 || value == 16, "flatw_u in {8, 16}");
             g_flatw_u = (int)value;
