@@ -318,9 +318,15 @@ __global__ void k_corr_norm_oop(const double* __restrict__ Cov, long long n, lon
 // waves are reduced in LDS in wave order and each K split writes its own
 // partial, summed in split order by k_cor_mul_sum (deterministic).
 // Cor is ld x ld with zero padding, so only V needs a bound check.
+// FUSE: the K splits of a 64-row tile also sum themselves: every split block
+// publishes its partial and counts in; the last one to arrive adds the ks
+// partials in split order (the same order as k_cor_mul_sum: deterministic)
+// into Y and re-arms the tile's counter -- no second launch.
+template <bool FUSE = false>
 __global__ __launch_bounds__(256) void k_cor_mul_part(const double* __restrict__ Cor, long long ldc, long long n,
                                                       const double* __restrict__ V, int ksteps,
-                                                      double* __restrict__ part) {
+                                                      double* __restrict__ part, unsigned* __restrict__ cnt = nullptr,
+                                                      double* __restrict__ Y = nullptr) {
     __shared__ double red[3][16 * 64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const long long i0 = (long long)blockIdx.x * 64;
@@ -378,6 +384,39 @@ __global__ __launch_bounds__(256) void k_cor_mul_part(const double* __restrict__
                 const double v = ((acc[t][reg] + red[0][q]) + red[1][q]) + red[2][q];
                 out[(4 * ((lane >> 4) + 4 * reg) + t) * kSB + (lane & 15)] = v;
             }
+        if (FUSE) __threadfence();  // this split's partial visible device-wide
+    }
+    if (FUSE) {
+        __shared__ int last;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const unsigned old = atomicAdd(cnt + blockIdx.x, 1u);
+            last = old == gridDim.y - 1;
+            if (last) {
+                __threadfence();  // acquire the other splits' partials
+                cnt[blockIdx.x] = 0u;
+            }
+        }
+        __syncthreads();
+        if (last) {
+            const int ks = (int)gridDim.y;
+            for (int e = threadIdx.x; e < 64 * kSB; e += 256) {
+                const long long i = i0 + e / kSB;
+                if (i >= n) continue;
+                const double* pp = part + (i0 * kSB + e);
+                double acc = 0.0;
+                int sp = 0;
+                for (; sp + 8 <= ks; sp += 8) {
+                    double v[8];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) v[u] = pp[(size_t)(sp + u) * ldc * kSB];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) acc += v[u];
+                }
+                for (; sp < ks; ++sp) acc += pp[(size_t)sp * ldc * kSB];
+                Y[i * kSB + e % kSB] = acc;
+            }
+        }
     }
 }
 
@@ -621,6 +660,7 @@ struct PcaWork {
     long long n = 0, ldc = 0;
     int nblk = 0, ks = 1, ksteps = 1;
     DBuf<double> part, G, R, mpart;
+    DBuf<unsigned> mcnt;  // per 64-row tile: K splits arrived (k_cor_mul_part<true>)
     std::vector<double> hG;
     PcaWork(long long n_, long long ldc_) : n(n_), ldc(ldc_) {
         nblk = (int)std::max<long long>(1, (n + kGramRows - 1) / kGramRows);
@@ -635,6 +675,8 @@ struct PcaWork {
         ksteps = (int)((steps + want - 1) / want);
         ks = (int)((steps + ksteps - 1) / ksteps);
         mpart.alloc((size_t)ks * ldc * kSB);
+        mcnt.alloc((size_t)rb);
+        HIP_CHECK(hipMemset(mcnt.p, 0, sizeof(unsigned) * rb));
     }
     // G = X^T Y on the device (B x B), fixed-order reduction
     void gram_dev(const double* X, const double* Y, hipStream_t s) {
@@ -651,11 +693,17 @@ struct PcaWork {
     void cor_mul(const double* Cor, const double* V, const double* x, bool d_use, double* Y, hipStream_t s) {
         {
             HH_KTIME("k_cor_mul", s);
-            hipLaunchKernelGGL(k_cor_mul_part, dim3((unsigned)(ldc / 64), (unsigned)ks), dim3(256), 0, s, Cor, ldc, n, V,
-                               ksteps, mpart.p);
+            hipLaunchKernelGGL(k_cor_mul_part<false>, dim3((unsigned)(ldc / 64), (unsigned)ks), dim3(256), 0, s, Cor, ldc,
+                               n, V, ksteps, mpart.p, nullptr, nullptr);
         }
         hipLaunchKernelGGL(k_cor_mul_sum, dim3((unsigned)((n * kSB + 255) / 256)), dim3(256), 0, s, mpart.p, ks, ldc, n,
                            x, d_use ? (const double*)G.p : nullptr, Y);
+    }
+    // Y = Cor V in one launch (the splits sum themselves)
+    void cor_mul_fused(const double* Cor, const double* V, double* Y, hipStream_t s) {
+        HH_KTIME("k_cor_mul", s);
+        hipLaunchKernelGGL(k_cor_mul_part<true>, dim3((unsigned)(ldc / 64), (unsigned)ks), dim3(256), 0, s, Cor, ldc, n,
+                           V, ksteps, mpart.p, mcnt.p, Y);
     }
     void put_small(const std::vector<double>& m, hipStream_t s) { R.upload(m.data(), m.size(), s); }
 };
@@ -927,6 +975,331 @@ __global__ void k_start_block(const double* __restrict__ X, long long n, double*
     out[t] = b == 0 ? 1.0 / sqrt((double)n) : X[i * kSB + b - 1];
 }
 
+// ------------------------------------ one-launch block orthogonalisation
+// The whole Gram-Schmidt + shifted CholeskyQR3 chain of one Krylov product
+// (or of a restart) in ONE launch instead of ~11: the chain is a sequence of
+// row-local steps separated by 16 x 16 (or nb x 16 x 16) reductions over all
+// rows, so a block owns 64 * TPB rows for the whole launch (kept in LDS) and
+// the reductions are grid-wide: per-block partials, a grid barrier, then a
+// fixed-order sum over the blocks (every block for a 16 x 16 Gram, a
+// reduce-scatter + second barrier for the nb x 16 x 16 projections).
+// Deterministic.  The per-block products run on v_mfma_f64_16x16x4f64:
+//   Gram / projection: A = X^T or Q^T (lane l: row 4c + l / 16, column l % 16),
+//   B = X (same lane map), D = 16 x 16 partial; X -= Q C: A = Q (16 rows),
+//   B = C.  D layout (f64): column = lane & 15, row = (lane >> 4) + 4 reg.
+// The grid is <= kOrthoMaxBlocks blocks of 256 threads (the chip holds
+// several such grids at once, one per stream), and every barrier wait is
+// bounded: a grid that cannot become co-resident sets *abort and runs to
+// its end (the host raises) instead of hanging.
+constexpr int kOrthoMaxBlocks = 64;
+constexpr int kOrthoMaxE = 8 * kSB * kSB;  // nb <= P <= 8 coefficient blocks
+enum { kOrthoFull = 0, kOrthoLast = 1, kOrthoStart = 2, kOrthoRitz = 3 };
+
+struct OrthoArgs {
+    const double* xin = nullptr;  // Full / Last: W = Cor Q_j; Start: the start block's rows
+    const double* Y = nullptr;    // Ritz: nb stacked 16 x 16 coefficient blocks
+    double* xout = nullptr;       // Ritz: X = Q Y out (the host's Ritz vectors)
+    const double* Q = nullptr;    // basis blocks (n x 16 each)
+    int nb = 0;
+    double* qnext = nullptr;       // Full: Q_{j+1}; Start / Ritz: Q_0
+    double *c1 = nullptr, *c2 = nullptr, *R = nullptr, *G = nullptr;  // small outputs (block 0)
+    int* fail = nullptr;           // one flag per Cholesky (written 0 / 1)
+    double *rpart = nullptr, *rout = nullptr, *gpart = nullptr;
+    unsigned long long* ctr = nullptr;  // barrier arrivals, monotone across launches
+    unsigned long long base = 0;
+    int* abort = nullptr;
+    long long n = 0;
+    int nblk = 0;
+    double shift_scale = 0.0;
+};
+
+// grid barrier (all blocks co-resident); bounded wait
+__device__ __forceinline__ void ortho_grid_sync(unsigned long long* ctr, unsigned long long target, int* abort) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();  // release this block's partials
+        atomicAdd(ctr, 1ull);
+        unsigned spins = 0;
+        while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            __builtin_amdgcn_s_sleep(1);
+            if ((++spins & 255u) == 0u &&
+                (spins >= (1u << 22) || __hip_atomic_load(abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+                atomicExch(abort, 1);
+                break;
+            }
+        }
+        __threadfence();  // acquire the other blocks' partials
+    }
+    __syncthreads();
+}
+
+template <int TPB>
+struct OrthoLds {
+    double x[TPB * 64][kSB + 1];  // the block's rows
+    double cm[kOrthoMaxE];        // reduced coefficients
+    double gs[kSB * kSB];         // reduced Gram
+    double ri[kSB * kSB];         // Cholesky factor R (upper, row-major)
+    double ws[4][kSB * kSB];      // per-wave MFMA partials
+};
+
+template <int MODE, int TPB>
+__global__ __launch_bounds__(256) void k_ortho(OrthoArgs A) {
+    constexpr int B = kSB, BB = kSB * kSB, RPB = 64 * TPB;
+    __shared__ OrthoLds<TPB> L;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6, lr = lane >> 4, lc = lane & 15;
+    const int nblk = A.nblk, g = blockIdx.x;
+    const long long n = A.n, r0 = (long long)g * RPB;
+    unsigned bar = 0;
+    auto gsync = [&]() {
+        ++bar;
+        ortho_grid_sync(A.ctr, A.base + (unsigned long long)bar * (unsigned long long)nblk, A.abort);
+    };
+    // ---- block-local pieces
+    auto gram_part = [&](double* dst) {  // dst[g][256] = X^T X over the block's rows
+        d4 acc = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int m = 0; m < TPB; ++m)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const double v = L.x[(w + 4 * m) * 16 + 4 * c + lr][lc];
+                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(v, v, acc, 0, 0, 0);
+            }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) L.ws[w][(lr + 4 * r) * B + lc] = acc[r];
+        __syncthreads();
+        dst[(size_t)g * BB + t] = ((L.ws[0][t] + L.ws[1][t]) + L.ws[2][t]) + L.ws[3][t];
+        __syncthreads();
+    };
+    auto proj_part = [&]() {  // rpart[g][k][256] = Q_k^T X over the block's rows; wave w: k = w, w + 4
+        for (int k = w; k < A.nb; k += 4) {
+            const double* Qk = A.Q + (size_t)k * n * B;
+            d4 acc = d4{0.0, 0.0, 0.0, 0.0};
+            constexpr int NC = RPB / 4;  // 4-row chunks of the block
+            constexpr int U = 16;
+#pragma unroll 1
+            for (int c0 = 0; c0 < NC; c0 += U) {
+                double q[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const long long i = r0 + 4 * (c0 + u) + lr;
+                    q[u] = i < n ? Qk[i * B + lc] : 0.0;
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+                    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(q[u], L.x[4 * (c0 + u) + lr][lc], acc, 0, 0, 0);
+            }
+            double* dst = A.rpart + (size_t)g * kOrthoMaxE + k * BB;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) dst[(lr + 4 * r) * B + lc] = acc[r];
+        }
+    };
+    // X (+|-)= sum_k Q_k cm_k over the block's rows (ADD: X = sum, X zero
+    // before); a k's 4 TPB loads in flight together, the next k's issued
+    // before this one's MFMAs
+    auto mul_q = [&](bool add) {
+        d4 acc[TPB];
+        double q[TPB][4], qn[TPB][4];
+        auto ld = [&](int k, double (&dst)[TPB][4]) {
+#pragma unroll
+            for (int m = 0; m < TPB; ++m) {
+                const long long i = r0 + (w + 4 * m) * 16 + lc;
+                const double* qr = A.Q + ((size_t)k * n + (i < n ? i : 0)) * B;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) dst[m][j] = i < n ? qr[4 * j + lr] : 0.0;
+            }
+        };
+#pragma unroll
+        for (int m = 0; m < TPB; ++m) acc[m] = d4{0.0, 0.0, 0.0, 0.0};
+        if (A.nb > 0) ld(0, q);
+        for (int k = 0; k < A.nb; ++k) {
+            if (k + 1 < A.nb) ld(k + 1, qn);
+#pragma unroll
+            for (int m = 0; m < TPB; ++m)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    acc[m] = __builtin_amdgcn_mfma_f64_16x16x4f64(q[m][j], L.cm[k * BB + (4 * j + lr) * B + lc],
+                                                                  acc[m], 0, 0, 0);
+#pragma unroll
+            for (int m = 0; m < TPB; ++m)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) q[m][j] = qn[m][j];
+        }
+#pragma unroll
+        for (int m = 0; m < TPB; ++m) {
+            const int rb = (w + 4 * m) * 16;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                double& x = L.x[rb + lr + 4 * r][lc];
+                x = add ? acc[m][r] : x - acc[m][r];
+            }
+        }
+        __syncthreads();
+    };
+    // L.gs = sum over blocks of gp (fixed block order), every block; all
+    // nblk loads in flight at once
+    auto reduce_gram = [&](const double* gp) {
+        double v[kOrthoMaxBlocks];
+#pragma unroll
+        for (int b = 0; b < kOrthoMaxBlocks; ++b) v[b] = b < nblk ? gp[(size_t)b * BB + t] : 0.0;
+        double acc = 0.0;
+#pragma unroll
+        for (int b = 0; b < kOrthoMaxBlocks; ++b) acc += v[b];  // trailing + 0.0: exact
+        L.gs[t] = acc;
+        __syncthreads();
+    };
+    // nb x 256 projection sums: barrier, reduce-scatter over the blocks,
+    // barrier, every block reads all of them into L.cm (block 0 also to `out`)
+    auto reduce_proj = [&](double* out) {
+        gsync();  // every block's partials are in
+        const int E = A.nb * BB, chunk = (E + nblk - 1) / nblk;
+        const int e1 = min(E, (g + 1) * chunk);
+        for (int e = g * chunk + t; e < e1; e += 256) {
+            double v[kOrthoMaxBlocks];
+#pragma unroll
+            for (int b = 0; b < kOrthoMaxBlocks; ++b) v[b] = b < nblk ? A.rpart[(size_t)b * kOrthoMaxE + e] : 0.0;
+            double acc = 0.0;
+#pragma unroll
+            for (int b = 0; b < kOrthoMaxBlocks; ++b) acc += v[b];
+            A.rout[e] = acc;
+        }
+        gsync();
+        for (int e = t; e < E; e += 256) {
+            const double v = A.rout[e];
+            L.cm[e] = v;
+            if (g == 0) out[e] = v;
+        }
+        __syncthreads();
+    };
+    // R = chol(L.gs + shift) in every wave (registers + shuffles), wave 0
+    // publishes it; not positive definite -> R = I and the flag
+    auto chol = [&](bool shifted, double* Rout, int* flag) {
+        double tr = 0.0;
+#pragma unroll
+        for (int i = 0; i < B; ++i) tr += L.gs[i * B + i];
+        const double shift = shifted ? A.shift_scale * tr : 0.0;
+        double gg[4], rrow[B];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) gg[q] = L.gs[(lr + 4 * q) * B + lc] + (lr + 4 * q == lc ? shift : 0.0);
+        bool okall = true;
+#pragma unroll
+        for (int j = 0; j < B; ++j) {
+            const double d = __shfl(gg[j >> 2], (j & 3) * 16 + j, 64);
+            const bool okd = d > 0;
+            okall = okall && okd;
+            const double rjj = okd ? sqrt(d) : 1.0;
+            const double gjc = __shfl(gg[j >> 2], (j & 3) * 16 + lc, 64);
+            const double rjc = lc == j ? rjj : (lc > j ? gjc / rjj : 0.0);
+            rrow[j] = rjc;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int a = lr + 4 * q;
+                const double rja = __shfl(rjc, a, 64);
+                if (a > j && lc > j) gg[q] -= rja * rjc;
+            }
+        }
+        if (t < B) {
+#pragma unroll
+            for (int j = 0; j < B; ++j) {
+                const double rv = okall ? rrow[j] : (j == lc ? 1.0 : 0.0);
+                L.ri[j * B + lc] = rv;
+                if (g == 0) Rout[j * B + lc] = rv;
+            }
+            if (t == 0 && g == 0) *flag = okall ? 0 : 1;
+        }
+        __syncthreads();
+    };
+    auto apply_rinv = [&]() {  // row <- row R^{-1} (forward substitution, a thread per row)
+        for (int r = t; r < RPB; r += 256) {
+            double x[B];
+#pragma unroll
+            for (int c = 0; c < B; ++c) {
+                double v = L.x[r][c];
+#pragma unroll
+                for (int a = 0; a < c; ++a) v -= x[a] * L.ri[a * B + c];
+                x[c] = v / L.ri[c * B + c];
+            }
+#pragma unroll
+            for (int c = 0; c < B; ++c) L.x[r][c] = x[c];
+        }
+        __syncthreads();
+    };
+    // one CholeskyQR pass on the rows (Gram -> barrier -> R -> X R^{-1});
+    // the Gram buffers alternate so a block's next partial never overwrites
+    // one another block may still be reading
+    unsigned gsel = 0;
+    auto cholqr = [&](bool shifted, double* Rout, int* flag) {
+        double* gp = A.gpart + (size_t)(gsel & 1u) * nblk * BB;
+        ++gsel;
+        gram_part(gp);
+        gsync();
+        reduce_gram(gp);
+        chol(shifted, Rout, flag);
+        apply_rinv();
+    };
+    auto store_rows = [&](double* dst) {
+        for (int e = t; e < RPB * B; e += 256) {
+            const long long i = r0 + e / B;
+            if (i < n) dst[i * B + e % B] = L.x[e / B][e % B];
+        }
+    };
+    // ---- the block's rows in
+    if (MODE != kOrthoRitz) {
+        for (int e = t; e < RPB * B; e += 256) {
+            const long long i = r0 + e / B;
+            L.x[e / B][e % B] = i < n ? A.xin[i * B + e % B] : 0.0;
+        }
+    } else {  // Ritz vectors X = Q Y out, then the start block [1 / sqrt(n) | X[:, 0..14]]
+        for (int e = t; e < A.nb * BB; e += 256) L.cm[e] = A.Y[e];
+        __syncthreads();
+        mul_q(true);
+        store_rows(A.xout);
+        __syncthreads();
+        const double c0 = 1.0 / sqrt((double)n);
+        for (int r = t; r < RPB; r += 256) {
+            const bool in = r0 + r < n;
+            for (int c = B - 1; c > 0; --c) L.x[r][c] = L.x[r][c - 1];
+            L.x[r][0] = in ? c0 : 0.0;
+        }
+    }
+    __syncthreads();
+    if (MODE == kOrthoFull) {
+        // pass A: X = W - Qa c1, shifted CholQR3 -> Q1 (factors R0..R2)
+        proj_part();
+        reduce_proj(A.c1);
+        mul_q(false);
+        cholqr(true, A.R, A.fail);
+        cholqr(true, A.R + BB, A.fail + 1);
+        cholqr(false, A.R + 2 * BB, A.fail + 2);
+        // pass B: X = Q1 - Qa c2, shifted CholQR3 -> Q_{j+1} (R3..R5)
+        proj_part();
+        reduce_proj(A.c2);
+        mul_q(false);
+        cholqr(true, A.R + 3 * BB, A.fail + 3);
+        cholqr(true, A.R + 4 * BB, A.fail + 4);
+        cholqr(false, A.R + 5 * BB, A.fail + 5);
+        store_rows(A.qnext);
+    } else if (MODE == kOrthoLast) {
+        // CGS2 coefficients of the last product and the Gram of its residual
+        proj_part();
+        reduce_proj(A.c1);
+        mul_q(false);
+        proj_part();
+        reduce_proj(A.c2);
+        mul_q(false);
+        gram_part(A.gpart);
+        gsync();
+        if (g == 0) {
+            reduce_gram(A.gpart);
+            A.G[t] = L.gs[t];
+        }
+    } else {
+        cholqr(true, A.R, A.fail);
+        cholqr(true, A.R + BB, A.fail + 1);
+        cholqr(false, A.R + 2 * BB, A.fail + 2);
+        store_rows(A.qnext);
+    }
+}
+
 // ---------------------------------------------- small symmetric eigen (host)
 // Householder tridiagonalisation T = Q^T A Q (Golub & Van Loan 8.3.1; A full
 // m x m row-major, destroyed), Q kept as reflectors (v_k, beta_k).
@@ -935,6 +1308,10 @@ struct Tridiag {
     std::vector<double> d, e, V, beta;  // e[i] = T[i+1][i]
 };
 static void tridiagonalize(int m, std::vector<double>& A, Tridiag& T) {
+    // only the lower triangle is read and updated (half the traffic of the
+    // full-matrix form; the m = 128 matrix does not fit L1): p = A22 v as
+    // one pass over the rows, each row giving a dot (j < i) and an axpy into
+    // p (j < i), four partial sums so the loops vectorise
     T.m = m;
     T.V.assign((size_t)m * m, 0.0);
     T.beta.assign(m, 0.0);
@@ -953,27 +1330,58 @@ static void tridiagonalize(int m, std::vector<double>& A, Tridiag& T) {
         T.beta[k] = beta;
         // A22 <- P A22 P, P = I - beta v v^T:  p = beta A22 v,
         // w = p - (beta / 2)(p^T v) v,  A22 -= v w^T + w v^T
+        const double* __restrict__ vr = v;
+        double* __restrict__ pr = p.data();
+        for (int i = k + 1; i < m; ++i) pr[i] = 0.0;
+        for (int i = k + 1; i < m; ++i) {
+            const double* __restrict__ ai = &A[(size_t)i * m];
+            const double vi = vr[i];
+            double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+            int j = k + 1;
+            for (; j + 4 <= i; j += 4) {
+                s0 += ai[j] * vr[j];
+                s1 += ai[j + 1] * vr[j + 1];
+                s2 += ai[j + 2] * vr[j + 2];
+                s3 += ai[j + 3] * vr[j + 3];
+                pr[j] += ai[j] * vi;
+                pr[j + 1] += ai[j + 1] * vi;
+                pr[j + 2] += ai[j + 2] * vi;
+                pr[j + 3] += ai[j + 3] * vi;
+            }
+            for (; j < i; ++j) {
+                s0 += ai[j] * vr[j];
+                pr[j] += ai[j] * vi;
+            }
+            pr[i] += ((s0 + s1) + (s2 + s3)) + ai[i] * vi;
+        }
         double pv = 0.0;
         for (int i = k + 1; i < m; ++i) {
-            double s = 0.0;
-            const double* ai = &A[(size_t)i * m];
-            for (int j = k + 1; j < m; ++j) s += ai[j] * v[j];
-            p[i] = beta * s;
-            pv += p[i] * v[i];
+            pr[i] *= beta;
+            pv += pr[i] * vr[i];
         }
-        for (int i = k + 1; i < m; ++i) w[i] = p[i] - 0.5 * beta * pv * v[i];
+        for (int i = k + 1; i < m; ++i) w[i] = pr[i] - 0.5 * beta * pv * vr[i];
+        const double* __restrict__ wr = w.data();
         for (int i = k + 1; i < m; ++i) {
-            double* ai = &A[(size_t)i * m];
-            for (int j = k + 1; j < m; ++j) ai[j] -= v[i] * w[j] + w[i] * v[j];
+            double* __restrict__ ai = &A[(size_t)i * m];
+            const double vi = vr[i], wi = wr[i];
+            for (int j = k + 1; j <= i; ++j) ai[j] -= vi * wr[j] + wi * vr[j];
         }
         A[(size_t)(k + 1) * m + k] = mu;
-        A[(size_t)k * m + k + 1] = mu;
-        for (int i = k + 2; i < m; ++i) A[(size_t)i * m + k] = A[(size_t)k * m + i] = 0.0;
+        for (int i = k + 2; i < m; ++i) A[(size_t)i * m + k] = 0.0;
     }
     T.d.resize(m);
     T.e.assign(m, 0.0);
     for (int i = 0; i < m; ++i) T.d[i] = A[(size_t)i * m + i];
     for (int i = 0; i + 1 < m; ++i) T.e[i] = A[(size_t)(i + 1) * m + i];
+}
+
+// sqrt(a^2 + b^2) without std::hypot's cost (a libm call per QL rotation was
+// half the host eigen time); scaled form only when a square could overflow
+static inline double fast_hypot(double a, double b) {
+    a = std::fabs(a);
+    b = std::fabs(b);
+    if (a < 1e150 && b < 1e150) return std::sqrt(a * a + b * b);
+    return std::hypot(a, b);
 }
 
 // eigenvalues of the symmetric tridiagonal (d, e) by implicit-shift QL
@@ -988,14 +1396,14 @@ static std::vector<double> tridiag_eigvals(std::vector<double> d, std::vector<do
             }
             if (mm == l) break;
             double g = (d[l + 1] - d[l]) / (2.0 * e[l]);
-            double r = std::hypot(g, 1.0);
+            double r = fast_hypot(g, 1.0);
             g = d[mm] - d[l] + e[l] / (g + (g >= 0 ? r : -r));
             double s = 1.0, c = 1.0, p = 0.0;
             int i = mm - 1;
             bool underflow = false;
             for (; i >= l; --i) {
                 const double f = s * e[i], b = c * e[i];
-                r = std::hypot(f, g);
+                r = fast_hypot(f, g);
                 e[i + 1] = r;
                 if (r == 0.0) {
                     d[i + 1] -= p;
@@ -1205,6 +1613,48 @@ static bool pca_krylov(PcaWork& wk, const double* cor, long long n, int k, doubl
     auto qreduce = [&](int nb, double* out) {  // c = sum of the qpart partials
         hipLaunchKernelGGL(k_gram_ms, dim3((unsigned)(nb * BB)), dim3(64), 0, s, qpart.p, nap, out);
     };
+    // one-launch orthogonalisation (k_ortho): a block owns 64 * tpb rows
+    const int tpb = nap <= 4 * kOrthoMaxBlocks ? 4 : 8;
+    const int oblk = (nap + tpb - 1) / tpb;
+    const bool coop = g_pca_coop && oblk <= kOrthoMaxBlocks;
+    DBuf<double> orp(coop ? (size_t)oblk * kOrthoMaxE : 1), oro(kOrthoMaxE), ogp(coop ? (size_t)2 * oblk * BB : 1);
+    DBuf<unsigned long long> octr(1);
+    octr.zero(s);
+    unsigned long long obase = 0;
+    int* abort_flag = fail.p + P * 8 + 7;
+    auto ortho = [&](int mode, OrthoArgs a, int nbar) {
+        a.Q = Q.p;
+        a.rpart = orp.p;
+        a.rout = oro.p;
+        a.gpart = ogp.p;
+        a.ctr = octr.p;
+        a.base = obase;
+        a.abort = abort_flag;
+        a.n = n;
+        a.nblk = oblk;
+        a.shift_scale = shift_scale;
+        HH_REQUIRE(a.nb >= 0 && a.nb <= 8 && oblk >= 1 && oblk <= kOrthoMaxBlocks, "k_ortho shape");
+        const dim3 grid((unsigned)oblk), blk(256);
+#define HH_ORTHO(M)                                                  \
+    do {                                                             \
+        if (tpb == 4) hipLaunchKernelGGL((k_ortho<M, 4>), grid, blk, 0, s, a); \
+        else hipLaunchKernelGGL((k_ortho<M, 8>), grid, blk, 0, s, a);          \
+    } while (0)
+        switch (mode) {
+            case kOrthoFull: HH_ORTHO(kOrthoFull); break;
+            case kOrthoLast: HH_ORTHO(kOrthoLast); break;
+            case kOrthoStart: HH_ORTHO(kOrthoStart); break;
+            default: HH_ORTHO(kOrthoRitz); break;
+        }
+#undef HH_ORTHO
+        HIP_CHECK(hipGetLastError());
+        obase += (unsigned long long)nbar * (unsigned long long)oblk;
+    };
+    auto check_abort = [&](const std::vector<int>& flags) {
+        if (coop && flags[P * 8 + 7])
+            throw Error(HH_ERR_HIP, "k_ortho: grid barrier timed out (blocks not co-resident); rerun with "
+                                    "hh_tune(\"pca_coop\", 0)");
+    };
     fail.zero(s);
     // start block: [1 / sqrt(n) | deterministic pseudo-random columns]; the
     // host source of the upload lives until the first cycle's synchronise
@@ -1214,8 +1664,17 @@ static bool pca_krylov(PcaWork& wk, const double* cor, long long n, int k, doubl
             for (int b = 0; b < B; ++b)
                 v0[i * B + b] = b == 0 ? 1.0 / std::sqrt((double)n) : (double)u01(mix64(0x5eedULL + i * B + b)) - 0.5;
         X.upload(v0.data(), v0.size(), s);
-        apply(X.p, 0, nullptr, nullptr, W.p, true, false);
-        scholqr3(W.p, Q.p, restartR, fail.p + P * 8, 0);
+        if (coop) {
+            OrthoArgs a;
+            a.xin = X.p;
+            a.qnext = Q.p;
+            a.R = restartR;
+            a.fail = fail.p + P * 8;
+            ortho(kOrthoStart, a, 3);
+        } else {
+            apply(X.p, 0, nullptr, nullptr, W.p, true, false);
+            scholqr3(W.p, Q.p, restartR, fail.p + P * 8, 0);
+        }
     }
     std::vector<double> cur((size_t)n * k), Xh((size_t)n * B);
     double last_bound = 1e300;
@@ -1223,14 +1682,32 @@ static bool pca_krylov(PcaWork& wk, const double* cor, long long n, int k, doubl
     bool done = false;
     while (!done && products + P <= max_products) {
         int pe = P;  // blocks of this cycle's basis
-        HIP_CHECK(hipMemsetAsync(fail.p, 0, sizeof(int) * P * 8, s));
+        if (!coop) HIP_CHECK(hipMemsetAsync(fail.p, 0, sizeof(int) * P * 8, s));  // k_ortho writes every flag
         for (int j = 0; j < P; ++j) {
             double* sl = smalls.p + (size_t)j * slot;
             double *c1 = sl, *c2 = sl + (size_t)P * BB, *R = sl + (size_t)2 * P * BB, *G = sl + (size_t)(2 * P + 6) * BB;
             double* Qj = Q.p + (size_t)j * n * B;
-            wk.cor_mul(cor, Qj, nullptr, false, W.p, s);
             ++products;
             const int nb = j + 1;
+            if (coop) {
+                wk.cor_mul_fused(cor, Qj, W.p, s);
+                OrthoArgs a;
+                a.xin = W.p;
+                a.nb = nb;
+                a.c1 = c1;
+                a.c2 = c2;
+                if (j < P - 1) {
+                    a.qnext = Q.p + (size_t)(j + 1) * n * B;
+                    a.R = R;
+                    a.fail = fail.p + j * 8;
+                    ortho(kOrthoFull, a, 10);
+                } else {
+                    a.G = G;
+                    ortho(kOrthoLast, a, 5);
+                }
+                continue;
+            }
+            wk.cor_mul(cor, Qj, nullptr, false, W.p, s);
             if (j < P - 1) {
                 // pass A: W1 = W - Qa c1 = Q1 RA;  pass B: W2 = Q1 - Qa c2 = Q_{j+1} RB
                 gram(Q.p, nb, W.p, c1);
@@ -1254,6 +1731,7 @@ static bool pca_krylov(PcaWork& wk, const double* cor, long long n, int k, doubl
         HIP_CHECK(hipStreamSynchronize(s));
         const auto c1 = std::chrono::steady_clock::now();
         const double t_w = std::chrono::duration<double, std::milli>(c1 - c0).count();
+        check_abort(hf);
         if (hf[P * 8] || hf[P * 8 + 1] || hf[P * 8 + 2]) return false;  // start block rank deficient
         for (int j = 0; j + 1 < P; ++j) {
             bool bad = false;
@@ -1340,16 +1818,7 @@ static bool pca_krylov(PcaWork& wk, const double* cor, long long n, int k, doubl
         const double t_e = std::chrono::duration<double, std::milli>(c3 - c2).count();
         // Ritz vectors X = Qa Y (top B), uploaded as nb stacked 16 x 16 blocks
         Ydev.upload(Y.data(), (size_t)mb * B, s);
-        hipLaunchKernelGGL(k_comb_mp, dim3(ge), dim3(256), 0, s, nullptr, Q.p, last + 1, Ydev.p, n, X.p);
-        X.download(Xh.data(), Xh.size(), s);
-        HIP_CHECK(hipStreamSynchronize(s));
         ++cycles;
-        for (int q = 0; q < k; ++q) {
-            double nn = 0.0;
-            for (long long i = 0; i < n; ++i) nn += Xh[i * B + q] * Xh[i * B + q];
-            const double inv = 1.0 / std::sqrt(nn);
-            for (long long i = 0; i < n; ++i) cur[q * n + i] = Xh[i * B + q] * inv;
-        }
         if (eigvals)
             for (int q = 0; q < k; ++q) eigvals[q] = ev[q];
         // Convergence from residuals of the PREVIOUS cycle's Ritz vectors:
@@ -1400,7 +1869,29 @@ static bool pca_krylov(PcaWork& wk, const double* cor, long long n, int k, doubl
             }
             last_bound = bound;
         }
-        if (!done) {
+        // Ritz vectors out (and, not done, the next cycle's start block Q_0
+        // from them: one k_ortho launch)
+        if (coop && !done) {
+            OrthoArgs a;
+            a.Y = Ydev.p;
+            a.nb = last + 1;
+            a.xout = X.p;
+            a.qnext = Q.p;
+            a.R = restartR;
+            a.fail = fail.p + P * 8;
+            ortho(kOrthoRitz, a, 3);
+        } else {
+            hipLaunchKernelGGL(k_comb_mp, dim3(ge), dim3(256), 0, s, nullptr, Q.p, last + 1, Ydev.p, n, X.p);
+        }
+        X.download(Xh.data(), Xh.size(), s);
+        HIP_CHECK(hipStreamSynchronize(s));
+        for (int q = 0; q < k; ++q) {
+            double nn = 0.0;
+            for (long long i = 0; i < n; ++i) nn += Xh[i * B + q] * Xh[i * B + q];
+            const double inv = 1.0 / std::sqrt(nn);
+            for (long long i = 0; i < n; ++i) cur[q * n + i] = Xh[i * B + q] * inv;
+        }
+        if (!done && !coop) {
             hipLaunchKernelGGL(k_start_block, dim3(ge), dim3(256), 0, s, X.p, n, T2.p);
             HIP_CHECK(hipMemsetAsync(fail.p + P * 8, 0, sizeof(int) * 8, s));
             apply(T2.p, 0, nullptr, nullptr, W.p, true, false);
@@ -1409,7 +1900,9 @@ static bool pca_krylov(PcaWork& wk, const double* cor, long long n, int k, doubl
     }
     // a budget-exhausted run leaves a restart block enqueued: drain the
     // stream before this function's buffers go back to the pool
+    fail.download(hf.data(), hf.size(), s);
     HIP_CHECK(hipStreamSynchronize(s));
+    check_abort(hf);
     if (!done) st.converged = 0;
     st.products = products;
     st.cycles = cycles;

@@ -1962,6 +1962,9 @@ int hh_tune(const char* key, int64_t value) {
             g_build_debug = value;
         } else if (k == "pca_debug") {
             g_pca_debug = (int)value;
+        } else if (k == "pca_coop") {
+            HH_REQUIRE(value == 0 || value == 1, "pca_coop in {0, 1}");
+            g_pca_coop = (int)value;
         } else if (k == "pca_p") {
             HH_REQUIRE(value >= 2 && value <= 8, "pca_p in [2, 8]");
             g_pca_p = (int)value;

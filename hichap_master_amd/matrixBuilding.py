@@ -253,11 +253,8 @@ def GenomeWideMatrixCorrection(Bins_Pos, Hap_Bins_Pos, T_M, H_M):
         gap = np.nonzero(cov < 0.1)[0]              # Gap_definedLowRes (:742-753)
         non_gap = _non_gap(L, gap)
         Beta[chro] = _snp_alpha(h_sum[ms:me + 1], h_sum[ps:pe + 1], t_sum[s:e + 1], non_gap)
-    Alpha = []
-    for i in Sort_Chromosomes(list(Beta.keys())):
-        Alpha.extend(Beta[i])
-    Alpha += Alpha
-    return sym_vc_rescale(H_M, np.array(Alpha), None, h_full.sum())
+    Alpha = np.concatenate([Beta[i] for i in Sort_Chromosomes(list(Beta.keys()))]).astype(np.float64)
+    return sym_vc_rescale(H_M, np.concatenate([Alpha, Alpha]), None, h_full.sum())
 
 
 def _gw_layout(Bins_Pos, Hap_Bins_Pos):
@@ -318,11 +315,10 @@ def GenomeWideMatrixCorrectionSparse(Bins_Pos, Hap_Bins_Pos, T_pixels, H_cells, 
             cov = _coverage(L - t_nz[s:e + 1], L)
             gap = np.nonzero(cov < 0.1)[0]              # Gap_definedLowRes (:742-753)
             Beta[c] = _snp_alpha(h_bs[s:e + 1], h_bs[n + s:n + e + 1], t_sum[s:e + 1], _non_gap(L, gap))
-        Alpha = []
-        for i in Sort_Chromosomes(list(Beta.keys())):
-            Alpha.extend(Beta[i])
-        Alpha += Alpha
-        Alpha = np.ascontiguousarray(Alpha, dtype=np.float64)
+        # the reference's list extend + `Alpha += Alpha` (:887-890) as one
+        # concatenate: the same values without 600 k boxed floats (40 ms)
+        Alpha = np.concatenate([Beta[i] for i in Sort_Chromosomes(list(Beta.keys()))]).astype(np.float64)
+        Alpha = np.ascontiguousarray(np.concatenate([Alpha, Alpha]))
         m = C.c_int64(0)
         if device_result:  # int32 / int32 / float64 device tensors, written in place by the library
             import torch

@@ -191,3 +191,54 @@ def test_pca_krylov_matches_subspace_iteration():
     assert out[1][1]["method"] == "krylov" and out[0][1]["method"] == "subspace"
     assert out[1][1]["products"] < out[0][1]["products"] / 2
     np.testing.assert_allclose(_match_sign(out[1][0][0], out[0][0][0]), out[0][0][0], atol=1e-11)
+
+
+def _pca_run(dM, coop):
+    from hichap_master_amd._lib import call
+    from hichap_master_amd.StructureFind import StructureFind
+    call("hh_tune", b"pca_coop", coop)
+    try:
+        sf = StructureFind(Res=C5_RES)
+        dec, G, NG = sf.Distance_Decay(M=dM, G_array=None)
+        pcs, Cor, OE = sf.Get_PCA(distance_bin=dec.copy(), M=dM, NG_array=NG)
+        return np.asarray(pcs), dict(sf.pca_status)
+    finally:
+        call("hh_tune", b"pca_coop", 1)
+
+
+def test_pca_one_launch_orthogonalisation_matches_multilaunch():
+    """k_ortho (the Gram-Schmidt + shifted CholeskyQR3 chain of a product in
+    one launch, grid barriers between the reductions) against the multi-launch
+    chain on C5 chr21: same components / eigenvalues to rounding, and
+    bitwise run-to-run (fixed-order reductions)."""
+    dM = _c5_matrix(20)
+    p0, s0 = _pca_run(dM, 0)
+    p1, s1 = _pca_run(dM, 1)
+    p2, _ = _pca_run(dM, 1)
+    assert s0["converged"] and s1["converged"]
+    assert abs(s1["products"] - s0["products"]) <= 8, (s0, s1)
+    for q in range(3):
+        np.testing.assert_allclose(_match_sign(p1[q], p0[q]), p0[q], atol=1e-11)
+    np.testing.assert_allclose(s1["eigvals"], s0["eigvals"], rtol=1e-12)
+    np.testing.assert_array_equal(p1, p2)
+
+
+def test_pca_one_launch_large_rows_per_block():
+    """n = 16 500 > 64 blocks x 256 rows: the 512-rows-per-block variant.
+    Low-rank planted spectrum with exactly known eigenvectors."""
+    n = 16500
+    rng = np.random.default_rng(9)
+    Z = rng.standard_normal((n, 6))
+    Z -= Z.mean(axis=0)
+    U, _ = np.linalg.qr(Z)  # orthonormal, orthogonal to 1
+    s = np.array([9.0, 6.0, 4.0, 2.0, 1.5, 1.0])
+    Cor = (U * (s - 0.01)) @ U.T
+    Cor += np.eye(n) * 0.01
+    Cor -= 0.01 / n  # 0.01 (I - 1 1^T / n) + U (s - 0.01) U^T: zero column means
+    comp = _comp_with_cor(Cor)
+    del Cor
+    pcs, ev, _ = comp.pca(3)
+    assert comp.pca_status["converged"]
+    for q in range(3):
+        np.testing.assert_allclose(_match_sign(pcs[q], U[:, q]), U[:, q], atol=1e-11)
+    np.testing.assert_allclose(ev, s[:3] ** 2, rtol=1e-11)
