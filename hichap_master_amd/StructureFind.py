@@ -194,6 +194,42 @@ class DeviceOE:
         return out if dtype is None else out.astype(dtype)
 
 
+class _ThunkDict(dict):
+    """{chrom: matrix} whose values are made by a thunk on first access."""
+
+    def __init__(self):
+        super().__init__()
+        self._thunks = {}
+
+    def put(self, key, thunk):
+        self._thunks[key] = thunk
+
+    def __getitem__(self, key):
+        if not dict.__contains__(self, key):
+            if key not in self._thunks:
+                raise KeyError(key)
+            dict.__setitem__(self, key, self._thunks.pop(key)())
+        return dict.__getitem__(self, key)
+
+    def __contains__(self, key):
+        return dict.__contains__(self, key) or key in self._thunks
+
+    def keys(self):
+        return list(dict.keys(self)) + [k for k in self._thunks if not dict.__contains__(self, k)]
+
+    def __iter__(self):
+        return iter(self.keys())
+
+    def __len__(self):
+        return len(self.keys())
+
+    def items(self):
+        return [(k, self[k]) for k in self.keys()]
+
+    def values(self):
+        return [self[k] for k in self.keys()]
+
+
 class StructureFind(TADCalling):
     """Numeric part of HiCHap's StructureFind (StructureFind.py:27); the TAD
     HMM / boundary-rule methods come from ``tads.TADCalling``."""
@@ -379,6 +415,9 @@ class StructureFind(TADCalling):
         trad = self.Loading_Tranditional_PC(Tranditional_PC_file) if self.Allelic is not False else None
         self.chroms, self.Matrix_Dict = chroms, Matrix_Dict
         self.Compartment_Dict, self.RawPCA = {}, {}
+        # the gap-refilled O/E and correlation matrices (:550-554), made on
+        # first access from the device-held ones (Plot_Compartment reads them)
+        self.Cor_Martrix_Dict, self.OE_Matrix_Dict = _ThunkDict(), _ThunkDict()
         for chro in chroms:
             M = np.asarray(Matrix_Dict[chro], dtype=np.float64)
             distance_bin, Gap, NonGap = self.Distance_Decay(M=M, G_array=None)
@@ -392,7 +431,36 @@ class StructureFind(TADCalling):
                 self.RawPCA[chro] = raw
                 out[NonGap] = self.Select_Allelic_PC(raw, trad[chro[1:]])[NonGap]
             self.Compartment_Dict[chro] = out
+            self.OE_Matrix_Dict.put(chro, lambda M=M, X=OE_M, NG=NonGap: self.Refill_Gap(M, X, NG, "OE"))
+            self.Cor_Martrix_Dict.put(chro, lambda M=M, X=Cor_M, NG=NonGap: self.Refill_Gap(M, X, NG, "Cor"))
         return self.Compartment_Dict
+
+    def Refill_Gap(self, M1, M2, NonGap, dtype):
+        """Refill_Gap (StructureFind.py:463-488): the n x n correlation or the
+        N x n O/E columns back at the non-gap positions of an N x N zero
+        matrix.  'Cor': R[NG[i], NG[j]] = M2[j][i].  'OE': the reference
+        transposes its output inside the loop (:483-486), so row and column
+        writes alternate (row NG[0], column NG[1], row NG[2], ...; later writes
+        win) and the result is transposed when len(NonGap) is odd -- kept as
+        is, since Plot_Compartment draws exactly that."""
+        N = np.shape(M1)[0]
+        NG = np.asarray(NonGap, dtype=np.int64)
+        X = np.asarray(M2, dtype=np.float64)
+        R = np.zeros((N, N), dtype=np.float64)
+        if dtype == "Cor":
+            R[np.ix_(NG, NG)] = X.T
+        elif dtype == "OE":
+            XT = X.T
+            flip = False
+            for i in range(len(NG)):
+                if flip:
+                    R[:, NG[i]] = XT[i]
+                else:
+                    R[NG[i], :] = XT[i]
+                flip = not flip
+            if flip:
+                R = R.T
+        return R
 
     def OutPut_PC_To_txt(self, out):
         """``chrom<TAB>value`` per bin (StructureFind.py:557-576; haplotype

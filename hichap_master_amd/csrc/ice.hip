@@ -2315,20 +2315,48 @@ int hh_ice_balance_cis_local(hh_matrix* m, const hh_ice_opts* o, int32_t world, 
                              int32_t* iters, int32_t* converged, double* sweep_seconds, void* stream) {
     hh_ice* S = nullptr;
     int rc = guard([&] {
-        HH_REQUIRE(m && o && world >= 1 && (world == 1 || allgather), "bad arguments");
-        HH_REQUIRE(m->cis_only, "hh_ice_balance_cis_local balances cis-only matrices");
-        HH_REQUIRE(max_local_bins >= m->n_bins, "max_local_bins is below this rank's bins");
+        HH_REQUIRE(o && world >= 1 && (world == 1 || allgather), "bad arguments");
     });
     if (rc) return rc;
-    rc = hh_ice_create(m, o, &S);
-    if (rc) return rc;
     rc = guard([&] {
-        HH_REQUIRE(S->full(), "the local matrix must hold every one of its rows");
         hipStream_t s = as_stream(stream);
         auto ok = [](int r) { if (r) throw Error(r, hh_last_error()); };
-        ok(hh_ice_marg_local(S, 0, nullptr, stream));
-        ok(hh_ice_filter_nnz(S, stream));
-        ok(hh_ice_marg_local(S, 1, nullptr, stream));
+        // this rank's setup; a failure is agreed on through the all-gather
+        // before the MAD exchange, so the other ranks raise instead of
+        // waiting in it
+        int err_rc = 0;
+        std::string err;
+        try {
+            HH_REQUIRE(m, "null matrix");
+            HH_REQUIRE(m->cis_only, "hh_ice_balance_cis_local balances cis-only matrices");
+            HH_REQUIRE(max_local_bins >= m->n_bins, "max_local_bins is below this rank's bins");
+            ok(hh_ice_create(m, o, &S));
+            HH_REQUIRE(S->full(), "the local matrix must hold every one of its rows");
+            ok(hh_ice_marg_local(S, 0, nullptr, stream));
+            ok(hh_ice_filter_nnz(S, stream));
+            ok(hh_ice_marg_local(S, 1, nullptr, stream));
+        } catch (const Error& e) {
+            err_rc = e.code;
+            err = e.what();
+        } catch (const std::exception& e) {
+            err_rc = HH_ERR_STATE;
+            err = e.what();
+        }
+        if (world > 1) {
+            DBuf<double> sb(1), gb((size_t)world);
+            const double v = err_rc ? 0.0 : 1.0;
+            std::vector<double> h(world, 0.0);
+            HIP_CHECK(hipMemcpyAsync(sb.p, &v, sizeof(double), hipMemcpyHostToDevice, s));
+            const int r = allgather(sb.p, 1, gb.p, user, stream);
+            if (r) HH_THROW(r < 0 ? r : HH_ERR_HIP, std::string("all-gather callback failed: ") + hh_last_error());
+            gb.download(h.data(), world, s);
+            HIP_CHECK(hipStreamSynchronize(s));
+            for (int q = 0; q < world; ++q)
+                if (h[q] != 1.0 && !err_rc)
+                    HH_THROW(HH_ERR_STATE, "rank " + std::to_string(q) + " of " + std::to_string(world) +
+                                               " failed; the cis-only run stopped on every rank");
+        }
+        if (err_rc) throw Error(err_rc, err);
         auto gather = [&](const std::vector<double>& loc) {
             if (world == 1) return loc;
             DBuf<double> send, recv;
@@ -2359,7 +2387,7 @@ int hh_ice_balance_cis_local(hh_matrix* m, const hh_ice_opts* o, int32_t world, 
             *sweep_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         ok(hh_ice_finalize(S, weights, scale, var, iters, converged, stream));
     });
-    hh_ice_free(S);
+    if (S) hh_ice_free(S);
     return rc;
 }
 

@@ -7,6 +7,8 @@
 #include <cstdio>
 #include <cmath>
 #include <numeric>
+#include <exception>
+#include <mutex>
 #include <thread>
 
 #include "ice_internal.hpp"
@@ -71,6 +73,34 @@ struct BlockTiles {
     std::vector<uint8_t> flat;
     int64_t ent_total = 0, entn_total = 0;
 };
+
+// fn(0 .. n-1) on nt host threads (work-stealing counter); the first
+// exception any thread throws stops the others and is rethrown here after
+// the join, so it reaches guard() as an error code instead of
+// std::terminate (a throwing std::thread body).
+template <class F>
+static void parallel_blocks(int nt, int64_t n, F&& fn) {
+    std::atomic<int64_t> next{0};
+    std::exception_ptr err;
+    std::mutex mu;
+    auto work = [&] {
+        try {
+            for (int64_t i; (i = next.fetch_add(1)) < n;) fn(i);
+        } catch (...) {
+            std::lock_guard<std::mutex> lk(mu);
+            if (!err) err = std::current_exception();
+            next.store(n);
+        }
+    };
+    std::vector<std::thread> th;
+    try {
+        for (int t = 1; t < nt; ++t) th.emplace_back(work);
+    } catch (...) {  // thread creation failed: run on fewer threads
+    }
+    work();
+    for (auto& t : th) t.join();
+    if (err) std::rethrow_exception(err);
+}
 
 void plan_block(const uint16_t* cntw, const uint16_t* cntn, int64_t nloc, int32_t nJ, int64_t rb, BlockTiles& B) {
     std::vector<uint32_t> rp(kR + 1), rpn(kR + 1);
@@ -203,14 +233,7 @@ TilePlan plan_tiles(const uint16_t* cntw, const uint16_t* cntn, int64_t nloc, in
     {
         const int nt = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)std::thread::hardware_concurrency(),
                                                                      (int64_t)16, P.nrb}));
-        std::atomic<int64_t> next{0};
-        auto work = [&] {
-            for (int64_t rb; (rb = next.fetch_add(1)) < P.nrb;) plan_block(cntw, cntn, nloc, nJ, rb, blocks[rb]);
-        };
-        std::vector<std::thread> th;
-        for (int t = 1; t < nt; ++t) th.emplace_back(work);
-        work();
-        for (auto& t : th) t.join();
+        parallel_blocks(nt, P.nrb, [&](int64_t rb) { plan_block(cntw, cntn, nloc, nJ, rb, blocks[rb]); });
     }
     const auto tp1 = std::chrono::steady_clock::now();
     // concatenation in block order.  Its cost was first-touch page faults of
@@ -248,9 +271,7 @@ TilePlan plan_tiles(const uint16_t* cntw, const uint16_t* cntn, int64_t nloc, in
     {
         const int nt = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)std::thread::hardware_concurrency(),
                                                                      (int64_t)16, P.nrb}));
-        std::atomic<int64_t> next{0};
-        auto copy = [&] {
-            for (int64_t rb; (rb = next.fetch_add(1)) < P.nrb;) {
+        parallel_blocks(nt, P.nrb, [&](int64_t rb) {
                 const BlockTiles& B = blocks[rb];
                 const size_t t0 = t_off[rb];
                 std::copy(B.rp.begin(), B.rp.end(), P.tile_rp.begin() + t0 * (kR + 1));
@@ -259,12 +280,7 @@ TilePlan plan_tiles(const uint16_t* cntw, const uint16_t* cntn, int64_t nloc, in
                 std::copy(B.perm.begin(), B.perm.end(), P.tile_perm.begin() + t0 * 2 * kR);
                 std::copy(B.band.begin(), B.band.end(), P.tile_band.begin() + t0 * 2 * kBandSlots);
                 std::copy(B.frec.begin(), B.frec.end(), P.frec.begin() + f_off[rb]);
-            }
-        };
-        std::vector<std::thread> th;
-        for (int t = 1; t < nt; ++t) th.emplace_back(copy);
-        copy();
-        for (auto& t : th) t.join();
+        });
     }
     int64_t ent = 0, entn = 0;
     for (int64_t rb = 0; rb < P.nrb; ++rb) {

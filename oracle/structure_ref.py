@@ -180,6 +180,25 @@ def compartment(M):
     return out, k, pcs, C
 
 
+def refill_gap(M1, M2, NonGap, dtype):
+    """Refill_Gap (StructureFind.py:463-488), loop for loop -- including the
+    transpose inside the 'OE' loop (:483-486)."""
+    R = np.zeros(np.shape(M1), dtype=float)
+    if dtype == "Cor":
+        tmp = np.zeros((np.shape(M1)[0], np.shape(M2)[0]), dtype=float)
+        for i in range(len(NonGap)):
+            tmp[NonGap[i]] = M2[i]
+        tmp = tmp.T
+        for i in range(len(NonGap)):
+            R[NonGap[i]] = tmp[i]
+    elif dtype == "OE":
+        M2 = np.asarray(M2).T
+        for i in range(len(NonGap)):
+            R[NonGap[i]] = M2[i]
+            R = R.T
+    return R
+
+
 # ------------------------------------------------------------------- TAD / DI
 def get_gap(M, min_tad, res):
     """Get_Gap (StructureFind.py:721-751) plus the first/last-bin rule of

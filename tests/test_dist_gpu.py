@@ -100,6 +100,54 @@ def test_balance_sharded_two_processes(cis_only, impl):
     np.testing.assert_array_equal(ws[0], ws[1])
 
 
+def _fail_worker(rank, world, port, case, outdir):
+    """rank 1 hands hh_ice_balance_sharded a shard that does not match
+    rank_rows: both ranks must raise (agreed status), neither may hang in the
+    exchange."""
+    import torch
+    import torch.distributed as tdist
+    from hichap_master_amd import _lib, dist, ice
+    torch.cuda.set_device(0)
+    _lib.load()
+    _lib.call("hh_set_device", 0)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    tdist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        b1, b2, c, off = case
+        n = int(off[-1])
+        rr = dist.partition_rows(np.bincount(b1, minlength=n) + np.bincount(b2, minlength=n), world)
+        lo, hi = int(rr[rank]), int(rr[rank + 1])
+        if rank == 1:
+            lo += 5  # not the rows rank_rows gives this rank
+        m = ice.ContactMatrix.from_pixels(b1, b2, c, n, off, row_range=(lo, hi))
+        cx = dist.CapiExchange(rr, world, rank, backend="gloo")
+        msg = "no error"
+        try:
+            dist.balance_capi(m, ice.IceOptions(max_iters=50), cx, torch.cuda.current_stream().cuda_stream)
+        except Exception as e:  # noqa: BLE001
+            msg = str(e)
+        cx.close()
+        m.close()
+        with open(os.path.join(outdir, f"err{rank}.txt"), "w") as f:
+            f.write(msg)
+    finally:
+        tdist.destroy_process_group()
+
+
+def test_sharded_failure_on_one_rank_raises_everywhere():
+    import torch.multiprocessing as mp
+    from hichap_master_amd import _lib
+    _lib.require_gpu()
+    rng = np.random.default_rng(5)
+    case = synth.coo_genome([500, 300], rng, A=20.0, trans_density=0.01)
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_fail_worker, args=(2, _free_port(), case, d), nprocs=2, start_method="spawn")
+        e0 = open(os.path.join(d, "err0.txt")).read()
+        e1 = open(os.path.join(d, "err1.txt")).read()
+    assert "rank 1 of 2 failed" in e0, e0
+    assert "does not hold rank_rows" in e1, e1
+
+
 def test_library_rccl_communicator_world1():
     """hh_comm_* (the library-owned RCCL communicator) at world 1 on the box's
     one GPU, and the C++ sharded balance at world 1 equal to hh_ice_balance."""

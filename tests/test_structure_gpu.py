@@ -208,3 +208,20 @@ def test_sliding_approach_vs_oracle_larger_and_errors(SF):
     np.testing.assert_allclose(_match_sign(pcs[0], p_ref[0]), p_ref[0], atol=1e-8)
     with pytest.raises(IndexError):
         SF(Res=400000).Get_PCA(distance_bin=dec.copy(), M=M, NG_array=NG, SA=True)
+
+
+def test_compartment_keeps_refilled_cor_and_oe(SF, golden):
+    """Compartment() fills Cor_Martrix_Dict / OE_Matrix_Dict with the
+    gap-refilled matrices (StructureFind.py:550-554) that Plot_Compartment
+    reads: against the reference's golden Cor / O/E through the reference's
+    Refill_Gap loops (oracle)."""
+    g = golden("compartment_n150")
+    M = g["M"]
+    sf = SF(Res=100000)
+    sf.Compartment(Matrix_Dict={"chr1": M})
+    NG = g["NG"]
+    np.testing.assert_allclose(sf.Cor_Martrix_Dict["chr1"], structure_ref.refill_gap(M, g["Cor"], NG, "Cor"),
+                               rtol=0, atol=1e-12)
+    np.testing.assert_allclose(sf.OE_Matrix_Dict["chr1"], structure_ref.refill_gap(M, g["OE"], NG, "OE"),
+                               rtol=1e-12, atol=0)
+    assert list(sf.Cor_Martrix_Dict) == ["chr1"] and "chr1" in sf.OE_Matrix_Dict

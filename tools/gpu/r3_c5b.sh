@@ -5,6 +5,8 @@ O=gpurun_out/r3
 C=${1:-unknown}
 timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_c5_gpu.py -m gpu > $O/r3_c5b_tests.log 2>&1
 rc=$?; echo "c5 tests rc=$rc"; tail -2 $O/r3_c5b_tests.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_dist_gpu.py tests/test_structure_gpu.py -m gpu > $O/r3_distst_tests.log 2>&1
+rc=$?; echo "dist/structure tests rc=$rc"; tail -2 $O/r3_distst_tests.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python3 -u tools/pca_trace.py 21 1 --p 8 > $O/r3_c5b_trace.log 2>&1 || exit 1
 tail -2 $O/r3_c5b_trace.log
 timeout -k 10 400 python3 -u bench.py --config c5 --steps 5 --warmup 1 > $O/r3_c5b_bench.log 2>&1 || exit 1
