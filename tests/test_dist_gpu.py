@@ -116,11 +116,11 @@ def _fail_worker(rank, world, port, case, outdir):
         b1, b2, c, off = case
         n = int(off[-1])
         rr = dist.partition_rows(np.bincount(b1, minlength=n) + np.bincount(b2, minlength=n), world)
-        lo, hi = int(rr[rank]), int(rr[rank + 1])
-        if rank == 1:
-            lo += 5  # not the rows rank_rows gives this rank
-        m = ice.ContactMatrix.from_pixels(b1, b2, c, n, off, row_range=(lo, hi))
-        cx = dist.CapiExchange(rr, world, rank, backend="gloo")
+        m = ice.ContactMatrix.from_pixels(b1, b2, c, n, off, row_range=(int(rr[rank]), int(rr[rank + 1])))
+        rr_seen = np.array(rr, dtype=np.int64)
+        if rank == 1:  # this rank's rank_rows disagree with the shard it holds
+            rr_seen[1] = rr[1] - 512 if rr[1] >= 512 else rr[1] + 512
+        cx = dist.CapiExchange(rr_seen, world, rank, backend="gloo")
         msg = "no error"
         try:
             dist.balance_capi(m, ice.IceOptions(max_iters=50), cx, torch.cuda.current_stream().cuda_stream)
@@ -139,7 +139,7 @@ def test_sharded_failure_on_one_rank_raises_everywhere():
     from hichap_master_amd import _lib
     _lib.require_gpu()
     rng = np.random.default_rng(5)
-    case = synth.coo_genome([500, 300], rng, A=20.0, trans_density=0.01)
+    case = synth.coo_genome([900, 700], rng, A=20.0, trans_density=0.01)
     with tempfile.TemporaryDirectory() as d:
         mp.start_processes(_fail_worker, args=(2, _free_port(), case, d), nprocs=2, start_method="spawn")
         e0 = open(os.path.join(d, "err0.txt")).read()
