@@ -318,11 +318,6 @@ __global__ void k_corr_norm_oop(const double* __restrict__ Cov, long long n, lon
 // waves are reduced in LDS in wave order and each K split writes its own
 // partial, summed in split order by k_cor_mul_sum (deterministic).
 // Cor is ld x ld with zero padding, so only V needs a bound check.
-// FUSE: the K splits of a 64-row tile also sum themselves: every split block
-// publishes its partial and counts in; the last one to arrive adds the ks
-// partials in split order (the same order as k_cor_mul_sum: deterministic)
-// into Y and re-arms the tile's counter -- no second launch.
-template <bool FUSE = false>
 __global__ __launch_bounds__(256) void k_cor_mul_part(const double* __restrict__ Cor, long long ldc, long long n,
                                                       const double* __restrict__ V, int ksteps,
                                                       double* __restrict__ part, unsigned* __restrict__ cnt = nullptr,
@@ -384,39 +379,6 @@ __global__ __launch_bounds__(256) void k_cor_mul_part(const double* __restrict__
                 const double v = ((acc[t][reg] + red[0][q]) + red[1][q]) + red[2][q];
                 out[(4 * ((lane >> 4) + 4 * reg) + t) * kSB + (lane & 15)] = v;
             }
-        if (FUSE) __threadfence();  // this split's partial visible device-wide
-    }
-    if (FUSE) {
-        __shared__ int last;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            const unsigned old = atomicAdd(cnt + blockIdx.x, 1u);
-            last = old == gridDim.y - 1;
-            if (last) {
-                __threadfence();  // acquire the other splits' partials
-                cnt[blockIdx.x] = 0u;
-            }
-        }
-        __syncthreads();
-        if (last) {
-            const int ks = (int)gridDim.y;
-            for (int e = threadIdx.x; e < 64 * kSB; e += 256) {
-                const long long i = i0 + e / kSB;
-                if (i >= n) continue;
-                const double* pp = part + (i0 * kSB + e);
-                double acc = 0.0;
-                int sp = 0;
-                for (; sp + 8 <= ks; sp += 8) {
-                    double v[8];
-#pragma unroll
-                    for (int u = 0; u < 8; ++u) v[u] = pp[(size_t)(sp + u) * ldc * kSB];
-#pragma unroll
-                    for (int u = 0; u < 8; ++u) acc += v[u];
-                }
-                for (; sp < ks; ++sp) acc += pp[(size_t)sp * ldc * kSB];
-                Y[i * kSB + e % kSB] = acc;
-            }
-        }
     }
 }
 
@@ -660,7 +622,6 @@ struct PcaWork {
     long long n = 0, ldc = 0;
     int nblk = 0, ks = 1, ksteps = 1;
     DBuf<double> part, G, R, mpart;
-    DBuf<unsigned> mcnt;  // per 64-row tile: K splits arrived (k_cor_mul_part<true>)
     std::vector<double> hG;
     PcaWork(long long n_, long long ldc_) : n(n_), ldc(ldc_) {
         nblk = (int)std::max<long long>(1, (n + kGramRows - 1) / kGramRows);
@@ -675,8 +636,6 @@ struct PcaWork {
         ksteps = (int)((steps + want - 1) / want);
         ks = (int)((steps + ksteps - 1) / ksteps);
         mpart.alloc((size_t)ks * ldc * kSB);
-        mcnt.alloc((size_t)rb);
-        HIP_CHECK(hipMemset(mcnt.p, 0, sizeof(unsigned) * rb));
     }
     // G = X^T Y on the device (B x B), fixed-order reduction
     void gram_dev(const double* X, const double* Y, hipStream_t s) {
@@ -693,17 +652,11 @@ struct PcaWork {
     void cor_mul(const double* Cor, const double* V, const double* x, bool d_use, double* Y, hipStream_t s) {
         {
             HH_KTIME("k_cor_mul", s);
-            hipLaunchKernelGGL(k_cor_mul_part<false>, dim3((unsigned)(ldc / 64), (unsigned)ks), dim3(256), 0, s, Cor, ldc,
-                               n, V, ksteps, mpart.p, nullptr, nullptr);
+            hipLaunchKernelGGL(k_cor_mul_part, dim3((unsigned)(ldc / 64), (unsigned)ks), dim3(256), 0, s, Cor, ldc, n, V,
+                               ksteps, mpart.p);
         }
         hipLaunchKernelGGL(k_cor_mul_sum, dim3((unsigned)((n * kSB + 255) / 256)), dim3(256), 0, s, mpart.p, ks, ldc, n,
                            x, d_use ? (const double*)G.p : nullptr, Y);
-    }
-    // Y = Cor V in one launch (the splits sum themselves)
-    void cor_mul_fused(const double* Cor, const double* V, double* Y, hipStream_t s) {
-        HH_KTIME("k_cor_mul", s);
-        hipLaunchKernelGGL(k_cor_mul_part<true>, dim3((unsigned)(ldc / 64), (unsigned)ks), dim3(256), 0, s, Cor, ldc, n,
-                           V, ksteps, mpart.p, mcnt.p, Y);
     }
     void put_small(const std::vector<double>& m, hipStream_t s) { R.upload(m.data(), m.size(), s); }
 };
@@ -993,6 +946,7 @@ __global__ void k_start_block(const double* __restrict__ X, long long n, double*
 // its end (the host raises) instead of hanging.
 constexpr int kOrthoMaxBlocks = 64;
 constexpr int kOrthoMaxE = 8 * kSB * kSB;  // nb <= P <= 8 coefficient blocks
+constexpr double kOrthoFastRatio = 1e3;    // scholqr3's two-pass branch (see there)
 enum { kOrthoFull = 0, kOrthoLast = 1, kOrthoStart = 2, kOrthoRitz = 3 };
 
 struct OrthoArgs {
@@ -1005,19 +959,24 @@ struct OrthoArgs {
     double *c1 = nullptr, *c2 = nullptr, *R = nullptr, *G = nullptr;  // small outputs (block 0)
     int* fail = nullptr;           // one flag per Cholesky (written 0 / 1)
     double *rpart = nullptr, *rout = nullptr, *gpart = nullptr;
-    unsigned long long* ctr = nullptr;  // barrier arrivals, monotone across launches
-    unsigned long long base = 0;
+    unsigned long long* ctr = nullptr;  // two barrier-arrival counters: this launch uses ctr[par] (from 0)
+    int par = 0;                         // and zeroes ctr[1 - par] for the next one
     int* abort = nullptr;
     long long n = 0;
     int nblk = 0;
     double shift_scale = 0.0;
+    long long* tstamp = nullptr;  // pca_debug >= 2: block 0's clock at the start, around each barrier, at the end
 };
 
 // grid barrier (all blocks co-resident); bounded wait
 __device__ __forceinline__ void ortho_grid_sync(unsigned long long* ctr, unsigned long long target, int* abort) {
     __syncthreads();
     if (threadIdx.x == 0) {
-        __threadfence();  // release this block's partials
+        // release only: this block's partials reach memory.  No acquire
+        // fence afterwards -- it would invalidate the XCD's L2 and every Q
+        // row read of the next phase would go to HBM; the cross-block data
+        // are read with agent-scope atomic loads (ld_agent) instead
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         atomicAdd(ctr, 1ull);
         unsigned spins = 0;
         while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
@@ -1028,9 +987,20 @@ __device__ __forceinline__ void ortho_grid_sync(unsigned long long* ctr, unsigne
                 break;
             }
         }
-        __threadfence();  // acquire the other blocks' partials
     }
     __syncthreads();
+}
+
+// a coherent (L2-bypassing) load of another block's partial
+__device__ __forceinline__ double ld_agent(const double* p) {
+    return __hip_atomic_load(const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ double readlane_d(double v, int lane) {
+    const unsigned long long u = __double_as_longlong(v);
+    const unsigned lo = __builtin_amdgcn_readlane((unsigned)u, lane);
+    const unsigned hi = __builtin_amdgcn_readlane((unsigned)(u >> 32), lane);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
 
 template <int TPB>
@@ -1039,7 +1009,9 @@ struct OrthoLds {
     double cm[kOrthoMaxE];        // reduced coefficients
     double gs[kSB * kSB];         // reduced Gram
     double ri[kSB * kSB];         // Cholesky factor R (upper, row-major)
-    double ws[4][kSB * kSB];      // per-wave MFMA partials
+    double rd[kSB];               // 1 / R[c][c]
+    int ok;                       // the last Cholesky succeeded
+    double ws[4][kOrthoMaxE];     // per-wave MFMA partials (Gram: the first 256 of each)
 };
 
 template <int MODE, int TPB>
@@ -1050,9 +1022,16 @@ __global__ __launch_bounds__(256) void k_ortho(OrthoArgs A) {
     const int nblk = A.nblk, g = blockIdx.x;
     const long long n = A.n, r0 = (long long)g * RPB;
     unsigned bar = 0;
+    auto stamp = [&](int k) {
+        if (A.tstamp && g == 0 && t == 0) A.tstamp[k] = (long long)wall_clock64();
+    };
+    stamp(0);
+    if (g == 0 && t == 0) A.ctr[1 - A.par] = 0ull;  // the previous launch's counter (it has completed)
     auto gsync = [&]() {
         ++bar;
-        ortho_grid_sync(A.ctr, A.base + (unsigned long long)bar * (unsigned long long)nblk, A.abort);
+        stamp(2 * bar - 1);
+        ortho_grid_sync(A.ctr + A.par, (unsigned long long)bar * (unsigned long long)nblk, A.abort);
+        stamp(2 * bar);
     };
     // ---- block-local pieces
     auto gram_part = [&](double* dst) {  // dst[g][256] = X^T X over the block's rows
@@ -1070,59 +1049,74 @@ __global__ __launch_bounds__(256) void k_ortho(OrthoArgs A) {
         dst[(size_t)g * BB + t] = ((L.ws[0][t] + L.ws[1][t]) + L.ws[2][t]) + L.ws[3][t];
         __syncthreads();
     };
-    auto proj_part = [&]() {  // rpart[g][k][256] = Q_k^T X over the block's rows; wave w: k = w, w + 4
-        for (int k = w; k < A.nb; k += 4) {
-            const double* Qk = A.Q + (size_t)k * n * B;
-            d4 acc = d4{0.0, 0.0, 0.0, 0.0};
-            constexpr int NC = RPB / 4;  // 4-row chunks of the block
-            constexpr int U = 16;
-#pragma unroll 1
-            for (int c0 = 0; c0 < NC; c0 += U) {
-                double q[U];
+    // rpart[g][k][256] = Q_k^T X over the block's rows: each wave its row
+    // groups, four k at a time with all their loads in flight (one round
+    // trip per four k), the waves' partials summed in wave order
+    auto proj_part = [&]() {
+        const int nb = A.nb;
+        for (int kc = 0; kc < nb; kc += 4) {
+            d4 acc[4];
 #pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const long long i = r0 + 4 * (c0 + u) + lr;
-                    q[u] = i < n ? Qk[i * B + lc] : 0.0;
-                }
+            for (int kk = 0; kk < 4; ++kk) acc[kk] = d4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-                for (int u = 0; u < U; ++u)
-                    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(q[u], L.x[4 * (c0 + u) + lr][lc], acc, 0, 0, 0);
+            for (int m = 0; m < TPB; ++m) {
+                double q[4][4];
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) {
+                        const long long i = r0 + (w + 4 * m) * 16 + 4 * c + lr;
+                        q[kk][c] = (kc + kk < nb && i < n) ? A.Q[((size_t)(kc + kk) * n + i) * B + lc] : 0.0;
+                    }
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+                    for (int c = 0; c < 4; ++c)
+                        acc[kk] = __builtin_amdgcn_mfma_f64_16x16x4f64(q[kk][c], L.x[(w + 4 * m) * 16 + 4 * c + lr][lc],
+                                                                       acc[kk], 0, 0, 0);
             }
-            double* dst = A.rpart + (size_t)g * kOrthoMaxE + k * BB;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) dst[(lr + 4 * r) * B + lc] = acc[r];
+            for (int kk = 0; kk < 4; ++kk)
+                if (kc + kk < nb)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) L.ws[w][(kc + kk) * BB + (lr + 4 * r) * B + lc] = acc[kk][r];
         }
+        __syncthreads();
+        for (int e = t; e < nb * BB; e += 256)
+            A.rpart[(size_t)g * kOrthoMaxE + e] = ((L.ws[0][e] + L.ws[1][e]) + L.ws[2][e]) + L.ws[3][e];
+        __syncthreads();
     };
     // X (+|-)= sum_k Q_k cm_k over the block's rows (ADD: X = sum, X zero
-    // before); a k's 4 TPB loads in flight together, the next k's issued
-    // before this one's MFMAs
+    // before); four k at a time with all their loads in flight
     auto mul_q = [&](bool add) {
+        const int nb = A.nb;
         d4 acc[TPB];
-        double q[TPB][4], qn[TPB][4];
-        auto ld = [&](int k, double (&dst)[TPB][4]) {
+#pragma unroll
+        for (int m = 0; m < TPB; ++m) acc[m] = d4{0.0, 0.0, 0.0, 0.0};
+        for (int kc = 0; kc < nb; kc += 4) {
+            double q[TPB][4][4];
 #pragma unroll
             for (int m = 0; m < TPB; ++m) {
                 const long long i = r0 + (w + 4 * m) * 16 + lc;
-                const double* qr = A.Q + ((size_t)k * n + (i < n ? i : 0)) * B;
 #pragma unroll
-                for (int j = 0; j < 4; ++j) dst[m][j] = i < n ? qr[4 * j + lr] : 0.0;
+                for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+                    for (int jj = 0; jj < 4; ++jj)
+                        q[m][kk][jj] =
+                            (kc + kk < nb && i < n) ? A.Q[((size_t)(kc + kk) * n + i) * B + 4 * jj + lr] : 0.0;
             }
-        };
 #pragma unroll
-        for (int m = 0; m < TPB; ++m) acc[m] = d4{0.0, 0.0, 0.0, 0.0};
-        if (A.nb > 0) ld(0, q);
-        for (int k = 0; k < A.nb; ++k) {
-            if (k + 1 < A.nb) ld(k + 1, qn);
+            for (int kk = 0; kk < 4; ++kk) {
+                double bcol[4];
 #pragma unroll
-            for (int m = 0; m < TPB; ++m)
+                for (int jj = 0; jj < 4; ++jj)
+                    bcol[jj] = kc + kk < nb ? L.cm[(kc + kk) * BB + (4 * jj + lr) * B + lc] : 0.0;
 #pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    acc[m] = __builtin_amdgcn_mfma_f64_16x16x4f64(q[m][j], L.cm[k * BB + (4 * j + lr) * B + lc],
-                                                                  acc[m], 0, 0, 0);
+                for (int m = 0; m < TPB; ++m)
 #pragma unroll
-            for (int m = 0; m < TPB; ++m)
-#pragma unroll
-                for (int j = 0; j < 4; ++j) q[m][j] = qn[m][j];
+                    for (int jj = 0; jj < 4; ++jj)
+                        acc[m] = __builtin_amdgcn_mfma_f64_16x16x4f64(q[m][kk][jj], bcol[jj], acc[m], 0, 0, 0);
+            }
         }
 #pragma unroll
         for (int m = 0; m < TPB; ++m) {
@@ -1140,7 +1134,7 @@ __global__ __launch_bounds__(256) void k_ortho(OrthoArgs A) {
     auto reduce_gram = [&](const double* gp) {
         double v[kOrthoMaxBlocks];
 #pragma unroll
-        for (int b = 0; b < kOrthoMaxBlocks; ++b) v[b] = b < nblk ? gp[(size_t)b * BB + t] : 0.0;
+        for (int b = 0; b < kOrthoMaxBlocks; ++b) v[b] = b < nblk ? ld_agent(gp + (size_t)b * BB + t) : 0.0;
         double acc = 0.0;
 #pragma unroll
         for (int b = 0; b < kOrthoMaxBlocks; ++b) acc += v[b];  // trailing + 0.0: exact
@@ -1156,7 +1150,8 @@ __global__ __launch_bounds__(256) void k_ortho(OrthoArgs A) {
         for (int e = g * chunk + t; e < e1; e += 256) {
             double v[kOrthoMaxBlocks];
 #pragma unroll
-            for (int b = 0; b < kOrthoMaxBlocks; ++b) v[b] = b < nblk ? A.rpart[(size_t)b * kOrthoMaxE + e] : 0.0;
+            for (int b = 0; b < kOrthoMaxBlocks; ++b)
+                v[b] = b < nblk ? ld_agent(A.rpart + (size_t)b * kOrthoMaxE + e) : 0.0;
             double acc = 0.0;
 #pragma unroll
             for (int b = 0; b < kOrthoMaxBlocks; ++b) acc += v[b];
@@ -1164,7 +1159,7 @@ __global__ __launch_bounds__(256) void k_ortho(OrthoArgs A) {
         }
         gsync();
         for (int e = t; e < E; e += 256) {
-            const double v = A.rout[e];
+            const double v = ld_agent(A.rout + e);
             L.cm[e] = v;
             if (g == 0) out[e] = v;
         }
@@ -1172,39 +1167,51 @@ __global__ __launch_bounds__(256) void k_ortho(OrthoArgs A) {
     };
     // R = chol(L.gs + shift) in every wave (registers + shuffles), wave 0
     // publishes it; not positive definite -> R = I and the flag
+    // R = chol(L.gs + shift) in wave 0: lane c holds column c and the pivot
+    // row / diagonal come from their lanes by v_readlane (the loop indices are
+    // compile-time: no LDS round trip per step, as the shuffles were); not
+    // positive definite -> R = I and the flag
     auto chol = [&](bool shifted, double* Rout, int* flag) {
-        double tr = 0.0;
+        if (w == 0) {
+            double tr = 0.0;
 #pragma unroll
-        for (int i = 0; i < B; ++i) tr += L.gs[i * B + i];
-        const double shift = shifted ? A.shift_scale * tr : 0.0;
-        double gg[4], rrow[B];
+            for (int i = 0; i < B; ++i) tr += L.gs[i * B + i];
+            const double shift = shifted ? A.shift_scale * tr : 0.0;
+            const int c = lc;
+            double gcol[B], rcol[B];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) gg[q] = L.gs[(lr + 4 * q) * B + lc] + (lr + 4 * q == lc ? shift : 0.0);
-        bool okall = true;
-#pragma unroll
-        for (int j = 0; j < B; ++j) {
-            const double d = __shfl(gg[j >> 2], (j & 3) * 16 + j, 64);
-            const bool okd = d > 0;
-            okall = okall && okd;
-            const double rjj = okd ? sqrt(d) : 1.0;
-            const double gjc = __shfl(gg[j >> 2], (j & 3) * 16 + lc, 64);
-            const double rjc = lc == j ? rjj : (lc > j ? gjc / rjj : 0.0);
-            rrow[j] = rjc;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int a = lr + 4 * q;
-                const double rja = __shfl(rjc, a, 64);
-                if (a > j && lc > j) gg[q] -= rja * rjc;
-            }
-        }
-        if (t < B) {
+            for (int a = 0; a < B; ++a) gcol[a] = L.gs[a * B + c] + (a == c ? shift : 0.0);
+            bool okall = true;
 #pragma unroll
             for (int j = 0; j < B; ++j) {
-                const double rv = okall ? rrow[j] : (j == lc ? 1.0 : 0.0);
-                L.ri[j * B + lc] = rv;
-                if (g == 0) Rout[j * B + lc] = rv;
+                const double d = readlane_d(gcol[j], j);
+                const bool okd = d > 0;
+                okall = okall && okd;
+                // 1 / sqrt(d) from v_rsq_f64 + one Newton step (the serial
+                // chain was 16 x (sqrt + divide) = 5 us of the pass)
+                const double dd = okd ? d : 1.0;
+                double y = __builtin_amdgcn_rsq(dd);
+                y = y * fma(-0.5 * dd * y, y, 1.5);
+                const double rjj = dd * y;
+                const double rjc = c == j ? rjj : (c > j ? gcol[j] * y : 0.0);
+                rcol[j] = rjc;
+#pragma unroll
+                for (int a = j + 1; a < B; ++a) {
+                    const double rja = readlane_d(rjc, a);
+                    if (c > j) gcol[a] -= rja * rjc;
+                }
             }
-            if (t == 0 && g == 0) *flag = okall ? 0 : 1;
+            if (lane < B) {
+#pragma unroll
+                for (int j = 0; j < B; ++j) {
+                    const double rv = okall ? rcol[j] : (j == c ? 1.0 : 0.0);
+                    L.ri[j * B + c] = rv;
+                    if (g == 0) Rout[j * B + c] = rv;
+                }
+                L.rd[c] = 1.0 / (okall ? rcol[c] : 1.0);
+                if (lane == 0) L.ok = okall ? 1 : 0;
+                if (lane == 0 && g == 0) *flag = okall ? 0 : 1;
+            }
         }
         __syncthreads();
     };
@@ -1216,7 +1223,7 @@ __global__ __launch_bounds__(256) void k_ortho(OrthoArgs A) {
                 double v = L.x[r][c];
 #pragma unroll
                 for (int a = 0; a < c; ++a) v -= x[a] * L.ri[a * B + c];
-                x[c] = v / L.ri[c * B + c];
+                x[c] = v * L.rd[c];
             }
 #pragma unroll
             for (int c = 0; c < B; ++c) L.x[r][c] = x[c];
@@ -1229,12 +1236,44 @@ __global__ __launch_bounds__(256) void k_ortho(OrthoArgs A) {
     unsigned gsel = 0;
     auto cholqr = [&](bool shifted, double* Rout, int* flag) {
         double* gp = A.gpart + (size_t)(gsel & 1u) * nblk * BB;
+        const bool st = gsel == 1;  // pca_debug 2: the second pass in detail
         ++gsel;
+        if (st) stamp(40);
         gram_part(gp);
+        if (st) stamp(41);
         gsync();
+        if (st) stamp(42);
         reduce_gram(gp);
+        if (st) stamp(43);
         chol(shifted, Rout, flag);
+        if (st) stamp(44);
         apply_rinv();
+        if (st) stamp(45);
+    };
+    // shifted CholeskyQR3 -> R3[0..2]: when the first (shifted) factor is
+    // well conditioned (diagonal ratio < kOrthoFastRatio: the block had no
+    // rounding-level direction), one plain pass finishes it (CholQR2's
+    // regime) and the third factor is the identity; otherwise shifted,
+    // shifted, plain.  Every block takes the same branch (same R).
+    auto scholqr3 = [&](double* R3, int* fl) {
+        cholqr(true, R3, fl);
+        double mx = 0.0, mn = 1e300;
+#pragma unroll
+        for (int i = 0; i < B; ++i) {
+            const double v = fabs(L.ri[i * B + i]);
+            mx = fmax(mx, v);
+            mn = fmin(mn, v);
+        }
+        if (L.ok && mn > 0.0 && mx < kOrthoFastRatio * mn) {
+            cholqr(false, R3 + BB, fl + 1);
+            if (g == 0) {
+                R3[2 * BB + t] = (t / B == t % B) ? 1.0 : 0.0;
+                if (t == 0) fl[2] = 0;
+            }
+        } else {
+            cholqr(true, R3 + BB, fl + 1);
+            cholqr(false, R3 + 2 * BB, fl + 2);
+        }
     };
     auto store_rows = [&](double* dst) {
         for (int e = t; e < RPB * B; e += 256) {
@@ -1243,7 +1282,7 @@ __global__ __launch_bounds__(256) void k_ortho(OrthoArgs A) {
         }
     };
     // ---- the block's rows in
-    if (MODE != kOrthoRitz) {
+    if (MODE != kOrthoRitz) {  // W (Full / Last) or the start block
         for (int e = t; e < RPB * B; e += 256) {
             const long long i = r0 + e / B;
             L.x[e / B][e % B] = i < n ? A.xin[i * B + e % B] : 0.0;
@@ -1267,16 +1306,12 @@ __global__ __launch_bounds__(256) void k_ortho(OrthoArgs A) {
         proj_part();
         reduce_proj(A.c1);
         mul_q(false);
-        cholqr(true, A.R, A.fail);
-        cholqr(true, A.R + BB, A.fail + 1);
-        cholqr(false, A.R + 2 * BB, A.fail + 2);
+        scholqr3(A.R, A.fail);
         // pass B: X = Q1 - Qa c2, shifted CholQR3 -> Q_{j+1} (R3..R5)
         proj_part();
         reduce_proj(A.c2);
         mul_q(false);
-        cholqr(true, A.R + 3 * BB, A.fail + 3);
-        cholqr(true, A.R + 4 * BB, A.fail + 4);
-        cholqr(false, A.R + 5 * BB, A.fail + 5);
+        scholqr3(A.R + 3 * BB, A.fail + 3);
         store_rows(A.qnext);
     } else if (MODE == kOrthoLast) {
         // CGS2 coefficients of the last product and the Gram of its residual
@@ -1293,11 +1328,11 @@ __global__ __launch_bounds__(256) void k_ortho(OrthoArgs A) {
             A.G[t] = L.gs[t];
         }
     } else {
-        cholqr(true, A.R, A.fail);
-        cholqr(true, A.R + BB, A.fail + 1);
-        cholqr(false, A.R + 2 * BB, A.fail + 2);
+        scholqr3(A.R, A.fail);
         store_rows(A.qnext);
     }
+    stamp(39);
+    if (A.tstamp && g == 0 && t == 0) A.tstamp[38] = bar;
 }
 
 // ---------------------------------------------- small symmetric eigen (host)
@@ -1618,21 +1653,23 @@ static bool pca_krylov(PcaWork& wk, const double* cor, long long n, int k, doubl
     const int oblk = (nap + tpb - 1) / tpb;
     const bool coop = g_pca_coop && oblk <= kOrthoMaxBlocks;
     DBuf<double> orp(coop ? (size_t)oblk * kOrthoMaxE : 1), oro(kOrthoMaxE), ogp(coop ? (size_t)2 * oblk * BB : 1);
-    DBuf<unsigned long long> octr(1);
+    DBuf<unsigned long long> octr(2);
     octr.zero(s);
-    unsigned long long obase = 0;
+    int opar = 0;
     int* abort_flag = fail.p + P * 8 + 7;
+    DBuf<long long> tst(g_pca_debug >= 2 ? 48 : 1);
     auto ortho = [&](int mode, OrthoArgs a, int nbar) {
         a.Q = Q.p;
         a.rpart = orp.p;
         a.rout = oro.p;
         a.gpart = ogp.p;
         a.ctr = octr.p;
-        a.base = obase;
+        a.par = opar;
         a.abort = abort_flag;
         a.n = n;
         a.nblk = oblk;
         a.shift_scale = shift_scale;
+        a.tstamp = g_pca_debug >= 2 ? tst.p : nullptr;
         HH_REQUIRE(a.nb >= 0 && a.nb <= 8 && oblk >= 1 && oblk <= kOrthoMaxBlocks, "k_ortho shape");
         const dim3 grid((unsigned)oblk), blk(256);
 #define HH_ORTHO(M)                                                  \
@@ -1648,7 +1685,19 @@ static bool pca_krylov(PcaWork& wk, const double* cor, long long n, int k, doubl
         }
 #undef HH_ORTHO
         HIP_CHECK(hipGetLastError());
-        obase += (unsigned long long)nbar * (unsigned long long)oblk;
+        opar ^= 1;
+        if (a.tstamp) {
+            long long h[48];
+            tst.download(h, 48, s);
+            HIP_CHECK(hipStreamSynchronize(s));
+            fprintf(stderr, "[ortho] mode=%d nb=%d nblk=%d tpb=%d us:", mode, a.nb, oblk, tpb);
+            const int nb_ = (int)h[38];
+            h[2 * nb_ + 1] = h[39];
+            for (int q = 1; q <= 2 * nb_ + 1; ++q) fprintf(stderr, " %.1f", (h[q] - h[q - 1]) / 100.0);
+            fprintf(stderr, " | barriers %d total %.1f | pass: gram %.1f sync %.1f reduce %.1f chol %.1f apply %.1f\n",
+                    nb_, (h[39] - h[0]) / 100.0, (h[41] - h[40]) / 100.0, (h[42] - h[41]) / 100.0,
+                    (h[43] - h[42]) / 100.0, (h[44] - h[43]) / 100.0, (h[45] - h[44]) / 100.0);
+        }
     };
     auto check_abort = [&](const std::vector<int>& flags) {
         if (coop && flags[P * 8 + 7])
@@ -1690,7 +1739,10 @@ static bool pca_krylov(PcaWork& wk, const double* cor, long long n, int k, doubl
             ++products;
             const int nb = j + 1;
             if (coop) {
-                wk.cor_mul_fused(cor, Qj, W.p, s);
+                // W = Cor Q_j (split-K MFMA + its fixed-order sum: a block
+                // of k_ortho summing the splits itself was slower -- 32 CUs
+                // pulling 8 MB have too few bytes in flight)
+                wk.cor_mul(cor, Qj, nullptr, false, W.p, s);
                 OrthoArgs a;
                 a.xin = W.p;
                 a.nb = nb;
