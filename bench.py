@@ -89,7 +89,7 @@ def config(name, nnz=None):
     return sizes, dict(A=A, trans_density=td, comp_block=200, seed=20201015), label, target, tf
 
 
-SWEEP_KERNELS = ("k_sweep_tiled", "k_sweep_flat", "k_sweep_band")  # band: <8> once, <4> twice per sweep
+SWEEP_KERNELS = ("k_sweep_tiled", "k_sweep_flat", "k_sweep_band", "k_sweep_uband")  # symmetric band: <8> once, <4> twice per sweep; upper band: <8>, <4> once each
 
 
 def pmc_traffic(kernels=SWEEP_KERNELS):
@@ -1103,8 +1103,9 @@ def main():
     # a shard stores both triangles of its rows: its share of the 12 B/pixel
     # algorithmic traffic is half its stored entries (= nnz_upper at N=1)
     shard_pix = float(inf["nnz_upper"]) if world == 1 else 0.5 * float(inf["n_entries"])
-    shard = torch.tensor([sweep_ms / max(launches, 1), shard_pix,
-                          float(inf["payload_bytes"]) + 8.0 * 513 * inf["n_tiles"]],
+    # bytes the state's sweep kernels read: tiles + row pointers + the bands
+    # (their upper halves only with the upper-band sweep)
+    shard = torch.tensor([sweep_ms / max(launches, 1), shard_pix, float(st.swept_bytes())],
                          dtype=torch.float64, device="cuda")
     if torch.distributed.is_initialized():
         allsh = [torch.zeros_like(shard) for _ in range(world)]
@@ -1155,9 +1156,12 @@ def main():
             phys = traffic if traffic else real_b
             achieved = phys / sweep_avg / 1e9
             pb = inf["payload_bytes"]
-            out["roofline"] = {"bound": "hbm", "kernel": ("ice sweep span: k_sweep_flat | k_sweep_tiled | k_sweep_bands (uint8 + 2 x 4-bit segments) on three streams"
+            ub = st.swept_bytes() < pb  # the upper-band sweep reads half the bands
+            band_k = ("k_sweep_ubands (upper halves of the uint8 + 4-bit bands, each count to its row and column)"
+                      if ub else "k_sweep_bands (uint8 + 2 x 4-bit segments)")
+            out["roofline"] = {"bound": "hbm", "kernel": (f"ice sweep span: k_sweep_flatw | k_sweep_tiled | {band_k} on three streams"
                                          if pb >= (8 << 30) else
-                                         "ice sweep: k_sweep_tiled, k_sweep_flat, k_sweep_bands (uint8 + 2 x 4-bit segments) on one stream"
+                                         f"ice sweep: k_sweep_tiled, k_sweep_flatw, {band_k} on one stream"
                                          if pb >= (1 << 30) else
                                          "ice sweep: k_sweep_all (tiled + band + flat bodies in one launch)")
                                + " (HIP events around the sweep; rocprof per-sweep span: tools/sweep_span.py)",

@@ -1123,6 +1123,386 @@ __global__ __launch_bounds__(kBandThreads, 4) void k_sweep_bands(BandSegs S, lon
     band_any<ABL, ROWS, DPP>(S, blockIdx.x, blockIdx.y, L, nloc, row_lo, n_bins, act, row_group, b, bpart);
 }
 
+// ---------------------------------------------------------------- K1d
+// Upper-band sweep (hh_tune "uband", default on).
+// The band arrays hold both triangles (row r: diagonals -W..W); this sweep
+// reads only the upper half of every row (diagonals d >= 0: half the bytes)
+// and lets each count feed both marginals it belongs to: row r gets
+// cnt * b[r + d] (row part) and column r + d gets cnt * b[r] (column part),
+// from one load and one conversion.
+//
+// Work: one wave per (512-row block, chunk of 1008 slots); a workgroup is 4
+// consecutive row blocks (2048 rows, globally aligned) of one chunk.  A wave
+// walks its rows in groups of 16; row r = gb + m is read shifted back by m
+// slots (funnel shift of the lane's previous and own bytes), so lane l's 16
+// counts of every row of the group sit in the same 16 columns
+// gb + base + 16 l + [0, 16) (base = diagonal of the chunk's slot 0), and
+//   w[16]  (registers) the bias of those columns, shared by the 16 rows,
+//   c[16]  (registers) the columns' partial column sums: c += cnt * b[row].
+// Row part: a dot per row, reduced across the wave by a halving butterfly.
+// After a group the lane windows move up 16 columns = one lane: w and c move
+// down one lane (DPP wave_shl:1), the lowest lane's 16 sums are complete (the
+// head, written to LDS), lane 63 takes the new window and starts from 0.  After
+// the last group the lanes hold the partial sums of the next 1008 columns (the
+// tail): added to the workgroup's LDS column buffer in two rounds (even
+// waves, then odd: their tails are disjoint), giving H (the workgroup's 2048
+// columns) and T (the next 1008, which belong to the next workgroup's heads).
+// Every sum's order is fixed by global positions only: deterministic, and the
+// same in a shard, which sweeps (from a halo copy of the rows above it) every
+// workgroup whose columns reach its rows.
+constexpr int kUbRows = 512;                       // rows per wave task
+constexpr int kUbWaves = 4;                        // row blocks per workgroup
+constexpr int kUbThreads = 64 * kUbWaves;
+constexpr int kUbGroupRows = kUbRows * kUbWaves;   // rows per workgroup (global alignment)
+constexpr int kUbChunk = 1008;                     // slots per chunk = 63 data lanes x 16
+constexpr int kUbCols = kUbGroupRows + kUbChunk;   // LDS column buffer (doubles)
+constexpr int kMaxUbChunks = 40;
+
+struct UbSeg {
+    const uint8_t* loc;   // slot 0 of local row row_lo
+    const uint8_t* halo;  // slot 0 of halo row halo_lo (shards)
+    long long stride;     // bytes per row
+    long long dlo;        // diagonal of slot 0
+    int bytes;            // readable bytes of a row from slot 0 (zero padding included)
+    int nc, ch, bits;     // chunks, first chunk index, bits per count
+};
+struct UbSegs {
+    UbSeg s[2];
+    int n;
+    uint8_t ord[kMaxUbChunks];  // grid row -> chunk (heaviest first)
+};
+struct UbArgs {
+    long long row_lo, row_hi, halo_lo, nloc, g_lo;
+    const uint8_t* act;
+    const uint16_t* row_group;
+    const double* b;
+    double* upart;  // per chunk c: R (row parts) at 3c, H at 3c + 1, T at 3c + 2, nloc each
+};
+
+template <int BITS>
+struct UbT;
+template <>
+struct UbT<8> {
+    typedef uint4 V;
+    static constexpr int LB = 16;  // bytes per lane per row
+    static __device__ __forceinline__ V zero() { return make_uint4(0u, 0u, 0u, 0u); }
+    static __device__ __forceinline__ V ld(const uint8_t* p) { return ld16(reinterpret_cast<const uint4*>(p)); }
+    template <int M>
+    static __device__ __forceinline__ V shift(const V prev, const V own) {
+        if (M == 0) return own;
+        constexpr int B = 128 - 8 * M;
+        return band_shift_q<B / 32>(prev, own, B % 32);
+    }
+    static __device__ __forceinline__ uint32_t cnt(const V v, int k) {
+        const uint32_t x = k < 4 ? v.x : k < 8 ? v.y : k < 12 ? v.z : v.w;
+        return (x >> (8 * (k & 3))) & 0xFFu;
+    }
+};
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+template <>
+struct UbT<4> {
+    typedef uint2 V;
+    static constexpr int LB = 8;
+    static __device__ __forceinline__ V zero() { return make_uint2(0u, 0u); }
+    static __device__ __forceinline__ V ld(const uint8_t* p) {
+        const u32x2 v = *reinterpret_cast<const u32x2*>(p);
+        return make_uint2(v.x, v.y);
+    }
+    // nibbles [16 - M, 32 - M) of prev ++ own
+    template <int M>
+    static __device__ __forceinline__ V shift(const V prev, const V own) {
+        if (M == 0) return own;
+        constexpr int B = 64 - 4 * M, Q = B / 32, R = B % 32;
+        const uint32_t d[4] = {prev.x, prev.y, own.x, own.y};
+        if (R == 0) return make_uint2(d[Q], d[Q + 1]);
+        return make_uint2(__builtin_amdgcn_alignbit(d[Q + 1], d[Q], R), __builtin_amdgcn_alignbit(d[Q + 2], d[Q + 1], R));
+    }
+    static __device__ __forceinline__ uint32_t cnt(const V v, int k) {
+        return ((k < 8 ? v.x : v.y) >> (4 * (k & 7))) & 0xFu;
+    }
+};
+
+// lane l <- lane l + 1 (lane 63 <- 0): DPP wave_shl:1
+__device__ __forceinline__ double dpp_shl1_d(double x) {
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), 0x130, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), 0x130, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
+
+// count -> double in program order (volatile): left free, the scheduler
+// converts a whole batch's counts up front and runs out of registers
+__device__ __forceinline__ double ub_cvt(uint32_t x) {
+    double r;
+    asm volatile("v_cvt_f64_u32 %0, %1" : "=v"(r) : "v"(x));
+    return r;
+}
+
+// b[c] for a band column: 0 outside the matrix or for a NaN bias (an empty
+// cis-only group, which no stored count touches)
+__device__ __forceinline__ double ub_bias(const double* __restrict__ b, long long c, long long n) {
+    const bool in = c >= 0 && c < n;
+    const double v = b[in ? c : 0];  // unconditional load (no branch per value)
+    return (in && v == v) ? v : 0.0;
+}
+
+// Halving butterfly over the 8 values of every lane: afterwards lane l holds
+// the wave-wide sum of value (l&1)*4 + (l&2) + (l&4)/4 (each pair's sum formed
+// once, in one lane: fixed order).
+template <int H, int MASK>
+__device__ __forceinline__ void ub_halve(double (&v)[8], int lane) {
+    const bool hi = (lane & MASK) != 0;
+#pragma unroll
+    for (int j = 0; j < H; ++j) {
+        const double send = hi ? v[j] : v[j + H];
+        const double keep = hi ? v[j + H] : v[j];
+        v[j] = keep + __shfl_xor(send, MASK, 64);
+    }
+}
+__device__ __forceinline__ double ub_reduce8(double (&v)[8], int lane) {
+    ub_halve<4, 1>(v, lane);
+    ub_halve<2, 2>(v, lane);
+    ub_halve<1, 4>(v, lane);
+    double x = v[0];
+    x += __shfl_xor(x, 8, 64);
+    x += __shfl_xor(x, 16, 64);
+    x += __shfl_xor(x, 32, 64);
+    return x;
+}
+__device__ __forceinline__ int ub_reduce8_row(int lane) { return (lane & 1) * 4 + (lane & 2) + ((lane >> 2) & 1); }
+
+// One wave task: rows [r0, r0 + kUbRows) x chunk kc of segment P.  Lanes 1..63
+// hold the chunk's 63 x 16 slots; lane 0 loads the 16 slots before them only
+// to hand them to lane 1 (DPP wave_shr:1) as the bytes its shifted rows reach
+// back into, and computes nothing (w = 0).  Heads go to heads[0, kUbRows);
+// the tail is left in col[] of lanes 1..63 (columns r0 + kUbRows + base +
+// 16 (lane - 1) + k).  The task's rows are all local or all halo (shards and
+// the halo start are 512-row aligned); rows past the stored ones read 0.
+// Every row is swept whatever its group's convergence flag: a converged
+// cis-only group's partials are not read (k_marg skips its rows), and band
+// counts never leave their chromosome.
+template <int BITS>
+__device__ __forceinline__ void ub_walk(const UbSeg& P, int kc, int chunk, long long r0, const UbArgs& a,
+                                        long long n_bins, double* __restrict__ heads, double (&col)[16]) {
+    using T = UbT<BITS>;
+    using V = typename T::V;
+    const int lane = threadIdx.x & 63;
+    const long long base = P.dlo + (long long)kc * kUbChunk;
+    int cb = (kc * kUbChunk + 16 * (lane - 1)) * BITS / 8;  // lane's bytes in a row (lane 0: the chunk's previous group)
+    // lanes outside the segment read the row's last bytes: zero padding in the
+    // nibble segment; in the uint8 band they hold diagonal W8's count, so
+    // those lanes mask their words to 0
+    const bool outside = cb < 0 || cb >= P.bytes;
+    const uint32_t msk = (BITS == 8 && outside) ? 0u : ~0u;
+    if (outside) cb = P.bytes - T::LB;
+    const long long rhi = a.row_hi < r0 + kUbRows ? a.row_hi : r0 + kUbRows;
+    const int nv = (int)(rhi - r0);  // stored rows of the task (uniform)
+    const uint8_t* __restrict__ rows = (r0 >= a.row_lo ? P.loc + (r0 - a.row_lo) * P.stride
+                                                       : P.halo + (r0 - a.halo_lo) * P.stride) + cb;
+    const long long stride = P.stride;
+    // rows past the stored ones read the last stored row: their counts only
+    // reach columns past the shard (or carry a zero bias past the matrix), and
+    // their row parts are not written
+    auto load_row = [&](int i) -> V { return T::ld(rows + (long long)(i < nv ? i : nv - 1) * stride); };
+    double w[16];
+    {
+        const long long c = r0 + base + 16 * (lane - 1);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) w[k] = lane ? ub_bias(a.b, c + k, n_bins) : 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) col[k] = 0.0;
+    double* __restrict__ R = a.upart + (size_t)(3 * chunk) * a.nloc;
+    // lanes 0..15: bias of the group's row lane; prefetched one group ahead
+    double bcur = lane < 16 ? ub_bias(a.b, r0 + lane, n_bins) : 0.0;
+    V buf[2][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) buf[0][j] = load_row(j);
+    const int ng = (nv + 15) / 16;
+#pragma unroll 1
+    for (int g = 0; g < kUbRows / 16; ++g) {
+        const long long gb = r0 + 16 * g;
+        // lanes 0..15: the next group's row biases; lanes 16..31: the window
+        // values lane 63 takes after this group
+        const double bnext = lane < 16   ? ub_bias(a.b, gb + 16 + lane, n_bins)
+                             : lane < 32 ? ub_bias(a.b, gb + 16 + base + 16 * 62 + (lane - 16), n_bins)
+                                         : 0.0;
+        if (g < ng) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                double racc[8];
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    const int bt = 2 * h + q;  // batch of 4 rows
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) buf[(bt + 1) & 1][j] = load_row(16 * g + 4 * (bt + 1) + j);
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int m = 4 * bt + j, mm = 4 * q + j;
+                        V own = buf[bt & 1][j];
+                        if (BITS == 8) {
+                            uint4& o = *reinterpret_cast<uint4*>(&own);
+                            o.x &= msk;
+                            o.y &= msk;
+                            o.z &= msk;
+                            o.w &= msk;
+                        }
+                        V prev;
+                        if (BITS == 8) {
+                            const uint4 o = *reinterpret_cast<const uint4*>(&own);
+                            const uint4 pv = dpp_shr1(o);
+                            prev = *reinterpret_cast<const V*>(&pv);
+                        } else {
+                            const uint2 o = *reinterpret_cast<const uint2*>(&own);
+                            const uint2 pv = make_uint2(__builtin_amdgcn_update_dpp(0u, o.x, 0x138, 0xF, 0xF, false),
+                                                        __builtin_amdgcn_update_dpp(0u, o.y, 0x138, 0xF, 0xF, false));
+                            prev = *reinterpret_cast<const V*>(&pv);
+                        }
+                        V sh;
+                        switch (m) {  // compile-time after unrolling
+                            case 0: sh = T::template shift<0>(prev, own); break;
+                            case 1: sh = T::template shift<1>(prev, own); break;
+                            case 2: sh = T::template shift<2>(prev, own); break;
+                            case 3: sh = T::template shift<3>(prev, own); break;
+                            case 4: sh = T::template shift<4>(prev, own); break;
+                            case 5: sh = T::template shift<5>(prev, own); break;
+                            case 6: sh = T::template shift<6>(prev, own); break;
+                            case 7: sh = T::template shift<7>(prev, own); break;
+                            case 8: sh = T::template shift<8>(prev, own); break;
+                            case 9: sh = T::template shift<9>(prev, own); break;
+                            case 10: sh = T::template shift<10>(prev, own); break;
+                            case 11: sh = T::template shift<11>(prev, own); break;
+                            case 12: sh = T::template shift<12>(prev, own); break;
+                            case 13: sh = T::template shift<13>(prev, own); break;
+                            case 14: sh = T::template shift<14>(prev, own); break;
+                            default: sh = T::template shift<15>(prev, own); break;
+                        }
+                        const double br = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(bcur), m),
+                                                           __builtin_amdgcn_readlane(__double2loint(bcur), m));
+                        // two partial row sums (even / odd slots): shorter dependent chains
+                        double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+                        for (int k = 0; k < 16; k += 2) {
+                            const double c0 = ub_cvt(T::cnt(sh, k)), c1 = ub_cvt(T::cnt(sh, k + 1));
+                            a0 = fma(c0, w[k], a0);
+                            a1 = fma(c1, w[k + 1], a1);
+                            col[k] = fma(c0, br, col[k]);
+                            col[k + 1] = fma(c1, br, col[k + 1]);
+                            // each count's two uses together: left free, the
+                            // compiler defers the column updates to the end of
+                            // the batch and parks every converted count in AGPRs
+                            asm volatile("" : "+v"(col[k]), "+v"(col[k + 1]), "+v"(a0), "+v"(a1));
+                        }
+                        racc[mm] = a0 + a1;
+                    }
+                    __builtin_amdgcn_sched_barrier(0);  // the next batch's loads stay after this one
+                }
+                const double s = ub_reduce8(racc, lane);
+                const long long r = gb + 8 * h + ub_reduce8_row(lane);
+                if (lane < 8 && r < rhi && r >= a.row_lo) R[r - a.row_lo] = s;
+            }
+        }
+        if (lane == 1) {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) heads[16 * g + k] = col[k];
+        }
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            col[k] = dpp_shl1_d(col[k]);
+            // lane 63 takes the new window value (DPP keeps `old` where the
+            // source lane is out of the wave); lane 0 computes nothing
+            const int nlo = __builtin_amdgcn_readlane(__double2loint(bnext), 16 + k);
+            const int nhi = __builtin_amdgcn_readlane(__double2hiint(bnext), 16 + k);
+            const int lo = __builtin_amdgcn_update_dpp(nlo, __double2loint(w[k]), 0x130, 0xF, 0xF, false);
+            const int hi = __builtin_amdgcn_update_dpp(nhi, __double2hiint(w[k]), 0x130, 0xF, 0xF, false);
+            w[k] = lane ? __hiloint2double(hi, lo) : 0.0;
+        }
+        bcur = bnext;
+    }
+}
+
+// One workgroup: rows [g * kUbGroupRows, + kUbGroupRows) x one chunk.
+__device__ __forceinline__ void ub_group(const UbSegs& S, long long grp, int chunk, const UbArgs& a, long long n_bins,
+                                         double* __restrict__ cbuf) {
+    int si = 0;
+    while (si + 1 < S.n && chunk >= S.s[si + 1].ch) ++si;
+    const UbSeg& P = S.s[si];
+    const int kc = chunk - P.ch;
+    const long long R0 = grp * kUbGroupRows;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const long long base = P.dlo + (long long)kc * kUbChunk;
+    for (int j = threadIdx.x; j < kUbChunk; j += kUbThreads) cbuf[kUbGroupRows + j] = 0.0;
+    const long long r0 = R0 + (long long)kUbRows * wave;
+    // rows this shard keeps, or columns it keeps, and rows it stores
+    const bool rows_here = r0 < a.row_hi && r0 + kUbRows > a.row_lo;
+    const bool cols_here = r0 + base < a.row_hi && r0 + kUbRows + base + kUbChunk > a.row_lo;
+    const bool stored = r0 + kUbRows > a.halo_lo && r0 < a.row_hi;
+    double col[16];
+    double* heads = cbuf + (size_t)kUbRows * wave;
+    if ((rows_here || cols_here) && stored) {
+        if (P.bits == 8)
+            ub_walk<8>(P, kc, chunk, r0, a, n_bins, heads, col);
+        else
+            ub_walk<4>(P, kc, chunk, r0, a, n_bins, heads, col);
+    } else {
+        for (int j = lane; j < kUbRows; j += 64) heads[j] = 0.0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) col[k] = 0.0;
+    }
+    // tails: even waves, then odd (wave w's tail covers the heads of w+1, w+2)
+#pragma unroll
+    for (int par = 0; par < 2; ++par) {
+        __syncthreads();
+        if ((wave & 1) == par && lane > 0) {
+            double* t = cbuf + (size_t)kUbRows * (wave + 1) + 16 * (lane - 1);
+#pragma unroll
+            for (int k = 0; k < 16; ++k) t[k] += col[k];
+        }
+    }
+    __syncthreads();
+    double* __restrict__ H = a.upart + (size_t)(3 * chunk + 1) * a.nloc;
+    double* __restrict__ Tt = a.upart + (size_t)(3 * chunk + 2) * a.nloc;
+    for (int j = threadIdx.x; j < kUbCols; j += kUbThreads) {
+        const long long c = R0 + base + j;
+        if (c >= a.row_lo && c < a.row_hi) (j < kUbGroupRows ? H : Tt)[c - a.row_lo] = cbuf[j];
+    }
+}
+
+// grid: (workgroups, chunks)
+__global__ __launch_bounds__(kUbThreads, 3) void k_sweep_ubands(UbSegs S, UbArgs a, long long n_bins) {
+    __shared__ double cbuf[kUbCols];
+    ub_group(S, a.g_lo + blockIdx.x, S.ord[blockIdx.y], a, n_bins, cbuf);
+}
+
+// Halo of a shard (rows [halo_lo, row_lo), upper halves only): every count a
+// halo row r' holds at diagonal d > 0 with r' + d in the shard is the shard
+// row's count at diagonal -d.  One thread per (halo row, upper byte).
+__global__ void k_ub_halo(const uint8_t* __restrict__ band, const uint8_t* __restrict__ band4, long long W8,
+                          long long W4, long long row_lo, long long row_hi, long long halo_lo,
+                          uint8_t* __restrict__ h8, uint8_t* __restrict__ h4) {
+    const long long nh = row_lo - halo_lo;
+    const long long st8 = band_stride(W8), st4 = band4_stride(W8, W4), sg = band4_seg(W8, W4);
+    const long long per = W8 + (W4 > W8 ? sg : 0);  // bytes per halo row: uint8 diagonals 1..W8, nibble bytes
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nh * per) return;
+    const long long hr = i / per, j = i % per, c = halo_lo + hr;
+    if (j < W8) {
+        const long long d = j + 1, r = c + d;
+        if (r >= row_lo && r < row_hi) h8[hr * st8 + W8 + d] = band[(r - row_lo) * st8 + (W8 - d)];
+    } else {
+        const long long jb = j - W8;  // byte of the positive nibble segment: nibbles 2 jb, 2 jb + 1
+        uint32_t v = 0;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const long long d = W8 + 1 + 2 * jb + q, r = c + d;
+            if (d <= W4 && r >= row_lo && r < row_hi) {
+                const long long nib = band4_nibble(-d, W8, W4);
+                v |= ((band4[(r - row_lo) * st4 + (nib >> 1)] >> (4 * (nib & 1))) & 0xFu) << (4 * q);
+            }
+        }
+        h4[hr * st4 + sg + jb] = (uint8_t)v;
+    }
+}
+
 // Small matrices (one chromosome, a shard of a few hundred MB): the whole
 // sweep -- tiled units, band blocks, flat units -- as ONE launch.  Each body
 // is latency-bound there (few blocks, each a short dependent chain), and run
@@ -1170,6 +1550,13 @@ __global__ __launch_bounds__(kSweepThreads, 4) void k_sweep_all(TileDev T, const
 // unconditionally from a clamped index and selected, so a batch's loads fly
 // together.  Summation order per row is unchanged (units in order, then band
 // chunks, wide entries, diagonal): bitwise the same marginals.
+// the upper-band partials k_marg adds (K1d): chunk c's R / H / T arrays at
+// part + 3c nloc, and the column of chunk c's slot 0 at row 0
+struct UbMarg {
+    const double* part;
+    int n;
+    long long base[kMaxUbChunks];
+};
 constexpr int kMargThreads = kR;
 constexpr int kMargU = 256;  // unit descriptors per LDS batch
 
@@ -1269,8 +1656,8 @@ __global__ __launch_bounds__(kMargThreads) void k_marg(TileDev T, const double* 
                                                        const uint16_t* __restrict__ row_group,
                                                        const uint8_t* __restrict__ act, const double* __restrict__ b,
                                                        long long row_lo, int nloc, const double* __restrict__ bpart,
-                                                       int nch, double* __restrict__ out, TileArgs ta, int G,
-                                                       int stats) {
+                                                       int nch, UbMarg ub, double* __restrict__ out, TileArgs ta,
+                                                       int G, int stats) {
     __shared__ int su_lo[kMargU], su_n[kMargU], su_slot[kMargU];
     __shared__ double sh[16];
     __shared__ int flag;
@@ -1321,6 +1708,17 @@ __global__ __launch_bounds__(kMargThreads) void k_marg(TileDev T, const double* 
             for (int q = 0; q < 8; ++q) s += x[q];
         }
         for (; c < nch; ++c) s += bpart[(long long)c * nloc + i];
+        // upper band (K1d): per chunk its row part, column head and, for the
+        // first kUbChunk columns of a workgroup, the previous workgroup's tail
+        for (c = 0; c < ub.n; ++c) {
+            const double* __restrict__ p = ub.part + (size_t)(3 * c) * nloc + i;
+            const long long t = row_lo + i - ub.base[c];
+            const bool tail = t >= kUbGroupRows && (t % kUbGroupRows) < kUbChunk;
+            const double x0 = p[0], x1 = p[nloc], x2 = p[tail ? 2LL * nloc : 0];
+            s += x0;
+            s += x1;
+            if (tail) s += x2;
+        }
         for (long long q = wide_ptr[i]; q < wide_ptr[i + 1]; ++q) s = fma(wide_cnt[q], b[wide_col[q]], s);
         const double br = b[row_lo + i];
         v = br * fma(2.0 * diag[i], br, s);
@@ -1543,6 +1941,12 @@ struct hh_ice {
     bool stats_fresh = false; // tile + group stats of the current marginals already made (fused k_marg)
     DBuf<double> bpart;  // dense band partials: n_band_chunks x nloc
     int32_t nch = 0;
+    // upper-band sweep (K1d): chunks, partials (R/H/T per chunk), a shard's
+    // halo rows [halo_lo, row_lo) (upper halves), workgroups [ub_glo, ub_ghi)
+    int32_t nchu = 0;
+    DBuf<double> upart;
+    DBuf<uint8_t> halo8, halo4;
+    int64_t halo_lo = 0, ub_glo = 0, ub_ghi = 0;
     DBuf<uint8_t> active;  // 2 x G (parity double buffer)
     DBuf<double> g_var, g_mean;
     DBuf<int32_t> g_iters;
@@ -1604,6 +2008,15 @@ static int64_t g_conc_min_bytes = 8LL << 30;
 static int g_band_rows = 0;   // rows per band block: 0 = auto (64 or 256)
 static int g_band_fused = 1;  // the band segments in one launch
 static int g_band_lpt = 1;      // band chunks dispatched heaviest first (0: uint8 first, index order)
+// upper-band sweep (K1d, round 3): read only the upper half of the bands, each
+// count feeding its row and its column.  0: the round-2 symmetric band kernels;
+// 1 (auto): the upper-band sweep when the WHOLE matrix's bands hold at least
+// g_uband_min_bytes (a wave walks 512 rows in sequence: on a single chromosome
+// that chain, not the bytes, sets the time -- C2 0.11 -> 0.54 ms per sweep);
+// 2: always.  Decided at hh_ice_create from the whole matrix, so every shard
+// of one matrix takes the same path.
+static int g_uband = 1;
+static int64_t g_uband_min_bytes = 1LL << 30;
 static int g_sweep_single = -1;  // whole sweep in one launch: -1 auto (below g_single_max_bytes), 0 off, 1 on
 static int64_t g_single_max_bytes = 1LL << 30;
 // diagnostic: per-block timeline of the last single-launch sweep (hh_sweep_trace)
@@ -1688,7 +2101,74 @@ static int band_segs(const hh_matrix* m, BandSegs& segs) {
     return ch;
 }
 
+// The upper-band segments (K1d): uint8 diagonals 0..W8 from slot W8 of each
+// row, nibble diagonals W8+1..W4 from the positive segment.  A chunk covers
+// 1024 slots; row m of a 16-row group reaches back m slots into the previous
+// chunk, so the last chunk must start within 15 slots of the segment end.
+static int ub_segs(const hh_ice* S, UbSegs& u) {
+    const hh_matrix* m = S->m;
+    const long long W8 = m->band_w, W4 = m->band_w4;
+    u = UbSegs{};
+    int ch = 0;
+    auto add = [&](const uint8_t* loc, const uint8_t* halo, long long stride, long long dlo, long long bytes,
+                   long long slots, int bits) {
+        const int nc = (int)((slots + 15 + kUbChunk - 1) / kUbChunk);
+        u.s[u.n++] = UbSeg{loc, halo, stride, dlo, (int)bytes, nc, ch, bits};
+        ch += nc;
+    };
+    if (W8 > 0)
+        add(m->band.p + W8, S->halo8.p ? S->halo8.p + W8 : nullptr, band_stride(W8), 0, W8 + 16, W8 + 1, 8);
+    if (W4 > W8) {
+        const long long sg = band4_seg(W8, W4);
+        add(m->band4.p + sg, S->halo4.p ? S->halo4.p + sg : nullptr, band4_stride(W8, W4), W8 + 1, sg, W4 - W8, 4);
+    }
+    HH_REQUIRE(ch <= kMaxUbChunks, "too many upper-band chunks");
+    // dispatch: full chunks first (every full chunk is the same count work),
+    // each segment's partial last chunk at the end
+    std::vector<std::pair<long long, int>> w;
+    for (int k = 0; k < u.n; ++k)
+        for (int c = 0; c < u.s[k].nc; ++c) {
+            const long long slots = u.s[k].bits == 8 ? W8 + 1 : W4 - W8;
+            w.push_back({-std::min<long long>(kUbChunk, slots + 15 - (long long)c * kUbChunk), u.s[k].ch + c});
+        }
+    std::stable_sort(w.begin(), w.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+    for (int y = 0; y < ch; ++y) u.ord[y] = (uint8_t)w[y].second;
+    return ch;
+}
+
+static UbArgs ub_args(hh_ice* S) {
+    const hh_matrix* m = S->m;
+    return UbArgs{m->row_lo, m->row_hi, S->halo_lo, S->nloc, S->ub_glo, S->act(), m->row_group.p, S->bias.p,
+                  S->upart.p};
+}
+
+static UbMarg ub_marg(const hh_ice* S) {
+    UbMarg u{};
+    u.part = S->upart.p;
+    u.n = S->nchu;
+    if (!S->nchu) return u;
+    UbSegs segs;
+    ub_segs(S, segs);
+    for (int k = 0; k < segs.n; ++k)
+        for (int c = 0; c < segs.s[k].nc; ++c) u.base[segs.s[k].ch + c] = segs.s[k].dlo + (long long)c * kUbChunk;
+    return u;
+}
+
+static void sweep_uband(hh_ice* S, hipStream_t s) {
+    UbSegs segs;
+    const int ch = ub_segs(S, segs);
+    const long long ng = S->ub_ghi - S->ub_glo;
+    if (!ch || ng <= 0) return;
+    hipLaunchKernelGGL(k_sweep_ubands, dim3((unsigned)ng, (unsigned)ch), dim3(kUbThreads), 0, s, segs, ub_args(S),
+                       (long long)S->m->n_bins);
+    HIP_CHECK(hipGetLastError());
+}
+
 static void sweep_band(hh_ice* S, hipStream_t s) {
+    if (S->nchu) {
+        if (S->nloc) sweep_uband(S, s);
+        return;
+    }
     const hh_matrix* m = S->m;
     if (!S->nch || !S->nloc) return;
     BandSegs segs;
@@ -1724,11 +2204,12 @@ static void sweep_band(hh_ice* S, hipStream_t s) {
 static void sweep_single(hh_ice* S, hipStream_t s) {
     const hh_matrix* m = S->m;
     BandSegs segs;
-    const int ch = (S->nch && S->nloc) ? band_segs(m, segs) : (segs = BandSegs{}, 0);
+    const int ch = (S->nch && S->nloc && !S->nchu) ? band_segs(m, segs) : (segs = BandSegs{}, 0);
     const int band_rb = (int)((S->nloc + 63) / 64);
     const int n_tiled = (int)(m->n_units - m->n_units_flat), n_flat = (int)m->n_units_flat;
     const long long n_band = ch ? (long long)band_rb * ch : 0;
     const long long grid = n_tiled + n_band + n_flat;
+    if (S->nchu && S->nloc) sweep_uband(S, s);  // its own launch (its registers would cap k_sweep_all's occupancy)
     if (!grid) return;
     HH_REQUIRE(grid < (1LL << 31), "sweep grid too large for one launch");
     unsigned long long* trace = grid <= g_trace_cap ? g_trace : nullptr;
@@ -1767,7 +2248,7 @@ static void marg_weighted(hh_ice* S, double* out, hipStream_t s, bool timed, int
         // kernel runs on a side stream so its blocks fill the CUs the tile
         // kernel leaves idle (both are HBM-bound; neither saturates alone)
         const int64_t bytes = 4 * m->n_slots + 2 * m->n_slots_narrow + (int64_t)m->band.n + (int64_t)m->band4.n;
-        const bool conc = g_band_concurrent && S->nch && S->nloc && m->n_units && bytes >= g_conc_min_bytes;
+        const bool conc = g_band_concurrent && (S->nch || S->nchu) && S->nloc && m->n_units && bytes >= g_conc_min_bytes;
         const bool single = g_sweep_nb == 2 &&
                             (g_sweep_single == 1 || (g_sweep_single == -1 && bytes < g_single_max_bytes));
         if (single) {
@@ -1802,7 +2283,8 @@ static void marg_weighted(hh_ice* S, double* out, hipStream_t s, bool timed, int
                           : 0;
     hipLaunchKernelGGL(k_marg, dim3(nblocks(S->nloc, kR)), dim3(kMargThreads), 0, s, m->dev(), S->part.p,
                        m->wide_ptr.p, m->wide_col.p, m->wide_cnt.p, m->diag.p, m->row_group.p, S->act(),
-                       S->bias.p, (long long)m->row_lo, (int)S->nloc, S->bpart.p, (int)S->nch, out, S->ta(),
+                       S->bias.p, (long long)m->row_lo, (int)S->nloc, S->bpart.p, S->nchu ? 0 : (int)S->nch,
+                       ub_marg(S), out, S->ta(),
                        (int)S->G, stats);
     HIP_CHECK(hipGetLastError());
     S->stats_fresh = stats != 0;
@@ -1933,6 +2415,12 @@ int hh_tune(const char* key, int64_t value) {
         } else if (k == "parse_ablate") {
             HH_REQUIRE(value >= 0 && value <= 3, "parse_ablate in [0, 3]");
             g_parse_ablate = (int)value;
+        } else if (k == "uband") {
+            HH_REQUIRE(value >= 0 && value <= 2, "uband: 0 (off), 1 (auto) or 2 (always)");
+            g_uband = (int)value;
+        } else if (k == "uband_min_bytes") {
+            HH_REQUIRE(value >= 0, "uband_min_bytes >= 0");
+            g_uband_min_bytes = value;
         } else if (k == "band_w") {
             HH_REQUIRE(value >= -1 && value <= kBandMaxW && (value <= 0 || value % 16 == 0),
                        "band_w: -1 (auto), 0 (off) or a multiple of 16 <= 16384");
@@ -2058,6 +2546,41 @@ int hh_ice_create(hh_matrix* m, const hh_ice_opts* o, hh_ice** out) {
         S->nch = m->band_w > 0 ? (int32_t)((band_stride(m->band_w) + kBandChunk - 1) / kBandChunk) : 0;
         if (m->band_w4 > m->band_w)
             S->nch += 2 * (int32_t)((band4_seg(m->band_w, m->band_w4) + kBandChunk - 1) / kBandChunk);
+        const int64_t band_all = m->n_bins * ((m->band_w > 0 ? band_stride(m->band_w) : 0) +
+                                              (m->band_w4 > m->band_w ? band4_stride(m->band_w, m->band_w4) : 0));
+        if (S->nch && (g_uband == 2 || (g_uband == 1 && band_all >= g_uband_min_bytes))) {
+            // upper-band sweep: workgroups whose rows or columns reach the
+            // shard, halo rows above it (upper halves from the shard's own
+            // lower halves), zeroed partials (positions no workgroup writes
+            // stay 0)
+            const long long dmax = std::max<long long>(m->band_w, m->band_w4);
+            S->ub_glo = std::max<long long>(0, m->row_lo - dmax - kUbCols) / kUbGroupRows;
+            S->ub_ghi = (m->row_hi + kUbGroupRows - 1) / kUbGroupRows;
+            S->halo_lo = std::min<long long>(m->row_lo, S->ub_glo * kUbGroupRows);
+            const long long nh = m->row_lo - S->halo_lo;
+            if (nh > 0) {
+                const long long W8 = m->band_w, W4 = m->band_w4;
+                const long long per = W8 + (W4 > W8 ? band4_seg(W8, W4) : 0);
+                if (W8 > 0) {
+                    S->halo8.alloc((size_t)(nh * band_stride(W8)));
+                    S->halo8.zero(s);
+                }
+                if (W4 > W8) {
+                    S->halo4.alloc((size_t)(nh * band4_stride(W8, W4)));
+                    S->halo4.zero(s);
+                }
+                const long long nthr = nh * per;
+                hipLaunchKernelGGL(k_ub_halo, dim3((unsigned)((nthr + 255) / 256)), dim3(256), 0, s, m->band.p,
+                                   m->band4.p, W8, W4, (long long)m->row_lo, (long long)m->row_hi, S->halo_lo,
+                                   S->halo8.p, S->halo4.p);
+                HIP_CHECK(hipGetLastError());
+            }
+            UbSegs segs;
+            S->nchu = ub_segs(S.get(), segs);
+            S->upart.alloc(std::max<int64_t>((int64_t)3 * S->nchu * S->nloc, 1));
+            S->upart.zero(s);
+            S->nch = 0;
+        }
         S->bpart.alloc(std::max<int64_t>((int64_t)S->nch * S->nloc, 1));
         // (the side streams of the three-stream sweep are made on first use)
 
@@ -2215,6 +2738,22 @@ int hh_ice_last_sweep_timing(const hh_ice* S, double* sweep_ms_total, int32_t* s
         if (sweep_ms_total) *sweep_ms_total = S->sweep_ms;
         if (sweep_launches) *sweep_launches = S->sweep_launches;
         if (iter_ms_total) *iter_ms_total = S->iter_ms;
+    });
+}
+
+int hh_ice_swept_bytes(const hh_ice* S, int64_t* bytes) {
+    return guard([&] {
+        HH_REQUIRE(S && bytes, "null");
+        const hh_matrix* m = S->m;
+        int64_t b = 4 * m->n_slots + 2 * m->n_slots_narrow + (int64_t)8 * (kR + 1) * m->n_tiles;
+        if (S->nchu) {
+            const long long W8 = m->band_w, W4 = m->band_w4;
+            const long long per = (W8 > 0 ? W8 + 16 : 0) + (W4 > W8 ? band4_seg(W8, W4) : 0);
+            b += (int64_t)per * (S->nloc + (m->row_lo - S->halo_lo));
+        } else {
+            b += (int64_t)m->band.n + (int64_t)m->band4.n;
+        }
+        *bytes = b;
     });
 }
 

@@ -73,16 +73,20 @@ __device__ __forceinline__ uint32_t poisson(float lam, uint64_t h) {
 }
 
 __device__ __forceinline__ uint32_t synth_count(const SynthDev& p, long long i, long long j) {
-    const float vi = p.vis[i], vj = p.vis[j];
-    if (vi == 0.f || vj == 0.f) return 0u;
     const long long lo = i < j ? i : j, hi = i < j ? j : i;
+    // visibilities in (lo, hi) order: float products do not commute bit for
+    // bit once chained, and (i, j) order made lam differ in the last place
+    // between the two triangles -- the Poisson draw then flipped by 1 for a
+    // few pixels, an asymmetric "symmetric" matrix (round 3 fix)
+    const float vi = p.vis[lo], vj = p.vis[hi];
+    if (vi == 0.f || vj == 0.f) return 0u;
     const long long d = hi - lo;
     if (d < p.ignore_diags) return 0u;
     const uint64_t h = p.ordered ? mix64(p.seed ^ mix64((uint64_t)i * 0x100000001B3ull + (uint64_t)j + 0x0DDull))
                                  : mix64(p.seed ^ mix64((uint64_t)lo * 0x100000001B3ull + (uint64_t)hi));
     if (p.chrom[i] == p.chrom[j]) {
         const float lam = p.A * exp2f(-p.decay * __log2f((float)d + 1.f)) *
-                          (1.f + p.comp * (float)(p.sgn[i] * p.sgn[j])) * vi * vj;
+                          (1.f + p.comp * (float)(p.sgn[lo] * p.sgn[hi])) * vi * vj;
         return poisson(lam, h);
     }
     if (p.cis_only) return 0u;

@@ -311,6 +311,12 @@ class IceState:
         call("hh_ice_last_sweep_timing", self._h, C.byref(ms), C.byref(k), C.byref(it))
         return ms.value, k.value, it.value
 
+    def swept_bytes(self):
+        """Payload bytes one sweep reads (hh_ice_swept_bytes)."""
+        b = C.c_int64(0)
+        call("hh_ice_swept_bytes", self._h, C.byref(b))
+        return b.value
+
     def finalize(self, stream=None):
         n = int(self.m.info()["n_bins"])
         G = self.n_groups

@@ -254,6 +254,11 @@ int hh_ice_finalize(hh_ice* s, double* weights, double* scale, double* var, int3
  * total ms of the sweep kernel, launches. */
 int hh_ice_last_sweep_timing(const hh_ice* s, double* sweep_ms_total, int32_t* sweep_launches,
                              double* iter_ms_total);
+/* Payload bytes one sweep of this state reads: tile entries + both segments'
+ * row pointers + the band bytes its band kernels stream (the upper halves
+ * only, plus a shard's halo rows, with the upper-band sweep).
+ * A measurement helper (bench.py's roofline), no computation. */
+int hh_ice_swept_bytes(const hh_ice* s, int64_t* bytes);
 
 /* ------------------------------------------------ sharded ICE in C
  * Genome-wide ICE over world processes (one GPU each), each holding the

@@ -1,0 +1,181 @@
+"""Upper-band ICE sweep (K1d): only the upper half of the dense
+diagonal bands is read, each count feeding its row's and its column's
+marginal.  Checked against the round-2 symmetric band sweep (itself pinned to
+the oracle, test_ice_gpu.py) and the oracle, and for bitwise shard invariance
+through the halo rows a shard copies from its own lower halves."""
+import numpy as np
+import pytest
+
+from hichap_master_amd import synth
+from oracle import ice_ref
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ice():
+    from hichap_master_amd import _lib, ice as ice_mod
+    _lib.require_gpu()
+    return ice_mod
+
+
+def _uband(on):
+    """on: the upper-band sweep whatever the size (these matrices are below
+    the automatic threshold); off: the symmetric band kernels"""
+    from hichap_master_amd import _lib
+    _lib.call("hh_tune", b"uband", 2 if on else 0)
+
+
+@pytest.fixture(autouse=True)
+def _force_uband():
+    from hichap_master_amd import _lib
+    _uband(True)
+    yield
+    _lib.call("hh_tune", b"uband", 1)
+
+
+def _balance_synth(ice, sizes, kw, opts, row_ranges=None):
+    """Balance the synthetic genome whole (row_ranges None) or as row shards
+    on one GPU with a manual marginal gather (the sharded driver's exchange)."""
+    import torch
+    n = int(np.sum(sizes))
+    if row_ranges is None:
+        m = ice.ContactMatrix.synthetic(sizes, **kw)
+        try:
+            return ice.balance_matrix(m, opts)
+        finally:
+            m.close()
+    rr = np.asarray(row_ranges, dtype=np.int64)
+    W = len(rr) - 1
+    shards = [ice.ContactMatrix.synthetic(sizes, row_range=(int(rr[k]), int(rr[k + 1])), **kw) for k in range(W)]
+    states = [ice.IceState(m, opts) for m in shards]
+    maxlen = int(np.max(np.diff(rr)))
+    loc = [torch.zeros(maxlen, dtype=torch.float64, device="cuda") for _ in range(W)]
+    gat = torch.zeros(W * maxlen, dtype=torch.float64, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+
+    def exchange(mode):
+        for k in range(W):
+            states[k].marg_local(mode, loc[k], s)
+        for k in range(W):
+            gat[k * maxlen:(k + 1) * maxlen].copy_(loc[k])
+        for k in range(W):
+            states[k].set_marg(gat, W, maxlen, rr, s)
+    try:
+        exchange(0)
+        for st_ in states:
+            st_.filter_nnz(s)
+        exchange(1)
+        for st_ in states:
+            st_.filter_count_mad(s)
+        for it in range(opts.max_iters):
+            exchange(2)
+            for st_ in states:
+                st_.update(s)
+            if it % 8 == 7 and states[0].active_groups(s) == 0:
+                break
+        res = [st_.finalize(s) for st_ in states]
+    finally:
+        for st_ in states:
+            st_.close()
+        for m in shards:
+            m.close()
+    for w, _ in res[1:]:
+        np.testing.assert_array_equal(w, res[0][0])
+    return res[0]
+
+
+# the C4 model (hg19 10 kb diploid, 5e9 pixels, 20 % trans: uint8 band to
+# ~2 768 diagonals, nibble band to ~9 584, several 1008-slot chunks each) on
+# a chr8-size chromosome, and on two chromosomes with trans contacts
+_C4_A, _C4_TD = None, None
+
+
+def _model(sizes):
+    global _C4_A, _C4_TD
+    if _C4_A is None:
+        _C4_A, _C4_TD = synth.calibrate(synth.genome_bins(10000, diploid=True), 5e9, 0.2)
+    return list(sizes), dict(A=_C4_A, trans_density=_C4_TD, comp_block=200, seed=20201015)
+
+
+_CHROM = [14637]
+_GENOME = [9036, 8120]
+
+
+@pytest.mark.parametrize("spec", [_CHROM, _GENOME], ids=["chrom", "genome"])
+def test_uband_matches_symmetric_sweep(ice, spec):
+    sizes, kw = _model(spec)
+    m = ice.ContactMatrix.synthetic(sizes, **kw)
+    inf = m.info()
+    m.close()
+    assert inf["band_w"] > 2 * 1008 and inf["band_w4"] - inf["band_w"] > 2 * 1008, inf  # several chunks per segment
+    opts = ice.IceOptions(max_iters=500)
+    _uband(False)
+    w0, s0 = _balance_synth(ice, sizes, kw, opts)
+    _uband(True)
+    w1, s1 = _balance_synth(ice, sizes, kw, opts)
+    assert s1["iters"] == s0["iters"]
+    np.testing.assert_allclose(w1, w0, rtol=1e-12, equal_nan=True)
+
+
+def test_uband_matches_oracle(ice):
+    """A small genome with both bands (incl. counts the bands cannot hold)."""
+    rng = np.random.default_rng(31)
+    b1, b2, c, off = synth.coo_genome([1400, 900], rng, A=60.0, trans_density=0.02)
+    c = c.copy()
+    c[::97] = 300
+    c[5::89] = 16
+    n = int(off[-1])
+    m = ice.ContactMatrix.from_pixels(b1, b2, c, n, off)
+    assert m.info()["band_w4"] > m.info()["band_w"] > 0
+    w, st = ice.balance_matrix(m)
+    m.close()
+    w_ref, st_ref = ice_ref.balance(b1, b2, c, n, off)
+    assert st["iters"] == st_ref["iters"]
+    np.testing.assert_allclose(w, w_ref, rtol=1e-9, equal_nan=True)
+
+
+@pytest.mark.parametrize("cuts", [[0, 4096, 14637], [0, 512, 3584, 6144, 14637], [0, 2560, 5120, 7680, 14637]])
+def test_uband_shards_bitwise(ice, cuts):
+    """Row shards (512-row aligned, workgroup-unaligned, shorter than the band)
+    give bitwise the one-shard weights: each shard sweeps the workgroups whose
+    columns reach it from halo rows rebuilt out of its own lower halves."""
+    sizes, kw = _model(_CHROM)
+    opts = ice.IceOptions(max_iters=300)
+    w_full, s_full = _balance_synth(ice, sizes, kw, opts)
+    w, s = _balance_synth(ice, sizes, kw, opts, row_ranges=cuts)
+    np.testing.assert_array_equal(w, w_full)
+    assert s["iters"] == s_full["iters"]
+
+
+def test_uband_shards_bitwise_genome_cis_only(ice):
+    sizes, kw = _model(_GENOME)
+    kw = dict(kw, cis_only=True)
+    opts = ice.IceOptions(max_iters=300)
+    w_full, s_full = _balance_synth(ice, sizes, kw, opts)
+    w, s = _balance_synth(ice, sizes, kw, opts, row_ranges=[0, 3072, 9216, 11264, 17156])
+    np.testing.assert_array_equal(w, w_full)
+    np.testing.assert_array_equal(s["iters"], s_full["iters"])  # per chromosome
+
+
+@pytest.mark.parametrize("mode", [0, 2], ids=["symmetric", "upper"])
+def test_one_sweep_row_sums_equal_export(ice, mode):
+    """b = 1: one sweep's marginals are the row sums of the exported table,
+    exactly (integer counts); the synthetic generator is symmetric bit for
+    bit (it once drew a few pixels of the two triangles 1 apart)."""
+    import torch
+    from hichap_master_amd import _lib
+    sizes, kw = _model(_CHROM)
+    n = sizes[0]
+    m = ice.ContactMatrix.synthetic(sizes, **kw)
+    b1, b2, c = m.export_upper()
+    want = np.bincount(b1, weights=c, minlength=n) + np.bincount(b2, weights=c, minlength=n)
+    _lib.call("hh_tune", b"uband", mode)
+    st = ice.IceState(m, ice.IceOptions(tol=0.0, max_iters=10, mad_max=0, min_nnz=0))
+    out = torch.zeros(n, dtype=torch.float64, device="cuda")
+    st.marg_local(2, out, None)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()
+    st.close()
+    m.close()
+    np.testing.assert_array_equal(got, want)

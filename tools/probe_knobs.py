@@ -57,6 +57,10 @@ def run_shard(n):
 
 for rep in range(2):
     for spec in a.settings:
+        if "uband=" in spec:  # create-time knob: a new ICE state
+            st.close()
+            tune(spec)
+            st = ice.IceState(m, ice.IceOptions(tol=0.0, max_iters=10**6, mad_max=0, min_nnz=0))
         tune(spec)
         if a.shard:
             run_shard(2)
