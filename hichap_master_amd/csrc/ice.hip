@@ -1150,12 +1150,17 @@ __global__ __launch_bounds__(kBandThreads, 4) void k_sweep_bands(BandSegs S, lon
 // Every sum's order is fixed by global positions only: deterministic, and the
 // same in a shard, which sweeps (from a halo copy of the rows above it) every
 // workgroup whose columns reach its rows.
-constexpr int kUbRows = 512;                       // rows per wave task
+constexpr int kUbRows = 128;                       // rows per wave task (the length of its serial walk)
 constexpr int kUbWaves = 4;                        // row blocks per workgroup
 constexpr int kUbThreads = 64 * kUbWaves;
 constexpr int kUbGroupRows = kUbRows * kUbWaves;   // rows per workgroup (global alignment)
 constexpr int kUbChunk = 1008;                     // slots per chunk = 63 data lanes x 16
 constexpr int kUbCols = kUbGroupRows + kUbChunk;   // LDS column buffer (doubles)
+// a workgroup's tails reach kUbTails workgroups ahead: per chunk the partial
+// arrays R (row parts), H (heads), T1 .. T_kUbTails (tails of the workgroups
+// 1 .. kUbTails behind)
+constexpr int kUbTails = (kUbChunk + kUbGroupRows - 1) / kUbGroupRows;
+constexpr int kUbArrs = 2 + kUbTails;
 constexpr int kMaxUbChunks = 40;
 
 struct UbSeg {
@@ -1176,7 +1181,7 @@ struct UbArgs {
     const uint8_t* act;
     const uint16_t* row_group;
     const double* b;
-    double* upart;  // per chunk c: R (row parts) at 3c, H at 3c + 1, T at 3c + 2, nloc each
+    double* upart;  // per chunk c: R at kUbArrs c, H at + 1, T1.. at + 2.., nloc each
 };
 
 template <int BITS>
@@ -1311,7 +1316,7 @@ __device__ __forceinline__ void ub_walk(const UbSeg& P, int kc, int chunk, long 
     }
 #pragma unroll
     for (int k = 0; k < 16; ++k) col[k] = 0.0;
-    double* __restrict__ R = a.upart + (size_t)(3 * chunk) * a.nloc;
+    double* __restrict__ R = a.upart + (size_t)(kUbArrs * chunk) * a.nloc;
     // lanes 0..15: bias of the group's row lane; prefetched one group ahead
     double bcur = lane < 16 ? ub_bias(a.b, r0 + lane, n_bins) : 0.0;
     V buf[2][4];
@@ -1430,7 +1435,7 @@ __device__ __forceinline__ void ub_group(const UbSegs& S, long long grp, int chu
     const long long R0 = grp * kUbGroupRows;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const long long base = P.dlo + (long long)kc * kUbChunk;
-    for (int j = threadIdx.x; j < kUbChunk; j += kUbThreads) cbuf[kUbGroupRows + j] = 0.0;
+    for (int j = threadIdx.x; j < kUbCols - kUbGroupRows; j += kUbThreads) cbuf[kUbGroupRows + j] = 0.0;
     const long long r0 = R0 + (long long)kUbRows * wave;
     // rows this shard keeps, or columns it keeps, and rows it stores
     const bool rows_here = r0 < a.row_hi && r0 + kUbRows > a.row_lo;
@@ -1448,22 +1453,22 @@ __device__ __forceinline__ void ub_group(const UbSegs& S, long long grp, int chu
 #pragma unroll
         for (int k = 0; k < 16; ++k) col[k] = 0.0;
     }
-    // tails: even waves, then odd (wave w's tail covers the heads of w+1, w+2)
-#pragma unroll
-    for (int par = 0; par < 2; ++par) {
+    // tails, one wave after the other (wave w's tail covers the heads of the
+    // next kUbChunk / kUbRows waves): a fixed order per column
+    for (int w = 0; w < kUbWaves; ++w) {
         __syncthreads();
-        if ((wave & 1) == par && lane > 0) {
+        if (wave == w && lane > 0) {
             double* t = cbuf + (size_t)kUbRows * (wave + 1) + 16 * (lane - 1);
 #pragma unroll
             for (int k = 0; k < 16; ++k) t[k] += col[k];
         }
     }
     __syncthreads();
-    double* __restrict__ H = a.upart + (size_t)(3 * chunk + 1) * a.nloc;
-    double* __restrict__ Tt = a.upart + (size_t)(3 * chunk + 2) * a.nloc;
+    // H: the workgroup's own columns; T_e: those of the workgroup e ahead
+    double* __restrict__ base_p = a.upart + (size_t)(kUbArrs * chunk + 1) * a.nloc;
     for (int j = threadIdx.x; j < kUbCols; j += kUbThreads) {
         const long long c = R0 + base + j;
-        if (c >= a.row_lo && c < a.row_hi) (j < kUbGroupRows ? H : Tt)[c - a.row_lo] = cbuf[j];
+        if (c >= a.row_lo && c < a.row_hi) base_p[(size_t)(j / kUbGroupRows) * a.nloc + (c - a.row_lo)] = cbuf[j];
     }
 }
 
@@ -1550,8 +1555,8 @@ __global__ __launch_bounds__(kSweepThreads, 4) void k_sweep_all(TileDev T, const
 // unconditionally from a clamped index and selected, so a batch's loads fly
 // together.  Summation order per row is unchanged (units in order, then band
 // chunks, wide entries, diagonal): bitwise the same marginals.
-// the upper-band partials k_marg adds (K1d): chunk c's R / H / T arrays at
-// part + 3c nloc, and the column of chunk c's slot 0 at row 0
+// the upper-band partials k_marg adds (K1d): chunk c's R / H / T1.. arrays at
+// part + kUbArrs c nloc, and the column of chunk c's slot 0 at row 0
 struct UbMarg {
     const double* part;
     int n;
@@ -1711,13 +1716,19 @@ __global__ __launch_bounds__(kMargThreads) void k_marg(TileDev T, const double* 
         // upper band (K1d): per chunk its row part, column head and, for the
         // first kUbChunk columns of a workgroup, the previous workgroup's tail
         for (c = 0; c < ub.n; ++c) {
-            const double* __restrict__ p = ub.part + (size_t)(3 * c) * nloc + i;
-            const long long t = row_lo + i - ub.base[c];
-            const bool tail = t >= kUbGroupRows && (t % kUbGroupRows) < kUbChunk;
-            const double x0 = p[0], x1 = p[nloc], x2 = p[tail ? 2LL * nloc : 0];
-            s += x0;
-            s += x1;
-            if (tail) s += x2;
+            const double* __restrict__ p = ub.part + (size_t)(kUbArrs * c) * nloc + i;
+            const long long t = row_lo + i - ub.base[c];  // column offset from the chunk's first workgroup
+            const long long q = t >= 0 ? t / kUbGroupRows : -1, o = t - q * kUbGroupRows;
+            double x[kUbArrs];
+            bool in[kUbArrs];
+            in[0] = in[1] = true;
+#pragma unroll
+            for (int e = 1; e <= kUbTails; ++e) in[1 + e] = q >= e && o + (long long)e * kUbGroupRows < kUbCols;
+#pragma unroll
+            for (int e = 0; e < kUbArrs; ++e) x[e] = p[in[e] ? (long long)e * nloc : 0];
+#pragma unroll
+            for (int e = 0; e < kUbArrs; ++e)
+                if (in[e]) s += x[e];
         }
         for (long long q = wide_ptr[i]; q < wide_ptr[i + 1]; ++q) s = fma(wide_cnt[q], b[wide_col[q]], s);
         const double br = b[row_lo + i];
@@ -2577,7 +2588,7 @@ int hh_ice_create(hh_matrix* m, const hh_ice_opts* o, hh_ice** out) {
             }
             UbSegs segs;
             S->nchu = ub_segs(S.get(), segs);
-            S->upart.alloc(std::max<int64_t>((int64_t)3 * S->nchu * S->nloc, 1));
+            S->upart.alloc(std::max<int64_t>((int64_t)kUbArrs * S->nchu * S->nloc, 1));
             S->upart.zero(s);
             S->nch = 0;
         }
