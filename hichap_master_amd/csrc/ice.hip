@@ -738,7 +738,7 @@ __global__ __launch_bounds__(kSweepThreads, 4) void k_sweep_flat(TileDev T, cons
 }
 
 // K1c' (round 3): the flat tiles swept by column tile.  A block takes a
-// group of up to kFlatGroup flat tiles sharing one column tile J (different
+// group of up to g_flat_group (44) flat tiles sharing one column tile J (different
 // row-blocks), stages b[J] once, and each of its 8 waves then walks whole
 // tiles on its own -- the next tile of the group from an LDS counter, the
 // tile's flat record in a per-wave LDS slot, its row sums in a per-wave LDS
@@ -749,10 +749,11 @@ __global__ __launch_bounds__(kSweepThreads, 4) void k_sweep_flat(TileDev T, cons
 // tile the walk is the round-2 one with the whole tile as the wave's range,
 // so a row's sum is a fixed function of the tile: deterministic, and the
 // same wherever the tile is swept.
+template <int NW>
 struct FlatWLds {
     double bl[kW];
-    uint16_t rec[kFlatWaves][kFrecU4 * 8];
-    double acc[kFlatWaves][kR];
+    uint16_t rec[NW][kFrecU4 * 8];
+    double acc[NW][kR];
     int next;
 };
 
@@ -764,13 +765,14 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-template <int U, int ABL, int PIPE = 2>
-__global__ __launch_bounds__(kSweepThreads, 2) void k_sweep_flatw(TileDev T, const uint8_t* __restrict__ act,
-                                                                const double* __restrict__ b, long long n_bins,
-                                                                double* __restrict__ part) {
-    static_assert(kSweepWaves == kFlatWaves, "one LDS slot per wave");
+// NW waves per block share one staged b[J]: the LDS (64 KB of bias + 8 KB
+// per wave) caps the block at 11 waves, and one block per CU is all that fits
+template <int U, int ABL, int PIPE = 2, int NW = kFlatWaves>
+__global__ __launch_bounds__(NW * 64, NW > 8 ? 3 : 2) void k_sweep_flatw(TileDev T, const uint8_t* __restrict__ act,
+                                                                       const double* __restrict__ b, long long n_bins,
+                                                                       double* __restrict__ part) {
     constexpr int UW = 2;
-    __shared__ __attribute__((aligned(16))) FlatWLds L;
+    __shared__ __attribute__((aligned(16))) FlatWLds<NW> L;
     const int k0 = T.fg_ptr[blockIdx.x], nk = T.fg_ptr[blockIdx.x + 1] - k0;
     {
         bool on = false;  // block-uniform: any active tile in the group
@@ -783,7 +785,7 @@ __global__ __launch_bounds__(kSweepThreads, 2) void k_sweep_flatw(TileDev T, con
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int J = T.tile_J[T.u_tlo[T.fg_unit[k0]]];
     if (threadIdx.x == 0) L.next = 0;
-    if (ABL != 2) stage_bias(L.bl, b, (long long)J * kW, n_bins);
+    if (ABL != 2 && threadIdx.x < kSweepThreads) stage_bias(L.bl, b, (long long)J * kW, n_bins);
     __syncthreads();
     const double* __restrict__ bl = L.bl;
     uint16_t* __restrict__ rec = L.rec[wave];
@@ -1285,9 +1287,15 @@ __device__ __forceinline__ int ub_reduce8_row(int lane) { return (lane & 1) * 4 
 // Every row is swept whatever its group's convergence flag: a converged
 // cis-only group's partials are not read (k_marg skips its rows), and band
 // counts never leave their chromosome.
+// LDS image of the workgroup's column biases: one pad double per 16 (a lane's
+// 16 window values are contiguous; lanes 136 B apart spread over the banks)
+__device__ __forceinline__ int ub_pad(int j) { return j + (j >> 4); }
+constexpr int kUbWin = kUbCols + kUbCols / 16 + 1;
+
 template <int BITS>
 __device__ __forceinline__ void ub_walk(const UbSeg& P, int kc, int chunk, long long r0, const UbArgs& a,
-                                        long long n_bins, double* __restrict__ heads, double (&col)[16]) {
+                                        long long n_bins, double* __restrict__ heads, double (&col)[16],
+                                        const double* __restrict__ cwin, const double* __restrict__ rowb) {
     using T = UbT<BITS>;
     using V = typename T::V;
     const int lane = threadIdx.x & 63;
@@ -1308,17 +1316,13 @@ __device__ __forceinline__ void ub_walk(const UbSeg& P, int kc, int chunk, long 
     // reach columns past the shard (or carry a zero bias past the matrix), and
     // their row parts are not written
     auto load_row = [&](int i) -> V { return T::ld(rows + (long long)(i < nv ? i : nv - 1) * stride); };
+    // the task's column biases and row biases come from the workgroup's LDS
+    // images (staged once per workgroup: no per-group global loads)
+    const int wo = (int)(r0 % kUbGroupRows);  // the task's offset in the workgroup
     double w[16];
-    {
-        const long long c = r0 + base + 16 * (lane - 1);
-#pragma unroll
-        for (int k = 0; k < 16; ++k) w[k] = lane ? ub_bias(a.b, c + k, n_bins) : 0.0;
-    }
 #pragma unroll
     for (int k = 0; k < 16; ++k) col[k] = 0.0;
     double* __restrict__ R = a.upart + (size_t)(kUbArrs * chunk) * a.nloc;
-    // lanes 0..15: bias of the group's row lane; prefetched one group ahead
-    double bcur = lane < 16 ? ub_bias(a.b, r0 + lane, n_bins) : 0.0;
     V buf[2][4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) buf[0][j] = load_row(j);
@@ -1326,12 +1330,12 @@ __device__ __forceinline__ void ub_walk(const UbSeg& P, int kc, int chunk, long 
 #pragma unroll 1
     for (int g = 0; g < kUbRows / 16; ++g) {
         const long long gb = r0 + 16 * g;
-        // lanes 0..15: the next group's row biases; lanes 16..31: the window
-        // values lane 63 takes after this group
-        const double bnext = lane < 16   ? ub_bias(a.b, gb + 16 + lane, n_bins)
-                             : lane < 32 ? ub_bias(a.b, gb + 16 + base + 16 * 62 + (lane - 16), n_bins)
-                                         : 0.0;
         if (g < ng) {
+            {  // lane l's 16 columns gb + base + 16 (l - 1) + [0, 16); lane 0 computes nothing
+                const double* src = cwin + ub_pad(wo + 16 * g + 16 * (lane > 0 ? lane - 1 : 0));
+#pragma unroll
+                for (int k = 0; k < 16; ++k) w[k] = lane ? src[k] : 0.0;
+            }
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 double racc[8];
@@ -1381,8 +1385,7 @@ __device__ __forceinline__ void ub_walk(const UbSeg& P, int kc, int chunk, long 
                             case 14: sh = T::template shift<14>(prev, own); break;
                             default: sh = T::template shift<15>(prev, own); break;
                         }
-                        const double br = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(bcur), m),
-                                                           __builtin_amdgcn_readlane(__double2loint(bcur), m));
+                        const double br = rowb[wo + 16 * g + m];  // wave-uniform LDS broadcast
                         // two partial row sums (even / odd slots): shorter dependent chains
                         double a0 = 0.0, a1 = 0.0;
 #pragma unroll
@@ -1411,23 +1414,14 @@ __device__ __forceinline__ void ub_walk(const UbSeg& P, int kc, int chunk, long 
             for (int k = 0; k < 16; ++k) heads[16 * g + k] = col[k];
         }
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            col[k] = dpp_shl1_d(col[k]);
-            // lane 63 takes the new window value (DPP keeps `old` where the
-            // source lane is out of the wave); lane 0 computes nothing
-            const int nlo = __builtin_amdgcn_readlane(__double2loint(bnext), 16 + k);
-            const int nhi = __builtin_amdgcn_readlane(__double2hiint(bnext), 16 + k);
-            const int lo = __builtin_amdgcn_update_dpp(nlo, __double2loint(w[k]), 0x130, 0xF, 0xF, false);
-            const int hi = __builtin_amdgcn_update_dpp(nhi, __double2hiint(w[k]), 0x130, 0xF, 0xF, false);
-            w[k] = lane ? __hiloint2double(hi, lo) : 0.0;
-        }
-        bcur = bnext;
+        for (int k = 0; k < 16; ++k) col[k] = dpp_shl1_d(col[k]);
     }
 }
 
 // One workgroup: rows [g * kUbGroupRows, + kUbGroupRows) x one chunk.
 __device__ __forceinline__ void ub_group(const UbSegs& S, long long grp, int chunk, const UbArgs& a, long long n_bins,
-                                         double* __restrict__ cbuf) {
+                                         double* __restrict__ cbuf, double* __restrict__ cwin,
+                                         double* __restrict__ rowb) {
     int si = 0;
     while (si + 1 < S.n && chunk >= S.s[si + 1].ch) ++si;
     const UbSeg& P = S.s[si];
@@ -1436,6 +1430,9 @@ __device__ __forceinline__ void ub_group(const UbSegs& S, long long grp, int chu
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const long long base = P.dlo + (long long)kc * kUbChunk;
     for (int j = threadIdx.x; j < kUbCols - kUbGroupRows; j += kUbThreads) cbuf[kUbGroupRows + j] = 0.0;
+    for (int j = threadIdx.x; j < kUbCols; j += kUbThreads) cwin[ub_pad(j)] = ub_bias(a.b, R0 + base + j, n_bins);
+    for (int j = threadIdx.x; j < kUbGroupRows; j += kUbThreads) rowb[j] = ub_bias(a.b, R0 + j, n_bins);
+    __syncthreads();
     const long long r0 = R0 + (long long)kUbRows * wave;
     // rows this shard keeps, or columns it keeps, and rows it stores
     const bool rows_here = r0 < a.row_hi && r0 + kUbRows > a.row_lo;
@@ -1445,9 +1442,9 @@ __device__ __forceinline__ void ub_group(const UbSegs& S, long long grp, int chu
     double* heads = cbuf + (size_t)kUbRows * wave;
     if ((rows_here || cols_here) && stored) {
         if (P.bits == 8)
-            ub_walk<8>(P, kc, chunk, r0, a, n_bins, heads, col);
+            ub_walk<8>(P, kc, chunk, r0, a, n_bins, heads, col, cwin, rowb);
         else
-            ub_walk<4>(P, kc, chunk, r0, a, n_bins, heads, col);
+            ub_walk<4>(P, kc, chunk, r0, a, n_bins, heads, col, cwin, rowb);
     } else {
         for (int j = lane; j < kUbRows; j += 64) heads[j] = 0.0;
 #pragma unroll
@@ -1475,7 +1472,9 @@ __device__ __forceinline__ void ub_group(const UbSegs& S, long long grp, int chu
 // grid: (workgroups, chunks)
 __global__ __launch_bounds__(kUbThreads, 3) void k_sweep_ubands(UbSegs S, UbArgs a, long long n_bins) {
     __shared__ double cbuf[kUbCols];
-    ub_group(S, a.g_lo + blockIdx.x, S.ord[blockIdx.y], a, n_bins, cbuf);
+    __shared__ double cwin[kUbWin];
+    __shared__ double rowb[kUbGroupRows];
+    ub_group(S, a.g_lo + blockIdx.x, S.ord[blockIdx.y], a, n_bins, cbuf, cwin, rowb);
 }
 
 // Halo of a shard (rows [halo_lo, row_lo), upper halves only): every count a
@@ -1715,20 +1714,29 @@ __global__ __launch_bounds__(kMargThreads) void k_marg(TileDev T, const double* 
         for (; c < nch; ++c) s += bpart[(long long)c * nloc + i];
         // upper band (K1d): per chunk its row part, column head and, for the
         // first kUbChunk columns of a workgroup, the previous workgroup's tail
-        for (c = 0; c < ub.n; ++c) {
-            const double* __restrict__ p = ub.part + (size_t)(kUbArrs * c) * nloc + i;
-            const long long t = row_lo + i - ub.base[c];  // column offset from the chunk's first workgroup
-            const long long q = t >= 0 ? t / kUbGroupRows : -1, o = t - q * kUbGroupRows;
-            double x[kUbArrs];
-            bool in[kUbArrs];
-            in[0] = in[1] = true;
+        // two chunks' loads in flight at a time (one chunk per iteration left a
+        // dependent load chain per chunk: k_marg 109 us at C4)
+        for (c = 0; c < ub.n; c += 2) {
+            double x[2][kUbArrs];
+            bool in[2][kUbArrs];
 #pragma unroll
-            for (int e = 1; e <= kUbTails; ++e) in[1 + e] = q >= e && o + (long long)e * kUbGroupRows < kUbCols;
+            for (int h = 0; h < 2; ++h) {
+                const int cc = c + h < ub.n ? c + h : c;
+                const double* __restrict__ p = ub.part + (size_t)(kUbArrs * cc) * nloc + i;
+                const long long t = row_lo + i - ub.base[cc];  // column offset from the chunk's first workgroup
+                const long long q = t >= 0 ? t / kUbGroupRows : -1, o = t - q * kUbGroupRows;
+                in[h][0] = in[h][1] = c + h < ub.n;
 #pragma unroll
-            for (int e = 0; e < kUbArrs; ++e) x[e] = p[in[e] ? (long long)e * nloc : 0];
+                for (int e = 1; e <= kUbTails; ++e)
+                    in[h][1 + e] = c + h < ub.n && q >= e && o + (long long)e * kUbGroupRows < kUbCols;
 #pragma unroll
-            for (int e = 0; e < kUbArrs; ++e)
-                if (in[e]) s += x[e];
+                for (int e = 0; e < kUbArrs; ++e) x[h][e] = p[in[h][e] ? (long long)e * nloc : 0];
+            }
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+                for (int e = 0; e < kUbArrs; ++e)
+                    if (in[h][e]) s += x[h][e];
         }
         for (long long q = wide_ptr[i]; q < wide_ptr[i + 1]; ++q) s = fma(wide_cnt[q], b[wide_col[q]], s);
         const double br = b[row_lo + i];
@@ -2002,6 +2010,12 @@ static int g_sweep_nb = 2;
 static int g_flatw_u = 8;     // uint4 per lane per step in k_sweep_flatw (8 or 16)
 static int g_band_dpp = 0;    // band sweep: a lane's previous 16 bytes by DPP shift (0: a second load;
                               // measured 4.34 vs 4.44 ms C4 sweep, profiles/r3_band_dpp_ab.log)
+// waves per k_sweep_flatw block (8, 10 or 11; they share one staged b[J] and
+// the block's LDS caps them at 11): the kernel waits on memory (SQ counters,
+// profiles/r3b_c4_sq_counters.json: VALU active 21 % of wave cycles), and 11
+// waves with 33-tile column groups (3 tiles per wave) took the C4 sweep from
+// 3.52 to 3.33 ms (profiles/r3b_flatw_waves_*_ab.log); 44-tile groups 1 % more
+static int g_flatw_waves = 11;
 static int g_flatw_pipe = 2;  // k_sweep_flatw: 1 = the next run's loads before the current step's walk,
                               // 2 = and the next tile's first runs before the current tile's row sums go out
 static int g_sweep_ablate = 0;
@@ -2046,7 +2060,15 @@ static void launch_sweep(const hh_matrix* m, const uint8_t* act, const double* b
                                        : g_flatw_pipe == 1 ? k_sweep_flatw<16, ABL, 1> : k_sweep_flatw<16, ABL, 0>)
                     : (g_flatw_pipe == 2 ? k_sweep_flatw<kFlatU, ABL, 2>
                        : g_flatw_pipe == 1 ? k_sweep_flatw<kFlatU, ABL, 1> : k_sweep_flatw<kFlatU, ABL, 0>);
-        hipLaunchKernelGGL(kern, dim3((unsigned)m->n_fgroups), dim3(kSweepThreads), 0, s, m->dev(), act, b,
+        int nw = 8;
+        if (g_flatw_waves == 10 && g_flatw_u != 16) {
+            kern = g_flatw_pipe == 2 ? k_sweep_flatw<kFlatU, ABL, 2, 10> : k_sweep_flatw<kFlatU, ABL, 0, 10>;
+            nw = 10;
+        } else if (g_flatw_waves == 11 && g_flatw_u != 16) {
+            kern = g_flatw_pipe == 2 ? k_sweep_flatw<kFlatU, ABL, 2, 11> : k_sweep_flatw<kFlatU, ABL, 0, 11>;
+            nw = 11;
+        }
+        hipLaunchKernelGGL(kern, dim3((unsigned)m->n_fgroups), dim3(64 * nw), 0, s, m->dev(), act, b,
                            (long long)m->n_bins, part);
     } else if (n_flat) {
         hipLaunchKernelGGL((k_sweep_flat<kFlatU, ABL>), dim3((unsigned)n_flat), dim3(kSweepThreads), 0, s, m->dev(),
@@ -2426,6 +2448,12 @@ int hh_tune(const char* key, int64_t value) {
         } else if (k == "parse_ablate") {
             HH_REQUIRE(value >= 0 && value <= 3, "parse_ablate in [0, 3]");
             g_parse_ablate = (int)value;
+        } else if (k == "flatw_waves") {
+            HH_REQUIRE(value == 8 || value == 10 || value == 11, "flatw_waves: 8, 10 or 11");
+            g_flatw_waves = (int)value;
+        } else if (k == "flat_group") {
+            HH_REQUIRE(value >= 1 && value <= 256, "flat_group: 1 .. 256");
+            g_flat_group = value;
         } else if (k == "uband") {
             HH_REQUIRE(value >= 0 && value <= 2, "uband: 0 (off), 1 (auto) or 2 (always)");
             g_uband = (int)value;

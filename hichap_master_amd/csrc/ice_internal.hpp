@@ -124,10 +124,10 @@ extern int64_t g_flat_max;       // hh_tune("flat_max"), build time
 // Column-grouped flat sweep (hh_tune "flat_cols", build time):
 // every flat tile is its own work unit (one partial per row per flat tile),
 // and the flat tiles of one column tile J are swept together in groups of up
-// to kFlatGroup by one block that stages b[J] once, each wave walking whole
+// to g_flat_group by one block that stages b[J] once, each wave walking whole
 // tiles on its own (no block barrier per tile).
 extern int64_t g_flat_cols;
-constexpr int kFlatGroup = 16;
+extern int64_t g_flat_group;   // tiles per column group (default 44)
 // minimum row length (uint4 per row) of band g
 __host__ __device__ constexpr uint32_t band_min(int g) { return g == 0 ? 48u : g == 1 ? 24u : g == 2 ? 12u : g == 3 ? 6u : 1u; }
 

@@ -20,6 +20,7 @@ int64_t g_unit_entries = 0;  // 0 = auto (plan_tiles)
 int g_flat_defer = 1;
 int64_t g_unit_lpt = 1;      // launch lists by unit cost class, largest first (0: row order)
 int64_t g_unit_lpt_lists = 1; // which lists: 1 tiled, 2 flat, 3 both (flat too: C4 sweep +1 %, profiles/r2b_modes_ab.log)
+int64_t g_flat_group = 44;  // flat tiles per column group (hh_tune "flat_group", build time): 4 per flatw wave
 int64_t g_flat_cols = 1;       // flat tiles as single-tile units swept in column groups (ice.hip k_sweep_flatw)
 int64_t g_tile_cost = 32768; // payload-word equivalent of one tile's fixed cost in the unit split (C4 shard 8/8: 0.79 -> 0.65 ms/iter)
 int64_t g_band_w = -1;       // -1 = auto (choose_band_w)
@@ -395,7 +396,7 @@ TilePlan plan_tiles(const uint16_t* cntw, const uint16_t* cntn, int64_t nloc, in
         }
     if (g_flat_cols && P.n_units_flat) {
         // flat groups: the flat units ordered by (column tile, row-block), cut
-        // into runs of <= kFlatGroup with one column tile; groups dispatched
+        // into runs of <= g_flat_group with one column tile; groups dispatched
         // by payload, largest first (a group's partials do not depend on it)
         std::vector<int32_t> fu;
         for (size_t u = 0; u < P.u_tlo.size(); ++u)
@@ -409,7 +410,7 @@ TilePlan plan_tiles(const uint16_t* cntw, const uint16_t* cntn, int64_t nloc, in
             size_t e = a;
             int64_t w = 0;
             const int32_t J = P.tile_J[P.u_tlo[fu[a]]];
-            while (e < fu.size() && e - a < (size_t)kFlatGroup && P.tile_J[P.u_tlo[fu[e]]] == J) {
+            while (e < fu.size() && e - a < (size_t)g_flat_group && P.tile_J[P.u_tlo[fu[e]]] == J) {
                 w += tile_words(P.u_tlo[fu[e]], 0, kR);
                 ++e;
             }

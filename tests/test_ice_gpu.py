@@ -318,6 +318,30 @@ def test_flat_tiles(ice, flat_max):
     assert sts["iters"] == st["iters"]
 
 
+def test_flat_block_shapes_bitwise(ice):
+    """The column-grouped flat kernel's block width (waves sharing one staged
+    b[J]) and group size (a build knob) change only who sweeps a flat tile,
+    not its per-row partials: bitwise the same weights."""
+    from hichap_master_amd import _lib
+    b1, b2, c, off = _case(41, sizes=(9000, 7000, 600), A=3.0, trans=0.0005)
+    n = int(off[-1])
+    res = []
+    try:
+        for waves, group in [(8, 16), (10, 16), (11, 33), (11, 1), (8, 64)]:
+            _lib.call("hh_tune", b"flatw_waves", waves)
+            _lib.call("hh_tune", b"flat_group", group)
+            m = ice.ContactMatrix.from_pixels(b1, b2, c, n, off)
+            assert m.info()["n_units_flat"] > 0
+            res.append(ice.balance_matrix(m, ice.IceOptions(max_iters=300)))
+            m.close()
+    finally:
+        _lib.call("hh_tune", b"flatw_waves", 11)
+        _lib.call("hh_tune", b"flat_group", 44)
+    for w, st in res[1:]:
+        np.testing.assert_array_equal(w, res[0][0])
+        assert st["iters"] == res[0][1]["iters"]
+
+
 @pytest.mark.parametrize("res,target,diploid", [(10000, 5e9, True)])
 def test_full_size_balanced_marginals(ice, res, target, diploid):
     """BASELINE C4 at full size (hg19 diploid whole genome at 10 kb, 5e9
