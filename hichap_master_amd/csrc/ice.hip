@@ -738,7 +738,7 @@ __global__ __launch_bounds__(kSweepThreads, 4) void k_sweep_flat(TileDev T, cons
 }
 
 // K1c' (round 3): the flat tiles swept by column tile.  A block takes a
-// group of up to g_flat_group (44) flat tiles sharing one column tile J (different
+// group of up to g_flat_group (auto: 11 .. 44) flat tiles sharing one column tile J (different
 // row-blocks), stages b[J] once, and each of its 8 waves then walks whole
 // tiles on its own -- the next tile of the group from an LDS counter, the
 // tile's flat record in a per-wave LDS slot, its row sums in a per-wave LDS
@@ -1299,7 +1299,6 @@ __device__ __forceinline__ void ub_walk(const UbSeg& P, int kc, int chunk, long 
     using T = UbT<BITS>;
     using V = typename T::V;
     const int lane = threadIdx.x & 63;
-    const long long base = P.dlo + (long long)kc * kUbChunk;
     int cb = (kc * kUbChunk + 16 * (lane - 1)) * BITS / 8;  // lane's bytes in a row (lane 0: the chunk's previous group)
     // lanes outside the segment read the row's last bytes: zero padding in the
     // nibble segment; in the uint8 band they hold diagonal W8's count, so
@@ -2416,7 +2415,7 @@ int hh_tune(const char* key, int64_t value) {
             HH_REQUIRE(value == 0 || value == 1, "band4 in {0, 1}");
             g_band4 = value;
         } else if (k == "flat_cols") {
-            HH_REQUIRE(value == 0 || value == 1, "flat_cols in {0, 1}");
+            HH_REQUIRE(value >= -1 && value <= 1, "flat_cols in {-1 (auto), 0, 1}");
             g_flat_cols = value;
         } else if (k == "flatw_pipe") {
             HH_REQUIRE(value >= 0 && value <= 2, "flatw_pipe in {0, 1, 2}");
@@ -2452,7 +2451,7 @@ int hh_tune(const char* key, int64_t value) {
             HH_REQUIRE(value == 8 || value == 10 || value == 11, "flatw_waves: 8, 10 or 11");
             g_flatw_waves = (int)value;
         } else if (k == "flat_group") {
-            HH_REQUIRE(value >= 1 && value <= 256, "flat_group: 1 .. 256");
+            HH_REQUIRE(value >= 0 && value <= 256, "flat_group: 0 (auto) .. 256");
             g_flat_group = value;
         } else if (k == "uband") {
             HH_REQUIRE(value >= 0 && value <= 2, "uband: 0 (off), 1 (auto) or 2 (always)");

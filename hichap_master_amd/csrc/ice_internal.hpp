@@ -127,7 +127,8 @@ extern int64_t g_flat_max;       // hh_tune("flat_max"), build time
 // to g_flat_group by one block that stages b[J] once, each wave walking whole
 // tiles on its own (no block barrier per tile).
 extern int64_t g_flat_cols;
-extern int64_t g_flat_group;   // tiles per column group (default 44)
+bool flat_cols_on(int32_t nJ);  // the column-grouped flat sweep for a matrix of nJ column tiles
+extern int64_t g_flat_group;   // tiles per column group (0 = auto, 11 .. 44)
 // minimum row length (uint4 per row) of band g
 __host__ __device__ constexpr uint32_t band_min(int g) { return g == 0 ? 48u : g == 1 ? 24u : g == 2 ? 12u : g == 3 ? 6u : 1u; }
 

@@ -20,8 +20,21 @@ int64_t g_unit_entries = 0;  // 0 = auto (plan_tiles)
 int g_flat_defer = 1;
 int64_t g_unit_lpt = 1;      // launch lists by unit cost class, largest first (0: row order)
 int64_t g_unit_lpt_lists = 1; // which lists: 1 tiled, 2 flat, 3 both (flat too: C4 sweep +1 %, profiles/r2b_modes_ab.log)
-int64_t g_flat_group = 44;  // flat tiles per column group (hh_tune "flat_group", build time): 4 per flatw wave
-int64_t g_flat_cols = 1;       // flat tiles as single-tile units swept in column groups (ice.hip k_sweep_flatw)
+// flat tiles per column group (hh_tune "flat_group", build time; results do not
+// depend on it): 0 = auto, up to 44 (4 per flatw wave) while that leaves >= 1024
+// groups, down to 11: an N = 8 C4 shard has ~10 700 flat tiles, and 44-tile
+// groups left its 256 CUs with under one group each (slowest shard sweep 0.617
+// -> 0.676 ms)
+int64_t g_flat_group = 0;
+// flat tiles as single-tile units swept in column groups (ice.hip k_sweep_flatw):
+// 1 on, 0 off (round-2 flat units: runs of tiles of one row-block, 8 waves
+// splitting each tile), -1 auto = on for matrices of >= 32 column tiles (>= 262 144
+// bins: C4, C4 haploid and every shard of them -- the whole matrix decides, so all
+// shards agree).  On the small ones the per-tile units cost: C3 sweep 0.74 ->
+// 0.81 ms, C2 0.084 -> 0.106 ms (the one-launch sweep's flat body must then sum
+// each tile with one wave; profiles/r3b_m3_*.log)
+int64_t g_flat_cols = -1;
+bool flat_cols_on(int32_t nJ) { return g_flat_cols > 0 || (g_flat_cols < 0 && nJ >= 32); }
 int64_t g_tile_cost = 32768; // payload-word equivalent of one tile's fixed cost in the unit split (C4 shard 8/8: 0.79 -> 0.65 ms/iter)
 int64_t g_band_w = -1;       // -1 = auto (choose_band_w)
 int64_t g_flat_max = 64;     // longest row (uint4) of a flat tile segment; 0 = no flat segments
@@ -180,7 +193,7 @@ void plan_block(const uint16_t* cntw, const uint16_t* cntn, int64_t nloc, int32_
                 // sum each row in that same order: wave 0 takes every row
                 uint32_t* f = fw + seg * 2 * (kFlatWaves + 1);
                 for (int w = 0; w <= kFlatWaves; ++w) {
-                    const uint32_t tq = g_flat_cols ? (w == 0 ? 0u : Q) : (uint32_t)(((uint64_t)Q * w) / kFlatWaves);
+                    const uint32_t tq = flat_cols_on(nJ) ? (w == 0 ? 0u : Q) : (uint32_t)(((uint64_t)Q * w) / kFlatWaves);
                     const int i = (int)(std::lower_bound(st, st + nfr, tq) - st);
                     f[2 * w] = st[i];
                     f[2 * w + 1] = (uint32_t)i;
@@ -365,7 +378,7 @@ TilePlan plan_tiles(const uint16_t* cntw, const uint16_t* cntn, int64_t nloc, in
                 emit(rb, t, t + 1, rlo, nr);
                 cur = t + 1;
                 cur_sz = 0;
-            } else if (g_flat_cols && P.tile_flat[t]) {
+            } else if (flat_cols_on(nJ) && P.tile_flat[t]) {
                 // column-grouped flat sweep: every flat tile its own unit
                 if (cur < t) emit(rb, cur, t, 0, nr);
                 emit(rb, t, t + 1, 0, nr);
@@ -394,7 +407,7 @@ TilePlan plan_tiles(const uint16_t* cntw, const uint16_t* cntn, int64_t nloc, in
             ++P.n_units_flat;
             for (int32_t t = P.u_tlo[u]; t < P.u_thi[u]; ++t) P.payload_bytes_flat += 4 * tile_words(t, 0, kR);
         }
-    if (g_flat_cols && P.n_units_flat) {
+    if (flat_cols_on(nJ) && P.n_units_flat) {
         // flat groups: the flat units ordered by (column tile, row-block), cut
         // into runs of <= g_flat_group with one column tile; groups dispatched
         // by payload, largest first (a group's partials do not depend on it)
@@ -405,12 +418,14 @@ TilePlan plan_tiles(const uint16_t* cntw, const uint16_t* cntn, int64_t nloc, in
             const int32_t ja = P.tile_J[P.u_tlo[a]], jb = P.tile_J[P.u_tlo[b]];
             return ja != jb ? ja < jb : P.u_rb[a] < P.u_rb[b];
         });
+        const size_t gmax = g_flat_group > 0 ? (size_t)g_flat_group
+                                             : std::min<size_t>(44, std::max<size_t>(11, fu.size() / 1024));
         std::vector<std::pair<int64_t, std::pair<int32_t, int32_t>>> groups;  // (-words, [lo, hi) in fu)
         for (size_t a = 0; a < fu.size();) {
             size_t e = a;
             int64_t w = 0;
             const int32_t J = P.tile_J[P.u_tlo[fu[a]]];
-            while (e < fu.size() && e - a < (size_t)g_flat_group && P.tile_J[P.u_tlo[fu[e]]] == J) {
+            while (e < fu.size() && e - a < gmax && P.tile_J[P.u_tlo[fu[e]]] == J) {
                 w += tile_words(P.u_tlo[fu[e]], 0, kR);
                 ++e;
             }

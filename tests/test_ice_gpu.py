@@ -290,8 +290,8 @@ def test_dense_band_widths(ice, band_w, band4):
     np.testing.assert_allclose(w, w_ref, rtol=1e-9, equal_nan=True)
 
 
-@pytest.mark.parametrize("flat_max", [0, 2, 24, 255])
-def test_flat_tiles(ice, flat_max):
+@pytest.mark.parametrize("flat_max,flat_cols", [(0, -1), (2, -1), (24, -1), (255, -1), (24, 1), (255, 1)])
+def test_flat_tiles(ice, flat_max, flat_cols):
     """Tiles whose rows are all short go to the flat (merge-path) sweep kernel;
     any threshold (none, few, most, all tiles flat) gives the oracle's weights,
     and a 3-shard run is bitwise equal to the whole-matrix run."""
@@ -299,6 +299,7 @@ def test_flat_tiles(ice, flat_max):
     b1, b2, c, off = _case(41, sizes=(9000, 7000, 600), A=3.0, trans=0.0005)
     n = int(off[-1])
     _lib.call("hh_tune", b"flat_max", flat_max)
+    _lib.call("hh_tune", b"flat_cols", flat_cols)  # 1: the column-grouped kernel (auto: big matrices only)
     try:
         m = ice.ContactMatrix.from_pixels(b1, b2, c, n, off)
         inf = m.info()
@@ -311,6 +312,7 @@ def test_flat_tiles(ice, flat_max):
         ws, sts = _sharded_weights(ice, b1, b2, c, off, np.array([0, 4096, 11264, n]))
     finally:
         _lib.call("hh_tune", b"flat_max", 64)
+        _lib.call("hh_tune", b"flat_cols", -1)
     w_ref, st_ref = ice_ref.balance(b1, b2, c, n, off, max_iters=300)
     assert st["iters"] == st_ref["iters"]
     np.testing.assert_allclose(w, w_ref, rtol=1e-9, equal_nan=True)
@@ -326,6 +328,7 @@ def test_flat_block_shapes_bitwise(ice):
     b1, b2, c, off = _case(41, sizes=(9000, 7000, 600), A=3.0, trans=0.0005)
     n = int(off[-1])
     res = []
+    _lib.call("hh_tune", b"flat_cols", 1)  # (auto: column groups only from 32 column tiles)
     try:
         for waves, group in [(8, 16), (10, 16), (11, 33), (11, 1), (8, 64)]:
             _lib.call("hh_tune", b"flatw_waves", waves)
@@ -336,7 +339,8 @@ def test_flat_block_shapes_bitwise(ice):
             m.close()
     finally:
         _lib.call("hh_tune", b"flatw_waves", 11)
-        _lib.call("hh_tune", b"flat_group", 44)
+        _lib.call("hh_tune", b"flat_group", 0)
+        _lib.call("hh_tune", b"flat_cols", -1)
     for w, st in res[1:]:
         np.testing.assert_array_equal(w, res[0][0])
         assert st["iters"] == res[0][1]["iters"]
