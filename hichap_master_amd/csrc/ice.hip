@@ -1468,12 +1468,24 @@ __device__ __forceinline__ void ub_group(const UbSegs& S, long long grp, int chu
     }
 }
 
-// grid: (workgroups, chunks)
-__global__ __launch_bounds__(kUbThreads, 3) void k_sweep_ubands(UbSegs S, UbArgs a, long long n_bins) {
+// grid: (workgroups, chunks).  xcd != 0: the blocks are re-dealt so that each
+// XCD (blocks b, b + 8, ... share one) takes a contiguous range of (workgroup,
+// chunk) pairs, chunks fastest: neighbouring chunks of the same rows, which
+// share the cache lines at their boundaries (a chunk is 1008 B of uint8 /
+// 504 B of nibbles per row, not a multiple of 128 B), run back to back on one L2
+__global__ __launch_bounds__(kUbThreads, 3) void k_sweep_ubands(UbSegs S, UbArgs a, long long n_bins, int xcd) {
     __shared__ double cbuf[kUbCols];
     __shared__ double cwin[kUbWin];
     __shared__ double rowb[kUbGroupRows];
-    ub_group(S, a.g_lo + blockIdx.x, S.ord[blockIdx.y], a, n_bins, cbuf, cwin, rowb);
+    long long grp = blockIdx.x;
+    int y = blockIdx.y;
+    if (xcd) {
+        const long long nb = (long long)gridDim.x * gridDim.y, b = blockIdx.x + (long long)blockIdx.y * gridDim.x;
+        const long long L = xcd_remap(b, nb);
+        y = (int)(L % gridDim.y);
+        grp = L / gridDim.y;
+    }
+    ub_group(S, a.g_lo + grp, S.ord[y], a, n_bins, cbuf, cwin, rowb);
 }
 
 // Halo of a shard (rows [halo_lo, row_lo), upper halves only): every count a
@@ -2041,6 +2053,7 @@ static int g_band_lpt = 1;      // band chunks dispatched heaviest first (0: uin
 // of one matrix takes the same path.
 static int g_uband = 1;
 static int64_t g_uband_min_bytes = 1LL << 30;
+static int g_ub_xcd = 1;  // upper-band blocks dealt in contiguous ranges per XCD (k_sweep_ubands)
 static int g_sweep_single = -1;  // whole sweep in one launch: -1 auto (below g_single_max_bytes), 0 off, 1 on
 static int64_t g_single_max_bytes = 1LL << 30;
 // diagnostic: per-block timeline of the last single-launch sweep (hh_sweep_trace)
@@ -2192,7 +2205,7 @@ static void sweep_uband(hh_ice* S, hipStream_t s) {
     const long long ng = S->ub_ghi - S->ub_glo;
     if (!ch || ng <= 0) return;
     hipLaunchKernelGGL(k_sweep_ubands, dim3((unsigned)ng, (unsigned)ch), dim3(kUbThreads), 0, s, segs, ub_args(S),
-                       (long long)S->m->n_bins);
+                       (long long)S->m->n_bins, g_ub_xcd);
     HIP_CHECK(hipGetLastError());
 }
 
@@ -2456,6 +2469,9 @@ int hh_tune(const char* key, int64_t value) {
         } else if (k == "uband") {
             HH_REQUIRE(value >= 0 && value <= 2, "uband: 0 (off), 1 (auto) or 2 (always)");
             g_uband = (int)value;
+        } else if (k == "ub_xcd") {
+            HH_REQUIRE(value == 0 || value == 1, "ub_xcd: 0 or 1");
+            g_ub_xcd = (int)value;
         } else if (k == "uband_min_bytes") {
             HH_REQUIRE(value >= 0, "uband_min_bytes >= 0");
             g_uband_min_bytes = value;
