@@ -196,7 +196,7 @@ def tad_scan_bench(m, st, stream, reps=5, res=10000, min_tad=200000, window=6000
 
 
 C5_RES = 25000
-C5_STREAMS = int(os.environ.get("HH_C5_STREAMS", "8"))
+C5_STREAMS = int(os.environ.get("HH_C5_STREAMS", "12"))  # 12 host threads / streams: 95.8 vs 89.9 chr/s with 8 (profiles/r3b_c5b_s*.log)
 
 
 def c5_sizes():
@@ -316,6 +316,7 @@ def run_c5(args, world, rank, local):
     _lib.call("hh_ktime_enable", 0)
     syrk_ms, syrk_n = _lib.ktime("k_syrk")
     mul_ms, mul_n = _lib.ktime("k_cor_mul")
+    orth_ms, orth_n = _lib.ktime("k_ortho")
     tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
     if torch.distributed.is_initialized():
         torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
@@ -334,7 +335,20 @@ def run_c5(args, world, rank, local):
                     "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": (mul_gbs / PEAK_HBM_GBS) if mul_gbs else None,
                     "total_ms": mul_ms, "launches": mul_n, "alg_bytes": mul_bytes,
                     "alg_bytes_note": "8 B x ld^2 (the padded correlation) per Cor.V product"}
-        dom, other = (mul_side, syrk_side) if mul_ms > syrk_ms else (syrk_side, mul_side)
+        # the Krylov orthogonalisation (one k_ortho launch per product): per
+        # cycle of P = 8 products block j reads the basis Q_0..Q_j twice (two
+        # Gram-Schmidt passes) and W / its CholeskyQR iterates ~3 times, and
+        # writes Q_{j+1}: ~(2 (j + 1) + 3) n x 16 x 8 B, 96 n x 128 B per cycle
+        orth_bytes = sum(prods[k] / 8.0 * 96.0 * ng[k] * 128.0 for k in mine)
+        orth_gbs = orth_bytes / (orth_ms / 1000.0) / 1e9 if orth_ms > 0 else None
+        orth_side = {"bound": "latency (grid barriers)", "kernel": "k_ortho", "achieved": orth_gbs,
+                     "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": (orth_gbs / PEAK_HBM_GBS) if orth_gbs else None,
+                     "total_ms": orth_ms, "launches": orth_n, "alg_bytes": orth_bytes,
+                     "alg_bytes_note": "estimate: ~96 n x 128 B per Krylov cycle of 8 products (basis read twice, "
+                                       "W and its CholeskyQR iterates, Q_{j+1} written); about 10 grid barriers "
+                                       "per launch set its time"}
+        sides = sorted([syrk_side, mul_side, orth_side], key=lambda d: -(d["total_ms"] or 0.0))
+        dom, other = sides[0], sides[1:]
         out = {
             "metric": "compartment PCA chromosomes/sec (C5: hg19 autosomes at 25 kb, dense per-chrom)",
             "value": len(sizes) * args.steps / elapsed, "unit": "chromosomes/s", "n_gpus": world,
@@ -349,8 +363,9 @@ def run_c5(args, world, rank, local):
                        "pca_all_converged": bool(all(conv[k] for k in mine)),
                        "serial_step_ms": round(serial_ms, 2), "serial_phase_ms": serial_phases},
             "roofline": dict(dom, traffic=None,
-                             kernel_timing="HIP events (hh_ktime) over one extra serialised pass after the timed steps",
-                             other_kernel=other),
+                             kernel_timing="HIP events (hh_ktime) over one extra serialised pass after the timed steps; "
+                                           "roofline = the kernel with the most time, other_kernels = the rest",
+                             other_kernels=other),
         }
         if world == 1 and not args.no_cpu:
             out["cpu_baseline"] = with_host(c5_cpu_baseline())

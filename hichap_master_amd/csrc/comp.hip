@@ -1672,6 +1672,7 @@ static bool pca_krylov(PcaWork& wk, const double* cor, long long n, int k, doubl
         a.tstamp = g_pca_debug >= 2 ? tst.p : nullptr;
         HH_REQUIRE(a.nb >= 0 && a.nb <= 8 && oblk >= 1 && oblk <= kOrthoMaxBlocks, "k_ortho shape");
         const dim3 grid((unsigned)oblk), blk(256);
+        HH_KTIME("k_ortho", s);  // bench.py's C5 line: the dominant kernel by time
 #define HH_ORTHO(M)                                                  \
     do {                                                             \
         if (tpb == 4) hipLaunchKernelGGL((k_ortho<M, 4>), grid, blk, 0, s, a); \

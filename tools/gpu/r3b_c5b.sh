@@ -1,0 +1,6 @@
+#!/bin/bash
+cd "${GRAFT_REPO_ROOT:-/root/repo}" && mkdir -p gpurun_out/r3b && export TMPDIR=/tmp
+O=gpurun_out/r3b
+for st in 12 16 22 8; do
+HH_C5_STREAMS=$st timeout -k 10 300 python3 -u bench.py --config c5 --no-cpu --steps 5 --warmup 1 > $O/c5b_s$st.log 2>&1; echo "streams $st rc=$?"; tail -1 $O/c5b_s$st.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['config']['serial_step_ms'])"
+done
