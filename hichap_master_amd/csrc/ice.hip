@@ -826,7 +826,21 @@ __global__ __launch_bounds__(NW * 64, NW > 8 ? 3 : 2) void k_sweep_flatw(TileDev
     if (cur.nfw) flat_load<UW>(cur.payw4, (uint32_t)lane * UW, 0u, cur.qbw, vw);
     for (;;) {
         const uint4* rg = T.frec + (size_t)T.tile_frec[cur.t] * kFrecU4;
-        for (int q = lane; q < kFrecU4; q += 64) reinterpret_cast<uint4*>(rec)[q] = rg[q];
+        // stage only the parts of the record the walk reads (the starts up
+        // to each segment's end, the row ids of the nonempty rows), and no
+        // narrow row ids when every row of the block is nonempty (they are
+        // then 0, 1, 2, ...: the dense trans tiles): ~1.1 of 4.1 KB per tile
+        const bool idn = cur.nfn == cur.nr;
+        {
+            uint4* r4 = reinterpret_cast<uint4*>(rec);
+            auto stage = [&](int h0, int h1) {  // uint16 range [h0, h1) of the record
+                for (int q = h0 / 8 + lane; q < (h1 + 7) / 8; q += 64) r4[q] = rg[q];
+            };
+            stage(0, cur.nfn + 1);
+            stage(kR + 1, kR + 1 + cur.nfw + 1);
+            if (!idn) stage(2 * (kR + 1), 2 * (kR + 1) + cur.nfn);
+            stage(2 * (kR + 1) + kR, 2 * (kR + 1) + kR + cur.nfw);
+        }
         wave_lds_sync();
         if (PIPE) flat_seg_c_pipe<U, ABL, 8>(cur.payn4, v, 0u, cur.qbn, 0, cur.nfn, fstn, cur.nfn, bl, acc, lane);
         else flat_seg_c<U, ABL, 8>(cur.payn4, v, 0u, cur.qbn, 0, cur.nfn, fstn, cur.nfn, bl, acc, lane);
@@ -839,7 +853,7 @@ __global__ __launch_bounds__(NW * 64, NW > 8 ? 3 : 2) void k_sweep_flatw(TileDev
         for (int q = 0; q < PL; ++q) {
             const int i = lane + 64 * q;
             cv[q] = i < cur.nfn ? acc[i] : 0.0;
-            cid[q] = i < cur.nfn ? (int)fidn[i] : -1;
+            cid[q] = i < cur.nfn ? (idn ? i : (int)fidn[i]) : -1;
         }
         wave_lds_sync();
 #pragma unroll
