@@ -784,6 +784,7 @@ __global__ __launch_bounds__(NW * 64, NW > 8 ? 3 : 2) void k_sweep_flatw(TileDev
     }
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int J = T.tile_J[T.u_tlo[T.fg_unit[k0]]];
+    const FlatDesc* __restrict__ desc = T.fg_desc + k0;
     if (threadIdx.x == 0) L.next = 0;
     if (ABL != 2 && threadIdx.x < kSweepThreads) stage_bias(L.bl, b, (long long)J * kW, n_bins);
     __syncthreads();
@@ -795,27 +796,25 @@ __global__ __launch_bounds__(NW * 64, NW > 8 ? 3 : 2) void k_sweep_flatw(TileDev
     const uint16_t* fidn = rec + 2 * (kR + 1);
     const uint16_t* fidw = fidn + kR;
     struct Tw {
-        int u, t, nr, nfn, nfw;
+        int slot, frec, nr, nfn, nfw;
         uint32_t qbn, qbw;
         const uint4 *payn4, *payw4;
     };
-    // the group's next active tile (LDS counter), false when none is left
+    // the group's next active tile (LDS counter), false when none is left:
+    // one descriptor load (round 3; it was unit -> tile -> split / entries,
+    // four dependent lookups per tile)
     auto grab = [&](Tw& x) -> bool {
         for (;;) {
             int k = 0;
             if (lane == 0) k = atomicAdd(&L.next, 1);
             k = __builtin_amdgcn_readfirstlane(__shfl(k, 0, 64));
             if (k >= nk) return false;
-            const int u = T.fg_unit[k0 + k];
+            const FlatDesc d = desc[k];
             bool on = false;
-            for (int g = T.u_glo[u]; g <= T.u_ghi[u]; ++g) on |= act[g] != 0;
+            for (int g = d.glo; g <= d.ghi; ++g) on |= act[g] != 0;
             if (!on) continue;  // a converged group's rows: k_marg never reads them
-            const int t = T.u_tlo[u];
-            const uint32_t* fw = T.tile_fw + (size_t)t * kFlatMeta;
-            const uint32_t* fww = fw + 2 * (kFlatWaves + 1);
-            x = Tw{u, t, T.u_rhi[u], (int)fw[2 * kFlatWaves + 1], (int)fww[2 * kFlatWaves + 1], fw[2 * kFlatWaves],
-                   fww[2 * kFlatWaves], reinterpret_cast<const uint4*>(T.payn + T.tile_entn[t]),
-                   reinterpret_cast<const uint4*>(T.pay + T.tile_ent[t])};
+            x = Tw{d.slot, d.frec, (int)d.nr, (int)d.nfn, (int)d.nfw, d.qbn, d.qbw,
+                   reinterpret_cast<const uint4*>(T.payn + d.entn), reinterpret_cast<const uint4*>(T.pay + d.ent)};
             return true;
         }
     };
@@ -825,7 +824,7 @@ __global__ __launch_bounds__(NW * 64, NW > 8 ? 3 : 2) void k_sweep_flatw(TileDev
     if (cur.nfn) flat_load<U>(cur.payn4, (uint32_t)lane * U, 0u, cur.qbn, v);
     if (cur.nfw) flat_load<UW>(cur.payw4, (uint32_t)lane * UW, 0u, cur.qbw, vw);
     for (;;) {
-        const uint4* rg = T.frec + (size_t)T.tile_frec[cur.t] * kFrecU4;
+        const uint4* rg = T.frec + (size_t)cur.frec * kFrecU4;
         // stage only the parts of the record the walk reads (the starts up
         // to each segment's end, the row ids of the nonempty rows), and no
         // narrow row ids when every row of the block is nonempty (they are
@@ -877,7 +876,7 @@ __global__ __launch_bounds__(NW * 64, NW > 8 ? 3 : 2) void k_sweep_flatw(TileDev
                 if (nxt.nfw) flat_load<UW>(nxt.payw4, (uint32_t)lane * UW, 0u, nxt.qbw, vw);
             }
         }
-        double* __restrict__ out = part + T.u_slot[cur.u];
+        double* __restrict__ out = part + cur.slot;
         for (int r = lane; r < cur.nr; r += 64) out[r] = acc[r];
         wave_lds_sync();  // this tile's LDS reads before the next tile's writes
         if (PIPE != 2) {

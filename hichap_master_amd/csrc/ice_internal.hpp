@@ -132,6 +132,19 @@ extern int64_t g_flat_group;   // tiles per column group (0 = auto, 11 .. 44)
 // minimum row length (uint4 per row) of band g
 __host__ __device__ constexpr uint32_t band_min(int g) { return g == 0 ? 48u : g == 1 ? 24u : g == 2 ? 12u : g == 3 ? 6u : 1u; }
 
+// One flat unit's descriptor in column-group order (k_sweep_flatw): every
+// field the sweep needs to start the tile, in one 48-byte record, so grabbing
+// the next tile is one (scalar) load instead of a chain of dependent lookups
+// (unit -> tile -> split / entries / record).
+struct FlatDesc {
+    long long entn, ent;     // first narrow / wide entry of the tile
+    int32_t frec, slot;      // flat record index, first unit partial
+    uint32_t qbn, qbw;       // narrow / wide uint4 counts
+    uint16_t nr, nfn, nfw;   // rows of the row-block, nonempty narrow / wide rows
+    uint16_t glo, ghi, pad_[3];  // ICE groups of the unit's rows
+};
+static_assert(sizeof(FlatDesc) == 48, "FlatDesc layout");
+
 // Host plan + arrays of the tiled layout.
 struct TilePlan {
     int64_t nloc = 0;      // local rows
@@ -165,6 +178,7 @@ struct TilePlan {
     std::vector<uint8_t> tile_flat;     // per tile: 1 = flat (every nonempty segment flat)
     std::vector<uint8_t> u_flat;        // per unit: 1 = swept by the flat kernel
     std::vector<int32_t> fg_ptr, fg_unit;  // flat groups (g_flat_cols): units of group g = fg_unit[fg_ptr[g] ..)
+    std::vector<FlatDesc> fg_desc;         // per fg_unit entry
     int64_t n_units_flat = 0;
     int64_t payload_bytes_flat = 0;     // payload of the flat units' tiles
     int64_t n_entries_padded = 0;     // wide slots
@@ -204,6 +218,7 @@ struct TileDev {
     const uint8_t* u_whole;
     const int32_t* fg_ptr;
     const int32_t* fg_unit;
+    const FlatDesc* fg_desc;
     int flat_defer;  // flat kernel: merge a tile's compact sums after the next tile's barrier (hh_tune "flat_defer")
 };
 
@@ -240,6 +255,7 @@ struct hh_matrix {
     hh::DBuf<uint16_t> frec;
     hh::DBuf<uint8_t> u_whole;
     hh::DBuf<int32_t> fg_ptr, fg_unit;  // column groups of the flat units (g_flat_cols)
+    hh::DBuf<hh::FlatDesc> fg_desc;
     int64_t n_fgroups = 0;
     hh::DBuf<long long> wide_ptr;  // local rows + 1
     hh::DBuf<int32_t> wide_col;
@@ -253,7 +269,7 @@ struct hh_matrix {
         return pay.bytes() + payn.bytes() + tile_entn.bytes() + tile_rpn.bytes() + tile_J.bytes() +
                tile_rb.bytes() + tile_ent.bytes() + tile_rp.bytes() +
                u_tlo.bytes() * 7 + blk_unit_ptr.bytes() + tile_perm.bytes() + tile_band.bytes() + u_whole.bytes() + tile_fw.bytes() + tile_frec.bytes() + frec.bytes() + blk_tile_ptr.bytes() + u_glo.bytes() * 2 +
-               fg_ptr.bytes() + fg_unit.bytes() +
+               fg_ptr.bytes() + fg_unit.bytes() + fg_desc.bytes() +
                wide_ptr.bytes() + wide_col.bytes() + wide_cnt.bytes() + diag.bytes() + row_nnz2.bytes() +
                row_sum2.bytes() + row_group.bytes() + band.bytes() + band4.bytes();
     }
@@ -261,7 +277,8 @@ struct hh_matrix {
         return hh::TileDev{pay.p, payn.p, tile_J.p, tile_ent.p, tile_rp.p, tile_entn.p, tile_rpn.p, u_tlo.p,
                            u_thi.p, u_rb.p, u_rlo.p, u_rhi.p, u_slot.p, u_glo.p, u_ghi.p, blk_unit_ptr.p,
                            u_order.p, tile_perm.p, tile_band.p, tile_fw.p, tile_frec.p,
-                           reinterpret_cast<const uint4*>(frec.p), u_whole.p, fg_ptr.p, fg_unit.p, hh::g_flat_defer};
+                           reinterpret_cast<const uint4*>(frec.p), u_whole.p, fg_ptr.p, fg_unit.p, fg_desc.p,
+                           hh::g_flat_defer};
     }
 };
 

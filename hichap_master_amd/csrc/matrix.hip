@@ -439,6 +439,25 @@ TilePlan plan_tiles(const uint16_t* cntw, const uint16_t* cntn, int64_t nloc, in
             for (int32_t k = g.second.first; k < g.second.second; ++k) P.fg_unit.push_back(fu[k]);
             P.fg_ptr.push_back((int32_t)P.fg_unit.size());
         }
+        P.fg_desc.reserve(P.fg_unit.size());
+        for (int32_t u : P.fg_unit) {
+            const int32_t t = P.u_tlo[u];
+            const uint32_t* fw = &P.tile_fw[(size_t)t * kFlatMeta];
+            const uint32_t* fww = fw + 2 * (kFlatWaves + 1);
+            FlatDesc d{};
+            d.entn = P.tile_entn[t];
+            d.ent = P.tile_ent[t];
+            d.frec = P.tile_frec[t];
+            d.slot = P.u_slot[u];
+            d.qbn = fw[2 * kFlatWaves];
+            d.qbw = fww[2 * kFlatWaves];
+            d.nr = (uint16_t)P.u_rhi[u];
+            d.nfn = (uint16_t)fw[2 * kFlatWaves + 1];
+            d.nfw = (uint16_t)fww[2 * kFlatWaves + 1];
+            d.glo = P.u_glo[u];
+            d.ghi = P.u_ghi[u];
+            P.fg_desc.push_back(d);
+        }
     }
     if (g_unit_lpt) {
         // each list by cost class (bit length of words + per-tile cost),
@@ -500,6 +519,7 @@ void upload_plan(const TilePlan& P, hh_matrix& m, hipStream_t s) {
     if (m.n_fgroups) {
         m.fg_ptr = to_device(P.fg_ptr, s);
         m.fg_unit = to_device(P.fg_unit, s);
+        m.fg_desc = to_device(P.fg_desc, s);
     }
     HIP_CHECK(hipStreamSynchronize(s));  // the plan's host vectors may die after return
 }
