@@ -83,11 +83,19 @@ __global__ void k_diag_reduce(const double* __restrict__ part, long long N, long
         for (long long k = klo; k <= klo + 2; ++k) {
             const long long delta = g - k * kCT;
             if (delta < -(kCT - 1) || delta > kCT - 1) continue;
-            for (long long I = 0; I < nT; ++I) {
-                const long long J = I + k;
-                if (J < 0 || J >= nT) continue;
-                acc += part[(size_t)(I * nT + J) * (2 * kCT - 1) + (delta + kCT - 1)];
+            // I over the tiles with 0 <= I + k < nT, in order; eight loads in flight
+            const long long I1 = k < 0 ? nT : nT - k;
+            const size_t step = (size_t)(nT + 1) * (2 * kCT - 1);
+            const double* p = part + (size_t)(k < 0 ? -k * nT : k) * (2 * kCT - 1) + (delta + kCT - 1);
+            long long I = k < 0 ? -k : 0;
+            for (; I + 8 <= I1; I += 8, p += 8 * step) {
+                double v[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) v[u] = p[u * step];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) acc += v[u];
             }
+            for (; I < I1; ++I, p += step) acc += *p;
         }
     }
     out[d] = acc;
@@ -149,7 +157,18 @@ __global__ __launch_bounds__(256) void k_oe_colsum(const double* __restrict__ M,
     const long long r0 = (long long)blockIdx.y * rows_per_chunk;
     const long long r1 = std::min<long long>(N, r0 + rows_per_chunk);
     double acc = 0.0;
-    for (long long i = r0; i < r1; ++i) acc += oe_value(M, dec, N, i, j);
+    long long i = r0;
+    for (; i + 8 <= r1; i += 8) {  // eight rows' loads in flight, summed in row order
+        double m[8], d[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            m[u] = M[(i + u) * N + j];
+            d[u] = dec[i + u > j ? i + u - j : j - i - u];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc += m[u] == 0.0 ? 0.0 : m[u] / d[u];
+    }
+    for (; i < r1; ++i) acc += oe_value(M, dec, N, i, j);
     part[(size_t)blockIdx.y * n + c] = acc;
 }
 
@@ -167,12 +186,17 @@ __global__ __launch_bounds__(256) void k_oe_center(const double* __restrict__ M,
                                                    const long long* __restrict__ ng, const double* __restrict__ mu,
                                                    long long N, long long n, long long Npad, long long ld,
                                                    double* __restrict__ Z) {
-    const long long t = (long long)blockIdx.x * 256 + threadIdx.x;
-    if (t >= Npad * ld) return;
-    const long long i = t / ld, c = t % ld;
-    double v = 0.0;
-    if (i < N && c < n) v = oe_value(M, dec, N, i, ng[c]) - mu[c];
-    Z[t] = v;
+    // rows on grid y (no 64-bit division per element), columns on x
+    const long long c = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (c >= ld) return;
+    const bool col = c < n;
+    const long long j = col ? ng[c] : 0;
+    const double m = col ? mu[c] : 0.0;
+    for (long long i = blockIdx.y; i < Npad; i += gridDim.y) {
+        double v = 0.0;
+        if (i < N && col) v = oe_value(M, dec, N, i, j) - m;
+        Z[i * ld + c] = v;
+    }
 }
 
 // Cov tile (bi, bj), bi <= bj, 128 x 128: 4 waves x (4 x 4) MFMA 16x16x4 f64
@@ -294,19 +318,35 @@ __global__ __launch_bounds__(256) void k_syrk_reduce(const double* __restrict__ 
 
 // numpy corrcoef: c /= sd[:, None]; c /= sd[None, :]; clip(-1, 1); then the
 // reference's NaN -> 0 (an inf cannot survive the clip).  Out of place.
-__global__ void k_corr_norm_oop(const double* __restrict__ Cov, long long n, long long ldc,
-                                double* __restrict__ Cor) {
-    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= ldc * ldc) return;  // the padding rows too: the split-K products read them (x 0)
-    const long long i = t / ldc, j = t % ldc;
-    double v = 0.0;
-    if (i < n && j < n) {
-        const double si = sqrt(Cov[i * ldc + i]), sj = sqrt(Cov[j * ldc + j]);
-        v = (Cov[i * ldc + j] / si) / sj;
-        if (v != v) v = 0.0;
-        else v = v < -1.0 ? -1.0 : (v > 1.0 ? 1.0 : v);
+// sd[i] = sqrt(Cov[i][i]) once (each element used to gather its column's
+// diagonal entry: one cache line per lane), then rows of 4-column groups.
+__global__ void k_cor_sd(const double* __restrict__ Cov, long long n, long long ldc, double* __restrict__ sd) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) sd[i] = sqrt(Cov[i * ldc + i]);
+}
+
+__global__ __launch_bounds__(256) void k_corr_norm_oop(const double* __restrict__ Cov, const double* __restrict__ sd,
+                                                       long long n, long long ldc, double* __restrict__ Cor) {
+    const long long j0 = ((long long)blockIdx.x * 256 + threadIdx.x) * 4;
+    if (j0 >= ldc) return;  // ldc is a multiple of 128
+    for (long long i = blockIdx.y; i < ldc; i += gridDim.y) {  // the padding rows too: the products read them (x 0)
+        const size_t o = (size_t)i * ldc + j0;
+        d4 v = d4{0.0, 0.0, 0.0, 0.0};
+        if (i < n) {
+            const d4 c = *reinterpret_cast<const d4*>(Cov + o);
+            const double si = sd[i];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const long long j = j0 + u;
+                if (j >= n) continue;
+                double x = (c[u] / si) / sd[j];
+                if (x != x) x = 0.0;
+                else x = x < -1.0 ? -1.0 : (x > 1.0 ? 1.0 : x);
+                v[u] = x;
+            }
+        }
+        *reinterpret_cast<d4*>(Cor + o) = v;
     }
-    Cor[t] = v;
 }
 
 // ------------------------------------------------------------------ K8
@@ -320,8 +360,7 @@ __global__ void k_corr_norm_oop(const double* __restrict__ Cov, long long n, lon
 // Cor is ld x ld with zero padding, so only V needs a bound check.
 __global__ __launch_bounds__(256) void k_cor_mul_part(const double* __restrict__ Cor, long long ldc, long long n,
                                                       const double* __restrict__ V, int ksteps,
-                                                      double* __restrict__ part, unsigned* __restrict__ cnt = nullptr,
-                                                      double* __restrict__ Y = nullptr) {
+                                                      double* __restrict__ part) {
     __shared__ double red[3][16 * 64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const long long i0 = (long long)blockIdx.x * 64;
@@ -446,7 +485,7 @@ __global__ __launch_bounds__(256) void k_select_stats(const double* __restrict__
                                                       const long long* __restrict__ ng,
                                                       const int8_t* __restrict__ cls, int K, double eps,
                                                       double* __restrict__ part) {
-    __shared__ double sh[16];
+    __shared__ double sh[4][24];
     const long long i = blockIdx.x;  // one row of Cor / O/E[NG, NG]
     double v[3][8];
 #pragma unroll
@@ -472,11 +511,23 @@ __global__ __launch_bounds__(256) void k_select_stats(const double* __restrict__
             }
         }
     }
-    for (int k = 0; k < K; ++k)
+    // block_sum's tree (xor butterfly per wave, then the waves in order from
+    // 0.0) for all 24 sums with one barrier instead of two per sum
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+#pragma unroll
         for (int q = 0; q < 8; ++q) {
-            const double s = block_sum(v[k][q], sh);
-            if (threadIdx.x == 0) part[((size_t)i * 3 + k) * 8 + q] = s;
+            const double s = wave_sum(v[k][q]);
+            if (lane == 0) sh[wid][k * 8 + q] = s;
         }
+    __syncthreads();
+    if (threadIdx.x < K * 8) {
+        double t = 0.0;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) t += sh[w][threadIdx.x];
+        part[(size_t)i * 24 + threadIdx.x] = t;
+    }
 }
 
 // ------------------------------------------------------------- host algebra
@@ -2123,7 +2174,8 @@ int hh_comp_correlation(hh_comp* c, const double* decline, const int64_t* ng, in
         // centred O/E, padded
         const long long Npad = (N + 15) / 16 * 16;
         DBuf<double> Z((size_t)Npad * c->ld);
-        hipLaunchKernelGGL(k_oe_center, dim3((unsigned)((Npad * c->ld + 255) / 256)), dim3(256), 0, s, Msrc, c->dec.p,
+        hipLaunchKernelGGL(k_oe_center, dim3((unsigned)((c->ld + 255) / 256), (unsigned)std::min<long long>(Npad, 65535)),
+                           dim3(256), 0, s, Msrc, c->dec.p,
                            c->ng.p, mu.p, N, (long long)n, Npad, c->ld, Z.p);
         // Cov = Z^T Z * (1 / (N - 1))  (np.cov: c *= true_divide(1, fact))
         DBuf<double> cov((size_t)c->ld * c->ld);
@@ -2148,8 +2200,11 @@ int hh_comp_correlation(hh_comp* c, const double* decline, const int64_t* ng, in
             }
         }
         c->cor.alloc((size_t)c->ld * c->ld);
-        hipLaunchKernelGGL(k_corr_norm_oop, dim3((unsigned)((c->ld * c->ld + 255) / 256)), dim3(256), 0, s, cov.p,
-                           (long long)n, c->ld, c->cor.p);
+        DBuf<double> sd(n);
+        hipLaunchKernelGGL(k_cor_sd, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, cov.p, (long long)n, c->ld,
+                           sd.p);
+        hipLaunchKernelGGL(k_corr_norm_oop, dim3((unsigned)((c->ld / 4 + 255) / 256), (unsigned)std::min<long long>(c->ld, 65535)),
+                           dim3(256), 0, s, cov.p, sd.p, (long long)n, c->ld, c->cor.p);
         HIP_CHECK(hipGetLastError());
         HIP_CHECK(hipStreamSynchronize(s));
     });
