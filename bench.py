@@ -324,17 +324,27 @@ def run_c5(args, world, rank, local):
     if rank == 0:
         flops = sum(float(sizes[k]) * ng[k] * (ng[k] + 1) for k in mine)  # one (serialised) pass
         syrk_tfs = flops / (syrk_ms / 1000.0) / 1e12 if syrk_ms > 0 else None
-        # Cor . V products: HBM-bound stream of the padded ld x ld correlation
+        # Cor . V products: HBM-bound stream of the padded ld x ld correlation,
+        # its upper triangle of 64 x 64 tiles with k_cor_sym (hh_tune cor_sym, default on)
         ld = {k: (ng[k] + 127) // 128 * 128 for k in mine}
-        mul_bytes = sum(8.0 * ld[k] * ld[k] * prods[k] for k in mine)
+        cor_sym = "cor_sym=0" not in os.environ.get("HH_TUNE", "")
+        if cor_sym:
+            mul_bytes = sum(8.0 * 4096 * (ld[k] // 64) * (ld[k] // 64 + 1) / 2 * prods[k] for k in mine)
+        else:
+            mul_bytes = sum(8.0 * ld[k] * ld[k] * prods[k] for k in mine)
         mul_gbs = mul_bytes / (mul_ms / 1000.0) / 1e9 if mul_ms > 0 else None
         syrk_side = {"bound": "mfma", "kernel": "k_syrk", "achieved": syrk_tfs, "peak": PEAK_F64_MFMA_TFS,
                      "unit": "TFLOP/s", "frac": (syrk_tfs / PEAK_F64_MFMA_TFS) if syrk_tfs else None,
                      "total_ms": syrk_ms, "launches": syrk_n, "flops": flops}
-        mul_side = {"bound": "hbm", "kernel": "k_cor_mul_part (+ k_cor_mul_sum)", "achieved": mul_gbs,
+        mul_side = {"bound": "hbm",
+                    "kernel": "k_cor_sym (+ k_cor_sym_sum)" if cor_sym else "k_cor_mul_part (+ k_cor_mul_sum)",
+                    "achieved": mul_gbs,
                     "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": (mul_gbs / PEAK_HBM_GBS) if mul_gbs else None,
                     "total_ms": mul_ms, "launches": mul_n, "alg_bytes": mul_bytes,
-                    "alg_bytes_note": "8 B x ld^2 (the padded correlation) per Cor.V product"}
+                    "alg_bytes_note": ("8 B x the upper triangle of 64 x 64 tiles of the padded correlation per "
+                                       "Cor.V product (k_cor_sym reads each off-diagonal tile once for both "
+                                       "products; its partials, 2 x 128 B x (ld / 256 + 1) per row, are not counted)")
+                    if cor_sym else "8 B x ld^2 (the padded correlation) per Cor.V product"}
         # the Krylov orthogonalisation (one k_ortho launch per product): per
         # cycle of P = 8 products block j reads the basis Q_0..Q_j twice (two
         # Gram-Schmidt passes) and W / its CholeskyQR iterates ~3 times, and

@@ -421,6 +421,157 @@ __global__ __launch_bounds__(256) void k_cor_mul_part(const double* __restrict__
     }
 }
 
+// Y = Cor V from the upper triangle only (half the bytes of k_cor_mul_part).
+// Cor in 64 x 64 tiles (a, b); a block owns a 256 x 256 rectangle (p, q),
+// p <= q, and wave w its 64-row tile a = 4p + w.  For tile (a, b):
+//   column product  Y[b cols] += Cor[a, b]^T V[a rows]   (a <= b)
+//   row product     Y[a rows] += Cor[a, b] V[b cols]     (a <  b)
+// so row i gets sum_{c in tiles <= tile(i)} Cor[c][i] V[c] from the column
+// products and sum_{c in tiles > tile(i)} Cor[i][c] V[c] from the row
+// products (Cor is symmetric up to the rounding of corrcoef's two divisions).
+// Column product: the lane's d4 of a Cor row is the MFMA A operand (as in
+// k_cor_mul_part, reduction over rows); row product: the wave's 16 x 64
+// chunk goes through LDS so that a lane's A operand runs along a row
+// (reduction over columns).  Column partials of the 4 waves are summed in
+// wave order -> part_c[p][col]; row partials accumulate over the
+// rectangle's column tiles in registers -> part_r[q][row].
+// k_cor_sym_sum adds, for row i in range P, part_c[0..P] then part_r[P..].
+// Deterministic (fixed order everywhere).
+constexpr int kCsR = 256;  // rectangle edge (4 tiles)
+constexpr int kCsW = 66;   // LDS row stride (doubles) of the transpose buffer
+
+__global__ __launch_bounds__(256, 2) void k_cor_sym(const double* __restrict__ Cor, long long ldc, long long n,
+                                                   const double* __restrict__ V, long long nr,
+                                                   double* __restrict__ part_c, double* __restrict__ part_r) {
+    // per-wave transpose buffer; at the end of a column tile the same space
+    // holds the wave's column partial (64 x 16 doubles)
+    __shared__ double Wt[4][16 * kCsW];
+    __shared__ double Vc[64 * kSB];  // V rows of the current column tile (row-product B operands)
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, lr = lane >> 4, lc = lane & 15;
+    long long p, q;
+    syrk_tile_ij(blockIdx.x, nr, p, q);
+    const long long R0 = p * kCsR + 64 * w;  // this wave's rows
+    const bool rows_ok = R0 < ldc;
+    const bool diag = p == q;
+    // column-product B operands (fixed rows): bv[g][j] = V[R0 + 16 g + 4 j + lr][lc]
+    double bv[4][4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const long long r = R0 + 16 * g + 4 * j + lr;
+            const double x = V[(r < n ? r : n - 1) * kSB + lc];
+            bv[g][j] = r < n ? x : 0.0;
+        }
+    d4 dr[4];  // row-product accumulators: rows R0 + 16 g + lr + 4 reg, column lc
+#pragma unroll
+    for (int g = 0; g < 4; ++g) dr[g] = d4{0.0, 0.0, 0.0, 0.0};
+    double* wt = Wt[w];
+    for (int ct = 0; ct < 4; ++ct) {
+        const long long C0 = q * kCsR + 64 * ct;
+        if (C0 >= ldc) break;  // uniform over the block
+        // tile (a, b) = (4p + w, 4q + ct): diagonal rectangle -> skip below, column product only on the diagonal
+        const bool col_on = rows_ok && (!diag || ct >= w);
+        const bool row_on = rows_ok && (!diag || ct > w);
+        for (int e = threadIdx.x; e < 64 * kSB; e += 256) {
+            const long long c = C0 + e / kSB;
+            Vc[e] = c < n ? V[c * kSB + e % kSB] : 0.0;
+        }
+        __syncthreads();
+        d4 acc[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc[t] = d4{0.0, 0.0, 0.0, 0.0};
+        if (col_on) {
+            const double* cp = Cor + (R0 + lr) * ldc + C0 + 4 * lc;
+            d4 av[4], an[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) av[j] = __builtin_nontemporal_load(reinterpret_cast<const d4*>(cp + 4 * j * ldc));
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                if (g < 3)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        an[j] = __builtin_nontemporal_load(
+                            reinterpret_cast<const d4*>(cp + (16 * (g + 1) + 4 * j) * ldc));
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+#pragma unroll
+                    for (int t = 0; t < 4; ++t)
+                        acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[j][t], bv[g][j], acc[t], 0, 0, 0);
+                if (row_on) {
+                    // the wave's 16 x 64 chunk -> LDS (row 4 j + lr), then A' = Wt[m = lc][4 cs + lr]
+                    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+#pragma unroll
+                        for (int t = 0; t < 4; ++t) wt[(4 * j + lr) * kCsW + 4 * lc + t] = av[j][t];
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+                    for (int cs = 0; cs < 16; ++cs)
+                        dr[g] = __builtin_amdgcn_mfma_f64_16x16x4f64(wt[lc * kCsW + 4 * cs + lr],
+                                                                      Vc[(4 * cs + lr) * kSB + lc], dr[g], 0, 0, 0);
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                }
+                if (g < 3)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) av[j] = an[j];
+            }
+        }
+        // column partial of this column tile: the 4 waves in order
+        // (D layout: column lc, row lr + 4 reg -> Cor column C0 + 4 (lr + 4 reg) + t)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int reg = 0; reg < 4; ++reg) wt[(4 * (lr + 4 * reg) + t) * kSB + lc] = acc[t][reg];
+        __syncthreads();
+        double* out = part_c + ((size_t)p * ldc + C0) * kSB;
+        for (int e = threadIdx.x; e < 64 * kSB; e += 256) out[e] = ((Wt[0][e] + Wt[1][e]) + Wt[2][e]) + Wt[3][e];
+        __syncthreads();
+    }
+    if (!rows_ok) return;
+    double* outr = part_r + ((size_t)q * ldc + R0) * kSB;
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) outr[(16 * g + lr + 4 * reg) * kSB + lc] = dr[g][reg];
+}
+
+// Y[i][b] = sum_{p <= P} part_c[p][i][b] + sum_{q >= P} part_r[q][i][b], P = i / 256
+__global__ void k_cor_sym_sum(const double* __restrict__ part_c, const double* __restrict__ part_r, long long ldc,
+                              long long n, long long nr, double* __restrict__ Y) {
+    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n * kSB) return;
+    const long long P = (t / kSB) / kCsR;
+    const size_t stride = (size_t)ldc * kSB;
+    double acc = 0.0;
+    const double* pc = part_c + t;
+    long long s = 0;
+    for (; s + 4 <= P + 1; s += 4) {
+        double v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = pc[(s + u) * stride];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc += v[u];
+    }
+    for (; s <= P; ++s) acc += pc[s * stride];
+    const double* pr = part_r + t;
+    s = P;
+    for (; s + 4 <= nr; s += 4) {
+        double v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = pr[(s + u) * stride];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc += v[u];
+    }
+    for (; s < nr; ++s) acc += pr[s * stride];
+    Y[t] = acc;
+}
+
 // Y[i][b] = sum_s part[s][i][b] - x_i d_b   (x nullptr -> 1; d nullptr -> none)
 __global__ void k_cor_mul_sum(const double* __restrict__ part, int ks, long long ldc, long long n,
                               const double* __restrict__ x, const double* __restrict__ d, double* __restrict__ Y) {
@@ -688,6 +839,7 @@ struct PcaWork {
         ks = (int)((steps + ksteps - 1) / ksteps);
         mpart.alloc((size_t)ks * ldc * kSB);
     }
+    DBuf<double> sym_c, sym_r;  // k_cor_sym partials (allocated at the first symmetric product)
     // G = X^T Y on the device (B x B), fixed-order reduction
     void gram_dev(const double* X, const double* Y, hipStream_t s) {
         hipLaunchKernelGGL(k_gram_part, dim3(nblk), dim3(256), 0, s, X, Y, n, part.p);
@@ -701,6 +853,20 @@ struct PcaWork {
     }
     // Y = Cor V - x d^T, d = row 0 of the last gram_dev (d_use) or none
     void cor_mul(const double* Cor, const double* V, const double* x, bool d_use, double* Y, hipStream_t s) {
+        if (!x && !d_use && g_cor_sym) {  // plain product: upper triangle only (k_cor_sym)
+            const long long nr = (ldc + kCsR - 1) / kCsR;
+            if (!sym_c.p) {
+                sym_c.alloc((size_t)nr * ldc * kSB);
+                sym_r.alloc((size_t)nr * ldc * kSB);
+            }
+            HH_KTIME("k_cor_mul", s);
+            // (occupancy 2: 190 VGPRs; forcing 3 spills and measured 98.9 vs 105.9 chromosomes/s)
+            hipLaunchKernelGGL(k_cor_sym, dim3((unsigned)(nr * (nr + 1) / 2)), dim3(256), 0, s, Cor, ldc, n, V, nr,
+                               sym_c.p, sym_r.p);
+            hipLaunchKernelGGL(k_cor_sym_sum, dim3((unsigned)((n * kSB + 255) / 256)), dim3(256), 0, s, sym_c.p,
+                               sym_r.p, ldc, n, nr, Y);
+            return;
+        }
         {
             HH_KTIME("k_cor_mul", s);
             hipLaunchKernelGGL(k_cor_mul_part, dim3((unsigned)(ldc / 64), (unsigned)ks), dim3(256), 0, s, Cor, ldc, n, V,

@@ -2520,6 +2520,9 @@ int hh_tune(const char* key, int64_t value) {
         } else if (k == "pca_coop") {
             HH_REQUIRE(value == 0 || value == 1, "pca_coop in {0, 1}");
             g_pca_coop = (int)value;
+        } else if (k == "cor_sym") {
+            HH_REQUIRE(value == 0 || value == 1, "cor_sym in {0, 1}");
+            g_cor_sym = (int)value;
         } else if (k == "pca_p") {
             HH_REQUIRE(value >= 2 && value <= 8, "pca_p in [2, 8]");
             g_pca_p = (int)value;

@@ -242,3 +242,37 @@ def test_pca_one_launch_large_rows_per_block():
     for q in range(3):
         np.testing.assert_allclose(_match_sign(pcs[q], U[:, q]), U[:, q], atol=1e-11)
     np.testing.assert_allclose(ev, s[:3] ** 2, rtol=1e-11)
+
+
+def _pca_run_sym(dM, sym):
+    from hichap_master_amd._lib import call
+    from hichap_master_amd.StructureFind import StructureFind
+    call("hh_tune", b"cor_sym", sym)
+    try:
+        sf = StructureFind(Res=C5_RES)
+        dec, G, NG = sf.Distance_Decay(M=dM, G_array=None)
+        pcs, Cor, OE = sf.Get_PCA(distance_bin=dec.copy(), M=dM, NG_array=NG)
+        return np.asarray(pcs), dict(sf.pca_status), NG.size
+    finally:
+        call("hh_tune", b"cor_sym", 1)
+
+
+@pytest.mark.parametrize("chrom", [21, 9])
+def test_pca_upper_triangle_product_matches_full(chrom):
+    """k_cor_sym (Cor V from the upper triangle of 64 x 64 tiles: column
+    products of the tiles on and above the diagonal, row products of those
+    strictly above) against the full-matrix split-K product: the same
+    components / eigenvalues to rounding (corrcoef's Cor is symmetric only up
+    to the rounding of its two divisions), and bitwise run-to-run; chr21 and
+    chr9 (padded orders 1 920 / 5 504 at this generator's gaps: neither a
+    multiple of the 256-row rectangle, so the last range is ragged)."""
+    dM = _c5_matrix(chrom - 1)
+    p0, s0, n = _pca_run_sym(dM, 0)
+    p1, s1, _ = _pca_run_sym(dM, 1)
+    p2, _, _ = _pca_run_sym(dM, 1)
+    assert s0["converged"] and s1["converged"]
+    assert abs(s1["products"] - s0["products"]) <= 8, (s0, s1)
+    for q in range(3):
+        np.testing.assert_allclose(_match_sign(p1[q], p0[q]), p0[q], atol=1e-11)
+    np.testing.assert_allclose(s1["eigvals"], s0["eigvals"], rtol=1e-12)
+    np.testing.assert_array_equal(p1, p2)
