@@ -1866,7 +1866,13 @@ static bool pca_krylov(PcaWork& wk, const double* cor, long long n, int k, doubl
         hipLaunchKernelGGL(k_gram_ms, dim3((unsigned)(nb * BB)), dim3(64), 0, s, qpart.p, nap, out);
     };
     // one-launch orthogonalisation (k_ortho): a block owns 64 * tpb rows
-    const int tpb = nap <= 4 * kOrthoMaxBlocks ? 4 : 8;
+    // (the fewest rows per block that fit the grid: more CUs pull the basis
+    // rows; 128 instead of 256 rows took the serial k_ortho 163 -> 144 ms)
+    int tpb = 8;
+    if (g_ortho_tpb > 0 && nap <= g_ortho_tpb * kOrthoMaxBlocks) tpb = g_ortho_tpb;
+    else
+        for (int t : {g_ortho_min_tpb, 2, 4})
+            if (t >= g_ortho_min_tpb && nap <= t * kOrthoMaxBlocks) { tpb = t; break; }
     const int oblk = (nap + tpb - 1) / tpb;
     const bool coop = g_pca_coop && oblk <= kOrthoMaxBlocks;
     DBuf<double> orp(coop ? (size_t)oblk * kOrthoMaxE : 1), oro(kOrthoMaxE), ogp(coop ? (size_t)2 * oblk * BB : 1);
@@ -1892,7 +1898,9 @@ static bool pca_krylov(PcaWork& wk, const double* cor, long long n, int k, doubl
         HH_KTIME("k_ortho", s);  // bench.py's C5 line: the dominant kernel by time
 #define HH_ORTHO(M)                                                  \
     do {                                                             \
-        if (tpb == 4) hipLaunchKernelGGL((k_ortho<M, 4>), grid, blk, 0, s, a); \
+        if (tpb == 1) hipLaunchKernelGGL((k_ortho<M, 1>), grid, blk, 0, s, a); \
+        else if (tpb == 2) hipLaunchKernelGGL((k_ortho<M, 2>), grid, blk, 0, s, a); \
+        else if (tpb == 4) hipLaunchKernelGGL((k_ortho<M, 4>), grid, blk, 0, s, a); \
         else hipLaunchKernelGGL((k_ortho<M, 8>), grid, blk, 0, s, a);          \
     } while (0)
         switch (mode) {

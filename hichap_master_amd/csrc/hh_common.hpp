@@ -111,6 +111,8 @@ inline int g_pca_method = 1;
 inline int g_syrk_split = -1;  // Cov K splits (hh_tune "syrk_split"): -1 auto, 0 never, n > 0 forced
 inline int g_pca_p = 8;
 inline int g_cor_sym = 1;  // hh_tune "cor_sym": Krylov Cor products read the upper triangle only (k_cor_sym)
+inline int g_ortho_tpb = 0;  // hh_tune "ortho_tpb": k_ortho rows per block / 64 (0: auto)
+inline int g_ortho_min_tpb = 2;  // hh_tune "ortho_min_tpb": the automatic choice's smallest rows per block / 64
 inline int g_pca_coop = 1;  // hh_tune "pca_coop": Krylov orthogonalisation in one launch per product (k_ortho)
 inline int g_pca_debug = 0;  // hh_tune "pca_debug": per-cycle trace on stderr
 

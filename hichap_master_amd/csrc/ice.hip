@@ -2523,6 +2523,13 @@ int hh_tune(const char* key, int64_t value) {
         } else if (k == "cor_sym") {
             HH_REQUIRE(value == 0 || value == 1, "cor_sym in {0, 1}");
             g_cor_sym = (int)value;
+        } else if (k == "ortho_tpb") {
+            HH_REQUIRE(value == 0 || value == 1 || value == 2 || value == 4 || value == 8,
+                       "ortho_tpb in {0 (auto), 1, 2, 4, 8}");
+            g_ortho_tpb = (int)value;
+        } else if (k == "ortho_min_tpb") {
+            HH_REQUIRE(value == 1 || value == 2, "ortho_min_tpb in {1, 2}");
+            g_ortho_min_tpb = (int)value;
         } else if (k == "pca_p") {
             HH_REQUIRE(value >= 2 && value <= 8, "pca_p in [2, 8]");
             g_pca_p = (int)value;
