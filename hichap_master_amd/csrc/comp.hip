@@ -19,6 +19,7 @@
 // All reductions are fixed-order (deterministic).
 #include <algorithm>
 #include <chrono>
+#include <cstring>
 #include <cmath>
 #include <limits>
 #include <numeric>
@@ -1823,12 +1824,23 @@ static bool pca_krylov(PcaWork& wk, const double* cor, long long n, int k, doubl
     double* galt = gpart2.p;
     // small outputs of one cycle, per block j: c1 [P], c2 [P], R x 6, G
     const int slot = (2 * P + 7) * BB;
-    DBuf<double> smalls((size_t)P * slot + 3 * BB);  // + the restart block's R factors
+    // + the restart block's R factors, then the Cholesky flags (ints: per
+    // block j slots j * 8 + 0..5; restart P * 8 + 0..2; abort P * 8 + 7):
+    // one download per cycle
+    const int nfl = P * 8 + 8;
+    DBuf<double> smalls((size_t)P * slot + 3 * BB + (nfl + 1) / 2);
     double* restartR = smalls.p + (size_t)P * slot;
-    DBuf<int> fail(P * 8 + 8);  // per block j: slots j * 8 + 0..5; restart: P * 8 + 0..2
+    struct {
+        int* p;
+    } fail{reinterpret_cast<int*>(smalls.p + (size_t)P * slot + 3 * BB)};
     DBuf<double> Ydev((size_t)P * B * B);
-    std::vector<double> hs((size_t)P * slot + 3 * BB);
-    std::vector<int> hf(P * 8 + 8);
+    std::vector<double> hs((size_t)P * slot + 3 * BB + (nfl + 1) / 2);
+    std::vector<int> hf(nfl);
+    auto download_smalls = [&]() {  // hs, hf <- the device (one copy), synchronised
+        smalls.download(hs.data(), hs.size(), s);
+        HIP_CHECK(hipStreamSynchronize(s));
+        std::memcpy(hf.data(), hs.data() + (size_t)P * slot + 3 * BB, sizeof(int) * nfl);
+    };
     auto gram = [&](const double* Xs, int nb, const double* Y, double* out) {
         hipLaunchKernelGGL(k_gram_mp, dim3((unsigned)nblk, (unsigned)nb), dim3(256), 0, s, Xs, nb, Y, n, nblk, part.p);
         hipLaunchKernelGGL(k_gram_ms, dim3((unsigned)(nb * BB)), dim3(64), 0, s, part.p, nblk, out);
@@ -1930,7 +1942,7 @@ static bool pca_krylov(PcaWork& wk, const double* cor, long long n, int k, doubl
             throw Error(HH_ERR_HIP, "k_ortho: grid barrier timed out (blocks not co-resident); rerun with "
                                     "hh_tune(\"pca_coop\", 0)");
     };
-    fail.zero(s);
+    HIP_CHECK(hipMemsetAsync(fail.p, 0, sizeof(int) * nfl, s));
     // start block: [1 / sqrt(n) | deterministic pseudo-random columns]; the
     // host source of the upload lives until the first cycle's synchronise
     std::vector<double> v0((size_t)n * B);
@@ -1952,6 +1964,9 @@ static bool pca_krylov(PcaWork& wk, const double* cor, long long n, int k, doubl
         }
     }
     std::vector<double> cur((size_t)n * k), Xh((size_t)n * B);
+    // Ritz coefficients: their upload's host source lives until the next
+    // cycle's synchronise
+    std::vector<double> ev, Y;
     double last_bound = 1e300;
     int products = 0, cycles = 0;
     bool done = false;
@@ -2003,10 +2018,8 @@ static bool pca_krylov(PcaWork& wk, const double* cor, long long n, int k, doubl
                 hipLaunchKernelGGL(k_gram_ms, dim3((unsigned)BB), dim3(64), 0, s, gcur, nap, G);
             }
         }
-        smalls.download(hs.data(), hs.size(), s);
-        fail.download(hf.data(), hf.size(), s);
         const auto c0 = std::chrono::steady_clock::now();
-        HIP_CHECK(hipStreamSynchronize(s));
+        download_smalls();
         const auto c1 = std::chrono::steady_clock::now();
         const double t_w = std::chrono::duration<double, std::milli>(c1 - c0).count();
         check_abort(hf);
@@ -2089,7 +2102,6 @@ static bool pca_krylov(PcaWork& wk, const double* cor, long long n, int k, doubl
                 for (int b = 0; b < B; ++b) H[(size_t)(o + a) * mb + o + b] += 0.5 * (extraG[a * B + b] + extraG[b * B + a]);
         }
         const auto c2 = std::chrono::steady_clock::now();
-        std::vector<double> ev, Y;
         sym_topk(mb, H, B, ev, Y);
         const auto c3 = std::chrono::steady_clock::now();
         const double t_h = std::chrono::duration<double, std::milli>(c2 - c1).count();
@@ -2161,14 +2173,8 @@ static bool pca_krylov(PcaWork& wk, const double* cor, long long n, int k, doubl
         } else {
             hipLaunchKernelGGL(k_comb_mp, dim3(ge), dim3(256), 0, s, nullptr, Q.p, last + 1, Ydev.p, n, X.p);
         }
-        X.download(Xh.data(), Xh.size(), s);
-        HIP_CHECK(hipStreamSynchronize(s));
-        for (int q = 0; q < k; ++q) {
-            double nn = 0.0;
-            for (long long i = 0; i < n; ++i) nn += Xh[i * B + q] * Xh[i * B + q];
-            const double inv = 1.0 / std::sqrt(nn);
-            for (long long i = 0; i < n; ++i) cur[q * n + i] = Xh[i * B + q] * inv;
-        }
+        // (the Ritz vectors stay on the device until the loop ends: no
+        // download and no synchronise per cycle)
         if (!done && !coop) {
             hipLaunchKernelGGL(k_start_block, dim3(ge), dim3(256), 0, s, X.p, n, T2.p);
             HIP_CHECK(hipMemsetAsync(fail.p + P * 8, 0, sizeof(int) * 8, s));
@@ -2178,9 +2184,18 @@ static bool pca_krylov(PcaWork& wk, const double* cor, long long n, int k, doubl
     }
     // a budget-exhausted run leaves a restart block enqueued: drain the
     // stream before this function's buffers go back to the pool
-    fail.download(hf.data(), hf.size(), s);
-    HIP_CHECK(hipStreamSynchronize(s));
+    download_smalls();
     check_abort(hf);
+    if (cycles > 0) {  // the last cycle's Ritz vectors
+        X.download(Xh.data(), Xh.size(), s);
+        HIP_CHECK(hipStreamSynchronize(s));
+        for (int q = 0; q < k; ++q) {
+            double nn = 0.0;
+            for (long long i = 0; i < n; ++i) nn += Xh[i * B + q] * Xh[i * B + q];
+            const double inv = 1.0 / std::sqrt(nn);
+            for (long long i = 0; i < n; ++i) cur[q * n + i] = Xh[i * B + q] * inv;
+        }
+    }
     if (!done) st.converged = 0;
     st.products = products;
     st.cycles = cycles;
