@@ -1233,26 +1233,50 @@ struct OrthoLds {
 };
 
 template <int MODE, int TPB>
-__global__ __launch_bounds__(256) void k_ortho(OrthoArgs A) {
+__global__ __launch_bounds__(256) void k_ortho(OrthoArgs Ain) {
+    // the arguments as locals (the lambdas below captured the by-value
+    // struct by reference, which kept a copy of it in scratch)
+    const auto A_G = Ain.G;
+    const auto A_Q = Ain.Q;
+    const auto A_R = Ain.R;
+    const auto A_Y = Ain.Y;
+    const auto A_abort = Ain.abort;
+    const auto A_c1 = Ain.c1;
+    const auto A_c2 = Ain.c2;
+    const auto A_ctr = Ain.ctr;
+    const auto A_fail = Ain.fail;
+    const auto A_gpart = Ain.gpart;
+    const auto A_n = Ain.n;
+    const auto A_nb = Ain.nb;
+    const auto A_nblk = Ain.nblk;
+    const auto A_par = Ain.par;
+    const auto A_qnext = Ain.qnext;
+    const auto A_rout = Ain.rout;
+    const auto A_rpart = Ain.rpart;
+    const auto A_shift_scale = Ain.shift_scale;
+    const auto A_tstamp = Ain.tstamp;
+    const auto A_xin = Ain.xin;
+    const auto A_xout = Ain.xout;
+
     constexpr int B = kSB, BB = kSB * kSB, RPB = 64 * TPB;
     __shared__ OrthoLds<TPB> L;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6, lr = lane >> 4, lc = lane & 15;
-    const int nblk = A.nblk, g = blockIdx.x;
-    const long long n = A.n, r0 = (long long)g * RPB;
+    const int nblk = A_nblk, g = blockIdx.x;
+    const long long n = A_n, r0 = (long long)g * RPB;
     unsigned bar = 0;
-    auto stamp = [&](int k) {
-        if (A.tstamp && g == 0 && t == 0) A.tstamp[k] = (long long)wall_clock64();
+    auto stamp = [&](int k) __attribute__((always_inline)) {
+        if (A_tstamp && g == 0 && t == 0) A_tstamp[k] = (long long)wall_clock64();
     };
     stamp(0);
-    if (g == 0 && t == 0) A.ctr[1 - A.par] = 0ull;  // the previous launch's counter (it has completed)
-    auto gsync = [&]() {
+    if (g == 0 && t == 0) A_ctr[1 - A_par] = 0ull;  // the previous launch's counter (it has completed)
+    auto gsync = [&]() __attribute__((always_inline)) {
         ++bar;
         stamp(2 * bar - 1);
-        ortho_grid_sync(A.ctr + A.par, (unsigned long long)bar * (unsigned long long)nblk, A.abort);
+        ortho_grid_sync(A_ctr + A_par, (unsigned long long)bar * (unsigned long long)nblk, A_abort);
         stamp(2 * bar);
     };
     // ---- block-local pieces
-    auto gram_part = [&](double* dst) {  // dst[g][256] = X^T X over the block's rows
+    auto gram_part = [&](double* dst) __attribute__((always_inline)) {  // dst[g][256] = X^T X over the block's rows
         d4 acc = d4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int m = 0; m < TPB; ++m)
@@ -1270,8 +1294,8 @@ __global__ __launch_bounds__(256) void k_ortho(OrthoArgs A) {
     // rpart[g][k][256] = Q_k^T X over the block's rows: each wave its row
     // groups, four k at a time with all their loads in flight (one round
     // trip per four k), the waves' partials summed in wave order
-    auto proj_part = [&]() {
-        const int nb = A.nb;
+    auto proj_part = [&]() __attribute__((always_inline)) {
+        const int nb = A_nb;
         for (int kc = 0; kc < nb; kc += 4) {
             d4 acc[4];
 #pragma unroll
@@ -1284,7 +1308,7 @@ __global__ __launch_bounds__(256) void k_ortho(OrthoArgs A) {
 #pragma unroll
                     for (int c = 0; c < 4; ++c) {
                         const long long i = r0 + (w + 4 * m) * 16 + 4 * c + lr;
-                        q[kk][c] = (kc + kk < nb && i < n) ? A.Q[((size_t)(kc + kk) * n + i) * B + lc] : 0.0;
+                        q[kk][c] = (kc + kk < nb && i < n) ? A_Q[((size_t)(kc + kk) * n + i) * B + lc] : 0.0;
                     }
 #pragma unroll
                 for (int kk = 0; kk < 4; ++kk)
@@ -1301,13 +1325,13 @@ __global__ __launch_bounds__(256) void k_ortho(OrthoArgs A) {
         }
         __syncthreads();
         for (int e = t; e < nb * BB; e += 256)
-            A.rpart[(size_t)g * kOrthoMaxE + e] = ((L.ws[0][e] + L.ws[1][e]) + L.ws[2][e]) + L.ws[3][e];
+            A_rpart[(size_t)g * kOrthoMaxE + e] = ((L.ws[0][e] + L.ws[1][e]) + L.ws[2][e]) + L.ws[3][e];
         __syncthreads();
     };
     // X (+|-)= sum_k Q_k cm_k over the block's rows (ADD: X = sum, X zero
     // before); four k at a time with all their loads in flight
-    auto mul_q = [&](bool add) {
-        const int nb = A.nb;
+    auto mul_q = [&](bool add) __attribute__((always_inline)) {
+        const int nb = A_nb;
         d4 acc[TPB];
 #pragma unroll
         for (int m = 0; m < TPB; ++m) acc[m] = d4{0.0, 0.0, 0.0, 0.0};
@@ -1321,7 +1345,7 @@ __global__ __launch_bounds__(256) void k_ortho(OrthoArgs A) {
 #pragma unroll
                     for (int jj = 0; jj < 4; ++jj)
                         q[m][kk][jj] =
-                            (kc + kk < nb && i < n) ? A.Q[((size_t)(kc + kk) * n + i) * B + 4 * jj + lr] : 0.0;
+                            (kc + kk < nb && i < n) ? A_Q[((size_t)(kc + kk) * n + i) * B + 4 * jj + lr] : 0.0;
             }
 #pragma unroll
             for (int kk = 0; kk < 4; ++kk) {
@@ -1349,7 +1373,7 @@ __global__ __launch_bounds__(256) void k_ortho(OrthoArgs A) {
     };
     // L.gs = sum over blocks of gp (fixed block order), every block; all
     // nblk loads in flight at once
-    auto reduce_gram = [&](const double* gp) {
+    auto reduce_gram = [&](const double* gp) __attribute__((always_inline)) {
         double v[kOrthoMaxBlocks];
 #pragma unroll
         for (int b = 0; b < kOrthoMaxBlocks; ++b) v[b] = b < nblk ? ld_agent(gp + (size_t)b * BB + t) : 0.0;
@@ -1361,23 +1385,23 @@ __global__ __launch_bounds__(256) void k_ortho(OrthoArgs A) {
     };
     // nb x 256 projection sums: barrier, reduce-scatter over the blocks,
     // barrier, every block reads all of them into L.cm (block 0 also to `out`)
-    auto reduce_proj = [&](double* out) {
+    auto reduce_proj = [&](double* out) __attribute__((always_inline)) {
         gsync();  // every block's partials are in
-        const int E = A.nb * BB, chunk = (E + nblk - 1) / nblk;
+        const int E = A_nb * BB, chunk = (E + nblk - 1) / nblk;
         const int e1 = min(E, (g + 1) * chunk);
         for (int e = g * chunk + t; e < e1; e += 256) {
             double v[kOrthoMaxBlocks];
 #pragma unroll
             for (int b = 0; b < kOrthoMaxBlocks; ++b)
-                v[b] = b < nblk ? ld_agent(A.rpart + (size_t)b * kOrthoMaxE + e) : 0.0;
+                v[b] = b < nblk ? ld_agent(A_rpart + (size_t)b * kOrthoMaxE + e) : 0.0;
             double acc = 0.0;
 #pragma unroll
             for (int b = 0; b < kOrthoMaxBlocks; ++b) acc += v[b];
-            A.rout[e] = acc;
+            A_rout[e] = acc;
         }
         gsync();
         for (int e = t; e < E; e += 256) {
-            const double v = ld_agent(A.rout + e);
+            const double v = ld_agent(A_rout + e);
             L.cm[e] = v;
             if (g == 0) out[e] = v;
         }
@@ -1389,12 +1413,12 @@ __global__ __launch_bounds__(256) void k_ortho(OrthoArgs A) {
     // row / diagonal come from their lanes by v_readlane (the loop indices are
     // compile-time: no LDS round trip per step, as the shuffles were); not
     // positive definite -> R = I and the flag
-    auto chol = [&](bool shifted, double* Rout, int* flag) {
+    auto chol = [&](bool shifted, double* Rout, int* flag) __attribute__((always_inline)) {
         if (w == 0) {
             double tr = 0.0;
 #pragma unroll
             for (int i = 0; i < B; ++i) tr += L.gs[i * B + i];
-            const double shift = shifted ? A.shift_scale * tr : 0.0;
+            const double shift = shifted ? A_shift_scale * tr : 0.0;
             const int c = lc;
             double gcol[B], rcol[B];
 #pragma unroll
@@ -1433,7 +1457,7 @@ __global__ __launch_bounds__(256) void k_ortho(OrthoArgs A) {
         }
         __syncthreads();
     };
-    auto apply_rinv = [&]() {  // row <- row R^{-1} (forward substitution, a thread per row)
+    auto apply_rinv = [&]() __attribute__((always_inline)) {  // row <- row R^{-1} (forward substitution, a thread per row)
         for (int r = t; r < RPB; r += 256) {
             double x[B];
 #pragma unroll
@@ -1452,8 +1476,8 @@ __global__ __launch_bounds__(256) void k_ortho(OrthoArgs A) {
     // the Gram buffers alternate so a block's next partial never overwrites
     // one another block may still be reading
     unsigned gsel = 0;
-    auto cholqr = [&](bool shifted, double* Rout, int* flag) {
-        double* gp = A.gpart + (size_t)(gsel & 1u) * nblk * BB;
+    auto cholqr = [&](bool shifted, double* Rout, int* flag) __attribute__((always_inline)) {
+        double* gp = A_gpart + (size_t)(gsel & 1u) * nblk * BB;
         const bool st = gsel == 1;  // pca_debug 2: the second pass in detail
         ++gsel;
         if (st) stamp(40);
@@ -1473,7 +1497,7 @@ __global__ __launch_bounds__(256) void k_ortho(OrthoArgs A) {
     // rounding-level direction), one plain pass finishes it (CholQR2's
     // regime) and the third factor is the identity; otherwise shifted,
     // shifted, plain.  Every block takes the same branch (same R).
-    auto scholqr3 = [&](double* R3, int* fl) {
+    auto scholqr3 = [&](double* R3, int* fl) __attribute__((always_inline)) {
         cholqr(true, R3, fl);
         double mx = 0.0, mn = 1e300;
 #pragma unroll
@@ -1493,7 +1517,7 @@ __global__ __launch_bounds__(256) void k_ortho(OrthoArgs A) {
             cholqr(false, R3 + 2 * BB, fl + 2);
         }
     };
-    auto store_rows = [&](double* dst) {
+    auto store_rows = [&](double* dst) __attribute__((always_inline)) {
         for (int e = t; e < RPB * B; e += 256) {
             const long long i = r0 + e / B;
             if (i < n) dst[i * B + e % B] = L.x[e / B][e % B];
@@ -1503,13 +1527,13 @@ __global__ __launch_bounds__(256) void k_ortho(OrthoArgs A) {
     if (MODE != kOrthoRitz) {  // W (Full / Last) or the start block
         for (int e = t; e < RPB * B; e += 256) {
             const long long i = r0 + e / B;
-            L.x[e / B][e % B] = i < n ? A.xin[i * B + e % B] : 0.0;
+            L.x[e / B][e % B] = i < n ? A_xin[i * B + e % B] : 0.0;
         }
     } else {  // Ritz vectors X = Q Y out, then the start block [1 / sqrt(n) | X[:, 0..14]]
-        for (int e = t; e < A.nb * BB; e += 256) L.cm[e] = A.Y[e];
+        for (int e = t; e < A_nb * BB; e += 256) L.cm[e] = A_Y[e];
         __syncthreads();
         mul_q(true);
-        store_rows(A.xout);
+        store_rows(A_xout);
         __syncthreads();
         const double c0 = 1.0 / sqrt((double)n);
         for (int r = t; r < RPB; r += 256) {
@@ -1522,35 +1546,35 @@ __global__ __launch_bounds__(256) void k_ortho(OrthoArgs A) {
     if (MODE == kOrthoFull) {
         // pass A: X = W - Qa c1, shifted CholQR3 -> Q1 (factors R0..R2)
         proj_part();
-        reduce_proj(A.c1);
+        reduce_proj(A_c1);
         mul_q(false);
-        scholqr3(A.R, A.fail);
+        scholqr3(A_R, A_fail);
         // pass B: X = Q1 - Qa c2, shifted CholQR3 -> Q_{j+1} (R3..R5)
         proj_part();
-        reduce_proj(A.c2);
+        reduce_proj(A_c2);
         mul_q(false);
-        scholqr3(A.R + 3 * BB, A.fail + 3);
-        store_rows(A.qnext);
+        scholqr3(A_R + 3 * BB, A_fail + 3);
+        store_rows(A_qnext);
     } else if (MODE == kOrthoLast) {
         // CGS2 coefficients of the last product and the Gram of its residual
         proj_part();
-        reduce_proj(A.c1);
+        reduce_proj(A_c1);
         mul_q(false);
         proj_part();
-        reduce_proj(A.c2);
+        reduce_proj(A_c2);
         mul_q(false);
-        gram_part(A.gpart);
+        gram_part(A_gpart);
         gsync();
         if (g == 0) {
-            reduce_gram(A.gpart);
-            A.G[t] = L.gs[t];
+            reduce_gram(A_gpart);
+            A_G[t] = L.gs[t];
         }
     } else {
-        scholqr3(A.R, A.fail);
-        store_rows(A.qnext);
+        scholqr3(A_R, A_fail);
+        store_rows(A_qnext);
     }
     stamp(39);
-    if (A.tstamp && g == 0 && t == 0) A.tstamp[38] = bar;
+    if (A_tstamp && g == 0 && t == 0) A_tstamp[38] = bar;
 }
 
 // ---------------------------------------------- small symmetric eigen (host)
