@@ -416,7 +416,10 @@ int hh_comp_set_cor(hh_comp* c, const double* cor, void* stream);
  * (and the fallback when the basis would not fit, n < 16 (pca_p + 1)): block
  * subspace iteration, max_iters iterations.  *iters = Cor products (Krylov)
  * or iterations (subspace).  Not converging is not an error: query
- * hh_comp_pca_status. */
+ * hh_comp_pca_status.  The Krylov products read only the upper triangle of
+ * Cor (hh_tune "cor_sym", default 1; 0: the full matrix), so a Cor set with
+ * hh_comp_set_cor is taken as symmetric; hh_tune "ortho_tpb" / "ortho_min_tpb"
+ * set the orthogonalisation's rows per block (/ 64). */
 int hh_comp_pca(hh_comp* c, int32_t k, double tol, int32_t max_iters, double* components, double* eigvals,
                 int32_t* iters, void* stream);
 /* Outcome of the last hh_comp_pca: converged (1/0), Cor products, Krylov
