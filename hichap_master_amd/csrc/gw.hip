@@ -128,10 +128,15 @@ constexpr int kGwStatBlocks = 2048;
 // (the host splits it: sum in the high 40 bits, nonzeros in the low 24), and
 // the table's count total in *total so the host can verify that no sum
 // reached 2^40 (else it reruns unpacked).  Needs n_bins < 2^24.
+// "same chromosome (block)" as a range test on the row's bounds [lo, hi):
+// the row's bounds are one broadcast load per wave (rows change rarely along
+// the sorted table) instead of a gather of the column's chromosome id
+__device__ __forceinline__ bool in_block(int2 bd, int32_t y) { return y >= bd.x && y < bd.y; }
+
 template <bool PACK>
 __global__ __launch_bounds__(256) void k_gw_tstats(const int32_t* __restrict__ a, const int32_t* __restrict__ b,
                                                    const uint32_t* __restrict__ v, long long nnz,
-                                                   const int32_t* __restrict__ chrom_of,
+                                                   const int2* __restrict__ cbd,
                                                    unsigned long long* __restrict__ rsum,
                                                    unsigned long long* __restrict__ rnz,
                                                    unsigned long long* __restrict__ rpk,
@@ -149,7 +154,7 @@ __global__ __launch_bounds__(256) void k_gw_tstats(const int32_t* __restrict__ a
             const int32_t y = b[i];
             const uint32_t cc = v[i];
             if (PACK) t += cc;
-            if (cc != 0u && chrom_of[x] == chrom_of[y]) {
+            if (cc != 0u && in_block(cbd[x], y)) {
                 c = cc;
                 one = 1;
                 if (x != y) {
@@ -188,7 +193,7 @@ __global__ __launch_bounds__(256) void k_gw_tstats(const int32_t* __restrict__ a
 constexpr int kTsWin = 8192;
 __global__ __launch_bounds__(256) void k_gw_tstats_win(const int32_t* __restrict__ a, const int32_t* __restrict__ b,
                                                        const uint32_t* __restrict__ v, long long nnz, long long per,
-                                                       long long n, const int32_t* __restrict__ chrom_of,
+                                                       long long n, const int2* __restrict__ cbd,
                                                        unsigned long long* __restrict__ rpk,
                                                        unsigned long long* __restrict__ total) {
     __shared__ unsigned long long win[kTsWin];
@@ -209,7 +214,7 @@ __global__ __launch_bounds__(256) void k_gw_tstats_win(const int32_t* __restrict
             const int32_t y = b[i];
             const uint32_t cc = v[i];
             t += cc;
-            if (cc != 0u && chrom_of[x] == chrom_of[y]) {
+            if (cc != 0u && in_block(cbd[x], y)) {
                 pk = ((unsigned long long)cc << 24) | 1ull;
                 if (x != y) {
                     const long long d = (long long)y - x0;
@@ -238,7 +243,7 @@ __global__ __launch_bounds__(256) void k_gw_tstats_win(const int32_t* __restrict
 // row: segmented), and sum(H)
 __global__ __launch_bounds__(256) void k_gw_hstats(const int32_t* __restrict__ r, const int32_t* __restrict__ c,
                                                    const uint32_t* __restrict__ v, long long nnz,
-                                                   const int32_t* __restrict__ block_of,
+                                                   const int2* __restrict__ bbd,
                                                    unsigned long long* __restrict__ bsum,
                                                    unsigned long long* __restrict__ total) {
     __shared__ unsigned long long wsum[4];
@@ -253,7 +258,7 @@ __global__ __launch_bounds__(256) void k_gw_hstats(const int32_t* __restrict__ r
             row = r[i];
             const uint32_t xx = v[i];
             t += xx;
-            if (xx && block_of[row] == block_of[c[i]]) x = xx;
+            if (xx && in_block(bbd[row], c[i])) x = xx;
         }
         seg_add_u64(row, x, bsum);
     }
@@ -596,13 +601,15 @@ void gw_create(hh_gw& G, const Id* t1, const Id* t2, const Cnt* tv, int64_t t_nn
     G.N2 = 2 * n;
     G.t_nnz = t_nnz;
     G.h_nnz = h_nnz;
-    std::vector<int32_t> chrom_of(n), block_of(2 * n);
+    // per bin: its chromosome's [lo, hi) in T, its same-haplotype block's in H
+    std::vector<int2> chrom_bd(n), block_bd(2 * n);
     for (int c = 0; c < n_chroms; ++c) {
         HH_REQUIRE(chrom_offsets[c] <= chrom_offsets[c + 1], "chrom_offsets not monotone");
+        const int32_t lo = (int32_t)chrom_offsets[c], hi = (int32_t)chrom_offsets[c + 1];
         for (int64_t b = chrom_offsets[c]; b < chrom_offsets[c + 1]; ++b) {
-            chrom_of[b] = c;
-            block_of[b] = c;                 // M copy of chromosome c
-            block_of[n + b] = n_chroms + c;  // P copy
+            chrom_bd[b] = make_int2(lo, hi);
+            block_bd[b] = make_int2(lo, hi);                                    // M copy of chromosome c
+            block_bd[n + b] = make_int2((int32_t)(n + lo), (int32_t)(n + hi));  // P copy
         }
     }
     constexpr bool COPY = !(std::is_same<Id, int32_t>::value && std::is_same<Cnt, int32_t>::value);
@@ -616,7 +623,7 @@ void gw_create(hh_gw& G, const Id* t1, const Id* t2, const Cnt* tv, int64_t t_nn
         G.Rp = reinterpret_cast<const int32_t*>(hr), G.Cp = reinterpret_cast<const int32_t*>(hc);
         G.Vp = reinterpret_cast<const uint32_t*>(hv);
     }
-    DBuf<int32_t> dch = to_device(chrom_of, s), dblk = to_device(block_of, s);
+    DBuf<int2> dch = to_device(chrom_bd, s), dblk = to_device(block_bd, s);
     DBuf<unsigned long long> trs(n), tnz(n), hbs(2 * n), htot(1);
     trs.zero(s);
     tnz.zero(s);
