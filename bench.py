@@ -196,6 +196,7 @@ def tad_scan_bench(m, st, stream, reps=5, res=10000, min_tad=200000, window=6000
 
 
 C5_RES = 25000
+C5_SCHED = os.environ.get("HH_C5_SCHED", "queue")  # "queue" (dynamic, largest first) or "static" (round-robin)
 C5_STREAMS = int(os.environ.get("HH_C5_STREAMS", "12"))  # 12 host threads / streams: 95.8 vs 89.9 chr/s with 8 (profiles/r3b_c5b_s*.log)
 
 
@@ -281,10 +282,24 @@ def run_c5(args, world, rank, local):
             conv[k] = sf.pca_status["converged"]
 
     def step(nstreams=C5_STREAMS):
-        # largest first, dealt round-robin to the stream workers
         order = sorted(mine, key=lambda k: -sizes[k])
-        lanes = [order[i::nstreams] for i in range(nstreams)]
-        futs = [pool.submit(lambda ks, st: [one(k, st) for k in ks], ks, st) for ks, st in zip(lanes, streams)]
+        if C5_SCHED == "static":  # largest first, dealt round-robin to the stream workers
+            lanes = [order[i::nstreams] for i in range(nstreams)]
+            futs = [pool.submit(lambda ks, st: [one(k, st) for k in ks], ks, st) for ks, st in zip(lanes, streams)]
+        else:  # largest first from one queue: a worker takes the next chromosome when its stream is free
+            import queue
+            todo = queue.SimpleQueue()
+            for k in order:
+                todo.put(k)
+
+            def worker(st):
+                while True:
+                    try:
+                        k = todo.get_nowait()
+                    except queue.Empty:
+                        return
+                    one(k, st)
+            futs = [pool.submit(worker, st) for st in streams[:nstreams]]
         for f in futs:
             f.result()
 
