@@ -988,9 +988,61 @@ def run_twostep(args, world, rank, local):
         print(json.dumps(out), flush=True)
 
 
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv):
+    """``bench.py --gpus N`` without a launcher: start N child ranks (one
+    process per GPU, RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in their
+    environment, as torch.distributed.run sets them) and return the exit
+    status.  Runs before anything touches the GPU in this process: counting
+    devices does not initialise HIP on this image, and the children bind their
+    own device.  Rank 0's stdout (the JSON line) passes through; if any rank
+    fails, the others are stopped (by PID) and the status is non-zero.
+    ``HH_DEVICE`` set = a path check with every rank on that one device
+    (``HH_DIST_BACKEND=gloo``), so no device count is required."""
+    import subprocess
+    if "HH_DEVICE" not in os.environ:
+        import torch
+        ndev = torch.cuda.device_count()
+        if ndev < n:
+            print(f"[bench] --gpus {n} needs {n} visible GPUs, this node has {ndev}; refusing to report "
+                  f"n_gpus={n} from fewer devices (set HH_DEVICE=<dev> HH_DIST_BACKEND=gloo for a one-device "
+                  f"path check)", file=sys.stderr, flush=True)
+            return 2
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HH_LAUNCHED="1")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env,
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    status = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            rc = p.poll()
+            if rc is None:
+                continue
+            live.remove(p)
+            if rc != 0 and status == 0:
+                status = rc if rc > 0 else 128 - rc
+                print(f"[bench] rank {procs.index(p)} exited with {rc}; stopping the other ranks",
+                      file=sys.stderr, flush=True)
+                for q in live:
+                    q.terminate()
+        time.sleep(0.05)
+    return status
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (ranks) to run on; without a launcher's WORLD_SIZE, bench.py starts them itself")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c4")
@@ -1006,6 +1058,14 @@ def main():
                     help="use the multi-GPU (all-gather) driver even at N=1 (path check)")
     args = ap.parse_args()
 
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None:
+        if (args.gpus or 1) > 1:  # no launcher: start the ranks ourselves (no GPU call in this process)
+            sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    elif args.gpus is not None and int(env_world) != args.gpus:
+        print(f"[bench] --gpus {args.gpus} but WORLD_SIZE={env_world}: the launcher and the flag disagree",
+              file=sys.stderr, flush=True)
+        sys.exit(2)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

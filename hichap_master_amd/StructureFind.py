@@ -431,9 +431,40 @@ class StructureFind(TADCalling):
                 self.RawPCA[chro] = raw
                 out[NonGap] = self.Select_Allelic_PC(raw, trad[chro[1:]])[NonGap]
             self.Compartment_Dict[chro] = out
-            self.OE_Matrix_Dict.put(chro, lambda M=M, X=OE_M, NG=NonGap: self.Refill_Gap(M, X, NG, "OE"))
-            self.Cor_Martrix_Dict.put(chro, lambda M=M, X=Cor_M, NG=NonGap: self.Refill_Gap(M, X, NG, "Cor"))
+            # thunks over host inputs only (M, decline, NonGap): this
+            # chromosome's device state (matrix, correlation, Krylov
+            # workspace) is freed now, not kept alive by the dicts
+            dec = np.array(distance_bin, dtype=np.float64)
+            for d, kind in ((self.OE_Matrix_Dict, "OE"), (self.Cor_Martrix_Dict, "Cor")):
+                d.put(chro, self._refill_thunk(M, dec, NonGap, SA, kind))
+            del Cor_M, OE_M
+            self._comp = self._comp_src = None
         return self.Compartment_Dict
+
+    def _refill_thunk(self, M, decline, NonGap, SA, kind):
+        """Refill_Gap(M, OE or Cor) made on first access from the host inputs:
+        the correlation (and the Sliding_Approach O/E) recomputed on the GPU
+        in a short-lived hh_comp, the plain O/E on the host."""
+        def make():
+            NG = np.asarray(NonGap, dtype=np.int64)
+            if kind == "OE" and not SA:
+                sub = M[:, NG]
+                d = np.abs(np.arange(M.shape[0])[:, None] - NG[None, :])
+                X = np.zeros_like(sub)
+                nz = sub != 0
+                X[nz] = sub[nz] / decline[d[nz]]
+                return self.Refill_Gap(M, X, NG, "OE")
+            comp = _Comp(M, self.stream)
+            try:
+                if SA:
+                    comp.sliding_oe(decline, 600000 // self.Res // 2)
+                comp.correlation(decline, NG)
+                X = np.asarray(DeviceCorrelation(comp) if kind == "Cor" else DeviceOE(comp))
+            finally:
+                call("hh_comp_free", comp.h)
+                comp.h = None
+            return self.Refill_Gap(M, X, NG, kind)
+        return make
 
     def Refill_Gap(self, M1, M2, NonGap, dtype):
         """Refill_Gap (StructureFind.py:463-488): the n x n correlation or the

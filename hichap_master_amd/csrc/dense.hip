@@ -312,10 +312,11 @@ static std::vector<uint8_t> gap_defined(const std::vector<long long>& zeros, lon
 
 // Dense N x N int64 from cells (row, col, count) with ids shifted by
 // `offset` (pairs.dense_from_pixels / the reference's per-line dense `+=`
-// result, matrixBuilding.py:554, :567-570, :1290-1301): out[r][c] = v, and
-// out[c][r] = v for an upper-triangle (symmetric) table.  Cells are unique
-// (cooler's tables, the binner's run-length output), so no two threads write
-// one element.
+// result, matrixBuilding.py:554, :567-570, :1290-1301): out[r][c] += v, and
+// out[c][r] += v (once on the diagonal) for an upper-triangle (symmetric)
+// table.  Repeated cells add up, as the reference's `Matrix[bin1][bin2] += 1`
+// does: int64 atomics, exact and independent of the order they land in
+// (cooler's tables and the binner's run-length output are unique anyway).
 __global__ void k_dense_scatter(const long long* __restrict__ r, const long long* __restrict__ c,
                                 const long long* __restrict__ v, long long nnz, long long N, long long offset,
                                 int sym, long long* __restrict__ out, unsigned long long* __restrict__ bad) {
@@ -326,8 +327,9 @@ __global__ void k_dense_scatter(const long long* __restrict__ r, const long long
         atomicMin(bad, (unsigned long long)k);
         return;
     }
-    out[a * N + b] = v[k];
-    if (sym) out[b * N + a] = v[k];
+    const unsigned long long x = (unsigned long long)v[k];  // two's complement: the same add for int64
+    atomicAdd((unsigned long long*)&out[a * N + b], x);
+    if (sym && a != b) atomicAdd((unsigned long long*)&out[b * N + a], x);
 }
 
 // Upper-triangle nonzeros of a dense fp64 N x N matrix in row-major (cooler)

@@ -1171,6 +1171,9 @@ constexpr int kUbThreads = 64 * kUbWaves;
 constexpr int kUbGroupRows = kUbRows * kUbWaves;   // rows per workgroup (global alignment)
 constexpr int kUbChunk = 1008;                     // slots per chunk = 63 data lanes x 16
 constexpr int kUbCols = kUbGroupRows + kUbChunk;   // LDS column buffer (doubles)
+// a workgroup's rows are all local or all halo only because shards are cut
+// at whole kR-row blocks: keep the workgroup a divisor of the row block
+static_assert(kR % kUbGroupRows == 0, "upper-band workgroups must not straddle a shard's row-block boundary");
 // a workgroup's tails reach kUbTails workgroups ahead: per chunk the partial
 // arrays R (row parts), H (heads), T1 .. T_kUbTails (tails of the workgroups
 // 1 .. kUbTails behind)
@@ -2161,7 +2164,7 @@ static int band_segs(const hh_matrix* m, BandSegs& segs) {
 
 // The upper-band segments (K1d): uint8 diagonals 0..W8 from slot W8 of each
 // row, nibble diagonals W8+1..W4 from the positive segment.  A chunk covers
-// 1024 slots; row m of a 16-row group reaches back m slots into the previous
+// kUbChunk (1008) slots; row m of a 16-row group reaches back m slots into the previous
 // chunk, so the last chunk must start within 15 slots of the segment end.
 static int ub_segs(const hh_ice* S, UbSegs& u) {
     const hh_matrix* m = S->m;

@@ -104,9 +104,13 @@ def TwoStepCorrection(TM, MM, PM):
     One C-ABI call (``hh_twostep``): each matrix is uploaded once, the gap /
     alpha glue runs in C++ with np.percentile semantics."""
     _lib.require_gpu()
-    if all(hasattr(X, "data_ptr") for X in (TM, MM, PM)):
+    on_dev = [bool(getattr(X, "is_cuda", False)) for X in (TM, MM, PM)]
+    if all(on_dev):
         return _twostep_device(TM, MM, PM)
-    mats = [np.ascontiguousarray(X, dtype=np.int64) for X in (TM, MM, PM)]
+    if any(on_dev):
+        raise ValueError("TM, MM, PM must all be device tensors or all host arrays")
+    # host arrays (NumPy, or CPU torch tensors: np.asarray takes them as is)
+    mats = [np.ascontiguousarray(np.asarray(X), dtype=np.int64) for X in (TM, MM, PM)]
     N = mats[0].shape[0]
     if any(X.ndim != 2 or X.shape != (N, N) for X in mats):
         raise ValueError("TM, MM, PM must be square matrices of the same size")

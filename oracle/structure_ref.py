@@ -110,9 +110,38 @@ def top_components(C, k=3):
     return V
 
 
-def get_pca(decline, M, NG, SA=False, res=None):
+def top_components_eigsh(C, k=3):
+    """The same components as ``top_components`` for large n, without a dense
+    SVD: the top-k eigenvectors of A = Xc^T Xc (Xc = C - 1 mu^T, the matrix
+    sklearn factors) by ARPACK (``scipy.sparse.linalg.eigsh``, tol 0 =
+    machine precision) on matrix-vector products with C only; sklearn>=1.5
+    signs.  Used where the exact SVD of n ~ 1e4 would take minutes (C5 chr1,
+    VERDICT r3 item 4)."""
+    from scipy.sparse.linalg import LinearOperator, eigsh
+    C = np.asarray(C, dtype=np.float64)
+    n = C.shape[1]
+    mu = C.mean(axis=0)
+    CT = C.T
+
+    def mv(v):
+        v = np.ravel(v)
+        w = C @ v - (mu @ v)           # Xc v
+        return CT @ w - mu * w.sum()   # Xc^T w
+
+    A = LinearOperator((n, n), matvec=mv, dtype=np.float64)
+    vals, vecs = eigsh(A, k=k, which="LA", tol=0, v0=np.ones(n) / np.sqrt(n), ncv=min(n, max(2 * k + 1, 24)))
+    order = np.argsort(vals)[::-1]
+    V = vecs[:, order].T.copy()
+    for r in range(V.shape[0]):
+        if V[r, np.argmax(np.abs(V[r]))] < 0:
+            V[r] = -V[r]
+    return V, vals[order]
+
+
+def get_pca(decline, M, NG, SA=False, res=None, solver="svd"):
     """Get_PCA (StructureFind.py:302-342). Returns (pcs, Cor, OE[:, NG]);
-    SA=True: Sliding_Approach with window 600 kb at resolution ``res``."""
+    SA=True: Sliding_Approach with window 600 kb at resolution ``res``;
+    ``solver="eigsh"``: components by top_components_eigsh (large n)."""
     if SA:
         dec = np.array(decline, dtype=np.float64)
         dec[dec == 0] = dec[np.nonzero(dec)].min()
@@ -120,7 +149,8 @@ def get_pca(decline, M, NG, SA=False, res=None):
     else:
         OE = oe_matrix(M, decline)[:, NG]
     C = pearson_columns(OE)
-    return top_components(C, 3), C, OE
+    pcs = top_components(C, 3) if solver == "svd" else top_components_eigsh(C, 3)[0]
+    return pcs, C, OE
 
 
 def means_minus(C, pc, eps=1e-5):
@@ -169,11 +199,11 @@ def select_allelic_pc(pcs_full, trad_pc):
     return pcs_full[int(np.argmax(pcc))], int(np.argmax(pcc))
 
 
-def compartment(M):
+def compartment(M, solver="svd"):
     """Traditional compartment call for one chromosome (Compartment :509-527).
     Returns (pc_full[N], selected_index, pcs, Cor)."""
     dec, G, NG = distance_decay(M)
-    pcs, C, OE = get_pca(dec, M, NG)
+    pcs, C, OE = get_pca(dec, M, NG, solver=solver)
     pc, k = select_pc(C, OE[NG], pcs)
     out = np.zeros(M.shape[0])
     out[NG] = pc

@@ -44,3 +44,31 @@ def test_bench_two_ranks_sharded_path():
     assert d["n_gpus"] == 2 and d["value"] > 0
     assert "sharded x2" in d["config"]["parallelism"]
     assert 0 < d["roofline"]["shard_nnz_upper"] < d["config"]["nnz_upper"]
+
+
+def test_bench_gpus_flag_launches_ranks_itself():
+    """``bench.py --gpus 2`` with no launcher starts its
+    own two ranks (here both on cuda:0 with the gloo exchange, HH_DEVICE) and
+    reports n_gpus 2 from the sharded path."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(HH_DEVICE="0", HH_DIST_BACKEND="gloo")
+    cmd = [sys.executable, "bench.py", "--gpus", "2", "--nnz", "2e8", "--steps", "3", "--warmup", "1"]
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=400)
+    assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-3000:])
+    d = _json_line(p.stdout)
+    assert KEYS <= set(d)
+    assert d["n_gpus"] == 2 and d["value"] > 0
+    assert "sharded x2" in d["config"]["parallelism"]
+
+
+def test_bench_gpus_flag_refuses_missing_devices():
+    """More GPUs asked than the box has: non-zero exit and no JSON line, not a
+    one-GPU number labelled n_gpus N."""
+    import torch
+    n = torch.cuda.device_count() + 1
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "HH_DEVICE")}
+    p = subprocess.run([sys.executable, "bench.py", "--gpus", str(n), "--config", "c1", "--steps", "2"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=120)
+    assert p.returncode != 0
+    assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert "visible GPUs" in p.stderr

@@ -276,3 +276,34 @@ def test_pca_upper_triangle_product_matches_full(chrom):
         np.testing.assert_allclose(_match_sign(p1[q], p0[q]), p0[q], atol=1e-11)
     np.testing.assert_allclose(s1["eigvals"], s0["eigvals"], rtol=1e-12)
     np.testing.assert_array_equal(p1, p2)
+
+
+@pytest.mark.parametrize("chrom", list(range(1, 23)))
+def test_c5_selected_pc_vs_oracle(chrom):
+    """every C5 autosome (chr1 at N = 9 971 included)
+    through the whole compartment call -- Distance_Decay, Get_PCA,
+    Select_PC_new -- against the oracle's (np.corrcoef Cor, top-3 by ARPACK
+    on the centred matrix, Select_PC_new restated): PC1 to 1e-10 after sign
+    alignment, the same selected PC index, and the A/B sign of every bin with
+    |PC| > 1e-8 equal (StructureFind.py:302-342, :374-423)."""
+    import sys
+    from hichap_master_amd.StructureFind import StructureFind
+    dM = _c5_matrix(chrom - 1)
+    sf = StructureFind(Res=C5_RES)
+    dec, G, NG = sf.Distance_Decay(M=dM, G_array=None)
+    pcs, Cor, OE = sf.Get_PCA(distance_bin=dec.copy(), M=dM, NG_array=NG)
+    assert sf.pca_status["converged"]
+    pc = sf.Select_PC_new(Cor, OE[NG], pcs)
+    k_gpu = int(np.argmax([abs(np.dot(pc, p)) for p in pcs]))
+    full = np.zeros(dM.shape[0])
+    full[NG] = pc
+    del Cor, OE, sf
+    M = dM.cpu().numpy()
+    del dM
+    ref_full, k_ref, p_ref, _ = structure_ref.compartment(M, solver="eigsh")
+    print(f"chr{chrom}: N={M.shape[0]} selected PC{k_ref + 1}", file=sys.stderr, flush=True)
+    np.testing.assert_allclose(_match_sign(pcs[0], p_ref[0]), p_ref[0], atol=1e-10)
+    assert k_gpu == k_ref
+    big = np.abs(ref_full) > 1e-8
+    np.testing.assert_array_equal(np.sign(full[big]), np.sign(ref_full[big]))
+    np.testing.assert_allclose(full, ref_full, atol=1e-9)

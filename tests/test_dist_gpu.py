@@ -26,7 +26,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, case, cis_only, outdir, impl="python"):
+def _worker(rank, world, port, case, cis_only, outdir, impl="python", rr_force=None):
     import torch
     import torch.distributed as tdist
     from hichap_master_amd import _lib, dist, ice
@@ -41,6 +41,8 @@ def _worker(rank, world, port, case, cis_only, outdir, impl="python"):
         b1, b2, c, off = case
         n = int(off[-1])
         rr = dist.partition_rows(np.bincount(b1, minlength=n) + np.bincount(b2, minlength=n), world)
+        if rr_force is not None:
+            rr = np.asarray(rr_force, dtype=np.int64)
         opts = ice.IceOptions(max_iters=400, cis_only=cis_only)
         if impl != "cis":
             m = ice.ContactMatrix.from_pixels(b1, b2, c, n, off, cis_only=cis_only,
@@ -178,7 +180,7 @@ def test_library_rccl_communicator_world1():
     assert s1["iters"] == s2["iters"]
 
 
-def _rccl_worker(rank, world, port, case, outdir):
+def _rccl_worker(rank, world, port, case, case1, outdir):
     """One rank per GPU over the library's own RCCL communicator (xGMI):
     genome-wide row shards (hh_ice_balance_sharded, one ncclAllGather of the
     marginals per iteration) and --cis-only by chromosome
@@ -201,8 +203,25 @@ def _rccl_worker(rank, world, port, case, outdir):
         m.close()
         wc, sc = dist.balance_cis_sharded(b1, b2, c, n, off, rank, world,
                                           ice.IceOptions(max_iters=400, cis_only=True), cx)
-        torch.cuda.synchronize()
         cx.close()
+        # the empty-rank cases an 8-GPU node meets on small matrices: one
+        # genome-wide shard without rows (world - 1 real shards, an empty one
+        # in the middle), and --cis-only with one chromosome (world - 1
+        # chromosome-less ranks)
+        w1 = dist.partition_rows(np.bincount(b1, minlength=n) + np.bincount(b2, minlength=n), world - 1)
+        rre = np.insert(w1, world // 2, w1[world // 2])
+        cxe = dist.CapiExchange(rre, world, rank, backend="nccl")
+        me = ice.ContactMatrix.from_pixels(b1, b2, c, n, off, row_range=(rre[rank], rre[rank + 1]))
+        we, se = dist.balance_capi(me, ice.IceOptions(max_iters=400), cxe, torch.cuda.current_stream().cuda_stream)
+        me.close()
+        e1, e2, ec, eoff = case1
+        w1c, s1c = dist.balance_cis_sharded(e1, e2, ec, int(eoff[-1]), eoff, rank, world,
+                                            ice.IceOptions(max_iters=400, cis_only=True), cxe)
+        torch.cuda.synchronize()
+        cxe.close()
+        np.save(os.path.join(outdir, f"we{rank}.npy"), we)
+        np.save(os.path.join(outdir, f"w1c{rank}.npy"), w1c)
+        np.save(os.path.join(outdir, f"ite{rank}.npy"), np.array([se["iters"]]))
         np.save(os.path.join(outdir, f"w{rank}.npy"), w)
         np.save(os.path.join(outdir, f"wc{rank}.npy"), wc)
         np.save(os.path.join(outdir, f"it{rank}.npy"), np.array([s_["iters"]]))
@@ -230,8 +249,11 @@ def test_rccl_every_gpu():
     n = int(off[-1])
     w_full, st_full = ice.balance(b1, b2, c, n, off, max_iters=400)
     wc_full, stc_full = ice.balance(b1, b2, c, n, off, cis_only=True, max_iters=400)
+    case1 = synth.coo_genome([1500], rng, A=25.0)
+    w1_full, _ = ice.balance(*case1[:3], int(case1[3][-1]), case1[3], cis_only=True, max_iters=400)
     with tempfile.TemporaryDirectory() as d:
-        mp.start_processes(_rccl_worker, args=(world, _free_port(), case, d), nprocs=world, start_method="spawn")
+        mp.start_processes(_rccl_worker, args=(world, _free_port(), case, case1, d), nprocs=world,
+                           start_method="spawn")
         for r in range(world):
             np.testing.assert_array_equal(np.load(os.path.join(d, f"w{r}.npy")), w_full)
             assert int(np.load(os.path.join(d, f"it{r}.npy"))[0]) == st_full["iters"]
@@ -239,3 +261,51 @@ def test_rccl_every_gpu():
             np.testing.assert_array_equal(np.isnan(wc), np.isnan(wc_full))
             np.testing.assert_allclose(wc, wc_full, rtol=1e-12, equal_nan=True)
             np.testing.assert_array_equal(np.load(os.path.join(d, f"itc{r}.npy")), stc_full["iters"])
+            np.testing.assert_array_equal(np.load(os.path.join(d, f"we{r}.npy")), w_full)
+            assert int(np.load(os.path.join(d, f"ite{r}.npy"))[0]) == st_full["iters"]
+            np.testing.assert_allclose(np.load(os.path.join(d, f"w1c{r}.npy")), w1_full, rtol=1e-12, equal_nan=True)
+
+
+@pytest.mark.parametrize("impl", ["capi", "python"])
+def test_empty_genomewide_shard_world3(impl):
+    """World 3 on a 2-row-block matrix: one rank holds no rows (what
+    partition_rows gives whenever ranks outnumber row blocks, e.g. the RCCL
+    test's 3 500 bins at world 8).  The empty rank still joins every
+    all-gather; every rank's weights equal the one-process run bitwise."""
+    import torch.multiprocessing as mp
+    from hichap_master_amd import _lib, ice
+    _lib.require_gpu()
+    rng = np.random.default_rng(44)
+    case = synth.coo_genome([600, 400], rng, A=25.0, trans_density=0.01)
+    b1, b2, c, off = case
+    n = int(off[-1])
+    w_full, st_full = ice.balance(b1, b2, c, n, off, max_iters=400)
+    for rr in ([0, 512, 512, n], [0, 0, 512, n], [0, 512, n, n]):
+        with tempfile.TemporaryDirectory() as d:
+            mp.start_processes(_worker, args=(3, _free_port(), case, False, d, impl, rr), nprocs=3,
+                               start_method="spawn")
+            for r in range(3):
+                np.testing.assert_array_equal(np.load(os.path.join(d, f"w{r}.npy")), w_full)
+                assert int(np.load(os.path.join(d, f"it{r}.npy"))[0]) == st_full["iters"]
+
+
+def test_chromosomeless_cis_ranks_world4():
+    """--cis-only over 4 ranks with 2 chromosomes: ranks 2 and 3 get no
+    chromosome and only join the MAD exchange and the final gather; every
+    rank's weights equal the one-process --cis-only run to 1e-12 with the
+    same per-chromosome iterations."""
+    import torch.multiprocessing as mp
+    from hichap_master_amd import _lib, ice
+    _lib.require_gpu()
+    rng = np.random.default_rng(45)
+    case = synth.coo_genome([900, 700], rng, A=25.0, trans_density=0.01)
+    b1, b2, c, off = case
+    n = int(off[-1])
+    w_full, st_full = ice.balance(b1, b2, c, n, off, cis_only=True, max_iters=400)
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_worker, args=(4, _free_port(), case, True, d, "cis"), nprocs=4, start_method="spawn")
+        for r in range(4):
+            w = np.load(os.path.join(d, f"w{r}.npy"))
+            np.testing.assert_array_equal(np.isnan(w), np.isnan(w_full))
+            np.testing.assert_allclose(w, w_full, rtol=1e-12, equal_nan=True)
+            np.testing.assert_array_equal(np.load(os.path.join(d, f"it{r}.npy")), st_full["iters"])

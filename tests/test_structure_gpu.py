@@ -227,3 +227,21 @@ def test_compartment_keeps_refilled_cor_and_oe(SF, golden):
     np.testing.assert_allclose(sf.OE_Matrix_Dict["chr1"], structure_ref.refill_gap(M, g["OE"], NG, "OE"),
                                rtol=1e-12, atol=0)
     assert list(sf.Cor_Martrix_Dict) == ["chr1"] and "chr1" in sf.OE_Matrix_Dict
+
+
+def test_compartment_frees_device_state_and_sa_thunks(SF, golden):
+    """Compartment() keeps no chromosome's hh_comp alive (the
+    refilled-matrix thunks are built from host inputs), and with SA=True the
+    refilled O/E and Cor equal Refill_Gap of Get_PCA's own SA outputs."""
+    g = golden("compartment_sa_n150")
+    M = g["M"]
+    res = int(g["res"]) if "res" in g else 20000
+    sf = SF(Res=res)
+    sf.Compartment(SA=True, Matrix_Dict={"chrA": M, "chrB": M[:120, :120].copy()})
+    assert sf._comp is None
+    for name, X in (("chrA", M), ("chrB", M[:120, :120])):
+        ref = SF(Res=res)
+        dec, G, NG = ref.Distance_Decay(M=X, G_array=None)
+        pcs, Cor, OE = ref.Get_PCA(distance_bin=dec, M=X, NG_array=NG, SA=True)
+        np.testing.assert_array_equal(sf.Cor_Martrix_Dict[name], ref.Refill_Gap(X, np.asarray(Cor), NG, "Cor"))
+        np.testing.assert_array_equal(sf.OE_Matrix_Dict[name], ref.Refill_Gap(X, np.asarray(OE), NG, "OE"))

@@ -125,3 +125,41 @@ def test_twostep_from_cells_and_device(mb):
     from hichap_master_amd._lib import HipLibraryError
     with pytest.raises(HipLibraryError, match="outside"):
         mb.dense_from_cells_device((np.array([off + N]), np.array([off]), np.array([1])), N, off)
+
+
+def test_dense_from_cells_repeated_cells_add_up(mb):
+    """Repeated (row, col) cells add up, as the reference's per-line
+    `Matrix[bin1][bin2] += 1` does (matrixBuilding.py:1291-1301): ordered and
+    symmetric tables, diagonal cells counted once, run-to-run identical."""
+    rng = np.random.default_rng(91)
+    N, off = 300, 50
+    r = rng.integers(0, N, 20000)
+    c = rng.integers(0, N, 20000)
+    v = rng.integers(1, 5, 20000)
+    want = np.zeros((N, N), np.int64)
+    np.add.at(want, (r, c), v)
+    D = mb.dense_from_cells_device((r + off, c + off, v), N, off)
+    np.testing.assert_array_equal(D.cpu().numpy(), want)
+    a, b = np.minimum(r, c), np.maximum(r, c)
+    ws = np.zeros((N, N), np.int64)
+    np.add.at(ws, (a, b), v)
+    ws = ws + np.triu(ws, 1).T
+    for _ in range(2):
+        D = mb.dense_from_cells_device((a + off, b + off, v), N, off, symmetric=True)
+        np.testing.assert_array_equal(D.cpu().numpy(), ws)
+
+
+def test_twostep_cpu_torch_tensors_take_the_host_path(mb):
+    """CPU torch tensors have data_ptr too: they go the host-array way
+    (ADVICE r3), not to the device-tensor form."""
+    import torch
+    N = 200
+    rng = np.random.default_rng(92)
+    TM = synth.dense_chrom(N, rng, A=60.0)
+    MM, PM = synth.haplotype_pair(TM, rng, drop_rows=5)
+    want = mb.TwoStepCorrection(TM, MM, PM)
+    got = mb.TwoStepCorrection(*(torch.from_numpy(X) for X in (TM, MM, PM)))
+    for a, b in zip(got, want):
+        np.testing.assert_array_equal(a, b)
+    with pytest.raises(ValueError):
+        mb.TwoStepCorrection(torch.from_numpy(TM).cuda(), MM, PM)
