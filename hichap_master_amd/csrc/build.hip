@@ -367,7 +367,7 @@ void build_from_device_pixels(const Id* b1, const Id* b2, const Cnt* cnt, int64_
     HH_REQUIRE(nnz == 0 || (b1 && b2 && cnt), "null pixel arrays");
     HH_REQUIRE(n_bins < kMaxBins, "n_bins must be < 2^30");
     HH_REQUIRE(0 <= row_lo && row_lo <= row_hi && row_hi <= n_bins, "bad row range");
-    HH_REQUIRE(row_lo % kR == 0 && (row_hi % kR == 0 || row_hi == n_bins), "shard rows must be aligned to 512-row blocks");
+    HH_REQUIRE((row_lo % kR == 0 || row_lo == n_bins) && (row_hi % kR == 0 || row_hi == n_bins), "shard rows must be aligned to 512-row blocks");
     HH_REQUIRE(chrom_offsets[0] == 0 && chrom_offsets[n_chroms] == n_bins, "chrom_offsets must span [0, n_bins]");
     HH_REQUIRE(n_chroms < 65535, "too many chromosomes");
     HH_REQUIRE(ignore_diags >= 0, "ignore_diags must be >= 0");

@@ -2638,7 +2638,7 @@ int hh_ice_create(hh_matrix* m, const hh_ice_opts* o, hh_ice** out) {
             S->ub_ghi = (m->row_hi + kUbGroupRows - 1) / kUbGroupRows;
             S->halo_lo = std::min<long long>(m->row_lo, S->ub_glo * kUbGroupRows);
             const long long nh = m->row_lo - S->halo_lo;
-            if (nh > 0) {
+            if (nh > 0 && S->nloc > 0) {  // (an empty shard sweeps nothing: no halo)
                 const long long W8 = m->band_w, W4 = m->band_w4;
                 const long long per = W8 + (W4 > W8 ? band4_seg(W8, W4) : 0);
                 if (W8 > 0) {

@@ -411,7 +411,7 @@ int hh_synth_build(const hh_synth_params* p, int64_t row_lo, int64_t row_hi, voi
         synth_setup(p, h, s);
         const int64_t n = h.dev.n;
         HH_REQUIRE(0 <= row_lo && row_lo <= row_hi && row_hi <= n, "bad row range");
-        HH_REQUIRE(row_lo % kR == 0 && (row_hi % kR == 0 || row_hi == n), "shard rows must be aligned to 512-row blocks");
+        HH_REQUIRE((row_lo % kR == 0 || row_lo == n) && (row_hi % kR == 0 || row_hi == n), "shard rows must be aligned to 512-row blocks");
         const int64_t nloc = row_hi - row_lo;
         const int nJ = h.dev.nJ;
         auto m = std::make_unique<hh_matrix>();
