@@ -129,7 +129,10 @@ class _Comp:
         conv, prods, cyc, meth = (C.c_int32(0) for _ in range(4))
         call("hh_comp_pca_status", self.h, C.byref(conv), C.byref(prods), C.byref(cyc), C.byref(meth))
         self.pca_status = {"converged": bool(conv.value), "products": prods.value, "cycles": cyc.value,
-                           "method": "krylov" if meth.value == 1 else "subspace", "eigvals": ev.copy()}
+                           "method": "krylov" if meth.value in (1, 2) else "subspace", "eigvals": ev.copy(),
+                           # the one-launch orthogonalisation's grid could not become co-resident and the
+                           # solve was redone on the multi-launch path (hh_comp_pca)
+                           "ortho_fallback": meth.value == 2}
         if not conv.value:
             warnings.warn(f"compartment PCA did not converge to {PCA_TOL:g} within its budget "
                           f"({prods.value} correlation products, {self.pca_status['method']}); "

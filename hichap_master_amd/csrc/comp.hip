@@ -764,7 +764,10 @@ struct hh_comp {
     DBuf<double> sa;             // N x N Sliding_Approach O/E (hh_comp_sliding_oe), used when sa_on
     int sa_on = 0;
     // last hh_comp_pca: converged flag, Cor products, Krylov cycles, method
+    // (0 subspace, 1 Krylov, 2 Krylov redone on the multi-launch path after a
+    // k_ortho barrier timeout)
     int pca_converged = 0, pca_products = 0, pca_cycles = 0, pca_method = 0;
+    int ortho_fallbacks = 0;
 };
 
 namespace hh {
@@ -1165,7 +1168,11 @@ __global__ void k_start_block(const double* __restrict__ X, long long n, double*
 constexpr int kOrthoMaxBlocks = 64;
 constexpr int kOrthoMaxE = 8 * kSB * kSB;  // nb <= P <= 8 coefficient blocks
 constexpr double kOrthoFastRatio = 1e3;    // scholqr3's two-pass branch (see there)
-enum { kOrthoFull = 0, kOrthoLast = 1, kOrthoStart = 2, kOrthoRitz = 3 };
+// a low-synch pass's Pythagorean Gram G_W - c^T c is used only when its
+// smallest pivot^2 is above this fraction of W's largest squared column norm
+// (its rounding, ~eps |W|^2, then perturbs the factor by < ~1e-6)
+constexpr double kOrthoPythFloor = 1e-10;
+enum { kOrthoFull = 0, kOrthoLast = 1, kOrthoStart = 2, kOrthoRitz = 3, kOrthoFullLS = 4 };
 
 struct OrthoArgs {
     const double* xin = nullptr;  // Full / Last: W = Cor Q_j; Start: the start block's rows
@@ -1385,9 +1392,9 @@ __global__ __launch_bounds__(256) void k_ortho(OrthoArgs Ain) {
     };
     // nb x 256 projection sums: barrier, reduce-scatter over the blocks,
     // barrier, every block reads all of them into L.cm (block 0 also to `out`)
-    auto reduce_proj = [&](double* out) __attribute__((always_inline)) {
+    auto reduce_proj = [&](double* out, int extra = 0) __attribute__((always_inline)) {
         gsync();  // every block's partials are in
-        const int E = A_nb * BB, chunk = (E + nblk - 1) / nblk;
+        const int E = (A_nb + extra) * BB, chunk = (E + nblk - 1) / nblk;
         const int e1 = min(E, (g + 1) * chunk);
         for (int e = g * chunk + t; e < e1; e += 256) {
             double v[kOrthoMaxBlocks];
@@ -1403,8 +1410,39 @@ __global__ __launch_bounds__(256) void k_ortho(OrthoArgs Ain) {
         for (int e = t; e < E; e += 256) {
             const double v = ld_agent(A_rout + e);
             L.cm[e] = v;
-            if (g == 0) out[e] = v;
+            if (g == 0 && e < A_nb * BB) out[e] = v;
         }
+        __syncthreads();
+    };
+    // low-synch passes (one reduction per pass): the block's Gram X^T X as
+    // coefficient block nb of its projection partials, reduced in the same
+    // reduce-scatter; then the Gram of X - Qa c by Pythagoras,
+    // G - c^T c (Qa orthonormal), into L.gs
+    auto gram_into_proj = [&]() __attribute__((always_inline)) {
+        d4 acc = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int m = 0; m < TPB; ++m)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const double v = L.x[(w + 4 * m) * 16 + 4 * c + lr][lc];
+                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(v, v, acc, 0, 0, 0);
+            }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) L.ws[w][(lr + 4 * r) * B + lc] = acc[r];
+        __syncthreads();
+        A_rpart[(size_t)g * kOrthoMaxE + (size_t)A_nb * BB + t] =
+            ((L.ws[0][t] + L.ws[1][t]) + L.ws[2][t]) + L.ws[3][t];
+        __syncthreads();
+    };
+    auto pythagoras = [&]() __attribute__((always_inline)) {
+        const int i = t / B, j = t % B;
+        double acc = 0.0;
+        for (int k = 0; k < A_nb; ++k) {
+            const double* ck = L.cm + k * BB;
+#pragma unroll
+            for (int m = 0; m < B; ++m) acc = fma(ck[m * B + i], ck[m * B + j], acc);
+        }
+        L.gs[t] = L.cm[A_nb * BB + t] - acc;
         __syncthreads();
     };
     // R = chol(L.gs + shift) in every wave (registers + shuffles), wave 0
@@ -1517,6 +1555,9 @@ __global__ __launch_bounds__(256) void k_ortho(OrthoArgs Ain) {
             cholqr(false, R3 + 2 * BB, fl + 2);
         }
     };
+    // (scholqr3 always computes the Gram of the rows in LDS: the robust
+    // fallback of a low-synch pass is the round-3 chain on X - Qa c)
+    auto scholqr3_direct = [&](double* R3, int* fl) __attribute__((always_inline)) { scholqr3(R3, fl); };
     auto store_rows = [&](double* dst) __attribute__((always_inline)) {
         for (int e = t; e < RPB * B; e += 256) {
             const long long i = r0 + e / B;
@@ -1543,7 +1584,49 @@ __global__ __launch_bounds__(256) void k_ortho(OrthoArgs Ain) {
         }
     }
     __syncthreads();
-    if (MODE == kOrthoFull) {
+    if (MODE == kOrthoFullLS) {
+        // Low-synch CGS2 (two reductions per product instead of ~8): each pass
+        // reduces the projections Qa^T X and the Gram X^T X together, forms
+        // the Gram of X - Qa c by Pythagoras and factors it.  Pass A's Gram
+        // loses digits when W lies nearly in span(Qa), so its (shifted)
+        // factor is taken only when well conditioned and not cancelled
+        // (every block decides from the same reduced numbers); else the
+        // residual's Gram is computed directly and shifted CholeskyQR3 runs,
+        // as in the round-3 path.  Pass B's Gram (Q1 against Qa) has no
+        // cancellation: Q1 is orthonormal to the working accuracy of pass A.
+        auto lowsync_pass = [&](double* cout, double* R3, int* fl, bool shifted) -> bool {
+            proj_part();
+            gram_into_proj();
+            reduce_proj(cout, 1);
+            double gwmax = 0.0;
+#pragma unroll
+            for (int i = 0; i < B; ++i) gwmax = fmax(gwmax, L.cm[A_nb * BB + i * B + i]);
+            pythagoras();
+            mul_q(false);
+            chol(shifted, R3, fl);
+            double mx = 0.0, mn = 1e300;
+#pragma unroll
+            for (int i = 0; i < B; ++i) {
+                const double v = fabs(L.ri[i * B + i]);
+                mx = fmax(mx, v);
+                mn = fmin(mn, v);
+            }
+            if (!(L.ok && mn > 0.0 && mx < kOrthoFastRatio * mn && mn * mn > kOrthoPythFloor * gwmax)) {
+                if (g == 0 && t == 0) *fl = 0;  // the robust path below sets the flags
+                return false;
+            }
+            apply_rinv();
+            if (g == 0) {
+                R3[BB + t] = (t / B == t % B) ? 1.0 : 0.0;
+                R3[2 * BB + t] = (t / B == t % B) ? 1.0 : 0.0;
+                if (t < 2) fl[1 + t] = 0;
+            }
+            return true;
+        };
+        if (!lowsync_pass(A_c1, A_R, A_fail, true)) scholqr3_direct(A_R, A_fail);
+        if (!lowsync_pass(A_c2, A_R + 3 * BB, A_fail + 3, false)) scholqr3_direct(A_R + 3 * BB, A_fail + 3);
+        store_rows(A_qnext);
+    } else if (MODE == kOrthoFull) {
         // pass A: X = W - Qa c1, shifted CholQR3 -> Q1 (factors R0..R2)
         proj_part();
         reduce_proj(A_c1);
@@ -1829,11 +1912,45 @@ struct PcaStatus {
     double bound = 0.0;                              // max_q ||r_q|| / gap_q (angle bound)
 };
 
+// k_ortho's grid barriers need every block of the grid resident at once.  A
+// k_ortho block takes a CU's LDS (one block per CU), and up to
+// GPU_MAX_HW_QUEUES kernels dispatch at the same time (one per hardware
+// queue; the C5 line runs 12 streams): the grid is capped at
+// CUs x blocks-per-CU / hardware queues, so every k_ortho grid that can be
+// dispatching at once fits the chip together (other kernels' blocks finish
+// and free their CUs; k_ortho grids never wait on each other).
+struct OrthoAbort : Error {
+    OrthoAbort() : Error(HH_ERR_HIP, "k_ortho: grid barrier timed out (blocks not co-resident)") {}
+};
+static int ortho_grid_cap(int tpb) {
+    static std::mutex mu;
+    static std::map<std::pair<int, int>, int> cache;  // (device, tpb) -> blocks
+    int dev = 0;
+    HIP_CHECK(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> lk(mu);
+    auto knob = [](int c) { return g_ortho_grid_cap > 0 ? std::max(1, std::min(c, g_ortho_grid_cap)) : c; };
+    auto it = cache.find({dev, tpb});
+    if (it != cache.end()) return knob(it->second);
+    int cus = 0, occ = 0;
+    HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    const void* fn = tpb == 1   ? (const void*)k_ortho<kOrthoFull, 1>
+                     : tpb == 2 ? (const void*)k_ortho<kOrthoFull, 2>
+                     : tpb == 4 ? (const void*)k_ortho<kOrthoFull, 4>
+                                : (const void*)k_ortho<kOrthoFull, 8>;
+    HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, 256, 0));
+    int hwq = 4;  // HIP's default number of hardware queues per process
+    if (const char* e = std::getenv("GPU_MAX_HW_QUEUES"))
+        if (std::atoi(e) > 0) hwq = std::atoi(e);
+    const int cap = std::max(1, std::min(std::max(1, occ) * std::max(1, cus) / hwq, kOrthoMaxBlocks));
+    cache[{dev, tpb}] = cap;
+    return knob(cap);
+}
+
 // Block Krylov PCA (see the K8 comment above).  Returns false when the
 // method cannot run (basis larger than the matrix, start block rank
 // deficient); the caller then falls back to subspace iteration.
 static bool pca_krylov(PcaWork& wk, const double* cor, long long n, int k, double tol, int max_products, int P,
-                       double* components, double* eigvals, PcaStatus& st, hipStream_t s) {
+                       double* components, double* eigvals, PcaStatus& st, hipStream_t s, bool allow_coop = true) {
     constexpr int B = kSB, BB = kSB * kSB;
     if (P < 2 || (long long)(P + 1) * B > n) return false;
     const int nblk = (int)((n + kGramRows - 1) / kGramRows);
@@ -1905,12 +2022,12 @@ static bool pca_krylov(PcaWork& wk, const double* cor, long long n, int k, doubl
     // (the fewest rows per block that fit the grid: more CUs pull the basis
     // rows; 128 instead of 256 rows took the serial k_ortho 163 -> 144 ms)
     int tpb = 8;
-    if (g_ortho_tpb > 0 && nap <= g_ortho_tpb * kOrthoMaxBlocks) tpb = g_ortho_tpb;
+    if (g_ortho_tpb > 0 && nap <= g_ortho_tpb * ortho_grid_cap(g_ortho_tpb)) tpb = g_ortho_tpb;
     else
         for (int t : {g_ortho_min_tpb, 2, 4})
-            if (t >= g_ortho_min_tpb && nap <= t * kOrthoMaxBlocks) { tpb = t; break; }
+            if (t >= g_ortho_min_tpb && nap <= t * ortho_grid_cap(t)) { tpb = t; break; }
     const int oblk = (nap + tpb - 1) / tpb;
-    const bool coop = g_pca_coop && oblk <= kOrthoMaxBlocks;
+    const bool coop = allow_coop && g_pca_coop && oblk <= ortho_grid_cap(tpb);
     DBuf<double> orp(coop ? (size_t)oblk * kOrthoMaxE : 1), oro(kOrthoMaxE), ogp(coop ? (size_t)2 * oblk * BB : 1);
     DBuf<unsigned long long> octr(2);
     octr.zero(s);
@@ -1940,7 +2057,11 @@ static bool pca_krylov(PcaWork& wk, const double* cor, long long n, int k, doubl
         else hipLaunchKernelGGL((k_ortho<M, 8>), grid, blk, 0, s, a);          \
     } while (0)
         switch (mode) {
-            case kOrthoFull: HH_ORTHO(kOrthoFull); break;
+            case kOrthoFull:
+                // low-synch CGS2 (two reductions per product; hh_tune "ortho_lowsync" 0: round 3's ~8)
+                if (g_ortho_lowsync) HH_ORTHO(kOrthoFullLS);
+                else HH_ORTHO(kOrthoFull);
+                break;
             case kOrthoLast: HH_ORTHO(kOrthoLast); break;
             case kOrthoStart: HH_ORTHO(kOrthoStart); break;
             default: HH_ORTHO(kOrthoRitz); break;
@@ -1962,9 +2083,8 @@ static bool pca_krylov(PcaWork& wk, const double* cor, long long n, int k, doubl
         }
     };
     auto check_abort = [&](const std::vector<int>& flags) {
-        if (coop && flags[P * 8 + 7])
-            throw Error(HH_ERR_HIP, "k_ortho: grid barrier timed out (blocks not co-resident); rerun with "
-                                    "hh_tune(\"pca_coop\", 0)");
+        // the caller redoes the whole solve on the multi-launch path
+        if (coop && (flags[P * 8 + 7] || g_ortho_abort_test)) throw OrthoAbort();
     };
     HIP_CHECK(hipMemsetAsync(fail.p, 0, sizeof(int) * nfl, s));
     // start block: [1 / sqrt(n) | deterministic pseudo-random columns]; the
@@ -2453,12 +2573,24 @@ int hh_comp_pca(hh_comp* c, int32_t k, double tol, int32_t max_iters, double* co
         PcaWork wk(n, c->ld);
         if (g_pca_method == 1) {
             PcaStatus st;
-            if (pca_krylov(wk, c->cor.p, n, k, tol, 2 * max_iters, g_pca_p, components, eigvals, st, s)) {
+            bool ok = false, fell_back = false;
+            try {
+                ok = pca_krylov(wk, c->cor.p, n, k, tol, 2 * max_iters, g_pca_p, components, eigvals, st, s);
+            } catch (const OrthoAbort&) {
+                // k_ortho's grid could not become co-resident (its bounded
+                // barrier wait gave up): the same solve on the multi-launch
+                // orthogonalisation, no grid barriers
+                c->ortho_fallbacks += 1;
+                fell_back = true;
+                st = PcaStatus{};
+                ok = pca_krylov(wk, c->cor.p, n, k, tol, 2 * max_iters, g_pca_p, components, eigvals, st, s, false);
+            }
+            if (ok) {
                 c->iters = st.products;
                 c->pca_converged = st.converged;
                 c->pca_products = st.products;
                 c->pca_cycles = st.cycles;
-                c->pca_method = 1;
+                c->pca_method = fell_back ? 2 : 1;
                 if (iters_out) *iters_out = st.products;
                 return;
             }

@@ -113,6 +113,9 @@ inline int g_pca_p = 8;
 inline int g_cor_sym = 1;  // hh_tune "cor_sym": Krylov Cor products read the upper triangle only (k_cor_sym)
 inline int g_ortho_tpb = 0;  // hh_tune "ortho_tpb": k_ortho rows per block / 64 (0: auto)
 inline int g_ortho_min_tpb = 2;  // hh_tune "ortho_min_tpb": the automatic choice's smallest rows per block / 64
+inline int g_ortho_lowsync = 1;     // hh_tune "ortho_lowsync": k_ortho's Full mode as low-synch CGS2 (0: round 3's 8 reductions)
+inline int g_ortho_grid_cap = 0;    // hh_tune "ortho_grid_cap": a lower cap on k_ortho's grid (0: occupancy-derived only)
+inline int g_ortho_abort_test = 0;  // hh_tune "ortho_abort_test": act as if k_ortho's barrier timed out (tests the fallback)
 inline int g_pca_coop = 1;  // hh_tune "pca_coop": Krylov orthogonalisation in one launch per product (k_ortho)
 inline int g_pca_debug = 0;  // hh_tune "pca_debug": per-cycle trace on stderr
 

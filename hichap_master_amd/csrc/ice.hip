@@ -2080,9 +2080,12 @@ template <int NB, int ABL>
 static void launch_sweep(const hh_matrix* m, const uint8_t* act, const double* b, double* part, hipStream_t s,
                          hipStream_t s_tiled) {
     const int n_tiled = (int)(m->n_units - m->n_units_flat), n_flat = (int)m->n_units_flat;
-    if (n_tiled)
+    if (n_tiled) {
+        HH_KTIME("k_sweep_tiled", s_tiled);  // per-kernel registry timing (probes; off by default)
         hipLaunchKernelGGL((k_sweep_tiled<NB, ABL>), dim3((unsigned)n_tiled), dim3(kSweepThreads), 0, s_tiled,
                            m->dev(), act, n_tiled, b, (long long)m->n_bins, part);
+    }
+    HH_KTIME(n_flat ? "k_sweep_flat" : nullptr, s);
     if (n_flat && m->n_fgroups) {
         auto kern = g_flatw_u == 16 ? (g_flatw_pipe == 2 ? k_sweep_flatw<16, ABL, 2>
                                        : g_flatw_pipe == 1 ? k_sweep_flatw<16, ABL, 1> : k_sweep_flatw<16, ABL, 0>)
@@ -2220,6 +2223,7 @@ static void sweep_uband(hh_ice* S, hipStream_t s) {
     const int ch = ub_segs(S, segs);
     const long long ng = S->ub_ghi - S->ub_glo;
     if (!ch || ng <= 0) return;
+    HH_KTIME("k_sweep_ubands", s);
     hipLaunchKernelGGL(k_sweep_ubands, dim3((unsigned)ng, (unsigned)ch), dim3(kUbThreads), 0, s, segs, ub_args(S),
                        (long long)S->m->n_bins, g_ub_xcd);
     HIP_CHECK(hipGetLastError());
@@ -2342,6 +2346,7 @@ static void marg_weighted(hh_ice* S, double* out, hipStream_t s, bool timed, int
     const int stats = (g_fuse_stats != 0 && S->full() && out == S->marg.p && S->n_tiles > 0)
                           ? (S->small_stats() ? 1 : 2)
                           : 0;
+    HH_KTIME(timed ? nullptr : "k_marg", s);
     hipLaunchKernelGGL(k_marg, dim3(nblocks(S->nloc, kR)), dim3(kMargThreads), 0, s, m->dev(), S->part.p,
                        m->wide_ptr.p, m->wide_col.p, m->wide_cnt.p, m->diag.p, m->row_group.p, S->act(),
                        S->bias.p, (long long)m->row_lo, (int)S->nloc, S->bpart.p, S->nchu ? 0 : (int)S->nch,
@@ -2520,6 +2525,13 @@ int hh_tune(const char* key, int64_t value) {
             g_build_debug = value;
         } else if (k == "pca_debug") {
             g_pca_debug = (int)value;
+        } else if (k == "ortho_lowsync") {
+            g_ortho_lowsync = value ? 1 : 0;
+        } else if (k == "ortho_grid_cap") {
+            HH_REQUIRE(value >= 0 && value <= 64, "ortho_grid_cap in [0, 64]");
+            g_ortho_grid_cap = (int)value;
+        } else if (k == "ortho_abort_test") {
+            g_ortho_abort_test = value ? 1 : 0;
         } else if (k == "pca_coop") {
             HH_REQUIRE(value == 0 || value == 1, "pca_coop in {0, 1}");
             g_pca_coop = (int)value;

@@ -164,42 +164,52 @@ def sweep_rate(bin1, bin2, count, n_bins, iters):
 # cooler's balance splits each sweep over a process pool (``cooler balance
 # --nproc``, default 8): every worker marginalises its chunks of the pixel
 # table with the current bias, the parent sums the partial vectors.  The
-# same here, for bench.py's multi-core CPU baseline (test infrastructure).
-_POOL_PIX = None
+# same here, for bench.py's multi-core CPU baseline (test infrastructure):
+# forked workers, the pixel table inherited, the bias and the partial
+# marginals in shared memory (no per-task pickling of 5 MB vectors).
+_POOL = None
 
 
-def _pool_chunk(args):
-    lo, hi, bias = args
-    b1, b2, c, n = _POOL_PIX
+def _pool_chunk(k):
+    b1, b2, c, n, cuts, bias_sh, out_sh = _POOL
+    lo, hi = int(cuts[k]), int(cuts[k + 1])
+    bias = np.frombuffer(bias_sh, dtype=np.float64)
+    out = np.frombuffer(out_sh, dtype=np.float64).reshape(-1, n)
     s1, s2 = b1[lo:hi], b2[lo:hi]
-    return marginalize(s1, s2, c[lo:hi] * bias[s1] * bias[s2], n)
+    out[k] = marginalize(s1, s2, c[lo:hi] * bias[s1] * bias[s2], n)
+    return k
 
 
-def sweep_rate_pool(bin1, bin2, count, n_bins, iters, nproc, chunks_per_proc=4):
+def sweep_rate_pool(bin1, bin2, count, n_bins, iters, nproc):
     """``sweep_rate`` with each sweep's marginal split over ``nproc`` forked
-    processes (cooler's balance pool; chunks summed in chunk order).
-    Returns the bias."""
+    processes (cooler's balance pool), one pixel chunk each, the partials
+    summed in chunk order.  Returns the bias."""
     import multiprocessing as mp
-    global _POOL_PIX
+    global _POOL
+    n = int(n_bins)
+    nch = max(1, int(nproc))
     b1 = np.asarray(bin1, np.int64)
     b2 = np.asarray(bin2, np.int64)
     c = np.asarray(count, np.float64)
-    _POOL_PIX = (b1, b2, c, int(n_bins))
-    nch = max(1, int(nproc) * int(chunks_per_proc))
     cuts = np.linspace(0, b1.size, nch + 1).astype(np.int64)
-    bias = np.ones(n_bins)
+    bias_sh = mp.RawArray("d", n)
+    out_sh = mp.RawArray("d", nch * n)
+    bias = np.frombuffer(bias_sh, dtype=np.float64)
+    out = np.frombuffer(out_sh, dtype=np.float64).reshape(nch, n)
+    bias[:] = 1.0
+    _POOL = (b1, b2, c, n, cuts, bias_sh, out_sh)
     try:
-        with mp.get_context("fork").Pool(int(nproc)) as pool:
+        with mp.get_context("fork").Pool(nch) as pool:
             for _ in range(iters):
-                parts = pool.map(_pool_chunk, [(int(cuts[k]), int(cuts[k + 1]), bias) for k in range(nch)])
-                marg = parts[0]
-                for q in parts[1:]:
-                    marg = marg + q
+                pool.map(_pool_chunk, range(nch), chunksize=1)
+                marg = out[0].copy()
+                for q in range(1, nch):
+                    marg += out[q]
                 nz = marg[marg != 0]
                 m = marg / nz.mean()
                 m[m == 0] = 1
-                bias = bias / m
+                bias /= m
                 _ = nz.var()
+        return bias.copy()
     finally:
-        _POOL_PIX = None
-    return bias
+        _POOL = None

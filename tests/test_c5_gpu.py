@@ -307,3 +307,29 @@ def test_c5_selected_pc_vs_oracle(chrom):
     big = np.abs(ref_full) > 1e-8
     np.testing.assert_array_equal(np.sign(full[big]), np.sign(ref_full[big]))
     np.testing.assert_allclose(full, ref_full, atol=1e-9)
+
+
+def test_pca_ortho_fallback_and_grid_cap():
+    """k_ortho's co-residency: (a) when its grid barrier gives up
+    (simulated: hh_tune ortho_abort_test), hh_comp_pca redoes the solve on the
+    multi-launch path and reports it -- same components as the multi-launch
+    run, bitwise; (b) a lower grid cap (fewer, taller blocks, as on a box with
+    more hardware queues) gives the same components to rounding."""
+    from hichap_master_amd._lib import call
+    dM = _c5_matrix(20)
+    p0, s0 = _pca_run(dM, 0)
+    call("hh_tune", b"ortho_abort_test", 1)
+    try:
+        p1, s1 = _pca_run(dM, 1)
+    finally:
+        call("hh_tune", b"ortho_abort_test", 0)
+    assert s1["ortho_fallback"] and s1["converged"] and not s0["ortho_fallback"]
+    np.testing.assert_array_equal(p1, p0)
+    call("hh_tune", b"ortho_grid_cap", 8)
+    try:
+        p2, s2 = _pca_run(dM, 1)
+    finally:
+        call("hh_tune", b"ortho_grid_cap", 0)
+    assert s2["converged"] and not s2["ortho_fallback"]
+    for q in range(3):
+        np.testing.assert_allclose(_match_sign(p2[q], p0[q]), p0[q], atol=1e-11)

@@ -39,10 +39,16 @@ def measure(world, rr, tag):
         torch.cuda.synchronize()
         _lib.call("hh_ktime_enable", 0)
         t, n = _lib.ktime("ice_sweep")
+        per = {}
+        for kn in ("k_sweep_ubands", "k_sweep_flat", "k_sweep_tiled", "k_marg"):
+            kt, kc = _lib.ktime(kn)
+            per[kn] = kt / max(kc, 1) if kc else 0.0
         inf = m.info()
         ms.append(t / max(n, 1))
         print(f"{tag} world={world} rank={r} rows=[{rr[r]},{rr[r+1]}) pixels={ru[rr[r]:rr[r+1]].sum():.4g} "
-              f"payload={inf['payload_bytes']/1e9:.2f}GB sweep={ms[-1]:.3f}ms", flush=True)
+              f"payload={inf['payload_bytes']/1e9:.2f}GB (flat {inf['payload_bytes_flat']/1e9:.2f}) "
+              f"units={inf['n_units']} flat_units={inf['n_units_flat']} sweep={ms[-1]:.3f}ms "
+              + " ".join(f"{k[2:]}={v:.3f}" for k, v in per.items()), flush=True)
         st.close()
         m.close()
     print(f"{tag} world={world}: max {max(ms):.3f} ms, mean {np.mean(ms):.3f} ms, "
