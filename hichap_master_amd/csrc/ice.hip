@@ -2057,6 +2057,7 @@ static int g_split_tiles = 1;      // with band_concurrent: tiled kernel on a se
 // faster for C3 (3.0 GB) and the N = 8 C4 shards (1.6-1.9 GB), three streams
 // 0.3 % faster for the whole C4 matrix (14.8 GB; profiles/r2_conc_probe.log)
 static int64_t g_conc_min_bytes = 8LL << 30;
+static int64_t g_conc_ub_min_bytes = 1LL << 30;  // the same with the upper-band sweep (round 4)
 static int g_band_rows = 0;   // rows per band block: 0 = auto (64 or 256)
 static int g_band_fused = 1;  // the band segments in one launch
 static int g_band_lpt = 1;      // band chunks dispatched heaviest first (0: uint8 first, index order)
@@ -2313,7 +2314,12 @@ static void marg_weighted(hh_ice* S, double* out, hipStream_t s, bool timed, int
         // kernel runs on a side stream so its blocks fill the CUs the tile
         // kernel leaves idle (both are HBM-bound; neither saturates alone)
         const int64_t bytes = 4 * m->n_slots + 2 * m->n_slots_narrow + (int64_t)m->band.n + (int64_t)m->band4.n;
-        const bool conc = g_band_concurrent && (S->nch || S->nchu) && S->nloc && m->n_units && bytes >= g_conc_min_bytes;
+        // (with the upper-band sweep -- C4 and its shards -- from 1 GB: the N = 8
+        // C4 shards (1.85 GB) sweep in 0.567 vs 0.637 ms max, N = 4 0.976 vs
+        // 1.018 ms; C3 (3.0 GB, no upper band) stays faster on one stream,
+        // 1250 vs 1177 it/s; profiles/r4f_conc_ab.log)
+        const bool conc = g_band_concurrent && (S->nch || S->nchu) && S->nloc && m->n_units &&
+                          (bytes >= g_conc_min_bytes || (S->nchu && bytes >= g_conc_ub_min_bytes));
         const bool single = g_sweep_nb == 2 &&
                             (g_sweep_single == 1 || (g_sweep_single == -1 && bytes < g_single_max_bytes));
         if (single) {
@@ -2525,6 +2531,9 @@ int hh_tune(const char* key, int64_t value) {
             g_build_debug = value;
         } else if (k == "pca_debug") {
             g_pca_debug = (int)value;
+        } else if (k == "conc_ub_min_bytes") {
+            HH_REQUIRE(value >= 0, "conc_ub_min_bytes >= 0");
+            g_conc_ub_min_bytes = value;
         } else if (k == "ortho_lowsync") {
             g_ortho_lowsync = value ? 1 : 0;
         } else if (k == "ortho_grid_cap") {
