@@ -542,6 +542,112 @@ __global__ __launch_bounds__(256, 2) void k_cor_sym(const double* __restrict__ C
         for (int reg = 0; reg < 4; ++reg) outr[(16 * g + lr + 4 * reg) * kSB + lc] = dr[g][reg];
 }
 
+// k_cor_sym with the rectangle's V rows staged once (all four column tiles,
+// one barrier) and each wave's first Cor loads of the next column tile issued
+// during the last row group of the current one: the per-column-tile global
+// latency of the V staging and of the first loads is no longer exposed.  The
+// same MFMA sequence and partial sums per tile: bitwise k_cor_sym's result
+// (hh_tune "cor_sym" 2, the default; 1 = k_cor_sym).
+__global__ __launch_bounds__(256, 2) void k_cor_sym_pf(const double* __restrict__ Cor, long long ldc, long long n,
+                                                      const double* __restrict__ V, long long nr,
+                                                      double* __restrict__ part_c, double* __restrict__ part_r) {
+    __shared__ double Wt[4][16 * kCsW];
+    __shared__ double Vc[4][64 * kSB];  // V rows of the rectangle's column tiles
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, lr = lane >> 4, lc = lane & 15;
+    long long p, q;
+    syrk_tile_ij(blockIdx.x, nr, p, q);
+    const long long R0 = p * kCsR + 64 * w;
+    const bool rows_ok = R0 < ldc;
+    const bool diag = p == q;
+    const int nct = (int)std::min<long long>(4, (ldc - q * kCsR + 63) / 64);  // column tiles inside the matrix
+    for (int e = threadIdx.x; e < 4 * 64 * kSB; e += 256) {
+        const long long c = q * kCsR + e / kSB;  // e / kSB = 64 ct + row within the tile
+        Vc[e / (64 * kSB)][e % (64 * kSB)] = c < n ? V[c * kSB + e % kSB] : 0.0;
+    }
+    double bv[4][4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const long long r = R0 + 16 * g + 4 * j + lr;
+            const double x = V[(r < n ? r : n - 1) * kSB + lc];
+            bv[g][j] = r < n ? x : 0.0;
+        }
+    d4 dr[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) dr[g] = d4{0.0, 0.0, 0.0, 0.0};
+    double* wt = Wt[w];
+    auto col_on = [&](int ct) { return rows_ok && ct < nct && (!diag || ct >= w); };
+    const double* cbase = Cor + (R0 + lr) * ldc + q * kCsR + 4 * lc;
+    auto load = [&](int ct, int g, d4 (&dst)[4]) __attribute__((always_inline)) {
+        const double* cp = cbase + 64 * ct + 16 * g * ldc;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) dst[j] = __builtin_nontemporal_load(reinterpret_cast<const d4*>(cp + 4 * j * ldc));
+    };
+    d4 av[4], an[4];
+    if (col_on(0)) load(0, 0, av);
+    __syncthreads();  // Vc staged
+    for (int ct = 0; ct < nct; ++ct) {
+        const long long C0 = q * kCsR + 64 * ct;
+        const bool con = col_on(ct);
+        const bool row_on = con && (!diag || ct > w);
+        const bool next_on = col_on(ct + 1);
+        const double* vct = Vc[ct];
+        d4 acc[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc[t] = d4{0.0, 0.0, 0.0, 0.0};
+        if (con) {
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                if (g < 3) load(ct, g + 1, an);
+                else if (next_on) load(ct + 1, 0, an);
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+#pragma unroll
+                    for (int t = 0; t < 4; ++t)
+                        acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[j][t], bv[g][j], acc[t], 0, 0, 0);
+                if (row_on) {
+                    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+#pragma unroll
+                        for (int t = 0; t < 4; ++t) wt[(4 * j + lr) * kCsW + 4 * lc + t] = av[j][t];
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+                    for (int cs = 0; cs < 16; ++cs)
+                        dr[g] = __builtin_amdgcn_mfma_f64_16x16x4f64(wt[lc * kCsW + 4 * cs + lr],
+                                                                      vct[(4 * cs + lr) * kSB + lc], dr[g], 0, 0, 0);
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                }
+                if (g < 3 || next_on)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) av[j] = an[j];
+            }
+        } else if (next_on) {
+            load(ct + 1, 0, av);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int reg = 0; reg < 4; ++reg) wt[(4 * (lr + 4 * reg) + t) * kSB + lc] = acc[t][reg];
+        __syncthreads();
+        double* out = part_c + ((size_t)p * ldc + C0) * kSB;
+        for (int e = threadIdx.x; e < 64 * kSB; e += 256) out[e] = ((Wt[0][e] + Wt[1][e]) + Wt[2][e]) + Wt[3][e];
+        __syncthreads();
+    }
+    if (!rows_ok) return;
+    double* outr = part_r + ((size_t)q * ldc + R0) * kSB;
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) outr[(16 * g + lr + 4 * reg) * kSB + lc] = dr[g][reg];
+}
+
 // Y[i][b] = sum_{p <= P} part_c[p][i][b] + sum_{q >= P} part_r[q][i][b], P = i / 256
 __global__ void k_cor_sym_sum(const double* __restrict__ part_c, const double* __restrict__ part_r, long long ldc,
                               long long n, long long nr, double* __restrict__ Y) {
@@ -865,8 +971,8 @@ struct PcaWork {
             }
             HH_KTIME("k_cor_mul", s);
             // (occupancy 2: 190 VGPRs; forcing 3 spills and measured 98.9 vs 105.9 chromosomes/s)
-            hipLaunchKernelGGL(k_cor_sym, dim3((unsigned)(nr * (nr + 1) / 2)), dim3(256), 0, s, Cor, ldc, n, V, nr,
-                               sym_c.p, sym_r.p);
+            hipLaunchKernelGGL(g_cor_sym == 2 ? k_cor_sym_pf : k_cor_sym, dim3((unsigned)(nr * (nr + 1) / 2)), dim3(256),
+                               0, s, Cor, ldc, n, V, nr, sym_c.p, sym_r.p);
             hipLaunchKernelGGL(k_cor_sym_sum, dim3((unsigned)((n * kSB + 255) / 256)), dim3(256), 0, s, sym_c.p,
                                sym_r.p, ldc, n, nr, Y);
             return;

@@ -254,7 +254,7 @@ def _pca_run_sym(dM, sym):
         pcs, Cor, OE = sf.Get_PCA(distance_bin=dec.copy(), M=dM, NG_array=NG)
         return np.asarray(pcs), dict(sf.pca_status), NG.size
     finally:
-        call("hh_tune", b"cor_sym", 1)
+        call("hh_tune", b"cor_sym", 2)
 
 
 @pytest.mark.parametrize("chrom", [21, 9])
@@ -333,3 +333,14 @@ def test_pca_ortho_fallback_and_grid_cap():
     assert s2["converged"] and not s2["ortho_fallback"]
     for q in range(3):
         np.testing.assert_allclose(_match_sign(p2[q], p0[q]), p0[q], atol=1e-11)
+
+
+def test_pca_pipelined_upper_triangle_product_bitwise():
+    """k_cor_sym_pf (V staged once per rectangle, the next column tile's
+    first loads in flight) against k_cor_sym: the same MFMA sequence and
+    partial sums, so bitwise the same components (chr9: ragged last range)."""
+    dM = _c5_matrix(8)
+    p1, s1, _ = _pca_run_sym(dM, 1)
+    p2, s2, _ = _pca_run_sym(dM, 2)
+    assert s1["products"] == s2["products"]
+    np.testing.assert_array_equal(p1, p2)
