@@ -71,6 +71,7 @@ struct SymArgs {
     const uint8_t* gap;   // nullptr: sum form (no gap)
     const double* s;      // pass 2/3: rowsum(Y)^(exponent), 0 -> 1
     double scale;         // pass 3: mean(X) / mean(C)
+    const double* scale_p = nullptr;  // pass 3: the same from device memory (no host round trip)
 };
 
 // Per-tile vectors staged once in LDS: alpha, gap flag and s for the 64
@@ -197,11 +198,12 @@ __global__ __launch_bounds__(256) void k_symvc(const T* __restrict__ X, SymArgs 
         acc = block_sum(acc, sh);
         if (threadIdx.x == 0) part[p] = acc;
     } else {
+        const double scale = a.scale_p ? *a.scale_p : a.scale;
         const int c = threadIdx.x & (kT - 1);
         for (int r = threadIdx.x >> 6; r < lim_r; r += 4) {
             if (c < lim_c) {
                 const double y = sym_value(diag_tile && r == c, has_gap, tv.gI[r], tv.gJ[c], st[r][c], stT[r][c]);
-                __builtin_nontemporal_store(a.scale * (y / (tv.sJ[c] * tv.sI[r])), &out[(I0 + r) * N + J0 + c]);
+                __builtin_nontemporal_store(scale * (y / (tv.sJ[c] * tv.sI[r])), &out[(I0 + r) * N + J0 + c]);
             }
         }
         if (!diag_tile) {
@@ -209,7 +211,7 @@ __global__ __launch_bounds__(256) void k_symvc(const T* __restrict__ X, SymArgs 
             for (int r = threadIdx.x >> 6; r < lim_c; r += 4) {
                 if (c < lim_r) {
                     const double y = sym_value(false, has_gap, tv.gI[c], tv.gJ[r], st[c][r], stT[c][r]);
-                    __builtin_nontemporal_store(a.scale * (y / (tv.sI[c] * tv.sJ[r])), &out[(J0 + r) * N + I0 + c]);
+                    __builtin_nontemporal_store(scale * (y / (tv.sI[c] * tv.sJ[r])), &out[(J0 + r) * N + I0 + c]);
                 }
             }
         }
@@ -224,11 +226,20 @@ __global__ void k_symvc_rows(const double* __restrict__ part, long long N, long 
     if (i >= N) return;
     const long long I = i / kT;
     const int r = (int)(i % kT);
+    // loads 8 tiles at a time (independent), added in J order: the same sum
+    auto at = [&](long long J) {
+        return J >= I ? part[pair_index(I, J, nT) * (2 * kT) + r] : part[pair_index(J, I, nT) * (2 * kT) + kT + r];
+    };
     double acc = 0.0;
-    for (long long J = 0; J < nT; ++J) {
-        if (J >= I) acc += part[pair_index(I, J, nT) * (2 * kT) + r];
-        else acc += part[pair_index(J, I, nT) * (2 * kT) + kT + r];
+    long long J = 0;
+    for (; J + 8 <= nT; J += 8) {
+        double x[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) x[u] = at(J + u);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc += x[u];
     }
+    for (; J < nT; ++J) acc += at(J);
     double v = pow(acc, exponent);
     if (v == 0.0) v = 1.0;
     s[i] = v;
@@ -243,38 +254,57 @@ __global__ __launch_bounds__(256) void k_slab_sum(const double* __restrict__ par
     if (threadIdx.x == 0) *out = acc;
 }
 
+// the mean rescale (raw_sum / N^2) / (sum C / N^2) on the device, the same
+// IEEE operations as on the host
+__global__ void k_symvc_scale(const double* __restrict__ tot, double raw_sum, double nn, double* __restrict__ scale) {
+    if (threadIdx.x == 0) *scale = (raw_sum / nn) / (*tot / nn);
+}
+
+// Workspace of one Trans2symmetry + Correct_VC + rescale chain (alive until
+// the stream has run it).
+struct SymvcWs {
+    DBuf<double> part, sv, tot;
+};
+
+// Enqueues the chain without a host round trip (the rescale factor is
+// formed and read on the device); `ws` must outlive the kernels.
+template <class T>
+static void symvc_enqueue(const T* dX, long long N, const double* dalpha, const uint8_t* dgap, double exponent,
+                          double raw_sum, double* dout, hipStream_t s, SymvcWs& ws) {
+    const long long nT = (N + kT - 1) / kT;
+    const long long npairs = nT * (nT + 1) / 2;
+    HH_REQUIRE(npairs < (1LL << 31), "matrix too large");
+    ws.part.alloc((size_t)npairs * 2 * kT);
+    ws.sv.alloc(N);
+    ws.tot.alloc(2);
+    SymArgs a{N, nT, dalpha, dgap, nullptr, 1.0};
+    {
+        HH_KTIME("k_symvc1", s);
+        hipLaunchKernelGGL((k_symvc<T, 1>), dim3((unsigned)npairs), dim3(256), 0, s, dX, a, ws.part.p, nullptr);
+    }
+    hipLaunchKernelGGL(k_symvc_rows, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, ws.part.p, N, nT, exponent,
+                       ws.sv.p);
+    a.s = ws.sv.p;
+    {
+        HH_KTIME("k_symvc2", s);
+        hipLaunchKernelGGL((k_symvc<T, 2>), dim3((unsigned)npairs), dim3(256), 0, s, dX, a, ws.part.p, nullptr);
+    }
+    hipLaunchKernelGGL(k_slab_sum, dim3(1), dim3(256), 0, s, ws.part.p, npairs, ws.tot.p);
+    hipLaunchKernelGGL(k_symvc_scale, dim3(1), dim3(64), 0, s, ws.tot.p, raw_sum, (double)N * (double)N,
+                       ws.tot.p + 1);
+    a.scale_p = ws.tot.p + 1;
+    {
+        HH_KTIME("k_symvc3", s);
+        hipLaunchKernelGGL((k_symvc<T, 3>), dim3((unsigned)npairs), dim3(256), 0, s, dX, a, ws.part.p, dout);
+    }
+    HIP_CHECK(hipGetLastError());
+}
+
 template <class T>
 static void symvc_run(const T* dX, long long N, const double* dalpha, const uint8_t* dgap, double exponent,
                       double raw_sum, double* dout, hipStream_t s) {
-    const long long nT = (N + kT - 1) / kT;
-    const long long npairs = nT * (nT + 1) / 2;
-    DBuf<double> part((size_t)npairs * 2 * kT);
-    DBuf<double> sv(N);
-    DBuf<double> tot(1);
-    SymArgs a{N, nT, dalpha, dgap, nullptr, 1.0};
-    HH_REQUIRE(npairs < (1LL << 31), "matrix too large");
-    {
-        HH_KTIME("k_symvc1", s);
-        hipLaunchKernelGGL((k_symvc<T, 1>), dim3((unsigned)npairs), dim3(256), 0, s, dX, a, part.p, nullptr);
-    }
-    hipLaunchKernelGGL(k_symvc_rows, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, part.p, N, nT, exponent,
-                       sv.p);
-    a.s = sv.p;
-    {
-        HH_KTIME("k_symvc2", s);
-        hipLaunchKernelGGL((k_symvc<T, 2>), dim3((unsigned)npairs), dim3(256), 0, s, dX, a, part.p, nullptr);
-    }
-    hipLaunchKernelGGL(k_slab_sum, dim3(1), dim3(256), 0, s, part.p, npairs, tot.p);
-    double sumC = 0.0;
-    HIP_CHECK(hipMemcpyAsync(&sumC, tot.p, sizeof(double), hipMemcpyDeviceToHost, s));
-    HIP_CHECK(hipStreamSynchronize(s));
-    const double nn = (double)N * (double)N;
-    a.scale = (raw_sum / nn) / (sumC / nn);
-    {
-        HH_KTIME("k_symvc3", s);
-        hipLaunchKernelGGL((k_symvc<T, 3>), dim3((unsigned)npairs), dim3(256), 0, s, dX, a, part.p, dout);
-    }
-    HIP_CHECK(hipGetLastError());
+    SymvcWs ws;
+    symvc_enqueue(dX, N, dalpha, dgap, exponent, raw_sum, dout, s, ws);
     HIP_CHECK(hipStreamSynchronize(s));
 }
 
@@ -282,9 +312,12 @@ static void symvc_run(const T* dX, long long N, const double* dalpha, const uint
 // virtual index (n-1)*q, floor/next clipped to the ends, _lerp's two-sided
 // form), so host-side gap and alpha decisions are bit-identical to the
 // reference's NumPy calls.
+// Only the two order statistics around the virtual index are needed: one
+// nth_element and a min over the rest (O(n); a full sort of the ~6 000
+// coverages / alphas of a chromosome was most of TwoStepCorrection's host
+// time between its passes, profiles/r4m_twostep_trace.log).
 static double np_percentile(std::vector<double> v, double pct) {
     HH_REQUIRE(!v.empty(), "percentile of an empty array");
-    std::sort(v.begin(), v.end());
     const long long n = (long long)v.size();
     const double q = pct / 100.0;
     const double vi = (double)(n - 1) * q;
@@ -292,7 +325,10 @@ static double np_percentile(std::vector<double> v, double pct) {
     if (vi >= (double)(n - 1)) prev = next = n - 1;
     if (vi < 0) prev = next = 0;
     const double gamma = vi - (vi >= (double)(n - 1) ? -1.0 : (double)prev);
-    const double a = v[prev], b = v[next], d = b - a;
+    std::nth_element(v.begin(), v.begin() + prev, v.end());
+    const double a = v[prev];
+    const double b = next == prev ? a : *std::min_element(v.begin() + prev + 1, v.end());
+    const double d = b - a;
     return gamma >= 0.5 ? b - d * (1.0 - gamma) : a + d * gamma;
 }
 
@@ -512,12 +548,15 @@ int hh_twostep(const int64_t* TM, const int64_t* MM, const int64_t* PM, int64_t 
             for (long long i = 0; i < N; ++i) t += (long long)sum[(k + 1) * N + i];
             raw[k] = (double)t;
         }
-        // outputs: on the host path TM's buffer holds Nor_MM, then MM's holds Nor_PM
+        // outputs: on the host path TM's buffer holds Nor_MM, then MM's holds
+        // Nor_PM; both chains enqueued back to back, one synchronisation
+        SymvcWs wm, wp;
         double* out_m = on_device ? nor_mm : (double*)buf[0].p;
-        symvc_run(d[1], N, dA.p, any_m ? dgm.p : nullptr, 2.0 / 3.0, raw[0], out_m, s);
+        symvc_enqueue(d[1], N, dA.p, any_m ? dgm.p : nullptr, 2.0 / 3.0, raw[0], out_m, s, wm);
         if (!on_device) HIP_CHECK(hipMemcpyAsync(nor_mm, out_m, cnt * 8, hipMemcpyDeviceToHost, s));
         double* out_p = on_device ? nor_pm : (double*)buf[1].p;
-        symvc_run(d[2], N, dA.p, any_p ? dgp.p : nullptr, 2.0 / 3.0, raw[1], out_p, s);
+        // (MM's buffer, read by the first chain, is written by the second: stream order)
+        symvc_enqueue(d[2], N, dA.p, any_p ? dgp.p : nullptr, 2.0 / 3.0, raw[1], out_p, s, wp);
         if (!on_device) HIP_CHECK(hipMemcpyAsync(nor_pm, out_p, cnt * 8, hipMemcpyDeviceToHost, s));
         HIP_CHECK(hipStreamSynchronize(s));
         std::copy(gm.begin(), gm.end(), gap_m);
