@@ -410,9 +410,15 @@ class StructureFind(TADCalling):
         """Compartment() (StructureFind.py:491-554): raw matrices from the
         cooler (or ``Matrix_Dict``), one selected PC per chromosome in
         ``Compartment_Dict`` (zeros at gap bins); haplotype data also keep
-        the three raw PCs in ``RawPCA``."""
-        if Matrix_Dict is None:
-            chroms, Matrix_Dict = self._chroms_and_matrices(False)
+        the three raw PCs in ``RawPCA``.  From a cooler file each
+        chromosome's raw matrix is built on the GPU from its pixels
+        (:499-513 fetch densely on the host: N^2 x 8 B through PCIe; here
+        only the pixel table crosses), ``Matrix_Dict`` a lazy dense view."""
+        from_file = Matrix_Dict is None
+        if from_file:
+            chroms = self._cooler_chroms()
+            from .tads import _LazyMatrices
+            Matrix_Dict = _LazyMatrices(self.cooler_fil, chroms, False)
         else:
             chroms = list(Matrix_Dict)
         trad = self.Loading_Tranditional_PC(Tranditional_PC_file) if self.Allelic is not False else None
@@ -422,7 +428,12 @@ class StructureFind(TADCalling):
         # first access from the device-held ones (Plot_Compartment reads them)
         self.Cor_Martrix_Dict, self.OE_Matrix_Dict = _ThunkDict(), _ThunkDict()
         for chro in chroms:
-            M = np.asarray(Matrix_Dict[chro], dtype=np.float64)
+            if from_file:
+                M = self._device_raw_matrix(chro)
+                M_host = (lambda chro=chro: np.asarray(Matrix_Dict[chro], dtype=np.float64))
+            else:
+                M = np.asarray(Matrix_Dict[chro], dtype=np.float64)
+                M_host = M
             distance_bin, Gap, NonGap = self.Distance_Decay(M=M, G_array=None)
             pca, Cor_M, OE_M = self.Get_PCA(distance_bin=distance_bin, M=M, NG_array=NonGap, SA=SA)
             out = np.zeros(M.shape[0], dtype=float)
@@ -439,16 +450,48 @@ class StructureFind(TADCalling):
             # workspace) is freed now, not kept alive by the dicts
             dec = np.array(distance_bin, dtype=np.float64)
             for d, kind in ((self.OE_Matrix_Dict, "OE"), (self.Cor_Martrix_Dict, "Cor")):
-                d.put(chro, self._refill_thunk(M, dec, NonGap, SA, kind))
-            del Cor_M, OE_M
+                d.put(chro, self._refill_thunk(M_host, dec, NonGap, SA, kind))
+            del Cor_M, OE_M, M
             self._comp = self._comp_src = None
         return self.Compartment_Dict
 
+    def _cooler_chroms(self):
+        """The chromosomes the reference's Compartment reads (:499-506)."""
+        from .coolio import Cooler
+        if not self.cooler_fil:
+            raise ValueError("no cooler file (StructureFind(cooler_fil=..., Res=...))")
+        with Cooler(self.cooler_fil) as c:
+            if self.Allelic is False:
+                return list(c.chromnames)
+            if self.Allelic in ("Maternal", "Paternal"):
+                return [x for x in c.chromnames if x.startswith(self.Allelic[0])]
+        raise ValueError(f"Unknown key word {self.Allelic}, only Maternal, Paternal, False allowed")
+
+    def _device_raw_matrix(self, chro):
+        """``cooler.matrix(balance=False).fetch(chro)`` as a float64 device
+        tensor built from the chromosome's pixels (hh_dense_from_cells:
+        symmetric scatter of the upper-triangle cells, exact int64, then one
+        conversion pass)."""
+        import torch
+        from .coolio import Cooler
+        from .matrixBuilding import dense_from_cells_device
+        with Cooler(self.cooler_fil) as c:
+            lo, hi = c.extent(chro)
+            b1, b2, v = c.pixel_rows(lo, hi)
+        keep = b2 < hi
+        D = dense_from_cells_device((b1[keep], b2[keep], v[keep]), hi - lo, lo, symmetric=True,
+                                    stream=None if self.stream is None else C.c_void_p(int(self.stream)))
+        return D.to(torch.float64)
+
     def _refill_thunk(self, M, decline, NonGap, SA, kind):
-        """Refill_Gap(M, OE or Cor) made on first access from the host inputs:
-        the correlation (and the Sliding_Approach O/E) recomputed on the GPU
-        in a short-lived hh_comp, the plain O/E on the host."""
+        """Refill_Gap(M, OE or Cor) made on first access from the host inputs
+        (``M`` an array or a zero-argument function giving it): the
+        correlation (and the Sliding_Approach O/E) recomputed on the GPU in a
+        short-lived hh_comp, the plain O/E on the host."""
         def make():
+            nonlocal M
+            if callable(M):
+                M = M()
             NG = np.asarray(NonGap, dtype=np.int64)
             if kind == "OE" and not SA:
                 sub = M[:, NG]
