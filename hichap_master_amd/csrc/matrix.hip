@@ -418,8 +418,11 @@ TilePlan plan_tiles(const uint16_t* cntw, const uint16_t* cntn, int64_t nloc, in
             const int32_t ja = P.tile_J[P.u_tlo[a]], jb = P.tile_J[P.u_tlo[b]];
             return ja != jb ? ja < jb : P.u_rb[a] < P.u_rb[b];
         });
+        // (>= ~512 groups: with the three-stream sweep at shard size the
+        // other kernels fill the flat launch's tail; N = 8 C4 shards mean
+        // 0.542 -> 0.534 ms with 22-tile groups, profiles/r4u_shard_knobs.log)
         const size_t gmax = g_flat_group > 0 ? (size_t)g_flat_group
-                                             : std::min<size_t>(44, std::max<size_t>(11, fu.size() / 1024));
+                                             : std::min<size_t>(44, std::max<size_t>(11, fu.size() / 512));
         std::vector<std::pair<int64_t, std::pair<int32_t, int32_t>>> groups;  // (-words, [lo, hi) in fu)
         for (size_t a = 0; a < fu.size();) {
             size_t e = a;
