@@ -15,6 +15,7 @@
 //      reduced in a fixed order (bitwise deterministic, no float atomics).
 #include <algorithm>
 #include <cmath>
+#include <cstring>
 #include <limits>
 #include <type_traits>
 #include <vector>
@@ -218,6 +219,86 @@ __global__ __launch_bounds__(256) void k_symvc(const T* __restrict__ X, SymArgs 
     }
 }
 
+// PASS 3 with one LDS tile (round 4, default; hh_tune "symvc_out"): both
+// tiles' X values are loaded into registers (lane = column, coalesced), the
+// (J, I) tile goes through LDS transposed for the (I, J) outputs, then the
+// (I, J) tile for the (J, I) outputs.  33 KB of LDS instead of 66 KB: 4
+// blocks per CU instead of 2.  The same operands and IEEE operations as
+// k_symvc<T, 3> (bitwise the same output).
+template <class T>
+__global__ __launch_bounds__(256) void k_symvc_out(const T* __restrict__ X, SymArgs a, double* __restrict__ out) {
+    __shared__ T tt[kT][kT + 1];
+    __shared__ TileVecs tv;
+    const long long p = blockIdx.x;
+    long long I = 0, rem = p;
+    while (rem >= a.nT - I) { rem -= a.nT - I; ++I; }
+    const long long J = I + rem;
+    const long long I0 = I * kT, J0 = J * kT, N = a.N;
+    const bool has_gap = a.gap != nullptr;
+    const bool diag_tile = I == J;
+    const int c = threadIdx.x & (kT - 1);
+    const int r0 = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: scalar row bases
+    // Clamped addresses and no select on any loaded value (a select lets the
+    // compiler sink each load into a branch with its own vmcnt(0) wait); a
+    // value read from a clamped address is never used: the outputs are
+    // guarded by lim_r / lim_c, and a valid output's operands are in range.
+    // The 32 matrix loads go first, the tile vectors after them.
+    const long long cj = J0 + c < N ? J0 + c : N - 1, ci = I0 + c < N ? I0 + c : N - 1;
+    T v[kT / 4], w[kT / 4];
+#pragma unroll
+    for (int k = 0; k < kT / 4; ++k) {
+        const int r = r0 + 4 * k;
+        const long long gi = I0 + r, ti = J0 + r;
+        v[k] = X[(gi < N ? gi : N - 1) * N + cj];
+        w[k] = X[(ti < N ? ti : N - 1) * N + ci];
+    }
+    if (threadIdx.x < kT) {
+        const int r = threadIdx.x;
+        const long long gi = I0 + r < N ? I0 + r : N - 1, gj = J0 + r < N ? J0 + r : N - 1;
+        tv.aI[r] = a.alpha[gi];
+        tv.aJ[r] = a.alpha[gj];
+        tv.sI[r] = a.s[gi];
+        tv.sJ[r] = a.s[gj];
+        if (has_gap) {
+            tv.gI[r] = a.gap[gi];
+            tv.gJ[r] = a.gap[gj];
+        } else {
+            tv.gI[r] = tv.gJ[r] = 0;
+        }
+    }
+    const double scale = *a.scale_p;
+    const int lim_r = (int)std::min<long long>(kT, N - I0), lim_c = (int)std::min<long long>(kT, N - J0);
+    // (I, J) outputs: S_ij = v / aI[r], S_ji = X[J0 + c][I0 + r] / aJ[c] = tt[r][c] / aJ[c]
+#pragma unroll
+    for (int k = 0; k < kT / 4; ++k) tt[c][r0 + 4 * k] = w[k];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kT / 4; ++k) {
+        const int r = r0 + 4 * k;
+        if (r < lim_r && c < lim_c) {
+            const double sij = (double)v[k] / tv.aI[r], sji = (double)tt[r][c] / tv.aJ[c];
+            const double y = sym_value(diag_tile && r == c, has_gap, tv.gI[r], tv.gJ[c], sij, sji);
+            __builtin_nontemporal_store(scale * (y / (tv.sJ[c] * tv.sI[r])), &out[(I0 + r) * N + J0 + c]);
+        }
+    }
+    if (diag_tile) return;
+    __syncthreads();
+    // (J, I) outputs: element (J0 + r, I0 + c) = Y[I0 + c][J0 + r];
+    // S[I0 + c][J0 + r] = tt[r][c] / aI[c], S[J0 + r][I0 + c] = w / aJ[r]
+#pragma unroll
+    for (int k = 0; k < kT / 4; ++k) tt[c][r0 + 4 * k] = v[k];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kT / 4; ++k) {
+        const int r = r0 + 4 * k;
+        if (r < lim_c && c < lim_r) {
+            const double sij = (double)tt[r][c] / tv.aI[c], sji = (double)w[k] / tv.aJ[r];
+            const double y = sym_value(false, has_gap, tv.gI[c], tv.gJ[r], sij, sji);
+            __builtin_nontemporal_store(scale * (y / (tv.sI[c] * tv.sJ[r])), &out[(J0 + r) * N + I0 + c]);
+        }
+    }
+}
+
 // rowsum(Y)_i from the pass-1 slab in a fixed order (J = 0 .. nT-1), then
 // s_i = rowsum^exponent, 0 -> 1.
 __global__ void k_symvc_rows(const double* __restrict__ part, long long N, long long nT, double exponent,
@@ -260,24 +341,378 @@ __global__ void k_symvc_scale(const double* __restrict__ tot, double raw_sum, do
     if (threadIdx.x == 0) *scale = (raw_sum / nn) / (*tot / nn);
 }
 
+// ---- passes 1-2 as row streams (round 4, default; hh_tune "symvc_stream") --
+// The tile-pair passes read S_ij and S_ji together through two LDS tiles
+// (~113 us each at N = 6 232: 2.8 TB/s, 2 blocks per CU).  Passes 1 and 2
+// only need sums, and Y's sums follow from plain row / column sums of S:
+//   R_i = sum_j S_ij = (sum_j X_ij) / alpha_i,   Ccol_i = sum_j S_ji
+//   gap form (Trans2symmetry :957-979):
+//     rowsum(Y)_i = (R_i + Ccol_i) / 2 + [i in G] sum_{j in G, j != i} |S_ij - S_ji| / 2
+//     (max(a, b) = (a + b) / 2 + |a - b| / 2 on the both-gap pairs)
+//   sum form (no gap, :947-955): rowsum(Y)_i = R_i + Ccol_i - S_ii
+//   Q = sum_ij S_ij / (s_i s_j) = sum_i (sum_j X_ij / s_j) / (alpha_i s_i)
+//   gap form: sum(C) = Q + sum_{i != j in G} |S_ij - S_ji| / (2 s_i s_j)
+//   sum form: sum(C) = 2 Q - sum_i S_ii / s_i^2
+// so each pass is one coalesced row-major stream over X (k_ts_gemv) plus a
+// gap-pair correction over |G|^2 elements (k_ts_gap).  Every partial is
+// summed in a fixed order (deterministic); the sums differ from the
+// tile-pair passes only by rounding (the int64 row sums are exact).
+// rows per block: hh_tune "symvc_rows" (g_symvc_rows; every wave of the block
+// takes every row of it)
+constexpr int kGW = 512;      // columns per wave (8 per lane, 512 B per load instruction)
+constexpr int kGB = 4 * kGW;  // columns per block: its 4 waves read 16 KB of a row together
+
+// Wave w of block (rc, cb) owns the 512-column span q = 4 cb + w and the
+// block's rows r0 .. r0 + gr - 1 (reading a row's 2 048 block columns
+// together keeps the HBM pages open; 64x64 tiles read 512 B per row and ran
+// at ~2.7 TB/s).
+// MODE 1: part_c[rc][j] = sum over the block's rows i of X_ij * (1 / alpha_i);
+//         part_r[q][i] = sum over the span's columns of X_ij (int64 exact for
+//         integer X, stored in the double slot's bits); the both-gap entries
+//         X_ij (i, j gaps) copied to the compact g x g matrix Xc.
+// MODE 2: part_r[q][i] = sum over the span's columns of X_ij * rs_j.
+template <class T, int MODE>
+__global__ __launch_bounds__(256) void k_ts_gemv(const T* __restrict__ X, long long N,
+                                                 const double* __restrict__ alpha, const double* __restrict__ rs,
+                                                 int gr, double* __restrict__ part_c, double* __restrict__ part_r,
+                                                 const int* __restrict__ gpos, T* __restrict__ Xc, long long ng) {
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const long long rc = blockIdx.x, q = (long long)blockIdx.y * 4 + w;
+    const long long r0 = rc * gr, c0 = q * kGW;
+    if (c0 >= N) return;  // wave-uniform; no block barrier below
+    double accc[8], bcol[8];
+    bool okc[8];
+    int gcol[8];        // MODE 1 with gaps: the column's compact index, -1 if not a gap
+    unsigned coff[8];   // clamped column offsets (elements) from the span's first column
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const long long c = c0 + lane + 64 * k;
+        okc[k] = c < N;
+        coff[k] = (unsigned)((okc[k] ? c : N - 1) - c0);
+        accc[k] = 0.0;
+        bcol[k] = (MODE == 2 && okc[k]) ? rs[c] : 0.0;
+        gcol[k] = (MODE == 1 && gpos && okc[k]) ? gpos[c] : -1;
+    }
+    const long long rend = std::min<long long>(r0 + gr, N);
+    constexpr int kB = 4;  // rows per batch: 32 loads in flight per lane
+#pragma unroll 1
+    for (long long i0 = r0; i0 < rend; i0 += kB) {
+        T x[kB][8];
+#pragma unroll
+        for (int b = 0; b < kB; ++b) {
+            const bool okr = i0 + b < rend;
+            // unconditional loads from clamped addresses (row clamped to the
+            // last one, columns to N - 1); the clamped values are weighted by
+            // zero or masked where they are summed -- a select on the loaded
+            // value lets the compiler sink each load into its own branch
+            // with a vmcnt(0) wait (measured: 32 serialised loads)
+            const T* row = X + (okr ? i0 + b : rend - 1) * N + c0;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) x[b][k] = row[coff[k]];
+        }
+#pragma unroll
+        for (int b = 0; b < kB; ++b) {
+            const long long i = i0 + b;
+            const bool okr = i < rend;
+            if (MODE == 1) {
+                // S_ij = X_ij / alpha_i as X_ij * (1 / alpha_i): within an ulp of the
+                // true quotient, and a division per element doubles the registers
+                const double ra = okr ? 1.0 / alpha[i] : 0.0;
+#pragma unroll
+                for (int k = 0; k < 8; ++k) accc[k] += (double)x[b][k] * ra;
+                if (gpos && okr) {
+                    const int gi = gpos[i];
+                    if (gi >= 0) {
+#pragma unroll
+                        for (int k = 0; k < 8; ++k)
+                            if (gcol[k] >= 0) Xc[(long long)gi * ng + gcol[k]] = x[b][k];
+                    }
+                }
+                if constexpr (std::is_integral_v<T>) {
+                    long long t = 0;
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) t += okc[k] ? (long long)x[b][k] : 0LL;
+                    t = wave_sum_ll(t);
+                    if (lane == 0 && okr) reinterpret_cast<long long*>(part_r)[q * N + i] = t;
+                } else {
+                    double t = 0.0;
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) t += okc[k] ? (double)x[b][k] : 0.0;
+                    t = wave_sum(t);
+                    if (lane == 0 && okr) part_r[q * N + i] = t;
+                }
+            } else {
+                double t = 0.0;
+#pragma unroll
+                for (int k = 0; k < 8; ++k) t += (double)x[b][k] * bcol[k];
+                t = wave_sum(t);
+                if (lane == 0 && okr) part_r[q * N + i] = t;
+            }
+        }
+    }
+    if (MODE == 1) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            if (okc[k]) part_c[rc * N + c0 + lane + 64 * k] = accc[k];
+    }
+}
+
+// The both-gap pairs' correction on the compact g x g matrix Xc (gap rows
+// and columns in index order): block (A, B) of 64 x 64 tiles gives, for each
+// compact row a of A,
+//   MODE 1: gpart[B][a] = sum_{b in B, b != a} |S_ab - S_ba| / 2
+//   MODE 2: gpart[B][a] = sum_{b in B, b != a} (|S_ab - S_ba| / 2) / (s_b s_a)
+// with S_ab = Xc[a][b] / alpha_{G[a]}; (B, A) is read coalesced and
+// transposed through LDS.
+template <class T, int MODE>
+__global__ __launch_bounds__(256) void k_ts_gap(const T* __restrict__ Xc, long long ng, const int* __restrict__ glist,
+                                                const double* __restrict__ alpha, const double* __restrict__ sv,
+                                                double* __restrict__ gpart) {
+    __shared__ T tt[kT][kT + 1];
+    __shared__ double aA[kT], aB[kT], sA[kT], sB[kT];
+    __shared__ double red[4][kT];
+    const long long A0 = (long long)blockIdx.x * kT, B0 = (long long)blockIdx.y * kT;
+    const int c = threadIdx.x & (kT - 1), r0 = threadIdx.x >> 6;
+    // clamped addresses, no select on loaded values (see k_symvc_out); a
+    // value from a clamped address is never used
+    const long long ca = A0 + c < ng ? A0 + c : ng - 1, cbb = B0 + c < ng ? B0 + c : ng - 1;
+    T xd[kT / 4];
+#pragma unroll
+    for (int k = 0; k < kT / 4; ++k) {
+        const int r = r0 + 4 * k;
+        const long long ra = A0 + r < ng ? A0 + r : ng - 1, rb = B0 + r < ng ? B0 + r : ng - 1;
+        tt[c][r] = Xc[rb * ng + ca];  // tt[c][r] = Xc[B0 + r][A0 + c]
+        xd[k] = Xc[ra * ng + cbb];    // Xc[A0 + r][B0 + c]
+    }
+    if (threadIdx.x < kT) {
+        const int r = threadIdx.x;
+        const int ga = glist[A0 + r < ng ? A0 + r : ng - 1], gb = glist[B0 + r < ng ? B0 + r : ng - 1];
+        aA[r] = alpha[ga];
+        aB[r] = alpha[gb];
+        sA[r] = MODE == 2 ? sv[ga] : 1.0;
+        sB[r] = MODE == 2 ? sv[gb] : 1.0;
+    }
+    __syncthreads();
+    // thread: row a = A0 + r (r = r0 + 4 k), column b = B0 + c; reduce over c
+#pragma unroll
+    for (int k = 0; k < kT / 4; ++k) {
+        const int r = r0 + 4 * k;
+        const long long a = A0 + r, b = B0 + c;
+        double d = 0.0;
+        if (a < ng && b < ng && a != b) {
+            const double sab = (double)xd[k] / aA[r], sba = (double)tt[r][c] / aB[c];
+            d = fabs(sab - sba) / 2.0;
+            if (MODE == 2) d = d / (sB[c] * sA[r]);
+        }
+        d = wave_sum(d);
+        if (c == 0) red[r0][k] = d;
+    }
+    __syncthreads();
+    if (threadIdx.x < kT) {
+        const int r = threadIdx.x;  // r = r0' + 4 k'
+        if (A0 + r < ng) gpart[blockIdx.y * ng + A0 + r] = red[r & 3][r >> 2];
+    }
+}
+
+// Ccol_j = sum over the row chunks of part_c[rc][j] (fixed order: wave w
+// sums a contiguous range of chunks, the 16 wave sums added in order).
+__global__ __launch_bounds__(1024) void k_ts_colsum(const double* __restrict__ part_c, long long N, long long nrc,
+                                                    double* __restrict__ ccol) {
+    __shared__ double red[16][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const long long j = (long long)blockIdx.x * 64 + lane;
+    const long long per = (nrc + 15) / 16, lo = std::min<long long>(nrc, w * per),
+                    hi = std::min<long long>(nrc, lo + per);
+    double acc = 0.0;
+    if (j < N) {
+        long long rc = lo;
+        for (; rc + 8 <= hi; rc += 8) {
+            double x[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) x[u] = part_c[(rc + u) * N + j];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) acc += x[u];
+        }
+        for (; rc < hi; ++rc) acc += part_c[rc * N + j];
+    }
+    red[w][lane] = acc;
+    __syncthreads();
+    if (threadIdx.x < 64 && j < N) {
+        double t = 0.0;
+        for (int k = 0; k < 16; ++k) t += red[k][threadIdx.x];
+        ccol[j] = t;
+    }
+}
+
+// rowsum(Y) from the MODE-1 partials (fixed order), s = rowsum^exponent
+// (0 -> 1) and 1 / s.
+template <class T>
+__global__ void k_ts_rows(const T* __restrict__ X, long long N, long long ncb,
+                          const double* __restrict__ ccol, const double* __restrict__ part_r,
+                          const double* __restrict__ alpha, const uint8_t* __restrict__ gap,
+                          const int* __restrict__ gpos, const double* __restrict__ gpart, long long ng,
+                          double exponent, double* __restrict__ sv, double* __restrict__ rsv) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    const double c = ccol[i];
+    double rsum;
+    if constexpr (std::is_integral_v<T>) {
+        long long t = 0;
+        for (long long cb = 0; cb < ncb; ++cb) t += reinterpret_cast<const long long*>(part_r)[cb * N + i];
+        rsum = (double)t;
+    } else {
+        double t = 0.0;
+        for (long long cb = 0; cb < ncb; ++cb) t += part_r[cb * N + i];
+        rsum = t;
+    }
+    const double ai = alpha[i];
+    const double r = rsum / ai;
+    double y;
+    if (gap) {
+        y = (r + c) / 2.0;
+        if (gpos && gpos[i] >= 0) {  // the both-gap pairs' max - mean, in tile order
+            const long long a = gpos[i], nbt = (ng + kT - 1) / kT;
+            double gc = 0.0;
+            for (long long B = 0; B < nbt; ++B) gc += gpart[B * ng + a];
+            y += gc;
+        }
+    } else {
+        y = (r + c) - (double)X[i * N + i] / ai;
+    }
+    double v = pow(y, exponent);
+    if (v == 0.0) v = 1.0;
+    sv[i] = v;
+    rsv[i] = 1.0 / v;
+}
+
+// Per-block partials of sum(C) from the MODE-2 row partials.
+template <class T>
+__global__ __launch_bounds__(256) void k_ts_q(const T* __restrict__ X, long long N, long long ncb,
+                                              const double* __restrict__ part_r, const double* __restrict__ alpha,
+                                              const double* __restrict__ sv, const uint8_t* __restrict__ gap,
+                                              const double* __restrict__ gpart2, long long ng,
+                                              double* __restrict__ part) {
+    __shared__ double sh[16];
+    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    double term = 0.0;
+    if (i < N) {
+        double u = 0.0;
+        for (long long cb = 0; cb < ncb; ++cb) u += part_r[cb * N + i];
+        const double ai = alpha[i], si = sv[i];
+        const double q = u / (ai * si);
+        if (gap) {
+            term = q;
+            if (i < ng) {  // compact gap row i's both-gap share of sum(C)
+                const long long nbt = (ng + kT - 1) / kT;
+                double g2 = 0.0;
+                for (long long B = 0; B < nbt; ++B) g2 += gpart2[B * ng + i];
+                term += g2;
+            }
+        } else {
+            const double sii = (double)X[i * N + i] / ai;
+            term = 2.0 * q - sii / (si * si);
+        }
+    }
+    term = block_sum(term, sh);
+    if (threadIdx.x == 0) part[blockIdx.x] = term;
+}
+
 // Workspace of one Trans2symmetry + Correct_VC + rescale chain (alive until
 // the stream has run it).
 struct SymvcWs {
     DBuf<double> part, sv, tot;
+    DBuf<double> part_c, part_r, rsv, ccol, gpart1, gpart2;  // streaming passes
+    DBuf<int> glist, gpos;
+    DBuf<char> xc;  // the compact both-gap matrix
+    std::vector<int> hgl, hgp;  // host sources of glist / gpos (alive until the copies ran)
 };
+
+// The gap rows (index order) and each row's position among them (-1: not a
+// gap), on the device, for the streaming passes' both-gap correction.
+struct GapIdx {
+    const int* gpos = nullptr;
+    const int* glist = nullptr;
+    long long ng = 0;
+};
+
+static void gap_index_host(const uint8_t* hgap, long long N, std::vector<int>& gl, std::vector<int>& gp) {
+    gl.clear();
+    gp.assign(N, -1);
+    for (long long i = 0; i < N; ++i)
+        if (hgap[i]) { gp[i] = (int)gl.size(); gl.push_back((int)i); }
+}
 
 // Enqueues the chain without a host round trip (the rescale factor is
 // formed and read on the device); `ws` must outlive the kernels.
 template <class T>
-static void symvc_enqueue(const T* dX, long long N, const double* dalpha, const uint8_t* dgap, double exponent,
-                          double raw_sum, double* dout, hipStream_t s, SymvcWs& ws) {
+static void symvc_enqueue(const T* dX, long long N, const double* dalpha, const uint8_t* dgap, GapIdx gi,
+                          double exponent, double raw_sum, double* dout, hipStream_t s, SymvcWs& ws) {
     const long long nT = (N + kT - 1) / kT;
     const long long npairs = nT * (nT + 1) / 2;
     HH_REQUIRE(npairs < (1LL << 31), "matrix too large");
-    ws.part.alloc((size_t)npairs * 2 * kT);
     ws.sv.alloc(N);
     ws.tot.alloc(2);
     SymArgs a{N, nT, dalpha, dgap, nullptr, 1.0};
+    if (g_symvc_stream) {
+        const int gr = g_symvc_rows;
+        const long long nrc = (N + gr - 1) / gr, ncb = (N + kGW - 1) / kGW;
+        HH_REQUIRE(ncb < 65536 && nrc < (1LL << 31), "matrix too large");
+        const long long nb = (N + 255) / 256;
+        ws.part_c.alloc((size_t)(nrc * N));
+        ws.part_r.alloc((size_t)(ncb * N));
+        ws.rsv.alloc(N);
+        ws.ccol.alloc(N);
+        ws.part.alloc((size_t)nb);
+        const long long ng = dgap ? gi.ng : 0;
+        if (ng) {
+            ws.xc.alloc((size_t)(ng * ng) * sizeof(T));
+            const long long nbt = (ng + kT - 1) / kT;
+            ws.gpart1.alloc((size_t)(nbt * ng));
+            ws.gpart2.alloc((size_t)(nbt * ng));
+        }
+        T* xc = ng ? (T*)ws.xc.p : nullptr;
+        const int* gpos = ng ? gi.gpos : nullptr;
+        const unsigned nbt = (unsigned)((ng + kT - 1) / kT);
+        const unsigned gcb = (unsigned)((N + kGB - 1) / kGB);
+        {
+            HH_KTIME("k_ts_gemv1", s);
+            hipLaunchKernelGGL((k_ts_gemv<T, 1>), dim3((unsigned)nrc, gcb), dim3(256), 0, s, dX, N, dalpha,
+                               (const double*)nullptr, gr, ws.part_c.p, ws.part_r.p, gpos, xc, ng);
+        }
+        if (ng)
+            hipLaunchKernelGGL((k_ts_gap<T, 1>), dim3(nbt, nbt), dim3(256), 0, s, (const T*)xc, ng, gi.glist, dalpha,
+                               (const double*)nullptr, ws.gpart1.p);
+        hipLaunchKernelGGL(k_ts_colsum, dim3((unsigned)((N + 63) / 64)), dim3(1024), 0, s, ws.part_c.p, N, nrc,
+                           ws.ccol.p);
+        hipLaunchKernelGGL((k_ts_rows<T>), dim3((unsigned)nb), dim3(256), 0, s, dX, N, ncb, ws.ccol.p,
+                           ws.part_r.p, dalpha, dgap, gpos, ws.gpart1.p, ng, exponent, ws.sv.p, ws.rsv.p);
+        if (ng)
+            hipLaunchKernelGGL((k_ts_gap<T, 2>), dim3(nbt, nbt), dim3(256), 0, s, (const T*)xc, ng, gi.glist, dalpha,
+                               ws.sv.p, ws.gpart2.p);
+        {
+            HH_KTIME("k_ts_gemv2", s);
+            hipLaunchKernelGGL((k_ts_gemv<T, 2>), dim3((unsigned)nrc, gcb), dim3(256), 0, s, dX, N, dalpha, ws.rsv.p,
+                               gr, ws.part_c.p, ws.part_r.p, (const int*)nullptr, (T*)nullptr, 0LL);
+        }
+        hipLaunchKernelGGL((k_ts_q<T>), dim3((unsigned)nb), dim3(256), 0, s, dX, N, ncb, ws.part_r.p, dalpha, ws.sv.p,
+                           dgap, ws.gpart2.p, ng, ws.part.p);
+        hipLaunchKernelGGL(k_slab_sum, dim3(1), dim3(256), 0, s, ws.part.p, nb, ws.tot.p);
+        hipLaunchKernelGGL(k_symvc_scale, dim3(1), dim3(64), 0, s, ws.tot.p, raw_sum, (double)N * (double)N,
+                           ws.tot.p + 1);
+        a.s = ws.sv.p;
+        a.scale_p = ws.tot.p + 1;
+        {
+            HH_KTIME("k_symvc3", s);
+            if (g_symvc_out)
+                hipLaunchKernelGGL((k_symvc_out<T>), dim3((unsigned)npairs), dim3(256), 0, s, dX, a, dout);
+            else
+                hipLaunchKernelGGL((k_symvc<T, 3>), dim3((unsigned)npairs), dim3(256), 0, s, dX, a, ws.part.p, dout);
+        }
+        HIP_CHECK(hipGetLastError());
+        return;
+    }
+    ws.part.alloc((size_t)npairs * 2 * kT);
     {
         HH_KTIME("k_symvc1", s);
         hipLaunchKernelGGL((k_symvc<T, 1>), dim3((unsigned)npairs), dim3(256), 0, s, dX, a, ws.part.p, nullptr);
@@ -301,10 +736,22 @@ static void symvc_enqueue(const T* dX, long long N, const double* dalpha, const 
 }
 
 template <class T>
-static void symvc_run(const T* dX, long long N, const double* dalpha, const uint8_t* dgap, double exponent,
+static void symvc_run(const T* dX, long long N, const double* dalpha, const uint8_t* dgap, const uint8_t* hgap,
+                      double exponent,
                       double raw_sum, double* dout, hipStream_t s) {
     SymvcWs ws;
-    symvc_enqueue(dX, N, dalpha, dgap, exponent, raw_sum, dout, s, ws);
+    GapIdx gi;
+    if (dgap && hgap) {
+        gap_index_host(hgap, N, ws.hgl, ws.hgp);
+        gi.ng = (long long)ws.hgl.size();
+        if (gi.ng) {
+            ws.gpos = to_device(ws.hgp, s);
+            ws.glist = to_device(ws.hgl, s);
+            gi.gpos = ws.gpos.p;
+            gi.glist = ws.glist.p;
+        }
+    }
+    symvc_enqueue(dX, N, dalpha, dgap, gi, exponent, raw_sum, dout, s, ws);
     HIP_CHECK(hipStreamSynchronize(s));
 }
 
@@ -332,14 +779,63 @@ static double np_percentile(std::vector<double> v, double pct) {
     return gamma >= 0.5 ? b - d * (1.0 - gamma) : a + d * gamma;
 }
 
-// Gap_defined (:915-929) from zero counts: cov = 1 - zeros / N
-static std::vector<uint8_t> gap_defined(const std::vector<long long>& zeros, long long N) {
-    std::vector<double> cov(N), nz;
+// Per-thread pinned host staging buffers (slot 0: downloads, 1: uploads),
+// grown on demand and kept for the process (never freed: freeing pinned
+// memory from a thread_local destructor at exit races the runtime's own
+// teardown).  A call synchronises its stream before returning, so the next
+// call on the thread may reuse them.
+struct PinnedStage {
+    void* p[2] = {nullptr, nullptr};
+    size_t cap[2] = {0, 0};
+    void* get(int slot, size_t bytes) {
+        if (bytes > cap[slot]) {
+            // the old buffer is idle (its copies completed before the last synchronisation)
+            if (p[slot]) HIP_CHECK(hipHostFree(p[slot]));
+            p[slot] = nullptr;
+            cap[slot] = 0;
+            const size_t want = std::max<size_t>(bytes, 1 << 20);
+            HIP_CHECK(hipHostMalloc(&p[slot], want, hipHostMallocDefault));
+            cap[slot] = want;
+        }
+        return p[slot];
+    }
+};
+static PinnedStage& pinned_stage() {
+    static thread_local PinnedStage* st = new PinnedStage();
+    return *st;
+}
+
+// Gap_defined (:915-929) from zero counts: cov = 1 - zeros / N.  cov is a
+// non-increasing function of the integer zero count, so the percentile's two
+// order statistics come from a count per zero count (O(N), no sort): the
+// k-th smallest nonzero cov is cov(the k-th largest zero count among them),
+// the same doubles as sorting the cov values.
+static std::vector<uint8_t> gap_defined(const long long* zeros, long long N) {
+    std::vector<double> cov(N);
+    std::vector<long long> cnt(N + 1, 0);
+    long long nnz = 0;
     for (long long i = 0; i < N; ++i) {
         cov[i] = 1.0 - ((double)zeros[i] / (double)N);
-        if (cov[i] != 0.0) nz.push_back(cov[i]);
+        HH_REQUIRE(zeros[i] >= 0 && zeros[i] <= N, "zero count out of range");
+        if (cov[i] != 0.0) { ++cnt[zeros[i]]; ++nnz; }
     }
-    double th = np_percentile(nz, 25.0);
+    HH_REQUIRE(nnz > 0, "percentile of an empty array");
+    auto kth = [&](long long k) {  // k-th smallest (0-based) nonzero cov
+        long long acc = 0;
+        for (long long z = N; z >= 0; --z) {
+            acc += cnt[z];
+            if (acc > k) return 1.0 - ((double)z / (double)N);
+        }
+        return 1.0;
+    };
+    const double q = 25.0 / 100.0;
+    const double vi = (double)(nnz - 1) * q;
+    long long prev = (long long)std::floor(vi), next = prev + 1;
+    if (vi >= (double)(nnz - 1)) prev = next = nnz - 1;
+    const double gamma = vi - (vi >= (double)(nnz - 1) ? -1.0 : (double)prev);
+    const double a = kth(prev), b = next == prev ? a : kth(next);
+    const double d = b - a;
+    double th = gamma >= 0.5 ? b - d * (1.0 - gamma) : a + d * gamma;  // np_percentile's lerp
     if (th > 0.2) th = 0.2;
     std::vector<uint8_t> g(N);
     for (long long i = 0; i < N; ++i) g[i] = cov[i] < th;
@@ -476,8 +972,20 @@ int hh_dense_symvc(const void* X, int32_t dtype, int64_t N, const double* alpha,
                 pg = dG.p;
             }
         }
-        if (dtype == 0) symvc_run((const long long*)px, N, pa, pg, exponent, raw_sum, po, s);
-        else symvc_run((const double*)px, N, pa, pg, exponent, raw_sum, po, s);
+        // the gap flags on the host too (the streaming passes list the gap rows there)
+        std::vector<uint8_t> hg;
+        if (gap) {
+            hg.resize(N);
+            if (on_device) {
+                HIP_CHECK(hipMemcpyAsync(hg.data(), gap, N, hipMemcpyDeviceToHost, s));
+                HIP_CHECK(hipStreamSynchronize(s));
+            } else {
+                std::copy(gap, gap + N, hg.begin());
+            }
+        }
+        const uint8_t* hgp = gap ? hg.data() : nullptr;
+        if (dtype == 0) symvc_run((const long long*)px, N, pa, pg, hgp, exponent, raw_sum, po, s);
+        else symvc_run((const double*)px, N, pa, pg, hgp, exponent, raw_sum, po, s);
         if (!on_device) {
             HIP_CHECK(hipMemcpyAsync(out, po, bytes, hipMemcpyDeviceToHost, s));
             HIP_CHECK(hipStreamSynchronize(s));
@@ -514,15 +1022,21 @@ int hh_twostep(const int64_t* TM, const int64_t* MM, const int64_t* PM, int64_t 
                                (const long long*)nullptr, (const long long*)nullptr, dsum.p + k * N, dz.p + k * N);
         }
         HIP_CHECK(hipGetLastError());
-        std::vector<double> sum((size_t)3 * N);
-        std::vector<long long> zeros((size_t)3 * N);
-        dsum.download(sum.data(), sum.size(), s);
-        dz.download(zeros.data(), zeros.size(), s);
+        // row statistics down and the per-call vectors up through pinned
+        // staging (DMA; pageable copies cost a staging pass each), the
+        // vectors in one packed upload
+        PinnedStage& st = pinned_stage();
+        const size_t dl_bytes = (size_t)3 * N * (sizeof(double) + sizeof(long long));
+        char* dl = (char*)st.get(0, dl_bytes);
+        double* sum = (double*)dl;
+        long long* zeros = (long long*)(dl + (size_t)3 * N * sizeof(double));
+        dsum.download(sum, (size_t)3 * N, s);
+        dz.download(zeros, (size_t)3 * N, s);
         HIP_CHECK(hipStreamSynchronize(s));
-        const std::vector<long long> zm(zeros.begin() + N, zeros.begin() + 2 * N), zp(zeros.begin() + 2 * N, zeros.end());
-        const std::vector<uint8_t> gm = gap_defined(zm, N), gp = gap_defined(zp, N);
+        const std::vector<uint8_t> gm = gap_defined(zeros + N, N), gp = gap_defined(zeros + 2 * N, N);
         // alpha over the union of non-gap bins (:994-1005)
         std::vector<double> alpha(N), ng;
+        ng.reserve(N);
         for (long long i = 0; i < N; ++i) alpha[i] = (sum[N + i] + sum[2 * N + i]) / (sum[i] + 1.0);
         double mx = -std::numeric_limits<double>::infinity();
         for (long long i = 0; i < N; ++i)
@@ -537,10 +1051,10 @@ int hh_twostep(const int64_t* TM, const int64_t* MM, const int64_t* PM, int64_t 
         const double th = np_percentile(ng, 20.0);
         for (long long i = 0; i < N; ++i)
             if (alpha[i] < th) alpha[i] = th;
-        DBuf<double> dA = to_device(alpha, s);
-        bool any_m = false, any_p = false;
-        for (long long i = 0; i < N; ++i) { any_m |= gm[i] != 0; any_p |= gp[i] != 0; }
-        DBuf<uint8_t> dgm = to_device(gm, s), dgp = to_device(gp, s);
+        std::vector<int> glm, gpm, glp, gpp;
+        gap_index_host(gm.data(), N, glm, gpm);
+        gap_index_host(gp.data(), N, glp, gpp);
+        const bool any_m = !glm.empty(), any_p = !glp.empty();
         // exact integer totals (MM.mean() * N^2)
         double raw[2];
         for (int k = 0; k < 2; ++k) {
@@ -548,15 +1062,34 @@ int hh_twostep(const int64_t* TM, const int64_t* MM, const int64_t* PM, int64_t 
             for (long long i = 0; i < N; ++i) t += (long long)sum[(k + 1) * N + i];
             raw[k] = (double)t;
         }
+        // packed upload: alpha | gpos_m | glist_m | gpos_p | glist_p | gap_m | gap_p (16-B aligned parts)
+        auto al = [](size_t b) { return (b + 15) & ~(size_t)15; };
+        const size_t o_gpm = al((size_t)N * 8), o_glm = o_gpm + al((size_t)N * 4), o_gpp = o_glm + al(glm.size() * 4 + 4),
+                     o_glp = o_gpp + al((size_t)N * 4), o_gm = o_glp + al(glp.size() * 4 + 4), o_gp = o_gm + al((size_t)N),
+                     up_bytes = o_gp + al((size_t)N);
+        char* up = (char*)st.get(1, up_bytes);
+        std::memcpy(up, alpha.data(), (size_t)N * 8);
+        std::memcpy(up + o_gpm, gpm.data(), (size_t)N * 4);
+        if (any_m) std::memcpy(up + o_glm, glm.data(), glm.size() * 4);
+        std::memcpy(up + o_gpp, gpp.data(), (size_t)N * 4);
+        if (any_p) std::memcpy(up + o_glp, glp.data(), glp.size() * 4);
+        std::memcpy(up + o_gm, gm.data(), (size_t)N);
+        std::memcpy(up + o_gp, gp.data(), (size_t)N);
+        DBuf<char> dup(up_bytes);
+        dup.upload(up, up_bytes, s);
+        const double* dA = (const double*)dup.p;
+        const uint8_t *dgm = (const uint8_t*)(dup.p + o_gm), *dgp = (const uint8_t*)(dup.p + o_gp);
+        GapIdx gim{(const int*)(dup.p + o_gpm), (const int*)(dup.p + o_glm), (long long)glm.size()};
+        GapIdx gip{(const int*)(dup.p + o_gpp), (const int*)(dup.p + o_glp), (long long)glp.size()};
         // outputs: on the host path TM's buffer holds Nor_MM, then MM's holds
         // Nor_PM; both chains enqueued back to back, one synchronisation
         SymvcWs wm, wp;
         double* out_m = on_device ? nor_mm : (double*)buf[0].p;
-        symvc_enqueue(d[1], N, dA.p, any_m ? dgm.p : nullptr, 2.0 / 3.0, raw[0], out_m, s, wm);
+        symvc_enqueue(d[1], N, dA, any_m ? dgm : nullptr, gim, 2.0 / 3.0, raw[0], out_m, s, wm);
         if (!on_device) HIP_CHECK(hipMemcpyAsync(nor_mm, out_m, cnt * 8, hipMemcpyDeviceToHost, s));
         double* out_p = on_device ? nor_pm : (double*)buf[1].p;
         // (MM's buffer, read by the first chain, is written by the second: stream order)
-        symvc_enqueue(d[2], N, dA.p, any_p ? dgp.p : nullptr, 2.0 / 3.0, raw[1], out_p, s, wp);
+        symvc_enqueue(d[2], N, dA, any_p ? dgp : nullptr, gip, 2.0 / 3.0, raw[1], out_p, s, wp);
         if (!on_device) HIP_CHECK(hipMemcpyAsync(nor_pm, out_p, cnt * 8, hipMemcpyDeviceToHost, s));
         HIP_CHECK(hipStreamSynchronize(s));
         std::copy(gm.begin(), gm.end(), gap_m);

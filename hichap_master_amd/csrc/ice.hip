@@ -2539,6 +2539,13 @@ int hh_tune(const char* key, int64_t value) {
         } else if (k == "ortho_grid_cap") {
             HH_REQUIRE(value >= 0 && value <= 64, "ortho_grid_cap in [0, 64]");
             g_ortho_grid_cap = (int)value;
+        } else if (k == "symvc_rows") {
+            HH_REQUIRE(value >= 16 && value <= 1024 && value % 16 == 0, "symvc_rows in [16, 1024], a multiple of 16");
+            g_symvc_rows = (int)value;
+        } else if (k == "symvc_out") {
+            g_symvc_out = value ? 1 : 0;
+        } else if (k == "symvc_stream") {
+            g_symvc_stream = value ? 1 : 0;
         } else if (k == "ortho_abort_test") {
             g_ortho_abort_test = value ? 1 : 0;
         } else if (k == "pca_coop") {

@@ -163,3 +163,42 @@ def test_twostep_cpu_torch_tensors_take_the_host_path(mb):
         np.testing.assert_array_equal(a, b)
     with pytest.raises(ValueError):
         mb.TwoStepCorrection(torch.from_numpy(TM).cuda(), MM, PM)
+
+
+def _twostep_with(mb, tune, *mats):
+    from hichap_master_amd import _lib
+    try:
+        for k, v in tune.items():
+            _lib.call("hh_tune", k.encode(), int(v))
+        return mb.TwoStepCorrection(*mats)
+    finally:
+        _lib.call("hh_tune", b"symvc_stream", 1)
+        _lib.call("hh_tune", b"symvc_out", 1)
+        _lib.call("hh_tune", b"symvc_rows", 32)
+
+
+@pytest.mark.parametrize("case", ["gaps_1000", "nogap_golden", "ragged_777"])
+def test_twostep_streaming_passes_match_tile_pairs(mb, golden, case):
+    """Passes 1-2 as row streams (k_ts_gemv + the both-gap correction) give
+    the tile-pair passes' result up to summation rounding, with the gap and
+    the no-gap (sum) forms; the one-LDS-tile pass 3 is bitwise the two-tile
+    one; the rows-per-block knob does not change the result beyond rounding."""
+    if case == "nogap_golden":
+        g = golden("twostep_nogapM_n80")
+        mats = (g["TM"], g["MM"], g["PM"])
+    else:
+        N, drop = (1000, 40) if case == "gaps_1000" else (777, 0)
+        rng = np.random.default_rng(N + 7)
+        TM = synth.dense_chrom(N, rng, A=60.0)
+        mats = (TM,) + tuple(synth.haplotype_pair(TM, rng, drop_rows=drop))
+    tiles = _twostep_with(mb, {"symvc_stream": 0, "symvc_out": 0}, *mats)
+    stream2 = _twostep_with(mb, {"symvc_stream": 1, "symvc_out": 0}, *mats)
+    stream1 = _twostep_with(mb, {"symvc_stream": 1, "symvc_out": 1}, *mats)
+    rows16 = _twostep_with(mb, {"symvc_rows": 16}, *mats)
+    for k in (2, 3):
+        np.testing.assert_array_equal(stream1[k], tiles[k])
+    for k in (0, 1):
+        np.testing.assert_allclose(stream1[k], tiles[k], rtol=1e-13, atol=0)
+        np.testing.assert_array_equal(stream1[k], stream2[k])
+        np.testing.assert_allclose(rows16[k], stream1[k], rtol=1e-13, atol=0)
+        np.testing.assert_array_equal(stream1[k], stream1[k].T)
