@@ -73,6 +73,7 @@ struct SymArgs {
     const double* s;      // pass 2/3: rowsum(Y)^(exponent), 0 -> 1
     double scale;         // pass 3: mean(X) / mean(C)
     const double* scale_p = nullptr;  // pass 3: the same from device memory (no host round trip)
+    const long long* ng_p = nullptr;  // streaming passes: the gap count on the device (gap form iff > 0)
 };
 
 // Per-tile vectors staged once in LDS: alpha, gap flag and s for the 64
@@ -136,7 +137,7 @@ __global__ __launch_bounds__(256) void k_symvc(const T* __restrict__ X, SymArgs 
     while (rem >= a.nT - I) { rem -= a.nT - I; ++I; }
     const long long J = I + rem;
     const long long I0 = I * kT, J0 = J * kT, N = a.N;
-    const bool has_gap = a.gap != nullptr;
+    const bool has_gap = a.gap != nullptr && (a.ng_p == nullptr || *a.ng_p > 0);
     if (threadIdx.x < kT) {
         const int r = threadIdx.x;
         const long long gi = I0 + r, gj = J0 + r;
@@ -234,7 +235,7 @@ __global__ __launch_bounds__(256) void k_symvc_out(const T* __restrict__ X, SymA
     while (rem >= a.nT - I) { rem -= a.nT - I; ++I; }
     const long long J = I + rem;
     const long long I0 = I * kT, J0 = J * kT, N = a.N;
-    const bool has_gap = a.gap != nullptr;
+    const bool has_gap = a.gap != nullptr && (a.ng_p == nullptr || *a.ng_p > 0);
     const bool diag_tile = I == J;
     const int c = threadIdx.x & (kT - 1);
     const int r0 = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: scalar row bases
@@ -337,8 +338,9 @@ __global__ __launch_bounds__(256) void k_slab_sum(const double* __restrict__ par
 
 // the mean rescale (raw_sum / N^2) / (sum C / N^2) on the device, the same
 // IEEE operations as on the host
-__global__ void k_symvc_scale(const double* __restrict__ tot, double raw_sum, double nn, double* __restrict__ scale) {
-    if (threadIdx.x == 0) *scale = (raw_sum / nn) / (*tot / nn);
+__global__ void k_symvc_scale(const double* __restrict__ tot, double raw_sum, const double* __restrict__ raw_p,
+                              double nn, double* __restrict__ scale) {
+    if (threadIdx.x == 0) *scale = ((raw_p ? *raw_p : raw_sum) / nn) / (*tot / nn);
 }
 
 // ---- passes 1-2 as row streams (round 4, default; hh_tune "symvc_stream") --
@@ -375,7 +377,8 @@ template <class T, int MODE>
 __global__ __launch_bounds__(256) void k_ts_gemv(const T* __restrict__ X, long long N,
                                                  const double* __restrict__ alpha, const double* __restrict__ rs,
                                                  int gr, double* __restrict__ part_c, double* __restrict__ part_r,
-                                                 const int* __restrict__ gpos, T* __restrict__ Xc, long long ng) {
+                                                 const int* __restrict__ gpos, T* __restrict__ Xc,
+                                                 const long long* __restrict__ ng_p) {
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const long long rc = blockIdx.x, q = (long long)blockIdx.y * 4 + w;
@@ -395,6 +398,7 @@ __global__ __launch_bounds__(256) void k_ts_gemv(const T* __restrict__ X, long l
         gcol[k] = (MODE == 1 && gpos && okc[k]) ? gpos[c] : -1;
     }
     const long long rend = std::min<long long>(r0 + gr, N);
+    const long long ng = (MODE == 1 && gpos) ? *ng_p : 0;  // Xc's row stride
     constexpr int kB = 4;  // rows per batch: 32 loads in flight per lane
 #pragma unroll 1
     for (long long i0 = r0; i0 < rend; i0 += kB) {
@@ -466,52 +470,58 @@ __global__ __launch_bounds__(256) void k_ts_gemv(const T* __restrict__ X, long l
 // with S_ab = Xc[a][b] / alpha_{G[a]}; (B, A) is read coalesced and
 // transposed through LDS.
 template <class T, int MODE>
-__global__ __launch_bounds__(256) void k_ts_gap(const T* __restrict__ Xc, long long ng, const int* __restrict__ glist,
-                                                const double* __restrict__ alpha, const double* __restrict__ sv,
-                                                double* __restrict__ gpart) {
+__global__ __launch_bounds__(256) void k_ts_gap(const T* __restrict__ Xc, const long long* __restrict__ ng_p,
+                                                const int* __restrict__ glist, const double* __restrict__ alpha,
+                                                const double* __restrict__ sv, double* __restrict__ gpart) {
     __shared__ T tt[kT][kT + 1];
     __shared__ double aA[kT], aB[kT], sA[kT], sB[kT];
     __shared__ double red[4][kT];
-    const long long A0 = (long long)blockIdx.x * kT, B0 = (long long)blockIdx.y * kT;
+    const long long ng = *ng_p, nbt = (ng + kT - 1) / kT;
     const int c = threadIdx.x & (kT - 1), r0 = threadIdx.x >> 6;
-    // clamped addresses, no select on loaded values (see k_symvc_out); a
-    // value from a clamped address is never used
-    const long long ca = A0 + c < ng ? A0 + c : ng - 1, cbb = B0 + c < ng ? B0 + c : ng - 1;
-    T xd[kT / 4];
+    // grid-stride over the nbt x nbt tiles (the gap count is known on the device only)
+    for (long long t = blockIdx.x; t < nbt * nbt; t += gridDim.x) {
+        const long long Ab = t / nbt, Bb = t % nbt;
+        const long long A0 = Ab * kT, B0 = Bb * kT;
+        // clamped addresses, no select on loaded values (see k_symvc_out); a
+        // value from a clamped address is never used
+        const long long ca = A0 + c < ng ? A0 + c : ng - 1, cbb = B0 + c < ng ? B0 + c : ng - 1;
+        T xd[kT / 4];
 #pragma unroll
-    for (int k = 0; k < kT / 4; ++k) {
-        const int r = r0 + 4 * k;
-        const long long ra = A0 + r < ng ? A0 + r : ng - 1, rb = B0 + r < ng ? B0 + r : ng - 1;
-        tt[c][r] = Xc[rb * ng + ca];  // tt[c][r] = Xc[B0 + r][A0 + c]
-        xd[k] = Xc[ra * ng + cbb];    // Xc[A0 + r][B0 + c]
-    }
-    if (threadIdx.x < kT) {
-        const int r = threadIdx.x;
-        const int ga = glist[A0 + r < ng ? A0 + r : ng - 1], gb = glist[B0 + r < ng ? B0 + r : ng - 1];
-        aA[r] = alpha[ga];
-        aB[r] = alpha[gb];
-        sA[r] = MODE == 2 ? sv[ga] : 1.0;
-        sB[r] = MODE == 2 ? sv[gb] : 1.0;
-    }
-    __syncthreads();
-    // thread: row a = A0 + r (r = r0 + 4 k), column b = B0 + c; reduce over c
-#pragma unroll
-    for (int k = 0; k < kT / 4; ++k) {
-        const int r = r0 + 4 * k;
-        const long long a = A0 + r, b = B0 + c;
-        double d = 0.0;
-        if (a < ng && b < ng && a != b) {
-            const double sab = (double)xd[k] / aA[r], sba = (double)tt[r][c] / aB[c];
-            d = fabs(sab - sba) / 2.0;
-            if (MODE == 2) d = d / (sB[c] * sA[r]);
+        for (int k = 0; k < kT / 4; ++k) {
+            const int r = r0 + 4 * k;
+            const long long ra = A0 + r < ng ? A0 + r : ng - 1, rb = B0 + r < ng ? B0 + r : ng - 1;
+            tt[c][r] = Xc[rb * ng + ca];  // tt[c][r] = Xc[B0 + r][A0 + c]
+            xd[k] = Xc[ra * ng + cbb];    // Xc[A0 + r][B0 + c]
         }
-        d = wave_sum(d);
-        if (c == 0) red[r0][k] = d;
-    }
-    __syncthreads();
-    if (threadIdx.x < kT) {
-        const int r = threadIdx.x;  // r = r0' + 4 k'
-        if (A0 + r < ng) gpart[blockIdx.y * ng + A0 + r] = red[r & 3][r >> 2];
+        if (threadIdx.x < kT) {
+            const int r = threadIdx.x;
+            const int ga = glist[A0 + r < ng ? A0 + r : ng - 1], gb = glist[B0 + r < ng ? B0 + r : ng - 1];
+            aA[r] = alpha[ga];
+            aB[r] = alpha[gb];
+            sA[r] = MODE == 2 ? sv[ga] : 1.0;
+            sB[r] = MODE == 2 ? sv[gb] : 1.0;
+        }
+        __syncthreads();
+        // thread: row a = A0 + r (r = r0 + 4 k), column b = B0 + c; reduce over c
+#pragma unroll
+        for (int k = 0; k < kT / 4; ++k) {
+            const int r = r0 + 4 * k;
+            const long long a = A0 + r, b = B0 + c;
+            double d = 0.0;
+            if (a < ng && b < ng && a != b) {
+                const double sab = (double)xd[k] / aA[r], sba = (double)tt[r][c] / aB[c];
+                d = fabs(sab - sba) / 2.0;
+                if (MODE == 2) d = d / (sB[c] * sA[r]);
+            }
+            d = wave_sum(d);
+            if (c == 0) red[r0][k] = d;
+        }
+        __syncthreads();
+        if (threadIdx.x < kT) {
+            const int r = threadIdx.x;  // r = r0' + 4 k'
+            if (A0 + r < ng) gpart[Bb * ng + A0 + r] = red[r & 3][r >> 2];
+        }
+        __syncthreads();
     }
 }
 
@@ -550,11 +560,12 @@ __global__ __launch_bounds__(1024) void k_ts_colsum(const double* __restrict__ p
 template <class T>
 __global__ void k_ts_rows(const T* __restrict__ X, long long N, long long ncb,
                           const double* __restrict__ ccol, const double* __restrict__ part_r,
-                          const double* __restrict__ alpha, const uint8_t* __restrict__ gap,
-                          const int* __restrict__ gpos, const double* __restrict__ gpart, long long ng,
-                          double exponent, double* __restrict__ sv, double* __restrict__ rsv) {
+                          const double* __restrict__ alpha, const int* __restrict__ gpos,
+                          const double* __restrict__ gpart, const long long* __restrict__ ng_p, double exponent,
+                          double* __restrict__ sv, double* __restrict__ rsv) {
     const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= N) return;
+    const long long ng = ng_p ? *ng_p : 0;  // gap form iff ng > 0 (Trans2symmetry :948)
     const double c = ccol[i];
     double rsum;
     if constexpr (std::is_integral_v<T>) {
@@ -569,9 +580,9 @@ __global__ void k_ts_rows(const T* __restrict__ X, long long N, long long ncb,
     const double ai = alpha[i];
     const double r = rsum / ai;
     double y;
-    if (gap) {
+    if (ng > 0) {
         y = (r + c) / 2.0;
-        if (gpos && gpos[i] >= 0) {  // the both-gap pairs' max - mean, in tile order
+        if (gpos[i] >= 0) {  // the both-gap pairs' max - mean, in tile order
             const long long a = gpos[i], nbt = (ng + kT - 1) / kT;
             double gc = 0.0;
             for (long long B = 0; B < nbt; ++B) gc += gpart[B * ng + a];
@@ -590,18 +601,18 @@ __global__ void k_ts_rows(const T* __restrict__ X, long long N, long long ncb,
 template <class T>
 __global__ __launch_bounds__(256) void k_ts_q(const T* __restrict__ X, long long N, long long ncb,
                                               const double* __restrict__ part_r, const double* __restrict__ alpha,
-                                              const double* __restrict__ sv, const uint8_t* __restrict__ gap,
-                                              const double* __restrict__ gpart2, long long ng,
-                                              double* __restrict__ part) {
+                                              const double* __restrict__ sv, const double* __restrict__ gpart2,
+                                              const long long* __restrict__ ng_p, double* __restrict__ part) {
     __shared__ double sh[16];
     const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    const long long ng = ng_p ? *ng_p : 0;
     double term = 0.0;
     if (i < N) {
         double u = 0.0;
         for (long long cb = 0; cb < ncb; ++cb) u += part_r[cb * N + i];
         const double ai = alpha[i], si = sv[i];
         const double q = u / (ai * si);
-        if (gap) {
+        if (ng > 0) {
             term = q;
             if (i < ng) {  // compact gap row i's both-gap share of sum(C)
                 const long long nbt = (ng + kT - 1) / kT;
@@ -624,16 +635,20 @@ struct SymvcWs {
     DBuf<double> part, sv, tot;
     DBuf<double> part_c, part_r, rsv, ccol, gpart1, gpart2;  // streaming passes
     DBuf<int> glist, gpos;
+    DBuf<long long> ngd;
     DBuf<char> xc;  // the compact both-gap matrix
     std::vector<int> hgl, hgp;  // host sources of glist / gpos (alive until the copies ran)
+    long long hng = 0;
 };
 
-// The gap rows (index order) and each row's position among them (-1: not a
-// gap), on the device, for the streaming passes' both-gap correction.
+// The gap rows (index order), each row's position among them (-1: not a
+// gap) and their count, on the device, for the streaming passes' both-gap
+// correction; ng_max bounds the count (sizes the compact matrix).
 struct GapIdx {
     const int* gpos = nullptr;
     const int* glist = nullptr;
-    long long ng = 0;
+    const long long* ng_p = nullptr;
+    long long ng_max = 0;
 };
 
 static void gap_index_host(const uint8_t* hgap, long long N, std::vector<int>& gl, std::vector<int>& gp) {
@@ -644,10 +659,14 @@ static void gap_index_host(const uint8_t* hgap, long long N, std::vector<int>& g
 }
 
 // Enqueues the chain without a host round trip (the rescale factor is
-// formed and read on the device); `ws` must outlive the kernels.
+// formed and read on the device); `ws` must outlive the kernels.  The
+// streaming passes take the gap form iff the device gap count is > 0; the
+// tile-pair passes (symvc_stream 0) iff dgap != nullptr.  raw_p: the mean
+// rescale's raw total on the device (else raw_sum).
 template <class T>
 static void symvc_enqueue(const T* dX, long long N, const double* dalpha, const uint8_t* dgap, GapIdx gi,
-                          double exponent, double raw_sum, double* dout, hipStream_t s, SymvcWs& ws) {
+                          double exponent, double raw_sum, const double* raw_p, double* dout, hipStream_t s,
+                          SymvcWs& ws) {
     const long long nT = (N + kT - 1) / kT;
     const long long npairs = nT * (nT + 1) / 2;
     HH_REQUIRE(npairs < (1LL << 31), "matrix too large");
@@ -664,44 +683,49 @@ static void symvc_enqueue(const T* dX, long long N, const double* dalpha, const 
         ws.rsv.alloc(N);
         ws.ccol.alloc(N);
         ws.part.alloc((size_t)nb);
-        const long long ng = dgap ? gi.ng : 0;
-        if (ng) {
-            ws.xc.alloc((size_t)(ng * ng) * sizeof(T));
-            const long long nbt = (ng + kT - 1) / kT;
-            ws.gpart1.alloc((size_t)(nbt * ng));
-            ws.gpart2.alloc((size_t)(nbt * ng));
+        const long long ngm = (dgap && gi.ng_p) ? gi.ng_max : 0;
+        const long long nbtm = (ngm + kT - 1) / kT;
+        if (ngm) {
+            ws.xc.alloc((size_t)(ngm * ngm) * sizeof(T));
+            ws.gpart1.alloc((size_t)(nbtm * ngm));
+            ws.gpart2.alloc((size_t)(nbtm * ngm));
         }
-        T* xc = ng ? (T*)ws.xc.p : nullptr;
-        const int* gpos = ng ? gi.gpos : nullptr;
-        const unsigned nbt = (unsigned)((ng + kT - 1) / kT);
+        T* xc = ngm ? (T*)ws.xc.p : nullptr;
+        const int* gpos = ngm ? gi.gpos : nullptr;
+        const long long* ng_p = ngm ? gi.ng_p : nullptr;
+        const unsigned ggrid = (unsigned)std::min<long long>(std::max<long long>(nbtm * nbtm, 1), 2048);
         const unsigned gcb = (unsigned)((N + kGB - 1) / kGB);
         {
             HH_KTIME("k_ts_gemv1", s);
             hipLaunchKernelGGL((k_ts_gemv<T, 1>), dim3((unsigned)nrc, gcb), dim3(256), 0, s, dX, N, dalpha,
-                               (const double*)nullptr, gr, ws.part_c.p, ws.part_r.p, gpos, xc, ng);
+                               (const double*)nullptr, gr, ws.part_c.p, ws.part_r.p, gpos, xc, ng_p);
         }
-        if (ng)
-            hipLaunchKernelGGL((k_ts_gap<T, 1>), dim3(nbt, nbt), dim3(256), 0, s, (const T*)xc, ng, gi.glist, dalpha,
+        if (ngm)
+            hipLaunchKernelGGL((k_ts_gap<T, 1>), dim3(ggrid), dim3(256), 0, s, (const T*)xc, ng_p, gi.glist, dalpha,
                                (const double*)nullptr, ws.gpart1.p);
         hipLaunchKernelGGL(k_ts_colsum, dim3((unsigned)((N + 63) / 64)), dim3(1024), 0, s, ws.part_c.p, N, nrc,
                            ws.ccol.p);
-        hipLaunchKernelGGL((k_ts_rows<T>), dim3((unsigned)nb), dim3(256), 0, s, dX, N, ncb, ws.ccol.p,
-                           ws.part_r.p, dalpha, dgap, gpos, ws.gpart1.p, ng, exponent, ws.sv.p, ws.rsv.p);
-        if (ng)
-            hipLaunchKernelGGL((k_ts_gap<T, 2>), dim3(nbt, nbt), dim3(256), 0, s, (const T*)xc, ng, gi.glist, dalpha,
+        hipLaunchKernelGGL((k_ts_rows<T>), dim3((unsigned)nb), dim3(256), 0, s, dX, N, ncb, ws.ccol.p, ws.part_r.p,
+                           dalpha, gpos, ws.gpart1.p, ng_p, exponent, ws.sv.p, ws.rsv.p);
+        if (ngm)
+            hipLaunchKernelGGL((k_ts_gap<T, 2>), dim3(ggrid), dim3(256), 0, s, (const T*)xc, ng_p, gi.glist, dalpha,
                                ws.sv.p, ws.gpart2.p);
         {
             HH_KTIME("k_ts_gemv2", s);
             hipLaunchKernelGGL((k_ts_gemv<T, 2>), dim3((unsigned)nrc, gcb), dim3(256), 0, s, dX, N, dalpha, ws.rsv.p,
-                               gr, ws.part_c.p, ws.part_r.p, (const int*)nullptr, (T*)nullptr, 0LL);
+                               gr, ws.part_c.p, ws.part_r.p, (const int*)nullptr, (T*)nullptr,
+                               (const long long*)nullptr);
         }
         hipLaunchKernelGGL((k_ts_q<T>), dim3((unsigned)nb), dim3(256), 0, s, dX, N, ncb, ws.part_r.p, dalpha, ws.sv.p,
-                           dgap, ws.gpart2.p, ng, ws.part.p);
+                           ws.gpart2.p, ng_p, ws.part.p);
         hipLaunchKernelGGL(k_slab_sum, dim3(1), dim3(256), 0, s, ws.part.p, nb, ws.tot.p);
-        hipLaunchKernelGGL(k_symvc_scale, dim3(1), dim3(64), 0, s, ws.tot.p, raw_sum, (double)N * (double)N,
+        hipLaunchKernelGGL(k_symvc_scale, dim3(1), dim3(64), 0, s, ws.tot.p, raw_sum, raw_p, (double)N * (double)N,
                            ws.tot.p + 1);
         a.s = ws.sv.p;
         a.scale_p = ws.tot.p + 1;
+        // pass 3's form: the device gap count (no gap array: the sum form)
+        if (!ng_p) a.gap = nullptr;
+        a.ng_p = ng_p;
         {
             HH_KTIME("k_symvc3", s);
             if (g_symvc_out)
@@ -725,8 +749,8 @@ static void symvc_enqueue(const T* dX, long long N, const double* dalpha, const 
         hipLaunchKernelGGL((k_symvc<T, 2>), dim3((unsigned)npairs), dim3(256), 0, s, dX, a, ws.part.p, nullptr);
     }
     hipLaunchKernelGGL(k_slab_sum, dim3(1), dim3(256), 0, s, ws.part.p, npairs, ws.tot.p);
-    hipLaunchKernelGGL(k_symvc_scale, dim3(1), dim3(64), 0, s, ws.tot.p, raw_sum, (double)N * (double)N,
-                       ws.tot.p + 1);
+    hipLaunchKernelGGL(k_symvc_scale, dim3(1), dim3(64), 0, s, ws.tot.p, raw_sum, (const double*)nullptr,
+                       (double)N * (double)N, ws.tot.p + 1);
     a.scale_p = ws.tot.p + 1;
     {
         HH_KTIME("k_symvc3", s);
@@ -737,21 +761,23 @@ static void symvc_enqueue(const T* dX, long long N, const double* dalpha, const 
 
 template <class T>
 static void symvc_run(const T* dX, long long N, const double* dalpha, const uint8_t* dgap, const uint8_t* hgap,
-                      double exponent,
-                      double raw_sum, double* dout, hipStream_t s) {
+                      double exponent, double raw_sum, double* dout, hipStream_t s) {
     SymvcWs ws;
     GapIdx gi;
     if (dgap && hgap) {
         gap_index_host(hgap, N, ws.hgl, ws.hgp);
-        gi.ng = (long long)ws.hgl.size();
-        if (gi.ng) {
+        ws.hng = (long long)ws.hgl.size();
+        if (ws.hng) {
             ws.gpos = to_device(ws.hgp, s);
             ws.glist = to_device(ws.hgl, s);
-            gi.gpos = ws.gpos.p;
-            gi.glist = ws.glist.p;
+            ws.ngd.alloc(1);
+            ws.ngd.upload(&ws.hng, 1, s);
+            gi = GapIdx{ws.gpos.p, ws.glist.p, ws.ngd.p, ws.hng};
+        } else {
+            dgap = nullptr;  // no gap rows: the sum form (Trans2symmetry :948)
         }
     }
-    symvc_enqueue(dX, N, dalpha, dgap, gi, exponent, raw_sum, dout, s, ws);
+    symvc_enqueue(dX, N, dalpha, dgap, gi, exponent, raw_sum, (const double*)nullptr, dout, s, ws);
     HIP_CHECK(hipStreamSynchronize(s));
 }
 
@@ -777,6 +803,308 @@ static double np_percentile(std::vector<double> v, double pct) {
     const double b = next == prev ? a : *std::min_element(v.begin() + prev + 1, v.end());
     const double d = b - a;
     return gamma >= 0.5 ? b - d * (1.0 - gamma) : a + d * gamma;
+}
+
+// ---- TwoStepCorrection's glue on the device (round 4; hh_tune "twostep_devglue") ----
+// Gap_defined, the SNP alpha and the raw totals from the row statistics
+// without a host round trip: the same doubles as the host glue (cov = 1 -
+// z / N, np.percentile's 'linear' order statistics found exactly by an
+// 8-bit radix select on the bit patterns of the non-negative values, the
+// same lerp), and the gap rows compacted in index order for the streaming
+// passes.
+struct SelLds {
+    unsigned hist[256];
+    unsigned long long prefix, minb;
+    long long k;
+    unsigned cnt;
+    int flag;
+};
+
+// k-th smallest (0-based) of the non-negative doubles x_i (i < n) with
+// take(i, x_i); every thread of the block calls it and gets the value.
+template <class Get>
+__device__ double block_kth(long long n, long long k, Get get, SelLds& L) {
+    __syncthreads();
+    if (threadIdx.x == 0) { L.prefix = 0; L.k = k; }
+    __syncthreads();
+    for (int shift = 56; shift >= 0; shift -= 8) {
+        for (int t = threadIdx.x; t < 256; t += blockDim.x) L.hist[t] = 0;
+        const unsigned long long pre = L.prefix;
+        const unsigned long long hm = shift == 56 ? 0ull : (~0ull << (shift + 8));
+        __syncthreads();
+        for (long long i = threadIdx.x; i < n; i += blockDim.x) {
+            double x;
+            if (!get(i, x)) continue;
+            const unsigned long long b = (unsigned long long)__double_as_longlong(x);
+            if ((b & hm) == (pre & hm)) atomicAdd(&L.hist[(b >> shift) & 255u], 1u);
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            long long acc = 0;
+            const long long kk = L.k;
+            int d = 0;
+            for (; d < 255; ++d) {
+                if (acc + (long long)L.hist[d] > kk) break;
+                acc += L.hist[d];
+            }
+            L.k = kk - acc;
+            L.prefix = pre | ((unsigned long long)d << shift);
+        }
+        __syncthreads();
+    }
+    return __longlong_as_double((long long)L.prefix);
+}
+
+// The same k-th smallest with the candidates' bit patterns held in
+// registers (kSelPer per thread; ~0 marks "not taken": a non-negative
+// double's top bit is 0, so it never matches a prefix), the digits the
+// candidates all share skipped (their min / max decide where the first
+// differing byte is), and the 256 bins scanned by one wave.
+constexpr int kSelPer = 16;  // N <= kSelPer * blockDim.x
+__device__ unsigned long long block_kth_regs(const unsigned long long (&b)[kSelPer], long long k,
+                                             unsigned long long lo, unsigned long long hi, SelLds& L) {
+    if (lo == hi) return lo;
+    const int hb = 63 - __clzll(lo ^ hi);
+    const int shift0 = (hb / 8) * 8;
+    __syncthreads();
+    if (threadIdx.x == 0) { L.prefix = shift0 == 56 ? 0ull : (lo & (~0ull << (shift0 + 8))); L.k = k; }
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    for (int shift = shift0; shift >= 0; shift -= 8) {
+        for (int t = threadIdx.x; t < 256; t += blockDim.x) L.hist[t] = 0;
+        const unsigned long long pre = L.prefix;
+        const unsigned long long hm = shift == 56 ? 0ull : (~0ull << (shift + 8));
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < kSelPer; ++u)
+            if (b[u] != ~0ull && (b[u] & hm) == (pre & hm)) atomicAdd(&L.hist[(b[u] >> shift) & 255u], 1u);
+        __syncthreads();
+        if (threadIdx.x < 64) {
+            const long long kk = L.k;
+            unsigned h[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) h[q] = L.hist[4 * lane + q];
+            long long own = (long long)h[0] + h[1] + h[2] + h[3], incl = own;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const long long y = __shfl_up(incl, o, 64);
+                if (lane >= o) incl += y;
+            }
+            const long long excl = incl - own;
+            if (excl <= kk && kk < incl) {
+                long long acc = excl;
+                int q = 0;
+                for (; q < 3; ++q) {
+                    if (acc + (long long)h[q] > kk) break;
+                    acc += h[q];
+                }
+                L.k = kk - acc;
+                L.prefix = pre | ((unsigned long long)(4 * lane + q) << shift);
+            }
+        }
+        __syncthreads();
+    }
+    return L.prefix;
+}
+
+// Block min / max of the taken bit patterns (every thread gets them).
+__device__ void block_minmax_bits(const unsigned long long (&b)[kSelPer], unsigned long long& lo,
+                                  unsigned long long& hi, SelLds& L) {
+    lo = ~0ull;
+    hi = 0;
+#pragma unroll
+    for (int u = 0; u < kSelPer; ++u)
+        if (b[u] != ~0ull) { lo = b[u] < lo ? b[u] : lo; hi = b[u] > hi ? b[u] : hi; }
+    __syncthreads();
+    if (threadIdx.x == 0) { L.minb = ~0ull; L.prefix = 0; }
+    __syncthreads();
+    atomicMin(&L.minb, lo);
+    atomicMax(&L.prefix, hi);
+    __syncthreads();
+    lo = L.minb;
+    hi = L.prefix;
+    __syncthreads();
+}
+
+// np.percentile(x[take], pct), 'linear' (the host np_percentile's steps);
+// nt = the number taken (> 0).  Register path when n fits kSelPer per thread.
+template <class Get>
+__device__ double block_percentile(long long n, long long nt, double pct, Get get, SelLds& L) {
+    const double q = pct / 100.0;
+    const double vi = (double)(nt - 1) * q;
+    long long prev = (long long)floor(vi), next = prev + 1;
+    if (vi >= (double)(nt - 1)) prev = next = nt - 1;
+    if (vi < 0) prev = next = 0;
+    const double gamma = vi - (vi >= (double)(nt - 1) ? -1.0 : (double)prev);
+    double a, b;
+    if (n <= (long long)kSelPer * blockDim.x) {
+        unsigned long long v[kSelPer];
+#pragma unroll
+        for (int u = 0; u < kSelPer; ++u) {
+            const long long i = threadIdx.x + (long long)u * blockDim.x;
+            double x = 0.0;
+            v[u] = (i < n && get(i, x)) ? (unsigned long long)__double_as_longlong(x) : ~0ull;
+        }
+        unsigned long long lo, hi;
+        block_minmax_bits(v, lo, hi, L);
+        const unsigned long long ab = block_kth_regs(v, prev, lo, hi, L);
+        a = __longlong_as_double((long long)ab);
+        b = a;
+        if (next != prev) {
+            unsigned c = 0;
+            unsigned long long mn = ~0ull;
+#pragma unroll
+            for (int u = 0; u < kSelPer; ++u)
+                if (v[u] != ~0ull) {
+                    if (v[u] <= ab) ++c;
+                    else mn = v[u] < mn ? v[u] : mn;
+                }
+            __syncthreads();
+            if (threadIdx.x == 0) { L.cnt = 0; L.minb = ~0ull; }
+            __syncthreads();
+            atomicAdd(&L.cnt, c);
+            atomicMin(&L.minb, mn);
+            __syncthreads();
+            b = (long long)L.cnt > next ? a : __longlong_as_double((long long)L.minb);
+            __syncthreads();
+        }
+    } else {
+        a = block_kth(n, prev, get, L);
+        b = a;
+        if (next != prev) {
+            // the next order statistic: a again if more than `next` values are <= a, else the smallest value > a
+            const unsigned long long ab = (unsigned long long)__double_as_longlong(a);
+            if (threadIdx.x == 0) { L.cnt = 0; L.minb = ~0ull; }
+            __syncthreads();
+            for (long long i = threadIdx.x; i < n; i += blockDim.x) {
+                double x;
+                if (!get(i, x)) continue;
+                const unsigned long long xb = (unsigned long long)__double_as_longlong(x);
+                if (xb <= ab) atomicAdd(&L.cnt, 1u);
+                else atomicMin(&L.minb, xb);
+            }
+            __syncthreads();
+            b = (long long)L.cnt > next ? a : __longlong_as_double((long long)L.minb);
+            __syncthreads();
+        }
+    }
+    const double d = b - a;
+    return gamma >= 0.5 ? b - d * (1.0 - gamma) : a + d * gamma;
+}
+
+// Gap_defined (:915-929) for MM (block 0) and PM (block 1) from their zero
+// counts, and the gap rows compacted (gpos: position or -1, glist, ng).
+// err bit 0: every coverage is zero (np.percentile of an empty array).
+__global__ __launch_bounds__(1024) void k_ts_gapdef(const long long* __restrict__ zeros, long long N,
+                                                    uint8_t* __restrict__ gap, int* __restrict__ gpos,
+                                                    int* __restrict__ glist, long long* __restrict__ ng,
+                                                    int* __restrict__ err) {
+    __shared__ SelLds L;
+    __shared__ int wtot[16];
+    const int m = blockIdx.x;
+    const long long* z = zeros + (1 + m) * N;
+    uint8_t* g = gap + m * N;
+    int* gp = gpos + m * N;
+    int* gl = glist + m * N;
+    auto cov_of = [&](long long i) { return 1.0 - ((double)z[i] / (double)N); };
+    auto get = [&](long long i, double& x) {
+        x = cov_of(i);
+        return x != 0.0;
+    };
+    if (threadIdx.x == 0) L.cnt = 0;
+    __syncthreads();
+    unsigned c = 0;
+    for (long long i = threadIdx.x; i < N; i += blockDim.x) c += cov_of(i) != 0.0;
+    atomicAdd(&L.cnt, c);
+    __syncthreads();
+    const long long nnz = L.cnt;
+    double th = 0.0;
+    if (nnz == 0) {
+        if (threadIdx.x == 0) atomicOr(err, 1);
+    } else {
+        th = block_percentile(N, nnz, 25.0, get, L);
+        if (th > 0.2) th = 0.2;
+    }
+    // flags and the ordered compaction
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    long long base = 0;
+    for (long long i0 = 0; i0 < N; i0 += blockDim.x) {
+        const long long i = i0 + threadIdx.x;
+        const bool f = i < N && cov_of(i) < th;
+        if (i < N) g[i] = f;
+        const unsigned long long bm = __ballot(f);
+        if (lane == 0) wtot[w] = __popcll(bm);
+        __syncthreads();
+        long long before = 0, tot = 0;
+        for (int k = 0; k < nw; ++k) {
+            if (k < w) before += wtot[k];
+            tot += wtot[k];
+        }
+        if (i < N) {
+            const long long pos = base + before + __popcll(bm & ((1ull << lane) - 1ull));
+            gp[i] = f ? (int)pos : -1;
+            if (f) gl[pos] = (int)i;
+        }
+        base += tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) ng[m] = base;
+}
+
+// alpha (:989-1005) over the union of MM's and PM's non-gap bins, and the
+// exact raw totals of MM and PM.  err bit 1: every bin is a gap.
+__global__ __launch_bounds__(1024) void k_ts_alpha(const double* __restrict__ sum, const uint8_t* __restrict__ gap,
+                                                   long long N, double* __restrict__ alpha, double* __restrict__ raw,
+                                                   int* __restrict__ err) {
+    __shared__ SelLds L;
+    __shared__ double wmx[16];
+    __shared__ long long wr[2][16];
+    const double *sT = sum, *sM = sum + N, *sP = sum + 2 * N;
+    const uint8_t *gm = gap, *gp = gap + N;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    double mx = -HUGE_VAL;
+    long long t0 = 0, t1 = 0;
+    unsigned nu = 0;
+    for (long long i = threadIdx.x; i < N; i += blockDim.x) {
+        const double a = (sM[i] + sP[i]) / (sT[i] + 1.0);
+        alpha[i] = a;
+        if (!gm[i] || !gp[i]) { mx = fmax(mx, a); ++nu; }
+        t0 += (long long)sM[i];
+        t1 += (long long)sP[i];
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o, 64));
+    t0 = wave_sum_ll(t0);
+    t1 = wave_sum_ll(t1);
+    if (threadIdx.x == 0) L.cnt = 0;
+    __syncthreads();
+    atomicAdd(&L.cnt, nu);
+    if (lane == 0) { wmx[w] = mx; wr[0][w] = t0; wr[1][w] = t1; }
+    __syncthreads();
+    mx = -HUGE_VAL;
+    long long r0 = 0, r1 = 0;
+    for (int k = 0; k < nw; ++k) { mx = fmax(mx, wmx[k]); r0 += wr[0][k]; r1 += wr[1][k]; }
+    const long long nng = L.cnt;
+    if (threadIdx.x == 0) {
+        raw[0] = (double)r0;
+        raw[1] = (double)r1;
+        if (nng == 0) atomicOr(err, 2);
+    }
+    if (nng == 0) return;  // block-uniform
+    for (long long i = threadIdx.x; i < N; i += blockDim.x) {
+        double a = alpha[i] / mx;
+        if (a == 0.0) a = 1.0;
+        alpha[i] = a;
+    }
+    __syncthreads();
+    auto get = [&](long long i, double& x) {
+        x = alpha[i];
+        return !gm[i] || !gp[i];
+    };
+    const double th = block_percentile(N, nng, 20.0, get, L);
+    __syncthreads();
+    for (long long i = threadIdx.x; i < N; i += blockDim.x)
+        if (alpha[i] < th) alpha[i] = th;
 }
 
 // Per-thread pinned host staging buffers (slot 0: downloads, 1: uploads),
@@ -1022,10 +1350,43 @@ int hh_twostep(const int64_t* TM, const int64_t* MM, const int64_t* PM, int64_t 
                                (const long long*)nullptr, (const long long*)nullptr, dsum.p + k * N, dz.p + k * N);
         }
         HIP_CHECK(hipGetLastError());
+        PinnedStage& st = pinned_stage();
+        if (g_symvc_stream && g_twostep_devglue) {
+            // the glue on the device: no host round trip between the row
+            // statistics and the corrections (one synchronisation at the end)
+            DBuf<uint8_t> dgf((size_t)2 * N);
+            DBuf<int> dgpos((size_t)2 * N), dglist((size_t)2 * N);
+            DBuf<long long> dng(2);
+            DBuf<double> dA(N), draw(2);
+            DBuf<int> derr(1);
+            HIP_CHECK(hipMemsetAsync(derr.p, 0, sizeof(int), s));
+            hipLaunchKernelGGL(k_ts_gapdef, dim3(2), dim3(1024), 0, s, (const long long*)dz.p, (long long)N, dgf.p,
+                               dgpos.p, dglist.p, dng.p, derr.p);
+            hipLaunchKernelGGL(k_ts_alpha, dim3(1), dim3(1024), 0, s, (const double*)dsum.p, (const uint8_t*)dgf.p,
+                               (long long)N, dA.p, draw.p, derr.p);
+            HIP_CHECK(hipGetLastError());
+            SymvcWs wm, wp;
+            const GapIdx gim{dgpos.p, dglist.p, dng.p, N}, gip{dgpos.p + N, dglist.p + N, dng.p + 1, N};
+            double* out_m = on_device ? nor_mm : (double*)buf[0].p;
+            symvc_enqueue(d[1], N, dA.p, dgf.p, gim, 2.0 / 3.0, 0.0, draw.p, out_m, s, wm);
+            if (!on_device) HIP_CHECK(hipMemcpyAsync(nor_mm, out_m, cnt * 8, hipMemcpyDeviceToHost, s));
+            double* out_p = on_device ? nor_pm : (double*)buf[1].p;
+            symvc_enqueue(d[2], N, dA.p, dgf.p + N, gip, 2.0 / 3.0, 0.0, draw.p + 1, out_p, s, wp);
+            if (!on_device) HIP_CHECK(hipMemcpyAsync(nor_pm, out_p, cnt * 8, hipMemcpyDeviceToHost, s));
+            char* dl = (char*)st.get(0, (size_t)2 * N + 16);
+            dgf.download((uint8_t*)dl, (size_t)2 * N, s);
+            derr.download((int*)(dl + (((size_t)2 * N + 7) & ~(size_t)7)), 1, s);
+            HIP_CHECK(hipStreamSynchronize(s));
+            const int e = *(int*)(dl + (((size_t)2 * N + 7) & ~(size_t)7));
+            HH_REQUIRE(!(e & 1), "percentile of an empty array");
+            HH_REQUIRE(!(e & 2), "every bin is a gap");
+            std::memcpy(gap_m, dl, (size_t)N);
+            std::memcpy(gap_p, dl + N, (size_t)N);
+            return;
+        }
         // row statistics down and the per-call vectors up through pinned
         // staging (DMA; pageable copies cost a staging pass each), the
         // vectors in one packed upload
-        PinnedStage& st = pinned_stage();
         const size_t dl_bytes = (size_t)3 * N * (sizeof(double) + sizeof(long long));
         char* dl = (char*)st.get(0, dl_bytes);
         double* sum = (double*)dl;
@@ -1062,13 +1423,15 @@ int hh_twostep(const int64_t* TM, const int64_t* MM, const int64_t* PM, int64_t 
             for (long long i = 0; i < N; ++i) t += (long long)sum[(k + 1) * N + i];
             raw[k] = (double)t;
         }
-        // packed upload: alpha | gpos_m | glist_m | gpos_p | glist_p | gap_m | gap_p (16-B aligned parts)
+        // packed upload: ng_m, ng_p | alpha | gpos_m | glist_m | gpos_p | glist_p | gap_m | gap_p (16-B aligned)
         auto al = [](size_t b) { return (b + 15) & ~(size_t)15; };
-        const size_t o_gpm = al((size_t)N * 8), o_glm = o_gpm + al((size_t)N * 4), o_gpp = o_glm + al(glm.size() * 4 + 4),
-                     o_glp = o_gpp + al((size_t)N * 4), o_gm = o_glp + al(glp.size() * 4 + 4), o_gp = o_gm + al((size_t)N),
-                     up_bytes = o_gp + al((size_t)N);
+        const size_t o_a = 16, o_gpm = o_a + al((size_t)N * 8), o_glm = o_gpm + al((size_t)N * 4),
+                     o_gpp = o_glm + al(glm.size() * 4 + 4), o_glp = o_gpp + al((size_t)N * 4),
+                     o_gm = o_glp + al(glp.size() * 4 + 4), o_gp = o_gm + al((size_t)N), up_bytes = o_gp + al((size_t)N);
         char* up = (char*)st.get(1, up_bytes);
-        std::memcpy(up, alpha.data(), (size_t)N * 8);
+        ((long long*)up)[0] = (long long)glm.size();
+        ((long long*)up)[1] = (long long)glp.size();
+        std::memcpy(up + o_a, alpha.data(), (size_t)N * 8);
         std::memcpy(up + o_gpm, gpm.data(), (size_t)N * 4);
         if (any_m) std::memcpy(up + o_glm, glm.data(), glm.size() * 4);
         std::memcpy(up + o_gpp, gpp.data(), (size_t)N * 4);
@@ -1077,19 +1440,20 @@ int hh_twostep(const int64_t* TM, const int64_t* MM, const int64_t* PM, int64_t 
         std::memcpy(up + o_gp, gp.data(), (size_t)N);
         DBuf<char> dup(up_bytes);
         dup.upload(up, up_bytes, s);
-        const double* dA = (const double*)dup.p;
+        const double* dA = (const double*)(dup.p + o_a);
         const uint8_t *dgm = (const uint8_t*)(dup.p + o_gm), *dgp = (const uint8_t*)(dup.p + o_gp);
-        GapIdx gim{(const int*)(dup.p + o_gpm), (const int*)(dup.p + o_glm), (long long)glm.size()};
-        GapIdx gip{(const int*)(dup.p + o_gpp), (const int*)(dup.p + o_glp), (long long)glp.size()};
+        const long long* dngs = (const long long*)dup.p;
+        GapIdx gim{(const int*)(dup.p + o_gpm), (const int*)(dup.p + o_glm), dngs, (long long)glm.size()};
+        GapIdx gip{(const int*)(dup.p + o_gpp), (const int*)(dup.p + o_glp), dngs + 1, (long long)glp.size()};
         // outputs: on the host path TM's buffer holds Nor_MM, then MM's holds
         // Nor_PM; both chains enqueued back to back, one synchronisation
         SymvcWs wm, wp;
         double* out_m = on_device ? nor_mm : (double*)buf[0].p;
-        symvc_enqueue(d[1], N, dA, any_m ? dgm : nullptr, gim, 2.0 / 3.0, raw[0], out_m, s, wm);
+        symvc_enqueue(d[1], N, dA, any_m ? dgm : nullptr, gim, 2.0 / 3.0, raw[0], (const double*)nullptr, out_m, s, wm);
         if (!on_device) HIP_CHECK(hipMemcpyAsync(nor_mm, out_m, cnt * 8, hipMemcpyDeviceToHost, s));
         double* out_p = on_device ? nor_pm : (double*)buf[1].p;
         // (MM's buffer, read by the first chain, is written by the second: stream order)
-        symvc_enqueue(d[2], N, dA, any_p ? dgp : nullptr, gip, 2.0 / 3.0, raw[1], out_p, s, wp);
+        symvc_enqueue(d[2], N, dA, any_p ? dgp : nullptr, gip, 2.0 / 3.0, raw[1], (const double*)nullptr, out_p, s, wp);
         if (!on_device) HIP_CHECK(hipMemcpyAsync(nor_pm, out_p, cnt * 8, hipMemcpyDeviceToHost, s));
         HIP_CHECK(hipStreamSynchronize(s));
         std::copy(gm.begin(), gm.end(), gap_m);

@@ -2544,6 +2544,8 @@ int hh_tune(const char* key, int64_t value) {
             g_symvc_rows = (int)value;
         } else if (k == "symvc_out") {
             g_symvc_out = value ? 1 : 0;
+        } else if (k == "twostep_devglue") {
+            g_twostep_devglue = value ? 1 : 0;
         } else if (k == "symvc_stream") {
             g_symvc_stream = value ? 1 : 0;
         } else if (k == "ortho_abort_test") {

@@ -175,6 +175,7 @@ def _twostep_with(mb, tune, *mats):
         _lib.call("hh_tune", b"symvc_stream", 1)
         _lib.call("hh_tune", b"symvc_out", 1)
         _lib.call("hh_tune", b"symvc_rows", 32)
+        _lib.call("hh_tune", b"twostep_devglue", 1)
 
 
 @pytest.mark.parametrize("case", ["gaps_1000", "nogap_golden", "ragged_777"])
@@ -182,7 +183,8 @@ def test_twostep_streaming_passes_match_tile_pairs(mb, golden, case):
     """Passes 1-2 as row streams (k_ts_gemv + the both-gap correction) give
     the tile-pair passes' result up to summation rounding, with the gap and
     the no-gap (sum) forms; the one-LDS-tile pass 3 is bitwise the two-tile
-    one; the rows-per-block knob does not change the result beyond rounding."""
+    one; the rows-per-block knob does not change the result beyond rounding;
+    the gap / alpha glue on the device gives the host glue's bits."""
     if case == "nogap_golden":
         g = golden("twostep_nogapM_n80")
         mats = (g["TM"], g["MM"], g["PM"])
@@ -195,6 +197,9 @@ def test_twostep_streaming_passes_match_tile_pairs(mb, golden, case):
     stream2 = _twostep_with(mb, {"symvc_stream": 1, "symvc_out": 0}, *mats)
     stream1 = _twostep_with(mb, {"symvc_stream": 1, "symvc_out": 1}, *mats)
     rows16 = _twostep_with(mb, {"symvc_rows": 16}, *mats)
+    hostglue = _twostep_with(mb, {"twostep_devglue": 0}, *mats)
+    for k in range(4):  # the device glue (gaps, alpha, raw totals) is bitwise the host glue
+        np.testing.assert_array_equal(stream1[k], hostglue[k])
     for k in (2, 3):
         np.testing.assert_array_equal(stream1[k], tiles[k])
     for k in (0, 1):
@@ -202,3 +207,17 @@ def test_twostep_streaming_passes_match_tile_pairs(mb, golden, case):
         np.testing.assert_array_equal(stream1[k], stream2[k])
         np.testing.assert_allclose(rows16[k], stream1[k], rtol=1e-13, atol=0)
         np.testing.assert_array_equal(stream1[k], stream1[k].T)
+
+
+@pytest.mark.parametrize("devglue", [1, 0])
+def test_twostep_all_zero_haplotype_raises(mb, devglue):
+    """An all-zero haplotype matrix has no nonzero coverage: NumPy's
+    percentile of an empty array raises in the reference (Gap_defined :922);
+    both glue paths raise instead of returning garbage."""
+    from hichap_master_amd import _lib
+    N = 200
+    rng = np.random.default_rng(5)
+    TM = synth.dense_chrom(N, rng, A=60.0)
+    Z = np.zeros_like(TM)
+    with pytest.raises(_lib.HipLibraryError, match="percentile of an empty array"):
+        _twostep_with(mb, {"twostep_devglue": devglue}, TM, Z, Z)
