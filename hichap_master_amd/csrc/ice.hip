@@ -810,8 +810,16 @@ __global__ __launch_bounds__(NW * 64, NW > 8 ? 3 : 2) void k_sweep_flatw(TileDev
             k = __builtin_amdgcn_readfirstlane(__shfl(k, 0, 64));
             if (k >= nk) return false;
             const FlatDesc d = desc[k];
+            // the tile's row groups' active flags, one per lane (one round
+            // trip; a loop over the groups compiled to one load -> wait each)
             bool on = false;
-            for (int g = d.glo; g <= d.ghi; ++g) on |= act[g] != 0;
+            const int ngr = d.ghi - d.glo + 1;
+            if (ngr <= 64) {
+                const uint8_t a = act[d.glo + (lane < ngr ? lane : ngr - 1)];
+                on = __ballot((a != 0) & (lane < ngr)) != 0;
+            } else {
+                for (int g = d.glo; g <= d.ghi; ++g) on |= act[g] != 0;
+            }
             if (!on) continue;  // a converged group's rows: k_marg never reads them
             x = Tw{d.slot, d.frec, (int)d.nr, (int)d.nfn, (int)d.nfw, d.qbn, d.qbw,
                    reinterpret_cast<const uint4*>(T.payn + d.entn), reinterpret_cast<const uint4*>(T.pay + d.ent)};
@@ -831,14 +839,35 @@ __global__ __launch_bounds__(NW * 64, NW > 8 ? 3 : 2) void k_sweep_flatw(TileDev
         // then 0, 1, 2, ...: the dense trans tiles): ~1.1 of 4.1 KB per tile
         const bool idn = cur.nfn == cur.nr;
         {
+            // the four uint16 ranges [h0, h1) of the record the walk reads,
+            // each at most 65 uint4 (kR = 512): two uint4 per lane.  All
+            // eight loads are issued before the first LDS store (a load loop
+            // per range compiled to load -> vmcnt(0) -> store, four to eight
+            // round trips per tile); a lane past a range's end re-reads the
+            // range's first uint4 (the same line: no extra bytes)
+            // and stores its copy back to the same LDS slot (no branch around
+            // the stores either, which would bring the waits back)
+            static_assert((kR + 1 + 7) / 8 + 1 <= 2 * 64, "record range > 2 uint4 per lane");
             uint4* r4 = reinterpret_cast<uint4*>(rec);
-            auto stage = [&](int h0, int h1) {  // uint16 range [h0, h1) of the record
-                for (int q = h0 / 8 + lane; q < (h1 + 7) / 8; q += 64) r4[q] = rg[q];
-            };
-            stage(0, cur.nfn + 1);
-            stage(kR + 1, kR + 1 + cur.nfw + 1);
-            if (!idn) stage(2 * (kR + 1), 2 * (kR + 1) + cur.nfn);
-            stage(2 * (kR + 1) + kR, 2 * (kR + 1) + kR + cur.nfw);
+            const int h0[4] = {0, kR + 1, 2 * (kR + 1), 2 * (kR + 1) + kR};
+            const int h1[4] = {cur.nfn + 1, kR + 1 + cur.nfw + 1, idn ? 2 * (kR + 1) : 2 * (kR + 1) + cur.nfn,
+                               2 * (kR + 1) + kR + cur.nfw};
+            uint4 tq[4][2];
+            int qs[4][2];
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int q0 = h0[g] / 8, q1 = (h1[g] + 7) / 8;
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int q = q0 + lane + 64 * h;
+                    qs[g][h] = q < q1 ? q : q0;
+                    tq[g][h] = rg[qs[g][h]];
+                }
+            }
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+#pragma unroll
+                for (int h = 0; h < 2; ++h) r4[qs[g][h]] = tq[g][h];
         }
         wave_lds_sync();
         if (PIPE) flat_seg_c_pipe<U, ABL, 8>(cur.payn4, v, 0u, cur.qbn, 0, cur.nfn, fstn, cur.nfn, bl, acc, lane);
