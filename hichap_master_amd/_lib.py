@@ -141,6 +141,7 @@ SIGNATURES = {
     "hh_gw_create_device": (C.c_int, [P, P, P, I64, P, P, P, I64, I64, P, I32, P, C.POINTER(P)]),
     "hh_gw_free": (C.c_int, [P]),
     "hh_gw_stats": (C.c_int, [P, P, P, P, PI64]),
+    "hh_gw_alpha": (C.c_int, [P, P, P]),
     "hh_gw_correct": (C.c_int, [P, P, F64, PI64, P]),
     "hh_gw_correct_count": (C.c_int, [P, P, F64, PI64, P]),
     "hh_gw_correct_write": (C.c_int, [P, P, P, P, P]),

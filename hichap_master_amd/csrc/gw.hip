@@ -25,8 +25,13 @@
 // Every sum is a fixed-order reduction (integer ones exact): deterministic.
 #include <algorithm>
 #include <cmath>
+#include <limits>
 #include <memory>
 #include <numeric>
+#include <thread>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <type_traits>
 
 #include "ice_internal.hpp"
@@ -547,6 +552,10 @@ struct hh_gw {
     int ib = 1;
     std::vector<unsigned long long> t_rowsum, t_nnz_row, h_blocksum;
     unsigned long long h_total = 0;
+    // the SNP alpha per chromosome (bin order), computed on the host while
+    // the GPU builds the column lists (hh_gw_alpha); ok 0: NumPy's own path
+    std::vector<double> alpha;
+    std::vector<int32_t> alpha_ok;
     // result (upper-triangle table of Nor)
     DBuf<int32_t> ob1, ob2;
     DBuf<double> ov;
@@ -557,6 +566,18 @@ namespace {
 
 const char* kErrWhat[5] = {"bin id out of range", "bin1 > bin2 in the traditional table (not upper triangle)",
                            "cells not sorted by (row, col)", "duplicate cell", "counts must be non-negative integers < 2^32"};
+
+// HH_GW_TIMING: host timestamps at gw_create's synchronisation points (stderr)
+struct GwClock {
+    bool on = std::getenv("HH_GW_TIMING") != nullptr;
+    std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+    void lap(const char* what) {
+        if (!on) return;
+        const auto u = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[gw_create] %s: %.2f ms\n", what, std::chrono::duration<double, std::milli>(u - t).count());
+        t = u;
+    }
+};
 
 // Validate a table (range, order, uniqueness, counts); COPY: convert it into
 // int32 / uint32 device arrays (host or int64 tables), else it is used in
@@ -569,19 +590,29 @@ unsigned gw_check(const Id* r, const Id* c, const Cnt* v, int64_t nnz, int64_t n
         Cc.alloc(std::max<int64_t>(nnz, 1));
         V.alloc(std::max<int64_t>(nnz, 1));
     }
+    GwClock ck;
     DBuf<unsigned long long> err(5);
     DBuf<unsigned> vmax(1);
+    ck.lap("check: alloc");
     vmax.zero(s);
     HIP_CHECK(hipMemsetAsync(err.p, 0xff, 5 * sizeof(unsigned long long), s));
     if (nnz > 0)
         hipLaunchKernelGGL((k_gw_check<Id, Cnt, COPY>), dim3((unsigned)std::max<long long>(1, std::min<long long>((nnz + 255) / 256, 16384))), dim3(256), 0, s, r, c, v,
                            (long long)nnz, (long long)nb, upper, R.p, Cc.p, V.p, err.p, vmax.p);
     HIP_CHECK(hipGetLastError());
+    ck.lap("check: launch");
+    // into pinned memory: a pageable download here measured ~18 ms of host
+    // wait beyond the kernel (HH_GW_TIMING)
     unsigned long long he[5];
     unsigned mx = 0;
-    err.download(he, 5, s);
-    vmax.download(&mx, 1, s);
+    char* pin = (char*)pinned_stage().get(0, 64);
+    err.download((unsigned long long*)pin, 5, s);
+    vmax.download((unsigned*)(pin + 48), 1, s);
+    ck.lap("check: downloads enqueued");
     HIP_CHECK(hipStreamSynchronize(s));
+    std::memcpy(he, pin, sizeof(he));
+    std::memcpy(&mx, pin + 48, sizeof(mx));
+    ck.lap("check: sync");
     int code = -1;
     unsigned long long at = ~0ull;
     for (int q = 0; q < 5; ++q)
@@ -590,6 +621,63 @@ unsigned gw_check(const Id* r, const Id* c, const Cnt* v, int64_t nnz, int64_t n
     return mx;
 }
 
+// GenomeWideMatrixCorrection's alpha step (:878-893) per chromosome, the
+// reference's NumPy expressions on the exact integer statistics, as
+// matrixBuilding.GenomeWideMatrixCorrectionSparse's glue computes them:
+// cov = 1 - zeros / L (Coverage_M :904), gap = cov < 0.1
+// (Gap_definedLowRes :742-753), alpha = (M + P) / (T + 1) / max over the
+// non-gap bins, 0 -> 1, floored at np.percentile(non-gap, 20).  A chromosome
+// whose max is not a positive finite number (NumPy's NaN / inf paths) or
+// that has no non-gap bin (np.max of an empty array raises) is left to the
+// NumPy path (ok 0).
+static void gw_alpha_host(hh_gw& G, const std::vector<int64_t>& off) {
+    const int64_t n = G.n;
+    const int nc = (int)off.size() - 1;
+    G.alpha.assign(n, 0.0);
+    G.alpha_ok.assign(nc, 0);
+    std::vector<double> ng;
+    std::vector<uint8_t> gap;
+    for (int c = 0; c < nc; ++c) {
+        const int64_t s = off[c], e = off[c + 1], L = e - s;
+        if (L <= 0) continue;
+        double mx = -std::numeric_limits<double>::infinity();
+        bool any = false;
+        gap.assign(L, 0);
+        for (int64_t i = s; i < e; ++i) {
+            const int64_t zeros = L - (int64_t)G.t_nnz_row[i];
+            const double cov = 1.0 - ((double)zeros / (double)L);
+            gap[i - s] = cov < 0.1;
+            const int64_t hp = (int64_t)G.h_blocksum[i] + (int64_t)G.h_blocksum[n + i];
+            const double a = (double)hp / (double)((int64_t)G.t_rowsum[i] + 1);
+            G.alpha[i] = a;
+            if (!gap[i - s]) {
+                mx = std::max(mx, a);
+                any = true;
+            }
+        }
+        if (!any || !(mx > 0.0) || !std::isfinite(mx)) continue;
+        ng.clear();
+        for (int64_t i = s; i < e; ++i) {
+            double a = G.alpha[i] / mx;
+            if (a == 0.0) a = 1.0;
+            G.alpha[i] = a;
+            if (!gap[i - s]) ng.push_back(a);
+        }
+        const double th = np_percentile(ng, 20.0);
+        for (int64_t i = s; i < e; ++i)
+            if (G.alpha[i] < th) G.alpha[i] = th;
+        G.alpha_ok[c] = 1;
+    }
+}
+
+// joins the alpha thread on every path out of gw_create
+struct ThreadJoin {
+    std::thread t;
+    ~ThreadJoin() {
+        if (t.joinable()) t.join();
+    }
+};
+
 template <class Id, class Cnt>
 void gw_create(hh_gw& G, const Id* t1, const Id* t2, const Cnt* tv, int64_t t_nnz, const Id* hr, const Id* hc,
                const Cnt* hv, int64_t h_nnz, int64_t n, const int64_t* chrom_offsets, int32_t n_chroms,
@@ -597,6 +685,13 @@ void gw_create(hh_gw& G, const Id* t1, const Id* t2, const Cnt* tv, int64_t t_nn
     HH_REQUIRE(n > 0 && n_chroms > 0 && chrom_offsets && t_nnz >= 0 && h_nnz >= 0, "bad arguments");
     HH_REQUIRE(chrom_offsets[0] == 0 && chrom_offsets[n_chroms] == n, "chrom_offsets must span [0, n]");
     HH_REQUIRE(2 * n < kMaxBins, "too many bins");
+    GwClock clk;
+    if (clk.on) {
+        HIP_CHECK(hipStreamSynchronize(s));
+        clk.lap("stream idle at entry");
+        HIP_CHECK(hipDeviceSynchronize());
+        clk.lap("device idle at entry");
+    }
     G.n = n;
     G.N2 = 2 * n;
     G.t_nnz = t_nnz;
@@ -613,8 +708,13 @@ void gw_create(hh_gw& G, const Id* t1, const Id* t2, const Cnt* tv, int64_t t_nn
         }
     }
     constexpr bool COPY = !(std::is_same<Id, int32_t>::value && std::is_same<Cnt, int32_t>::value);
-    gw_check<Id, Cnt, COPY>(t1, t2, tv, t_nnz, n, 1, G.tA, G.tB, G.tV, "traditional table", s);
-    const unsigned hmax = gw_check<Id, Cnt, COPY>(hr, hc, hv, h_nnz, 2 * n, 0, G.R, G.C, G.V, "haplotype cells", s);
+    clk.lap("setup");
+    unsigned hmax = 0;
+    {
+        HH_KTIME("gw_check", s);
+        gw_check<Id, Cnt, COPY>(t1, t2, tv, t_nnz, n, 1, G.tA, G.tB, G.tV, "traditional table", s);
+        hmax = gw_check<Id, Cnt, COPY>(hr, hc, hv, h_nnz, 2 * n, 0, G.R, G.C, G.V, "haplotype cells", s);
+    }
     if (COPY) {
         G.tAp = G.tA.p, G.tBp = G.tB.p, G.tVp = G.tV.p, G.Rp = G.R.p, G.Cp = G.C.p, G.Vp = G.V.p;
     } else {  // validated int32 device tables, read in place (counts >= 0: as uint32)
@@ -623,7 +723,19 @@ void gw_create(hh_gw& G, const Id* t1, const Id* t2, const Cnt* tv, int64_t t_nn
         G.Rp = reinterpret_cast<const int32_t*>(hr), G.Cp = reinterpret_cast<const int32_t*>(hc);
         G.Vp = reinterpret_cast<const uint32_t*>(hv);
     }
-    DBuf<int2> dch = to_device(chrom_bd, s), dblk = to_device(block_bd, s);
+    clk.lap("checks");
+    // host <-> device transfers of gw_create / gw_prepare go through the
+    // per-thread pinned staging buffers: pageable copies measured 20+ ms
+    // each here (the 4.9 MB alpha upload: 24 ms for ~0.1 ms of DMA)
+    DBuf<int2> dch(n), dblk(2 * n);
+    {
+        const size_t b1 = (size_t)n * sizeof(int2), b2 = (size_t)2 * n * sizeof(int2);
+        char* up = (char*)pinned_stage().get(1, b1 + b2);
+        std::memcpy(up, chrom_bd.data(), b1);
+        std::memcpy(up + b1, block_bd.data(), b2);
+        dch.upload((const int2*)up, n, s);
+        dblk.upload((const int2*)(up + b1), 2 * n, s);
+    }
     DBuf<unsigned long long> trs(n), tnz(n), hbs(2 * n), htot(1);
     trs.zero(s);
     tnz.zero(s);
@@ -634,6 +746,7 @@ void gw_create(hh_gw& G, const Id* t1, const Id* t2, const Cnt* tv, int64_t t_nn
     DBuf<unsigned long long> tpk(tpack ? n : 1), ttot(1);
     if (tpack) tpk.zero(s);
     ttot.zero(s);
+    HH_KTIME("gw_stats_to_end", s);  // (from the statistics to the end of create)
     if (t_nnz > 0) {
         if (tpack) {
             const long long nb = std::min<long long>(8192, (t_nnz + 65535) / 65536);
@@ -652,32 +765,57 @@ void gw_create(hh_gw& G, const Id* t1, const Id* t2, const Cnt* tv, int64_t t_nn
     G.t_rowsum.resize(n);
     G.t_nnz_row.resize(n);
     G.h_blocksum.resize(2 * n);
-    trs.download(G.t_rowsum.data(), n, s);
-    tnz.download(G.t_nnz_row.data(), n, s);
-    hbs.download(G.h_blocksum.data(), 2 * n, s);
-    htot.download(&G.h_total, 1, s);
-    if (tpack && t_nnz > 0) {
-        unsigned long long tt = 0;
-        ttot.download(&tt, 1, s);
-        std::vector<unsigned long long> pk(n);
-        tpk.download(pk.data(), n, s);
+    {
+        // pinned layout: t_rowsum n | t_nnz n | h_blocksum 2n | h_total | t_total | packed n
+        unsigned long long* pin = (unsigned long long*)pinned_stage().get(0, ((size_t)5 * n + 2) * 8);
+        unsigned long long *p_trs = pin, *p_tnz = pin + n, *p_hbs = pin + 2 * n, *p_htot = pin + 4 * n,
+                           *p_ttot = pin + 4 * n + 1, *p_pk = pin + 4 * n + 2;
+        const bool packed = tpack && t_nnz > 0;
+        trs.download(p_trs, n, s);
+        tnz.download(p_tnz, n, s);
+        hbs.download(p_hbs, 2 * n, s);
+        htot.download(p_htot, 1, s);
+        if (packed) {
+            ttot.download(p_ttot, 1, s);
+            tpk.download(p_pk, n, s);
+        }
         HIP_CHECK(hipStreamSynchronize(s));
-        if (tt < (1ull << 39)) {  // no row + column sum (<= 2 tt) can have carried into bit 64
-            for (int64_t y = 0; y < n; ++y) {
-                G.t_rowsum[y] += pk[y] >> 24;
-                G.t_nnz_row[y] += pk[y] & 0xffffffull;
+        std::copy(p_trs, p_trs + n, G.t_rowsum.begin());
+        std::copy(p_tnz, p_tnz + n, G.t_nnz_row.begin());
+        std::copy(p_hbs, p_hbs + 2 * n, G.h_blocksum.begin());
+        G.h_total = *p_htot;
+        if (packed) {
+            if (*p_ttot < (1ull << 39)) {  // no row + column sum (<= 2 tt) can have carried into bit 64
+                for (int64_t y = 0; y < n; ++y) {
+                    G.t_rowsum[y] += p_pk[y] >> 24;
+                    G.t_nnz_row[y] += p_pk[y] & 0xffffffull;
+                }
+            } else {  // counts too large for the packed field: the two-atomic pass
+                trs.zero(s);
+                tnz.zero(s);
+                hipLaunchKernelGGL(k_gw_tstats<false>, sgrid(t_nnz), dim3(256), 0, s, G.tAp, G.tBp, G.tVp,
+                                   (long long)t_nnz, dch.p, trs.p, tnz.p, nullptr, nullptr);
+                HIP_CHECK(hipGetLastError());
+                trs.download(p_trs, n, s);
+                tnz.download(p_tnz, n, s);
+                HIP_CHECK(hipStreamSynchronize(s));
+                std::copy(p_trs, p_trs + n, G.t_rowsum.begin());
+                std::copy(p_tnz, p_tnz + n, G.t_nnz_row.begin());
             }
-        } else {  // counts too large for the packed field: the two-atomic pass
-            trs.zero(s);
-            tnz.zero(s);
-            hipLaunchKernelGGL(k_gw_tstats<false>, sgrid(t_nnz), dim3(256), 0, s, G.tAp, G.tBp, G.tVp,
-                               (long long)t_nnz, dch.p, trs.p, tnz.p, nullptr, nullptr);
-            HIP_CHECK(hipGetLastError());
-            trs.download(G.t_rowsum.data(), n, s);
-            tnz.download(G.t_nnz_row.data(), n, s);
-            HIP_CHECK(hipStreamSynchronize(s));
         }
     }
+    // the alpha glue on a host thread while the GPU builds the column lists
+    // (row pointers, column keys, the radix sort: ~45 ms at 10 kb diploid)
+    clk.lap("statistics");
+    std::vector<int64_t> offv(chrom_offsets, chrom_offsets + n_chroms + 1);
+    ThreadJoin alpha_thread;
+    alpha_thread.t = std::thread([&G, offv]() {
+        try {
+            gw_alpha_host(G, offv);
+        } catch (...) {
+            std::fill(G.alpha_ok.begin(), G.alpha_ok.end(), 0);
+        }
+    });
     // H row pointers and column lists
     G.hptr.alloc(2 * n + 1);
     if (h_nnz > 0)
@@ -712,8 +850,12 @@ void gw_create(hh_gw& G, const Id* t1, const Id* t2, const Cnt* tv, int64_t t_nn
         ntot.download(&hn, 1, s);
         HIP_CHECK(hipStreamSynchronize(s));
     }
+    clk.lap("column keys");
     G.n_keys = (int64_t)hn;
-    dev_sort_u64(G.keys, G.n_keys, cbits, s, G.ib);  // keys in index order: only the column bits
+    {
+        HH_KTIME("gw_sort", s);
+        dev_sort_u64(G.keys, G.n_keys, cbits, s, G.ib);  // keys in index order: only the column bits
+    }
     G.cptr.alloc(2 * n + 1);
     hipLaunchKernelGGL(k_px_keyptr_gw, dim3((unsigned)((hn + 1 + 255) / 256)), dim3(256), 0, s, G.keys.p,
                        (long long)hn, G.ib, (long long)(2 * n), G.cptr.p);
@@ -721,7 +863,11 @@ void gw_create(hh_gw& G, const Id* t1, const Id* t2, const Cnt* tv, int64_t t_nn
         hipLaunchKernelGGL(k_gw_pack, dim3((unsigned)((hn + 255) / 256)), dim3(256), 0, s, G.keys.p, (long long)hn,
                            G.ib >= 64 ? ~0ull : ((1ull << G.ib) - 1ull), G.Rp, G.Vp);
     HIP_CHECK(hipGetLastError());
+    clk.lap("sort");
     HIP_CHECK(hipStreamSynchronize(s));
+    clk.lap("key pointers");
+    alpha_thread.t.join();
+    clk.lap("alpha join");
 }
 
 }  // namespace
@@ -772,6 +918,15 @@ int hh_gw_free(hh_gw* g) {
     });
 }
 
+int hh_gw_alpha(const hh_gw* g, double* alpha, int32_t* chrom_ok) {
+    return guard([&] {
+        HH_REQUIRE(g && alpha && chrom_ok, "null");
+        HH_REQUIRE((int64_t)g->alpha.size() == g->n, "alpha not computed");
+        std::copy(g->alpha.begin(), g->alpha.end(), alpha);
+        std::copy(g->alpha_ok.begin(), g->alpha_ok.end(), chrom_ok);
+    });
+}
+
 int hh_gw_stats(const hh_gw* g, int64_t* t_rowsum, int64_t* t_nnz_row, int64_t* h_blocksum, int64_t* h_total) {
     return guard([&] {
         HH_REQUIRE(g, "null");
@@ -798,19 +953,32 @@ struct GwScratch {
 template <int FMT>
 void gw_prepare(hh_gw* g, const double* alpha, double exponent, GwScratch& W, hipStream_t s) {
     const int64_t N2 = g->N2;
+    GwClock ck;
     W.dal.alloc(N2);
     W.sv.alloc(N2);
     W.rowc.alloc(N2);
-    W.dal.upload(alpha, N2, s);
+    ck.lap("prepare: allocs");
+    {
+        double* up = (double*)pinned_stage().get(1, (size_t)N2 * sizeof(double));
+        std::memcpy(up, alpha, (size_t)N2 * sizeof(double));
+        W.dal.upload(up, N2, s);
+    }
+    ck.lap("prepare: alpha upload");
     W.ustart.alloc(N2);
     W.lstart.alloc(N2);
     W.len.alloc(N2 + 1);
     W.roff.alloc(N2 + 1);
     GwDev d{g->Rp, g->Cp, g->Vp, g->hptr.p, g->keys.p, g->cptr.p, (long long)N2, W.dal.p, W.ustart.p, W.lstart.p};
     const unsigned wg = (unsigned)((N2 * 64 + 255) / 256);
-    hipLaunchKernelGGL(k_gw_marg<FMT>, dim3(wg), dim3(256), 0, s, d, exponent, W.sv.p);
-    hipLaunchKernelGGL((k_gw_merge<FMT, 0>), dim3(wg), dim3(256), 0, s, d, W.sv.p, 0.0, W.len.p, W.rowc.p,
-                       (int32_t*)nullptr, (int32_t*)nullptr, (double*)nullptr);
+    {
+        HH_KTIME("gw_marg", s);
+        hipLaunchKernelGGL(k_gw_marg<FMT>, dim3(wg), dim3(256), 0, s, d, exponent, W.sv.p);
+    }
+    {
+        HH_KTIME("gw_merge0", s);
+        hipLaunchKernelGGL((k_gw_merge<FMT, 0>), dim3(wg), dim3(256), 0, s, d, W.sv.p, 0.0, W.len.p, W.rowc.p,
+                           (int32_t*)nullptr, (int32_t*)nullptr, (double*)nullptr);
+    }
     HIP_CHECK(hipMemsetAsync(W.len.p + N2, 0, sizeof(long long), s));
     DBuf<unsigned long long> tot(1);
     dev_excl_scan_i64(W.len.p, W.roff.p, N2 + 1, tot.p, s);
@@ -822,9 +990,15 @@ void gw_prepare(hh_gw* g, const double* alpha, double exponent, GwScratch& W, hi
     HIP_CHECK(hipGetLastError());
     std::vector<double> hp(nbk);
     unsigned long long m = 0;
-    part.download(hp.data(), nbk, s);
-    tot.download(&m, 1, s);
+    ck.lap("prepare: kernels enqueued");
+    char* pin = (char*)pinned_stage().get(0, (size_t)nbk * sizeof(double) + 16);
+    part.download((double*)(pin + 16), nbk, s);
+    tot.download((unsigned long long*)pin, 1, s);
+    ck.lap("prepare: downloads enqueued");
     HIP_CHECK(hipStreamSynchronize(s));
+    std::memcpy(hp.data(), pin + 16, (size_t)nbk * sizeof(double));
+    std::memcpy(&m, pin, sizeof(m));
+    ck.lap("prepare: sync");
     double csum = 0.0;
     for (double x : hp) csum += x;
     const double NN = (double)N2 * (double)N2;

@@ -5,6 +5,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cmath>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -303,6 +305,56 @@ struct PinnedBuf {
         if (count) HIP_CHECK(hipHostMalloc((void**)&p, count * sizeof(T), hipHostMallocDefault));
     }
 };
+
+// np.percentile(v, pct) with the default 'linear' method (NumPy 2.x:
+// virtual index (n-1)*q, floor/next clipped to the ends, _lerp's two-sided
+// form), so host-side gap and alpha decisions are bit-identical to the
+// reference's NumPy calls.
+// Only the two order statistics around the virtual index are needed: one
+// nth_element and a min over the rest (O(n); a full sort of the ~6 000
+// coverages / alphas of a chromosome was most of TwoStepCorrection's host
+// time between its passes, profiles/r4m_twostep_trace.log).
+inline double np_percentile(std::vector<double> v, double pct) {
+    HH_REQUIRE(!v.empty(), "percentile of an empty array");
+    const long long n = (long long)v.size();
+    const double q = pct / 100.0;
+    const double vi = (double)(n - 1) * q;
+    long long prev = (long long)std::floor(vi), next = prev + 1;
+    if (vi >= (double)(n - 1)) prev = next = n - 1;
+    if (vi < 0) prev = next = 0;
+    const double gamma = vi - (vi >= (double)(n - 1) ? -1.0 : (double)prev);
+    std::nth_element(v.begin(), v.begin() + prev, v.end());
+    const double a = v[prev];
+    const double b = next == prev ? a : *std::min_element(v.begin() + prev + 1, v.end());
+    const double d = b - a;
+    return gamma >= 0.5 ? b - d * (1.0 - gamma) : a + d * gamma;
+}
+
+// Per-thread pinned host staging buffers (slot 0: downloads, 1: uploads),
+// grown on demand and kept for the process (never freed: freeing pinned
+// memory from a thread_local destructor at exit races the runtime's own
+// teardown).  A call synchronises its stream before returning, so the next
+// call on the thread may reuse them.
+struct PinnedStage {
+    void* p[2] = {nullptr, nullptr};
+    size_t cap[2] = {0, 0};
+    void* get(int slot, size_t bytes) {
+        if (bytes > cap[slot]) {
+            // the old buffer is idle (its copies completed before the last synchronisation)
+            if (p[slot]) HIP_CHECK(hipHostFree(p[slot]));
+            p[slot] = nullptr;
+            cap[slot] = 0;
+            const size_t want = std::max<size_t>(bytes, 1 << 20);
+            HIP_CHECK(hipHostMalloc(&p[slot], want, hipHostMallocDefault));
+            cap[slot] = want;
+        }
+        return p[slot];
+    }
+};
+inline PinnedStage& pinned_stage() {
+    static thread_local PinnedStage* st = new PinnedStage();
+    return *st;
+}
 
 // ---------------------------------------------------------------- device
 constexpr int kWave = 64;

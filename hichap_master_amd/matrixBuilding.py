@@ -278,7 +278,7 @@ def _gw_layout(Bins_Pos, Hap_Bins_Pos):
 
 
 def GenomeWideMatrixCorrectionSparse(Bins_Pos, Hap_Bins_Pos, T_pixels, H_cells, exponent=VC_EXPONENT,
-                                     stream=None, device_result=False):
+                                     stream=None, device_result=False, numpy_alpha=False):
     """GenomeWideMatrixCorrection (matrixBuilding.py:857-901) on pixel tables:
     the whole-genome diploid matrices at 10 kb are 607 282 x 607 282, which the
     reference's dense form cannot hold.
@@ -289,9 +289,21 @@ def GenomeWideMatrixCorrectionSparse(Bins_Pos, Hap_Bins_Pos, T_pixels, H_cells, 
     host arrays or int32 device tensors (then both must be).  Returns the
     upper triangle of the corrected matrix as (bin1, bin2, value), cooler
     order — the table NPZ2Cooler writes for it (:1613, :1628-1633).  The alpha
-    step runs here with the reference's NumPy expressions on exact integer row
-    sums computed on the GPU (hh_gw_stats)."""
+    step (:878-893) uses the reference's NumPy expressions on exact integer
+    row sums computed on the GPU: in C++ overlapped with the column-list
+    build (hh_gw_alpha), or here with NumPy (numpy_alpha=True; the same
+    bits, tests/test_gw_sparse_gpu.py)."""
     _lib.require_gpu()
+    import os
+    import time
+    tick = [time.perf_counter()]
+    timing = os.environ.get("HH_GW_TIMING")
+
+    def lap(what):  # HH_GW_TIMING=1: host-side phase times (diagnostic)
+        if timing:
+            t = time.perf_counter()
+            print(f"[gw] {what}: {1e3 * (t - tick[0]):.2f} ms", flush=True)
+            tick[0] = t
     off, order = _gw_layout(Bins_Pos, Hap_Bins_Pos)
     n = int(off[-1])
     h = C.c_void_p()
@@ -307,14 +319,30 @@ def GenomeWideMatrixCorrectionSparse(Bins_Pos, Hap_Bins_Pos, T_pixels, H_cells, 
         hc = [np.ascontiguousarray(x, dtype=dt) for x, dt in zip(H_cells, (np.int64, np.int64, np.float64))]
         call("hh_gw_create", ptr(t[0]), ptr(t[1]), ptr(t[2]), t[0].size, ptr(hc[0]), ptr(hc[1]), ptr(hc[2]),
              hc[0].size, n, ptr(off), len(order), stream, C.byref(h))
+    lap("create")
     try:
-        t_sum = np.empty(n, np.int64)
-        t_nz = np.empty(n, np.int64)
-        h_bs = np.empty(2 * n, np.int64)
-        h_tot = C.c_int64(0)
-        call("hh_gw_stats", h, ptr(t_sum), ptr(t_nz), ptr(h_bs), C.byref(h_tot))
+        # the alpha step: computed by hh_gw_create on a host thread while the
+        # GPU built the column lists (the same NumPy operations in C++); a
+        # chromosome it leaves (no non-gap bin, a max that is not positive
+        # finite) takes the NumPy expressions below, as does numpy_alpha=True
+        a_bins = np.empty(n, np.float64)
+        ok = np.zeros(len(order), np.int32)
+        if not numpy_alpha:
+            call("hh_gw_alpha", h, ptr(a_bins), ptr(ok))
+        stats = None
         Beta = {}
-        for c, (s, e) in Bins_Pos.items():
+        for k, c in enumerate(order):
+            s, e = Bins_Pos[c]
+            if ok[k]:
+                Beta[c] = a_bins[s:e + 1]
+                continue
+            if stats is None:
+                t_sum = np.empty(n, np.int64)
+                t_nz = np.empty(n, np.int64)
+                h_bs = np.empty(2 * n, np.int64)
+                h_tot = C.c_int64(0)
+                call("hh_gw_stats", h, ptr(t_sum), ptr(t_nz), ptr(h_bs), C.byref(h_tot))
+                stats = True
             L = e - s + 1
             cov = _coverage(L - t_nz[s:e + 1], L)
             gap = np.nonzero(cov < 0.1)[0]              # Gap_definedLowRes (:742-753)
@@ -323,13 +351,17 @@ def GenomeWideMatrixCorrectionSparse(Bins_Pos, Hap_Bins_Pos, T_pixels, H_cells, 
         # concatenate: the same values without 600 k boxed floats (40 ms)
         Alpha = np.concatenate([Beta[i] for i in Sort_Chromosomes(list(Beta.keys()))]).astype(np.float64)
         Alpha = np.ascontiguousarray(np.concatenate([Alpha, Alpha]))
+        lap("alpha")
         m = C.c_int64(0)
         if device_result:  # int32 / int32 / float64 device tensors, written in place by the library
             import torch
             call("hh_gw_correct_count", h, ptr(Alpha), float(exponent), C.byref(m), stream)
+            lap("correct_count")
             m = int(m.value)
             out = [torch.empty(max(m, 1), dtype=dt, device="cuda") for dt in (torch.int32, torch.int32, torch.float64)]
+            lap("outputs")
             call("hh_gw_correct_write", h, *(C.c_void_p(t.data_ptr()) for t in out), stream)
+            lap("correct_write")
             return tuple(t[:m] for t in out)
         call("hh_gw_correct", h, ptr(Alpha), float(exponent), C.byref(m), stream)
         m = int(m.value)
@@ -340,6 +372,7 @@ def GenomeWideMatrixCorrectionSparse(Bins_Pos, Hap_Bins_Pos, T_pixels, H_cells, 
         return b1, b2, v
     finally:
         call("hh_gw_free", h)
+        lap("free")
 
 
 # ---------------------------------------------------------- pair binning

@@ -365,6 +365,12 @@ int hh_gw_free(hh_gw* g);
  * row within its same-chromosome same-haplotype block (M_M / P_P); *h_total =
  * sum(H).  Any pointer may be NULL. */
 int hh_gw_stats(const hh_gw* g, int64_t* t_rowsum, int64_t* t_nnz_row, int64_t* h_blocksum, int64_t* h_total);
+/* The alpha step (:878-893) per chromosome on those statistics, computed by
+ * hh_gw_create on a host thread while the column lists build: alpha[n] in
+ * bin order, chrom_ok[n_chroms] (layout order) 0 where the caller must use
+ * NumPy's own path (no non-gap bin, or a max that is not positive finite).
+ * Replaces matrixBuilding.py:878-886's Python loop. */
+int hh_gw_alpha(const hh_gw* g, double* alpha, int32_t* chrom_ok);
 /* alpha[2n] (host): the concatenated, duplicated SNP-density factors;
  * exponent: 2/3.  *out_nnz = upper-triangle pixels of the result. */
 int hh_gw_correct(hh_gw* g, const double* alpha, double exponent, int64_t* out_nnz, void* stream);

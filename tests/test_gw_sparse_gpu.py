@@ -236,3 +236,50 @@ def test_large_h_counts_index_keys(mb):
     b1, b2, v = mb.GenomeWideMatrixCorrectionSparse(bins, hbins, tp, hc)
     ref = hichap_ref.genome_wide_correction(bins, hbins, T, H)
     _check_upper(b1, b2, v, ref, 1e-12)
+
+
+def test_cpp_alpha_is_numpy_alpha(mb, golden):
+    """The alpha step computed in C++ while the column lists build
+    (hh_gw_alpha) gives the NumPy expressions' bits: the corrected tables are
+    identical, on the reference golden, on random layouts with gaps and on
+    the 10 kb diploid layout at reduced depth; a chromosome without non-gap
+    bins takes NumPy's path and raises the same error."""
+    g = golden("genomewide_3chrom")
+    bins, hbins = _layout([str(x) for x in g["names"]], [int(x) for x in g["sizes"]])
+    tp, hc = _tables(g["T_M"], g["H_M"])
+    a = mb.GenomeWideMatrixCorrectionSparse(bins, hbins, tp, hc)
+    b = mb.GenomeWideMatrixCorrectionSparse(bins, hbins, tp, hc, numpy_alpha=True)
+    for x, y in zip(a, b):
+        np.testing.assert_array_equal(x, y)
+    rng = np.random.default_rng(3)
+    sizes = [120, 7, 64, 200]
+    n = sum(sizes)
+    T = np.triu(rng.poisson(1.0, size=(n, n)) * (rng.random((n, n)) < 0.3))
+    T[:, 130:140] = 0  # gap rows / columns
+    T[130:140, :] = 0
+    H = rng.poisson(0.7, size=(2 * n, 2 * n)) * (rng.random((2 * n, 2 * n)) < 0.2)
+    bins, hbins = _layout(["1", "2", "3", "X"], sizes)
+    tp, hc = _tables(T, H)
+    a = mb.GenomeWideMatrixCorrectionSparse(bins, hbins, tp, hc)
+    b = mb.GenomeWideMatrixCorrectionSparse(bins, hbins, tp, hc, numpy_alpha=True)
+    for x, y in zip(a, b):
+        np.testing.assert_array_equal(x, y)
+    T2 = T.copy()
+    T2[120:127, :] = 0  # chromosome "2": every bin a gap -> np.max of an empty array
+    T2[:, 120:127] = 0
+    tp2, _ = _tables(T2, H)
+    for na in (False, True):
+        with pytest.raises(ValueError):
+            mb.GenomeWideMatrixCorrectionSparse(bins, hbins, tp2, hc, numpy_alpha=na)
+    bins, hap, T, H, N2 = _gw_10kb(2e8, 2e8)  # (at 5e7 some chromosome has no non-gap bin: both paths raise)
+    try:
+        a = [x.cpu().numpy() for x in mb.GenomeWideMatrixCorrectionSparse(
+            bins, hap, (T.bin1, T.bin2, T.count), (H.bin1, H.bin2, H.count), device_result=True)]
+        b = [x.cpu().numpy() for x in mb.GenomeWideMatrixCorrectionSparse(
+            bins, hap, (T.bin1, T.bin2, T.count), (H.bin1, H.bin2, H.count), device_result=True,
+            numpy_alpha=True)]
+    finally:
+        T.close()
+        H.close()
+    for x, y in zip(a, b):
+        np.testing.assert_array_equal(x, y)
