@@ -2083,9 +2083,15 @@ static bool pca_krylov(PcaWork& wk, const double* cor, long long n, int k, doubl
     DBuf<double> Ydev((size_t)P * B * B);
     std::vector<double> hs((size_t)P * slot + 3 * BB + (nfl + 1) / 2);
     std::vector<int> hf(nfl);
+    // host transfers through the thread's pinned staging buffers (slot 0
+    // down, slot 1 up): pageable copies stalled the genome-wide correction
+    // by ~20 ms each when issued to an idle GPU (profiles/r4gw)
+    PinnedStage& pin = pinned_stage();
     auto download_smalls = [&]() {  // hs, hf <- the device (one copy), synchronised
-        smalls.download(hs.data(), hs.size(), s);
+        double* h = (double*)pin.get(0, hs.size() * sizeof(double));
+        smalls.download(h, hs.size(), s);
         HIP_CHECK(hipStreamSynchronize(s));
+        std::memcpy(hs.data(), h, hs.size() * sizeof(double));
         std::memcpy(hf.data(), hs.data() + (size_t)P * slot + 3 * BB, sizeof(int) * nfl);
     };
     auto gram = [&](const double* Xs, int nb, const double* Y, double* out) {
@@ -2200,7 +2206,9 @@ static bool pca_krylov(PcaWork& wk, const double* cor, long long n, int k, doubl
         for (long long i = 0; i < n; ++i)
             for (int b = 0; b < B; ++b)
                 v0[i * B + b] = b == 0 ? 1.0 / std::sqrt((double)n) : (double)u01(mix64(0x5eedULL + i * B + b)) - 0.5;
-        X.upload(v0.data(), v0.size(), s);
+        double* h = (double*)pin.get(1, v0.size() * sizeof(double));
+        std::memcpy(h, v0.data(), v0.size() * sizeof(double));
+        X.upload(h, v0.size(), s);
         if (coop) {
             OrthoArgs a;
             a.xin = X.p;
@@ -2357,7 +2365,12 @@ static bool pca_krylov(PcaWork& wk, const double* cor, long long n, int k, doubl
         const double t_h = std::chrono::duration<double, std::milli>(c2 - c1).count();
         const double t_e = std::chrono::duration<double, std::milli>(c3 - c2).count();
         // Ritz vectors X = Qa Y (top B), uploaded as nb stacked 16 x 16 blocks
-        Ydev.upload(Y.data(), (size_t)mb * B, s);
+        {
+            // (slot 1's previous upload completed: download_smalls synchronised since)
+            double* h = (double*)pin.get(1, (size_t)mb * B * sizeof(double));
+            std::memcpy(h, Y.data(), (size_t)mb * B * sizeof(double));
+            Ydev.upload(h, (size_t)mb * B, s);
+        }
         ++cycles;
         if (eigvals)
             for (int q = 0; q < k; ++q) eigvals[q] = ev[q];
@@ -2437,8 +2450,10 @@ static bool pca_krylov(PcaWork& wk, const double* cor, long long n, int k, doubl
     download_smalls();
     check_abort(hf);
     if (cycles > 0) {  // the last cycle's Ritz vectors
-        X.download(Xh.data(), Xh.size(), s);
+        double* h = (double*)pin.get(0, Xh.size() * sizeof(double));
+        X.download(h, Xh.size(), s);
         HIP_CHECK(hipStreamSynchronize(s));
+        std::memcpy(Xh.data(), h, Xh.size() * sizeof(double));
         for (int q = 0; q < k; ++q) {
             double nn = 0.0;
             for (long long i = 0; i < n; ++i) nn += Xh[i * B + q] * Xh[i * B + q];
