@@ -373,7 +373,7 @@ constexpr int kGB = 4 * kGW;  // columns per block: its 4 waves read 16 KB of a 
 //         integer X, stored in the double slot's bits); the both-gap entries
 //         X_ij (i, j gaps) copied to the compact g x g matrix Xc.
 // MODE 2: part_r[q][i] = sum over the span's columns of X_ij * rs_j.
-template <class T, int MODE>
+template <class T, int MODE, bool ROWS = true>
 __global__ __launch_bounds__(256) void k_ts_gemv(const T* __restrict__ X, long long N,
                                                  const double* __restrict__ alpha, const double* __restrict__ rs,
                                                  int gr, double* __restrict__ part_c, double* __restrict__ part_r,
@@ -433,7 +433,9 @@ __global__ __launch_bounds__(256) void k_ts_gemv(const T* __restrict__ X, long l
                             if (gcol[k] >= 0) Xc[(long long)gi * ng + gcol[k]] = x[b][k];
                     }
                 }
-                if constexpr (std::is_integral_v<T>) {
+                if constexpr (!ROWS) {
+                    // the row sums come from k_rowstats (hh_twostep)
+                } else if constexpr (std::is_integral_v<T>) {
                     long long t = 0;
 #pragma unroll
                     for (int k = 0; k < 8; ++k) t += okc[k] ? (long long)x[b][k] : 0LL;
@@ -562,13 +564,15 @@ __global__ void k_ts_rows(const T* __restrict__ X, long long N, long long ncb,
                           const double* __restrict__ ccol, const double* __restrict__ part_r,
                           const double* __restrict__ alpha, const int* __restrict__ gpos,
                           const double* __restrict__ gpart, const long long* __restrict__ ng_p, double exponent,
-                          double* __restrict__ sv, double* __restrict__ rsv) {
+                          const double* __restrict__ rowsum_in, double* __restrict__ sv, double* __restrict__ rsv) {
     const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= N) return;
     const long long ng = ng_p ? *ng_p : 0;  // gap form iff ng > 0 (Trans2symmetry :948)
     const double c = ccol[i];
     double rsum;
-    if constexpr (std::is_integral_v<T>) {
+    if (rowsum_in) {
+        rsum = rowsum_in[i];  // k_rowstats' exact integer row sum (the same double)
+    } else if constexpr (std::is_integral_v<T>) {
         long long t = 0;
         for (long long cb = 0; cb < ncb; ++cb) t += reinterpret_cast<const long long*>(part_r)[cb * N + i];
         rsum = (double)t;
@@ -666,7 +670,7 @@ static void gap_index_host(const uint8_t* hgap, long long N, std::vector<int>& g
 template <class T>
 static void symvc_enqueue(const T* dX, long long N, const double* dalpha, const uint8_t* dgap, GapIdx gi,
                           double exponent, double raw_sum, const double* raw_p, double* dout, hipStream_t s,
-                          SymvcWs& ws) {
+                          SymvcWs& ws, const double* rowsum_in = nullptr) {
     const long long nT = (N + kT - 1) / kT;
     const long long npairs = nT * (nT + 1) / 2;
     HH_REQUIRE(npairs < (1LL << 31), "matrix too large");
@@ -697,7 +701,8 @@ static void symvc_enqueue(const T* dX, long long N, const double* dalpha, const 
         const unsigned gcb = (unsigned)((N + kGB - 1) / kGB);
         {
             HH_KTIME("k_ts_gemv1", s);
-            hipLaunchKernelGGL((k_ts_gemv<T, 1>), dim3((unsigned)nrc, gcb), dim3(256), 0, s, dX, N, dalpha,
+            auto kern = rowsum_in ? k_ts_gemv<T, 1, false> : k_ts_gemv<T, 1, true>;
+            hipLaunchKernelGGL(kern, dim3((unsigned)nrc, gcb), dim3(256), 0, s, dX, N, dalpha,
                                (const double*)nullptr, gr, ws.part_c.p, ws.part_r.p, gpos, xc, ng_p);
         }
         if (ngm)
@@ -706,7 +711,7 @@ static void symvc_enqueue(const T* dX, long long N, const double* dalpha, const 
         hipLaunchKernelGGL(k_ts_colsum, dim3((unsigned)((N + 63) / 64)), dim3(1024), 0, s, ws.part_c.p, N, nrc,
                            ws.ccol.p);
         hipLaunchKernelGGL((k_ts_rows<T>), dim3((unsigned)nb), dim3(256), 0, s, dX, N, ncb, ws.ccol.p, ws.part_r.p,
-                           dalpha, gpos, ws.gpart1.p, ng_p, exponent, ws.sv.p, ws.rsv.p);
+                           dalpha, gpos, ws.gpart1.p, ng_p, exponent, rowsum_in, ws.sv.p, ws.rsv.p);
         if (ngm)
             hipLaunchKernelGGL((k_ts_gap<T, 2>), dim3(ggrid), dim3(256), 0, s, (const T*)xc, ng_p, gi.glist, dalpha,
                                ws.sv.p, ws.gpart2.p);
@@ -1320,10 +1325,10 @@ int hh_twostep(const int64_t* TM, const int64_t* MM, const int64_t* PM, int64_t 
             SymvcWs wm, wp;
             const GapIdx gim{dgpos.p, dglist.p, dng.p, N}, gip{dgpos.p + N, dglist.p + N, dng.p + 1, N};
             double* out_m = on_device ? nor_mm : (double*)buf[0].p;
-            symvc_enqueue(d[1], N, dA.p, dgf.p, gim, 2.0 / 3.0, 0.0, draw.p, out_m, s, wm);
+            symvc_enqueue(d[1], N, dA.p, dgf.p, gim, 2.0 / 3.0, 0.0, draw.p, out_m, s, wm, dsum.p + N);
             if (!on_device) HIP_CHECK(hipMemcpyAsync(nor_mm, out_m, cnt * 8, hipMemcpyDeviceToHost, s));
             double* out_p = on_device ? nor_pm : (double*)buf[1].p;
-            symvc_enqueue(d[2], N, dA.p, dgf.p + N, gip, 2.0 / 3.0, 0.0, draw.p + 1, out_p, s, wp);
+            symvc_enqueue(d[2], N, dA.p, dgf.p + N, gip, 2.0 / 3.0, 0.0, draw.p + 1, out_p, s, wp, dsum.p + 2 * N);
             if (!on_device) HIP_CHECK(hipMemcpyAsync(nor_pm, out_p, cnt * 8, hipMemcpyDeviceToHost, s));
             char* dl = (char*)st.get(0, (size_t)2 * N + 16);
             dgf.download((uint8_t*)dl, (size_t)2 * N, s);
@@ -1401,11 +1406,13 @@ int hh_twostep(const int64_t* TM, const int64_t* MM, const int64_t* PM, int64_t 
         // Nor_PM; both chains enqueued back to back, one synchronisation
         SymvcWs wm, wp;
         double* out_m = on_device ? nor_mm : (double*)buf[0].p;
-        symvc_enqueue(d[1], N, dA, any_m ? dgm : nullptr, gim, 2.0 / 3.0, raw[0], (const double*)nullptr, out_m, s, wm);
+        symvc_enqueue(d[1], N, dA, any_m ? dgm : nullptr, gim, 2.0 / 3.0, raw[0], (const double*)nullptr, out_m, s, wm,
+                      dsum.p + N);
         if (!on_device) HIP_CHECK(hipMemcpyAsync(nor_mm, out_m, cnt * 8, hipMemcpyDeviceToHost, s));
         double* out_p = on_device ? nor_pm : (double*)buf[1].p;
         // (MM's buffer, read by the first chain, is written by the second: stream order)
-        symvc_enqueue(d[2], N, dA, any_p ? dgp : nullptr, gip, 2.0 / 3.0, raw[1], (const double*)nullptr, out_p, s, wp);
+        symvc_enqueue(d[2], N, dA, any_p ? dgp : nullptr, gip, 2.0 / 3.0, raw[1], (const double*)nullptr, out_p, s, wp,
+                      dsum.p + 2 * N);
         if (!on_device) HIP_CHECK(hipMemcpyAsync(nor_pm, out_p, cnt * 8, hipMemcpyDeviceToHost, s));
         HIP_CHECK(hipStreamSynchronize(s));
         std::copy(gm.begin(), gm.end(), gap_m);
