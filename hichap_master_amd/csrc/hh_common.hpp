@@ -356,6 +356,47 @@ inline PinnedStage& pinned_stage() {
     return *st;
 }
 
+// Synchronous host transfers through the thread's pinned staging: pageable
+// hipMemcpyAsync measured ~20 ms for a few MB (and 18 ms for 40 bytes) in
+// processes holding tens of GB of device memory (the genome-wide correction,
+// profiles/r4gw; the matrix build's count download), pinned DMA ~0.1 ms.
+// PinnedDown batches downloads (slot 0) behind one synchronisation.
+struct PinnedDown {
+    struct Item {
+        const void* d;
+        void* h;
+        size_t bytes, off;
+    };
+    std::vector<Item> items;
+    size_t total = 0;
+    template <class T>
+    void add(const T* d, T* h, size_t count) {
+        if (!count) return;
+        items.push_back(Item{d, h, count * sizeof(T), total});
+        total += (count * sizeof(T) + 15) & ~size_t(15);
+    }
+    void run(hipStream_t s) {
+        if (items.empty()) return;
+        char* base = (char*)pinned_stage().get(0, total);
+        for (const Item& it : items)
+            HIP_CHECK(hipMemcpyAsync(base + it.off, it.d, it.bytes, hipMemcpyDeviceToHost, s));
+        HIP_CHECK(hipStreamSynchronize(s));
+        for (const Item& it : items) std::memcpy(it.h, base + it.off, it.bytes);
+        items.clear();
+        total = 0;
+    }
+};
+// host -> device through pinned staging (slot 1), synchronised (the slot is
+// free again on return)
+template <class T>
+inline void upload_pinned_sync(T* d, const T* h, size_t count, hipStream_t s) {
+    if (!count) return;
+    char* base = (char*)pinned_stage().get(1, count * sizeof(T));
+    std::memcpy(base, h, count * sizeof(T));
+    HIP_CHECK(hipMemcpyAsync(d, base, count * sizeof(T), hipMemcpyHostToDevice, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+}
+
 // ---------------------------------------------------------------- device
 constexpr int kWave = 64;
 

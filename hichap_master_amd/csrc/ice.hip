@@ -2439,9 +2439,12 @@ static void filter_count_mad(hh_ice* S, hipStream_t s,
     HIP_CHECK(hipGetLastError());
     if (S->o.mad_max <= 0) return;
     std::vector<double> marg(S->n), bias(S->n);
-    S->marg.download(marg.data(), S->n, s);
-    S->bias.download(bias.data(), S->n, s);
-    HIP_CHECK(hipStreamSynchronize(s));
+    {
+        PinnedDown dl;
+        dl.add(S->marg.p, marg.data(), (size_t)S->n);
+        dl.add(S->bias.p, bias.data(), (size_t)S->n);
+        dl.run(s);
+    }
     const auto& off = S->m->chrom_offsets;
     std::vector<double> pos;
     for (int c = 0; c < S->m->n_chroms; ++c) {
@@ -2461,8 +2464,7 @@ static void filter_count_mad(hh_ice* S, hipStream_t s,
     const double cutoff = std::exp(med - S->o.mad_max * np_median(dev));
     for (int64_t i = 0; i < S->n; ++i)
         if (marg[i] < cutoff) bias[i] = 0.0;
-    S->bias.upload(bias.data(), S->n, s);
-    HIP_CHECK(hipStreamSynchronize(s));
+    upload_pinned_sync(S->bias.p, bias.data(), (size_t)S->n, s);
 }
 
 extern "C" {
@@ -2678,7 +2680,7 @@ int hh_ice_create(hh_matrix* m, const hh_ice_opts* o, hh_ice** out) {
         S->counter.zero(s);
         S->bias.alloc(S->n);
         std::vector<double> ones(S->n, 1.0);
-        S->bias.upload(ones.data(), S->n, s);
+        upload_pinned_sync(S->bias.p, ones.data(), (size_t)S->n, s);
         S->marg.alloc(S->n);
         S->marg.zero(s);
         S->part.alloc(std::max<int64_t>(m->n_part, 1));
@@ -2917,12 +2919,15 @@ int hh_ice_finalize(hh_ice* S, double* weights, double* scale, double* var, int3
         std::vector<double> b(S->n), gm(G), gv(G);
         std::vector<int32_t> gi(G);
         std::vector<uint8_t> ge(G);
-        S->bias.download(b.data(), S->n, s);
-        S->g_mean.download(gm.data(), G, s);
-        S->g_var.download(gv.data(), G, s);
-        S->g_iters.download(gi.data(), G, s);
-        S->g_empty.download(ge.data(), G, s);
-        HIP_CHECK(hipStreamSynchronize(s));
+        {
+            PinnedDown dl;
+            dl.add(S->bias.p, b.data(), (size_t)S->n);
+            dl.add(S->g_mean.p, gm.data(), (size_t)G);
+            dl.add(S->g_var.p, gv.data(), (size_t)G);
+            dl.add(S->g_iters.p, gi.data(), (size_t)G);
+            dl.add(S->g_empty.p, ge.data(), (size_t)G);
+            dl.run(s);
+        }
         for (int g = 0; g < G; ++g) {
             const double sc = gm[g];
             for (int64_t i = S->glo[g]; i < S->ghi[g]; ++i) {

@@ -14,7 +14,7 @@ __global__ void k_touch(double* p, size_t n) {
 }
 
 int main() {
-    const size_t sizes[] = {8, 1024, 100 << 10, 1 << 20, 5 << 20};
+    const size_t sizes[] = {8, 100 << 10, 5 << 20};
     const size_t big = 64 << 20;
     double* dbig = nullptr;
     char* d = nullptr;
@@ -25,6 +25,7 @@ int main() {
     std::vector<char> pg(8 << 20, 1);
     hipStream_t s;
     CK(hipStreamCreate(&s));
+    for (double idle_us : {0.0, 2000.0, 20000.0})
     for (int pinned = 0; pinned < 2; ++pinned)
         for (int dir = 0; dir < 2; ++dir)
             for (size_t b : sizes) {
@@ -33,6 +34,10 @@ int main() {
                 for (int r = 0; r < reps; ++r) {
                     hipLaunchKernelGGL(k_touch, dim3(1024), dim3(256), 0, s, dbig, big);
                     CK(hipStreamSynchronize(s));
+                    if (idle_us) {  // host work while the GPU idles
+                        auto w = std::chrono::steady_clock::now();
+                        while (std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - w).count() < idle_us) {}
+                    }
                     char* h = pinned ? pin : pg.data();
                     auto t0 = std::chrono::steady_clock::now();
                     if (dir == 0) CK(hipMemcpyAsync(d, h, b, hipMemcpyHostToDevice, s));
@@ -40,8 +45,8 @@ int main() {
                     CK(hipStreamSynchronize(s));
                     tot += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
                 }
-                std::printf("%s %s %8zu B: %9.1f us\n", pinned ? "pinned  " : "pageable", dir ? "D2H" : "H2D", b,
-                            tot / reps);
+                std::printf("idle %6.0f us %s %s %8zu B: %9.1f us\n", idle_us, pinned ? "pinned  " : "pageable",
+                            dir ? "D2H" : "H2D", b, tot / reps);
             }
     return 0;
 }
