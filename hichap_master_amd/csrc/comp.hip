@@ -1513,7 +1513,22 @@ __global__ __launch_bounds__(256) void k_ortho(OrthoArgs Ain) {
             A_rout[e] = acc;
         }
         gsync();
-        for (int e = t; e < E; e += 256) {
+        // every coefficient loaded before the first is stored (clamped
+        // addresses, no select): a loop of load -> use compiled to one
+        // round trip per 256 coefficients, up to 8 in a row (ISA-checked)
+        constexpr int kIt = kOrthoMaxE / 256;
+        double cv[kIt];
+#pragma unroll
+        for (int q = 0; q < kIt; ++q) cv[q] = ld_agent(A_rout + min(t + 256 * q, E - 1));
+#pragma unroll
+        for (int q = 0; q < kIt; ++q) {
+            const int e = t + 256 * q;
+            if (e < E) {
+                L.cm[e] = cv[q];
+                if (g == 0 && e < A_nb * BB) out[e] = cv[q];
+            }
+        }
+        for (int e = t + 256 * kIt; e < E; e += 256) {  // (E <= kOrthoMaxE: not reached)
             const double v = ld_agent(A_rout + e);
             L.cm[e] = v;
             if (g == 0 && e < A_nb * BB) out[e] = v;
@@ -1672,9 +1687,21 @@ __global__ __launch_bounds__(256) void k_ortho(OrthoArgs Ain) {
     };
     // ---- the block's rows in
     if (MODE != kOrthoRitz) {  // W (Full / Last) or the start block
-        for (int e = t; e < RPB * B; e += 256) {
+        // all the block's row loads in flight at once (clamped rows, zeroed
+        // by a 0 / 1 factor: `i < n ? load : 0` compiled to one round trip
+        // per 256 elements, 8 in a row; ISA-checked)
+        constexpr int kIt = RPB * B / 256;
+        double xv[kIt];
+#pragma unroll
+        for (int q = 0; q < kIt; ++q) {
+            const int e = t + 256 * q;
             const long long i = r0 + e / B;
-            L.x[e / B][e % B] = i < n ? A_xin[i * B + e % B] : 0.0;
+            xv[q] = A_xin[(i < n ? i : n - 1) * B + e % B];
+        }
+#pragma unroll
+        for (int q = 0; q < kIt; ++q) {
+            const int e = t + 256 * q;
+            L.x[e / B][e % B] = xv[q] * (r0 + e / B < n ? 1.0 : 0.0);
         }
     } else {  // Ritz vectors X = Q Y out, then the start block [1 / sqrt(n) | X[:, 0..14]]
         for (int e = t; e < A_nb * BB; e += 256) L.cm[e] = A_Y[e];
