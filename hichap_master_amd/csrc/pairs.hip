@@ -70,12 +70,19 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_tile_sum(const T* __restr
                                                                 unsigned long long* __restrict__ sums) {
     __shared__ unsigned long long sh[4];
     const long long base = (long long)blockIdx.x * kScanTile;
-    unsigned long long s = 0;
+    // every load unconditional (an `if (i < n)` load compiled to one round
+    // trip each): indices past n re-read in[n - 1], subtracted once at the end
+    unsigned long long s = 0, over = 0;
+    T xs[kScanItems];
 #pragma unroll
     for (int r = 0; r < kScanItems; ++r) {
         const long long i = base + (long long)r * kScanThreads + threadIdx.x;
-        if (i < n) s += (unsigned long long)in[i];
+        xs[r] = in[i < n ? i : n - 1];
+        over += i >= n;
     }
+#pragma unroll
+    for (int r = 0; r < kScanItems; ++r) s += (unsigned long long)xs[r];
+    s -= over * (unsigned long long)in[n - 1];
     unsigned long long tot = 0;
     (void)block_excl_scan_u64(s, sh, &tot);
     if (threadIdx.x == 0) sums[blockIdx.x] = tot;
@@ -90,13 +97,17 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_tile_apply(const T* __res
     __shared__ unsigned long long sh[4];
     const long long base = (long long)blockIdx.x * kScanTile + (long long)threadIdx.x * kScanItems;
     unsigned long long v[kScanItems];
-    unsigned long long s = 0;
+    unsigned long long s = 0, over = 0;
+    // unconditional loads as in k_scan_tile_sum; a thread's items past n
+    // follow its valid ones, so only its total needs the correction
 #pragma unroll
     for (int r = 0; r < kScanItems; ++r) {
         const long long i = base + r;
-        v[r] = i < n ? (unsigned long long)in[i] : 0ull;
+        v[r] = (unsigned long long)in[i < n ? i : n - 1];
         s += v[r];
+        over += i >= n;
     }
+    s -= over * (unsigned long long)in[n - 1];
     unsigned long long run = tile_off[blockIdx.x] + block_excl_scan_u64(s, sh, nullptr);
 #pragma unroll
     for (int r = 0; r < kScanItems; ++r) {
