@@ -195,7 +195,16 @@ __global__ __launch_bounds__(256) void k_gw_tstats(const int32_t* __restrict__ a
 // (segmented, one atomic per row run).  1.5e9 same-address-free but
 // one-per-pixel global atomics were the whole 17.7 ms of k_gw_tstats at
 // 10 kb whole genome.  Integer sums: exact, order-free.
+//
+// Round 4: a block walks its run in chunks of kStChunk pixels, each thread's
+// kStItems pixels loaded together from clamped addresses (the per-pixel
+// `if (i < p1)` loads were one memory round trip each, 1.1 TB/s); a chunk
+// whose first and last pixel share a row (the common case: ~5 000 pixels
+// per row at 10 kb) sums its row end in registers, one wave reduction and
+// one atomic per wave, instead of a segmented scan per pixel.
 constexpr int kTsWin = 8192;
+constexpr int kStItems = 8;
+constexpr int kStChunk = 256 * kStItems;
 __global__ __launch_bounds__(256) void k_gw_tstats_win(const int32_t* __restrict__ a, const int32_t* __restrict__ b,
                                                        const uint32_t* __restrict__ v, long long nnz, long long per,
                                                        long long n, const int2* __restrict__ cbd,
@@ -209,26 +218,63 @@ __global__ __launch_bounds__(256) void k_gw_tstats_win(const int32_t* __restrict
     const long long x0 = a[p0];
     for (int c = threadIdx.x; c < kTsWin; c += 256) win[c] = 0ull;
     __syncthreads();
-    const long long endr = p0 + (p1 - p0 + 255) / 256 * 256;  // whole waves iterate together
     unsigned long long t = 0;
-    for (long long i = p0 + threadIdx.x; i < endr; i += 256) {
-        long long x = 0x7fffffffLL;
-        unsigned long long pk = 0;
-        if (i < p1) {
-            x = a[i];
-            const int32_t y = b[i];
-            const uint32_t cc = v[i];
-            t += cc;
-            if (cc != 0u && in_block(cbd[x], y)) {
-                pk = ((unsigned long long)cc << 24) | 1ull;
-                if (x != y) {
-                    const long long d = (long long)y - x0;
-                    if (d < kTsWin) atomicAdd(&win[d], pk);
-                    else atomicAdd(rpk + y, pk);
+    for (long long c0 = p0; c0 < p1; c0 += kStChunk) {
+        const long long last = std::min(c0 + kStChunk, p1) - 1;
+        const int32_t xf = a[c0], xl = a[last];
+        int32_t xs[kStItems], ys[kStItems];
+        uint32_t cs[kStItems];
+#pragma unroll
+        for (int k = 0; k < kStItems; ++k) {
+            const long long i = std::min(c0 + k * 256 + threadIdx.x, last);
+            xs[k] = a[i];
+            ys[k] = b[i];
+            cs[k] = v[i];
+        }
+#pragma unroll
+        for (int k = 0; k < kStItems; ++k)  // past the run: count 0 (clamped duplicates of the last pixel)
+            cs[k] &= 0u - (uint32_t)(c0 + k * 256 + threadIdx.x <= last);
+        if (xf == xl) {
+            const int2 bd = cbd[xf];
+            unsigned long long racc = 0;
+#pragma unroll
+            for (int k = 0; k < kStItems; ++k) {
+                const uint32_t cc = cs[k];
+                const int32_t y = ys[k];
+                t += cc;
+                if (cc != 0u && in_block(bd, y)) {
+                    const unsigned long long pk = ((unsigned long long)cc << 24) | 1ull;
+                    racc += pk;
+                    if (xf != y) {
+                        const long long d = (long long)y - x0;
+                        if (d < kTsWin) atomicAdd(&win[d], pk);
+                        else atomicAdd(rpk + y, pk);
+                    }
                 }
             }
+            racc = (unsigned long long)wave_sum_ll((long long)racc);
+            if ((threadIdx.x & 63) == 0 && racc) atomicAdd(rpk + xf, racc);
+        } else {
+            int2 bds[kStItems];
+#pragma unroll
+            for (int k = 0; k < kStItems; ++k) bds[k] = cbd[xs[k]];
+#pragma unroll
+            for (int k = 0; k < kStItems; ++k) {
+                const uint32_t cc = cs[k];
+                const int32_t x = xs[k], y = ys[k];
+                t += cc;
+                unsigned long long pk = 0;
+                if (cc != 0u && in_block(bds[k], y)) {
+                    pk = ((unsigned long long)cc << 24) | 1ull;
+                    if (x != y) {
+                        const long long d = (long long)y - x0;
+                        if (d < kTsWin) atomicAdd(&win[d], pk);
+                        else atomicAdd(rpk + y, pk);
+                    }
+                }
+                seg_add_u64(x, pk, rpk);  // rows non-decreasing across the wave (clamped lanes: pk 0)
+            }
         }
-        seg_add_u64(x, pk, rpk);
     }
     __syncthreads();
     for (int c = threadIdx.x; c < kTsWin; c += 256) {
@@ -245,27 +291,53 @@ __global__ __launch_bounds__(256) void k_gw_tstats_win(const int32_t* __restrict
 }
 
 // H row sums within the same-chromosome same-haplotype block (H sorted by
-// row: segmented), and sum(H)
+// row: segmented), and sum(H).  A block walks a contiguous run in chunks as
+// k_gw_tstats_win does (batched clamped loads; a one-row chunk sums in
+// registers).
 __global__ __launch_bounds__(256) void k_gw_hstats(const int32_t* __restrict__ r, const int32_t* __restrict__ c,
-                                                   const uint32_t* __restrict__ v, long long nnz,
+                                                   const uint32_t* __restrict__ v, long long nnz, long long per,
                                                    const int2* __restrict__ bbd,
                                                    unsigned long long* __restrict__ bsum,
                                                    unsigned long long* __restrict__ total) {
     __shared__ unsigned long long wsum[4];
-    const long long stride = (long long)gridDim.x * blockDim.x;
-    const long long start = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    const long long end = (nnz + 63) / 64 * 64;
+    const long long p0 = (long long)blockIdx.x * per;
+    if (p0 >= nnz) return;  // block-uniform
+    const long long p1 = std::min(nnz, p0 + per);
     unsigned long long t = 0;
-    for (long long i = start; i < end; i += stride) {
-        long long row = 0x7fffffffLL;
-        unsigned long long x = 0;
-        if (i < nnz) {
-            row = r[i];
-            const uint32_t xx = v[i];
-            t += xx;
-            if (xx && in_block(bbd[row], c[i])) x = xx;
+    for (long long c0 = p0; c0 < p1; c0 += kStChunk) {
+        const long long last = std::min(c0 + kStChunk, p1) - 1;
+        const int32_t xf = r[c0], xl = r[last];
+        int32_t xs[kStItems], ys[kStItems];
+        uint32_t cs[kStItems];
+#pragma unroll
+        for (int k = 0; k < kStItems; ++k) {
+            const long long i = std::min(c0 + k * 256 + threadIdx.x, last);
+            xs[k] = r[i];
+            ys[k] = c[i];
+            cs[k] = v[i];
         }
-        seg_add_u64(row, x, bsum);
+#pragma unroll
+        for (int k = 0; k < kStItems; ++k) cs[k] &= 0u - (uint32_t)(c0 + k * 256 + threadIdx.x <= last);
+        if (xf == xl) {
+            const int2 bd = bbd[xf];
+            unsigned long long racc = 0;
+#pragma unroll
+            for (int k = 0; k < kStItems; ++k) {
+                t += cs[k];
+                racc += in_block(bd, ys[k]) ? (unsigned long long)cs[k] : 0ull;
+            }
+            racc = (unsigned long long)wave_sum_ll((long long)racc);
+            if ((threadIdx.x & 63) == 0 && racc) atomicAdd(bsum + xf, racc);
+        } else {
+            int2 bds[kStItems];
+#pragma unroll
+            for (int k = 0; k < kStItems; ++k) bds[k] = bbd[xs[k]];
+#pragma unroll
+            for (int k = 0; k < kStItems; ++k) {
+                t += cs[k];
+                seg_add_u64(xs[k], in_block(bds[k], ys[k]) ? (unsigned long long)cs[k] : 0ull, bsum);
+            }
+        }
     }
     t = (unsigned long long)wave_sum_ll((long long)t);
     if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = t;
@@ -758,9 +830,12 @@ void gw_create(hh_gw& G, const Id* t1, const Id* t2, const Cnt* tv, int64_t t_nn
             hipLaunchKernelGGL(k_gw_tstats<false>, sgrid(t_nnz), dim3(256), 0, s, G.tAp, G.tBp, G.tVp,
                                (long long)t_nnz, dch.p, trs.p, tnz.p, nullptr, nullptr);
     }
-    if (h_nnz > 0)
-        hipLaunchKernelGGL(k_gw_hstats, sgrid(h_nnz), dim3(256), 0, s, G.Rp, G.Cp, G.Vp, (long long)h_nnz, dblk.p,
-                           hbs.p, htot.p);
+    if (h_nnz > 0) {
+        const long long nb = std::min<long long>(8192, (h_nnz + 65535) / 65536);
+        const long long per = ((h_nnz + nb - 1) / nb + 255) / 256 * 256;
+        hipLaunchKernelGGL(k_gw_hstats, dim3((unsigned)((h_nnz + per - 1) / per)), dim3(256), 0, s, G.Rp, G.Cp, G.Vp,
+                           (long long)h_nnz, per, dblk.p, hbs.p, htot.p);
+    }
     HIP_CHECK(hipGetLastError());
     G.t_rowsum.resize(n);
     G.t_nnz_row.resize(n);
