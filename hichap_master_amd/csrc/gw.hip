@@ -205,11 +205,83 @@ __global__ __launch_bounds__(256) void k_gw_tstats(const int32_t* __restrict__ a
 constexpr int kTsWin = 8192;
 constexpr int kStItems = 8;
 constexpr int kStChunk = 256 * kStItems;
+
+// CHECK: the statistics kernels also validate their table (k_gw_check's
+// rules and codes: range, upper triangle, (row, col) order, duplicates,
+// negative counts; first offending entry per code), so an int32 device table
+// is read once instead of twice.  Every address they form is clamped to the
+// table's ids, so invalid input yields garbage statistics but no stray
+// access, and gw_create throws before using them.  The previous entry of a
+// wave's first lane is a scalar load (wave-uniform address).
+__device__ __forceinline__ int gw_code(int32_t x, int32_t y, uint32_t cnt, int32_t px, int32_t py, bool has_prev,
+                                       long long nb, bool upper) {
+    if (x < 0 || y < 0 || x >= nb || y >= nb) return 1;
+    if (upper && x > y) return 2;
+    if (has_prev) {
+        if (px > x || (px == x && py > y)) return 3;
+        if (px == x && py == y) return 4;
+    }
+    return (int32_t)cnt < 0 ? 5 : 0;
+}
+
+struct StCheck {
+    unsigned long long* errs;  // 5 codes: first offending entry (atomicMin)
+    unsigned* vmax;            // largest count (H only), or nullptr
+    long long* hptr;           // H row pointers (nb + 1), or nullptr
+};
+
+// Loads one chunk: each thread's kStItems entries (clamped to `last`) and,
+// with CHECK, validates the ones inside the run.  Returns the thread's
+// largest count seen (CHECK).
+template <bool CHECK>
+__device__ __forceinline__ unsigned st_load(const int32_t* __restrict__ a, const int32_t* __restrict__ b,
+                                            const uint32_t* __restrict__ v, long long c0, long long last, long long nb,
+                                            bool upper, int32_t* xs, int32_t* ys, uint32_t* cs, StCheck ck,
+                                            int32_t* pxs) {
+    int32_t pys[kStItems];
+    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+#pragma unroll
+    for (int k = 0; k < kStItems; ++k) {
+        const long long i = std::min(c0 + k * 256 + threadIdx.x, last);
+        xs[k] = a[i];
+        ys[k] = b[i];
+        cs[k] = v[i];
+        if (CHECK) {
+            const long long j = std::min(std::max(c0 + k * 256 + wv * 64 - 1, 0LL), last);
+            pxs[k] = a[j];
+            pys[k] = b[j];
+        }
+    }
+    unsigned mx = 0u;
+    if (CHECK) {
+        const int lane = threadIdx.x & 63;
+#pragma unroll
+        for (int k = 0; k < kStItems; ++k) {
+            const long long i = c0 + k * 256 + threadIdx.x;
+            const int32_t upx = __shfl_up(xs[k], 1, 64), upy = __shfl_up(ys[k], 1, 64);
+            const int32_t px = lane ? upx : pxs[k], py = lane ? upy : pys[k];
+            const int code = i <= last ? gw_code(xs[k], ys[k], cs[k], px, py, i > 0, nb, upper) : 0;
+            if (code) atomicMin(ck.errs + code - 1, (unsigned long long)i);
+            else if (i <= last) mx = max(mx, cs[k]);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < kStItems; ++k)  // past the run: count 0 (clamped duplicates of the last entry)
+        cs[k] &= 0u - (uint32_t)(c0 + k * 256 + threadIdx.x <= last);
+    return mx;
+}
+
+__device__ __forceinline__ int32_t clamp_id(int32_t x, long long nb) {
+    return (int32_t)std::min<long long>(std::max<int32_t>(x, 0), nb - 1);
+}
+__device__ __forceinline__ bool ok_id(int32_t x, long long nb) { return x >= 0 && x < nb; }
+
+template <bool CHECK>
 __global__ __launch_bounds__(256) void k_gw_tstats_win(const int32_t* __restrict__ a, const int32_t* __restrict__ b,
                                                        const uint32_t* __restrict__ v, long long nnz, long long per,
                                                        long long n, const int2* __restrict__ cbd,
                                                        unsigned long long* __restrict__ rpk,
-                                                       unsigned long long* __restrict__ total) {
+                                                       unsigned long long* __restrict__ total, StCheck ck) {
     __shared__ unsigned long long win[kTsWin];
     __shared__ unsigned long long wsum[4];
     const long long p0 = (long long)blockIdx.x * per;
@@ -224,18 +296,11 @@ __global__ __launch_bounds__(256) void k_gw_tstats_win(const int32_t* __restrict
         const int32_t xf = a[c0], xl = a[last];
         int32_t xs[kStItems], ys[kStItems];
         uint32_t cs[kStItems];
-#pragma unroll
-        for (int k = 0; k < kStItems; ++k) {
-            const long long i = std::min(c0 + k * 256 + threadIdx.x, last);
-            xs[k] = a[i];
-            ys[k] = b[i];
-            cs[k] = v[i];
-        }
-#pragma unroll
-        for (int k = 0; k < kStItems; ++k)  // past the run: count 0 (clamped duplicates of the last pixel)
-            cs[k] &= 0u - (uint32_t)(c0 + k * 256 + threadIdx.x <= last);
+        int32_t pxs[kStItems];
+        st_load<CHECK>(a, b, v, c0, last, n, true, xs, ys, cs, ck, pxs);
         if (xf == xl) {
-            const int2 bd = cbd[xf];
+            const bool okx = ok_id(xf, n);
+            const int2 bd = cbd[clamp_id(xf, n)];
             unsigned long long racc = 0;
 #pragma unroll
             for (int k = 0; k < kStItems; ++k) {
@@ -247,28 +312,28 @@ __global__ __launch_bounds__(256) void k_gw_tstats_win(const int32_t* __restrict
                     racc += pk;
                     if (xf != y) {
                         const long long d = (long long)y - x0;
-                        if (d < kTsWin) atomicAdd(&win[d], pk);
+                        if (d >= 0 && d < kTsWin) atomicAdd(&win[d], pk);
                         else atomicAdd(rpk + y, pk);
                     }
                 }
             }
             racc = (unsigned long long)wave_sum_ll((long long)racc);
-            if ((threadIdx.x & 63) == 0 && racc) atomicAdd(rpk + xf, racc);
+            if ((threadIdx.x & 63) == 0 && racc && okx) atomicAdd(rpk + xf, racc);
         } else {
             int2 bds[kStItems];
 #pragma unroll
-            for (int k = 0; k < kStItems; ++k) bds[k] = cbd[xs[k]];
+            for (int k = 0; k < kStItems; ++k) bds[k] = cbd[clamp_id(xs[k], n)];
 #pragma unroll
             for (int k = 0; k < kStItems; ++k) {
                 const uint32_t cc = cs[k];
                 const int32_t x = xs[k], y = ys[k];
                 t += cc;
                 unsigned long long pk = 0;
-                if (cc != 0u && in_block(bds[k], y)) {
+                if (cc != 0u && ok_id(x, n) && in_block(bds[k], y)) {
                     pk = ((unsigned long long)cc << 24) | 1ull;
                     if (x != y) {
                         const long long d = (long long)y - x0;
-                        if (d < kTsWin) atomicAdd(&win[d], pk);
+                        if (d >= 0 && d < kTsWin) atomicAdd(&win[d], pk);
                         else atomicAdd(rpk + y, pk);
                     }
                 }
@@ -293,33 +358,44 @@ __global__ __launch_bounds__(256) void k_gw_tstats_win(const int32_t* __restrict
 // H row sums within the same-chromosome same-haplotype block (H sorted by
 // row: segmented), and sum(H).  A block walks a contiguous run in chunks as
 // k_gw_tstats_win does (batched clamped loads; a one-row chunk sums in
-// registers).
+// registers).  CHECK: validates H too and records its largest count.
+template <bool CHECK>
 __global__ __launch_bounds__(256) void k_gw_hstats(const int32_t* __restrict__ r, const int32_t* __restrict__ c,
                                                    const uint32_t* __restrict__ v, long long nnz, long long per,
-                                                   const int2* __restrict__ bbd,
+                                                   long long nb, const int2* __restrict__ bbd,
                                                    unsigned long long* __restrict__ bsum,
-                                                   unsigned long long* __restrict__ total) {
+                                                   unsigned long long* __restrict__ total, StCheck ck) {
     __shared__ unsigned long long wsum[4];
+    __shared__ unsigned wmx[4];
     const long long p0 = (long long)blockIdx.x * per;
     if (p0 >= nnz) return;  // block-uniform
     const long long p1 = std::min(nnz, p0 + per);
     unsigned long long t = 0;
+    unsigned mx = 0u;
     for (long long c0 = p0; c0 < p1; c0 += kStChunk) {
         const long long last = std::min(c0 + kStChunk, p1) - 1;
         const int32_t xf = r[c0], xl = r[last];
         int32_t xs[kStItems], ys[kStItems];
         uint32_t cs[kStItems];
+        int32_t pxs[kStItems];
+        mx = max(mx, st_load<CHECK>(r, c, v, c0, last, nb, false, xs, ys, cs, ck, pxs));
+        if (CHECK) {  // H row pointers (k_px_rowptr_gw's rule): ptr[q] = first entry with row >= q
+            const int lane = threadIdx.x & 63;
 #pragma unroll
-        for (int k = 0; k < kStItems; ++k) {
-            const long long i = std::min(c0 + k * 256 + threadIdx.x, last);
-            xs[k] = r[i];
-            ys[k] = c[i];
-            cs[k] = v[i];
+            for (int k = 0; k < kStItems; ++k) {
+                const long long i = c0 + k * 256 + threadIdx.x;
+                const int32_t up = __shfl_up(xs[k], 1, 64);
+                const long long prev = i == 0 ? -1 : (long long)(lane ? up : pxs[k]);
+                const long long cur = xs[k];
+                if (i <= last && prev < cur && cur < nb) {
+                    for (long long q = std::max(prev + 1, 0LL); q <= cur; ++q) ck.hptr[q] = i;
+                }
+                if (i == nnz - 1 && cur >= 0 && cur < nb)
+                    for (long long q = cur + 1; q <= nb; ++q) ck.hptr[q] = nnz;
+            }
         }
-#pragma unroll
-        for (int k = 0; k < kStItems; ++k) cs[k] &= 0u - (uint32_t)(c0 + k * 256 + threadIdx.x <= last);
         if (xf == xl) {
-            const int2 bd = bbd[xf];
+            const int2 bd = bbd[clamp_id(xf, nb)];
             unsigned long long racc = 0;
 #pragma unroll
             for (int k = 0; k < kStItems; ++k) {
@@ -327,24 +403,36 @@ __global__ __launch_bounds__(256) void k_gw_hstats(const int32_t* __restrict__ r
                 racc += in_block(bd, ys[k]) ? (unsigned long long)cs[k] : 0ull;
             }
             racc = (unsigned long long)wave_sum_ll((long long)racc);
-            if ((threadIdx.x & 63) == 0 && racc) atomicAdd(bsum + xf, racc);
+            if ((threadIdx.x & 63) == 0 && racc && ok_id(xf, nb)) atomicAdd(bsum + xf, racc);
         } else {
             int2 bds[kStItems];
 #pragma unroll
-            for (int k = 0; k < kStItems; ++k) bds[k] = bbd[xs[k]];
+            for (int k = 0; k < kStItems; ++k) bds[k] = bbd[clamp_id(xs[k], nb)];
 #pragma unroll
             for (int k = 0; k < kStItems; ++k) {
                 t += cs[k];
-                seg_add_u64(xs[k], in_block(bds[k], ys[k]) ? (unsigned long long)cs[k] : 0ull, bsum);
+                seg_add_u64(xs[k], ok_id(xs[k], nb) && in_block(bds[k], ys[k]) ? (unsigned long long)cs[k] : 0ull,
+                            bsum);
             }
         }
     }
     t = (unsigned long long)wave_sum_ll((long long)t);
-    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = t;
+    if (CHECK) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) mx = max(mx, (unsigned)__shfl_xor((int)mx, o, 64));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        wsum[threadIdx.x >> 6] = t;
+        wmx[threadIdx.x >> 6] = mx;
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
         const unsigned long long bt = wsum[0] + wsum[1] + wsum[2] + wsum[3];
         if (bt) atomicAdd(total, bt);
+        if (CHECK && ck.vmax) {
+            const unsigned m = max(max(wmx[0], wmx[1]), max(wmx[2], wmx[3]));
+            if (m) atomicMax(ck.vmax, m);
+        }
     }
 }
 
@@ -367,10 +455,17 @@ __global__ __launch_bounds__(256) void k_gw_colkeys(const int32_t* __restrict__ 
     const long long c0 = (long long)blockIdx.x * kColChunk;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     unsigned long long mk[kColItems];
+    int32_t rr[kColItems], cc[kColItems];
+#pragma unroll
+    for (int k = 0; k < kColItems; ++k) {  // loads issued together (clamped; the tail masked below)
+        const long long i = std::min(c0 + (long long)k * 256 + threadIdx.x, nnz - 1);
+        rr[k] = r[i];
+        cc[k] = c[i];
+    }
 #pragma unroll
     for (int k = 0; k < kColItems; ++k) {
         const long long i = c0 + (long long)k * 256 + threadIdx.x;
-        mk[k] = __ballot(i < nnz && r[i] != c[i]);
+        mk[k] = __ballot((i < nnz) & (rr[k] != cc[k]));
         if (lane == 0) wcnt[k][wave] = (unsigned)__popcll(mk[k]);
     }
     __syncthreads();
@@ -385,6 +480,11 @@ __global__ __launch_bounds__(256) void k_gw_colkeys(const int32_t* __restrict__ 
         if (PASS == 0) cnt_or_base[blockIdx.x] = tot;
     }
     if (PASS == 0) return;
+    uint32_t vv[kColItems];
+    if (fmt) {
+#pragma unroll
+        for (int k = 0; k < kColItems; ++k) vv[k] = v[std::min(c0 + (long long)k * 256 + threadIdx.x, nnz - 1)];
+    }
     __syncthreads();
     const unsigned long long base = (unsigned long long)cnt_or_base[blockIdx.x];
 #pragma unroll
@@ -392,8 +492,8 @@ __global__ __launch_bounds__(256) void k_gw_colkeys(const int32_t* __restrict__ 
         if (!((mk[k] >> lane) & 1ull)) continue;
         const long long i = c0 + (long long)k * 256 + threadIdx.x;
         keys[base + wcnt[k][wave] + __popcll(mk[k] & ((1ull << lane) - 1ull))] =
-            fmt ? ((unsigned long long)c[i] << 44) | ((unsigned long long)r[i] << 24) | (unsigned long long)v[i]
-                : ((unsigned long long)c[i] << ib) | (unsigned long long)i;
+            fmt ? ((unsigned long long)cc[k] << 44) | ((unsigned long long)rr[k] << 24) | (unsigned long long)vv[k]
+                : ((unsigned long long)cc[k] << ib) | (unsigned long long)i;
     }
 }
 
@@ -455,7 +555,12 @@ struct GwDev {
 
 // per row r (one wave): rowsum(S)_r and the off-diagonal column sum of S in
 // column r, in list order (fixed xor-tree per chunk): the symmetric marginal
-// of Y; u/l starts for the merge
+// of Y; u/l starts for the merge.  Round 4: kMargWin windows of 64 per step,
+// their loads issued together from clamped addresses (out-of-row lanes
+// weighted 0: the same per-window sums in the same order), and the starts
+// counted on the way (cells left of the diagonal, list rows <= r) instead of
+// two serial binary searches by lane 0 (~25 dependent loads per row).
+constexpr int kMargWin = 4;
 template <int FMT>
 __global__ __launch_bounds__(256) void k_gw_marg(GwDev g, double exponent, double* __restrict__ s_out) {
     const long long r = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -464,29 +569,47 @@ __global__ __launch_bounds__(256) void k_gw_marg(GwDev g, double exponent, doubl
     const long long h0 = g.hptr[r], h1 = g.hptr[r + 1];
     double acc = 0.0;
     const double ar = g.alpha[r];
-    for (long long q0 = h0; q0 < h1; q0 += 64) {
-        const long long q = q0 + lane;
-        double x = q < h1 ? (double)g.V[q] / ar : 0.0;
-        acc += wave_sum(x);
+    long long nlo = 0;
+    for (long long q0 = h0; q0 < h1; q0 += 64 * kMargWin) {
+        uint32_t vv[kMargWin];
+        int32_t cc[kMargWin];
+#pragma unroll
+        for (int u = 0; u < kMargWin; ++u) {
+            const long long q = std::min(q0 + u * 64 + lane, h1 - 1);
+            vv[u] = g.V[q];
+            cc[u] = g.C[q];
+        }
+#pragma unroll
+        for (int u = 0; u < kMargWin; ++u) {
+            const bool in = q0 + u * 64 + lane < h1;
+            acc += wave_sum((double)vv[u] / ar * (in ? 1.0 : 0.0));
+            nlo += __popcll(__ballot(in & (cc[u] < (int32_t)r)));
+        }
     }
     const long long c0 = g.cptr[r], c1 = g.cptr[r + 1];
     double acc2 = 0.0;
-    for (long long q0 = c0; q0 < c1; q0 += 64) {
-        const long long q = q0 + lane;
-        double x = 0.0;
-        if (q < c1) {
-            const unsigned long long e = g.lrv[q];
-            x = lrv_val<FMT>(e) / g.alpha[lrv_row<FMT>(e)];
+    long long nle = 0;
+    for (long long q0 = c0; q0 < c1; q0 += 64 * kMargWin) {
+        unsigned long long e[kMargWin];
+        double al[kMargWin];
+#pragma unroll
+        for (int u = 0; u < kMargWin; ++u) e[u] = g.lrv[std::min(q0 + u * 64 + lane, c1 - 1)];
+#pragma unroll
+        for (int u = 0; u < kMargWin; ++u) al[u] = g.alpha[lrv_row<FMT>(e[u])];
+#pragma unroll
+        for (int u = 0; u < kMargWin; ++u) {
+            const bool in = q0 + u * 64 + lane < c1;
+            acc2 += wave_sum(lrv_val<FMT>(e[u]) / al[u] * (in ? 1.0 : 0.0));
+            nle += __popcll(__ballot(in & (lrv_row<FMT>(e[u]) <= (int32_t)r)));
         }
-        acc2 += wave_sum(x);
     }
     if (lane == 0) {
         const double m = acc + acc2;
         double sv = pow(m, exponent);
         if (sv == 0.0) sv = 1.0;
         s_out[r] = sv;
-        g.ustart[r] = lower_bound_i32(g.C, h0, h1, (int32_t)r);
-        g.lstart[r] = lower_bound_keyrow<FMT>(g.lrv, c0, c1, (int32_t)(r + 1));
+        g.ustart[r] = h0 + nlo;  // first cell with col >= r (the row is sorted)
+        g.lstart[r] = c0 + nle;  // first list entry with row > r
     }
 }
 
@@ -651,6 +774,15 @@ struct GwClock {
     }
 };
 
+// the first offending entry over the five codes (k_gw_check / gw_code)
+void throw_first_error(const unsigned long long* he, const char* what) {
+    int code = -1;
+    unsigned long long at = ~0ull;
+    for (int q = 0; q < 5; ++q)
+        if (he[q] < at) { at = he[q]; code = q; }
+    if (code >= 0) HH_THROW(HH_ERR_ARG, std::string(what) + ": " + kErrWhat[code] + " at entry " + std::to_string(at));
+}
+
 // Validate a table (range, order, uniqueness, counts); COPY: convert it into
 // int32 / uint32 device arrays (host or int64 tables), else it is used in
 // place (int32 device tables).  Returns the largest count.
@@ -685,11 +817,7 @@ unsigned gw_check(const Id* r, const Id* c, const Cnt* v, int64_t nnz, int64_t n
     std::memcpy(he, pin, sizeof(he));
     std::memcpy(&mx, pin + 48, sizeof(mx));
     ck.lap("check: sync");
-    int code = -1;
-    unsigned long long at = ~0ull;
-    for (int q = 0; q < 5; ++q)
-        if (he[q] < at) { at = he[q]; code = q; }
-    if (code >= 0) HH_THROW(HH_ERR_ARG, std::string(what) + ": " + kErrWhat[code] + " at entry " + std::to_string(at));
+    throw_first_error(he, what);
     return mx;
 }
 
@@ -782,7 +910,12 @@ void gw_create(hh_gw& G, const Id* t1, const Id* t2, const Cnt* tv, int64_t t_nn
     constexpr bool COPY = !(std::is_same<Id, int32_t>::value && std::is_same<Cnt, int32_t>::value);
     clk.lap("setup");
     unsigned hmax = 0;
-    {
+    const bool tpack = n < (1LL << 24);
+    // int32 device tables: validated by the statistics kernels themselves
+    // (one read of each table instead of two); the others are converted and
+    // validated first
+    const bool fused = !COPY && tpack;
+    if (!fused) {
         HH_KTIME("gw_check", s);
         gw_check<Id, Cnt, COPY>(t1, t2, tv, t_nnz, n, 1, G.tA, G.tB, G.tV, "traditional table", s);
         hmax = gw_check<Id, Cnt, COPY>(hr, hc, hv, h_nnz, 2 * n, 0, G.R, G.C, G.V, "haplotype cells", s);
@@ -814,17 +947,26 @@ void gw_create(hh_gw& G, const Id* t1, const Id* t2, const Cnt* tv, int64_t t_nn
     hbs.zero(s);
     htot.zero(s);
     auto sgrid = [](int64_t nnz) { return dim3((unsigned)std::min<int64_t>(kGwStatBlocks, (nnz + 255) / 256)); };
-    const bool tpack = n < (1LL << 24);
     DBuf<unsigned long long> tpk(tpack ? n : 1), ttot(1);
     if (tpack) tpk.zero(s);
     ttot.zero(s);
+    DBuf<unsigned long long> errs(10);
+    DBuf<unsigned> vmx(1);
+    HIP_CHECK(hipMemsetAsync(errs.p, 0xff, 10 * sizeof(unsigned long long), s));
+    vmx.zero(s);
+    G.hptr.alloc(2 * n + 1);
+    const StCheck ckT{errs.p, nullptr, nullptr}, ckH{errs.p + 5, vmx.p, G.hptr.p};
     HH_KTIME("gw_stats_to_end", s);  // (from the statistics to the end of create)
     if (t_nnz > 0) {
         if (tpack) {
             const long long nb = std::min<long long>(8192, (t_nnz + 65535) / 65536);
             const long long per = ((t_nnz + nb - 1) / nb + 255) / 256 * 256;
-            hipLaunchKernelGGL(k_gw_tstats_win, dim3((unsigned)((t_nnz + per - 1) / per)), dim3(256), 0, s, G.tAp,
-                               G.tBp, G.tVp, (long long)t_nnz, per, (long long)n, dch.p, tpk.p, ttot.p);
+            if (fused)
+                hipLaunchKernelGGL(k_gw_tstats_win<true>, dim3((unsigned)((t_nnz + per - 1) / per)), dim3(256), 0, s,
+                                   G.tAp, G.tBp, G.tVp, (long long)t_nnz, per, (long long)n, dch.p, tpk.p, ttot.p, ckT);
+            else
+                hipLaunchKernelGGL(k_gw_tstats_win<false>, dim3((unsigned)((t_nnz + per - 1) / per)), dim3(256), 0, s,
+                                   G.tAp, G.tBp, G.tVp, (long long)t_nnz, per, (long long)n, dch.p, tpk.p, ttot.p, ckT);
         }
         else
             hipLaunchKernelGGL(k_gw_tstats<false>, sgrid(t_nnz), dim3(256), 0, s, G.tAp, G.tBp, G.tVp,
@@ -833,16 +975,21 @@ void gw_create(hh_gw& G, const Id* t1, const Id* t2, const Cnt* tv, int64_t t_nn
     if (h_nnz > 0) {
         const long long nb = std::min<long long>(8192, (h_nnz + 65535) / 65536);
         const long long per = ((h_nnz + nb - 1) / nb + 255) / 256 * 256;
-        hipLaunchKernelGGL(k_gw_hstats, dim3((unsigned)((h_nnz + per - 1) / per)), dim3(256), 0, s, G.Rp, G.Cp, G.Vp,
-                           (long long)h_nnz, per, dblk.p, hbs.p, htot.p);
+        if (fused)
+            hipLaunchKernelGGL(k_gw_hstats<true>, dim3((unsigned)((h_nnz + per - 1) / per)), dim3(256), 0, s, G.Rp,
+                               G.Cp, G.Vp, (long long)h_nnz, per, (long long)(2 * n), dblk.p, hbs.p, htot.p, ckH);
+        else
+            hipLaunchKernelGGL(k_gw_hstats<false>, dim3((unsigned)((h_nnz + per - 1) / per)), dim3(256), 0, s, G.Rp,
+                               G.Cp, G.Vp, (long long)h_nnz, per, (long long)(2 * n), dblk.p, hbs.p, htot.p, ckH);
     }
     HIP_CHECK(hipGetLastError());
     G.t_rowsum.resize(n);
     G.t_nnz_row.resize(n);
     G.h_blocksum.resize(2 * n);
     {
-        // pinned layout: t_rowsum n | t_nnz n | h_blocksum 2n | h_total | t_total | packed n
-        unsigned long long* pin = (unsigned long long*)pinned_stage().get(0, ((size_t)5 * n + 2) * 8);
+        // pinned layout: t_rowsum n | t_nnz n | h_blocksum 2n | h_total | t_total | packed n | errs 10 | vmax
+        unsigned long long* pin = (unsigned long long*)pinned_stage().get(0, ((size_t)5 * n + 13) * 8);
+        unsigned long long* p_err = pin + 5 * n + 2;
         unsigned long long *p_trs = pin, *p_tnz = pin + n, *p_hbs = pin + 2 * n, *p_htot = pin + 4 * n,
                            *p_ttot = pin + 4 * n + 1, *p_pk = pin + 4 * n + 2;
         const bool packed = tpack && t_nnz > 0;
@@ -854,7 +1001,16 @@ void gw_create(hh_gw& G, const Id* t1, const Id* t2, const Cnt* tv, int64_t t_nn
             ttot.download(p_ttot, 1, s);
             tpk.download(p_pk, n, s);
         }
+        if (fused) {
+            errs.download(p_err, 10, s);
+            vmx.download((unsigned*)(p_err + 10), 1, s);
+        }
         HIP_CHECK(hipStreamSynchronize(s));
+        if (fused) {
+            throw_first_error(p_err, "traditional table");
+            throw_first_error(p_err + 5, "haplotype cells");
+            hmax = *(const unsigned*)(p_err + 10);
+        }
         std::copy(p_trs, p_trs + n, G.t_rowsum.begin());
         std::copy(p_tnz, p_tnz + n, G.t_nnz_row.begin());
         std::copy(p_hbs, p_hbs + 2 * n, G.h_blocksum.begin());
@@ -891,13 +1047,12 @@ void gw_create(hh_gw& G, const Id* t1, const Id* t2, const Cnt* tv, int64_t t_nn
             std::fill(G.alpha_ok.begin(), G.alpha_ok.end(), 0);
         }
     });
-    // H row pointers and column lists
-    G.hptr.alloc(2 * n + 1);
-    if (h_nnz > 0)
+    // H row pointers (unless the fused statistics wrote them) and column lists
+    if (h_nnz == 0)
+        HIP_CHECK(hipMemsetAsync(G.hptr.p, 0, (2 * n + 1) * sizeof(long long), s));
+    else if (!fused)
         hipLaunchKernelGGL(k_px_rowptr_gw, dim3((unsigned)((h_nnz + 1 + 255) / 256)), dim3(256), 0, s, G.Rp,
                            (long long)h_nnz, (long long)(2 * n), G.hptr.p);
-    else
-        HIP_CHECK(hipMemsetAsync(G.hptr.p, 0, (2 * n + 1) * sizeof(long long), s));
     int cbits = 1;
     while (cbits < 40 && ((int64_t)1 << cbits) < 2 * n) ++cbits;
     // packed keys (col | row | count) when ids fit 20 bits and counts 24

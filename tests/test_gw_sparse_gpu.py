@@ -124,6 +124,53 @@ def test_device_tables_and_errors(mb):
         mb.GenomeWideMatrixCorrectionSparse(bins, bad, tp, hc)
 
 
+def test_device_tables_validated_by_statistics_kernels(mb):
+    """int32 device tables are validated inside the statistics kernels (no
+    separate check pass): every error code, in either table, is reported with
+    the same message and entry as the host tables' separate check, including
+    errors at a chunk's first lane and the first entry."""
+    import torch
+    from hichap_master_amd._lib import HipLibraryError
+    rng = np.random.default_rng(21)
+    sizes = [900, 700]
+    n = sum(sizes)
+    T = np.triu(rng.poisson(0.4, size=(n, n)))
+    H = rng.poisson(0.25, size=(2 * n, 2 * n))
+    bins, hbins = _layout(["1", "2"], sizes)
+    tp, hc = _tables(T, H)
+    assert tp[0].size > 40000 and hc[0].size > 100000  # several chunks per block
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=np.int32)).cuda()
+
+    def msg(tabs_t, tabs_h, dev):
+        conv = (lambda x: [t(a) for a in x]) if dev else (lambda x: [np.asarray(a, dtype=np.int64) for a in x])
+        with pytest.raises(HipLibraryError) as e:
+            mb.GenomeWideMatrixCorrectionSparse(bins, hbins, conv(tabs_t), conv(tabs_h))
+        return str(e.value)
+
+    cases = []
+    for which, (r, c, v), nb in (("T", tp, n), ("H", hc, 2 * n)):
+        m = r.size
+        for at in (0, 2048, 2047 + 64, m // 2 + 1, m - 1):
+            for kind in ("range", "order", "dup", "neg") + (("upper",) if which == "T" else ()):
+                rr, cc, vv = (np.array(x, dtype=np.int64) for x in (r, c, v))
+                if kind == "range":
+                    cc[at] = nb
+                elif kind == "neg":
+                    vv[at] = -3
+                elif kind == "upper":
+                    rr[at], cc[at] = cc[at] + 1, rr[at]
+                elif at > 0:
+                    rr[at], cc[at] = rr[at - 1], cc[at - 1] - (kind == "order")
+                else:
+                    continue
+                cases.append((which, (rr, cc, vv)))
+    for which, bad in cases:
+        tt, hh = (bad, hc) if which == "T" else (tp, bad)
+        m_host, m_dev = msg(tt, hh, False), msg(tt, hh, True)
+        # the same text after the entry point's name (hh_gw_create vs hh_gw_create_device)
+        assert m_host.split(": ", 1)[1] == m_dev.split(": ", 1)[1], (which, m_host, m_dev)
+
+
 def test_default_wholeres_matches_dense(mb):
     """500 kb diploid hg19 (2n = 12 174): sparse == oracle (dense)."""
     from tests.test_fullsize_gpu import _diploid_inputs
