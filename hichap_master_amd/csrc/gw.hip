@@ -436,67 +436,11 @@ __global__ __launch_bounds__(256) void k_gw_hstats(const int32_t* __restrict__ r
     }
 }
 
-// off-diagonal cells keyed by column: (col << ib) | index.  One block per
-// kColChunk cells; PASS 0 counts the block's keys, PASS 1 writes them at the
-// scanned base in cell order, so the keys arrive in index order and the sort
-// orders only the column bits (stable: 3 radix passes instead of 7).
-constexpr int kColItems = 16;
-constexpr int kColChunk = 256 * kColItems;
-// FMT 1 (ids < 2^20, counts < 2^24): the key IS the packed cell, col << 44 |
-// row << 24 | count, and the sort orders its column bits (the cells arrive in
-// row order, the sort is stable): no index, no gather afterwards.  FMT 0:
-// col << ib | index, then k_gw_pack.
-template <int PASS>
-__global__ __launch_bounds__(256) void k_gw_colkeys(const int32_t* __restrict__ r, const int32_t* __restrict__ c,
-                                                    const uint32_t* __restrict__ v, int fmt,
-                                                    long long nnz, int ib, unsigned long long* __restrict__ keys,
-                                                    long long* __restrict__ cnt_or_base) {
-    __shared__ unsigned wcnt[kColItems][4];
-    const long long c0 = (long long)blockIdx.x * kColChunk;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    unsigned long long mk[kColItems];
-    int32_t rr[kColItems], cc[kColItems];
-#pragma unroll
-    for (int k = 0; k < kColItems; ++k) {  // loads issued together (clamped; the tail masked below)
-        const long long i = std::min(c0 + (long long)k * 256 + threadIdx.x, nnz - 1);
-        rr[k] = r[i];
-        cc[k] = c[i];
-    }
-#pragma unroll
-    for (int k = 0; k < kColItems; ++k) {
-        const long long i = c0 + (long long)k * 256 + threadIdx.x;
-        mk[k] = __ballot((i < nnz) & (rr[k] != cc[k]));
-        if (lane == 0) wcnt[k][wave] = (unsigned)__popcll(mk[k]);
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned tot = 0;
-        for (int k = 0; k < kColItems; ++k)
-            for (int w = 0; w < 4; ++w) {
-                const unsigned n = wcnt[k][w];
-                wcnt[k][w] = tot;
-                tot += n;
-            }
-        if (PASS == 0) cnt_or_base[blockIdx.x] = tot;
-    }
-    if (PASS == 0) return;
-    uint32_t vv[kColItems];
-    if (fmt) {
-#pragma unroll
-        for (int k = 0; k < kColItems; ++k) vv[k] = v[std::min(c0 + (long long)k * 256 + threadIdx.x, nnz - 1)];
-    }
-    __syncthreads();
-    const unsigned long long base = (unsigned long long)cnt_or_base[blockIdx.x];
-#pragma unroll
-    for (int k = 0; k < kColItems; ++k) {
-        if (!((mk[k] >> lane) & 1ull)) continue;
-        const long long i = c0 + (long long)k * 256 + threadIdx.x;
-        keys[base + wcnt[k][wave] + __popcll(mk[k] & ((1ull << lane) - 1ull))] =
-            fmt ? ((unsigned long long)cc[k] << 44) | ((unsigned long long)rr[k] << 24) | (unsigned long long)vv[k]
-                : ((unsigned long long)cc[k] << ib) | (unsigned long long)i;
-    }
-}
-
+// Column lists: H's off-diagonal cells keyed by column and sorted stably by
+// the column bits (dev_sort_cells_by_col, pairs.hip; keys formed in its first
+// radix pass).  FMT 1 (ids < 2^20, counts < 2^24): the key IS the packed
+// cell, col << 44 | row << 24 | count (no index, no gather afterwards).
+// FMT 0: col << ib | index, then k_gw_pack.
 // column-list entry -> (row, count): FMT 0 row | count << 32 (after
 // k_gw_pack), FMT 1 the packed sort key col << 44 | row << 24 | count
 template <int FMT>
@@ -741,7 +685,7 @@ struct hh_gw {
     DBuf<uint32_t> tV, V;
     const int32_t *tAp = nullptr, *tBp = nullptr, *Rp = nullptr, *Cp = nullptr;
     const uint32_t *tVp = nullptr, *Vp = nullptr;
-    int fmt = 0;  // column-list entry format (k_gw_colkeys)
+    int fmt = 0;  // column-list entry format (RsCells, pairs.hip)
     DBuf<long long> hptr, cptr;
     DBuf<unsigned long long> keys;  // column-sorted cells, (row, count) packed after hh_gw_create
     int ib = 1;
@@ -1065,27 +1009,15 @@ void gw_create(hh_gw& G, const Id* t1, const Id* t2, const Cnt* tv, int64_t t_nn
     }
     HH_REQUIRE(G.ib + cbits <= 64, "haplotype matrix too large for 64-bit column keys");
     G.keys.alloc(std::max<int64_t>(h_nnz, 1));
-    unsigned long long hn = 0;
-    if (h_nnz > 0) {
-        const long long nblk = (h_nnz + kColChunk - 1) / kColChunk;
-        DBuf<long long> bcnt(nblk + 1), bbase(nblk + 1);
-        DBuf<unsigned long long> ntot(1);
-        HIP_CHECK(hipMemsetAsync(bcnt.p + nblk, 0, sizeof(long long), s));
-        hipLaunchKernelGGL(k_gw_colkeys<0>, dim3((unsigned)nblk), dim3(256), 0, s, G.Rp, G.Cp, G.Vp, G.fmt,
-                           (long long)h_nnz, G.ib, G.keys.p, bcnt.p);
-        dev_excl_scan_i64(bcnt.p, bbase.p, nblk + 1, ntot.p, s);
-        hipLaunchKernelGGL(k_gw_colkeys<1>, dim3((unsigned)nblk), dim3(256), 0, s, G.Rp, G.Cp, G.Vp, G.fmt,
-                           (long long)h_nnz, G.ib, G.keys.p, bbase.p);
-        HIP_CHECK(hipGetLastError());
-        ntot.download(&hn, 1, s);
-        HIP_CHECK(hipStreamSynchronize(s));
-    }
-    clk.lap("column keys");
-    G.n_keys = (int64_t)hn;
     {
         HH_KTIME("gw_sort", s);
-        dev_sort_u64(G.keys, G.n_keys, cbits, s, G.ib);  // keys in index order: only the column bits
+        // the column keys are formed inside the first radix pass (in cell
+        // order, so only the column bits are sorted); were a count pass, a
+        // key write pass and a full first pass over the written keys
+        G.n_keys = dev_sort_cells_by_col(G.Rp, G.Cp, G.Vp, h_nnz, G.fmt, G.ib, cbits, G.keys, s);
     }
+    const unsigned long long hn = (unsigned long long)G.n_keys;
+    clk.lap("column keys + sort");
     G.cptr.alloc(2 * n + 1);
     hipLaunchKernelGGL(k_px_keyptr_gw, dim3((unsigned)((hn + 1 + 255) / 256)), dim3(256), 0, s, G.keys.p,
                        (long long)hn, G.ib, (long long)(2 * n), G.cptr.p);

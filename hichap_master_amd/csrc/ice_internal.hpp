@@ -299,6 +299,8 @@ void upload_plan(const TilePlan& P, hh_matrix& m, hipStream_t s);
 // stable LSD radix sort of the key bits [lo_bit, lo_bit + bits) (keys whose
 // lower bits are already in order -- an index -- need only the upper ones)
 void dev_sort_u64(DBuf<unsigned long long>& keys, int64_t n, int bits, hipStream_t s, int lo_bit = 0);
+int64_t dev_sort_cells_by_col(const int32_t* r, const int32_t* c, const uint32_t* v, int64_t nnz, int fmt, int ib,
+                              int cbits, DBuf<unsigned long long>& keys, hipStream_t s);
 void dev_excl_scan_i64(const long long* in, long long* out, long long n, unsigned long long* total_dev, hipStream_t s);
 // Device build from a host pixel table (build.hip); false = not a sorted
 // upper-triangle table (nothing built).  g_host_build forces the host builder.

@@ -886,12 +886,48 @@ __global__ void k_count_nl(TextView tv, long long upto, unsigned long long* __re
 }
 
 // ------------------------------------------------------------ radix sort
+// Key sources of a pass: entry i of the input -> (key, valid).  Loads are
+// unconditional from clamped addresses (a conditional load compiles to one
+// round trip each).
+struct RsKeys {  // a key array
+    const unsigned long long* k;
+    long long n;
+    __device__ __forceinline__ void get(long long i, unsigned long long& key, bool& ok) const {
+        key = k[i < n ? i : n - 1];
+        ok = i < n;
+    }
+};
+// H's off-diagonal cells keyed by column (the genome-wide correction's
+// column lists, gw.hip): fmt 1 the packed cell col << 44 | row << 24 | count,
+// fmt 0 col << ib | index.  Diagonal cells are not keys.
+struct RsCells {
+    const int32_t* r;
+    const int32_t* c;
+    const uint32_t* v;
+    long long n;
+    int fmt, ib;
+    __device__ __forceinline__ void get(long long i, unsigned long long& key, bool& ok) const {
+        const long long q = i < n ? i : n - 1;
+        const int32_t rr = r[q], cc = c[q];
+        const uint32_t vv = v[q];
+        ok = (i < n) & (rr != cc);
+        // both forms, selected by mask: a `fmt ?` here became a branch per
+        // entry, which kept each entry's loads from issuing with the others
+        const unsigned long long k1 =
+            ((unsigned long long)cc << 44) | ((unsigned long long)rr << 24) | (unsigned long long)vv;
+        const unsigned long long k0 = ((unsigned long long)cc << (ib & 63)) | (unsigned long long)i;
+        const unsigned long long m = 0ull - (unsigned long long)(fmt != 0);
+        key = (k1 & m) | (k0 & ~m);
+    }
+};
+
 // Digit histogram of one 4096-key tile: each wave counts its 1 024 keys by
 // ballot matching into wave-private LDS counters (no LDS atomics: a skewed
 // digit -- the high bits of a row index -- serialised them), then the four
 // waves' counts are summed.
-__global__ __launch_bounds__(kScanThreads) void k_rs_hist(const unsigned long long* __restrict__ keys, long long n,
-                                                          int shift, long long n_tiles, unsigned* __restrict__ hist) {
+template <class Src>
+__global__ __launch_bounds__(kScanThreads) void k_rs_hist(Src src, int shift, long long n_tiles,
+                                                          unsigned* __restrict__ hist) {
     constexpr int NW = kScanThreads / 64;
     constexpr int PER = kScanTile / NW;
     __shared__ unsigned wcnt[NW][256];
@@ -900,15 +936,13 @@ __global__ __launch_bounds__(kScanThreads) void k_rs_hist(const unsigned long lo
     for (int k = 0; k < NW; ++k) wcnt[k][tid] = 0;
     const long long base = (long long)blockIdx.x * kScanTile;
     unsigned long long kv[kScanItems];
+    bool okv[kScanItems];
 #pragma unroll
-    for (int r = 0; r < kScanItems; ++r) {
-        const long long i = base + w * PER + r * 64 + lane;
-        kv[r] = i < n ? keys[i] : 0ull;
-    }
+    for (int r = 0; r < kScanItems; ++r) src.get(base + w * PER + r * 64 + lane, kv[r], okv[r]);
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < kScanItems; ++r) {
-        const bool v = base + w * PER + r * 64 + lane < n;
+        const bool v = okv[r];
         const unsigned d = (unsigned)((kv[r] >> shift) & 0xff);
         unsigned long long m = __ballot(v);
 #pragma unroll
@@ -931,8 +965,8 @@ __global__ __launch_bounds__(kScanThreads) void k_rs_hist(const unsigned long lo
 // barrier inside the ranking loop (round 1: three per step, 48 per tile).
 // Then one scan over (digit, wave) places the waves' runs in key order, the
 // tile is staged in LDS in digit order and written digit run by digit run.
-__global__ __launch_bounds__(kScanThreads) void k_rs_scatter(const unsigned long long* __restrict__ in,
-                                                             unsigned long long* __restrict__ out, long long n,
+template <class Src>
+__global__ __launch_bounds__(kScanThreads) void k_rs_scatter(Src src, unsigned long long* __restrict__ out,
                                                              int shift, long long n_tiles,
                                                              const unsigned* __restrict__ hist_off) {
     constexpr int NW = kScanThreads / 64;
@@ -944,21 +978,18 @@ __global__ __launch_bounds__(kScanThreads) void k_rs_scatter(const unsigned long
     __shared__ unsigned long long sh[4];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const long long base = (long long)blockIdx.x * kScanTile;
-    const int nvalid = (int)min((long long)kScanTile, n - base);
 #pragma unroll
     for (int k = 0; k < NW; ++k) wcnt[k][tid] = 0;
     unsigned long long kv[kScanItems];
+    bool okv[kScanItems];
 #pragma unroll
-    for (int r = 0; r < kScanItems; ++r) {
-        const int j = w * PER + r * 64 + lane;
-        kv[r] = j < nvalid ? in[base + j] : 0ull;
-    }
+    for (int r = 0; r < kScanItems; ++r) src.get(base + w * PER + r * 64 + lane, kv[r], okv[r]);
     __syncthreads();
     const unsigned long long lt = (1ull << lane) - 1ull;
     unsigned rk[kScanItems];
 #pragma unroll
     for (int r = 0; r < kScanItems; ++r) {
-        const bool v = w * PER + r * 64 + lane < nvalid;
+        const bool v = okv[r];
         const unsigned d = (unsigned)((kv[r] >> shift) & 0xff);
         unsigned long long m = __ballot(v);
 #pragma unroll
@@ -976,7 +1007,8 @@ __global__ __launch_bounds__(kScanThreads) void k_rs_scatter(const unsigned long
     unsigned tot = 0;
 #pragma unroll
     for (int k = 0; k < NW; ++k) tot += wcnt[k][tid];
-    const unsigned st = (unsigned)block_excl_scan_u64(tot, sh, nullptr);
+    unsigned long long nk = 0;  // the tile's keys
+    const unsigned st = (unsigned)block_excl_scan_u64(tot, sh, &nk);
     start[tid] = st;
     gofs_lo[tid] = hist_off[(long long)tid * n_tiles + blockIdx.x];
     {
@@ -991,12 +1023,11 @@ __global__ __launch_bounds__(kScanThreads) void k_rs_scatter(const unsigned long
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < kScanItems; ++r) {
-        const bool v = w * PER + r * 64 + lane < nvalid;
         const unsigned d = (unsigned)((kv[r] >> shift) & 0xff);
-        if (v) stage[wcnt[w][d] + rk[r]] = kv[r];
+        if (okv[r]) stage[wcnt[w][d] + rk[r]] = kv[r];
     }
     __syncthreads();
-    for (int j = tid; j < nvalid; j += kScanThreads) {
+    for (int j = tid; j < (int)nk; j += kScanThreads) {
         const unsigned long long key = stage[j];
         const unsigned d = (unsigned)((key >> shift) & 0xff);
         out[(long long)gofs_lo[d] + (j - (long long)start[d])] = key;
@@ -1365,14 +1396,14 @@ static void sort_keys(DBuf<unsigned long long>& keys, int64_t n, int bits, hipSt
     for (int shift = lo_bit; shift < lo_bit + bits; shift += 8, ++passes) {
         {
             HH_KTIME("k_rs_hist", s);
-            hipLaunchKernelGGL(k_rs_hist, dim3((unsigned)tiles), dim3(kScanThreads), 0, s, a, (long long)n, shift,
-                               tiles, hist.p);
+            hipLaunchKernelGGL(k_rs_hist<RsKeys>, dim3((unsigned)tiles), dim3(kScanThreads), 0, s,
+                               RsKeys{a, (long long)n}, shift, tiles, hist.p);
         }
         exclusive_scan<unsigned, unsigned>(hist.p, off.p, 256 * tiles, nullptr, s);
         {
             HH_KTIME("k_rs_scatter", s);
-            hipLaunchKernelGGL(k_rs_scatter, dim3((unsigned)tiles), dim3(kScanThreads), 0, s, a, b, (long long)n,
-                               shift, tiles, off.p);
+            hipLaunchKernelGGL(k_rs_scatter<RsKeys>, dim3((unsigned)tiles), dim3(kScanThreads), 0, s,
+                               RsKeys{a, (long long)n}, b, shift, tiles, off.p);
         }
         HIP_CHECK(hipGetLastError());
         std::swap(a, b);
@@ -1384,6 +1415,41 @@ static void sort_keys(DBuf<unsigned long long>& keys, int64_t n, int bits, hipSt
 // Shared with the device matrix build (build.hip, ice_internal.hpp).
 void dev_sort_u64(DBuf<unsigned long long>& keys, int64_t n, int bits, hipStream_t s, int lo_bit) {
     sort_keys(keys, n, bits, s, lo_bit);
+}
+
+// The genome-wide correction's column lists (gw.hip): H's off-diagonal cells
+// keyed by column (RsCells) and sorted stably by the cbits column bits.  The
+// first radix pass reads the cells themselves (its histogram and scatter
+// form the keys; no key array is written and re-read first), the rest sort
+// the keys.  Returns the key count; keys must hold nnz entries.
+int64_t dev_sort_cells_by_col(const int32_t* r, const int32_t* c, const uint32_t* v, int64_t nnz, int fmt, int ib,
+                              int cbits, DBuf<unsigned long long>& keys, hipStream_t s) {
+    if (nnz <= 0) return 0;
+    const long long tiles = (nnz + kScanTile - 1) / kScanTile;
+    const RsCells src{r, c, v, (long long)nnz, fmt, ib};
+    int64_t hn = 0;
+    {
+        DBuf<unsigned> hist(256 * tiles), off(256 * tiles);
+        DBuf<unsigned long long> tot(1);
+        {
+            HH_KTIME("k_rs_hist", s);
+            hipLaunchKernelGGL(k_rs_hist<RsCells>, dim3((unsigned)tiles), dim3(kScanThreads), 0, s, src, ib, tiles,
+                               hist.p);
+        }
+        exclusive_scan<unsigned, unsigned>(hist.p, off.p, 256 * tiles, tot.p, s);
+        {
+            HH_KTIME("k_rs_scatter", s);
+            hipLaunchKernelGGL(k_rs_scatter<RsCells>, dim3((unsigned)tiles), dim3(kScanThreads), 0, s, src, keys.p,
+                               ib, tiles, off.p);
+        }
+        HIP_CHECK(hipGetLastError());
+        unsigned long long* pin = (unsigned long long*)pinned_stage().get(0, 8);
+        tot.download(pin, 1, s);
+        HIP_CHECK(hipStreamSynchronize(s));
+        hn = (int64_t)*pin;
+    }
+    if (cbits > 8) sort_keys(keys, hn, cbits - 8, s, ib + 8);
+    return hn;
 }
 void dev_excl_scan_i64(const long long* in, long long* out, long long n, unsigned long long* total_dev, hipStream_t s) {
     exclusive_scan<long long, long long>(in, out, n, total_dev, s);
