@@ -196,15 +196,15 @@ __global__ __launch_bounds__(256) void k_gw_tstats(const int32_t* __restrict__ a
 // one-per-pixel global atomics were the whole 17.7 ms of k_gw_tstats at
 // 10 kb whole genome.  Integer sums: exact, order-free.
 //
-// Round 4: a block walks its run in chunks of kStChunk pixels, each thread's
-// kStItems pixels loaded together from clamped addresses (the per-pixel
+// Round 4: a block walks its run in chunks of 256 x IT pixels, each thread's
+// IT pixels loaded together from clamped addresses (the per-pixel
 // `if (i < p1)` loads were one memory round trip each, 1.1 TB/s); a chunk
 // whose first and last pixel share a row (the common case: ~5 000 pixels
 // per row at 10 kb) sums its row end in registers, one wave reduction and
 // one atomic per wave, instead of a segmented scan per pixel.
 constexpr int kTsWin = 8192;
-constexpr int kStItems = 8;
-constexpr int kStChunk = 256 * kStItems;
+// entries per thread per chunk (a template parameter: T 16, H 8 measured)
+constexpr int kStItemsT = 8, kStItemsH = 8;
 
 // CHECK: the statistics kernels also validate their table (k_gw_check's
 // rules and codes: range, upper triangle, (row, col) order, duplicates,
@@ -233,15 +233,15 @@ struct StCheck {
 // Loads one chunk: each thread's kStItems entries (clamped to `last`) and,
 // with CHECK, validates the ones inside the run.  Returns the thread's
 // largest count seen (CHECK).
-template <bool CHECK>
+template <int IT, bool CHECK>
 __device__ __forceinline__ unsigned st_load(const int32_t* __restrict__ a, const int32_t* __restrict__ b,
                                             const uint32_t* __restrict__ v, long long c0, long long last, long long nb,
                                             bool upper, int32_t* xs, int32_t* ys, uint32_t* cs, StCheck ck,
                                             int32_t* pxs) {
-    int32_t pys[kStItems];
+    int32_t pys[IT];
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
 #pragma unroll
-    for (int k = 0; k < kStItems; ++k) {
+    for (int k = 0; k < IT; ++k) {
         const long long i = std::min(c0 + k * 256 + threadIdx.x, last);
         xs[k] = a[i];
         ys[k] = b[i];
@@ -256,7 +256,7 @@ __device__ __forceinline__ unsigned st_load(const int32_t* __restrict__ a, const
     if (CHECK) {
         const int lane = threadIdx.x & 63;
 #pragma unroll
-        for (int k = 0; k < kStItems; ++k) {
+        for (int k = 0; k < IT; ++k) {
             const long long i = c0 + k * 256 + threadIdx.x;
             const int32_t upx = __shfl_up(xs[k], 1, 64), upy = __shfl_up(ys[k], 1, 64);
             const int32_t px = lane ? upx : pxs[k], py = lane ? upy : pys[k];
@@ -266,7 +266,7 @@ __device__ __forceinline__ unsigned st_load(const int32_t* __restrict__ a, const
         }
     }
 #pragma unroll
-    for (int k = 0; k < kStItems; ++k)  // past the run: count 0 (clamped duplicates of the last entry)
+    for (int k = 0; k < IT; ++k)  // past the run: count 0 (clamped duplicates of the last entry)
         cs[k] &= 0u - (uint32_t)(c0 + k * 256 + threadIdx.x <= last);
     return mx;
 }
@@ -276,34 +276,35 @@ __device__ __forceinline__ int32_t clamp_id(int32_t x, long long nb) {
 }
 __device__ __forceinline__ bool ok_id(int32_t x, long long nb) { return x >= 0 && x < nb; }
 
-template <bool CHECK>
+template <int IT, bool CHECK>
 __global__ __launch_bounds__(256) void k_gw_tstats_win(const int32_t* __restrict__ a, const int32_t* __restrict__ b,
                                                        const uint32_t* __restrict__ v, long long nnz, long long per,
                                                        long long n, const int2* __restrict__ cbd,
                                                        unsigned long long* __restrict__ rpk,
-                                                       unsigned long long* __restrict__ total, StCheck ck) {
-    __shared__ unsigned long long win[kTsWin];
+                                                       unsigned long long* __restrict__ total, StCheck ck,
+                                                       int wsz) {
+    extern __shared__ unsigned long long win[];  // wsz entries (kTsWin unless HH_GW_TSWIN)
     __shared__ unsigned long long wsum[4];
     const long long p0 = (long long)blockIdx.x * per;
     if (p0 >= nnz) return;  // block-uniform
     const long long p1 = std::min(nnz, p0 + per);
     const long long x0 = a[p0];
-    for (int c = threadIdx.x; c < kTsWin; c += 256) win[c] = 0ull;
+    for (int c = threadIdx.x; c < wsz; c += 256) win[c] = 0ull;
     __syncthreads();
     unsigned long long t = 0;
-    for (long long c0 = p0; c0 < p1; c0 += kStChunk) {
-        const long long last = std::min(c0 + kStChunk, p1) - 1;
+    for (long long c0 = p0; c0 < p1; c0 += (256 * IT)) {
+        const long long last = std::min(c0 + (256 * IT), p1) - 1;
         const int32_t xf = a[c0], xl = a[last];
-        int32_t xs[kStItems], ys[kStItems];
-        uint32_t cs[kStItems];
-        int32_t pxs[kStItems];
-        st_load<CHECK>(a, b, v, c0, last, n, true, xs, ys, cs, ck, pxs);
+        int32_t xs[IT], ys[IT];
+        uint32_t cs[IT];
+        int32_t pxs[IT];
+        st_load<IT, CHECK>(a, b, v, c0, last, n, true, xs, ys, cs, ck, pxs);
         if (xf == xl) {
             const bool okx = ok_id(xf, n);
             const int2 bd = cbd[clamp_id(xf, n)];
             unsigned long long racc = 0;
 #pragma unroll
-            for (int k = 0; k < kStItems; ++k) {
+            for (int k = 0; k < IT; ++k) {
                 const uint32_t cc = cs[k];
                 const int32_t y = ys[k];
                 t += cc;
@@ -312,7 +313,7 @@ __global__ __launch_bounds__(256) void k_gw_tstats_win(const int32_t* __restrict
                     racc += pk;
                     if (xf != y) {
                         const long long d = (long long)y - x0;
-                        if (d >= 0 && d < kTsWin) atomicAdd(&win[d], pk);
+                        if (d >= 0 && d < wsz) atomicAdd(&win[d], pk);
                         else atomicAdd(rpk + y, pk);
                     }
                 }
@@ -320,11 +321,11 @@ __global__ __launch_bounds__(256) void k_gw_tstats_win(const int32_t* __restrict
             racc = (unsigned long long)wave_sum_ll((long long)racc);
             if ((threadIdx.x & 63) == 0 && racc && okx) atomicAdd(rpk + xf, racc);
         } else {
-            int2 bds[kStItems];
+            int2 bds[IT];
 #pragma unroll
-            for (int k = 0; k < kStItems; ++k) bds[k] = cbd[clamp_id(xs[k], n)];
+            for (int k = 0; k < IT; ++k) bds[k] = cbd[clamp_id(xs[k], n)];
 #pragma unroll
-            for (int k = 0; k < kStItems; ++k) {
+            for (int k = 0; k < IT; ++k) {
                 const uint32_t cc = cs[k];
                 const int32_t x = xs[k], y = ys[k];
                 t += cc;
@@ -333,7 +334,7 @@ __global__ __launch_bounds__(256) void k_gw_tstats_win(const int32_t* __restrict
                     pk = ((unsigned long long)cc << 24) | 1ull;
                     if (x != y) {
                         const long long d = (long long)y - x0;
-                        if (d >= 0 && d < kTsWin) atomicAdd(&win[d], pk);
+                        if (d >= 0 && d < wsz) atomicAdd(&win[d], pk);
                         else atomicAdd(rpk + y, pk);
                     }
                 }
@@ -342,7 +343,7 @@ __global__ __launch_bounds__(256) void k_gw_tstats_win(const int32_t* __restrict
         }
     }
     __syncthreads();
-    for (int c = threadIdx.x; c < kTsWin; c += 256) {
+    for (int c = threadIdx.x; c < wsz; c += 256) {
         const unsigned long long w = win[c];
         if (w && x0 + c < n) atomicAdd(rpk + x0 + c, w);
     }
@@ -359,7 +360,7 @@ __global__ __launch_bounds__(256) void k_gw_tstats_win(const int32_t* __restrict
 // row: segmented), and sum(H).  A block walks a contiguous run in chunks as
 // k_gw_tstats_win does (batched clamped loads; a one-row chunk sums in
 // registers).  CHECK: validates H too and records its largest count.
-template <bool CHECK>
+template <int IT, bool CHECK>
 __global__ __launch_bounds__(256) void k_gw_hstats(const int32_t* __restrict__ r, const int32_t* __restrict__ c,
                                                    const uint32_t* __restrict__ v, long long nnz, long long per,
                                                    long long nb, const int2* __restrict__ bbd,
@@ -372,17 +373,17 @@ __global__ __launch_bounds__(256) void k_gw_hstats(const int32_t* __restrict__ r
     const long long p1 = std::min(nnz, p0 + per);
     unsigned long long t = 0;
     unsigned mx = 0u;
-    for (long long c0 = p0; c0 < p1; c0 += kStChunk) {
-        const long long last = std::min(c0 + kStChunk, p1) - 1;
+    for (long long c0 = p0; c0 < p1; c0 += (256 * IT)) {
+        const long long last = std::min(c0 + (256 * IT), p1) - 1;
         const int32_t xf = r[c0], xl = r[last];
-        int32_t xs[kStItems], ys[kStItems];
-        uint32_t cs[kStItems];
-        int32_t pxs[kStItems];
-        mx = max(mx, st_load<CHECK>(r, c, v, c0, last, nb, false, xs, ys, cs, ck, pxs));
+        int32_t xs[IT], ys[IT];
+        uint32_t cs[IT];
+        int32_t pxs[IT];
+        mx = max(mx, st_load<IT, CHECK>(r, c, v, c0, last, nb, false, xs, ys, cs, ck, pxs));
         if (CHECK) {  // H row pointers (k_px_rowptr_gw's rule): ptr[q] = first entry with row >= q
             const int lane = threadIdx.x & 63;
 #pragma unroll
-            for (int k = 0; k < kStItems; ++k) {
+            for (int k = 0; k < IT; ++k) {
                 const long long i = c0 + k * 256 + threadIdx.x;
                 const int32_t up = __shfl_up(xs[k], 1, 64);
                 const long long prev = i == 0 ? -1 : (long long)(lane ? up : pxs[k]);
@@ -398,18 +399,18 @@ __global__ __launch_bounds__(256) void k_gw_hstats(const int32_t* __restrict__ r
             const int2 bd = bbd[clamp_id(xf, nb)];
             unsigned long long racc = 0;
 #pragma unroll
-            for (int k = 0; k < kStItems; ++k) {
+            for (int k = 0; k < IT; ++k) {
                 t += cs[k];
                 racc += in_block(bd, ys[k]) ? (unsigned long long)cs[k] : 0ull;
             }
             racc = (unsigned long long)wave_sum_ll((long long)racc);
             if ((threadIdx.x & 63) == 0 && racc && ok_id(xf, nb)) atomicAdd(bsum + xf, racc);
         } else {
-            int2 bds[kStItems];
+            int2 bds[IT];
 #pragma unroll
-            for (int k = 0; k < kStItems; ++k) bds[k] = bbd[clamp_id(xs[k], nb)];
+            for (int k = 0; k < IT; ++k) bds[k] = bbd[clamp_id(xs[k], nb)];
 #pragma unroll
-            for (int k = 0; k < kStItems; ++k) {
+            for (int k = 0; k < IT; ++k) {
                 t += cs[k];
                 seg_add_u64(xs[k], ok_id(xs[k], nb) && in_block(bds[k], ys[k]) ? (unsigned long long)cs[k] : 0ull,
                             bsum);
@@ -899,18 +900,31 @@ void gw_create(hh_gw& G, const Id* t1, const Id* t2, const Cnt* tv, int64_t t_nn
     HIP_CHECK(hipMemsetAsync(errs.p, 0xff, 10 * sizeof(unsigned long long), s));
     vmx.zero(s);
     G.hptr.alloc(2 * n + 1);
+    // HH_GW_ST_ITEMS="T,H": entries per thread of the statistics kernels (8 / 16; A/B runs)
+    int st_items_t = kStItemsT, st_items_h = kStItemsH;
+    if (const char* e = std::getenv("HH_GW_ST_ITEMS")) std::sscanf(e, "%d,%d", &st_items_t, &st_items_h);
+    // HH_GW_TSWIN: LDS column window of the T statistics (entries, <= 8192)
+    int wsz = kTsWin;
+    if (const char* e = std::getenv("HH_GW_TSWIN")) wsz = std::max(256, std::min(kTsWin, std::atoi(e)));
     const StCheck ckT{errs.p, nullptr, nullptr}, ckH{errs.p + 5, vmx.p, G.hptr.p};
     HH_KTIME("gw_stats_to_end", s);  // (from the statistics to the end of create)
     if (t_nnz > 0) {
         if (tpack) {
             const long long nb = std::min<long long>(8192, (t_nnz + 65535) / 65536);
             const long long per = ((t_nnz + nb - 1) / nb + 255) / 256 * 256;
-            if (fused)
-                hipLaunchKernelGGL(k_gw_tstats_win<true>, dim3((unsigned)((t_nnz + per - 1) / per)), dim3(256), 0, s,
-                                   G.tAp, G.tBp, G.tVp, (long long)t_nnz, per, (long long)n, dch.p, tpk.p, ttot.p, ckT);
-            else
-                hipLaunchKernelGGL(k_gw_tstats_win<false>, dim3((unsigned)((t_nnz + per - 1) / per)), dim3(256), 0, s,
-                                   G.tAp, G.tBp, G.tVp, (long long)t_nnz, per, (long long)n, dch.p, tpk.p, ttot.p, ckT);
+            auto launch_t = [&](auto it) {
+                constexpr int IT = decltype(it)::value;
+                if (fused)
+                    hipLaunchKernelGGL((k_gw_tstats_win<IT, true>), dim3((unsigned)((t_nnz + per - 1) / per)), dim3(256),
+                                       (size_t)wsz * 8, s, G.tAp, G.tBp, G.tVp, (long long)t_nnz, per, (long long)n,
+                                       dch.p, tpk.p, ttot.p, ckT, wsz);
+                else
+                    hipLaunchKernelGGL((k_gw_tstats_win<IT, false>), dim3((unsigned)((t_nnz + per - 1) / per)),
+                                       dim3(256), (size_t)wsz * 8, s, G.tAp, G.tBp, G.tVp, (long long)t_nnz, per,
+                                       (long long)n, dch.p, tpk.p, ttot.p, ckT, wsz);
+            };
+            if (st_items_t == 8) launch_t(std::integral_constant<int, 8>{});
+            else launch_t(std::integral_constant<int, kStItemsT>{});
         }
         else
             hipLaunchKernelGGL(k_gw_tstats<false>, sgrid(t_nnz), dim3(256), 0, s, G.tAp, G.tBp, G.tVp,
@@ -919,12 +933,19 @@ void gw_create(hh_gw& G, const Id* t1, const Id* t2, const Cnt* tv, int64_t t_nn
     if (h_nnz > 0) {
         const long long nb = std::min<long long>(8192, (h_nnz + 65535) / 65536);
         const long long per = ((h_nnz + nb - 1) / nb + 255) / 256 * 256;
-        if (fused)
-            hipLaunchKernelGGL(k_gw_hstats<true>, dim3((unsigned)((h_nnz + per - 1) / per)), dim3(256), 0, s, G.Rp,
-                               G.Cp, G.Vp, (long long)h_nnz, per, (long long)(2 * n), dblk.p, hbs.p, htot.p, ckH);
-        else
-            hipLaunchKernelGGL(k_gw_hstats<false>, dim3((unsigned)((h_nnz + per - 1) / per)), dim3(256), 0, s, G.Rp,
-                               G.Cp, G.Vp, (long long)h_nnz, per, (long long)(2 * n), dblk.p, hbs.p, htot.p, ckH);
+        auto launch_h = [&](auto it) {
+            constexpr int IT = decltype(it)::value;
+            if (fused)
+                hipLaunchKernelGGL((k_gw_hstats<IT, true>), dim3((unsigned)((h_nnz + per - 1) / per)), dim3(256), 0, s,
+                                   G.Rp, G.Cp, G.Vp, (long long)h_nnz, per, (long long)(2 * n), dblk.p, hbs.p, htot.p,
+                                   ckH);
+            else
+                hipLaunchKernelGGL((k_gw_hstats<IT, false>), dim3((unsigned)((h_nnz + per - 1) / per)), dim3(256), 0,
+                                   s, G.Rp, G.Cp, G.Vp, (long long)h_nnz, per, (long long)(2 * n), dblk.p, hbs.p,
+                                   htot.p, ckH);
+        };
+        if (st_items_h == 16) launch_h(std::integral_constant<int, 16>{});
+        else launch_h(std::integral_constant<int, kStItemsH>{});
     }
     HIP_CHECK(hipGetLastError());
     G.t_rowsum.resize(n);
