@@ -589,6 +589,9 @@ __global__ __launch_bounds__(256) void k_gw_merge(GwDev g, const double* __restr
     const double ar = g.alpha[r], sr = s[r];
     long long pos = PASS ? len_or_off[r] : 0;
     double csum = 0.0;
+    __shared__ int slot_k[4][64];
+    __shared__ double slot_v[4][64];
+    const int wv = threadIdx.x >> 6;
     while (ia < a1 || ib < b1) {
         // windows (padded with +inf keys)
         const bool ina = ia + lane < a1, inb = ib + lane < b1;
@@ -601,31 +604,43 @@ __global__ __launch_bounds__(256) void k_gw_merge(GwDev g, const double* __restr
             kb = lrv_row<FMT>(e);
             vb = lrv_val<FMT>(e) / g.alpha[kb];
         }
-        // merge path: x = number of A elements among the first d = lane + 1
-        // merged ones; A[x - 1] <= B[d - x] (A wins ties)
-        const int d = lane + 1;
-        int lo = d > 64 ? d - 64 : 0, hi = d < 64 ? d : 64;
-        while (__any(lo < hi)) {
-            const int mid = (lo + hi) >> 1;
-            const int am = __shfl(ka, min(mid, 63), 64);
-            const int bm = __shfl(kb, min(max(d - 1 - mid, 0), 63), 64);
-            if (lo < hi) {
-                if (am <= bm) lo = mid + 1;  // A[mid] is among the first d
-                else hi = mid;
-            }
+        // merged position of every element (ties: A first, so a B element
+        // directly follows its A partner): A[l] at l + #(B < A[l]), B[l] at
+        // l + #(A <= B[l]), each count a branch-free 64-entry binary search
+        // over the other (sorted, +inf padded) window; the elements land in
+        // the wave's LDS slots and lane l reads merged element l.  (Round 3's
+        // per-lane merge-path search over both windows was ~170 of the
+        // window's ~350 instructions: the kernel was VALU-bound.)
+        int pa = 0, pb = 0;
+#pragma unroll
+        for (int st = 32; st >= 1; st >>= 1) {
+            const int qb = __shfl(kb, pa + st - 1, 64);
+            const int qa = __shfl(ka, pb + st - 1, 64);
+            pa += qb < ka ? st : 0;
+            pb += qa <= kb ? st : 0;
         }
-        const int x = lo;                         // A elements in the first lane + 1
-        const int xu = __shfl_up(x, 1, 64);       // (every lane shuffles)
-        const int xp = lane ? xu : 0;             // ... in the first lane
-        const bool fromA = x > xp;
-        const int src = fromA ? xp : lane - xp;   // index in that window
-        // every lane takes part in every shuffle (a lane reading from a lane
-        // outside the active mask of a divergent shuffle gets nothing)
-        const int srcl = min(src, 63);
-        const int key_a = __shfl(ka, srcl, 64), key_b = __shfl(kb, srcl, 64);
-        const double val_a = __shfl(va, srcl, 64), val_b = __shfl(vb, srcl, 64);
-        const int key = fromA ? key_a : key_b;
-        const double val = fromA ? val_a : val_b;
+        const int kb63 = __shfl(kb, 63, 64), ka63 = __shfl(ka, 63, 64);
+        pa += (pa == 63 && kb63 < ka) ? 1 : 0;
+        pb += (pb == 63 && ka63 <= kb) ? 1 : 0;
+        const int posA = lane + pa, posB = lane + pb;
+        if (posA < 64) {
+            slot_k[wv][posA] = ka;
+            slot_v[wv][posA] = va;
+        }
+        if (posB < 64) {
+            slot_k[wv][posB] = kb | (int)0x80000000;  // high bit: from B (keys < 2^31)
+            slot_v[wv][posB] = vb;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const int kraw = slot_k[wv][lane];
+        const bool fromA = kraw >= 0;
+        const int key = kraw & 0x7fffffff;
+        const double val = slot_v[wv][lane];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();  // the slots are rewritten next window
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         // the next merged element (tie partner?)
         const int key_n = __shfl_down(key, 1, 64);
         const bool fromA_n = __shfl_down(fromA ? 1 : 0, 1, 64) != 0;
@@ -649,7 +664,7 @@ __global__ __launch_bounds__(256) void k_gw_merge(GwDev g, const double* __restr
             ov[q] = rf * cv;
         }
         pos += __popcll(em);
-        const int xa = __shfl(x, M - 1, 64);  // A elements among the M consumed
+        const int xa = __popcll(__ballot(posA < M));  // A elements among the M consumed
         ia += xa;
         ib += M - xa;
     }
