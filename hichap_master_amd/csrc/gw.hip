@@ -95,14 +95,31 @@ __global__ void k_px_rowptr_gw(const int32_t* __restrict__ A, long long nnz, lon
     for (long long r = lo + 1; r <= hi; ++r) ptr[r] = i;
 }
 
-// the same from the high bits of sorted keys
-__global__ void k_px_keyptr_gw(const unsigned long long* __restrict__ keys, long long n, int ib, long long nr,
-                               long long* __restrict__ ptr) {
-    const long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k > n) return;
-    const long long lo = k == 0 ? -1 : (long long)(keys[k - 1] >> ib);
-    const long long hi = k == n ? nr : (long long)(keys[k] >> ib);
-    for (long long r = lo + 1; r <= hi; ++r) ptr[r] = k;
+// the same from the high bits of sorted keys (n >= 1): kKpItems keys per
+// thread loaded together (clamped), the previous key by a shuffle (a wave's
+// first lane: a scalar load)
+constexpr int kKpItems = 8;
+__global__ __launch_bounds__(256) void k_px_keyptr_gw(const unsigned long long* __restrict__ keys, long long n, int ib,
+                                                      long long nr, long long* __restrict__ ptr) {
+    const long long base = (long long)blockIdx.x * (256 * kKpItems);
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    long long cur[kKpItems], prv[kKpItems];
+#pragma unroll
+    for (int q = 0; q < kKpItems; ++q) {
+        const long long k = base + q * 256 + threadIdx.x;
+        cur[q] = (long long)(keys[std::min(k, n - 1)] >> ib);
+        prv[q] = (long long)(keys[std::min(std::max(base + q * 256 + wv * 64 - 1, 0LL), n - 1)] >> ib);
+    }
+#pragma unroll
+    for (int q = 0; q < kKpItems; ++q) {
+        const long long k = base + q * 256 + threadIdx.x;
+        const long long up = __shfl_up(cur[q], 1, 64);
+        if (k > n) continue;
+        const long long lo = k == 0 ? -1 : (lane ? up : prv[q]);
+        const long long hi = k == n ? nr : cur[q];
+        for (long long r = lo + 1; r <= hi; ++r) ptr[r] = k;
+    }
 }
 
 // Wave-segmented integer sums: lanes hold (key, val) with keys non-decreasing
@@ -1055,8 +1072,11 @@ void gw_create(hh_gw& G, const Id* t1, const Id* t2, const Cnt* tv, int64_t t_nn
     const unsigned long long hn = (unsigned long long)G.n_keys;
     clk.lap("column keys + sort");
     G.cptr.alloc(2 * n + 1);
-    hipLaunchKernelGGL(k_px_keyptr_gw, dim3((unsigned)((hn + 1 + 255) / 256)), dim3(256), 0, s, G.keys.p,
-                       (long long)hn, G.ib, (long long)(2 * n), G.cptr.p);
+    if (hn == 0)
+        HIP_CHECK(hipMemsetAsync(G.cptr.p, 0, (2 * n + 1) * sizeof(long long), s));
+    else
+        hipLaunchKernelGGL(k_px_keyptr_gw, dim3((unsigned)((hn + 1 + 256 * kKpItems - 1) / (256 * kKpItems))),
+                           dim3(256), 0, s, G.keys.p, (long long)hn, G.ib, (long long)(2 * n), G.cptr.p);
     if (hn && !G.fmt)
         hipLaunchKernelGGL(k_gw_pack, dim3((unsigned)((hn + 255) / 256)), dim3(256), 0, s, G.keys.p, (long long)hn,
                            G.ib >= 64 ? ~0ull : ((1ull << G.ib) - 1ull), G.Rp, G.Vp);
