@@ -920,6 +920,20 @@ struct RsCells {
         key = (k1 & m) | (k0 & ~m);
     }
 };
+// The same cells for a histogram: the digit bits of either form are the
+// column's (col << ib), so the counts are not read
+struct RsCellCols {
+    const int32_t* r;
+    const int32_t* c;
+    long long n;
+    int ib;
+    __device__ __forceinline__ void get(long long i, unsigned long long& key, bool& ok) const {
+        const long long q = i < n ? i : n - 1;
+        const int32_t rr = r[q], cc = c[q];
+        ok = (i < n) & (rr != cc);
+        key = (unsigned long long)cc << (ib & 63);
+    }
+};
 
 // Digit histogram of one 4096-key tile: each wave counts its 1 024 keys by
 // ballot matching into wave-private LDS counters (no LDS atomics: a skewed
@@ -1433,8 +1447,8 @@ int64_t dev_sort_cells_by_col(const int32_t* r, const int32_t* c, const uint32_t
         DBuf<unsigned long long> tot(1);
         {
             HH_KTIME("k_rs_hist", s);
-            hipLaunchKernelGGL(k_rs_hist<RsCells>, dim3((unsigned)tiles), dim3(kScanThreads), 0, s, src, ib, tiles,
-                               hist.p);
+            hipLaunchKernelGGL(k_rs_hist<RsCellCols>, dim3((unsigned)tiles), dim3(kScanThreads), 0, s,
+                               RsCellCols{r, c, (long long)nnz, ib}, ib, tiles, hist.p);
         }
         exclusive_scan<unsigned, unsigned>(hist.p, off.p, 256 * tiles, tot.p, s);
         {
