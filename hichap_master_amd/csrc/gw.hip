@@ -609,18 +609,36 @@ __global__ __launch_bounds__(256) void k_gw_merge(GwDev g, const double* __restr
     __shared__ int slot_k[4][64];
     __shared__ double slot_v[4][64];
     const int wv = threadIdx.x >> 6;
+    // Software-pipelined windows: the raw cells of the current window (cur)
+    // and of the 64 after it (nxt) are in registers; a window's consumption
+    // (<= 64 of each list) shifts cur / nxt by shuffles, and the loads of the
+    // following 64 are issued at the end of the window, one window ahead of
+    // use.  Loads from clamped addresses (the row's last cell; its values on
+    // padding lanes are never used: their keys are +inf).  Measured
+    // (rocprof SQ counters): the one-window-at-a-time loop spent ~77 % of its
+    // wave cycles parked on s_waitcnt (three dependent round trips per window:
+    // cells, alpha, s); now two.
+    const long long aq = std::max(a1 - 1, 0LL), bq = std::max(b1 - 1, 0LL);
+    int32_t ca = 0, na = 0;
+    uint32_t cva = 0u, nva = 0u;
+    unsigned long long ce = 0ull, ne = 0ull;
+    if (ia < a1 || ib < b1) {  // (an empty row of an empty table has no cell to clamp to)
+        ca = g.C[std::min(ia + lane, aq)];
+        cva = g.V[std::min(ia + lane, aq)];
+        ce = g.lrv[std::min(ib + lane, bq)];
+        na = g.C[std::min(ia + 64 + lane, aq)];
+        nva = g.V[std::min(ia + 64 + lane, aq)];
+        ne = g.lrv[std::min(ib + 64 + lane, bq)];
+    }
     while (ia < a1 || ib < b1) {
         // windows (padded with +inf keys)
         const bool ina = ia + lane < a1, inb = ib + lane < b1;
-        const int ka = ina ? g.C[ia + lane] : kMergeInf;
-        const double va = ina ? (double)g.V[ia + lane] / ar : 0.0;
-        int kb = kMergeInf;
-        double vb = 0.0;
-        if (inb) {
-            const unsigned long long e = g.lrv[ib + lane];
-            kb = lrv_row<FMT>(e);
-            vb = lrv_val<FMT>(e) / g.alpha[kb];
-        }
+        const int ka = ina ? ca : kMergeInf;
+        const int32_t kb_raw = lrv_row<FMT>(ce);
+        const int kb = inb ? kb_raw : kMergeInf;
+        const double alb = g.alpha[inb ? kb_raw : 0];
+        const double va = (double)cva / ar;
+        const double vb = lrv_val<FMT>(ce) / alb;
         // merged position of every element (ties: A first, so a B element
         // directly follows its A partner): A[l] at l + #(B < A[l]), B[l] at
         // l + #(A <= B[l]), each count a branch-free 64-entry binary search
@@ -682,8 +700,23 @@ __global__ __launch_bounds__(256) void k_gw_merge(GwDev g, const double* __restr
         }
         pos += __popcll(em);
         const int xa = __popcll(__ballot(posA < M));  // A elements among the M consumed
+        const int xb = M - xa;
         ia += xa;
-        ib += M - xa;
+        ib += xb;
+        // shift: the new window = cur[xa ..] ++ nxt[.. xa); nxt from memory
+        {
+            const int sa = (lane + xa) & 63, sb = (lane + xb) & 63;
+            const bool fa = lane + xa < 64, fb = lane + xb < 64;
+            const int32_t a_c = __shfl(ca, sa, 64), a_n = __shfl(na, sa, 64);
+            const uint32_t v_c = (uint32_t)__shfl((int)cva, sa, 64), v_n = (uint32_t)__shfl((int)nva, sa, 64);
+            const unsigned long long e_c = __shfl(ce, sb, 64), e_n = __shfl(ne, sb, 64);
+            ca = fa ? a_c : a_n;
+            cva = fa ? v_c : v_n;
+            ce = fb ? e_c : e_n;
+        }
+        na = g.C[std::min(ia + 64 + lane, aq)];
+        nva = g.V[std::min(ia + 64 + lane, aq)];
+        ne = g.lrv[std::min(ib + 64 + lane, bq)];
     }
     if (PASS == 0) {
         csum = wave_sum(csum);
