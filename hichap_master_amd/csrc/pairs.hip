@@ -890,6 +890,7 @@ __global__ void k_count_nl(TextView tv, long long upto, unsigned long long* __re
 // unconditional from clamped addresses (a conditional load compiles to one
 // round trip each).
 struct RsKeys {  // a key array
+    static constexpr bool kTile = false;
     const unsigned long long* k;
     long long n;
     __device__ __forceinline__ void get(long long i, unsigned long long& key, bool& ok) const {
@@ -901,11 +902,51 @@ struct RsKeys {  // a key array
 // column lists, gw.hip): fmt 1 the packed cell col << 44 | row << 24 | count,
 // fmt 0 col << ib | index.  Diagonal cells are not keys.
 struct RsCells {
+    static constexpr bool kTile = true;
     const int32_t* r;
     const int32_t* c;
     const uint32_t* v;
     long long n;
     int fmt, ib;
+    // Whole-tile fast path (block-uniform): a full tile of 16-byte aligned
+    // packed-format (fmt 1) cells is read as 16-byte loads, thread t taking
+    // cells [16 t, 16 t + 16) of the tile -- 12 loads per thread instead of
+    // 48 four-byte ones (the per-entry form's scatter was bound by issuing
+    // them, SQ_WAIT_INST_ANY 0.53).  The key keeps validity: row == col is a
+    // diagonal cell (not a key).
+    __device__ __forceinline__ bool tile_vec(long long base) const {
+        return fmt == 1 && base + kScanTile <= n &&
+               ((reinterpret_cast<uintptr_t>(r) | reinterpret_cast<uintptr_t>(c) | reinterpret_cast<uintptr_t>(v)) &
+                15) == 0;
+    }
+    __device__ __forceinline__ void load16(long long base, int t, unsigned long long* key, bool* ok) const {
+        const int4* r4 = reinterpret_cast<const int4*>(r + base) + 4 * t;
+        const int4* c4 = reinterpret_cast<const int4*>(c + base) + 4 * t;
+        const uint4* v4 = reinterpret_cast<const uint4*>(v + base) + 4 * t;
+        int4 ra[4], ca[4];
+        uint4 va[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            ra[j] = r4[j];
+            ca[j] = c4[j];
+            va[j] = v4[j];
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int32_t rr[4] = {ra[j].x, ra[j].y, ra[j].z, ra[j].w};
+            const int32_t cc[4] = {ca[j].x, ca[j].y, ca[j].z, ca[j].w};
+            const uint32_t vv[4] = {va[j].x, va[j].y, va[j].z, va[j].w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                key[4 * j + q] = ((unsigned long long)cc[q] << 44) | ((unsigned long long)rr[q] << 24) |
+                                 (unsigned long long)vv[q];
+                ok[4 * j + q] = rr[q] != cc[q];
+            }
+        }
+    }
+    __device__ __forceinline__ static bool ok_of(unsigned long long key) {  // fmt 1
+        return ((key >> 24) & 0xFFFFFull) != (key >> 44);
+    }
     __device__ __forceinline__ void get(long long i, unsigned long long& key, bool& ok) const {
         const long long q = i < n ? i : n - 1;
         const int32_t rr = r[q], cc = c[q];
@@ -923,10 +964,35 @@ struct RsCells {
 // The same cells for a histogram: the digit bits of either form are the
 // column's (col << ib), so the counts are not read
 struct RsCellCols {
+    static constexpr bool kTile = true;
     const int32_t* r;
     const int32_t* c;
     long long n;
     int ib;
+    __device__ __forceinline__ bool tile_vec(long long base) const {
+        return base + kScanTile <= n &&
+               ((reinterpret_cast<uintptr_t>(r) | reinterpret_cast<uintptr_t>(c)) & 15) == 0;
+    }
+    __device__ __forceinline__ void load16(long long base, int t, unsigned long long* key, bool* ok) const {
+        const int4* r4 = reinterpret_cast<const int4*>(r + base) + 4 * t;
+        const int4* c4 = reinterpret_cast<const int4*>(c + base) + 4 * t;
+        int4 ra[4], ca[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            ra[j] = r4[j];
+            ca[j] = c4[j];
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int32_t rr[4] = {ra[j].x, ra[j].y, ra[j].z, ra[j].w};
+            const int32_t cc[4] = {ca[j].x, ca[j].y, ca[j].z, ca[j].w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                key[4 * j + q] = (unsigned long long)cc[q] << (ib & 63);
+                ok[4 * j + q] = rr[q] != cc[q];
+            }
+        }
+    }
     __device__ __forceinline__ void get(long long i, unsigned long long& key, bool& ok) const {
         const long long q = i < n ? i : n - 1;
         const int32_t rr = r[q], cc = c[q];
@@ -951,8 +1017,14 @@ __global__ __launch_bounds__(kScanThreads) void k_rs_hist(Src src, int shift, lo
     const long long base = (long long)blockIdx.x * kScanTile;
     unsigned long long kv[kScanItems];
     bool okv[kScanItems];
+    bool vec = false;
+    if constexpr (Src::kTile) vec = src.tile_vec(base);
+    if (vec) {  // counts are order-free: each thread's 16 consecutive entries
+        if constexpr (Src::kTile) src.load16(base, tid, kv, okv);
+    } else {
 #pragma unroll
-    for (int r = 0; r < kScanItems; ++r) src.get(base + w * PER + r * 64 + lane, kv[r], okv[r]);
+        for (int r = 0; r < kScanItems; ++r) src.get(base + w * PER + r * 64 + lane, kv[r], okv[r]);
+    }
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < kScanItems; ++r) {
@@ -986,7 +1058,9 @@ __global__ __launch_bounds__(kScanThreads) void k_rs_scatter(Src src, unsigned l
     constexpr int NW = kScanThreads / 64;
     constexpr int PER = kScanTile / NW;  // keys per wave
     static_assert(PER == 64 * kScanItems, "a wave's run is kScanItems steps of 64 keys");
-    __shared__ unsigned long long stage[kScanTile];
+    // kScanTile / 16 entries of padding: the vector loader writes 16
+    // consecutive entries per thread at 17-entry strides (fewer bank conflicts)
+    __shared__ unsigned long long stage[kScanTile + kScanTile / 16];
     __shared__ unsigned wcnt[NW][256];
     __shared__ unsigned start[256], gofs_lo[256];
     __shared__ unsigned long long sh[4];
@@ -996,8 +1070,30 @@ __global__ __launch_bounds__(kScanThreads) void k_rs_scatter(Src src, unsigned l
     for (int k = 0; k < NW; ++k) wcnt[k][tid] = 0;
     unsigned long long kv[kScanItems];
     bool okv[kScanItems];
+    bool vec = false;
+    if constexpr (Src::kTile) vec = src.tile_vec(base);
+    if (vec) {
+        if constexpr (Src::kTile) {
+            // 16-byte loads (thread t: entries 16 t ..), then through LDS into
+            // the ranking order (wave w's entries w * PER + r * 64 + lane)
+            unsigned long long k16[kScanItems];
+            bool o16[kScanItems];
+            src.load16(base, tid, k16, o16);
 #pragma unroll
-    for (int r = 0; r < kScanItems; ++r) src.get(base + w * PER + r * 64 + lane, kv[r], okv[r]);
+            for (int k = 0; k < kScanItems; ++k) stage[tid * 17 + k] = k16[k];
+            __syncthreads();
+#pragma unroll
+            for (int r = 0; r < kScanItems; ++r) {
+                const int e = w * PER + r * 64 + lane;
+                kv[r] = stage[e + (e >> 4)];
+                okv[r] = Src::ok_of(kv[r]);
+            }
+            (void)o16;
+        }
+    } else {
+#pragma unroll
+        for (int r = 0; r < kScanItems; ++r) src.get(base + w * PER + r * 64 + lane, kv[r], okv[r]);
+    }
     __syncthreads();
     const unsigned long long lt = (1ull << lane) - 1ull;
     unsigned rk[kScanItems];
