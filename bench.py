@@ -113,6 +113,27 @@ def pmc_traffic(kernels=SWEEP_KERNELS):
     return tot, meta, os.path.relpath(files[-1], ROOT)
 
 
+def gw_pmc_traffic():
+    """HBM bytes per genome-wide correction from the newest committed
+    rocprofv3 PMC summary of the gw bench (profiles/*_gw_pmc.json,
+    tools/pmc_summary.py): every kernel of the run except the synthetic-input
+    generator, summed over its dispatches, divided by the number of
+    corrections (the output-writing merge runs once per correction);
+    (None, None) without one."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_gw_pmc.json")))
+    if not files:
+        return None, None
+    data = json.load(open(files[-1]))
+    runs = [v.get("dispatches", 0) for k, v in data.items() if k != "_meta" and "k_gw_merge" in k and "1>" in k]
+    n_corr = max(runs) if runs else 0
+    if not n_corr:
+        return None, None
+    tot = sum(v["traffic_bytes"] * v.get("dispatches", 0) for k, v in data.items()
+              if k != "_meta" and "synth" not in k)
+    return tot / n_corr, os.path.relpath(files[-1], ROOT)
+
+
 def host_info():
     """The CPU every cpu_baseline ran on: model name and how many logical CPUs
     the machine has / this process may use (a GPU box shares its host)."""
@@ -881,6 +902,10 @@ def run_gw(args, world, rank, local):
         out_bytes = 16.0 * info["out_nnz"]  # int32 bin1 + int32 bin2 + fp64 value
         step_s = elapsed / args.steps
         alg = in_bytes + out_bytes
+        # physical HBM bytes per correction (2 x FETCH_SIZE + WRITE_SIZE over
+        # every kernel, MI355X_MICROARCH.md's gfx950 correction), when a PMC
+        # summary of this line is committed
+        gw_traffic, gw_traffic_src = gw_pmc_traffic()
         out = {
             "metric": "sparse GenomeWideMatrixCorrection, hg19 10 kb diploid (T table + imputed H cells -> corrected table)",
             "value": args.steps / elapsed, "unit": "corrections/s", "n_gpus": 1, "steps": args.steps,
@@ -895,7 +920,9 @@ def run_gw(args, world, rank, local):
             "roofline": {"bound": "hbm", "kernel": "the whole correction (hh_gw_create + hh_gw_correct: ~25 kernels, "
                                                    "per-kernel times in profiles/*gw_kernel_stats.csv)",
                          "achieved": alg / step_s / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                         "frac": alg / step_s / 1e9 / PEAK_HBM_GBS, "traffic": None,
+                         "frac": alg / step_s / 1e9 / PEAK_HBM_GBS, "traffic": gw_traffic,
+                         "traffic_source": gw_traffic_src,
+                         "traffic_GBps": gw_traffic / step_s / 1e9 if gw_traffic else None,
                          "alg_bytes_per_launch": alg,
                          "alg_bytes_note": "12 B per T pixel and H cell read (int32 ids, int32 count) + 16 B per "
                                            "corrected upper cell written (int32 bin1, bin2, fp64 value)"},
