@@ -923,6 +923,9 @@ def run_gw(args, world, rank, local):
                          "frac": alg / step_s / 1e9 / PEAK_HBM_GBS, "traffic": gw_traffic,
                          "traffic_source": gw_traffic_src,
                          "traffic_GBps": gw_traffic / step_s / 1e9 if gw_traffic else None,
+                         "traffic_note": "2 x FETCH_SIZE + WRITE_SIZE summed over the correction's kernels (the "
+                                         "gfx950 doubling assumes wide streaming reads, so the gathers' share "
+                                         "- alpha / s lookups in the marginals and merges - is an upper bound)",
                          "alg_bytes_per_launch": alg,
                          "alg_bytes_note": "12 B per T pixel and H cell read (int32 ids, int32 count) + 16 B per "
                                            "corrected upper cell written (int32 bin1, bin2, fp64 value)"},
