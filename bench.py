@@ -92,17 +92,49 @@ def config(name, nnz=None):
 SWEEP_KERNELS = ("k_sweep_tiled", "k_sweep_flat", "k_sweep_band", "k_sweep_uband")  # symmetric band: <8> once, <4> twice per sweep; upper band: <8>, <4> once each
 
 
-def pmc_traffic(kernels=SWEEP_KERNELS):
-    """HBM bytes per ICE sweep (the three sweep kernels, one launch each)
-    from the newest committed rocprofv3 PMC summary of the C4 bench
-    (tools/pmc_summary.py), its metadata (commit, the layout's real bytes per
-    sweep) and the file name; (None, None, None) without one."""
+# sources whose code decides a line's HBM traffic: a committed PMC summary
+# counts for a run only when it was taken from these same sources on the same
+# workload (a stale summary must not be reported as this run's)
+PMC_SOURCES = {
+    "c4": ("ice.hip", "ice_internal.hpp", "hh_common.hpp", "matrix.hip", "synth.hip", "build.hip"),
+    "gw": ("gw.hip", "pairs.hip", "hh_common.hpp", "ice_internal.hpp", "synth.hip"),
+}
+
+
+def src_sha(line):
+    """sha256 over the sources of PMC_SOURCES[line] (hichap_master_amd/csrc)."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in PMC_SOURCES[line]:
+        with open(os.path.join(ROOT, "hichap_master_amd", "csrc", f), "rb") as fh:
+            h.update(f.encode() + b"\0" + fh.read())
+    return h.hexdigest()[:16]
+
+
+def pmc_pick(line, workload):
+    """The committed PMC summary (profiles/*_<line>_pmc.json) whose _meta
+    names this build's sources (src_sha) and this run's workload; None when
+    none matches (the line then reports traffic null)."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_c4_pmc.json")))
-    if not files:
+    want = src_sha(line)
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_{line}_pmc.json")), reverse=True):
+        data = json.load(open(f))
+        meta = data.get("_meta") or {}
+        wl = meta.get("workload") or {}
+        if meta.get("src_sha") == want and all(wl.get(k) == v for k, v in workload.items()):
+            return data, meta, os.path.relpath(f, ROOT)
+    return None
+
+
+def pmc_traffic(workload, kernels=SWEEP_KERNELS):
+    """HBM bytes per ICE sweep (the sweep kernels, one launch each) from the
+    committed rocprofv3 PMC summary of the C4 bench taken at these sources on
+    this workload (tools/pmc_summary.py), its metadata (commit, the layout's
+    real bytes per sweep) and the file name; (None, None, None) without one."""
+    got = pmc_pick("c4", workload)
+    if got is None:
         return None, None, None
-    data = json.load(open(files[-1]))
-    meta = data.get("_meta", {})
+    data, meta, src = got
     hits = [v for k, v in data.items() if k != "_meta" and any(name in k for name in kernels)]
     if not hits:
         return None, None, None
@@ -110,28 +142,27 @@ def pmc_traffic(kernels=SWEEP_KERNELS):
     # segments) has k times as many dispatches as the once-per-sweep kernels
     base = min(v.get("dispatches", 1) or 1 for v in hits)
     tot = sum(v["traffic_bytes"] * (v.get("dispatches", base) or base) / base for v in hits)
-    return tot, meta, os.path.relpath(files[-1], ROOT)
+    return tot, meta, src
 
 
-def gw_pmc_traffic():
-    """HBM bytes per genome-wide correction from the newest committed
-    rocprofv3 PMC summary of the gw bench (profiles/*_gw_pmc.json,
-    tools/pmc_summary.py): every kernel of the run except the synthetic-input
-    generator, summed over its dispatches, divided by the number of
-    corrections (the output-writing merge runs once per correction);
-    (None, None) without one."""
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_gw_pmc.json")))
-    if not files:
+def gw_pmc_traffic(workload):
+    """HBM bytes per genome-wide correction from the committed rocprofv3 PMC
+    summary of the gw bench taken at these sources on this workload
+    (profiles/*_gw_pmc.json, tools/pmc_summary.py): every kernel of the run
+    except the synthetic-input generator, summed over its dispatches, divided
+    by the number of corrections (the output-writing merge runs once per
+    correction); (None, None) without one."""
+    got = pmc_pick("gw", workload)
+    if got is None:
         return None, None
-    data = json.load(open(files[-1]))
+    data, _, src = got
     runs = [v.get("dispatches", 0) for k, v in data.items() if k != "_meta" and "k_gw_merge" in k and "1>" in k]
     n_corr = max(runs) if runs else 0
     if not n_corr:
         return None, None
     tot = sum(v["traffic_bytes"] * v.get("dispatches", 0) for k, v in data.items()
               if k != "_meta" and "synth" not in k)
-    return tot / n_corr, os.path.relpath(files[-1], ROOT)
+    return tot / n_corr, src
 
 
 def host_info():
@@ -905,7 +936,7 @@ def run_gw(args, world, rank, local):
         # physical HBM bytes per correction (2 x FETCH_SIZE + WRITE_SIZE over
         # every kernel, MI355X_MICROARCH.md's gfx950 correction), when a PMC
         # summary of this line is committed
-        gw_traffic, gw_traffic_src = gw_pmc_traffic()
+        gw_traffic, gw_traffic_src = gw_pmc_traffic({"T_pixels": T.nnz, "H_cells": H.nnz})
         out = {
             "metric": "sparse GenomeWideMatrixCorrection, hg19 10 kb diploid (T table + imputed H cells -> corrected table)",
             "value": args.steps / elapsed, "unit": "corrections/s", "n_gpus": 1, "steps": args.steps,
@@ -1299,7 +1330,7 @@ def main():
                        "tiles": inf["n_tiles"], "units": inf["n_units"],
                        "hbm_bytes_matrix": inf["device_bytes"]},
         }
-        traffic, meta, traffic_src = (pmc_traffic() if args.config == "c4" and args.nnz is None
+        traffic, meta, traffic_src = (pmc_traffic({"n_bins": n, "nnz_upper": nnz_total}) if args.config == "c4"
                                       else (None, None, None))
         if launches:
             # per launch on the slowest rank (= the whole matrix at N=1)

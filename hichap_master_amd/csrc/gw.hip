@@ -840,11 +840,11 @@ unsigned gw_check(const Id* r, const Id* c, const Cnt* v, int64_t nnz, int64_t n
 // whose max is not a positive finite number (NumPy's NaN / inf paths) or
 // that has no non-gap bin (np.max of an empty array raises) is left to the
 // NumPy path (ok 0).
+// G.alpha / G.alpha_ok are sized (n, 0 everywhere) by the caller on its own
+// thread before this runs, so a throw here leaves every chromosome to NumPy.
 static void gw_alpha_host(hh_gw& G, const std::vector<int64_t>& off) {
     const int64_t n = G.n;
     const int nc = (int)off.size() - 1;
-    G.alpha.assign(n, 0.0);
-    G.alpha_ok.assign(nc, 0);
     std::vector<double> ng;
     std::vector<uint8_t> gap;
     for (int c = 0; c < nc; ++c) {
@@ -888,13 +888,21 @@ struct ThreadJoin {
     }
 };
 
+// Argument checks of hh_gw_create*, before anything touches the device.  The
+// column sort (dev_sort_cells_by_col, pairs.hip) keeps its radix offsets in
+// 32 bits, so the haplotype cells are capped below 2^32 - 1.
+static void gw_check_args(int64_t t_nnz, int64_t h_nnz, int64_t n, const int64_t* chrom_offsets, int32_t n_chroms) {
+    HH_REQUIRE(n > 0 && n_chroms > 0 && chrom_offsets && t_nnz >= 0 && h_nnz >= 0, "bad arguments");
+    HH_REQUIRE(chrom_offsets[0] == 0 && chrom_offsets[n_chroms] == n, "chrom_offsets must span [0, n]");
+    HH_REQUIRE(2 * n < kMaxBins, "too many bins");
+    HH_REQUIRE(h_nnz < (int64_t)0xFFFFFFFFLL, "too many haplotype cells: the column sort holds < 2^32 - 1");
+}
+
 template <class Id, class Cnt>
 void gw_create(hh_gw& G, const Id* t1, const Id* t2, const Cnt* tv, int64_t t_nnz, const Id* hr, const Id* hc,
                const Cnt* hv, int64_t h_nnz, int64_t n, const int64_t* chrom_offsets, int32_t n_chroms,
                hipStream_t s) {
-    HH_REQUIRE(n > 0 && n_chroms > 0 && chrom_offsets && t_nnz >= 0 && h_nnz >= 0, "bad arguments");
-    HH_REQUIRE(chrom_offsets[0] == 0 && chrom_offsets[n_chroms] == n, "chrom_offsets must span [0, n]");
-    HH_REQUIRE(2 * n < kMaxBins, "too many bins");
+    gw_check_args(t_nnz, h_nnz, n, chrom_offsets, n_chroms);
     GwClock clk;
     if (clk.on) {
         HIP_CHECK(hipStreamSynchronize(s));
@@ -1069,6 +1077,8 @@ void gw_create(hh_gw& G, const Id* t1, const Id* t2, const Cnt* tv, int64_t t_nn
     // (row pointers, column keys, the radix sort: ~45 ms at 10 kb diploid)
     clk.lap("statistics");
     std::vector<int64_t> offv(chrom_offsets, chrom_offsets + n_chroms + 1);
+    G.alpha.assign(n, 0.0);  // sized here: a failure on the thread leaves ok = 0 for every chromosome
+    G.alpha_ok.assign(n_chroms, 0);
     ThreadJoin alpha_thread;
     alpha_thread.t = std::thread([&G, offv]() {
         try {
@@ -1132,6 +1142,7 @@ int hh_gw_create(const int64_t* t_bin1, const int64_t* t_bin2, const double* t_c
         HH_REQUIRE(out, "null");
         HH_REQUIRE((t_nnz == 0 || (t_bin1 && t_bin2 && t_count)) && (h_nnz == 0 || (h_row && h_col && h_count)),
                    "null arrays");
+        gw_check_args(t_nnz, h_nnz, n, chrom_offsets, n_chroms);
         hipStream_t s = as_stream(stream);
         auto G = std::make_unique<hh_gw>();
         HIP_CHECK(hipGetDevice(&G->device));
@@ -1154,6 +1165,7 @@ int hh_gw_create_device(const int32_t* t_bin1, const int32_t* t_bin2, const int3
                         const int64_t* chrom_offsets, int32_t n_chroms, void* stream, hh_gw** out) {
     return guard([&] {
         HH_REQUIRE(out, "null");
+        gw_check_args(t_nnz, h_nnz, n, chrom_offsets, n_chroms);
         auto G = std::make_unique<hh_gw>();
         HIP_CHECK(hipGetDevice(&G->device));
         gw_create<int32_t, int32_t>(*G, t_bin1, t_bin2, t_count, t_nnz, h_row, h_col, h_count, h_nnz, n,

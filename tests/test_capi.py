@@ -37,3 +37,19 @@ def test_version_and_error_plumbing():
     rc = lib.hh_matrix_get_info(None, None)
     assert rc == -1
     assert b"null" in lib.hh_last_error()
+
+
+def test_gw_create_refuses_too_many_haplotype_cells():
+    # the column sort keeps 32-bit radix offsets: >= 2^32 - 1 cells must be
+    # refused before anything touches the device
+    import ctypes as C
+    import numpy as np
+    lib = _lib.load()
+    off = np.array([0, 10], dtype=np.int64)
+    out = C.c_void_p()
+    for fn in (lib.hh_gw_create_device, lib.hh_gw_create):
+        rc = fn(None, None, None, 0, C.c_void_p(8), C.c_void_p(8), C.c_void_p(8), (1 << 32) - 1, 10,
+                off.ctypes.data_as(C.c_void_p), 1, None, C.byref(out))
+        assert rc != 0
+        assert b"2^32" in lib.hh_last_error()
+        assert not out.value

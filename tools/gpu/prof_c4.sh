@@ -16,5 +16,5 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d /tmp/pc4b -o c4 --output-f
 cp $(find /tmp/pc4b -name "c4_kernel_stats.csv" | head -1) $O/${TAG}_c4_kernel_stats_1stream.csv
 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d /tmp/pc4f -o f --output-format csv -- python3 $R/bench.py --no-cpu --steps 3 --warmup 1 > $O/c4_pmc_f.log 2>&1 || exit 1
 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d /tmp/pc4w -o w --output-format csv -- python3 $R/bench.py --no-cpu --steps 3 --warmup 1 > $O/c4_pmc_w.log 2>&1 || exit 1
-python3 $R/tools/pmc_summary.py $(find /tmp/pc4f -name "*counter_collection.csv" | head -1) $(find /tmp/pc4w -name "*counter_collection.csv" | head -1) $O/${TAG}_c4_pmc.json "$COMMIT" $RB > $O/c4_pmc_summary.log 2>&1 || exit 1
+python3 $R/tools/pmc_summary.py $(find /tmp/pc4f -name "*counter_collection.csv" | head -1) $(find /tmp/pc4w -name "*counter_collection.csv" | head -1) $O/${TAG}_c4_pmc.json "$COMMIT" $RB c4 $O/c4_bench.log > $O/c4_pmc_summary.log 2>&1 || exit 1
 head -12 $O/c4_pmc_summary.log | cut -c1-200
