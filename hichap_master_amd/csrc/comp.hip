@@ -2066,11 +2066,25 @@ static int ortho_grid_cap(int tpb) {
     if (it != cache.end()) return knob(it->second);
     int cus = 0, occ = 0;
     HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    const void* fn = tpb == 1   ? (const void*)k_ortho<kOrthoFull, 1>
-                     : tpb == 2 ? (const void*)k_ortho<kOrthoFull, 2>
-                     : tpb == 4 ? (const void*)k_ortho<kOrthoFull, 4>
-                                : (const void*)k_ortho<kOrthoFull, 8>;
-    HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, 256, 0));
+    // the smallest co-residency over every k_ortho instance the solver
+    // launches at this tpb (the modes differ in code and registers)
+    auto occ_of = [](auto mode_c, auto tpb_c) {
+        int o = 0;
+        HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &o, (const void*)k_ortho<decltype(mode_c)::value, decltype(tpb_c)::value>, 256, 0));
+        return o;
+    };
+    auto occ_all = [&](auto tpb_c) {
+        return std::min({occ_of(std::integral_constant<int, kOrthoFull>{}, tpb_c),
+                         occ_of(std::integral_constant<int, kOrthoFullLS>{}, tpb_c),
+                         occ_of(std::integral_constant<int, kOrthoLast>{}, tpb_c),
+                         occ_of(std::integral_constant<int, kOrthoStart>{}, tpb_c),
+                         occ_of(std::integral_constant<int, kOrthoRitz>{}, tpb_c)});
+    };
+    occ = tpb == 1   ? occ_all(std::integral_constant<int, 1>{})
+          : tpb == 2 ? occ_all(std::integral_constant<int, 2>{})
+          : tpb == 4 ? occ_all(std::integral_constant<int, 4>{})
+                     : occ_all(std::integral_constant<int, 8>{});
     int hwq = 4;  // HIP's default number of hardware queues per process
     if (const char* e = std::getenv("GPU_MAX_HW_QUEUES"))
         if (std::atoi(e) > 0) hwq = std::atoi(e);
@@ -2226,6 +2240,10 @@ static bool pca_krylov(PcaWork& wk, const double* cor, long long n, int k, doubl
         if (coop && (flags[P * 8 + 7] || g_ortho_abort_test)) throw OrthoAbort();
     };
     HIP_CHECK(hipMemsetAsync(fail.p, 0, sizeof(int) * nfl, s));
+    // hh_tune("ortho_abort_test", 2): the abort flag raised before the first
+    // k_ortho launch, so every block leaves its grid barriers early and the
+    // workspace is left partly written -- the fallback must recover from that
+    if (coop && g_ortho_abort_test == 2) HIP_CHECK(hipMemsetAsync(abort_flag, 1, 1, s));
     // start block: [1 / sqrt(n) | deterministic pseudo-random columns]; the
     // host source of the upload lives until the first cycle's synchronise
     std::vector<double> v0((size_t)n * B);

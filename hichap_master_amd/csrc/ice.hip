@@ -2580,7 +2580,8 @@ int hh_tune(const char* key, int64_t value) {
         } else if (k == "symvc_stream") {
             g_symvc_stream = value ? 1 : 0;
         } else if (k == "ortho_abort_test") {
-            g_ortho_abort_test = value ? 1 : 0;
+            HH_REQUIRE(value >= 0 && value <= 2, "ortho_abort_test in {0, 1, 2}");
+            g_ortho_abort_test = (int)value;
         } else if (k == "pca_coop") {
             HH_REQUIRE(value == 0 || value == 1, "pca_coop in {0, 1}");
             g_pca_coop = (int)value;

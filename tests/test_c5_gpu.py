@@ -318,13 +318,17 @@ def test_pca_ortho_fallback_and_grid_cap():
     from hichap_master_amd._lib import call
     dM = _c5_matrix(20)
     p0, s0 = _pca_run(dM, 0)
-    call("hh_tune", b"ortho_abort_test", 1)
-    try:
-        p1, s1 = _pca_run(dM, 1)
-    finally:
-        call("hh_tune", b"ortho_abort_test", 0)
-    assert s1["ortho_fallback"] and s1["converged"] and not s0["ortho_fallback"]
-    np.testing.assert_array_equal(p1, p0)
+    # 1: the abort reported after a completed cooperative launch; 2: the
+    # abort raised inside the first k_ortho launch (blocks leave their grid
+    # barriers early, the workspace is partly written)
+    for mode in (1, 2):
+        call("hh_tune", b"ortho_abort_test", mode)
+        try:
+            p1, s1 = _pca_run(dM, 1)
+        finally:
+            call("hh_tune", b"ortho_abort_test", 0)
+        assert s1["ortho_fallback"] and s1["converged"] and not s0["ortho_fallback"]
+        np.testing.assert_array_equal(p1, p0)
     call("hh_tune", b"ortho_grid_cap", 8)
     try:
         p2, s2 = _pca_run(dM, 1)

@@ -221,3 +221,31 @@ def test_twostep_all_zero_haplotype_raises(mb, devglue):
     Z = np.zeros_like(TM)
     with pytest.raises(_lib.HipLibraryError, match="percentile of an empty array"):
         _twostep_with(mb, {"twostep_devglue": devglue}, TM, Z, Z)
+
+
+def test_twostep_devglue_block_select_path_bitwise(mb):
+    """N > 16384 (kSelPer * 1024) takes the device glue's second percentile
+    path (block_kth + LDS atomics, dense.hip block_percentile); its gaps,
+    alpha and outputs are bitwise the host glue's."""
+    import torch
+    N = 16500
+    g = torch.Generator(device="cuda").manual_seed(11)
+    i = torch.arange(N, device="cuda", dtype=torch.float64)
+    lam = 40.0 / ((i[:, None] - i[None, :]).abs() + 1.0)
+    TM = torch.poisson(lam, generator=g).to(torch.int64)
+    TM = torch.triu(TM) + torch.triu(TM, 1).T
+    MM = torch.poisson(0.4 * lam, generator=g).to(torch.int64)
+    PM = torch.poisson(0.4 * lam, generator=g).to(torch.int64)
+    del lam
+    MM[100:400] = 0  # gap rows: the gap form of Trans2symmetry
+    PM[9000:9100] = 0
+    torch.cuda.synchronize()
+    dev = _twostep_with(mb, {"twostep_devglue": 1}, TM, MM, PM)
+    host = _twostep_with(mb, {"twostep_devglue": 0}, TM, MM, PM)
+    for a, b in zip(dev, host):
+        if hasattr(a, "device"):
+            assert torch.equal(torch.as_tensor(a), torch.as_tensor(b))
+        else:
+            np.testing.assert_array_equal(a, b)
+    gm = dev[2].cpu().numpy() if hasattr(dev[2], "cpu") else dev[2]
+    assert 300 <= len(gm) < N  # the zeroed rows are gaps, most rows are not
