@@ -91,6 +91,7 @@ SIGNATURES = {
     "hh_ice_finalize": (C.c_int, [P, P, P, P, P, P, P]),
     "hh_ice_last_sweep_timing": (C.c_int, [P, PF64, PI32, PF64]),
     "hh_ice_swept_bytes": (C.c_int, [P, PI64]),
+    "hh_ice_get_bias": (C.c_int, [P, P, P]),
     "hh_sweep_trace": (C.c_int, [P, I64, PI64]),
     "hh_comm_unique_id": (C.c_int, [P]),
     "hh_comm_init": (C.c_int, [P, I32, I32, C.POINTER(P)]),

@@ -2883,6 +2883,15 @@ int hh_ice_last_sweep_timing(const hh_ice* S, double* sweep_ms_total, int32_t* s
     });
 }
 
+int hh_ice_get_bias(const hh_ice* S, double* bias, void* stream) {
+    return guard([&] {
+        HH_REQUIRE(S && bias, "null");
+        hipStream_t s = as_stream(stream);
+        S->bias.download(bias, S->n, s);
+        HIP_CHECK(hipStreamSynchronize(s));
+    });
+}
+
 int hh_ice_swept_bytes(const hh_ice* S, int64_t* bytes) {
     return guard([&] {
         HH_REQUIRE(S && bytes, "null");

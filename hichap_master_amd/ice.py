@@ -317,6 +317,12 @@ class IceState:
         call("hh_ice_swept_bytes", self._h, C.byref(b))
         return b.value
 
+    def bias(self, stream=None):
+        """The current bias vector b (n_bins, host; checking only)."""
+        b = np.empty(int(self.m.info()["n_bins"]))
+        call("hh_ice_get_bias", self._h, ptr(b), stream)
+        return b
+
     def finalize(self, stream=None):
         n = int(self.m.info()["n_bins"])
         G = self.n_groups

@@ -259,6 +259,10 @@ int hh_ice_last_sweep_timing(const hh_ice* s, double* sweep_ms_total, int32_t* s
  * only, plus a shard's halo rows, with the upper-band sweep).
  * A measurement helper (bench.py's roofline), no computation. */
 int hh_ice_swept_bytes(const hh_ice* s, int64_t* bytes);
+/* The current bias vector b (all n_bins entries, every rank holds the whole
+ * vector; 0 = masked) to host memory (synchronous; checking only: the
+ * marginal of the next sweep is marg_i = b_i sum_j A_ij b_j). */
+int hh_ice_get_bias(const hh_ice* s, double* bias, void* stream);
 
 /* ------------------------------------------------ sharded ICE in C
  * Genome-wide ICE over world processes (one GPU each), each holding the
