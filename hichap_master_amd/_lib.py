@@ -11,7 +11,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libhichap_hip.so")
+# HH_LIB: another build of the library (build experiments, e.g. -DHH_KWBITS=12)
+LIB_PATH = os.environ.get("HH_LIB") or os.path.join(_HERE, "libhichap_hip.so")
 
 HH_OK = 0
 

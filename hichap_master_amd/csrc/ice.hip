@@ -2497,6 +2497,9 @@ int hh_tune(const char* key, int64_t value) {
         } else if (k == "flatw_u") {
             HH_REQUIRE(value == 8 || value == 16, "flatw_u in {8, 16}");
             g_flatw_u = (int)value;
+        } else if (k == "upper_tiles") {
+            HH_REQUIRE(value == 0 || value == 1, "upper_tiles in {0, 1}");
+            g_upper_tiles = value;
         } else if (k == "flat_max") {
             HH_REQUIRE(value >= 0 && value <= 255, "flat_max in [0, 255]");
             g_flat_max = value;

@@ -28,7 +28,10 @@
 namespace hh {
 
 constexpr int kR = 512;                 // rows per row-block
-constexpr int kWBits = 13;
+#ifndef HH_KWBITS
+#define HH_KWBITS 13
+#endif
+constexpr int kWBits = HH_KWBITS;       // (build experiments: -DHH_KWBITS=12)
 constexpr int kW = 1 << kWBits;         // columns per tile
 constexpr uint32_t kColMask = kW - 1;
 constexpr uint32_t kCntMax = 65535u;    // largest count stored in a tile (wide entry)
@@ -62,6 +65,11 @@ constexpr uint32_t kBand4MaxCnt = 15u;
 extern double g_band4_density;      // hh_tune("band4_density_pct"), default 25 %
 extern double g_band8_big;          // hh_tune("band8_big_pct"), default 5 %
 extern int64_t g_band4;             // hh_tune("band4"): 1 nibble band on (default), 0 off
+// Upper-triangle tiles (build time, hh_tune "upper_tiles"): a tile entry
+// (r, c) is stored only when c's column tile is not left of r's, J(c) >=
+// J(r) (J = x >> kWBits); entries of strictly upper tiles then feed their row
+// and their column
+extern int64_t g_upper_tiles;
 struct BandWidths {
     int32_t w8 = 0, w4 = 0;         // uint8 band |d| <= w8; nibble band w8 < |d| <= w4 (w4 == w8: none)
 };

@@ -41,6 +41,7 @@ int64_t g_flat_max = 64;     // longest row (uint4) of a flat tile segment; 0 = 
 int64_t g_build_debug = 0;
 int64_t g_host_build = 0;    // hh_tune("host_build"): 1 = host builder for every pixel table
 
+int64_t g_upper_tiles = 0;
 int64_t g_band4 = 1;         // nibble band on
 double g_band4_density = 0.25;
 double g_band8_big = 0.05;

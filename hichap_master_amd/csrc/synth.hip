@@ -36,6 +36,7 @@ struct SynthDev {
     int band_w;            // uint8 band half-width W8 (0 = none)
     int band_w4;           // nibble band outer width W4 (== band_w: none)
     int ordered;           // 1: independent draws for (i, j) and (j, i) (asymmetric cells)
+    int upper;             // g_upper_tiles: tile entries only where J(col) >= J(row)
 };
 
 __global__ void k_synth_bins(SynthDev p, float vis_sigma, float gap_frac, int comp_block,
@@ -130,7 +131,8 @@ __global__ __launch_bounds__(256) void k_synth_rows(SynthDev p, long long row_lo
     const long long rb = w / kR;
     const int k = (int)(w % kR);
     const unsigned long long lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    long long upper = 0, nnz = 0, work = 0, sum_lane = 0, nb_lane = 0, nbu_lane = 0;
+    long long upper = 0, nnz = 0, work = 0, sum_lane = 0, nb_lane = 0, nbu_lane = 0, nd_lane = 0;
+    const int Jr = (int)(r >> kWBits);
     int curJ = -1;
     long long tw = 0, tn = 0;      // wide / narrow entries of the current tile
     long long pos = 0, posn = 0;   // PASS 1: next write positions
@@ -171,6 +173,11 @@ __global__ __launch_bounds__(256) void k_synth_rows(SynthDev p, long long row_lo
             sum_lane += kc;
             kc = 0;
         }
+        if (p.upper && kc > 0 && J < Jr) {  // lower tile: stored as its mirror (the column side of row j)
+            nd_lane += 1;
+            sum_lane += kc;
+            kc = 0;
+        }
         const unsigned long long mask = __ballot(kc > 0);
         if (mask == 0ull) continue;
         if (J != curJ) {
@@ -202,7 +209,7 @@ __global__ __launch_bounds__(256) void k_synth_rows(SynthDev p, long long row_lo
     const long long s = wave_sum_ll(sum_lane);
     // band entries were counted per lane; tile entries per wave (ballots)
     const long long nband = wave_sum_ll(nb_lane);
-    nnz += nband;
+    nnz += nband + wave_sum_ll(nd_lane);
     upper += wave_sum_ll(nbu_lane);
     work += ((long long)p.band_w + band4_stride(p.band_w, p.band_w4) / 2) / 2;  // band bytes per row, in 4-byte words
     const uint32_t dg = p.ignore_diags == 0 ? synth_count(p, r, r) : 0u;
@@ -273,6 +280,7 @@ void synth_setup(const hh_synth_params* p, SynthHost& h, hipStream_t s) {
     d.ignore_diags = p->ignore_diags;
     d.cis_only = p->cis_only ? 1 : 0;
     d.seed = p->seed;
+    d.upper = g_upper_tiles ? 1 : 0;
     {
         const BandWidths bw = synth_band_w(p, h.offsets);
         d.band_w = bw.w8;
