@@ -25,6 +25,7 @@ ice.balance on the same pixel table, and fetch against a dense build.
 from __future__ import annotations
 
 import json
+import os
 import time
 
 import numpy as np
@@ -236,10 +237,46 @@ def cooler_tree(chromsizes, binsize, bin1, bin2, count, metadata=None, assembly=
     }
 
 
-def create_cooler(path, resolutions, metadata=None, assembly=None):
-    """Write a new file holding one cooler per resolution, as NPZ2Cooler
-    does (group ``/<res>``, URI ``path::<res>``).  ``resolutions`` maps
-    res -> (chromsizes [(name, length)], bin1, bin2, count)."""
-    tree = {str(res): cooler_tree(cs, res, b1, b2, c, metadata, assembly)
-            for res, (cs, b1, b2, c) in resolutions.items()}
+def create_cooler(path, resolutions, metadata=None, assembly=None, mode="w"):
+    """Write a file holding one cooler per resolution, as NPZ2Cooler does
+    (group ``/<res>``, URI ``path::<res>``).  ``resolutions`` maps res ->
+    (chromsizes [(name, length)], bin1, bin2, count[, metadata]).  mode "a"
+    keeps the resolution groups an existing file already holds (those not
+    given here; NPZ2Cooler's mode='a', :193-196): the file is rewritten with
+    their pixels, bins (weight columns and attributes included) and
+    metadata."""
+    tree = {}
+    if mode == "a" and os.path.exists(path):
+        for grp in cooler_groups(path):
+            if grp not in {str(r) for r in resolutions}:
+                tree[grp] = _regroup(path, grp)
+    for res, spec in resolutions.items():
+        cs, b1, b2, c = spec[:4]
+        meta = spec[4] if len(spec) > 4 else metadata
+        tree[str(res)] = cooler_tree(cs, int(res), b1, b2, c, meta, assembly)
     h5.write_file(path, tree)
+
+
+def cooler_groups(path):
+    """Top-level groups of a file that hold a cooler (a ``pixels`` group)."""
+    with h5.File(path) as f:
+        return [k for k in f.root.keys() if "pixels" in f.root[k]]
+
+
+def _regroup(path, grp):
+    """One existing cooler group as a write_file tree (rewriting a file)."""
+    with Cooler(f"{path}::{grp}") as c:
+        cs = [(n, int(c.chromsizes[n])) for n in c.chromnames]
+        b1, b2, cnt = c.pixels_table()
+        meta = c.info.get("metadata")
+        try:
+            meta = json.loads(meta) if isinstance(meta, str) else meta
+        except ValueError:
+            meta = {"metadata": meta}
+        t = cooler_tree(cs, int(c.binsize), b1, b2, cnt, meta, c.info.get("assembly"))
+        g = c._g("bins")
+        for k in g.keys():
+            if k not in ("chrom", "start", "end"):
+                d = g[k]
+                t["bins"][k] = {"@attrs": dict(d.attrs), "@data": d.read()}
+    return t

@@ -16,6 +16,7 @@ decisions are bit-identical (``np.percentile`` linear interpolation, the
 from __future__ import annotations
 
 import ctypes as C
+import json
 import os
 
 import numpy as np
@@ -616,3 +617,365 @@ def HaplotypeMatrixBuilding(BedFiles, genomeSize, wholeRes, localRes, Imputation
                                  Imputation_region, Imputation_min, Imputation_ratio, UW, UL)
     DataSets["Imputated_Whole"], DataSets["Imputated_Local"] = IW, IL
     return DataSets
+
+
+# ------------------------------------------------- matrix construction (:617-717, :1495-1860)
+# `hichap matrix` drops in here: the pairs are binned on the GPU (PairBinner),
+# the tables written as multi-resolution coolers with NPZ2Cooler's layout
+# (coolio / h5.py; cooler itself is absent), and `cooler balance
+# --ignore-diags 1 [--cis-only] --force` replaced by coolio.balance_cooler
+# (the GPU ICE path, ice.py) in place.
+S_DTYPE = np.dtype({"names": ["bin1", "bin2", "IF"], "formats": [np.int64, np.int64, np.float64]})
+
+
+def _chrom_ok(c, chroms):
+    # NPZ2Cooler's chromosome filter (:145, :150-151, :215)
+    chroms = set(chroms)
+    return (not chroms) or (c.isdigit() and "#" in chroms) or (c in chroms)
+
+
+def _sparse_rec(x, y, v):
+    t = np.zeros(len(v), dtype=S_DTYPE)
+    t["bin1"], t["bin2"], t["IF"] = x, y, v
+    return t
+
+
+def WholeMatrixToSparseDict(Bins, Matrix):
+    """Dense whole-genome matrix -> {chrom: upper-triangle block, 'c1_c2':
+    full inter block (c1 before c2 in Sort_Chromosomes order)} in
+    chromosome-local bins (:457-505).  ``Matrix`` may be a torch tensor."""
+    M = Matrix.cpu().numpy() if hasattr(Matrix, "cpu") else np.asarray(Matrix)
+    order = Sort_Chromosomes(list(Bins))
+    lib = {}
+    for i, c1 in enumerate(order):
+        s1, e1 = Bins[c1][0], Bins[c1][1] + 1
+        for c2 in order[i:]:
+            s2, e2 = Bins[c2][0], Bins[c2][1] + 1
+            blk = M[s1:e1, s2:e2]
+            if c1 == c2:
+                blk = np.triu(blk)
+            x, y = np.nonzero(blk)
+            lib[c1 if c1 == c2 else c1 + "_" + c2] = _sparse_rec(x, y, blk[x, y])
+    return lib
+
+
+def IntraMatrixToSparseDict(Dict):
+    """{chrom: dense N x N} -> {chrom: upper-triangle pixels} (:508-525)."""
+    out = {}
+    for chro, M in Dict.items():
+        T = np.triu(M.cpu().numpy() if hasattr(M, "cpu") else np.asarray(M))
+        x, y = np.nonzero(T)
+        out[chro] = _sparse_rec(x, y, T[x, y])
+    return out
+
+
+def _genome_chromsizes(genomeSizes_file, chroms):
+    """NPZ2Cooler.readChromSize (:212-223), Sort_Chromosomes order (:135-138)."""
+    lines = open(genomeSizes_file) if isinstance(genomeSizes_file, (str, os.PathLike)) else genomeSizes_file
+    sizes = {}
+    try:
+        for line in lines:
+            if isinstance(line, bytes):
+                line = line.decode()
+            f = line.strip().split()
+            if f and _chrom_ok(f[0].lstrip("chr"), chroms):
+                sizes[f[0].lstrip("chr")] = int(f[1])
+    finally:
+        if isinstance(genomeSizes_file, (str, os.PathLike)):
+            lines.close()
+    return [(c, sizes[c]) for c in Sort_Chromosomes(list(sizes))]
+
+
+def _upper_sum(x, y, v, n):
+    """Sum equal (x, y) pixels; (key-sorted) arrays."""
+    if x.size == 0:
+        return x, y, v
+    key = x * n + y
+    uk, inv = np.unique(key, return_inverse=True)
+    return uk // n, uk % n, np.bincount(inv, v, minlength=uk.size)
+
+
+def npz2cooler_tables(datasets, genomeSizes_file, chroms=("#", "X"), onlyIntra=True, dtype="int"):
+    """The pixel tables NPZ2Cooler writes (:100-303), one per resolution:
+    {res: (chromsizes [(name, length)], bin1, bin2, count)}.  Bins are
+    cooler's ``binnify`` (ceil(length / res) per chromosome, only the
+    chromosomes the data names); each block's local bins are offset by the
+    cumulative bin counts exactly as ``_generator`` offsets them (:296-299),
+    the intra blocks symmetrised then cut to the upper triangle (a lower
+    entry's value lands on its mirror, :290-293), pixels sorted by (bin1,
+    bin2) with equal ones summed (create_from_unordered's merge).  count is
+    int32 for dtype 'int' (traditional / unimputed), float64 otherwise."""
+    full = _genome_chromsizes(genomeSizes_file, chroms)
+    names = [c for c, _ in full]
+    out = {}
+    for res, lib in datasets.items():
+        Map = {}
+        for key in lib:
+            if "_" not in key and _chrom_ok(key, chroms):
+                Map[(key, key)] = key
+                continue
+            part = key.split("_")
+            if len(part) == 2 and _chrom_ok(part[0], chroms) and _chrom_ok(part[1], chroms):
+                Map[(part[0], part[1])] = key
+        subset = {c for pair in Map for c in pair}
+        cs = [(c, L) for c, L in full if c in subset]
+        cum = np.cumsum([-(-L // res) for _, L in cs]).astype(np.int64)  # bin_cumnums (:225-235)
+        nb = int(cum[-1]) if cum.size else 0
+        xs, ys, vs = [], [], []
+        for i, ci_name in enumerate(names):
+            for j in range(i, len(names)):
+                c1, c2 = ci_name, names[j]
+                if onlyIntra and c1 != c2:
+                    continue
+                ci, cj = i, j
+                if (c1, c2) not in Map:
+                    if (c2, c1) not in Map:
+                        continue
+                    c1, c2, ci, cj = c2, c1, j, i
+                d = lib[Map[(c1, c2)]]
+                x = np.asarray(d["bin1"], np.int64)
+                y = np.asarray(d["bin2"], np.int64)
+                v = np.asarray(d["IF"], np.float64)
+                if x.size == 0:
+                    continue
+                if ci > cj:
+                    x, y, ci, cj = y, x, cj, ci
+                if ci == cj:
+                    # lil: M[y, x] = M[x, y] then triu (:290-293): the upper
+                    # cell takes its lower mirror's value where one exists
+                    L = int(max(x.max(), y.max())) + 1
+                    x, y, v = _upper_sum(x, y, v, L)
+                    low = x > y
+                    ux, uy = np.where(low, y, x), np.where(low, x, y)
+                    o = np.lexsort((~low, uy, ux))  # per cell: the lower entry first
+                    ux, uy, v = ux[o], uy[o], v[o]
+                    first = np.ones(ux.size, bool)
+                    first[1:] = (ux[1:] != ux[:-1]) | (uy[1:] != uy[:-1])
+                    x, y, v = ux[first], uy[first], v[first]
+                else:
+                    x, y, v = _upper_sum(x, y, v, int(y.max()) + 1)
+                nz = v != 0
+                x, y, v = x[nz], y[nz], v[nz]
+                if ci > 0:
+                    x = x + cum[ci - 1]  # (positional, as the reference's Series access)
+                if cj > 0:
+                    y = y + cum[cj - 1]
+                xs.append(x)
+                ys.append(y)
+                vs.append(v)
+        if xs:
+            b1, b2, val = _upper_sum(np.concatenate(xs), np.concatenate(ys), np.concatenate(vs),
+                                     max(nb, int(max(map(np.max, ys)))) + 1)
+        else:
+            b1 = b2 = np.zeros(0, np.int64)
+            val = np.zeros(0)
+        out[res] = (cs, b1, b2, val.astype(np.int32) if dtype == "int" else val.astype(np.float64))
+    return out
+
+
+class NPZ2Cooler:
+    """Save the reference's sparse dicts into a multi-resolution cooler
+    (:100-210): ``datasets`` = {res: lib}, one ``outfil::res`` group per
+    resolution, appended to an existing file (mode 'a'); metadata
+    {'onlyIntra': str(onlyIntra)} as the reference stores it."""
+
+    def __init__(self, datasets, outfil, genomeSizes_file, chroms=("#", "X"), onlyIntra=True, dtype="int"):
+        from . import coolio
+        self.outfil = os.path.abspath(os.path.expanduser(outfil))
+        self.onlyIntra = onlyIntra
+        tabs = npz2cooler_tables(datasets, genomeSizes_file, chroms, onlyIntra, dtype)
+        meta = {"onlyIntra": str(onlyIntra)}
+        coolio.create_cooler(self.outfil, {res: t + (meta,) for res, t in tabs.items()}, mode="a")
+
+
+def merge_coolers(output_uri, input_uris):
+    """cooler.merge_coolers as TraditionalMatrixConstruction calls it
+    (:680-695): the inputs' pixels of one resolution summed into
+    ``output_uri`` (appended to its file); every input must have the same
+    bins."""
+    from . import coolio
+    tabs, cs, meta = [], None, None
+    for uri in input_uris:
+        with coolio.Cooler(uri) as c:
+            cur = [(n, int(c.chromsizes[n])) for n in c.chromnames]
+            if cs is not None and (cur != cs or c.binsize != binsize):
+                raise ValueError(f"merge_coolers: {uri} has different bins")
+            cs, binsize = cur, c.binsize
+            meta = c.info.get("metadata")
+            tabs.append(c.pixels_table())
+    b1 = np.concatenate([np.asarray(t[0], np.int64) for t in tabs])
+    b2 = np.concatenate([np.asarray(t[1], np.int64) for t in tabs])
+    dt = tabs[0][2].dtype
+    v = np.concatenate([np.asarray(t[2], np.float64) for t in tabs])
+    n = int(sum(-(-L // binsize) for _, L in cs)) + 1
+    b1, b2, v = _upper_sum(b1, b2, v, max(n, int(b2.max(initial=0)) + 1))
+    path, grp = output_uri.split("::") if "::" in output_uri else (output_uri, str(binsize))
+    try:
+        meta = json.loads(meta) if isinstance(meta, str) else meta
+    except ValueError:
+        meta = None
+    coolio.create_cooler(path, {grp: (cs, b1, b2, v.astype(dt), meta)}, mode="a")
+
+
+def _balance_all(coolers, wholeRes, localRes):
+    """The `cooler balance --ignore-diags 1 [--cis-only] --force` calls
+    (:699-714, :1533-1544): genome-wide for wholeRes, --cis-only for
+    localRes, weights written in place."""
+    from . import coolio
+    for res in wholeRes:
+        for f in coolers:
+            coolio.balance_cooler(f"{f}::{res}", ignore_diags=1, cis_only=False)
+    for res in localRes:
+        for f in coolers:
+            coolio.balance_cooler(f"{f}::{res}", ignore_diags=1, cis_only=True)
+
+
+def TraditionalMatrixConstruction(OutPath, RepPath, genomeSize, wholeRes, localRes, chroms=("#", "X"),
+                                  balance=True):
+    """`hichap matrix` for traditional (non-allelic) data (:617-717): per
+    replicate directory every ``*_Valid.bed`` binned on the GPU (all files
+    of a replicate together, as the reference's ``cat``), written to
+    ``OutPath/Cooler/<prefix>Multi.cool`` (whole-genome groups for wholeRes,
+    intra-chromosome groups for localRes), the replicates merged into
+    ``Merged_Multi.cool``, then every cooler balanced in place.  Returns the
+    cooler paths (replicates, then merged).  (The reference takes the bed
+    files in os.listdir order; sorted here -- the counts do not depend on it,
+    the prefix is the first name.)"""
+    CoolerPath = os.path.join(OutPath, "Cooler")
+    os.makedirs(CoolerPath, exist_ok=True)
+    reps = []
+    for rep_p in RepPath:
+        files = sorted(i for i in os.listdir(rep_p) if "_Valid.bed" in i)
+        if not files:
+            raise FileNotFoundError(f"no *_Valid.bed in {rep_p}")
+        prefix = files[0].split("Valid")[0]
+        Whole_Lib, Local_Lib = TraditionalMatrixBuilding([os.path.join(rep_p, f) for f in files], genomeSize,
+                                                         wholeRes, localRes, chroms)
+        out = os.path.join(CoolerPath, prefix + "Multi.cool")
+        if os.path.exists(out):
+            os.remove(out)  # written afresh (the reference appends into an existing file)
+        NPZ2Cooler(Whole_Lib, out, genomeSize, chroms, onlyIntra=False, dtype="int")
+        NPZ2Cooler(Local_Lib, out, genomeSize, chroms, onlyIntra=True, dtype="int")
+        reps.append(out)
+    merged = os.path.join(CoolerPath, "Merged_Multi.cool")
+    if os.path.exists(merged):
+        os.remove(merged)
+    for res in list(wholeRes) + list(localRes):
+        merge_coolers(f"{merged}::{res}", [f"{r}::{res}" for r in reps])
+    coolers = reps + [merged]
+    if balance:
+        _balance_all(coolers, wholeRes, localRes)
+    return coolers
+
+
+def _hap_genome(genomeSize, chroms, out_path):
+    """Hap_genomeSize (:1551-1565): 'M' + chrom and 'P' + chrom lines."""
+    lines = open(genomeSize).read().splitlines() if isinstance(genomeSize, (str, os.PathLike)) else \
+        [x.decode() if isinstance(x, bytes) else x for x in genomeSize]
+    hap, names = [], []
+    for line in lines:
+        f = line.strip().split()
+        if not f:
+            continue
+        f[0] = f[0].lstrip("chr")
+        if _chrom_ok(f[0], chroms):
+            names += ["M" + f[0], "P" + f[0]]
+            hap += ["M" + "\t".join(f) + "\n", "P" + "\t".join(f) + "\n"]
+    with open(out_path, "w") as fh:
+        fh.writelines(hap)
+    return out_path, names
+
+
+def _haplotype_coolers(OutPath, prefix, genomeSize, wholeRes, localRes, chroms, DataSets):
+    """The cooler part of HaplotypeMatrixBuilding (:1501-1638) on its
+    DataSets: traditional cooler (int, ICE-balanced in place), unimputed
+    haplotype cooler (int), two-step corrected imputed haplotype cooler
+    (float: GenomeWideMatrixCorrection per wholeRes, IntraChromMatrixCorrection
+    per localRes) and the gap file ``<prefix>Imputated_Gap.npz``."""
+    trad = os.path.join(OutPath, prefix + "Traditional_Multi.cool")
+    for f in (trad,):
+        if os.path.exists(f):
+            os.remove(f)
+    W = {res: WholeMatrixToSparseDict(DataSets["Tradition_Whole"][res]["Bins"],
+                                      DataSets["Tradition_Whole"][res]["Matrix"]) for res in wholeRes}
+    L = {res: IntraMatrixToSparseDict(DataSets["Tradition_Local"][res]) for res in localRes}
+    NPZ2Cooler(W, trad, genomeSize, chroms, onlyIntra=False, dtype="int")
+    NPZ2Cooler(L, trad, genomeSize, chroms, onlyIntra=True, dtype="int")
+    _balance_all([trad], wholeRes, localRes)
+    hap_gs, hap_chroms = _hap_genome(genomeSize, chroms, os.path.join(OutPath, "Hap_genomeSize"))
+    unimp = os.path.join(OutPath, prefix + "UnImputated_Haplotype_Multi.cool")
+    imp = os.path.join(OutPath, prefix + "Imputated_Haplotype_Multi.cool")
+    for f in (unimp, imp):
+        if os.path.exists(f):
+            os.remove(f)
+    W = {res: WholeMatrixToSparseDict(DataSets["UnImputated_Whole"][res]["Bins"],
+                                      DataSets["UnImputated_Whole"][res]["Matrix"]) for res in wholeRes}
+    L = {res: IntraMatrixToSparseDict(DataSets["UnImputated_Local"][res]) for res in localRes}
+    NPZ2Cooler(W, unimp, hap_gs, hap_chroms, onlyIntra=False, dtype="int")
+    NPZ2Cooler(L, unimp, hap_gs, hap_chroms, onlyIntra=True, dtype="int")
+    BW = {}
+    for res in wholeRes:
+        hb = DataSets["Imputated_Whole"][res]["Bins"]
+        Bal = GenomeWideMatrixCorrection(DataSets["Tradition_Whole"][res]["Bins"], hb,
+                                         DataSets["Tradition_Whole"][res]["Matrix"],
+                                         DataSets["Imputated_Whole"][res]["Matrix"])
+        BW[res] = WholeMatrixToSparseDict(hb, Bal)
+    BL, Gap_Local = {}, {}
+    for res in localRes:
+        Nor_Lib, Gap_Lib = IntraChromMatrixCorrection(DataSets["Tradition_Local"][res],
+                                                      DataSets["Imputated_Local"][res])
+        BL[res] = IntraMatrixToSparseDict(Nor_Lib)
+        Gap_Local[str(res)] = Gap_Lib
+    # np.savez of the per-resolution dicts, as the reference saves them (:1616-1617)
+    np.savez(os.path.join(OutPath, prefix + "Imputated_Gap.npz"),
+             **{k: np.array(v, dtype=object) for k, v in Gap_Local.items()})
+    NPZ2Cooler(BW, imp, hap_gs, hap_chroms, onlyIntra=False, dtype="float")
+    NPZ2Cooler(BL, imp, hap_gs, hap_chroms, onlyIntra=True, dtype="float")
+    return trad, unimp, imp
+
+
+_HAP_BEDS = ("Bi_Allelic", "M_M", "M_P", "P_P", "P_M")
+
+
+def _haplotype_bed_files(BedPath):
+    """The five allelic beds of a replicate directory (:1061-1074)."""
+    files = sorted(i for i in os.listdir(BedPath) if any(k + ".bed" in i for k in _HAP_BEDS))
+    found = {k: [os.path.join(BedPath, f) for f in files if k + ".bed" in f] for k in _HAP_BEDS}
+    for k in ("Bi_Allelic", "M_M", "M_P", "P_P", "P_M"):
+        if not found[k]:
+            raise FileNotFoundError(f"Missing file {k}.bed in {BedPath}")
+    return files[0].split("Valid")[0], {k: v if len(v) > 1 else v[0] for k, v in found.items()}
+
+
+def HaplotypeMatrixConstruction(OutPath, RepPath, genomeSize, wholeRes, localRes, Imputation_region=10000000,
+                                Imputation_min=2, Imputation_ratio=0.9, chroms=("#", "X")):
+    """`hichap matrix` for haplotype-resolved data (:1641-1860): per replicate
+    the GPU builds the traditional, unimputed and imputed matrices
+    (HaplotypeMatrixBuilding), writes its three coolers + gap file under
+    ``OutPath/Cooler`` (traditional ICE-balanced in place, imputed two-step
+    corrected); with several replicates their matrices are summed and the
+    same is written with prefix ``Merged_``.  Returns {prefix: (traditional,
+    unimputed, imputed) cooler paths}.  (The reference's one-replicate path
+    omits genomeSize and raises TypeError, :1676-1683; here it runs.)"""
+    CoolerPath = os.path.join(OutPath, "Cooler")
+    os.makedirs(CoolerPath, exist_ok=True)
+    out, All = {}, None
+    for rep_p in RepPath:
+        prefix, beds = _haplotype_bed_files(rep_p)
+        DataSets = HaplotypeMatrixBuilding(beds, genomeSize, wholeRes, localRes, Imputation_region, Imputation_min,
+                                           Imputation_ratio, chroms)
+        out[prefix] = _haplotype_coolers(CoolerPath, prefix, genomeSize, wholeRes, localRes, chroms, DataSets)
+        if len(RepPath) == 1:
+            return out
+        if All is None:
+            All = DataSets
+        else:
+            for kind in ("Tradition", "UnImputated", "Imputated"):
+                for res in wholeRes:
+                    All[kind + "_Whole"][res]["Matrix"] = All[kind + "_Whole"][res]["Matrix"] + \
+                        DataSets[kind + "_Whole"][res]["Matrix"]
+                for res in localRes:
+                    for k in All[kind + "_Local"][res]:
+                        All[kind + "_Local"][res][k] = All[kind + "_Local"][res][k] + DataSets[kind + "_Local"][res][k]
+    out["Merged_"] = _haplotype_coolers(CoolerPath, "Merged_", genomeSize, wholeRes, localRes, chroms, All)
+    return out
