@@ -193,6 +193,7 @@ struct PxRows {
     const long long* lo_ptr;            // nloc + 1
     long long row_lo, nloc;
     int nJ, band_w, band_w4;
+    int upper;  // g_upper_tiles: tile entries only where J(col) >= J(row)
     // PASS 0
     uint16_t* cnt;
     uint16_t* cntn;
@@ -282,6 +283,10 @@ __global__ __launch_bounds__(256) void k_px_rows(PxRows p) {
         const int J = (int)(col >> kWBits);
         unsigned long long mask = __ballot(valid);
         ent_wave += __popcll(mask) + __popcll(mwl);
+        if (p.upper) {  // a lower-tile entry is stored as its mirror (the column side of row col)
+            valid = valid && J >= (int)(r >> kWBits);
+            mask = __ballot(valid);
+        }
         while (mask) {
             const int first = __ffsll((long long)mask) - 1;
             const int Jr = __shfl(J, first, 64);
@@ -509,6 +514,7 @@ void build_from_device_pixels(const Id* b1, const Id* b2, const Cnt* cnt, int64_
     P.nJ = nJ;
     P.band_w = W;
     P.band_w4 = W4;
+    P.upper = g_upper_tiles ? 1 : 0;
     P.cnt = cnt_w.p;
     P.cntn = cnt_n.p;
     P.row_band = rband.p;

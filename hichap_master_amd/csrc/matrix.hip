@@ -749,6 +749,7 @@ int hh_matrix_from_pixels(const int64_t* bin1, const int64_t* bin2, const double
                     continue;
                 }
                 if (vals[k] > kCntMax) ++wptr[r + 1];
+                else if (g_upper_tiles && (cols[k] >> kWBits) < ((row_lo + r) >> kWBits)) continue;  // stored as its mirror
                 else if (vals[k] <= kNarrowMax) ++cntn[(size_t)r * nJ + (cols[k] >> kWBits)];
                 else ++cntw[(size_t)r * nJ + (cols[k] >> kWBits)];
             }
@@ -771,6 +772,7 @@ int hh_matrix_from_pixels(const int64_t* bin1, const int64_t* bin2, const double
                 if (in_band(row_lo + r, cols[q], vals[q]) || in_nib(row_lo + r, cols[q], vals[q])) continue;
                 if (vals[q] > kCntMax) { wcol[wp] = cols[q]; wcnt[wp++] = vals[q]; continue; }
                 const int32_t J = cols[q] >> kWBits;
+                if (g_upper_tiles && J < (int32_t)((row_lo + r) >> kWBits)) continue;
                 if (J != curJ) {
                     const int32_t t = P.tile_of[rb * nJ + J];
                     pos = P.tile_ent[t] + P.tile_rp[(size_t)t * (kR + 1) + k];
