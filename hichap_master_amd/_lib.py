@@ -31,7 +31,7 @@ class MatrixInfo(C.Structure):
         "n_units", "n_wide", "device_bytes", "n_slots_narrow", "payload_bytes")] + [
         (n, C.c_int32) for n in ("n_chroms", "ignore_diags", "cis_only", "device", "band_w", "n_units_flat")] + [
         ("n_band", C.c_int64), ("payload_bytes_flat", C.c_int64)] + [
-        (n, C.c_int32) for n in ("band_w4", "pad2_")]
+        (n, C.c_int32) for n in ("band_w4", "upper")]
 
 
 class SynthParams(C.Structure):
@@ -98,6 +98,8 @@ SIGNATURES = {
     "hh_comm_init": (C.c_int, [P, I32, I32, C.POINTER(P)]),
     "hh_comm_free": (C.c_int, [P]),
     "hh_comm_allgather": (C.c_int, [P, I64, P, P, P]),
+    "hh_comm_reduce_scatter": (C.c_int, [P, I64, P, P, P]),
+    "hh_ice_set_column_exchange": (C.c_int, [P, I32, I32, P, P, P, P, P]),
     "hh_ice_balance_sharded": (C.c_int, [P, C.POINTER(IceOpts), I32, I32, P, P, P, P, P, P, P, P, PF64, P]),
     "hh_ice_balance_cis_local": (C.c_int, [P, C.POINTER(IceOpts), I32, I64, P, P, P, P, P, P, P, PF64, P]),
     "hh_ice_filters_sharded": (C.c_int, [P, I32, P, P, P, P]),

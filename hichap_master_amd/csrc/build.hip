@@ -514,7 +514,7 @@ void build_from_device_pixels(const Id* b1, const Id* b2, const Cnt* cnt, int64_
     P.nJ = nJ;
     P.band_w = W;
     P.band_w4 = W4;
-    P.upper = g_upper_tiles ? 1 : 0;
+    P.upper = upper_tiles_on(nJ) ? 1 : 0;
     P.cnt = cnt_w.p;
     P.cntn = cnt_n.p;
     P.row_band = rband.p;
@@ -546,7 +546,7 @@ void build_from_device_pixels(const Id* b1, const Id* b2, const Cnt* cnt, int64_
     phase("download counts");
     std::vector<uint16_t> bg = bin_groups(*m);
     std::vector<uint16_t> rgroup(bg.begin() + row_lo, bg.begin() + row_hi);
-    TilePlan TP = plan_tiles(hc.data(), hnarrow.data(), nloc, nJ, rgroup);
+    TilePlan TP = plan_tiles(hc.data(), hnarrow.data(), nloc, nJ, rgroup, row_lo, P.upper != 0);
     phase("plan_tiles (host)");
     upload_plan(TP, *m, s);
     phase("upload plan");

@@ -70,6 +70,15 @@ int hh_comm_allgather(const double* send, int64_t count, double* recv, void* com
     });
 }
 
+int hh_comm_reduce_scatter(const int64_t* send, int64_t count, int64_t* recv, void* comm, void* stream) {
+    return guard([&] {
+        auto* c = static_cast<hh_comm*>(comm);
+        HH_REQUIRE(c && c->comm && count >= 0, "bad arguments");
+        nccl_check(ncclReduceScatter(send, recv, (size_t)count, ncclInt64, ncclSum, c->comm, as_stream(stream)),
+                   "ncclReduceScatter");
+    });
+}
+
 }  // extern "C"
 
 namespace {
@@ -161,6 +170,11 @@ struct Sharded {
             local.alloc(maxlen);
             local.zero(hh::as_stream(stream));
             gathered.alloc((size_t)world * maxlen);
+            // the column side of upper-triangle tiles: RCCL's reduce-scatter
+            // when the exchange is the library's own, else through `ag`
+            const bool rccl = ag == hh_comm_allgather;
+            ok(hh_ice_set_column_exchange(S, world, -1, rr.data(), rccl ? hh_comm_reduce_scatter : nullptr,
+                                          rccl ? user : nullptr, ag, user));
         });
     }
     void filters() {

@@ -91,15 +91,53 @@ __device__ __forceinline__ uint4 ld16(const uint4* p) {
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 
+// Column side of a strictly upper tile: every stored count
+// also feeds its column, count * B[row] added to the block's int64 LDS column
+// accumulator -- at the entry's own byte offset, since the accumulator uses
+// the bias slice's rotated image.  B = round(b * 2^e) with one power-of-two
+// scale per sweep (k_fixscale), so the integer sums are exact whatever order
+// the waves add in: deterministic, and the same on any number of GPUs.
+typedef unsigned long long u64;
+__device__ __forceinline__ u64 fixb(double b, double scale) { return (u64)__double2ll_rn(b * scale); }
+__device__ __forceinline__ void lds_add_u64(u64* cacc, uint32_t byteoff, u64 v) {
+    __hip_atomic_fetch_add(reinterpret_cast<u64*>(reinterpret_cast<char*>(cacc) + byteoff), v, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// (branch-free: a padding entry adds 0 at offset 0; B < 2^62 / count total,
+// so count * B is the 64-bit product of a small count and B)
+__device__ __forceinline__ u64 cmul(uint32_t c, u64 B) {
+    return (u64)c * (uint32_t)B + ((u64)(c * (uint32_t)(B >> 32)) << 32);
+}
+template <int EPV>
+__device__ __forceinline__ void col_add(const uint4 v, u64 B, u64* __restrict__ cacc) {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        if constexpr (EPV == 8) {  // narrow: byteoff | count (0..7), two per word
+            lds_add_u64(cacc, w[i] & 0xFFF8u, cmul(w[i] & 7u, B));
+            lds_add_u64(cacc, (w[i] >> 16) & 0xFFF8u, cmul((w[i] >> 16) & 7u, B));
+        } else {  // wide: count << 16 | byteoff
+            lds_add_u64(cacc, w[i] & 0xFFFFu, cmul(w[i] >> 16, B));
+        }
+    }
+}
+
 // Rows of one segment of a tile (EPV entries per uint4: 8 narrow uint16, 4
 // wide uint32).  Lane groups of G lanes take one row each, NB rows per group
 // at a time (their loads issued together).  acc[v] (v = row
 // index within the unit, + nr for the wide segment) is owned by one lane
 // group per tile -> fixed summation order.
-template <int G, int NB, int ABL, int EPV>
+// COL: the tile is strictly upper (column side into cacc, B from bblk = b of
+// the row-block's first row, scaled by `scale`)
+struct ColArgs {
+    const u64* bblk;  // B = round(b 2^e) of the tile's row-block (k_fixscale), row 0 first
+    u64* cacc;
+};
+
+template <int G, int NB, int ABL, int EPV, bool COL = false>
 __device__ __forceinline__ void tile_rows(const uint4* __restrict__ pay4, const uint32_t* __restrict__ rp,
                                           const double* __restrict__ bl, double* __restrict__ acc, int ra,
-                                          int rb, int wave, int lane) {
+                                          int rb, int wave, int lane, ColArgs ca = ColArgs{}) {
     constexpr int RP = 64 / G;              // rows per wave step
     constexpr int S = kSweepWaves * RP;     // row distance between a wave's batches
     constexpr int SH = EPV == 8 ? 3 : 2;
@@ -108,13 +146,16 @@ __device__ __forceinline__ void tile_rows(const uint4* __restrict__ pay4, const 
     for (int r0 = ra + wave * RP; r0 < rb; r0 += NB * S) {
         uint32_t q[NB], qe[NB];
         double a[NB], a1[NB];
+        u64 B[NB];
 #pragma unroll
         for (int k = 0; k < NB; ++k) {
             const int r = r0 + k * S + gi;
             q[k] = qe[k] = 0;
+            B[k] = 0;
             if (r < rb) {
                 q[k] = (rp[r] >> SH) + li;
                 qe[k] = rp[r + 1] >> SH;
+                if (COL) B[k] = ca.bblk[r];
             }
             a[k] = 0.0;
             a1[k] = 0.0;
@@ -141,6 +182,7 @@ __device__ __forceinline__ void tile_rows(const uint4* __restrict__ pay4, const 
                 } else {
                     tile_dot(v[k], bl, a[k], a1[k]);
                 }
+                if (COL) col_add<EPV>(v[k], B[k], ca.cacc);
                 q[k] += G;
                 more |= q[k] < qe[k];
             }
@@ -160,11 +202,11 @@ __device__ __forceinline__ void tile_rows(const uint4* __restrict__ pay4, const 
 // band of the tile's length order (perm[lo..hi), all within a 2x length
 // range) go to lane groups of width G, so the rows a wave carries at once
 // have similar lengths and few lanes idle.
-template <int G, int NB, int ABL, int EPV>
+template <int G, int NB, int ABL, int EPV, bool COL = false>
 __device__ __forceinline__ void band_rows(const uint4* __restrict__ pay4, const uint32_t* __restrict__ rp,
                                           const uint16_t* __restrict__ perm, int lo, int hi,
                                           const double* __restrict__ bl, double* __restrict__ acc, int wave,
-                                          int lane) {
+                                          int lane, ColArgs ca = ColArgs{}) {
     constexpr int RP = 64 / G;
     constexpr int S = kSweepWaves * RP;
     constexpr int SH = EPV == 8 ? 3 : 2;
@@ -174,16 +216,19 @@ __device__ __forceinline__ void band_rows(const uint4* __restrict__ pay4, const 
         uint32_t q[NB], qe[NB];
         int row[NB];
         double a[NB], a1[NB];
+        u64 B[NB];
 #pragma unroll
         for (int k = 0; k < NB; ++k) {
             const int v = v0 + k * S + gi;
             q[k] = qe[k] = 0;
             row[k] = -1;
+            B[k] = 0;
             if (v < hi) {
                 const int r = perm[v];
                 row[k] = r;
                 q[k] = (rp[r] >> SH) + li;
                 qe[k] = rp[r + 1] >> SH;
+                if (COL) B[k] = ca.bblk[r];
             }
             a[k] = 0.0;
             a1[k] = 0.0;
@@ -210,6 +255,7 @@ __device__ __forceinline__ void band_rows(const uint4* __restrict__ pay4, const 
                 } else {
                     tile_dot(v[k], bl, a[k], a1[k]);
                 }
+                if (COL) col_add<EPV>(v[k], B[k], ca.cacc);
                 q[k] += G;
                 more |= q[k] < qe[k];
             }
@@ -289,11 +335,11 @@ __device__ __forceinline__ void flat_load(const uint4* __restrict__ pay4, uint32
 // holds the lane's run [s, s + U), s = q0 + lane U.  ic = the row holding
 // q0 - 1 (q0 at the first step); rows [.., i1) belong to the wave; fst =
 // uint4 starts of the segment's nonempty rows (fst[nfr] = end), fr = their ids.
-template <int U, int ABL, int EPV>
+template <int U, int ABL, int EPV, bool COL = false>
 __device__ __forceinline__ void flat_step(const uint4 (&v)[U], uint32_t q0, uint32_t qb, int& ic, int i1,
                                           const uint16_t* __restrict__ fst, const uint16_t* __restrict__ fr,
                                           int nfr, const double* __restrict__ bl, double* __restrict__ acc,
-                                          int lane) {
+                                          int lane, ColArgs ca = ColArgs{}) {
     const uint32_t s = q0 + (uint32_t)lane * U;
     const bool act = s < qb;
     // row of s: the largest i with start <= s; at most lane U + 1 rows
@@ -309,6 +355,11 @@ __device__ __forceinline__ void flat_step(const uint4 (&v)[U], uint32_t q0, uint
     for (int k = 0; k < U; ++k) {
         nb[k] = fst[min(lo + 1 + k, nfr)];
         rid[k] = fr[min(lo + k, nfr - 1)];
+    }
+    u64 Bq[COL ? U : 1];  // the column side's B of rows lo..
+    if (COL) {
+#pragma unroll
+        for (int k = 0; k < U; ++k) Bq[k] = ca.bblk[rid[k]];
     }
     double x = 0.0, h = 0.0, cv[U];
     uint32_t cr[U];
@@ -341,6 +392,13 @@ __device__ __forceinline__ void flat_step(const uint4 (&v)[U], uint32_t q0, uint
             }
         }
         x += ABL == 1 ? (double)(v[k].x + v[k].y + v[k].z + v[k].w) : flat_dot<EPV>(v[k], bl);
+        if (COL) {
+            u64 B = Bq[0];
+#pragma unroll
+            for (int jj = 1; jj <= k; ++jj)
+                if (j == jj) B = Bq[jj];
+            col_add<EPV>(v[k], B, ca.cacc);
+        }
     }
     uint32_t orow = rid[0];
 #pragma unroll
@@ -381,10 +439,11 @@ __device__ __forceinline__ void flat_step(const uint4 (&v)[U], uint32_t q0, uint
 // tail + heads of one that continues), later steps add through lane 0 -- so
 // no row ids, no stash and no read-modify-write inside the walk (registers
 // for U = 8).  accc[i] is mapped to the row accumulator after the segment.
-template <int U, int ABL, int EPV>
+template <int U, int ABL, int EPV, bool COL = false>
 __device__ __forceinline__ void flat_step_c(const uint4 (&v)[U], uint32_t q0, uint32_t qb, int& ic, int i1,
                                             const uint16_t* __restrict__ fst, int nfr,
-                                            const double* __restrict__ bl, double* __restrict__ accc, int lane) {
+                                            const double* __restrict__ bl, double* __restrict__ accc, int lane,
+                                            ColArgs ca = ColArgs{}, const uint16_t* __restrict__ fid = nullptr) {
     const uint32_t s = q0 + (uint32_t)lane * U;
     const bool act = s < qb;
     int lo = ic, hi = min(i1 - 1, ic + lane * U + 1);
@@ -396,6 +455,18 @@ __device__ __forceinline__ void flat_step_c(const uint4 (&v)[U], uint32_t q0, ui
     uint32_t nb[U];
 #pragma unroll
     for (int k = 0; k < U - 1; ++k) nb[k] = fst[min(lo + 1 + k, nfr)];
+    // the column side's B of compact rows lo .. lo + CB - 1 (fid: their row
+    // ids, null = identity); a run reaching further rows (rare: ~3 uint4 per
+    // row) loads those on the spot
+    constexpr int CB = COL ? (U < 4 ? U : 4) : 1;
+    u64 Bq[CB];
+    if (COL) {
+#pragma unroll
+        for (int k = 0; k < CB; ++k) {
+            const int i = min(lo + k, nfr - 1);
+            Bq[k] = ca.bblk[fid ? (int)fid[i] : i];
+        }
+    }
     double x = 0.0, h = 0.0;
     bool inhead = head;
     int j = 0;
@@ -418,6 +489,17 @@ __device__ __forceinline__ void flat_step_c(const uint4 (&v)[U], uint32_t q0, ui
             }
         }
         x += ABL == 1 ? (double)(v[k].x + v[k].y + v[k].z + v[k].w) : flat_dot<EPV>(v[k], bl);
+        if (COL) {
+            u64 B = Bq[0];
+#pragma unroll
+            for (int jj = 1; jj < CB && jj <= k; ++jj)
+                if (j == jj) B = Bq[jj];
+            if (k >= CB && j >= CB) {
+                const int i = min(lo + j, nfr - 1);
+                B = ca.bblk[fid ? (int)fid[i] : i];
+            }
+            col_add<EPV>(v[k], B, ca.cacc);
+        }
     }
     if (inhead) h = x;
     const bool tail = act && !inhead;
@@ -438,14 +520,15 @@ __device__ __forceinline__ void flat_step_c(const uint4 (&v)[U], uint32_t q0, ui
     ic = __shfl(lo + j, 63, 64);
 }
 
-template <int U, int ABL, int EPV>
+template <int U, int ABL, int EPV, bool COL = false>
 __device__ __forceinline__ void flat_seg_c(const uint4* __restrict__ pay4, uint4 (&v)[U], uint32_t qa, uint32_t qb,
                                            int i0, int i1, const uint16_t* __restrict__ fst, int nfr,
-                                           const double* __restrict__ bl, double* __restrict__ accc, int lane) {
+                                           const double* __restrict__ bl, double* __restrict__ accc, int lane,
+                                           ColArgs ca = ColArgs{}, const uint16_t* __restrict__ fid = nullptr) {
     if (i0 >= i1) return;
     int ic = i0;
     for (uint32_t q0 = qa;;) {
-        flat_step_c<U, ABL, EPV>(v, q0, qb, ic, i1, fst, nfr, bl, accc, lane);
+        flat_step_c<U, ABL, EPV, COL>(v, q0, qb, ic, i1, fst, nfr, bl, accc, lane, ca, fid);
         q0 += 64u * U;
         if (q0 >= qb) break;
         flat_load<U>(pay4, q0 + (uint32_t)lane * U, qa, qb, v);
@@ -455,17 +538,18 @@ __device__ __forceinline__ void flat_seg_c(const uint4* __restrict__ pay4, uint4
 // flat_seg_c / flat_seg with the next step's run loaded before the current
 // step is walked (two runs in registers: the one-wave-per-tile kernel has
 // the VGPRs for it); the same steps in the same order, bitwise the same sums
-template <int U, int ABL, int EPV>
+template <int U, int ABL, int EPV, bool COL = false>
 __device__ __forceinline__ void flat_seg_c_pipe(const uint4* __restrict__ pay4, uint4 (&v)[U], uint32_t qa, uint32_t qb,
                                                 int i0, int i1, const uint16_t* __restrict__ fst, int nfr,
-                                                const double* __restrict__ bl, double* __restrict__ accc, int lane) {
+                                                const double* __restrict__ bl, double* __restrict__ accc, int lane,
+                                                ColArgs ca = ColArgs{}, const uint16_t* __restrict__ fid = nullptr) {
     if (i0 >= i1) return;
     int ic = i0;
     for (uint32_t q0 = qa;;) {
         const uint32_t qn = q0 + 64u * U;
         uint4 vn[U];
         if (qn < qb) flat_load<U>(pay4, qn + (uint32_t)lane * U, qa, qb, vn);
-        flat_step_c<U, ABL, EPV>(v, q0, qb, ic, i1, fst, nfr, bl, accc, lane);
+        flat_step_c<U, ABL, EPV, COL>(v, q0, qb, ic, i1, fst, nfr, bl, accc, lane, ca, fid);
         if (qn >= qb) break;
 #pragma unroll
         for (int k = 0; k < U; ++k) v[k] = vn[k];
@@ -473,18 +557,18 @@ __device__ __forceinline__ void flat_seg_c_pipe(const uint4* __restrict__ pay4, 
     }
 }
 
-template <int U, int ABL, int EPV>
+template <int U, int ABL, int EPV, bool COL = false>
 __device__ __forceinline__ void flat_seg_pipe(const uint4* __restrict__ pay4, uint4 (&v)[U], uint32_t qa, uint32_t qb,
                                               int i0, int i1, const uint16_t* __restrict__ fst,
                                               const uint16_t* __restrict__ fr, int nfr, const double* __restrict__ bl,
-                                              double* __restrict__ acc, int lane) {
+                                              double* __restrict__ acc, int lane, ColArgs ca = ColArgs{}) {
     if (i0 >= i1) return;
     int ic = i0;
     for (uint32_t q0 = qa;;) {
         const uint32_t qn = q0 + 64u * U;
         uint4 vn[U];
         if (qn < qb) flat_load<U>(pay4, qn + (uint32_t)lane * U, qa, qb, vn);
-        flat_step<U, ABL, EPV>(v, q0, qb, ic, i1, fst, fr, nfr, bl, acc, lane);
+        flat_step<U, ABL, EPV, COL>(v, q0, qb, ic, i1, fst, fr, nfr, bl, acc, lane, ca);
         if (qn >= qb) break;
 #pragma unroll
         for (int k = 0; k < U; ++k) v[k] = vn[k];
@@ -495,40 +579,40 @@ __device__ __forceinline__ void flat_seg_pipe(const uint4* __restrict__ pay4, ui
 // A wave's rows [i0, i1) = uint4 [qa, qb) of one segment, the first step's
 // run already loaded into v (its loads were issued before the tile's LDS
 // staging, so they fly while the block stages).
-template <int U, int ABL, int EPV>
+template <int U, int ABL, int EPV, bool COL = false>
 __device__ __forceinline__ void flat_seg(const uint4* __restrict__ pay4, uint4 (&v)[U], uint32_t qa, uint32_t qb,
                                          int i0, int i1, const uint16_t* __restrict__ fst,
                                          const uint16_t* __restrict__ fr, int nfr, const double* __restrict__ bl,
-                                         double* __restrict__ acc, int lane) {
+                                         double* __restrict__ acc, int lane, ColArgs ca = ColArgs{}) {
     if (i0 >= i1) return;
     int ic = i0;
     for (uint32_t q0 = qa;;) {
-        flat_step<U, ABL, EPV>(v, q0, qb, ic, i1, fst, fr, nfr, bl, acc, lane);
+        flat_step<U, ABL, EPV, COL>(v, q0, qb, ic, i1, fst, fr, nfr, bl, acc, lane, ca);
         q0 += 64u * U;
         if (q0 >= qb) break;
         flat_load<U>(pay4, q0 + (uint32_t)lane * U, qa, qb, v);
     }
 }
 
-template <int NB, int ABL, int EPV>
+template <int NB, int ABL, int EPV, bool COL = false>
 __device__ __forceinline__ void sweep_bands(const uint16_t* band, const uint4* pay4, const uint32_t* rp,
                                             const uint16_t* perm, const double* bl, double* acc, int wave,
-                                            int lane) {
-    if (band[1] > band[0]) band_rows<64, NB, ABL, EPV>(pay4, rp, perm, band[0], band[1], bl, acc, wave, lane);
-    if (band[2] > band[1]) band_rows<32, NB, ABL, EPV>(pay4, rp, perm, band[1], band[2], bl, acc, wave, lane);
-    if (band[3] > band[2]) band_rows<16, NB, ABL, EPV>(pay4, rp, perm, band[2], band[3], bl, acc, wave, lane);
-    if (band[4] > band[3]) band_rows<8, NB, ABL, EPV>(pay4, rp, perm, band[3], band[4], bl, acc, wave, lane);
-    if (band[5] > band[4]) band_rows<4, NB, ABL, EPV>(pay4, rp, perm, band[4], band[5], bl, acc, wave, lane);
+                                            int lane, ColArgs ca = ColArgs{}) {
+    if (band[1] > band[0]) band_rows<64, NB, ABL, EPV, COL>(pay4, rp, perm, band[0], band[1], bl, acc, wave, lane, ca);
+    if (band[2] > band[1]) band_rows<32, NB, ABL, EPV, COL>(pay4, rp, perm, band[1], band[2], bl, acc, wave, lane, ca);
+    if (band[3] > band[2]) band_rows<16, NB, ABL, EPV, COL>(pay4, rp, perm, band[2], band[3], bl, acc, wave, lane, ca);
+    if (band[4] > band[3]) band_rows<8, NB, ABL, EPV, COL>(pay4, rp, perm, band[3], band[4], bl, acc, wave, lane, ca);
+    if (band[5] > band[4]) band_rows<4, NB, ABL, EPV, COL>(pay4, rp, perm, band[4], band[5], bl, acc, wave, lane, ca);
 }
 
-template <int NB, int ABL, int EPV>
+template <int NB, int ABL, int EPV, bool COL = false>
 __device__ __forceinline__ void sweep_rows(uint32_t mean, const uint4* pay4, const uint32_t* rp, const double* bl,
-                                           double* acc, int ra, int rb, int wave, int lane) {
-    if (mean >= 48) tile_rows<64, NB, ABL, EPV>(pay4, rp, bl, acc, ra, rb, wave, lane);
-    else if (mean >= 24) tile_rows<32, NB, ABL, EPV>(pay4, rp, bl, acc, ra, rb, wave, lane);
-    else if (mean >= 12) tile_rows<16, NB, ABL, EPV>(pay4, rp, bl, acc, ra, rb, wave, lane);
-    else if (mean >= 6) tile_rows<8, NB, ABL, EPV>(pay4, rp, bl, acc, ra, rb, wave, lane);
-    else tile_rows<4, NB, ABL, EPV>(pay4, rp, bl, acc, ra, rb, wave, lane);
+                                           double* acc, int ra, int rb, int wave, int lane, ColArgs ca = ColArgs{}) {
+    if (mean >= 48) tile_rows<64, NB, ABL, EPV, COL>(pay4, rp, bl, acc, ra, rb, wave, lane, ca);
+    else if (mean >= 24) tile_rows<32, NB, ABL, EPV, COL>(pay4, rp, bl, acc, ra, rb, wave, lane, ca);
+    else if (mean >= 12) tile_rows<16, NB, ABL, EPV, COL>(pay4, rp, bl, acc, ra, rb, wave, lane, ca);
+    else if (mean >= 6) tile_rows<8, NB, ABL, EPV, COL>(pay4, rp, bl, acc, ra, rb, wave, lane, ca);
+    else tile_rows<4, NB, ABL, EPV, COL>(pay4, rp, bl, acc, ra, rb, wave, lane, ca);
 }
 
 // The tile's 8192 bias values -> LDS (rotated image), coalesced 16-B loads
@@ -560,6 +644,7 @@ __device__ __forceinline__ void stage_bias(double* __restrict__ bl, const double
 // for small matrices: k_sweep_all, a union of the three)
 struct TiledLds {
     double bl[kW];
+    u64 cacc[kW];         // column side of the current upper tile (rotated image)
     double acc2[2 * kR];  // narrow rows, then wide rows
     uint32_t rps[kR + 1], rpsn[kR + 1];
     uint16_t perm[2 * kR];
@@ -567,13 +652,24 @@ struct TiledLds {
 };
 struct FlatLds {
     double bl[kW];
+    u64 cacc[kW];
     double acc[kR];    // row sums (narrow + wide)
     double accc[kR];   // narrow sums by compact row
     uint16_t rec[kFrecU4 * 8];
 };
 
+// the block's column accumulator -> its slot (column order), zeroed for the
+// next tile; every thread moves its own columns (no barrier between)
+__device__ __forceinline__ void flush_cols(u64* __restrict__ cacc, u64* __restrict__ dst, int nthr) {
+    for (int k = threadIdx.x; k < kW; k += nthr) {
+        const uint32_t sk = swz((uint32_t)k);
+        dst[k] = cacc[sk];
+        cacc[sk] = 0;
+    }
+}
+
 // One tiled-kernel work unit u.
-template <int NB, int ABL>
+template <int NB, int ABL, bool UP>
 __device__ __forceinline__ void sweep_tiled_unit(const TileDev& T, const uint8_t* __restrict__ act, int u,
                                                  const double* __restrict__ b, long long n_bins,
                                                  double* __restrict__ part, TiledLds& L) {
@@ -592,9 +688,19 @@ __device__ __forceinline__ void sweep_tiled_unit(const TileDev& T, const uint8_t
     const bool whole = T.u_whole[u] != 0;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     for (int k = threadIdx.x; k < 2 * (rb - ra); k += kSweepThreads) acc2[k] = 0.0;
+    // upper-triangle tiles: the column side into L.cacc, one slot per tile
+    const int urb = T.u_rb[u];
+    const ColArgs ca{T.bfix + T.row_lo + (long long)urb * kR, L.cacc};
+    const int upper = UP ? T.upper : 0;  // (UP: kernels with the column-side code)
+    if (upper)
+        for (int k = threadIdx.x; k < kW; k += kSweepThreads) L.cacc[k] = 0;
+    int cslot = -1;  // the previous tile's column slot (its flush is pending)
     for (int t = T.u_tlo[u]; t < T.u_thi[u]; ++t) {
         const long long c0 = (long long)T.tile_J[t] * kW;
         __syncthreads();  // previous tile's LDS reads are done
+        if (UP && cslot >= 0) flush_cols(L.cacc, T.colpart + (size_t)cslot * kW, kSweepThreads);
+        const bool up = tile_is_upper(upper, T.row_lo, urb, T.tile_J[t]);
+        cslot = up ? T.u_cslot[u] + (t - T.u_tlo[u]) : -1;
         if (ABL != 2) stage_bias(bl, b, c0, n_bins);  // ABL 2: timing ablation, no staging
         {
             const uint32_t* rpg = T.tile_rp + (size_t)t * (kR + 1);
@@ -618,24 +724,40 @@ __device__ __forceinline__ void sweep_tiled_unit(const TileDev& T, const uint8_t
         // width from each segment's mean uint4 count per row.
         const int nr = rb - ra;
         if (whole) {  // ra == 0: acc2 index = row
-            if (totn) sweep_bands<NB, ABL, 8>(band, payn4, rpsn, perm, bl, acc2, wave, lane);
-            if (totw) sweep_bands<NB, ABL, 4>(band + kBandSlots, payw4, rps, perm + kR, bl, acc2 + nr, wave, lane);
+            if (UP && cslot >= 0) {
+                if (totn) sweep_bands<NB, ABL, 8, true>(band, payn4, rpsn, perm, bl, acc2, wave, lane, ca);
+                if (totw)
+                    sweep_bands<NB, ABL, 4, true>(band + kBandSlots, payw4, rps, perm + kR, bl, acc2 + nr, wave, lane,
+                                                  ca);
+            } else {
+                if (totn) sweep_bands<NB, ABL, 8>(band, payn4, rpsn, perm, bl, acc2, wave, lane);
+                if (totw) sweep_bands<NB, ABL, 4>(band + kBandSlots, payw4, rps, perm + kR, bl, acc2 + nr, wave, lane);
+            }
         } else {
-            if (totn) sweep_rows<NB, ABL, 8>(totn / 8 / (uint32_t)nr, payn4, rpsn, bl, acc2, ra, rb, wave, lane);
-            if (totw) sweep_rows<NB, ABL, 4>(totw / 4 / (uint32_t)nr, payw4, rps, bl, acc2 + nr, ra, rb, wave, lane);
+            if (UP && cslot >= 0) {
+                if (totn)
+                    sweep_rows<NB, ABL, 8, true>(totn / 8 / (uint32_t)nr, payn4, rpsn, bl, acc2, ra, rb, wave, lane, ca);
+                if (totw)
+                    sweep_rows<NB, ABL, 4, true>(totw / 4 / (uint32_t)nr, payw4, rps, bl, acc2 + nr, ra, rb, wave, lane,
+                                                 ca);
+            } else {
+                if (totn) sweep_rows<NB, ABL, 8>(totn / 8 / (uint32_t)nr, payn4, rpsn, bl, acc2, ra, rb, wave, lane);
+                if (totw) sweep_rows<NB, ABL, 4>(totw / 4 / (uint32_t)nr, payw4, rps, bl, acc2 + nr, ra, rb, wave, lane);
+            }
         }
     }
     __syncthreads();
+    if (UP && cslot >= 0) flush_cols(L.cacc, T.colpart + (size_t)cslot * kW, kSweepThreads);
     for (int k = threadIdx.x; k < rb - ra; k += kSweepThreads) part[T.u_slot[u] + k] = acc2[k] + acc2[(rb - ra) + k];
 }
 
-template <int NB, int ABL>
+template <int NB, int ABL, bool UP>
 __global__ __launch_bounds__(kSweepThreads, 4) void k_sweep_tiled(TileDev T, const uint8_t* __restrict__ act,
                                                                 int n_list, const double* __restrict__ b,
                                                                 long long n_bins, double* __restrict__ part) {
     __shared__ __attribute__((aligned(16))) TiledLds L;
     if ((int)blockIdx.x >= n_list) return;
-    sweep_tiled_unit<NB, ABL>(T, act, T.u_order[blockIdx.x], b, n_bins, part, L);  // tiled units lead the list
+    sweep_tiled_unit<NB, ABL, UP>(T, act, T.u_order[blockIdx.x], b, n_bins, part, L);  // tiled units lead the list
 }
 
 // K1c: the flat tiles (whole row-blocks whose rows are all short).  Per
@@ -646,7 +768,7 @@ __global__ __launch_bounds__(kSweepThreads, 4) void k_sweep_tiled(TileDev T, con
 // record (compacted row starts + row ids) into LDS in one pass; the narrow
 // segment accumulates by compact row (flat_step_c), the few wide rows by row
 // id, and after a barrier the compact sums are added to their rows.
-template <int U, int ABL>
+template <int U, int ABL, bool UP>
 __device__ __forceinline__ void sweep_flat_unit(const TileDev& T, const uint8_t* __restrict__ act, int u,
                                                 const double* __restrict__ b, long long n_bins,
                                                 double* __restrict__ part, FlatLds& L) {
@@ -668,6 +790,12 @@ __device__ __forceinline__ void sweep_flat_unit(const TileDev& T, const uint8_t*
     const uint16_t* fidn = rec + 2 * (kR + 1);
     const uint16_t* fidw = fidn + kR;
     for (int k = threadIdx.x; k < nr; k += kSweepThreads) acc[k] = 0.0;
+    const int urb = T.u_rb[u];
+    const ColArgs ca{T.bfix + T.row_lo + (long long)urb * kR, L.cacc};
+    const int upper = UP ? T.upper : 0;
+    if (upper)
+        for (int k = threadIdx.x; k < kW; k += kSweepThreads) L.cacc[k] = 0;
+    int cslot = -1;
     const int t0 = T.u_tlo[u], t1 = T.u_thi[u];
     // a flat unit's tiles have consecutive flat records (plan order)
     const uint4* rg0 = T.frec + (size_t)T.tile_frec[t0] * kFrecU4;
@@ -708,11 +836,18 @@ __device__ __forceinline__ void sweep_flat_unit(const TileDev& T, const uint8_t*
         const uint4* rg = rg0 + (size_t)(t - t0) * kFrecU4;
         __syncthreads();  // previous tile's walk (LDS reads, accc / acc writes) is done
         for (int k = threadIdx.x; k < nfn_prev; k += kSweepThreads) acc[fidn_prev[k]] += accc[k];
+        if (UP && cslot >= 0) flush_cols(L.cacc, T.colpart + (size_t)cslot * kW, kSweepThreads);
+        cslot = tile_is_upper(upper, T.row_lo, urb, cm.J) ? T.u_cslot[u] + (t - t0) : -1;
         if (ABL != 2) stage_bias(bl, b, (long long)cm.J * kW, n_bins);
         for (int k = threadIdx.x; k < kFrecU4; k += kSweepThreads) reinterpret_cast<uint4*>(rec)[k] = rg[k];
         __syncthreads();
-        flat_seg_c<U, ABL, 8>(payn4, v, qan, qbn, i0n, i1n, fstn, nfn, bl, accc, lane);
-        flat_seg<UW, ABL, 4>(payw4, vw, qaw, qbw, i0w, i1w, fstw, fidw, nfw, bl, acc, lane);
+        if (UP && cslot >= 0) {
+            flat_seg_c<U, ABL, 8, true>(payn4, v, qan, qbn, i0n, i1n, fstn, nfn, bl, accc, lane, ca, fidn);
+            flat_seg<UW, ABL, 4, true>(payw4, vw, qaw, qbw, i0w, i1w, fstw, fidw, nfw, bl, acc, lane, ca);
+        } else {
+            flat_seg_c<U, ABL, 8>(payn4, v, qan, qbn, i0n, i1n, fstn, nfn, bl, accc, lane);
+            flat_seg<UW, ABL, 4>(payw4, vw, qaw, qbw, i0w, i1w, fstw, fidw, nfw, bl, acc, lane);
+        }
         if (defer) {
             nfn_prev = nfn;
             fidn_prev = reinterpret_cast<const uint16_t*>(rg) + 2 * (kR + 1);
@@ -723,18 +858,19 @@ __device__ __forceinline__ void sweep_flat_unit(const TileDev& T, const uint8_t*
     }
     __syncthreads();  // the last tile's compact sums complete
     for (int k = threadIdx.x; k < nfn_prev; k += kSweepThreads) acc[fidn_prev[k]] += accc[k];
+    if (UP && cslot >= 0) flush_cols(L.cacc, T.colpart + (size_t)cslot * kW, kSweepThreads);
     __syncthreads();
     for (int k = threadIdx.x; k < nr; k += kSweepThreads) part[T.u_slot[u] + k] = acc[k];
 }
 
-template <int U, int ABL>
+template <int U, int ABL, bool UP>
 __global__ __launch_bounds__(kSweepThreads, 4) void k_sweep_flat(TileDev T, const uint8_t* __restrict__ act,
                                                                int n_list, int list_off,
                                                                const double* __restrict__ b, long long n_bins,
                                                                double* __restrict__ part) {
     __shared__ __attribute__((aligned(16))) FlatLds L;
     if ((int)blockIdx.x >= n_list) return;
-    sweep_flat_unit<U, ABL>(T, act, T.u_order[list_off + blockIdx.x], b, n_bins, part, L);
+    sweep_flat_unit<U, ABL, UP>(T, act, T.u_order[list_off + blockIdx.x], b, n_bins, part, L);
 }
 
 // K1c' (round 3): the flat tiles swept by column tile.  A block takes a
@@ -752,6 +888,7 @@ __global__ __launch_bounds__(kSweepThreads, 4) void k_sweep_flat(TileDev T, cons
 template <int NW>
 struct FlatWLds {
     double bl[kW];
+    u64 cacc[kW];  // the group's column side (its strictly upper tiles), one slot per group
     uint16_t rec[NW][kFrecU4 * 8];
     double acc[NW][kR];
     int next;
@@ -767,7 +904,7 @@ __device__ __forceinline__ void wave_lds_sync() {
 
 // NW waves per block share one staged b[J]: the LDS (64 KB of bias + 8 KB
 // per wave) caps the block at 11 waves, and one block per CU is all that fits
-template <int U, int ABL, int PIPE = 2, int NW = kFlatWaves>
+template <int U, int ABL, int PIPE = 2, int NW = kFlatWaves, bool UP = false>
 __global__ __launch_bounds__(NW * 64, NW > 8 ? 3 : 2) void k_sweep_flatw(TileDev T, const uint8_t* __restrict__ act,
                                                                        const double* __restrict__ b, long long n_bins,
                                                                        double* __restrict__ part) {
@@ -785,8 +922,11 @@ __global__ __launch_bounds__(NW * 64, NW > 8 ? 3 : 2) void k_sweep_flatw(TileDev
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int J = T.tile_J[T.u_tlo[T.fg_unit[k0]]];
     const FlatDesc* __restrict__ desc = T.fg_desc + k0;
+    const int cslot = UP && T.upper ? T.fg_cslot[blockIdx.x] : -1;
     if (threadIdx.x == 0) L.next = 0;
     if (ABL != 2 && threadIdx.x < kSweepThreads) stage_bias(L.bl, b, (long long)J * kW, n_bins);
+    if (cslot >= 0)
+        for (int k = threadIdx.x; k < kW; k += NW * 64) L.cacc[k] = 0;
     __syncthreads();
     const double* __restrict__ bl = L.bl;
     uint16_t* __restrict__ rec = L.rec[wave];
@@ -799,6 +939,8 @@ __global__ __launch_bounds__(NW * 64, NW > 8 ? 3 : 2) void k_sweep_flatw(TileDev
         int slot, frec, nr, nfn, nfw;
         uint32_t qbn, qbw;
         const uint4 *payn4, *payw4;
+        int up;
+        const u64* bblk;
     };
     // the group's next active tile (LDS counter), false when none is left:
     // one descriptor load (round 3; it was unit -> tile -> split / entries,
@@ -822,16 +964,17 @@ __global__ __launch_bounds__(NW * 64, NW > 8 ? 3 : 2) void k_sweep_flatw(TileDev
             }
             if (!on) continue;  // a converged group's rows: k_marg never reads them
             x = Tw{d.slot, d.frec, (int)d.nr, (int)d.nfn, (int)d.nfw, d.qbn, d.qbw,
-                   reinterpret_cast<const uint4*>(T.payn + d.entn), reinterpret_cast<const uint4*>(T.pay + d.ent)};
+                   reinterpret_cast<const uint4*>(T.payn + d.entn), reinterpret_cast<const uint4*>(T.pay + d.ent),
+                   cslot >= 0 && d.upper ? 1 : 0, T.bfix + T.row_lo + (long long)d.rb * kR};
             return true;
         }
     };
     Tw cur;
-    if (!grab(cur)) return;
+    const bool any = grab(cur);
     uint4 v[U], vw[UW];
-    if (cur.nfn) flat_load<U>(cur.payn4, (uint32_t)lane * U, 0u, cur.qbn, v);
-    if (cur.nfw) flat_load<UW>(cur.payw4, (uint32_t)lane * UW, 0u, cur.qbw, vw);
-    for (;;) {
+    if (any && cur.nfn) flat_load<U>(cur.payn4, (uint32_t)lane * U, 0u, cur.qbn, v);
+    if (any && cur.nfw) flat_load<UW>(cur.payw4, (uint32_t)lane * UW, 0u, cur.qbw, vw);
+    for (; any;) {
         const uint4* rg = T.frec + (size_t)cur.frec * kFrecU4;
         // stage only the parts of the record the walk reads (the starts up
         // to each segment's end, the row ids of the nonempty rows), and no
@@ -870,8 +1013,14 @@ __global__ __launch_bounds__(NW * 64, NW > 8 ? 3 : 2) void k_sweep_flatw(TileDev
                 for (int h = 0; h < 2; ++h) r4[qs[g][h]] = tq[g][h];
         }
         wave_lds_sync();
-        if (PIPE) flat_seg_c_pipe<U, ABL, 8>(cur.payn4, v, 0u, cur.qbn, 0, cur.nfn, fstn, cur.nfn, bl, acc, lane);
-        else flat_seg_c<U, ABL, 8>(cur.payn4, v, 0u, cur.qbn, 0, cur.nfn, fstn, cur.nfn, bl, acc, lane);
+        const ColArgs ca{cur.bblk, L.cacc};
+        if (UP && cur.up) {  // (not software-pipelined: the column side needs the registers)
+            flat_seg_c<U, ABL, 8, true>(cur.payn4, v, 0u, cur.qbn, 0, cur.nfn, fstn, cur.nfn, bl, acc, lane, ca,
+                                        idn ? nullptr : fidn);
+        } else {
+            if (PIPE) flat_seg_c_pipe<U, ABL, 8>(cur.payn4, v, 0u, cur.qbn, 0, cur.nfn, fstn, cur.nfn, bl, acc, lane);
+            else flat_seg_c<U, ABL, 8>(cur.payn4, v, 0u, cur.qbn, 0, cur.nfn, fstn, cur.nfn, bl, acc, lane);
+        }
         wave_lds_sync();
         // compact narrow sums -> rows (zeros for rows without narrow entries)
         constexpr int PL = kR / 64;
@@ -891,8 +1040,15 @@ __global__ __launch_bounds__(NW * 64, NW > 8 ? 3 : 2) void k_sweep_flatw(TileDev
         for (int q = 0; q < PL; ++q)
             if (cid[q] >= 0) acc[cid[q]] = cv[q];
         wave_lds_sync();
-        if (PIPE) flat_seg_pipe<UW, ABL, 4>(cur.payw4, vw, 0u, cur.qbw, 0, cur.nfw, fstw, fidw, cur.nfw, bl, acc, lane);
-        else flat_seg<UW, ABL, 4>(cur.payw4, vw, 0u, cur.qbw, 0, cur.nfw, fstw, fidw, cur.nfw, bl, acc, lane);
+        if (UP && cur.up) {
+            if (PIPE)
+                flat_seg_pipe<UW, ABL, 4, true>(cur.payw4, vw, 0u, cur.qbw, 0, cur.nfw, fstw, fidw, cur.nfw, bl, acc, lane,
+                                                ca);
+            else flat_seg<UW, ABL, 4, true>(cur.payw4, vw, 0u, cur.qbw, 0, cur.nfw, fstw, fidw, cur.nfw, bl, acc, lane, ca);
+        } else {
+            if (PIPE) flat_seg_pipe<UW, ABL, 4>(cur.payw4, vw, 0u, cur.qbw, 0, cur.nfw, fstw, fidw, cur.nfw, bl, acc, lane);
+            else flat_seg<UW, ABL, 4>(cur.payw4, vw, 0u, cur.qbw, 0, cur.nfw, fstw, fidw, cur.nfw, bl, acc, lane);
+        }
         wave_lds_sync();
         // PIPE 2: the next tile's first runs are in flight while this tile's
         // row sums go out
@@ -917,6 +1073,10 @@ __global__ __launch_bounds__(NW * 64, NW > 8 ? 3 : 2) void k_sweep_flatw(TileDev
         }
         if (!more) break;
         cur = nxt;
+    }
+    if (UP && cslot >= 0) {  // every wave's adds are in: the group's column partial out
+        __syncthreads();
+        flush_cols(L.cacc, T.colpart + (size_t)cslot * kW, NW * 64);
     }
 }
 
@@ -1569,7 +1729,7 @@ __global__ void k_ub_halo(const uint8_t* __restrict__ band, const uint8_t* __res
 // as three kernels their ramps and tails add up; in one grid the blocks of
 // all three share the CUs.  Same bodies, same partials: bitwise the same.
 static_assert(kBandThreads == kSweepThreads, "one block shape");
-template <int NB, int U, int ABL>
+template <int NB, int U, int ABL, bool UP>
 __global__ __launch_bounds__(kSweepThreads, 4) void k_sweep_all(TileDev T, const uint8_t* __restrict__ act,
                                                               int n_tiled, int n_band, BandSegs S, int band_rb,
                                                               long long nloc, long long row_lo,
@@ -1587,12 +1747,12 @@ __global__ __launch_bounds__(kSweepThreads, 4) void k_sweep_all(TileDev T, const
     const int x = blockIdx.x;
     const unsigned long long t0 = trace ? wall_clock64() : 0ull;
     if (x < n_tiled) {
-        sweep_tiled_unit<NB, ABL>(T, act, T.u_order[x], b, n_bins, part, L.t);
+        sweep_tiled_unit<NB, ABL, UP>(T, act, T.u_order[x], b, n_bins, part, L.t);
     } else if (x < n_tiled + n_band) {
         const int y = x - n_tiled;
         band_any<ABL, 64>(S, y % band_rb, y / band_rb, L.band, nloc, row_lo, n_bins, act, row_group, b, bpart);
     } else {
-        sweep_flat_unit<U, ABL>(T, act, T.u_order[x - n_band], b, n_bins, part, L.f);  // flat units follow the tiled
+        sweep_flat_unit<U, ABL, UP>(T, act, T.u_order[x - n_band], b, n_bins, part, L.f);  // flat units follow the tiled
     }
     if (trace) {  // diagnostic block timeline (hh_tune "sweep_trace"): start, end, CU of each block
         __syncthreads();
@@ -1717,7 +1877,7 @@ __global__ __launch_bounds__(kMargThreads) void k_marg(TileDev T, const double* 
                                                        const uint8_t* __restrict__ act, const double* __restrict__ b,
                                                        long long row_lo, int nloc, const double* __restrict__ bpart,
                                                        int nch, UbMarg ub, double* __restrict__ out, TileArgs ta,
-                                                       int G, int stats) {
+                                                       int G, int stats, const u64* __restrict__ colacc) {
     __shared__ int su_lo[kMargU], su_n[kMargU], su_slot[kMargU];
     __shared__ double sh[16];
     __shared__ int flag;
@@ -1794,6 +1954,9 @@ __global__ __launch_bounds__(kMargThreads) void k_marg(TileDev T, const double* 
                 for (int e = 0; e < kUbArrs; ++e)
                     if (in[h][e]) s += x[h][e];
         }
+        // the column side of the upper-triangle tiles: sum_k count_k B[row_k]
+        // over the stored entries of this column (exact int64), / 2^e
+        if (colacc) s += (double)(long long)colacc[i] * T.fix[1];
         for (long long q = wide_ptr[i]; q < wide_ptr[i + 1]; ++q) s = fma(wide_cnt[q], b[wide_col[q]], s);
         const double br = b[row_lo + i];
         v = br * fma(2.0 * diag[i], br, s);
@@ -1804,6 +1967,79 @@ __global__ __launch_bounds__(kMargThreads) void k_marg(TileDev T, const double* 
     for (int t = ta.blk_tile_ptr[B]; t < ta.blk_tile_ptr[B + 1]; ++t)
         if (act[ta.tile_group[t]] != 0) tile_stats(ta, t, row_lo + i, v, sh);
     if (stats == 1 && last_block(ta.counter, &flag)) stats_tail(ta, act, G);  // 2: tile sums only (big mode)
+}
+
+// Column side of the upper-triangle tiles, per column c of [c0, c0 + n):
+// the sum of the slots of its column tile (plan order; integers: exact).
+__global__ __launch_bounds__(256) void k_colsum(const u64* __restrict__ colpart, const int32_t* __restrict__ jslot_ptr,
+                                                const int32_t* __restrict__ jslot, long long c0, long long n,
+                                                u64* __restrict__ out) {
+    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const long long c = c0 + i;
+    const int J = (int)(c >> kWBits), k = (int)(c & (kW - 1));
+    const int a = jslot_ptr[J], e = jslot_ptr[J + 1];
+    u64 acc = 0;
+    int q = a;
+    for (; q + 8 <= e; q += 8) {  // eight loads in flight
+        u64 x[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) x[r] = colpart[(size_t)jslot[q + r] * kW + k];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) acc += x[r];
+    }
+    for (; q < e; ++q) acc += colpart[(size_t)jslot[q] * kW + k];
+    out[i] = acc;
+}
+
+// This sweep's fixed-point scale 2^e from the bias maximum the last update
+// left (bmax[p], double bits) and the largest raw marginal rmax (a bound on
+// any column's count total): every column sum count * round(b 2^e) stays
+// below 2^62.  fix = {2^e, 2^-e}; the other bmax slot is cleared for the
+// update that follows.
+// Every thread derives the same e from the same two numbers, converts its
+// bins' bias to B = round(b 2^e) (the walks then load B, no conversion in the
+// hot loops; NaN / negative -> 0); thread 0 also clears the other slot.
+__global__ __launch_bounds__(256) void k_fixscale(unsigned long long* __restrict__ bmax, int p, double rmax,
+                                                  double* __restrict__ fix, const double* __restrict__ b, long long n,
+                                                  u64* __restrict__ bfix) {
+    double bm = __longlong_as_double((long long)bmax[p]);
+    if (!(bm > 0.0) || !(bm < 1e300)) bm = 1.0;
+    const double r = rmax > 1.0 ? rmax : 1.0;
+    const int e = 61 - ilogb(r) - ilogb(bm);  // r < 2^(ilogb r + 1), bm < 2^(ilogb bm + 1)
+    const double sc = ldexp(1.0, e);
+    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) {
+        const double x = b[i];
+        bfix[i] = x > 0.0 ? (u64)__double2ll_rn(x * sc) : 0ull;  // (x < bm * 2: below 2^62)
+    }
+    if (i == 0) {
+        fix[0] = sc;
+        fix[1] = ldexp(1.0, -e);
+        bmax[1 - p] = 0ull;
+    }
+}
+
+// the all-bins column vector -> the per-rank padded blocks of the column
+// exchange (rank k's rows at k * maxlen)
+__global__ void k_colpad(const u64* __restrict__ col, int world, long long maxlen,
+                         const long long* __restrict__ rank_rows, u64* __restrict__ out) {
+    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (long long)world * maxlen) return;
+    const int k = (int)(t / maxlen);
+    const long long off = t - (long long)k * maxlen;
+    const long long lo = rank_rows[k], hi = rank_rows[k + 1];
+    out[t] = lo + off < hi ? col[lo + off] : 0ull;
+}
+
+// the all-gather fallback of the column exchange: rank `rank`'s block summed
+// over the gathered vectors (world x (world x maxlen)), in rank order
+__global__ void k_colgather(const u64* __restrict__ all, int world, long long maxlen, int rank, u64* __restrict__ out) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= maxlen) return;
+    u64 acc = 0;
+    for (int r = 0; r < world; ++r) acc += all[((size_t)r * world + rank) * maxlen + i];
+    out[i] = acc;
 }
 
 __global__ void k_scatter(const double* __restrict__ g, int world, long long maxlen,
@@ -1879,16 +2115,29 @@ __global__ __launch_bounds__(kR) void k_stats2(TileArgs ta, const uint8_t* __res
     if (threadIdx.x == 0) ta.tile_sq[t] = q;
 }
 
+// the largest finite positive bias of the wave's rows -> *bmax (double
+// bits: for positive doubles the unsigned order is the numeric order); the
+// next sweep's fixed-point scale (k_fixscale) comes from it
+__device__ __forceinline__ void bias_max(double v, unsigned long long* bmax) {
+    if (!bmax) return;
+    double m = (v > 0.0 && v < 1e300) ? v : 0.0;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmax(m, __shfl_xor(m, o, 64));
+    if ((threadIdx.x & 63) == 0 && m > 0.0) atomicMax(bmax, (unsigned long long)__double_as_longlong(m));
+}
+
 __global__ __launch_bounds__(kR) void k_update_big(TileArgs ta, const uint8_t* __restrict__ act,
                                                    uint8_t* __restrict__ nxt, const double* __restrict__ marg,
                                                    double* __restrict__ bias, GroupState gs, double tol,
-                                                   int max_iters) {
+                                                   int max_iters, unsigned long long* __restrict__ bmax) {
     __shared__ double sh[16];
     const int t = blockIdx.x;
     const int g = ta.tile_group[t];
     const bool first = t == ta.group_tile_ptr[g];
     if (act[g] == 0) {
         if (first && threadIdx.x == 0) nxt[g] = 0;
+        const long long row = ta.tile_lo[t] + threadIdx.x;
+        bias_max(row < ta.tile_hi[t] ? bias[row] : 0.0, bmax);
         return;
     }
     double cnt, sum, sq;
@@ -1907,11 +2156,14 @@ __global__ __launch_bounds__(kR) void k_update_big(TileArgs ta, const uint8_t* _
         return;
     }
     const double mean = sum / cnt;
+    double bnew = 0.0;
     if (in) {
         double m = marg[row] / mean;
         if (m == 0.0) m = 1.0;
-        bias[row] /= m;
+        bnew = bias[row] / m;
+        bias[row] = bnew;
     }
+    bias_max(bnew, bmax);
     if (first && threadIdx.x == 0) {
         const double var = sq / cnt;
         gs.var[g] = var;
@@ -1929,31 +2181,38 @@ __global__ __launch_bounds__(kR) void k_update_big(TileArgs ta, const uint8_t* _
 __global__ __launch_bounds__(kR) void k_update(TileArgs ta, const uint8_t* __restrict__ act,
                                                uint8_t* __restrict__ nxt, const double* __restrict__ marg,
                                                double* __restrict__ bias, GroupState gs, double tol,
-                                               int max_iters, int G) {
+                                               int max_iters, int G, unsigned long long* __restrict__ bmax) {
     __shared__ double sh[16];
     __shared__ int flag;
     const int t = blockIdx.x;
     const int g = ta.tile_group[t];
-    if (act[g] != 0) {
-        const double cnt = ta.g_cnt[g], sum = ta.g_sum[g];
+    {
         const long long row = ta.tile_lo[t] + threadIdx.x;
         const bool in = row < ta.tile_hi[t];
-        double q = 0.0;
-        if (cnt == 0.0) {  // no nonzero marginal: cooler sets the group's bias to NaN
-            if (in) bias[row] = __builtin_nan("");
-        } else if (in) {
-            const double mean = sum / cnt;
-            const double x = marg[row];
-            double m = x / mean;
-            if (m == 0.0) m = 1.0;
-            bias[row] /= m;
-            if (x != 0.0) {
-                const double d = x - mean;
-                q = d * d;
+        double bnew = 0.0;
+        if (act[g] != 0) {
+            const double cnt = ta.g_cnt[g], sum = ta.g_sum[g];
+            double q = 0.0;
+            if (cnt == 0.0) {  // no nonzero marginal: cooler sets the group's bias to NaN
+                if (in) bias[row] = __builtin_nan("");
+            } else if (in) {
+                const double mean = sum / cnt;
+                const double x = marg[row];
+                double m = x / mean;
+                if (m == 0.0) m = 1.0;
+                bnew = bias[row] / m;
+                bias[row] = bnew;
+                if (x != 0.0) {
+                    const double d = x - mean;
+                    q = d * d;
+                }
             }
+            q = block_sum(q, sh);
+            if (threadIdx.x == 0) ta.tile_sq[t] = q;
+        } else if (in) {
+            bnew = bias[row];
         }
-        q = block_sum(q, sh);
-        if (threadIdx.x == 0) ta.tile_sq[t] = q;
+        bias_max(bnew, bmax);
     }
     if (!last_block(ta.counter + 1, &flag)) return;
     const int w = threadIdx.x >> 6, nw = blockDim.x >> 6, lane = threadIdx.x & 63;
@@ -2028,6 +2287,26 @@ struct hh_ice {
     DBuf<uint8_t> g_empty;
     DBuf<long long> rank_rows;
     std::vector<int64_t> h_rank_rows;
+    // upper-triangle tiles: column slots, the all-bins column
+    // vector (int64 fixed point), the fixed-point scale {2^e, 2^-e} and the
+    // bias maximum (double bits, parity double buffer) it comes from; rmax =
+    // the largest raw marginal (global once the filters have seen the
+    // gathered marginals)
+    DBuf<unsigned long long> colpart, colacc, bmax, bfix;
+    DBuf<double> fix;
+    double rmax = 1.0;
+    bool rmax_global = false;
+    // the column exchange of a shard: int64 reduce-scatter over the ranks'
+    // padded row blocks (a caller's hh_reduce_fn, else through the all-gather)
+    int32_t cx_world = 1, cx_rank = 0;
+    int64_t cx_maxlen = 0;
+    std::vector<int64_t> cx_rr;
+    DBuf<long long> cx_rr_dev;
+    hh_reduce_fn cx_fn = nullptr;
+    void* cx_user = nullptr;
+    hh_allgather_fn cx_ag = nullptr;
+    void* cx_ag_user = nullptr;
+    DBuf<unsigned long long> cx_send, cx_recv, cx_all;
     int32_t iters_done = 0;
     PinnedBuf<uint8_t> h_active;
     // timing of the last hh_ice_run
@@ -2072,6 +2351,7 @@ static int g_band_dpp = 0;    // band sweep: a lane's previous 16 bytes by DPP s
 // waves with 33-tile column groups (3 tiles per wave) took the C4 sweep from
 // 3.52 to 3.33 ms (profiles/r3b_flatw_waves_*_ab.log); 44-tile groups 1 % more
 static int g_flatw_waves = 11;
+static int g_flatw_waves_up = 8;  // k_sweep_flatw with the column side: 8 (no spills) or 11
 static int g_flatw_pipe = 2;  // k_sweep_flatw: 1 = the next run's loads before the current step's walk,
                               // 2 = and the next tile's first runs before the current tile's row sums go out
 static int g_sweep_ablate = 0;
@@ -2106,14 +2386,14 @@ static int64_t g_single_max_bytes = 1LL << 30;
 static unsigned long long* g_trace = nullptr;
 static int64_t g_trace_cap = 0, g_trace_n = 0;
 
-template <int NB, int ABL>
-static void launch_sweep(const hh_matrix* m, const uint8_t* act, const double* b, double* part, hipStream_t s,
-                         hipStream_t s_tiled) {
+template <int NB, int ABL, bool UP>
+static void launch_sweep_up(const hh_matrix* m, const TileDev& T, const uint8_t* act, const double* b, double* part,
+                            hipStream_t s, hipStream_t s_tiled) {
     const int n_tiled = (int)(m->n_units - m->n_units_flat), n_flat = (int)m->n_units_flat;
     if (n_tiled) {
         HH_KTIME("k_sweep_tiled", s_tiled);  // per-kernel registry timing (probes; off by default)
-        hipLaunchKernelGGL((k_sweep_tiled<NB, ABL>), dim3((unsigned)n_tiled), dim3(kSweepThreads), 0, s_tiled,
-                           m->dev(), act, n_tiled, b, (long long)m->n_bins, part);
+        hipLaunchKernelGGL((k_sweep_tiled<NB, ABL, UP>), dim3((unsigned)n_tiled), dim3(kSweepThreads), 0, s_tiled,
+                           T, act, n_tiled, b, (long long)m->n_bins, part);
     }
     HH_KTIME(n_flat ? "k_sweep_flat" : nullptr, s);
     if (n_flat && m->n_fgroups) {
@@ -2122,44 +2402,60 @@ static void launch_sweep(const hh_matrix* m, const uint8_t* act, const double* b
                     : (g_flatw_pipe == 2 ? k_sweep_flatw<kFlatU, ABL, 2>
                        : g_flatw_pipe == 1 ? k_sweep_flatw<kFlatU, ABL, 1> : k_sweep_flatw<kFlatU, ABL, 0>);
         int nw = 8;
-        if (g_flatw_waves == 10 && g_flatw_u != 16) {
+        if (UP) {
+            // the column side's registers: 8 waves (2 per SIMD, 256 VGPRs; at
+            // 11 waves the walk spills), or 11 with hh_tune flatw_waves_up
+            nw = g_flatw_waves_up == 11 ? 11 : 8;
+            kern = nw == 11 ? k_sweep_flatw<kFlatU, ABL, 2, 11, true> : k_sweep_flatw<kFlatU, ABL, 2, 8, true>;
+        } else if (g_flatw_waves == 10 && g_flatw_u != 16) {
             kern = g_flatw_pipe == 2 ? k_sweep_flatw<kFlatU, ABL, 2, 10> : k_sweep_flatw<kFlatU, ABL, 0, 10>;
             nw = 10;
         } else if (g_flatw_waves == 11 && g_flatw_u != 16) {
             kern = g_flatw_pipe == 2 ? k_sweep_flatw<kFlatU, ABL, 2, 11> : k_sweep_flatw<kFlatU, ABL, 0, 11>;
             nw = 11;
         }
-        hipLaunchKernelGGL(kern, dim3((unsigned)m->n_fgroups), dim3(64 * nw), 0, s, m->dev(), act, b,
+        hipLaunchKernelGGL(kern, dim3((unsigned)m->n_fgroups), dim3(64 * nw), 0, s, T, act, b,
                            (long long)m->n_bins, part);
     } else if (n_flat) {
-        hipLaunchKernelGGL((k_sweep_flat<kFlatU, ABL>), dim3((unsigned)n_flat), dim3(kSweepThreads), 0, s, m->dev(),
+        hipLaunchKernelGGL((k_sweep_flat<kFlatU, ABL, UP>), dim3((unsigned)n_flat), dim3(kSweepThreads), 0, s, T,
                            act, n_flat, n_tiled, b, (long long)m->n_bins, part);
     }
 }
 
+template <int NB, int ABL>
+static void launch_sweep(const hh_matrix* m, const TileDev& T, const uint8_t* act, const double* b, double* part,
+                         hipStream_t s, hipStream_t s_tiled) {
+    if (T.upper) launch_sweep_up<NB, ABL, true>(m, T, act, b, part, s, s_tiled);
+    else launch_sweep_up<NB, ABL, false>(m, T, act, b, part, s, s_tiled);
+}
+
 template <int ABL>
-static void launch_sweep_nb(const hh_matrix* m, const uint8_t* act, const double* b, double* part, hipStream_t s,
-                            hipStream_t st) {
+static void launch_sweep_nb(const hh_matrix* m, const TileDev& T, const uint8_t* act, const double* b, double* part,
+                            hipStream_t s, hipStream_t st) {
     switch (g_sweep_nb) {
-        case 1: launch_sweep<1, ABL>(m, act, b, part, s, st); break;
-        case 2: launch_sweep<2, ABL>(m, act, b, part, s, st); break;
-        case 8: launch_sweep<8, ABL>(m, act, b, part, s, st); break;
-        default: launch_sweep<4, ABL>(m, act, b, part, s, st); break;
+        case 1: launch_sweep<1, ABL>(m, T, act, b, part, s, st); break;
+        case 2: launch_sweep<2, ABL>(m, T, act, b, part, s, st); break;
+        case 8: launch_sweep<8, ABL>(m, T, act, b, part, s, st); break;
+        default: launch_sweep<4, ABL>(m, T, act, b, part, s, st); break;
     }
 }
 
 // s_tiled: stream of the tiled kernel (= s, or a side stream joined by the caller)
-static void sweep(const hh_matrix* m, const uint8_t* act, const double* b, double* part, hipStream_t s,
-                  hipStream_t s_tiled = nullptr) {
+static void sweep(const hh_matrix* m, const TileDev& T, const uint8_t* act, const double* b, double* part,
+                  hipStream_t s, hipStream_t s_tiled = nullptr) {
     if (m->n_units == 0) return;
     if (!s_tiled) s_tiled = s;
     switch (g_sweep_ablate) {
-        case 1: launch_sweep_nb<1>(m, act, b, part, s, s_tiled); break;
-        case 2: launch_sweep_nb<2>(m, act, b, part, s, s_tiled); break;
-        default: launch_sweep_nb<0>(m, act, b, part, s, s_tiled); break;
+        case 1: launch_sweep_nb<1>(m, T, act, b, part, s, s_tiled); break;
+        case 2: launch_sweep_nb<2>(m, T, act, b, part, s, s_tiled); break;
+        default: launch_sweep_nb<0>(m, T, act, b, part, s, s_tiled); break;
     }
     HIP_CHECK(hipGetLastError());
 }
+
+// the tile view of a state's matrix (column slots and scale when the layout
+// has upper-triangle tiles)
+static TileDev tdev(const hh_ice* S) { return S->m->dev(S->colpart.p, S->fix.p, S->bfix.p); }
 
 // The matrix's band segments; returns their total chunk count.
 // Dispatch order of the band chunks: by work (counts in the chunk) descending,
@@ -2309,10 +2605,14 @@ static void sweep_single(hh_ice* S, hipStream_t s) {
     HH_REQUIRE(grid < (1LL << 31), "sweep grid too large for one launch");
     unsigned long long* trace = grid <= g_trace_cap ? g_trace : nullptr;
     if (trace) g_trace_n = grid;
-    auto kern = g_sweep_ablate == 1   ? k_sweep_all<2, kFlatU, 1>
-                : g_sweep_ablate == 2 ? k_sweep_all<2, kFlatU, 2>
-                                      : k_sweep_all<2, kFlatU, 0>;  // ablations: timing diagnostics only
-    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kSweepThreads), 0, s, m->dev(), S->act(), n_tiled,
+    const bool up = m->upper && S->colpart.p;
+    auto kern = up ? (g_sweep_ablate == 1   ? k_sweep_all<2, kFlatU, 1, true>
+                      : g_sweep_ablate == 2 ? k_sweep_all<2, kFlatU, 2, true>
+                                            : k_sweep_all<2, kFlatU, 0, true>)
+                   : (g_sweep_ablate == 1   ? k_sweep_all<2, kFlatU, 1, false>
+                      : g_sweep_ablate == 2 ? k_sweep_all<2, kFlatU, 2, false>
+                                            : k_sweep_all<2, kFlatU, 0, false>);  // ablations: timing diagnostics only
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kSweepThreads), 0, s, tdev(S), S->act(), n_tiled,
                        (int)n_band, segs, band_rb, (long long)S->nloc, (long long)m->row_lo, m->row_group.p,
                        S->bias.p, (long long)m->n_bins, S->part.p, S->bpart.p, trace);
     HIP_CHECK(hipGetLastError());
@@ -2336,7 +2636,15 @@ static void ensure_side_streams(hh_ice* S) {
 
 static void marg_weighted(hh_ice* S, double* out, hipStream_t s, bool timed, int slot) {
     hh_matrix* m = S->m;
+    const bool up = m->upper && S->colpart.p;
+    const bool shard_x = up && S->cx_world > 1;  // the column side crosses ranks
+    HH_REQUIRE(!shard_x || S->rmax_global,
+               "upper-triangle tiles on a shard: run the filters on the gathered marginals first (global scale)");
     if (timed) HIP_CHECK(hipEventRecord(S->ev[2 * slot], s));
+    if (up)
+        hipLaunchKernelGGL(k_fixscale, dim3(nblocks(std::max<int64_t>(S->n, 1), 256)), dim3(256), 0, s, S->bmax.p,
+                           S->iters_done & 1, S->rmax, S->fix.p, S->bias.p, (long long)S->n, S->bfix.p);
+    const TileDev T = tdev(S);
     {
         HH_KTIME(timed ? nullptr : "ice_sweep", s);  // registry timing for the sharded driver (tiled + flat + band)
         // the two sweeps write disjoint partials (part / bpart): the band
@@ -2349,7 +2657,9 @@ static void marg_weighted(hh_ice* S, double* out, hipStream_t s, bool timed, int
         // 1250 vs 1177 it/s; profiles/r4f_conc_ab.log)
         const bool conc = g_band_concurrent && (S->nch || S->nchu) && S->nloc && m->n_units &&
                           (bytes >= g_conc_min_bytes || (S->nchu && bytes >= g_conc_ub_min_bytes));
-        const bool single = g_sweep_nb == 2 &&
+        // (not with upper tiles in column-grouped flat units: their column
+        // side has one slot per group, which only k_sweep_flatw fills)
+        const bool single = g_sweep_nb == 2 && !(up && m->n_fgroups) &&
                             (g_sweep_single == 1 || (g_sweep_single == -1 && bytes < g_single_max_bytes));
         if (single) {
             sweep_single(S, s);
@@ -2360,18 +2670,44 @@ static void marg_weighted(hh_ice* S, double* out, hipStream_t s, bool timed, int
             sweep_band(S, S->side);
             HIP_CHECK(hipEventRecord(S->join, S->side));
             if (g_split_tiles) HIP_CHECK(hipStreamWaitEvent(S->side2, S->fork, 0));
-            sweep(m, S->act(), S->bias.p, S->part.p, s, g_split_tiles ? S->side2 : s);
+            sweep(m, T, S->act(), S->bias.p, S->part.p, s, g_split_tiles ? S->side2 : s);
             if (g_split_tiles) {
                 HIP_CHECK(hipEventRecord(S->join2, S->side2));
                 HIP_CHECK(hipStreamWaitEvent(s, S->join2, 0));
             }
             HIP_CHECK(hipStreamWaitEvent(s, S->join, 0));
         } else {
-            sweep(m, S->act(), S->bias.p, S->part.p, s);
+            sweep(m, T, S->act(), S->bias.p, S->part.p, s);
             sweep_band(S, s);
+        }
+        if (up && S->n > 0) {  // every column's upper-tile side: the slots of its column tile
+            hipLaunchKernelGGL(k_colsum, dim3(nblocks(S->n, 256)), dim3(256), 0, s, S->colpart.p, m->jslot_ptr.p,
+                               m->jslot.p, 0LL, (long long)S->n, S->colacc.p);
+            HIP_CHECK(hipGetLastError());
         }
     }
     if (timed) HIP_CHECK(hipEventRecord(S->ev[2 * slot + 1], s));
+    // the column side of this shard's rows: summed over the ranks
+    const unsigned long long* col_own = up ? S->colacc.p + m->row_lo : nullptr;
+    if (shard_x) {
+        const long long tot = (long long)S->cx_world * S->cx_maxlen;
+        hipLaunchKernelGGL(k_colpad, dim3(nblocks(tot, kThreads)), dim3(kThreads), 0, s, S->colacc.p, S->cx_world,
+                           (long long)S->cx_maxlen, S->cx_rr_dev.p, S->cx_send.p);
+        HIP_CHECK(hipGetLastError());
+        int rc = 0;
+        if (S->cx_fn) {
+            rc = S->cx_fn(reinterpret_cast<const int64_t*>(S->cx_send.p), S->cx_maxlen,
+                          reinterpret_cast<int64_t*>(S->cx_recv.p), S->cx_user, s);
+        } else {  // through the all-gather: every rank's padded vector, summed here in rank order
+            rc = S->cx_ag(reinterpret_cast<const double*>(S->cx_send.p), tot, reinterpret_cast<double*>(S->cx_all.p),
+                          S->cx_ag_user, s);
+            if (!rc)
+                hipLaunchKernelGGL(k_colgather, dim3(nblocks(S->cx_maxlen, kThreads)), dim3(kThreads), 0, s,
+                                   S->cx_all.p, S->cx_world, (long long)S->cx_maxlen, S->cx_rank, S->cx_recv.p);
+        }
+        if (rc) HH_THROW(rc < 0 ? rc : HH_ERR_HIP, std::string("column exchange failed: ") + hh_last_error());
+        col_own = S->cx_recv.p;
+    }
     S->stats_fresh = false;
     if (S->nloc == 0) return;
     // stats fused into k_marg when this GPU holds every row and `out` is the
@@ -2382,13 +2718,19 @@ static void marg_weighted(hh_ice* S, double* out, hipStream_t s, bool timed, int
                           ? (S->small_stats() ? 1 : 2)
                           : 0;
     HH_KTIME(timed ? nullptr : "k_marg", s);
-    hipLaunchKernelGGL(k_marg, dim3(nblocks(S->nloc, kR)), dim3(kMargThreads), 0, s, m->dev(), S->part.p,
+    hipLaunchKernelGGL(k_marg, dim3(nblocks(S->nloc, kR)), dim3(kMargThreads), 0, s, T, S->part.p,
                        m->wide_ptr.p, m->wide_col.p, m->wide_cnt.p, m->diag.p, m->row_group.p, S->act(),
                        S->bias.p, (long long)m->row_lo, (int)S->nloc, S->bpart.p, S->nchu ? 0 : (int)S->nch,
                        ub_marg(S), out, S->ta(),
-                       (int)S->G, stats);
+                       (int)S->G, stats, col_own);
     HIP_CHECK(hipGetLastError());
     S->stats_fresh = stats != 0;
+}
+
+// the bias-maximum slot the update of this iteration fills (read by the next
+// sweep's k_fixscale, which cleared it)
+static unsigned long long* bmax_next(hh_ice* S) {
+    return S->bmax.p ? S->bmax.p + (1 - (S->iters_done & 1)) : nullptr;
 }
 
 static void update(hh_ice* S, hipStream_t s) {
@@ -2400,14 +2742,14 @@ static void update(hh_ice* S, hipStream_t s) {
                 hipLaunchKernelGGL(k_stats1<true>, dim3(S->n_tiles), dim3(kR), 0, s, ta, S->act(), S->marg.p,
                                    (int)S->G);
             hipLaunchKernelGGL(k_update, dim3(S->n_tiles), dim3(kR), 0, s, ta, S->act(), S->nxt(), S->marg.p,
-                               S->bias.p, gs, S->o.tol, S->o.max_iters, (int)S->G);
+                               S->bias.p, gs, S->o.tol, S->o.max_iters, (int)S->G, bmax_next(S));
         } else {
             if (!S->stats_fresh)
                 hipLaunchKernelGGL(k_stats1<false>, dim3(S->n_tiles), dim3(kR), 0, s, ta, S->act(), S->marg.p,
                                    (int)S->G);
             hipLaunchKernelGGL(k_stats2, dim3(S->n_tiles), dim3(kR), 0, s, ta, S->act(), S->marg.p);
             hipLaunchKernelGGL(k_update_big, dim3(S->n_tiles), dim3(kR), 0, s, ta, S->act(), S->nxt(), S->marg.p,
-                               S->bias.p, gs, S->o.tol, S->o.max_iters);
+                               S->bias.p, gs, S->o.tol, S->o.max_iters, bmax_next(S));
         }
         HIP_CHECK(hipGetLastError());
     }
@@ -2497,8 +2839,11 @@ int hh_tune(const char* key, int64_t value) {
         } else if (k == "flatw_u") {
             HH_REQUIRE(value == 8 || value == 16, "flatw_u in {8, 16}");
             g_flatw_u = (int)value;
+        } else if (k == "flatw_waves_up") {
+            HH_REQUIRE(value == 8 || value == 11, "flatw_waves_up in {8, 11}");
+            g_flatw_waves_up = (int)value;
         } else if (k == "upper_tiles") {
-            HH_REQUIRE(value == 0 || value == 1, "upper_tiles in {0, 1}");
+            HH_REQUIRE(value >= -1 && value <= 1, "upper_tiles in {-1 (auto), 0, 1}");
             g_upper_tiles = value;
         } else if (k == "flat_max") {
             HH_REQUIRE(value >= 0 && value <= 255, "flat_max in [0, 255]");
@@ -2728,6 +3073,27 @@ int hh_ice_create(hh_matrix* m, const hh_ice_opts* o, hh_ice** out) {
         }
         S->bpart.alloc(std::max<int64_t>((int64_t)S->nch * S->nloc, 1));
         // (the side streams of the three-stream sweep are made on first use)
+        if (m->upper && m->n_cslots > 0) {
+            S->colpart.alloc((size_t)m->n_cslots * kW);
+            S->colpart.zero(s);
+        }
+        if (m->upper) {
+            S->colacc.alloc((size_t)std::max<int64_t>(S->n, 1));
+            S->colacc.zero(s);
+            // the initial bias is 1 (filters only zero entries): bmax slot 0 = 1.0
+            const unsigned long long one[2] = {0x3FF0000000000000ull, 0ull};
+            S->bmax = to_device(std::vector<unsigned long long>(one, one + 2), s);
+            S->fix.alloc(2);
+            S->bfix.alloc((size_t)std::max<int64_t>(S->n, 1));
+            // the largest raw marginal bounds every column's count total; a
+            // shard's own rows are not enough (columns of other ranks): the
+            // filters set the global one from the gathered marginals
+            std::vector<double> rs((size_t)S->nloc);
+            if (S->nloc) m->row_sum2.download(rs.data(), (size_t)S->nloc, s);
+            HIP_CHECK(hipStreamSynchronize(s));
+            for (double x : rs) S->rmax = std::max(S->rmax, x);
+            S->rmax_global = S->full();
+        }
 
         S->tile_cnt.alloc(std::max(S->n_tiles, 1));
         S->tile_sum.alloc(std::max(S->n_tiles, 1));
@@ -2817,6 +3183,17 @@ int hh_ice_filter_nnz(hh_ice* S, void* stream) {
 int hh_ice_filter_count_mad(hh_ice* S, void* stream) {
     return guard([&] {
         HH_REQUIRE(S, "null");
+        if (S->m->upper && !S->full()) {
+            // S->marg holds every bin's raw marginal here (gathered, mode 1):
+            // the global count bound of the column side's fixed-point scale
+            std::vector<double> mg((size_t)S->n);
+            S->marg.download(mg.data(), (size_t)S->n, as_stream(stream));
+            HIP_CHECK(hipStreamSynchronize(as_stream(stream)));
+            double r = 1.0;
+            for (double x : mg) r = std::max(r, x);
+            S->rmax = r;
+            S->rmax_global = true;
+        }
         filter_count_mad(S, as_stream(stream), nullptr);
     });
 }
@@ -2883,6 +3260,51 @@ int hh_ice_last_sweep_timing(const hh_ice* S, double* sweep_ms_total, int32_t* s
         if (sweep_ms_total) *sweep_ms_total = S->sweep_ms;
         if (sweep_launches) *sweep_launches = S->sweep_launches;
         if (iter_ms_total) *iter_ms_total = S->iter_ms;
+    });
+}
+
+int hh_ice_set_column_exchange(hh_ice* S, int32_t world, int32_t rank, const int64_t* rank_rows, hh_reduce_fn reduce,
+                               void* reduce_user, hh_allgather_fn allgather, void* allgather_user) {
+    return guard([&] {
+        HH_REQUIRE(S && world >= 1 && rank_rows && rank >= -1 && rank < world, "bad arguments");
+        HH_REQUIRE(world == 1 || reduce || allgather || (S->cx_fn && S->cx_world == world),
+                   "a reduce or all-gather function is required for world > 1");
+        std::vector<int64_t> rr(rank_rows, rank_rows + world + 1);
+        HH_REQUIRE(rr[0] == 0 && rr[world] == S->n, "rank_rows must span [0, n_bins]");
+        int64_t maxlen = 1;
+        for (int k = 0; k < world; ++k) {
+            HH_REQUIRE(rr[k] <= rr[k + 1], "rank_rows not monotone");
+            maxlen = std::max<int64_t>(maxlen, rr[k + 1] - rr[k]);
+        }
+        if (rank < 0) {  // this shard's block (any of equal empty ranges: its rows are none)
+            for (int k = 0; k < world && rank < 0; ++k)
+                if (rr[k] == S->m->row_lo && rr[k + 1] == S->m->row_hi) rank = k;
+            HH_REQUIRE(rank >= 0, "the matrix shard is none of rank_rows' ranges");
+        }
+        HH_REQUIRE(rr[rank] == S->m->row_lo && rr[rank + 1] == S->m->row_hi,
+                   "the matrix shard does not hold rank_rows[rank] .. rank_rows[rank + 1]");
+        if (!reduce && S->cx_fn && S->cx_world == world) {
+            reduce = S->cx_fn;
+            reduce_user = S->cx_user;
+        }
+        S->cx_world = world;
+        S->cx_rank = rank;
+        S->cx_maxlen = maxlen;
+        S->cx_fn = reduce;
+        S->cx_user = reduce_user;
+        S->cx_ag = allgather;
+        S->cx_ag_user = allgather_user;
+        if (rr != S->cx_rr) {
+            S->cx_rr = rr;
+            std::vector<long long> ll(rr.begin(), rr.end());
+            S->cx_rr_dev = to_device(ll, 0);
+            HIP_CHECK(hipStreamSynchronize(0));
+        }
+        if (world > 1 && S->m->upper) {
+            S->cx_send.alloc((size_t)world * maxlen);
+            S->cx_recv.alloc((size_t)maxlen);
+            if (!reduce) S->cx_all.alloc((size_t)world * world * maxlen);
+        }
     });
 }
 

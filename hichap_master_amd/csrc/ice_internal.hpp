@@ -29,9 +29,12 @@ namespace hh {
 
 constexpr int kR = 512;                 // rows per row-block
 #ifndef HH_KWBITS
-#define HH_KWBITS 13
+#define HH_KWBITS 12
 #endif
-constexpr int kWBits = HH_KWBITS;       // (build experiments: -DHH_KWBITS=12)
+// 4096-column tiles (round 5): a column-grouped block stages the tile's bias
+// slice (32 KB) AND the int64 column accumulator of the upper-triangle tiles
+// (32 KB) in LDS beside 11 waves' walk state
+constexpr int kWBits = HH_KWBITS;
 constexpr int kW = 1 << kWBits;         // columns per tile
 constexpr uint32_t kColMask = kW - 1;
 constexpr uint32_t kCntMax = 65535u;    // largest count stored in a tile (wide entry)
@@ -136,6 +139,7 @@ extern int64_t g_flat_max;       // hh_tune("flat_max"), build time
 // tiles on its own (no block barrier per tile).
 extern int64_t g_flat_cols;
 bool flat_cols_on(int32_t nJ);  // the column-grouped flat sweep for a matrix of nJ column tiles
+bool upper_tiles_on(int32_t nJ);  // upper-triangle tiles for a matrix of nJ column tiles (g_upper_tiles)
 extern int64_t g_flat_group;   // tiles per column group (0 = auto, 11 .. 44)
 // minimum row length (uint4 per row) of band g
 __host__ __device__ constexpr uint32_t band_min(int g) { return g == 0 ? 48u : g == 1 ? 24u : g == 2 ? 12u : g == 3 ? 6u : 1u; }
@@ -149,7 +153,9 @@ struct FlatDesc {
     int32_t frec, slot;      // flat record index, first unit partial
     uint32_t qbn, qbw;       // narrow / wide uint4 counts
     uint16_t nr, nfn, nfw;   // rows of the row-block, nonempty narrow / wide rows
-    uint16_t glo, ghi, pad_[3];  // ICE groups of the unit's rows
+    uint16_t glo, ghi;       // ICE groups of the unit's rows
+    uint16_t upper;          // 1: strictly upper tile (its entries also feed their columns)
+    uint32_t rb;             // local row-block (global first row = row_lo + kR rb)
 };
 static_assert(sizeof(FlatDesc) == 48, "FlatDesc layout");
 
@@ -187,6 +193,15 @@ struct TilePlan {
     std::vector<uint8_t> u_flat;        // per unit: 1 = swept by the flat kernel
     std::vector<int32_t> fg_ptr, fg_unit;  // flat groups (g_flat_cols): units of group g = fg_unit[fg_ptr[g] ..)
     std::vector<FlatDesc> fg_desc;         // per fg_unit entry
+    // upper-triangle tiles (g_upper_tiles): the column side of a strictly
+    // upper tile (J > J(its rows)) goes to an int64 slot of kW columns -- one
+    // per tile of a tiled / flat unit (u_cslot[u] + tile offset), one per
+    // flat column group (fg_cslot) -- and k_colsum adds, per column tile J,
+    // the slots jslot[jslot_ptr[J] ..) in a fixed order (integers: exact)
+    int upper = 0;
+    int64_t row_lo = 0;
+    std::vector<int32_t> u_cslot, fg_cslot, jslot_ptr, jslot;
+    int64_t n_cslots = 0;
     int64_t n_units_flat = 0;
     int64_t payload_bytes_flat = 0;     // payload of the flat units' tiles
     int64_t n_entries_padded = 0;     // wide slots
@@ -198,7 +213,11 @@ struct TilePlan {
 // (row-major, nloc x nJ, unpadded; cntn may be null).  row_group: ICE group
 // per local row.  Units are sized in 4-byte payload words.
 TilePlan plan_tiles(const uint16_t* cntw, const uint16_t* cntn, int64_t nloc, int32_t nJ,
-                    const std::vector<uint16_t>& row_group);
+                    const std::vector<uint16_t>& row_group, int64_t row_lo, bool upper);
+// a tile of (local) row-block rb and column tile J holds the column side
+__host__ __device__ __forceinline__ bool tile_is_upper(int upper, long long row_lo, int rb, int J) {
+    return upper && J > (int)((row_lo + (long long)rb * kR) >> kWBits);
+}
 
 struct TileDev {
     const uint32_t* pay;
@@ -228,6 +247,13 @@ struct TileDev {
     const int32_t* fg_unit;
     const FlatDesc* fg_desc;
     int flat_defer;  // flat kernel: merge a tile's compact sums after the next tile's barrier (hh_tune "flat_defer")
+    int upper;                      // the layout has upper-triangle tiles
+    long long row_lo;               // first row of the matrix (global)
+    const int32_t* u_cslot;         // per unit: its tiles' column slots (upper)
+    const int32_t* fg_cslot;        // per flat group: its column slot (upper)
+    unsigned long long* colpart;    // n_cslots x kW column partials (int64 fixed point)
+    const double* fix;              // {2^e, 2^-e}: this sweep's fixed-point scale of b
+    const unsigned long long* bfix; // B = round(b 2^e) of every bin (k_fixscale)
 };
 
 extern int g_flat_defer;
@@ -265,6 +291,9 @@ struct hh_matrix {
     hh::DBuf<int32_t> fg_ptr, fg_unit;  // column groups of the flat units (g_flat_cols)
     hh::DBuf<hh::FlatDesc> fg_desc;
     int64_t n_fgroups = 0;
+    int32_t upper = 0;             // upper-triangle tiles (g_upper_tiles at build time)
+    int64_t n_cslots = 0;
+    hh::DBuf<int32_t> u_cslot, fg_cslot, jslot_ptr, jslot;
     hh::DBuf<long long> wide_ptr;  // local rows + 1
     hh::DBuf<int32_t> wide_col;
     hh::DBuf<double> wide_cnt;
@@ -277,16 +306,19 @@ struct hh_matrix {
         return pay.bytes() + payn.bytes() + tile_entn.bytes() + tile_rpn.bytes() + tile_J.bytes() +
                tile_rb.bytes() + tile_ent.bytes() + tile_rp.bytes() +
                u_tlo.bytes() * 7 + blk_unit_ptr.bytes() + tile_perm.bytes() + tile_band.bytes() + u_whole.bytes() + tile_fw.bytes() + tile_frec.bytes() + frec.bytes() + blk_tile_ptr.bytes() + u_glo.bytes() * 2 +
-               fg_ptr.bytes() + fg_unit.bytes() + fg_desc.bytes() +
+               fg_ptr.bytes() + fg_unit.bytes() + fg_desc.bytes() + u_cslot.bytes() + fg_cslot.bytes() +
+               jslot_ptr.bytes() + jslot.bytes() +
                wide_ptr.bytes() + wide_col.bytes() + wide_cnt.bytes() + diag.bytes() + row_nnz2.bytes() +
                row_sum2.bytes() + row_group.bytes() + band.bytes() + band4.bytes();
     }
-    hh::TileDev dev() const {
+    hh::TileDev dev(unsigned long long* colpart = nullptr, const double* fix = nullptr,
+                    const unsigned long long* bfix = nullptr) const {
         return hh::TileDev{pay.p, payn.p, tile_J.p, tile_ent.p, tile_rp.p, tile_entn.p, tile_rpn.p, u_tlo.p,
                            u_thi.p, u_rb.p, u_rlo.p, u_rhi.p, u_slot.p, u_glo.p, u_ghi.p, blk_unit_ptr.p,
                            u_order.p, tile_perm.p, tile_band.p, tile_fw.p, tile_frec.p,
                            reinterpret_cast<const uint4*>(frec.p), u_whole.p, fg_ptr.p, fg_unit.p, fg_desc.p,
-                           hh::g_flat_defer};
+                           hh::g_flat_defer, upper && colpart ? 1 : 0, (long long)row_lo, u_cslot.p, fg_cslot.p,
+                           colpart, fix, bfix};
     }
 };
 

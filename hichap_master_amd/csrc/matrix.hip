@@ -41,7 +41,11 @@ int64_t g_flat_max = 64;     // longest row (uint4) of a flat tile segment; 0 = 
 int64_t g_build_debug = 0;
 int64_t g_host_build = 0;    // hh_tune("host_build"): 1 = host builder for every pixel table
 
-int64_t g_upper_tiles = 0;
+// upper-triangle tiles; off keeps both triangles in every tile
+int64_t g_upper_tiles = -1;
+// auto (-1): with the column-grouped flat sweep (the large matrices, whose
+// sweep is HBM-bound on the tile bytes); 1 forces them on (tests), 0 off
+bool upper_tiles_on(int32_t nJ) { return g_upper_tiles > 0 || (g_upper_tiles < 0 && flat_cols_on(nJ)); }
 int64_t g_band4 = 1;         // nibble band on
 double g_band4_density = 0.25;
 double g_band8_big = 0.05;
@@ -233,10 +237,12 @@ void plan_block(const uint16_t* cntw, const uint16_t* cntn, int64_t nloc, int32_
 }  // namespace
 
 TilePlan plan_tiles(const uint16_t* cntw, const uint16_t* cntn, int64_t nloc, int32_t nJ,
-                    const std::vector<uint16_t>& row_group) {
+                    const std::vector<uint16_t>& row_group, int64_t row_lo, bool upper) {
     TilePlan P;
     P.nloc = nloc;
     P.nJ = nJ;
+    P.upper = upper ? 1 : 0;
+    P.row_lo = row_lo;
     P.nrb = (nloc + kR - 1) / kR;
     P.tile_of.assign((size_t)P.nrb * nJ, -1);
     P.blk_tile_ptr.assign(P.nrb + 1, 0);
@@ -460,8 +466,46 @@ TilePlan plan_tiles(const uint16_t* cntw, const uint16_t* cntn, int64_t nloc, in
             d.nfw = (uint16_t)fww[2 * kFlatWaves + 1];
             d.glo = P.u_glo[u];
             d.ghi = P.u_ghi[u];
+            d.upper = tile_is_upper(P.upper, row_lo, P.u_rb[u], P.tile_J[t]) ? 1 : 0;
+            d.rb = (uint32_t)P.u_rb[u];
             P.fg_desc.push_back(d);
         }
+    }
+    // column slots of the upper tiles' column side: per flat group one (if
+    // any of its tiles is strictly upper), per tile of every other unit one;
+    // per column tile J the list of its slots in slot order (k_colsum)
+    P.u_cslot.assign(P.u_tlo.size(), -1);
+    if (P.upper) {
+        std::vector<std::vector<int32_t>> byJ((size_t)nJ);
+        auto grouped = [&](size_t u) { return flat_cols_on(nJ) && P.u_flat[u]; };
+        for (size_t u = 0; u < P.u_tlo.size(); ++u) {
+            if (grouped(u)) continue;
+            bool any = false;
+            for (int32_t t = P.u_tlo[u]; t < P.u_thi[u]; ++t) any |= tile_is_upper(1, row_lo, P.u_rb[u], P.tile_J[t]);
+            if (!any) continue;
+            P.u_cslot[u] = (int32_t)P.n_cslots;
+            for (int32_t t = P.u_tlo[u]; t < P.u_thi[u]; ++t)
+                if (tile_is_upper(1, row_lo, P.u_rb[u], P.tile_J[t]))
+                    byJ[(size_t)P.tile_J[t]].push_back((int32_t)(P.n_cslots + (t - P.u_tlo[u])));
+            P.n_cslots += P.u_thi[u] - P.u_tlo[u];
+        }
+        const size_t ng = P.fg_ptr.empty() ? 0 : P.fg_ptr.size() - 1;
+        P.fg_cslot.assign(ng, -1);
+        for (size_t g = 0; g < ng; ++g) {
+            bool any = false;
+            for (int32_t k = P.fg_ptr[g]; k < P.fg_ptr[g + 1]; ++k) any |= P.fg_desc[k].upper != 0;
+            if (!any) continue;
+            P.fg_cslot[g] = (int32_t)P.n_cslots;
+            byJ[(size_t)P.tile_J[P.u_tlo[P.fg_unit[P.fg_ptr[g]]]]].push_back((int32_t)P.n_cslots);
+            ++P.n_cslots;
+        }
+        P.jslot_ptr.assign((size_t)nJ + 1, 0);
+        for (int32_t J = 0; J < nJ; ++J) {
+            std::sort(byJ[J].begin(), byJ[J].end());
+            P.jslot.insert(P.jslot.end(), byJ[J].begin(), byJ[J].end());
+            P.jslot_ptr[J + 1] = (int32_t)P.jslot.size();
+        }
+        if (P.n_cslots > INT32_MAX / kW) HH_THROW(HH_ERR_ARG, "plan too large (column slots)");
     }
     if (g_unit_lpt) {
         // each list by cost class (bit length of words + per-tile cost),
@@ -524,6 +568,14 @@ void upload_plan(const TilePlan& P, hh_matrix& m, hipStream_t s) {
         m.fg_ptr = to_device(P.fg_ptr, s);
         m.fg_unit = to_device(P.fg_unit, s);
         m.fg_desc = to_device(P.fg_desc, s);
+    }
+    m.upper = P.upper;
+    m.n_cslots = P.n_cslots;
+    if (P.upper) {
+        m.u_cslot = to_device(P.u_cslot, s);
+        if (!P.fg_cslot.empty()) m.fg_cslot = to_device(P.fg_cslot, s);
+        m.jslot_ptr = to_device(P.jslot_ptr, s);
+        if (!P.jslot.empty()) m.jslot = to_device(P.jslot, s);
     }
     HIP_CHECK(hipStreamSynchronize(s));  // the plan's host vectors may die after return
 }
@@ -730,6 +782,7 @@ int hh_matrix_from_pixels(const int64_t* bin1, const int64_t* bin2, const double
         // tile counts: narrow (count <= 7) and wide entries per (row, tile);
         // counts > kCntMax go to the wide list
         const int32_t nJ = (int32_t)((n_bins + kW - 1) / kW);
+        const bool upper = upper_tiles_on(nJ);
         std::vector<uint16_t> cntw((size_t)nloc * nJ, 0), cntn((size_t)nloc * nJ, 0);
         std::vector<long long> wptr(nloc + 1, 0);
         std::vector<uint8_t> band((size_t)nloc * band_stride(W), 0);
@@ -749,7 +802,7 @@ int hh_matrix_from_pixels(const int64_t* bin1, const int64_t* bin2, const double
                     continue;
                 }
                 if (vals[k] > kCntMax) ++wptr[r + 1];
-                else if (g_upper_tiles && (cols[k] >> kWBits) < ((row_lo + r) >> kWBits)) continue;  // stored as its mirror
+                else if (upper && (cols[k] >> kWBits) < ((row_lo + r) >> kWBits)) continue;  // stored as its mirror
                 else if (vals[k] <= kNarrowMax) ++cntn[(size_t)r * nJ + (cols[k] >> kWBits)];
                 else ++cntw[(size_t)r * nJ + (cols[k] >> kWBits)];
             }
@@ -757,7 +810,7 @@ int hh_matrix_from_pixels(const int64_t* bin1, const int64_t* bin2, const double
         for (int64_t r = 0; r < nloc; ++r) wptr[r + 1] += wptr[r];
         std::vector<uint16_t> bg = bin_groups(*m);
         std::vector<uint16_t> rgroup(bg.begin() + row_lo, bg.begin() + row_hi);
-        TilePlan P = plan_tiles(cntw.data(), cntn.data(), nloc, nJ, rgroup);
+        TilePlan P = plan_tiles(cntw.data(), cntn.data(), nloc, nJ, rgroup, row_lo, upper);
         // fill payloads + wide list
         std::vector<uint32_t> pay(P.n_entries_padded, 0u);
         std::vector<uint16_t> payn(P.n_narrow_padded, 0u);
@@ -772,7 +825,7 @@ int hh_matrix_from_pixels(const int64_t* bin1, const int64_t* bin2, const double
                 if (in_band(row_lo + r, cols[q], vals[q]) || in_nib(row_lo + r, cols[q], vals[q])) continue;
                 if (vals[q] > kCntMax) { wcol[wp] = cols[q]; wcnt[wp++] = vals[q]; continue; }
                 const int32_t J = cols[q] >> kWBits;
-                if (g_upper_tiles && J < (int32_t)((row_lo + r) >> kWBits)) continue;
+                if (upper && J < (int32_t)((row_lo + r) >> kWBits)) continue;
                 if (J != curJ) {
                     const int32_t t = P.tile_of[rb * nJ + J];
                     pos = P.tile_ent[t] + P.tile_rp[(size_t)t * (kR + 1) + k];
@@ -829,7 +882,7 @@ int hh_matrix_get_info(const hh_matrix* m, hh_matrix_info* info) {
         info->n_slots_narrow = m->n_slots_narrow;
         info->payload_bytes = 4 * m->n_slots + 2 * m->n_slots_narrow + (int64_t)m->band.n + (int64_t)m->band4.n;
         info->band_w4 = m->band_w4;
-        info->pad2_ = 0;
+        info->upper = m->upper;
         info->band_w = m->band_w;
         info->n_units_flat = (int32_t)m->n_units_flat;
         info->n_band = m->n_band;

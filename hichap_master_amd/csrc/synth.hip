@@ -280,7 +280,7 @@ void synth_setup(const hh_synth_params* p, SynthHost& h, hipStream_t s) {
     d.ignore_diags = p->ignore_diags;
     d.cis_only = p->cis_only ? 1 : 0;
     d.seed = p->seed;
-    d.upper = g_upper_tiles ? 1 : 0;
+    d.upper = upper_tiles_on(d.nJ) ? 1 : 0;
     {
         const BandWidths bw = synth_band_w(p, h.offsets);
         d.band_w = bw.w8;
@@ -465,7 +465,7 @@ int hh_synth_build(const hh_synth_params* p, int64_t row_lo, int64_t row_hi, voi
         cntn.release();
         std::vector<uint16_t> bg = bin_groups(*m);
         std::vector<uint16_t> rgroup(bg.begin() + row_lo, bg.begin() + row_hi);
-        TilePlan P = plan_tiles(hc.data(), hn.data(), nloc, nJ, rgroup);
+        TilePlan P = plan_tiles(hc.data(), hn.data(), nloc, nJ, rgroup, row_lo, h.dev.upper != 0);
         upload_plan(P, *m, s);
         m->row_group = to_device(rgroup, s);
         DBuf<int32_t> tof = to_device(P.tile_of, s);

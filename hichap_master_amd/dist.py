@@ -119,6 +119,14 @@ class Exchange:
         be = dist.get_backend(group) if dist.is_initialized() else "none"
         self.fused = be == "nccl"
 
+    def reduce_callback(self):
+        """An hh_reduce_fn over this group: the column side of the
+        upper-triangle tiles (per-rank padded int64 blocks summed, this
+        rank's block returned; integer sums, so any reduction order is
+        exact)."""
+        return _python_reduce_scatter(self.world, self.dist.get_rank(self.group), self.group,
+                                      on_device=self.fused)
+
     def all_gather(self):
         if self.world == 1:
             self.gathered.copy_(self.local)
@@ -137,6 +145,9 @@ def _stream():
 
 def run_filters(backend, ex: Exchange):
     s = _stream()
+    bind = getattr(backend, "bind_exchange", None)
+    if bind is not None:  # the column side of upper-triangle tiles crosses ranks
+        bind(ex)
     backend.marg_local(0, ex.local, s)
     ex.all_gather()
     backend.set_marg(ex.gathered, ex.world, ex.maxlen, ex.rank_rows, s)
@@ -271,6 +282,39 @@ def _python_allgather(world, group=None):
             g = torch.cat(parts).cuda()
             torch.cuda.synchronize()
             call("hh_device_copy", C.c_void_p(recv), C.c_void_p(g.data_ptr()), 8 * int(count) * world, st)
+            call("hh_synchronize", st)
+            return 0
+        except Exception:  # never raise through C
+            return -2
+    return _cb_type()(cb)
+
+
+def _python_reduce_scatter(world, rank, group=None, on_device=False):
+    """An hh_reduce_fn over torch.distributed: ``send`` holds ``world``
+    blocks of ``count`` int64, ``recv`` gets the element-wise sum of every
+    rank's block ``rank``.  ``on_device``: reduce_scatter_tensor on the
+    device (nccl); otherwise an all_reduce through host memory (gloo)."""
+    import ctypes as C
+    import torch
+    import torch.distributed as tdist
+    from ._lib import call
+
+    def cb(send, count, recv, user, stream):
+        try:
+            st = C.c_void_p(stream) if stream else None
+            n = int(count)
+            buf = torch.empty(world * n, dtype=torch.int64, device="cuda")
+            call("hh_device_copy", C.c_void_p(buf.data_ptr()), C.c_void_p(send), 8 * world * n, st)
+            call("hh_synchronize", st)
+            if on_device:
+                out = torch.empty(n, dtype=torch.int64, device="cuda")
+                tdist.reduce_scatter_tensor(out, buf, group=group)
+            else:
+                cpu = buf.cpu()
+                tdist.all_reduce(cpu, group=group)
+                out = cpu[rank * n:(rank + 1) * n].cuda()
+            torch.cuda.synchronize()
+            call("hh_device_copy", C.c_void_p(recv), C.c_void_p(out.data_ptr()), 8 * n, st)
             call("hh_synchronize", st)
             return 0
         except Exception:  # never raise through C

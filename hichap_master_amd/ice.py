@@ -280,6 +280,17 @@ class IceState:
     def marg_local(self, mode, out=None, stream=None):
         call("hh_ice_marg_local", self._h, int(mode), ptr(out), stream)
 
+    def bind_exchange(self, ex):
+        """Register ``ex``'s int64 reduce-scatter for the column side of the
+        upper-triangle tiles (hh_ice_set_column_exchange; a no-op for a
+        whole matrix or a layout without them)."""
+        if ex.world <= 1:
+            return
+        self._rs = ex.reduce_callback()  # kept alive with the state
+        rr = np.ascontiguousarray(ex.rank_rows, dtype=np.int64)
+        call("hh_ice_set_column_exchange", self._h, int(ex.world), -1, ptr(rr), C.cast(self._rs, C.c_void_p),
+             None, None, None)
+
     def set_marg(self, gathered, world, maxlen, rank_rows, stream=None):
         rr = np.ascontiguousarray(rank_rows, dtype=np.int64)
         call("hh_ice_set_marg", self._h, ptr(gathered), int(world), int(maxlen), ptr(rr), stream)

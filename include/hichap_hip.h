@@ -123,7 +123,7 @@ typedef struct {
     int64_t n_band;        /* nonzero entries held by the band               */
     int64_t payload_bytes_flat; /* part of payload_bytes in flat-kernel tiles */
     int32_t band_w4;       /* nibble band outer width (== band_w: none)      */
-    int32_t pad2_;
+    int32_t upper;         /* 1: upper-triangle tiles         */
 } hh_matrix_info;
 
 /* Build from cooler's pixel table (host arrays; any order: a sorted
@@ -281,6 +281,23 @@ int hh_comm_unique_id(uint8_t* id128);
 int hh_comm_init(const uint8_t* id128, int32_t world, int32_t rank, hh_comm** out);
 int hh_comm_free(hh_comm* c);
 int hh_comm_allgather(const double* send, int64_t count, double* recv, void* comm, void* stream);
+/* Upper-triangle tiles store an entry of a strictly upper
+ * tile once, and its column side belongs to the rank owning that column: a
+ * shard's marginals need a second exchange per sweep, an int64 reduce-scatter
+ * of the ranks' padded row blocks (integer sums: exact, the same bits on any
+ * number of ranks).  `reduce(send, count, recv, user, stream)`: send = world x
+ * count int64 (rank-major blocks), recv = count: the sum over the ranks of this
+ * rank's block; 0 = ok.  hh_comm_reduce_scatter is RCCL's (user = the
+ * hh_comm).  hh_ice_*_sharded register the exchange themselves (RCCL's when
+ * their all-gather is hh_comm_allgather, else a reduction through the
+ * all-gather callback: world x its bytes); a caller that drives
+ * hh_ice_marg_local on a shard registers it once after hh_ice_create
+ * (rank -1: inferred from the matrix's row range; reduce NULL keeps one
+ * registered before for the same world). */
+typedef int (*hh_reduce_fn)(const int64_t* send, int64_t count, int64_t* recv, void* user, void* stream);
+int hh_comm_reduce_scatter(const int64_t* send, int64_t count, int64_t* recv, void* comm, void* stream);
+int hh_ice_set_column_exchange(hh_ice* s, int32_t world, int32_t rank, const int64_t* rank_rows, hh_reduce_fn reduce,
+                               void* reduce_user, hh_allgather_fn allgather, void* allgather_user);
 /* The whole balance (filters, iterations to convergence, finalize) on this
  * rank's shard `m`; outputs as hh_ice_balance (weights for every bin, identical
  * on every rank). */

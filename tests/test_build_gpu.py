@@ -49,6 +49,15 @@ def _genome(seed, sizes=(900, 700, 500), A=30.0, trans=0.01, big=False):
     return b1, b2, c, off
 
 
+@pytest.fixture
+def upper_tiles():
+    """upper-triangle tiles forced on; auto afterwards"""
+    from hichap_master_amd._lib import call
+    call("hh_tune", b"upper_tiles", 1)
+    yield
+    call("hh_tune", b"upper_tiles", -1)
+
+
 @pytest.mark.parametrize("ignore_diags,cis_only,big", [(1, False, False), (0, False, True), (2, True, False),
                                                        (1, True, True)])
 def test_device_build_equals_host_build(ice, ignore_diags, cis_only, big):
@@ -62,6 +71,35 @@ def test_device_build_equals_host_build(ice, ignore_diags, cis_only, big):
     wh, sh = ice.balance_matrix(mh, opts)
     np.testing.assert_array_equal(wd, wh)
     np.testing.assert_array_equal(np.atleast_1d(sd["iters"]), np.atleast_1d(sh["iters"]))
+    w_ref, st_ref = ice_ref.balance(b1, b2, c, n, off, ignore_diags=ignore_diags, cis_only=cis_only, max_iters=300)
+    np.testing.assert_allclose(wd, w_ref, rtol=1e-9, equal_nan=True)
+
+
+@pytest.mark.parametrize("ignore_diags,cis_only,big", [(1, False, True), (2, True, False)])
+def test_device_build_equals_host_build_upper_tiles(ice, upper_tiles, ignore_diags, cis_only, big):
+    """The same with upper-triangle tiles: both builders keep an entry of a
+    lower tile only as its mirror; weights bitwise equal, the oracle's within
+    the ICE tolerance, and close to the both-triangle layout: the column
+    side rounds b to b * 2^e (e from the raw-marginal bound; counts to 2e6
+    here cost ~22 bits of it), so up to ~1e-11 of a converged weight."""
+    from hichap_master_amd._lib import call
+    b1, b2, c, off = _genome(13 + ignore_diags, sizes=(5000, 4000, 700), big=big)
+    n = int(off[-1])
+    md = ice.ContactMatrix.from_pixels(b1, b2, c, n, off, ignore_diags, cis_only)
+    mh = _host_build(ice, b1, b2, c, n, off, ignore_diags, cis_only)
+    assert md.info()["upper"] == 1 and mh.info()["upper"] == 1
+    _same_matrix(ice, md, mh)
+    opts = ice.IceOptions(ignore_diags=ignore_diags, cis_only=cis_only, max_iters=300)
+    wd, sd = ice.balance_matrix(md, opts)
+    wh, sh = ice.balance_matrix(mh, opts)
+    np.testing.assert_array_equal(wd, wh)
+    np.testing.assert_array_equal(np.atleast_1d(sd["iters"]), np.atleast_1d(sh["iters"]))
+    call("hh_tune", b"upper_tiles", 0)
+    mb = ice.ContactMatrix.from_pixels(b1, b2, c, n, off, ignore_diags, cis_only)
+    assert mb.info()["upper"] == 0 and mb.info()["payload_bytes"] > md.info()["payload_bytes"]
+    wb, sb = ice.balance_matrix(mb, opts)
+    np.testing.assert_array_equal(np.atleast_1d(sd["iters"]), np.atleast_1d(sb["iters"]))
+    np.testing.assert_allclose(wd, wb, rtol=1e-12 if not big else 1e-10, equal_nan=True)
     w_ref, st_ref = ice_ref.balance(b1, b2, c, n, off, ignore_diags=ignore_diags, cis_only=cis_only, max_iters=300)
     np.testing.assert_allclose(wd, w_ref, rtol=1e-9, equal_nan=True)
 

@@ -35,6 +35,9 @@ def _worker(rank, world, port, case, cis_only, outdir, impl="python", rr_force=N
     _lib.call("hh_set_device", 0)
     _lib.call("hh_tune", b"conc_min_bytes", 0)  # three sweep streams even on this small shard
     _lib.call("hh_tune", b"sweep_single", 0)    # (the single launch is checked first: off)
+    if impl.endswith("_upper"):  # upper-triangle tiles: the column side crosses the ranks
+        impl = impl[:-len("_upper")]
+        _lib.call("hh_tune", b"upper_tiles", 1)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     tdist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -100,6 +103,41 @@ def test_balance_sharded_two_processes(cis_only, impl):
         np.testing.assert_allclose(w, wr, rtol=1e-9, equal_nan=True)
         np.testing.assert_array_equal(it, np.atleast_1d(st_full["iters"]))
     np.testing.assert_array_equal(ws[0], ws[1])
+
+
+@pytest.mark.parametrize("impl", ["python", "capi"])
+def test_upper_tiles_two_processes(impl):
+    """Upper-triangle tiles over two processes: the column side of each
+    rank's strictly upper tiles reaches the other rank's rows through the
+    int64 exchange (a torch.distributed reduce callback for the Python
+    driver, the all-gather fallback summed in rank order for the C++ loop):
+    every rank's weights equal the one-process upper-tile run bitwise."""
+    import torch.multiprocessing as mp
+    from hichap_master_amd import _lib, ice
+    from oracle import ice_ref
+    _lib.require_gpu()
+    rng = np.random.default_rng(23)
+    case = synth.coo_genome([5000, 4000, 700], rng, A=8.0, trans_density=0.002)
+    b1, b2, c, off = case
+    n = int(off[-1])
+    _lib.call("hh_tune", b"upper_tiles", 1)
+    try:
+        m = ice.ContactMatrix.from_pixels(b1, b2, c, n, off)
+        assert m.info()["upper"] == 1
+        w_full, st_full = ice.balance_matrix(m, ice.IceOptions(max_iters=400))
+        m.close()
+    finally:
+        _lib.call("hh_tune", b"upper_tiles", -1)
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_worker, args=(2, _free_port(), case, False, d, impl + "_upper"), nprocs=2,
+                           start_method="spawn")
+        ws = [np.load(os.path.join(d, f"w{r}.npy")) for r in range(2)]
+        its = [np.load(os.path.join(d, f"it{r}.npy")) for r in range(2)]
+    wr, _ = ice_ref.balance(b1, b2, c, n, off, max_iters=400)
+    for w, it in zip(ws, its):
+        np.testing.assert_array_equal(w, w_full)
+        np.testing.assert_array_equal(it, np.atleast_1d(st_full["iters"]))
+    np.testing.assert_allclose(w_full, wr, rtol=1e-9, equal_nan=True)
 
 
 def _fail_worker(rank, world, port, case, outdir):

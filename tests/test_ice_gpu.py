@@ -115,42 +115,21 @@ def test_invalid_counts_rejected(ice):
 
 def _sharded_weights(ice, b1, b2, c, off, rr, max_iters=300):
     """Row shards on one GPU with a manual marginal gather (the sharded
-    driver's exchange, without a process group)."""
-    import torch
+    driver's exchange, without a process group; the column side of
+    upper-triangle tiles through one thread per shard)."""
+    from tests.shard_exchange import balance_states
     n = int(off[-1])
     opts = ice.IceOptions(max_iters=max_iters)
     W = len(rr) - 1
     shards = [ice.ContactMatrix.from_pixels(b1, b2, c, n, off, row_range=(rr[k], rr[k + 1])) for k in range(W)]
     states = [ice.IceState(m, opts) for m in shards]
-    maxlen = int(np.max(np.diff(rr)))
-    loc = [torch.zeros(maxlen, dtype=torch.float64, device="cuda") for _ in range(W)]
-    gat = torch.zeros(W * maxlen, dtype=torch.float64, device="cuda")
-    s = torch.cuda.current_stream().cuda_stream
-
-    def exchange(mode):
-        for k in range(W):
-            states[k].marg_local(mode, loc[k], s)
-        for k in range(W):
-            gat[k * maxlen:(k + 1) * maxlen].copy_(loc[k])
-        for k in range(W):
-            states[k].set_marg(gat, W, maxlen, rr, s)
-    exchange(0)
-    for st_ in states:
-        st_.filter_nnz(s)
-    exchange(1)
-    for st_ in states:
-        st_.filter_count_mad(s)
-    for it in range(max_iters):
-        exchange(2)
+    try:
+        res = balance_states(states, rr, max_iters)
+    finally:
         for st_ in states:
-            st_.update(s)
-        if it % 8 == 7 and states[0].active_groups(s) == 0:
-            break
-    res = [st_.finalize(s) for st_ in states]
-    for st_ in states:
-        st_.close()
-    for m in shards:
-        m.close()
+            st_.close()
+        for m in shards:
+            m.close()
     for w, _ in res[1:]:
         np.testing.assert_array_equal(w, res[0][0])
     return res[0]
@@ -290,16 +269,20 @@ def test_dense_band_widths(ice, band_w, band4):
     np.testing.assert_allclose(w, w_ref, rtol=1e-9, equal_nan=True)
 
 
+@pytest.mark.parametrize("upper", [0, 1])
 @pytest.mark.parametrize("flat_max,flat_cols", [(0, -1), (2, -1), (24, -1), (255, -1), (24, 1), (255, 1)])
-def test_flat_tiles(ice, flat_max, flat_cols):
+def test_flat_tiles(ice, flat_max, flat_cols, upper):
     """Tiles whose rows are all short go to the flat (merge-path) sweep kernel;
     any threshold (none, few, most, all tiles flat) gives the oracle's weights,
-    and a 3-shard run is bitwise equal to the whole-matrix run."""
+    and a 3-shard run is bitwise equal to the whole-matrix run -- with both
+    triangles in every tile, and with upper-triangle tiles (the column side in
+    fixed point, exchanged between the shards as int64)."""
     from hichap_master_amd import _lib
     b1, b2, c, off = _case(41, sizes=(9000, 7000, 600), A=3.0, trans=0.0005)
     n = int(off[-1])
     _lib.call("hh_tune", b"flat_max", flat_max)
     _lib.call("hh_tune", b"flat_cols", flat_cols)  # 1: the column-grouped kernel (auto: big matrices only)
+    _lib.call("hh_tune", b"upper_tiles", upper)
     try:
         m = ice.ContactMatrix.from_pixels(b1, b2, c, n, off)
         inf = m.info()
@@ -309,10 +292,13 @@ def test_flat_tiles(ice, flat_max, flat_cols):
             assert inf["n_units_flat"] > 0
         w, st = ice.balance_matrix(m, ice.IceOptions(max_iters=300))
         m.close()
+        if upper:
+            assert inf["upper"] == 1
         ws, sts = _sharded_weights(ice, b1, b2, c, off, np.array([0, 4096, 11264, n]))
     finally:
         _lib.call("hh_tune", b"flat_max", 64)
         _lib.call("hh_tune", b"flat_cols", -1)
+        _lib.call("hh_tune", b"upper_tiles", -1)
     w_ref, st_ref = ice_ref.balance(b1, b2, c, n, off, max_iters=300)
     assert st["iters"] == st_ref["iters"]
     np.testing.assert_allclose(w, w_ref, rtol=1e-9, equal_nan=True)
@@ -320,18 +306,22 @@ def test_flat_tiles(ice, flat_max, flat_cols):
     assert sts["iters"] == st["iters"]
 
 
-def test_flat_block_shapes_bitwise(ice):
+@pytest.mark.parametrize("upper", [0, 1])
+def test_flat_block_shapes_bitwise(ice, upper):
     """The column-grouped flat kernel's block width (waves sharing one staged
     b[J]) and group size (a build knob) change only who sweeps a flat tile,
-    not its per-row partials: bitwise the same weights."""
+    not its per-row partials (nor, with upper-triangle tiles, its exact
+    fixed-point column partials): bitwise the same weights."""
     from hichap_master_amd import _lib
     b1, b2, c, off = _case(41, sizes=(9000, 7000, 600), A=3.0, trans=0.0005)
     n = int(off[-1])
     res = []
     _lib.call("hh_tune", b"flat_cols", 1)  # (auto: column groups only from 32 column tiles)
+    _lib.call("hh_tune", b"upper_tiles", upper)
     try:
         for waves, group in [(8, 16), (10, 16), (11, 33), (11, 1), (8, 64)]:
             _lib.call("hh_tune", b"flatw_waves", waves)
+            _lib.call("hh_tune", b"flatw_waves_up", 11 if waves == 11 else 8)
             _lib.call("hh_tune", b"flat_group", group)
             m = ice.ContactMatrix.from_pixels(b1, b2, c, n, off)
             assert m.info()["n_units_flat"] > 0
@@ -339,8 +329,10 @@ def test_flat_block_shapes_bitwise(ice):
             m.close()
     finally:
         _lib.call("hh_tune", b"flatw_waves", 11)
+        _lib.call("hh_tune", b"flatw_waves_up", 8)
         _lib.call("hh_tune", b"flat_group", 0)
         _lib.call("hh_tune", b"flat_cols", -1)
+        _lib.call("hh_tune", b"upper_tiles", -1)
     for w, st in res[1:]:
         np.testing.assert_array_equal(w, res[0][0])
         assert st["iters"] == res[0][1]["iters"]

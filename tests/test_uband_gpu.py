@@ -19,6 +19,13 @@ def ice():
     return ice_mod
 
 
+def _upper(on):
+    """upper-triangle tiles forced on / off (these matrices
+    are below the automatic threshold)"""
+    from hichap_master_amd import _lib
+    _lib.call("hh_tune", b"upper_tiles", 1 if on else 0)
+
+
 def _uband(on):
     """on: the upper-band sweep whatever the size (these matrices are below
     the automatic threshold); off: the symmetric band kernels"""
@@ -32,13 +39,12 @@ def _force_uband():
     _uband(True)
     yield
     _lib.call("hh_tune", b"uband", 1)
+    _lib.call("hh_tune", b"upper_tiles", -1)
 
 
 def _balance_synth(ice, sizes, kw, opts, row_ranges=None):
     """Balance the synthetic genome whole (row_ranges None) or as row shards
     on one GPU with a manual marginal gather (the sharded driver's exchange)."""
-    import torch
-    n = int(np.sum(sizes))
     if row_ranges is None:
         m = ice.ContactMatrix.synthetic(sizes, **kw)
         try:
@@ -49,32 +55,9 @@ def _balance_synth(ice, sizes, kw, opts, row_ranges=None):
     W = len(rr) - 1
     shards = [ice.ContactMatrix.synthetic(sizes, row_range=(int(rr[k]), int(rr[k + 1])), **kw) for k in range(W)]
     states = [ice.IceState(m, opts) for m in shards]
-    maxlen = int(np.max(np.diff(rr)))
-    loc = [torch.zeros(maxlen, dtype=torch.float64, device="cuda") for _ in range(W)]
-    gat = torch.zeros(W * maxlen, dtype=torch.float64, device="cuda")
-    s = torch.cuda.current_stream().cuda_stream
-
-    def exchange(mode):
-        for k in range(W):
-            states[k].marg_local(mode, loc[k], s)
-        for k in range(W):
-            gat[k * maxlen:(k + 1) * maxlen].copy_(loc[k])
-        for k in range(W):
-            states[k].set_marg(gat, W, maxlen, rr, s)
+    from tests.shard_exchange import balance_states
     try:
-        exchange(0)
-        for st_ in states:
-            st_.filter_nnz(s)
-        exchange(1)
-        for st_ in states:
-            st_.filter_count_mad(s)
-        for it in range(opts.max_iters):
-            exchange(2)
-            for st_ in states:
-                st_.update(s)
-            if it % 8 == 7 and states[0].active_groups(s) == 0:
-                break
-        res = [st_.finalize(s) for st_ in states]
+        res = balance_states(states, rr, opts.max_iters)
     finally:
         for st_ in states:
             st_.close()
@@ -116,6 +99,10 @@ def test_uband_matches_symmetric_sweep(ice, spec):
     w1, s1 = _balance_synth(ice, sizes, kw, opts)
     assert s1["iters"] == s0["iters"]
     np.testing.assert_allclose(w1, w0, rtol=1e-12, equal_nan=True)
+    _upper(True)  # + upper-triangle tiles: the tiles' column side in fixed point
+    w2, s2 = _balance_synth(ice, sizes, kw, opts)
+    assert s2["iters"] == s0["iters"]
+    np.testing.assert_allclose(w2, w0, rtol=1e-12, equal_nan=True)
 
 
 def test_uband_matches_oracle(ice):
@@ -135,11 +122,15 @@ def test_uband_matches_oracle(ice):
     np.testing.assert_allclose(w, w_ref, rtol=1e-9, equal_nan=True)
 
 
+@pytest.mark.parametrize("upper", [0, 1])
 @pytest.mark.parametrize("cuts", [[0, 4096, 14637], [0, 512, 3584, 6144, 14637], [0, 2560, 5120, 7680, 14637]])
-def test_uband_shards_bitwise(ice, cuts):
+def test_uband_shards_bitwise(ice, cuts, upper):
     """Row shards (512-row aligned, workgroup-unaligned, shorter than the band)
     give bitwise the one-shard weights: each shard sweeps the workgroups whose
-    columns reach it from halo rows rebuilt out of its own lower halves."""
+    columns reach it from halo rows rebuilt out of its own lower halves; with
+    upper-triangle tiles the column side's int64 partials are summed over the
+    shards (exact: bitwise too)."""
+    _upper(upper)
     sizes, kw = _model(_CHROM)
     opts = ice.IceOptions(max_iters=300)
     w_full, s_full = _balance_synth(ice, sizes, kw, opts)
@@ -148,7 +139,9 @@ def test_uband_shards_bitwise(ice, cuts):
     assert s["iters"] == s_full["iters"]
 
 
-def test_uband_shards_bitwise_genome_cis_only(ice):
+@pytest.mark.parametrize("upper", [0, 1])
+def test_uband_shards_bitwise_genome_cis_only(ice, upper):
+    _upper(upper)
     sizes, kw = _model(_GENOME)
     kw = dict(kw, cis_only=True)
     opts = ice.IceOptions(max_iters=300)
@@ -158,16 +151,20 @@ def test_uband_shards_bitwise_genome_cis_only(ice):
     np.testing.assert_array_equal(s["iters"], s_full["iters"])  # per chromosome
 
 
+@pytest.mark.parametrize("upper", [0, 1], ids=["both_triangles", "upper_tiles"])
 @pytest.mark.parametrize("mode", [0, 2], ids=["symmetric", "upper"])
-def test_one_sweep_row_sums_equal_export(ice, mode):
+def test_one_sweep_row_sums_equal_export(ice, mode, upper):
     """b = 1: one sweep's marginals are the row sums of the exported table,
-    exactly (integer counts); the synthetic generator is symmetric bit for
-    bit (it once drew a few pixels of the two triangles 1 apart)."""
+    exactly (integer counts; with upper-triangle tiles the column side's
+    fixed point holds b = 1 exactly); the synthetic generator is symmetric bit
+    for bit (it once drew a few pixels of the two triangles 1 apart)."""
     import torch
     from hichap_master_amd import _lib
+    _upper(upper)
     sizes, kw = _model(_CHROM)
     n = sizes[0]
     m = ice.ContactMatrix.synthetic(sizes, **kw)
+    assert m.info()["upper"] == upper
     b1, b2, c = m.export_upper()
     want = np.bincount(b1, weights=c, minlength=n) + np.bincount(b2, weights=c, minlength=n)
     _lib.call("hh_tune", b"uband", mode)
