@@ -83,10 +83,19 @@ def config(name, nnz=None):
     elif name == "c1":
         sizes = [5000]
         target, tf, label = nnz or 2e6, 0.0, "single-chrom-40kb-5000-bins"
+    elif name == "cis":
+        # `cooler balance --cis-only` on the 10 kb file (matrixBuilding.py:713,
+        # :1542, :1766): hg19 haploid, every chromosome its own ICE group, at
+        # C2's per-chromosome density (chr1: 5e7 pixels) -> 6.1e8 cis pixels
+        sizes = synth.genome_bins(10000)
+        target, tf, label = nnz or 6.1e8, 0.0, "hg19-10kb-haploid-cisonly"
     else:
         raise SystemExit(f"unknown config {name}")
     A, td = synth.calibrate(sizes, target, tf)
-    return sizes, dict(A=A, trans_density=td, comp_block=200, seed=20201015), label, target, tf
+    kw = dict(A=A, trans_density=td, comp_block=200, seed=20201015)
+    if name == "cis":
+        kw["cis_only"] = True
+    return sizes, kw, label, target, tf
 
 
 SWEEP_KERNELS = ("k_sweep_tiled", "k_sweep_flat", "k_sweep_band", "k_sweep_uband")  # symmetric band: <8> once, <4> twice per sweep; upper band: <8>, <4> once each
@@ -1193,7 +1202,7 @@ def main():
     rc, ru = ice.synth_row_counts(sizes, **kw)
     rank_rows = dist.partition_rows(rc, world)
     m = ice.ContactMatrix.synthetic(sizes, row_range=(rank_rows[rank], rank_rows[rank + 1]), **kw)
-    opts = ice.IceOptions(tol=0.0, max_iters=1 << 30)
+    opts = ice.IceOptions(tol=0.0, max_iters=1 << 30, cis_only=bool(kw.get("cis_only")))
     st = ice.IceState(m, opts)
     stream = torch.cuda.current_stream().cuda_stream
     if world > 1:
@@ -1322,6 +1331,10 @@ def main():
                                           "genome-wide at 10 kb, matrixBuilding.py:1536-1538; trans fraction 0.6: "
                                           "it has only 2.36e9 cis pairs, so 5e9 pixels need >= 53 % trans"}
                           if args.config == "c4h" else {}),
+                       **({"config_note": "cooler balance --cis-only (matrixBuilding.py:713): every chromosome "
+                                          "its own ICE group in one matrix, all iterated (tol 0), one launch "
+                                          "chain per iteration for the whole genome", "cis_only": True}
+                          if args.config == "cis" else {}),
                        "trans_fraction_target": tf, "resolution_bp": 40000 if args.config in ("c1", "c3") else 10000,
                        "parallelism": f"rows sharded x{world} (measured-cost partition), {'RCCL' if backend == 'nccl' else backend} all-gather of marginals, loop in {'C++ (hh_ice_run_sharded)' if dist_impl == 'capi' else 'Python'}" if world > 1
                        else "single GPU", "generate_s": round(gen_s, 2),

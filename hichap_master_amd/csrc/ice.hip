@@ -642,17 +642,19 @@ __device__ __forceinline__ void stage_bias(double* __restrict__ bl, const double
 
 // LDS of the three sweep bodies (one kernel each, or all three in one launch
 // for small matrices: k_sweep_all, a union of the three)
+template <bool UP>
 struct TiledLds {
     double bl[kW];
-    u64 cacc[kW];         // column side of the current upper tile (rotated image)
+    u64 cacc[UP ? kW : 1];  // column side of the current upper tile (rotated image)
     double acc2[2 * kR];  // narrow rows, then wide rows
     uint32_t rps[kR + 1], rpsn[kR + 1];
     uint16_t perm[2 * kR];
     uint16_t band[2 * kBandSlots];
 };
+template <bool UP>
 struct FlatLds {
     double bl[kW];
-    u64 cacc[kW];
+    u64 cacc[UP ? kW : 1];
     double acc[kR];    // row sums (narrow + wide)
     double accc[kR];   // narrow sums by compact row
     uint16_t rec[kFrecU4 * 8];
@@ -672,7 +674,7 @@ __device__ __forceinline__ void flush_cols(u64* __restrict__ cacc, u64* __restri
 template <int NB, int ABL, bool UP>
 __device__ __forceinline__ void sweep_tiled_unit(const TileDev& T, const uint8_t* __restrict__ act, int u,
                                                  const double* __restrict__ b, long long n_bins,
-                                                 double* __restrict__ part, TiledLds& L) {
+                                                 double* __restrict__ part, TiledLds<UP>& L) {
     double* __restrict__ bl = L.bl;
     double* __restrict__ acc2 = L.acc2;
     uint32_t* __restrict__ rps = L.rps;
@@ -755,7 +757,7 @@ template <int NB, int ABL, bool UP>
 __global__ __launch_bounds__(kSweepThreads, 4) void k_sweep_tiled(TileDev T, const uint8_t* __restrict__ act,
                                                                 int n_list, const double* __restrict__ b,
                                                                 long long n_bins, double* __restrict__ part) {
-    __shared__ __attribute__((aligned(16))) TiledLds L;
+    __shared__ __attribute__((aligned(16))) TiledLds<UP> L;
     if ((int)blockIdx.x >= n_list) return;
     sweep_tiled_unit<NB, ABL, UP>(T, act, T.u_order[blockIdx.x], b, n_bins, part, L);  // tiled units lead the list
 }
@@ -771,7 +773,7 @@ __global__ __launch_bounds__(kSweepThreads, 4) void k_sweep_tiled(TileDev T, con
 template <int U, int ABL, bool UP>
 __device__ __forceinline__ void sweep_flat_unit(const TileDev& T, const uint8_t* __restrict__ act, int u,
                                                 const double* __restrict__ b, long long n_bins,
-                                                double* __restrict__ part, FlatLds& L) {
+                                                double* __restrict__ part, FlatLds<UP>& L) {
     static_assert(kSweepWaves == kFlatWaves, "one plan split per wave");
     constexpr int UW = 2;  // wide runs: few wide entries in flat tiles
     double* __restrict__ bl = L.bl;
@@ -868,7 +870,7 @@ __global__ __launch_bounds__(kSweepThreads, 4) void k_sweep_flat(TileDev T, cons
                                                                int n_list, int list_off,
                                                                const double* __restrict__ b, long long n_bins,
                                                                double* __restrict__ part) {
-    __shared__ __attribute__((aligned(16))) FlatLds L;
+    __shared__ __attribute__((aligned(16))) FlatLds<UP> L;
     if ((int)blockIdx.x >= n_list) return;
     sweep_flat_unit<U, ABL, UP>(T, act, T.u_order[list_off + blockIdx.x], b, n_bins, part, L);
 }
@@ -885,10 +887,10 @@ __global__ __launch_bounds__(kSweepThreads, 4) void k_sweep_flat(TileDev T, cons
 // tile the walk is the round-2 one with the whole tile as the wave's range,
 // so a row's sum is a fixed function of the tile: deterministic, and the
 // same wherever the tile is swept.
-template <int NW>
+template <int NW, bool UP>
 struct FlatWLds {
     double bl[kW];
-    u64 cacc[kW];  // the group's column side (its strictly upper tiles), one slot per group
+    u64 cacc[UP ? kW : 1];  // the group's column side (its strictly upper tiles), one slot per group
     uint16_t rec[NW][kFrecU4 * 8];
     double acc[NW][kR];
     int next;
@@ -909,7 +911,7 @@ __global__ __launch_bounds__(NW * 64, NW > 8 ? 3 : 2) void k_sweep_flatw(TileDev
                                                                        const double* __restrict__ b, long long n_bins,
                                                                        double* __restrict__ part) {
     constexpr int UW = 2;
-    __shared__ __attribute__((aligned(16))) FlatWLds<NW> L;
+    __shared__ __attribute__((aligned(16))) FlatWLds<NW, UP> L;
     const int k0 = T.fg_ptr[blockIdx.x], nk = T.fg_ptr[blockIdx.x + 1] - k0;
     {
         bool on = false;  // block-uniform: any active tile in the group
@@ -1739,8 +1741,8 @@ __global__ __launch_bounds__(kSweepThreads, 4) void k_sweep_all(TileDev T, const
                                                               double* __restrict__ bpart,
                                                               unsigned long long* __restrict__ trace) {
     __shared__ __attribute__((aligned(16))) union Lds {
-        TiledLds t;
-        FlatLds f;
+        TiledLds<UP> t;
+        FlatLds<UP> f;
         BandLds<64> band;
     } L;
     // grid: [tiled units | band blocks (n_band = band_rb x chunks) | flat units]
@@ -2145,7 +2147,10 @@ __global__ __launch_bounds__(kR) void k_update_big(TileArgs ta, const uint8_t* _
     const long long row = ta.tile_lo[t] + threadIdx.x;
     const bool in = row < ta.tile_hi[t];
     if (cnt == 0.0) {  // no nonzero marginal: cooler sets the group's bias to NaN
-        if (in) bias[row] = __builtin_nan("");
+        // (0 until the finalize turns it into NaN: a NaN here would leak
+        // into the neighbouring chromosomes' rows through the dense bands'
+        // zero slots across the boundary, 0 * NaN)
+        if (in) bias[row] = 0.0;
         if (first && threadIdx.x == 0) {
             gs.empty[g] = 1;
             gs.var[g] = 0.0;
@@ -2193,8 +2198,8 @@ __global__ __launch_bounds__(kR) void k_update(TileArgs ta, const uint8_t* __res
         if (act[g] != 0) {
             const double cnt = ta.g_cnt[g], sum = ta.g_sum[g];
             double q = 0.0;
-            if (cnt == 0.0) {  // no nonzero marginal: cooler sets the group's bias to NaN
-                if (in) bias[row] = __builtin_nan("");
+            if (cnt == 0.0) {  // no nonzero marginal: cooler's NaN, as 0 until the finalize (k_update_big)
+                if (in) bias[row] = 0.0;
             } else if (in) {
                 const double mean = sum / cnt;
                 const double x = marg[row];
@@ -2402,17 +2407,19 @@ static void launch_sweep_up(const hh_matrix* m, const TileDev& T, const uint8_t*
                     : (g_flatw_pipe == 2 ? k_sweep_flatw<kFlatU, ABL, 2>
                        : g_flatw_pipe == 1 ? k_sweep_flatw<kFlatU, ABL, 1> : k_sweep_flatw<kFlatU, ABL, 0>);
         int nw = 8;
-        if (UP) {
+        if constexpr (UP) {
             // the column side's registers: 8 waves (2 per SIMD, 256 VGPRs; at
             // 11 waves the walk spills), or 11 with hh_tune flatw_waves_up
             nw = g_flatw_waves_up == 11 ? 11 : 8;
             kern = nw == 11 ? k_sweep_flatw<kFlatU, ABL, 2, 11, true> : k_sweep_flatw<kFlatU, ABL, 2, 8, true>;
-        } else if (g_flatw_waves == 10 && g_flatw_u != 16) {
-            kern = g_flatw_pipe == 2 ? k_sweep_flatw<kFlatU, ABL, 2, 10> : k_sweep_flatw<kFlatU, ABL, 0, 10>;
-            nw = 10;
-        } else if (g_flatw_waves == 11 && g_flatw_u != 16) {
-            kern = g_flatw_pipe == 2 ? k_sweep_flatw<kFlatU, ABL, 2, 11> : k_sweep_flatw<kFlatU, ABL, 0, 11>;
-            nw = 11;
+        } else {
+            if (g_flatw_waves == 10 && g_flatw_u != 16) {
+                kern = g_flatw_pipe == 2 ? k_sweep_flatw<kFlatU, ABL, 2, 10> : k_sweep_flatw<kFlatU, ABL, 0, 10>;
+                nw = 10;
+            } else if (g_flatw_waves == 11 && g_flatw_u != 16) {
+                kern = g_flatw_pipe == 2 ? k_sweep_flatw<kFlatU, ABL, 2, 11> : k_sweep_flatw<kFlatU, ABL, 0, 11>;
+                nw = 11;
+            }
         }
         hipLaunchKernelGGL(kern, dim3((unsigned)m->n_fgroups), dim3(64 * nw), 0, s, T, act, b,
                            (long long)m->n_bins, part);
@@ -2425,8 +2432,10 @@ static void launch_sweep_up(const hh_matrix* m, const TileDev& T, const uint8_t*
 template <int NB, int ABL>
 static void launch_sweep(const hh_matrix* m, const TileDev& T, const uint8_t* act, const double* b, double* part,
                          hipStream_t s, hipStream_t s_tiled) {
-    if (T.upper) launch_sweep_up<NB, ABL, true>(m, T, act, b, part, s, s_tiled);
-    else launch_sweep_up<NB, ABL, false>(m, T, act, b, part, s, s_tiled);
+    if constexpr (kUpperBuild) {
+        if (T.upper) return launch_sweep_up<NB, ABL, true>(m, T, act, b, part, s, s_tiled);
+    }
+    launch_sweep_up<NB, ABL, false>(m, T, act, b, part, s, s_tiled);
 }
 
 template <int ABL>
@@ -2605,13 +2614,15 @@ static void sweep_single(hh_ice* S, hipStream_t s) {
     HH_REQUIRE(grid < (1LL << 31), "sweep grid too large for one launch");
     unsigned long long* trace = grid <= g_trace_cap ? g_trace : nullptr;
     if (trace) g_trace_n = grid;
-    const bool up = m->upper && S->colpart.p;
-    auto kern = up ? (g_sweep_ablate == 1   ? k_sweep_all<2, kFlatU, 1, true>
-                      : g_sweep_ablate == 2 ? k_sweep_all<2, kFlatU, 2, true>
-                                            : k_sweep_all<2, kFlatU, 0, true>)
-                   : (g_sweep_ablate == 1   ? k_sweep_all<2, kFlatU, 1, false>
-                      : g_sweep_ablate == 2 ? k_sweep_all<2, kFlatU, 2, false>
-                                            : k_sweep_all<2, kFlatU, 0, false>);  // ablations: timing diagnostics only
+    auto kern = g_sweep_ablate == 1   ? k_sweep_all<2, kFlatU, 1, false>
+                : g_sweep_ablate == 2 ? k_sweep_all<2, kFlatU, 2, false>
+                                      : k_sweep_all<2, kFlatU, 0, false>;  // ablations: timing diagnostics only
+    if constexpr (kUpperBuild) {
+        if (m->upper && S->colpart.p)
+            kern = g_sweep_ablate == 1   ? k_sweep_all<2, kFlatU, 1, true>
+                   : g_sweep_ablate == 2 ? k_sweep_all<2, kFlatU, 2, true>
+                                         : k_sweep_all<2, kFlatU, 0, true>;
+    }
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kSweepThreads), 0, s, tdev(S), S->act(), n_tiled,
                        (int)n_band, segs, band_rb, (long long)S->nloc, (long long)m->row_lo, m->row_group.p,
                        S->bias.p, (long long)m->n_bins, S->part.p, S->bpart.p, trace);
@@ -2844,6 +2855,8 @@ int hh_tune(const char* key, int64_t value) {
             g_flatw_waves_up = (int)value;
         } else if (k == "upper_tiles") {
             HH_REQUIRE(value >= -1 && value <= 1, "upper_tiles in {-1 (auto), 0, 1}");
+            HH_REQUIRE(kUpperBuild || value != 1,
+                       "upper-triangle tiles need the 4096-column build (libhichap_hip_up.so, -DHH_KWBITS=12)");
             g_upper_tiles = value;
         } else if (k == "flat_max") {
             HH_REQUIRE(value >= 0 && value <= 255, "flat_max in [0, 255]");

@@ -29,12 +29,13 @@ namespace hh {
 
 constexpr int kR = 512;                 // rows per row-block
 #ifndef HH_KWBITS
-#define HH_KWBITS 12
+#define HH_KWBITS 13
 #endif
-// 4096-column tiles (round 5): a column-grouped block stages the tile's bias
-// slice (32 KB) AND the int64 column accumulator of the upper-triangle tiles
-// (32 KB) in LDS beside 11 waves' walk state
+// 8192-column tiles.  The upper-triangle tiles need the
+// 4096-column build (-DHH_KWBITS=12, libhichap_hip_up.so): their blocks
+// stage the bias slice AND an int64 column accumulator in LDS
 constexpr int kWBits = HH_KWBITS;
+constexpr bool kUpperBuild = HH_KWBITS <= 12;  // upper-triangle tiles available
 constexpr int kW = 1 << kWBits;         // columns per tile
 constexpr uint32_t kColMask = kW - 1;
 constexpr uint32_t kCntMax = 65535u;    // largest count stored in a tile (wide entry)

@@ -43,9 +43,13 @@ int64_t g_host_build = 0;    // hh_tune("host_build"): 1 = host builder for ever
 
 // upper-triangle tiles; off keeps both triangles in every tile
 int64_t g_upper_tiles = -1;
-// auto (-1): with the column-grouped flat sweep (the large matrices, whose
-// sweep is HBM-bound on the tile bytes); 1 forces them on (tests), 0 off
-bool upper_tiles_on(int32_t nJ) { return g_upper_tiles > 0 || (g_upper_tiles < 0 && flat_cols_on(nJ)); }
+// auto (-1): with the column-grouped flat sweep (the large matrices); 1
+// forces them on (tests), 0 off.  Only in the 4096-column build: measured
+// slower than both triangles in 8192-column tiles (the column side's LDS
+// atomics cost more than the bytes they save), so the default build has none
+bool upper_tiles_on(int32_t nJ) {
+    return kUpperBuild && (g_upper_tiles > 0 || (g_upper_tiles < 0 && flat_cols_on(nJ)));
+}
 int64_t g_band4 = 1;         // nibble band on
 double g_band4_density = 0.25;
 double g_band8_big = 0.05;

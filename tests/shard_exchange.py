@@ -82,3 +82,17 @@ def balance_states(states, rr, max_iters):
             if it % 8 == 7 and states[0].active_groups(s) == 0:
                 break
         return [st_.finalize(s) for st_ in states]
+
+
+def require_uptiles():
+    """Skip unless the loaded library has upper-triangle tiles (the 4096-column
+    build, libhichap_hip_up.so; tests/test_uptiles_variant_gpu.py runs these
+    cases against it in a child process)."""
+    import pytest
+    from hichap_master_amd._lib import HipLibraryError, call
+    try:
+        call("hh_tune", b"upper_tiles", 1)
+    except HipLibraryError:
+        pytest.skip("upper-triangle tiles: 4096-column build only (run by test_uptiles_variant_gpu.py)")
+    finally:
+        call("hh_tune", b"upper_tiles", -1)

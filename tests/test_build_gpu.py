@@ -51,8 +51,11 @@ def _genome(seed, sizes=(900, 700, 500), A=30.0, trans=0.01, big=False):
 
 @pytest.fixture
 def upper_tiles():
-    """upper-triangle tiles forced on; auto afterwards"""
+    """upper-triangle tiles forced on (the 4096-column build
+    only); auto afterwards"""
     from hichap_master_amd._lib import call
+    from tests.shard_exchange import require_uptiles
+    require_uptiles()
     call("hh_tune", b"upper_tiles", 1)
     yield
     call("hh_tune", b"upper_tiles", -1)
@@ -76,7 +79,7 @@ def test_device_build_equals_host_build(ice, ignore_diags, cis_only, big):
 
 
 @pytest.mark.parametrize("ignore_diags,cis_only,big", [(1, False, True), (2, True, False)])
-def test_device_build_equals_host_build_upper_tiles(ice, upper_tiles, ignore_diags, cis_only, big):
+def test_device_build_equals_host_build_uptiles(ice, upper_tiles, ignore_diags, cis_only, big):
     """The same with upper-triangle tiles: both builders keep an entry of a
     lower tile only as its mirror; weights bitwise equal, the oracle's within
     the ICE tolerance, and close to the both-triangle layout: the column

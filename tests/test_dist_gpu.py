@@ -106,7 +106,7 @@ def test_balance_sharded_two_processes(cis_only, impl):
 
 
 @pytest.mark.parametrize("impl", ["python", "capi"])
-def test_upper_tiles_two_processes(impl):
+def test_uptiles_two_processes(impl):
     """Upper-triangle tiles over two processes: the column side of each
     rank's strictly upper tiles reaches the other rank's rows through the
     int64 exchange (a torch.distributed reduce callback for the Python
@@ -115,7 +115,9 @@ def test_upper_tiles_two_processes(impl):
     import torch.multiprocessing as mp
     from hichap_master_amd import _lib, ice
     from oracle import ice_ref
+    from tests.shard_exchange import require_uptiles
     _lib.require_gpu()
+    require_uptiles()
     rng = np.random.default_rng(23)
     case = synth.coo_genome([5000, 4000, 700], rng, A=8.0, trans_density=0.002)
     b1, b2, c, off = case

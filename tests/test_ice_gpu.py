@@ -105,6 +105,25 @@ def test_empty_chromosome_cis_only(ice):
     assert np.isnan(st["scale"][1]) and np.isnan(sr["scale"][1])
 
 
+def test_cis_only_empty_group_between_active_ones(ice):
+    """--cis-only with a chromosome whose bins all fail the filters between
+    two active ones: cooler gives it NaN weights at its first iteration; that
+    NaN must not reach the neighbours' rows through the dense bands' zero
+    slots across the chromosome boundaries (it once did: 0 * NaN)."""
+    b1, b2, c, off = _case(9, sizes=(500, 300, 400), A=40.0, trans=0.0)
+    chrom = np.repeat(np.arange(3), np.diff(off))
+    mid = chrom[b1] == 1
+    keep = ~mid | (np.arange(b1.size) % 97 == 0)  # a few pixels: every bin < min_nnz
+    b1, b2, c = b1[keep], b2[keep], c[keep]
+    n = int(off[-1])
+    w, st = ice.balance(b1, b2, c, n, off, cis_only=True, max_iters=300)
+    wr, sr = ice_ref.balance(b1, b2, c, n, off, cis_only=True, max_iters=300)
+    assert np.isnan(w[500:800]).all() and np.isfinite(w[:500]).any() and np.isfinite(w[800:]).any()
+    np.testing.assert_array_equal(np.isnan(w), np.isnan(wr))
+    np.testing.assert_allclose(w, wr, rtol=1e-9, equal_nan=True)
+    np.testing.assert_array_equal(st["iters"], sr["iters"])
+
+
 def test_invalid_counts_rejected(ice):
     from hichap_master_amd._lib import HipLibraryError
     with pytest.raises(HipLibraryError):
@@ -269,7 +288,7 @@ def test_dense_band_widths(ice, band_w, band4):
     np.testing.assert_allclose(w, w_ref, rtol=1e-9, equal_nan=True)
 
 
-@pytest.mark.parametrize("upper", [0, 1])
+@pytest.mark.parametrize("upper", [0, 1], ids=["both", "uptiles"])
 @pytest.mark.parametrize("flat_max,flat_cols", [(0, -1), (2, -1), (24, -1), (255, -1), (24, 1), (255, 1)])
 def test_flat_tiles(ice, flat_max, flat_cols, upper):
     """Tiles whose rows are all short go to the flat (merge-path) sweep kernel;
@@ -278,6 +297,9 @@ def test_flat_tiles(ice, flat_max, flat_cols, upper):
     triangles in every tile, and with upper-triangle tiles (the column side in
     fixed point, exchanged between the shards as int64)."""
     from hichap_master_amd import _lib
+    if upper:
+        from tests.shard_exchange import require_uptiles
+        require_uptiles()
     b1, b2, c, off = _case(41, sizes=(9000, 7000, 600), A=3.0, trans=0.0005)
     n = int(off[-1])
     _lib.call("hh_tune", b"flat_max", flat_max)
@@ -306,13 +328,16 @@ def test_flat_tiles(ice, flat_max, flat_cols, upper):
     assert sts["iters"] == st["iters"]
 
 
-@pytest.mark.parametrize("upper", [0, 1])
+@pytest.mark.parametrize("upper", [0, 1], ids=["both", "uptiles"])
 def test_flat_block_shapes_bitwise(ice, upper):
     """The column-grouped flat kernel's block width (waves sharing one staged
     b[J]) and group size (a build knob) change only who sweeps a flat tile,
     not its per-row partials (nor, with upper-triangle tiles, its exact
     fixed-point column partials): bitwise the same weights."""
     from hichap_master_amd import _lib
+    if upper:
+        from tests.shard_exchange import require_uptiles
+        require_uptiles()
     b1, b2, c, off = _case(41, sizes=(9000, 7000, 600), A=3.0, trans=0.0005)
     n = int(off[-1])
     res = []

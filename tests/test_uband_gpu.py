@@ -21,8 +21,11 @@ def ice():
 
 def _upper(on):
     """upper-triangle tiles forced on / off (these matrices
-    are below the automatic threshold)"""
+    are below the automatic threshold); on: only in the 4096-column build"""
     from hichap_master_amd import _lib
+    if on:
+        from tests.shard_exchange import require_uptiles
+        require_uptiles()
     _lib.call("hh_tune", b"upper_tiles", 1 if on else 0)
 
 
@@ -85,8 +88,9 @@ _CHROM = [14637]
 _GENOME = [9036, 8120]
 
 
+@pytest.mark.parametrize("upper", [0, 1], ids=["both", "uptiles"])
 @pytest.mark.parametrize("spec", [_CHROM, _GENOME], ids=["chrom", "genome"])
-def test_uband_matches_symmetric_sweep(ice, spec):
+def test_uband_matches_symmetric_sweep(ice, spec, upper):
     sizes, kw = _model(spec)
     m = ice.ContactMatrix.synthetic(sizes, **kw)
     inf = m.info()
@@ -99,6 +103,8 @@ def test_uband_matches_symmetric_sweep(ice, spec):
     w1, s1 = _balance_synth(ice, sizes, kw, opts)
     assert s1["iters"] == s0["iters"]
     np.testing.assert_allclose(w1, w0, rtol=1e-12, equal_nan=True)
+    if not upper:
+        return
     _upper(True)  # + upper-triangle tiles: the tiles' column side in fixed point
     w2, s2 = _balance_synth(ice, sizes, kw, opts)
     assert s2["iters"] == s0["iters"]
@@ -122,7 +128,7 @@ def test_uband_matches_oracle(ice):
     np.testing.assert_allclose(w, w_ref, rtol=1e-9, equal_nan=True)
 
 
-@pytest.mark.parametrize("upper", [0, 1])
+@pytest.mark.parametrize("upper", [0, 1], ids=["both", "uptiles"])
 @pytest.mark.parametrize("cuts", [[0, 4096, 14637], [0, 512, 3584, 6144, 14637], [0, 2560, 5120, 7680, 14637]])
 def test_uband_shards_bitwise(ice, cuts, upper):
     """Row shards (512-row aligned, workgroup-unaligned, shorter than the band)
@@ -139,7 +145,7 @@ def test_uband_shards_bitwise(ice, cuts, upper):
     assert s["iters"] == s_full["iters"]
 
 
-@pytest.mark.parametrize("upper", [0, 1])
+@pytest.mark.parametrize("upper", [0, 1], ids=["both", "uptiles"])
 def test_uband_shards_bitwise_genome_cis_only(ice, upper):
     _upper(upper)
     sizes, kw = _model(_GENOME)
@@ -151,7 +157,7 @@ def test_uband_shards_bitwise_genome_cis_only(ice, upper):
     np.testing.assert_array_equal(s["iters"], s_full["iters"])  # per chromosome
 
 
-@pytest.mark.parametrize("upper", [0, 1], ids=["both_triangles", "upper_tiles"])
+@pytest.mark.parametrize("upper", [0, 1], ids=["both", "uptiles"])
 @pytest.mark.parametrize("mode", [0, 2], ids=["symmetric", "upper"])
 def test_one_sweep_row_sums_equal_export(ice, mode, upper):
     """b = 1: one sweep's marginals are the row sums of the exported table,
