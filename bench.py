@@ -1089,6 +1089,102 @@ def run_twostep(args, world, rank, local):
         print(json.dumps(out), flush=True)
 
 
+def _dense_pair_device(N, gen, rng, A=60.0, drop_rows=0):
+    """synth.dense_chrom + synth.haplotype_pair on the device (torch Poisson /
+    binomial draws; the bin profile from synth.bin_profile): T, M, P as int64
+    N x N device tensors."""
+    import torch
+    from hichap_master_amd import synth
+    s, v, _ = synth.bin_profile(N, rng, 0.02, (5, 15))
+    s = torch.from_numpy(np.asarray(s, np.float64)).cuda()
+    v = torch.from_numpy(np.asarray(v, np.float64)).cuda()
+    i = torch.arange(N, device="cuda", dtype=torch.float64)
+    lam = A * ((i[:, None] - i[None, :]).abs() + 1.0) ** -1.08
+    lam *= (1.0 + 0.3 * s[:, None] * s[None, :]) * v[:, None] * v[None, :]
+    up = torch.poisson(torch.triu(lam), generator=gen)
+    del lam
+    TM = torch.triu(up) + torch.triu(up, 1).T
+    del up
+    base = torch.binomial(TM, torch.full_like(TM, 0.4), generator=gen)
+    MM = torch.binomial(base, torch.full_like(base, 0.5), generator=gen)
+    PM = base - MM
+    del base
+    for X in (MM, PM):
+        X -= torch.binomial(torch.triu(X, 1), torch.full_like(X, 0.15), generator=gen)
+        if drop_rows:
+            rows = torch.from_numpy(rng.choice(N, size=drop_rows, replace=False)).cuda()
+            X[rows, :] = torch.binomial(X[rows, :], torch.full_like(X[rows, :], 0.02), generator=gen)
+            X[:, rows] = torch.binomial(X[:, rows], torch.full_like(X[:, rows], 0.02), generator=gen)
+    return tuple(X.to(torch.int64).contiguous() for X in (TM, MM, PM))
+
+
+def run_twostep_genome(args, world, rank, local):
+    """IntraChromMatrixCorrection (matrixBuilding.py:1026-1041, :1607-1614)
+    over a whole localRes set: hg19 chromosomes 1-22 + X at 40 kb (HiCHap's
+    default chroms ['#', 'X'] and localRes), synthetic T / imputed M, P on the
+    device.  A step = every chromosome's two-step correction in one
+    hh_twostep_batch call (chains on 4 streams, largest first).  Also timed:
+    the same chromosomes one TwoStepCorrection call after the other."""
+    import torch
+    from hichap_master_amd import matrixBuilding as mb, synth
+    names = [str(c) for c in range(1, 23)] + ["X"]
+    Ns = synth.chrom_bins([synth.HG19[c] for c in names], 40000)
+    gen = torch.Generator(device="cuda").manual_seed(20201025)
+    rng = np.random.default_rng(20201025)
+    tra, hap = {}, {}
+    for c, N in zip(names, Ns):
+        T, M, P = _dense_pair_device(int(N), gen, rng, drop_rows=max(1, int(N) // 50))
+        tra[c], hap["M" + c], hap["P" + c] = T, M, P
+    torch.cuda.synchronize()
+    for _ in range(args.warmup):
+        mb.IntraChromMatrixCorrection(tra, hap)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = mb.IntraChromMatrixCorrection(tra, hap)
+        del out
+    torch.cuda.synchronize()
+    step = (time.perf_counter() - t0) / args.steps
+    # one chromosome after the other (the per-call path)
+    ks = max(1, min(3, args.steps))
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(ks):
+        for c in names:
+            mb.TwoStepCorrection(tra[c], hap["M" + c], hap["P" + c])
+    torch.cuda.synchronize()
+    seq = (time.perf_counter() - t1) / ks
+    sq = float(sum(int(N) ** 2 for N in Ns))
+    alg = 40.0 * sq  # SURVEY 8(d): 3 int64 reads + 2 fp64 writes per element
+    if rank == 0:
+        out = {"metric": "IntraChromMatrixCorrection (TwoStepCorrection per chromosome), hg19 1-22 + X at 40 kb",
+               "value": 1.0 / step, "unit": "genomes/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+               "ms_per_step": 1000.0 * step, "higher_is_better": True, "scaling": "replicas", "vs_baseline": None,
+               "dtype": "int64 in, f64 out", "data": "synthetic (device Poisson / binomial draws, synth model)",
+               "config": {"workload": "twostep-hg19-40kb-genome", "chromosomes": len(names),
+                          "bins": int(sum(int(N) for N in Ns)), "sum_N2": sq, "streams": mb.TWOSTEP_STREAMS},
+               "roofline": {"bound": "hbm", "kernel": "hh_twostep_batch (per chromosome: k_rowstats x3, device glue, "
+                                                       "two streaming symmetrisation chains)",
+                            "achieved": alg / step / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                            "frac": alg / step / 1e9 / PEAK_HBM_GBS, "traffic": None, "alg_bytes_per_launch": alg,
+                            "note": "40 B per matrix element (3 int64 reads + 2 fp64 writes), the whole genome per step"},
+               "sequential_ms": 1000.0 * seq,
+               "note": "sequential_ms: the same 23 chromosomes as one TwoStepCorrection call each"}
+        if not args.no_cpu:
+            from oracle import hichap_ref
+            k = names.index("21")
+            T, M, P = (X.cpu().numpy() for X in (tra["21"], hap["M21"], hap["P21"]))
+            t = time.perf_counter()
+            hichap_ref.two_step_correction(T, M, P)
+            dt = time.perf_counter() - t
+            est = dt * sq / float(int(Ns[k]) ** 2)
+            out["cpu_baseline"] = with_host({"value": 1.0 / est, "unit": "genomes/s (extrapolated by sum N^2)",
+                                             "cores": 1, "kind": "port",
+                                             "sample": f"oracle/hichap_ref.two_step_correction (vectorised NumPy) on "
+                                                       f"chr21 (N = {int(Ns[k])}): {dt:.3f} s, x sum N^2 / N21^2"})
+        print(json.dumps(out), flush=True)
+
+
 def _free_port():
     import socket
     with socket.socket() as s:
@@ -1190,9 +1286,10 @@ def main():
         else:
             tdist.init_process_group(backend)
 
-    if args.config in ("c5", "pairs", "loops", "dropin", "e2e", "gw", "twostep"):
+    if args.config in ("c5", "pairs", "loops", "dropin", "e2e", "gw", "twostep", "twostep_genome"):
         {"c5": run_c5, "pairs": run_pairs, "loops": run_loops, "dropin": run_dropin,
-         "e2e": run_e2e, "gw": run_gw, "twostep": run_twostep}[args.config](args, world, rank, local)
+         "e2e": run_e2e, "gw": run_gw, "twostep": run_twostep,
+         "twostep_genome": run_twostep_genome}[args.config](args, world, rank, local)
         if torch.distributed.is_initialized():
             torch.distributed.destroy_process_group()
         return

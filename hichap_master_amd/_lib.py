@@ -107,6 +107,7 @@ SIGNATURES = {
     "hh_dense_rowstats": (C.c_int, [P, I32, I64, P, P, P, P, I32, P]),
     "hh_dense_symvc": (C.c_int, [P, I32, I64, P, P, F64, F64, P, I32, P]),
     "hh_twostep": (C.c_int, [P, P, P, I64, P, P, P, P, I32, P]),
+    "hh_twostep_batch": (C.c_int, [I32, P, P, P, P, P, P, P, P, I32, P]),
     "hh_dense_from_cells": (C.c_int, [P, P, P, I64, I64, I64, I32, I32, P, P]),
     "hh_dense_upper_count": (C.c_int, [P, I64, PI64, P]),
     "hh_dense_upper_write": (C.c_int, [P, I64, P, P, P, P]),

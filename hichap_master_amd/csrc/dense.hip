@@ -1420,6 +1420,121 @@ int hh_twostep(const int64_t* TM, const int64_t* MM, const int64_t* PM, int64_t 
     });
 }
 
+// IntraChromMatrixCorrection (matrixBuilding.py:1026-1041) over a whole
+// localRes set: every chromosome's chain (row statistics, the device glue, the
+// two symmetrisation chains) enqueued at once, chromosomes largest first dealt
+// to the least-loaded of n_streams streams (by N^2), one synchronisation at
+// the end.  The small chromosomes' latency-bound launches run beside the big
+// ones' streaming passes instead of after them.  Per chromosome the same
+// kernels in the same order as hh_twostep: bitwise the same results.
+namespace {
+struct TsWork {
+    DBuf<double> dsum, dA, draw;
+    DBuf<long long> dz, dng;
+    DBuf<uint8_t> dgf;
+    DBuf<int> dgpos, dglist;
+    SymvcWs wm, wp;
+};
+std::vector<hipStream_t>& ts_streams(int k) {
+    static std::vector<hipStream_t> v;
+    while ((int)v.size() < k) {
+        hipStream_t s;
+        HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        v.push_back(s);
+    }
+    return v;
+}
+}  // namespace
+
+int hh_twostep_batch(int32_t n, const int64_t* const* TM, const int64_t* const* MM, const int64_t* const* PM,
+                     const int64_t* N, double* const* nor_mm, double* const* nor_pm, uint8_t* gap_m,
+                     uint8_t* gap_p, int32_t n_streams, void* stream) {
+    return guard([&] {
+        HH_REQUIRE(n >= 0 && (n == 0 || (TM && MM && PM && N && nor_mm && nor_pm && gap_m && gap_p)), "bad arguments");
+        HH_REQUIRE(n_streams >= 1 && n_streams <= 16, "n_streams in [1, 16]");
+        HH_REQUIRE(g_symvc_stream && g_twostep_devglue, "hh_twostep_batch needs the streaming device-glue chain");
+        if (n == 0) return;
+        std::vector<int64_t> goff((size_t)n + 1, 0);
+        for (int c = 0; c < n; ++c) {
+            HH_REQUIRE(TM[c] && MM[c] && PM[c] && nor_mm[c] && nor_pm[c] && N[c] > 0, "bad chromosome arguments");
+            goff[c + 1] = goff[c] + N[c];
+        }
+        hipStream_t s0 = as_stream(stream);
+        std::vector<int> order(n);
+        for (int c = 0; c < n; ++c) order[c] = c;
+        std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return N[a] > N[b]; });
+        const int K = std::min(n_streams, n);
+        std::vector<hipStream_t>& ss = ts_streams(K);
+        std::vector<double> load(K, 0.0);
+        std::vector<int> sid(n);
+        for (int c : order) {  // LPT on N^2 (the streaming passes' bytes)
+            const int k = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+            sid[c] = k;
+            load[k] += (double)N[c] * (double)N[c];
+        }
+        // every buffer before the first launch (the pool hands out nothing
+        // a launched chain still uses), the error flags zeroed on s0
+        std::vector<TsWork> w((size_t)n);
+        DBuf<int> derr((size_t)n);
+        HIP_CHECK(hipMemsetAsync(derr.p, 0, sizeof(int) * n, s0));
+        for (int c = 0; c < n; ++c) {
+            const size_t Nc = (size_t)N[c];
+            w[c].dsum.alloc(3 * Nc);
+            w[c].dz.alloc(3 * Nc);
+            w[c].dgf.alloc(2 * Nc);
+            w[c].dgpos.alloc(2 * Nc);
+            w[c].dglist.alloc(2 * Nc);
+            w[c].dng.alloc(2);
+            w[c].dA.alloc(Nc);
+            w[c].draw.alloc(2);
+        }
+        hipEvent_t fork;
+        HIP_CHECK(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
+        HIP_CHECK(hipEventRecord(fork, s0));
+        for (int k = 0; k < K; ++k) HIP_CHECK(hipStreamWaitEvent(ss[k], fork, 0));
+        const size_t gbytes = (size_t)2 * goff[n], ebytes = (size_t)n * sizeof(int);
+        char* dl = (char*)pinned_stage().get(0, ((gbytes + 15) & ~(size_t)15) + ebytes);
+        int* herr = (int*)(dl + ((gbytes + 15) & ~(size_t)15));
+        for (int c : order) {
+            hipStream_t s = ss[sid[c]];
+            TsWork& x = w[c];
+            const long long Nc = N[c];
+            const long long* d[3] = {(const long long*)TM[c], (const long long*)MM[c], (const long long*)PM[c]};
+            for (int k = 0; k < 3; ++k)
+                hipLaunchKernelGGL((k_rowstats<long long>), dim3((unsigned)Nc), dim3(256), 0, s, d[k], Nc,
+                                   (const long long*)nullptr, (const long long*)nullptr, x.dsum.p + k * Nc,
+                                   x.dz.p + k * Nc);
+            hipLaunchKernelGGL(k_ts_gapdef, dim3(2), dim3(1024), 0, s, (const long long*)x.dz.p, Nc, x.dgf.p,
+                               x.dgpos.p, x.dglist.p, x.dng.p, derr.p + c);
+            hipLaunchKernelGGL(k_ts_alpha, dim3(1), dim3(1024), 0, s, (const double*)x.dsum.p,
+                               (const uint8_t*)x.dgf.p, Nc, x.dA.p, x.draw.p, derr.p + c);
+            HIP_CHECK(hipGetLastError());
+            const GapIdx gim{x.dgpos.p, x.dglist.p, x.dng.p, Nc}, gip{x.dgpos.p + Nc, x.dglist.p + Nc, x.dng.p + 1, Nc};
+            symvc_enqueue(d[1], Nc, x.dA.p, x.dgf.p, gim, 2.0 / 3.0, 0.0, x.draw.p, nor_mm[c], s, x.wm,
+                          x.dsum.p + Nc);
+            symvc_enqueue(d[2], Nc, x.dA.p, x.dgf.p + Nc, gip, 2.0 / 3.0, 0.0, x.draw.p + 1, nor_pm[c], s, x.wp,
+                          x.dsum.p + 2 * Nc);
+            HIP_CHECK(hipMemcpyAsync(dl + 2 * goff[c], x.dgf.p, (size_t)2 * Nc, hipMemcpyDeviceToHost, s));
+        }
+        for (int k = 0; k < K; ++k) {
+            hipEvent_t j;
+            HIP_CHECK(hipEventCreateWithFlags(&j, hipEventDisableTiming));
+            HIP_CHECK(hipEventRecord(j, ss[k]));
+            HIP_CHECK(hipStreamWaitEvent(s0, j, 0));
+            HIP_CHECK(hipEventDestroy(j));
+        }
+        HIP_CHECK(hipEventDestroy(fork));
+        derr.download(herr, (size_t)n, s0);
+        HIP_CHECK(hipStreamSynchronize(s0));
+        for (int c = 0; c < n; ++c) {
+            HH_REQUIRE(!(herr[c] & 1), "percentile of an empty array (chromosome " + std::to_string(c) + ")");
+            HH_REQUIRE(!(herr[c] & 2), "every bin is a gap (chromosome " + std::to_string(c) + ")");
+            std::memcpy(gap_m + goff[c], dl + 2 * goff[c], (size_t)N[c]);
+            std::memcpy(gap_p + goff[c], dl + 2 * goff[c] + N[c], (size_t)N[c]);
+        }
+    });
+}
+
 int hh_dense_from_cells(const int64_t* row, const int64_t* col, const int64_t* count, int64_t nnz, int64_t N,
                         int64_t offset, int32_t symmetric, int32_t on_device, int64_t* out, void* stream) {
     return guard([&] {

@@ -205,8 +205,17 @@ def TwoStepCorrectionPixels(N, T_pixels, MM_cells, PM_cells, offset=0, output="u
     return res[0], res[1], gm, gp
 
 
-def IntraChromMatrixCorrection(Tra_Lib, Hap_Lib):
-    """Per-chromosome TwoStepCorrection (matrixBuilding.py:1026-1041)."""
+TWOSTEP_STREAMS = 4  # hh_twostep_batch streams (the box's hardware queues per process)
+
+
+def IntraChromMatrixCorrection(Tra_Lib, Hap_Lib, n_streams=TWOSTEP_STREAMS, stream=None):
+    """Per-chromosome TwoStepCorrection (matrixBuilding.py:1026-1041).  With
+    device tensors, every chromosome in one ``hh_twostep_batch`` call (chains
+    on ``n_streams`` streams, largest first; outputs device tensors)."""
+    keys = list(Tra_Lib.keys())
+    mats = [(Tra_Lib[c], Hap_Lib["M" + c], Hap_Lib["P" + c]) for c in keys]
+    if mats and all(bool(getattr(X, "is_cuda", False)) for t in mats for X in t):
+        return _intra_batch_device(keys, mats, n_streams, stream)
     Nor_Lib, Gap_Lib = {}, {}
     for chro in Tra_Lib.keys():
         Nor_MM, Nor_PM, Gap_M, Gap_P = TwoStepCorrection(Tra_Lib[chro], Hap_Lib["M" + chro], Hap_Lib["P" + chro])
@@ -214,6 +223,34 @@ def IntraChromMatrixCorrection(Tra_Lib, Hap_Lib):
         Nor_Lib["P" + chro] = Nor_PM
         Gap_Lib["M" + chro] = Gap_M
         Gap_Lib["P" + chro] = Gap_P
+    return Nor_Lib, Gap_Lib
+
+
+def _intra_batch_device(keys, mats, n_streams, stream=None):
+    import torch
+    _lib.require_gpu()
+    Ns = []
+    for T, M, P in mats:
+        N = int(T.shape[0])
+        for X in (T, M, P):
+            if tuple(X.shape) != (N, N) or X.dtype != torch.int64 or not X.is_contiguous():
+                raise ValueError("TM, MM, PM must be contiguous int64 N x N device tensors")
+        Ns.append(N)
+    nm = [torch.empty((N, N), dtype=torch.float64, device=mats[0][0].device) for N in Ns]
+    npm = [torch.empty((N, N), dtype=torch.float64, device=mats[0][0].device) for N in Ns]
+    n = len(keys)
+    arr = lambda xs: (C.c_void_p * n)(*[C.c_void_p(x.data_ptr()) for x in xs])
+    Narr = np.asarray(Ns, dtype=np.int64)
+    gm = np.empty(int(Narr.sum()), np.uint8)
+    gp = np.empty(int(Narr.sum()), np.uint8)
+    call("hh_twostep_batch", n, arr([t[0] for t in mats]), arr([t[1] for t in mats]), arr([t[2] for t in mats]),
+         ptr(Narr), arr(nm), arr(npm), ptr(gm), ptr(gp), int(n_streams), stream)
+    off = np.concatenate([[0], np.cumsum(Narr)])
+    Nor_Lib, Gap_Lib = {}, {}
+    for k, c in enumerate(keys):
+        Nor_Lib["M" + c], Nor_Lib["P" + c] = nm[k], npm[k]
+        Gap_Lib["M" + c] = np.nonzero(gm[off[k]:off[k + 1]])[0].astype(np.int64)
+        Gap_Lib["P" + c] = np.nonzero(gp[off[k]:off[k + 1]])[0].astype(np.int64)
     return Nor_Lib, Gap_Lib
 
 

@@ -358,6 +358,15 @@ int hh_dense_upper_count(const double* X, int64_t N, int64_t* nnz, void* stream)
 int hh_dense_upper_write(const double* X, int64_t N, int32_t* bin1, int32_t* bin2, double* value, void* stream);
 int hh_twostep(const int64_t* TM, const int64_t* MM, const int64_t* PM, int64_t N, double* nor_mm, double* nor_pm,
                uint8_t* gap_m, uint8_t* gap_p, int32_t on_device, void* stream);
+/* IntraChromMatrixCorrection (matrixBuilding.py:1026-1041): hh_twostep over
+ * n chromosomes in one call, device pointers only (TM[c], MM[c], PM[c] int64
+ * N[c] x N[c]; nor_mm[c], nor_pm[c] fp64 outputs).  Chromosomes largest first
+ * on the least-loaded of n_streams (1..16) streams, one synchronisation at
+ * the end; per chromosome bitwise hh_twostep's results.  gap_m / gap_p (host)
+ * receive every chromosome's flags concatenated in argument order. */
+int hh_twostep_batch(int32_t n, const int64_t* const* TM, const int64_t* const* MM, const int64_t* const* PM,
+                     const int64_t* N, double* const* nor_mm, double* const* nor_pm, uint8_t* gap_m,
+                     uint8_t* gap_p, int32_t n_streams, void* stream);
 
 /* ------------------------------------ sparse genome-wide correction
  * GenomeWideMatrixCorrection (matrixBuilding.py:857-901) on pixel tables

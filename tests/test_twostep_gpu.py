@@ -249,3 +249,43 @@ def test_twostep_devglue_block_select_path_bitwise(mb):
             np.testing.assert_array_equal(a, b)
     gm = dev[2].cpu().numpy() if hasattr(dev[2], "cpu") else dev[2]
     assert 300 <= len(gm) < N  # the zeroed rows are gaps, most rows are not
+
+
+@pytest.mark.parametrize("n_streams", [1, 4])
+def test_intra_chrom_batch_equals_per_chromosome(mb, n_streams):
+    """IntraChromMatrixCorrection on device tensors: every chromosome in one
+    hh_twostep_batch call (chains on several streams, largest first) is
+    bitwise the per-chromosome hh_twostep, gaps included; one chromosome with
+    gap rows, one without, sizes from 37 to 2 100 bins."""
+    import torch
+    rng = np.random.default_rng(77)
+    tra, hap = {}, {}
+    for c, N, drop in (("1", 2100, 40), ("2", 1500, 0), ("3", 37, 0), ("X", 900, 12), ("4", 1200, 25)):
+        TM = synth.dense_chrom(N, rng, A=50.0)
+        MM, PM = synth.haplotype_pair(TM, rng, drop_rows=drop)
+        tra[c] = torch.from_numpy(TM).cuda()
+        hap["M" + c], hap["P" + c] = torch.from_numpy(MM).cuda(), torch.from_numpy(PM).cuda()
+    nor, gaps = mb.IntraChromMatrixCorrection(tra, hap, n_streams=n_streams)
+    assert set(nor) == {h + c for c in tra for h in "MP"}
+    for c in tra:
+        one = mb.TwoStepCorrection(tra[c], hap["M" + c], hap["P" + c])
+        assert torch.equal(nor["M" + c], one[0]) and torch.equal(nor["P" + c], one[1])
+        np.testing.assert_array_equal(gaps["M" + c], one[2])
+        np.testing.assert_array_equal(gaps["P" + c], one[3])
+    ref = hichap_ref.two_step_correction(tra["X"].cpu().numpy(), hap["MX"].cpu().numpy(), hap["PX"].cpu().numpy())
+    np.testing.assert_allclose(nor["MX"].cpu().numpy(), ref[0], rtol=1e-11)
+    np.testing.assert_array_equal(gaps["PX"], ref[3])
+
+
+def test_intra_chrom_batch_error_names_the_chromosome(mb):
+    import torch
+    from hichap_master_amd import _lib
+    rng = np.random.default_rng(3)
+    TM = synth.dense_chrom(300, rng, A=60.0)
+    MM, PM = synth.haplotype_pair(TM, rng)
+    d = lambda X: torch.from_numpy(np.ascontiguousarray(X)).cuda()
+    Z = np.zeros_like(TM)
+    tra = {"1": d(TM), "2": d(TM)}
+    hap = {"M1": d(MM), "P1": d(PM), "M2": d(Z), "P2": d(Z)}
+    with pytest.raises(_lib.HipLibraryError, match=r"percentile of an empty array \(chromosome 1\)"):
+        mb.IntraChromMatrixCorrection(tra, hap)
