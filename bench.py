@@ -1344,12 +1344,18 @@ def main():
         # filters (untimed), then warmup + timed iterations in one C++ loop each
         st.marg_local(0, None, stream); st.filter_nnz(stream)
         st.marg_local(1, None, stream); st.filter_count_mad(stream)
+        # the timed loop without per-sweep HIP events (their markers cost the
+        # small matrices' iterations microseconds); the sweep time for the
+        # roofline from a few more iterations with the events on, after it
+        _lib.call("hh_tune", b"iter_events", 0)
         st.run(args.warmup, stream)
         barrier()
         t_start = time.perf_counter()
         st.run(args.steps, stream)
         barrier()
         elapsed = time.perf_counter() - t_start
+        _lib.call("hh_tune", b"iter_events", 1)
+        st.run(max(1, min(args.steps, 5)), stream)
         sweep_ms, launches, iter_ms = st.last_timing()
     else:
         # the iteration loop in C++ (hh_ice_run_sharded) with the library's

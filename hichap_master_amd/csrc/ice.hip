@@ -2378,14 +2378,17 @@ static int g_band_lpt = 1;      // band chunks dispatched heaviest first (0: uin
 // upper-band sweep (K1d, round 3): read only the upper half of the bands, each
 // count feeding its row and its column.  0: the round-2 symmetric band kernels;
 // 1 (auto): the upper-band sweep when the WHOLE matrix's bands hold at least
-// g_uband_min_bytes (a wave walks 512 rows in sequence: on a single chromosome
-// that chain, not the bytes, sets the time -- C2 0.11 -> 0.54 ms per sweep);
-// 2: always.  Decided at hh_ice_create from the whole matrix, so every shard
-// of one matrix takes the same path.
+// g_uband_min_bytes (a wave walks its rows in sequence: on one small
+// chromosome that chain, not the bytes, sets the time -- C2's 0.06 GB of
+// bands); 2: always.  From 128 MB (round 5, was 1 GB): C3 (0.22 GB of bands)
+// 0.773 -> 0.717 ms per sweep, the 10 kb cis-only genome (0.78 GB) 0.69 ->
+// 0.56 ms (profiles/r5f, r5g).  Decided at hh_ice_create from the whole
+// matrix, so every shard of one matrix takes the same path.
 static int g_uband = 1;
-static int64_t g_uband_min_bytes = 1LL << 30;
+static int64_t g_uband_min_bytes = 128LL << 20;
 static int g_ub_xcd = 1;  // upper-band blocks dealt in contiguous ranges per XCD (k_sweep_ubands)
 static int g_sweep_single = -1;  // whole sweep in one launch: -1 auto (below g_single_max_bytes), 0 off, 1 on
+static int g_iter_events = 1;    // hh_ice_run: HIP events around every sweep (0: first / last only)
 static int64_t g_single_max_bytes = 1LL << 30;
 // diagnostic: per-block timeline of the last single-launch sweep (hh_sweep_trace)
 static unsigned long long* g_trace = nullptr;
@@ -2970,6 +2973,9 @@ int hh_tune(const char* key, int64_t value) {
             g_trace_cap = g_trace_n = 0;
             if (value) HIP_CHECK(hipMalloc(&g_trace, (size_t)value * 3 * sizeof(unsigned long long)));
             g_trace_cap = value;
+        } else if (k == "iter_events") {
+            HH_REQUIRE(value == 0 || value == 1, "iter_events in {0, 1}");
+            g_iter_events = (int)value;
         } else if (k == "sweep_single") {
             HH_REQUIRE(value >= -1 && value <= 1, "sweep_single in {-1 (auto), 0, 1}");
             g_sweep_single = (int)value;
@@ -3246,14 +3252,15 @@ int hh_ice_run(hh_ice* S, int32_t n, void* stream) {
             S->ev.push_back(e);
         }
         HIP_CHECK(hipEventRecord(S->ev[2 * n], s));
+        const bool ev = g_iter_events != 0;  // (0: no per-sweep events; sweep_ms then 0)
         for (int k = 0; k < n; ++k) {
-            marg_weighted(S, S->marg.p, s, true, k);
+            marg_weighted(S, S->marg.p, s, ev, k);
             update(S, s);
         }
         HIP_CHECK(hipEventRecord(S->ev[2 * n + 1], s));
         HIP_CHECK(hipStreamSynchronize(s));
         double tot = 0.0;
-        for (int k = 0; k < n; ++k) {
+        for (int k = 0; ev && k < n; ++k) {
             float ms = 0.f;
             HIP_CHECK(hipEventElapsedTime(&ms, S->ev[2 * k], S->ev[2 * k + 1]));
             tot += ms;

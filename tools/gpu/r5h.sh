@@ -1,14 +1,12 @@
 #!/bin/bash
-# uband rule for mid-size matrices (C3, C4 haploid, cis) and the TwoStep
-# genome line's kernel profile.   tools/gpu/r5g.sh outdir
+# TwoStep batch stream scaling; the new uband rule on C3 / cis.  tools/gpu/r5h.sh outdir
 cd "${GRAFT_REPO_ROOT:-/root/repo}" && R=$PWD && export TMPDIR=/tmp
 O=$R/gpurun_out/$1; mkdir -p $O
-for cfg in c3 c4h; do
-timeout -k 10 300 python3 -u tools/probe_knobs.py --config $cfg --iters 20 "uband=0" "uband=2" "uband=2,conc_ub_min_bytes=0" "uband=0,conc_min_bytes=0" > $O/${cfg}_knobs.log 2>&1 || { tail -20 $O/${cfg}_knobs.log; exit 1; }
-cat $O/${cfg}_knobs.log
-done
-bash tools/gpu/prof_line.sh $1 twostep_genome --steps 5 --warmup 1
-for cfg in c2 cis; do
+timeout -k 10 200 python3 -u tools/probe_twostep.py 1 2 4 8 16 > $O/ts_q4.log 2>&1 || { tail -20 $O/ts_q4.log; exit 1; }
+cat $O/ts_q4.log
+GPU_MAX_HW_QUEUES=16 timeout -k 10 200 python3 -u tools/probe_twostep.py 4 8 16 > $O/ts_q16.log 2>&1 || { tail -20 $O/ts_q16.log; exit 1; }
+cat $O/ts_q16.log
+for cfg in c3 cis c2; do
 timeout -k 10 300 python3 -u bench.py --config $cfg --no-cpu > $O/${cfg}_bench.log 2>&1 || { tail -20 $O/${cfg}_bench.log; exit 1; }
 grep '^{"metric"' $O/${cfg}_bench.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; print(d['config']['workload'], round(d['value'],1), round(d['ms_per_step'],4), 'sweep', round(r['sweep_ms_avg'],4), 'iter', round(r['iter_ms_avg'],4))"
 done
