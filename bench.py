@@ -1123,8 +1123,9 @@ def run_twostep_genome(args, world, rank, local):
     over a whole localRes set: hg19 chromosomes 1-22 + X at 40 kb (HiCHap's
     default chroms ['#', 'X'] and localRes), synthetic T / imputed M, P on the
     device.  A step = every chromosome's two-step correction in one
-    hh_twostep_batch call (chains on 4 streams, largest first).  Also timed:
-    the same chromosomes one TwoStepCorrection call after the other."""
+    hh_twostep_batch call (every pass of every chromosome in one shared
+    launch).  Also timed: the same chromosomes one TwoStepCorrection call
+    after the other."""
     import torch
     from hichap_master_amd import matrixBuilding as mb, synth
     names = [str(c) for c in range(1, 23)] + ["X"]
@@ -1162,9 +1163,11 @@ def run_twostep_genome(args, world, rank, local):
                "ms_per_step": 1000.0 * step, "higher_is_better": True, "scaling": "replicas", "vs_baseline": None,
                "dtype": "int64 in, f64 out", "data": "synthetic (device Poisson / binomial draws, synth model)",
                "config": {"workload": "twostep-hg19-40kb-genome", "chromosomes": len(names),
-                          "bins": int(sum(int(N) for N in Ns)), "sum_N2": sq, "streams": mb.TWOSTEP_STREAMS},
-               "roofline": {"bound": "hbm", "kernel": "hh_twostep_batch (per chromosome: k_rowstats x3, device glue, "
-                                                       "two streaming symmetrisation chains)",
+                          "bins": int(sum(int(N) for N in Ns)), "sum_N2": sq,
+                          "launches": "shared per pass" if mb.TWOSTEP_STREAMS == 0 else f"{mb.TWOSTEP_STREAMS} streams"},
+               "roofline": {"bound": "hbm", "kernel": "hh_twostep_batch (shared launches: k_rowstats_b, k_ts_gapdef_b, "
+                                                       "k_ts_alpha_b, then the symmetrisation passes k_sv_*_b of every "
+                                                       "chromosome's MM and PM)",
                             "achieved": alg / step / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                             "frac": alg / step / 1e9 / PEAK_HBM_GBS, "traffic": None, "alg_bytes_per_launch": alg,
                             "note": "40 B per matrix element (3 int64 reads + 2 fp64 writes), the whole genome per step"},

@@ -27,13 +27,11 @@ namespace hh {
 constexpr int kT = 64;  // dense tile edge
 
 template <class T>
-__global__ __launch_bounds__(256) void k_rowstats(const T* __restrict__ X, long long N,
-                                                  const long long* __restrict__ lo,
-                                                  const long long* __restrict__ hi, double* __restrict__ sum,
-                                                  long long* __restrict__ zeros) {
+__device__ __forceinline__ void rowstats_row(const T* __restrict__ X, long long N, long long i,
+                                             const long long* __restrict__ lo, const long long* __restrict__ hi,
+                                             double* __restrict__ sum, long long* __restrict__ zeros) {
     __shared__ double shd[16];
     __shared__ long long shz[16];
-    const long long i = blockIdx.x;
     const long long a = lo ? lo[i] : 0, b = hi ? hi[i] : N;
     const T* row = X + i * N;
     long long zc = 0;
@@ -59,6 +57,34 @@ __global__ __launch_bounds__(256) void k_rowstats(const T* __restrict__ X, long 
         zeros[i] = z;
         sum[i] = std::is_integral_v<T> ? (double)s : d;
     }
+}
+
+template <class T>
+__global__ __launch_bounds__(256) void k_rowstats(const T* __restrict__ X, long long N,
+                                                  const long long* __restrict__ lo,
+                                                  const long long* __restrict__ hi, double* __restrict__ sum,
+                                                  long long* __restrict__ zeros) {
+    rowstats_row<T>(X, N, blockIdx.x, lo, hi, sum, zeros);
+}
+
+// The row statistics of many int64 matrices in one launch (hh_twostep_batch):
+// matrix m's rows are blocks [row0[m], row0[m + 1])
+struct RsDesc {
+    const long long* X;
+    long long N;
+    double* sum;
+    long long* zeros;
+};
+__global__ __launch_bounds__(256) void k_rowstats_b(const RsDesc* __restrict__ d, const long long* __restrict__ row0,
+                                                    int nd) {
+    const long long b = blockIdx.x;
+    int lo = 0, hi = nd - 1;  // the last m with row0[m] <= b
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (row0[mid] <= b) lo = mid; else hi = mid - 1;
+    }
+    const RsDesc m = d[lo];
+    rowstats_row<long long>(m.X, m.N, b - row0[lo], nullptr, nullptr, m.sum, m.zeros);
 }
 
 // Pair (I, J), I <= J, of an nT x nT tile grid -> linear index.
@@ -227,10 +253,10 @@ __global__ __launch_bounds__(256) void k_symvc(const T* __restrict__ X, SymArgs 
 // blocks per CU instead of 2.  The same operands and IEEE operations as
 // k_symvc<T, 3> (bitwise the same output).
 template <class T>
-__global__ __launch_bounds__(256) void k_symvc_out(const T* __restrict__ X, SymArgs a, double* __restrict__ out) {
+__device__ __forceinline__ void symvc_out_body(const T* __restrict__ X, const SymArgs& a, double* __restrict__ out,
+                                               long long p) {
     __shared__ T tt[kT][kT + 1];
     __shared__ TileVecs tv;
-    const long long p = blockIdx.x;
     long long I = 0, rem = p;
     while (rem >= a.nT - I) { rem -= a.nT - I; ++I; }
     const long long J = I + rem;
@@ -298,6 +324,11 @@ __global__ __launch_bounds__(256) void k_symvc_out(const T* __restrict__ X, SymA
             __builtin_nontemporal_store(scale * (y / (tv.sI[c] * tv.sJ[r])), &out[(J0 + r) * N + I0 + c]);
         }
     }
+}
+
+template <class T>
+__global__ __launch_bounds__(256) void k_symvc_out(const T* __restrict__ X, SymArgs a, double* __restrict__ out) {
+    symvc_out_body<T>(X, a, out, blockIdx.x);
 }
 
 // rowsum(Y)_i from the pass-1 slab in a fixed order (J = 0 .. nT-1), then
@@ -374,14 +405,14 @@ constexpr int kGB = 4 * kGW;  // columns per block: its 4 waves read 16 KB of a 
 //         X_ij (i, j gaps) copied to the compact g x g matrix Xc.
 // MODE 2: part_r[q][i] = sum over the span's columns of X_ij * rs_j.
 template <class T, int MODE, bool ROWS = true>
-__global__ __launch_bounds__(256) void k_ts_gemv(const T* __restrict__ X, long long N,
-                                                 const double* __restrict__ alpha, const double* __restrict__ rs,
-                                                 int gr, double* __restrict__ part_c, double* __restrict__ part_r,
-                                                 const int* __restrict__ gpos, T* __restrict__ Xc,
-                                                 const long long* __restrict__ ng_p) {
+__device__ __forceinline__ void ts_gemv_body(const T* __restrict__ X, long long N, const double* __restrict__ alpha,
+                                             const double* __restrict__ rs, int gr, double* __restrict__ part_c,
+                                             double* __restrict__ part_r, const int* __restrict__ gpos,
+                                             T* __restrict__ Xc, const long long* __restrict__ ng_p, long long bx,
+                                             long long by) {
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const long long rc = blockIdx.x, q = (long long)blockIdx.y * 4 + w;
+    const long long rc = bx, q = by * 4 + w;
     const long long r0 = rc * gr, c0 = q * kGW;
     if (c0 >= N) return;  // wave-uniform; no block barrier below
     double accc[8], bcol[8];
@@ -464,6 +495,15 @@ __global__ __launch_bounds__(256) void k_ts_gemv(const T* __restrict__ X, long l
     }
 }
 
+template <class T, int MODE, bool ROWS = true>
+__global__ __launch_bounds__(256) void k_ts_gemv(const T* __restrict__ X, long long N,
+                                                 const double* __restrict__ alpha, const double* __restrict__ rs,
+                                                 int gr, double* __restrict__ part_c, double* __restrict__ part_r,
+                                                 const int* __restrict__ gpos, T* __restrict__ Xc,
+                                                 const long long* __restrict__ ng_p) {
+    ts_gemv_body<T, MODE, ROWS>(X, N, alpha, rs, gr, part_c, part_r, gpos, Xc, ng_p, blockIdx.x, blockIdx.y);
+}
+
 // The both-gap pairs' correction on the compact g x g matrix Xc (gap rows
 // and columns in index order): block (A, B) of 64 x 64 tiles gives, for each
 // compact row a of A,
@@ -472,16 +512,17 @@ __global__ __launch_bounds__(256) void k_ts_gemv(const T* __restrict__ X, long l
 // with S_ab = Xc[a][b] / alpha_{G[a]}; (B, A) is read coalesced and
 // transposed through LDS.
 template <class T, int MODE>
-__global__ __launch_bounds__(256) void k_ts_gap(const T* __restrict__ Xc, const long long* __restrict__ ng_p,
-                                                const int* __restrict__ glist, const double* __restrict__ alpha,
-                                                const double* __restrict__ sv, double* __restrict__ gpart) {
+__device__ __forceinline__ void ts_gap_body(const T* __restrict__ Xc, const long long* __restrict__ ng_p,
+                                            const int* __restrict__ glist, const double* __restrict__ alpha,
+                                            const double* __restrict__ sv, double* __restrict__ gpart, long long bx,
+                                            long long gdx) {
     __shared__ T tt[kT][kT + 1];
     __shared__ double aA[kT], aB[kT], sA[kT], sB[kT];
     __shared__ double red[4][kT];
     const long long ng = *ng_p, nbt = (ng + kT - 1) / kT;
     const int c = threadIdx.x & (kT - 1), r0 = threadIdx.x >> 6;
     // grid-stride over the nbt x nbt tiles (the gap count is known on the device only)
-    for (long long t = blockIdx.x; t < nbt * nbt; t += gridDim.x) {
+    for (long long t = bx; t < nbt * nbt; t += gdx) {
         const long long Ab = t / nbt, Bb = t % nbt;
         const long long A0 = Ab * kT, B0 = Bb * kT;
         // clamped addresses, no select on loaded values (see k_symvc_out); a
@@ -527,13 +568,20 @@ __global__ __launch_bounds__(256) void k_ts_gap(const T* __restrict__ Xc, const 
     }
 }
 
+template <class T, int MODE>
+__global__ __launch_bounds__(256) void k_ts_gap(const T* __restrict__ Xc, const long long* __restrict__ ng_p,
+                                                const int* __restrict__ glist, const double* __restrict__ alpha,
+                                                const double* __restrict__ sv, double* __restrict__ gpart) {
+    ts_gap_body<T, MODE>(Xc, ng_p, glist, alpha, sv, gpart, blockIdx.x, gridDim.x);
+}
+
 // Ccol_j = sum over the row chunks of part_c[rc][j] (fixed order: wave w
 // sums a contiguous range of chunks, the 16 wave sums added in order).
-__global__ __launch_bounds__(1024) void k_ts_colsum(const double* __restrict__ part_c, long long N, long long nrc,
-                                                    double* __restrict__ ccol) {
+__device__ __forceinline__ void ts_colsum_body(const double* __restrict__ part_c, long long N, long long nrc,
+                                               double* __restrict__ ccol, long long bx) {
     __shared__ double red[16][64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const long long j = (long long)blockIdx.x * 64 + lane;
+    const long long j = bx * 64 + lane;
     const long long per = (nrc + 15) / 16, lo = std::min<long long>(nrc, w * per),
                     hi = std::min<long long>(nrc, lo + per);
     double acc = 0.0;
@@ -557,15 +605,21 @@ __global__ __launch_bounds__(1024) void k_ts_colsum(const double* __restrict__ p
     }
 }
 
+__global__ __launch_bounds__(1024) void k_ts_colsum(const double* __restrict__ part_c, long long N, long long nrc,
+                                                    double* __restrict__ ccol) {
+    ts_colsum_body(part_c, N, nrc, ccol, blockIdx.x);
+}
+
 // rowsum(Y) from the MODE-1 partials (fixed order), s = rowsum^exponent
 // (0 -> 1) and 1 / s.
 template <class T>
-__global__ void k_ts_rows(const T* __restrict__ X, long long N, long long ncb,
-                          const double* __restrict__ ccol, const double* __restrict__ part_r,
-                          const double* __restrict__ alpha, const int* __restrict__ gpos,
-                          const double* __restrict__ gpart, const long long* __restrict__ ng_p, double exponent,
-                          const double* __restrict__ rowsum_in, double* __restrict__ sv, double* __restrict__ rsv) {
-    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void ts_rows_body(const T* __restrict__ X, long long N, long long ncb,
+                                             const double* __restrict__ ccol, const double* __restrict__ part_r,
+                                             const double* __restrict__ alpha, const int* __restrict__ gpos,
+                                             const double* __restrict__ gpart, const long long* __restrict__ ng_p,
+                                             double exponent, const double* __restrict__ rowsum_in,
+                                             double* __restrict__ sv, double* __restrict__ rsv, long long bx) {
+    const long long i = bx * blockDim.x + threadIdx.x;
     if (i >= N) return;
     const long long ng = ng_p ? *ng_p : 0;  // gap form iff ng > 0 (Trans2symmetry :948)
     const double c = ccol[i];
@@ -601,14 +655,23 @@ __global__ void k_ts_rows(const T* __restrict__ X, long long N, long long ncb,
     rsv[i] = 1.0 / v;
 }
 
+template <class T>
+__global__ void k_ts_rows(const T* __restrict__ X, long long N, long long ncb,
+                          const double* __restrict__ ccol, const double* __restrict__ part_r,
+                          const double* __restrict__ alpha, const int* __restrict__ gpos,
+                          const double* __restrict__ gpart, const long long* __restrict__ ng_p, double exponent,
+                          const double* __restrict__ rowsum_in, double* __restrict__ sv, double* __restrict__ rsv) {
+    ts_rows_body<T>(X, N, ncb, ccol, part_r, alpha, gpos, gpart, ng_p, exponent, rowsum_in, sv, rsv, blockIdx.x);
+}
+
 // Per-block partials of sum(C) from the MODE-2 row partials.
 template <class T>
-__global__ __launch_bounds__(256) void k_ts_q(const T* __restrict__ X, long long N, long long ncb,
-                                              const double* __restrict__ part_r, const double* __restrict__ alpha,
-                                              const double* __restrict__ sv, const double* __restrict__ gpart2,
-                                              const long long* __restrict__ ng_p, double* __restrict__ part) {
+__device__ __forceinline__ void ts_q_body(const T* __restrict__ X, long long N, long long ncb,
+                                          const double* __restrict__ part_r, const double* __restrict__ alpha,
+                                          const double* __restrict__ sv, const double* __restrict__ gpart2,
+                                          const long long* __restrict__ ng_p, double* __restrict__ part, long long bx) {
     __shared__ double sh[16];
-    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    const long long i = bx * 256 + threadIdx.x;
     const long long ng = ng_p ? *ng_p : 0;
     double term = 0.0;
     if (i < N) {
@@ -630,7 +693,15 @@ __global__ __launch_bounds__(256) void k_ts_q(const T* __restrict__ X, long long
         }
     }
     term = block_sum(term, sh);
-    if (threadIdx.x == 0) part[blockIdx.x] = term;
+    if (threadIdx.x == 0) part[bx] = term;
+}
+
+template <class T>
+__global__ __launch_bounds__(256) void k_ts_q(const T* __restrict__ X, long long N, long long ncb,
+                                              const double* __restrict__ part_r, const double* __restrict__ alpha,
+                                              const double* __restrict__ sv, const double* __restrict__ gpart2,
+                                              const long long* __restrict__ ng_p, double* __restrict__ part) {
+    ts_q_body<T>(X, N, ncb, part_r, alpha, sv, gpart2, ng_p, part, blockIdx.x);
 }
 
 // Workspace of one Trans2symmetry + Correct_VC + rescale chain (alive until
@@ -977,13 +1048,12 @@ __device__ double block_percentile(long long n, long long nt, double pct, Get ge
 // Gap_defined (:915-929) for MM (block 0) and PM (block 1) from their zero
 // counts, and the gap rows compacted (gpos: position or -1, glist, ng).
 // err bit 0: every coverage is zero (np.percentile of an empty array).
-__global__ __launch_bounds__(1024) void k_ts_gapdef(const long long* __restrict__ zeros, long long N,
-                                                    uint8_t* __restrict__ gap, int* __restrict__ gpos,
-                                                    int* __restrict__ glist, long long* __restrict__ ng,
-                                                    int* __restrict__ err) {
+__device__ __forceinline__ void ts_gapdef_body(const long long* __restrict__ zeros, long long N,
+                                               uint8_t* __restrict__ gap, int* __restrict__ gpos,
+                                               int* __restrict__ glist, long long* __restrict__ ng,
+                                               int* __restrict__ err, int m) {
     __shared__ SelLds L;
     __shared__ int wtot[16];
-    const int m = blockIdx.x;
     const long long* z = zeros + (1 + m) * N;
     uint8_t* g = gap + m * N;
     int* gp = gpos + m * N;
@@ -1033,11 +1103,18 @@ __global__ __launch_bounds__(1024) void k_ts_gapdef(const long long* __restrict_
     if (threadIdx.x == 0) ng[m] = base;
 }
 
+__global__ __launch_bounds__(1024) void k_ts_gapdef(const long long* __restrict__ zeros, long long N,
+                                                    uint8_t* __restrict__ gap, int* __restrict__ gpos,
+                                                    int* __restrict__ glist, long long* __restrict__ ng,
+                                                    int* __restrict__ err) {
+    ts_gapdef_body(zeros, N, gap, gpos, glist, ng, err, blockIdx.x);
+}
+
 // alpha (:989-1005) over the union of MM's and PM's non-gap bins, and the
 // exact raw totals of MM and PM.  err bit 1: every bin is a gap.
-__global__ __launch_bounds__(1024) void k_ts_alpha(const double* __restrict__ sum, const uint8_t* __restrict__ gap,
-                                                   long long N, double* __restrict__ alpha, double* __restrict__ raw,
-                                                   int* __restrict__ err) {
+__device__ __forceinline__ void ts_alpha_body(const double* __restrict__ sum, const uint8_t* __restrict__ gap,
+                                              long long N, double* __restrict__ alpha, double* __restrict__ raw,
+                                              int* __restrict__ err) {
     __shared__ SelLds L;
     __shared__ double wmx[16];
     __shared__ long long wr[2][16];
@@ -1087,6 +1164,130 @@ __global__ __launch_bounds__(1024) void k_ts_alpha(const double* __restrict__ su
     __syncthreads();
     for (long long i = threadIdx.x; i < N; i += blockDim.x)
         if (alpha[i] < th) alpha[i] = th;
+}
+
+__global__ __launch_bounds__(1024) void k_ts_alpha(const double* __restrict__ sum, const uint8_t* __restrict__ gap,
+                                                   long long N, double* __restrict__ alpha, double* __restrict__ raw,
+                                                   int* __restrict__ err) {
+    ts_alpha_body(sum, gap, N, alpha, raw, err);
+}
+
+// the glue of many chromosomes in one launch each (hh_twostep_batch)
+struct TsDesc {
+    long long N;
+    const long long* zeros;  // 3N: T, M, P
+    const double* sum;       // 3N
+    uint8_t* gap;            // 2N
+    int* gpos;               // 2N
+    int* glist;              // 2N
+    long long* ng;           // 2
+    double* alpha;           // N
+    double* raw;             // 2
+    int* err;
+};
+__global__ __launch_bounds__(1024) void k_ts_gapdef_b(const TsDesc* __restrict__ D) {
+    const TsDesc d = D[blockIdx.x >> 1];
+    ts_gapdef_body(d.zeros, d.N, d.gap, d.gpos, d.glist, d.ng, d.err, blockIdx.x & 1);
+}
+__global__ __launch_bounds__(1024) void k_ts_alpha_b(const TsDesc* __restrict__ D) {
+    const TsDesc d = D[blockIdx.x];
+    ts_alpha_body(d.sum, d.gap, d.N, d.alpha, d.raw, d.err);
+}
+
+// One symmetrisation chain (Trans2symmetry + Correct_VC + rescale of one
+// haplotype matrix, the streaming passes of symvc_enqueue) as data: every
+// chain's pass k runs in ONE launch, blocks [off[k][c], off[k][c + 1]) for
+// chain c (hh_twostep_batch).  The same bodies with the same arguments as
+// the per-chain launches: bitwise the same results.
+struct SvDesc {
+    const long long* X;
+    long long N, nrc, gcb, ncb, nb, ggrid, npairs, nT;
+    int gr;
+    const double* alpha;
+    const uint8_t* gap;
+    const int* gpos;
+    const int* glist;
+    const long long* ng_p;
+    long long* xc;
+    double *part_c, *part_r, *ccol, *sv, *rsv, *gpart1, *gpart2, *part, *tot;
+    const double* rowsum_in;
+    const double* raw_p;
+    double* out;
+};
+enum { kSvGemv = 0, kSvGap, kSvColsum, kSvRows, kSvQ, kSvOut, kSvPhases };
+
+__device__ __forceinline__ int sv_find(const long long* __restrict__ off, int nd, long long b) {
+    int lo = 0, hi = nd - 1;  // the last chain with off[c] <= b
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (off[mid] <= b) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) void k_sv_gemv_b(const SvDesc* __restrict__ D, const long long* __restrict__ off,
+                                                   int nd) {
+    const int c = sv_find(off, nd, blockIdx.x);
+    const SvDesc& d = D[c];
+    const long long l = (long long)blockIdx.x - off[c];
+    if (MODE == 1)
+        ts_gemv_body<long long, 1, false>(d.X, d.N, d.alpha, nullptr, d.gr, d.part_c, d.part_r, d.gpos, d.xc, d.ng_p,
+                                          l % d.nrc, l / d.nrc);
+    else
+        ts_gemv_body<long long, 2, true>(d.X, d.N, d.alpha, d.rsv, d.gr, d.part_c, d.part_r, nullptr, nullptr,
+                                         nullptr, l % d.nrc, l / d.nrc);
+}
+template <int MODE>
+__global__ __launch_bounds__(256) void k_sv_gap_b(const SvDesc* __restrict__ D, const long long* __restrict__ off,
+                                                  int nd) {
+    const int c = sv_find(off, nd, blockIdx.x);
+    const SvDesc& d = D[c];
+    ts_gap_body<long long, MODE>(d.xc, d.ng_p, d.glist, d.alpha, MODE == 2 ? d.sv : nullptr,
+                                 MODE == 2 ? d.gpart2 : d.gpart1, (long long)blockIdx.x - off[c], d.ggrid);
+}
+__global__ __launch_bounds__(1024) void k_sv_colsum_b(const SvDesc* __restrict__ D, const long long* __restrict__ off,
+                                                      int nd) {
+    const int c = sv_find(off, nd, blockIdx.x);
+    const SvDesc& d = D[c];
+    ts_colsum_body(d.part_c, d.N, d.nrc, d.ccol, (long long)blockIdx.x - off[c]);
+}
+__global__ __launch_bounds__(256) void k_sv_rows_b(const SvDesc* __restrict__ D, const long long* __restrict__ off,
+                                                   int nd, double exponent) {
+    const int c = sv_find(off, nd, blockIdx.x);
+    const SvDesc& d = D[c];
+    ts_rows_body<long long>(d.X, d.N, d.ncb, d.ccol, d.part_r, d.alpha, d.gpos, d.gpart1, d.ng_p, exponent,
+                            d.rowsum_in, d.sv, d.rsv, (long long)blockIdx.x - off[c]);
+}
+__global__ __launch_bounds__(256) void k_sv_q_b(const SvDesc* __restrict__ D, const long long* __restrict__ off,
+                                                int nd) {
+    const int c = sv_find(off, nd, blockIdx.x);
+    const SvDesc& d = D[c];
+    ts_q_body<long long>(d.X, d.N, d.ncb, d.part_r, d.alpha, d.sv, d.gpart2, d.ng_p, d.part,
+                         (long long)blockIdx.x - off[c]);
+}
+// k_slab_sum + k_symvc_scale of every chain (one block each; the same
+// fixed-order sum and the same IEEE operations)
+__global__ __launch_bounds__(256) void k_sv_fin_b(const SvDesc* __restrict__ D) {
+    __shared__ double sh[16];
+    const SvDesc& d = D[blockIdx.x];
+    double acc = 0.0;
+    for (long long k = threadIdx.x; k < d.nb; k += 256) acc += d.part[k];
+    acc = block_sum(acc, sh);
+    if (threadIdx.x == 0) {
+        d.tot[0] = acc;
+        const double nn = (double)d.N * (double)d.N;
+        d.tot[1] = (*d.raw_p / nn) / (acc / nn);
+    }
+}
+__global__ __launch_bounds__(256) void k_sv_out_b(const SvDesc* __restrict__ D, const long long* __restrict__ off,
+                                                  int nd) {
+    const int c = sv_find(off, nd, blockIdx.x);
+    const SvDesc& d = D[c];
+    SymArgs a{d.N, d.nT, d.alpha, d.gap, d.sv, 1.0};
+    a.scale_p = d.tot + 1;
+    a.ng_p = d.ng_p;
+    symvc_out_body<long long>(d.X, a, d.out, (long long)blockIdx.x - off[c]);
 }
 
 
@@ -1427,6 +1628,7 @@ int hh_twostep(const int64_t* TM, const int64_t* MM, const int64_t* PM, int64_t 
 // the end.  The small chromosomes' latency-bound launches run beside the big
 // ones' streaming passes instead of after them.  Per chromosome the same
 // kernels in the same order as hh_twostep: bitwise the same results.
+extern "C++" {
 namespace {
 struct TsWork {
     DBuf<double> dsum, dA, draw;
@@ -1445,13 +1647,14 @@ std::vector<hipStream_t>& ts_streams(int k) {
     return v;
 }
 }  // namespace
+}  // extern "C++"
 
 int hh_twostep_batch(int32_t n, const int64_t* const* TM, const int64_t* const* MM, const int64_t* const* PM,
                      const int64_t* N, double* const* nor_mm, double* const* nor_pm, uint8_t* gap_m,
                      uint8_t* gap_p, int32_t n_streams, void* stream) {
     return guard([&] {
         HH_REQUIRE(n >= 0 && (n == 0 || (TM && MM && PM && N && nor_mm && nor_pm && gap_m && gap_p)), "bad arguments");
-        HH_REQUIRE(n_streams >= 1 && n_streams <= 16, "n_streams in [1, 16]");
+        HH_REQUIRE(n_streams >= 0 && n_streams <= 16, "n_streams in [0, 16]");
         HH_REQUIRE(g_symvc_stream && g_twostep_devglue, "hh_twostep_batch needs the streaming device-glue chain");
         if (n == 0) return;
         std::vector<int64_t> goff((size_t)n + 1, 0);
@@ -1463,7 +1666,7 @@ int hh_twostep_batch(int32_t n, const int64_t* const* TM, const int64_t* const* 
         std::vector<int> order(n);
         for (int c = 0; c < n; ++c) order[c] = c;
         std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return N[a] > N[b]; });
-        const int K = std::min(n_streams, n);
+        const int K = std::max(1, std::min(n_streams, n));
         std::vector<hipStream_t>& ss = ts_streams(K);
         std::vector<double> load(K, 0.0);
         std::vector<int> sid(n);
@@ -1488,6 +1691,132 @@ int hh_twostep_batch(int32_t n, const int64_t* const* TM, const int64_t* const* 
             w[c].dA.alloc(Nc);
             w[c].draw.alloc(2);
         }
+        // shared launches for the row statistics (every matrix's rows) and
+        // the glue (every chromosome's gap flags, alpha, raw totals), then
+        // each chromosome's two symmetrisation chains on the streams
+        std::vector<RsDesc> rs((size_t)3 * n);
+        std::vector<long long> row0((size_t)3 * n + 1, 0);
+        std::vector<TsDesc> td((size_t)n);
+        for (int c = 0; c < n; ++c) {
+            TsWork& x = w[c];
+            const long long* d[3] = {(const long long*)TM[c], (const long long*)MM[c], (const long long*)PM[c]};
+            for (int k = 0; k < 3; ++k) {
+                rs[3 * c + k] = RsDesc{d[k], N[c], x.dsum.p + k * N[c], x.dz.p + k * N[c]};
+                row0[3 * c + k + 1] = row0[3 * c + k] + N[c];
+            }
+            td[c] = TsDesc{N[c], x.dz.p, x.dsum.p, x.dgf.p, x.dgpos.p, x.dglist.p, x.dng.p, x.dA.p, x.draw.p,
+                           derr.p + c};
+        }
+        HH_REQUIRE(row0.back() < (1LL << 31), "too many rows for one launch");
+        const size_t b_rs = rs.size() * sizeof(RsDesc), b_r0 = row0.size() * 8, b_td = td.size() * sizeof(TsDesc);
+        const size_t o_r0 = (b_rs + 15) & ~(size_t)15, o_td = o_r0 + ((b_r0 + 15) & ~(size_t)15);
+        DBuf<char> ddesc(o_td + b_td);
+        {
+            char* up = (char*)pinned_stage().get(1, o_td + b_td);
+            std::memcpy(up, rs.data(), b_rs);
+            std::memcpy(up + o_r0, row0.data(), b_r0);
+            std::memcpy(up + o_td, td.data(), b_td);
+            ddesc.upload(up, o_td + b_td, s0);
+        }
+        hipLaunchKernelGGL(k_rowstats_b, dim3((unsigned)row0.back()), dim3(256), 0, s0, (const RsDesc*)ddesc.p,
+                           (const long long*)(ddesc.p + o_r0), 3 * n);
+        hipLaunchKernelGGL(k_ts_gapdef_b, dim3((unsigned)(2 * n)), dim3(1024), 0, s0,
+                           (const TsDesc*)(ddesc.p + o_td));
+        hipLaunchKernelGGL(k_ts_alpha_b, dim3((unsigned)n), dim3(1024), 0, s0, (const TsDesc*)(ddesc.p + o_td));
+        HIP_CHECK(hipGetLastError());
+        if (n_streams == 0) {
+            // every chain's passes in shared launches: chain 2c = MM of
+            // chromosome c, 2c + 1 = PM, largest chromosomes first
+            const int nd = 2 * n;
+            std::vector<SvDesc> sd((size_t)nd);
+            std::vector<long long> off((size_t)kSvPhases * (nd + 1), 0);
+            const int gr = g_symvc_rows;
+            int j = 0;
+            for (int c : order) {
+                TsWork& x = w[c];
+                const long long Nc = N[c];
+                for (int h = 0; h < 2; ++h, ++j) {
+                    SymvcWs& ws = h ? x.wp : x.wm;
+                    SvDesc d{};
+                    d.X = (const long long*)(h ? PM[c] : MM[c]);
+                    d.N = Nc;
+                    d.gr = gr;
+                    d.nrc = (Nc + gr - 1) / gr;
+                    d.gcb = (Nc + kGB - 1) / kGB;
+                    d.ncb = (Nc + kGW - 1) / kGW;
+                    d.nb = (Nc + 255) / 256;
+                    d.nT = (Nc + kT - 1) / kT;
+                    d.npairs = d.nT * (d.nT + 1) / 2;
+                    const long long nbtm = (Nc + kT - 1) / kT;  // the gap count's bound: N (device count)
+                    d.ggrid = std::min<long long>(std::max<long long>(nbtm * nbtm, 1), 2048);
+                    HH_REQUIRE(d.gcb < 65536 && d.npairs < (1LL << 31), "matrix too large");
+                    ws.sv.alloc(Nc);
+                    ws.tot.alloc(2);
+                    ws.part_c.alloc((size_t)(d.nrc * Nc));
+                    ws.part_r.alloc((size_t)(d.ncb * Nc));
+                    ws.rsv.alloc(Nc);
+                    ws.ccol.alloc(Nc);
+                    ws.part.alloc((size_t)d.nb);
+                    ws.xc.alloc((size_t)(Nc * Nc) * sizeof(long long));
+                    ws.gpart1.alloc((size_t)(nbtm * Nc));
+                    ws.gpart2.alloc((size_t)(nbtm * Nc));
+                    d.alpha = x.dA.p;
+                    d.gap = x.dgf.p + h * Nc;
+                    d.gpos = x.dgpos.p + h * Nc;
+                    d.glist = x.dglist.p + h * Nc;
+                    d.ng_p = x.dng.p + h;
+                    d.xc = (long long*)ws.xc.p;
+                    d.part_c = ws.part_c.p, d.part_r = ws.part_r.p, d.ccol = ws.ccol.p, d.sv = ws.sv.p;
+                    d.rsv = ws.rsv.p, d.gpart1 = ws.gpart1.p, d.gpart2 = ws.gpart2.p, d.part = ws.part.p;
+                    d.tot = ws.tot.p;
+                    d.rowsum_in = x.dsum.p + (1 + h) * Nc;
+                    d.raw_p = x.draw.p + h;
+                    d.out = h ? nor_pm[c] : nor_mm[c];
+                    sd[j] = d;
+                    const long long nblk[kSvPhases] = {d.nrc * d.gcb, d.ggrid, (Nc + 63) / 64, d.nb, d.nb, d.npairs};
+                    for (int k = 0; k < kSvPhases; ++k) off[(size_t)k * (nd + 1) + j + 1] = off[(size_t)k * (nd + 1) + j] + nblk[k];
+                }
+            }
+            for (int k = 0; k < kSvPhases; ++k)
+                HH_REQUIRE(off[(size_t)k * (nd + 1) + nd] < (1LL << 31), "too many blocks for one launch");
+            const size_t b_sd = sd.size() * sizeof(SvDesc), o_off = (b_sd + 15) & ~(size_t)15;
+            DBuf<char> dsv(o_off + off.size() * 8);
+            {
+                char* up = (char*)pinned_stage().get(0, o_off + off.size() * 8);
+                std::memcpy(up, sd.data(), b_sd);
+                std::memcpy(up + o_off, off.data(), off.size() * 8);
+                dsv.upload(up, o_off + off.size() * 8, s0);
+                HIP_CHECK(hipStreamSynchronize(s0));  // slot 0 is reused for the downloads below
+            }
+            const SvDesc* D = (const SvDesc*)dsv.p;
+            auto O = [&](int k) { return (const long long*)(dsv.p + o_off) + (size_t)k * (nd + 1); };
+            auto grid = [&](int k) { return dim3((unsigned)off[(size_t)k * (nd + 1) + nd]); };
+            const double ex = 2.0 / 3.0;
+            hipLaunchKernelGGL(k_sv_gemv_b<1>, grid(kSvGemv), dim3(256), 0, s0, D, O(kSvGemv), nd);
+            hipLaunchKernelGGL(k_sv_gap_b<1>, grid(kSvGap), dim3(256), 0, s0, D, O(kSvGap), nd);
+            hipLaunchKernelGGL(k_sv_colsum_b, grid(kSvColsum), dim3(1024), 0, s0, D, O(kSvColsum), nd);
+            hipLaunchKernelGGL(k_sv_rows_b, grid(kSvRows), dim3(256), 0, s0, D, O(kSvRows), nd, ex);
+            hipLaunchKernelGGL(k_sv_gap_b<2>, grid(kSvGap), dim3(256), 0, s0, D, O(kSvGap), nd);
+            hipLaunchKernelGGL(k_sv_gemv_b<2>, grid(kSvGemv), dim3(256), 0, s0, D, O(kSvGemv), nd);
+            hipLaunchKernelGGL(k_sv_q_b, grid(kSvQ), dim3(256), 0, s0, D, O(kSvQ), nd);
+            hipLaunchKernelGGL(k_sv_fin_b, dim3((unsigned)nd), dim3(256), 0, s0, D);
+            hipLaunchKernelGGL(k_sv_out_b, grid(kSvOut), dim3(256), 0, s0, D, O(kSvOut), nd);
+            HIP_CHECK(hipGetLastError());
+            const size_t gbytes = (size_t)2 * goff[n], ebytes = (size_t)n * sizeof(int);
+            char* dl = (char*)pinned_stage().get(0, ((gbytes + 15) & ~(size_t)15) + ebytes);
+            int* herr = (int*)(dl + ((gbytes + 15) & ~(size_t)15));
+            for (int c = 0; c < n; ++c)
+                HIP_CHECK(hipMemcpyAsync(dl + 2 * goff[c], w[c].dgf.p, (size_t)2 * N[c], hipMemcpyDeviceToHost, s0));
+            derr.download(herr, (size_t)n, s0);
+            HIP_CHECK(hipStreamSynchronize(s0));
+            for (int c = 0; c < n; ++c) {
+                HH_REQUIRE(!(herr[c] & 1), "percentile of an empty array (chromosome " + std::to_string(c) + ")");
+                HH_REQUIRE(!(herr[c] & 2), "every bin is a gap (chromosome " + std::to_string(c) + ")");
+                std::memcpy(gap_m + goff[c], dl + 2 * goff[c], (size_t)N[c]);
+                std::memcpy(gap_p + goff[c], dl + 2 * goff[c] + N[c], (size_t)N[c]);
+            }
+            return;
+        }
         hipEvent_t fork;
         HIP_CHECK(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
         HIP_CHECK(hipEventRecord(fork, s0));
@@ -1500,15 +1829,6 @@ int hh_twostep_batch(int32_t n, const int64_t* const* TM, const int64_t* const* 
             TsWork& x = w[c];
             const long long Nc = N[c];
             const long long* d[3] = {(const long long*)TM[c], (const long long*)MM[c], (const long long*)PM[c]};
-            for (int k = 0; k < 3; ++k)
-                hipLaunchKernelGGL((k_rowstats<long long>), dim3((unsigned)Nc), dim3(256), 0, s, d[k], Nc,
-                                   (const long long*)nullptr, (const long long*)nullptr, x.dsum.p + k * Nc,
-                                   x.dz.p + k * Nc);
-            hipLaunchKernelGGL(k_ts_gapdef, dim3(2), dim3(1024), 0, s, (const long long*)x.dz.p, Nc, x.dgf.p,
-                               x.dgpos.p, x.dglist.p, x.dng.p, derr.p + c);
-            hipLaunchKernelGGL(k_ts_alpha, dim3(1), dim3(1024), 0, s, (const double*)x.dsum.p,
-                               (const uint8_t*)x.dgf.p, Nc, x.dA.p, x.draw.p, derr.p + c);
-            HIP_CHECK(hipGetLastError());
             const GapIdx gim{x.dgpos.p, x.dglist.p, x.dng.p, Nc}, gip{x.dgpos.p + Nc, x.dglist.p + Nc, x.dng.p + 1, Nc};
             symvc_enqueue(d[1], Nc, x.dA.p, x.dgf.p, gim, 2.0 / 3.0, 0.0, x.draw.p, nor_mm[c], s, x.wm,
                           x.dsum.p + Nc);

@@ -205,13 +205,14 @@ def TwoStepCorrectionPixels(N, T_pixels, MM_cells, PM_cells, offset=0, output="u
     return res[0], res[1], gm, gp
 
 
-TWOSTEP_STREAMS = 4  # hh_twostep_batch streams (the box's hardware queues per process)
+TWOSTEP_STREAMS = 0  # hh_twostep_batch: 0 = every pass of every chromosome in one shared launch
 
 
 def IntraChromMatrixCorrection(Tra_Lib, Hap_Lib, n_streams=TWOSTEP_STREAMS, stream=None):
     """Per-chromosome TwoStepCorrection (matrixBuilding.py:1026-1041).  With
-    device tensors, every chromosome in one ``hh_twostep_batch`` call (chains
-    on ``n_streams`` streams, largest first; outputs device tensors)."""
+    device tensors, every chromosome in one ``hh_twostep_batch`` call (shared
+    launches per pass, or with ``n_streams`` > 0 the chains on that many
+    streams; outputs device tensors)."""
     keys = list(Tra_Lib.keys())
     mats = [(Tra_Lib[c], Hap_Lib["M" + c], Hap_Lib["P" + c]) for c in keys]
     if mats and all(bool(getattr(X, "is_cuda", False)) for t in mats for X in t):

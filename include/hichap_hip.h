@@ -360,10 +360,14 @@ int hh_twostep(const int64_t* TM, const int64_t* MM, const int64_t* PM, int64_t 
                uint8_t* gap_m, uint8_t* gap_p, int32_t on_device, void* stream);
 /* IntraChromMatrixCorrection (matrixBuilding.py:1026-1041): hh_twostep over
  * n chromosomes in one call, device pointers only (TM[c], MM[c], PM[c] int64
- * N[c] x N[c]; nor_mm[c], nor_pm[c] fp64 outputs).  Chromosomes largest first
- * on the least-loaded of n_streams (1..16) streams, one synchronisation at
- * the end; per chromosome bitwise hh_twostep's results.  gap_m / gap_p (host)
- * receive every chromosome's flags concatenated in argument order. */
+ * N[c] x N[c]; nor_mm[c], nor_pm[c] fp64 outputs).  The row statistics and
+ * the gap / alpha glue of every chromosome run as shared launches; then
+ * n_streams = 0: every pass of every chromosome's two symmetrisation chains
+ * in one shared launch per pass; 1..16: each chain's launches on the
+ * least-loaded of that many streams, largest chromosomes first.  One
+ * synchronisation at the end; per chromosome bitwise hh_twostep's results.
+ * gap_m / gap_p (host) receive every chromosome's flags concatenated in
+ * argument order. */
 int hh_twostep_batch(int32_t n, const int64_t* const* TM, const int64_t* const* MM, const int64_t* const* PM,
                      const int64_t* N, double* const* nor_mm, double* const* nor_pm, uint8_t* gap_m,
                      uint8_t* gap_p, int32_t n_streams, void* stream);

@@ -251,12 +251,13 @@ def test_twostep_devglue_block_select_path_bitwise(mb):
     assert 300 <= len(gm) < N  # the zeroed rows are gaps, most rows are not
 
 
-@pytest.mark.parametrize("n_streams", [1, 4])
+@pytest.mark.parametrize("n_streams", [0, 1, 4])
 def test_intra_chrom_batch_equals_per_chromosome(mb, n_streams):
     """IntraChromMatrixCorrection on device tensors: every chromosome in one
-    hh_twostep_batch call (chains on several streams, largest first) is
-    bitwise the per-chromosome hh_twostep, gaps included; one chromosome with
-    gap rows, one without, sizes from 37 to 2 100 bins."""
+    hh_twostep_batch call (0: shared launches per pass; else the chains on
+    several streams, largest first) is bitwise the per-chromosome
+    hh_twostep, gaps included; one chromosome with gap rows, one without,
+    sizes from 37 to 2 100 bins."""
     import torch
     rng = np.random.default_rng(77)
     tra, hap = {}, {}
