@@ -290,3 +290,25 @@ def test_intra_chrom_batch_error_names_the_chromosome(mb):
     hap = {"M1": d(MM), "P1": d(PM), "M2": d(Z), "P2": d(Z)}
     with pytest.raises(_lib.HipLibraryError, match=r"percentile of an empty array \(chromosome 1\)"):
         mb.IntraChromMatrixCorrection(tra, hap)
+
+
+def test_intra_chrom_batch_wide_counts_fallback(mb):
+    """The shared-launch batch reads 32-bit copies of MM / PM; a chromosome
+    whose counts do not fit (here one cell of 2^33) falls back to the int64
+    matrix for its own passes: still bitwise the per-chromosome result."""
+    import torch
+    rng = np.random.default_rng(78)
+    tra, hap = {}, {}
+    for c, N, big in (("1", 700, True), ("2", 500, False)):
+        TM = synth.dense_chrom(N, rng, A=50.0)
+        MM, PM = synth.haplotype_pair(TM, rng, drop_rows=5)
+        if big:
+            MM[3, 10] = 2 ** 33
+            TM[3, 10] = TM[10, 3] = 2 ** 34
+        tra[c] = torch.from_numpy(TM).cuda()
+        hap["M" + c], hap["P" + c] = torch.from_numpy(MM).cuda(), torch.from_numpy(PM).cuda()
+    nor, gaps = mb.IntraChromMatrixCorrection(tra, hap, n_streams=0)
+    for c in tra:
+        one = mb.TwoStepCorrection(tra[c], hap["M" + c], hap["P" + c])
+        assert torch.equal(nor["M" + c], one[0]) and torch.equal(nor["P" + c], one[1])
+        np.testing.assert_array_equal(gaps["M" + c], one[2])
