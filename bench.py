@@ -175,20 +175,23 @@ def gw_pmc_traffic(workload):
     return tot / n_corr, src
 
 
-def c5_pmc_traffic(workload, kernels, launches):
+def c5_pmc_traffic(workload, kernels, primary, launches):
     """HBM bytes of one serial C5 pass in the kernels whose names contain any
     of `kernels` (rocprofv3 PMC summary of the C5 bench at these sources on
-    this workload, profiles/*_c5_pmc.json): the summary's per-dispatch average
-    of each such kernel x `launches` (its dispatches per pass, from the HIP
-    event registry); (None, None) without a summary."""
+    this workload, profiles/*_c5_pmc.json): their bytes over the profiled run
+    (per-dispatch average x dispatches, every template instance) divided by
+    the passes that run held -- the `primary` kernel's dispatches over its
+    `launches` per pass (HIP event registry); (None, None) without one."""
     got = pmc_pick("c5", workload)
     if got is None:
         return None, None
     data, _, src = got
-    per = [v["traffic_bytes"] for k, v in data.items() if k != "_meta" and any(s in k for s in kernels)]
-    if not per:
+    items = [(k, v) for k, v in data.items() if k != "_meta"]
+    tot = sum(v["traffic_bytes"] * v.get("dispatches", 0) for k, v in items if any(s in k for s in kernels))
+    nprim = sum(v.get("dispatches", 0) for k, v in items if primary in k)
+    if not tot or not nprim or not launches:
         return None, None
-    return sum(per) * launches, src
+    return tot / (nprim / float(launches)), src
 
 
 def host_info():
@@ -485,9 +488,10 @@ def run_c5(args, world, rank, local):
         # (2 x FETCH_SIZE + WRITE_SIZE, the guide's gfx950 correction)
         wl = {"workload": "hg19-autosomes-25kb-compartment", "n_chroms": len(sizes),
               "bins_total": int(np.sum(sizes))}
-        for side, names, nl in ((orth_side, ("k_ortho",), orth_n),
-                                (mul_side, ("k_cor_sym", "k_cor_mul") if cor_sym else ("k_cor_mul",), mul_n)):
-            tr, src = c5_pmc_traffic(wl, names, nl)
+        for side, names, prim, nl in ((orth_side, ("k_ortho",), "k_ortho", orth_n),
+                                      (mul_side, ("k_cor_sym",) if cor_sym else ("k_cor_mul",),
+                                       "k_cor_sym_pf" if cor_sym else "k_cor_mul_part", mul_n)):
+            tr, src = c5_pmc_traffic(wl, names, prim, nl)
             side["traffic"] = tr
             side["traffic_source"] = src
             if tr and side["total_ms"]:

@@ -26,10 +26,13 @@ namespace hh {
 
 constexpr int kT = 64;  // dense tile edge
 
+// x32 (integer T only, may be null): the row copied as uint32; *ovf set
+// when a value does not fit (the later passes then read X itself)
 template <class T>
 __device__ __forceinline__ void rowstats_row(const T* __restrict__ X, long long N, long long i,
                                              const long long* __restrict__ lo, const long long* __restrict__ hi,
-                                             double* __restrict__ sum, long long* __restrict__ zeros) {
+                                             double* __restrict__ sum, long long* __restrict__ zeros,
+                                             uint32_t* __restrict__ x32 = nullptr, int* __restrict__ ovf = nullptr) {
     __shared__ double shd[16];
     __shared__ long long shz[16];
     const long long a = lo ? lo[i] : 0, b = hi ? hi[i] : N;
@@ -37,12 +40,21 @@ __device__ __forceinline__ void rowstats_row(const T* __restrict__ X, long long 
     long long zc = 0;
     double sd = 0.0;
     long long si = 0;
+    bool bad = false;
     for (long long j = a + threadIdx.x; j < b; j += 256) {
         const T v = row[j];
         zc += v == T(0);
-        if constexpr (std::is_integral_v<T>) si += (long long)v;  // integer: exact
-        else sd += (double)v;
+        if constexpr (std::is_integral_v<T>) {
+            si += (long long)v;  // integer: exact
+            if (x32) {
+                bad |= (unsigned long long)v > 0xFFFFFFFFull;  // (negative: huge as unsigned)
+                x32[i * N + j] = (uint32_t)v;
+            }
+        } else {
+            sd += (double)v;
+        }
     }
+    if (x32 && __ballot(bad) != 0ull && (threadIdx.x & 63) == 0) atomicOr(ovf, 1);
     // reduce
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     zc = wave_sum_ll(zc);
@@ -74,6 +86,8 @@ struct RsDesc {
     long long N;
     double* sum;
     long long* zeros;
+    uint32_t* x32;  // null: no copy
+    int* ovf;
 };
 __global__ __launch_bounds__(256) void k_rowstats_b(const RsDesc* __restrict__ d, const long long* __restrict__ row0,
                                                     int nd) {
@@ -84,7 +98,7 @@ __global__ __launch_bounds__(256) void k_rowstats_b(const RsDesc* __restrict__ d
         if (row0[mid] <= b) lo = mid; else hi = mid - 1;
     }
     const RsDesc m = d[lo];
-    rowstats_row<long long>(m.X, m.N, b - row0[lo], nullptr, nullptr, m.sum, m.zeros);
+    rowstats_row<long long>(m.X, m.N, b - row0[lo], nullptr, nullptr, m.sum, m.zeros, m.x32, m.ovf);
 }
 
 // Pair (I, J), I <= J, of an nT x nT tile grid -> linear index.
@@ -1201,6 +1215,8 @@ __global__ __launch_bounds__(1024) void k_ts_alpha_b(const TsDesc* __restrict__ 
 // the per-chain launches: bitwise the same results.
 struct SvDesc {
     const long long* X;
+    const uint32_t* x32;  // the uint32 copy (k_rowstats_b), read unless *ovf
+    const int* ovf;
     long long N, nrc, gcb, ncb, nb, ggrid, npairs, nT;
     int gr;
     const double* alpha;
@@ -1225,26 +1241,43 @@ __device__ __forceinline__ int sv_find(const long long* __restrict__ off, int nd
     return lo;
 }
 
+// the chain's matrix as uint32 (its k_rowstats_b copy) unless a value did
+// not fit; the same integers either way: bitwise the same doubles
+__device__ __forceinline__ bool sv_narrow(const SvDesc& d) { return d.x32 && *d.ovf == 0; }
+
 template <int MODE>
 __global__ __launch_bounds__(256) void k_sv_gemv_b(const SvDesc* __restrict__ D, const long long* __restrict__ off,
                                                    int nd) {
     const int c = sv_find(off, nd, blockIdx.x);
     const SvDesc& d = D[c];
     const long long l = (long long)blockIdx.x - off[c];
-    if (MODE == 1)
-        ts_gemv_body<long long, 1, false>(d.X, d.N, d.alpha, nullptr, d.gr, d.part_c, d.part_r, d.gpos, d.xc, d.ng_p,
-                                          l % d.nrc, l / d.nrc);
-    else
-        ts_gemv_body<long long, 2, true>(d.X, d.N, d.alpha, d.rsv, d.gr, d.part_c, d.part_r, nullptr, nullptr,
-                                         nullptr, l % d.nrc, l / d.nrc);
+    if (sv_narrow(d)) {
+        if (MODE == 1)
+            ts_gemv_body<uint32_t, 1, false>(d.x32, d.N, d.alpha, nullptr, d.gr, d.part_c, d.part_r, d.gpos,
+                                             (uint32_t*)d.xc, d.ng_p, l % d.nrc, l / d.nrc);
+        else
+            ts_gemv_body<uint32_t, 2, true>(d.x32, d.N, d.alpha, d.rsv, d.gr, d.part_c, d.part_r, nullptr, nullptr,
+                                            nullptr, l % d.nrc, l / d.nrc);
+    } else {
+        if (MODE == 1)
+            ts_gemv_body<long long, 1, false>(d.X, d.N, d.alpha, nullptr, d.gr, d.part_c, d.part_r, d.gpos, d.xc,
+                                              d.ng_p, l % d.nrc, l / d.nrc);
+        else
+            ts_gemv_body<long long, 2, true>(d.X, d.N, d.alpha, d.rsv, d.gr, d.part_c, d.part_r, nullptr, nullptr,
+                                             nullptr, l % d.nrc, l / d.nrc);
+    }
 }
 template <int MODE>
 __global__ __launch_bounds__(256) void k_sv_gap_b(const SvDesc* __restrict__ D, const long long* __restrict__ off,
                                                   int nd) {
     const int c = sv_find(off, nd, blockIdx.x);
     const SvDesc& d = D[c];
-    ts_gap_body<long long, MODE>(d.xc, d.ng_p, d.glist, d.alpha, MODE == 2 ? d.sv : nullptr,
-                                 MODE == 2 ? d.gpart2 : d.gpart1, (long long)blockIdx.x - off[c], d.ggrid);
+    if (sv_narrow(d))
+        ts_gap_body<uint32_t, MODE>((const uint32_t*)d.xc, d.ng_p, d.glist, d.alpha, MODE == 2 ? d.sv : nullptr,
+                                    MODE == 2 ? d.gpart2 : d.gpart1, (long long)blockIdx.x - off[c], d.ggrid);
+    else
+        ts_gap_body<long long, MODE>(d.xc, d.ng_p, d.glist, d.alpha, MODE == 2 ? d.sv : nullptr,
+                                     MODE == 2 ? d.gpart2 : d.gpart1, (long long)blockIdx.x - off[c], d.ggrid);
 }
 __global__ __launch_bounds__(1024) void k_sv_colsum_b(const SvDesc* __restrict__ D, const long long* __restrict__ off,
                                                       int nd) {
@@ -1256,15 +1289,23 @@ __global__ __launch_bounds__(256) void k_sv_rows_b(const SvDesc* __restrict__ D,
                                                    int nd, double exponent) {
     const int c = sv_find(off, nd, blockIdx.x);
     const SvDesc& d = D[c];
-    ts_rows_body<long long>(d.X, d.N, d.ncb, d.ccol, d.part_r, d.alpha, d.gpos, d.gpart1, d.ng_p, exponent,
-                            d.rowsum_in, d.sv, d.rsv, (long long)blockIdx.x - off[c]);
+    if (sv_narrow(d))
+        ts_rows_body<uint32_t>(d.x32, d.N, d.ncb, d.ccol, d.part_r, d.alpha, d.gpos, d.gpart1, d.ng_p, exponent,
+                               d.rowsum_in, d.sv, d.rsv, (long long)blockIdx.x - off[c]);
+    else
+        ts_rows_body<long long>(d.X, d.N, d.ncb, d.ccol, d.part_r, d.alpha, d.gpos, d.gpart1, d.ng_p, exponent,
+                                d.rowsum_in, d.sv, d.rsv, (long long)blockIdx.x - off[c]);
 }
 __global__ __launch_bounds__(256) void k_sv_q_b(const SvDesc* __restrict__ D, const long long* __restrict__ off,
                                                 int nd) {
     const int c = sv_find(off, nd, blockIdx.x);
     const SvDesc& d = D[c];
-    ts_q_body<long long>(d.X, d.N, d.ncb, d.part_r, d.alpha, d.sv, d.gpart2, d.ng_p, d.part,
-                         (long long)blockIdx.x - off[c]);
+    if (sv_narrow(d))
+        ts_q_body<uint32_t>(d.x32, d.N, d.ncb, d.part_r, d.alpha, d.sv, d.gpart2, d.ng_p, d.part,
+                            (long long)blockIdx.x - off[c]);
+    else
+        ts_q_body<long long>(d.X, d.N, d.ncb, d.part_r, d.alpha, d.sv, d.gpart2, d.ng_p, d.part,
+                             (long long)blockIdx.x - off[c]);
 }
 // k_slab_sum + k_symvc_scale of every chain (one block each; the same
 // fixed-order sum and the same IEEE operations)
@@ -1287,7 +1328,8 @@ __global__ __launch_bounds__(256) void k_sv_out_b(const SvDesc* __restrict__ D, 
     SymArgs a{d.N, d.nT, d.alpha, d.gap, d.sv, 1.0};
     a.scale_p = d.tot + 1;
     a.ng_p = d.ng_p;
-    symvc_out_body<long long>(d.X, a, d.out, (long long)blockIdx.x - off[c]);
+    if (sv_narrow(d)) symvc_out_body<uint32_t>(d.x32, a, d.out, (long long)blockIdx.x - off[c]);
+    else symvc_out_body<long long>(d.X, a, d.out, (long long)blockIdx.x - off[c]);
 }
 
 
@@ -1631,6 +1673,7 @@ int hh_twostep(const int64_t* TM, const int64_t* MM, const int64_t* PM, int64_t 
 extern "C++" {
 namespace {
 struct TsWork {
+    DBuf<uint32_t> x32[2];  // MM / PM as uint32 (shared-launch mode)
     DBuf<double> dsum, dA, draw;
     DBuf<long long> dz, dng;
     DBuf<uint8_t> dgf;
@@ -1678,8 +1721,13 @@ int hh_twostep_batch(int32_t n, const int64_t* const* TM, const int64_t* const* 
         // every buffer before the first launch (the pool hands out nothing
         // a launched chain still uses), the error flags zeroed on s0
         std::vector<TsWork> w((size_t)n);
-        DBuf<int> derr((size_t)n);
+        DBuf<int> derr((size_t)n), dovf((size_t)2 * n);
         HIP_CHECK(hipMemsetAsync(derr.p, 0, sizeof(int) * n, s0));
+        HIP_CHECK(hipMemsetAsync(dovf.p, 0, sizeof(int) * 2 * n, s0));
+        // the shared passes read 32-bit copies of MM / PM (hg19 40 kb genome
+        // 7.6 -> 7.0 ms; every pass on the copy beat the write pass on the
+        // int64 matrix, 7.4 ms: profiles/r5l2/)
+        const bool narrow = n_streams == 0;
         for (int c = 0; c < n; ++c) {
             const size_t Nc = (size_t)N[c];
             w[c].dsum.alloc(3 * Nc);
@@ -1690,6 +1738,8 @@ int hh_twostep_batch(int32_t n, const int64_t* const* TM, const int64_t* const* 
             w[c].dng.alloc(2);
             w[c].dA.alloc(Nc);
             w[c].draw.alloc(2);
+            if (narrow)
+                for (int h = 0; h < 2; ++h) w[c].x32[h].alloc(Nc * Nc);
         }
         // shared launches for the row statistics (every matrix's rows) and
         // the glue (every chromosome's gap flags, alpha, raw totals), then
@@ -1701,7 +1751,8 @@ int hh_twostep_batch(int32_t n, const int64_t* const* TM, const int64_t* const* 
             TsWork& x = w[c];
             const long long* d[3] = {(const long long*)TM[c], (const long long*)MM[c], (const long long*)PM[c]};
             for (int k = 0; k < 3; ++k) {
-                rs[3 * c + k] = RsDesc{d[k], N[c], x.dsum.p + k * N[c], x.dz.p + k * N[c]};
+                rs[3 * c + k] = RsDesc{d[k], N[c], x.dsum.p + k * N[c], x.dz.p + k * N[c],
+                                       narrow && k ? x.x32[k - 1].p : nullptr, narrow && k ? dovf.p + 2 * c + k - 1 : nullptr};
                 row0[3 * c + k + 1] = row0[3 * c + k] + N[c];
             }
             td[c] = TsDesc{N[c], x.dz.p, x.dsum.p, x.dgf.p, x.dgpos.p, x.dglist.p, x.dng.p, x.dA.p, x.draw.p,
@@ -1739,6 +1790,8 @@ int hh_twostep_batch(int32_t n, const int64_t* const* TM, const int64_t* const* 
                     SymvcWs& ws = h ? x.wp : x.wm;
                     SvDesc d{};
                     d.X = (const long long*)(h ? PM[c] : MM[c]);
+                    d.x32 = x.x32[h].p;
+                    d.ovf = dovf.p + 2 * c + h;
                     d.N = Nc;
                     d.gr = gr;
                     d.nrc = (Nc + gr - 1) / gr;
@@ -1748,7 +1801,9 @@ int hh_twostep_batch(int32_t n, const int64_t* const* TM, const int64_t* const* 
                     d.nT = (Nc + kT - 1) / kT;
                     d.npairs = d.nT * (d.nT + 1) / 2;
                     const long long nbtm = (Nc + kT - 1) / kT;  // the gap count's bound: N (device count)
-                    d.ggrid = std::min<long long>(std::max<long long>(nbtm * nbtm, 1), 2048);
+                    // (the gap passes grid-stride over the device gap count's
+                    // tiles: 64 blocks per chain, not one per possible tile)
+                    d.ggrid = std::min<long long>(std::max<long long>(nbtm * nbtm, 1), 64);
                     HH_REQUIRE(d.gcb < 65536 && d.npairs < (1LL << 31), "matrix too large");
                     ws.sv.alloc(Nc);
                     ws.tot.alloc(2);
