@@ -98,14 +98,15 @@ def config(name, nnz=None):
     return sizes, kw, label, target, tf
 
 
-SWEEP_KERNELS = ("k_sweep_tiled", "k_sweep_flat", "k_sweep_band", "k_sweep_uband")  # symmetric band: <8> once, <4> twice per sweep; upper band: <8>, <4> once each
+SWEEP_KERNELS = ("k_sweep_tiled", "k_sweep_flat", "k_sweep_band", "k_sweep_uband", "k_sweep_all")  # symmetric band: <8> once, <4> twice per sweep; upper band: <8>, <4> once each
 
 
 # sources whose code decides a line's HBM traffic: a committed PMC summary
 # counts for a run only when it was taken from these same sources on the same
 # workload (a stale summary must not be reported as this run's)
+_ICE_SOURCES = ("ice.hip", "ice_internal.hpp", "hh_common.hpp", "matrix.hip", "synth.hip", "build.hip")
 PMC_SOURCES = {
-    "c4": ("ice.hip", "ice_internal.hpp", "hh_common.hpp", "matrix.hip", "synth.hip", "build.hip"),
+    "c4": _ICE_SOURCES, "c4h": _ICE_SOURCES, "c3": _ICE_SOURCES, "c2": _ICE_SOURCES, "cis": _ICE_SOURCES,
     "gw": ("gw.hip", "pairs.hip", "hh_common.hpp", "ice_internal.hpp", "synth.hip"),
     "c5": ("comp.hip", "hh_common.hpp"),
 }
@@ -136,12 +137,13 @@ def pmc_pick(line, workload):
     return None
 
 
-def pmc_traffic(workload, kernels=SWEEP_KERNELS):
+def pmc_traffic(workload, kernels=SWEEP_KERNELS, line="c4"):
     """HBM bytes per ICE sweep (the sweep kernels, one launch each) from the
-    committed rocprofv3 PMC summary of the C4 bench taken at these sources on
-    this workload (tools/pmc_summary.py), its metadata (commit, the layout's
-    real bytes per sweep) and the file name; (None, None, None) without one."""
-    got = pmc_pick("c4", workload)
+    committed rocprofv3 PMC summary of the `line` bench (c4, c4h, c3, c2,
+    cis) taken at these sources on this workload (tools/pmc_summary.py), its
+    metadata (commit, the layout's real bytes per sweep) and the file name;
+    (None, None, None) without one."""
+    got = pmc_pick(line, workload)
     if got is None:
         return None, None, None
     data, meta, src = got
@@ -1482,8 +1484,8 @@ def main():
                        "tiles": inf["n_tiles"], "units": inf["n_units"],
                        "hbm_bytes_matrix": inf["device_bytes"]},
         }
-        traffic, meta, traffic_src = (pmc_traffic({"n_bins": n, "nnz_upper": nnz_total}) if args.config == "c4"
-                                      else (None, None, None))
+        traffic, meta, traffic_src = (pmc_traffic({"n_bins": n, "nnz_upper": nnz_total}, line=args.config)
+                                      if args.config in PMC_SOURCES else (None, None, None))
         if launches:
             # per launch on the slowest rank (= the whole matrix at N=1)
             sweep_avg = shard_sweep_ms / 1000.0
