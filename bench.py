@@ -1312,7 +1312,7 @@ def main():
     from hichap_master_amd import _lib, dist, ice
     _lib.load()
     _lib.call("hh_set_device", local)
-    for key in ("pca_p", "pca_method", "build_debug"):  # eigensolver / build-trace knobs (measurement)
+    for key in ("pca_p", "pca_method", "pca_debug", "build_debug"):  # eigensolver / build-trace knobs (measurement)
         if os.environ.get("HH_" + key.upper()):
             _lib.call("hh_tune", key.encode(), int(os.environ["HH_" + key.upper()]))
     if world > 1 or args.sharded:
