@@ -1829,18 +1829,24 @@ static void tridiagonalize(int m, std::vector<double>& A, Tridiag& T) {
         for (int i = k + 1; i < m; ++i) {
             const double* __restrict__ ai = &A[(size_t)i * m];
             const double vi = vr[i];
-            double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+            // the four partial sums and the axpy as one 4-wide vector each
+            // (lane q: elements j + q, the same IEEE operations in the same
+            // order as four scalar accumulators; the compiler's vectorisers
+            // left this loop scalar)
+            typedef double hd4 __attribute__((ext_vector_type(4)));
+            hd4 sv = {0.0, 0.0, 0.0, 0.0};
+            const hd4 viv = {vi, vi, vi, vi};
             int j = k + 1;
             for (; j + 4 <= i; j += 4) {
-                s0 += ai[j] * vr[j];
-                s1 += ai[j + 1] * vr[j + 1];
-                s2 += ai[j + 2] * vr[j + 2];
-                s3 += ai[j + 3] * vr[j + 3];
-                pr[j] += ai[j] * vi;
-                pr[j + 1] += ai[j + 1] * vi;
-                pr[j + 2] += ai[j + 2] * vi;
-                pr[j + 3] += ai[j + 3] * vi;
+                hd4 a, x, q;
+                __builtin_memcpy(&a, ai + j, sizeof(a));
+                __builtin_memcpy(&x, vr + j, sizeof(x));
+                __builtin_memcpy(&q, pr + j, sizeof(q));
+                sv += a * x;
+                q += a * viv;
+                __builtin_memcpy(pr + j, &q, sizeof(q));
             }
+            double s0 = sv.x, s1 = sv.y, s2 = sv.z, s3 = sv.w;
             for (; j < i; ++j) {
                 s0 += ai[j] * vr[j];
                 pr[j] += ai[j] * vi;
