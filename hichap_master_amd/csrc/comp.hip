@@ -1596,10 +1596,14 @@ __global__ __launch_bounds__(256) void k_ortho(OrthoArgs Ain) {
                 const double rjj = dd * y;
                 const double rjc = c == j ? rjj : (c > j ? gcol[j] * y : 0.0);
                 rcol[j] = rjc;
+                // the trailing update without a lane predicate: lanes c < j
+                // have rjc = 0, and lane j's column is not read again (its
+                // pivot and rcol are final), so only lanes c > j matter and
+                // they take the same fma as before (no selects per element)
 #pragma unroll
                 for (int a = j + 1; a < B; ++a) {
                     const double rja = readlane_d(rjc, a);
-                    if (c > j) gcol[a] -= rja * rjc;
+                    gcol[a] -= rja * rjc;
                 }
             }
             if (lane < B) {
@@ -1832,7 +1836,8 @@ static void tridiagonalize(int m, std::vector<double>& A, Tridiag& T) {
             // the four partial sums and the axpy as one 4-wide vector each
             // (lane q: elements j + q, the same IEEE operations in the same
             // order as four scalar accumulators; the compiler's vectorisers
-            // left this loop scalar)
+            // left this loop scalar.  Two rows interleaved, for two dot
+            // chains in flight, measured slower)
             typedef double hd4 __attribute__((ext_vector_type(4)));
             hd4 sv = {0.0, 0.0, 0.0, 0.0};
             const hd4 viv = {vi, vi, vi, vi};
@@ -1927,67 +1932,91 @@ static std::vector<double> tridiag_eigvals(std::vector<double> d, std::vector<do
     return d;
 }
 
-// eigenvector of the tridiagonal for eigenvalue lam: inverse iteration with
-// a Gaussian elimination with partial pivoting (two superdiagonals)
-static void tridiag_invit(const Tridiag& T, double lam, double tnorm, uint64_t seed, std::vector<double>& x) {
+// eigenvectors of the tridiagonal for the k eigenvalues lam[q]: inverse
+// iteration with a Gaussian elimination with partial pivoting (two
+// superdiagonals), the k shifts side by side (X[i * k + q]: lane q is one
+// independent solve; the pivot choice is a per-lane select, so each lane runs
+// exactly the operations of a solve on its own)
+static void tridiag_invit(const Tridiag& T, const double* lam, int k, double tnorm, std::vector<double>& X) {
     const int m = T.m;
     const double pert = std::max(tnorm, 1e-300) * 1e-14;
-    const double sh = lam + pert;
+    const size_t mk = (size_t)m * k;
     // rows: (sub a_i, diag b_i, sup c_i) of T - sh I
-    std::vector<double> l(m, 0.0), u0(m), u1(m, 0.0), u2(m, 0.0);
-    std::vector<char> piv(m, 0);
-    {
-        // LU with partial pivoting of the tridiagonal
-        std::vector<double> b(m), c(m, 0.0), a(m, 0.0);
-        for (int i = 0; i < m; ++i) b[i] = T.d[i] - sh;
-        for (int i = 0; i + 1 < m; ++i) c[i] = a[i + 1] = T.e[i];
-        // current row i holds (u0 = diag, u1 = sup, u2 = sup2)
-        double cd = b[0], cs = m > 1 ? c[0] : 0.0, cs2 = 0.0;
-        for (int i = 0; i < m; ++i) {
-            if (i == m - 1) {
-                u0[i] = cd == 0.0 ? pert : cd;
-                u1[i] = u2[i] = 0.0;
-                break;
-            }
-            const double na = a[i + 1], nb = b[i + 1], nc = i + 2 < m ? c[i + 1] : 0.0;
-            if (std::fabs(na) > std::fabs(cd)) {  // swap rows i and i+1
-                piv[i] = 1;
-                u0[i] = na; u1[i] = nb; u2[i] = nc;
-                const double f = cd / na;
-                l[i] = f;
-                cd = cs - f * nb;
-                cs = cs2 - f * nc;
-                cs2 = 0.0;
-            } else {
-                if (cd == 0.0) cd = pert;
-                u0[i] = cd; u1[i] = cs; u2[i] = cs2;
-                const double f = na / cd;
-                l[i] = f;
-                cd = nb - f * cs;
-                cs = nc - f * cs2;
-                cs2 = 0.0;
-            }
+    std::vector<double> l(mk, 0.0), u0(mk), u1(mk, 0.0), u2(mk, 0.0), sh(k), cd(k), cs(k), cs2(k, 0.0);
+    std::vector<unsigned char> piv(mk, 0);
+    for (int q = 0; q < k; ++q) {
+        sh[q] = lam[q] + pert;
+        cd[q] = T.d[0] - sh[q];
+        cs[q] = m > 1 ? T.e[0] : 0.0;
+    }
+    // LU with partial pivoting; the current row i holds (cd = diag, cs = sup,
+    // cs2 = sup2)
+    for (int i = 0; i + 1 < m; ++i) {
+        const double na = T.e[i], nc = i + 2 < m ? T.e[i + 1] : 0.0;
+        double* __restrict__ li = &l[(size_t)i * k];
+        double* __restrict__ a0 = &u0[(size_t)i * k];
+        double* __restrict__ a1 = &u1[(size_t)i * k];
+        double* __restrict__ a2 = &u2[(size_t)i * k];
+        unsigned char* __restrict__ pv = &piv[(size_t)i * k];
+        for (int q = 0; q < k; ++q) {
+            const double nb = T.d[i + 1] - sh[q];
+            const bool sw = std::fabs(na) > std::fabs(cd[q]);  // swap rows i and i+1
+            const double cdk = cd[q] == 0.0 ? pert : cd[q];     // (kept row: a zero pivot perturbed)
+            const double f = sw ? cd[q] / na : na / cdk;
+            pv[q] = sw ? 1 : 0;
+            a0[q] = sw ? na : cdk;
+            a1[q] = sw ? nb : cs[q];
+            a2[q] = sw ? nc : cs2[q];
+            li[q] = f;
+            const double ncd = sw ? cs[q] - f * nb : nb - f * cs[q];
+            const double ncs = sw ? cs2[q] - f * nc : nc - f * cs2[q];
+            cd[q] = ncd;
+            cs[q] = ncs;
+            cs2[q] = 0.0;
         }
     }
-    x.assign(m, 0.0);
-    for (int i = 0; i < m; ++i) x[i] = 1.0 + 0.1 * ((double)u01(mix64(seed + (uint64_t)i)) - 0.5);
+    for (int q = 0; q < k; ++q) u0[(size_t)(m - 1) * k + q] = cd[q] == 0.0 ? pert : cd[q];
+    X.assign(mk, 0.0);
+    for (int i = 0; i < m; ++i)
+        for (int q = 0; q < k; ++q)
+            X[(size_t)i * k + q] = 1.0 + 0.1 * ((double)u01(mix64(0x7e57ULL * (q + 1) + (uint64_t)i)) - 0.5);
+    std::vector<double> nn(k);
     for (int it = 0; it < 3; ++it) {
         // forward: apply the row operations
         for (int i = 0; i + 1 < m; ++i) {
-            if (piv[i]) std::swap(x[i], x[i + 1]);
-            x[i + 1] -= l[i] * x[i];
+            double* __restrict__ x0 = &X[(size_t)i * k];
+            double* __restrict__ x1 = x0 + k;
+            const double* __restrict__ li = &l[(size_t)i * k];
+            const unsigned char* __restrict__ pv = &piv[(size_t)i * k];
+            for (int q = 0; q < k; ++q) {
+                const double a = pv[q] ? x1[q] : x0[q], b = pv[q] ? x0[q] : x1[q];
+                x0[q] = a;
+                x1[q] = b - li[q] * a;
+            }
         }
         // back substitution with U
         for (int i = m - 1; i >= 0; --i) {
-            double s = x[i];
-            if (i + 1 < m) s -= u1[i] * x[i + 1];
-            if (i + 2 < m) s -= u2[i] * x[i + 2];
-            x[i] = s / u0[i];
+            double* __restrict__ xi = &X[(size_t)i * k];
+            const double* __restrict__ a0 = &u0[(size_t)i * k];
+            const double* __restrict__ a1 = &u1[(size_t)i * k];
+            const double* __restrict__ a2 = &u2[(size_t)i * k];
+            if (i + 2 < m) {
+                const double* __restrict__ x1 = xi + k;
+                const double* __restrict__ x2 = xi + 2 * k;
+                for (int q = 0; q < k; ++q) xi[q] = ((xi[q] - a1[q] * x1[q]) - a2[q] * x2[q]) / a0[q];
+            } else if (i + 1 < m) {
+                const double* __restrict__ x1 = xi + k;
+                for (int q = 0; q < k; ++q) xi[q] = (xi[q] - a1[q] * x1[q]) / a0[q];
+            } else {
+                for (int q = 0; q < k; ++q) xi[q] = xi[q] / a0[q];
+            }
         }
-        double nn = 0.0;
-        for (double v : x) nn += v * v;
-        nn = 1.0 / std::sqrt(nn);
-        for (double& v : x) v *= nn;
+        for (int q = 0; q < k; ++q) nn[q] = 0.0;
+        for (int i = 0; i < m; ++i)
+            for (int q = 0; q < k; ++q) nn[q] += X[(size_t)i * k + q] * X[(size_t)i * k + q];
+        for (int q = 0; q < k; ++q) nn[q] = 1.0 / std::sqrt(nn[q]);
+        for (int i = 0; i < m; ++i)
+            for (int q = 0; q < k; ++q) X[(size_t)i * k + q] *= nn[q];
     }
 }
 
@@ -2001,33 +2030,44 @@ static void sym_topk(int m, std::vector<double> H, int k, std::vector<double>& e
     for (int i = 0; i < m; ++i)
         tnorm = std::max(tnorm, std::fabs(T.d[i]) + (i ? std::fabs(T.e[i - 1]) : 0.0) + std::fabs(T.e[i]));
     evals.assign(ev.begin(), ev.begin() + k);
-    evecs.assign((size_t)m * k, 0.0);  // column q of an m x k row-major matrix
-    std::vector<std::vector<double>> ys(k);
+    // column q of an m x k row-major matrix: the k inverse iterations side
+    // by side, Gram-Schmidt per vector, the reflectors applied to all k
+    tridiag_invit(T, ev.data(), k, tnorm, evecs);
+    std::vector<double> yq(m), yr(m);
     for (int q = 0; q < k; ++q) {
-        tridiag_invit(T, ev[q], tnorm, 0x7e57ULL * (q + 1), ys[q]);
+        for (int i = 0; i < m; ++i) yq[i] = evecs[(size_t)i * k + q];
         // two Gram-Schmidt passes against the previous vectors (clusters)
         for (int pass = 0; pass < 2; ++pass)
             for (int r = 0; r < q; ++r) {
                 double dot = 0.0;
-                for (int i = 0; i < m; ++i) dot += ys[q][i] * ys[r][i];
-                for (int i = 0; i < m; ++i) ys[q][i] -= dot * ys[r][i];
+                for (int i = 0; i < m; ++i) dot += yq[i] * evecs[(size_t)i * k + r];
+                for (int i = 0; i < m; ++i) yq[i] -= dot * evecs[(size_t)i * k + r];
             }
         double nn = 0.0;
-        for (double v : ys[q]) nn += v * v;
+        for (double v : yq) nn += v * v;
         nn = 1.0 / std::sqrt(nn);
-        for (double& v : ys[q]) v *= nn;
-        // back-transform: x = P_0 P_1 ... P_{m-3} y
-        std::vector<double>& x = ys[q];
-        std::vector<double> y = x;
-        for (int kk = m - 3; kk >= 0; --kk) {
-            if (T.beta[kk] == 0.0) continue;
-            const double* v = &T.V[(size_t)kk * m];
-            double dot = 0.0;
-            for (int i = kk + 1; i < m; ++i) dot += v[i] * y[i];
-            dot *= T.beta[kk];
-            for (int i = kk + 1; i < m; ++i) y[i] -= dot * v[i];
+        for (int i = 0; i < m; ++i) evecs[(size_t)i * k + q] = yq[i] * nn;
+    }
+    // back-transform: x = P_0 P_1 ... P_{m-3} y, every column at once (per
+    // column the same dot and update order as one vector at a time)
+    std::vector<double> dot(k);
+    for (int kk = m - 3; kk >= 0; --kk) {
+        if (T.beta[kk] == 0.0) continue;
+        const double* __restrict__ v = &T.V[(size_t)kk * m];
+        double* __restrict__ dq = dot.data();
+        double* __restrict__ Yb = evecs.data();
+        for (int q = 0; q < k; ++q) dq[q] = 0.0;
+        for (int i = kk + 1; i < m; ++i) {
+            const double vi = v[i];
+            const double* __restrict__ yi = Yb + (size_t)i * k;
+            for (int q = 0; q < k; ++q) dq[q] += vi * yi[q];
         }
-        for (int i = 0; i < m; ++i) evecs[(size_t)i * k + q] = y[i];
+        for (int q = 0; q < k; ++q) dq[q] *= T.beta[kk];
+        for (int i = kk + 1; i < m; ++i) {
+            const double vi = v[i];
+            double* __restrict__ yi = Yb + (size_t)i * k;
+            for (int q = 0; q < k; ++q) yi[q] -= dq[q] * vi;
+        }
     }
 }
 
@@ -2395,9 +2435,38 @@ static bool pca_krylov(PcaWork& wk, const double* cor, long long n, int k, doubl
         // Xc Q = Q_+ S with row 0 (the 1/sqrt(n) coordinate) removed
         for (int c = 0; c < m; ++c) St[(size_t)c * ldS] = 0.0;
         std::vector<double> H((size_t)mb * mb, 0.0);
+        // four columns b at a time: four independent dot chains in flight,
+        // each summed over r in order as one column alone
         for (int a = 0; a < mb; ++a) {
-            const double* sa = &St[(size_t)a * ldS];
-            for (int b = a; b < mb; ++b) {
+            const double* __restrict__ sa = &St[(size_t)a * ldS];
+            int b = a;
+            for (; b + 4 <= mb; b += 4) {
+                const double* __restrict__ s0 = &St[(size_t)b * ldS];
+                const double* __restrict__ s1 = s0 + ldS;
+                const double* __restrict__ s2 = s1 + ldS;
+                const double* __restrict__ s3 = s2 + ldS;
+                const int L0 = std::min(slen[a], slen[b]), L1 = std::min(slen[a], slen[b + 1]),
+                          L2 = std::min(slen[a], slen[b + 2]), L3 = std::min(slen[a], slen[b + 3]);
+                const int Lc = std::min(std::min(L0, L1), std::min(L2, L3));
+                double c0 = 0.0, c1 = 0.0, c2 = 0.0, c3 = 0.0;
+                int r = 0;
+                for (; r < Lc; ++r) {
+                    const double x = sa[r];
+                    c0 += x * s0[r];
+                    c1 += x * s1[r];
+                    c2 += x * s2[r];
+                    c3 += x * s3[r];
+                }
+                for (int q = r; q < L0; ++q) c0 += sa[q] * s0[q];
+                for (int q = r; q < L1; ++q) c1 += sa[q] * s1[q];
+                for (int q = r; q < L2; ++q) c2 += sa[q] * s2[q];
+                for (int q = r; q < L3; ++q) c3 += sa[q] * s3[q];
+                H[(size_t)a * mb + b] = H[(size_t)b * mb + a] = c0;
+                H[(size_t)a * mb + b + 1] = H[(size_t)(b + 1) * mb + a] = c1;
+                H[(size_t)a * mb + b + 2] = H[(size_t)(b + 2) * mb + a] = c2;
+                H[(size_t)a * mb + b + 3] = H[(size_t)(b + 3) * mb + a] = c3;
+            }
+            for (; b < mb; ++b) {
                 const double* sb = &St[(size_t)b * ldS];
                 const int L = std::min(slen[a], slen[b]);
                 double acc = 0.0;
