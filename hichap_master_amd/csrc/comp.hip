@@ -1731,16 +1731,22 @@ __global__ __launch_bounds__(256) void k_ortho(OrthoArgs Ain) {
         // residual's Gram is computed directly and shifted CholeskyQR3 runs,
         // as in the round-3 path.  Pass B's Gram (Q1 against Qa) has no
         // cancellation: Q1 is orthonormal to the working accuracy of pass A.
-        auto lowsync_pass = [&](double* cout, double* R3, int* fl, bool shifted) -> bool {
+        auto lowsync_pass = [&](double* cout, double* R3, int* fl, bool shifted, int so) -> bool {
+            stamp(so);
             proj_part();
+            stamp(so + 1);
             gram_into_proj();
             reduce_proj(cout, 1);
+            stamp(so + 2);
             double gwmax = 0.0;
 #pragma unroll
             for (int i = 0; i < B; ++i) gwmax = fmax(gwmax, L.cm[A_nb * BB + i * B + i]);
             pythagoras();
+            stamp(so + 3);
             mul_q(false);
+            stamp(so + 4);
             chol(shifted, R3, fl);
+            stamp(so + 5);
             double mx = 0.0, mn = 1e300;
 #pragma unroll
             for (int i = 0; i < B; ++i) {
@@ -1753,6 +1759,7 @@ __global__ __launch_bounds__(256) void k_ortho(OrthoArgs Ain) {
                 return false;
             }
             apply_rinv();
+            stamp(so + 6);
             if (g == 0) {
                 R3[BB + t] = (t / B == t % B) ? 1.0 : 0.0;
                 R3[2 * BB + t] = (t / B == t % B) ? 1.0 : 0.0;
@@ -1760,8 +1767,8 @@ __global__ __launch_bounds__(256) void k_ortho(OrthoArgs Ain) {
             }
             return true;
         };
-        if (!lowsync_pass(A_c1, A_R, A_fail, true)) scholqr3_direct(A_R, A_fail);
-        if (!lowsync_pass(A_c2, A_R + 3 * BB, A_fail + 3, false)) scholqr3_direct(A_R + 3 * BB, A_fail + 3);
+        if (!lowsync_pass(A_c1, A_R, A_fail, true, 20)) scholqr3_direct(A_R, A_fail);
+        if (!lowsync_pass(A_c2, A_R + 3 * BB, A_fail + 3, false, 28)) scholqr3_direct(A_R + 3 * BB, A_fail + 3);
         store_rows(A_qnext);
     } else if (MODE == kOrthoFull) {
         // pass A: X = W - Qa c1, shifted CholQR3 -> Q1 (factors R0..R2)
@@ -2279,6 +2286,12 @@ static bool pca_krylov(PcaWork& wk, const double* cor, long long n, int k, doubl
             fprintf(stderr, " | barriers %d total %.1f | pass: gram %.1f sync %.1f reduce %.1f chol %.1f apply %.1f\n",
                     nb_, (h[39] - h[0]) / 100.0, (h[41] - h[40]) / 100.0, (h[42] - h[41]) / 100.0,
                     (h[43] - h[42]) / 100.0, (h[44] - h[43]) / 100.0, (h[45] - h[44]) / 100.0);
+            if (mode == kOrthoFull && g_ortho_lowsync)
+                for (int so : {20, 28})
+                    fprintf(stderr, "[ortho-ls] nb=%d pass=%d us: proj %.2f gram+reduce %.2f pyth %.2f mulq %.2f chol %.2f apply %.2f\n",
+                            a.nb, so == 28, (h[so + 1] - h[so]) / 100.0, (h[so + 2] - h[so + 1]) / 100.0,
+                            (h[so + 3] - h[so + 2]) / 100.0, (h[so + 4] - h[so + 3]) / 100.0,
+                            (h[so + 5] - h[so + 4]) / 100.0, (h[so + 6] - h[so + 5]) / 100.0);
         }
     };
     auto check_abort = [&](const std::vector<int>& flags) {
