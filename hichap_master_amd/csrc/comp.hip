@@ -19,6 +19,7 @@
 // All reductions are fixed-order (deterministic).
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <cmath>
 #include <limits>
@@ -1297,10 +1298,27 @@ struct OrthoArgs {
     int nblk = 0;
     double shift_scale = 0.0;
     long long* tstamp = nullptr;  // pca_debug >= 2: block 0's clock at the start, around each barrier, at the end
+    int pre = 1;                  // FullLS basis-row prefetch: 0 off, 1 mul_q's, 2 also pass B's proj_part
 };
 
-// grid barrier (all blocks co-resident); bounded wait
-__device__ __forceinline__ void ortho_grid_sync(unsigned long long* ctr, unsigned long long target, int* abort) {
+// HH_ORTHO_PRE (environment, read once): OrthoArgs::pre for the experiments.
+// Measured (profiles/r5s, serial k_ortho per C5 pass): 0 84.2 ms, 1 81.2 ms,
+// 2 81.6 ms -- the prefetched rows make mul_q ~3x faster but queue ahead of
+// the reduction's loads, so the reduction gets slower by most of it
+static int ortho_pre_level() {
+    static const int v = [] {
+        const char* e = std::getenv("HH_ORTHO_PRE");
+        return e ? std::atoi(e) : 1;
+    }();
+    return v;
+}
+
+// grid barrier (all blocks co-resident); bounded wait.  `between` runs after
+// this block's arrival and before its wait (loads issued there do not hold
+// up the arrival's release fence)
+template <typename F>
+__device__ __forceinline__ void ortho_grid_sync(unsigned long long* ctr, unsigned long long target, int* abort,
+                                                F&& between) {
     __syncthreads();
     if (threadIdx.x == 0) {
         // release only: this block's partials reach memory.  No acquire
@@ -1309,6 +1327,9 @@ __device__ __forceinline__ void ortho_grid_sync(unsigned long long* ctr, unsigne
         // are read with agent-scope atomic loads (ld_agent) instead
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         atomicAdd(ctr, 1ull);
+    }
+    between();
+    if (threadIdx.x == 0) {
         unsigned spins = 0;
         while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
             __builtin_amdgcn_s_sleep(1);
@@ -1370,6 +1391,7 @@ __global__ __launch_bounds__(256) void k_ortho(OrthoArgs Ain) {
     const auto A_tstamp = Ain.tstamp;
     const auto A_xin = Ain.xin;
     const auto A_xout = Ain.xout;
+    const int A_pre = Ain.pre;
 
     constexpr int B = kSB, BB = kSB * kSB, RPB = 64 * TPB;
     __shared__ OrthoLds<TPB> L;
@@ -1382,12 +1404,13 @@ __global__ __launch_bounds__(256) void k_ortho(OrthoArgs Ain) {
     };
     stamp(0);
     if (g == 0 && t == 0) A_ctr[1 - A_par] = 0ull;  // the previous launch's counter (it has completed)
-    auto gsync = [&]() __attribute__((always_inline)) {
+    auto gsync_then = [&](auto&& between) __attribute__((always_inline)) {
         ++bar;
         stamp(2 * bar - 1);
-        ortho_grid_sync(A_ctr + A_par, (unsigned long long)bar * (unsigned long long)nblk, A_abort);
+        ortho_grid_sync(A_ctr + A_par, (unsigned long long)bar * (unsigned long long)nblk, A_abort, between);
         stamp(2 * bar);
     };
+    auto gsync = [&]() __attribute__((always_inline)) { gsync_then([] {}); };
     // ---- block-local pieces
     auto gram_part = [&](double* dst) __attribute__((always_inline)) {  // dst[g][256] = X^T X over the block's rows
         d4 acc = d4{0.0, 0.0, 0.0, 0.0};
@@ -1484,6 +1507,99 @@ __global__ __launch_bounds__(256) void k_ortho(OrthoArgs Ain) {
         }
         __syncthreads();
     };
+    // FullLS at TPB <= 2: the block's basis rows for the next proj_part /
+    // mul_q are loaded ahead of the step before them (the row loads, a grid
+    // reduction, the Cholesky), so their round trip overlaps it.  The same
+    // MFMAs on the same operands in the same order as proj_part / mul_q
+    // (bitwise the same results); nb <= 8 blocks in one register set.
+    constexpr bool kPre = MODE == kOrthoFullLS && TPB <= 2;
+    constexpr int kPT = kPre ? TPB : 1, kPK = kPre ? 8 : 4;
+    double qb[kPK][kPT][4];
+    auto pre_proj = [&]() __attribute__((always_inline)) {  // proj_part's operand layout
+        const int nb = A_nb;
+#pragma unroll
+        for (int k = 0; k < kPK; ++k)
+#pragma unroll
+            for (int m = 0; m < kPT; ++m)
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const long long i = r0 + (w + 4 * m) * 16 + 4 * c + lr;
+                    qb[k][m][c] = (k < nb && i < n) ? A_Q[((size_t)k * n + i) * B + lc] : 0.0;
+                }
+    };
+    auto pre_mul = [&]() __attribute__((always_inline)) {  // mul_q's operand layout
+        const int nb = A_nb;
+#pragma unroll
+        for (int k = 0; k < kPK; ++k)
+#pragma unroll
+            for (int m = 0; m < kPT; ++m) {
+                const long long i = r0 + (w + 4 * m) * 16 + lc;
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj)
+                    qb[k][m][jj] = (k < nb && i < n) ? A_Q[((size_t)k * n + i) * B + 4 * jj + lr] : 0.0;
+            }
+    };
+    auto proj_part_pre = [&]() __attribute__((always_inline)) {
+        const int nb = A_nb;
+#pragma unroll
+        for (int kc = 0; kc < kPK; kc += 4) {
+            if (kc < nb) {
+                d4 acc[4];
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk) acc[kk] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                for (int m = 0; m < kPT; ++m)
+#pragma unroll
+                    for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+                        for (int c = 0; c < 4; ++c)
+                            acc[kk] = __builtin_amdgcn_mfma_f64_16x16x4f64(
+                                qb[kc + kk][m][c], L.x[(w + 4 * m) * 16 + 4 * c + lr][lc], acc[kk], 0, 0, 0);
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk)
+                    if (kc + kk < nb)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) L.ws[w][(kc + kk) * BB + (lr + 4 * r) * B + lc] = acc[kk][r];
+            }
+        }
+        __syncthreads();
+        for (int e = t; e < nb * BB; e += 256)
+            A_rpart[(size_t)g * kOrthoMaxE + e] = ((L.ws[0][e] + L.ws[1][e]) + L.ws[2][e]) + L.ws[3][e];
+        __syncthreads();
+    };
+    auto mul_q_pre = [&](bool add) __attribute__((always_inline)) {
+        const int nb = A_nb;
+        d4 acc[kPT];
+#pragma unroll
+        for (int m = 0; m < kPT; ++m) acc[m] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int kc = 0; kc < kPK; kc += 4) {
+            if (kc < nb) {
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk) {
+                    double bcol[4];
+#pragma unroll
+                    for (int jj = 0; jj < 4; ++jj)
+                        bcol[jj] = kc + kk < nb ? L.cm[(kc + kk) * BB + (4 * jj + lr) * B + lc] : 0.0;
+#pragma unroll
+                    for (int m = 0; m < kPT; ++m)
+#pragma unroll
+                        for (int jj = 0; jj < 4; ++jj)
+                            acc[m] = __builtin_amdgcn_mfma_f64_16x16x4f64(qb[kc + kk][m][jj], bcol[jj], acc[m], 0, 0, 0);
+                }
+            }
+        }
+#pragma unroll
+        for (int m = 0; m < kPT; ++m) {
+            const int rb = (w + 4 * m) * 16;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                double& x = L.x[rb + lr + 4 * r][lc];
+                x = add ? acc[m][r] : x - acc[m][r];
+            }
+        }
+        __syncthreads();
+    };
     // L.gs = sum over blocks of gp (fixed block order), every block; all
     // nblk loads in flight at once
     auto reduce_gram = [&](const double* gp) __attribute__((always_inline)) {
@@ -1498,8 +1614,8 @@ __global__ __launch_bounds__(256) void k_ortho(OrthoArgs Ain) {
     };
     // nb x 256 projection sums: barrier, reduce-scatter over the blocks,
     // barrier, every block reads all of them into L.cm (block 0 also to `out`)
-    auto reduce_proj = [&](double* out, int extra = 0) __attribute__((always_inline)) {
-        gsync();  // every block's partials are in
+    auto reduce_proj_then = [&](double* out, int extra, auto&& between) __attribute__((always_inline)) {
+        gsync_then(between);  // every block's partials are in
         const int E = (A_nb + extra) * BB, chunk = (E + nblk - 1) / nblk;
         const int e1 = min(E, (g + 1) * chunk);
         for (int e = g * chunk + t; e < e1; e += 256) {
@@ -1534,6 +1650,9 @@ __global__ __launch_bounds__(256) void k_ortho(OrthoArgs Ain) {
             if (g == 0 && e < A_nb * BB) out[e] = v;
         }
         __syncthreads();
+    };
+    auto reduce_proj = [&](double* out, int extra = 0) __attribute__((always_inline)) {
+        reduce_proj_then(out, extra, [] {});
     };
     // low-synch passes (one reduction per pass): the block's Gram X^T X as
     // coefficient block nb of its projection partials, reduced in the same
@@ -1690,6 +1809,8 @@ __global__ __launch_bounds__(256) void k_ortho(OrthoArgs Ain) {
         }
     };
     // ---- the block's rows in
+    if constexpr (kPre)
+        if (A_pre >= 1) pre_proj();  // (pass A's basis rows first: in flight with W's)
     if (MODE != kOrthoRitz) {  // W (Full / Last) or the start block
         // all the block's row loads in flight at once (clamped rows, zeroed
         // by a 0 / 1 factor: `i < n ? load : 0` compiled to one round trip
@@ -1733,17 +1854,25 @@ __global__ __launch_bounds__(256) void k_ortho(OrthoArgs Ain) {
         // cancellation: Q1 is orthonormal to the working accuracy of pass A.
         auto lowsync_pass = [&](double* cout, double* R3, int* fl, bool shifted, int so) -> bool {
             stamp(so);
-            proj_part();
+            const bool pre = kPre && A_pre >= 1;
+            if (pre && (so == 20 || A_pre >= 2)) proj_part_pre();
+            else proj_part();
             stamp(so + 1);
             gram_into_proj();
-            reduce_proj(cout, 1);
+            if (pre) reduce_proj_then(cout, 1, pre_mul);  // mul_q's rows in flight across the barrier
+            else reduce_proj(cout, 1);
             stamp(so + 2);
             double gwmax = 0.0;
 #pragma unroll
             for (int i = 0; i < B; ++i) gwmax = fmax(gwmax, L.cm[A_nb * BB + i * B + i]);
             pythagoras();
             stamp(so + 3);
-            mul_q(false);
+            if (pre) {
+                mul_q_pre(false);
+                if (so == 20 && A_pre >= 2) pre_proj();  // pass B's basis rows, in flight across the Cholesky
+            } else {
+                mul_q(false);
+            }
             stamp(so + 4);
             chol(shifted, R3, fl);
             stamp(so + 5);
@@ -2252,6 +2381,7 @@ static bool pca_krylov(PcaWork& wk, const double* cor, long long n, int k, doubl
         a.nblk = oblk;
         a.shift_scale = shift_scale;
         a.tstamp = g_pca_debug >= 2 ? tst.p : nullptr;
+        a.pre = ortho_pre_level();
         HH_REQUIRE(a.nb >= 0 && a.nb <= 8 && oblk >= 1 && oblk <= kOrthoMaxBlocks, "k_ortho shape");
         const dim3 grid((unsigned)oblk), blk(256);
         HH_KTIME("k_ortho", s);  // bench.py's C5 line: the dominant kernel by time
