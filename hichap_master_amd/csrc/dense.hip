@@ -41,8 +41,7 @@ __device__ __forceinline__ void rowstats_row(const T* __restrict__ X, long long 
     double sd = 0.0;
     long long si = 0;
     bool bad = false;
-    for (long long j = a + threadIdx.x; j < b; j += 256) {
-        const T v = row[j];
+    auto take = [&](T v, long long j) __attribute__((always_inline)) {
         zc += v == T(0);
         if constexpr (std::is_integral_v<T>) {
             si += (long long)v;  // integer: exact
@@ -53,7 +52,18 @@ __device__ __forceinline__ void rowstats_row(const T* __restrict__ X, long long 
         } else {
             sd += (double)v;
         }
+    };
+    // four loads in flight per thread (each thread still takes its elements
+    // in ascending j: the same double sum)
+    long long j = a + threadIdx.x;
+    for (; j + 3 * 256 < b; j += 4 * 256) {
+        const T v0 = row[j], v1 = row[j + 256], v2 = row[j + 512], v3 = row[j + 768];
+        take(v0, j);
+        take(v1, j + 256);
+        take(v2, j + 512);
+        take(v3, j + 768);
     }
+    for (; j < b; j += 256) take(row[j], j);
     if (x32 && __ballot(bad) != 0ull && (threadIdx.x & 63) == 0) atomicOr(ovf, 1);
     // reduce
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -262,14 +272,18 @@ __global__ __launch_bounds__(256) void k_symvc(const T* __restrict__ X, SymArgs 
 
 // PASS 3 with one LDS tile (round 4, default; hh_tune "symvc_out"): both
 // tiles' X values are loaded into registers (lane = column, coalesced), the
-// (J, I) tile goes through LDS transposed for the (I, J) outputs, then the
-// (I, J) tile for the (J, I) outputs.  33 KB of LDS instead of 66 KB: 4
-// blocks per CU instead of 2.  The same operands and IEEE operations as
-// k_symvc<T, 3> (bitwise the same output).
+// (J, I) tile goes through LDS transposed for the (I, J) outputs.  Y and C are
+// symmetric, so each (J, I) output is the (I, J) output at the transposed
+// position -- the same operands and IEEE operations (round 5: computed once,
+// sent through the same LDS space transposed, instead of recomputing the two
+// true divisions of S and the third of C per element): bitwise k_symvc<T, 3>.
 template <class T>
 __device__ __forceinline__ void symvc_out_body(const T* __restrict__ X, const SymArgs& a, double* __restrict__ out,
                                                long long p) {
-    __shared__ T tt[kT][kT + 1];
+    __shared__ union {
+        T tt[kT][kT + 1];       // the (J, I) tile, transposed
+        double dt[kT][kT + 1];  // then the (I, J) outputs, transposed
+    } u;
     __shared__ TileVecs tv;
     long long I = 0, rem = p;
     while (rem >= a.nT - I) { rem -= a.nT - I; ++I; }
@@ -311,32 +325,27 @@ __device__ __forceinline__ void symvc_out_body(const T* __restrict__ X, const Sy
     const int lim_r = (int)std::min<long long>(kT, N - I0), lim_c = (int)std::min<long long>(kT, N - J0);
     // (I, J) outputs: S_ij = v / aI[r], S_ji = X[J0 + c][I0 + r] / aJ[c] = tt[r][c] / aJ[c]
 #pragma unroll
-    for (int k = 0; k < kT / 4; ++k) tt[c][r0 + 4 * k] = w[k];
+    for (int k = 0; k < kT / 4; ++k) u.tt[c][r0 + 4 * k] = w[k];
     __syncthreads();
+    double o[kT / 4];
 #pragma unroll
     for (int k = 0; k < kT / 4; ++k) {
         const int r = r0 + 4 * k;
-        if (r < lim_r && c < lim_c) {
-            const double sij = (double)v[k] / tv.aI[r], sji = (double)tt[r][c] / tv.aJ[c];
-            const double y = sym_value(diag_tile && r == c, has_gap, tv.gI[r], tv.gJ[c], sij, sji);
-            __builtin_nontemporal_store(scale * (y / (tv.sJ[c] * tv.sI[r])), &out[(I0 + r) * N + J0 + c]);
-        }
+        const double sij = (double)v[k] / tv.aI[r], sji = (double)u.tt[r][c] / tv.aJ[c];
+        const double y = sym_value(diag_tile && r == c, has_gap, tv.gI[r], tv.gJ[c], sij, sji);
+        o[k] = scale * (y / (tv.sJ[c] * tv.sI[r]));
+        if (r < lim_r && c < lim_c) __builtin_nontemporal_store(o[k], &out[(I0 + r) * N + J0 + c]);
     }
     if (diag_tile) return;
-    __syncthreads();
-    // (J, I) outputs: element (J0 + r, I0 + c) = Y[I0 + c][J0 + r];
-    // S[I0 + c][J0 + r] = tt[r][c] / aI[c], S[J0 + r][I0 + c] = w / aJ[r]
+    __syncthreads();  // every tt read done: the space takes the outputs
+    // (J, I) outputs: element (J0 + r, I0 + c) = C[I0 + c][J0 + r] (symmetric)
 #pragma unroll
-    for (int k = 0; k < kT / 4; ++k) tt[c][r0 + 4 * k] = v[k];
+    for (int k = 0; k < kT / 4; ++k) u.dt[c][r0 + 4 * k] = o[k];
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < kT / 4; ++k) {
         const int r = r0 + 4 * k;
-        if (r < lim_c && c < lim_r) {
-            const double sij = (double)tt[r][c] / tv.aI[c], sji = (double)w[k] / tv.aJ[r];
-            const double y = sym_value(false, has_gap, tv.gI[c], tv.gJ[r], sij, sji);
-            __builtin_nontemporal_store(scale * (y / (tv.sI[c] * tv.sJ[r])), &out[(J0 + r) * N + I0 + c]);
-        }
+        if (r < lim_c && c < lim_r) __builtin_nontemporal_store(u.dt[r][c], &out[(J0 + r) * N + I0 + c]);
     }
 }
 
