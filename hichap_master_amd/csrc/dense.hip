@@ -26,13 +26,15 @@ namespace hh {
 
 constexpr int kT = 64;  // dense tile edge
 
-// x32 (integer T only, may be null): the row copied as uint32; *ovf set
-// when a value does not fit (the later passes then read X itself)
+// x16 (integer T only, may be null): the row copied as uint16, a count >=
+// 0xFFFF stored as 0xFFFF (the passes that read the copy take such entries
+// from X itself); *ovf set when a value does not fit 32 bits (the later
+// passes then read X throughout)
 template <class T>
 __device__ __forceinline__ void rowstats_row(const T* __restrict__ X, long long N, long long i,
                                              const long long* __restrict__ lo, const long long* __restrict__ hi,
                                              double* __restrict__ sum, long long* __restrict__ zeros,
-                                             uint32_t* __restrict__ x32 = nullptr, int* __restrict__ ovf = nullptr) {
+                                             uint16_t* __restrict__ x16 = nullptr, int* __restrict__ ovf = nullptr) {
     __shared__ double shd[16];
     __shared__ long long shz[16];
     const long long a = lo ? lo[i] : 0, b = hi ? hi[i] : N;
@@ -45,9 +47,9 @@ __device__ __forceinline__ void rowstats_row(const T* __restrict__ X, long long 
         zc += v == T(0);
         if constexpr (std::is_integral_v<T>) {
             si += (long long)v;  // integer: exact
-            if (x32) {
+            if (x16) {
                 bad |= (unsigned long long)v > 0xFFFFFFFFull;  // (negative: huge as unsigned)
-                x32[i * N + j] = (uint32_t)v;
+                x16[i * N + j] = (uint16_t)((unsigned long long)v < 0xFFFFull ? v : 0xFFFF);
             }
         } else {
             sd += (double)v;
@@ -64,7 +66,7 @@ __device__ __forceinline__ void rowstats_row(const T* __restrict__ X, long long 
         take(v3, j + 768);
     }
     for (; j < b; j += 256) take(row[j], j);
-    if (x32 && __ballot(bad) != 0ull && (threadIdx.x & 63) == 0) atomicOr(ovf, 1);
+    if (x16 && __ballot(bad) != 0ull && (threadIdx.x & 63) == 0) atomicOr(ovf, 1);
     // reduce
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     zc = wave_sum_ll(zc);
@@ -96,7 +98,7 @@ struct RsDesc {
     long long N;
     double* sum;
     long long* zeros;
-    uint32_t* x32;  // null: no copy
+    uint16_t* x16;  // null: no copy
     int* ovf;
 };
 __global__ __launch_bounds__(256) void k_rowstats_b(const RsDesc* __restrict__ d, const long long* __restrict__ row0,
@@ -108,7 +110,7 @@ __global__ __launch_bounds__(256) void k_rowstats_b(const RsDesc* __restrict__ d
         if (row0[mid] <= b) lo = mid; else hi = mid - 1;
     }
     const RsDesc m = d[lo];
-    rowstats_row<long long>(m.X, m.N, b - row0[lo], nullptr, nullptr, m.sum, m.zeros, m.x32, m.ovf);
+    rowstats_row<long long>(m.X, m.N, b - row0[lo], nullptr, nullptr, m.sum, m.zeros, m.x16, m.ovf);
 }
 
 // Pair (I, J), I <= J, of an nT x nT tile grid -> linear index.
@@ -277,9 +279,9 @@ __global__ __launch_bounds__(256) void k_symvc(const T* __restrict__ X, SymArgs 
 // position -- the same operands and IEEE operations (round 5: computed once,
 // sent through the same LDS space transposed, instead of recomputing the two
 // true divisions of S and the third of C per element): bitwise k_symvc<T, 3>.
-template <class T>
-__device__ __forceinline__ void symvc_out_body(const T* __restrict__ X, const SymArgs& a, double* __restrict__ out,
-                                               long long p, int cnt = 1) {
+template <class T, class L = T>  // L: the element type read (see ts_gemv_body)
+__device__ __forceinline__ void symvc_out_body(const L* __restrict__ X, const SymArgs& a, double* __restrict__ out,
+                                               long long p, int cnt = 1, const long long* __restrict__ Xe = nullptr) {
     // `cnt` consecutive pairs p, p + 1, ...: the next pair's matrix loads are
     // issued before this pair's transposed outputs are written (two pairs per
     // block: 1.88 -> 1.86 ms per genome; plain stores instead of the
@@ -312,14 +314,34 @@ __device__ __forceinline__ void symvc_out_body(const T* __restrict__ X, const Sy
         for (int k = 0; k < kT / 4; ++k) {
             const int r = r0 + 4 * k;
             const long long gi = I0 + r, ti = J0 + r;
-            v[k] = X[(gi < N ? gi : N - 1) * N + cj];
-            w[k] = X[(ti < N ? ti : N - 1) * N + ci];
+            v[k] = (T)X[(gi < N ? gi : N - 1) * N + cj];
+            w[k] = (T)X[(ti < N ? ti : N - 1) * N + ci];
+        }
+    };
+    // escaped counts (rare): from the int64 matrix -- at the pair's first use
+    // of v / w, so a prefetched pair's loads stay in flight until then
+    auto patch = [&]() __attribute__((always_inline)) {
+        if constexpr (!std::is_same_v<L, T>) {
+            const long long cj = J0 + c < N ? J0 + c : N - 1, ci = I0 + c < N ? I0 + c : N - 1;
+            bool esc = false;
+#pragma unroll
+            for (int k = 0; k < kT / 4; ++k) esc |= (v[k] == (T)0xFFFF) | (w[k] == (T)0xFFFF);
+            if (__ballot(esc) != 0ull) {
+#pragma unroll
+                for (int k = 0; k < kT / 4; ++k) {
+                    const int r = r0 + 4 * k;
+                    const long long gi = I0 + r, ti = J0 + r;
+                    if (v[k] == (T)0xFFFF) v[k] = (T)Xe[(gi < N ? gi : N - 1) * N + cj];
+                    if (w[k] == (T)0xFFFF) w[k] = (T)Xe[(ti < N ? ti : N - 1) * N + ci];
+                }
+            }
         }
     };
     decode(p);
     load();
     for (int it = 0; it < cnt; ++it) {
         if (it) __syncthreads();  // the previous pair's LDS reads are done
+        patch();
         const long long cI0 = I0, cJ0 = J0;
         const bool diag_tile = cI0 == cJ0;
         if (threadIdx.x < kT) {
@@ -446,12 +468,14 @@ constexpr int kGB = 4 * kGW;  // columns per block: its 4 waves read 16 KB of a 
 //         integer X, stored in the double slot's bits); the both-gap entries
 //         X_ij (i, j gaps) copied to the compact g x g matrix Xc.
 // MODE 2: part_r[q][i] = sum over the span's columns of X_ij * rs_j.
-template <class T, int MODE, bool ROWS = true>
-__device__ __forceinline__ void ts_gemv_body(const T* __restrict__ X, long long N, const double* __restrict__ alpha,
+// L: the element type read (uint16_t: the batch's copy, 0xFFFF entries taken
+// from the int64 matrix Xe); T: the value type the pass computes with.
+template <class T, int MODE, bool ROWS = true, class L = T>
+__device__ __forceinline__ void ts_gemv_body(const L* __restrict__ X, long long N, const double* __restrict__ alpha,
                                              const double* __restrict__ rs, int gr, double* __restrict__ part_c,
                                              double* __restrict__ part_r, const int* __restrict__ gpos,
                                              T* __restrict__ Xc, const long long* __restrict__ ng_p, long long bx,
-                                             long long by) {
+                                             long long by, const long long* __restrict__ Xe = nullptr) {
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const long long rc = bx, q = by * 4 + w;
@@ -484,9 +508,25 @@ __device__ __forceinline__ void ts_gemv_body(const T* __restrict__ X, long long 
             // zero or masked where they are summed -- a select on the loaded
             // value lets the compiler sink each load into its own branch
             // with a vmcnt(0) wait (measured: 32 serialised loads)
-            const T* row = X + (okr ? i0 + b : rend - 1) * N + c0;
+            const L* row = X + (okr ? i0 + b : rend - 1) * N + c0;
 #pragma unroll
-            for (int k = 0; k < 8; ++k) x[b][k] = row[coff[k]];
+            for (int k = 0; k < 8; ++k) x[b][k] = (T)row[coff[k]];
+        }
+        if constexpr (!std::is_same_v<L, T>) {  // escaped counts (rare): from the int64 matrix
+            bool esc = false;
+#pragma unroll
+            for (int b = 0; b < kB; ++b)
+#pragma unroll
+                for (int k = 0; k < 8; ++k) esc |= x[b][k] == (T)0xFFFF;
+            if (__ballot(esc) != 0ull) {
+#pragma unroll
+                for (int b = 0; b < kB; ++b) {
+                    const long long* rowe = Xe + (i0 + b < rend ? i0 + b : rend - 1) * N + c0;
+#pragma unroll
+                    for (int k = 0; k < 8; ++k)
+                        if (x[b][k] == (T)0xFFFF) x[b][k] = (T)rowe[coff[k]];
+                }
+            }
         }
 #pragma unroll
         for (int b = 0; b < kB; ++b) {
@@ -1243,7 +1283,7 @@ __global__ __launch_bounds__(1024) void k_ts_alpha_b(const TsDesc* __restrict__ 
 // the per-chain launches: bitwise the same results.
 struct SvDesc {
     const long long* X;
-    const uint32_t* x32;  // the uint32 copy (k_rowstats_b), read unless *ovf
+    const uint16_t* x16;  // the uint16 copy with escapes (k_rowstats_b), read unless *ovf
     const int* ovf;
     long long N, nrc, gcb, ncb, nb, ggrid, npairs, nT;
     int gr;
@@ -1270,9 +1310,10 @@ __device__ __forceinline__ int sv_find(const long long* __restrict__ off, int nd
     return lo;
 }
 
-// the chain's matrix as uint32 (its k_rowstats_b copy) unless a value did
-// not fit; the same integers either way: bitwise the same doubles
-__device__ __forceinline__ bool sv_narrow(const SvDesc& d) { return d.x32 && *d.ovf == 0; }
+// the chain's matrix as its uint16 k_rowstats_b copy (0xFFFF entries from the
+// int64 matrix) unless a value did not fit 32 bits; the same integers either
+// way: bitwise the same doubles
+__device__ __forceinline__ bool sv_narrow(const SvDesc& d) { return d.x16 && *d.ovf == 0; }
 
 template <int MODE>
 __global__ __launch_bounds__(256) void k_sv_gemv_b(const SvDesc* __restrict__ D, const long long* __restrict__ off,
@@ -1282,11 +1323,11 @@ __global__ __launch_bounds__(256) void k_sv_gemv_b(const SvDesc* __restrict__ D,
     const long long l = (long long)blockIdx.x - off[c];
     if (sv_narrow(d)) {
         if (MODE == 1)
-            ts_gemv_body<uint32_t, 1, false>(d.x32, d.N, d.alpha, nullptr, d.gr, d.part_c, d.part_r, d.gpos,
-                                             (uint32_t*)d.xc, d.ng_p, l % d.nrc, l / d.nrc);
+            ts_gemv_body<uint32_t, 1, false, uint16_t>(d.x16, d.N, d.alpha, nullptr, d.gr, d.part_c, d.part_r, d.gpos,
+                                                       (uint32_t*)d.xc, d.ng_p, l % d.nrc, l / d.nrc, d.X);
         else
-            ts_gemv_body<uint32_t, 2, true>(d.x32, d.N, d.alpha, d.rsv, d.gr, d.part_c, d.part_r, nullptr, nullptr,
-                                            nullptr, l % d.nrc, l / d.nrc);
+            ts_gemv_body<uint32_t, 2, true, uint16_t>(d.x16, d.N, d.alpha, d.rsv, d.gr, d.part_c, d.part_r, nullptr,
+                                                      nullptr, nullptr, l % d.nrc, l / d.nrc, d.X);
     } else {
         if (MODE == 1)
             ts_gemv_body<long long, 1, false>(d.X, d.N, d.alpha, nullptr, d.gr, d.part_c, d.part_r, d.gpos, d.xc,
@@ -1314,27 +1355,21 @@ __global__ __launch_bounds__(1024) void k_sv_colsum_b(const SvDesc* __restrict__
     const SvDesc& d = D[c];
     ts_colsum_body(d.part_c, d.N, d.nrc, d.ccol, (long long)blockIdx.x - off[c]);
 }
+// (rows / q read only the diagonal of X: from the int64 matrix, the same
+// integers as the copy)
 __global__ __launch_bounds__(256) void k_sv_rows_b(const SvDesc* __restrict__ D, const long long* __restrict__ off,
                                                    int nd, double exponent) {
     const int c = sv_find(off, nd, blockIdx.x);
     const SvDesc& d = D[c];
-    if (sv_narrow(d))
-        ts_rows_body<uint32_t>(d.x32, d.N, d.ncb, d.ccol, d.part_r, d.alpha, d.gpos, d.gpart1, d.ng_p, exponent,
-                               d.rowsum_in, d.sv, d.rsv, (long long)blockIdx.x - off[c]);
-    else
-        ts_rows_body<long long>(d.X, d.N, d.ncb, d.ccol, d.part_r, d.alpha, d.gpos, d.gpart1, d.ng_p, exponent,
-                                d.rowsum_in, d.sv, d.rsv, (long long)blockIdx.x - off[c]);
+    ts_rows_body<long long>(d.X, d.N, d.ncb, d.ccol, d.part_r, d.alpha, d.gpos, d.gpart1, d.ng_p, exponent,
+                            d.rowsum_in, d.sv, d.rsv, (long long)blockIdx.x - off[c]);
 }
 __global__ __launch_bounds__(256) void k_sv_q_b(const SvDesc* __restrict__ D, const long long* __restrict__ off,
                                                 int nd) {
     const int c = sv_find(off, nd, blockIdx.x);
     const SvDesc& d = D[c];
-    if (sv_narrow(d))
-        ts_q_body<uint32_t>(d.x32, d.N, d.ncb, d.part_r, d.alpha, d.sv, d.gpart2, d.ng_p, d.part,
-                            (long long)blockIdx.x - off[c]);
-    else
-        ts_q_body<long long>(d.X, d.N, d.ncb, d.part_r, d.alpha, d.sv, d.gpart2, d.ng_p, d.part,
-                             (long long)blockIdx.x - off[c]);
+    ts_q_body<long long>(d.X, d.N, d.ncb, d.part_r, d.alpha, d.sv, d.gpart2, d.ng_p, d.part,
+                         (long long)blockIdx.x - off[c]);
 }
 // k_slab_sum + k_symvc_scale of every chain (one block each; the same
 // fixed-order sum and the same IEEE operations)
@@ -1360,7 +1395,7 @@ __global__ __launch_bounds__(256) void k_sv_out_b(const SvDesc* __restrict__ D, 
     // two consecutive tile pairs per block (kSvOutPairs)
     const long long p = kSvOutPairs * ((long long)blockIdx.x - off[c]);
     const int cnt = (int)std::min<long long>(kSvOutPairs, d.npairs - p);
-    if (sv_narrow(d)) symvc_out_body<uint32_t>(d.x32, a, d.out, p, cnt);
+    if (sv_narrow(d)) symvc_out_body<uint32_t, uint16_t>(d.x16, a, d.out, p, cnt, d.X);
     else symvc_out_body<long long>(d.X, a, d.out, p, cnt);
 }
 
@@ -1705,7 +1740,7 @@ int hh_twostep(const int64_t* TM, const int64_t* MM, const int64_t* PM, int64_t 
 extern "C++" {
 namespace {
 struct TsWork {
-    DBuf<uint32_t> x32[2];  // MM / PM as uint32 (shared-launch mode)
+    DBuf<uint16_t> x16[2];  // MM / PM as uint16 with escapes (shared-launch mode)
     DBuf<double> dsum, dA, draw;
     DBuf<long long> dz, dng;
     DBuf<uint8_t> dgf;
@@ -1771,7 +1806,7 @@ int hh_twostep_batch(int32_t n, const int64_t* const* TM, const int64_t* const* 
             w[c].dA.alloc(Nc);
             w[c].draw.alloc(2);
             if (narrow)
-                for (int h = 0; h < 2; ++h) w[c].x32[h].alloc(Nc * Nc);
+                for (int h = 0; h < 2; ++h) w[c].x16[h].alloc(Nc * Nc);
         }
         // shared launches for the row statistics (every matrix's rows) and
         // the glue (every chromosome's gap flags, alpha, raw totals), then
@@ -1784,7 +1819,7 @@ int hh_twostep_batch(int32_t n, const int64_t* const* TM, const int64_t* const* 
             const long long* d[3] = {(const long long*)TM[c], (const long long*)MM[c], (const long long*)PM[c]};
             for (int k = 0; k < 3; ++k) {
                 rs[3 * c + k] = RsDesc{d[k], N[c], x.dsum.p + k * N[c], x.dz.p + k * N[c],
-                                       narrow && k ? x.x32[k - 1].p : nullptr, narrow && k ? dovf.p + 2 * c + k - 1 : nullptr};
+                                       narrow && k ? x.x16[k - 1].p : nullptr, narrow && k ? dovf.p + 2 * c + k - 1 : nullptr};
                 row0[3 * c + k + 1] = row0[3 * c + k] + N[c];
             }
             td[c] = TsDesc{N[c], x.dz.p, x.dsum.p, x.dgf.p, x.dgpos.p, x.dglist.p, x.dng.p, x.dA.p, x.draw.p,
@@ -1822,7 +1857,7 @@ int hh_twostep_batch(int32_t n, const int64_t* const* TM, const int64_t* const* 
                     SymvcWs& ws = h ? x.wp : x.wm;
                     SvDesc d{};
                     d.X = (const long long*)(h ? PM[c] : MM[c]);
-                    d.x32 = x.x32[h].p;
+                    d.x16 = x.x16[h].p;
                     d.ovf = dovf.p + 2 * c + h;
                     d.N = Nc;
                     d.gr = gr;

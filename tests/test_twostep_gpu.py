@@ -292,9 +292,37 @@ def test_intra_chrom_batch_error_names_the_chromosome(mb):
         mb.IntraChromMatrixCorrection(tra, hap)
 
 
+def test_intra_chrom_batch_escaped_counts(mb):
+    """The shared-launch batch reads 16-bit copies of MM / PM; counts of
+    0xFFFF and above (here 65 535, 65 536, 70 000 and 3e9, on and off the
+    diagonal, in both triangles) are stored as 0xFFFF and read from the int64
+    matrix: still bitwise the per-chromosome result."""
+    import torch
+    rng = np.random.default_rng(79)
+    tra, hap = {}, {}
+    for c, N in (("1", 700), ("2", 130), ("3", 64)):
+        TM = synth.dense_chrom(N, rng, A=50.0)
+        MM, PM = synth.haplotype_pair(TM, rng, drop_rows=5)
+        for (i, j), v in (((0, 0), 65535), ((3, 10), 65536), ((10, 3), 70000), ((N - 1, N - 1), 3_000_000_000),
+                          ((N // 2, 1), 65535), ((1, N // 2), 123456)):
+            MM[i, j] = v
+            PM[j, i] = v + 1
+            TM[i, j] += 2 * v
+            TM[j, i] = TM[i, j]
+        tra[c] = torch.from_numpy(TM).cuda()
+        hap["M" + c], hap["P" + c] = torch.from_numpy(MM).cuda(), torch.from_numpy(PM).cuda()
+    nor, gaps = mb.IntraChromMatrixCorrection(tra, hap, n_streams=0)
+    for c in tra:
+        one = mb.TwoStepCorrection(tra[c], hap["M" + c], hap["P" + c])
+        assert torch.equal(nor["M" + c], one[0]) and torch.equal(nor["P" + c], one[1])
+        np.testing.assert_array_equal(gaps["M" + c], one[2])
+        np.testing.assert_array_equal(gaps["P" + c], one[3])
+
+
 def test_intra_chrom_batch_wide_counts_fallback(mb):
-    """The shared-launch batch reads 32-bit copies of MM / PM; a chromosome
-    whose counts do not fit (here one cell of 2^33) falls back to the int64
+    """The shared-launch batch reads 16-bit copies of MM / PM (escapes up to
+    32 bits); a chromosome whose counts do not fit (here one cell of 2^33)
+    falls back to the int64
     matrix for its own passes: still bitwise the per-chromosome result."""
     import torch
     rng = np.random.default_rng(78)
