@@ -1594,6 +1594,19 @@ int hh_twostep(const int64_t* TM, const int64_t* MM, const int64_t* PM, int64_t 
                uint8_t* gap_m, uint8_t* gap_p, int32_t on_device, void* stream) {
     return guard([&] {
         HH_REQUIRE(TM && MM && PM && nor_mm && nor_pm && gap_m && gap_p && N > 0, "bad arguments");
+        if (on_device && g_symvc_stream && g_twostep_devglue && g_symvc_out) {
+            // device matrices at the default chain: the shared-launch batch of
+            // one chromosome (its uint16 copies read a quarter of the int64
+            // bytes; bitwise this chain, test_twostep_gpu.py)
+            const int64_t* t[1] = {TM};
+            const int64_t* m[1] = {MM};
+            const int64_t* q[1] = {PM};
+            double* om[1] = {nor_mm};
+            double* op[1] = {nor_pm};
+            const int rc = hh_twostep_batch(1, t, m, q, &N, om, op, gap_m, gap_p, 0, stream);
+            if (rc) HH_THROW(rc, std::string(hh_last_error()));
+            return;
+        }
         hipStream_t s = as_stream(stream);
         const size_t cnt = (size_t)N * N;
         const long long* src[3] = {(const long long*)TM, (const long long*)MM, (const long long*)PM};
@@ -1870,7 +1883,10 @@ int hh_twostep_batch(int32_t n, const int64_t* const* TM, const int64_t* const* 
                     const long long nbtm = (Nc + kT - 1) / kT;  // the gap count's bound: N (device count)
                     // (the gap passes grid-stride over the device gap count's
                     // tiles: 64 blocks per chain, not one per possible tile)
-                    d.ggrid = std::min<long long>(std::max<long long>(nbtm * nbtm, 1), 64);
+                    // (64 per chain for a genome -- more measured slower --, up to
+                    // 1 024 for one chromosome, as its own launch would take)
+                    const long long gcap = std::max<long long>(64, 2048 / nd);
+                    d.ggrid = std::min<long long>(std::max<long long>(nbtm * nbtm, 1), gcap);
                     HH_REQUIRE(d.gcb < 65536 && d.npairs < (1LL << 31), "matrix too large");
                     ws.sv.alloc(Nc);
                     ws.tot.alloc(2);

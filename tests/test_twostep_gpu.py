@@ -251,6 +251,15 @@ def test_twostep_devglue_block_select_path_bitwise(mb):
     assert 300 <= len(gm) < N  # the zeroed rows are gaps, most rows are not
 
 
+
+def _per_chrom_host(mb, T, M, P):
+    """The per-chromosome hh_twostep chain on host arrays (the device path of
+    TwoStepCorrection runs the one-chromosome batch): float64 CPU tensors and
+    the gap arrays."""
+    import torch
+    one = mb.TwoStepCorrection(*(X.cpu().numpy() for X in (T, M, P)))
+    return torch.from_numpy(one[0]), torch.from_numpy(one[1]), one[2], one[3]
+
 @pytest.mark.parametrize("n_streams", [0, 1, 4])
 def test_intra_chrom_batch_equals_per_chromosome(mb, n_streams):
     """IntraChromMatrixCorrection on device tensors: every chromosome in one
@@ -269,8 +278,10 @@ def test_intra_chrom_batch_equals_per_chromosome(mb, n_streams):
     nor, gaps = mb.IntraChromMatrixCorrection(tra, hap, n_streams=n_streams)
     assert set(nor) == {h + c for c in tra for h in "MP"}
     for c in tra:
-        one = mb.TwoStepCorrection(tra[c], hap["M" + c], hap["P" + c])
-        assert torch.equal(nor["M" + c], one[0]) and torch.equal(nor["P" + c], one[1])
+        one = _per_chrom_host(mb, tra[c], hap["M" + c], hap["P" + c])
+        assert torch.equal(nor["M" + c].cpu(), one[0]) and torch.equal(nor["P" + c].cpu(), one[1])
+        dev = mb.TwoStepCorrection(tra[c], hap["M" + c], hap["P" + c])  # device: the one-chromosome batch
+        assert torch.equal(dev[0], nor["M" + c]) and torch.equal(dev[1], nor["P" + c])
         np.testing.assert_array_equal(gaps["M" + c], one[2])
         np.testing.assert_array_equal(gaps["P" + c], one[3])
     ref = hichap_ref.two_step_correction(tra["X"].cpu().numpy(), hap["MX"].cpu().numpy(), hap["PX"].cpu().numpy())
@@ -313,8 +324,8 @@ def test_intra_chrom_batch_escaped_counts(mb):
         hap["M" + c], hap["P" + c] = torch.from_numpy(MM).cuda(), torch.from_numpy(PM).cuda()
     nor, gaps = mb.IntraChromMatrixCorrection(tra, hap, n_streams=0)
     for c in tra:
-        one = mb.TwoStepCorrection(tra[c], hap["M" + c], hap["P" + c])
-        assert torch.equal(nor["M" + c], one[0]) and torch.equal(nor["P" + c], one[1])
+        one = _per_chrom_host(mb, tra[c], hap["M" + c], hap["P" + c])
+        assert torch.equal(nor["M" + c].cpu(), one[0]) and torch.equal(nor["P" + c].cpu(), one[1])
         np.testing.assert_array_equal(gaps["M" + c], one[2])
         np.testing.assert_array_equal(gaps["P" + c], one[3])
 
@@ -337,6 +348,6 @@ def test_intra_chrom_batch_wide_counts_fallback(mb):
         hap["M" + c], hap["P" + c] = torch.from_numpy(MM).cuda(), torch.from_numpy(PM).cuda()
     nor, gaps = mb.IntraChromMatrixCorrection(tra, hap, n_streams=0)
     for c in tra:
-        one = mb.TwoStepCorrection(tra[c], hap["M" + c], hap["P" + c])
-        assert torch.equal(nor["M" + c], one[0]) and torch.equal(nor["P" + c], one[1])
+        one = _per_chrom_host(mb, tra[c], hap["M" + c], hap["P" + c])
+        assert torch.equal(nor["M" + c].cpu(), one[0]) and torch.equal(nor["P" + c].cpu(), one[1])
         np.testing.assert_array_equal(gaps["M" + c], one[2])
