@@ -26,6 +26,13 @@ namespace hh {
 
 constexpr int kT = 64;  // dense tile edge
 
+// lane `l`'s double (wave-uniform l)
+__device__ __forceinline__ double readlane_dbl(double v, int l) {
+    const unsigned long long u = __double_as_longlong(v);
+    const unsigned lo = __builtin_amdgcn_readlane((unsigned)u, l), hi = __builtin_amdgcn_readlane((unsigned)(u >> 32), l);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
 // x16 (integer T only, may be null): the row copied as uint16, a count >=
 // 0xFFFF stored as 0xFFFF (the passes that read the copy take such entries
 // from X itself); *ovf set when a value does not fit 32 bits (the later
@@ -496,6 +503,16 @@ __device__ __forceinline__ void ts_gemv_body(const L* __restrict__ X, long long 
     }
     const long long rend = std::min<long long>(r0 + gr, N);
     const long long ng = (MODE == 1 && gpos) ? *ng_p : 0;  // Xc's row stride
+    // MODE 1: the block's rows' 1 / alpha and gap positions, one lane per row
+    // (gr <= 64), taken by v_readlane in the row loop instead of a dependent
+    // load per row
+    const bool lane_rows = MODE == 1 && gr <= 64;
+    double ra_l = 0.0;
+    int gp_l = -1;
+    if (lane_rows && r0 + lane < rend) {
+        ra_l = 1.0 / alpha[r0 + lane];
+        if (gpos) gp_l = gpos[r0 + lane];
+    }
     constexpr int kB = 4;  // rows per batch: 32 loads in flight per lane
 #pragma unroll 1
     for (long long i0 = r0; i0 < rend; i0 += kB) {
@@ -535,11 +552,17 @@ __device__ __forceinline__ void ts_gemv_body(const L* __restrict__ X, long long 
             if (MODE == 1) {
                 // S_ij = X_ij / alpha_i as X_ij * (1 / alpha_i): within an ulp of the
                 // true quotient, and a division per element doubles the registers
-                const double ra = okr ? 1.0 / alpha[i] : 0.0;
+                double ra;
+                if (lane_rows) {
+                    const int li = (int)(i - r0) & 63;  // (i >= rend: the value is not used)
+                    ra = okr ? readlane_dbl(ra_l, li) : 0.0;
+                } else {
+                    ra = okr ? 1.0 / alpha[i] : 0.0;
+                }
 #pragma unroll
                 for (int k = 0; k < 8; ++k) accc[k] += (double)x[b][k] * ra;
                 if (gpos && okr) {
-                    const int gi = gpos[i];
+                    const int gi = lane_rows ? __builtin_amdgcn_readlane(gp_l, (int)(i - r0)) : gpos[i];
                     if (gi >= 0) {
 #pragma unroll
                         for (int k = 0; k < 8; ++k)
