@@ -1324,6 +1324,22 @@ struct SvDesc {
 enum { kSvGemv = 0, kSvGap, kSvColsum, kSvRows, kSvQ, kSvOut, kSvPhases };
 constexpr int kSvOutPairs = 2;  // tile pairs per k_sv_out_b block
 
+// pinned staging of hh_twostep_batch's pass descriptors (the thread's; idle
+// again after each call's final synchronisation)
+static void* ts_desc_stage(size_t bytes) {
+    static thread_local void* p = nullptr;
+    static thread_local size_t cap = 0;
+    if (bytes > cap) {
+        if (p) HIP_CHECK(hipHostFree(p));
+        p = nullptr;
+        cap = 0;
+        const size_t want = std::max<size_t>(bytes, 1 << 20);
+        HIP_CHECK(hipHostMalloc(&p, want, hipHostMallocDefault));
+        cap = want;
+    }
+    return p;
+}
+
 __device__ __forceinline__ int sv_find(const long long* __restrict__ off, int nd, long long b) {
     int lo = 0, hi = nd - 1;  // the last chain with off[c] <= b
     while (lo < hi) {
@@ -1945,11 +1961,13 @@ int hh_twostep_batch(int32_t n, const int64_t* const* TM, const int64_t* const* 
             const size_t b_sd = sd.size() * sizeof(SvDesc), o_off = (b_sd + 15) & ~(size_t)15;
             DBuf<char> dsv(o_off + off.size() * 8);
             {
-                char* up = (char*)pinned_stage().get(0, o_off + off.size() * 8);
+                // a staging buffer of its own (slot 0 takes the downloads
+                // below): no host wait for the row statistics before the
+                // passes are enqueued
+                char* up = (char*)ts_desc_stage(o_off + off.size() * 8);
                 std::memcpy(up, sd.data(), b_sd);
                 std::memcpy(up + o_off, off.data(), off.size() * 8);
                 dsv.upload(up, o_off + off.size() * 8, s0);
-                HIP_CHECK(hipStreamSynchronize(s0));  // slot 0 is reused for the downloads below
             }
             const SvDesc* D = (const SvDesc*)dsv.p;
             auto O = [&](int k) { return (const long long*)(dsv.p + o_off) + (size_t)k * (nd + 1); };
