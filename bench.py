@@ -1230,6 +1230,42 @@ def _free_port():
         return s.getsockname()[1]
 
 
+def visible_gpu_count():
+    """GPUs this process may use, counted WITHOUT loading the HIP runtime (the
+    launcher must not initialise HIP before its ranks start, and torch loads
+    libamdhip64 on import): the KFD topology in sysfs (nodes whose
+    ``gfx_target_version`` is nonzero; ``HH_KFD_TOPOLOGY`` overrides the path
+    for tests), narrowed by ROCR_ / HIP_ / CUDA_VISIBLE_DEVICES.  Where the
+    topology cannot be read, a child process counts through torch."""
+    import glob
+    import subprocess
+    root = os.environ.get("HH_KFD_TOPOLOGY", "/sys/class/kfd/kfd/topology/nodes")
+    nodes = glob.glob(os.path.join(root, "*", "properties"))
+    n = 0
+    for path in nodes:
+        try:
+            with open(path) as f:
+                for line in f:
+                    key, _, val = line.strip().partition(" ")
+                    if key == "gfx_target_version":
+                        n += int(val) != 0
+                        break
+        except (OSError, ValueError):
+            continue
+    if not nodes:
+        p = subprocess.run([sys.executable, "-c", "import torch; print(torch.cuda.device_count())"],
+                           capture_output=True, text=True, timeout=600)
+        try:
+            n = int(p.stdout.strip().splitlines()[-1])
+        except (ValueError, IndexError):
+            n = 0
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([x for x in v.split(",") if x.strip()]))
+    return n
+
+
 def launch_ranks(n, argv):
     """``bench.py --gpus N`` without a launcher: start N child ranks (one
     process per GPU, RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in their
@@ -1242,8 +1278,7 @@ def launch_ranks(n, argv):
     (``HH_DIST_BACKEND=gloo``), so no device count is required."""
     import subprocess
     if "HH_DEVICE" not in os.environ:
-        import torch
-        ndev = torch.cuda.device_count()
+        ndev = visible_gpu_count()
         if ndev < n:
             print(f"[bench] --gpus {n} needs {n} visible GPUs, this node has {ndev}; refusing to report "
                   f"n_gpus={n} from fewer devices (set HH_DEVICE=<dev> HH_DIST_BACKEND=gloo for a one-device "

@@ -94,6 +94,7 @@ SIGNATURES = {
     "hh_ice_swept_bytes": (C.c_int, [P, PI64]),
     "hh_ice_get_bias": (C.c_int, [P, P, P]),
     "hh_sweep_trace": (C.c_int, [P, I64, PI64]),
+    "hh_matrix_stream_probe": (C.c_int, [P, I32, PF64, I32]),
     "hh_comm_unique_id": (C.c_int, [P]),
     "hh_comm_init": (C.c_int, [P, I32, I32, C.POINTER(P)]),
     "hh_comm_free": (C.c_int, [P]),

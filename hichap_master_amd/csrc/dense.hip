@@ -1799,8 +1799,15 @@ struct TsWork {
     DBuf<int> dgpos, dglist;
     SymvcWs wm, wp;
 };
+// the side streams, per device (a stream belongs to the device current at
+// its creation)
 std::vector<hipStream_t>& ts_streams(int k) {
-    static std::vector<hipStream_t> v;
+    static std::mutex mu;
+    static std::map<int, std::vector<hipStream_t>> by_dev;
+    int dev = 0;
+    HIP_CHECK(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> lk(mu);
+    std::vector<hipStream_t>& v = by_dev[dev];
     while ((int)v.size() < k) {
         hipStream_t s;
         HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
@@ -1810,6 +1817,37 @@ std::vector<hipStream_t>& ts_streams(int k) {
 }
 }  // namespace
 }  // extern "C++"
+
+// Waits for s0 and the side streams when a batch is left by an exception
+// after its first launch: the buffers it hands back to the pool may still be
+// in use by enqueued kernels (the pool's reuse rule: every entry point
+// synchronises before returning).  Declared after the batch's buffers, so it
+// runs before they are released.
+struct TsSyncOnThrow {
+    hipStream_t s0;
+    std::vector<hipStream_t>* side;
+    int nside;
+    ~TsSyncOnThrow() {
+        if (!std::uncaught_exceptions()) return;
+        (void)hipStreamSynchronize(s0);
+        for (int k = 0; side && k < nside; ++k) (void)hipStreamSynchronize((*side)[k]);
+    }
+};
+
+// device bytes hh_twostep_batch allocates for one chromosome of N bins (its
+// TsWork and two chains' SymvcWs), an upper bound
+static size_t twostep_ws_bytes(int64_t N, bool narrow) {
+    const double n = (double)N, gr = (double)g_symvc_rows;
+    const double nbtm = std::ceil(n / kT), nrc = std::ceil(n / gr), ncb = std::ceil(n / kGW);
+    double b = n * (3 * 8 + 3 * 8 + 2 + 2 * 4 + 2 * 4 + 8) + 64 + (narrow ? 2 * n * n * 2 : 0);
+    b += 2 * (n * 8 * 3 + 16 + nrc * n * 8 + ncb * n * 8 + std::ceil(n / 256) * 8 + n * n * 8 + 2 * nbtm * n * 8);
+    return (size_t)b + 64 * 512;  // + the pool's 512-byte rounding of ~60 buffers
+}
+
+static void twostep_batch_impl(int32_t n, const int64_t* const* TM, const int64_t* const* MM,
+                               const int64_t* const* PM, const int64_t* N, double* const* nor_mm,
+                               double* const* nor_pm, uint8_t* gap_m, uint8_t* gap_p, int32_t n_streams,
+                               hipStream_t s0, int c_base);
 
 int hh_twostep_batch(int32_t n, const int64_t* const* TM, const int64_t* const* MM, const int64_t* const* PM,
                      const int64_t* N, double* const* nor_mm, double* const* nor_pm, uint8_t* gap_m,
@@ -1825,6 +1863,44 @@ int hh_twostep_batch(int32_t n, const int64_t* const* TM, const int64_t* const* 
             goff[c + 1] = goff[c] + N[c];
         }
         hipStream_t s0 = as_stream(stream);
+        // the workspace grows with the sum over chromosomes (a genome-wide
+        // localRes set at 10 kb: ~100 GB beside its 190 GB of inputs and
+        // outputs), so the chromosomes go in consecutive groups whose
+        // workspace fits the budget: the free device memory plus what the
+        // pool holds, less a margin (hh_tune twostep_budget_mb overrides).
+        // A chromosome's results do not depend on its group (per-chain
+        // descriptors, partials at fixed places): bitwise the same.
+        const bool narrow = n_streams == 0;
+        size_t budget = (size_t)g_twostep_budget;
+        if (!budget) {
+            size_t fr = 0, tot = 0;
+            HIP_CHECK(hipMemGetInfo(&fr, &tot));
+            size_t cached = 0;
+            {
+                std::lock_guard<std::mutex> lk(g_pool_mu);
+                cached = g_pool_cached;
+            }
+            const size_t avail = fr + cached, margin = std::max<size_t>(size_t(2) << 30, tot / 32);
+            budget = avail > margin ? avail - margin : 0;
+        }
+        for (int a = 0; a < n;) {
+            int b = a + 1;
+            size_t used = twostep_ws_bytes(N[a], narrow);
+            while (b < n && used + twostep_ws_bytes(N[b], narrow) <= budget) used += twostep_ws_bytes(N[b++], narrow);
+            twostep_batch_impl(b - a, TM + a, MM + a, PM + a, N + a, nor_mm + a, nor_pm + a, gap_m + goff[a],
+                               gap_p + goff[a], n_streams, s0, a);
+            a = b;
+        }
+    });
+}
+
+static void twostep_batch_impl(int32_t n, const int64_t* const* TM, const int64_t* const* MM,
+                               const int64_t* const* PM, const int64_t* N, double* const* nor_mm,
+                               double* const* nor_pm, uint8_t* gap_m, uint8_t* gap_p, int32_t n_streams,
+                               hipStream_t s0, int c_base) {
+    {
+        std::vector<int64_t> goff((size_t)n + 1, 0);
+        for (int c = 0; c < n; ++c) goff[c + 1] = goff[c] + N[c];
         std::vector<int> order(n);
         for (int c = 0; c < n; ++c) order[c] = c;
         std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return N[a] > N[b]; });
@@ -1888,18 +1964,19 @@ int hh_twostep_batch(int32_t n, const int64_t* const* TM, const int64_t* const* 
             std::memcpy(up + o_td, td.data(), b_td);
             ddesc.upload(up, o_td + b_td, s0);
         }
-        hipLaunchKernelGGL(k_rowstats_b, dim3((unsigned)row0.back()), dim3(256), 0, s0, (const RsDesc*)ddesc.p,
-                           (const long long*)(ddesc.p + o_r0), 3 * n);
-        hipLaunchKernelGGL(k_ts_gapdef_b, dim3((unsigned)(2 * n)), dim3(1024), 0, s0,
-                           (const TsDesc*)(ddesc.p + o_td));
-        hipLaunchKernelGGL(k_ts_alpha_b, dim3((unsigned)n), dim3(1024), 0, s0, (const TsDesc*)(ddesc.p + o_td));
-        HIP_CHECK(hipGetLastError());
+        // shared-launch mode: every chain's workspace, descriptors and checks
+        // before the first launch (an allocation failure or a
+        // failed check after it left kernels writing pool memory)
+        const int nd = 2 * n;
+        std::vector<SvDesc> sd;
+        std::vector<long long> off;
+        DBuf<char> dsv;
+        size_t o_off = 0;
+        TsSyncOnThrow sync_guard{s0, &ss, K};
         if (n_streams == 0) {
-            // every chain's passes in shared launches: chain 2c = MM of
-            // chromosome c, 2c + 1 = PM, largest chromosomes first
-            const int nd = 2 * n;
-            std::vector<SvDesc> sd((size_t)nd);
-            std::vector<long long> off((size_t)kSvPhases * (nd + 1), 0);
+            // chain 2c = MM of chromosome c, 2c + 1 = PM, largest chromosomes first
+            sd.resize((size_t)nd);
+            off.assign((size_t)kSvPhases * (nd + 1), 0);
             const int gr = g_symvc_rows;
             int j = 0;
             for (int c : order) {
@@ -1958,8 +2035,9 @@ int hh_twostep_batch(int32_t n, const int64_t* const* TM, const int64_t* const* 
             }
             for (int k = 0; k < kSvPhases; ++k)
                 HH_REQUIRE(off[(size_t)k * (nd + 1) + nd] < (1LL << 31), "too many blocks for one launch");
-            const size_t b_sd = sd.size() * sizeof(SvDesc), o_off = (b_sd + 15) & ~(size_t)15;
-            DBuf<char> dsv(o_off + off.size() * 8);
+            const size_t b_sd = sd.size() * sizeof(SvDesc);
+            o_off = (b_sd + 15) & ~(size_t)15;
+            dsv.alloc(o_off + off.size() * 8);
             {
                 // a staging buffer of its own (slot 0 takes the downloads
                 // below): no host wait for the row statistics before the
@@ -1969,6 +2047,14 @@ int hh_twostep_batch(int32_t n, const int64_t* const* TM, const int64_t* const* 
                 std::memcpy(up + o_off, off.data(), off.size() * 8);
                 dsv.upload(up, o_off + off.size() * 8, s0);
             }
+        }
+        hipLaunchKernelGGL(k_rowstats_b, dim3((unsigned)row0.back()), dim3(256), 0, s0, (const RsDesc*)ddesc.p,
+                           (const long long*)(ddesc.p + o_r0), 3 * n);
+        hipLaunchKernelGGL(k_ts_gapdef_b, dim3((unsigned)(2 * n)), dim3(1024), 0, s0,
+                           (const TsDesc*)(ddesc.p + o_td));
+        hipLaunchKernelGGL(k_ts_alpha_b, dim3((unsigned)n), dim3(1024), 0, s0, (const TsDesc*)(ddesc.p + o_td));
+        HIP_CHECK(hipGetLastError());
+        if (n_streams == 0) {
             const SvDesc* D = (const SvDesc*)dsv.p;
             auto O = [&](int k) { return (const long long*)(dsv.p + o_off) + (size_t)k * (nd + 1); };
             auto grid = [&](int k) { return dim3((unsigned)off[(size_t)k * (nd + 1) + nd]); };
@@ -1991,8 +2077,8 @@ int hh_twostep_batch(int32_t n, const int64_t* const* TM, const int64_t* const* 
             derr.download(herr, (size_t)n, s0);
             HIP_CHECK(hipStreamSynchronize(s0));
             for (int c = 0; c < n; ++c) {
-                HH_REQUIRE(!(herr[c] & 1), "percentile of an empty array (chromosome " + std::to_string(c) + ")");
-                HH_REQUIRE(!(herr[c] & 2), "every bin is a gap (chromosome " + std::to_string(c) + ")");
+                HH_REQUIRE(!(herr[c] & 1), "percentile of an empty array (chromosome " + std::to_string(c_base + c) + ")");
+                HH_REQUIRE(!(herr[c] & 2), "every bin is a gap (chromosome " + std::to_string(c_base + c) + ")");
                 std::memcpy(gap_m + goff[c], dl + 2 * goff[c], (size_t)N[c]);
                 std::memcpy(gap_p + goff[c], dl + 2 * goff[c] + N[c], (size_t)N[c]);
             }
@@ -2028,12 +2114,12 @@ int hh_twostep_batch(int32_t n, const int64_t* const* TM, const int64_t* const* 
         derr.download(herr, (size_t)n, s0);
         HIP_CHECK(hipStreamSynchronize(s0));
         for (int c = 0; c < n; ++c) {
-            HH_REQUIRE(!(herr[c] & 1), "percentile of an empty array (chromosome " + std::to_string(c) + ")");
-            HH_REQUIRE(!(herr[c] & 2), "every bin is a gap (chromosome " + std::to_string(c) + ")");
+            HH_REQUIRE(!(herr[c] & 1), "percentile of an empty array (chromosome " + std::to_string(c_base + c) + ")");
+            HH_REQUIRE(!(herr[c] & 2), "every bin is a gap (chromosome " + std::to_string(c_base + c) + ")");
             std::memcpy(gap_m + goff[c], dl + 2 * goff[c], (size_t)N[c]);
             std::memcpy(gap_p + goff[c], dl + 2 * goff[c] + N[c], (size_t)N[c]);
         }
-    });
+    }
 }
 
 int hh_dense_from_cells(const int64_t* row, const int64_t* col, const int64_t* count, int64_t nnz, int64_t N,

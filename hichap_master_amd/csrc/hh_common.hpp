@@ -120,6 +120,7 @@ inline int g_ortho_grid_cap = 0;    // hh_tune "ortho_grid_cap": a lower cap on 
 inline int g_symvc_rows = 32;  // hh_tune "symvc_rows": rows per k_ts_gemv block (multiple of 16)
 inline int g_symvc_out = 1;  // hh_tune "symvc_out": TwoStep pass 3 with one LDS tile (k_symvc_out; 0: k_symvc<T, 3>)
 inline int g_twostep_devglue = 1;  // hh_tune "twostep_devglue": TwoStep gap / alpha glue on the device (0: host)
+inline int64_t g_twostep_budget = 0;  // hh_tune "twostep_budget_mb": hh_twostep_batch workspace budget (0: free HBM)
 inline int g_symvc_stream = 1;  // hh_tune "symvc_stream": TwoStep passes 1-2 as row-streaming GEMVs (0: the 64x64 tile-pair passes)
 inline int g_ortho_abort_test = 0;  // hh_tune "ortho_abort_test": act as if k_ortho's barrier timed out (tests the fallback)
 inline int g_pca_coop = 1;  // hh_tune "pca_coop": Krylov orthogonalisation in one launch per product (k_ortho)

@@ -151,6 +151,11 @@ int hh_matrix_from_pixels_device(const int32_t* bin1, const int32_t* bin2, const
                                  int32_t cis_only, int64_t row_lo, int64_t row_hi, void* stream, hh_matrix** out);
 int hh_matrix_free(hh_matrix* m);
 int hh_matrix_get_info(const hh_matrix* m, hh_matrix_info* info);
+/* Diagnostic read rates of a matrix's own buffers (no sweep work): out[2i] =
+ * ms per pass, out[2i+1] = bytes, for i = 0 wide / 1 narrow tile entries,
+ * 2 uint8 / 3 nibble band (linear reads), 4-6 the flat tiles' payload in the
+ * flat sweep's order, streamed only.  nout >= 14. */
+int hh_matrix_stream_probe(const hh_matrix* m, int32_t reps, double* out, int32_t nout);
 /* Copy the stored upper-triangle pixels (bin1 <= bin2, bin1 in the local rows
  * for which bin1 is the row) back to the host; *nnz_inout = capacity on entry,
  * count on exit.  For checking only. */

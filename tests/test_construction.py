@@ -283,3 +283,29 @@ def test_haplotype_construction_end_to_end(golden, tmp_path):
     assert _read_tables(trad)[res][5] is not None  # balanced in place
     gaps = np.load(os.path.join(tmp_path, "Cooler", "S0_Imputated_Gap.npz"), allow_pickle=True)  # our own file
     assert sorted(gaps.files) == [str(r) for r in sorted(p["localRes"])]
+    # every localRes group of the imputed cooler: the oracle's
+    # IntraChromMatrixCorrection (TwoStepCorrection per chromosome,
+    # matrixBuilding.py:1026-1041, called at :1607-1614) of the imputed local
+    # matrices, as NPZ2Cooler's float tables; the gap file's arrays are the
+    # oracle's Gap_M / Gap_P (:1616-1617)
+    got_all = _read_tables(imp)
+    for lres in p["localRes"]:
+        T_loc, I_loc = ds["Tradition_Local"][lres], ds["Imputated_Local"][lres]
+        nor, gap_want = {}, {}
+        for c in T_loc:
+            nmm, npm, gm, gp = hichap_ref.two_step_correction(*(np.asarray(X, dtype=np.int64) for X in
+                                                                 (T_loc[c], I_loc["M" + c], I_loc["P" + c])))
+            nor["M" + c], nor["P" + c] = nmm, npm
+            gap_want["M" + c], gap_want["P" + c] = gm, gp
+        want_l = cooler_ref.npz2cooler_tables({lres: cooler_ref.intra_to_sparse_dict(nor)}, hap_lines, hap_chroms,
+                                              True, dtype="float")[lres]
+        got_l = got_all[lres]
+        assert got_l[0] == want_l[0]
+        np.testing.assert_array_equal(got_l[1], want_l[1])
+        np.testing.assert_array_equal(got_l[2], want_l[2])
+        assert got_l[3].dtype == np.float64
+        np.testing.assert_allclose(got_l[3], want_l[3], rtol=1e-12, atol=0)
+        gap_got = gaps[str(lres)].item()
+        assert sorted(gap_got) == sorted(gap_want)
+        for k in gap_want:
+            np.testing.assert_array_equal(np.asarray(gap_got[k], dtype=np.int64), gap_want[k])

@@ -363,6 +363,34 @@ def test_flat_block_shapes_bitwise(ice, upper):
         assert st["iters"] == res[0][1]["iters"]
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("cis_only", [0, 1])
+def test_flatw_early_claim_bitwise(ice, cis_only):
+    """k_sweep_flatw3 (flatw_pipe 3: the next tile claimed during the walk,
+    its record prefetched with its payload, active flags from LDS) walks the
+    same tiles with the same sums as k_sweep_flatw: bitwise the same weights
+    and iterations, genome-wide (one ICE group) and --cis-only (a group per
+    chromosome, converging at different iterations: the skip path)."""
+    from hichap_master_amd import _lib
+    b1, b2, c, off = _case(43, sizes=(9000, 7000, 600), A=3.0, trans=0.0005)
+    n = int(off[-1])
+    res = []
+    _lib.call("hh_tune", b"flat_cols", 1)
+    try:
+        for pipe in (2, 3, 2, 3):
+            _lib.call("hh_tune", b"flatw_pipe", pipe)
+            m = ice.ContactMatrix.from_pixels(b1, b2, c, n, off, cis_only=cis_only)
+            assert m.info()["n_units_flat"] > 0
+            res.append(ice.balance_matrix(m, ice.IceOptions(max_iters=300)))
+            m.close()
+    finally:
+        _lib.call("hh_tune", b"flatw_pipe", 2)
+        _lib.call("hh_tune", b"flat_cols", -1)
+    for w, st in res[1:]:
+        np.testing.assert_array_equal(w, res[0][0])
+        assert st["iters"] == res[0][1]["iters"]
+
+
 def _full_config(cfg):
     """Sizes and generator parameters of BASELINE C4 (hg19 diploid 10 kb, 5e9
     pixels, 20 % trans) / C3 (hg19 40 kb, 8e8 pixels, 85 % trans: at 40 kb

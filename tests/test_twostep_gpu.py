@@ -26,6 +26,44 @@ def test_twostep_matches_reference_golden(mb, golden, name):
     np.testing.assert_allclose(npm, g["Nor_PM"], rtol=1e-12, atol=0)
 
 
+@pytest.mark.parametrize("name", ["twostep_gaps_n96", "twostep_gaps_n160", "twostep_nogapM_n80"])
+def test_twostep_golden_through_device_batch(mb, golden, name):
+    """The reference's own outputs through the path the twostep benches time:
+    device tensors into TwoStepCorrection (hh_twostep -> the one-chromosome
+    hh_twostep_batch) and into IntraChromMatrixCorrection with shared launches
+    (n_streams 0) and with chains on streams; twostep_nogapM_n80 is the SUM
+    branch of Trans2symmetry (matrixBuilding.py:948-952)."""
+    import torch
+    g = golden(name)
+    dev = [torch.from_numpy(np.ascontiguousarray(g[k], dtype=np.int64)).cuda() for k in ("TM", "MM", "PM")]
+    nmm, npm, gm, gp = mb.TwoStepCorrection(*dev)
+    np.testing.assert_array_equal(gm, g["Gap_M"])
+    np.testing.assert_array_equal(gp, g["Gap_P"])
+    np.testing.assert_allclose(nmm.cpu().numpy(), g["Nor_MM"], rtol=1e-12, atol=0)
+    np.testing.assert_allclose(npm.cpu().numpy(), g["Nor_PM"], rtol=1e-12, atol=0)
+    for ns in (0, 2):
+        nor, gaps = mb.IntraChromMatrixCorrection({"7": dev[0]}, {"M7": dev[1], "P7": dev[2]}, n_streams=ns)
+        np.testing.assert_array_equal(gaps["M7"], g["Gap_M"])
+        np.testing.assert_array_equal(gaps["P7"], g["Gap_P"])
+        np.testing.assert_allclose(nor["M7"].cpu().numpy(), g["Nor_MM"], rtol=1e-12, atol=0)
+        np.testing.assert_allclose(nor["P7"].cpu().numpy(), g["Nor_PM"], rtol=1e-12, atol=0)
+    # the three goldens as one genome-wide batch (shared launches across
+    # chromosomes of different sizes and branches)
+    names = ["twostep_gaps_n96", "twostep_gaps_n160", "twostep_nogapM_n80"]
+    gs = [golden(nm) for nm in names]
+    tra = {str(i): torch.from_numpy(np.ascontiguousarray(x["TM"], dtype=np.int64)).cuda() for i, x in enumerate(gs)}
+    hap = {}
+    for i, x in enumerate(gs):
+        hap["M%d" % i] = torch.from_numpy(np.ascontiguousarray(x["MM"], dtype=np.int64)).cuda()
+        hap["P%d" % i] = torch.from_numpy(np.ascontiguousarray(x["PM"], dtype=np.int64)).cuda()
+    nor, gaps = mb.IntraChromMatrixCorrection(tra, hap, n_streams=0)
+    for i, x in enumerate(gs):
+        np.testing.assert_array_equal(gaps["M%d" % i], x["Gap_M"])
+        np.testing.assert_array_equal(gaps["P%d" % i], x["Gap_P"])
+        np.testing.assert_allclose(nor["M%d" % i].cpu().numpy(), x["Nor_MM"], rtol=1e-12, atol=0)
+        np.testing.assert_allclose(nor["P%d" % i].cpu().numpy(), x["Nor_PM"], rtol=1e-12, atol=0)
+
+
 def test_genomewide_matches_reference_golden(mb, golden):
     g = golden("genomewide_3chrom")
     names = [str(x) for x in g["names"]]
@@ -287,6 +325,47 @@ def test_intra_chrom_batch_equals_per_chromosome(mb, n_streams):
     ref = hichap_ref.two_step_correction(tra["X"].cpu().numpy(), hap["MX"].cpu().numpy(), hap["PX"].cpu().numpy())
     np.testing.assert_allclose(nor["MX"].cpu().numpy(), ref[0], rtol=1e-11)
     np.testing.assert_array_equal(gaps["PX"], ref[3])
+
+
+@pytest.mark.parametrize("n_streams", [0, 3])
+def test_intra_chrom_batch_memory_budget_bitwise(mb, n_streams):
+    """hh_twostep_batch splits the chromosomes into consecutive groups whose
+    workspace fits a device-memory budget (the workspace grows
+    with the sum over chromosomes); with a budget so small that every
+    chromosome is its own group the results are bitwise those of one batch,
+    and an error still names the chromosome by its index in the call."""
+    import torch
+    from hichap_master_amd import _lib
+    rng = np.random.default_rng(91)
+    tra, hap = {}, {}
+    for c, N, drop in (("1", 1700, 30), ("2", 64, 0), ("3", 1100, 0), ("4", 800, 9)):
+        TM = synth.dense_chrom(N, rng, A=50.0)
+        MM, PM = synth.haplotype_pair(TM, rng, drop_rows=drop)
+        tra[c] = torch.from_numpy(TM).cuda()
+        hap["M" + c], hap["P" + c] = torch.from_numpy(MM).cuda(), torch.from_numpy(PM).cuda()
+    full, gfull = mb.IntraChromMatrixCorrection(tra, hap, n_streams=n_streams)
+    for mbytes in (1, 40):
+        _lib.call("hh_tune", b"twostep_budget_mb", mbytes)
+        try:
+            part, gpart = mb.IntraChromMatrixCorrection(tra, hap, n_streams=n_streams)
+        finally:
+            _lib.call("hh_tune", b"twostep_budget_mb", 0)
+        for k in full:
+            assert torch.equal(part[k], full[k]), (mbytes, k)
+            np.testing.assert_array_equal(gpart[k], gfull[k])
+    Z = torch.zeros_like(tra["3"])
+    bad = dict(hap, M3=Z, P3=Z)
+    _lib.call("hh_tune", b"twostep_budget_mb", 1)
+    try:
+        with pytest.raises(_lib.HipLibraryError, match=r"percentile of an empty array \(chromosome 2\)"):
+            mb.IntraChromMatrixCorrection(tra, bad, n_streams=n_streams)
+    finally:
+        _lib.call("hh_tune", b"twostep_budget_mb", 0)
+    # the library is usable after the failed call (its buffers were not
+    # handed back while kernels still wrote them)
+    again, _ = mb.IntraChromMatrixCorrection(tra, hap, n_streams=n_streams)
+    for k in full:
+        assert torch.equal(again[k], full[k])
 
 
 def test_intra_chrom_batch_error_names_the_chromosome(mb):

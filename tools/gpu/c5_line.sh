@@ -1,5 +1,5 @@
 #!/bin/bash
-# C5 after a k_ortho change: tests, the line, the serial low-synch breakdown.  tools/gpu/r5r.sh outdir
+# C5 tests, the line and the serial low-synch k_ortho breakdown.  tools/gpu/c5_line.sh outdir
 cd "${GRAFT_REPO_ROOT:-/root/repo}" && R=$PWD && export TMPDIR=/tmp
 O=$R/gpurun_out/$1; mkdir -p $O
 timeout -k 10 600 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_c5_gpu.py tests/test_structure_gpu.py > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }

@@ -1,5 +1,5 @@
 #!/bin/bash
-# The whole -m gpu suite and smoke() at the current build.  tools/gpu/r5final_tests.sh outdir
+# The whole -m gpu suite and smoke() at the current build.  tools/gpu/suite.sh outdir
 cd "${GRAFT_REPO_ROOT:-/root/repo}" && R=$PWD && export TMPDIR=/tmp
 O=$R/gpurun_out/$1; mkdir -p $O
 timeout -k 10 1000 python3 -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread > $O/gpu_tests.log 2>&1 || { tail -40 $O/gpu_tests.log; exit 1; }

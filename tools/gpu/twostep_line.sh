@@ -1,5 +1,5 @@
 #!/bin/bash
-# TwoStep pass 3 change: tests, the twostep lines, kernel stats of the per-genome line.  tools/gpu/r5u.sh outdir
+# TwoStep tests, the twostep lines, kernel stats of the per-genome line.  tools/gpu/twostep_line.sh outdir
 cd "${GRAFT_REPO_ROOT:-/root/repo}" && R=$PWD && export TMPDIR=/tmp
 O=$R/gpurun_out/$1; mkdir -p $O
 timeout -k 10 600 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_twostep_gpu.py > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }

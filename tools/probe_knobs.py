@@ -24,6 +24,8 @@ ap.add_argument("--nnz", type=float, default=5e9)
 ap.add_argument("--iters", type=int, default=10)
 ap.add_argument("--config", default="", help="a bench.py config (c2, c3, ...) instead of C4")
 ap.add_argument("--shard", default="", help="k/N: build only shard k of N (equal 512-row blocks)")
+ap.add_argument("--stream", action="store_true", help="first the read rates of the matrix's own buffers "
+                "(hh_matrix_stream_probe: linear reads; the flat tiles streamed in the flat sweep's order)")
 a = ap.parse_args()
 _lib.load(); _lib.require_gpu()
 if a.config:
@@ -46,6 +48,17 @@ print(f"build {time.time()-t0:.1f}s band_w={inf['band_w']} band_w4={inf['band_w4
       f"{inf['n_units_flat']} units, band {(2 * inf['band_w'] + 16) * (inf['row_hi'] - inf['row_lo']) / 1e9:.2f} GB, band4 "
       f"{(inf['band_w4'] - inf['band_w'] + 32) * (inf['band_w4'] > inf['band_w']) * (inf['row_hi'] - inf['row_lo']) / 1e9:.2f} GB) "
       f"tiles {inf['n_tiles']}", flush=True)
+if a.stream:
+    import ctypes as C
+    out = (C.c_double * 14)()
+    names = ["wide tile entries", "narrow tile entries", "uint8 band", "nibble band",
+             "flat tiles, 11 waves, 1 block/CU", "flat tiles, 11 waves", "flat tiles, 16 waves"]
+    for rep in range(2):
+        _lib.call("hh_matrix_stream_probe", m.handle, 5, out, 14)
+        for i, nm in enumerate(names):
+            if out[2 * i + 1] > 0:
+                print(f"[stream {rep}] {nm}: {out[2*i+1]/1e9:.3f} GB in {out[2*i]:.3f} ms = "
+                      f"{out[2*i+1]/out[2*i]/1e9:.2f} TB/s", flush=True)
 st = ice.IceState(m, ice.IceOptions(tol=0.0, max_iters=10**6, mad_max=0, min_nnz=0))
 def run_shard(n):
     """A shard cannot use hh_ice_run: one-rank sharded loop, wall time."""
