@@ -109,6 +109,8 @@ PMC_SOURCES = {
     "c4": _ICE_SOURCES, "c4h": _ICE_SOURCES, "c3": _ICE_SOURCES, "c2": _ICE_SOURCES, "cis": _ICE_SOURCES,
     "gw": ("gw.hip", "pairs.hip", "hh_common.hpp", "ice_internal.hpp", "synth.hip"),
     "c5": ("comp.hip", "hh_common.hpp"),
+    "twostep": ("dense.hip", "hh_common.hpp", "ice_internal.hpp"),
+    "twostep_genome": ("dense.hip", "hh_common.hpp", "ice_internal.hpp"),
 }
 
 
@@ -175,6 +177,27 @@ def gw_pmc_traffic(workload):
     tot = sum(v["traffic_bytes"] * v.get("dispatches", 0) for k, v in data.items()
               if k != "_meta" and "synth" not in k)
     return tot / n_corr, src
+
+
+def twostep_pmc_traffic(line, workload):
+    """HBM bytes per step of a TwoStep line (one hh_twostep_batch call: the
+    chr1 device call or the whole 40 kb genome) from the committed PMC summary
+    of that line at these sources on this workload (profiles/*_<line>_pmc.json):
+    the batch kernels (k_rowstats_b, k_ts_*_b, k_sv_*_b; the bench's untimed
+    host-array / pixel-table calls run other kernels) summed over their
+    dispatches, divided by the dispatches of the output pass k_sv_out_b (one
+    per batch call); (None, None) without one."""
+    got = pmc_pick(line, workload)
+    if got is None:
+        return None, None
+    data, _, src = got
+    items = [(k, v) for k, v in data.items() if k != "_meta"]
+    batch = [(k, v) for k, v in items if any(s in k for s in ("k_rowstats_b", "k_ts_gapdef_b", "k_ts_alpha_b",
+                                                               "k_sv_"))]
+    calls = sum(v.get("dispatches", 0) for k, v in batch if "k_sv_out_b" in k)
+    if not calls:
+        return None, None
+    return sum(v["traffic_bytes"] * v.get("dispatches", 0) for k, v in batch) / calls, src
 
 
 def c5_pmc_traffic(workload, kernels, primary, launches):
@@ -1113,6 +1136,11 @@ def run_twostep(args, world, rank, local):
                "host_arrays_ms": 1000.0 * host_s, "cells_in_upper_out_ms": 1000.0 * cells_s,
                "note": "host_arrays_ms: numpy N x N in / out (PCIe: 1.55 GB per call); cells_in_upper_out_ms: "
                        "pixel tables in, corrected upper tables out (TwoStepCorrectionPixels)"}
+        tr, tr_src = twostep_pmc_traffic("twostep", {"workload": "twostep-chr1-40kb", "N": N})
+        if tr:
+            out["roofline"].update(traffic=tr, traffic_source=tr_src, traffic_GBps=tr / step / 1e9,
+                                   traffic_frac=tr / step / 1e9 / PEAK_HBM_GBS,
+                                   traffic_note="2 x FETCH_SIZE + WRITE_SIZE of the batch kernels per call")
         if not args.no_cpu:
             from oracle import hichap_ref
             t = time.perf_counter()
@@ -1208,6 +1236,12 @@ def run_twostep_genome(args, world, rank, local):
                             "note": "40 B per matrix element (3 int64 reads + 2 fp64 writes), the whole genome per step"},
                "sequential_ms": 1000.0 * seq,
                "note": "sequential_ms: the same 23 chromosomes as one TwoStepCorrection call each"}
+        tr, tr_src = twostep_pmc_traffic("twostep_genome", {"workload": "twostep-hg19-40kb-genome",
+                                                            "bins": int(sum(int(N) for N in Ns)), "sum_N2": sq})
+        if tr:
+            out["roofline"].update(traffic=tr, traffic_source=tr_src, traffic_GBps=tr / step / 1e9,
+                                   traffic_frac=tr / step / 1e9 / PEAK_HBM_GBS,
+                                   traffic_note="2 x FETCH_SIZE + WRITE_SIZE of the batch kernels per genome")
         if not args.no_cpu:
             from oracle import hichap_ref
             k = names.index("21")

@@ -557,6 +557,29 @@ __device__ __forceinline__ void flat_seg_c_pipe(const uint4* __restrict__ pay4, 
     }
 }
 
+// flat_seg_c_pipe with two runs in flight ahead of the one being walked (v:
+// the current run, vn: the next, both loaded by the caller; k_sweep_flatw3
+// DEPTH 2): the same steps in the same order, bitwise the same sums
+template <int U, int ABL, int EPV>
+__device__ __forceinline__ void flat_seg_c_pipe2(const uint4* __restrict__ pay4, uint4 (&v)[U], uint4 (&vn)[U],
+                                                 uint32_t qb, int i1, const uint16_t* __restrict__ fst, int nfr,
+                                                 const double* __restrict__ bl, double* __restrict__ accc, int lane) {
+    if (i1 <= 0) return;
+    int ic = 0;
+    for (uint32_t q0 = 0;;) {
+        const uint32_t qnn = q0 + 128u * U;
+        uint4 vnn[U];
+        if (qnn < qb) flat_load<U>(pay4, qnn + (uint32_t)lane * U, 0u, qb, vnn);
+        flat_step_c<U, ABL, EPV>(v, q0, qb, ic, i1, fst, nfr, bl, accc, lane);
+        q0 += 64u * U;
+        if (q0 >= qb) break;
+#pragma unroll
+        for (int k = 0; k < U; ++k) v[k] = vn[k];
+#pragma unroll
+        for (int k = 0; k < U; ++k) vn[k] = vnn[k];
+    }
+}
+
 template <int U, int ABL, int EPV, bool COL = false>
 __device__ __forceinline__ void flat_seg_pipe(const uint4* __restrict__ pay4, uint4 (&v)[U], uint32_t qa, uint32_t qb,
                                               int i0, int i1, const uint16_t* __restrict__ fst,
@@ -1105,7 +1128,7 @@ struct FlatW3Lds {
     uint8_t act[64];
 };
 
-template <int U, int ABL, int NW = kFlatWaves>
+template <int U, int ABL, int NW = kFlatWaves, int DEPTH = 1>
 __global__ __launch_bounds__(NW * 64, NW > 8 ? 3 : 2) void k_sweep_flatw3(TileDev T, const uint8_t* __restrict__ act,
                                                                         const double* __restrict__ b,
                                                                         long long n_bins, double* __restrict__ part) {
@@ -1207,9 +1230,15 @@ __global__ __launch_bounds__(NW * 64, NW > 8 ? 3 : 2) void k_sweep_flatw3(TileDe
     Tw cur;
     uint32_t dw = 0;
     bool any = settle(claim(dw), dw, cur);
-    uint4 v[U], vw[UW];
+    uint4 v[U], vn[DEPTH > 1 ? U : 1], vw[UW];
+    // the first narrow run(s) of a tile (DEPTH 2: the first two)
+    auto first_runs = [&](const Tw& x) {
+        if (x.nfn) flat_load<U>(x.payn4, (uint32_t)lane * U, 0u, x.qbn, v);
+        if constexpr (DEPTH > 1)
+            if (64u * U < x.qbn) flat_load<U>(x.payn4, 64u * U + (uint32_t)lane * U, 0u, x.qbn, vn);
+    };
     if (any) {
-        if (cur.nfn) flat_load<U>(cur.payn4, (uint32_t)lane * U, 0u, cur.qbn, v);
+        first_runs(cur);
         if (cur.nfw) flat_load<UW>(cur.payw4, (uint32_t)lane * UW, 0u, cur.qbw, vw);
         rec_load(cur);
     }
@@ -1224,7 +1253,10 @@ __global__ __launch_bounds__(NW * 64, NW > 8 ? 3 : 2) void k_sweep_flatw3(TileDe
         const int kn = claim(dwn);
         wave_lds_sync();
         const bool idn = cur.nfn == cur.nr;
-        flat_seg_c_pipe<U, ABL, 8>(cur.payn4, v, 0u, cur.qbn, 0, cur.nfn, fstn, cur.nfn, bl, acc, lane);
+        if constexpr (DEPTH > 1)
+            flat_seg_c_pipe2<U, ABL, 8>(cur.payn4, v, vn, cur.qbn, cur.nfn, fstn, cur.nfn, bl, acc, lane);
+        else
+            flat_seg_c_pipe<U, ABL, 8>(cur.payn4, v, 0u, cur.qbn, 0, cur.nfn, fstn, cur.nfn, bl, acc, lane);
         wave_lds_sync();
         constexpr int PL = kR / 64;
         double cv[PL];
@@ -1248,7 +1280,7 @@ __global__ __launch_bounds__(NW * 64, NW > 8 ? 3 : 2) void k_sweep_flatw3(TileDe
         Tw nxt;
         const bool more = settle(kn, dwn, nxt);
         if (more) {
-            if (nxt.nfn) flat_load<U>(nxt.payn4, (uint32_t)lane * U, 0u, nxt.qbn, v);
+            first_runs(nxt);
             if (nxt.nfw) flat_load<UW>(nxt.payw4, (uint32_t)lane * UW, 0u, nxt.qbw, vw);
             rec_load(nxt);
         }
@@ -2670,10 +2702,15 @@ static void launch_sweep_up(const hh_matrix* m, const TileDev& T, const uint8_t*
             if (g_flatw_waves == 10 && g_flatw_u != 16) {
                 kern = g_flatw_pipe == 2 ? k_sweep_flatw<kFlatU, ABL, 2, 10> : k_sweep_flatw<kFlatU, ABL, 0, 10>;
                 nw = 10;
+            } else if (g_flatw_pipe >= 3 && g_flatw_u != 16) {
+                // k_sweep_flatw3: the per-tile chain off the critical path
+                // (pipe 3: one run ahead; 4: two), 11 or 8 waves
+                nw = g_flatw_waves == 8 ? 8 : 11;
+                kern = nw == 8 ? (g_flatw_pipe == 4 ? k_sweep_flatw3<kFlatU, ABL, 8, 2> : k_sweep_flatw3<kFlatU, ABL, 8, 1>)
+                               : (g_flatw_pipe == 4 ? k_sweep_flatw3<kFlatU, ABL, 11, 2>
+                                                    : k_sweep_flatw3<kFlatU, ABL, 11, 1>);
             } else if (g_flatw_waves == 11 && g_flatw_u != 16) {
-                kern = g_flatw_pipe == 3   ? k_sweep_flatw3<kFlatU, ABL, 11>
-                       : g_flatw_pipe == 2 ? k_sweep_flatw<kFlatU, ABL, 2, 11>
-                                           : k_sweep_flatw<kFlatU, ABL, 0, 11>;
+                kern = g_flatw_pipe == 2 ? k_sweep_flatw<kFlatU, ABL, 2, 11> : k_sweep_flatw<kFlatU, ABL, 0, 11>;
                 nw = 11;
             }
         }
@@ -3102,7 +3139,7 @@ int hh_tune(const char* key, int64_t value) {
             HH_REQUIRE(value >= -1 && value <= 1, "flat_cols in {-1 (auto), 0, 1}");
             g_flat_cols = value;
         } else if (k == "flatw_pipe") {
-            HH_REQUIRE(value >= 0 && value <= 3, "flatw_pipe in {0, 1, 2, 3}");
+            HH_REQUIRE(value >= 0 && value <= 4, "flatw_pipe in {0, 1, 2, 3, 4}");
             g_flatw_pipe = (int)value;
         } else if (k == "band_dpp") {
             HH_REQUIRE(value == 0 || value == 1, "band_dpp in {0, 1}");

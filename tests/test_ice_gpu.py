@@ -367,8 +367,9 @@ def test_flat_block_shapes_bitwise(ice, upper):
 @pytest.mark.parametrize("cis_only", [0, 1])
 def test_flatw_early_claim_bitwise(ice, cis_only):
     """k_sweep_flatw3 (flatw_pipe 3: the next tile claimed during the walk,
-    its record prefetched with its payload, active flags from LDS) walks the
-    same tiles with the same sums as k_sweep_flatw: bitwise the same weights
+    its record prefetched with its payload, active flags from LDS; 4: two
+    narrow runs in flight ahead; 8 or 11 waves) walks the same tiles with the
+    same sums as k_sweep_flatw: bitwise the same weights
     and iterations, genome-wide (one ICE group) and --cis-only (a group per
     chromosome, converging at different iterations: the skip path)."""
     from hichap_master_amd import _lib
@@ -377,14 +378,16 @@ def test_flatw_early_claim_bitwise(ice, cis_only):
     res = []
     _lib.call("hh_tune", b"flat_cols", 1)
     try:
-        for pipe in (2, 3, 2, 3):
+        for pipe, waves in ((2, 11), (3, 11), (4, 8), (3, 8), (4, 11), (3, 11)):
             _lib.call("hh_tune", b"flatw_pipe", pipe)
+            _lib.call("hh_tune", b"flatw_waves", waves)
             m = ice.ContactMatrix.from_pixels(b1, b2, c, n, off, cis_only=cis_only)
             assert m.info()["n_units_flat"] > 0
             res.append(ice.balance_matrix(m, ice.IceOptions(max_iters=300)))
             m.close()
     finally:
         _lib.call("hh_tune", b"flatw_pipe", 2)
+        _lib.call("hh_tune", b"flatw_waves", 11)
         _lib.call("hh_tune", b"flat_cols", -1)
     for w, st in res[1:]:
         np.testing.assert_array_equal(w, res[0][0])

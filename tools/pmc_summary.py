@@ -8,7 +8,7 @@ the bytes; WRITE_SIZE is exact for 16-B/lane stores.  traffic_bytes =
 
   pmc_summary.py fetch.csv write.csv out.json [commit] [real_bytes_per_sweep] [line bench.log]
 
-With `line` (c4 | c4h | c3 | c2 | cis | gw | c5) and the profiled bench's log, _meta records the
+With `line` (c4 | c4h | c3 | c2 | cis | gw | c5 | twostep | twostep_genome) and the profiled bench's log, _meta records the
 sources' fingerprint (bench.src_sha) and the workload of that run, so bench.py
 reports the traffic only for runs of the same build on the same workload."""
 import collections
@@ -20,6 +20,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 WORKLOAD_KEYS = {"c4": ("n_bins", "nnz_upper"), "gw": ("T_pixels", "H_cells"),
                  "c5": ("workload", "n_chroms", "bins_total"),
+                 "twostep": ("workload", "N"), "twostep_genome": ("workload", "bins", "sum_N2"),
                  **{k: ("n_bins", "nnz_upper") for k in ("c4h", "c3", "c2", "cis")}}
 
 
