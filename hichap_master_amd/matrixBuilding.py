@@ -826,11 +826,26 @@ class NPZ2Cooler:
         coolio.create_cooler(self.outfil, {res: t + (meta,) for res, t in tabs.items()}, mode="a")
 
 
-def merge_coolers(output_uri, input_uris):
+def _write_coolers(outfil, parts, genomeSize, chroms):
+    """Several NPZ2Cooler calls into one file as ONE write (every
+    append rewrites the whole file, so one call per part made the file I/O
+    quadratic in the resolutions): ``parts`` = [(datasets, onlyIntra, dtype)],
+    the same groups, tables and metadata as the calls one after the other."""
+    from . import coolio
+    spec = {}
+    for datasets, onlyIntra, dtype in parts:
+        meta = {"onlyIntra": str(onlyIntra)}
+        for res, t in npz2cooler_tables(datasets, genomeSize, chroms, onlyIntra, dtype).items():
+            spec[res] = t + (meta,)
+    coolio.create_cooler(os.path.abspath(os.path.expanduser(outfil)), spec, mode="a")
+
+
+def merge_coolers(output_uri, input_uris, write=True):
     """cooler.merge_coolers as TraditionalMatrixConstruction calls it
     (:680-695): the inputs' pixels of one resolution summed into
     ``output_uri`` (appended to its file); every input must have the same
-    bins."""
+    bins.  write=False: return (group, table spec) instead, for one
+    create_cooler over every resolution."""
     from . import coolio
     tabs, cs, meta = [], None, None
     for uri in input_uris:
@@ -852,7 +867,19 @@ def merge_coolers(output_uri, input_uris):
         meta = json.loads(meta) if isinstance(meta, str) else meta
     except ValueError:
         meta = None
+    if not write:
+        return path, grp, (cs, b1, b2, v.astype(dt), meta)
     coolio.create_cooler(path, {grp: (cs, b1, b2, v.astype(dt), meta)}, mode="a")
+
+
+def _merge_all(merged, reps, resolutions):
+    """merge_coolers for every resolution into ``merged`` as one write."""
+    from . import coolio
+    spec = {}
+    for res in resolutions:
+        _, grp, t = merge_coolers(f"{merged}::{res}", [f"{r}::{res}" for r in reps], write=False)
+        spec[grp] = t
+    coolio.create_cooler(merged, spec, mode="a")
 
 
 def _balance_all(coolers, wholeRes, localRes):
@@ -892,14 +919,12 @@ def TraditionalMatrixConstruction(OutPath, RepPath, genomeSize, wholeRes, localR
         out = os.path.join(CoolerPath, prefix + "Multi.cool")
         if os.path.exists(out):
             os.remove(out)  # written afresh (the reference appends into an existing file)
-        NPZ2Cooler(Whole_Lib, out, genomeSize, chroms, onlyIntra=False, dtype="int")
-        NPZ2Cooler(Local_Lib, out, genomeSize, chroms, onlyIntra=True, dtype="int")
+        _write_coolers(out, [(Whole_Lib, False, "int"), (Local_Lib, True, "int")], genomeSize, chroms)
         reps.append(out)
     merged = os.path.join(CoolerPath, "Merged_Multi.cool")
     if os.path.exists(merged):
         os.remove(merged)
-    for res in list(wholeRes) + list(localRes):
-        merge_coolers(f"{merged}::{res}", [f"{r}::{res}" for r in reps])
+    _merge_all(merged, reps, list(wholeRes) + list(localRes))
     coolers = reps + [merged]
     if balance:
         _balance_all(coolers, wholeRes, localRes)
@@ -937,8 +962,7 @@ def _haplotype_coolers(OutPath, prefix, genomeSize, wholeRes, localRes, chroms, 
     W = {res: WholeMatrixToSparseDict(DataSets["Tradition_Whole"][res]["Bins"],
                                       DataSets["Tradition_Whole"][res]["Matrix"]) for res in wholeRes}
     L = {res: IntraMatrixToSparseDict(DataSets["Tradition_Local"][res]) for res in localRes}
-    NPZ2Cooler(W, trad, genomeSize, chroms, onlyIntra=False, dtype="int")
-    NPZ2Cooler(L, trad, genomeSize, chroms, onlyIntra=True, dtype="int")
+    _write_coolers(trad, [(W, False, "int"), (L, True, "int")], genomeSize, chroms)
     _balance_all([trad], wholeRes, localRes)
     hap_gs, hap_chroms = _hap_genome(genomeSize, chroms, os.path.join(OutPath, "Hap_genomeSize"))
     unimp = os.path.join(OutPath, prefix + "UnImputated_Haplotype_Multi.cool")
@@ -949,8 +973,7 @@ def _haplotype_coolers(OutPath, prefix, genomeSize, wholeRes, localRes, chroms, 
     W = {res: WholeMatrixToSparseDict(DataSets["UnImputated_Whole"][res]["Bins"],
                                       DataSets["UnImputated_Whole"][res]["Matrix"]) for res in wholeRes}
     L = {res: IntraMatrixToSparseDict(DataSets["UnImputated_Local"][res]) for res in localRes}
-    NPZ2Cooler(W, unimp, hap_gs, hap_chroms, onlyIntra=False, dtype="int")
-    NPZ2Cooler(L, unimp, hap_gs, hap_chroms, onlyIntra=True, dtype="int")
+    _write_coolers(unimp, [(W, False, "int"), (L, True, "int")], hap_gs, hap_chroms)
     BW = {}
     for res in wholeRes:
         hb = DataSets["Imputated_Whole"][res]["Bins"]
@@ -967,8 +990,7 @@ def _haplotype_coolers(OutPath, prefix, genomeSize, wholeRes, localRes, chroms, 
     # np.savez of the per-resolution dicts, as the reference saves them (:1616-1617)
     np.savez(os.path.join(OutPath, prefix + "Imputated_Gap.npz"),
              **{k: np.array(v, dtype=object) for k, v in Gap_Local.items()})
-    NPZ2Cooler(BW, imp, hap_gs, hap_chroms, onlyIntra=False, dtype="float")
-    NPZ2Cooler(BL, imp, hap_gs, hap_chroms, onlyIntra=True, dtype="float")
+    _write_coolers(imp, [(BW, False, "float"), (BL, True, "float")], hap_gs, hap_chroms)
     return trad, unimp, imp
 
 
