@@ -582,6 +582,7 @@ void build_from_device_pixels(const Id* b1, const Id* b2, const Cnt* cnt, int64_
     P.wide_cnt = m->wide_cnt.p;
     if (nloc) hipLaunchKernelGGL((k_px_rows<1>), rgrid, dim3(256), 0, s, P);
     HIP_CHECK(hipGetLastError());
+    finalize_flat_layout(*m, s);
     HIP_CHECK(hipStreamSynchronize(s));  // scratch buffers return to the pool
     phase("pass 1");
     int64_t nb = 0, ent = 0, up = 0;

@@ -43,6 +43,7 @@ constexpr int kThreads = 256;
 constexpr int kSweepThreads = 512;
 constexpr int kSweepWaves = kSweepThreads / 64;
 constexpr int kFlatU = 8;  // uint4 per lane per step in flat narrow segments
+static_assert(kFlatU == kFlatIlvU, "k_sweep_flatw walks the interleaved layout's runs");
 
 // Entry decode: the byte offset of the staged bias value is a field of the
 // entry (ice_internal.hpp), so an entry costs mask, shift, cvt, LDS read and
@@ -331,6 +332,33 @@ __device__ __forceinline__ void flat_load(const uint4* __restrict__ pay4, uint32
     }
 }
 
+// The same run [q0 + U lane, + U) of a step chunk of an interleaved segment
+// (finalize_flat_layout: element k of the chunk's runs stored contiguously,
+// cnt_k lanes): U coalesced loads, the registers flat_load would fill.
+template <int U>
+__device__ __forceinline__ void flat_load_ilv(const uint4* __restrict__ pay4, uint32_t q0, uint32_t qb, int lane,
+                                              uint4 (&v)[U]) {
+    static_assert(U == kFlatIlvU, "interleaved segments are laid out for kFlatIlvU uint4 per lane");
+    const uint4 zero = make_uint4(0u, 0u, 0u, 0u);
+    const uint32_t m = qb - q0 < 64u * U ? qb - q0 : 64u * U;
+    uint32_t base = q0;
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+        const uint32_t cnt = flat_ilv_cnt(m, k);
+        const bool on = (uint32_t)lane < cnt;
+        const uint4 x = ld16(pay4 + base + (on ? (uint32_t)lane : 0u));
+        v[k] = on ? x : zero;
+        base += cnt;
+    }
+}
+// a run of a plain (lane-major) or interleaved segment
+template <int U, bool ILV>
+__device__ __forceinline__ void flat_run(const uint4* __restrict__ pay4, uint32_t q0, uint32_t qa, uint32_t qb,
+                                         int lane, uint4 (&v)[U]) {
+    if constexpr (ILV) flat_load_ilv<U>(pay4, q0, qb, lane, v);
+    else flat_load<U>(pay4, q0 + (uint32_t)lane * U, qa, qb, v);
+}
+
 // One step of a wave over uint4 [q0, q0 + 64 U) of its range [.., qb): v
 // holds the lane's run [s, s + U), s = q0 + lane U.  ic = the row holding
 // q0 - 1 (q0 at the first step); rows [.., i1) belong to the wave; fst =
@@ -520,7 +548,7 @@ __device__ __forceinline__ void flat_step_c(const uint4 (&v)[U], uint32_t q0, ui
     ic = __shfl(lo + j, 63, 64);
 }
 
-template <int U, int ABL, int EPV, bool COL = false>
+template <int U, int ABL, int EPV, bool COL = false, bool ILV = false>
 __device__ __forceinline__ void flat_seg_c(const uint4* __restrict__ pay4, uint4 (&v)[U], uint32_t qa, uint32_t qb,
                                            int i0, int i1, const uint16_t* __restrict__ fst, int nfr,
                                            const double* __restrict__ bl, double* __restrict__ accc, int lane,
@@ -531,14 +559,14 @@ __device__ __forceinline__ void flat_seg_c(const uint4* __restrict__ pay4, uint4
         flat_step_c<U, ABL, EPV, COL>(v, q0, qb, ic, i1, fst, nfr, bl, accc, lane, ca, fid);
         q0 += 64u * U;
         if (q0 >= qb) break;
-        flat_load<U>(pay4, q0 + (uint32_t)lane * U, qa, qb, v);
+        flat_run<U, ILV>(pay4, q0, qa, qb, lane, v);
     }
 }
 
 // flat_seg_c / flat_seg with the next step's run loaded before the current
 // step is walked (two runs in registers: the one-wave-per-tile kernel has
 // the VGPRs for it); the same steps in the same order, bitwise the same sums
-template <int U, int ABL, int EPV, bool COL = false>
+template <int U, int ABL, int EPV, bool COL = false, bool ILV = false>
 __device__ __forceinline__ void flat_seg_c_pipe(const uint4* __restrict__ pay4, uint4 (&v)[U], uint32_t qa, uint32_t qb,
                                                 int i0, int i1, const uint16_t* __restrict__ fst, int nfr,
                                                 const double* __restrict__ bl, double* __restrict__ accc, int lane,
@@ -548,35 +576,12 @@ __device__ __forceinline__ void flat_seg_c_pipe(const uint4* __restrict__ pay4, 
     for (uint32_t q0 = qa;;) {
         const uint32_t qn = q0 + 64u * U;
         uint4 vn[U];
-        if (qn < qb) flat_load<U>(pay4, qn + (uint32_t)lane * U, qa, qb, vn);
+        if (qn < qb) flat_run<U, ILV>(pay4, qn, qa, qb, lane, vn);
         flat_step_c<U, ABL, EPV, COL>(v, q0, qb, ic, i1, fst, nfr, bl, accc, lane, ca, fid);
         if (qn >= qb) break;
 #pragma unroll
         for (int k = 0; k < U; ++k) v[k] = vn[k];
         q0 = qn;
-    }
-}
-
-// flat_seg_c_pipe with two runs in flight ahead of the one being walked (v:
-// the current run, vn: the next, both loaded by the caller; k_sweep_flatw3
-// DEPTH 2): the same steps in the same order, bitwise the same sums
-template <int U, int ABL, int EPV>
-__device__ __forceinline__ void flat_seg_c_pipe2(const uint4* __restrict__ pay4, uint4 (&v)[U], uint4 (&vn)[U],
-                                                 uint32_t qb, int i1, const uint16_t* __restrict__ fst, int nfr,
-                                                 const double* __restrict__ bl, double* __restrict__ accc, int lane) {
-    if (i1 <= 0) return;
-    int ic = 0;
-    for (uint32_t q0 = 0;;) {
-        const uint32_t qnn = q0 + 128u * U;
-        uint4 vnn[U];
-        if (qnn < qb) flat_load<U>(pay4, qnn + (uint32_t)lane * U, 0u, qb, vnn);
-        flat_step_c<U, ABL, EPV>(v, q0, qb, ic, i1, fst, nfr, bl, accc, lane);
-        q0 += 64u * U;
-        if (q0 >= qb) break;
-#pragma unroll
-        for (int k = 0; k < U; ++k) v[k] = vn[k];
-#pragma unroll
-        for (int k = 0; k < U; ++k) vn[k] = vnn[k];
     }
 }
 
@@ -997,7 +1002,7 @@ __global__ __launch_bounds__(NW * 64, NW > 8 ? 3 : 2) void k_sweep_flatw(TileDev
     Tw cur;
     const bool any = grab(cur);
     uint4 v[U], vw[UW];
-    if (any && cur.nfn) flat_load<U>(cur.payn4, (uint32_t)lane * U, 0u, cur.qbn, v);
+    if (any && cur.nfn) flat_load_ilv<U>(cur.payn4, 0u, cur.qbn, lane, v);
     if (any && cur.nfw) flat_load<UW>(cur.payw4, (uint32_t)lane * UW, 0u, cur.qbw, vw);
     for (; any;) {
         const uint4* rg = T.frec + (size_t)cur.frec * kFrecU4;
@@ -1040,11 +1045,14 @@ __global__ __launch_bounds__(NW * 64, NW > 8 ? 3 : 2) void k_sweep_flatw(TileDev
         wave_lds_sync();
         const ColArgs ca{cur.bblk, L.cacc};
         if (UP && cur.up) {  // (not software-pipelined: the column side needs the registers)
-            flat_seg_c<U, ABL, 8, true>(cur.payn4, v, 0u, cur.qbn, 0, cur.nfn, fstn, cur.nfn, bl, acc, lane, ca,
-                                        idn ? nullptr : fidn);
+            flat_seg_c<U, ABL, 8, true, true>(cur.payn4, v, 0u, cur.qbn, 0, cur.nfn, fstn, cur.nfn, bl, acc, lane,
+                                              ca, idn ? nullptr : fidn);
         } else {
-            if (PIPE) flat_seg_c_pipe<U, ABL, 8>(cur.payn4, v, 0u, cur.qbn, 0, cur.nfn, fstn, cur.nfn, bl, acc, lane);
-            else flat_seg_c<U, ABL, 8>(cur.payn4, v, 0u, cur.qbn, 0, cur.nfn, fstn, cur.nfn, bl, acc, lane);
+            if (PIPE)
+                flat_seg_c_pipe<U, ABL, 8, false, true>(cur.payn4, v, 0u, cur.qbn, 0, cur.nfn, fstn, cur.nfn, bl, acc,
+                                                        lane);
+            else
+                flat_seg_c<U, ABL, 8, false, true>(cur.payn4, v, 0u, cur.qbn, 0, cur.nfn, fstn, cur.nfn, bl, acc, lane);
         }
         wave_lds_sync();
         // compact narrow sums -> rows (zeros for rows without narrow entries)
@@ -1082,7 +1090,7 @@ __global__ __launch_bounds__(NW * 64, NW > 8 ? 3 : 2) void k_sweep_flatw(TileDev
         if (PIPE == 2) {
             more = grab(nxt);
             if (more) {
-                if (nxt.nfn) flat_load<U>(nxt.payn4, (uint32_t)lane * U, 0u, nxt.qbn, v);
+                if (nxt.nfn) flat_load_ilv<U>(nxt.payn4, 0u, nxt.qbn, lane, v);
                 if (nxt.nfw) flat_load<UW>(nxt.payw4, (uint32_t)lane * UW, 0u, nxt.qbw, vw);
             }
         }
@@ -1092,7 +1100,7 @@ __global__ __launch_bounds__(NW * 64, NW > 8 ? 3 : 2) void k_sweep_flatw(TileDev
         if (PIPE != 2) {
             more = grab(nxt);
             if (more) {
-                if (nxt.nfn) flat_load<U>(nxt.payn4, (uint32_t)lane * U, 0u, nxt.qbn, v);
+                if (nxt.nfn) flat_load_ilv<U>(nxt.payn4, 0u, nxt.qbn, lane, v);
                 if (nxt.nfw) flat_load<UW>(nxt.payw4, (uint32_t)lane * UW, 0u, nxt.qbw, vw);
             }
         }
@@ -1105,208 +1113,25 @@ __global__ __launch_bounds__(NW * 64, NW > 8 ? 3 : 2) void k_sweep_flatw(TileDev
     }
 }
 
-// K1c'' (round 6, hh_tune flatw_pipe 3): k_sweep_flatw with the per-tile
-// chain taken off the wave's critical path.  In k_sweep_flatw a wave, after
-// its walk, claims the next tile (LDS counter -> descriptor -> the rows'
-// active flags: two dependent global round trips), issues its first payload
-// runs and only then loads its flat record (a third round trip) -- about a
-// tile's worth of latency in which the wave has at most one run in flight.
-// Here the next tile is claimed right after the current record is staged: its
-// descriptor comes in as one dword per lane (a vector load, so it waits on
-// vmcnt behind the payload runs already in flight, not on the LDS queue the
-// walk uses), its active flags from an LDS copy of act (matrices with <= 64
-// ICE groups; a single-group matrix needs none), and after the walk the next
-// tile's payload runs AND record are issued together, the record held in
-// registers while this tile's row sums go out.  The walk is k_sweep_flatw's:
-// the same sums in the same order, bitwise the same partials.
-template <int NW>
-struct FlatW3Lds {
-    double bl[kW];
-    uint16_t rec[NW][kFrecU4 * 8];
-    double acc[NW][kR];
-    int next;
-    uint8_t act[64];
-};
-
-template <int U, int ABL, int NW = kFlatWaves, int DEPTH = 1>
-__global__ __launch_bounds__(NW * 64, NW > 8 ? 3 : 2) void k_sweep_flatw3(TileDev T, const uint8_t* __restrict__ act,
-                                                                        const double* __restrict__ b,
-                                                                        long long n_bins, double* __restrict__ part) {
-    constexpr int UW = 2;
-    __shared__ __attribute__((aligned(16))) FlatW3Lds<NW> L;
-    const int k0 = T.fg_ptr[blockIdx.x], nk = T.fg_ptr[blockIdx.x + 1] - k0;
-    const int ng = T.ngroups;  // ICE groups of the matrix (0: unknown -> global flags)
-    {
-        bool on = false;  // block-uniform: any active tile in the group
-        for (int k = 0; k < nk && !on; ++k) {
-            const int u = T.fg_unit[k0 + k];
-            for (int g = T.u_glo[u]; g <= T.u_ghi[u]; ++g) on |= act[g] != 0;
-        }
-        if (!on) return;
-    }
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    if (threadIdx.x == 0) L.next = 0;
-    if (ng > 1 && ng <= 64 && threadIdx.x < ng) L.act[threadIdx.x] = act[threadIdx.x];
-    if (ABL != 2 && threadIdx.x < kSweepThreads) stage_bias(L.bl, b, (long long)T.tile_J[T.u_tlo[T.fg_unit[k0]]] * kW, n_bins);
-    __syncthreads();
-    const double* __restrict__ bl = L.bl;
-    uint16_t* __restrict__ rec = L.rec[wave];
-    double* __restrict__ acc = L.acc[wave];
-    const uint16_t* fstn = rec;
-    const uint16_t* fstw = rec + (kR + 1);
-    const uint16_t* fidn = rec + 2 * (kR + 1);
-    const uint16_t* fidw = fidn + kR;
-    const uint32_t* dsc = reinterpret_cast<const uint32_t*>(T.fg_desc + k0);
-    constexpr int DW = (int)(sizeof(FlatDesc) / 4);
-    struct Tw {
-        int slot, frec, nr, nfn, nfw;
-        uint32_t qbn, qbw;
-        const uint4 *payn4, *payw4;
-    };
-    // claim a tile: its index (LDS counter) and its descriptor, one dword per
-    // lane, in flight; -1 when the group is exhausted
-    auto claim = [&](uint32_t& dw) -> int {
-        int k = 0;
-        if (lane == 0) k = atomicAdd(&L.next, 1);
-        k = __builtin_amdgcn_readfirstlane(__shfl(k, 0, 64));
-        if (k >= nk) return -1;
-        dw = dsc[(size_t)k * DW + (lane < DW ? lane : 0)];
-        return k;
-    };
-    auto field = [&](uint32_t dw, int i) -> uint32_t { return (uint32_t)__builtin_amdgcn_readlane((int)dw, i); };
-    auto decode = [&](uint32_t dw, Tw& x) {
-        const long long entn = (long long)(((uint64_t)field(dw, 1) << 32) | field(dw, 0));
-        const long long ent = (long long)(((uint64_t)field(dw, 3) << 32) | field(dw, 2));
-        const uint32_t w8 = field(dw, 8), w9 = field(dw, 9);
-        x = Tw{(int)field(dw, 5), (int)field(dw, 4), (int)(w8 & 0xFFFFu), (int)(w8 >> 16), (int)(w9 & 0xFFFFu),
-               field(dw, 6), field(dw, 7), reinterpret_cast<const uint4*>(T.payn + entn),
-               reinterpret_cast<const uint4*>(T.pay + ent)};
-    };
-    // the claimed tile's rows active?  (glo = hi half of dword 9, ghi = lo half of 10)
-    auto active = [&](uint32_t dw) -> bool {
-        if (ng == 1) return true;
-        const int glo = (int)(field(dw, 9) >> 16), ghi = (int)(field(dw, 10) & 0xFFFFu);
-        bool on = false;
-        if (ng > 1 && ng <= 64) {
-            for (int g = glo; g <= ghi; ++g) on |= L.act[g] != 0;
-        } else {
-            const int ngr = ghi - glo + 1;
-            if (ngr <= 64) {
-                const uint8_t a = act[glo + (lane < ngr ? lane : ngr - 1)];
-                on = __ballot((a != 0) & (lane < ngr)) != 0;
-            } else {
-                for (int g = glo; g <= ghi; ++g) on |= act[g] != 0;
-            }
-        }
-        return on;
-    };
-    // the next active tile, descriptor already in dw for the first candidate
-    auto settle = [&](int k, uint32_t dw, Tw& x) -> bool {
-        while (k >= 0 && !active(dw)) k = claim(dw);
-        if (k < 0) return false;
-        decode(dw, x);
-        return true;
-    };
-    // the record ranges the walk reads (k_sweep_flatw), loaded into registers
-    uint4 tq[8];
-    int qs[8];
-    auto rec_load = [&](const Tw& x) {
-        const uint4* rg = T.frec + (size_t)x.frec * kFrecU4;
-        const bool idn = x.nfn == x.nr;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const int g = i >> 1, h = i & 1;
-            const int h0 = g == 0 ? 0 : g == 1 ? kR + 1 : g == 2 ? 2 * (kR + 1) : 2 * (kR + 1) + kR;
-            const int h1 = g == 0   ? x.nfn + 1
-                           : g == 1 ? kR + 1 + x.nfw + 1
-                           : g == 2 ? (idn ? 2 * (kR + 1) : 2 * (kR + 1) + x.nfn)
-                                    : 2 * (kR + 1) + kR + x.nfw;
-            const int q0 = h0 / 8, q1 = (h1 + 7) / 8;
-            const int q = q0 + lane + 64 * h;
-            qs[i] = q < q1 ? q : q0;
-            tq[i] = rg[qs[i]];
-        }
-    };
-    Tw cur;
-    uint32_t dw = 0;
-    bool any = settle(claim(dw), dw, cur);
-    uint4 v[U], vn[DEPTH > 1 ? U : 1], vw[UW];
-    // the first narrow run(s) of a tile (DEPTH 2: the first two)
-    auto first_runs = [&](const Tw& x) {
-        if (x.nfn) flat_load<U>(x.payn4, (uint32_t)lane * U, 0u, x.qbn, v);
-        if constexpr (DEPTH > 1)
-            if (64u * U < x.qbn) flat_load<U>(x.payn4, 64u * U + (uint32_t)lane * U, 0u, x.qbn, vn);
-    };
-    if (any) {
-        first_runs(cur);
-        if (cur.nfw) flat_load<UW>(cur.payw4, (uint32_t)lane * UW, 0u, cur.qbw, vw);
-        rec_load(cur);
-    }
-    for (; any;) {
-        {
-            uint4* r4 = reinterpret_cast<uint4*>(rec);
-            r4[qs[0]] = tq[0], r4[qs[1]] = tq[1], r4[qs[2]] = tq[2], r4[qs[3]] = tq[3];
-            r4[qs[4]] = tq[4], r4[qs[5]] = tq[5], r4[qs[6]] = tq[6], r4[qs[7]] = tq[7];
-        }
-        // the next tile claimed now: its descriptor flies during the walk
-        uint32_t dwn = 0;
-        const int kn = claim(dwn);
-        wave_lds_sync();
-        const bool idn = cur.nfn == cur.nr;
-        if constexpr (DEPTH > 1)
-            flat_seg_c_pipe2<U, ABL, 8>(cur.payn4, v, vn, cur.qbn, cur.nfn, fstn, cur.nfn, bl, acc, lane);
-        else
-            flat_seg_c_pipe<U, ABL, 8>(cur.payn4, v, 0u, cur.qbn, 0, cur.nfn, fstn, cur.nfn, bl, acc, lane);
-        wave_lds_sync();
-        constexpr int PL = kR / 64;
-        double cv[PL];
-        int cid[PL];
-#pragma unroll
-        for (int q = 0; q < PL; ++q) {
-            const int i = lane + 64 * q;
-            cv[q] = i < cur.nfn ? acc[i] : 0.0;
-            cid[q] = i < cur.nfn ? (idn ? i : (int)fidn[i]) : -1;
-        }
-        wave_lds_sync();
-#pragma unroll
-        for (int q = 0; q < PL; ++q) acc[lane + 64 * q] = 0.0;
-        wave_lds_sync();
-#pragma unroll
-        for (int q = 0; q < PL; ++q)
-            if (cid[q] >= 0) acc[cid[q]] = cv[q];
-        wave_lds_sync();
-        flat_seg_pipe<UW, ABL, 4>(cur.payw4, vw, 0u, cur.qbw, 0, cur.nfw, fstw, fidw, cur.nfw, bl, acc, lane);
-        wave_lds_sync();
-        Tw nxt;
-        const bool more = settle(kn, dwn, nxt);
-        if (more) {
-            first_runs(nxt);
-            if (nxt.nfw) flat_load<UW>(nxt.payw4, (uint32_t)lane * UW, 0u, nxt.qbw, vw);
-            rec_load(nxt);
-        }
-        double* __restrict__ out = part + cur.slot;
-        for (int r = lane; r < cur.nr; r += 64) out[r] = acc[r];
-        wave_lds_sync();  // this tile's LDS reads before the next tile's writes
-        if (!more) break;
-        cur = nxt;
-    }
-}
-
 // ---- diagnostics (hh_matrix_stream_probe): read rates of the layout's own
 // buffers without any of the sweep's work, to separate what the buffers and
 // access shapes allow from what the sweep kernels' structure costs.
 // A linear grid-stride read, 8 uint4 per lane in flight.
+// LM: lane-major runs (thread t reads U consecutive uint4, as the flat walk
+// loads them) instead of coalesced instructions.
+template <bool LM = false>
 __global__ __launch_bounds__(256) void k_stream_probe(const uint4* __restrict__ p, long long n16,
                                                       unsigned* __restrict__ sink) {
     constexpr int U = 8;
     uint32_t x = 0;
     const long long step = (long long)gridDim.x * 256 * U;
-    for (long long i0 = (long long)blockIdx.x * 256 * U + threadIdx.x; i0 < n16; i0 += step) {
+    for (long long b0 = (long long)blockIdx.x * 256 * U; b0 < n16; b0 += step) {
+        const long long i0 = LM ? b0 + (long long)threadIdx.x * U : b0 + threadIdx.x;
         uint4 v[U];
 #pragma unroll
         for (int k = 0; k < U; ++k) {
-            const long long i = i0 + 256LL * k;
-            v[k] = ld16(p + (i < n16 ? i : i0));
+            const long long i = LM ? i0 + k : i0 + 256LL * k;
+            v[k] = ld16(p + (i < n16 ? i : b0));
         }
 #pragma unroll
         for (int k = 0; k < U; ++k) x ^= v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
@@ -1317,7 +1142,21 @@ __global__ __launch_bounds__(256) void k_stream_probe(const uint4* __restrict__ 
 // The flat tiles' payload as k_sweep_flatw reaches it (column groups, a wave
 // per tile from an LDS counter, one descriptor load per tile, two runs of U
 // uint4 per lane in flight) but streamed only: no record, no walk, no bias.
-template <int NW, int PADB>
+// COAL: each run loaded as U coalesced instructions (lane l reads uint4 q0 +
+// 64 j + l) instead of the walk's lane-major runs (lane l reads q0 + U l + j).
+template <int U>
+__device__ __forceinline__ void flat_load_coal(const uint4* __restrict__ pay4, uint32_t q0, uint32_t qb, int lane,
+                                               uint4 (&v)[U]) {
+    const uint4 zero = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+        const uint32_t q = q0 + 64u * k + (uint32_t)lane;
+        const bool on = q < qb;
+        const uint4 x = ld16(pay4 + (on ? q : 0u));
+        v[k] = on ? x : zero;
+    }
+}
+template <int NW, int PADB, bool COAL = false>
 __global__ __launch_bounds__(NW * 64) void k_flat_stream_probe(TileDev T, unsigned* __restrict__ sink) {
     constexpr int U = kFlatU, UW = 2;
     __shared__ int next;
@@ -1336,12 +1175,18 @@ __global__ __launch_bounds__(NW * 64) void k_flat_stream_probe(TileDev T, unsign
         const uint4* pn = reinterpret_cast<const uint4*>(T.payn + d.entn);
         const uint4* pw = reinterpret_cast<const uint4*>(T.pay + d.ent);
         uint4 a[U], c[UW];
-        if (d.qbn) flat_load<U>(pn, (uint32_t)lane * U, 0u, d.qbn, a);
+        if (d.qbn) {
+            if (COAL) flat_load_coal<U>(pn, 0u, d.qbn, lane, a);
+            else flat_load<U>(pn, (uint32_t)lane * U, 0u, d.qbn, a);
+        }
         if (d.qbw) flat_load<UW>(pw, (uint32_t)lane * UW, 0u, d.qbw, c);
         for (uint32_t q0 = 0; q0 < d.qbn; q0 += 64u * U) {
             uint4 bn[U];
             const uint32_t qn = q0 + 64u * U;
-            if (qn < d.qbn) flat_load<U>(pn, qn + (uint32_t)lane * U, 0u, d.qbn, bn);
+            if (qn < d.qbn) {
+                if (COAL) flat_load_coal<U>(pn, qn, d.qbn, lane, bn);
+                else flat_load<U>(pn, qn + (uint32_t)lane * U, 0u, d.qbn, bn);
+            }
 #pragma unroll
             for (int j = 0; j < U; ++j) x ^= a[j].x ^ a[j].y ^ a[j].z ^ a[j].w;
             if (qn >= d.qbn) break;
@@ -2630,7 +2475,6 @@ namespace hh {
 
 // Tuning knobs (hh_tune; no effect on results except the ablations).
 static int g_sweep_nb = 2;
-static int g_flatw_u = 8;     // uint4 per lane per step in k_sweep_flatw (8 or 16)
 static int g_band_dpp = 0;    // band sweep: a lane's previous 16 bytes by DPP shift (0: a second load;
                               // measured 4.34 vs 4.44 ms C4 sweep, profiles/r3_band_dpp_ab.log)
 // waves per k_sweep_flatw block (8, 10 or 11; they share one staged b[J] and
@@ -2688,10 +2532,12 @@ static void launch_sweep_up(const hh_matrix* m, const TileDev& T, const uint8_t*
     }
     HH_KTIME(n_flat ? "k_sweep_flat" : nullptr, s);
     if (n_flat && m->n_fgroups) {
-        auto kern = g_flatw_u == 16 ? (g_flatw_pipe == 2 ? k_sweep_flatw<16, ABL, 2>
-                                       : g_flatw_pipe == 1 ? k_sweep_flatw<16, ABL, 1> : k_sweep_flatw<16, ABL, 0>)
-                    : (g_flatw_pipe == 2 ? k_sweep_flatw<kFlatU, ABL, 2>
-                       : g_flatw_pipe == 1 ? k_sweep_flatw<kFlatU, ABL, 1> : k_sweep_flatw<kFlatU, ABL, 0>);
+        // (the column-grouped flat tiles' narrow segments are interleaved for
+        // kFlatU uint4 per lane: finalize_flat_layout)
+        HH_REQUIRE(m->flat_perm, "column-grouped flat tiles without the interleaved layout");
+        auto kern = g_flatw_pipe == 2   ? k_sweep_flatw<kFlatU, ABL, 2>
+                    : g_flatw_pipe == 1 ? k_sweep_flatw<kFlatU, ABL, 1>
+                                        : k_sweep_flatw<kFlatU, ABL, 0>;
         int nw = 8;
         if constexpr (UP) {
             // the column side's registers: 8 waves (2 per SIMD, 256 VGPRs; at
@@ -2699,17 +2545,10 @@ static void launch_sweep_up(const hh_matrix* m, const TileDev& T, const uint8_t*
             nw = g_flatw_waves_up == 11 ? 11 : 8;
             kern = nw == 11 ? k_sweep_flatw<kFlatU, ABL, 2, 11, true> : k_sweep_flatw<kFlatU, ABL, 2, 8, true>;
         } else {
-            if (g_flatw_waves == 10 && g_flatw_u != 16) {
+            if (g_flatw_waves == 10) {
                 kern = g_flatw_pipe == 2 ? k_sweep_flatw<kFlatU, ABL, 2, 10> : k_sweep_flatw<kFlatU, ABL, 0, 10>;
                 nw = 10;
-            } else if (g_flatw_pipe >= 3 && g_flatw_u != 16) {
-                // k_sweep_flatw3: the per-tile chain off the critical path
-                // (pipe 3: one run ahead; 4: two), 11 or 8 waves
-                nw = g_flatw_waves == 8 ? 8 : 11;
-                kern = nw == 8 ? (g_flatw_pipe == 4 ? k_sweep_flatw3<kFlatU, ABL, 8, 2> : k_sweep_flatw3<kFlatU, ABL, 8, 1>)
-                               : (g_flatw_pipe == 4 ? k_sweep_flatw3<kFlatU, ABL, 11, 2>
-                                                    : k_sweep_flatw3<kFlatU, ABL, 11, 1>);
-            } else if (g_flatw_waves == 11 && g_flatw_u != 16) {
+            } else if (g_flatw_waves == 11) {
                 kern = g_flatw_pipe == 2 ? k_sweep_flatw<kFlatU, ABL, 2, 11> : k_sweep_flatw<kFlatU, ABL, 0, 11>;
                 nw = 11;
             }
@@ -2757,11 +2596,7 @@ static void sweep(const hh_matrix* m, const TileDev& T, const uint8_t* act, cons
 
 // the tile view of a state's matrix (column slots and scale when the layout
 // has upper-triangle tiles)
-static TileDev tdev(const hh_ice* S) {
-    TileDev T = S->m->dev(S->colpart.p, S->fix.p, S->bfix.p);
-    T.ngroups = S->G;
-    return T;
-}
+static TileDev tdev(const hh_ice* S) { return S->m->dev(S->colpart.p, S->fix.p, S->bfix.p); }
 
 // The matrix's band segments; returns their total chunk count.
 // Dispatch order of the band chunks: by work (counts in the chunk) descending,
@@ -2967,7 +2802,9 @@ static void marg_weighted(hh_ice* S, double* out, hipStream_t s, bool timed, int
                           (bytes >= g_conc_min_bytes || (S->nchu && bytes >= g_conc_ub_min_bytes));
         // (not with upper tiles in column-grouped flat units: their column
         // side has one slot per group, which only k_sweep_flatw fills)
-        const bool single = g_sweep_nb == 2 && !(up && m->n_fgroups) &&
+        // (k_sweep_all walks flat tiles per unit in the plain layout: never on
+        // a layout with column-grouped, interleaved flat tiles)
+        const bool single = g_sweep_nb == 2 && !(up && m->n_fgroups) && !m->flat_perm &&
                             (g_sweep_single == 1 || (g_sweep_single == -1 && bytes < g_single_max_bytes));
         if (single) {
             sweep_single(S, s);
@@ -3139,14 +2976,13 @@ int hh_tune(const char* key, int64_t value) {
             HH_REQUIRE(value >= -1 && value <= 1, "flat_cols in {-1 (auto), 0, 1}");
             g_flat_cols = value;
         } else if (k == "flatw_pipe") {
-            HH_REQUIRE(value >= 0 && value <= 4, "flatw_pipe in {0, 1, 2, 3, 4}");
+            HH_REQUIRE(value >= 0 && value <= 2, "flatw_pipe in {0, 1, 2}");
             g_flatw_pipe = (int)value;
         } else if (k == "band_dpp") {
             HH_REQUIRE(value == 0 || value == 1, "band_dpp in {0, 1}");
             g_band_dpp = (int)value;
-        } else if (k == "flatw_u") {
-            HH_REQUIRE(value == 8 || value == 16, "flatw_u in {8, 16}");
-            g_flatw_u = (int)value;
+        } else if (k == "flatw_u") {  // (16 measured slower in round 4; the interleaved layout is for 8)
+            HH_REQUIRE(value == 8, "flatw_u: 8 (the interleaved flat layout's run length)");
         } else if (k == "flatw_waves_up") {
             HH_REQUIRE(value == 8 || value == 11, "flatw_waves_up in {8, 11}");
             g_flatw_waves_up = (int)value;
@@ -3654,10 +3490,12 @@ int hh_ice_swept_bytes(const hh_ice* S, int64_t* bytes) {
 // bytes of probe i: 0 wide tile entries, 1 narrow tile entries, 2 uint8 band,
 // 3 nibble band (linear reads); 4-6 the flat tiles' payload in
 // k_sweep_flatw's order, streamed only: 11 waves at its LDS footprint (one
-// block per CU), 11 waves and 16 waves without it.
+// block per CU), 11 waves and 16 waves without it; 7-8 the same with
+// coalesced run loads (11 waves one block per CU, 8 waves); 9 the narrow
+// entries linearly with lane-major runs.
 int hh_matrix_stream_probe(const hh_matrix* m, int32_t reps, double* out, int32_t nout) {
     return guard([&] {
-        HH_REQUIRE(m && out && nout >= 14 && reps > 0, "stream probe: 14 outputs");
+        HH_REQUIRE(m && out && nout >= 20 && reps > 0, "stream probe: 20 outputs");
         for (int i = 0; i < nout; ++i) out[i] = 0.0;
         HIP_CHECK(hipSetDevice(m->device));
         hipStream_t s;
@@ -3677,12 +3515,16 @@ int hh_matrix_stream_probe(const hh_matrix* m, int32_t reps, double* out, int32_
             out[2 * i] = ms / reps;
             out[2 * i + 1] = bytes;
         };
-        auto lin = [&](int i, const void* p, size_t bytes) {
+        auto lin = [&](int i, const void* p, size_t bytes, bool lm = false) {
             const long long n16 = (long long)(bytes / 16);
             if (!n16) return;
             timed(i, (double)n16 * 16, [&] {
-                hipLaunchKernelGGL(k_stream_probe, dim3(4096), dim3(256), 0, s, reinterpret_cast<const uint4*>(p), n16,
-                                   sink.p);
+                if (lm)
+                    hipLaunchKernelGGL(k_stream_probe<true>, dim3(4096), dim3(256), 0, s,
+                                       reinterpret_cast<const uint4*>(p), n16, sink.p);
+                else
+                    hipLaunchKernelGGL(k_stream_probe<false>, dim3(4096), dim3(256), 0, s,
+                                       reinterpret_cast<const uint4*>(p), n16, sink.p);
             });
         };
         lin(0, m->pay.p, m->pay.bytes());
@@ -3696,7 +3538,12 @@ int hh_matrix_stream_probe(const hh_matrix* m, int32_t reps, double* out, int32_
             timed(4, fb, [&] { hipLaunchKernelGGL((k_flat_stream_probe<11, 152000>), dim3(g), dim3(704), 0, s, T, sink.p); });
             timed(5, fb, [&] { hipLaunchKernelGGL((k_flat_stream_probe<11, 0>), dim3(g), dim3(704), 0, s, T, sink.p); });
             timed(6, fb, [&] { hipLaunchKernelGGL((k_flat_stream_probe<16, 0>), dim3(g), dim3(1024), 0, s, T, sink.p); });
+            timed(7, fb, [&] {
+                hipLaunchKernelGGL((k_flat_stream_probe<11, 152000, true>), dim3(g), dim3(704), 0, s, T, sink.p);
+            });
+            timed(8, fb, [&] { hipLaunchKernelGGL((k_flat_stream_probe<8, 0, true>), dim3(g), dim3(512), 0, s, T, sink.p); });
         }
+        lin(9, m->payn.p, m->payn.bytes(), true);
         HIP_CHECK(hipGetLastError());
         HIP_CHECK(hipStreamSynchronize(s));
         HIP_CHECK(hipEventDestroy(e0));

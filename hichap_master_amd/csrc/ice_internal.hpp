@@ -255,7 +255,6 @@ struct TileDev {
     unsigned long long* colpart;    // n_cslots x kW column partials (int64 fixed point)
     const double* fix;              // {2^e, 2^-e}: this sweep's fixed-point scale of b
     const unsigned long long* bfix; // B = round(b 2^e) of every bin (k_fixscale)
-    int ngroups = 0;                // ICE groups of the matrix (k_sweep_flatw3; 0 = unknown)
 };
 
 extern int g_flat_defer;
@@ -294,6 +293,7 @@ struct hh_matrix {
     hh::DBuf<hh::FlatDesc> fg_desc;
     int64_t n_fgroups = 0;
     int32_t upper = 0;             // upper-triangle tiles (g_upper_tiles at build time)
+    int32_t flat_perm = 0;         // column-grouped flat tiles' narrow segments interleaved (finalize_flat_layout)
     int64_t n_cslots = 0;
     hh::DBuf<int32_t> u_cslot, fg_cslot, jslot_ptr, jslot;
     hh::DBuf<long long> wide_ptr;  // local rows + 1
@@ -335,6 +335,34 @@ inline std::vector<uint16_t> bin_groups(const hh_matrix& m) {
 }
 // Upload the plan arrays (not the payload) into m.
 void upload_plan(const TilePlan& P, hh_matrix& m, hipStream_t s);
+
+// Interleaved flat segments (round 6).  The flat walk gives lane l of a wave
+// the run of kFlatIlvU consecutive uint4 [q0 + U l, q0 + U l + U) of a step;
+// loaded as such (lane-major) every load instruction touches 64 lines 128 B
+// apart, and the flat tiles stream at 3.5 TB/s however many loads are in
+// flight (hh_matrix_stream_probe: 6.0 TB/s for the same tiles with coalesced
+// instructions).  So the column-grouped flat tiles' narrow segments are stored
+// per step chunk of m <= 64 U uint4 (chunks aligned to the segment start) in
+// element-major order: element k of every lane's run first (lanes 0 ..
+// cnt_k - 1, cnt_k = ceil((m - k) / U)), then element k + 1: instruction k
+// of a step reads cnt_k consecutive uint4 into exactly the registers the
+// lane-major load filled -- the walk and its sums are unchanged, bitwise.
+constexpr int kFlatIlvU = 8;
+__host__ __device__ inline uint32_t flat_ilv_cnt(uint32_t m, int k) {
+    return m > (uint32_t)k ? (m - (uint32_t)k + kFlatIlvU - 1) / kFlatIlvU : 0u;
+}
+// chunk-relative stored position of chunk-relative logical uint4 i (chunk of m)
+__host__ __device__ inline uint32_t flat_ilv_pos(uint32_t m, uint32_t i) {
+    const int k = (int)(i % kFlatIlvU);
+    uint32_t b = 0;
+    for (int j = 0; j < k; ++j) b += flat_ilv_cnt(m, j);
+    return b + i / kFlatIlvU;
+}
+// After a builder wrote the payload: interleave the column-grouped flat
+// tiles' narrow segments (m.flat_perm = 1); no-op without column groups.
+void finalize_flat_layout(hh_matrix& m, hipStream_t s);
+// A copy of m's narrow payload in the plain (lane-major) order (export).
+void narrow_payload_plain(const hh_matrix& m, DBuf<uint16_t>& out, hipStream_t s);
 // Device helpers shared with the pair binner (pairs.hip): stable LSD radix
 // sort of n 64-bit keys on their low `bits` bits (synchronous), exclusive
 // scan of n int64 values (*total_dev = the sum, may be null; asynchronous).

@@ -532,6 +532,54 @@ TilePlan plan_tiles(const uint16_t* cntw, const uint16_t* cntn, int64_t nloc, in
     return P;
 }
 
+// One block per column-grouped flat tile, one wave per step chunk: the
+// chunk's 64 U uint4 in registers (every load done before any store: in
+// place), stored in the other order.  INV: interleaved -> plain.
+template <bool INV>
+__global__ __launch_bounds__(256) void k_flat_interleave(const FlatDesc* __restrict__ desc, uint16_t* __restrict__ payn) {
+    constexpr int U = kFlatIlvU;
+    const FlatDesc d = desc[blockIdx.x];
+    uint4* __restrict__ p = reinterpret_cast<uint4*>(payn + d.entn);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    for (uint32_t q0 = 64u * U * (uint32_t)w; q0 < d.qbn; q0 += 64u * U * (uint32_t)nw) {
+        const uint32_t m = d.qbn - q0 < 64u * U ? d.qbn - q0 : 64u * U;
+        uint4 v[U];
+        uint32_t src[U], dst[U];
+        bool ok[U];
+        uint32_t base = 0;
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            const uint32_t plain = (uint32_t)lane * U + k, ilv = base + (uint32_t)lane;
+            ok[k] = plain < m;
+            src[k] = q0 + (INV ? ilv : plain);
+            dst[k] = q0 + (INV ? plain : ilv);
+            base += flat_ilv_cnt(m, k);
+        }
+#pragma unroll
+        for (int k = 0; k < U; ++k) v[k] = p[ok[k] ? src[k] : q0];
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the whole chunk read before it is rewritten
+#pragma unroll
+        for (int k = 0; k < U; ++k)
+            if (ok[k]) p[dst[k]] = v[k];
+    }
+}
+
+void finalize_flat_layout(hh_matrix& m, hipStream_t s) {
+    m.flat_perm = 0;
+    if (!m.n_fgroups || !m.fg_desc.n) return;
+    hipLaunchKernelGGL(k_flat_interleave<false>, dim3((unsigned)m.fg_desc.n), dim3(256), 0, s, m.fg_desc.p, m.payn.p);
+    HIP_CHECK(hipGetLastError());
+    m.flat_perm = 1;
+}
+
+void narrow_payload_plain(const hh_matrix& m, DBuf<uint16_t>& out, hipStream_t s) {
+    out.alloc(std::max<size_t>(m.payn.n, 1));
+    if (m.payn.n) HIP_CHECK(hipMemcpyAsync(out.p, m.payn.p, m.payn.bytes(), hipMemcpyDeviceToDevice, s));
+    if (m.flat_perm && m.fg_desc.n)
+        hipLaunchKernelGGL(k_flat_interleave<true>, dim3((unsigned)m.fg_desc.n), dim3(256), 0, s, m.fg_desc.p, out.p);
+    HIP_CHECK(hipGetLastError());
+}
+
 void upload_plan(const TilePlan& P, hh_matrix& m, hipStream_t s) {
     m.nJ = P.nJ;
     m.nrb = P.nrb;
@@ -858,6 +906,7 @@ int hh_matrix_from_pixels(const int64_t* bin1, const int64_t* bin2, const double
         m->band4 = to_device(band4, s);
         m->nnz_upper = nnz_upper;
         m->n_entries = deg[nloc];
+        finalize_flat_layout(*m, s);
         HIP_CHECK(hipStreamSynchronize(s));  // host vectors die here
         *out = m.release();
     });
@@ -909,7 +958,9 @@ int hh_matrix_export_upper(const hh_matrix* m, int64_t* bin1, int64_t* bin2, dou
         std::vector<uint16_t> payn(m->payn.n);
         std::vector<int32_t> tJ(m->tile_J.n), trb(m->tile_rb.n), wcol(m->wide_col.n);
         std::vector<long long> tent(m->tile_ent.n), tentn(m->tile_entn.n), wptr(m->wide_ptr.n);
-        m->payn.download(payn.data(), payn.size(), 0);
+        DBuf<uint16_t> plain;
+        narrow_payload_plain(*m, plain, 0);
+        plain.download(payn.data(), payn.size(), 0);
         m->tile_rpn.download(rpn.data(), rpn.size(), 0);
         m->tile_entn.download(tentn.data(), tentn.size(), 0);
         std::vector<double> wcnt(m->wide_cnt.n), diag(nloc);

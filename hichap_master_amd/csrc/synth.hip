@@ -493,6 +493,7 @@ int hh_synth_build(const hh_synth_params* p, int64_t row_lo, int64_t row_hi, voi
                                    (long long)nloc, o);
         }
         HIP_CHECK(hipGetLastError());
+        finalize_flat_layout(*m, s);
         std::vector<long long> wz(nloc + 1, 0);  // no wide entries (counts clamped)
         m->wide_ptr = to_device(wz, s);
         HIP_CHECK(hipStreamSynchronize(s));

@@ -154,7 +154,8 @@ int hh_matrix_get_info(const hh_matrix* m, hh_matrix_info* info);
 /* Diagnostic read rates of a matrix's own buffers (no sweep work): out[2i] =
  * ms per pass, out[2i+1] = bytes, for i = 0 wide / 1 narrow tile entries,
  * 2 uint8 / 3 nibble band (linear reads), 4-6 the flat tiles' payload in the
- * flat sweep's order, streamed only.  nout >= 14. */
+ * flat sweep's order, streamed only; 7-8 the same with coalesced run loads;
+ * 9 the narrow entries linearly in lane-major runs.  nout >= 20. */
 int hh_matrix_stream_probe(const hh_matrix* m, int32_t reps, double* out, int32_t nout);
 /* Copy the stored upper-triangle pixels (bin1 <= bin2, bin1 in the local rows
  * for which bin1 is the row) back to the host; *nnz_inout = capacity on entry,

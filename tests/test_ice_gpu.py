@@ -365,24 +365,33 @@ def test_flat_block_shapes_bitwise(ice, upper):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("cis_only", [0, 1])
-def test_flatw_early_claim_bitwise(ice, cis_only):
-    """k_sweep_flatw3 (flatw_pipe 3: the next tile claimed during the walk,
-    its record prefetched with its payload, active flags from LDS; 4: two
-    narrow runs in flight ahead; 8 or 11 waves) walks the same tiles with the
-    same sums as k_sweep_flatw: bitwise the same weights
-    and iterations, genome-wide (one ICE group) and --cis-only (a group per
-    chromosome, converging at different iterations: the skip path)."""
+def test_flat_interleaved_layout(ice, cis_only):
+    """Column-grouped flat tiles are stored interleaved (finalize_flat_layout:
+    element k of every lane's run contiguous, so k_sweep_flatw loads them with
+    coalesced instructions into the registers the lane-major loads filled).
+    The layout exports to the same pixels (the export de-interleaves), the
+    weights equal the oracle with the same iterations, and every block shape
+    and pipeline depth of k_sweep_flatw gives bitwise the same weights,
+    genome-wide and --cis-only (per-chromosome groups converging at
+    different iterations).  flat_cols 1 forces column groups on this small
+    matrix; the single-launch sweep is never used on such a layout."""
     from hichap_master_amd import _lib
     b1, b2, c, off = _case(43, sizes=(9000, 7000, 600), A=3.0, trans=0.0005)
     n = int(off[-1])
     res = []
     _lib.call("hh_tune", b"flat_cols", 1)
     try:
-        for pipe, waves in ((2, 11), (3, 11), (4, 8), (3, 8), (4, 11), (3, 11)):
+        for pipe, waves in ((2, 11), (0, 11), (2, 8), (2, 10), (1, 11)):
             _lib.call("hh_tune", b"flatw_pipe", pipe)
             _lib.call("hh_tune", b"flatw_waves", waves)
             m = ice.ContactMatrix.from_pixels(b1, b2, c, n, off, cis_only=cis_only)
             assert m.info()["n_units_flat"] > 0
+            if not res:
+                e1, e2, ec = m.export_upper()
+                f1, f2, fc = _filtered_upper(b1, b2, c, off, 1, cis_only)
+                np.testing.assert_array_equal(e1, f1)
+                np.testing.assert_array_equal(e2, f2)
+                np.testing.assert_array_equal(ec, fc)
             res.append(ice.balance_matrix(m, ice.IceOptions(max_iters=300)))
             m.close()
     finally:
@@ -392,6 +401,9 @@ def test_flatw_early_claim_bitwise(ice, cis_only):
     for w, st in res[1:]:
         np.testing.assert_array_equal(w, res[0][0])
         np.testing.assert_array_equal(st["iters"], res[0][1]["iters"])
+    wr, sr = ice_ref.balance(b1, b2, c, n, off, cis_only=bool(cis_only), max_iters=300)
+    np.testing.assert_allclose(res[0][0], wr, rtol=1e-9, equal_nan=True)
+    np.testing.assert_array_equal(res[0][1]["iters"], sr["iters"])
 
 
 def _full_config(cfg):

@@ -50,11 +50,13 @@ print(f"build {time.time()-t0:.1f}s band_w={inf['band_w']} band_w4={inf['band_w4
       f"tiles {inf['n_tiles']}", flush=True)
 if a.stream:
     import ctypes as C
-    out = (C.c_double * 14)()
+    out = (C.c_double * 20)()
     names = ["wide tile entries", "narrow tile entries", "uint8 band", "nibble band",
-             "flat tiles, 11 waves, 1 block/CU", "flat tiles, 11 waves", "flat tiles, 16 waves"]
+             "flat tiles, 11 waves, 1 block/CU", "flat tiles, 11 waves", "flat tiles, 16 waves",
+             "flat tiles coalesced, 11 waves, 1 block/CU", "flat tiles coalesced, 8 waves",
+             "narrow tile entries, lane-major runs"]
     for rep in range(2):
-        _lib.call("hh_matrix_stream_probe", m.handle, 5, out, 14)
+        _lib.call("hh_matrix_stream_probe", m.handle, 5, out, 20)
         for i, nm in enumerate(names):
             if out[2 * i + 1] > 0:
                 print(f"[stream {rep}] {nm}: {out[2*i+1]/1e9:.3f} GB in {out[2*i]:.3f} ms = "
