@@ -1113,6 +1113,188 @@ __global__ __launch_bounds__(NW * 64, NW > 8 ? 3 : 2) void k_sweep_flatw(TileDev
     }
 }
 
+// K1c'' (round 6, hh_tune flatw_pipe 3): k_sweep_flatw with the per-tile
+// chain taken off the wave's critical path.  In k_sweep_flatw a wave, after
+// its walk, claims the next tile (LDS counter -> descriptor -> the rows'
+// active flags: two dependent global round trips), issues its first payload
+// runs and only then loads its flat record (a third round trip) -- about a
+// tile's worth of latency in which the wave has at most one run in flight.
+// Here the next tile is claimed right after the current record is staged: its
+// descriptor comes in as one dword per lane (a vector load, so it waits on
+// vmcnt behind the payload runs already in flight, not on the LDS queue the
+// walk uses), its active flags from an LDS copy of act (matrices with <= 64
+// ICE groups; a single-group matrix needs none), and after the walk the next
+// tile's payload runs AND record are issued together, the record held in
+// registers while this tile's row sums go out.  The walk is k_sweep_flatw's:
+// the same sums in the same order, bitwise the same partials.
+template <int NW>
+struct FlatW3Lds {
+    double bl[kW];
+    uint16_t rec[NW][kFrecU4 * 8];
+    double acc[NW][kR];
+    int next;
+    uint8_t act[64];
+};
+
+template <int U, int ABL, int NW = kFlatWaves>
+__global__ __launch_bounds__(NW * 64, NW > 8 ? 3 : 2) void k_sweep_flatw3(TileDev T, const uint8_t* __restrict__ act,
+                                                                        const double* __restrict__ b,
+                                                                        long long n_bins, double* __restrict__ part) {
+    constexpr int UW = 2;
+    __shared__ __attribute__((aligned(16))) FlatW3Lds<NW> L;
+    const int k0 = T.fg_ptr[blockIdx.x], nk = T.fg_ptr[blockIdx.x + 1] - k0;
+    const int ng = T.ngroups;  // ICE groups of the matrix (0: unknown -> global flags)
+    {
+        bool on = false;  // block-uniform: any active tile in the group
+        for (int k = 0; k < nk && !on; ++k) {
+            const int u = T.fg_unit[k0 + k];
+            for (int g = T.u_glo[u]; g <= T.u_ghi[u]; ++g) on |= act[g] != 0;
+        }
+        if (!on) return;
+    }
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (threadIdx.x == 0) L.next = 0;
+    if (ng > 1 && ng <= 64 && threadIdx.x < ng) L.act[threadIdx.x] = act[threadIdx.x];
+    if (ABL != 2 && threadIdx.x < kSweepThreads) stage_bias(L.bl, b, (long long)T.tile_J[T.u_tlo[T.fg_unit[k0]]] * kW, n_bins);
+    __syncthreads();
+    const double* __restrict__ bl = L.bl;
+    uint16_t* __restrict__ rec = L.rec[wave];
+    double* __restrict__ acc = L.acc[wave];
+    const uint16_t* fstn = rec;
+    const uint16_t* fstw = rec + (kR + 1);
+    const uint16_t* fidn = rec + 2 * (kR + 1);
+    const uint16_t* fidw = fidn + kR;
+    const uint32_t* dsc = reinterpret_cast<const uint32_t*>(T.fg_desc + k0);
+    constexpr int DW = (int)(sizeof(FlatDesc) / 4);
+    struct Tw {
+        int slot, frec, nr, nfn, nfw;
+        uint32_t qbn, qbw;
+        const uint4 *payn4, *payw4;
+    };
+    // claim a tile: its index (LDS counter) and its descriptor, one dword per
+    // lane, in flight; -1 when the group is exhausted
+    auto claim = [&](uint32_t& dw) -> int {
+        int k = 0;
+        if (lane == 0) k = atomicAdd(&L.next, 1);
+        k = __builtin_amdgcn_readfirstlane(__shfl(k, 0, 64));
+        if (k >= nk) return -1;
+        dw = dsc[(size_t)k * DW + (lane < DW ? lane : 0)];
+        return k;
+    };
+    auto field = [&](uint32_t dw, int i) -> uint32_t { return (uint32_t)__builtin_amdgcn_readlane((int)dw, i); };
+    auto decode = [&](uint32_t dw, Tw& x) {
+        const long long entn = (long long)(((uint64_t)field(dw, 1) << 32) | field(dw, 0));
+        const long long ent = (long long)(((uint64_t)field(dw, 3) << 32) | field(dw, 2));
+        const uint32_t w8 = field(dw, 8), w9 = field(dw, 9);
+        x = Tw{(int)field(dw, 5), (int)field(dw, 4), (int)(w8 & 0xFFFFu), (int)(w8 >> 16), (int)(w9 & 0xFFFFu),
+               field(dw, 6), field(dw, 7), reinterpret_cast<const uint4*>(T.payn + entn),
+               reinterpret_cast<const uint4*>(T.pay + ent)};
+    };
+    // the claimed tile's rows active?  (glo = hi half of dword 9, ghi = lo half of 10)
+    auto active = [&](uint32_t dw) -> bool {
+        if (ng == 1) return true;
+        const int glo = (int)(field(dw, 9) >> 16), ghi = (int)(field(dw, 10) & 0xFFFFu);
+        bool on = false;
+        if (ng > 1 && ng <= 64) {
+            for (int g = glo; g <= ghi; ++g) on |= L.act[g] != 0;
+        } else {
+            const int ngr = ghi - glo + 1;
+            if (ngr <= 64) {
+                const uint8_t a = act[glo + (lane < ngr ? lane : ngr - 1)];
+                on = __ballot((a != 0) & (lane < ngr)) != 0;
+            } else {
+                for (int g = glo; g <= ghi; ++g) on |= act[g] != 0;
+            }
+        }
+        return on;
+    };
+    // the next active tile, descriptor already in dw for the first candidate
+    auto settle = [&](int k, uint32_t dw, Tw& x) -> bool {
+        while (k >= 0 && !active(dw)) k = claim(dw);
+        if (k < 0) return false;
+        decode(dw, x);
+        return true;
+    };
+    // the record ranges the walk reads (k_sweep_flatw), loaded into registers
+    uint4 tq[8];
+    int qs[8];
+    auto rec_load = [&](const Tw& x) {
+        const uint4* rg = T.frec + (size_t)x.frec * kFrecU4;
+        const bool idn = x.nfn == x.nr;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int g = i >> 1, h = i & 1;
+            const int h0 = g == 0 ? 0 : g == 1 ? kR + 1 : g == 2 ? 2 * (kR + 1) : 2 * (kR + 1) + kR;
+            const int h1 = g == 0   ? x.nfn + 1
+                           : g == 1 ? kR + 1 + x.nfw + 1
+                           : g == 2 ? (idn ? 2 * (kR + 1) : 2 * (kR + 1) + x.nfn)
+                                    : 2 * (kR + 1) + kR + x.nfw;
+            const int q0 = h0 / 8, q1 = (h1 + 7) / 8;
+            const int q = q0 + lane + 64 * h;
+            qs[i] = q < q1 ? q : q0;
+            tq[i] = rg[qs[i]];
+        }
+    };
+    Tw cur;
+    uint32_t dw = 0;
+    bool any = settle(claim(dw), dw, cur);
+    uint4 v[U], vw[UW];
+    // the first narrow run of a tile (interleaved segment: coalesced loads)
+    auto first_runs = [&](const Tw& x) {
+        if (x.nfn) flat_load_ilv<U>(x.payn4, 0u, x.qbn, lane, v);
+    };
+    if (any) {
+        first_runs(cur);
+        if (cur.nfw) flat_load<UW>(cur.payw4, (uint32_t)lane * UW, 0u, cur.qbw, vw);
+        rec_load(cur);
+    }
+    for (; any;) {
+        {
+            uint4* r4 = reinterpret_cast<uint4*>(rec);
+            r4[qs[0]] = tq[0], r4[qs[1]] = tq[1], r4[qs[2]] = tq[2], r4[qs[3]] = tq[3];
+            r4[qs[4]] = tq[4], r4[qs[5]] = tq[5], r4[qs[6]] = tq[6], r4[qs[7]] = tq[7];
+        }
+        // the next tile claimed now: its descriptor flies during the walk
+        uint32_t dwn = 0;
+        const int kn = claim(dwn);
+        wave_lds_sync();
+        const bool idn = cur.nfn == cur.nr;
+        flat_seg_c_pipe<U, ABL, 8, false, true>(cur.payn4, v, 0u, cur.qbn, 0, cur.nfn, fstn, cur.nfn, bl, acc, lane);
+        wave_lds_sync();
+        constexpr int PL = kR / 64;
+        double cv[PL];
+        int cid[PL];
+#pragma unroll
+        for (int q = 0; q < PL; ++q) {
+            const int i = lane + 64 * q;
+            cv[q] = i < cur.nfn ? acc[i] : 0.0;
+            cid[q] = i < cur.nfn ? (idn ? i : (int)fidn[i]) : -1;
+        }
+        wave_lds_sync();
+#pragma unroll
+        for (int q = 0; q < PL; ++q) acc[lane + 64 * q] = 0.0;
+        wave_lds_sync();
+#pragma unroll
+        for (int q = 0; q < PL; ++q)
+            if (cid[q] >= 0) acc[cid[q]] = cv[q];
+        wave_lds_sync();
+        flat_seg_pipe<UW, ABL, 4>(cur.payw4, vw, 0u, cur.qbw, 0, cur.nfw, fstw, fidw, cur.nfw, bl, acc, lane);
+        wave_lds_sync();
+        Tw nxt;
+        const bool more = settle(kn, dwn, nxt);
+        if (more) {
+            first_runs(nxt);
+            if (nxt.nfw) flat_load<UW>(nxt.payw4, (uint32_t)lane * UW, 0u, nxt.qbw, vw);
+            rec_load(nxt);
+        }
+        double* __restrict__ out = part + cur.slot;
+        for (int r = lane; r < cur.nr; r += 64) out[r] = acc[r];
+        wave_lds_sync();  // this tile's LDS reads before the next tile's writes
+        if (!more) break;
+        cur = nxt;
+    }
+}
+
 // ---- diagnostics (hh_matrix_stream_probe): read rates of the layout's own
 // buffers without any of the sweep's work, to separate what the buffers and
 // access shapes allow from what the sweep kernels' structure costs.
@@ -2548,6 +2730,9 @@ static void launch_sweep_up(const hh_matrix* m, const TileDev& T, const uint8_t*
             if (g_flatw_waves == 10) {
                 kern = g_flatw_pipe == 2 ? k_sweep_flatw<kFlatU, ABL, 2, 10> : k_sweep_flatw<kFlatU, ABL, 0, 10>;
                 nw = 10;
+            } else if (g_flatw_pipe == 3) {  // k_sweep_flatw3 (8 or 11 waves)
+                nw = g_flatw_waves == 8 ? 8 : 11;
+                kern = nw == 8 ? k_sweep_flatw3<kFlatU, ABL, 8> : k_sweep_flatw3<kFlatU, ABL, 11>;
             } else if (g_flatw_waves == 11) {
                 kern = g_flatw_pipe == 2 ? k_sweep_flatw<kFlatU, ABL, 2, 11> : k_sweep_flatw<kFlatU, ABL, 0, 11>;
                 nw = 11;
@@ -2596,7 +2781,11 @@ static void sweep(const hh_matrix* m, const TileDev& T, const uint8_t* act, cons
 
 // the tile view of a state's matrix (column slots and scale when the layout
 // has upper-triangle tiles)
-static TileDev tdev(const hh_ice* S) { return S->m->dev(S->colpart.p, S->fix.p, S->bfix.p); }
+static TileDev tdev(const hh_ice* S) {
+    TileDev T = S->m->dev(S->colpart.p, S->fix.p, S->bfix.p);
+    T.ngroups = S->G;
+    return T;
+}
 
 // The matrix's band segments; returns their total chunk count.
 // Dispatch order of the band chunks: by work (counts in the chunk) descending,
@@ -2976,7 +3165,7 @@ int hh_tune(const char* key, int64_t value) {
             HH_REQUIRE(value >= -1 && value <= 1, "flat_cols in {-1 (auto), 0, 1}");
             g_flat_cols = value;
         } else if (k == "flatw_pipe") {
-            HH_REQUIRE(value >= 0 && value <= 2, "flatw_pipe in {0, 1, 2}");
+            HH_REQUIRE(value >= 0 && value <= 3, "flatw_pipe in {0, 1, 2, 3}");
             g_flatw_pipe = (int)value;
         } else if (k == "band_dpp") {
             HH_REQUIRE(value == 0 || value == 1, "band_dpp in {0, 1}");

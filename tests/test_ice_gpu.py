@@ -371,7 +371,9 @@ def test_flat_interleaved_layout(ice, cis_only):
     coalesced instructions into the registers the lane-major loads filled).
     The layout exports to the same pixels (the export de-interleaves), the
     weights equal the oracle with the same iterations, and every block shape
-    and pipeline depth of k_sweep_flatw gives bitwise the same weights,
+    and pipeline depth of k_sweep_flatw (and k_sweep_flatw3, flatw_pipe 3:
+    the next tile claimed during the walk, its record loaded with its first
+    run, active flags from LDS) gives bitwise the same weights,
     genome-wide and --cis-only (per-chromosome groups converging at
     different iterations).  flat_cols 1 forces column groups on this small
     matrix; the single-launch sweep is never used on such a layout."""
@@ -381,7 +383,7 @@ def test_flat_interleaved_layout(ice, cis_only):
     res = []
     _lib.call("hh_tune", b"flat_cols", 1)
     try:
-        for pipe, waves in ((2, 11), (0, 11), (2, 8), (2, 10), (1, 11)):
+        for pipe, waves in ((2, 11), (0, 11), (2, 8), (2, 10), (1, 11), (3, 11), (3, 8)):
             _lib.call("hh_tune", b"flatw_pipe", pipe)
             _lib.call("hh_tune", b"flatw_waves", waves)
             m = ice.ContactMatrix.from_pixels(b1, b2, c, n, off, cis_only=cis_only)
