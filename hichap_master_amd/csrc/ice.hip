@@ -368,6 +368,13 @@ __device__ __forceinline__ void flat_step(const uint4 (&v)[U], uint32_t q0, uint
                                           const uint16_t* __restrict__ fst, const uint16_t* __restrict__ fr,
                                           int nfr, const double* __restrict__ bl, double* __restrict__ acc,
                                           int lane, ColArgs ca = ColArgs{}) {
+    if constexpr (ABL == 3) {  // timing ablation (flat_step_c)
+        uint32_t t = 0;
+#pragma unroll
+        for (int k = 0; k < U; ++k) t ^= v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
+        if (lane < nfr && t == 0x9E3779B9u) acc[lane] = (double)t;
+        return;
+    }
     const uint32_t s = q0 + (uint32_t)lane * U;
     const bool act = s < qb;
     // row of s: the largest i with start <= s; at most lane U + 1 rows
@@ -472,6 +479,13 @@ __device__ __forceinline__ void flat_step_c(const uint4 (&v)[U], uint32_t q0, ui
                                             const uint16_t* __restrict__ fst, int nfr,
                                             const double* __restrict__ bl, double* __restrict__ accc, int lane,
                                             ColArgs ca = ColArgs{}, const uint16_t* __restrict__ fid = nullptr) {
+    if constexpr (ABL == 3) {  // timing ablation: the walk's skeleton only (no search, scan or gathers)
+        uint32_t t = 0;
+#pragma unroll
+        for (int k = 0; k < U; ++k) t ^= v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
+        if (lane < nfr && t == 0x9E3779B9u) accc[lane] = (double)t;
+        return;
+    }
     const uint32_t s = q0 + (uint32_t)lane * U;
     const bool act = s < qb;
     int lo = ic, hi = min(i1 - 1, ic + lane * U + 1);
@@ -2774,6 +2788,7 @@ static void sweep(const hh_matrix* m, const TileDev& T, const uint8_t* act, cons
     switch (g_sweep_ablate) {
         case 1: launch_sweep_nb<1>(m, T, act, b, part, s, s_tiled); break;
         case 2: launch_sweep_nb<2>(m, T, act, b, part, s, s_tiled); break;
+        case 3: launch_sweep_nb<3>(m, T, act, b, part, s, s_tiled); break;
         default: launch_sweep_nb<0>(m, T, act, b, part, s, s_tiled); break;
     }
     HIP_CHECK(hipGetLastError());
@@ -3153,7 +3168,7 @@ int hh_tune(const char* key, int64_t value) {
             HH_REQUIRE(value == 1 || value == 2 || value == 4 || value == 8, "sweep_nb must be 1, 2, 4 or 8");
             g_sweep_nb = (int)value;
         } else if (k == "sweep_ablate") {
-            HH_REQUIRE(value >= 0 && value <= 2, "sweep_ablate must be 0, 1 or 2");
+            HH_REQUIRE(value >= 0 && value <= 3, "sweep_ablate must be 0, 1, 2 or 3");
             g_sweep_ablate = (int)value;
         } else if (k == "band4_density_pct" || k == "band8_big_pct") {
             HH_REQUIRE(value >= 1 && value <= 100, "percent in [1, 100]");
