@@ -474,11 +474,20 @@ __device__ __forceinline__ void flat_step(const uint4 (&v)[U], uint32_t q0, uint
 // tail + heads of one that continues), later steps add through lane 0 -- so
 // no row ids, no stash and no read-modify-write inside the walk (registers
 // for U = 8).  accc[i] is mapped to the row accumulator after the segment.
-template <int U, int ABL, int EPV, bool COL = false>
+// BM (round 6): the rows of a run from the tile's row-start bitmap (bit p =
+// a nonempty row starts at uint4 p; lane l's run is byte q0 / 8 + l): the
+// row of s is ic + the start bits in [q0, s] (a wave prefix of the lanes'
+// popcounts by four ballots), the row starts inside the run are the byte's
+// bits -- one LDS byte per lane instead of a binary search over the starts
+// (up to 9 dependent LDS reads) plus U - 1 start reads.  ic enters as the row
+// holding q0 - 1 (i0 - 1 before the first step).  The same rows, the same
+// sums in the same order: bitwise the search's.
+template <int U, int ABL, int EPV, bool COL = false, bool BM = false>
 __device__ __forceinline__ void flat_step_c(const uint4 (&v)[U], uint32_t q0, uint32_t qb, int& ic, int i1,
                                             const uint16_t* __restrict__ fst, int nfr,
                                             const double* __restrict__ bl, double* __restrict__ accc, int lane,
-                                            ColArgs ca = ColArgs{}, const uint16_t* __restrict__ fid = nullptr) {
+                                            ColArgs ca = ColArgs{}, const uint16_t* __restrict__ fid = nullptr,
+                                            const uint8_t* __restrict__ bm = nullptr) {
     if constexpr (ABL == 3) {  // timing ablation: the walk's skeleton only (no search, scan or gathers)
         uint32_t t = 0;
 #pragma unroll
@@ -488,15 +497,33 @@ __device__ __forceinline__ void flat_step_c(const uint4 (&v)[U], uint32_t q0, ui
     }
     const uint32_t s = q0 + (uint32_t)lane * U;
     const bool act = s < qb;
-    int lo = ic, hi = min(i1 - 1, ic + lane * U + 1);
-    while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if ((uint32_t)fst[mid] <= s) lo = mid; else hi = mid - 1;
-    }
-    const bool head = (uint32_t)fst[lo] < s;
-    uint32_t nb[U];
+    int lo;
+    bool head;
+    uint32_t nb[U], Bm = 0;
+    int tot = 0;
+    if constexpr (BM) {
+        static_assert(U == 8, "a lane's run is one byte of the row-start bitmap");
+        Bm = bm[(q0 >> 3) + (uint32_t)lane];
+        const uint32_t c = (uint32_t)__popc(Bm);
+        const unsigned long long m0 = __ballot(c & 1u), m1 = __ballot(c & 2u), m2 = __ballot(c & 4u),
+                                 m3 = __ballot(c & 8u);
+        const unsigned long long below = lane ? (~0ull >> (64 - lane)) : 0ull;
+        const int excl = __popcll(m0 & below) + 2 * __popcll(m1 & below) + 4 * __popcll(m2 & below) +
+                         8 * __popcll(m3 & below);
+        tot = __popcll(m0) + 2 * __popcll(m1) + 4 * __popcll(m2) + 8 * __popcll(m3);
+        lo = ic + excl + (int)(Bm & 1u);
+        head = (Bm & 1u) == 0u;
+    } else {
+        lo = ic;
+        int hi = min(i1 - 1, ic + lane * U + 1);
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if ((uint32_t)fst[mid] <= s) lo = mid; else hi = mid - 1;
+        }
+        head = (uint32_t)fst[lo] < s;
 #pragma unroll
-    for (int k = 0; k < U - 1; ++k) nb[k] = fst[min(lo + 1 + k, nfr)];
+        for (int k = 0; k < U - 1; ++k) nb[k] = fst[min(lo + 1 + k, nfr)];
+    }
     // the column side's B of compact rows lo .. lo + CB - 1 (fid: their row
     // ids, null = identity); a run reaching further rows (rare: ~3 uint4 per
     // row) loads those on the spot
@@ -515,11 +542,17 @@ __device__ __forceinline__ void flat_step_c(const uint4 (&v)[U], uint32_t q0, ui
 #pragma unroll
     for (int k = 0; k < U; ++k) {
         if (k > 0) {
-            uint32_t nxt = nb[0];
+            bool starts;
+            if constexpr (BM) {
+                starts = ((Bm >> k) & 1u) != 0u;  // (no bits past qb)
+            } else {
+                uint32_t nxt = nb[0];
 #pragma unroll
-            for (int jj = 1; jj < k; ++jj)
-                if (j == jj) nxt = nb[jj];
-            if (s + k == nxt && s + k < qb) {
+                for (int jj = 1; jj < k; ++jj)
+                    if (j == jj) nxt = nb[jj];
+                starts = s + k == nxt && s + k < qb;
+            }
+            if (starts) {
                 if (inhead) {
                     h = x;
                     inhead = false;
@@ -559,7 +592,7 @@ __device__ __forceinline__ void flat_step_c(const uint4 (&v)[U], uint32_t q0, ui
     const double Hr = __shfl_down(H, 1, 64);
     if (tail) accc[lo + j] = x + (lane < 63 ? Hr : 0.0);  // the row's first write
     if (lane == 0 && head) accc[lo] += H;                 // continues a row of an earlier step
-    ic = __shfl(lo + j, 63, 64);
+    ic = BM ? ic + tot : __shfl(lo + j, 63, 64);
 }
 
 template <int U, int ABL, int EPV, bool COL = false, bool ILV = false>
@@ -580,18 +613,19 @@ __device__ __forceinline__ void flat_seg_c(const uint4* __restrict__ pay4, uint4
 // flat_seg_c / flat_seg with the next step's run loaded before the current
 // step is walked (two runs in registers: the one-wave-per-tile kernel has
 // the VGPRs for it); the same steps in the same order, bitwise the same sums
-template <int U, int ABL, int EPV, bool COL = false, bool ILV = false>
+template <int U, int ABL, int EPV, bool COL = false, bool ILV = false, bool BM = false>
 __device__ __forceinline__ void flat_seg_c_pipe(const uint4* __restrict__ pay4, uint4 (&v)[U], uint32_t qa, uint32_t qb,
                                                 int i0, int i1, const uint16_t* __restrict__ fst, int nfr,
                                                 const double* __restrict__ bl, double* __restrict__ accc, int lane,
-                                                ColArgs ca = ColArgs{}, const uint16_t* __restrict__ fid = nullptr) {
+                                                ColArgs ca = ColArgs{}, const uint16_t* __restrict__ fid = nullptr,
+                                                const uint8_t* __restrict__ bm = nullptr) {
     if (i0 >= i1) return;
-    int ic = i0;
+    int ic = BM ? i0 - 1 : i0;
     for (uint32_t q0 = qa;;) {
         const uint32_t qn = q0 + 64u * U;
         uint4 vn[U];
         if (qn < qb) flat_run<U, ILV>(pay4, qn, qa, qb, lane, vn);
-        flat_step_c<U, ABL, EPV, COL>(v, q0, qb, ic, i1, fst, nfr, bl, accc, lane, ca, fid);
+        flat_step_c<U, ABL, EPV, COL, BM>(v, q0, qb, ic, i1, fst, nfr, bl, accc, lane, ca, fid, bm);
         if (qn >= qb) break;
 #pragma unroll
         for (int k = 0; k < U; ++k) v[k] = vn[k];
@@ -929,6 +963,7 @@ __global__ __launch_bounds__(kSweepThreads, 4) void k_sweep_flat(TileDev T, cons
 // tile the walk is the round-2 one with the whole tile as the wave's range,
 // so a row's sum is a fixed function of the tile: deterministic, and the
 // same wherever the tile is swept.
+
 template <int NW, bool UP>
 struct FlatWLds {
     double bl[kW];
@@ -946,9 +981,32 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// The narrow segment's row-start bitmap built over its staged starts (the
+// record's fstn area, 1 026 B: segments of <= kFlatBmMax uint4, whole 512-bit
+// steps zero-padded); fst[0..nfn) are read into registers first.
+constexpr uint32_t kFlatBmMax = 8192;
+__device__ __forceinline__ void flat_bitmap_build(uint16_t* __restrict__ rec, int nfn, int lane) {
+    uint32_t st[kR / 64];
+#pragma unroll
+    for (int r = 0; r < kR / 64; ++r) {
+        const int i = lane + 64 * r;
+        st[r] = i < nfn ? (uint32_t)rec[i] : 0xFFFFFFFFu;
+    }
+    wave_lds_sync();
+    uint32_t* bm32 = reinterpret_cast<uint32_t*>(rec);
+#pragma unroll
+    for (int r = 0; r < (int)(kFlatBmMax / 32 / 64); ++r) bm32[lane + 64 * r] = 0u;
+    wave_lds_sync();
+#pragma unroll
+    for (int r = 0; r < kR / 64; ++r)
+        if (st[r] != 0xFFFFFFFFu) atomicOr(&bm32[st[r] >> 5], 1u << (st[r] & 31u));
+    wave_lds_sync();
+}
+static_assert(kFlatBmMax / 8 <= 2 * (kR + 1), "the bitmap fits the record's narrow starts");
+
 // NW waves per block share one staged b[J]: the LDS (64 KB of bias + 8 KB
 // per wave) caps the block at 11 waves, and one block per CU is all that fits
-template <int U, int ABL, int PIPE = 2, int NW = kFlatWaves, bool UP = false>
+template <int U, int ABL, int PIPE = 2, int NW = kFlatWaves, bool UP = false, bool BMW = false>
 __global__ __launch_bounds__(NW * 64, NW > 8 ? 3 : 2) void k_sweep_flatw(TileDev T, const uint8_t* __restrict__ act,
                                                                        const double* __restrict__ b, long long n_bins,
                                                                        double* __restrict__ part) {
@@ -1061,6 +1119,11 @@ __global__ __launch_bounds__(NW * 64, NW > 8 ? 3 : 2) void k_sweep_flatw(TileDev
         if (UP && cur.up) {  // (not software-pipelined: the column side needs the registers)
             flat_seg_c<U, ABL, 8, true, true>(cur.payn4, v, 0u, cur.qbn, 0, cur.nfn, fstn, cur.nfn, bl, acc, lane,
                                               ca, idn ? nullptr : fidn);
+        } else if (BMW && cur.qbn <= kFlatBmMax) {  // the row-start bitmap walk
+            flat_bitmap_build(rec, cur.nfn, lane);
+            flat_seg_c_pipe<U, ABL, 8, false, true, true>(cur.payn4, v, 0u, cur.qbn, 0, cur.nfn, fstn, cur.nfn, bl,
+                                                          acc, lane, ColArgs{}, nullptr,
+                                                          reinterpret_cast<const uint8_t*>(rec));
         } else {
             if (PIPE)
                 flat_seg_c_pipe<U, ABL, 8, false, true>(cur.payn4, v, 0u, cur.qbn, 0, cur.nfn, fstn, cur.nfn, bl, acc,
@@ -1150,7 +1213,7 @@ struct FlatW3Lds {
     uint8_t act[64];
 };
 
-template <int U, int ABL, int NW = kFlatWaves>
+template <int U, int ABL, int NW = kFlatWaves, bool BMW = false>
 __global__ __launch_bounds__(NW * 64, NW > 8 ? 3 : 2) void k_sweep_flatw3(TileDev T, const uint8_t* __restrict__ act,
                                                                         const double* __restrict__ b,
                                                                         long long n_bins, double* __restrict__ part) {
@@ -1273,7 +1336,15 @@ __global__ __launch_bounds__(NW * 64, NW > 8 ? 3 : 2) void k_sweep_flatw3(TileDe
         const int kn = claim(dwn);
         wave_lds_sync();
         const bool idn = cur.nfn == cur.nr;
-        flat_seg_c_pipe<U, ABL, 8, false, true>(cur.payn4, v, 0u, cur.qbn, 0, cur.nfn, fstn, cur.nfn, bl, acc, lane);
+        if (BMW && cur.qbn <= kFlatBmMax) {
+            flat_bitmap_build(rec, cur.nfn, lane);
+            flat_seg_c_pipe<U, ABL, 8, false, true, true>(cur.payn4, v, 0u, cur.qbn, 0, cur.nfn, fstn, cur.nfn, bl,
+                                                          acc, lane, ColArgs{}, nullptr,
+                                                          reinterpret_cast<const uint8_t*>(rec));
+        } else {
+            flat_seg_c_pipe<U, ABL, 8, false, true>(cur.payn4, v, 0u, cur.qbn, 0, cur.nfn, fstn, cur.nfn, bl, acc,
+                                                    lane);
+        }
         wave_lds_sync();
         constexpr int PL = kR / 64;
         double cv[PL];
@@ -2679,6 +2750,7 @@ static int g_band_dpp = 0;    // band sweep: a lane's previous 16 bytes by DPP s
 // waves with 33-tile column groups (3 tiles per wave) took the C4 sweep from
 // 3.52 to 3.33 ms (profiles/r3b_flatw_waves_*_ab.log); 44-tile groups 1 % more
 static int g_flatw_waves = 11;
+static int g_flat_bm = 0;  // k_sweep_flatw(3): the narrow walk by row-start bitmap (round 6)
 static int g_flatw_waves_up = 8;  // k_sweep_flatw with the column side: 8 (no spills) or 11
 static int g_flatw_pipe = 2;  // k_sweep_flatw: 1 = the next run's loads before the current step's walk,
                               // 2 = and the next tile's first runs before the current tile's row sums go out
@@ -2746,9 +2818,12 @@ static void launch_sweep_up(const hh_matrix* m, const TileDev& T, const uint8_t*
                 nw = 10;
             } else if (g_flatw_pipe == 3) {  // k_sweep_flatw3 (8 or 11 waves)
                 nw = g_flatw_waves == 8 ? 8 : 11;
-                kern = nw == 8 ? k_sweep_flatw3<kFlatU, ABL, 8> : k_sweep_flatw3<kFlatU, ABL, 11>;
+                kern = nw == 8 ? (g_flat_bm ? k_sweep_flatw3<kFlatU, ABL, 8, true> : k_sweep_flatw3<kFlatU, ABL, 8>)
+                               : (g_flat_bm ? k_sweep_flatw3<kFlatU, ABL, 11, true> : k_sweep_flatw3<kFlatU, ABL, 11>);
             } else if (g_flatw_waves == 11) {
-                kern = g_flatw_pipe == 2 ? k_sweep_flatw<kFlatU, ABL, 2, 11> : k_sweep_flatw<kFlatU, ABL, 0, 11>;
+                kern = g_flatw_pipe == 2 ? (g_flat_bm ? k_sweep_flatw<kFlatU, ABL, 2, 11, false, true>
+                                                      : k_sweep_flatw<kFlatU, ABL, 2, 11>)
+                                         : k_sweep_flatw<kFlatU, ABL, 0, 11>;
                 nw = 11;
             }
         }
@@ -3187,6 +3262,9 @@ int hh_tune(const char* key, int64_t value) {
             g_band_dpp = (int)value;
         } else if (k == "flatw_u") {  // (16 measured slower in round 4; the interleaved layout is for 8)
             HH_REQUIRE(value == 8, "flatw_u: 8 (the interleaved flat layout's run length)");
+        } else if (k == "flat_bm") {
+            HH_REQUIRE(value == 0 || value == 1, "flat_bm in {0, 1}");
+            g_flat_bm = (int)value;
         } else if (k == "flatw_waves_up") {
             HH_REQUIRE(value == 8 || value == 11, "flatw_waves_up in {8, 11}");
             g_flatw_waves_up = (int)value;
