@@ -549,6 +549,16 @@ __global__ __launch_bounds__(256, 2) void k_cor_sym(const double* __restrict__ C
 // latency of the V staging and of the first loads is no longer exposed.  The
 // same MFMA sequence and partial sums per tile: bitwise k_cor_sym's result
 // (hh_tune "cor_sym" 2, the default; 1 = k_cor_sym).
+// COAL (round 6, hh_tune "cor_sym" 3): lane (lr, lc) loads the doubles
+// Cor[row][C0 + lc + 16 t] (t = 0..3) instead of the d4 Cor[row][C0 + 4 lc ..
+// 4 lc + 3]: every load instruction then reads 4 rows x 128 contiguous bytes
+// (whole lines) instead of 16-byte pieces 32 bytes apart (the lane-major shape
+// that held the flat ICE tiles at 3.5 TB/s).  The k-rows of
+// each MFMA are the same; only which lane holds which output column changes
+// (acc[t] row i = column C0 + i + 16 t instead of C0 + 4 i + t), so every
+// output element is summed over the same terms in the same order: bitwise
+// k_cor_sym_pf's result.
+template <bool COAL>
 __global__ __launch_bounds__(256, 2) void k_cor_sym_pf(const double* __restrict__ Cor, long long ldc, long long n,
                                                       const double* __restrict__ V, long long nr,
                                                       double* __restrict__ part_c, double* __restrict__ part_r) {
@@ -579,11 +589,18 @@ __global__ __launch_bounds__(256, 2) void k_cor_sym_pf(const double* __restrict_
     for (int g = 0; g < 4; ++g) dr[g] = d4{0.0, 0.0, 0.0, 0.0};
     double* wt = Wt[w];
     auto col_on = [&](int ct) { return rows_ok && ct < nct && (!diag || ct >= w); };
-    const double* cbase = Cor + (R0 + lr) * ldc + q * kCsR + 4 * lc;
+    const double* cbase = Cor + (R0 + lr) * ldc + q * kCsR + (COAL ? lc : 4 * lc);
     auto load = [&](int ct, int g, d4 (&dst)[4]) __attribute__((always_inline)) {
         const double* cp = cbase + 64 * ct + 16 * g * ldc;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) dst[j] = __builtin_nontemporal_load(reinterpret_cast<const d4*>(cp + 4 * j * ldc));
+        for (int j = 0; j < 4; ++j) {
+            if constexpr (COAL) {
+#pragma unroll
+                for (int t = 0; t < 4; ++t) dst[j][t] = __builtin_nontemporal_load(cp + 4 * j * ldc + 16 * t);
+            } else {
+                dst[j] = __builtin_nontemporal_load(reinterpret_cast<const d4*>(cp + 4 * j * ldc));
+            }
+        }
     };
     d4 av[4], an[4];
     if (col_on(0)) load(0, 0, av);
@@ -612,7 +629,8 @@ __global__ __launch_bounds__(256, 2) void k_cor_sym_pf(const double* __restrict_
 #pragma unroll
                     for (int j = 0; j < 4; ++j)
 #pragma unroll
-                        for (int t = 0; t < 4; ++t) wt[(4 * j + lr) * kCsW + 4 * lc + t] = av[j][t];
+                        for (int t = 0; t < 4; ++t)
+                            wt[(4 * j + lr) * kCsW + (COAL ? lc + 16 * t : 4 * lc + t)] = av[j][t];
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                     __builtin_amdgcn_wave_barrier();
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -635,7 +653,8 @@ __global__ __launch_bounds__(256, 2) void k_cor_sym_pf(const double* __restrict_
 #pragma unroll
         for (int t = 0; t < 4; ++t)
 #pragma unroll
-            for (int reg = 0; reg < 4; ++reg) wt[(4 * (lr + 4 * reg) + t) * kSB + lc] = acc[t][reg];
+            for (int reg = 0; reg < 4; ++reg)
+                wt[(COAL ? (lr + 4 * reg) + 16 * t : 4 * (lr + 4 * reg) + t) * kSB + lc] = acc[t][reg];
         __syncthreads();
         double* out = part_c + ((size_t)p * ldc + C0) * kSB;
         for (int e = threadIdx.x; e < 64 * kSB; e += 256) out[e] = ((Wt[0][e] + Wt[1][e]) + Wt[2][e]) + Wt[3][e];
@@ -972,7 +991,10 @@ struct PcaWork {
             }
             HH_KTIME("k_cor_mul", s);
             // (occupancy 2: 190 VGPRs; forcing 3 spills and measured 98.9 vs 105.9 chromosomes/s)
-            hipLaunchKernelGGL(g_cor_sym == 2 ? k_cor_sym_pf : k_cor_sym, dim3((unsigned)(nr * (nr + 1) / 2)), dim3(256),
+            hipLaunchKernelGGL(g_cor_sym == 3   ? k_cor_sym_pf<true>
+                               : g_cor_sym == 2 ? k_cor_sym_pf<false>
+                                                : k_cor_sym,
+                               dim3((unsigned)(nr * (nr + 1) / 2)), dim3(256),
                                0, s, Cor, ldc, n, V, nr, sym_c.p, sym_r.p);
             hipLaunchKernelGGL(k_cor_sym_sum, dim3((unsigned)((n * kSB + 255) / 256)), dim3(256), 0, s, sym_c.p,
                                sym_r.p, ldc, n, nr, Y);

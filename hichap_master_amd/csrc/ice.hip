@@ -3365,7 +3365,7 @@ int hh_tune(const char* key, int64_t value) {
             HH_REQUIRE(value == 0 || value == 1, "pca_coop in {0, 1}");
             g_pca_coop = (int)value;
         } else if (k == "cor_sym") {
-            HH_REQUIRE(value >= 0 && value <= 2, "cor_sym in {0, 1, 2}");
+            HH_REQUIRE(value >= 0 && value <= 3, "cor_sym in {0, 1, 2, 3}");
             g_cor_sym = (int)value;
         } else if (k == "ortho_tpb") {
             HH_REQUIRE(value == 0 || value == 1 || value == 2 || value == 4 || value == 8,

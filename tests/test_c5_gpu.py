@@ -348,3 +348,8 @@ def test_pca_pipelined_upper_triangle_product_bitwise():
     p2, s2, _ = _pca_run_sym(dM, 2)
     assert s1["products"] == s2["products"]
     np.testing.assert_array_equal(p1, p2)
+    # cor_sym 3: the same kernel with whole-line Cor loads (each output
+    # column summed over the same rows in the same order): bitwise too
+    p3, s3, _ = _pca_run_sym(dM, 3)
+    assert s3["products"] == s2["products"]
+    np.testing.assert_array_equal(p3, p2)
