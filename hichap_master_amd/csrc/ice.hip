@@ -474,20 +474,11 @@ __device__ __forceinline__ void flat_step(const uint4 (&v)[U], uint32_t q0, uint
 // tail + heads of one that continues), later steps add through lane 0 -- so
 // no row ids, no stash and no read-modify-write inside the walk (registers
 // for U = 8).  accc[i] is mapped to the row accumulator after the segment.
-// BM (round 6): the rows of a run from the tile's row-start bitmap (bit p =
-// a nonempty row starts at uint4 p; lane l's run is byte q0 / 8 + l): the
-// row of s is ic + the start bits in [q0, s] (a wave prefix of the lanes'
-// popcounts by four ballots), the row starts inside the run are the byte's
-// bits -- one LDS byte per lane instead of a binary search over the starts
-// (up to 9 dependent LDS reads) plus U - 1 start reads.  ic enters as the row
-// holding q0 - 1 (i0 - 1 before the first step).  The same rows, the same
-// sums in the same order: bitwise the search's.
-template <int U, int ABL, int EPV, bool COL = false, bool BM = false>
+template <int U, int ABL, int EPV, bool COL = false>
 __device__ __forceinline__ void flat_step_c(const uint4 (&v)[U], uint32_t q0, uint32_t qb, int& ic, int i1,
                                             const uint16_t* __restrict__ fst, int nfr,
                                             const double* __restrict__ bl, double* __restrict__ accc, int lane,
-                                            ColArgs ca = ColArgs{}, const uint16_t* __restrict__ fid = nullptr,
-                                            const uint8_t* __restrict__ bm = nullptr) {
+                                            ColArgs ca = ColArgs{}, const uint16_t* __restrict__ fid = nullptr) {
     if constexpr (ABL == 3) {  // timing ablation: the walk's skeleton only (no search, scan or gathers)
         uint32_t t = 0;
 #pragma unroll
@@ -497,33 +488,15 @@ __device__ __forceinline__ void flat_step_c(const uint4 (&v)[U], uint32_t q0, ui
     }
     const uint32_t s = q0 + (uint32_t)lane * U;
     const bool act = s < qb;
-    int lo;
-    bool head;
-    uint32_t nb[U], Bm = 0;
-    int tot = 0;
-    if constexpr (BM) {
-        static_assert(U == 8, "a lane's run is one byte of the row-start bitmap");
-        Bm = bm[(q0 >> 3) + (uint32_t)lane];
-        const uint32_t c = (uint32_t)__popc(Bm);
-        const unsigned long long m0 = __ballot(c & 1u), m1 = __ballot(c & 2u), m2 = __ballot(c & 4u),
-                                 m3 = __ballot(c & 8u);
-        const unsigned long long below = lane ? (~0ull >> (64 - lane)) : 0ull;
-        const int excl = __popcll(m0 & below) + 2 * __popcll(m1 & below) + 4 * __popcll(m2 & below) +
-                         8 * __popcll(m3 & below);
-        tot = __popcll(m0) + 2 * __popcll(m1) + 4 * __popcll(m2) + 8 * __popcll(m3);
-        lo = ic + excl + (int)(Bm & 1u);
-        head = (Bm & 1u) == 0u;
-    } else {
-        lo = ic;
-        int hi = min(i1 - 1, ic + lane * U + 1);
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if ((uint32_t)fst[mid] <= s) lo = mid; else hi = mid - 1;
-        }
-        head = (uint32_t)fst[lo] < s;
-#pragma unroll
-        for (int k = 0; k < U - 1; ++k) nb[k] = fst[min(lo + 1 + k, nfr)];
+    int lo = ic, hi = min(i1 - 1, ic + lane * U + 1);
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if ((uint32_t)fst[mid] <= s) lo = mid; else hi = mid - 1;
     }
+    const bool head = (uint32_t)fst[lo] < s;
+    uint32_t nb[U];
+#pragma unroll
+    for (int k = 0; k < U - 1; ++k) nb[k] = fst[min(lo + 1 + k, nfr)];
     // the column side's B of compact rows lo .. lo + CB - 1 (fid: their row
     // ids, null = identity); a run reaching further rows (rare: ~3 uint4 per
     // row) loads those on the spot
@@ -542,16 +515,11 @@ __device__ __forceinline__ void flat_step_c(const uint4 (&v)[U], uint32_t q0, ui
 #pragma unroll
     for (int k = 0; k < U; ++k) {
         if (k > 0) {
-            bool starts;
-            if constexpr (BM) {
-                starts = ((Bm >> k) & 1u) != 0u;  // (no bits past qb)
-            } else {
-                uint32_t nxt = nb[0];
+            uint32_t nxt = nb[0];
 #pragma unroll
-                for (int jj = 1; jj < k; ++jj)
-                    if (j == jj) nxt = nb[jj];
-                starts = s + k == nxt && s + k < qb;
-            }
+            for (int jj = 1; jj < k; ++jj)
+                if (j == jj) nxt = nb[jj];
+            const bool starts = s + k == nxt && s + k < qb;
             if (starts) {
                 if (inhead) {
                     h = x;
@@ -592,7 +560,7 @@ __device__ __forceinline__ void flat_step_c(const uint4 (&v)[U], uint32_t q0, ui
     const double Hr = __shfl_down(H, 1, 64);
     if (tail) accc[lo + j] = x + (lane < 63 ? Hr : 0.0);  // the row's first write
     if (lane == 0 && head) accc[lo] += H;                 // continues a row of an earlier step
-    ic = BM ? ic + tot : __shfl(lo + j, 63, 64);
+    ic = __shfl(lo + j, 63, 64);
 }
 
 template <int U, int ABL, int EPV, bool COL = false, bool ILV = false>
@@ -613,19 +581,18 @@ __device__ __forceinline__ void flat_seg_c(const uint4* __restrict__ pay4, uint4
 // flat_seg_c / flat_seg with the next step's run loaded before the current
 // step is walked (two runs in registers: the one-wave-per-tile kernel has
 // the VGPRs for it); the same steps in the same order, bitwise the same sums
-template <int U, int ABL, int EPV, bool COL = false, bool ILV = false, bool BM = false>
+template <int U, int ABL, int EPV, bool COL = false, bool ILV = false>
 __device__ __forceinline__ void flat_seg_c_pipe(const uint4* __restrict__ pay4, uint4 (&v)[U], uint32_t qa, uint32_t qb,
                                                 int i0, int i1, const uint16_t* __restrict__ fst, int nfr,
                                                 const double* __restrict__ bl, double* __restrict__ accc, int lane,
-                                                ColArgs ca = ColArgs{}, const uint16_t* __restrict__ fid = nullptr,
-                                                const uint8_t* __restrict__ bm = nullptr) {
+                                                ColArgs ca = ColArgs{}, const uint16_t* __restrict__ fid = nullptr) {
     if (i0 >= i1) return;
-    int ic = BM ? i0 - 1 : i0;
+    int ic = i0;
     for (uint32_t q0 = qa;;) {
         const uint32_t qn = q0 + 64u * U;
         uint4 vn[U];
         if (qn < qb) flat_run<U, ILV>(pay4, qn, qa, qb, lane, vn);
-        flat_step_c<U, ABL, EPV, COL, BM>(v, q0, qb, ic, i1, fst, nfr, bl, accc, lane, ca, fid, bm);
+        flat_step_c<U, ABL, EPV, COL>(v, q0, qb, ic, i1, fst, nfr, bl, accc, lane, ca, fid);
         if (qn >= qb) break;
 #pragma unroll
         for (int k = 0; k < U; ++k) v[k] = vn[k];
@@ -981,32 +948,10 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// The narrow segment's row-start bitmap built over its staged starts (the
-// record's fstn area, 1 026 B: segments of <= kFlatBmMax uint4, whole 512-bit
-// steps zero-padded); fst[0..nfn) are read into registers first.
-constexpr uint32_t kFlatBmMax = 8192;
-__device__ __forceinline__ void flat_bitmap_build(uint16_t* __restrict__ rec, int nfn, int lane) {
-    uint32_t st[kR / 64];
-#pragma unroll
-    for (int r = 0; r < kR / 64; ++r) {
-        const int i = lane + 64 * r;
-        st[r] = i < nfn ? (uint32_t)rec[i] : 0xFFFFFFFFu;
-    }
-    wave_lds_sync();
-    uint32_t* bm32 = reinterpret_cast<uint32_t*>(rec);
-#pragma unroll
-    for (int r = 0; r < (int)(kFlatBmMax / 32 / 64); ++r) bm32[lane + 64 * r] = 0u;
-    wave_lds_sync();
-#pragma unroll
-    for (int r = 0; r < kR / 64; ++r)
-        if (st[r] != 0xFFFFFFFFu) atomicOr(&bm32[st[r] >> 5], 1u << (st[r] & 31u));
-    wave_lds_sync();
-}
-static_assert(kFlatBmMax / 8 <= 2 * (kR + 1), "the bitmap fits the record's narrow starts");
 
 // NW waves per block share one staged b[J]: the LDS (64 KB of bias + 8 KB
 // per wave) caps the block at 11 waves, and one block per CU is all that fits
-template <int U, int ABL, int PIPE = 2, int NW = kFlatWaves, bool UP = false, bool BMW = false>
+template <int U, int ABL, int PIPE = 2, int NW = kFlatWaves, bool UP = false>
 __global__ __launch_bounds__(NW * 64, NW > 8 ? 3 : 2) void k_sweep_flatw(TileDev T, const uint8_t* __restrict__ act,
                                                                        const double* __restrict__ b, long long n_bins,
                                                                        double* __restrict__ part) {
@@ -1119,11 +1064,6 @@ __global__ __launch_bounds__(NW * 64, NW > 8 ? 3 : 2) void k_sweep_flatw(TileDev
         if (UP && cur.up) {  // (not software-pipelined: the column side needs the registers)
             flat_seg_c<U, ABL, 8, true, true>(cur.payn4, v, 0u, cur.qbn, 0, cur.nfn, fstn, cur.nfn, bl, acc, lane,
                                               ca, idn ? nullptr : fidn);
-        } else if (BMW && cur.qbn <= kFlatBmMax) {  // the row-start bitmap walk
-            flat_bitmap_build(rec, cur.nfn, lane);
-            flat_seg_c_pipe<U, ABL, 8, false, true, true>(cur.payn4, v, 0u, cur.qbn, 0, cur.nfn, fstn, cur.nfn, bl,
-                                                          acc, lane, ColArgs{}, nullptr,
-                                                          reinterpret_cast<const uint8_t*>(rec));
         } else {
             if (PIPE)
                 flat_seg_c_pipe<U, ABL, 8, false, true>(cur.payn4, v, 0u, cur.qbn, 0, cur.nfn, fstn, cur.nfn, bl, acc,
@@ -1187,196 +1127,6 @@ __global__ __launch_bounds__(NW * 64, NW > 8 ? 3 : 2) void k_sweep_flatw(TileDev
     if (UP && cslot >= 0) {  // every wave's adds are in: the group's column partial out
         __syncthreads();
         flush_cols(L.cacc, T.colpart + (size_t)cslot * kW, NW * 64);
-    }
-}
-
-// K1c'' (round 6, hh_tune flatw_pipe 3): k_sweep_flatw with the per-tile
-// chain taken off the wave's critical path.  In k_sweep_flatw a wave, after
-// its walk, claims the next tile (LDS counter -> descriptor -> the rows'
-// active flags: two dependent global round trips), issues its first payload
-// runs and only then loads its flat record (a third round trip) -- about a
-// tile's worth of latency in which the wave has at most one run in flight.
-// Here the next tile is claimed right after the current record is staged: its
-// descriptor comes in as one dword per lane (a vector load, so it waits on
-// vmcnt behind the payload runs already in flight, not on the LDS queue the
-// walk uses), its active flags from an LDS copy of act (matrices with <= 64
-// ICE groups; a single-group matrix needs none), and after the walk the next
-// tile's payload runs AND record are issued together, the record held in
-// registers while this tile's row sums go out.  The walk is k_sweep_flatw's:
-// the same sums in the same order, bitwise the same partials.
-template <int NW>
-struct FlatW3Lds {
-    double bl[kW];
-    uint16_t rec[NW][kFrecU4 * 8];
-    double acc[NW][kR];
-    int next;
-    uint8_t act[64];
-};
-
-template <int U, int ABL, int NW = kFlatWaves, bool BMW = false>
-__global__ __launch_bounds__(NW * 64, NW > 8 ? 3 : 2) void k_sweep_flatw3(TileDev T, const uint8_t* __restrict__ act,
-                                                                        const double* __restrict__ b,
-                                                                        long long n_bins, double* __restrict__ part) {
-    constexpr int UW = 2;
-    __shared__ __attribute__((aligned(16))) FlatW3Lds<NW> L;
-    const int k0 = T.fg_ptr[blockIdx.x], nk = T.fg_ptr[blockIdx.x + 1] - k0;
-    const int ng = T.ngroups;  // ICE groups of the matrix (0: unknown -> global flags)
-    {
-        bool on = false;  // block-uniform: any active tile in the group
-        for (int k = 0; k < nk && !on; ++k) {
-            const int u = T.fg_unit[k0 + k];
-            for (int g = T.u_glo[u]; g <= T.u_ghi[u]; ++g) on |= act[g] != 0;
-        }
-        if (!on) return;
-    }
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    if (threadIdx.x == 0) L.next = 0;
-    if (ng > 1 && ng <= 64 && threadIdx.x < ng) L.act[threadIdx.x] = act[threadIdx.x];
-    if (ABL != 2 && threadIdx.x < kSweepThreads) stage_bias(L.bl, b, (long long)T.tile_J[T.u_tlo[T.fg_unit[k0]]] * kW, n_bins);
-    __syncthreads();
-    const double* __restrict__ bl = L.bl;
-    uint16_t* __restrict__ rec = L.rec[wave];
-    double* __restrict__ acc = L.acc[wave];
-    const uint16_t* fstn = rec;
-    const uint16_t* fstw = rec + (kR + 1);
-    const uint16_t* fidn = rec + 2 * (kR + 1);
-    const uint16_t* fidw = fidn + kR;
-    const uint32_t* dsc = reinterpret_cast<const uint32_t*>(T.fg_desc + k0);
-    constexpr int DW = (int)(sizeof(FlatDesc) / 4);
-    struct Tw {
-        int slot, frec, nr, nfn, nfw;
-        uint32_t qbn, qbw;
-        const uint4 *payn4, *payw4;
-    };
-    // claim a tile: its index (LDS counter) and its descriptor, one dword per
-    // lane, in flight; -1 when the group is exhausted
-    auto claim = [&](uint32_t& dw) -> int {
-        int k = 0;
-        if (lane == 0) k = atomicAdd(&L.next, 1);
-        k = __builtin_amdgcn_readfirstlane(__shfl(k, 0, 64));
-        if (k >= nk) return -1;
-        dw = dsc[(size_t)k * DW + (lane < DW ? lane : 0)];
-        return k;
-    };
-    auto field = [&](uint32_t dw, int i) -> uint32_t { return (uint32_t)__builtin_amdgcn_readlane((int)dw, i); };
-    auto decode = [&](uint32_t dw, Tw& x) {
-        const long long entn = (long long)(((uint64_t)field(dw, 1) << 32) | field(dw, 0));
-        const long long ent = (long long)(((uint64_t)field(dw, 3) << 32) | field(dw, 2));
-        const uint32_t w8 = field(dw, 8), w9 = field(dw, 9);
-        x = Tw{(int)field(dw, 5), (int)field(dw, 4), (int)(w8 & 0xFFFFu), (int)(w8 >> 16), (int)(w9 & 0xFFFFu),
-               field(dw, 6), field(dw, 7), reinterpret_cast<const uint4*>(T.payn + entn),
-               reinterpret_cast<const uint4*>(T.pay + ent)};
-    };
-    // the claimed tile's rows active?  (glo = hi half of dword 9, ghi = lo half of 10)
-    auto active = [&](uint32_t dw) -> bool {
-        if (ng == 1) return true;
-        const int glo = (int)(field(dw, 9) >> 16), ghi = (int)(field(dw, 10) & 0xFFFFu);
-        bool on = false;
-        if (ng > 1 && ng <= 64) {
-            for (int g = glo; g <= ghi; ++g) on |= L.act[g] != 0;
-        } else {
-            const int ngr = ghi - glo + 1;
-            if (ngr <= 64) {
-                const uint8_t a = act[glo + (lane < ngr ? lane : ngr - 1)];
-                on = __ballot((a != 0) & (lane < ngr)) != 0;
-            } else {
-                for (int g = glo; g <= ghi; ++g) on |= act[g] != 0;
-            }
-        }
-        return on;
-    };
-    // the next active tile, descriptor already in dw for the first candidate
-    auto settle = [&](int k, uint32_t dw, Tw& x) -> bool {
-        while (k >= 0 && !active(dw)) k = claim(dw);
-        if (k < 0) return false;
-        decode(dw, x);
-        return true;
-    };
-    // the record ranges the walk reads (k_sweep_flatw), loaded into registers
-    uint4 tq[8];
-    int qs[8];
-    auto rec_load = [&](const Tw& x) {
-        const uint4* rg = T.frec + (size_t)x.frec * kFrecU4;
-        const bool idn = x.nfn == x.nr;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const int g = i >> 1, h = i & 1;
-            const int h0 = g == 0 ? 0 : g == 1 ? kR + 1 : g == 2 ? 2 * (kR + 1) : 2 * (kR + 1) + kR;
-            const int h1 = g == 0   ? x.nfn + 1
-                           : g == 1 ? kR + 1 + x.nfw + 1
-                           : g == 2 ? (idn ? 2 * (kR + 1) : 2 * (kR + 1) + x.nfn)
-                                    : 2 * (kR + 1) + kR + x.nfw;
-            const int q0 = h0 / 8, q1 = (h1 + 7) / 8;
-            const int q = q0 + lane + 64 * h;
-            qs[i] = q < q1 ? q : q0;
-            tq[i] = rg[qs[i]];
-        }
-    };
-    Tw cur;
-    uint32_t dw = 0;
-    bool any = settle(claim(dw), dw, cur);
-    uint4 v[U], vw[UW];
-    // the first narrow run of a tile (interleaved segment: coalesced loads)
-    auto first_runs = [&](const Tw& x) {
-        if (x.nfn) flat_load_ilv<U>(x.payn4, 0u, x.qbn, lane, v);
-    };
-    if (any) {
-        first_runs(cur);
-        if (cur.nfw) flat_load<UW>(cur.payw4, (uint32_t)lane * UW, 0u, cur.qbw, vw);
-        rec_load(cur);
-    }
-    for (; any;) {
-        {
-            uint4* r4 = reinterpret_cast<uint4*>(rec);
-            r4[qs[0]] = tq[0], r4[qs[1]] = tq[1], r4[qs[2]] = tq[2], r4[qs[3]] = tq[3];
-            r4[qs[4]] = tq[4], r4[qs[5]] = tq[5], r4[qs[6]] = tq[6], r4[qs[7]] = tq[7];
-        }
-        // the next tile claimed now: its descriptor flies during the walk
-        uint32_t dwn = 0;
-        const int kn = claim(dwn);
-        wave_lds_sync();
-        const bool idn = cur.nfn == cur.nr;
-        if (BMW && cur.qbn <= kFlatBmMax) {
-            flat_bitmap_build(rec, cur.nfn, lane);
-            flat_seg_c_pipe<U, ABL, 8, false, true, true>(cur.payn4, v, 0u, cur.qbn, 0, cur.nfn, fstn, cur.nfn, bl,
-                                                          acc, lane, ColArgs{}, nullptr,
-                                                          reinterpret_cast<const uint8_t*>(rec));
-        } else {
-            flat_seg_c_pipe<U, ABL, 8, false, true>(cur.payn4, v, 0u, cur.qbn, 0, cur.nfn, fstn, cur.nfn, bl, acc,
-                                                    lane);
-        }
-        wave_lds_sync();
-        constexpr int PL = kR / 64;
-        double cv[PL];
-        int cid[PL];
-#pragma unroll
-        for (int q = 0; q < PL; ++q) {
-            const int i = lane + 64 * q;
-            cv[q] = i < cur.nfn ? acc[i] : 0.0;
-            cid[q] = i < cur.nfn ? (idn ? i : (int)fidn[i]) : -1;
-        }
-        wave_lds_sync();
-#pragma unroll
-        for (int q = 0; q < PL; ++q) acc[lane + 64 * q] = 0.0;
-        wave_lds_sync();
-#pragma unroll
-        for (int q = 0; q < PL; ++q)
-            if (cid[q] >= 0) acc[cid[q]] = cv[q];
-        wave_lds_sync();
-        flat_seg_pipe<UW, ABL, 4>(cur.payw4, vw, 0u, cur.qbw, 0, cur.nfw, fstw, fidw, cur.nfw, bl, acc, lane);
-        wave_lds_sync();
-        Tw nxt;
-        const bool more = settle(kn, dwn, nxt);
-        if (more) {
-            first_runs(nxt);
-            if (nxt.nfw) flat_load<UW>(nxt.payw4, (uint32_t)lane * UW, 0u, nxt.qbw, vw);
-            rec_load(nxt);
-        }
-        double* __restrict__ out = part + cur.slot;
-        for (int r = lane; r < cur.nr; r += 64) out[r] = acc[r];
-        wave_lds_sync();  // this tile's LDS reads before the next tile's writes
-        if (!more) break;
-        cur = nxt;
     }
 }
 
@@ -2750,7 +2500,6 @@ static int g_band_dpp = 0;    // band sweep: a lane's previous 16 bytes by DPP s
 // waves with 33-tile column groups (3 tiles per wave) took the C4 sweep from
 // 3.52 to 3.33 ms (profiles/r3b_flatw_waves_*_ab.log); 44-tile groups 1 % more
 static int g_flatw_waves = 11;
-static int g_flat_bm = 0;  // k_sweep_flatw(3): the narrow walk by row-start bitmap (round 6)
 static int g_flatw_waves_up = 8;  // k_sweep_flatw with the column side: 8 (no spills) or 11
 static int g_flatw_pipe = 2;  // k_sweep_flatw: 1 = the next run's loads before the current step's walk,
                               // 2 = and the next tile's first runs before the current tile's row sums go out
@@ -2816,14 +2565,8 @@ static void launch_sweep_up(const hh_matrix* m, const TileDev& T, const uint8_t*
             if (g_flatw_waves == 10) {
                 kern = g_flatw_pipe == 2 ? k_sweep_flatw<kFlatU, ABL, 2, 10> : k_sweep_flatw<kFlatU, ABL, 0, 10>;
                 nw = 10;
-            } else if (g_flatw_pipe == 3) {  // k_sweep_flatw3 (8 or 11 waves)
-                nw = g_flatw_waves == 8 ? 8 : 11;
-                kern = nw == 8 ? (g_flat_bm ? k_sweep_flatw3<kFlatU, ABL, 8, true> : k_sweep_flatw3<kFlatU, ABL, 8>)
-                               : (g_flat_bm ? k_sweep_flatw3<kFlatU, ABL, 11, true> : k_sweep_flatw3<kFlatU, ABL, 11>);
             } else if (g_flatw_waves == 11) {
-                kern = g_flatw_pipe == 2 ? (g_flat_bm ? k_sweep_flatw<kFlatU, ABL, 2, 11, false, true>
-                                                      : k_sweep_flatw<kFlatU, ABL, 2, 11>)
-                                         : k_sweep_flatw<kFlatU, ABL, 0, 11>;
+                kern = g_flatw_pipe == 2 ? k_sweep_flatw<kFlatU, ABL, 2, 11> : k_sweep_flatw<kFlatU, ABL, 0, 11>;
                 nw = 11;
             }
         }
@@ -2871,11 +2614,7 @@ static void sweep(const hh_matrix* m, const TileDev& T, const uint8_t* act, cons
 
 // the tile view of a state's matrix (column slots and scale when the layout
 // has upper-triangle tiles)
-static TileDev tdev(const hh_ice* S) {
-    TileDev T = S->m->dev(S->colpart.p, S->fix.p, S->bfix.p);
-    T.ngroups = S->G;
-    return T;
-}
+static TileDev tdev(const hh_ice* S) { return S->m->dev(S->colpart.p, S->fix.p, S->bfix.p); }
 
 // The matrix's band segments; returns their total chunk count.
 // Dispatch order of the band chunks: by work (counts in the chunk) descending,
@@ -3255,16 +2994,16 @@ int hh_tune(const char* key, int64_t value) {
             HH_REQUIRE(value >= -1 && value <= 1, "flat_cols in {-1 (auto), 0, 1}");
             g_flat_cols = value;
         } else if (k == "flatw_pipe") {
-            HH_REQUIRE(value >= 0 && value <= 3, "flatw_pipe in {0, 1, 2, 3}");
+            HH_REQUIRE(value >= 0 && value <= 2, "flatw_pipe in {0, 1, 2}");
             g_flatw_pipe = (int)value;
         } else if (k == "band_dpp") {
             HH_REQUIRE(value == 0 || value == 1, "band_dpp in {0, 1}");
             g_band_dpp = (int)value;
         } else if (k == "flatw_u") {  // (16 measured slower in round 4; the interleaved layout is for 8)
             HH_REQUIRE(value == 8, "flatw_u: 8 (the interleaved flat layout's run length)");
-        } else if (k == "flat_bm") {
-            HH_REQUIRE(value == 0 || value == 1, "flat_bm in {0, 1}");
-            g_flat_bm = (int)value;
+        } else if (k == "syrk_coal") {
+            HH_REQUIRE(value == 0 || value == 1, "syrk_coal in {0, 1}");
+            g_syrk_coal = (int)value;
         } else if (k == "flatw_waves_up") {
             HH_REQUIRE(value == 8 || value == 11, "flatw_waves_up in {8, 11}");
             g_flatw_waves_up = (int)value;

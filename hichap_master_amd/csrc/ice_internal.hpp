@@ -255,7 +255,6 @@ struct TileDev {
     unsigned long long* colpart;    // n_cslots x kW column partials (int64 fixed point)
     const double* fix;              // {2^e, 2^-e}: this sweep's fixed-point scale of b
     const unsigned long long* bfix; // B = round(b 2^e) of every bin (k_fixscale)
-    int ngroups = 0;                // ICE groups of the matrix (k_sweep_flatw3; 0 = unknown)
 };
 
 extern int g_flat_defer;

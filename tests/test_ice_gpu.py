@@ -371,10 +371,7 @@ def test_flat_interleaved_layout(ice, cis_only):
     coalesced instructions into the registers the lane-major loads filled).
     The layout exports to the same pixels (the export de-interleaves), the
     weights equal the oracle with the same iterations, and every block shape
-    and pipeline depth of k_sweep_flatw (and k_sweep_flatw3, flatw_pipe 3:
-    the next tile claimed during the walk, its record loaded with its first
-    run, active flags from LDS; flat_bm 1: rows from a row-start bitmap
-    instead of a binary search) gives bitwise the same weights,
+    and pipeline depth of k_sweep_flatw gives bitwise the same weights,
     genome-wide and --cis-only (per-chromosome groups converging at
     different iterations).  flat_cols 1 forces column groups on this small
     matrix; the single-launch sweep is never used on such a layout."""
@@ -384,11 +381,9 @@ def test_flat_interleaved_layout(ice, cis_only):
     res = []
     _lib.call("hh_tune", b"flat_cols", 1)
     try:
-        for pipe, waves, bm in ((2, 11, 0), (0, 11, 0), (2, 8, 0), (2, 10, 0), (1, 11, 0), (3, 11, 0), (3, 8, 0),
-                                (2, 11, 1), (3, 11, 1)):
+        for pipe, waves in ((2, 11), (0, 11), (2, 8), (2, 10), (1, 11)):
             _lib.call("hh_tune", b"flatw_pipe", pipe)
             _lib.call("hh_tune", b"flatw_waves", waves)
-            _lib.call("hh_tune", b"flat_bm", bm)
             m = ice.ContactMatrix.from_pixels(b1, b2, c, n, off, cis_only=cis_only)
             assert m.info()["n_units_flat"] > 0
             if not res:
@@ -402,7 +397,6 @@ def test_flat_interleaved_layout(ice, cis_only):
     finally:
         _lib.call("hh_tune", b"flatw_pipe", 2)
         _lib.call("hh_tune", b"flatw_waves", 11)
-        _lib.call("hh_tune", b"flat_bm", 0)
         _lib.call("hh_tune", b"flat_cols", -1)
     for w, st in res[1:]:
         np.testing.assert_array_equal(w, res[0][0])
