@@ -1076,24 +1076,29 @@ __global__ __launch_bounds__(NW * 64, NW > 8 ? 3 : 2) void k_sweep_flatw(TileDev
                 flat_seg_c<U, ABL, 8, false, true>(cur.payn4, v, 0u, cur.qbn, 0, cur.nfn, fstn, cur.nfn, bl, acc, lane);
         }
         wave_lds_sync();
-        // compact narrow sums -> rows (zeros for rows without narrow entries)
-        constexpr int PL = kR / 64;
-        double cv[PL];
-        int cid[PL];
+        // compact narrow sums -> rows (zeros for rows without narrow entries).
+        // Every row of the block nonempty (idn: most flat tiles are trans
+        // tiles, ~45 entries per row): compact row = row and every row had
+        // its first write, so the three-sync pass is skipped (round 6)
+        if (!idn) {
+            constexpr int PL = kR / 64;
+            double cv[PL];
+            int cid[PL];
 #pragma unroll
-        for (int q = 0; q < PL; ++q) {
-            const int i = lane + 64 * q;
-            cv[q] = i < cur.nfn ? acc[i] : 0.0;
-            cid[q] = i < cur.nfn ? (idn ? i : (int)fidn[i]) : -1;
+            for (int q = 0; q < PL; ++q) {
+                const int i = lane + 64 * q;
+                cv[q] = i < cur.nfn ? acc[i] : 0.0;
+                cid[q] = i < cur.nfn ? (int)fidn[i] : -1;
+            }
+            wave_lds_sync();
+#pragma unroll
+            for (int q = 0; q < PL; ++q) acc[lane + 64 * q] = 0.0;
+            wave_lds_sync();
+#pragma unroll
+            for (int q = 0; q < PL; ++q)
+                if (cid[q] >= 0) acc[cid[q]] = cv[q];
+            wave_lds_sync();
         }
-        wave_lds_sync();
-#pragma unroll
-        for (int q = 0; q < PL; ++q) acc[lane + 64 * q] = 0.0;
-        wave_lds_sync();
-#pragma unroll
-        for (int q = 0; q < PL; ++q)
-            if (cid[q] >= 0) acc[cid[q]] = cv[q];
-        wave_lds_sync();
         if (UP && cur.up) {
             if (PIPE)
                 flat_seg_pipe<UW, ABL, 4, true>(cur.payw4, vw, 0u, cur.qbw, 0, cur.nfw, fstw, fidw, cur.nfw, bl, acc, lane,
