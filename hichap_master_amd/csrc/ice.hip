@@ -346,7 +346,11 @@ __device__ __forceinline__ void flat_load_ilv(const uint4* __restrict__ pay4, ui
     for (int k = 0; k < U; ++k) {
         const uint32_t cnt = flat_ilv_cnt(m, k);
         const bool on = (uint32_t)lane < cnt;
-        const uint4 x = ld16(pay4 + base + (on ? (uint32_t)lane : 0u));
+        // off lanes re-read the chunk's first uint4 (in the segment: m >= 1).
+        // Not base: with m < U the elements k >= m have no lane (cnt 0) and
+        // base is then q0 + m, one past the segment -- past the end of the
+        // payload buffer for its last tile (an illegal access, r6e)
+        const uint4 x = ld16(pay4 + (on ? base + (uint32_t)lane : q0));
         v[k] = on ? x : zero;
         base += cnt;
     }
