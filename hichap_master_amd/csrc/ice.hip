@@ -349,7 +349,7 @@ __device__ __forceinline__ void flat_load_ilv(const uint4* __restrict__ pay4, ui
         // off lanes re-read the chunk's first uint4 (in the segment: m >= 1).
         // Not base: with m < U the elements k >= m have no lane (cnt 0) and
         // base is then q0 + m, one past the segment -- past the end of the
-        // payload buffer for its last tile (an illegal access, r6e)
+        // payload buffer for its last tile
         const uint4 x = ld16(pay4 + (on ? base + (uint32_t)lane : q0));
         v[k] = on ? x : zero;
         base += cnt;
@@ -1004,20 +1004,16 @@ __global__ __launch_bounds__(NW * 64, NW > 8 ? 3 : 2) void k_sweep_flatw(TileDev
             if (k >= nk) return false;
             const FlatDesc d = desc[k];
             // the tile's row groups' active flags, one per lane (one round
-            // trip; a loop over the groups compiled to one load -> wait each).
-            // One ICE group (genome-wide): the block's entry check covered it,
-            // no round trip per tile (round 6)
-            if (!T.one_group) {
-                bool on = false;
-                const int ngr = d.ghi - d.glo + 1;
-                if (ngr <= 64) {
-                    const uint8_t a = act[d.glo + (lane < ngr ? lane : ngr - 1)];
-                    on = __ballot((a != 0) & (lane < ngr)) != 0;
-                } else {
-                    for (int g = d.glo; g <= d.ghi; ++g) on |= act[g] != 0;
-                }
-                if (!on) continue;  // a converged group's rows: k_marg never reads them
+            // trip; a loop over the groups compiled to one load -> wait each)
+            bool on = false;
+            const int ngr = d.ghi - d.glo + 1;
+            if (ngr <= 64) {
+                const uint8_t a = act[d.glo + (lane < ngr ? lane : ngr - 1)];
+                on = __ballot((a != 0) & (lane < ngr)) != 0;
+            } else {
+                for (int g = d.glo; g <= d.ghi; ++g) on |= act[g] != 0;
             }
+            if (!on) continue;  // a converged group's rows: k_marg never reads them
             x = Tw{d.slot, d.frec, (int)d.nr, (int)d.nfn, (int)d.nfw, d.qbn, d.qbw,
                    reinterpret_cast<const uint4*>(T.payn + d.entn), reinterpret_cast<const uint4*>(T.pay + d.ent),
                    cslot >= 0 && d.upper ? 1 : 0, T.bfix + T.row_lo + (long long)d.rb * kR};
@@ -1080,29 +1076,24 @@ __global__ __launch_bounds__(NW * 64, NW > 8 ? 3 : 2) void k_sweep_flatw(TileDev
                 flat_seg_c<U, ABL, 8, false, true>(cur.payn4, v, 0u, cur.qbn, 0, cur.nfn, fstn, cur.nfn, bl, acc, lane);
         }
         wave_lds_sync();
-        // compact narrow sums -> rows (zeros for rows without narrow entries).
-        // Every row of the block nonempty (idn: most flat tiles are trans
-        // tiles, ~45 entries per row): compact row = row and every row had
-        // its first write, so the three-sync pass is skipped (round 6)
-        if (!idn) {
-            constexpr int PL = kR / 64;
-            double cv[PL];
-            int cid[PL];
+        // compact narrow sums -> rows (zeros for rows without narrow entries)
+        constexpr int PL = kR / 64;
+        double cv[PL];
+        int cid[PL];
 #pragma unroll
-            for (int q = 0; q < PL; ++q) {
-                const int i = lane + 64 * q;
-                cv[q] = i < cur.nfn ? acc[i] : 0.0;
-                cid[q] = i < cur.nfn ? (int)fidn[i] : -1;
-            }
-            wave_lds_sync();
-#pragma unroll
-            for (int q = 0; q < PL; ++q) acc[lane + 64 * q] = 0.0;
-            wave_lds_sync();
-#pragma unroll
-            for (int q = 0; q < PL; ++q)
-                if (cid[q] >= 0) acc[cid[q]] = cv[q];
-            wave_lds_sync();
+        for (int q = 0; q < PL; ++q) {
+            const int i = lane + 64 * q;
+            cv[q] = i < cur.nfn ? acc[i] : 0.0;
+            cid[q] = i < cur.nfn ? (idn ? i : (int)fidn[i]) : -1;
         }
+        wave_lds_sync();
+#pragma unroll
+        for (int q = 0; q < PL; ++q) acc[lane + 64 * q] = 0.0;
+        wave_lds_sync();
+#pragma unroll
+        for (int q = 0; q < PL; ++q)
+            if (cid[q] >= 0) acc[cid[q]] = cv[q];
+        wave_lds_sync();
         if (UP && cur.up) {
             if (PIPE)
                 flat_seg_pipe<UW, ABL, 4, true>(cur.payw4, vw, 0u, cur.qbw, 0, cur.nfw, fstw, fidw, cur.nfw, bl, acc, lane,
@@ -1838,8 +1829,7 @@ __device__ __forceinline__ void ub_group(const UbSegs& S, long long grp, int chu
 // chunk) pairs, chunks fastest: neighbouring chunks of the same rows, which
 // share the cache lines at their boundaries (a chunk is 1008 B of uint8 /
 // 504 B of nibbles per row, not a multiple of 128 B), run back to back on one L2
-template <int OCC = 3>
-__global__ __launch_bounds__(kUbThreads, OCC) void k_sweep_ubands(UbSegs S, UbArgs a, long long n_bins, int xcd) {
+__global__ __launch_bounds__(kUbThreads, 3) void k_sweep_ubands(UbSegs S, UbArgs a, long long n_bins, int xcd) {
     __shared__ double cbuf[kUbCols];
     __shared__ double cwin[kUbWin];
     __shared__ double rowb[kUbGroupRows];
@@ -2544,7 +2534,6 @@ static int g_band_lpt = 1;      // band chunks dispatched heaviest first (0: uin
 // matrix, so every shard of one matrix takes the same path.
 static int g_uband = 1;
 static int64_t g_uband_min_bytes = 128LL << 20;
-static int g_ub_occ = 3;  // k_sweep_ubands waves per SIMD the registers are fitted to (3: 136 VGPRs; 4: <= 128)
 static int g_ub_xcd = 1;  // upper-band blocks dealt in contiguous ranges per XCD (k_sweep_ubands)
 static int g_sweep_single = -1;  // whole sweep in one launch: -1 auto (below g_single_max_bytes), 0 off, 1 on
 static int g_iter_events = 1;    // hh_ice_run: HIP events around every sweep (0: first / last only)
@@ -2629,11 +2618,7 @@ static void sweep(const hh_matrix* m, const TileDev& T, const uint8_t* act, cons
 
 // the tile view of a state's matrix (column slots and scale when the layout
 // has upper-triangle tiles)
-static TileDev tdev(const hh_ice* S) {
-    TileDev T = S->m->dev(S->colpart.p, S->fix.p, S->bfix.p);
-    T.one_group = S->G == 1 ? 1 : 0;
-    return T;
-}
+static TileDev tdev(const hh_ice* S) { return S->m->dev(S->colpart.p, S->fix.p, S->bfix.p); }
 
 // The matrix's band segments; returns their total chunk count.
 // Dispatch order of the band chunks: by work (counts in the chunk) descending,
@@ -2728,8 +2713,8 @@ static void sweep_uband(hh_ice* S, hipStream_t s) {
     const long long ng = S->ub_ghi - S->ub_glo;
     if (!ch || ng <= 0) return;
     HH_KTIME("k_sweep_ubands", s);
-    hipLaunchKernelGGL(g_ub_occ == 4 ? k_sweep_ubands<4> : k_sweep_ubands<3>, dim3((unsigned)ng, (unsigned)ch),
-                       dim3(kUbThreads), 0, s, segs, ub_args(S), (long long)S->m->n_bins, g_ub_xcd);
+    hipLaunchKernelGGL(k_sweep_ubands, dim3((unsigned)ng, (unsigned)ch), dim3(kUbThreads), 0, s, segs, ub_args(S),
+                       (long long)S->m->n_bins, g_ub_xcd);
     HIP_CHECK(hipGetLastError());
 }
 
@@ -3020,9 +3005,6 @@ int hh_tune(const char* key, int64_t value) {
             g_band_dpp = (int)value;
         } else if (k == "flatw_u") {  // (16 measured slower in round 4; the interleaved layout is for 8)
             HH_REQUIRE(value == 8, "flatw_u: 8 (the interleaved flat layout's run length)");
-        } else if (k == "ub_occ") {
-            HH_REQUIRE(value == 3 || value == 4, "ub_occ in {3, 4}");
-            g_ub_occ = (int)value;
         } else if (k == "syrk_coal") {
             HH_REQUIRE(value == 0 || value == 1, "syrk_coal in {0, 1}");
             g_syrk_coal = (int)value;

@@ -255,7 +255,6 @@ struct TileDev {
     unsigned long long* colpart;    // n_cslots x kW column partials (int64 fixed point)
     const double* fix;              // {2^e, 2^-e}: this sweep's fixed-point scale of b
     const unsigned long long* bfix; // B = round(b 2^e) of every bin (k_fixscale)
-    int one_group = 0;              // the matrix has one ICE group (genome-wide): no per-tile active flags
 };
 
 extern int g_flat_defer;
