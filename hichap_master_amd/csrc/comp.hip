@@ -224,11 +224,10 @@ __device__ __forceinline__ void syrk_tile_ij(long long t, long long nt, long lon
     bj = b + rem;
 }
 
-// COAL (round 6): thread t loads the doubles Z[row][lc0 + 32 u] (lc0 = t % 32,
-// u = 0..3) instead of the d4 Z[row][4 (t % 32) ..]: whole 256-byte row
-// pieces per load instruction rather than 16-byte pieces 32 bytes apart.  The
-// same values land in the same LDS cells: bitwise the same Cov.
-template <bool SPLIT, bool COAL = false>
+// (round 6: loading whole 256-byte row pieces per instruction -- thread t the
+// doubles Z[row][t % 32 + 32 u] -- instead of a d4 per lane measured slower:
+// k_syrk 78.4 -> 100.3 ms per C5 pass, profiles/r6h/; not kept)
+template <bool SPLIT>
 __global__ __launch_bounds__(256, 2) void k_syrk(const double* __restrict__ Z, long long ld, long long Kpad,
                                               long long nt, long long kc, double scale, double* __restrict__ C,
                                               long long ldc, double* __restrict__ P) {
@@ -250,22 +249,15 @@ __global__ __launch_bounds__(256, 2) void k_syrk(const double* __restrict__ Z, l
 #pragma unroll
         for (int b = 0; b < 4; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
     // 16 rows x 128 cols per operand: thread -> rows lr, lr + 8; 4 doubles at lc
-    const int lr = threadIdx.x / 32, lc = COAL ? threadIdx.x % 32 : (threadIdx.x % 32) * 4;
+    const int lr = threadIdx.x / 32, lc = (threadIdx.x % 32) * 4;
     d4 va[2], vb[2];
     auto load = [&](long long k0) {
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const double* za = Z + (k0 + lr + 8 * h) * ld + i0 + lc;
             const double* zb = Z + (k0 + lr + 8 * h) * ld + j0 + lc;
-            if constexpr (COAL) {
-#pragma unroll
-                for (int u = 0; u < 4; ++u) va[h][u] = za[32 * u];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) vb[h][u] = diag ? va[h][u] : zb[32 * u];
-            } else {
-                va[h] = *reinterpret_cast<const d4*>(za);
-                vb[h] = diag ? va[h] : *reinterpret_cast<const d4*>(zb);
-            }
+            va[h] = *reinterpret_cast<const d4*>(za);
+            vb[h] = diag ? va[h] : *reinterpret_cast<const d4*>(zb);
         }
     };
     if (kb < ke) load(kb);
@@ -273,16 +265,8 @@ __global__ __launch_bounds__(256, 2) void k_syrk(const double* __restrict__ Z, l
         __syncthreads();  // previous step's LDS reads are done
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-            if constexpr (COAL) {
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    As[lr + 8 * h][lc + 32 * u] = va[h][u];
-                    Bs[lr + 8 * h][lc + 32 * u] = vb[h][u];
-                }
-            } else {
-                *reinterpret_cast<d4*>(&As[lr + 8 * h][lc]) = va[h];
-                *reinterpret_cast<d4*>(&Bs[lr + 8 * h][lc]) = vb[h];
-            }
+            *reinterpret_cast<d4*>(&As[lr + 8 * h][lc]) = va[h];
+            *reinterpret_cast<d4*>(&Bs[lr + 8 * h][lc]) = vb[h];
         }
         __syncthreads();
         if (k0 + 16 < ke) load(k0 + 16);
@@ -2950,10 +2934,10 @@ int hh_comp_correlation(hh_comp* c, const double* decline, const int64_t* ng, in
         {
             HH_KTIME("k_syrk", s);  // (split K: the reduction is inside the timed span)
             if (ns == 1) {
-                hipLaunchKernelGGL((g_syrk_coal ? k_syrk<false, true> : k_syrk<false, false>), dim3((unsigned)ntile),
+                hipLaunchKernelGGL(k_syrk<false>, dim3((unsigned)ntile),
                                    dim3(256), 0, s, Z.p, c->ld, Npad, nt, Npad, scale, cov.p, c->ld, nullptr);
             } else {
-                hipLaunchKernelGGL((g_syrk_coal ? k_syrk<true, true> : k_syrk<true, false>), dim3((unsigned)(ns * ntile)),
+                hipLaunchKernelGGL(k_syrk<true>, dim3((unsigned)(ns * ntile)),
                                    dim3(256), 0, s, Z.p, c->ld, Npad, nt, kc, scale, nullptr, c->ld, P.p);
                 hipLaunchKernelGGL(k_syrk_reduce, dim3((unsigned)((ntile * kSyTile + 255) / 256)), dim3(256), 0, s,
                                    P.p, ns, nt, scale, cov.p, c->ld);

@@ -113,7 +113,6 @@ inline int g_pca_method = 1;
 inline int g_syrk_split = -1;  // Cov K splits (hh_tune "syrk_split"): -1 auto, 0 never, n > 0 forced
 inline int g_pca_p = 8;
 inline int g_cor_sym = 3;  // hh_tune "cor_sym": Krylov Cor products read the upper triangle only (1 k_cor_sym, 2 k_cor_sym_pf, 3 the same with whole-line loads; 0 full)
-inline int g_syrk_coal = 1;  // hh_tune "syrk_coal": k_syrk operand loads as whole lines (round 6; 0: a d4 per lane)
 inline int g_ortho_tpb = 0;  // hh_tune "ortho_tpb": k_ortho rows per block / 64 (0: auto)
 inline int g_ortho_min_tpb = 2;  // hh_tune "ortho_min_tpb": the automatic choice's smallest rows per block / 64
 inline int g_ortho_lowsync = 1;     // hh_tune "ortho_lowsync": k_ortho's Full mode as low-synch CGS2 (0: round 3's 8 reductions)

@@ -3005,9 +3005,6 @@ int hh_tune(const char* key, int64_t value) {
             g_band_dpp = (int)value;
         } else if (k == "flatw_u") {  // (16 measured slower in round 4; the interleaved layout is for 8)
             HH_REQUIRE(value == 8, "flatw_u: 8 (the interleaved flat layout's run length)");
-        } else if (k == "syrk_coal") {
-            HH_REQUIRE(value == 0 || value == 1, "syrk_coal in {0, 1}");
-            g_syrk_coal = (int)value;
         } else if (k == "flatw_waves_up") {
             HH_REQUIRE(value == 8 || value == 11, "flatw_waves_up in {8, 11}");
             g_flatw_waves_up = (int)value;

@@ -339,28 +339,6 @@ def test_pca_ortho_fallback_and_grid_cap():
         np.testing.assert_allclose(_match_sign(p2[q], p0[q]), p0[q], atol=1e-11)
 
 
-def test_syrk_whole_line_loads_bitwise():
-    """k_syrk with whole-line operand loads (syrk_coal 1, the default) puts
-    the same values in the same LDS cells as the d4-per-lane loads: the
-    correlation matrix and the components are bitwise the same (chr9 at
-    25 kb: split-K and a ragged last tile)."""
-    from hichap_master_amd._lib import call
-    from hichap_master_amd.StructureFind import StructureFind
-    dM = _c5_matrix(8)
-    out = []
-    for coal in (0, 1):
-        call("hh_tune", b"syrk_coal", coal)
-        try:
-            sf = StructureFind(Res=C5_RES)
-            dec, G, NG = sf.Distance_Decay(M=dM, G_array=None)
-            pcs, Cor, OE = sf.Get_PCA(distance_bin=dec.copy(), M=dM, NG_array=NG)
-            out.append((np.asarray(pcs), np.asarray(Cor)))
-        finally:
-            call("hh_tune", b"syrk_coal", 1)
-    np.testing.assert_array_equal(out[0][1], out[1][1])
-    np.testing.assert_array_equal(out[0][0], out[1][0])
-
-
 def test_pca_pipelined_upper_triangle_product_bitwise():
     """k_cor_sym_pf (V staged once per rectangle, the next column tile's
     first loads in flight) against k_cor_sym: the same MFMA sequence and
