@@ -2514,6 +2514,7 @@ static int g_sweep_ablate = 0;
 // +2 %, profiles/r1v8_knobs_split.log).  All write disjoint partials.
 static int g_band_concurrent = 1;  // dense-band sweep on a side stream, beside the tiles
 static int g_split_tiles = 1;      // with band_concurrent: tiled kernel on a second side stream
+static int g_conc_order = 0;       // three-stream sweep launch order: 0 band, tiled, flat; 1 flat, band, tiled
 // below this payload the fork / join costs more than the overlap gains.
 // Round 2, with the band kernel at 8 waves per SIMD: one stream is 4-5 %
 // faster for C3 (3.0 GB) and the N = 8 C4 shards (1.6-1.9 GB), three streams
@@ -2544,13 +2545,16 @@ static int64_t g_trace_cap = 0, g_trace_n = 0;
 
 template <int NB, int ABL, bool UP>
 static void launch_sweep_up(const hh_matrix* m, const TileDev& T, const uint8_t* act, const double* b, double* part,
-                            hipStream_t s, hipStream_t s_tiled) {
+                            hipStream_t s, hipStream_t s_tiled, int which) {
     const int n_tiled = (int)(m->n_units - m->n_units_flat), n_flat = (int)m->n_units_flat;
-    if (n_tiled) {
+    auto tiled = [&] {
+        if (!n_tiled) return;
         HH_KTIME("k_sweep_tiled", s_tiled);  // per-kernel registry timing (probes; off by default)
         hipLaunchKernelGGL((k_sweep_tiled<NB, ABL, UP>), dim3((unsigned)n_tiled), dim3(kSweepThreads), 0, s_tiled,
                            T, act, n_tiled, b, (long long)m->n_bins, part);
-    }
+    };
+    if (which & 1) tiled();
+    if (!(which & 2)) return;
     HH_KTIME(n_flat ? "k_sweep_flat" : nullptr, s);
     if (n_flat && m->n_fgroups) {
         // (the column-grouped flat tiles' narrow segments are interleaved for
@@ -2584,34 +2588,35 @@ static void launch_sweep_up(const hh_matrix* m, const TileDev& T, const uint8_t*
 
 template <int NB, int ABL>
 static void launch_sweep(const hh_matrix* m, const TileDev& T, const uint8_t* act, const double* b, double* part,
-                         hipStream_t s, hipStream_t s_tiled) {
+                         hipStream_t s, hipStream_t s_tiled, int which) {
     if constexpr (kUpperBuild) {
-        if (T.upper) return launch_sweep_up<NB, ABL, true>(m, T, act, b, part, s, s_tiled);
+        if (T.upper) return launch_sweep_up<NB, ABL, true>(m, T, act, b, part, s, s_tiled, which);
     }
-    launch_sweep_up<NB, ABL, false>(m, T, act, b, part, s, s_tiled);
+    launch_sweep_up<NB, ABL, false>(m, T, act, b, part, s, s_tiled, which);
 }
 
 template <int ABL>
 static void launch_sweep_nb(const hh_matrix* m, const TileDev& T, const uint8_t* act, const double* b, double* part,
-                            hipStream_t s, hipStream_t st) {
+                            hipStream_t s, hipStream_t st, int which) {
     switch (g_sweep_nb) {
-        case 1: launch_sweep<1, ABL>(m, T, act, b, part, s, st); break;
-        case 2: launch_sweep<2, ABL>(m, T, act, b, part, s, st); break;
-        case 8: launch_sweep<8, ABL>(m, T, act, b, part, s, st); break;
-        default: launch_sweep<4, ABL>(m, T, act, b, part, s, st); break;
+        case 1: launch_sweep<1, ABL>(m, T, act, b, part, s, st, which); break;
+        case 2: launch_sweep<2, ABL>(m, T, act, b, part, s, st, which); break;
+        case 8: launch_sweep<8, ABL>(m, T, act, b, part, s, st, which); break;
+        default: launch_sweep<4, ABL>(m, T, act, b, part, s, st, which); break;
     }
 }
 
-// s_tiled: stream of the tiled kernel (= s, or a side stream joined by the caller)
+// s_tiled: stream of the tiled kernel (= s, or a side stream joined by the
+// caller); which: 1 the tiled kernel, 2 the flat kernel, 3 both
 static void sweep(const hh_matrix* m, const TileDev& T, const uint8_t* act, const double* b, double* part,
-                  hipStream_t s, hipStream_t s_tiled = nullptr) {
+                  hipStream_t s, hipStream_t s_tiled = nullptr, int which = 3) {
     if (m->n_units == 0) return;
     if (!s_tiled) s_tiled = s;
     switch (g_sweep_ablate) {
-        case 1: launch_sweep_nb<1>(m, T, act, b, part, s, s_tiled); break;
-        case 2: launch_sweep_nb<2>(m, T, act, b, part, s, s_tiled); break;
-        case 3: launch_sweep_nb<3>(m, T, act, b, part, s, s_tiled); break;
-        default: launch_sweep_nb<0>(m, T, act, b, part, s, s_tiled); break;
+        case 1: launch_sweep_nb<1>(m, T, act, b, part, s, s_tiled, which); break;
+        case 2: launch_sweep_nb<2>(m, T, act, b, part, s, s_tiled, which); break;
+        case 3: launch_sweep_nb<3>(m, T, act, b, part, s, s_tiled, which); break;
+        default: launch_sweep_nb<0>(m, T, act, b, part, s, s_tiled, which); break;
     }
     HIP_CHECK(hipGetLastError());
 }
@@ -2834,10 +2839,18 @@ static void marg_weighted(hh_ice* S, double* out, hipStream_t s, bool timed, int
             ensure_side_streams(S);
             HIP_CHECK(hipEventRecord(S->fork, s));
             HIP_CHECK(hipStreamWaitEvent(S->side, S->fork, 0));
-            sweep_band(S, S->side);
-            HIP_CHECK(hipEventRecord(S->join, S->side));
             if (g_split_tiles) HIP_CHECK(hipStreamWaitEvent(S->side2, S->fork, 0));
-            sweep(m, T, S->act(), S->bias.p, S->part.p, s, g_split_tiles ? S->side2 : s);
+            if (g_conc_order) {
+                // the flat blocks (most of a CU's LDS) dispatched first, then
+                // the band blocks beside them, then the tiled kernel
+                sweep(m, T, S->act(), S->bias.p, S->part.p, s, s, 2);
+                sweep_band(S, S->side);
+                sweep(m, T, S->act(), S->bias.p, S->part.p, s, g_split_tiles ? S->side2 : s, 1);
+            } else {
+                sweep_band(S, S->side);
+                sweep(m, T, S->act(), S->bias.p, S->part.p, s, g_split_tiles ? S->side2 : s);
+            }
+            HIP_CHECK(hipEventRecord(S->join, S->side));
             if (g_split_tiles) {
                 HIP_CHECK(hipEventRecord(S->join2, S->side2));
                 HIP_CHECK(hipStreamWaitEvent(s, S->join2, 0));
@@ -3065,6 +3078,9 @@ int hh_tune(const char* key, int64_t value) {
         } else if (k == "fuse_stats") {
             HH_REQUIRE(value >= -1 && value <= 2, "fuse_stats in {-1, 0, 1, 2}");
             g_fuse_stats = (int)value;
+        } else if (k == "conc_order") {
+            HH_REQUIRE(value == 0 || value == 1, "conc_order in {0, 1}");
+            g_conc_order = (int)value;
         } else if (k == "split_tiles") {
             HH_REQUIRE(value == 0 || value == 1, "split_tiles in {0, 1}");
             g_split_tiles = (int)value;

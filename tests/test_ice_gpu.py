@@ -555,12 +555,14 @@ def test_saturated_counts_match_oracle(ice):
     np.testing.assert_allclose(w, wr, rtol=1e-9, equal_nan=True)
 
 
-@pytest.mark.parametrize("conc,split", [(1, 0), (1, 1)])
-def test_band_concurrent_bitwise(ice, conc, split):
+@pytest.mark.parametrize("conc,split,order,fcols", [(1, 0, 0, -1), (1, 1, 0, -1), (1, 1, 1, 1), (1, 0, 1, 1)])
+def test_band_concurrent_bitwise(ice, conc, split, order, fcols):
     """Sweep kernels on one stream, or the band sweep / tiled kernel on side
     streams (hh_tune band_concurrent / split_tiles, default on for matrices of
-    >= conc_min_bytes of payload; forced here on a small one): each kernel
-    writes its own partials, so the weights are bitwise equal."""
+    >= conc_min_bytes of payload; forced here on a small one), launched band
+    first or flat first (conc_order), with the plain or the column-grouped
+    flat tiles (flat_cols): each kernel writes its own partials, so the
+    weights are bitwise equal."""
     from hichap_master_amd import _lib
     b1, b2, c, off = _case(17, sizes=(1500, 900), A=60.0)
     n = int(off[-1])
@@ -568,17 +570,21 @@ def test_band_concurrent_bitwise(ice, conc, split):
     # the single-launch sweep (auto below 1 GB) is checked before the
     # concurrent one: switch it off so side / side2 really run
     _lib.call("hh_tune", b"sweep_single", 0)
+    _lib.call("hh_tune", b"flat_cols", fcols)
     try:
         w0, s0 = ice.balance(b1, b2, c, n, off, max_iters=300)  # one stream
         _lib.call("hh_tune", b"band_concurrent", conc)
         _lib.call("hh_tune", b"split_tiles", split)
+        _lib.call("hh_tune", b"conc_order", order)
         _lib.call("hh_tune", b"conc_min_bytes", 0)
         w1, s1 = ice.balance(b1, b2, c, n, off, max_iters=300)
     finally:
         _lib.call("hh_tune", b"band_concurrent", 1)
         _lib.call("hh_tune", b"split_tiles", 1)
+        _lib.call("hh_tune", b"conc_order", 0)
         _lib.call("hh_tune", b"conc_min_bytes", 8 << 30)
         _lib.call("hh_tune", b"sweep_single", -1)
+        _lib.call("hh_tune", b"flat_cols", -1)
     np.testing.assert_array_equal(w1, w0)
     assert s1["iters"] == s0["iters"]
 
