@@ -2514,7 +2514,7 @@ static int g_sweep_ablate = 0;
 // +2 %, profiles/r1v8_knobs_split.log).  All write disjoint partials.
 static int g_band_concurrent = 1;  // dense-band sweep on a side stream, beside the tiles
 static int g_split_tiles = 1;      // with band_concurrent: tiled kernel on a second side stream
-static int g_conc_order = 0;       // three-stream sweep launch order: 0 band, tiled, flat; 1 flat, band, tiled
+static int g_conc_order = 1;       // three-stream sweep launch order: 0 band, tiled, flat; 1 flat, band, tiled; 2 flat, tiled, band
 // below this payload the fork / join costs more than the overlap gains.
 // Round 2, with the band kernel at 8 waves per SIMD: one stream is 4-5 %
 // faster for C3 (3.0 GB) and the N = 8 C4 shards (1.6-1.9 GB), three streams
@@ -2840,12 +2840,17 @@ static void marg_weighted(hh_ice* S, double* out, hipStream_t s, bool timed, int
             HIP_CHECK(hipEventRecord(S->fork, s));
             HIP_CHECK(hipStreamWaitEvent(S->side, S->fork, 0));
             if (g_split_tiles) HIP_CHECK(hipStreamWaitEvent(S->side2, S->fork, 0));
-            if (g_conc_order) {
+            if (g_conc_order == 1) {
                 // the flat blocks (most of a CU's LDS) dispatched first, then
-                // the band blocks beside them, then the tiled kernel
+                // the band blocks, then the tiled kernel (C4: sweep 2.98 ->
+                // 2.89 ms, profiles/r6j/)
                 sweep(m, T, S->act(), S->bias.p, S->part.p, s, s, 2);
                 sweep_band(S, S->side);
                 sweep(m, T, S->act(), S->bias.p, S->part.p, s, g_split_tiles ? S->side2 : s, 1);
+            } else if (g_conc_order == 2) {  // flat, tiled, band
+                sweep(m, T, S->act(), S->bias.p, S->part.p, s, s, 2);
+                sweep(m, T, S->act(), S->bias.p, S->part.p, s, g_split_tiles ? S->side2 : s, 1);
+                sweep_band(S, S->side);
             } else {
                 sweep_band(S, S->side);
                 sweep(m, T, S->act(), S->bias.p, S->part.p, s, g_split_tiles ? S->side2 : s);
@@ -3079,7 +3084,7 @@ int hh_tune(const char* key, int64_t value) {
             HH_REQUIRE(value >= -1 && value <= 2, "fuse_stats in {-1, 0, 1, 2}");
             g_fuse_stats = (int)value;
         } else if (k == "conc_order") {
-            HH_REQUIRE(value == 0 || value == 1, "conc_order in {0, 1}");
+            HH_REQUIRE(value >= 0 && value <= 2, "conc_order in {0, 1, 2}");
             g_conc_order = (int)value;
         } else if (k == "split_tiles") {
             HH_REQUIRE(value == 0 || value == 1, "split_tiles in {0, 1}");

@@ -555,7 +555,7 @@ def test_saturated_counts_match_oracle(ice):
     np.testing.assert_allclose(w, wr, rtol=1e-9, equal_nan=True)
 
 
-@pytest.mark.parametrize("conc,split,order,fcols", [(1, 0, 0, -1), (1, 1, 0, -1), (1, 1, 1, 1), (1, 0, 1, 1)])
+@pytest.mark.parametrize("conc,split,order,fcols", [(1, 0, 0, -1), (1, 1, 0, 1), (1, 1, 1, 1), (1, 0, 1, -1), (1, 1, 2, 1)])
 def test_band_concurrent_bitwise(ice, conc, split, order, fcols):
     """Sweep kernels on one stream, or the band sweep / tiled kernel on side
     streams (hh_tune band_concurrent / split_tiles, default on for matrices of
@@ -581,7 +581,7 @@ def test_band_concurrent_bitwise(ice, conc, split, order, fcols):
     finally:
         _lib.call("hh_tune", b"band_concurrent", 1)
         _lib.call("hh_tune", b"split_tiles", 1)
-        _lib.call("hh_tune", b"conc_order", 0)
+        _lib.call("hh_tune", b"conc_order", 1)
         _lib.call("hh_tune", b"conc_min_bytes", 8 << 30)
         _lib.call("hh_tune", b"sweep_single", -1)
         _lib.call("hh_tune", b"flat_cols", -1)
