@@ -50,7 +50,7 @@ def _worker(rank, world, port, case, outdir):
     tdist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2])
+@pytest.mark.parametrize("world", [2, 4])
 def test_sharded_balance_gloo_matches_oracle(world):
     import torch.multiprocessing as mp
     from oracle import ice_ref
