@@ -1112,14 +1112,16 @@ def run_twostep(args, world, rank, local):
             fn()
         torch.cuda.synchronize()
         return (time.perf_counter() - t) / k
-    host_s = wall(lambda: mb.TwoStepCorrection(TM, MM, PM))
     i, j = np.nonzero(np.triu(TM))
     tp = (i, j, TM[i, j])
     cells = []
     for X in (MM, PM):
         r, c = np.nonzero(X)
         cells.append((r, c, X[r, c]))
-    cells_s = wall(lambda: mb.TwoStepCorrectionPixels(N, tp, cells[0], cells[1]))
+    # (--main-only, the PMC passes: no other calls, so every batch dispatch
+    # in the profile is a step's)
+    host_s = float("nan") if args.main_only else wall(lambda: mb.TwoStepCorrection(TM, MM, PM))
+    cells_s = float("nan") if args.main_only else wall(lambda: mb.TwoStepCorrectionPixels(N, tp, cells[0], cells[1]))
     alg = 3 * 8.0 * N * N + 2 * 8.0 * N * N  # 3 int64 reads + 2 fp64 writes
     if rank == 0:
         out = {"metric": "TwoStepCorrection, hg19 chr1 at 40 kb (N = 6232), device-resident",
@@ -1210,14 +1212,16 @@ def run_twostep_genome(args, world, rank, local):
     torch.cuda.synchronize()
     step = (time.perf_counter() - t0) / args.steps
     # one chromosome after the other (the per-call path)
-    ks = max(1, min(3, args.steps))
+    # (--main-only, the PMC passes: skipped, so every batch dispatch in the
+    # profile is a whole-genome step's)
+    ks = 0 if args.main_only else max(1, min(3, args.steps))
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     for _ in range(ks):
         for c in names:
             mb.TwoStepCorrection(tra[c], hap["M" + c], hap["P" + c])
     torch.cuda.synchronize()
-    seq = (time.perf_counter() - t1) / ks
+    seq = (time.perf_counter() - t1) / ks if ks else float("nan")
     sq = float(sum(int(N) ** 2 for N in Ns))
     alg = 40.0 * sq  # 3 int64 reads + 2 fp64 writes per element
     if rank == 0:
@@ -1352,6 +1356,8 @@ def main():
     ap.add_argument("--config", default="c4")
     ap.add_argument("--nnz", type=float, default=None)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--main-only", action="store_true",
+                    help="TwoStep lines: time the step only, no side measurements (the PMC passes)")
     ap.add_argument("--pairs", type=float, default=2e8, help="pairs per rank for --config pairs")
     ap.add_argument("--iters", type=int, default=200, help="ICE iteration cap for --config dropin / e2e")
     ap.add_argument("--fixed-iters", action="store_true", help="dropin: tol 0 (exactly --iters iterations)")
