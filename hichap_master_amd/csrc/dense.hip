@@ -286,18 +286,30 @@ __global__ __launch_bounds__(256) void k_symvc(const T* __restrict__ X, SymArgs 
 // position -- the same operands and IEEE operations (round 5: computed once,
 // sent through the same LDS space transposed, instead of recomputing the two
 // true divisions of S and the third of C per element): bitwise k_symvc<T, 3>.
+// its LDS, declared by the kernel: one copy whichever element types the
+// kernel instantiates the body with (two instantiations each declaring its
+// own had k_sv_out_b at 70 KB per block, 2 blocks per CU)
+struct SvOutLds {
+    double u[kT][kT + 1];  // the (J, I) tile transposed (as T), then the (I, J) outputs transposed
+    TileVecs tv;
+};
+template <class T>
+__device__ __forceinline__ T (&sv_tt(SvOutLds& S))[kT][kT + 1] {
+    static_assert(sizeof(T) <= sizeof(double), "element wider than the LDS cell");
+    return *reinterpret_cast<T(*)[kT][kT + 1]>(&S.u);
+}
+
 template <class T, class L = T>  // L: the element type read (see ts_gemv_body)
-__device__ __forceinline__ void symvc_out_body(const L* __restrict__ X, const SymArgs& a, double* __restrict__ out,
-                                               long long p, int cnt = 1, const long long* __restrict__ Xe = nullptr) {
+__device__ __forceinline__ void symvc_out_body(SvOutLds& S, const L* __restrict__ X, const SymArgs& a,
+                                               double* __restrict__ out, long long p, int cnt = 1,
+                                               const long long* __restrict__ Xe = nullptr) {
     // `cnt` consecutive pairs p, p + 1, ...: the next pair's matrix loads are
     // issued before this pair's transposed outputs are written (two pairs per
     // block: 1.88 -> 1.86 ms per genome; plain stores instead of the
     // nontemporal ones: 2.22 ms)
-    __shared__ union {
-        T tt[kT][kT + 1];       // the (J, I) tile, transposed
-        double dt[kT][kT + 1];  // then the (I, J) outputs, transposed
-    } u;
-    __shared__ TileVecs tv;
+    T (&tt)[kT][kT + 1] = sv_tt<T>(S);  // the (J, I) tile, transposed
+    double (&dt)[kT][kT + 1] = S.u;     // then the (I, J) outputs, transposed
+    TileVecs& tv = S.tv;
     const long long N = a.N;
     const bool has_gap = a.gap != nullptr && (a.ng_p == nullptr || *a.ng_p > 0);
     const int c = threadIdx.x & (kT - 1);
@@ -368,13 +380,13 @@ __device__ __forceinline__ void symvc_out_body(const L* __restrict__ X, const Sy
         const int lim_r = (int)std::min<long long>(kT, N - cI0), lim_c = (int)std::min<long long>(kT, N - cJ0);
         // (I, J) outputs: S_ij = v / aI[r], S_ji = X[J0 + c][I0 + r] / aJ[c] = tt[r][c] / aJ[c]
 #pragma unroll
-        for (int k = 0; k < kT / 4; ++k) u.tt[c][r0 + 4 * k] = w[k];
+        for (int k = 0; k < kT / 4; ++k) tt[c][r0 + 4 * k] = w[k];
         __syncthreads();
         double o[kT / 4];
 #pragma unroll
         for (int k = 0; k < kT / 4; ++k) {
             const int r = r0 + 4 * k;
-            const double sij = (double)v[k] / tv.aI[r], sji = (double)u.tt[r][c] / tv.aJ[c];
+            const double sij = (double)v[k] / tv.aI[r], sji = (double)tt[r][c] / tv.aJ[c];
             const double y = sym_value(diag_tile && r == c, has_gap, tv.gI[r], tv.gJ[c], sij, sji);
             o[k] = scale * (y / (tv.sJ[c] * tv.sI[r]));
             if (r < lim_r && c < lim_c) __builtin_nontemporal_store(o[k], &out[(cI0 + r) * N + cJ0 + c]);
@@ -387,19 +399,20 @@ __device__ __forceinline__ void symvc_out_body(const L* __restrict__ X, const Sy
         __syncthreads();  // every tt read done: the space takes the outputs
         // (J, I) outputs: element (J0 + r, I0 + c) = C[I0 + c][J0 + r] (symmetric)
 #pragma unroll
-        for (int k = 0; k < kT / 4; ++k) u.dt[c][r0 + 4 * k] = o[k];
+        for (int k = 0; k < kT / 4; ++k) dt[c][r0 + 4 * k] = o[k];
         __syncthreads();
 #pragma unroll
         for (int k = 0; k < kT / 4; ++k) {
             const int r = r0 + 4 * k;
-            if (r < lim_c && c < lim_r) __builtin_nontemporal_store(u.dt[r][c], &out[(cJ0 + r) * N + cI0 + c]);
+            if (r < lim_c && c < lim_r) __builtin_nontemporal_store(dt[r][c], &out[(cJ0 + r) * N + cI0 + c]);
         }
     }
 }
 
 template <class T>
 __global__ __launch_bounds__(256) void k_symvc_out(const T* __restrict__ X, SymArgs a, double* __restrict__ out) {
-    symvc_out_body<T>(X, a, out, blockIdx.x);
+    __shared__ SvOutLds S;
+    symvc_out_body<T>(S, X, a, out, blockIdx.x);
 }
 
 // rowsum(Y)_i from the pass-1 slab in a fixed order (J = 0 .. nT-1), then
@@ -1424,8 +1437,9 @@ __global__ __launch_bounds__(256) void k_sv_fin_b(const SvDesc* __restrict__ D) 
         d.tot[1] = (*d.raw_p / nn) / (acc / nn);
     }
 }
-__global__ __launch_bounds__(256) void k_sv_out_b(const SvDesc* __restrict__ D, const long long* __restrict__ off,
+__global__ __launch_bounds__(256, 4) void k_sv_out_b(const SvDesc* __restrict__ D, const long long* __restrict__ off,
                                                   int nd) {
+    __shared__ SvOutLds S;
     const int c = sv_find(off, nd, blockIdx.x);
     const SvDesc& d = D[c];
     SymArgs a{d.N, d.nT, d.alpha, d.gap, d.sv, 1.0};
@@ -1434,8 +1448,8 @@ __global__ __launch_bounds__(256) void k_sv_out_b(const SvDesc* __restrict__ D, 
     // two consecutive tile pairs per block (kSvOutPairs)
     const long long p = kSvOutPairs * ((long long)blockIdx.x - off[c]);
     const int cnt = (int)std::min<long long>(kSvOutPairs, d.npairs - p);
-    if (sv_narrow(d)) symvc_out_body<uint32_t, uint16_t>(d.x16, a, d.out, p, cnt, d.X);
-    else symvc_out_body<long long>(d.X, a, d.out, p, cnt);
+    if (sv_narrow(d)) symvc_out_body<uint32_t, uint16_t>(S, d.x16, a, d.out, p, cnt, d.X);
+    else symvc_out_body<long long>(S, d.X, a, d.out, p, cnt);
 }
 
 // Pass 3 by row bands (round 6; hh_tune "sv_out_rows", default 1): block
