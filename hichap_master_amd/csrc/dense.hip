@@ -288,7 +288,12 @@ __global__ __launch_bounds__(256) void k_symvc(const T* __restrict__ X, SymArgs 
 // true divisions of S and the third of C per element): bitwise k_symvc<T, 3>.
 // its LDS, declared by the kernel: one copy whichever element types the
 // kernel instantiates the body with (two instantiations each declaring its
-// own had k_sv_out_b at 70 KB per block, 2 blocks per CU)
+// own had k_sv_out_b at 70 KB per block, 2 blocks per CU; with one copy and
+// 4 waves per SIMD the 40 kb genome's output pass takes 1.79 -> 1.62 ms).
+// Measured and not kept (round 6): the pass by row bands -- each output
+// row's 2 KB written by one wave, every element computed at its own
+// position -- 1.69 ms: twice the divisions, and the 512-byte row pieces of
+// the tile pairs were not what bound it (profiles/r6q/)
 struct SvOutLds {
     double u[kT][kT + 1];  // the (J, I) tile transposed (as T), then the (I, J) outputs transposed
     TileVecs tv;
@@ -1452,168 +1457,6 @@ __global__ __launch_bounds__(256, 4) void k_sv_out_b(const SvDesc* __restrict__ 
     else symvc_out_body<long long>(S, d.X, a, d.out, p, cnt);
 }
 
-// Pass 3 by row bands (round 6; hh_tune "sv_out_rows", default 1): block
-// (band, chunk) writes out[i][j] for its kRB rows i and kCW columns j, each
-// output row's kCW x 8 = 2 KB written by one wave back to back.  The
-// tile-pair form above writes 512-B pieces of 64 different rows (the
-// (J, I) tile too), a DRAM page each per piece, and ran at ~3 TB/s.  Every
-// element is computed for its own position -- the lower triangle's too,
-// instead of the upper value sent through LDS -- with the tile-pair form's
-// operands in its order: at i > j the operands of (j, i) (S_ji first, the
-// gap flags of j then i, s_i s_j), so the same IEEE operations give bitwise
-// the same values.  X[j][i] of the block's columns comes through LDS (kCW
-// rows x kRB columns, escapes patched from the int64 matrix).
-int g_sv_out_rows = 1;
-constexpr int kRB = 32, kCW = 256;
-
-// the narrow chains (uint16 copy, values < 2^32): the strip through LDS
-__device__ __forceinline__ void symvc_outr_narrow(const uint16_t* __restrict__ X, const SvDesc& d, long long band,
-                                                  long long chunk, const long long* __restrict__ Xe,
-                                                  uint32_t (*tt)[kRB + 1]) {
-    __shared__ double aR[kRB], sR[kRB];
-    __shared__ uint8_t gR[kRB];
-    const long long N = d.N, i0 = band * kRB, j0 = chunk * kCW;
-    const int t = threadIdx.x, lane = t & 63;
-    const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-    const bool has_gap = d.gap != nullptr && *d.ng_p > 0;
-    const double scale = d.tot[1];
-    constexpr int kE = kCW * kRB / 256 / 2;  // strip elements per thread per half
-    // the strip X[j0 .. j0 + kCW)[i0 .. i0 + kRB) in two halves: 32 lanes per
-    // row (64 contiguous bytes of the copy), a half's loads all in flight
-#pragma unroll
-    for (int hf = 0; hf < 2; ++hf) {
-        uint32_t sv[kE];
-#pragma unroll
-        for (int q = 0; q < kE; ++q) {
-            const int e = t + 256 * (q + kE * hf), jj = e / kRB, ii = e % kRB;
-            const long long r = j0 + jj < N ? j0 + jj : N - 1, c = i0 + ii < N ? i0 + ii : N - 1;
-            sv[q] = X[r * N + c];
-        }
-        bool esc = false;  // escaped counts (rare): from the int64 matrix
-#pragma unroll
-        for (int q = 0; q < kE; ++q) esc |= sv[q] == 0xFFFFu;
-        if (__ballot(esc) != 0ull) {
-#pragma unroll
-            for (int q = 0; q < kE; ++q) {
-                const int e = t + 256 * (q + kE * hf), jj = e / kRB, ii = e % kRB;
-                const long long r = j0 + jj < N ? j0 + jj : N - 1, c = i0 + ii < N ? i0 + ii : N - 1;
-                if (sv[q] == 0xFFFFu) sv[q] = (uint32_t)Xe[r * N + c];
-            }
-        }
-#pragma unroll
-        for (int q = 0; q < kE; ++q) {
-            const int e = t + 256 * (q + kE * hf);
-            tt[e / kRB][e % kRB] = sv[q];
-        }
-    }
-    if (t < kRB) {
-        const long long i = i0 + t < N ? i0 + t : N - 1;
-        aR[t] = d.alpha[i];
-        sR[t] = d.sv[i];
-        gR[t] = has_gap ? d.gap[i] : 0;
-    }
-    constexpr int kR4 = kRB / 4, kC = kCW / 64;
-    double aC[kC], sC[kC];
-    bool gC[kC];
-#pragma unroll
-    for (int k = 0; k < kC; ++k) {
-        const long long j = j0 + lane + 64 * k < N ? j0 + lane + 64 * k : N - 1;
-        aC[k] = d.alpha[j];
-        sC[k] = d.sv[j];
-        gC[k] = has_gap && d.gap[j];
-    }
-    // this wave's rows, every row's loads in flight first
-    uint32_t xv[kR4][kC];
-#pragma unroll
-    for (int q = 0; q < kR4; ++q) {
-        const long long i = i0 + w * kR4 + q, ic = i < N ? i : N - 1;
-#pragma unroll
-        for (int k = 0; k < kC; ++k) {
-            const long long j = j0 + lane + 64 * k, jc = j < N ? j : N - 1;
-            xv[q][k] = X[ic * N + jc];
-        }
-    }
-    {
-        bool esc = false;
-#pragma unroll
-        for (int q = 0; q < kR4; ++q)
-#pragma unroll
-            for (int k = 0; k < kC; ++k) esc |= xv[q][k] == 0xFFFFu;
-        if (__ballot(esc) != 0ull) {
-#pragma unroll
-            for (int q = 0; q < kR4; ++q) {
-                const long long i = i0 + w * kR4 + q, ic = i < N ? i : N - 1;
-#pragma unroll
-                for (int k = 0; k < kC; ++k) {
-                    const long long j = j0 + lane + 64 * k, jc = j < N ? j : N - 1;
-                    if (xv[q][k] == 0xFFFFu) xv[q][k] = (uint32_t)Xe[ic * N + jc];
-                }
-            }
-        }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < kR4; ++q) {
-        const int ii = w * kR4 + q;
-        const long long i = i0 + ii;
-        if (i >= N) break;  // (wave-uniform)
-        const double ai = aR[ii], si = sR[ii];
-        const bool gi = gR[ii] != 0;
-        double* orow = d.out + i * N;
-#pragma unroll
-        for (int k = 0; k < kC; ++k) {
-            const int jj = lane + 64 * k;
-            const long long j = j0 + jj;
-            const double sij = (double)xv[q][k] / ai, sji = (double)tt[jj][ii] / aC[k];
-            const bool lo = i > j;  // lower triangle: the operands of (j, i), in its order
-            const double y = sym_value(i == j, has_gap, lo ? gC[k] : gi, lo ? gi : gC[k], lo ? sji : sij, lo ? sij : sji);
-            const double ss = lo ? si * sC[k] : sC[k] * si;
-            if (j < N) __builtin_nontemporal_store(scale * (y / ss), orow + j);
-        }
-    }
-}
-
-// a chain whose counts do not fit 32 bits (rare): the same values from the
-// int64 matrix, X[j][i] read directly (no LDS strip, not unrolled)
-__device__ __forceinline__ void symvc_outr_wide(const long long* __restrict__ X, const SvDesc& d, long long band,
-                                                long long chunk) {
-    const long long N = d.N, i0 = band * kRB, j0 = chunk * kCW;
-    const int t = threadIdx.x, lane = t & 63;
-    const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-    const bool has_gap = d.gap != nullptr && *d.ng_p > 0;
-    const double scale = d.tot[1];
-    constexpr int kR4 = kRB / 4, kC = kCW / 64;
-#pragma unroll 1
-    for (int q = 0; q < kR4; ++q) {
-        const long long i = i0 + w * kR4 + q;
-        if (i >= N) break;
-        const double ai = d.alpha[i], si = d.sv[i];
-        const bool gi = has_gap && d.gap[i];
-#pragma unroll 1
-        for (int k = 0; k < kC; ++k) {
-            const long long j = j0 + lane + 64 * k;
-            if (j >= N) continue;
-            const double aj = d.alpha[j], sj = d.sv[j];
-            const bool gj = has_gap && d.gap[j];
-            const double sij = (double)X[i * N + j] / ai, sji = (double)X[j * N + i] / aj;
-            const bool lo = i > j;
-            const double y = sym_value(i == j, has_gap, lo ? gj : gi, lo ? gi : gj, lo ? sji : sij, lo ? sij : sji);
-            const double ss = lo ? si * sj : sj * si;
-            __builtin_nontemporal_store(scale * (y / ss), d.out + i * N + j);
-        }
-    }
-}
-
-__global__ __launch_bounds__(256) void k_sv_outr_b(const SvDesc* __restrict__ D, const long long* __restrict__ off,
-                                                   int nd) {
-    __shared__ uint32_t tt[kCW][kRB + 1];  // tt[jj][ii] = X[j0 + jj][i0 + ii]
-    const int c = sv_find(off, nd, blockIdx.x);
-    const SvDesc& d = D[c];
-    const long long l = (long long)blockIdx.x - off[c], ncw = (d.N + kCW - 1) / kCW;
-    if (sv_narrow(d)) symvc_outr_narrow(d.x16, d, l / ncw, l % ncw, d.X, tt);
-    else symvc_outr_wide(d.X, d, l / ncw, l % ncw);
-}
-
 
 // Gap_defined (:915-929) from zero counts: cov = 1 - zeros / N.  cov is a
 // non-increasing function of the integer zero count, so the percentile's two
@@ -2205,8 +2048,7 @@ static void twostep_batch_impl(int32_t n, const int64_t* const* TM, const int64_
                     sd[j] = d;
                     const long long nblk[kSvPhases] = {d.nrc * d.gcb, d.ggrid,  (Nc + 63) / 64,
                                                        d.nb,         d.nb,
-                                                       g_sv_out_rows ? ((Nc + kRB - 1) / kRB) * ((Nc + kCW - 1) / kCW)
-                                                                     : (d.npairs + kSvOutPairs - 1) / kSvOutPairs};
+                                                       (d.npairs + kSvOutPairs - 1) / kSvOutPairs};
                     for (int k = 0; k < kSvPhases; ++k) off[(size_t)k * (nd + 1) + j + 1] = off[(size_t)k * (nd + 1) + j] + nblk[k];
                 }
             }
@@ -2244,8 +2086,7 @@ static void twostep_batch_impl(int32_t n, const int64_t* const* TM, const int64_
             hipLaunchKernelGGL(k_sv_gemv_b<2>, grid(kSvGemv), dim3(256), 0, s0, D, O(kSvGemv), nd);
             hipLaunchKernelGGL(k_sv_q_b, grid(kSvQ), dim3(256), 0, s0, D, O(kSvQ), nd);
             hipLaunchKernelGGL(k_sv_fin_b, dim3((unsigned)nd), dim3(256), 0, s0, D);
-            if (g_sv_out_rows) hipLaunchKernelGGL(k_sv_outr_b, grid(kSvOut), dim3(256), 0, s0, D, O(kSvOut), nd);
-            else hipLaunchKernelGGL(k_sv_out_b, grid(kSvOut), dim3(256), 0, s0, D, O(kSvOut), nd);
+            hipLaunchKernelGGL(k_sv_out_b, grid(kSvOut), dim3(256), 0, s0, D, O(kSvOut), nd);
             HIP_CHECK(hipGetLastError());
             const size_t gbytes = (size_t)2 * goff[n], ebytes = (size_t)n * sizeof(int);
             char* dl = (char*)pinned_stage().get(0, ((gbytes + 15) & ~(size_t)15) + ebytes);

@@ -2514,7 +2514,6 @@ static int g_sweep_ablate = 0;
 // +2 %, profiles/r1v8_knobs_split.log).  All write disjoint partials.
 static int g_band_concurrent = 1;  // dense-band sweep on a side stream, beside the tiles
 static int g_split_tiles = 1;      // with band_concurrent: tiled kernel on a second side stream
-extern int g_sv_out_rows;          // dense.hip
 static int g_conc_order = 1;       // three-stream sweep launch order: 0 band, tiled, flat; 1 flat, band, tiled; 2 flat, tiled, band
 // below this payload the fork / join costs more than the overlap gains.
 // Round 2, with the band kernel at 8 waves per SIMD: one stream is 4-5 %
@@ -3084,9 +3083,6 @@ int hh_tune(const char* key, int64_t value) {
         } else if (k == "fuse_stats") {
             HH_REQUIRE(value >= -1 && value <= 2, "fuse_stats in {-1, 0, 1, 2}");
             g_fuse_stats = (int)value;
-        } else if (k == "sv_out_rows") {  // (dense.hip: TwoStep batch output pass by row bands)
-            HH_REQUIRE(value == 0 || value == 1, "sv_out_rows in {0, 1}");
-            g_sv_out_rows = (int)value;
         } else if (k == "conc_order") {
             HH_REQUIRE(value >= 0 && value <= 2, "conc_order in {0, 1, 2}");
             g_conc_order = (int)value;

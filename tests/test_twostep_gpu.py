@@ -327,41 +327,6 @@ def test_intra_chrom_batch_equals_per_chromosome(mb, n_streams):
     np.testing.assert_array_equal(gaps["PX"], ref[3])
 
 
-def test_intra_chrom_batch_row_band_output_bitwise(mb):
-    """The batch's output pass by row bands (sv_out_rows 1, the default: each
-    element computed at its own position, the lower triangle's from the
-    operands of its mirror in the mirror's order) against the tile-pair pass
-    (0: each pair's value written to both positions): bitwise, on sizes that
-    are no multiple of the 32-row bands or 256-column chunks, with escaped
-    counts in both triangles and a chromosome past 32 bits."""
-    import torch
-    from hichap_master_amd import _lib
-    rng = np.random.default_rng(83)
-    tra, hap = {}, {}
-    for c, N, drop in (("1", 1000, 20), ("2", 257, 0), ("3", 31, 0), ("4", 600, 9)):
-        TM = synth.dense_chrom(N, rng, A=50.0)
-        MM, PM = synth.haplotype_pair(TM, rng, drop_rows=drop)
-        if c == "1":
-            for (i, j), v in (((3, 10), 65536), ((10, 3), 70000), ((N - 1, 2), 65535)):
-                MM[i, j] = v
-                PM[j, i] = v + 1
-                TM[i, j] += 2 * v
-                TM[j, i] = TM[i, j]
-        if c == "4":
-            MM[3, 10] = 2 ** 33
-            TM[3, 10] = TM[10, 3] = 2 ** 34
-        tra[c] = torch.from_numpy(TM).cuda()
-        hap["M" + c], hap["P" + c] = torch.from_numpy(MM).cuda(), torch.from_numpy(PM).cuda()
-    rows, _ = mb.IntraChromMatrixCorrection(tra, hap, n_streams=0)
-    _lib.call("hh_tune", b"sv_out_rows", 0)
-    try:
-        pairs, _ = mb.IntraChromMatrixCorrection(tra, hap, n_streams=0)
-    finally:
-        _lib.call("hh_tune", b"sv_out_rows", 1)
-    for k in rows:
-        assert torch.equal(rows[k], pairs[k]), k
-
-
 @pytest.mark.parametrize("n_streams", [0, 3])
 def test_intra_chrom_batch_memory_budget_bitwise(mb, n_streams):
     """hh_twostep_batch splits the chromosomes into consecutive groups whose
