@@ -1120,8 +1120,8 @@ def run_twostep(args, world, rank, local):
         cells.append((r, c, X[r, c]))
     # (--main-only, the PMC passes: no other calls, so every batch dispatch
     # in the profile is a step's)
-    host_s = float("nan") if args.main_only else wall(lambda: mb.TwoStepCorrection(TM, MM, PM))
-    cells_s = float("nan") if args.main_only else wall(lambda: mb.TwoStepCorrectionPixels(N, tp, cells[0], cells[1]))
+    host_s = None if args.main_only else wall(lambda: mb.TwoStepCorrection(TM, MM, PM))
+    cells_s = None if args.main_only else wall(lambda: mb.TwoStepCorrectionPixels(N, tp, cells[0], cells[1]))
     alg = 3 * 8.0 * N * N + 2 * 8.0 * N * N  # 3 int64 reads + 2 fp64 writes
     if rank == 0:
         out = {"metric": "TwoStepCorrection, hg19 chr1 at 40 kb (N = 6232), device-resident",
@@ -1135,7 +1135,8 @@ def run_twostep(args, world, rank, local):
                             "achieved": alg / step / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                             "frac": alg / step / 1e9 / PEAK_HBM_GBS, "traffic": None,
                             "alg_bytes_per_launch": alg},
-               "host_arrays_ms": 1000.0 * host_s, "cells_in_upper_out_ms": 1000.0 * cells_s,
+               "host_arrays_ms": None if args.main_only else 1000.0 * host_s,
+               "cells_in_upper_out_ms": None if args.main_only else 1000.0 * cells_s,
                "note": "host_arrays_ms: numpy N x N in / out (PCIe: 1.55 GB per call); cells_in_upper_out_ms: "
                        "pixel tables in, corrected upper tables out (TwoStepCorrectionPixels)"}
         tr, tr_src = twostep_pmc_traffic("twostep", {"workload": "twostep-chr1-40kb", "N": N})
@@ -1221,7 +1222,7 @@ def run_twostep_genome(args, world, rank, local):
         for c in names:
             mb.TwoStepCorrection(tra[c], hap["M" + c], hap["P" + c])
     torch.cuda.synchronize()
-    seq = (time.perf_counter() - t1) / ks if ks else float("nan")
+    seq = (time.perf_counter() - t1) / ks if ks else None
     sq = float(sum(int(N) ** 2 for N in Ns))
     alg = 40.0 * sq  # 3 int64 reads + 2 fp64 writes per element
     if rank == 0:
@@ -1238,7 +1239,7 @@ def run_twostep_genome(args, world, rank, local):
                             "achieved": alg / step / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                             "frac": alg / step / 1e9 / PEAK_HBM_GBS, "traffic": None, "alg_bytes_per_launch": alg,
                             "note": "40 B per matrix element (3 int64 reads + 2 fp64 writes), the whole genome per step"},
-               "sequential_ms": 1000.0 * seq,
+               "sequential_ms": None if args.main_only else 1000.0 * seq,
                "note": "sequential_ms: the same 23 chromosomes as one TwoStepCorrection call each"}
         tr, tr_src = twostep_pmc_traffic("twostep_genome", {"workload": "twostep-hg19-40kb-genome",
                                                             "bins": int(sum(int(N) for N in Ns)), "sum_N2": sq})
