@@ -634,14 +634,22 @@ __global__ __launch_bounds__(256) void k_ts_gemv(const T* __restrict__ X, long l
 //   MODE 2: gpart[B][a] = sum_{b in B, b != a} (|S_ab - S_ba| / 2) / (s_b s_a)
 // with S_ab = Xc[a][b] / alpha_{G[a]}; (B, A) is read coalesced and
 // transposed through LDS.
+// (its LDS declared by the kernel: one copy for both element types of the
+// batch kernel, which had 58 KB per block with a copy per instantiation)
+struct GapLds {
+    double tt[kT][kT + 1];  // as T
+    double aA[kT], aB[kT], sA[kT], sB[kT];
+    double red[4][kT];
+};
 template <class T, int MODE>
-__device__ __forceinline__ void ts_gap_body(const T* __restrict__ Xc, const long long* __restrict__ ng_p,
+__device__ __forceinline__ void ts_gap_body(GapLds& S, const T* __restrict__ Xc, const long long* __restrict__ ng_p,
                                             const int* __restrict__ glist, const double* __restrict__ alpha,
                                             const double* __restrict__ sv, double* __restrict__ gpart, long long bx,
                                             long long gdx) {
-    __shared__ T tt[kT][kT + 1];
-    __shared__ double aA[kT], aB[kT], sA[kT], sB[kT];
-    __shared__ double red[4][kT];
+    static_assert(sizeof(T) <= sizeof(double), "element wider than the LDS cell");
+    T (&tt)[kT][kT + 1] = *reinterpret_cast<T(*)[kT][kT + 1]>(&S.tt);
+    double *aA = S.aA, *aB = S.aB, *sA = S.sA, *sB = S.sB;
+    double (&red)[4][kT] = S.red;
     const long long ng = *ng_p, nbt = (ng + kT - 1) / kT;
     const int c = threadIdx.x & (kT - 1), r0 = threadIdx.x >> 6;
     // grid-stride over the nbt x nbt tiles (the gap count is known on the device only)
@@ -695,7 +703,8 @@ template <class T, int MODE>
 __global__ __launch_bounds__(256) void k_ts_gap(const T* __restrict__ Xc, const long long* __restrict__ ng_p,
                                                 const int* __restrict__ glist, const double* __restrict__ alpha,
                                                 const double* __restrict__ sv, double* __restrict__ gpart) {
-    ts_gap_body<T, MODE>(Xc, ng_p, glist, alpha, sv, gpart, blockIdx.x, gridDim.x);
+    __shared__ GapLds S;
+    ts_gap_body<T, MODE>(S, Xc, ng_p, glist, alpha, sv, gpart, blockIdx.x, gridDim.x);
 }
 
 // Ccol_j = sum over the row chunks of part_c[rc][j] (fixed order: wave w
@@ -1395,15 +1404,16 @@ __global__ __launch_bounds__(256) void k_sv_gemv_b(const SvDesc* __restrict__ D,
     }
 }
 template <int MODE>
-__global__ __launch_bounds__(256) void k_sv_gap_b(const SvDesc* __restrict__ D, const long long* __restrict__ off,
+__global__ __launch_bounds__(256, 3) void k_sv_gap_b(const SvDesc* __restrict__ D, const long long* __restrict__ off,
                                                   int nd) {
+    __shared__ GapLds S;
     const int c = sv_find(off, nd, blockIdx.x);
     const SvDesc& d = D[c];
     if (sv_narrow(d))
-        ts_gap_body<uint32_t, MODE>((const uint32_t*)d.xc, d.ng_p, d.glist, d.alpha, MODE == 2 ? d.sv : nullptr,
+        ts_gap_body<uint32_t, MODE>(S, (const uint32_t*)d.xc, d.ng_p, d.glist, d.alpha, MODE == 2 ? d.sv : nullptr,
                                     MODE == 2 ? d.gpart2 : d.gpart1, (long long)blockIdx.x - off[c], d.ggrid);
     else
-        ts_gap_body<long long, MODE>(d.xc, d.ng_p, d.glist, d.alpha, MODE == 2 ? d.sv : nullptr,
+        ts_gap_body<long long, MODE>(S, d.xc, d.ng_p, d.glist, d.alpha, MODE == 2 ? d.sv : nullptr,
                                      MODE == 2 ? d.gpart2 : d.gpart1, (long long)blockIdx.x - off[c], d.ggrid);
 }
 __global__ __launch_bounds__(1024) void k_sv_colsum_b(const SvDesc* __restrict__ D, const long long* __restrict__ off,
