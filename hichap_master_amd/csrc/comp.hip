@@ -1318,15 +1318,14 @@ struct OrthoArgs {
     double *c1 = nullptr, *c2 = nullptr, *R = nullptr, *G = nullptr;  // small outputs (block 0)
     int* fail = nullptr;           // one flag per Cholesky (written 0 / 1)
     double *rpart = nullptr, *rout = nullptr, *gpart = nullptr;
-    unsigned long long* ctr = nullptr;  // barrier counters, a set per launch parity: this launch uses set par
-    int par = 0;                         // (from 0) and zeroes set 1 - par for the next one
+    unsigned long long* ctr = nullptr;  // two barrier-arrival counters: this launch uses ctr[par] (from 0)
+    int par = 0;                         // and zeroes ctr[1 - par] for the next one
     int* abort = nullptr;
     long long n = 0;
     int nblk = 0;
     double shift_scale = 0.0;
     long long* tstamp = nullptr;  // pca_debug >= 2: block 0's clock at the start, around each barrier, at the end
     int pre = 1;                  // FullLS basis-row prefetch: 0 off, 1 mul_q's, 2 also pass B's proj_part
-    int xbar = 1;                 // grid barriers: 1 XCD-hierarchical (ortho_grid_sync_x), 0 one counter
 };
 
 // HH_ORTHO_PRE (environment, read once): OrthoArgs::pre for the experiments.
@@ -1369,50 +1368,6 @@ __device__ __forceinline__ void ortho_grid_sync(unsigned long long* ctr, unsigne
         }
     }
     __syncthreads();
-}
-
-// XCD-hierarchical form of ortho_grid_sync (round 6; HH_ORTHO_BAR=0 keeps
-// the one-counter form): blocks b with equal b % 8 (one XCD under the
-// round-robin placement; any grouping is correct) arrive on their group's
-// counter, the group's last arriver on the top counter, and every block waits
-// on the top counter -- fan-in on eight words instead of one (the guide's
-// barrier-xcd row).  Counters are monotonic within a launch: group g's
-// barrier k completes at k x (its block count), the top at k x (groups).
-constexpr int kOrthoCtrStride = 16;  // u64 words between counters (their own 128-B lines)
-constexpr int kOrthoCtrs = 9;        // top + 8 groups, per launch parity
-template <typename F>
-__device__ __forceinline__ void ortho_grid_sync_x(unsigned long long* ctr, unsigned bar, int nblk, int* abort,
-                                                  F&& between) {
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const int g = (int)(blockIdx.x & 7u);
-        const unsigned long long ng = (unsigned long long)(nblk / 8 + (g < nblk % 8 ? 1 : 0));
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        const unsigned long long old = atomicAdd(ctr + kOrthoCtrStride * (1 + g), 1ull);
-        if (old + 1ull == (unsigned long long)bar * ng) atomicAdd(ctr, 1ull);  // the group is in
-    }
-    between();
-    if (threadIdx.x == 0) {
-        const unsigned long long target = (unsigned long long)bar * (unsigned long long)(nblk < 8 ? nblk : 8);
-        unsigned spins = 0;
-        while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-            __builtin_amdgcn_s_sleep(1);
-            if ((++spins & 255u) == 0u &&
-                (spins >= (1u << 22) || __hip_atomic_load(abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
-                atomicExch(abort, 1);
-                break;
-            }
-        }
-    }
-    __syncthreads();
-}
-
-static int ortho_bar_level() {
-    static const int v = [] {
-        const char* e = std::getenv("HH_ORTHO_BAR");
-        return e ? std::atoi(e) : 1;
-    }();
-    return v;
 }
 
 // a coherent (L2-bypassing) load of another block's partial
@@ -1464,7 +1419,6 @@ __global__ __launch_bounds__(256) void k_ortho(OrthoArgs Ain) {
     const auto A_xin = Ain.xin;
     const auto A_xout = Ain.xout;
     const int A_pre = Ain.pre;
-    const int A_xbar = Ain.xbar;
 
     constexpr int B = kSB, BB = kSB * kSB, RPB = 64 * TPB;
     __shared__ OrthoLds<TPB> L;
@@ -1476,14 +1430,11 @@ __global__ __launch_bounds__(256) void k_ortho(OrthoArgs Ain) {
         if (A_tstamp && g == 0 && t == 0) A_tstamp[k] = (long long)wall_clock64();
     };
     stamp(0);
-    if (g == 0 && t == 0)  // the previous launch's counters (it has completed)
-        for (int k = 0; k < kOrthoCtrs; ++k) A_ctr[(size_t)(1 - A_par) * kOrthoCtrs * kOrthoCtrStride + k * kOrthoCtrStride] = 0ull;
+    if (g == 0 && t == 0) A_ctr[1 - A_par] = 0ull;  // the previous launch's counter (it has completed)
     auto gsync_then = [&](auto&& between) __attribute__((always_inline)) {
         ++bar;
         stamp(2 * bar - 1);
-        unsigned long long* const cb = A_ctr + (size_t)A_par * kOrthoCtrs * kOrthoCtrStride;
-        if (A_xbar) ortho_grid_sync_x(cb, bar, nblk, A_abort, between);
-        else ortho_grid_sync(cb, (unsigned long long)bar * (unsigned long long)nblk, A_abort, between);
+        ortho_grid_sync(A_ctr + A_par, (unsigned long long)bar * (unsigned long long)nblk, A_abort, between);
         stamp(2 * bar);
     };
     auto gsync = [&]() __attribute__((always_inline)) { gsync_then([] {}); };
@@ -2440,7 +2391,7 @@ static bool pca_krylov(PcaWork& wk, const double* cor, long long n, int k, doubl
     const int oblk = (nap + tpb - 1) / tpb;
     const bool coop = allow_coop && g_pca_coop && oblk <= ortho_grid_cap(tpb);
     DBuf<double> orp(coop ? (size_t)oblk * kOrthoMaxE : 1), oro(kOrthoMaxE), ogp(coop ? (size_t)2 * oblk * BB : 1);
-    DBuf<unsigned long long> octr((size_t)2 * kOrthoCtrs * kOrthoCtrStride);
+    DBuf<unsigned long long> octr(2);
     octr.zero(s);
     int opar = 0;
     int* abort_flag = fail.p + P * 8 + 7;
@@ -2458,7 +2409,6 @@ static bool pca_krylov(PcaWork& wk, const double* cor, long long n, int k, doubl
         a.shift_scale = shift_scale;
         a.tstamp = g_pca_debug >= 2 ? tst.p : nullptr;
         a.pre = ortho_pre_level();
-        a.xbar = ortho_bar_level() ? 1 : 0;
         HH_REQUIRE(a.nb >= 0 && a.nb <= 8 && oblk >= 1 && oblk <= kOrthoMaxBlocks, "k_ortho shape");
         const dim3 grid((unsigned)oblk), blk(256);
         HH_KTIME("k_ortho", s);  // bench.py's C5 line: the dominant kernel by time
