@@ -495,7 +495,7 @@ constexpr int kGB = 4 * kGW;  // columns per block: its 4 waves read 16 KB of a 
 // MODE 2: part_r[q][i] = sum over the span's columns of X_ij * rs_j.
 // L: the element type read (uint16_t: the batch's copy, 0xFFFF entries taken
 // from the int64 matrix Xe); T: the value type the pass computes with.
-template <class T, int MODE, bool ROWS = true, class L = T>
+template <class T, int MODE, bool ROWS = true, class L = T, int KB = 4>
 __device__ __forceinline__ void ts_gemv_body(const L* __restrict__ X, long long N, const double* __restrict__ alpha,
                                              const double* __restrict__ rs, int gr, double* __restrict__ part_c,
                                              double* __restrict__ part_r, const int* __restrict__ gpos,
@@ -531,7 +531,7 @@ __device__ __forceinline__ void ts_gemv_body(const L* __restrict__ X, long long 
         ra_l = 1.0 / alpha[r0 + lane];
         if (gpos) gp_l = gpos[r0 + lane];
     }
-    constexpr int kB = 4;  // rows per batch: 32 loads in flight per lane
+    constexpr int kB = KB;  // rows per batch: 8 KB loads in flight per lane
 #pragma unroll 1
     for (long long i0 = r0; i0 < rend; i0 += kB) {
         T x[kB][8];
@@ -1395,16 +1395,18 @@ __global__ __launch_bounds__(256) void k_sv_gemv_b(const SvDesc* __restrict__ D,
             ts_gemv_body<uint32_t, 2, true, uint16_t>(d.x16, d.N, d.alpha, d.rsv, d.gr, d.part_c, d.part_r, nullptr,
                                                       nullptr, nullptr, l % d.nrc, l / d.nrc, d.X);
     } else {
+        // (the rare wide chains: 2 rows per batch, so that their registers do
+        // not set the kernel's -- the same rows in the same order)
         if (MODE == 1)
-            ts_gemv_body<long long, 1, false>(d.X, d.N, d.alpha, nullptr, d.gr, d.part_c, d.part_r, d.gpos, d.xc,
-                                              d.ng_p, l % d.nrc, l / d.nrc);
+            ts_gemv_body<long long, 1, false, long long, 2>(d.X, d.N, d.alpha, nullptr, d.gr, d.part_c, d.part_r,
+                                                            d.gpos, d.xc, d.ng_p, l % d.nrc, l / d.nrc);
         else
-            ts_gemv_body<long long, 2, true>(d.X, d.N, d.alpha, d.rsv, d.gr, d.part_c, d.part_r, nullptr, nullptr,
-                                             nullptr, l % d.nrc, l / d.nrc);
+            ts_gemv_body<long long, 2, true, long long, 2>(d.X, d.N, d.alpha, d.rsv, d.gr, d.part_c, d.part_r,
+                                                           nullptr, nullptr, nullptr, l % d.nrc, l / d.nrc);
     }
 }
 template <int MODE>
-__global__ __launch_bounds__(256, 3) void k_sv_gap_b(const SvDesc* __restrict__ D, const long long* __restrict__ off,
+__global__ __launch_bounds__(256, 4) void k_sv_gap_b(const SvDesc* __restrict__ D, const long long* __restrict__ off,
                                                   int nd) {
     __shared__ GapLds S;
     const int c = sv_find(off, nd, blockIdx.x);
