@@ -1063,11 +1063,7 @@ __global__ __launch_bounds__(kScanThreads) void k_rs_scatter(Src src, unsigned l
     __shared__ unsigned long long stage[kScanTile + kScanTile / 16];
     __shared__ unsigned wcnt[NW][256];
     __shared__ unsigned start[256], gofs_lo[256];
-    // the block scan's 4 words in stage's first entries: stage is dead
-    // between the keys' load into registers and the staging after the scan
-    // (a barrier on either side), and 32 B of LDS of its own had the block at
-    // 40 992 B -- 3 blocks per CU instead of 4
-    unsigned long long* const sh = stage;
+    __shared__ unsigned long long sh[4];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const long long base = (long long)blockIdx.x * kScanTile;
 #pragma unroll
